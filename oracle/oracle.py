@@ -1,0 +1,138 @@
+"""ORACLE (test infrastructure, not product code): ctypes binding of ``liborc_replay.so``,
+the CPU restatement of the reference placement replay (see ``replay.cpp``).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
+import this module — as the checker / the timed CPU baseline, never as the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborc_replay.so")
+
+_P = C.c_void_p
+
+
+class OrcGraph(C.Structure):
+    _fields_ = [
+        ("n_tasks", C.c_int64), ("n_workers", C.c_int64), ("n_prefixes", C.c_int64), ("n_groups", C.c_int64),
+        ("dep_ptr", _P), ("dep_idx", _P), ("prio", _P), ("prefix_id", _P), ("group_id", _P),
+        ("wanted", _P), ("rootish_override", _P), ("nbytes", _P), ("start", _P), ("stop", _P),
+        ("nthreads", _P), ("group_prefix", _P), ("prefix_default_dur", _P),
+        ("bandwidth", C.c_int64), ("default_data_size", C.c_int64), ("unknown_duration", C.c_double),
+        ("saturation", C.c_double),
+    ]
+
+
+class OrcResult(C.Structure):
+    _fields_ = [
+        ("pl_task", _P), ("pl_worker", _P), ("pl_comm", _P), ("pl_start", _P), ("pl_wsnbytes", _P),
+        ("pl_route", _P), ("n_placements", C.c_int64),
+        ("max_rounds", C.c_int64), ("n_rounds", C.c_int64), ("round_nplaced", _P), ("round_occ", _P),
+        ("round_wnbytes", _P), ("round_nproc", _P), ("round_idle", _P), ("round_sat", _P), ("round_itc", _P),
+        ("round_nqueued", _P), ("final_state", _P), ("seconds", C.c_double), ("error", C.c_char * 256),
+    ]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.orc_replay.argtypes = [C.POINTER(OrcGraph), C.POINTER(OrcResult)]
+        _lib.orc_replay.restype = C.c_int
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def replay(g: dict, config: dict, *, snapshots: bool = True, max_rounds: int | None = None) -> dict:
+    """Replay graph ``g`` (graph dict, ``distributed_amd/graphs.py``) under ``config``
+    ({bandwidth, default_data_size, unknown_duration, saturation}) and return the
+    placement records + per-round snapshots as numpy arrays."""
+    n = int(g["n_tasks"])
+    w = len(g["nthreads"])
+    sat = config["saturation"]
+    sat = math.inf if sat == "inf" else float(sat)
+    keep = []
+
+    def arr(x, dt):
+        a = np.ascontiguousarray(x, dtype=dt)
+        keep.append(a)
+        return a
+
+    gs = OrcGraph(
+        n_tasks=n, n_workers=w, n_prefixes=len(g["prefix_default_dur"]), n_groups=len(g["group_prefix"]),
+        dep_ptr=_ptr(arr(g["dep_ptr"], np.int64)), dep_idx=_ptr(arr(g["dep_idx"], np.int32)),
+        prio=_ptr(arr(g["prio"], np.int64)), prefix_id=_ptr(arr(g["prefix_id"], np.int32)),
+        group_id=_ptr(arr(g["group_id"], np.int32)), wanted=_ptr(arr(g["wanted"], np.uint8)),
+        rootish_override=_ptr(arr(g["rootish_override"], np.int8)), nbytes=_ptr(arr(g["nbytes"], np.int64)),
+        start=_ptr(arr(g["start"], np.float64)), stop=_ptr(arr(g["stop"], np.float64)),
+        nthreads=_ptr(arr(g["nthreads"], np.int32)), group_prefix=_ptr(arr(g["group_prefix"], np.int32)),
+        prefix_default_dur=_ptr(arr(g["prefix_default_dur"], np.float64)),
+        bandwidth=int(config["bandwidth"]), default_data_size=int(config["default_data_size"]),
+        unknown_duration=float(config["unknown_duration"]), saturation=sat,
+    )
+    R = int(max_rounds or (n + 2))
+    out = dict(
+        pl_task=np.zeros(n, np.int32), pl_worker=np.zeros(n, np.int32), pl_comm=np.zeros(n, np.int64),
+        pl_start=np.zeros(n, np.float64), pl_wsnbytes=np.zeros(n, np.int64), pl_route=np.zeros(n, np.int8),
+        round_nplaced=np.zeros(R, np.int32), final_state=np.zeros(n, np.uint8),
+    )
+    res = OrcResult(pl_task=_ptr(out["pl_task"]), pl_worker=_ptr(out["pl_worker"]), pl_comm=_ptr(out["pl_comm"]),
+                    pl_start=_ptr(out["pl_start"]), pl_wsnbytes=_ptr(out["pl_wsnbytes"]),
+                    pl_route=_ptr(out["pl_route"]), max_rounds=R, round_nplaced=_ptr(out["round_nplaced"]),
+                    final_state=_ptr(out["final_state"]))
+    if snapshots:
+        snap = dict(round_occ=np.zeros((R, w)), round_wnbytes=np.zeros((R, w), np.int64),
+                    round_nproc=np.zeros((R, w), np.int32), round_idle=np.zeros((R, w), np.uint8),
+                    round_sat=np.zeros((R, w), np.uint8), round_itc=np.zeros((R, w), np.uint8),
+                    round_nqueued=np.zeros(R, np.int32))
+        out.update(snap)
+        for k, v in snap.items():
+            setattr(res, k, _ptr(v))
+    rc = lib().orc_replay(C.byref(gs), C.byref(res))
+    if rc != 0:
+        raise RuntimeError("oracle replay failed: " + res.error.decode())
+    np_ = int(res.n_placements)
+    nr = int(res.n_rounds)
+    for k in ("pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route"):
+        out[k] = out[k][:np_]
+    for k in list(out):
+        if k.startswith("round_"):
+            out[k] = out[k][:nr]
+    out["seconds"] = float(res.seconds)
+    out["n_rounds"] = nr
+    return out
+
+
+def load_fixture(path: str):
+    """Load a ``tests/golden/*.npz`` fixture -> (graph dict, config, expected outputs)."""
+    import json
+
+    z = np.load(path, allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    g = {k: z[k] for k in ("dep_ptr", "dep_idx", "prio", "prefix_id", "group_id", "wanted", "rootish_override",
+                           "nbytes", "start", "stop", "nthreads", "group_prefix", "prefix_default_dur")}
+    g["n_tasks"] = len(g["prio"])
+    g["prefix_names"] = meta["prefix_names"]
+    g["group_names"] = meta["group_names"]
+    g["name"] = meta["name"]
+    exp = {k: z[k] for k in z.files if k.startswith(("pl_", "round_", "final_"))}
+    return g, meta["config"], exp, meta

@@ -1,0 +1,23 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP engine parity / smoke)")
+    config.addinivalue_line("markers", "slow: long CPU test")
+
+
+def golden_files():
+    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN

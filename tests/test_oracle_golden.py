@@ -1,0 +1,54 @@
+"""The oracle (oracle/replay.cpp) against the reference's own outputs.
+
+The fixtures were produced by replaying the reference ``SchedulerState``
+(tests/golden/gen_golden.py). Every placement tuple must match bit-for-bit —
+task, worker, comm_bytes, the fp64 objective start time, ws.nbytes and route —
+and so must every per-round worker snapshot (occupancy fp64, nbytes, processing
+count, idle / saturated / idle_task_count membership, queue length).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden_files
+from oracle import oracle
+
+PL_KEYS = ("pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")
+ROUND_KEYS = ("round_nplaced", "round_occ", "round_wnbytes", "round_nproc", "round_idle", "round_sat",
+              "round_itc", "round_nqueued", "final_state")
+
+
+def assert_same(out, exp, keys):
+    for k in keys:
+        a, b = out[k], exp[k]
+        assert a.shape == b.shape, (k, a.shape, b.shape)
+        bad = np.nonzero(a.reshape(-1) != b.reshape(-1))[0]
+        assert len(bad) == 0, f"{k}: {len(bad)} mismatches, first at flat index {bad[0]}: {a.reshape(-1)[bad[0]]!r} vs {b.reshape(-1)[bad[0]]!r}"
+
+
+@pytest.mark.parametrize("name", golden_files())
+def test_oracle_matches_reference(name):
+    g, cfg, exp, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
+    out = oracle.replay(g, cfg)
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+
+
+def test_scenario_saturation_counts():
+    # distributed/tests/test_scheduler.py:637-683 expected (a, b) task counts
+    for sat, counts in (("1.1", (3, 2)), ("2.5", (5, 3)), ("2.0", (4, 2)), ("1.0", (2, 1)), ("0.1", (1, 1))):
+        g, cfg, exp, meta = oracle.load_fixture(os.path.join(GOLDEN, f"sat_factor_{sat}.npz"))
+        out = oracle.replay(g, cfg)
+        assert tuple(out["round_nproc"][0]) == counts
+    g, cfg, exp, meta = oracle.load_fixture(os.path.join(GOLDEN, "sat_factor_inf.npz"))
+    out = oracle.replay(g, cfg)
+    a, b = out["round_nproc"][0]
+    assert a > b and a + b == 10
+
+
+def test_scenario_occupancy_includes_communication():
+    # distributed/tests/test_scheduler.py:1760-1799: 0.5 s unknown compute + 2 s network
+    g, cfg, exp, meta = oracle.load_fixture(os.path.join(GOLDEN, "occupancy_comm.npz"))
+    out = oracle.replay(g, cfg)
+    assert out["round_occ"][1][1] == 2.5
+    assert out["pl_worker"][2] == 1 and out["pl_comm"][2] == 200_000_000
