@@ -1,0 +1,65 @@
+"""ctypes binding of ``libdgplace.so`` (C ABI: ``include/dgplace.h``).
+
+The HIP library is the product path: there is no CPU fallback. If the shared
+library is missing or no GPU is visible, the calls raise instead of silently
+computing placements some other way.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libdgplace.so")
+
+_P = C.c_void_p
+_i32p = C.POINTER(C.c_int32)
+
+# name -> (restype, argtypes); the list is also what tests check the library exports
+SIGNATURES = {
+    "dgp_abi_version": (C.c_int, []),
+    "dgp_create": (_P, [C.c_int]),
+    "dgp_destroy": (None, [_P]),
+    "dgp_last_error": (C.c_char_p, [_P]),
+    "dgp_set_config": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_double, C.c_double]),
+    "dgp_set_workers": (C.c_int, [_P, C.c_int32, _P]),
+    "dgp_set_graph": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P]),
+    "dgp_set_task_results": (C.c_int, [_P, _P, _P, _P]),
+    "dgp_reset": (C.c_int, [_P]),
+    "dgp_update_graph": (C.c_int, [_P]),
+    "dgp_run_rounds": (C.c_int, [_P, C.c_int64, _P]),
+    "dgp_tasks_finished": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P]),
+    "dgp_num_placements": (C.c_int64, [_P]),
+    "dgp_get_placements": (C.c_int, [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, _P]),
+    "dgp_enable_snapshots": (C.c_int, [_P, C.c_int64]),
+    "dgp_get_snapshots": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dgp_get_task_states": (C.c_int, [_P, _P]),
+    "dgp_kernel_times": (C.c_int, [_P, _P, _P, C.c_int32]),
+    "dgp_set_timing": (C.c_int, [_P, C.c_int]),
+}
+
+ABI_VERSION = 1
+_lib = None
+
+
+class DgpError(RuntimeError):
+    pass
+
+
+def load() -> C.CDLL:
+    """Load libdgplace.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DgpError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                       " (the HIP engine has no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.dgp_abi_version() != ABI_VERSION:
+        raise DgpError(f"libdgplace ABI {lib.dgp_abi_version()} != {ABI_VERSION}")
+    _lib = lib
+    return lib

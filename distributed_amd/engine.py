@@ -1,0 +1,178 @@
+"""Host wrapper of the HIP placement engine (``libdgplace.so``).
+
+``PlacementEngine`` owns one device engine. It takes a graph dict
+(``distributed_amd/graphs.py``) and the scheduler knobs of ``distributed.yaml``,
+keeps the graph resident in HBM and replays the reference placement path on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+DEFAULT_CONFIG = {  # distributed/distributed.yaml:13,16,24,28
+    "bandwidth": 100_000_000,
+    "default_data_size": 1024,
+    "unknown_duration": 0.5,
+    "saturation": 1.1,
+}
+
+KERNEL_NAMES = ("frontier_release", "candidate_commbytes", "commit", "other")
+
+
+class PlacementEngine:
+    """One device engine bound to HIP device ``device``."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = self.lib.dgp_create(int(device))
+        if not h:
+            raise _lib.DgpError(f"dgp_create({device}) failed: no HIP device visible (no CPU fallback)")
+        self.h = h
+        self.n_tasks = 0
+        self.n_workers = 0
+        self._keep = []
+
+    # ------------------------------------------------------------------ plumbing
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self.lib.dgp_last_error(self.h)
+            raise _lib.DgpError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.dgp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ------------------------------------------------------------------- set-up
+    def set_config(self, config: dict | None = None):
+        cfg = dict(DEFAULT_CONFIG, **(config or {}))
+        sat = cfg["saturation"]
+        sat = math.inf if sat == "inf" else float(sat)
+        self._check(self.lib.dgp_set_config(self.h, int(cfg["bandwidth"]), int(cfg["default_data_size"]),
+                                            float(cfg["unknown_duration"]), sat), "dgp_set_config")
+        self.config = cfg
+
+    def set_workers(self, nthreads):
+        nt = np.ascontiguousarray(nthreads, dtype=np.int32)
+        self._check(self.lib.dgp_set_workers(self.h, len(nt), _ptr(nt)), "dgp_set_workers")
+        self.n_workers = len(nt)
+
+    def set_graph(self, g: dict):
+        arrs = {
+            "dep_ptr": np.ascontiguousarray(g["dep_ptr"], np.int64),
+            "dep_idx": np.ascontiguousarray(g["dep_idx"], np.int32),
+            "prio": np.ascontiguousarray(g["prio"], np.int64),
+            "prefix_id": np.ascontiguousarray(g["prefix_id"], np.int32),
+            "prefix_default_dur": np.ascontiguousarray(g["prefix_default_dur"], np.float64),
+            "group_id": np.ascontiguousarray(g["group_id"], np.int32),
+            "wanted": np.ascontiguousarray(g["wanted"], np.uint8),
+            "rootish_override": np.ascontiguousarray(g["rootish_override"], np.int8),
+        }
+        n = len(arrs["prio"])
+        self._check(self.lib.dgp_set_graph(
+            self.h, n, _ptr(arrs["dep_ptr"]), _ptr(arrs["dep_idx"]), _ptr(arrs["prio"]), _ptr(arrs["prefix_id"]),
+            len(arrs["prefix_default_dur"]), _ptr(arrs["prefix_default_dur"]), _ptr(arrs["group_id"]),
+            len(g["group_prefix"]), _ptr(arrs["wanted"]), _ptr(arrs["rootish_override"])), "dgp_set_graph")
+        self.n_tasks = n
+        res = [np.ascontiguousarray(g["nbytes"], np.int64), np.ascontiguousarray(g["start"], np.float64),
+               np.ascontiguousarray(g["stop"], np.float64)]
+        self._check(self.lib.dgp_set_task_results(self.h, *[_ptr(a) for a in res]), "dgp_set_task_results")
+
+    def load(self, g: dict, config: dict | None = None, *, snapshots: int = 0):
+        """Configure workers + config + graph in one go (the usual set-up)."""
+        self.set_workers(g["nthreads"])
+        self.set_config(config)
+        if snapshots:
+            self._check(self.lib.dgp_enable_snapshots(self.h, int(snapshots)), "dgp_enable_snapshots")
+        self.set_graph(g)
+        return self
+
+    # ------------------------------------------------------------------- replay
+    def reset(self):
+        self._check(self.lib.dgp_reset(self.h), "dgp_reset")
+
+    def update_graph(self):
+        self._check(self.lib.dgp_update_graph(self.h), "dgp_update_graph")
+
+    def run_rounds(self, max_rounds: int = -1) -> int:
+        n = C.c_int64(0)
+        self._check(self.lib.dgp_run_rounds(self.h, int(max_rounds), C.byref(n)), "dgp_run_rounds")
+        return int(n.value)
+
+    def replay(self) -> int:
+        """update_graph + every round; returns the number of placements."""
+        self.update_graph()
+        self.run_rounds(-1)
+        return self.num_placements()
+
+    def tasks_finished(self, tasks, nbytes, start, stop):
+        arrs = [np.ascontiguousarray(tasks, np.int32), np.ascontiguousarray(nbytes, np.int64),
+                np.ascontiguousarray(start, np.float64), np.ascontiguousarray(stop, np.float64)]
+        self._check(self.lib.dgp_tasks_finished(self.h, len(arrs[0]), *[_ptr(a) for a in arrs]),
+                    "dgp_tasks_finished")
+
+    # ------------------------------------------------------------------ results
+    def num_placements(self) -> int:
+        n = self.lib.dgp_num_placements(self.h)
+        if n < 0:
+            self._check(-2, "dgp_num_placements")
+        return int(n)
+
+    def placements(self, offset: int = 0, count: int | None = None) -> dict:
+        n = self.num_placements()
+        if count is None:
+            count = n - offset
+        out = dict(pl_task=np.zeros(count, np.int32), pl_worker=np.zeros(count, np.int32),
+                   pl_comm=np.zeros(count, np.int64), pl_start=np.zeros(count, np.float64),
+                   pl_wsnbytes=np.zeros(count, np.int64), pl_route=np.zeros(count, np.int8))
+        self._check(self.lib.dgp_get_placements(self.h, offset, count, *[_ptr(out[k]) for k in (
+            "pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")]), "dgp_get_placements")
+        return out
+
+    def snapshots(self, max_rounds: int) -> dict:
+        W = self.n_workers
+        R = int(max_rounds)
+        out = dict(round_nplaced=np.zeros(R, np.int32), round_occ=np.zeros((R, W)),
+                   round_wnbytes=np.zeros((R, W), np.int64), round_nproc=np.zeros((R, W), np.int32),
+                   round_idle=np.zeros((R, W), np.uint8), round_sat=np.zeros((R, W), np.uint8),
+                   round_itc=np.zeros((R, W), np.uint8), round_nqueued=np.zeros(R, np.int32))
+        n = C.c_int64(0)
+        self._check(self.lib.dgp_get_snapshots(self.h, C.byref(n), *[_ptr(out[k]) for k in (
+            "round_nplaced", "round_occ", "round_wnbytes", "round_nproc", "round_idle", "round_sat", "round_itc",
+            "round_nqueued")]), "dgp_get_snapshots")
+        return {k: v[:n.value] for k, v in out.items()}
+
+    def task_states(self) -> np.ndarray:
+        st = np.zeros(self.n_tasks, np.uint8)
+        self._check(self.lib.dgp_get_task_states(self.h, _ptr(st)), "dgp_get_task_states")
+        return st
+
+    def set_timing(self, on: bool = True):
+        self._check(self.lib.dgp_set_timing(self.h, 1 if on else 0), "dgp_set_timing")
+
+    def kernel_times(self) -> dict:
+        ms = np.zeros(4)
+        n = np.zeros(4, np.int64)
+        self._check(self.lib.dgp_kernel_times(self.h, _ptr(ms), _ptr(n), 4), "dgp_kernel_times")
+        return {name: (float(ms[i]), int(n[i])) for i, name in enumerate(KERNEL_NAMES)}

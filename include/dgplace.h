@@ -1,0 +1,122 @@
+/* dgplace — MI355X-native placement engine for the dask.distributed scheduler hot path.
+ *
+ * C ABI of libdgplace.so (built from the HIP sources in distributed_amd/csrc for gfx950).
+ * Plain pointers and sizes only; every call returns 0 on success or a negative
+ * DGP_E* code, and dgp_last_error() describes the failure. Host buffers are
+ * borrowed for the duration of the call. One engine = one device + one HIP
+ * stream; calls must come from one host thread (the scheduler's event loop).
+ *
+ * Reference interfaces each entry point replaces (paths relative to
+ * /root/reference/distributed/):
+ *   dgp_set_workers       Scheduler.add_worker -> WorkerState(...) + check_idle_saturated
+ *                         (scheduler.py:4308-4441, :4418)
+ *   dgp_set_graph         Scheduler._create_taskstate_from_graph / _generate_taskstates
+ *                         (scheduler.py:4512-4611, :4753): TaskState graph, priorities,
+ *                         who_wants, TaskPrefix/TaskGroup membership, _rootish overrides
+ *   dgp_update_graph      the update_graph stimulus: every runnable task recommended
+ *                         "waiting" in priority order and transitioned (:4600-4651, :2045)
+ *   dgp_tasks_finished    Scheduler.handle_task_finished (:5783-5797) for a batch of
+ *                         completions, in order: stimulus_task_finished -> _transitions
+ *                         -> stimulus_queue_slots_maybe_opened (:5025, :4983)
+ *   dgp_run_rounds        the synthetic executor of the replay protocol: round k completes
+ *                         the tasks placed in round k-1 (tests/golden/gen_golden.py)
+ *   dgp_get_placements    the compute-task decisions (_add_to_processing :3199 /
+ *                         _task_to_msg :3421): task, worker, comm bytes, objective, route
+ *   dgp_steal_balance     WorkStealing.balance (stealing.py:401-503, _get_thief :532)
+ */
+#ifndef DGPLACE_H
+#define DGPLACE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DGP_ABI_VERSION 1
+
+#define DGP_OK 0
+#define DGP_E_ARG -1     /* invalid argument / shape */
+#define DGP_E_HIP -2     /* HIP runtime error (no device, OOM, launch failure) */
+#define DGP_E_STATE -3   /* call out of order (e.g. rounds before update_graph) */
+#define DGP_E_DEVICE -4  /* the device engine detected an inconsistent state */
+
+/* placement routes (which reference decide_worker path produced it) */
+#define DGP_ROUTE_NONROOTISH 0   /* decide_worker_non_rootish -> decide_worker (:2247, :8550) */
+#define DGP_ROUTE_ROOTISH_Q 1    /* decide_worker_rootish_queuing_enabled (:2195) */
+#define DGP_ROUTE_ROOTISH_NOQ 2  /* decide_worker_rootish_queuing_disabled (:2135) */
+#define DGP_ROUTE_FASTPATH 3     /* no-dependency fast path of decide_worker_non_rootish (:2283-2305) */
+
+/* task states (TaskState.state) */
+#define DGP_RELEASED 0
+#define DGP_WAITING 1
+#define DGP_PROCESSING 2
+#define DGP_QUEUED 3
+#define DGP_NO_WORKER 4
+#define DGP_MEMORY 5
+
+typedef struct dgp_engine dgp_engine;
+
+int dgp_abi_version(void);
+
+/* Create an engine on HIP device `device`. Returns NULL on failure (no device). */
+dgp_engine* dgp_create(int device);
+void dgp_destroy(dgp_engine* e);
+const char* dgp_last_error(const dgp_engine* e);
+
+/* distributed.scheduler.{bandwidth, default-data-size, unknown-task-duration,
+ * worker-saturation} (distributed.yaml:13,16,28,24). saturation may be +inf. */
+int dgp_set_config(dgp_engine* e, int64_t bandwidth, int64_t default_data_size, double unknown_duration,
+                   double saturation);
+
+/* Register n_workers running workers with the given thread counts (index = worker id). */
+int dgp_set_workers(dgp_engine* e, int32_t n_workers, const int32_t* nthreads);
+
+/* Upload the task graph (CSR dependencies, deduplicated). prio: unique sort keys of
+ * TaskState.priority (smaller runs first). wanted: task has a client future.
+ * rootish_override: -1 none, 0/1 = TaskState._rootish. Graph stays resident in HBM. */
+int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const int32_t* dep_idx,
+                  const int64_t* prio, const int32_t* prefix_id, int32_t n_prefixes,
+                  const double* prefix_default_duration, const int32_t* group_id, int32_t n_groups,
+                  const uint8_t* wanted, const int8_t* rootish_override);
+
+/* Per-task completion reports used by dgp_run_rounds: output nbytes and the compute
+ * startstops interval of the task-finished message. */
+int dgp_set_task_results(dgp_engine* e, const int64_t* nbytes, const double* start, const double* stop);
+
+/* Reset all dynamic state (tasks released, workers empty, placement log cleared). */
+int dgp_reset(dgp_engine* e);
+
+/* The update_graph stimulus. */
+int dgp_update_graph(dgp_engine* e);
+
+/* Run synthetic-executor rounds until no task is processing or max_rounds (<0: no
+ * limit) rounds ran. *n_rounds_out receives the number of rounds executed. */
+int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out);
+
+/* One batch of task-finished stimuli, processed in the given order. */
+int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* tasks, const int64_t* nbytes,
+                       const double* start, const double* stop);
+
+/* Placement log (run_id order). */
+int64_t dgp_num_placements(dgp_engine* e);
+int dgp_get_placements(dgp_engine* e, int64_t offset, int64_t count, int32_t* task, int32_t* worker,
+                       int64_t* comm_bytes, double* start_time, int64_t* ws_nbytes, int8_t* route);
+
+/* Per-round worker snapshots (state after update_graph and after each round). */
+int dgp_enable_snapshots(dgp_engine* e, int64_t max_rounds);
+int dgp_get_snapshots(dgp_engine* e, int64_t* n_rounds, int32_t* nplaced, double* occupancy, int64_t* ws_nbytes,
+                      int32_t* nprocessing, uint8_t* idle, uint8_t* saturated, uint8_t* idle_task_count,
+                      int32_t* nqueued);
+int dgp_get_task_states(dgp_engine* e, uint8_t* state);
+
+/* Device timing of the engine's kernels over the work since the last reset:
+ * for kernel id k (0 frontier_release, 1 candidate_commbytes, 2 commit, 3 other)
+ * total milliseconds (HIP events on the engine's stream) and launch count. */
+int dgp_kernel_times(dgp_engine* e, double* ms, int64_t* launches, int32_t n);
+int dgp_set_timing(dgp_engine* e, int enabled);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DGPLACE_H */

@@ -1,0 +1,78 @@
+"""HIP engine parity (needs an MI355X).
+
+* every golden fixture (produced by the reference SchedulerState itself) must be
+  reproduced bit-for-bit: the placement log (task, worker, comm bytes, fp64
+  objective, ws.nbytes, route) and every per-round worker snapshot;
+* larger synthetic graphs must match the oracle (oracle/replay.cpp) bit-for-bit.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden_files
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+PL_KEYS = ("pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")
+ROUND_KEYS = ("round_nplaced", "round_occ", "round_wnbytes", "round_nproc", "round_idle", "round_sat",
+              "round_itc", "round_nqueued")
+
+
+def assert_same(out, exp, keys):
+    for k in keys:
+        a, b = np.asarray(out[k]), np.asarray(exp[k])
+        assert a.shape == b.shape, (k, a.shape, b.shape)
+        bad = np.nonzero(a.reshape(-1) != b.reshape(-1))[0]
+        assert len(bad) == 0, (f"{k}: {len(bad)} mismatches, first at flat index {bad[0]}: "
+                               f"{a.reshape(-1)[bad[0]]!r} vs {b.reshape(-1)[bad[0]]!r}")
+
+
+@pytest.fixture(scope="module")
+def engine_cls():
+    from distributed_amd.engine import PlacementEngine
+
+    return PlacementEngine
+
+
+@pytest.mark.parametrize("name", golden_files())
+def test_engine_matches_reference_fixture(engine_cls, name):
+    g, cfg, exp, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
+    R = len(exp["round_nplaced"]) + 2
+    with engine_cls(0) as eng:
+        eng.load(g, cfg, snapshots=R)
+        eng.replay()
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+@pytest.mark.parametrize("sat", [1.1, "inf"])
+@pytest.mark.parametrize("n,w", [(100_000, 1024), (30_000, 4096)])
+def test_engine_matches_oracle_random_dag(engine_cls, n, w, sat):
+    from distributed_amd import graphs
+
+    g = graphs.random_dag(n, w, seed=42)
+    cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": sat}
+    ref = oracle.replay(g, cfg, snapshots=False)
+    with engine_cls(0) as eng:
+        eng.load(g, cfg)
+        eng.replay()
+        out = eng.placements()
+    assert_same(out, ref, PL_KEYS)
+
+
+def test_engine_matches_oracle_tree_reduce(engine_cls):
+    from distributed_amd import graphs
+
+    g = graphs.map_tree_reduce(200_000, 2048, seed=3)
+    cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": 1.1}
+    ref = oracle.replay(g, cfg, snapshots=False)
+    with engine_cls(0) as eng:
+        eng.load(g, cfg)
+        eng.replay()
+        out = eng.placements()
+    assert_same(out, ref, PL_KEYS)
