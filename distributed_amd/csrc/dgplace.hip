@@ -575,7 +575,7 @@ __device__ void completion_stimulus(const Dev& D, int t, unsigned long long key)
   double duration = D.res_stop[t] - D.res_start[t];
   double old = D.pdur[p];
   D.pdur[p] = old < 0 ? duration : 0.5 * duration + 0.5 * old;
-  D.cur_nbytes[t] = D.res_nbytes[t];  // set_nbytes (who_has is empty)
+  // set_nbytes (:1480) was applied by k_frontier_release
   // _exit_processing_common -> WorkerState.remove_from_processing :759-771
   D.proc_on[t] = -1;
   wdict_dec(D, w, p);
@@ -590,11 +590,9 @@ __device__ void completion_stimulus(const Dev& D, int t, unsigned long long key)
     }
   }
   check_idle_saturated(D, w);
-  // _add_to_memory :3283-3335 — add_replica
-  if (!holds(D, t, w)) {
-    D.holders[(size_t)t * D.WB + (w >> 6)] |= 1ull << (w & 63);
-    D.w_nbytes[w] += get_nbytes(D, t);
-  }
+  // _add_to_memory :3283-3335 — add_replica (the who_has bit was published by
+  // k_frontier_release; the replica is new, so ws.nbytes grows by get_nbytes)
+  D.w_nbytes[w] += get_nbytes(D, t);
   D.state[t] = S_MEMORY;
   // releases (popped before the frontier: LIFO of the recommendations dict)
   for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
@@ -646,6 +644,12 @@ __global__ void k_frontier_release(Dev D, const int32_t* L, int64_t n, unsigned 
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     int t = L[j];
     unsigned long long key = round_tag | (unsigned long long)j;
+    // the replica this completion creates (who_has / nbytes) is known before the ordered
+    // commit: publish it now so k_candidate_commbytes sees it. No stimulus earlier in the
+    // round can read it (only t's dependents do, and they become ready at j or later).
+    int w = D.proc_on[t];
+    if (w >= 0) atomicOr(&D.holders[(size_t)t * D.WB + (w >> 6)], 1ull << (w & 63));
+    D.cur_nbytes[t] = D.res_nbytes[t];
     for (int64_t k = D.dpt_ptr[t]; k < D.dpt_ptr[t + 1]; k++) {
       int x = D.dpt_idx[k];
       atomicMax(&D.ready_key[x], key);
