@@ -822,6 +822,9 @@ struct dgp_engine {
   double kms[4] = {0, 0, 0, 0};
   int64_t klaunch[4] = {0, 0, 0, 0};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> evpool;          // (start, stop) pairs recorded around launches
+  std::vector<int> evkind;                 // kernel id per recorded pair
+  size_t evused = 0;
   int32_t* d_batch = nullptr;
   int64_t batch_cap = 0;
 };
@@ -871,17 +874,43 @@ int check_device_error(dgp_engine* e) {
   return 0;
 }
 
+// resolve recorded (start, stop) event pairs into per-kernel totals
+int resolve_timing(dgp_engine* e) {
+  if (e->evused == 0) return 0;
+  HIPCHK(e, hipEventSynchronize(e->evpool[2 * (e->evused - 1) + 1]));
+  for (size_t i = 0; i < e->evused; i++) {
+    float ms = 0;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->evpool[2 * i], e->evpool[2 * i + 1]));
+    e->kms[e->evkind[i]] += ms;
+  }
+  e->evused = 0;
+  return 0;
+}
+
 template <class F>
 int timed_launch(dgp_engine* e, int kid, F&& launch) {
-  if (e->timing) HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+  size_t slot = e->evused;
+  if (e->timing) {
+    if (slot == (1u << 15)) {
+      if (int rc = resolve_timing(e)) return rc;
+      slot = 0;
+    }
+    if (2 * slot + 1 >= e->evpool.size()) {
+      hipEvent_t a, b;
+      HIPCHK(e, hipEventCreate(&a));
+      HIPCHK(e, hipEventCreate(&b));
+      e->evpool.push_back(a);
+      e->evpool.push_back(b);
+      e->evkind.push_back(0);
+    }
+    e->evkind[slot] = kid;
+    HIPCHK(e, hipEventRecord(e->evpool[2 * slot], e->stream));
+  }
   launch();
   HIPCHK(e, hipGetLastError());
   if (e->timing) {
-    HIPCHK(e, hipEventRecord(e->ev1, e->stream));
-    HIPCHK(e, hipEventSynchronize(e->ev1));
-    float ms = 0;
-    HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
-    e->kms[kid] += ms;
+    HIPCHK(e, hipEventRecord(e->evpool[2 * slot + 1], e->stream));
+    e->evused = slot + 1;
   }
   e->klaunch[kid]++;
   return 0;
@@ -977,6 +1006,7 @@ void dgp_destroy(dgp_engine* e) {
   (void)hipFree(e->ctl);
   (void)hipEventDestroy(e->ev0);
   (void)hipEventDestroy(e->ev1);
+  for (hipEvent_t ev : e->evpool) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1210,6 +1240,7 @@ int dgp_reset(dgp_engine* e) {
   e->graph_done = false;
   e->rounds_done = 0;
   e->round_start = e->round_end = 0;
+  e->evused = 0;
   for (int k = 0; k < 4; k++) {
     e->kms[k] = 0;
     e->klaunch[k] = 0;
@@ -1348,6 +1379,7 @@ int dgp_get_task_states(dgp_engine* e, uint8_t* state) {
 
 int dgp_kernel_times(dgp_engine* e, double* ms, int64_t* launches, int32_t n) {
   if (!e) return DGP_E_ARG;
+  if (int rc = resolve_timing(e)) return rc;
   for (int k = 0; k < n && k < 4; k++) {
     if (ms) ms[k] = e->kms[k];
     if (launches) launches[k] = e->klaunch[k];
