@@ -36,6 +36,7 @@ SIGNATURES = {
     "dgp_get_task_states": (C.c_int, [_P, _P]),
     "dgp_kernel_times": (C.c_int, [_P, _P, _P, C.c_int32]),
     "dgp_set_timing": (C.c_int, [_P, C.c_int]),
+    "dgp_stats": (C.c_int, [_P, _P, C.c_int32]),
 }
 
 ABI_VERSION = 1

@@ -7,6 +7,7 @@ import subprocess
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 SRC = [os.path.join(PKG, "csrc", "dgplace.hip")]
+DEPS = [os.path.join(PKG, "csrc", "dgp_device.h")]
 OUT = os.path.join(PKG, "libdgplace.so")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 # -ffp-contract=off: no fused multiply-add, so fp64 results round exactly like the
@@ -16,7 +17,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fn
 
 
 def build(force: bool = False) -> str:
-    newest = max(os.path.getmtime(p) for p in SRC + [os.path.join(PKG, "..", "include", "dgplace.h")])
+    newest = max(os.path.getmtime(p) for p in SRC + DEPS + [os.path.join(PKG, "..", "include", "dgplace.h")])
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= newest:
         return OUT
     tmp = OUT + ".tmp"

@@ -1,0 +1,1625 @@
+// dgplace device side: state layout, the reference's placement semantics as device
+// functions, and the kernels of one replay round. Included by dgplace.hip only.
+//
+// Reference: /root/reference/distributed/scheduler.py (SchedulerState) unless noted.
+// Arithmetic follows CPython's evaluation order of the reference expressions; the
+// translation unit is compiled with -ffp-contract=off (no fused multiply-add).
+//
+// Round structure (one wave of completions L[0..n)):
+//   k_round_begin         reset per-round counters, n = |L|
+//   k_frontier_release    all completions in parallel: publish the new replicas, atomic
+//                         decrement of dependents' waiting_on and dependencies' waiters,
+//                         tag every task with the position j of the completion that
+//                         releases it (_add_to_memory :3298-3314)
+//   k_candidate_commbytes one wave per newly ready task: candidate union + exact comm
+//                         bytes per candidate (decide_worker :8571-8587, worker_objective
+//                         :3136-3138) — HBM-bound gather of replica bitset rows
+//   k_events              per completion stimulus j: the workers it may touch (its own,
+//                         the holders of dependencies it releases, the candidates of the
+//                         tasks it releases) and whether it needs global state
+//   k_commit              ordered commit by deterministic reservation: in every step each
+//                         pending stimulus reserves its workers with atomicMin(owner, j);
+//                         a stimulus whose workers are all its own has no earlier pending
+//                         stimulus touching them and commits concurrently with the others
+//                         (identical to the sequential order). Stimuli that read global
+//                         state (rootish / no-dependency placements, queue refill near
+//                         exhaustion) run alone, cooperatively, in order.
+// SchedulerState-global quantities that only feed check_idle_saturated's idle/saturated
+// sets (total_occupancy :1877) are kept as an ordered record log and folded in by the
+// log walker (k_walk) whenever a consumer needs them: before a global stimulus, for
+// snapshots, and at the end of a replay.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dgp {
+
+constexpr int PMAX = 8;        // distinct prefixes in one worker's task_prefix_count
+constexpr int PMAX_G = 64;     // distinct prefixes in _task_prefix_count_global
+constexpr int TOUCH_MAX = 24;  // workers one stimulus may reserve (more -> runs as global)
+constexpr int CTA = 1024;      // threads of the commit / dispatch workgroup
+constexpr int FL_MAX = 256;    // frontier tasks one global stimulus stages in LDS per chunk
+
+enum : uint8_t { S_RELEASED = 0, S_WAITING, S_PROCESSING, S_QUEUED, S_NO_WORKER, S_MEMORY };
+enum : uint8_t { TF_WANTED = 1, TF_ROOTISH = 2 };
+enum : uint8_t { WF_IDLE = 1, WF_SAT = 2, WF_ITC = 4 };
+enum : uint8_t { EV_GLOBAL = 1 };
+enum : int32_t { REC_NONE = 0, REC_COMPLETE = 1, REC_PLACE = 2 };
+enum : int { ERR_NONE = 0, ERR_PREFIX_CAP, ERR_NO_CANDIDATES, ERR_BAD_STATE, ERR_QUEUE, ERR_POOL, ERR_GPREFIX_CAP,
+             ERR_REC_CAP, ERR_STAGE_CAP, ERR_NO_WORKER };
+enum : int { ROUTE_NONROOTISH = 0, ROUTE_ROOTISH_Q = 1, ROUTE_ROOTISH_NOQ = 2, ROUTE_FASTPATH = 3 };
+
+// device-resident control block
+struct Ctl {
+  unsigned long long n_placed;    // placement log length (== next run_id)
+  unsigned long long n_frontier;  // tasks released by the current round's completions
+  unsigned long long pool_used;   // candidate pool entries used by the current round
+  unsigned long long rec_used;    // record log length
+  long long round_start, round_n; // current round = placement log slice
+  long long round_counter;        // tags ready/release keys
+  long long qhead, qlen;          // SchedulerState.queued (sorted array slice)
+  long long n_tasks;              // SchedulerState.n_tasks
+  long long n_itc;                // |idle_task_count| (eager)
+  long long itc_slots;            // sum of _task_slots_available over idle_task_count (eager)
+  long long n_unrunnable;
+  // ---- walker state: SchedulerState as of record walk_pos
+  unsigned long long walk_pos;
+  long long n_idle, n_sat;        // |idle|, |saturated|
+  double g_netocc;                // _network_occ_global
+  int g_plen;                     // _task_prefix_count_global, insertion ordered
+  int g_pfx[PMAX_G];
+  long long g_pcnt[PMAX_G];
+  // ----
+  long long rounds_nonempty;      // rounds that completed at least one task
+  const int32_t* round_L;         // completion list of the current round
+  long long dr_steps;             // deterministic-reservation steps (diagnostics)
+  long long n_global_events;
+  int error;
+  int err_task;
+};
+
+// one sub-step of a stimulus that changes SchedulerState-global counts and is followed
+// by check_idle_saturated(w) (completion: remove_from_processing; placement: add_to_processing)
+struct Rec {
+  int32_t kind;
+  int32_t task;
+  int32_t w;
+  int32_t prefix;
+  int64_t dnet;  // change of _network_occ_global
+  double occ;    // WorkerState.occupancy of w at its check
+  int32_t nproc; // len(w.processing) at its check
+  int32_t pad;
+};
+
+struct Dev {
+  int32_t N, W, WB, P, G, Wp;
+  int64_t bandwidth, default_data_size;
+  double unknown_duration, saturation;
+  int32_t sat_inf;
+  int64_t total_nthreads;
+  // graph (static)
+  const int64_t* dep_ptr;
+  const int32_t* dep_idx;
+  const int64_t* dpt_ptr;
+  const int32_t* dpt_idx;  // dependents, each row in ascending priority
+  const int64_t* prio;
+  const int32_t* prefix;
+  const int32_t* group;
+  const uint8_t* tflags;
+  const int32_t* order;  // all tasks in ascending priority
+  // synthetic completion reports
+  int64_t* res_nbytes;
+  double* res_start;
+  double* res_stop;
+  // task state
+  uint8_t* state;
+  int32_t* remaining;  // |waiting_on|
+  int32_t* waiters;    // |waiters|
+  int32_t* proc_on;    // processing_on, -1 when not processing
+  int64_t* cur_nbytes;
+  unsigned long long* holders;  // who_has bitsets [N][WB]
+  unsigned long long* ready_key;
+  unsigned long long* release_key;
+  // candidate pool of newly ready tasks
+  int64_t* cand_off;
+  int32_t* cand_n;
+  int32_t* pool_w;
+  int64_t* pool_comm;
+  int64_t pool_cap;
+  int32_t* frontier;
+  // workers
+  int32_t* w_nthreads;
+  int32_t* w_cap;  // max(ceil(saturation * nthreads), 1)
+  int32_t* w_nproc;
+  int32_t* w_plen;
+  int32_t* w_pfx;
+  int32_t* w_pcnt;
+  int64_t* w_netocc;
+  int64_t* w_nbytes;
+  uint8_t* w_flags;
+  int64_t* w_itcslots;
+  unsigned long long* w_lastcheck;  // record index of the worker's latest check
+  double* t_key;                    // tournament tree over idle_task_count
+  int32_t* t_idx;
+  // prefixes
+  double* pdur_cur;   // TaskPrefix.duration_average after all committed completions
+  double* pdur_walk;  // ... as of the walker position
+  double* pmaxexec;   // TaskPrefix.max_exec_time (no heartbeats in the replay: -1)
+  double* durv;       // per-round table: durations in effect at stimulus j, [n][P]
+  // groups
+  int64_t* g_size;
+  int64_t* g_relwait;  // states["released"] + states["waiting"]
+  int64_t* g_left;     // last_worker_tasks_left
+  int32_t* g_lastw;    // last_worker
+  // queue
+  int32_t* qarr;
+  // placement log
+  int32_t* pl_task;
+  int32_t* pl_worker;
+  int64_t* pl_comm;
+  double* pl_start;
+  int64_t* pl_wsnbytes;
+  int8_t* pl_route;
+  // record log
+  Rec* rec;
+  int64_t rec_cap;
+  // per-round stimulus metadata
+  int32_t* ev_w;
+  int32_t* ev_nf;
+  uint8_t* ev_flags;
+  int32_t* ev_ntouch;
+  int32_t* ev_touch;
+  int64_t* ev_plbase;
+  int64_t* ev_recbase;
+  int32_t* ev_npl;
+  int32_t* ev_pops;
+  int32_t* ev_popmax;
+  // per-round placement staging
+  int32_t* st_task;
+  int32_t* st_worker;
+  int64_t* st_comm;
+  double* st_start;
+  int64_t* st_wsnbytes;
+  int8_t* st_route;
+  int64_t st_cap;
+  // ready list of update_graph
+  int32_t* ready;
+  // snapshots
+  int64_t snap_cap;
+  int32_t* snap_nplaced;
+  double* snap_occ;
+  int64_t* snap_nbytes;
+  int32_t* snap_nproc;
+  uint8_t* snap_flags;
+  int32_t* snap_nqueued;
+  Ctl* ctl;
+};
+
+// ============================================================== small helpers
+
+__device__ __forceinline__ int64_t get_nbytes(const Dev& D, int t) {  // TaskState.get_nbytes :1477
+  int64_t v = D.cur_nbytes[t];
+  return v >= 0 ? v : D.default_data_size;
+}
+__device__ __forceinline__ bool holds(const Dev& D, int d, int w) {
+  return (D.holders[(size_t)d * D.WB + (w >> 6)] >> (w & 63)) & 1ull;
+}
+__device__ __forceinline__ void set_error(const Dev& D, int code, int task) {
+  if (atomicCAS(&D.ctl->error, 0, code) == 0) D.ctl->err_task = task;
+}
+__device__ __forceinline__ double prefix_duration(const Dev& D, const double* dur, int p) {  // :1892-1899
+  double d = dur[p];
+  if (d < 0) {
+    if (D.pmaxexec[p] > 0)
+      d = 2 * D.pmaxexec[p];
+    else
+      d = D.unknown_duration;
+  }
+  return d;
+}
+// WorkerState.occupancy :840 -> _calc_occupancy :1884-1903 (dict insertion order)
+__device__ double occupancy(const Dev& D, int w, const double* dur) {
+  double res = 0.0;
+  const int n = D.w_plen[w];
+  const int* pf = D.w_pfx + (size_t)w * PMAX;
+  const int* pc = D.w_pcnt + (size_t)w * PMAX;
+  for (int i = 0; i < n; i++) res += prefix_duration(D, dur, pf[i]) * (double)pc[i];
+  return res + (double)D.w_netocc[w] / (double)D.bandwidth;
+}
+// SchedulerState.total_occupancy :1877 at the walker position
+__device__ double total_occupancy_walk(const Dev& D) {
+  const Ctl* c = D.ctl;
+  double res = 0.0;
+  for (int i = 0; i < c->g_plen; i++) res += prefix_duration(D, D.pdur_walk, c->g_pfx[i]) * (double)c->g_pcnt[i];
+  return res + c->g_netocc / (double)D.bandwidth;
+}
+__device__ __forceinline__ double ewma(double old, double duration) {  // TaskPrefix.add_duration :977-985
+  return old < 0 ? duration : 0.5 * duration + 0.5 * old;
+}
+
+// insertion-ordered {prefix: count} dicts with delete-on-zero (:733-784)
+__device__ bool wdict_inc(const Dev& D, int w, int p) {
+  int* pf = D.w_pfx + (size_t)w * PMAX;
+  int* pc = D.w_pcnt + (size_t)w * PMAX;
+  int n = D.w_plen[w];
+  for (int i = 0; i < n; i++)
+    if (pf[i] == p) {
+      pc[i]++;
+      return true;
+    }
+  if (n == PMAX) return false;
+  pf[n] = p;
+  pc[n] = 1;
+  D.w_plen[w] = n + 1;
+  return true;
+}
+__device__ void wdict_dec(const Dev& D, int w, int p) {
+  int* pf = D.w_pfx + (size_t)w * PMAX;
+  int* pc = D.w_pcnt + (size_t)w * PMAX;
+  int n = D.w_plen[w];
+  for (int i = 0; i < n; i++)
+    if (pf[i] == p) {
+      if (--pc[i] == 0) {
+        for (int k = i + 1; k < n; k++) {
+          pf[k - 1] = pf[k];
+          pc[k - 1] = pc[k];
+        }
+        D.w_plen[w] = n - 1;
+      }
+      return;
+    }
+}
+__device__ bool gdict_inc(const Dev& D, int p) {
+  Ctl* c = D.ctl;
+  for (int i = 0; i < c->g_plen; i++)
+    if (c->g_pfx[i] == p) {
+      c->g_pcnt[i]++;
+      return true;
+    }
+  if (c->g_plen == PMAX_G) return false;
+  c->g_pfx[c->g_plen] = p;
+  c->g_pcnt[c->g_plen] = 1;
+  c->g_plen++;
+  return true;
+}
+__device__ void gdict_dec(const Dev& D, int p) {
+  Ctl* c = D.ctl;
+  for (int i = 0; i < c->g_plen; i++)
+    if (c->g_pfx[i] == p) {
+      if (--c->g_pcnt[i] == 0) {
+        for (int k = i + 1; k < c->g_plen; k++) {
+          c->g_pfx[k - 1] = c->g_pfx[k];
+          c->g_pcnt[k - 1] = c->g_pcnt[k];
+        }
+        c->g_plen--;
+      }
+      return;
+    }
+}
+
+__device__ __forceinline__ int64_t task_slots_available(const Dev& D, int w) {  // :8762-8767
+  return (int64_t)D.w_cap[w] - (int64_t)D.w_nproc[w];  // len(long_running) == 0 in the replay
+}
+__device__ __forceinline__ bool worker_full(const Dev& D, int w) {  // :8770-8773
+  if (D.sat_inf) return false;
+  return task_slots_available(D, w) <= 0;
+}
+
+// ===================================================== idle_task_count (eager part)
+
+// tournament tree: argmin over idle_task_count of (len(processing)/nthreads, index)
+// (decide_worker_rootish_queuing_enabled :2230-2233). Only global stimuli use it; it is
+// rebuilt cooperatively before they run and then maintained by their single lane.
+__device__ void tree_update(const Dev& D, int w) {
+  double key = (D.w_flags[w] & WF_ITC) ? (double)D.w_nproc[w] / (double)D.w_nthreads[w] : INFINITY;
+  int pos = D.Wp + w;
+  D.t_key[pos] = key;
+  D.t_idx[pos] = w;
+  double k = key;
+  int i = w;
+  while (pos > 1) {
+    int sib = pos ^ 1;
+    double sk = D.t_key[sib];
+    int si = D.t_idx[sib];
+    if (sk < k || (sk == k && si < i)) {
+      k = sk;
+      i = si;
+    }
+    pos >>= 1;
+    D.t_key[pos] = k;
+    D.t_idx[pos] = i;
+  }
+}
+__device__ void tree_rebuild_coop(const Dev& D) {  // all threads of the block
+  for (int i = threadIdx.x; i < D.Wp; i += blockDim.x) {
+    int pos = D.Wp + i;
+    bool on = i < D.W && (D.w_flags[i] & WF_ITC);
+    D.t_key[pos] = on ? (double)D.w_nproc[i] / (double)D.w_nthreads[i] : INFINITY;
+    D.t_idx[pos] = i;
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (int half = D.Wp >> 1; half >= 1; half >>= 1) {
+    for (int pos = half + threadIdx.x; pos < 2 * half; pos += blockDim.x) {
+      double a = D.t_key[2 * pos], b = D.t_key[2 * pos + 1];
+      int ia = D.t_idx[2 * pos], ib = D.t_idx[2 * pos + 1];
+      bool right = b < a || (b == a && ib < ia);
+      D.t_key[pos] = right ? b : a;
+      D.t_idx[pos] = right ? ib : ia;
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
+// the idle_task_count part of check_idle_saturated (:2992-2995): depends only on w
+__device__ void itc_check(const Dev& D, int w, bool maintain_tree) {
+  bool on = !worker_full(D, w);
+  uint8_t fl = D.w_flags[w];
+  bool was = (fl & WF_ITC) != 0;
+  if (on != was) {
+    D.w_flags[w] = on ? (fl | WF_ITC) : (fl & ~WF_ITC);
+    atomicAdd((unsigned long long*)&D.ctl->n_itc, on ? 1ull : (unsigned long long)-1ll);
+  }
+  int64_t contrib = on ? task_slots_available(D, w) : 0;
+  int64_t delta = contrib - D.w_itcslots[w];
+  if (delta) atomicAdd((unsigned long long*)&D.ctl->itc_slots, (unsigned long long)delta);
+  D.w_itcslots[w] = contrib;
+  if (maintain_tree) tree_update(D, w);
+}
+
+// ====================================================== record log and its walker
+
+// write the record of one sub-step and note it as w's latest check_idle_saturated
+__device__ void emit(const Dev& D, int64_t slot, int32_t kind, int32_t task, int32_t w, int32_t prefix, int64_t dnet,
+                     const double* dur) {
+  if (slot >= D.rec_cap) {
+    set_error(D, ERR_REC_CAP, task);
+    return;
+  }
+  Rec r;
+  r.kind = kind;
+  r.task = task;
+  r.w = w;
+  r.prefix = prefix;
+  r.dnet = dnet;
+  r.occ = occupancy(D, w, dur);
+  r.nproc = D.w_nproc[w];
+  r.pad = 0;
+  D.rec[slot] = r;
+  D.w_lastcheck[w] = (unsigned long long)slot;
+}
+
+// the idle / saturated part of check_idle_saturated (:2949-2991 + is_unoccupied :2997)
+__device__ void walk_flags(const Dev& D, int w, double occ, int64_t p) {
+  Ctl* c = D.ctl;
+  int64_t nt = D.w_nthreads[w];
+  uint8_t fl = D.w_flags[w];
+  bool idle = false, sat = false;
+  double avg = -1;
+  if (p < nt) {
+    idle = true;
+  } else {
+    avg = total_occupancy_walk(D) / (double)D.total_nthreads;
+    idle = occ < (double)nt * avg / 2;
+  }
+  if (!idle && p > nt) {
+    double pending = occ * (double)(p - nt) / (double)(p * nt);
+    if (0.4 < pending) {
+      if (avg < 0) avg = total_occupancy_walk(D) / (double)D.total_nthreads;
+      sat = pending > 1.9 * avg;
+    }
+  }
+  if (idle != ((fl & WF_IDLE) != 0)) c->n_idle += idle ? 1 : -1;
+  if (sat != ((fl & WF_SAT) != 0)) c->n_sat += sat ? 1 : -1;
+  D.w_flags[w] = (fl & ~(WF_IDLE | WF_SAT)) | (idle ? WF_IDLE : 0) | (sat ? WF_SAT : 0);
+}
+
+// fold records [walk_pos, end) into the walker state (single lane)
+__device__ void walk_to(const Dev& D, unsigned long long end) {
+  Ctl* c = D.ctl;
+  for (unsigned long long i = c->walk_pos; i < end; i++) {
+    Rec r = D.rec[i];
+    if (r.kind == REC_NONE) continue;
+    if (r.kind == REC_COMPLETE) {
+      D.pdur_walk[r.prefix] = ewma(D.pdur_walk[r.prefix], D.res_stop[r.task] - D.res_start[r.task]);
+      gdict_dec(D, r.prefix);
+    } else {
+      if (!gdict_inc(D, r.prefix)) set_error(D, ERR_GPREFIX_CAP, r.task);
+    }
+    c->g_netocc += (double)r.dnet;
+    if (D.w_lastcheck[r.w] == i) walk_flags(D, r.w, r.occ, r.nproc);
+  }
+  if (end > c->walk_pos) c->walk_pos = end;
+}
+
+// ============================================================ objective & needs
+
+struct Obj {  // worker_objective tuple (:3131-3146) + canonical worker-index tie-break
+  double start;
+  int64_t nbytes;
+  int32_t w;
+};
+__device__ __forceinline__ bool obj_less(const Obj& a, const Obj& b) {
+  if (a.start != b.start) return a.start < b.start;
+  if (a.nbytes != b.nbytes) return a.nbytes < b.nbytes;
+  return a.w < b.w;
+}
+__device__ __forceinline__ Obj objective(const Dev& D, int w, int64_t comm, const double* dur) {
+  double stack_time = occupancy(D, w, dur) / (double)D.w_nthreads[w];
+  double start_time = stack_time + (double)comm / (double)D.bandwidth;
+  return Obj{start_time, D.w_nbytes[w], w};
+}
+__device__ int64_t comm_bytes(const Dev& D, int t, int w) {  // worker_objective's sum :3136-3138
+  int64_t comm = 0;
+  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+    int d = D.dep_idx[k];
+    if (!holds(D, d, w)) comm += get_nbytes(D, d);
+  }
+  return comm;
+}
+// needs_what[w][d] > 0 <=> another dependent of d is processing on w (w does not hold d):
+// WorkerState._inc/_dec_needs_replica (:800-823) without a per-worker map
+__device__ bool needed_elsewhere(const Dev& D, int d, int w, int except) {
+  for (int64_t k = D.dpt_ptr[d]; k < D.dpt_ptr[d + 1]; k++) {
+    int x = D.dpt_idx[k];
+    if (x != except && D.proc_on[x] == w) return true;
+  }
+  return false;
+}
+
+// ================================================================= mutations
+
+// processing->memory of t on w (:2366-2442) up to the frontier; returns the record slot used
+__device__ void do_completion(const Dev& D, int t, int w, int64_t rslot, const double* dur) {
+  int p = D.prefix[t];
+  D.proc_on[t] = -1;  // _exit_processing_common -> remove_from_processing :759-771
+  wdict_dec(D, w, p);
+  D.w_nproc[w]--;
+  int64_t dnet = 0;
+  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+    int d = D.dep_idx[k];
+    if (!holds(D, d, w) && !needed_elsewhere(D, d, w, t)) {
+      int64_t nb = get_nbytes(D, d);
+      D.w_netocc[w] -= nb;
+      dnet -= nb;
+    }
+  }
+  emit(D, rslot, REC_COMPLETE, t, w, p, dnet, dur);  // check_idle_saturated(ws) :3276
+  // add_replica (:3148): the who_has bit and nbytes were published by k_frontier_release
+  D.w_nbytes[w] += get_nbytes(D, t);
+  D.state[t] = S_MEMORY;
+}
+
+// _transition_memory_released (:2444-2505) -> remove_all_replicas (:3161-3171)
+__device__ void release_task(const Dev& D, int t) {
+  int64_t nb = get_nbytes(D, t);
+  unsigned long long* row = D.holders + (size_t)t * D.WB;
+  for (int wd = 0; wd < D.WB; wd++) {
+    unsigned long long bits = row[wd];
+    while (bits) {
+      int b = __ffsll((long long)bits) - 1;
+      bits &= bits - 1;
+      D.w_nbytes[wd * 64 + b] -= nb;
+    }
+    row[wd] = 0;
+  }
+  D.state[t] = S_RELEASED;
+  atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], 1ull);
+}
+
+// the releases of completion stimulus (t, key): popped before the frontier (LIFO)
+__device__ void do_releases(const Dev& D, int t, unsigned long long key) {
+  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+    int d = D.dep_idx[k];
+    if (D.release_key[d] == key && D.waiters[d] == 0 && !(D.tflags[d] & TF_WANTED) && D.state[d] == S_MEMORY)
+      release_task(D, d);
+  }
+  if (D.dpt_ptr[t + 1] == D.dpt_ptr[t] && !(D.tflags[t] & TF_WANTED)) release_task(D, t);
+}
+
+__device__ __forceinline__ bool is_frontier(const Dev& D, int x, unsigned long long key) {
+  return D.ready_key[x] == key && D.state[x] == S_WAITING && D.remaining[x] == 0;
+}
+
+// _add_to_processing :3199-3256 (+ WorkerState.add_to_processing :733): record, mutate
+__device__ void do_place(const Dev& D, int t, int w, int route, int64_t comm, int64_t plslot, int64_t rslot,
+                         const double* dur, bool maintain_tree) {
+  if (comm < 0) comm = comm_bytes(D, t, w);
+  Obj o = objective(D, w, comm, dur);
+  D.st_task[plslot] = t;
+  D.st_worker[plslot] = w;
+  D.st_comm[plslot] = comm;
+  D.st_start[plslot] = o.start;
+  D.st_wsnbytes[plslot] = D.w_nbytes[w];
+  D.st_route[plslot] = (int8_t)route;
+  int p = D.prefix[t];
+  if (!wdict_inc(D, w, p)) set_error(D, ERR_PREFIX_CAP, t);
+  D.w_nproc[w]++;
+  int64_t dnet = 0;
+  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+    int d = D.dep_idx[k];
+    if (!holds(D, d, w) && !needed_elsewhere(D, d, w, t)) {
+      int64_t nb = get_nbytes(D, d);
+      D.w_netocc[w] += nb;
+      dnet += nb;
+    }
+  }
+  if (t >= 0) {
+    D.proc_on[t] = w;
+    if (D.state[t] == S_WAITING) atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], (unsigned long long)-1ll);
+    D.state[t] = S_PROCESSING;
+  }
+  emit(D, rslot, REC_PLACE, t, w, p, dnet, dur);  // check_idle_saturated(ws) :3212
+  itc_check(D, w, maintain_tree);
+  atomicAdd((unsigned long long*)&D.ctl->n_tasks, 1ull);
+}
+
+// ======================================================= local stimulus (one lane)
+
+// a completion stimulus whose placements only read the workers it reserved
+__device__ void exec_local(const Dev& D, int j, int t, int w, unsigned long long key, const double* dur,
+                           int64_t plbase, int64_t recbase, int popmax, int pop_prefix) {
+  do_completion(D, t, w, recbase, dur);
+  itc_check(D, w, false);
+  do_releases(D, t, key);
+  int64_t npl = 0, nrec = 1;
+  for (int64_t k = D.dpt_ptr[t]; k < D.dpt_ptr[t + 1]; k++) {
+    int x = D.dpt_idx[k];
+    if (!is_frontier(D, x, key)) continue;
+    // decide_worker (:8550-8593) over the precomputed candidates
+    int n = D.cand_n[x];
+    int64_t off = D.cand_off[x];
+    if (n <= 0) {
+      set_error(D, ERR_NO_CANDIDATES, x);
+      return;
+    }
+    int best = D.pool_w[off];
+    int64_t bcomm = D.pool_comm[off];
+    if (n > 1) {
+      Obj bo = objective(D, best, bcomm, dur);
+      for (int i = 1; i < n; i++) {
+        Obj o = objective(D, D.pool_w[off + i], D.pool_comm[off + i], dur);
+        if (obj_less(o, bo)) {
+          bo = o;
+          best = o.w;
+          bcomm = D.pool_comm[off + i];
+        }
+      }
+    }
+    do_place(D, x, best, ROUTE_NONROOTISH, bcomm, plbase + npl, recbase + nrec, dur, false);
+    npl++;
+    nrec++;
+  }
+  // stimulus_queue_slots_maybe_opened (:4983): with a non-empty queue every other
+  // worker is full, so the open slots are w's; the queued tasks are resolved in order later
+  int pops = 0;
+  if (popmax > 0 && (D.w_flags[w] & WF_ITC)) {
+    int64_t slots = task_slots_available(D, w);
+    for (int64_t i = 0; i < slots && pops < popmax; i++) {
+      // place a placeholder (task -1) of the queue's prefix on w: route rootish-queuing
+      int64_t plslot = plbase + npl, rslot = recbase + nrec;
+      Obj o = objective(D, w, 0, dur);
+      D.st_task[plslot] = -1;
+      D.st_worker[plslot] = w;
+      D.st_comm[plslot] = 0;
+      D.st_start[plslot] = o.start;
+      D.st_wsnbytes[plslot] = D.w_nbytes[w];
+      D.st_route[plslot] = ROUTE_ROOTISH_Q;
+      if (!wdict_inc(D, w, pop_prefix)) set_error(D, ERR_PREFIX_CAP, -1);
+      D.w_nproc[w]++;
+      emit(D, rslot, REC_PLACE, -1, w, pop_prefix, 0, dur);
+      itc_check(D, w, false);
+      atomicAdd((unsigned long long*)&D.ctl->n_tasks, 1ull);
+      npl++;
+      nrec++;
+      pops++;
+    }
+  }
+  D.ev_npl[j] = (int32_t)npl;
+  D.ev_pops[j] = pops;
+}
+
+
+// ======================================================= block-level collectives
+
+// exclusive prefix sum of one int64 per thread over the block; *total = block sum
+__device__ int64_t block_excl_scan(int64_t v, int64_t* total) {
+  __shared__ int64_t s_w[CTA / 64];
+  __shared__ int64_t s_tot;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int64_t incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t run = 0;
+    for (int i = 0; i < nw; i++) {
+      int64_t t = s_w[i];
+      s_w[i] = run;
+      run += t;
+    }
+    s_tot = run;
+  }
+  __syncthreads();
+  int64_t res = s_w[wid] + incl - v;
+  *total = s_tot;
+  __syncthreads();
+  return res;
+}
+
+struct ArgBest {
+  Obj o;
+  int64_t comm;
+};
+// block argmin of worker_objective; threads with w < 0 contribute nothing
+__device__ ArgBest block_argmin(Obj o, int64_t comm, bool valid) {
+  __shared__ double s_start[CTA / 64];
+  __shared__ int64_t s_nb[CTA / 64];
+  __shared__ int32_t s_w[CTA / 64];
+  __shared__ int64_t s_comm[CTA / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (!valid) {
+    o.start = INFINITY;
+    o.nbytes = INT64_MAX;
+    o.w = INT32_MAX;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    Obj q{__shfl_xor(o.start, off), __shfl_xor(o.nbytes, off), __shfl_xor(o.w, off)};
+    int64_t qc = __shfl_xor(comm, off);
+    if (obj_less(q, o)) {
+      o = q;
+      comm = qc;
+    }
+  }
+  if (lane == 0) {
+    s_start[wid] = o.start;
+    s_nb[wid] = o.nbytes;
+    s_w[wid] = o.w;
+    s_comm[wid] = comm;
+  }
+  __syncthreads();
+  ArgBest b{Obj{s_start[0], s_nb[0], s_w[0]}, s_comm[0]};
+  for (int i = 1; i < nw; i++) {
+    Obj q{s_start[i], s_nb[i], s_w[i]};
+    if (obj_less(q, b.o)) {
+      b.o = q;
+      b.comm = s_comm[i];
+    }
+  }
+  __syncthreads();
+  return b;
+}
+
+// ordered list of the workers in the pool `idle if idle else all` into LDS (first `cap`)
+__device__ int64_t gather_pool(const Dev& D, bool use_idle, int32_t* list, int cap) {
+  int64_t base = 0;
+  for (int w0 = 0; w0 < D.W; w0 += blockDim.x) {
+    int w = w0 + threadIdx.x;
+    bool in = w < D.W && (!use_idle || (D.w_flags[w] & WF_IDLE));
+    int64_t tot;
+    int64_t pos = block_excl_scan(in ? 1 : 0, &tot);
+    if (in && base + pos < cap) list[base + pos] = w;
+    base += tot;
+  }
+  __syncthreads();
+  return base;
+}
+
+// ====================================================== global stimulus (cooperative)
+
+// state shared by the lanes of a cooperative global stimulus / the update_graph dispatcher
+struct CoopShared {
+  int op;
+  int x;
+  int best;
+  int64_t best_comm;
+  int nlist;
+  int pos;
+  int done;
+  int32_t list[FL_MAX];
+  int32_t pool[32];
+  int64_t pool_n;
+};
+enum : int { OP_NONE = 0, OP_ARGMIN_POOL, OP_FASTPATH, OP_KTH };
+
+// eager application of a sub-step (global stimuli): what the walker would do with its record
+__device__ void apply_now(const Dev& D, int32_t kind, int t, int w, int p, int64_t dnet, const double* dur) {
+  Ctl* c = D.ctl;
+  if (kind == REC_COMPLETE) {
+    D.pdur_walk[p] = ewma(D.pdur_walk[p], D.res_stop[t] - D.res_start[t]);
+    gdict_dec(D, p);
+  } else if (!gdict_inc(D, p)) {
+    set_error(D, ERR_GPREFIX_CAP, t);
+  }
+  c->g_netocc += (double)dnet;
+  walk_flags(D, w, occupancy(D, w, dur), D.w_nproc[w]);
+}
+
+// _add_to_processing for global stimuli: staging slot from the overflow area
+__device__ void place_eager(const Dev& D, int t, int w, int route, int64_t comm, int64_t* stage_next,
+                            const double* dur) {
+  int64_t slot = (*stage_next)++;
+  if (slot >= D.st_cap) {
+    set_error(D, ERR_STAGE_CAP, t);
+    return;
+  }
+  // do_place emits into the record log; global stimuli apply instead (records slot unused)
+  if (comm < 0) comm = comm_bytes(D, t, w);
+  Obj o = objective(D, w, comm, dur);
+  D.st_task[slot] = t;
+  D.st_worker[slot] = w;
+  D.st_comm[slot] = comm;
+  D.st_start[slot] = o.start;
+  D.st_wsnbytes[slot] = D.w_nbytes[w];
+  D.st_route[slot] = (int8_t)route;
+  int p = D.prefix[t];
+  if (!wdict_inc(D, w, p)) set_error(D, ERR_PREFIX_CAP, t);
+  D.w_nproc[w]++;
+  int64_t dnet = 0;
+  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+    int d = D.dep_idx[k];
+    if (!holds(D, d, w) && !needed_elsewhere(D, d, w, t)) {
+      int64_t nb = get_nbytes(D, d);
+      D.w_netocc[w] += nb;
+      dnet += nb;
+    }
+  }
+  D.proc_on[t] = w;
+  if (D.state[t] == S_WAITING) atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], (unsigned long long)-1ll);
+  D.state[t] = S_PROCESSING;
+  apply_now(D, REC_PLACE, t, w, p, dnet, dur);
+  itc_check(D, w, true);
+  D.ctl->n_tasks++;
+}
+
+__device__ void queue_insert(const Dev& D, int t) {  // HeapSet.add as a sorted array
+  Ctl* c = D.ctl;
+  long long lo = c->qhead, pos = c->qhead + c->qlen;
+  int64_t pr = D.prio[t];
+  while (pos > lo && D.prio[D.qarr[pos - 1]] > pr) {
+    D.qarr[pos] = D.qarr[pos - 1];
+    pos--;
+  }
+  D.qarr[pos] = t;
+  c->qlen++;
+}
+
+// lane 0: first half of _transition_waiting_processing (:2313-2336) for task x. Either
+// finishes it (returns OP_NONE) or names the collective it needs.
+__device__ int dispatch_prepare(const Dev& D, int x, CoopShared& S, int64_t* stage_next, const double* dur) {
+  Ctl* c = D.ctl;
+  if (D.tflags[x] & TF_ROOTISH) {
+    if (D.sat_inf) {  // decide_worker_rootish_queuing_disabled :2135-2193
+      int gi = D.group[x];
+      if (D.g_lastw[gi] >= 0 && D.g_left[gi] != 0) {
+        int w = D.g_lastw[gi];
+        D.g_lastw[gi] = D.g_relwait[gi] > 1 ? w : -1;
+        D.g_left[gi] -= 1;
+        place_eager(D, x, w, ROUTE_ROOTISH_NOQ, -1, stage_next, dur);
+        return OP_NONE;
+      }
+      return OP_ARGMIN_POOL;
+    }
+    // decide_worker_rootish_queuing_enabled :2195-2245
+    if (c->n_itc == 0) {  // -> queued (:2761)
+      D.state[x] = S_QUEUED;
+      atomicAdd((unsigned long long*)&D.g_relwait[D.group[x]], (unsigned long long)-1ll);
+      queue_insert(D, x);
+      return OP_NONE;
+    }
+    place_eager(D, x, D.t_idx[1], ROUTE_ROOTISH_Q, -1, stage_next, dur);
+    return OP_NONE;
+  }
+  if (D.dep_ptr[x + 1] > D.dep_ptr[x]) {  // decide_worker over the candidates
+    int n = D.cand_n[x];
+    int64_t off = D.cand_off[x];
+    if (n <= 0) {
+      set_error(D, ERR_NO_CANDIDATES, x);
+      return OP_NONE;
+    }
+    int best = D.pool_w[off];
+    int64_t bcomm = D.pool_comm[off];
+    if (n > 1) {
+      Obj bo = objective(D, best, bcomm, dur);
+      for (int i = 1; i < n; i++) {
+        Obj o = objective(D, D.pool_w[off + i], D.pool_comm[off + i], dur);
+        if (obj_less(o, bo)) {
+          bo = o;
+          best = o.w;
+          bcomm = D.pool_comm[off + i];
+        }
+      }
+    }
+    place_eager(D, x, best, ROUTE_NONROOTISH, bcomm, stage_next, dur);
+    return OP_NONE;
+  }
+  // no-dependency fast path :2283-2305
+  bool use_idle = c->n_idle > 0;
+  int64_t n = use_idle ? c->n_idle : D.W;
+  if (n >= 20 && !use_idle) {
+    place_eager(D, x, (int)(c->n_tasks % n), ROUTE_FASTPATH, -1, stage_next, dur);
+    return OP_NONE;
+  }
+  return n < 20 ? OP_FASTPATH : OP_KTH;
+}
+
+// all lanes: the collective part, then lane 0 finishes the placement
+__device__ void dispatch_collective(const Dev& D, CoopShared& S, int64_t* stage_next, const double* dur) {
+  int op = S.op, x = S.x;
+  Ctl* c = D.ctl;
+  if (op == OP_ARGMIN_POOL) {
+    bool use_idle = c->n_idle > 0;
+    Obj best{INFINITY, INT64_MAX, INT32_MAX};
+    int64_t bcomm = 0;
+    bool have = false;
+    for (int w = threadIdx.x; w < D.W; w += blockDim.x) {
+      if (use_idle && !(D.w_flags[w] & WF_IDLE)) continue;
+      int64_t cm = comm_bytes(D, x, w);
+      Obj o = objective(D, w, cm, dur);
+      if (!have || obj_less(o, best)) {
+        best = o;
+        bcomm = cm;
+        have = true;
+      }
+    }
+    ArgBest b = block_argmin(best, bcomm, have);
+    if (threadIdx.x == 0) {
+      int gi = D.group[x];
+      int w = b.o.w;
+      if (w == INT32_MAX) {
+        D.state[x] = S_NO_WORKER;
+        atomicAdd((unsigned long long*)&D.g_relwait[gi], (unsigned long long)-1ll);
+        c->n_unrunnable++;
+      } else {
+        D.g_left[gi] = (int64_t)floor(((double)D.g_size[gi] / (double)D.total_nthreads) * (double)D.w_nthreads[w]);
+        D.g_lastw[gi] = D.g_relwait[gi] > 1 ? w : -1;
+        D.g_left[gi] -= 1;
+        place_eager(D, x, w, ROUTE_ROOTISH_NOQ, b.comm, stage_next, dur);
+      }
+    }
+  } else {  // fast path over an ordered pool
+    bool use_idle = c->n_idle > 0;
+    int64_t n = gather_pool(D, use_idle, S.pool, 32);
+    if (op == OP_KTH) {
+      // pool[n_tasks % n] — n >= 20 idle workers: find the k-th idle worker
+      int64_t k = c->n_tasks % n;
+      int64_t base = 0;
+      __shared__ int s_kth;
+      for (int w0 = 0; w0 < D.W; w0 += blockDim.x) {
+        int w = w0 + threadIdx.x;
+        bool in = w < D.W && (D.w_flags[w] & WF_IDLE);
+        int64_t tot;
+        int64_t pos = block_excl_scan(in ? 1 : 0, &tot);
+        if (in && base + pos == k) s_kth = w;
+        base += tot;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) place_eager(D, x, s_kth, ROUTE_FASTPATH, -1, stage_next, dur);
+    } else if (threadIdx.x == 0) {
+      int best = S.pool[0];
+      double bocc = occupancy(D, best, dur);
+      for (int64_t i = 1; i < n; i++) {
+        double o = occupancy(D, S.pool[i], dur);
+        if (o < bocc) {
+          best = S.pool[i];
+          bocc = o;
+        }
+      }
+      if (bocc == 0) {
+        int64_t start = c->n_tasks % n;
+        for (int64_t i = 0; i < n; i++) {
+          int cand = S.pool[(i + start) % n];
+          if (occupancy(D, cand, dur) == 0) {
+            best = cand;
+            break;
+          }
+        }
+      }
+      place_eager(D, x, best, ROUTE_FASTPATH, -1, stage_next, dur);
+    }
+  }
+  __syncthreads();
+}
+
+// dispatch S.list[0..nlist) in order (all lanes)
+__device__ void dispatch_list_coop(const Dev& D, CoopShared& S, int64_t* stage_next, const double* dur) {
+  if (threadIdx.x == 0) S.pos = 0;
+  __syncthreads();
+  while (true) {
+    if (threadIdx.x == 0) {
+      S.op = OP_NONE;
+      while (S.pos < S.nlist) {
+        int x = S.list[S.pos];
+        int op = dispatch_prepare(D, x, S, stage_next, dur);
+        if (op != OP_NONE) {
+          S.op = op;
+          S.x = x;
+          break;
+        }
+        S.pos++;
+      }
+    }
+    __syncthreads();
+    if (S.op == OP_NONE) break;
+    dispatch_collective(D, S, stage_next, dur);
+    if (threadIdx.x == 0) S.pos++;
+    __syncthreads();
+  }
+}
+
+// Scheduler.stimulus_queue_slots_maybe_opened :4983-5023 (lane 0, tree maintained)
+__device__ void queue_refill_eager(const Dev& D, int64_t* stage_next, const double* dur) {
+  Ctl* c = D.ctl;
+  if (c->qlen == 0) return;
+  int64_t slots = c->itc_slots;
+  for (int64_t k = 0; k < slots; k++) {
+    if (c->qlen == 0) return;
+    if (c->n_itc == 0) continue;  // stays queued
+    int q = D.qarr[c->qhead];
+    c->qhead++;
+    c->qlen--;
+    place_eager(D, q, D.t_idx[1], ROUTE_ROOTISH_Q, -1, stage_next, dur);
+  }
+}
+
+// resolve the queued tasks taken by local stimuli [from, to) (all lanes)
+__device__ void resolve_pops_coop(const Dev& D, const int32_t* L, int from, int to) {
+  Ctl* c = D.ctl;
+  int64_t base = 0;
+  for (int j0 = from; j0 < to; j0 += blockDim.x) {
+    int j = j0 + threadIdx.x;
+    int64_t k = (j < to) ? D.ev_pops[j] : 0;
+    int64_t tot;
+    int64_t off = block_excl_scan(k, &tot);
+    if (k > 0) {
+      int w = D.ev_w[j];
+      int64_t st0 = D.ev_plbase[j] + D.ev_npl[j] - k;
+      for (int64_t i = 0; i < k; i++) {
+        int q = D.qarr[c->qhead + base + off + i];
+        D.st_task[st0 + i] = q;
+        D.proc_on[q] = w;
+        D.state[q] = S_PROCESSING;
+      }
+    }
+    base += tot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    c->qhead += base;
+    c->qlen -= base;
+    if (c->qlen < 0) set_error(D, ERR_QUEUE, -1);
+  }
+  __syncthreads();
+}
+
+
+// ================================================================== kernels
+
+__global__ void k_init_workers(Dev D) {
+  for (int w = blockIdx.x * blockDim.x + threadIdx.x; w < D.W; w += gridDim.x * blockDim.x) {
+    D.w_nproc[w] = 0;
+    D.w_plen[w] = 0;
+    D.w_netocc[w] = 0;
+    D.w_nbytes[w] = 0;
+    D.w_itcslots[w] = 0;
+    D.w_lastcheck[w] = ~0ull;
+    // Scheduler.add_worker ends with check_idle_saturated(ws) (:4418): a worker with no
+    // tasks is idle (p < nthreads), never saturated, and in idle_task_count unless its
+    // slot count is 0
+    bool itc = !worker_full(D, w);
+    D.w_flags[w] = WF_IDLE | (itc ? WF_ITC : 0);
+    if (itc) {
+      D.w_itcslots[w] = task_slots_available(D, w);
+      atomicAdd((unsigned long long*)&D.ctl->n_itc, 1ull);
+      atomicAdd((unsigned long long*)&D.ctl->itc_slots, (unsigned long long)D.w_itcslots[w]);
+    }
+    atomicAdd((unsigned long long*)&D.ctl->n_idle, 1ull);
+  }
+}
+
+// update_graph, part 1 (:4600-4611 -> _transition_released_waiting :2078-2119), every
+// task in parallel: waiting_on = dependencies without a replica; waiters = dependents
+// (all of them go to waiting in the same stimulus; priorities are topological)
+__global__ void k_ug_init(Dev D) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < D.N; t += gridDim.x * blockDim.x) {
+    int wo = 0;
+    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+      const unsigned long long* row = D.holders + (size_t)D.dep_idx[k] * D.WB;
+      bool any = false;
+      for (int wd = 0; wd < D.WB && !any; wd++) any = row[wd] != 0;
+      wo += any ? 0 : 1;
+    }
+    D.remaining[t] = wo;
+    D.waiters[t] = (int32_t)(D.dpt_ptr[t + 1] - D.dpt_ptr[t]);
+    D.state[t] = S_WAITING;
+  }
+}
+
+// update_graph, part 2: the tasks that went waiting -> processing, in priority order,
+// dispatched one by one (they read global state); once idle_task_count is empty every
+// further root-ish task is queued in bulk (:2761) — order-preserving.
+__global__ void __launch_bounds__(CTA) k_ug_dispatch(Dev D) {
+  __shared__ CoopShared S;
+  __shared__ int64_t s_nr, s_pos;
+  Ctl* c = D.ctl;
+  // ready list in priority order
+  int64_t base = 0;
+  for (int i0 = 0; i0 < D.N; i0 += blockDim.x) {
+    int i = i0 + threadIdx.x;
+    int t = i < D.N ? D.order[i] : -1;
+    bool r = t >= 0 && D.remaining[t] == 0;
+    int64_t tot;
+    int64_t pos = block_excl_scan(r ? 1 : 0, &tot);
+    if (r) D.ready[base + pos] = t;
+    base += tot;
+  }
+  if (threadIdx.x == 0) {
+    s_nr = base;
+    s_pos = 0;
+  }
+  tree_rebuild_coop(D);
+  int64_t stage_next = 0;  // lane 0's overflow staging cursor
+  const double* dur = D.pdur_cur;
+  bool bulk_done = false;
+  while (true) {
+    __syncthreads();
+    int64_t pos = s_pos, nr = s_nr;
+    if (pos >= nr) break;
+    // bulk queueing once idle_task_count is empty (saturation finite)
+    if (!bulk_done && !D.sat_inf && c->n_itc == 0) {
+      int64_t qb = c->qhead + c->qlen, kept = 0, queued = 0;
+      for (int64_t i0 = pos; i0 < nr; i0 += blockDim.x) {
+        int64_t i = i0 + threadIdx.x;
+        int x = i < nr ? D.ready[i] : -1;
+        bool q = x >= 0 && (D.tflags[x] & TF_ROOTISH);
+        bool k = x >= 0 && !q;
+        int64_t tq, tk;
+        int64_t oq = block_excl_scan(q ? 1 : 0, &tq);
+        int64_t ok = block_excl_scan(k ? 1 : 0, &tk);
+        if (q) {
+          D.qarr[qb + queued + oq] = x;
+          D.state[x] = S_QUEUED;
+          atomicAdd((unsigned long long*)&D.g_relwait[D.group[x]], (unsigned long long)-1ll);
+        }
+        if (k) D.ready[pos + kept + ok] = x;
+        queued += tq;
+        kept += tk;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        c->qlen += queued;
+        s_nr = pos + kept;
+      }
+      bulk_done = true;
+      continue;
+    }
+    int64_t chunk = nr - pos < FL_MAX ? nr - pos : FL_MAX;
+    // stop the chunk at the point where the bulk path takes over
+    if (threadIdx.x == 0) {
+      S.nlist = (int)chunk;
+      for (int64_t i = 0; i < chunk; i++) S.list[i] = D.ready[pos + i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) S.pos = 0;
+    __syncthreads();
+    while (true) {
+      if (threadIdx.x == 0) {
+        S.op = OP_NONE;
+        S.done = 0;
+        while (S.pos < S.nlist) {
+          int x = S.list[S.pos];
+          if (!bulk_done && !D.sat_inf && (D.tflags[x] & TF_ROOTISH) && c->n_itc == 0) {
+            S.done = 1;  // hand the rest to the bulk path
+            break;
+          }
+          int op = dispatch_prepare(D, x, S, &stage_next, dur);
+          if (op != OP_NONE) {
+            S.op = op;
+            S.x = x;
+            break;
+          }
+          S.pos++;
+        }
+      }
+      __syncthreads();
+      if (S.op == OP_NONE) break;
+      dispatch_collective(D, S, &stage_next, dur);
+      if (threadIdx.x == 0) S.pos++;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) s_pos = pos + S.pos;
+  }
+  __syncthreads();
+  // the stimulus' placements become the placement log head (run_id order)
+  __shared__ int64_t s_np;
+  if (threadIdx.x == 0) s_np = stage_next;
+  __syncthreads();
+  int64_t np = s_np;
+  for (int64_t i = threadIdx.x; i < np; i += blockDim.x) {
+    D.pl_task[i] = D.st_task[i];
+    D.pl_worker[i] = D.st_worker[i];
+    D.pl_comm[i] = D.st_comm[i];
+    D.pl_start[i] = D.st_start[i];
+    D.pl_wsnbytes[i] = D.st_wsnbytes[i];
+    D.pl_route[i] = D.st_route[i];
+  }
+  if (threadIdx.x == 0) {
+    c->n_placed = np;
+    c->round_start = 0;
+    c->round_n = 0;
+  }
+}
+
+// start of a round: its completion list is the slice of the placement log made by the
+// previous stimulus batch
+__global__ void k_round_begin(Dev D, long long* next_start, const int32_t* ext, long long ext_n) {
+  Ctl* c = D.ctl;
+  if (ext) {  // an explicit batch of completions (dgp_tasks_finished)
+    c->round_L = ext;
+    c->round_n = ext_n;
+    *next_start = (long long)c->n_placed;
+  } else {
+    c->round_L = D.pl_task + *next_start;
+    c->round_n = (long long)c->n_placed - *next_start;
+    *next_start = (long long)c->n_placed;
+  }
+  c->n_frontier = 0;
+  c->pool_used = 0;
+  c->round_counter++;
+  if (c->round_n > 0) c->rounds_nonempty++;
+}
+
+__global__ void k_frontier_release(Dev D) {
+  const Ctl* c = D.ctl;
+  const int64_t n = c->round_n;
+  const int32_t* L = c->round_L;
+  const unsigned long long tag = (unsigned long long)c->round_counter << 32;
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    int t = L[j];
+    unsigned long long key = tag | (unsigned long long)j;
+    // the replica this completion creates is known before the ordered commit: publish it
+    // now (who_has bit, set_nbytes) so k_candidate_commbytes sees it. Only t's dependents
+    // read it, and they become ready at j or later.
+    int w = D.proc_on[t];
+    if (w >= 0) atomicOr(&D.holders[(size_t)t * D.WB + (w >> 6)], 1ull << (w & 63));
+    D.cur_nbytes[t] = D.res_nbytes[t];
+    for (int64_t k = D.dpt_ptr[t]; k < D.dpt_ptr[t + 1]; k++) {
+      int x = D.dpt_idx[k];
+      atomicMax(&D.ready_key[x], key);
+      if (atomicSub(&D.remaining[x], 1) == 1) {
+        unsigned long long f = atomicAdd(&D.ctl->n_frontier, 1ull);
+        D.frontier[f] = x;
+      }
+    }
+    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+      int d = D.dep_idx[k];
+      atomicMax(&D.release_key[d], key);
+      atomicSub(&D.waiters[d], 1);
+    }
+  }
+}
+
+// one wave per newly ready task: candidate workers (OR of the dependencies' replica
+// bitsets) and, per candidate, the exact comm bytes (total minus what it holds)
+__global__ void k_candidate_commbytes(Dev D) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t nF = (int64_t)D.ctl->n_frontier;
+  for (int64_t i = wave; i < nF; i += nwaves) {
+    int x = D.frontier[i];
+    int64_t d0 = D.dep_ptr[x], d1 = D.dep_ptr[x + 1];
+    if (d1 == d0 || (D.tflags[x] & TF_ROOTISH)) {
+      if (lane == 0) D.cand_n[x] = 0;
+      continue;
+    }
+    int64_t tot = 0;
+    for (int64_t k = d0 + lane; k < d1; k += 64) tot += get_nbytes(D, D.dep_idx[k]);
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    int total_c = 0;
+    for (int wd0 = 0; wd0 < D.WB; wd0 += 64) {
+      int wd = wd0 + lane;
+      unsigned long long acc = 0;
+      if (wd < D.WB)
+        for (int64_t k = d0; k < d1; k++) acc |= D.holders[(size_t)D.dep_idx[k] * D.WB + wd];
+      int cnt = __popcll(acc);
+      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+      total_c += cnt;
+    }
+    int64_t base = 0;
+    if (lane == 0) {
+      base = (int64_t)atomicAdd(&D.ctl->pool_used, (unsigned long long)total_c);
+      if (base + total_c > D.pool_cap) set_error(D, ERR_POOL, x);
+    }
+    base = __shfl(base, 0);
+    if (base + total_c > D.pool_cap) continue;
+    int64_t pos = base;
+    for (int wd0 = 0; wd0 < D.WB; wd0 += 64) {
+      int wd = wd0 + lane;
+      unsigned long long acc = 0;
+      if (wd < D.WB)
+        for (int64_t k = d0; k < d1; k++) acc |= D.holders[(size_t)D.dep_idx[k] * D.WB + wd];
+      int cnt = __popcll(acc);
+      int incl = cnt;
+      for (int o = 1; o < 64; o <<= 1) {
+        int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      int64_t p = pos + incl - cnt;
+      while (acc) {
+        int b = __ffsll((long long)acc) - 1;
+        acc &= acc - 1;
+        D.pool_w[p++] = wd * 64 + b;
+      }
+      pos += __shfl(incl, 63);
+    }
+    for (int ci = lane; ci < total_c; ci += 64) {
+      int cw = D.pool_w[base + ci];
+      int64_t held = 0;
+      for (int64_t k = d0; k < d1; k++) {
+        int d = D.dep_idx[k];
+        if (holds(D, d, cw)) held += get_nbytes(D, d);
+      }
+      D.pool_comm[base + ci] = tot - held;
+    }
+    if (lane == 0) {
+      D.cand_off[x] = base;
+      D.cand_n[x] = total_c;
+    }
+  }
+}
+
+enum : uint8_t { EV_MAYQUEUE = 2 };
+
+// per completion stimulus j: the workers it may touch and whether it reads global state
+__global__ void k_events(Dev D) {
+  const Ctl* c = D.ctl;
+  const int64_t n = c->round_n;
+  const int32_t* L = c->round_L;
+  const unsigned long long tag = (unsigned long long)c->round_counter << 32;
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    int t = L[j];
+    unsigned long long key = tag | (unsigned long long)j;
+    int w = D.proc_on[t];
+    int32_t* touch = D.ev_touch + (size_t)j * TOUCH_MAX;
+    int nt = 0;
+    uint8_t fl = 0;
+    auto add = [&](int x) {
+      for (int i = 0; i < nt; i++)
+        if (touch[i] == x) return;
+      if (nt < TOUCH_MAX)
+        touch[nt++] = x;
+      else
+        fl |= EV_GLOBAL;
+    };
+    add(w);
+    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+      int d = D.dep_idx[k];
+      if (D.release_key[d] == key && D.waiters[d] == 0 && !(D.tflags[d] & TF_WANTED)) {
+        const unsigned long long* row = D.holders + (size_t)d * D.WB;
+        for (int wd = 0; wd < D.WB; wd++) {
+          unsigned long long bits = row[wd];
+          while (bits) {
+            int b = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            add(wd * 64 + b);
+          }
+        }
+      }
+    }
+    int nf = 0;
+    for (int64_t k = D.dpt_ptr[t]; k < D.dpt_ptr[t + 1]; k++) {
+      int x = D.dpt_idx[k];
+      if (!is_frontier(D, x, key)) continue;
+      nf++;
+      if (D.tflags[x] & TF_ROOTISH) {
+        fl |= EV_GLOBAL | (D.sat_inf ? 0 : EV_MAYQUEUE);
+      } else if (D.dep_ptr[x + 1] == D.dep_ptr[x]) {
+        fl |= EV_GLOBAL;
+      } else {
+        int cn = D.cand_n[x];
+        int64_t off = D.cand_off[x];
+        for (int i = 0; i < cn; i++) add(D.pool_w[off + i]);
+      }
+    }
+    D.ev_w[j] = w;
+    D.ev_nf[j] = nf;
+    D.ev_flags[j] = fl;
+    D.ev_ntouch[j] = nt;
+  }
+}
+
+// global stimulus j (all lanes): waits for nothing — every earlier stimulus has committed
+__device__ void exec_global(const Dev& D, const int32_t* L, int j, unsigned long long key, const double* dur,
+                            CoopShared& S, int64_t* stage_next, int* resolved_upto) {
+  Ctl* c = D.ctl;
+  resolve_pops_coop(D, L, *resolved_upto, j);
+  if (threadIdx.x == 0) {
+    *resolved_upto = j;
+    walk_to(D, (unsigned long long)D.ev_recbase[j]);
+  }
+  __syncthreads();
+  tree_rebuild_coop(D);
+  __shared__ int64_t s_st0;
+  __shared__ int64_t s_dpos;
+  int t = L[j];
+  if (threadIdx.x == 0) {
+    s_st0 = *stage_next;
+    int w = D.proc_on[t];
+    int p = D.prefix[t];
+    D.proc_on[t] = -1;
+    wdict_dec(D, w, p);
+    D.w_nproc[w]--;
+    int64_t dnet = 0;
+    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+      int d = D.dep_idx[k];
+      if (!holds(D, d, w) && !needed_elsewhere(D, d, w, t)) {
+        int64_t nb = get_nbytes(D, d);
+        D.w_netocc[w] -= nb;
+        dnet -= nb;
+      }
+    }
+    apply_now(D, REC_COMPLETE, t, w, p, dnet, dur);
+    itc_check(D, w, true);
+    D.w_nbytes[w] += get_nbytes(D, t);
+    D.state[t] = S_MEMORY;
+    do_releases(D, t, key);
+    s_dpos = D.dpt_ptr[t];
+    c->n_global_events++;
+  }
+  __syncthreads();
+  // frontier in ascending priority, in chunks of FL_MAX
+  while (true) {
+    if (threadIdx.x == 0) {
+      S.nlist = 0;
+      int64_t k = s_dpos;
+      for (; k < D.dpt_ptr[t + 1] && S.nlist < FL_MAX; k++) {
+        int x = D.dpt_idx[k];
+        if (is_frontier(D, x, key)) S.list[S.nlist++] = x;
+      }
+      s_dpos = k;
+    }
+    __syncthreads();
+    if (S.nlist == 0) break;
+    dispatch_list_coop(D, S, stage_next, dur);
+  }
+  if (threadIdx.x == 0) {
+    queue_refill_eager(D, stage_next, dur);
+    D.ev_plbase[j] = s_st0;
+    D.ev_npl[j] = (int32_t)(*stage_next - s_st0);
+    D.ev_pops[j] = 0;
+    *resolved_upto = j + 1;
+  }
+  __syncthreads();
+}
+
+// the ordered commit of one round (one workgroup; owner[] in dynamic LDS)
+__global__ void __launch_bounds__(CTA) k_commit(Dev D) {
+  extern __shared__ __attribute__((aligned(16))) int owner[];
+  __shared__ CoopShared S;
+  __shared__ int win[CTA];
+  __shared__ int s_nwin, s_next, s_gfirst, s_uniform, s_firstq, s_qbad, s_pop_prefix, s_resolved, s_err;
+  __shared__ int64_t s_stage_next;
+  Ctl* c = D.ctl;
+  const int n = (int)c->round_n;
+  if (n == 0) return;
+  const int32_t* L = c->round_L;
+  const unsigned long long tag = (unsigned long long)c->round_counter << 32;
+  const int P = D.P;
+  const int tid = threadIdx.x;
+
+  // ---- durations in effect at each stimulus (TaskPrefix.add_duration EWMA, in order)
+  if (tid == 0) {
+    s_uniform = 1;
+    s_firstq = INT32_MAX;
+    s_qbad = 0;
+    s_resolved = 0;
+  }
+  __syncthreads();
+  for (int j = tid; j < n; j += blockDim.x) {
+    int t = L[j];
+    double cur = D.pdur_cur[D.prefix[t]];
+    if (!(cur >= 0 && D.res_stop[t] - D.res_start[t] == cur)) s_uniform = 0;
+    if (D.ev_flags[j] & EV_MAYQUEUE) atomicMin(&s_firstq, j);
+  }
+  __syncthreads();
+  const bool uniform = s_uniform != 0;
+  if (uniform) {
+    for (int p = tid; p < P; p += blockDim.x) D.durv[p] = D.pdur_cur[p];
+  } else {
+    // one lane per prefix walks the stimuli in order
+    for (int p = tid; p < P; p += blockDim.x) {
+      double v = D.pdur_cur[p];
+      for (int j = 0; j < n; j++) {
+        int t = L[j];
+        if (D.prefix[t] == p) v = ewma(v, D.res_stop[t] - D.res_start[t]);
+        D.durv[(size_t)j * P + p] = v;
+      }
+      D.pdur_cur[p] = v;
+    }
+  }
+  // ---- classification, queue bound, staging / record offsets
+  const long long qlen0 = c->qlen;
+  int64_t run_pop = 0, run_pub = 0, run_rub = 0;
+  const int64_t rec0 = (int64_t)c->rec_used;
+  if (qlen0 > 0 && tid == 0) {
+    // the queued tasks local stimuli may take must all be dependency-free with one prefix
+    int q0 = D.qarr[c->qhead];
+    s_pop_prefix = D.prefix[q0];
+  }
+  __syncthreads();
+  for (int j0 = 0; j0 < n; j0 += blockDim.x) {
+    int j = j0 + tid;
+    bool in = j < n;
+    int popmax = (in && qlen0 > 0) ? D.w_cap[D.ev_w[j]] : 0;
+    int64_t tot;
+    int64_t pexcl = block_excl_scan(popmax, &tot);
+    uint8_t fl = in ? D.ev_flags[j] : 0;
+    if (in && popmax > 0 && run_pop + pexcl + popmax > qlen0) fl |= EV_GLOBAL;
+    if (in && j > s_firstq) fl |= EV_GLOBAL;
+    run_pop += tot;
+    if (in) D.ev_flags[j] = fl;
+    bool glob = (fl & EV_GLOBAL) != 0;
+    int64_t pub = (in && !glob) ? D.ev_nf[j] + popmax : 0;
+    int64_t rub = (in && !glob) ? 1 + D.ev_nf[j] + popmax : 0;
+    if (in) D.ev_popmax[j] = glob ? 0 : popmax;
+    int64_t po = block_excl_scan(pub, &tot);
+    if (in) D.ev_plbase[j] = run_pub + po;
+    run_pub += tot;
+    int64_t ro = block_excl_scan(rub, &tot);
+    if (in) D.ev_recbase[j] = rec0 + run_rub + ro;
+    run_rub += tot;
+  }
+  if (qlen0 > 0) {
+    int64_t rng = run_pop < qlen0 ? run_pop : qlen0;
+    for (int64_t i = tid; i < rng; i += blockDim.x) {
+      int q = D.qarr[c->qhead + i];
+      if (D.dep_ptr[q + 1] != D.dep_ptr[q] || D.prefix[q] != s_pop_prefix) s_qbad = 1;
+    }
+    __syncthreads();
+    if (s_qbad)
+      for (int j = tid; j < n; j += blockDim.x)
+        if (D.ev_popmax[j] > 0) {
+          D.ev_flags[j] |= EV_GLOBAL;
+          D.ev_popmax[j] = 0;  // its reserved slots stay unused (REC_NONE / not copied)
+        }
+  }
+  if (rec0 + run_rub > D.rec_cap || run_pub > D.st_cap) {
+    if (tid == 0) set_error(D, rec0 + run_rub > D.rec_cap ? ERR_REC_CAP : ERR_STAGE_CAP, -1);
+    return;
+  }
+  for (int64_t i = tid; i < run_rub; i += blockDim.x) D.rec[rec0 + i].kind = REC_NONE;
+  for (int i = tid; i < D.W; i += blockDim.x) owner[i] = INT32_MAX;
+  if (tid == 0) {
+    c->rec_used = (unsigned long long)(rec0 + run_rub);
+    s_stage_next = run_pub;
+    s_next = n < CTA ? n : CTA;
+    s_nwin = s_next;
+  }
+  for (int i = tid; i < CTA; i += blockDim.x) win[i] = i < n ? i : -1;
+  __threadfence_block();
+  __syncthreads();
+
+  // ---- deterministic-reservation commit
+  while (true) {
+    __syncthreads();
+    int nwin = s_nwin;
+    if (nwin == 0) break;
+    int first = win[0];
+    if (D.ev_flags[first] & EV_GLOBAL) {
+      const double* dur = D.durv + (uniform ? 0 : (size_t)first * P);
+      int64_t sn = s_stage_next;
+      int resolved = s_resolved;
+      exec_global(D, L, first, tag | (unsigned long long)first, dur, S, &sn, &resolved);
+      if (tid == 0) {
+        s_stage_next = sn;
+        s_resolved = resolved;
+        if (sn > D.st_cap) set_error(D, ERR_STAGE_CAP, -1);
+      }
+      // drop win[0]
+      int v = (tid + 1 < nwin) ? win[tid + 1] : -1;
+      __syncthreads();
+      if (tid < CTA) win[tid] = v;
+      __syncthreads();
+      if (tid == 0) {
+        s_nwin = nwin - 1;
+        if (s_next < n) win[s_nwin++] = s_next++;
+        s_err = c->error;
+      }
+      __syncthreads();
+      if (s_err) break;
+      continue;
+    }
+    if (tid == 0) s_gfirst = INT32_MAX;
+    __syncthreads();
+    int j = tid < nwin ? win[tid] : -1;
+    if (j >= 0 && (D.ev_flags[j] & EV_GLOBAL)) atomicMin(&s_gfirst, j);
+    __syncthreads();
+    const int gfirst = s_gfirst;
+    const bool active = j >= 0 && j < gfirst;
+    const int32_t* touch = active ? D.ev_touch + (size_t)j * TOUCH_MAX : nullptr;
+    const int nt = active ? D.ev_ntouch[j] : 0;
+    for (int i = 0; i < nt; i++) atomicMin(&owner[touch[i]], j);
+    __syncthreads();
+    bool mine = active;
+    for (int i = 0; i < nt && mine; i++) mine = owner[touch[i]] == j;
+    if (mine) {
+      const double* dur = D.durv + (uniform ? 0 : (size_t)j * P);
+      exec_local(D, j, L[j], D.ev_w[j], tag | (unsigned long long)j, dur, D.ev_plbase[j], D.ev_recbase[j],
+                 D.ev_popmax[j], qlen0 > 0 ? s_pop_prefix : 0);
+    }
+    __syncthreads();
+    for (int i = 0; i < nt; i++) owner[touch[i]] = INT32_MAX;
+    // compact the window (keep order), refill with the next stimuli
+    bool keep = j >= 0 && !mine;
+    int64_t tot;
+    int64_t pos = block_excl_scan(keep ? 1 : 0, &tot);
+    __syncthreads();
+    if (keep) win[pos] = j;
+    __syncthreads();
+    if (tid == 0) {
+      int m = (int)tot;
+      while (m < CTA && s_next < n) win[m++] = s_next++;
+      s_nwin = m;
+      c->dr_steps++;
+      s_err = c->error;
+    }
+    __syncthreads();
+    if (s_err) break;
+  }
+  __syncthreads();
+  // ---- queued tasks taken by local stimuli, then the placement log in stimulus order
+  resolve_pops_coop(D, L, s_resolved, n);
+  int64_t run = 0;
+  const int64_t dst0 = (int64_t)c->n_placed;
+  for (int j0 = 0; j0 < n; j0 += blockDim.x) {
+    int j = j0 + tid;
+    int64_t cnt = j < n ? D.ev_npl[j] : 0;
+    int64_t tot;
+    int64_t off = block_excl_scan(cnt, &tot);
+    if (cnt > 0) {
+      int64_t src = D.ev_plbase[j], dst = dst0 + run + off;
+      for (int64_t i = 0; i < cnt; i++) {
+        D.pl_task[dst + i] = D.st_task[src + i];
+        D.pl_worker[dst + i] = D.st_worker[src + i];
+        D.pl_comm[dst + i] = D.st_comm[src + i];
+        D.pl_start[dst + i] = D.st_start[src + i];
+        D.pl_wsnbytes[dst + i] = D.st_wsnbytes[src + i];
+        D.pl_route[dst + i] = D.st_route[src + i];
+      }
+    }
+    run += tot;
+  }
+  __syncthreads();
+  if (tid == 0) c->n_placed = (unsigned long long)(dst0 + run);
+}
+
+// fold the whole record log into idle / saturated (single lane)
+__global__ void k_walk(Dev D) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) walk_to(D, D.ctl->rec_used);
+}
+
+__global__ void k_snapshot(Dev D, long long* prev_placed, int after_round) {
+  if (after_round && D.ctl->round_n == 0) return;
+  int64_t r = D.ctl->rounds_nonempty;
+  if (r >= D.snap_cap) return;
+  for (int w = blockIdx.x * blockDim.x + threadIdx.x; w < D.W; w += gridDim.x * blockDim.x) {
+    size_t o = (size_t)r * D.W + w;
+    D.snap_occ[o] = occupancy(D, w, D.pdur_cur);
+    D.snap_nbytes[o] = D.w_nbytes[w];
+    D.snap_nproc[o] = D.w_nproc[w];
+    D.snap_flags[o] = D.w_flags[w];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    D.snap_nplaced[r] = (int32_t)((long long)D.ctl->n_placed - *prev_placed);
+    D.snap_nqueued[r] = (int32_t)D.ctl->qlen;
+    *prev_placed = (long long)D.ctl->n_placed;
+  }
+}
+
+}  // namespace dgp

@@ -25,7 +25,7 @@ DEFAULT_CONFIG = {  # distributed/distributed.yaml:13,16,24,28
     "saturation": 1.1,
 }
 
-KERNEL_NAMES = ("frontier_release", "candidate_commbytes", "commit", "other")
+KERNEL_NAMES = ("frontier_release", "candidate_commbytes", "commit", "other")  # ids of dgp_kernel_times
 
 
 class PlacementEngine:
@@ -170,6 +170,12 @@ class PlacementEngine:
 
     def set_timing(self, on: bool = True):
         self._check(self.lib.dgp_set_timing(self.h, 1 if on else 0), "dgp_set_timing")
+
+    def stats(self) -> dict:
+        out = np.zeros(6, np.int64)
+        self._check(self.lib.dgp_stats(self.h, _ptr(out), 6), "dgp_stats")
+        return dict(zip(("placements", "rounds", "dr_steps", "global_stimuli", "records", "walk_pos"),
+                        map(int, out)))
 
     def kernel_times(self) -> dict:
         ms = np.zeros(4)

@@ -116,6 +116,11 @@ int dgp_get_task_states(dgp_engine* e, uint8_t* state);
 int dgp_kernel_times(dgp_engine* e, double* ms, int64_t* launches, int32_t n);
 int dgp_set_timing(dgp_engine* e, int enabled);
 
+/* Engine counters: out[0] placements, [1] non-empty rounds, [2] deterministic-reservation
+ * steps of the ordered commit, [3] stimuli that ran as global (in order, alone),
+ * [4] record-log length, [5] record-log walker position. */
+int dgp_stats(dgp_engine* e, int64_t* out, int32_t n);
+
 #ifdef __cplusplus
 }
 #endif
