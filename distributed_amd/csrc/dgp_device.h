@@ -47,7 +47,7 @@ enum : uint8_t { WF_IDLE = 1, WF_SAT = 2, WF_ITC = 4 };
 enum : uint8_t { EV_GLOBAL = 1 };
 enum : int32_t { REC_NONE = 0, REC_COMPLETE = 1, REC_PLACE = 2 };
 enum : int { ERR_NONE = 0, ERR_PREFIX_CAP, ERR_NO_CANDIDATES, ERR_BAD_STATE, ERR_QUEUE, ERR_POOL, ERR_GPREFIX_CAP,
-             ERR_REC_CAP, ERR_STAGE_CAP, ERR_NO_WORKER };
+             ERR_REC_CAP, ERR_STAGE_CAP, ERR_NO_WORKER, ERR_NEEDS_CAP };
 enum : int { ROUTE_NONROOTISH = 0, ROUTE_ROOTISH_Q = 1, ROUTE_ROOTISH_NOQ = 2, ROUTE_FASTPATH = 3 };
 
 // device-resident control block
@@ -74,6 +74,9 @@ struct Ctl {
   long long rounds_nonempty;      // rounds that completed at least one task
   const int32_t* round_L;         // completion list of the current round
   long long dr_steps;             // deterministic-reservation steps (diagnostics)
+  unsigned long long prof2[16];   // exec_local_wave phase cycles (diagnostics)
+  unsigned long long prof[8];     // k_commit phase cycles (s_memtime): setup, local steps, global
+                                  // stimuli, finish, walker, max step, -, -
   long long n_global_events;
   int error;
   int err_task;
@@ -140,6 +143,7 @@ struct Dev {
   uint8_t* w_flags;
   int64_t* w_itcslots;
   unsigned long long* w_lastcheck;  // record index of the worker's latest check
+  uint32_t* w_needs;                // needs_what lines [W][NEEDS_W]
   double* t_key;                    // tournament tree over idle_task_count
   int32_t* t_idx;
   // prefixes
@@ -193,8 +197,39 @@ struct Dev {
   int32_t* snap_nproc;
   uint8_t* snap_flags;
   int32_t* snap_nqueued;
+  int32_t lds_workers;  // commit kernel: worker state lives in dynamic LDS
   Ctl* ctl;
 };
+
+// dynamic LDS of the commit kernel: owner[W] reservation table, then (lds_workers) the
+// worker state arrays, each 16-byte aligned
+extern __shared__ __attribute__((aligned(16))) char dgp_smem[];
+__device__ __forceinline__ size_t lds_al(size_t b) { return (b + 15) & ~(size_t)15; }
+// carve: owner[W] (16-byte aligned), then the worker arrays over Wa = W rounded up to 4
+// workers, so every array starts 16-byte aligned. Byte offsets per worker:
+constexpr int LDS_CUM[12] = {0, 4, 8, 12, 16, 16 + 4 * PMAX, 16 + 8 * PMAX, 24 + 8 * PMAX, 32 + 8 * PMAX,
+                             40 + 8 * PMAX, 48 + 8 * PMAX, 49 + 8 * PMAX};
+template <int K>
+__device__ __forceinline__ char* lds_field_k(int W) {
+  const size_t Wa = ((size_t)W + 3) & ~(size_t)3;
+  return dgp_smem + lds_al((size_t)W * 4) + Wa * LDS_CUM[K];
+}
+__device__ __forceinline__ char* lds_field(int W, int k) {
+  const size_t Wa = ((size_t)W + 3) & ~(size_t)3;
+  return dgp_smem + lds_al((size_t)W * 4) + Wa * LDS_CUM[k];
+}
+#define WK_(D, f, k, T) ((D).lds_workers ? (T*)lds_field_k<k>((D).W) : (D).f)
+#define WK_nthreads(D) WK_(D, w_nthreads, 0, int32_t)
+#define WK_cap(D) WK_(D, w_cap, 1, int32_t)
+#define WK_nproc(D) WK_(D, w_nproc, 2, int32_t)
+#define WK_plen(D) WK_(D, w_plen, 3, int32_t)
+#define WK_pfx(D) WK_(D, w_pfx, 4, int32_t)
+#define WK_pcnt(D) WK_(D, w_pcnt, 5, int32_t)
+#define WK_netocc(D) WK_(D, w_netocc, 6, int64_t)
+#define WK_nbytes(D) WK_(D, w_nbytes, 7, int64_t)
+#define WK_itcslots(D) WK_(D, w_itcslots, 8, int64_t)
+#define WK_lastcheck(D) WK_(D, w_lastcheck, 9, unsigned long long)
+#define WK_flags(D) WK_(D, w_flags, 10, uint8_t)
 
 // ============================================================== small helpers
 
@@ -221,11 +256,11 @@ __device__ __forceinline__ double prefix_duration(const Dev& D, const double* du
 // WorkerState.occupancy :840 -> _calc_occupancy :1884-1903 (dict insertion order)
 __device__ double occupancy(const Dev& D, int w, const double* dur) {
   double res = 0.0;
-  const int n = D.w_plen[w];
-  const int* pf = D.w_pfx + (size_t)w * PMAX;
-  const int* pc = D.w_pcnt + (size_t)w * PMAX;
+  const int n = WK_plen(D)[w];
+  const int* pf = WK_pfx(D) + (size_t)w * PMAX;
+  const int* pc = WK_pcnt(D) + (size_t)w * PMAX;
   for (int i = 0; i < n; i++) res += prefix_duration(D, dur, pf[i]) * (double)pc[i];
-  return res + (double)D.w_netocc[w] / (double)D.bandwidth;
+  return res + (double)WK_netocc(D)[w] / (double)D.bandwidth;
 }
 // SchedulerState.total_occupancy :1877 at the walker position
 __device__ double total_occupancy_walk(const Dev& D) {
@@ -240,9 +275,9 @@ __device__ __forceinline__ double ewma(double old, double duration) {  // TaskPr
 
 // insertion-ordered {prefix: count} dicts with delete-on-zero (:733-784)
 __device__ bool wdict_inc(const Dev& D, int w, int p) {
-  int* pf = D.w_pfx + (size_t)w * PMAX;
-  int* pc = D.w_pcnt + (size_t)w * PMAX;
-  int n = D.w_plen[w];
+  int* pf = WK_pfx(D) + (size_t)w * PMAX;
+  int* pc = WK_pcnt(D) + (size_t)w * PMAX;
+  int n = WK_plen(D)[w];
   for (int i = 0; i < n; i++)
     if (pf[i] == p) {
       pc[i]++;
@@ -251,13 +286,13 @@ __device__ bool wdict_inc(const Dev& D, int w, int p) {
   if (n == PMAX) return false;
   pf[n] = p;
   pc[n] = 1;
-  D.w_plen[w] = n + 1;
+  WK_plen(D)[w] = n + 1;
   return true;
 }
 __device__ void wdict_dec(const Dev& D, int w, int p) {
-  int* pf = D.w_pfx + (size_t)w * PMAX;
-  int* pc = D.w_pcnt + (size_t)w * PMAX;
-  int n = D.w_plen[w];
+  int* pf = WK_pfx(D) + (size_t)w * PMAX;
+  int* pc = WK_pcnt(D) + (size_t)w * PMAX;
+  int n = WK_plen(D)[w];
   for (int i = 0; i < n; i++)
     if (pf[i] == p) {
       if (--pc[i] == 0) {
@@ -265,7 +300,7 @@ __device__ void wdict_dec(const Dev& D, int w, int p) {
           pf[k - 1] = pf[k];
           pc[k - 1] = pc[k];
         }
-        D.w_plen[w] = n - 1;
+        WK_plen(D)[w] = n - 1;
       }
       return;
     }
@@ -299,7 +334,7 @@ __device__ void gdict_dec(const Dev& D, int p) {
 }
 
 __device__ __forceinline__ int64_t task_slots_available(const Dev& D, int w) {  // :8762-8767
-  return (int64_t)D.w_cap[w] - (int64_t)D.w_nproc[w];  // len(long_running) == 0 in the replay
+  return (int64_t)WK_cap(D)[w] - (int64_t)WK_nproc(D)[w];  // len(long_running) == 0 in the replay
 }
 __device__ __forceinline__ bool worker_full(const Dev& D, int w) {  // :8770-8773
   if (D.sat_inf) return false;
@@ -312,7 +347,7 @@ __device__ __forceinline__ bool worker_full(const Dev& D, int w) {  // :8770-877
 // (decide_worker_rootish_queuing_enabled :2230-2233). Only global stimuli use it; it is
 // rebuilt cooperatively before they run and then maintained by their single lane.
 __device__ void tree_update(const Dev& D, int w) {
-  double key = (D.w_flags[w] & WF_ITC) ? (double)D.w_nproc[w] / (double)D.w_nthreads[w] : INFINITY;
+  double key = (WK_flags(D)[w] & WF_ITC) ? (double)WK_nproc(D)[w] / (double)WK_nthreads(D)[w] : INFINITY;
   int pos = D.Wp + w;
   D.t_key[pos] = key;
   D.t_idx[pos] = w;
@@ -331,11 +366,11 @@ __device__ void tree_update(const Dev& D, int w) {
     D.t_idx[pos] = i;
   }
 }
-__device__ void tree_rebuild_coop(const Dev& D) {  // all threads of the block
+__device__ __attribute__((noinline)) void tree_rebuild_coop(const Dev& D) {  // all threads of the block
   for (int i = threadIdx.x; i < D.Wp; i += blockDim.x) {
     int pos = D.Wp + i;
-    bool on = i < D.W && (D.w_flags[i] & WF_ITC);
-    D.t_key[pos] = on ? (double)D.w_nproc[i] / (double)D.w_nthreads[i] : INFINITY;
+    bool on = i < D.W && (WK_flags(D)[i] & WF_ITC);
+    D.t_key[pos] = on ? (double)WK_nproc(D)[i] / (double)WK_nthreads(D)[i] : INFINITY;
     D.t_idx[pos] = i;
   }
   __threadfence_block();
@@ -356,16 +391,16 @@ __device__ void tree_rebuild_coop(const Dev& D) {  // all threads of the block
 // the idle_task_count part of check_idle_saturated (:2992-2995): depends only on w
 __device__ void itc_check(const Dev& D, int w, bool maintain_tree) {
   bool on = !worker_full(D, w);
-  uint8_t fl = D.w_flags[w];
+  uint8_t fl = WK_flags(D)[w];
   bool was = (fl & WF_ITC) != 0;
   if (on != was) {
-    D.w_flags[w] = on ? (fl | WF_ITC) : (fl & ~WF_ITC);
+    WK_flags(D)[w] = on ? (fl | WF_ITC) : (fl & ~WF_ITC);
     atomicAdd((unsigned long long*)&D.ctl->n_itc, on ? 1ull : (unsigned long long)-1ll);
   }
   int64_t contrib = on ? task_slots_available(D, w) : 0;
-  int64_t delta = contrib - D.w_itcslots[w];
+  int64_t delta = contrib - WK_itcslots(D)[w];
   if (delta) atomicAdd((unsigned long long*)&D.ctl->itc_slots, (unsigned long long)delta);
-  D.w_itcslots[w] = contrib;
+  WK_itcslots(D)[w] = contrib;
   if (maintain_tree) tree_update(D, w);
 }
 
@@ -385,17 +420,17 @@ __device__ void emit(const Dev& D, int64_t slot, int32_t kind, int32_t task, int
   r.prefix = prefix;
   r.dnet = dnet;
   r.occ = occupancy(D, w, dur);
-  r.nproc = D.w_nproc[w];
+  r.nproc = WK_nproc(D)[w];
   r.pad = 0;
   D.rec[slot] = r;
-  D.w_lastcheck[w] = (unsigned long long)slot;
+  WK_lastcheck(D)[w] = (unsigned long long)slot;
 }
 
 // the idle / saturated part of check_idle_saturated (:2949-2991 + is_unoccupied :2997)
 __device__ void walk_flags(const Dev& D, int w, double occ, int64_t p) {
   Ctl* c = D.ctl;
-  int64_t nt = D.w_nthreads[w];
-  uint8_t fl = D.w_flags[w];
+  int64_t nt = WK_nthreads(D)[w];
+  uint8_t fl = WK_flags(D)[w];
   bool idle = false, sat = false;
   double avg = -1;
   if (p < nt) {
@@ -413,11 +448,11 @@ __device__ void walk_flags(const Dev& D, int w, double occ, int64_t p) {
   }
   if (idle != ((fl & WF_IDLE) != 0)) c->n_idle += idle ? 1 : -1;
   if (sat != ((fl & WF_SAT) != 0)) c->n_sat += sat ? 1 : -1;
-  D.w_flags[w] = (fl & ~(WF_IDLE | WF_SAT)) | (idle ? WF_IDLE : 0) | (sat ? WF_SAT : 0);
+  WK_flags(D)[w] = (fl & ~(WF_IDLE | WF_SAT)) | (idle ? WF_IDLE : 0) | (sat ? WF_SAT : 0);
 }
 
 // fold records [walk_pos, end) into the walker state (single lane)
-__device__ void walk_to(const Dev& D, unsigned long long end) {
+__device__ __attribute__((noinline)) void walk_to(const Dev& D, unsigned long long end) {
   Ctl* c = D.ctl;
   for (unsigned long long i = c->walk_pos; i < end; i++) {
     Rec r = D.rec[i];
@@ -429,7 +464,7 @@ __device__ void walk_to(const Dev& D, unsigned long long end) {
       if (!gdict_inc(D, r.prefix)) set_error(D, ERR_GPREFIX_CAP, r.task);
     }
     c->g_netocc += (double)r.dnet;
-    if (D.w_lastcheck[r.w] == i) walk_flags(D, r.w, r.occ, r.nproc);
+    if (WK_lastcheck(D)[r.w] == i) walk_flags(D, r.w, r.occ, r.nproc);
   }
   if (end > c->walk_pos) c->walk_pos = end;
 }
@@ -447,9 +482,9 @@ __device__ __forceinline__ bool obj_less(const Obj& a, const Obj& b) {
   return a.w < b.w;
 }
 __device__ __forceinline__ Obj objective(const Dev& D, int w, int64_t comm, const double* dur) {
-  double stack_time = occupancy(D, w, dur) / (double)D.w_nthreads[w];
+  double stack_time = occupancy(D, w, dur) / (double)WK_nthreads(D)[w];
   double start_time = stack_time + (double)comm / (double)D.bandwidth;
-  return Obj{start_time, D.w_nbytes[w], w};
+  return Obj{start_time, WK_nbytes(D)[w], w};
 }
 __device__ int64_t comm_bytes(const Dev& D, int t, int w) {  // worker_objective's sum :3136-3138
   int64_t comm = 0;
@@ -459,14 +494,81 @@ __device__ int64_t comm_bytes(const Dev& D, int t, int w) {  // worker_objective
   }
   return comm;
 }
-// needs_what[w][d] > 0 <=> another dependent of d is processing on w (w does not hold d):
-// WorkerState._inc/_dec_needs_replica (:800-823) without a per-worker map
+// needs_what[w][d] > 0 <=> another dependent of d is processing on w (w does not hold d)
 __device__ bool needed_elsewhere(const Dev& D, int d, int w, int except) {
   for (int64_t k = D.dpt_ptr[d]; k < D.dpt_ptr[d + 1]; k++) {
     int x = D.dpt_idx[k];
     if (x != except && D.proc_on[x] == w) return true;
   }
   return false;
+}
+
+// WorkerState.needs_what (:800-823) as one 128-byte line per worker: up to NEEDS_W - 1
+// entries (d << 8 | count), 0 = empty. Only the stimulus owning the worker touches it.
+// A worker that needs more dependencies at once (a shuffle barrier, rootish pile-ups)
+// switches to exact scans of the dependents' processing_on (needed_elsewhere) until
+// it has nothing processing again.
+constexpr int NEEDS_W = 32;
+constexpr uint32_t NEEDS_OVF = 0xffffffffu;  // in the last slot: scan mode
+__device__ __forceinline__ uint32_t* needs_line(const Dev& D, int w) { return D.w_needs + (size_t)w * NEEDS_W; }
+__device__ __forceinline__ bool needs_overflowed(const Dev& D, int w) {
+  return needs_line(D, w)[NEEDS_W - 1] == NEEDS_OVF;
+}
+// _inc_needs_replica: bytes w newly needs (0 if d was needed already); t = task being placed
+__device__ int64_t needs_inc(const Dev& D, int w, int d, int t) {
+  uint32_t* line = needs_line(D, w);
+  if (line[NEEDS_W - 1] != NEEDS_OVF) {
+    const uint32_t key = (uint32_t)d << 8;
+    int empty = -1;
+    for (int q = 0; q < NEEDS_W / 4; q++) {
+      uint4 v = reinterpret_cast<const uint4*>(line)[q];
+      uint32_t e[4] = {v.x, v.y, v.z, v.w};
+      for (int i = 0; i < 4; i++) {
+        int slot = 4 * q + i;
+        if (e[i] != 0 && (e[i] & ~0xffu) == key && slot < NEEDS_W - 1) {
+          if ((e[i] & 0xffu) != 0xffu) {
+            line[slot] = e[i] + 1;
+            return 0;
+          }
+          line[NEEDS_W - 1] = NEEDS_OVF;  // count saturated: scan mode
+          return needed_elsewhere(D, d, w, t) ? 0 : get_nbytes(D, d);
+        }
+        if (e[i] == 0 && empty < 0 && slot < NEEDS_W - 1) empty = slot;
+      }
+    }
+    if (empty >= 0) {
+      line[empty] = key | 1u;
+      return get_nbytes(D, d);
+    }
+    line[NEEDS_W - 1] = NEEDS_OVF;  // full: scan mode
+  }
+  return needed_elsewhere(D, d, w, t) ? 0 : get_nbytes(D, d);
+}
+// _dec_needs_replica (only when d is in needs_what); t = task leaving w (processing_on cleared)
+__device__ int64_t needs_dec(const Dev& D, int w, int d, int t) {
+  uint32_t* line = needs_line(D, w);
+  if (line[NEEDS_W - 1] != NEEDS_OVF) {
+    const uint32_t key = (uint32_t)d << 8;
+    for (int q = 0; q < NEEDS_W / 4; q++) {
+      uint4 v = reinterpret_cast<const uint4*>(line)[q];
+      uint32_t e[4] = {v.x, v.y, v.z, v.w};
+      for (int i = 0; i < 4; i++)
+        if (e[i] != 0 && (e[i] & ~0xffu) == key) {
+          uint32_t ne = e[i] - 1;
+          bool gone = (ne & 0xffu) == 0;
+          line[4 * q + i] = gone ? 0u : ne;
+          return gone ? get_nbytes(D, d) : 0;
+        }
+    }
+    return 0;
+  }
+  return (!holds(D, d, w) && !needed_elsewhere(D, d, w, t)) ? get_nbytes(D, d) : 0;
+}
+// a worker with nothing processing needs nothing: leave scan mode
+__device__ __forceinline__ void needs_maybe_reset(const Dev& D, int w) {
+  uint32_t* line = needs_line(D, w);
+  if (line[NEEDS_W - 1] == NEEDS_OVF && WK_nproc(D)[w] == 0)
+    for (int i = 0; i < NEEDS_W; i++) line[i] = 0;
 }
 
 // ================================================================= mutations
@@ -476,19 +578,16 @@ __device__ void do_completion(const Dev& D, int t, int w, int64_t rslot, const d
   int p = D.prefix[t];
   D.proc_on[t] = -1;  // _exit_processing_common -> remove_from_processing :759-771
   wdict_dec(D, w, p);
-  D.w_nproc[w]--;
+  WK_nproc(D)[w]--;
   int64_t dnet = 0;
-  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
-    int d = D.dep_idx[k];
-    if (!holds(D, d, w) && !needed_elsewhere(D, d, w, t)) {
-      int64_t nb = get_nbytes(D, d);
-      D.w_netocc[w] -= nb;
-      dnet -= nb;
-    }
+  if (D.dep_ptr[t + 1] > D.dep_ptr[t]) {
+    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) dnet -= needs_dec(D, w, D.dep_idx[k], t);
+    WK_netocc(D)[w] += dnet;
   }
+  needs_maybe_reset(D, w);
   emit(D, rslot, REC_COMPLETE, t, w, p, dnet, dur);  // check_idle_saturated(ws) :3276
   // add_replica (:3148): the who_has bit and nbytes were published by k_frontier_release
-  D.w_nbytes[w] += get_nbytes(D, t);
+  WK_nbytes(D)[w] += get_nbytes(D, t);
   D.state[t] = S_MEMORY;
 }
 
@@ -501,7 +600,7 @@ __device__ void release_task(const Dev& D, int t) {
     while (bits) {
       int b = __ffsll((long long)bits) - 1;
       bits &= bits - 1;
-      D.w_nbytes[wd * 64 + b] -= nb;
+      WK_nbytes(D)[wd * 64 + b] -= nb;
     }
     row[wd] = 0;
   }
@@ -532,19 +631,18 @@ __device__ void do_place(const Dev& D, int t, int w, int route, int64_t comm, in
   D.st_worker[plslot] = w;
   D.st_comm[plslot] = comm;
   D.st_start[plslot] = o.start;
-  D.st_wsnbytes[plslot] = D.w_nbytes[w];
+  D.st_wsnbytes[plslot] = WK_nbytes(D)[w];
   D.st_route[plslot] = (int8_t)route;
   int p = D.prefix[t];
   if (!wdict_inc(D, w, p)) set_error(D, ERR_PREFIX_CAP, t);
-  D.w_nproc[w]++;
+  WK_nproc(D)[w]++;
   int64_t dnet = 0;
-  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
-    int d = D.dep_idx[k];
-    if (!holds(D, d, w) && !needed_elsewhere(D, d, w, t)) {
-      int64_t nb = get_nbytes(D, d);
-      D.w_netocc[w] += nb;
-      dnet += nb;
+  if (D.dep_ptr[t + 1] > D.dep_ptr[t]) {
+    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+      int d = D.dep_idx[k];
+      if (!holds(D, d, w)) dnet += needs_inc(D, w, d, t);
     }
+    WK_netocc(D)[w] += dnet;
   }
   if (t >= 0) {
     D.proc_on[t] = w;
@@ -595,7 +693,7 @@ __device__ void exec_local(const Dev& D, int j, int t, int w, unsigned long long
   // stimulus_queue_slots_maybe_opened (:4983): with a non-empty queue every other
   // worker is full, so the open slots are w's; the queued tasks are resolved in order later
   int pops = 0;
-  if (popmax > 0 && (D.w_flags[w] & WF_ITC)) {
+  if (popmax > 0 && (WK_flags(D)[w] & WF_ITC)) {
     int64_t slots = task_slots_available(D, w);
     for (int64_t i = 0; i < slots && pops < popmax; i++) {
       // place a placeholder (task -1) of the queue's prefix on w: route rootish-queuing
@@ -605,10 +703,10 @@ __device__ void exec_local(const Dev& D, int j, int t, int w, unsigned long long
       D.st_worker[plslot] = w;
       D.st_comm[plslot] = 0;
       D.st_start[plslot] = o.start;
-      D.st_wsnbytes[plslot] = D.w_nbytes[w];
+      D.st_wsnbytes[plslot] = WK_nbytes(D)[w];
       D.st_route[plslot] = ROUTE_ROOTISH_Q;
       if (!wdict_inc(D, w, pop_prefix)) set_error(D, ERR_PREFIX_CAP, -1);
-      D.w_nproc[w]++;
+      WK_nproc(D)[w]++;
       emit(D, rslot, REC_PLACE, -1, w, pop_prefix, 0, dur);
       itc_check(D, w, false);
       atomicAdd((unsigned long long*)&D.ctl->n_tasks, 1ull);
@@ -621,6 +719,458 @@ __device__ void exec_local(const Dev& D, int j, int t, int w, unsigned long long
   D.ev_pops[j] = pops;
 }
 
+
+// ================================================= local stimulus, one wave per stimulus
+//
+// Memory discipline (gfx950 counts loads and stores on one in-order vmcnt): every global
+// load of the stimulus is issued before any global store, the loads are spread over the
+// wave's lanes, worker state is touched only through typed LDS (ds_*) or global
+// accessors, and all global stores happen in one final phase.
+
+template <bool LW>
+struct WS;  // worker-state accessors: LW = state in the commit kernel's LDS carve
+template <>
+struct WS<true> {
+  static __device__ __forceinline__ int32_t* nthreads(const Dev& D) { return (int32_t*)lds_field_k<0>(D.W); }
+  static __device__ __forceinline__ int32_t* cap(const Dev& D) { return (int32_t*)lds_field_k<1>(D.W); }
+  static __device__ __forceinline__ int32_t* nproc(const Dev& D) { return (int32_t*)lds_field_k<2>(D.W); }
+  static __device__ __forceinline__ int32_t* plen(const Dev& D) { return (int32_t*)lds_field_k<3>(D.W); }
+  static __device__ __forceinline__ int32_t* pfx(const Dev& D) { return (int32_t*)lds_field_k<4>(D.W); }
+  static __device__ __forceinline__ int32_t* pcnt(const Dev& D) { return (int32_t*)lds_field_k<5>(D.W); }
+  static __device__ __forceinline__ int64_t* netocc(const Dev& D) { return (int64_t*)lds_field_k<6>(D.W); }
+  static __device__ __forceinline__ int64_t* nbytes(const Dev& D) { return (int64_t*)lds_field_k<7>(D.W); }
+  static __device__ __forceinline__ int64_t* itcslots(const Dev& D) { return (int64_t*)lds_field_k<8>(D.W); }
+  static __device__ __forceinline__ unsigned long long* lastcheck(const Dev& D) {
+    return (unsigned long long*)lds_field_k<9>(D.W);
+  }
+  static __device__ __forceinline__ uint8_t* flags(const Dev& D) { return (uint8_t*)lds_field_k<10>(D.W); }
+};
+template <>
+struct WS<false> {
+  static __device__ __forceinline__ int32_t* nthreads(const Dev& D) { return D.w_nthreads; }
+  static __device__ __forceinline__ int32_t* cap(const Dev& D) { return D.w_cap; }
+  static __device__ __forceinline__ int32_t* nproc(const Dev& D) { return D.w_nproc; }
+  static __device__ __forceinline__ int32_t* plen(const Dev& D) { return D.w_plen; }
+  static __device__ __forceinline__ int32_t* pfx(const Dev& D) { return D.w_pfx; }
+  static __device__ __forceinline__ int32_t* pcnt(const Dev& D) { return D.w_pcnt; }
+  static __device__ __forceinline__ int64_t* netocc(const Dev& D) { return D.w_netocc; }
+  static __device__ __forceinline__ int64_t* nbytes(const Dev& D) { return D.w_nbytes; }
+  static __device__ __forceinline__ int64_t* itcslots(const Dev& D) { return D.w_itcslots; }
+  static __device__ __forceinline__ unsigned long long* lastcheck(const Dev& D) { return D.w_lastcheck; }
+  static __device__ __forceinline__ uint8_t* flags(const Dev& D) { return D.w_flags; }
+};
+
+template <bool LW>
+__device__ __forceinline__ double occ_w(const Dev& D, int w, const double* dur) {  // _calc_occupancy :1884
+  using S = WS<LW>;
+  double res = 0.0;
+  const int n = S::plen(D)[w];
+  const int32_t* pf = S::pfx(D) + (size_t)w * PMAX;
+  const int32_t* pc = S::pcnt(D) + (size_t)w * PMAX;
+  for (int i = 0; i < n; i++) res += prefix_duration(D, dur, pf[i]) * (double)pc[i];
+  return res + (double)S::netocc(D)[w] / (double)D.bandwidth;
+}
+template <bool LW>
+__device__ __forceinline__ bool wd_inc(const Dev& D, int w, int p) {
+  using S = WS<LW>;
+  int32_t* pf = S::pfx(D) + (size_t)w * PMAX;
+  int32_t* pc = S::pcnt(D) + (size_t)w * PMAX;
+  int n = S::plen(D)[w];
+  for (int i = 0; i < n; i++)
+    if (pf[i] == p) {
+      pc[i]++;
+      return true;
+    }
+  if (n == PMAX) return false;
+  pf[n] = p;
+  pc[n] = 1;
+  S::plen(D)[w] = n + 1;
+  return true;
+}
+template <bool LW>
+__device__ __forceinline__ void wd_dec(const Dev& D, int w, int p) {
+  using S = WS<LW>;
+  int32_t* pf = S::pfx(D) + (size_t)w * PMAX;
+  int32_t* pc = S::pcnt(D) + (size_t)w * PMAX;
+  int n = S::plen(D)[w];
+  for (int i = 0; i < n; i++)
+    if (pf[i] == p) {
+      if (--pc[i] == 0) {
+        for (int k2 = i + 1; k2 < n; k2++) {
+          pf[k2 - 1] = pf[k2];
+          pc[k2 - 1] = pc[k2];
+        }
+        S::plen(D)[w] = n - 1;
+      }
+      return;
+    }
+}
+// idle_task_count part of check_idle_saturated; the global counters change by the returned deltas
+template <bool LW>
+__device__ __forceinline__ void itc_local(const Dev& D, int w, int64_t& d_itc, int64_t& d_slots) {
+  using S = WS<LW>;
+  int64_t slots = D.sat_inf ? 0 : (int64_t)S::cap(D)[w] - (int64_t)S::nproc(D)[w];
+  bool on = D.sat_inf || slots > 0;
+  uint8_t fl = S::flags(D)[w];
+  bool was = (fl & WF_ITC) != 0;
+  if (on != was) {
+    S::flags(D)[w] = on ? (fl | WF_ITC) : (fl & ~WF_ITC);
+    d_itc += on ? 1 : -1;
+  }
+  int64_t contrib = on ? slots : 0;
+  d_slots += contrib - S::itcslots(D)[w];
+  S::itcslots(D)[w] = contrib;
+}
+
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// one needs_what line cached in the lanes (entry `lane`), see NeedsLine layout above
+struct LaneLine {
+  int w;        // worker, -1 unused
+  uint32_t e;   // this lane's entry
+  bool dirty;
+};
+
+template <bool LW>
+__device__ void exec_local_wave(const Dev& D, int j, int t, int w, unsigned long long key, const double* dur,
+                                int64_t plbase, int64_t recbase, int popmax, int pop_prefix) {
+  using S = WS<LW>;
+  const int lane = threadIdx.x & 63;
+  unsigned long long _ts = __builtin_amdgcn_s_memtime();
+  // ------------------------------------------------------------ gather (loads only)
+  const int64_t d0 = D.dep_ptr[t], d1 = D.dep_ptr[t + 1];
+  const int64_t e0 = D.dpt_ptr[t], e1 = D.dpt_ptr[t + 1];
+  const int k = (int)(d1 - d0), f = (int)(e1 - e0);
+  const int p = D.prefix[t];
+  const int64_t nbt = get_nbytes(D, t);
+  const bool t_wanted = (D.tflags[t] & TF_WANTED) != 0;
+  const int dl = lane < k ? D.dep_idx[d0 + lane] : -1;
+  const int xl = lane < f ? D.dpt_idx[e0 + lane] : -1;
+  LaneLine ln[9];
+  ln[0].w = w;
+  ln[0].e = lane < NEEDS_W ? needs_line(D, w)[lane] : 0u;
+  ln[0].dirty = false;
+  for (int q = 1; q < 9; q++) {
+    ln[q].w = -1;
+    ln[q].e = 0;
+    ln[q].dirty = false;
+  }
+  const int64_t nbd = dl >= 0 ? get_nbytes(D, dl) : 0;
+  const bool hd = dl >= 0 ? holds(D, dl, w) : true;
+  const bool reld = dl >= 0 && D.release_key[dl] == key && D.waiters[dl] == 0 && !(D.tflags[dl] & TF_WANTED);
+  const bool fr = xl >= 0 && is_frontier(D, xl, key);
+  const unsigned long long frmask = __ballot(fr);
+  const unsigned long long relmask = __ballot(reld);
+  const bool self_rel = f == 0 && !t_wanted;
+  const bool w_ovf = __shfl(ln[0].e, NEEDS_W - 1) == NEEDS_OVF;
+  { unsigned long long _t = __builtin_amdgcn_s_memtime(); if (lane == 0) atomicAdd(&D.ctl->prof2[0], _t - _ts); _ts = _t; }
+  // records (lane r holds record r) and placements (lane q holds placement q)
+  int r_kind = REC_NONE, r_task = -1, r_w = 0, r_prefix = 0, r_np = 0;
+  int64_t r_dnet = 0;
+  double r_occ = 0;
+  int q_task = -1, q_w = 0;
+  int64_t q_comm = 0, q_wsnb = 0;
+  double q_start = 0;
+  int8_t q_route = 0;
+  int nrec = 0, npl = 0;
+  int64_t d_itc = 0, d_slots = 0;
+  int xw = -1;  // in a frontier task's lane: the worker it was placed on
+
+  // ------------------------------------------------------ completion (:2366-2442)
+  int64_t dnet = 0;
+  if (k > 0) {
+    if (!w_ovf) {
+      for (int i = 0; i < k; i++) {  // _dec_needs_replica for every dependency in needs_what
+        const uint32_t key_i = (uint32_t)__shfl(dl, i) << 8;
+        const unsigned long long m = __ballot(lane < NEEDS_W - 1 && ln[0].e != 0 && (ln[0].e & ~0xffu) == key_i);
+        if (m) {
+          const int ml = __ffsll((long long)m) - 1;
+          if (lane == ml) {
+            ln[0].e -= 1;
+            if ((ln[0].e & 0xffu) == 0) ln[0].e = 0;
+          }
+          ln[0].dirty = true;
+          if (__shfl(ln[0].e, ml) == 0) dnet -= __shfl(nbd, i);
+        }
+      }
+    } else {
+      const int64_t mine = (dl >= 0 && !hd && !needed_elsewhere(D, dl, w, t)) ? nbd : 0;
+      dnet = -wave_sum64(mine);
+    }
+  }
+  if (lane == 0) {
+    wd_dec<LW>(D, w, p);
+    S::nproc(D)[w]--;
+    S::netocc(D)[w] += dnet;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (w_ovf && S::nproc(D)[w] == 0) {  // nothing processing: leave scan mode
+    ln[0].e = 0;
+    ln[0].dirty = true;
+  }
+  {
+    const double o = occ_w<LW>(D, w, dur);
+    const int np = S::nproc(D)[w];
+    if (lane == 0) {
+      r_kind = REC_COMPLETE;
+      r_task = t;
+      r_w = w;
+      r_prefix = p;
+      r_dnet = dnet;
+      r_occ = o;
+      r_np = np;
+      S::lastcheck(D)[w] = (unsigned long long)recbase;
+      itc_local<LW>(D, w, d_itc, d_slots);
+      S::nbytes(D)[w] += nbt;  // add_replica
+    }
+    nrec = 1;
+  }
+  __builtin_amdgcn_wave_barrier();
+  { unsigned long long _t = __builtin_amdgcn_s_memtime(); if (lane == 0) atomicAdd(&D.ctl->prof2[1], _t - _ts); _ts = _t; }
+  // releases (popped before the frontier); remove_all_replicas -> holders' nbytes
+  {
+    unsigned long long rm = relmask;
+    while (rm) {
+      const int i = __ffsll((long long)rm) - 1;
+      rm &= rm - 1;
+      const int d = __shfl(dl, i);
+      const int64_t nb = __shfl(nbd, i);
+      for (int wd = lane; wd < D.WB; wd += 64) {
+        unsigned long long bits = D.holders[(size_t)d * D.WB + wd];
+        while (bits) {
+          const int b = __ffsll((long long)bits) - 1;
+          bits &= bits - 1;
+          atomicAdd((unsigned long long*)&S::nbytes(D)[wd * 64 + b], (unsigned long long)(-nb));
+        }
+      }
+    }
+    if (self_rel && lane == 0) S::nbytes(D)[w] -= nbt;  // t's only replica is on w
+  }
+  __builtin_amdgcn_wave_barrier();
+
+  { unsigned long long _t = __builtin_amdgcn_s_memtime(); if (lane == 0) atomicAdd(&D.ctl->prof2[2], _t - _ts); _ts = _t; }
+  // ------------------------------------------ frontier placements, ascending priority
+  unsigned long long fm = frmask;
+  while (fm) {
+    const int fi = __ffsll((long long)fm) - 1;
+    fm &= fm - 1;
+    const int x = __shfl(xl, fi);
+    const int px = D.prefix[x];
+    const int cn = D.cand_n[x];
+    const int64_t co = D.cand_off[x];
+    const int64_t xd0 = D.dep_ptr[x], xd1 = D.dep_ptr[x + 1];
+    const int kx = (int)(xd1 - xd0);
+    const int cl = lane < cn ? D.pool_w[co + lane] : -1;
+    const int64_t cm = lane < cn ? D.pool_comm[co + lane] : 0;
+    const int dxl = lane < kx ? D.dep_idx[xd0 + lane] : -1;
+    const int64_t nbx = dxl >= 0 ? get_nbytes(D, dxl) : 0;
+  { unsigned long long _t = __builtin_amdgcn_s_memtime(); if (lane == 0) atomicAdd(&D.ctl->prof2[3], _t - _ts); _ts = _t; }
+    // decide_worker (:8550-8593): argmin of worker_objective over the candidates
+    Obj o{INFINITY, INT64_MAX, INT32_MAX};
+    if (cl >= 0) o = Obj{occ_w<LW>(D, cl, dur) / (double)S::nthreads(D)[cl] + (double)cm / (double)D.bandwidth,
+                         S::nbytes(D)[cl], cl};
+    int64_t ocm = cm;
+    for (int off = 32; off > 0; off >>= 1) {
+      Obj q{__shfl_xor(o.start, off), __shfl_xor(o.nbytes, off), __shfl_xor(o.w, off)};
+      const int64_t qc = __shfl_xor(ocm, off);
+      if (obj_less(q, o)) {
+        o = q;
+        ocm = qc;
+      }
+    }
+    const int c = o.w;
+  { unsigned long long _t = __builtin_amdgcn_s_memtime(); if (lane == 0) atomicAdd(&D.ctl->prof2[4], _t - _ts); _ts = _t; }
+    const bool hx = dxl >= 0 ? holds(D, dxl, c) : true;
+    // the needs_what line of c in the lanes
+    int li = -1;
+    for (int q = 0; q < 9; q++)
+      if (li < 0 && ln[q].w == c) li = q;
+    if (li < 0)
+      for (int q = 1; q < 9; q++)
+        if (li < 0 && ln[q].w < 0) {
+          li = q;
+          ln[q].w = c;
+          ln[q].e = lane < NEEDS_W ? needs_line(D, c)[lane] : 0u;
+          ln[q].dirty = false;
+        }
+    // (k_events caps the frontier at 8 tasks, so a slot is always free)
+    uint32_t e = 0;
+    for (int q = 0; q < 9; q++)
+      if (q == li) e = ln[q].e;
+    bool ovf = __shfl(e, NEEDS_W - 1) == NEEDS_OVF;
+  { unsigned long long _t = __builtin_amdgcn_s_memtime(); if (lane == 0) atomicAdd(&D.ctl->prof2[5], _t - _ts); _ts = _t; }
+    int64_t dnx = 0;
+    bool dirty = false;
+    for (int i = 0; i < kx && !ovf; i++) {  // _inc_needs_replica
+      if (__shfl(hx, i)) continue;
+      const uint32_t key_i = (uint32_t)__shfl(dxl, i) << 8;
+      const unsigned long long m = __ballot(lane < NEEDS_W - 1 && e != 0 && (e & ~0xffu) == key_i);
+      if (m) {
+        const int ml = __ffsll((long long)m) - 1;
+        if ((__shfl(e, ml) & 0xffu) == 0xffu) {
+          ovf = true;
+          break;
+        }
+        if (lane == ml) e += 1;
+      } else {
+        const unsigned long long em = __ballot(lane < NEEDS_W - 1 && e == 0);
+        if (!em) {
+          ovf = true;
+          break;
+        }
+        if (lane == __ffsll((long long)em) - 1) e = key_i | 1u;
+        dnx += __shfl(nbx, i);
+      }
+      dirty = true;
+    }
+    if (ovf) {
+      // scan mode for c: publish the processing_on of this stimulus' earlier placements
+      // first (the scan reads them), then decide each dependency exactly
+      if (lane == NEEDS_W - 1) e = NEEDS_OVF;
+      dirty = true;
+      if (xw >= 0) D.proc_on[xl] = xw;
+      __threadfence_block();
+      const int64_t mine = (dxl >= 0 && !hx && !needed_elsewhere(D, dxl, c, x)) ? nbx : 0;
+      dnx = wave_sum64(mine);
+    }
+    for (int q = 0; q < 9; q++)
+      if (q == li) {
+        ln[q].e = e;
+        ln[q].dirty = ln[q].dirty || dirty;
+      }
+    // _add_to_processing (:3199): record, WorkerState.add_to_processing, check_idle_saturated
+    if (lane == npl) {
+      q_task = x;
+      q_w = c;
+      q_comm = ocm;
+      q_start = o.start;
+      q_wsnb = o.nbytes;
+      q_route = ROUTE_NONROOTISH;
+    }
+    if (lane == 0) {
+      if (!wd_inc<LW>(D, c, px)) set_error(D, ERR_PREFIX_CAP, x);
+      S::nproc(D)[c]++;
+      S::netocc(D)[c] += dnx;
+    }
+    __builtin_amdgcn_wave_barrier();
+    {
+      const double oc = occ_w<LW>(D, c, dur);
+      const int np = S::nproc(D)[c];
+      if (lane == nrec) {
+        r_kind = REC_PLACE;
+        r_task = x;
+        r_w = c;
+        r_prefix = px;
+        r_dnet = dnx;
+        r_occ = oc;
+        r_np = np;
+      }
+      if (lane == 0) {
+        S::lastcheck(D)[c] = (unsigned long long)(recbase + nrec);
+        itc_local<LW>(D, c, d_itc, d_slots);
+      }
+    }
+    if (lane == fi) xw = c;
+    npl++;
+    nrec++;
+    __builtin_amdgcn_wave_barrier();
+  { unsigned long long _t = __builtin_amdgcn_s_memtime(); if (lane == 0) atomicAdd(&D.ctl->prof2[6], _t - _ts); _ts = _t; }
+  }
+  // ----------------- queue refill: with a non-empty queue only w can have open slots
+  int pops = 0;
+  if (popmax > 0) {
+    int64_t slots = S::cap(D)[w] - (int64_t)S::nproc(D)[w];
+    if (!(S::flags(D)[w] & WF_ITC)) slots = 0;
+    for (int64_t i = 0; i < slots && pops < popmax; i++) {
+      const double o0 = occ_w<LW>(D, w, dur);
+      const int64_t nb0 = S::nbytes(D)[w];
+      if (lane == npl) {
+        q_task = -1;  // resolved in queue order after the commit
+        q_w = w;
+        q_comm = 0;
+        q_start = o0 / (double)S::nthreads(D)[w];
+        q_wsnb = nb0;
+        q_route = ROUTE_ROOTISH_Q;
+      }
+      if (lane == 0) {
+        if (!wd_inc<LW>(D, w, pop_prefix)) set_error(D, ERR_PREFIX_CAP, -1);
+        S::nproc(D)[w]++;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const double o1 = occ_w<LW>(D, w, dur);
+      const int np = S::nproc(D)[w];
+      if (lane == nrec) {
+        r_kind = REC_PLACE;
+        r_task = -1;
+        r_w = w;
+        r_prefix = pop_prefix;
+        r_dnet = 0;
+        r_occ = o1;
+        r_np = np;
+      }
+      if (lane == 0) {
+        S::lastcheck(D)[w] = (unsigned long long)(recbase + nrec);
+        itc_local<LW>(D, w, d_itc, d_slots);
+      }
+      __builtin_amdgcn_wave_barrier();
+      npl++;
+      nrec++;
+      pops++;
+    }
+  }
+
+  { unsigned long long _t = __builtin_amdgcn_s_memtime(); if (lane == 0) atomicAdd(&D.ctl->prof2[7], _t - _ts); _ts = _t; }
+  // ----------------------------------------------------------------- store phase
+  if (lane == 0) {
+    D.state[t] = self_rel ? S_RELEASED : S_MEMORY;
+    D.proc_on[t] = -1;
+    if (self_rel) atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], 1ull);
+    D.ev_npl[j] = npl;
+    D.ev_pops[j] = pops;
+    if (d_itc) atomicAdd((unsigned long long*)&D.ctl->n_itc, (unsigned long long)d_itc);
+    if (d_slots) atomicAdd((unsigned long long*)&D.ctl->itc_slots, (unsigned long long)d_slots);
+    atomicAdd((unsigned long long*)&D.ctl->n_tasks, (unsigned long long)npl);
+  }
+  if (self_rel)
+    for (int wd = lane; wd < D.WB; wd += 64) D.holders[(size_t)t * D.WB + wd] = 0;
+  if (reld) {
+    D.state[dl] = S_RELEASED;
+    for (int wd = 0; wd < D.WB; wd++) D.holders[(size_t)dl * D.WB + wd] = 0;
+    atomicAdd((unsigned long long*)&D.g_relwait[D.group[dl]], 1ull);
+  }
+  if (xw >= 0) {
+    D.state[xl] = S_PROCESSING;
+    D.proc_on[xl] = xw;
+    atomicAdd((unsigned long long*)&D.g_relwait[D.group[xl]], (unsigned long long)-1ll);
+  }
+  for (int q = 0; q < 9; q++)
+    if (ln[q].w >= 0 && __ballot(ln[q].dirty) && lane < NEEDS_W) needs_line(D, ln[q].w)[lane] = ln[q].e;
+  if (lane < nrec) {
+    Rec r;
+    r.kind = r_kind;
+    r.task = r_task;
+    r.w = r_w;
+    r.prefix = r_prefix;
+    r.dnet = r_dnet;
+    r.occ = r_occ;
+    r.nproc = r_np;
+    r.pad = 0;
+    D.rec[recbase + lane] = r;
+  }
+  if (lane < npl) {
+    const int64_t sl = plbase + lane;
+    D.st_task[sl] = q_task;
+    D.st_worker[sl] = q_w;
+    D.st_comm[sl] = q_comm;
+    D.st_start[sl] = q_start;
+    D.st_wsnbytes[sl] = q_wsnb;
+    D.st_route[sl] = q_route;
+  }
+  { unsigned long long _t = __builtin_amdgcn_s_memtime(); if (lane == 0) atomicAdd(&D.ctl->prof2[8], _t - _ts); _ts = _t; }
+}
 
 // ======================================================= block-level collectives
 
@@ -700,7 +1250,7 @@ __device__ int64_t gather_pool(const Dev& D, bool use_idle, int32_t* list, int c
   int64_t base = 0;
   for (int w0 = 0; w0 < D.W; w0 += blockDim.x) {
     int w = w0 + threadIdx.x;
-    bool in = w < D.W && (!use_idle || (D.w_flags[w] & WF_IDLE));
+    bool in = w < D.W && (!use_idle || (WK_flags(D)[w] & WF_IDLE));
     int64_t tot;
     int64_t pos = block_excl_scan(in ? 1 : 0, &tot);
     if (in && base + pos < cap) list[base + pos] = w;
@@ -737,7 +1287,7 @@ __device__ void apply_now(const Dev& D, int32_t kind, int t, int w, int p, int64
     set_error(D, ERR_GPREFIX_CAP, t);
   }
   c->g_netocc += (double)dnet;
-  walk_flags(D, w, occupancy(D, w, dur), D.w_nproc[w]);
+  walk_flags(D, w, occupancy(D, w, dur), WK_nproc(D)[w]);
 }
 
 // _add_to_processing for global stimuli: staging slot from the overflow area
@@ -755,19 +1305,18 @@ __device__ void place_eager(const Dev& D, int t, int w, int route, int64_t comm,
   D.st_worker[slot] = w;
   D.st_comm[slot] = comm;
   D.st_start[slot] = o.start;
-  D.st_wsnbytes[slot] = D.w_nbytes[w];
+  D.st_wsnbytes[slot] = WK_nbytes(D)[w];
   D.st_route[slot] = (int8_t)route;
   int p = D.prefix[t];
   if (!wdict_inc(D, w, p)) set_error(D, ERR_PREFIX_CAP, t);
-  D.w_nproc[w]++;
+  WK_nproc(D)[w]++;
   int64_t dnet = 0;
-  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
-    int d = D.dep_idx[k];
-    if (!holds(D, d, w) && !needed_elsewhere(D, d, w, t)) {
-      int64_t nb = get_nbytes(D, d);
-      D.w_netocc[w] += nb;
-      dnet += nb;
+  if (D.dep_ptr[t + 1] > D.dep_ptr[t]) {
+    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+      int d = D.dep_idx[k];
+      if (!holds(D, d, w)) dnet += needs_inc(D, w, d, t);
     }
+    WK_netocc(D)[w] += dnet;
   }
   D.proc_on[t] = w;
   if (D.state[t] == S_WAITING) atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], (unsigned long long)-1ll);
@@ -849,7 +1398,7 @@ __device__ int dispatch_prepare(const Dev& D, int x, CoopShared& S, int64_t* sta
 }
 
 // all lanes: the collective part, then lane 0 finishes the placement
-__device__ void dispatch_collective(const Dev& D, CoopShared& S, int64_t* stage_next, const double* dur) {
+__device__ __attribute__((noinline)) void dispatch_collective(const Dev& D, CoopShared& S, int64_t* stage_next, const double* dur) {
   int op = S.op, x = S.x;
   Ctl* c = D.ctl;
   if (op == OP_ARGMIN_POOL) {
@@ -858,7 +1407,7 @@ __device__ void dispatch_collective(const Dev& D, CoopShared& S, int64_t* stage_
     int64_t bcomm = 0;
     bool have = false;
     for (int w = threadIdx.x; w < D.W; w += blockDim.x) {
-      if (use_idle && !(D.w_flags[w] & WF_IDLE)) continue;
+      if (use_idle && !(WK_flags(D)[w] & WF_IDLE)) continue;
       int64_t cm = comm_bytes(D, x, w);
       Obj o = objective(D, w, cm, dur);
       if (!have || obj_less(o, best)) {
@@ -876,7 +1425,7 @@ __device__ void dispatch_collective(const Dev& D, CoopShared& S, int64_t* stage_
         atomicAdd((unsigned long long*)&D.g_relwait[gi], (unsigned long long)-1ll);
         c->n_unrunnable++;
       } else {
-        D.g_left[gi] = (int64_t)floor(((double)D.g_size[gi] / (double)D.total_nthreads) * (double)D.w_nthreads[w]);
+        D.g_left[gi] = (int64_t)floor(((double)D.g_size[gi] / (double)D.total_nthreads) * (double)WK_nthreads(D)[w]);
         D.g_lastw[gi] = D.g_relwait[gi] > 1 ? w : -1;
         D.g_left[gi] -= 1;
         place_eager(D, x, w, ROUTE_ROOTISH_NOQ, b.comm, stage_next, dur);
@@ -892,7 +1441,7 @@ __device__ void dispatch_collective(const Dev& D, CoopShared& S, int64_t* stage_
       __shared__ int s_kth;
       for (int w0 = 0; w0 < D.W; w0 += blockDim.x) {
         int w = w0 + threadIdx.x;
-        bool in = w < D.W && (D.w_flags[w] & WF_IDLE);
+        bool in = w < D.W && (WK_flags(D)[w] & WF_IDLE);
         int64_t tot;
         int64_t pos = block_excl_scan(in ? 1 : 0, &tot);
         if (in && base + pos == k) s_kth = w;
@@ -927,7 +1476,7 @@ __device__ void dispatch_collective(const Dev& D, CoopShared& S, int64_t* stage_
 }
 
 // dispatch S.list[0..nlist) in order (all lanes)
-__device__ void dispatch_list_coop(const Dev& D, CoopShared& S, int64_t* stage_next, const double* dur) {
+__device__ __attribute__((noinline)) void dispatch_list_coop(const Dev& D, CoopShared& S, int64_t* stage_next, const double* dur) {
   if (threadIdx.x == 0) S.pos = 0;
   __syncthreads();
   while (true) {
@@ -953,7 +1502,7 @@ __device__ void dispatch_list_coop(const Dev& D, CoopShared& S, int64_t* stage_n
 }
 
 // Scheduler.stimulus_queue_slots_maybe_opened :4983-5023 (lane 0, tree maintained)
-__device__ void queue_refill_eager(const Dev& D, int64_t* stage_next, const double* dur) {
+__device__ __attribute__((noinline)) void queue_refill_eager(const Dev& D, int64_t* stage_next, const double* dur) {
   Ctl* c = D.ctl;
   if (c->qlen == 0) return;
   int64_t slots = c->itc_slots;
@@ -968,7 +1517,7 @@ __device__ void queue_refill_eager(const Dev& D, int64_t* stage_next, const doub
 }
 
 // resolve the queued tasks taken by local stimuli [from, to) (all lanes)
-__device__ void resolve_pops_coop(const Dev& D, const int32_t* L, int from, int to) {
+__device__ __attribute__((noinline)) void resolve_pops_coop(const Dev& D, const int32_t* L, int from, int to) {
   Ctl* c = D.ctl;
   int64_t base = 0;
   for (int j0 = from; j0 < to; j0 += blockDim.x) {
@@ -1000,23 +1549,25 @@ __device__ void resolve_pops_coop(const Dev& D, const int32_t* L, int from, int 
 
 // ================================================================== kernels
 
-__global__ void k_init_workers(Dev D) {
+__global__ void k_init_workers(const Dev* __restrict__ Dp) {
+  const Dev& D = *Dp;
   for (int w = blockIdx.x * blockDim.x + threadIdx.x; w < D.W; w += gridDim.x * blockDim.x) {
-    D.w_nproc[w] = 0;
-    D.w_plen[w] = 0;
-    D.w_netocc[w] = 0;
-    D.w_nbytes[w] = 0;
-    D.w_itcslots[w] = 0;
-    D.w_lastcheck[w] = ~0ull;
+    WK_nproc(D)[w] = 0;
+    WK_plen(D)[w] = 0;
+    WK_netocc(D)[w] = 0;
+    WK_nbytes(D)[w] = 0;
+    WK_itcslots(D)[w] = 0;
+    WK_lastcheck(D)[w] = ~0ull;
+    for (int i = 0; i < NEEDS_W; i++) D.w_needs[(size_t)w * NEEDS_W + i] = 0;
     // Scheduler.add_worker ends with check_idle_saturated(ws) (:4418): a worker with no
     // tasks is idle (p < nthreads), never saturated, and in idle_task_count unless its
     // slot count is 0
     bool itc = !worker_full(D, w);
-    D.w_flags[w] = WF_IDLE | (itc ? WF_ITC : 0);
+    WK_flags(D)[w] = WF_IDLE | (itc ? WF_ITC : 0);
     if (itc) {
-      D.w_itcslots[w] = task_slots_available(D, w);
+      WK_itcslots(D)[w] = task_slots_available(D, w);
       atomicAdd((unsigned long long*)&D.ctl->n_itc, 1ull);
-      atomicAdd((unsigned long long*)&D.ctl->itc_slots, (unsigned long long)D.w_itcslots[w]);
+      atomicAdd((unsigned long long*)&D.ctl->itc_slots, (unsigned long long)WK_itcslots(D)[w]);
     }
     atomicAdd((unsigned long long*)&D.ctl->n_idle, 1ull);
   }
@@ -1025,7 +1576,8 @@ __global__ void k_init_workers(Dev D) {
 // update_graph, part 1 (:4600-4611 -> _transition_released_waiting :2078-2119), every
 // task in parallel: waiting_on = dependencies without a replica; waiters = dependents
 // (all of them go to waiting in the same stimulus; priorities are topological)
-__global__ void k_ug_init(Dev D) {
+__global__ void k_ug_init(const Dev* __restrict__ Dp) {
+  const Dev& D = *Dp;
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < D.N; t += gridDim.x * blockDim.x) {
     int wo = 0;
     for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
@@ -1043,7 +1595,8 @@ __global__ void k_ug_init(Dev D) {
 // update_graph, part 2: the tasks that went waiting -> processing, in priority order,
 // dispatched one by one (they read global state); once idle_task_count is empty every
 // further root-ish task is queued in bulk (:2761) — order-preserving.
-__global__ void __launch_bounds__(CTA) k_ug_dispatch(Dev D) {
+__global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp) {
+  const Dev& D = *Dp;
   __shared__ CoopShared S;
   __shared__ int64_t s_nr, s_pos;
   Ctl* c = D.ctl;
@@ -1157,7 +1710,7 @@ __global__ void __launch_bounds__(CTA) k_ug_dispatch(Dev D) {
 
 // start of a round: its completion list is the slice of the placement log made by the
 // previous stimulus batch
-__global__ void k_round_begin(Dev D, long long* next_start, const int32_t* ext, long long ext_n) {
+__device__ void round_begin(const Dev& D, long long* next_start, const int32_t* ext, long long ext_n) {
   Ctl* c = D.ctl;
   if (ext) {  // an explicit batch of completions (dgp_tasks_finished)
     c->round_L = ext;
@@ -1173,13 +1726,16 @@ __global__ void k_round_begin(Dev D, long long* next_start, const int32_t* ext, 
   c->round_counter++;
   if (c->round_n > 0) c->rounds_nonempty++;
 }
+__global__ void k_round_begin(const Dev* __restrict__ Dp, long long* next_start, const int32_t* ext, long long ext_n) {
+  round_begin(*Dp, next_start, ext, ext_n);
+}
 
-__global__ void k_frontier_release(Dev D) {
+__device__ void frontier_release_body(const Dev& D, int64_t gtid, int64_t gthreads) {
   const Ctl* c = D.ctl;
   const int64_t n = c->round_n;
   const int32_t* L = c->round_L;
   const unsigned long long tag = (unsigned long long)c->round_counter << 32;
-  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t j = gtid; j < n; j += gthreads) {
     int t = L[j];
     unsigned long long key = tag | (unsigned long long)j;
     // the replica this completion creates is known before the ordered commit: publish it
@@ -1204,12 +1760,14 @@ __global__ void k_frontier_release(Dev D) {
   }
 }
 
+__global__ void k_frontier_release(const Dev* __restrict__ Dp) {
+  frontier_release_body(*Dp, blockIdx.x * (int64_t)blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+}
+
 // one wave per newly ready task: candidate workers (OR of the dependencies' replica
 // bitsets) and, per candidate, the exact comm bytes (total minus what it holds)
-__global__ void k_candidate_commbytes(Dev D) {
+__device__ void candidate_body(const Dev& D, int64_t wave, int64_t nwaves) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t nF = (int64_t)D.ctl->n_frontier;
   for (int64_t i = wave; i < nF; i += nwaves) {
     int x = D.frontier[i];
@@ -1274,15 +1832,19 @@ __global__ void k_candidate_commbytes(Dev D) {
   }
 }
 
+__global__ void k_candidate_commbytes(const Dev* __restrict__ Dp) {
+  candidate_body(*Dp, (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6, ((int64_t)gridDim.x * blockDim.x) >> 6);
+}
+
 enum : uint8_t { EV_MAYQUEUE = 2 };
 
 // per completion stimulus j: the workers it may touch and whether it reads global state
-__global__ void k_events(Dev D) {
+__device__ void events_body(const Dev& D, int64_t gtid, int64_t gthreads) {
   const Ctl* c = D.ctl;
   const int64_t n = c->round_n;
   const int32_t* L = c->round_L;
   const unsigned long long tag = (unsigned long long)c->round_counter << 32;
-  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t j = gtid; j < n; j += gthreads) {
     int t = L[j];
     unsigned long long key = tag | (unsigned long long)j;
     int w = D.proc_on[t];
@@ -1313,6 +1875,9 @@ __global__ void k_events(Dev D) {
       }
     }
     int nf = 0;
+    // the one-wave local executor handles <= 64 dependencies / dependents / candidates
+    // and <= 8 released tasks per stimulus; anything bigger runs as a global stimulus
+    if (D.dep_ptr[t + 1] - D.dep_ptr[t] > 64 || D.dpt_ptr[t + 1] - D.dpt_ptr[t] > 64) fl |= EV_GLOBAL;
     for (int64_t k = D.dpt_ptr[t]; k < D.dpt_ptr[t + 1]; k++) {
       int x = D.dpt_idx[k];
       if (!is_frontier(D, x, key)) continue;
@@ -1324,24 +1889,31 @@ __global__ void k_events(Dev D) {
       } else {
         int cn = D.cand_n[x];
         int64_t off = D.cand_off[x];
-        for (int i = 0; i < cn; i++) add(D.pool_w[off + i]);
+        if (cn > 64 || D.dep_ptr[x + 1] - D.dep_ptr[x] > 64) fl |= EV_GLOBAL;
+        for (int i = 0; i < cn && i < 64; i++) add(D.pool_w[off + i]);
       }
     }
+    if (nf > 8) fl |= EV_GLOBAL;
     D.ev_w[j] = w;
     D.ev_nf[j] = nf;
     D.ev_flags[j] = fl;
     D.ev_ntouch[j] = nt;
   }
 }
+__global__ void k_events(const Dev* __restrict__ Dp) {
+  events_body(*Dp, blockIdx.x * (int64_t)blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+}
 
 // global stimulus j (all lanes): waits for nothing — every earlier stimulus has committed
-__device__ void exec_global(const Dev& D, const int32_t* L, int j, unsigned long long key, const double* dur,
+__device__ __attribute__((noinline)) void exec_global(const Dev& D, const int32_t* L, int j, unsigned long long key, const double* dur,
                             CoopShared& S, int64_t* stage_next, int* resolved_upto) {
   Ctl* c = D.ctl;
   resolve_pops_coop(D, L, *resolved_upto, j);
   if (threadIdx.x == 0) {
     *resolved_upto = j;
+    unsigned long long tw = __builtin_amdgcn_s_memtime();
     walk_to(D, (unsigned long long)D.ev_recbase[j]);
+    (void)tw;
   }
   __syncthreads();
   tree_rebuild_coop(D);
@@ -1354,19 +1926,16 @@ __device__ void exec_global(const Dev& D, const int32_t* L, int j, unsigned long
     int p = D.prefix[t];
     D.proc_on[t] = -1;
     wdict_dec(D, w, p);
-    D.w_nproc[w]--;
+    WK_nproc(D)[w]--;
     int64_t dnet = 0;
-    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
-      int d = D.dep_idx[k];
-      if (!holds(D, d, w) && !needed_elsewhere(D, d, w, t)) {
-        int64_t nb = get_nbytes(D, d);
-        D.w_netocc[w] -= nb;
-        dnet -= nb;
-      }
+    if (D.dep_ptr[t + 1] > D.dep_ptr[t]) {
+      for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) dnet -= needs_dec(D, w, D.dep_idx[k], t);
+      WK_netocc(D)[w] += dnet;
     }
+    needs_maybe_reset(D, w);
     apply_now(D, REC_COMPLETE, t, w, p, dnet, dur);
     itc_check(D, w, true);
-    D.w_nbytes[w] += get_nbytes(D, t);
+    WK_nbytes(D)[w] += get_nbytes(D, t);
     D.state[t] = S_MEMORY;
     do_releases(D, t, key);
     s_dpos = D.dpt_ptr[t];
@@ -1398,16 +1967,72 @@ __device__ void exec_global(const Dev& D, const int32_t* L, int j, unsigned long
   __syncthreads();
 }
 
-// the ordered commit of one round (one workgroup; owner[] in dynamic LDS)
-__global__ void __launch_bounds__(CTA) k_commit(Dev D) {
-  extern __shared__ __attribute__((aligned(16))) int owner[];
+// bytes of dynamic LDS per worker when the commit keeps worker state on chip
+constexpr int LDS_WORKER_BYTES = 4 + 4 + 4 + 4 + 4 * PMAX + 4 * PMAX + 8 + 8 + 8 + 8 + 1;
+constexpr int LDS_WORKERS_MAX = 1024;
+
+// copy worker state between HBM (D.w_*) and the LDS carve (dir 0: load, 1: store back)
+__device__ void workers_lds(const Dev& D, int dir) {
+  const int W = D.W;
+  int32_t* nth = (int32_t*)lds_field(W, 0);
+  int32_t* cap = (int32_t*)lds_field(W, 1);
+  int32_t* npr = (int32_t*)lds_field(W, 2);
+  int32_t* pl = (int32_t*)lds_field(W, 3);
+  int32_t* pf = (int32_t*)lds_field(W, 4);
+  int32_t* pc = (int32_t*)lds_field(W, 5);
+  int64_t* no = (int64_t*)lds_field(W, 6);
+  int64_t* nb = (int64_t*)lds_field(W, 7);
+  int64_t* its = (int64_t*)lds_field(W, 8);
+  unsigned long long* lc = (unsigned long long*)lds_field(W, 9);
+  uint8_t* fl = (uint8_t*)lds_field(W, 10);
+  for (int w = threadIdx.x; w < W; w += blockDim.x) {
+    if (dir == 0) {
+      nth[w] = D.w_nthreads[w];
+      cap[w] = D.w_cap[w];
+      npr[w] = D.w_nproc[w];
+      pl[w] = D.w_plen[w];
+      no[w] = D.w_netocc[w];
+      nb[w] = D.w_nbytes[w];
+      its[w] = D.w_itcslots[w];
+      lc[w] = D.w_lastcheck[w];
+      fl[w] = D.w_flags[w];
+    } else {
+      D.w_nproc[w] = npr[w];
+      D.w_plen[w] = pl[w];
+      D.w_netocc[w] = no[w];
+      D.w_nbytes[w] = nb[w];
+      D.w_itcslots[w] = its[w];
+      D.w_lastcheck[w] = lc[w];
+      D.w_flags[w] = fl[w];
+    }
+  }
+  for (int i = threadIdx.x; i < W * PMAX; i += blockDim.x) {
+    if (dir == 0) {
+      pf[i] = D.w_pfx[i];
+      pc[i] = D.w_pcnt[i];
+    } else {
+      D.w_pfx[i] = pf[i];
+      D.w_pcnt[i] = pc[i];
+    }
+  }
+}
+
+// the ordered commit of one round (one workgroup; owner[] and, for W <= 1024, the
+// worker state in dynamic LDS)
+__device__ void commit_body(const Dev& D, bool manage_lds) {
+  int* owner = (int*)dgp_smem;
   __shared__ CoopShared S;
-  __shared__ int win[CTA];
-  __shared__ int s_nwin, s_next, s_gfirst, s_uniform, s_firstq, s_qbad, s_pop_prefix, s_resolved, s_err;
+  __shared__ int s_base, s_gfirst, s_uniform, s_firstq, s_qbad, s_pop_prefix, s_resolved, s_err, s_isg, s_ncommit;
+  __shared__ int s_commit[CTA];
   __shared__ int64_t s_stage_next;
   Ctl* c = D.ctl;
   const int n = (int)c->round_n;
   if (n == 0) return;
+  unsigned long long t_0 = __builtin_amdgcn_s_memtime(), t_a;
+  if (manage_lds && D.lds_workers) {
+    workers_lds(D, 0);
+    __syncthreads();
+  }
   const int32_t* L = c->round_L;
   const unsigned long long tag = (unsigned long long)c->round_counter << 32;
   const int P = D.P;
@@ -1419,6 +2044,7 @@ __global__ void __launch_bounds__(CTA) k_commit(Dev D) {
     s_firstq = INT32_MAX;
     s_qbad = 0;
     s_resolved = 0;
+    s_err = 0;
   }
   __syncthreads();
   for (int j = tid; j < n; j += blockDim.x) {
@@ -1426,6 +2052,7 @@ __global__ void __launch_bounds__(CTA) k_commit(Dev D) {
     double cur = D.pdur_cur[D.prefix[t]];
     if (!(cur >= 0 && D.res_stop[t] - D.res_start[t] == cur)) s_uniform = 0;
     if (D.ev_flags[j] & EV_MAYQUEUE) atomicMin(&s_firstq, j);
+    D.ev_npl[j] = -1;  // not committed yet
   }
   __syncthreads();
   const bool uniform = s_uniform != 0;
@@ -1447,11 +2074,7 @@ __global__ void __launch_bounds__(CTA) k_commit(Dev D) {
   const long long qlen0 = c->qlen;
   int64_t run_pop = 0, run_pub = 0, run_rub = 0;
   const int64_t rec0 = (int64_t)c->rec_used;
-  if (qlen0 > 0 && tid == 0) {
-    // the queued tasks local stimuli may take must all be dependency-free with one prefix
-    int q0 = D.qarr[c->qhead];
-    s_pop_prefix = D.prefix[q0];
-  }
+  if (qlen0 > 0 && tid == 0) s_pop_prefix = D.prefix[D.qarr[c->qhead]];
   __syncthreads();
   for (int j0 = 0; j0 < n; j0 += blockDim.x) {
     int j = j0 + tid;
@@ -1461,6 +2084,7 @@ __global__ void __launch_bounds__(CTA) k_commit(Dev D) {
     int64_t pexcl = block_excl_scan(popmax, &tot);
     uint8_t fl = in ? D.ev_flags[j] : 0;
     if (in && popmax > 0 && run_pop + pexcl + popmax > qlen0) fl |= EV_GLOBAL;
+    if (in && popmax > 56) fl |= EV_GLOBAL;  // records / placements of a local stimulus fit in one wave
     if (in && j > s_firstq) fl |= EV_GLOBAL;
     run_pop += tot;
     if (in) D.ev_flags[j] = fl;
@@ -1491,6 +2115,10 @@ __global__ void __launch_bounds__(CTA) k_commit(Dev D) {
   }
   if (rec0 + run_rub > D.rec_cap || run_pub > D.st_cap) {
     if (tid == 0) set_error(D, rec0 + run_rub > D.rec_cap ? ERR_REC_CAP : ERR_STAGE_CAP, -1);
+    if (manage_lds && D.lds_workers) {
+      __syncthreads();
+      workers_lds(D, 1);
+    }
     return;
   }
   for (int64_t i = tid; i < run_rub; i += blockDim.x) D.rec[rec0 + i].kind = REC_NONE;
@@ -1498,81 +2126,93 @@ __global__ void __launch_bounds__(CTA) k_commit(Dev D) {
   if (tid == 0) {
     c->rec_used = (unsigned long long)(rec0 + run_rub);
     s_stage_next = run_pub;
-    s_next = n < CTA ? n : CTA;
-    s_nwin = s_next;
+    s_base = 0;
   }
-  for (int i = tid; i < CTA; i += blockDim.x) win[i] = i < n ? i : -1;
   __threadfence_block();
   __syncthreads();
+  t_a = __builtin_amdgcn_s_memtime();
+  if (tid == 0) c->prof[0] += t_a - t_0;
 
-  // ---- deterministic-reservation commit
+  // ---- deterministic-reservation commit over the slice [base, base + CTA)
   while (true) {
+    unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+    const int base = s_base;
+    if (base >= n || s_err) break;
+    if (tid == 0) {
+      s_isg = (D.ev_flags[base] & EV_GLOBAL) ? 1 : 0;
+      s_gfirst = INT32_MAX;
+      s_ncommit = 0;
+    }
     __syncthreads();
-    int nwin = s_nwin;
-    if (nwin == 0) break;
-    int first = win[0];
-    if (D.ev_flags[first] & EV_GLOBAL) {
-      const double* dur = D.durv + (uniform ? 0 : (size_t)first * P);
+    if (s_isg) {
+      const double* dur = D.durv + (uniform ? 0 : (size_t)base * P);
       int64_t sn = s_stage_next;
       int resolved = s_resolved;
-      exec_global(D, L, first, tag | (unsigned long long)first, dur, S, &sn, &resolved);
+      exec_global(D, L, base, tag | (unsigned long long)base, dur, S, &sn, &resolved);
       if (tid == 0) {
         s_stage_next = sn;
         s_resolved = resolved;
         if (sn > D.st_cap) set_error(D, ERR_STAGE_CAP, -1);
-      }
-      // drop win[0]
-      int v = (tid + 1 < nwin) ? win[tid + 1] : -1;
-      __syncthreads();
-      if (tid < CTA) win[tid] = v;
-      __syncthreads();
-      if (tid == 0) {
-        s_nwin = nwin - 1;
-        if (s_next < n) win[s_nwin++] = s_next++;
+        int b = base + 1;
+        while (b < n && D.ev_npl[b] >= 0) b++;
+        s_base = b;
         s_err = c->error;
+        c->prof[2] += __builtin_amdgcn_s_memtime() - ts0;
       }
       __syncthreads();
-      if (s_err) break;
       continue;
     }
-    if (tid == 0) s_gfirst = INT32_MAX;
+    const int j = base + tid;
+    const bool pending = j < n && D.ev_npl[j] < 0;
+    if (pending && (D.ev_flags[j] & EV_GLOBAL)) atomicMin(&s_gfirst, j);
     __syncthreads();
-    int j = tid < nwin ? win[tid] : -1;
-    if (j >= 0 && (D.ev_flags[j] & EV_GLOBAL)) atomicMin(&s_gfirst, j);
-    __syncthreads();
-    const int gfirst = s_gfirst;
-    const bool active = j >= 0 && j < gfirst;
-    const int32_t* touch = active ? D.ev_touch + (size_t)j * TOUCH_MAX : nullptr;
+    const bool active = pending && j < s_gfirst;
+    const int32_t* touch = D.ev_touch + (size_t)(active ? j : 0) * TOUCH_MAX;
     const int nt = active ? D.ev_ntouch[j] : 0;
     for (int i = 0; i < nt; i++) atomicMin(&owner[touch[i]], j);
     __syncthreads();
     bool mine = active;
     for (int i = 0; i < nt && mine; i++) mine = owner[touch[i]] == j;
-    if (mine) {
-      const double* dur = D.durv + (uniform ? 0 : (size_t)j * P);
-      exec_local(D, j, L[j], D.ev_w[j], tag | (unsigned long long)j, dur, D.ev_plbase[j], D.ev_recbase[j],
-                 D.ev_popmax[j], qlen0 > 0 ? s_pop_prefix : 0);
+    unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+    if (mine) s_commit[atomicAdd(&s_ncommit, 1)] = j;
+    __syncthreads();
+    {
+      const int nc = s_ncommit;
+      for (int q = tid >> 6; q < nc; q += blockDim.x >> 6) {
+        const int jj = s_commit[q];
+        const double* dur = D.durv + (uniform ? 0 : (size_t)jj * P);
+        const unsigned long long kk = tag | (unsigned long long)jj;
+        unsigned long long tx = __builtin_amdgcn_s_memtime();
+        if (D.lds_workers)
+          exec_local_wave<true>(D, jj, L[jj], D.ev_w[jj], kk, dur, D.ev_plbase[jj], D.ev_recbase[jj],
+                                D.ev_popmax[jj], qlen0 > 0 ? s_pop_prefix : 0);
+        else
+          exec_local_wave<false>(D, jj, L[jj], D.ev_w[jj], kk, dur, D.ev_plbase[jj], D.ev_recbase[jj],
+                                 D.ev_popmax[jj], qlen0 > 0 ? s_pop_prefix : 0);
+        if ((tid & 63) == 0) {
+          unsigned long long dx = __builtin_amdgcn_s_memtime() - tx;
+          atomicMax(&c->prof[6], dx);
+          atomicAdd(&c->prof[7], dx);
+        }
+      }
     }
     __syncthreads();
+    if (tid == 0) c->prof[4] += ts1 - ts0;  // reservation part of the step
     for (int i = 0; i < nt; i++) owner[touch[i]] = INT32_MAX;
-    // compact the window (keep order), refill with the next stimuli
-    bool keep = j >= 0 && !mine;
-    int64_t tot;
-    int64_t pos = block_excl_scan(keep ? 1 : 0, &tot);
-    __syncthreads();
-    if (keep) win[pos] = j;
-    __syncthreads();
     if (tid == 0) {
-      int m = (int)tot;
-      while (m < CTA && s_next < n) win[m++] = s_next++;
-      s_nwin = m;
+      int b = base;
+      while (b < n && D.ev_npl[b] >= 0) b++;
+      s_base = b;
       c->dr_steps++;
       s_err = c->error;
+      unsigned long long dt = __builtin_amdgcn_s_memtime() - ts0;
+      c->prof[1] += dt;
+      if (dt > c->prof[5]) c->prof[5] = dt;
     }
     __syncthreads();
-    if (s_err) break;
   }
   __syncthreads();
+  unsigned long long t_f = __builtin_amdgcn_s_memtime();
   // ---- queued tasks taken by local stimuli, then the placement log in stimulus order
   resolve_pops_coop(D, L, s_resolved, n);
   int64_t run = 0;
@@ -1580,6 +2220,7 @@ __global__ void __launch_bounds__(CTA) k_commit(Dev D) {
   for (int j0 = 0; j0 < n; j0 += blockDim.x) {
     int j = j0 + tid;
     int64_t cnt = j < n ? D.ev_npl[j] : 0;
+    if (cnt < 0) cnt = 0;
     int64_t tot;
     int64_t off = block_excl_scan(cnt, &tot);
     if (cnt > 0) {
@@ -1597,29 +2238,85 @@ __global__ void __launch_bounds__(CTA) k_commit(Dev D) {
   }
   __syncthreads();
   if (tid == 0) c->n_placed = (unsigned long long)(dst0 + run);
+  if (manage_lds && D.lds_workers) {
+    __syncthreads();
+    workers_lds(D, 1);
+  }
+  if (tid == 0) c->prof[3] += __builtin_amdgcn_s_memtime() - t_f;
 }
+__global__ void __launch_bounds__(CTA) k_commit(const Dev* __restrict__ Dp) { commit_body(*Dp, true); }
 
 // fold the whole record log into idle / saturated (single lane)
-__global__ void k_walk(Dev D) {
+__global__ void k_walk(const Dev* __restrict__ Dp) {
+  const Dev& D = *Dp;
   if (threadIdx.x == 0 && blockIdx.x == 0) walk_to(D, D.ctl->rec_used);
 }
 
-__global__ void k_snapshot(Dev D, long long* prev_placed, int after_round) {
+__device__ void snapshot_body(const Dev& D, long long* prev_placed, int after_round, int64_t gtid, int64_t gthreads,
+                              bool leader) {
   if (after_round && D.ctl->round_n == 0) return;
   int64_t r = D.ctl->rounds_nonempty;
   if (r >= D.snap_cap) return;
-  for (int w = blockIdx.x * blockDim.x + threadIdx.x; w < D.W; w += gridDim.x * blockDim.x) {
+  for (int64_t w = gtid; w < D.W; w += gthreads) {
     size_t o = (size_t)r * D.W + w;
     D.snap_occ[o] = occupancy(D, w, D.pdur_cur);
-    D.snap_nbytes[o] = D.w_nbytes[w];
-    D.snap_nproc[o] = D.w_nproc[w];
-    D.snap_flags[o] = D.w_flags[w];
+    D.snap_nbytes[o] = WK_nbytes(D)[w];
+    D.snap_nproc[o] = WK_nproc(D)[w];
+    D.snap_flags[o] = WK_flags(D)[w];
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (leader) {
     D.snap_nplaced[r] = (int32_t)((long long)D.ctl->n_placed - *prev_placed);
     D.snap_nqueued[r] = (int32_t)D.ctl->qlen;
     *prev_placed = (long long)D.ctl->n_placed;
   }
+}
+__global__ void k_snapshot(const Dev* __restrict__ Dp, long long* prev_placed, int after_round) {
+  snapshot_body(*Dp, prev_placed, after_round, blockIdx.x * (int64_t)blockDim.x + threadIdx.x,
+                (int64_t)gridDim.x * blockDim.x, blockIdx.x == 0 && threadIdx.x == 0);
+}
+
+// the whole synthetic-executor replay in one workgroup: every phase of every round runs
+// on the commit's CU, so the round's data stays in its L1 / L2 and worker state stays in
+// LDS for the whole replay; no launches or host synchronisation between rounds
+__global__ void __launch_bounds__(CTA) k_replay(const Dev* __restrict__ Dp, long long* next_start, long long max_rounds,
+                                                long long* prev_placed, int snapshots) {
+  const Dev& D = *Dp;
+  __shared__ long long s_n;
+  __shared__ int s_stop;
+  if (D.lds_workers) workers_lds(D, 0);
+  __syncthreads();
+  for (long long r = 0; max_rounds < 0 || r < max_rounds; r++) {
+    if (threadIdx.x == 0) {
+      round_begin(D, next_start, nullptr, 0);
+      s_n = D.ctl->round_n;
+      s_stop = D.ctl->error != 0;
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (s_n == 0 || s_stop) break;
+    frontier_release_body(D, threadIdx.x, blockDim.x);
+    __threadfence_block();
+    __syncthreads();
+    candidate_body(D, threadIdx.x >> 6, blockDim.x >> 6);
+    __threadfence_block();
+    __syncthreads();
+    events_body(D, threadIdx.x, blockDim.x);
+    __threadfence_block();
+    __syncthreads();
+    commit_body(D, false);
+    __threadfence_block();
+    __syncthreads();
+    if (snapshots) {
+      if (threadIdx.x == 0) walk_to(D, D.ctl->rec_used);
+      __threadfence_block();
+      __syncthreads();
+      snapshot_body(D, prev_placed, 1, threadIdx.x, blockDim.x, threadIdx.x == 0);
+      __threadfence_block();
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  if (D.lds_workers) workers_lds(D, 1);
 }
 
 }  // namespace dgp

@@ -33,6 +33,7 @@ struct dgp_engine {
   dgp::Dev D{};
   dgp::Ctl* ctl = nullptr;
   long long* d_aux = nullptr;  // [0] next round start, [1] placements at the last snapshot
+  dgp::Dev* d_dev = nullptr;    // [0] Dev for every kernel, [1] Dev with lds_workers for k_commit
   std::vector<void*> allocs;
   std::vector<void*> graph_allocs;
   bool have_config = false, have_workers = false, have_graph = false, have_results = false;
@@ -96,10 +97,10 @@ int check_device_error(dgp_engine* e, dgp::Ctl* out = nullptr) {
     static const char* names[] = {"none", "worker prefix dict overflow (PMAX)", "task without candidates",
                                   "inconsistent task state", "queue underflow", "candidate pool overflow",
                                   "global prefix dict overflow", "record log overflow", "staging overflow",
-                                  "no worker"};
+                                  "no worker", "needs_what line overflow"};
     char buf[200];
     snprintf(buf, sizeof buf, "device engine error %d (%s) at task %d", c.error,
-             (c.error >= 0 && c.error <= 9) ? names[c.error] : "?", c.err_task);
+             (c.error >= 0 && c.error <= 10) ? names[c.error] : "?", c.err_task);
     return fail(e, DGP_E_DEVICE, buf);
   }
   return 0;
@@ -146,6 +147,15 @@ int timed_launch(dgp_engine* e, int kid, F&& launch) {
   return 0;
 }
 
+// publish the host-side Dev (pointers, sizes, config) to the device copies the kernels read
+int sync_dev(dgp_engine* e) {
+  dgp::Dev h[2] = {e->D, e->D};
+  h[0].lds_workers = 0;
+  h[1].lds_workers = e->D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
+  HIPCHK(e, hipMemcpy(e->d_dev, h, sizeof h, hipMemcpyHostToDevice));
+  return 0;
+}
+
 int grid_for(int64_t n, int per_block, int cap) {
   int64_t b = (n + per_block - 1) / per_block;
   if (b < 1) b = 1;
@@ -155,33 +165,38 @@ int grid_for(int64_t n, int per_block, int cap) {
 
 // enqueue one round (no host synchronisation); ext != nullptr: explicit completion batch
 int enqueue_round(dgp_engine* e, const int32_t* ext, int64_t ext_n) {
-  dgp::Dev D = e->D;
+  const dgp::Dev& D = e->D;
+  const dgp::Dev* DP = e->d_dev;
+  const dgp::Dev* DPC = e->d_dev + 1;
   hipStream_t s = e->stream;
   const int64_t N = D.N;
-  const int big = grid_for(N, 256, 2048);
-  const size_t lds = (size_t)D.W * sizeof(int);
-  hipLaunchKernelGGL(dgp::k_round_begin, dim3(1), dim3(1), 0, s, D, e->d_aux, ext, (long long)ext_n);
+  const int big = grid_for(N, 256, 128);
+  const int lds_workers = D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;  // matches sync_dev
+  const size_t lds = (((size_t)D.W * sizeof(int) + 15) & ~(size_t)15) +
+                     (lds_workers ? (((size_t)D.W + 3) & ~(size_t)3) * dgp::LDS_WORKER_BYTES + 64 : 0);
+  if (lds > 160 * 1024) return fail(e, DGP_E_ARG, "commit LDS exceeds 160 KiB");
+  hipLaunchKernelGGL(dgp::k_round_begin, dim3(1), dim3(1), 0, s, DP, e->d_aux, ext, (long long)ext_n);
   HIPCHK(e, hipGetLastError());
-  if (int rc = timed_launch(e, 0, [&] { hipLaunchKernelGGL(dgp::k_frontier_release, dim3(big), dim3(256), 0, s, D); }))
+  if (int rc = timed_launch(e, 0, [&] { hipLaunchKernelGGL(dgp::k_frontier_release, dim3(big), dim3(256), 0, s, DP); }))
     return rc;
   if (int rc = timed_launch(e, 1, [&] {
-        hipLaunchKernelGGL(dgp::k_candidate_commbytes, dim3(grid_for(N, 4, 2048)), dim3(256), 0, s, D);
+        hipLaunchKernelGGL(dgp::k_candidate_commbytes, dim3(grid_for(N, 4, 256)), dim3(256), 0, s, DP);
       }))
     return rc;
-  if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_events, dim3(big), dim3(256), 0, s, D); })) return rc;
-  if (int rc = timed_launch(e, 2, [&] { hipLaunchKernelGGL(dgp::k_commit, dim3(1), dim3(dgp::CTA), lds, s, D); }))
+  if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_events, dim3(big), dim3(256), 0, s, DP); })) return rc;
+  if (int rc = timed_launch(e, 2, [&] { hipLaunchKernelGGL(dgp::k_commit, dim3(1), dim3(dgp::CTA), lds, s, DPC); }))
     return rc;
   if (e->snap_rounds > 0) {
-    hipLaunchKernelGGL(dgp::k_walk, dim3(1), dim3(64), 0, s, D);
-    hipLaunchKernelGGL(dgp::k_snapshot, dim3(8), dim3(256), 0, s, D, e->d_aux + 1, 1);
+    hipLaunchKernelGGL(dgp::k_walk, dim3(1), dim3(64), 0, s, DP);
+    hipLaunchKernelGGL(dgp::k_snapshot, dim3(8), dim3(256), 0, s, DP, e->d_aux + 1, 1);
     HIPCHK(e, hipGetLastError());
   }
   return 0;
 }
 
 int walk(dgp_engine* e) {
-  dgp::Dev D = e->D;
-  return timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_walk, dim3(1), dim3(64), 0, e->stream, D); });
+  const dgp::Dev* DP = e->d_dev;
+  return timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_walk, dim3(1), dim3(64), 0, e->stream, DP); });
 }
 
 }  // namespace
@@ -201,7 +216,8 @@ dgp_engine* dgp_create(int device) {
     return nullptr;
   }
   if (hipMalloc((void**)&e->ctl, sizeof(dgp::Ctl)) != hipSuccess ||
-      hipMalloc((void**)&e->d_aux, 4 * sizeof(long long)) != hipSuccess) {
+      hipMalloc((void**)&e->d_aux, 4 * sizeof(long long)) != hipSuccess ||
+      hipMalloc((void**)&e->d_dev, 2 * sizeof(dgp::Dev)) != hipSuccess) {
     (void)hipStreamDestroy(e->stream);
     delete e;
     return nullptr;
@@ -223,6 +239,7 @@ void dgp_destroy(dgp_engine* e) {
   if (e->d_batch) (void)hipFree(e->d_batch);
   (void)hipFree(e->ctl);
   (void)hipFree(e->d_aux);
+  (void)hipFree(e->d_dev);
   for (hipEvent_t ev : e->evpool) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
   delete e;
@@ -278,6 +295,7 @@ int dgp_set_workers(dgp_engine* e, int32_t n_workers, const int32_t* nthreads) {
   rc |= dalloc(e, &D.w_flags, n_workers, e->allocs);
   rc |= dalloc(e, &D.w_itcslots, n_workers, e->allocs);
   rc |= dalloc(e, &D.w_lastcheck, n_workers, e->allocs);
+  rc |= dalloc(e, &D.w_needs, (size_t)n_workers * dgp::NEEDS_W, e->allocs);
   rc |= dalloc(e, &D.t_key, 2 * (size_t)D.Wp, e->allocs);
   rc |= dalloc(e, &D.t_idx, 2 * (size_t)D.Wp, e->allocs);
   if (rc) return DGP_E_HIP;
@@ -291,7 +309,7 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
                   const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override) {
   if (!e) return DGP_E_ARG;
   if (!e->have_workers) return fail(e, DGP_E_STATE, "dgp_set_workers must come first");
-  if (n_tasks <= 0 || n_tasks >= (1ll << 31)) return fail(e, DGP_E_ARG, "n_tasks out of range");
+  if (n_tasks <= 0 || n_tasks >= (1ll << 24) - 1) return fail(e, DGP_E_ARG, "n_tasks out of range (< 2^24 - 1)");
   if (n_prefixes <= 0 || n_groups <= 0) return fail(e, DGP_E_ARG, "need prefixes and groups");
   if (n_prefixes > 4096) return fail(e, DGP_E_ARG, "at most 4096 task prefixes");
   HIPCHK(e, hipSetDevice(e->device));
@@ -476,7 +494,8 @@ int dgp_reset(dgp_engine* e) {
   HIPCHK(e, hipMemcpyAsync(D.g_relwait, e->group_sizes.data(), D.G * 8, hipMemcpyHostToDevice, s));
   HIPCHK(e, hipMemsetAsync(D.g_left, 0, D.G * 8, s));
   HIPCHK(e, hipMemsetAsync(D.g_lastw, 0xff, D.G * 4, s));
-  hipLaunchKernelGGL(dgp::k_init_workers, dim3(grid_for(D.W, 256, 256)), dim3(256), 0, s, D);
+  if (int rc = sync_dev(e)) return rc;
+  hipLaunchKernelGGL(dgp::k_init_workers, dim3(grid_for(D.W, 256, 256)), dim3(256), 0, s, e->d_dev);
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipStreamSynchronize(s));
   e->graph_done = false;
@@ -492,16 +511,17 @@ int dgp_update_graph(dgp_engine* e) {
   if (!e || !e->have_graph || !e->have_config) return fail(e, DGP_E_STATE, "config, workers and graph first");
   if (e->graph_done) return fail(e, DGP_E_STATE, "update_graph already ran (dgp_reset first)");
   HIPCHK(e, hipSetDevice(e->device));
-  dgp::Dev D = e->D;
+  if (int rc = sync_dev(e)) return rc;
+  const dgp::Dev* DP = e->d_dev;
   hipStream_t s = e->stream;
   if (int rc = timed_launch(e, 3, [&] {
-        hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(D.N, 256, 2048)), dim3(256), 0, s, D);
+        hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(e->D.N, 256, 2048)), dim3(256), 0, s, DP);
       }))
     return rc;
-  if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, D); }))
+  if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP); }))
     return rc;
   if (e->snap_rounds > 0) {
-    hipLaunchKernelGGL(dgp::k_snapshot, dim3(8), dim3(256), 0, s, D, e->d_aux + 1, 0);
+    hipLaunchKernelGGL(dgp::k_snapshot, dim3(8), dim3(256), 0, s, DP, e->d_aux + 1, 0);
     HIPCHK(e, hipGetLastError());
   }
   e->graph_done = true;
@@ -512,19 +532,23 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (!e->have_results) return fail(e, DGP_E_STATE, "dgp_set_task_results first");
   HIPCHK(e, hipSetDevice(e->device));
+  if (int rc = sync_dev(e)) return rc;
   dgp::Ctl c;
   if (int rc = check_device_error(e, &c)) return rc;
   const long long r0 = c.rounds_nonempty;
-  int64_t enq = 0;
-  while (max_rounds < 0 || enq < max_rounds) {
-    int batch = e->rounds_per_sync;
-    if (max_rounds >= 0) batch = (int)std::min<int64_t>(batch, max_rounds - enq);
-    for (int b = 0; b < batch; b++)
-      if (int rc = enqueue_round(e, nullptr, 0)) return rc;
-    enq += batch;
-    if (int rc = check_device_error(e, &c)) return rc;
-    if (c.round_n == 0) break;  // the last round found nothing to complete
-  }
+  // every round in one persistent workgroup (k_replay); worker state in LDS when it fits
+  const dgp::Dev& D = e->D;
+  const int lds_workers = D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
+  const size_t lds = (((size_t)D.W * sizeof(int) + 15) & ~(size_t)15) +
+                     (lds_workers ? (((size_t)D.W + 3) & ~(size_t)3) * dgp::LDS_WORKER_BYTES + 64 : 0);
+  if (lds > 160 * 1024) return fail(e, DGP_E_ARG, "commit LDS exceeds 160 KiB");
+  const dgp::Dev* DPC = e->d_dev + 1;
+  const int snaps = e->snap_rounds > 0 ? 1 : 0;
+  if (int rc = timed_launch(e, 2, [&] {
+        hipLaunchKernelGGL(dgp::k_replay, dim3(1), dim3(dgp::CTA), lds, e->stream, DPC, e->d_aux, (long long)max_rounds,
+                           e->d_aux + 1, snaps);
+      }))
+    return rc;
   if (int rc = walk(e)) return rc;
   if (int rc = check_device_error(e, &c)) return rc;
   if (n_rounds_out) *n_rounds_out = c.rounds_nonempty - r0;
@@ -554,6 +578,7 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* tasks, const int
     HIPCHK(e, hipMemcpyAsync(e->D.res_stop + t, stop + i, 8, hipMemcpyHostToDevice, e->stream));
   }
   HIPCHK(e, hipMemcpyAsync(e->d_batch, tasks, n * 4, hipMemcpyHostToDevice, e->stream));
+  if (int rc = sync_dev(e)) return rc;
   if (int rc = enqueue_round(e, e->d_batch, n)) return rc;
   if (int rc = walk(e)) return rc;
   return check_device_error(e);
@@ -657,9 +682,11 @@ int dgp_stats(dgp_engine* e, int64_t* out, int32_t n) {
   if (!e || !out) return DGP_E_ARG;
   dgp::Ctl c;
   if (int rc = read_ctl(e, &c)) return rc;
-  int64_t v[6] = {(int64_t)c.n_placed, c.rounds_nonempty, c.dr_steps, c.n_global_events, (int64_t)c.rec_used,
-                  (int64_t)c.walk_pos};
-  for (int i = 0; i < n && i < 6; i++) out[i] = v[i];
+  int64_t v[30] = {(int64_t)c.n_placed, c.rounds_nonempty, c.dr_steps, c.n_global_events, (int64_t)c.rec_used,
+                   (int64_t)c.walk_pos};
+  for (int i = 0; i < 8; i++) v[6 + i] = (int64_t)c.prof[i];
+  for (int i = 0; i < 16; i++) v[14 + i] = (int64_t)c.prof2[i];
+  for (int i = 0; i < n && i < 30; i++) out[i] = v[i];
   return 0;
 }
 

@@ -118,7 +118,8 @@ int dgp_set_timing(dgp_engine* e, int enabled);
 
 /* Engine counters: out[0] placements, [1] non-empty rounds, [2] deterministic-reservation
  * steps of the ordered commit, [3] stimuli that ran as global (in order, alone),
- * [4] record-log length, [5] record-log walker position. */
+ * [4] record-log length, [5] record-log walker position, [6..13] commit-kernel phase
+ * cycles (s_memtime): setup, local steps, global stimuli, finish, walker, longest step. */
 int dgp_stats(dgp_engine* e, int64_t* out, int32_t n);
 
 #ifdef __cplusplus
