@@ -95,6 +95,11 @@ struct Rec {
   int32_t pad;
 };
 
+namespace st {
+struct SRec;
+struct Pos;
+}  // namespace st
+
 struct Dev {
   int32_t N, W, WB, P, G, Wp;
   int64_t bandwidth, default_data_size;
@@ -199,6 +204,39 @@ struct Dev {
   int32_t* snap_nqueued;
   int32_t lds_workers;  // commit kernel: worker state lives in dynamic LDS
   Ctl* ctl;
+  // ---- stream engine (dgp_stream.h)
+  int32_t* gw_nproc;  // worker state in the stream layout when it does not fit in LDS
+  uint16_t* gw_nthreads;
+  uint16_t* gw_cap;
+  uint32_t* gw_plen;
+  uint16_t* gw_pfx;
+  uint16_t* gw_pcnt;
+  int64_t* gw_netocc;
+  int64_t* gw_nbytes;
+  uint32_t* gw_mask;
+  uint32_t* gw_needs;
+  uint8_t* gw_wflags;
+  uint32_t* gw_needs_ext;    // needs_what overflow entries [W][NXW]
+  uint32_t* gw_needs_saved;  // needs_what lines between launches [W][NLW]
+  int32_t* run_id;           // placement-log position of each placed task
+  int32_t* holder_of;        // the worker a task runs / ran on (its single replica)
+  int32_t* fr_mark;          // stimulus whose completion empties the task's waiting_on
+  int32_t* rel_mark;         // stimulus whose completion empties the task's waiters
+  uint4* desc;               // descriptor ring [DR][NE]
+  long long* desc_tag;
+  int32_t* s2_task;  // per-slot staging of placements [WIN][PLC]
+  int32_t* s2_worker;
+  int64_t* s2_comm;
+  double* s2_start;
+  int64_t* s2_wsnb;
+  int8_t* s2_route;
+  st::SRec* srec;  // per-slot staging of records [WIN][PLC]
+  st::SRec* rlog;  // the record log
+  int64_t rlog_cap;
+  st::Pos* pos;
+  int32_t dbg_task;    // stream debug: dump the candidate keys of this frontier task
+  double* dbgbuf;      // [64][8]
+  int32_t dbg;  // stream debug: 1 every stimulus waits for all earlier ones, 2 every stimulus global
 };
 
 // dynamic LDS of the commit kernel: owner[W] reservation table, then (lds_workers) the

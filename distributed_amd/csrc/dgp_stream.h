@@ -1,0 +1,1889 @@
+// dgplace stream engine: the completion replay as one dataflow pipeline in a single
+// persistent workgroup (gfx950, 16 waves). Included by dgplace.hip after dgp_device.h.
+//
+// The synthetic executor completes placements in run_id order, so the replay after
+// update_graph is ONE ordered stream of completion stimuli r = 0, 1, 2, ... (stimulus r
+// completes placement r; it is processed after the stimulus that created placement r).
+// Sequential semantics only order stimuli that share a worker: a completion on w, its
+// releases (the replicas' holders) and its frontier placements (the candidates of the
+// released tasks) read and write only those workers' state, and while the queue is
+// non-empty every worker but w is full, so the queue refill touches only w
+// (stimulus_queue_slots_maybe_opened :4983 -> decide_worker_rootish_queuing_enabled
+// :2195). Everything else is global and handled in order.
+//
+// Waves (roles):
+//   SEQ  sequencer: in stimulus order, turns each finished stimulus' staged placements
+//        into placement-log entries (run_id order), resolves the queued tasks its pops
+//        took (HeapSet order), appends its records to the record log, frees its slot,
+//        counts rounds and takes the per-round snapshots.
+//   BLD  builder: per completion, in order, the waiting_on / waiters decrements
+//        (_add_to_memory :3298-3314): marks each task with the stimulus that releases
+//        it to the frontier (fr_mark) or to "released" (rel_mark).
+//   PRE  prefetcher: per stimulus, a 1 KiB descriptor in a global ring: the completing
+//        task, its dependencies, the releases and every frontier task with its
+//        dependencies' holders and sizes (the candidate set of decide_worker :8571).
+//   REG  registrar: in order, copies descriptors into the LDS window (32 slots), folds
+//        the prefix EWMA (TaskPrefix.add_duration :977), and registers the stimulus on
+//        the workers it touches: mask[w] bit per in-flight slot; the stimulus waits for
+//        every earlier in-flight stimulus that shares a worker.
+//   WLK  walker: folds the record log in order into SchedulerState's global quantities
+//        (_task_prefix_count_global, _network_occ_global -> total_occupancy :1877) and
+//        the idle / saturated sets of check_idle_saturated (:2949).
+//   EXE  executors (the other waves): pick any ready stimulus and run it on the worker
+//        state in LDS; stimuli that read global state run alone, in order.
+#pragma once
+
+namespace dgp {
+namespace st {
+
+constexpr int WIN = 32;          // in-flight stimulus slots (LDS window)
+constexpr int NE = 48;           // 16-byte descriptor entries per stimulus
+constexpr int DR = 4096;         // descriptor ring (global) — how far PRE may run ahead
+constexpr int PLC = 64;          // staged placements / records per stimulus
+constexpr int KT_MAX = 24;       // dependencies of the completing task in local mode
+constexpr int KX_MAX = 8;        // dependencies of a frontier task in local mode
+constexpr int PD = 8;            // prefixes whose durations ride in the descriptor
+constexpr int PMW = 8;           // prefix dict entries per worker
+constexpr int NLW = 12;          // needs_what words per worker in LDS: 11 entries + control
+constexpr int NXW = 52;          // overflow entries per worker (global) before scan mode
+constexpr int PG = 64;           // walker's global prefix dict
+constexpr int BIG = 1 << 24;     // registration guard of a slot's predecessor count
+constexpr uint32_t NL_OVF = 0xffffffffu;
+constexpr int N_ROLE = 5;        // waves 0..4 are SEQ, BLD, PRE, REG, WLK; the rest execute
+constexpr int E_HDR = 7;         // header entries: 0 ids, 1 sizes/counts, 2 duration, 3..6 durations
+
+enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8 };
+enum : int { K_COMPLETE = 1, K_PLACE = 2 };
+enum : int { SERR_NONE = 0, SERR_PREFIX = 11, SERR_WATCHDOG = 12, SERR_QUEUE = 13, SERR_NEEDS = 14,
+             SERR_REC = 15, SERR_CAND = 16, SERR_STAGE = 17 };
+
+// persistent stream position (global, survives launches)
+struct Pos {
+  long long seq, bld, pre, reg;  // stimuli sequenced / built / prefetched / registered
+  long long rec_len, walk;       // record log length / records folded
+  long long runid_upto;          // placement-log entries whose run_id / holder are set
+  long long round_end;           // end of the current round (stimulus index), -1 before the first launch
+  long long round_start_saved;   // start of the current round
+  long long prev_placed;         // log length at the last snapshot
+};
+
+// one record of the record log (one check_idle_saturated sub-step)
+struct SRec {
+  int32_t w;
+  int16_t p;
+  int8_t kind;
+  int8_t pad;
+  int32_t nproc;
+  int32_t task;
+  int64_t dnet;
+  double occ;
+  double dur;  // completion: the observed duration (stop - start) for the prefix EWMA
+};
+
+// LDS control block
+struct SCtl {
+  int stop, error, err_task;
+  int inv_ok;          // queue non-empty => every worker full (only globals change it)
+  int q_anon;          // queued tasks share one prefix and have no dependencies
+  int q_prefix;
+  int capmax;          // max slot cap over workers
+  int global_pending;  // a registered global stimulus has not finished
+  int busy_exe;        // executors between claim and retirement
+  unsigned ready;      // slots whose stimulus may run
+  long long seq_pos, log_len, rec_len, walk_pos, bld_pos, pre_pos, reg_pos, reg_limit;
+  long long qhead, qlen, n_tasks;
+  long long round_end, rounds_left, prev_placed;
+  long long rounds_nonempty, snap_idx;
+  int snaps;
+  // walker state (SchedulerState globals as of walk_pos)
+  int g_plen;
+  int g_pfx[PG];
+  long long g_pcnt[PG];
+  double g_netocc;
+  double wdur[PD];  // prefix EWMA as of walk_pos (raw duration_average)
+  long long n_idle, n_sat;
+  unsigned long long prof[16];
+};
+
+// ------------------------------------------------------------------ small helpers
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ unsigned rlu(unsigned v, int l) { return (unsigned)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ int64_t mk64(unsigned lo, unsigned hi) { return (int64_t)(((uint64_t)hi << 32) | lo); }
+__device__ __forceinline__ double mkd(unsigned lo, unsigned hi) {
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ unsigned lo32(int64_t v) { return (unsigned)(uint64_t)v; }
+__device__ __forceinline__ unsigned hi32(int64_t v) { return (unsigned)((uint64_t)v >> 32); }
+__device__ __forceinline__ unsigned dlo(double v) { return lo32(__double_as_longlong(v)); }
+__device__ __forceinline__ unsigned dhi(double v) { return hi32(__double_as_longlong(v)); }
+__device__ __forceinline__ int64_t shfl64(int64_t v, int l) { return __shfl(v, l); }
+__device__ __forceinline__ int64_t wsum64(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ int wsum(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ int wmax(int v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ unsigned long long ballot(bool b) { return __ballot(b); }
+__device__ __forceinline__ unsigned long long mclk() { return __builtin_amdgcn_s_memtime(); }
+__device__ __forceinline__ void wbar() { __builtin_amdgcn_wave_barrier(); }
+__device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+template <class T>
+__device__ __forceinline__ T vload(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <class T>
+__device__ __forceinline__ void vstore(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// ------------------------------------------------------------ worker state access
+// LW: state in LDS (dynamic carve), else in the global gw_* arrays (same layout)
+struct WPtr {
+  int32_t* nproc;
+  uint16_t* nthreads;
+  uint16_t* cap;
+  uint32_t* plen;      // low byte: dict length
+  uint16_t* pfx;       // [W][PMW]
+  uint16_t* pcnt;      // [W][PMW]
+  int64_t* netocc;
+  int64_t* nbytes;
+  uint32_t* mask;      // in-flight slots touching the worker
+  uint32_t* needs;     // [W][NLW]: (d << 8 | count), slot NLW-1 = control (1: overflow
+                       // entries in use, NL_OVF: scan mode)
+  uint8_t* wflags;     // walker's idle / saturated bits
+};
+
+extern __shared__ __attribute__((aligned(16))) char st_smem[];
+
+__device__ __forceinline__ size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
+__host__ __device__ constexpr size_t lds_worker_bytes(int W) {
+  return ((size_t)W * 4 + 15) / 16 * 16 * 2 /* nproc plen */ + ((size_t)W * 2 + 15) / 16 * 16 * 2 +
+         ((size_t)W * PMW * 2 + 15) / 16 * 16 * 2 + ((size_t)W * 8 + 15) / 16 * 16 * 2 +
+         ((size_t)W * 4 + 15) / 16 * 16 + ((size_t)W * NLW * 4 + 15) / 16 * 16 + ((size_t)W + 15) / 16 * 16;
+}
+
+template <bool LW>
+__device__ __forceinline__ WPtr wptr(const Dev& D) {
+  WPtr p;
+  if (LW) {
+    const size_t W = D.W;
+    char* b = st_smem;
+    p.nproc = (int32_t*)b;      b += al16(W * 4);
+    p.nthreads = (uint16_t*)b;  b += al16(W * 2);
+    p.cap = (uint16_t*)b;       b += al16(W * 2);
+    p.plen = (uint32_t*)b;      b += al16(W * 4);
+    p.pfx = (uint16_t*)b;       b += al16(W * PMW * 2);
+    p.pcnt = (uint16_t*)b;      b += al16(W * PMW * 2);
+    p.netocc = (int64_t*)b;     b += al16(W * 8);
+    p.nbytes = (int64_t*)b;     b += al16(W * 8);
+    p.mask = (uint32_t*)b;      b += al16(W * 4);
+    p.needs = (uint32_t*)b;     b += al16(W * NLW * 4);
+    p.wflags = (uint8_t*)b;
+  } else {
+    p.nproc = D.gw_nproc;
+    p.nthreads = D.gw_nthreads;
+    p.cap = D.gw_cap;
+    p.plen = D.gw_plen;
+    p.pfx = D.gw_pfx;
+    p.pcnt = D.gw_pcnt;
+    p.netocc = D.gw_netocc;
+    p.nbytes = D.gw_nbytes;
+    p.mask = D.gw_mask;
+    p.needs = D.gw_needs;
+    p.wflags = D.gw_wflags;
+  }
+  return p;
+}
+
+// LDS of the stream kernel besides the worker carve
+struct SLds {
+  uint4 desc[WIN][NE];        // descriptors of the in-flight window
+  uint16_t touch[WIN][NE];    // distinct workers each in-flight stimulus touches
+  int32_t ntouch[WIN];
+  uint32_t flags[WIN];
+  int32_t pred[WIN];
+  int32_t npl[WIN], npops[WIN], nrec[WIN];
+  long long done_tag[WIN];
+  long long sid[WIN];         // stimulus registered in each slot
+  SCtl c;
+};
+
+// prefix durations of a descriptor (entries 3..6, two doubles each) -> lane p holds dur_p
+__device__ __forceinline__ double desc_durs(const uint4& e) {
+  const int lane = lane_id();
+  const int src = 3 + ((lane & (PD - 1)) >> 1);
+  const unsigned x = __shfl(e.x, src), y = __shfl(e.y, src), z = __shfl(e.z, src), w = __shfl(e.w, src);
+  return (lane & 1) ? mkd(z, w) : mkd(x, y);
+}
+
+// _calc_occupancy (:1884-1903) of worker c (per lane); durv = lane p holds the resolved
+// duration of prefix p; all lanes must be active (shuffles)
+template <bool LW>
+__device__ __forceinline__ double occ_of(const WPtr& P, const Dev& D, int c, double durv) {
+  const uint32_t n = P.plen[c] & 0xffu;
+  const uint4 pf = *reinterpret_cast<const uint4*>(P.pfx + (size_t)c * PMW);
+  const uint4 pc = *reinterpret_cast<const uint4*>(P.pcnt + (size_t)c * PMW);
+  const uint32_t pfw[4] = {pf.x, pf.y, pf.z, pf.w};
+  const uint32_t pcw[4] = {pc.x, pc.y, pc.z, pc.w};
+  const int nmax = wmax((int)n);
+  double res = 0.0;
+#pragma unroll
+  for (int i = 0; i < PMW; i++) {
+    if (i >= nmax) break;
+    const uint32_t pfi = (pfw[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
+    const uint32_t pci = (pcw[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
+    const double dv = __shfl(durv, (int)(pfi & (PD - 1)));
+    if ((uint32_t)i < n) res += dv * (double)pci;
+  }
+  return res + (double)P.netocc[c] / (double)D.bandwidth;
+}
+
+// insertion-ordered {prefix: count} with delete-on-zero (:733-784), packed 8 x u16
+__device__ __forceinline__ bool dict_add(uint4& pf, uint4& pc, uint32_t& n, int p, int delta) {
+  uint32_t pfw[4] = {pf.x, pf.y, pf.z, pf.w};
+  uint32_t pcw[4] = {pc.x, pc.y, pc.z, pc.w};
+  auto get = [&](const uint32_t* a, int i) { return (a[i >> 1] >> ((i & 1) * 16)) & 0xffffu; };
+  auto put = [&](uint32_t* a, int i, uint32_t v) {
+    const int sh = (i & 1) * 16;
+    a[i >> 1] = (a[i >> 1] & ~(0xffffu << sh)) | ((v & 0xffffu) << sh);
+  };
+  int at = -1;
+#pragma unroll
+  for (int i = 0; i < PMW; i++)
+    if (at < 0 && (uint32_t)i < n && get(pfw, i) == (uint32_t)p) at = i;
+  bool ok = true;
+  if (delta > 0) {
+    if (at >= 0) {
+      uint32_t v = get(pcw, at);
+      if (v == 0xffffu) ok = false;
+      else put(pcw, at, v + 1);
+    } else if (n < (uint32_t)PMW) {
+      put(pfw, (int)n, (uint32_t)p);
+      put(pcw, (int)n, 1);
+      n++;
+    } else {
+      ok = false;
+    }
+  } else if (at >= 0) {
+    uint32_t v = get(pcw, at) - 1;
+    if (v == 0) {
+#pragma unroll
+      for (int i = 0; i < PMW - 1; i++)
+        if (i >= at && (uint32_t)(i + 1) < n) {
+          put(pfw, i, get(pfw, i + 1));
+          put(pcw, i, get(pcw, i + 1));
+        }
+      put(pfw, (int)n - 1, 0);
+      put(pcw, (int)n - 1, 0);
+      n--;
+    } else {
+      put(pcw, at, v);
+    }
+  }
+  pf = make_uint4(pfw[0], pfw[1], pfw[2], pfw[3]);
+  pc = make_uint4(pcw[0], pcw[1], pcw[2], pcw[3]);
+  return ok;
+}
+
+// occupancy from a dict held in registers (uniform across lanes)
+__device__ __forceinline__ double occ_regs(const uint4& pf, const uint4& pc, uint32_t n, int64_t netocc,
+                                           double durv, int64_t bw) {
+  const uint32_t pfw[4] = {pf.x, pf.y, pf.z, pf.w};
+  const uint32_t pcw[4] = {pc.x, pc.y, pc.z, pc.w};
+  double res = 0.0;
+#pragma unroll
+  for (int i = 0; i < PMW; i++) {
+    if ((uint32_t)i >= n) break;
+    const uint32_t pfi = (pfw[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
+    const uint32_t pci = (pcw[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
+    res += __shfl(durv, (int)(pfi & (PD - 1))) * (double)pci;
+  }
+  return res + (double)netocc / (double)bw;
+}
+
+__device__ __forceinline__ double resolve_dur(const Dev& D, double d) {  // _calc_occupancy :1892-1899
+  return d < 0 ? D.unknown_duration : d;  // max_exec_time stays -1 without heartbeats
+}
+
+__device__ void serr(SCtl& S, int code, int task) {
+  if (atomicCAS(&S.error, 0, code) == 0) S.err_task = task;
+  vstore(&S.stop, 1);
+}
+
+
+constexpr unsigned long long WATCHDOG = 40000000000ull;  // s_memtime ticks without progress (~16 s)
+
+__device__ __forceinline__ int64_t nbv(const Dev& D, int64_t v) { return v >= 0 ? v : D.default_data_size; }
+
+// ============================================================ walker (records -> flags)
+// SchedulerState globals folded in record order, held in registers (uniform over lanes;
+// lane p holds the raw duration_average of prefix p).
+struct WState {
+  int n;             // _task_prefix_count_global, insertion ordered
+  int pf[PD];
+  long long cnt[PD];
+  double netocc;     // _network_occ_global (holds integers < 2^53: exact in any order)
+  double wd;         // lane p: TaskPrefix.duration_average
+  long long n_idle, n_sat;
+};
+
+__device__ __forceinline__ void ws_load(const SCtl& S, WState& g) {
+  const int lane = lane_id();
+  g.n = S.g_plen;
+#pragma unroll
+  for (int i = 0; i < PD; i++) {
+    g.pf[i] = S.g_pfx[i];
+    g.cnt[i] = S.g_pcnt[i];
+  }
+  g.netocc = S.g_netocc;
+  g.wd = S.wdur[lane & (PD - 1)];
+  g.n_idle = S.n_idle;
+  g.n_sat = S.n_sat;
+}
+__device__ __forceinline__ void ws_store(SCtl& S, const WState& g) {
+  const int lane = lane_id();
+  if (lane == 0) {
+    S.g_plen = g.n;
+#pragma unroll
+    for (int i = 0; i < PD; i++) {
+      S.g_pfx[i] = g.pf[i];
+      S.g_pcnt[i] = g.cnt[i];
+    }
+    S.g_netocc = g.netocc;
+    S.n_idle = g.n_idle;
+    S.n_sat = g.n_sat;
+  }
+  if (lane < PD) S.wdur[lane] = g.wd;
+}
+__device__ __forceinline__ bool gdict_add(WState& g, int p, int delta) {
+  int at = -1;
+#pragma unroll
+  for (int i = 0; i < PD; i++)
+    if (at < 0 && i < g.n && g.pf[i] == p) at = i;
+  if (delta > 0) {
+    if (at >= 0) {
+#pragma unroll
+      for (int i = 0; i < PD; i++)
+        if (i == at) g.cnt[i]++;
+      return true;
+    }
+    if (g.n >= PD) return false;
+#pragma unroll
+    for (int i = 0; i < PD; i++)
+      if (i == g.n) {
+        g.pf[i] = p;
+        g.cnt[i] = 1;
+      }
+    g.n++;
+    return true;
+  }
+  if (at < 0) return true;
+  long long v = 0;
+#pragma unroll
+  for (int i = 0; i < PD; i++)
+    if (i == at) v = --g.cnt[i];
+  if (v == 0) {
+#pragma unroll
+    for (int i = 0; i < PD - 1; i++)
+      if (i >= at && i + 1 < g.n) {
+        g.pf[i] = g.pf[i + 1];
+        g.cnt[i] = g.cnt[i + 1];
+      }
+    g.n--;
+  }
+  return true;
+}
+// SchedulerState.total_occupancy :1877 (prefix dict order)
+__device__ __forceinline__ double ws_total_occ(const Dev& D, const WState& g) {
+  const double rv = resolve_dur(D, g.wd);
+  double res = 0.0;
+#pragma unroll
+  for (int i = 0; i < PD; i++) {
+    const double dv = __shfl(rv, g.pf[i] & (PD - 1));
+    if (i < g.n) res += dv * (double)g.cnt[i];
+  }
+  return res + g.netocc / (double)D.bandwidth;
+}
+
+// one record: the global-count update of its sub-step, then check_idle_saturated's idle /
+// saturated part for its worker (:2949-2991, is_unoccupied :2997). All lanes, uniform.
+template <bool LW>
+__device__ __forceinline__ void ws_fold(const Dev& D, const WPtr& P, SCtl& S, WState& g, int kind, int w, int p,
+                                        long long dnet, double occ, int nproc, double dobs) {
+  const int lane = lane_id();
+  if (kind == K_COMPLETE) {
+    if (lane == p) g.wd = g.wd < 0 ? dobs : 0.5 * dobs + 0.5 * g.wd;
+    gdict_add(g, p, -1);
+  } else if (!gdict_add(g, p, +1)) {
+    serr(S, SERR_PREFIX, -1);
+  }
+  g.netocc += (double)dnet;
+  const long long nt = P.nthreads[w];
+  const long long pp = nproc;
+  bool idle, sat = false;
+  double avg = -1.0;
+  if (pp < nt) {
+    idle = true;
+  } else {
+    avg = ws_total_occ(D, g) / (double)D.total_nthreads;
+    idle = occ < (double)nt * avg / 2;
+  }
+  if (!idle && pp > nt) {
+    const double pending = occ * (double)(pp - nt) / (double)(pp * nt);
+    if (0.4 < pending) {
+      if (avg < 0) avg = ws_total_occ(D, g) / (double)D.total_nthreads;
+      sat = pending > 1.9 * avg;
+    }
+  }
+  const uint8_t fo = P.wflags[w];
+  const uint8_t fn = (idle ? WF_IDLE : 0) | (sat ? WF_SAT : 0);
+  if (fo != fn) {
+    g.n_idle += (idle ? 1 : 0) - ((fo & WF_IDLE) ? 1 : 0);
+    g.n_sat += (sat ? 1 : 0) - ((fo & WF_SAT) ? 1 : 0);
+    if (lane == 0) P.wflags[w] = fn;
+  }
+}
+
+template <bool LW>
+__device__ void role_wlk(const Dev& D, SLds& L, const WPtr& P) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  WState g;
+  while (true) {
+    const long long wp = S.walk_pos;  // WLK (and a running global stimulus) write it
+    const long long rl_ = vload(&S.rec_len);
+    if (wp >= rl_) {
+      if (vload(&S.stop)) break;
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    lds_fence();
+    const int m = (int)min(rl_ - wp, (long long)64);
+    SRec rc{};
+    if (lane < m) rc = D.rlog[wp + lane];
+    ws_load(S, g);
+    const unsigned long long t0 = mclk();
+    for (int i = 0; i < m; i++) {
+      const int kind = rl(rc.kind, i);
+      const int w = rl(rc.w, i);
+      const int p = rl(rc.p, i);
+      const long long dnet = mk64(rlu(lo32(rc.dnet), i), rlu(hi32(rc.dnet), i));
+      const double occ = mkd(rlu(dlo(rc.occ), i), rlu(dhi(rc.occ), i));
+      const int np = rl(rc.nproc, i);
+      const double dob = mkd(rlu(dlo(rc.dur), i), rlu(dhi(rc.dur), i));
+      ws_fold<LW>(D, P, S, g, kind, w, p, dnet, occ, np, dob);
+    }
+    ws_store(S, g);
+    lds_fence();
+    if (lane == 0) {
+      S.prof[4] += mclk() - t0;
+      vstore(&S.walk_pos, wp + m);
+    }
+  }
+}
+
+// ====================================================================== sequencer
+template <bool LW>
+__device__ void snapshot(const Dev& D, SLds& L, const WPtr& P) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  const long long idx = S.rounds_nonempty;
+  if (idx >= D.snap_cap) return;
+  const double durv = resolve_dur(D, S.wdur[lane & (PD - 1)]);
+  for (int c0 = 0; c0 < D.W; c0 += 64) {
+    const int c = min(c0 + lane, D.W - 1);
+    const double o = occ_of<LW>(P, D, c, durv);
+    if (c0 + lane < D.W) {
+      const size_t k = (size_t)idx * D.W + c;
+      D.snap_occ[k] = o;
+      D.snap_nbytes[k] = P.nbytes[c];
+      D.snap_nproc[k] = P.nproc[c];
+      const bool itc = D.sat_inf || (int)P.cap[c] - P.nproc[c] > 0;
+      D.snap_flags[k] = P.wflags[c] | (itc ? WF_ITC : 0);
+    }
+  }
+  if (lane == 0) {
+    D.snap_nplaced[idx] = (int32_t)(S.log_len - S.prev_placed);
+    D.snap_nqueued[idx] = (int32_t)S.qlen;
+    S.prev_placed = S.log_len;
+  }
+}
+
+// every stimulus of the round is sequenced: count it, snapshot, open the next round.
+// Returns true when the replay stops here.
+template <bool LW>
+__device__ bool round_end_step(const Dev& D, SLds& L, const WPtr& P, long long& round_start) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  if (S.round_end > round_start) {
+    if (lane == 0) S.rounds_nonempty++;
+    wbar();
+    if (S.snaps) {
+      const unsigned long long t0 = mclk();
+      while (vload(&S.walk_pos) != vload(&S.rec_len) || vload(&S.busy_exe) != 0) {
+        if (vload(&S.stop)) return true;
+        if (mclk() - t0 > WATCHDOG) {
+          serr(S, SERR_WATCHDOG, -2);
+          return true;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      lds_fence();
+      snapshot<LW>(D, L, P);
+      __threadfence_block();
+    }
+    if (S.rounds_left > 0) {
+      if (lane == 0) S.rounds_left--;
+      wbar();
+      if (S.rounds_left == 0) {
+        round_start = S.round_end;
+        if (lane == 0) vstore(&S.stop, 1);
+        return true;
+      }
+    }
+  }
+  round_start = S.round_end;
+  if (lane == 0) S.round_end = S.log_len;
+  wbar();
+  if (S.round_end == round_start) {  // the round just opened is empty: replay finished
+    if (lane == 0) vstore(&S.stop, 1);
+    return true;
+  }
+  if (lane == 0 && (S.snaps || S.rounds_left > 0)) vstore(&S.reg_limit, S.round_end);
+  lds_fence();
+  return false;
+}
+
+template <bool LW>
+__device__ void role_seq(const Dev& D, SLds& L, const WPtr& P, long long& round_start) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  unsigned long long t_idle = mclk();
+  while (true) {
+    if (vload(&S.stop)) break;
+    const long long sp = S.seq_pos;
+    const long long re = S.round_end;
+    const long long r = sp + lane;
+    const bool dn = lane < WIN && r < re && vload(&L.done_tag[r & (WIN - 1)]) == r + 1;
+    const unsigned long long b = ballot(dn);
+    const int m = (int)__builtin_ctzll(~b);
+    if (m == 0) {
+      if (sp == re) {
+        if (round_end_step<LW>(D, L, P, round_start)) break;
+        t_idle = mclk();
+        continue;
+      }
+      if (mclk() - t_idle > WATCHDOG) {
+        serr(S, SERR_WATCHDOG, (int)sp);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    lds_fence();
+    const unsigned long long t0 = mclk();
+    const int s = (int)(r & (WIN - 1));
+    int npl = 0, nrec = 0, npop = 0;
+    bool direct = false;
+    if (lane < m) {
+      npl = L.npl[s];
+      nrec = L.nrec[s];
+      npop = L.npops[s];
+      direct = (L.flags[s] & F_GLOBAL) != 0;
+    }
+    int ipl = npl, irc = nrec, ipo = npop;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int a = __shfl_up(ipl, o), b2 = __shfl_up(irc, o), c2 = __shfl_up(ipo, o);
+      if (lane >= o) {
+        ipl += a;
+        irc += b2;
+        ipo += c2;
+      }
+    }
+    const int tpl = __shfl(ipl, 63), trc = __shfl(irc, 63), tpo = __shfl(ipo, 63);
+    const long long lb = S.log_len + (ipl - npl), rb = S.rec_len + (irc - nrec), qb = S.qhead + (ipo - npop);
+    if (lane < m && !direct) {
+      const size_t st0 = (size_t)s * PLC;
+      int popk = 0;
+      for (int j = 0; j < npl; j++) {
+        int task = D.s2_task[st0 + j];
+        const int w = D.s2_worker[st0 + j];
+        const long long pos = lb + j;
+        if (task < 0) {  // a queued task taken by the stimulus' refill: HeapSet order
+          task = D.qarr[qb + popk++];
+          D.state[task] = S_PROCESSING;
+          D.proc_on[task] = w;
+        }
+        D.pl_task[pos] = task;
+        D.pl_worker[pos] = w;
+        D.pl_comm[pos] = D.s2_comm[st0 + j];
+        D.pl_start[pos] = D.s2_start[st0 + j];
+        D.pl_wsnbytes[pos] = D.s2_wsnb[st0 + j];
+        D.pl_route[pos] = D.s2_route[st0 + j];
+        D.run_id[task] = (int32_t)pos;
+        D.holder_of[task] = w;
+      }
+      for (int j = 0; j < nrec; j++) D.rlog[rb + j] = D.srec[st0 + j];
+    }
+    if (rb + trc > D.rlog_cap) serr(S, SERR_REC, (int)sp);
+    __threadfence_block();
+    if (lane == 0) {
+      S.log_len += tpl;
+      S.rec_len += trc;
+      S.qhead += tpo;
+      S.qlen -= tpo;
+      S.n_tasks += tpl;
+      S.prof[0] += mclk() - t0;
+      S.prof[8] += 1;
+    }
+    lds_fence();
+    if (lane == 0) vstore(&S.seq_pos, sp + m);
+    t_idle = mclk();
+  }
+}
+
+// ======================================================================= builder
+__device__ void role_bld(const Dev& D, SLds& L) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  while (true) {
+    if (vload(&S.stop)) break;
+    const long long a = S.bld_pos;
+    const long long e = min(a + 64, vload(&S.log_len));
+    if (e <= a) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    lds_fence();
+    const unsigned long long t0 = mclk();
+    const long long r = a + lane;
+    if (r < e) {
+      const int t = D.pl_task[r];
+      const int w = D.pl_worker[r];
+      // the replica this completion creates (who_has, :3148)
+      atomicOr(&D.holders[(size_t)t * D.WB + (w >> 6)], 1ull << (w & 63));
+      const int64_t f0 = D.dpt_ptr[t], f1 = D.dpt_ptr[t + 1];
+      for (int64_t k = f0; k < f1; k++) {  // waiting_on.discard (:3298-3307)
+        const int x = D.dpt_idx[k];
+        if (atomicSub(&D.remaining[x], 1) == 1) {
+          int s = -1;  // the stimulus that empties waiting_on: the dependency completed last
+          for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++) s = max(s, D.run_id[D.dep_idx[q]]);
+          D.fr_mark[x] = s;
+        }
+      }
+      const int64_t k0 = D.dep_ptr[t], k1 = D.dep_ptr[t + 1];
+      for (int64_t k = k0; k < k1; k++) {  // waiters.discard -> release (:3309-3314)
+        const int d = D.dep_idx[k];
+        if (atomicSub(&D.waiters[d], 1) == 1 && !(D.tflags[d] & TF_WANTED)) {
+          int s = -1;
+          for (int64_t q = D.dpt_ptr[d]; q < D.dpt_ptr[d + 1]; q++) s = max(s, D.run_id[D.dpt_idx[q]]);
+          D.rel_mark[d] = s;
+        }
+      }
+    }
+    __threadfence_block();
+    wbar();
+    if (lane == 0) {
+      S.prof[1] += mclk() - t0;
+      vstore(&S.bld_pos, e);
+    }
+  }
+}
+
+// ==================================================================== prefetcher
+// descriptor of stimulus r (one lane): see E_HDR for the header layout
+__device__ void build_desc(const Dev& D, long long r) {
+  uint4* E = D.desc + (size_t)(r & (DR - 1)) * NE;
+  const int t = D.pl_task[r];
+  const int w = D.pl_worker[r];
+  const int p = D.prefix[t];
+  const int g = D.group[t];
+  const uint8_t tf = D.tflags[t];
+  const int64_t nbt = nbv(D, D.res_nbytes[t]);
+  const double dobs = D.res_stop[t] - D.res_start[t];
+  const int64_t k0 = D.dep_ptr[t], k1 = D.dep_ptr[t + 1];
+  const int64_t f0 = D.dpt_ptr[t], f1 = D.dpt_ptr[t + 1];
+  const int kt = (int)(k1 - k0);
+  uint32_t flags = 0;
+  if (f1 == f0 && !(tf & TF_WANTED)) flags |= F_SELFREL;
+  if (kt > KT_MAX) flags |= F_GLOBAL;
+  int n = E_HDR, nrel = 0, nf = 0;
+  if (!(flags & F_GLOBAL)) {
+    for (int64_t k = k0; k < k1; k++) {
+      const int d = D.dep_idx[k];
+      const int64_t nb = nbv(D, D.res_nbytes[d]);
+      E[n++] = make_uint4((unsigned)d, (unsigned)D.holder_of[d], lo32(nb), hi32(nb));
+    }
+    for (int64_t k = k0; k < k1; k++) {
+      const int d = D.dep_idx[k];
+      if (D.rel_mark[d] != (int)r) continue;
+      if (n >= NE) {
+        flags |= F_GLOBAL;
+        break;
+      }
+      const int64_t nb = nbv(D, D.res_nbytes[d]);
+      E[n++] = make_uint4((unsigned)D.holder_of[d], (unsigned)d, lo32(nb), hi32(nb));
+      nrel++;
+    }
+  }
+  for (int64_t k = f0; k < f1; k++) {  // dependents in ascending priority = frontier order
+    const int x = D.dpt_idx[k];
+    if (D.fr_mark[x] != (int)r) continue;
+    nf++;
+    if (flags & F_GLOBAL) continue;
+    const int64_t x0 = D.dep_ptr[x], x1 = D.dep_ptr[x + 1];
+    const int kx = (int)(x1 - x0);
+    if ((D.tflags[x] & TF_ROOTISH) || kx > KX_MAX || n + 1 + kx > NE) {
+      flags |= F_GLOBAL;
+      continue;
+    }
+    E[n++] = make_uint4((unsigned)x, (unsigned)D.prefix[x], (unsigned)kx, (unsigned)D.group[x]);
+    for (int64_t q = x0; q < x1; q++) {
+      const int d = D.dep_idx[q];
+      const int64_t nb = nbv(D, D.res_nbytes[d]);
+      E[n++] = make_uint4((unsigned)d, (unsigned)D.holder_of[d], lo32(nb), hi32(nb));
+    }
+  }
+  if (nf > 255) flags |= F_GLOBAL;
+  E[0] = make_uint4((unsigned)t, (unsigned)w, (unsigned)p, flags);
+  E[1] = make_uint4(lo32(nbt), hi32(nbt),
+                    (unsigned)(min(kt, 255) | (nrel << 8) | (min(nf, 255) << 16) | (n << 24)), (unsigned)g);
+  E[2] = make_uint4(dlo(dobs), dhi(dobs), 0u, 0u);
+}
+
+__device__ void role_pre(const Dev& D, SLds& L) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  while (true) {
+    if (vload(&S.stop)) break;
+    const long long a = S.pre_pos;
+    const long long e = min(min(a + 64, vload(&S.bld_pos)), vload(&S.seq_pos) + DR);
+    if (e <= a) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    lds_fence();
+    const unsigned long long t0 = mclk();
+    const long long r = a + lane;
+    if (r < e) build_desc(D, r);
+    __threadfence_block();
+    if (r < e) D.desc_tag[r & (DR - 1)] = r + 1;
+    __threadfence_block();
+    wbar();
+    if (lane == 0) {
+      S.prof[2] += mclk() - t0;
+      vstore(&S.pre_pos, e);
+    }
+  }
+}
+
+// ===================================================================== registrar
+template <bool LW>
+__device__ void role_reg(const Dev& D, SLds& L, const WPtr& P) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  double dur = lane < D.P ? D.pdur_cur[lane] : -1.0;  // lane p: duration_average as of reg_pos
+  unsigned long long t_idle = mclk();
+  while (true) {
+    if (vload(&S.stop)) break;
+    const long long r = S.reg_pos;
+    const long long lim = min(min(vload(&S.pre_pos), vload(&S.reg_limit)), vload(&S.seq_pos) + WIN);
+    if (r >= lim || vload(&S.global_pending)) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    lds_fence();
+    const unsigned long long t0 = mclk();
+    const int s = (int)(r & (WIN - 1));
+    uint4 E = make_uint4(0, 0, 0, 0);
+    if (lane < NE) E = D.desc[(size_t)(r & (DR - 1)) * NE + lane];
+    if (D.desc_tag[r & (DR - 1)] != r + 1) {
+      serr(S, SERR_STAGE, (int)r);
+      break;
+    }
+    // TaskPrefix.add_duration (:977-985) of the completing task's prefix
+    const int p = rl((int)E.z, 0);
+    const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
+    if (lane == p) dur = dur < 0 ? dobs : 0.5 * dobs + 0.5 * dur;
+    const double rv = resolve_dur(D, dur);
+    {
+      const int src = 2 * (max(lane - 3, 0) & 3);
+      const double a0 = __shfl(rv, src), a1 = __shfl(rv, src + 1);
+      if (lane >= 3 && lane < 7) E = make_uint4(dlo(a0), dhi(a0), dlo(a1), dhi(a1));
+    }
+    uint32_t flags = rlu(E.w, 0);
+    const int w = rl((int)E.y, 0);
+    const unsigned cnts = rlu(E.z, 1);
+    const int kt = cnts & 0xff, nrel = (cnts >> 8) & 0xff, nf = (cnts >> 16) & 0xff;
+    if (D.dbg & 1) flags |= F_EXACT;
+    if (D.dbg & 2) flags |= F_GLOBAL;
+    if (!(flags & F_GLOBAL)) {
+      const int capw = D.sat_inf ? 0 : (int)P.cap[w];
+      if (nf + capw + 1 > PLC) flags |= F_GLOBAL;
+      if (vload(&S.qlen) > 0 && (!S.inv_ok || !S.q_anon)) flags |= F_GLOBAL;
+    }
+    if (lane == 0) E.w = flags;
+    if (lane < NE) L.desc[s][lane] = E;
+    int tw = -1;
+    bool keep = false;
+    if (!(flags & F_GLOBAL)) {
+      if (lane == 0) tw = w;
+      if (lane >= E_HDR + kt && lane < E_HDR + kt + nrel) tw = (int)E.x;
+      int off = E_HDR + kt + nrel;
+      for (int j = 0; j < nf; j++) {
+        const int kx = rl((int)E.z, off) & 0xff;
+        if (lane > off && lane <= off + kx) tw = (int)E.y;
+        off += 1 + kx;
+      }
+      keep = tw >= 0;
+      unsigned long long rem = ballot(keep);
+      while (rem) {  // keep the first lane of every distinct worker
+        const int i = __builtin_ctzll(rem);
+        const int v = rl(tw, i);
+        const unsigned long long same = ballot(tw == v);
+        if (tw == v && lane != i) keep = false;
+        rem &= ~same;
+      }
+      const unsigned long long km = ballot(keep);
+      const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0));
+      if (keep) L.touch[s][pos] = (uint16_t)tw;
+      if (lane == 0) L.ntouch[s] = __builtin_popcountll(km);
+    } else {
+      flags |= F_TOUCHALL;
+      if (lane == 0) L.ntouch[s] = 0;
+    }
+    if (lane == 0) {
+      L.flags[s] = flags;
+      L.pred[s] = BIG;
+      L.sid[s] = r;
+    }
+    lds_fence();
+    const unsigned bit = 1u << s;
+    int cnt = 0;
+    if (flags & F_TOUCHALL) {
+      for (int c = lane; c < D.W; c += 64) cnt += __builtin_popcount(atomicOr(&P.mask[c], bit) & ~bit);
+    } else if (keep) {
+      cnt = __builtin_popcount(atomicOr(&P.mask[tw], bit) & ~bit);
+    }
+    const int tot = wsum(cnt);
+    if (lane == 0) {
+      const int old = atomicAdd(&L.pred[s], tot - BIG);
+      if (old + tot - BIG == 0) atomicOr(&S.ready, bit);
+      if (flags & F_GLOBAL) vstore(&S.global_pending, 1);
+      S.prof[3] += mclk() - t0;
+      vstore(&S.reg_pos, r + 1);
+    }
+    lds_fence();
+    t_idle = mclk();
+  }
+  (void)t_idle;
+  if (lane < D.P && lane < PD) D.pdur_cur[lane] = dur;
+}
+
+// ===================================================================== executors
+// needs_what of one worker (:800-823): LDS line in lanes 0..NLW-2, control word in lane
+// NLW-1 (count of entries << 8 | 1 when overflow entries are in use; NL_OVF: scan mode),
+// overflow entries in D.gw_needs_ext (global), scan mode = exact needed_elsewhere checks.
+__device__ __forceinline__ bool st_needed_elsewhere(const Dev& D, int d, int w, int except) {
+  for (int64_t k = D.dpt_ptr[d]; k < D.dpt_ptr[d + 1]; k++) {
+    const int x = D.dpt_idx[k];
+    if (x != except && D.proc_on[x] == w) return true;
+  }
+  return false;
+}
+
+template <bool LW>
+__device__ __forceinline__ uint32_t line_load(const WPtr& P, int c) {
+  return lane_id() < NLW ? P.needs[(size_t)c * NLW + lane_id()] : 0u;
+}
+template <bool LW>
+__device__ __forceinline__ void line_store(const WPtr& P, int c, uint32_t nl) {
+  if (lane_id() < NLW) P.needs[(size_t)c * NLW + lane_id()] = nl;
+}
+__device__ __forceinline__ int line_used(uint32_t nl) { return __builtin_popcountll(ballot(lane_id() < NLW - 1 && nl != 0)); }
+
+// _dec_needs_replica for dependency d (held elsewhere) of the task leaving worker c
+// (returns the bytes c no longer needs)
+__device__ int64_t needs_dec(const Dev& D, SCtl& S, int c, uint32_t& nl, int d, int64_t nb, int except) {
+  const int lane = lane_id();
+  const uint32_t ctl = __shfl(nl, NLW - 1);
+  if (ctl == NL_OVF) return st_needed_elsewhere(D, d, c, except) ? 0 : nb;
+  const unsigned long long m = ballot(lane < NLW - 1 && nl != 0 && (nl >> 8) == (uint32_t)d);
+  if (m) {
+    const int ml = __builtin_ctzll(m);
+    const uint32_t v = rlu(nl, ml) - 1;
+    const bool gone = (v & 0xffu) == 0;
+    if (lane == ml) nl = gone ? 0u : v;
+    if (gone && lane == NLW - 1) nl -= 0x100u;
+    return gone ? nb : 0;
+  }
+  const int ext = (int)(ctl >> 8) - line_used(nl);
+  if (ext > 0) {
+    uint32_t* X = D.gw_needs_ext + (size_t)c * NXW;
+    const uint32_t xe = lane < NXW ? __hip_atomic_load(X + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const unsigned long long mx = ballot(lane < NXW && xe != 0 && (xe >> 8) == (uint32_t)d);
+    if (mx) {
+      const int ml = __builtin_ctzll(mx);
+      const uint32_t v = rlu(xe, ml) - 1;
+      const bool gone = (v & 0xffu) == 0;
+      if (lane == ml) __hip_atomic_store(X + ml, gone ? 0u : v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (gone && lane == NLW - 1) nl -= 0x100u;
+      __threadfence_block();
+      return gone ? nb : 0;
+    }
+  }
+  serr(S, SERR_NEEDS, d);
+  return 0;
+}
+
+// _inc_needs_replica for dependency d (not held by c) of task `except` placed on c
+// (returns the bytes c newly needs)
+__device__ int64_t needs_inc(const Dev& D, SCtl& S, int c, uint32_t& nl, int d, int64_t nb, int except) {
+  const int lane = lane_id();
+  const uint32_t ctl = __shfl(nl, NLW - 1);
+  if (ctl == NL_OVF) return st_needed_elsewhere(D, d, c, except) ? 0 : nb;
+  const unsigned long long m = ballot(lane < NLW - 1 && nl != 0 && (nl >> 8) == (uint32_t)d);
+  if (m) {
+    const int ml = __builtin_ctzll(m);
+    if ((rlu(nl, ml) & 0xffu) == 0xffu) {
+      serr(S, SERR_NEEDS, d);
+      return 0;
+    }
+    if (lane == ml) nl += 1;
+    return 0;
+  }
+  const int used = line_used(nl);
+  const int ext = (int)(ctl >> 8) - used;
+  uint32_t* X = D.gw_needs_ext + (size_t)c * NXW;
+  uint32_t xe = 0;
+  if (ext > 0) {
+    xe = lane < NXW ? __hip_atomic_load(X + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const unsigned long long mx = ballot(lane < NXW && xe != 0 && (xe >> 8) == (uint32_t)d);
+    if (mx) {
+      const int ml = __builtin_ctzll(mx);
+      if ((rlu(xe, ml) & 0xffu) == 0xffu) {
+        serr(S, SERR_NEEDS, d);
+        return 0;
+      }
+      if (lane == ml) __hip_atomic_store(X + ml, xe + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_block();
+      return 0;
+    }
+  }
+  const unsigned long long em = ballot(lane < NLW - 1 && nl == 0);
+  if (em) {
+    if (lane == __builtin_ctzll(em)) nl = ((uint32_t)d << 8) | 1u;
+    if (lane == NLW - 1) nl += 0x100u;
+    return nb;
+  }
+  if (ext < NXW) {
+    const unsigned long long ex = ballot(lane < NXW && xe == 0);
+    const int ml = __builtin_ctzll(ex);
+    if (lane == ml) __hip_atomic_store(X + ml, ((uint32_t)d << 8) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == NLW - 1) nl = nl + 0x100u;
+    __threadfence_block();
+    return nb;
+  }
+  // full: scan mode from here on (only reached when every earlier stimulus has retired)
+  if (lane == NLW - 1) nl = NL_OVF;
+  return nb;
+}
+
+// a worker with nothing processing needs nothing (leave scan / overflow mode)
+__device__ void needs_reset(const Dev& D, int c, uint32_t& nl) {
+  const int lane = lane_id();
+  const uint32_t ctl = __shfl(nl, NLW - 1);
+  if (ctl == NL_OVF || (ctl >> 8) != 0) {
+    if (lane < NXW) __hip_atomic_store(D.gw_needs_ext + (size_t)c * NXW + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence_block();
+  }
+  if (lane < NLW) nl = 0;
+}
+
+// per-stimulus outputs in lanes: record k in lane k, placement q in lane q
+struct Out {
+  int nrec, npl;
+  int r_kind, r_w, r_p, r_np, r_task;
+  int64_t r_dnet;
+  double r_occ, r_dur;
+  int q_task, q_w, q_route;
+  int64_t q_comm, q_wsnb;
+  double q_start;
+  __device__ void rec(int kind, int w, int p, int64_t dnet, double occ, int np, int task, double dur) {
+    if (lane_id() == nrec) {
+      r_kind = kind;
+      r_w = w;
+      r_p = p;
+      r_dnet = dnet;
+      r_occ = occ;
+      r_np = np;
+      r_task = task;
+      r_dur = dur;
+    }
+    nrec++;
+  }
+  __device__ void place(int task, int w, int64_t comm, double start, int64_t wsnb, int route) {
+    if (lane_id() == npl) {
+      q_task = task;
+      q_w = w;
+      q_comm = comm;
+      q_start = start;
+      q_wsnb = wsnb;
+      q_route = route;
+    }
+    npl++;
+  }
+};
+
+// WorkerState.add_to_processing / remove_from_processing on the dict of c (:733-771)
+template <bool LW>
+__device__ __forceinline__ bool dict_update(const WPtr& P, int c, int p, int delta, uint4& pf, uint4& pc, uint32_t& n) {
+  pf = *reinterpret_cast<const uint4*>(P.pfx + (size_t)c * PMW);
+  pc = *reinterpret_cast<const uint4*>(P.pcnt + (size_t)c * PMW);
+  n = P.plen[c] & 0xffu;
+  const bool ok = dict_add(pf, pc, n, p, delta);
+  if (lane_id() == 0) {
+    *reinterpret_cast<uint4*>(P.pfx + (size_t)c * PMW) = pf;
+    *reinterpret_cast<uint4*>(P.pcnt + (size_t)c * PMW) = pc;
+    P.plen[c] = n;
+  }
+  return ok;
+}
+
+// release the workers of slot s (the waiting successors may run) — LDS state only
+template <bool LW>
+__device__ void release_slot(const Dev& D, SLds& L, const WPtr& P, int s, bool all) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  const unsigned bit = 1u << s;
+  auto rel = [&](int c) {
+    unsigned succ = atomicAnd(&P.mask[c], ~bit) & ~bit;
+    while (succ) {
+      const int b = __builtin_ctz(succ);
+      succ &= succ - 1;
+      if (atomicSub(&L.pred[b], 1) == 1) atomicOr(&S.ready, 1u << b);
+    }
+  };
+  if (all) {
+    for (int c = lane; c < D.W; c += 64) rel(c);
+  } else {
+    const int nt = L.ntouch[s];
+    if (lane < nt) rel((int)L.touch[s][lane]);
+  }
+}
+
+// stage outputs, publish counts, retire: after this SEQ may consume the slot
+__device__ void finish_slot(const Dev& D, SLds& L, int s, long long r, const Out& o, int npops, bool direct) {
+  const int lane = lane_id();
+  if (!direct) {
+    const size_t st0 = (size_t)s * PLC;
+    if (lane < o.npl) {
+      D.s2_task[st0 + lane] = o.q_task;
+      D.s2_worker[st0 + lane] = o.q_w;
+      D.s2_comm[st0 + lane] = o.q_comm;
+      D.s2_start[st0 + lane] = o.q_start;
+      D.s2_wsnb[st0 + lane] = o.q_wsnb;
+      D.s2_route[st0 + lane] = (int8_t)o.q_route;
+    }
+    if (lane < o.nrec) {
+      SRec rc;
+      rc.w = o.r_w;
+      rc.p = (int16_t)o.r_p;
+      rc.kind = (int8_t)o.r_kind;
+      rc.pad = 0;
+      rc.nproc = o.r_np;
+      rc.task = o.r_task;
+      rc.dnet = o.r_dnet;
+      rc.occ = o.r_occ;
+      rc.dur = o.r_dur;
+      D.srec[st0 + lane] = rc;
+    }
+  }
+  if (lane == 0) {
+    L.npl[s] = o.npl;
+    L.nrec[s] = direct ? 0 : o.nrec;
+    L.npops[s] = npops;
+  }
+  __threadfence_block();
+  if (lane == 0) vstore(&L.done_tag[s], r + 1);
+}
+
+// objective key of lane's candidate: worker_objective (:3131-3146) + canonical index
+struct Key {
+  double start;
+  int64_t nb;
+  int w;
+  int64_t comm;
+};
+__device__ __forceinline__ bool key_less(const Key& a, const Key& b) {
+  if (a.start != b.start) return a.start < b.start;
+  if (a.nb != b.nb) return a.nb < b.nb;
+  return a.w < b.w;
+}
+__device__ __forceinline__ Key key_at(const Key& k, int l) {
+  Key o;
+  o.start = mkd(rlu(dlo(k.start), l), rlu(dhi(k.start), l));
+  o.nb = mk64(rlu(lo32(k.nb), l), rlu(hi32(k.nb), l));
+  o.w = rl(k.w, l);
+  o.comm = mk64(rlu(lo32(k.comm), l), rlu(hi32(k.comm), l));
+  return o;
+}
+
+// a stimulus whose effects stay on the workers it registered. Returns false (nothing
+// changed) when it needs every earlier stimulus retired first (needs scan mode).
+template <bool LW>
+__device__ bool exe_local(const Dev& D, SLds& L, const WPtr& P, int s, long long r, int qmode, bool exact) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  const uint4 E = lane < NE ? L.desc[s][lane] : make_uint4(0, 0, 0, 0);
+  const int t = rl((int)E.x, 0), w = rl((int)E.y, 0), p = rl((int)E.z, 0);
+  const uint32_t flags = rlu(E.w, 0);
+  const int64_t nbt = mk64(rlu(E.x, 1), rlu(E.y, 1));
+  const unsigned cnts = rlu(E.z, 1);
+  const int grp_t = rl((int)E.w, 1);
+  const int kt = cnts & 0xff, nrel = (cnts >> 8) & 0xff, nf = (cnts >> 16) & 0xff;
+  const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
+  const double durv = desc_durs(E);
+  const int TD = E_HDR, RL0 = E_HDR + kt, FX0 = RL0 + nrel;
+  // ---- capacity check of the needs tables this stimulus may grow
+  if (!exact) {
+    int tot_new = 0, off = FX0;
+    for (int j = 0; j < nf; j++) {
+      const int kx = rl((int)E.z, off) & 0xff;
+      tot_new += kx;
+      off += 1 + kx;
+    }
+    const int ntch = L.ntouch[s];
+    bool bad = false;
+    if (lane < ntch) {
+      const int c = L.touch[s][lane];
+      const uint32_t ctl = P.needs[(size_t)c * NLW + NLW - 1];
+      bad = ctl == NL_OVF || (int)(ctl >> 8) + tot_new > NLW - 1 + NXW;
+    }
+    if (ballot(bad)) return false;
+  }
+  Out o;
+  o.nrec = 0;
+  o.npl = 0;
+  // ------------------------------------------- completion: processing -> memory (:2366)
+  uint4 pf, pc;
+  uint32_t pn;
+  const int np0 = P.nproc[w];
+  const int64_t no0 = P.netocc[w];
+  dict_update<LW>(P, w, p, -1, pf, pc, pn);
+  uint32_t nl = line_load<LW>(P, w);
+  int64_t dnet = 0;
+  for (int i = 0; i < kt; i++) {  // _dec_needs_replica for the dependencies w needed
+    const int L_ = TD + i;
+    const int h = rl((int)E.y, L_);
+    if (h == w) continue;
+    const int d = rl((int)E.x, L_);
+    const int64_t nb = mk64(rlu(E.z, L_), rlu(E.w, L_));
+    dnet -= needs_dec(D, S, w, nl, d, nb, t);
+  }
+  const int npw = np0 - 1;
+  if (npw == 0) needs_reset(D, w, nl);
+  line_store<LW>(P, w, nl);
+  if (lane == 0) {
+    P.nproc[w] = npw;
+    P.netocc[w] = no0 + dnet;
+  }
+  const double occw = occ_regs(pf, pc, pn, no0 + dnet, durv, D.bandwidth);
+  o.rec(K_COMPLETE, w, p, dnet, occw, npw, t, dobs);
+  // add_replica (:3148), then the releases popped before the frontier (LIFO, :3309-3314)
+  if (lane == 0) atomicAdd((unsigned long long*)&P.nbytes[w], (unsigned long long)nbt);
+  if (flags & F_SELFREL) {
+    if (lane == 0) atomicAdd((unsigned long long*)&P.nbytes[w], (unsigned long long)(-nbt));
+  }
+  if (lane >= RL0 && lane < RL0 + nrel) {
+    const int64_t nb = mk64(E.z, E.w);
+    atomicAdd((unsigned long long*)&P.nbytes[(int)E.x], (unsigned long long)(-nb));
+  }
+  // ------------------------------ frontier in ascending priority: decide_worker (:8550)
+  int off = FX0;
+  for (int j = 0; j < nf; j++) {
+    const int x = rl((int)E.x, off), px = rl((int)E.y, off), kx = rl((int)E.z, off) & 0xff;
+    const int gx = rl((int)E.w, off);
+    const bool in = lane > off && lane <= off + kx;
+    const int h = (int)E.y;
+    int64_t comm = 0;
+    bool rep = in;
+    for (int i = 0; i < kx; i++) {
+      const int L2 = off + 1 + i;
+      const int hi = rl((int)E.y, L2);
+      const int64_t nbi = mk64(rlu(E.z, L2), rlu(E.w, L2));
+      if (in && hi != h) comm += nbi;
+      if (in && L2 < lane && hi == h) rep = false;
+    }
+    const int c = in ? h : w;
+    const double oc = occ_of<LW>(P, D, c, durv);
+    Key k;
+    k.start = oc / (double)P.nthreads[c] + (double)comm / (double)D.bandwidth;
+    k.nb = P.nbytes[c];
+    k.w = c;
+    k.comm = comm;
+    if (x == D.dbg_task && in) {
+      double* B = D.dbgbuf + (size_t)lane * 8;
+      B[0] = c;
+      B[1] = k.start;
+      B[2] = (double)k.nb;
+      B[3] = (double)comm;
+      B[4] = oc;
+      B[5] = P.nproc[c];
+      B[6] = (double)P.netocc[c];
+      B[7] = (double)(P.plen[c] & 0xff) + 100.0 * r;
+    }
+    const unsigned long long reps = ballot(rep);
+    if (!reps) {
+      serr(S, SERR_CAND, x);
+      return true;
+    }
+    Key best = key_at(k, __builtin_ctzll(reps));
+    for (unsigned long long rm = reps & (reps - 1); rm; rm &= rm - 1) {
+      const Key q = key_at(k, __builtin_ctzll(rm));
+      if (key_less(q, best)) best = q;
+    }
+    const int cb = best.w;
+    // _add_to_processing (:3199): record, WorkerState.add_to_processing, check_idle_saturated
+    o.place(x, cb, best.comm, best.start, best.nb, ROUTE_NONROOTISH);
+    const int npc0 = P.nproc[cb];
+    const int64_t noc0 = P.netocc[cb];
+    if (!dict_update<LW>(P, cb, px, +1, pf, pc, pn)) serr(S, SERR_PREFIX, x);
+    uint32_t nlc = line_load<LW>(P, cb);
+    int64_t dn = 0;
+    if (exact) {  // scan mode reads processing_on of this stimulus' earlier placements
+      __threadfence_block();
+    }
+    for (int i = 0; i < kx; i++) {
+      const int L2 = off + 1 + i;
+      if (rl((int)E.y, L2) == cb) continue;
+      const int d = rl((int)E.x, L2);
+      const int64_t nb = mk64(rlu(E.z, L2), rlu(E.w, L2));
+      dn += needs_inc(D, S, cb, nlc, d, nb, x);
+    }
+    line_store<LW>(P, cb, nlc);
+    if (lane == 0) {
+      P.nproc[cb] = npc0 + 1;
+      P.netocc[cb] = noc0 + dn;
+      D.proc_on[x] = cb;
+      D.state[x] = S_PROCESSING;
+      atomicAdd((unsigned long long*)&D.g_relwait[gx], (unsigned long long)-1ll);
+    }
+    const double occc = occ_regs(pf, pc, pn, noc0 + dn, durv, D.bandwidth);
+    o.rec(K_PLACE, cb, px, dn, occc, npc0 + 1, x, 0.0);
+    off += 1 + kx;
+  }
+  // -------------- stimulus_queue_slots_maybe_opened (:4983): only w can have open slots
+  int pops = 0;
+  if (qmode != 0 && !D.sat_inf) {
+    const int slots = (int)P.cap[w] - P.nproc[w];
+    if (slots > 0) {
+      pops = slots;
+      if (qmode == 3) pops = (int)min((long long)slots, vload(&S.qlen));
+    }
+    for (int i = 0; i < pops; i++) {
+      const int np1 = P.nproc[w];
+      const int64_t nw = P.netocc[w];
+      const double ow = occ_of<LW>(P, D, w, durv);
+      o.place(-1, w, 0, ow / (double)P.nthreads[w] + 0.0 / (double)D.bandwidth, P.nbytes[w], ROUTE_ROOTISH_Q);
+      if (!dict_update<LW>(P, w, S.q_prefix, +1, pf, pc, pn)) serr(S, SERR_PREFIX, -1);
+      if (lane == 0) P.nproc[w] = np1 + 1;
+      o.rec(K_PLACE, w, S.q_prefix, 0, occ_regs(pf, pc, pn, nw, durv, D.bandwidth), np1 + 1, -1, 0.0);
+    }
+  }
+  // ------------------------------------------------ retire: LDS state, then successors
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS writes above are performed
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  release_slot<LW>(D, L, P, s, false);
+  // replica bookkeeping in HBM (TaskState fields; the walker / globals read them later)
+  if (lane == 0) {
+    D.cur_nbytes[t] = nbt;
+    D.proc_on[t] = -1;
+    D.state[t] = (flags & F_SELFREL) ? S_RELEASED : S_MEMORY;
+    if (flags & F_SELFREL) {
+      atomicAdd((unsigned long long*)&D.g_relwait[grp_t], 1ull);
+      D.holders[(size_t)t * D.WB + (w >> 6)] = 0;
+    }
+  }
+  if (lane >= RL0 && lane < RL0 + nrel) {
+    const int d = (int)E.y, hd = (int)E.x;
+    D.state[d] = S_RELEASED;
+    D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
+    atomicAdd((unsigned long long*)&D.g_relwait[D.group[d]], 1ull);
+  }
+  finish_slot(D, L, s, r, o, pops, false);
+  return true;
+}
+
+// wave argmin over all workers of a key computed per worker (global stimuli)
+template <class F>
+__device__ __forceinline__ Key argmin_workers(const Dev& D, F&& key_of) {
+  const int lane = lane_id();
+  Key best{INFINITY, INT64_MAX, INT32_MAX, 0};
+  for (int c0 = 0; c0 < D.W; c0 += 64) {
+    const int c = min(c0 + lane, D.W - 1);
+    Key k;
+    const bool ok = key_of(c, k) && c0 + lane < D.W;
+    if (ok && key_less(k, best)) best = k;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    Key q;
+    q.start = __shfl_xor(best.start, o);
+    q.nb = __shfl_xor(best.nb, o);
+    q.w = __shfl_xor(best.w, o);
+    q.comm = __shfl_xor(best.comm, o);
+    if (key_less(q, best)) best = q;
+  }
+  return best;
+}
+
+// a stimulus that reads SchedulerState-global state: every earlier stimulus has retired,
+// every later one waits, the walker is caught up. Exact restatement of the whole
+// transition (:2366-2442, :2313-2336, :4983-5023) for any route; placements go straight
+// into the placement log, records are folded as they happen.
+template <bool LW>
+__device__ void exe_global(const Dev& D, SLds& L, const WPtr& P, int s, long long r) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  const uint4 E = lane < NE ? L.desc[s][lane] : make_uint4(0, 0, 0, 0);
+  const int t = rl((int)E.x, 0), w = rl((int)E.y, 0), p = rl((int)E.z, 0);
+  const int64_t nbt = mk64(rlu(E.x, 1), rlu(E.y, 1));
+  const int grp_t = rl((int)E.w, 1);
+  const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
+  const double durv = desc_durs(E);
+  WState g;
+  ws_load(S, g);
+  const long long lpos = S.log_len;
+  int npl = 0;
+  auto put_log = [&](int task, int wk, int64_t comm, double start, int64_t wsnb, int route) {
+    if (lane == 0) {
+      const long long pos = lpos + npl;
+      D.pl_task[pos] = task;
+      D.pl_worker[pos] = wk;
+      D.pl_comm[pos] = comm;
+      D.pl_start[pos] = start;
+      D.pl_wsnbytes[pos] = wsnb;
+      D.pl_route[pos] = (int8_t)route;
+      D.run_id[task] = (int32_t)pos;
+      D.holder_of[task] = wk;
+    }
+    npl++;
+  };
+  auto comm_bytes = [&](int x, int c) -> int64_t {  // worker_objective's sum :3136-3138
+    int64_t v = 0;
+    for (int64_t k = D.dep_ptr[x] + lane; k < D.dep_ptr[x + 1]; k += 64) {
+      const int d = D.dep_idx[k];
+      if (D.holder_of[d] != c) v += nbv(D, D.res_nbytes[d]);
+    }
+    return wsum64(v);
+  };
+  uint4 pf, pc;
+  uint32_t pn;
+  // _add_to_processing (:3199) of x on c; x WAITING (frontier) or QUEUED (refill)
+  auto place_x = [&](int x, int c, int route, int64_t comm, bool was_waiting) {
+    if (comm < 0) comm = comm_bytes(x, c);
+    const double oc = occ_of<LW>(P, D, c, durv);
+    put_log(x, c, comm, oc / (double)P.nthreads[c] + (double)comm / (double)D.bandwidth, P.nbytes[c], route);
+    const int px = D.prefix[x];
+    const int np0 = P.nproc[c];
+    const int64_t no0 = P.netocc[c];
+    if (!dict_update<LW>(P, c, px, +1, pf, pc, pn)) serr(S, SERR_PREFIX, x);
+    uint32_t nl = line_load<LW>(P, c);
+    int64_t dn = 0;
+    for (int64_t k = D.dep_ptr[x]; k < D.dep_ptr[x + 1]; k++) {
+      const int d = D.dep_idx[k];
+      if (D.holder_of[d] == c) continue;
+      dn += needs_inc(D, S, c, nl, d, nbv(D, D.res_nbytes[d]), x);
+    }
+    line_store<LW>(P, c, nl);
+    if (lane == 0) {
+      P.nproc[c] = np0 + 1;
+      P.netocc[c] = no0 + dn;
+      D.proc_on[x] = c;
+      D.state[x] = S_PROCESSING;
+      if (was_waiting) atomicAdd((unsigned long long*)&D.g_relwait[D.group[x]], (unsigned long long)-1ll);
+    }
+    __threadfence_block();
+    ws_fold<LW>(D, P, S, g, K_PLACE, c, px, dn, occ_regs(pf, pc, pn, no0 + dn, durv, D.bandwidth), np0 + 1, 0.0);
+  };
+  auto itc_argmin = [&]() -> int {  // decide_worker_rootish_queuing_enabled :2230-2233
+    Key b = argmin_workers(D, [&](int c, Key& k) {
+      if (!D.sat_inf && (int)P.cap[c] - P.nproc[c] <= 0) return false;
+      k.start = (double)P.nproc[c] / (double)P.nthreads[c];
+      k.nb = 0;
+      k.w = c;
+      k.comm = 0;
+      return true;
+    });
+    return b.w == INT32_MAX ? -1 : b.w;
+  };
+  bool queue_changed = false;
+  // ------------------------------------------------------------- completion (:2366)
+  {
+    const int np0 = P.nproc[w];
+    const int64_t no0 = P.netocc[w];
+    dict_update<LW>(P, w, p, -1, pf, pc, pn);
+    uint32_t nl = line_load<LW>(P, w);
+    int64_t dnet = 0;
+    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+      const int d = D.dep_idx[k];
+      if (D.holder_of[d] == w) continue;
+      dnet -= needs_dec(D, S, w, nl, d, nbv(D, D.res_nbytes[d]), t);
+    }
+    if (np0 - 1 == 0) needs_reset(D, w, nl);
+    line_store<LW>(P, w, nl);
+    if (lane == 0) {
+      P.nproc[w] = np0 - 1;
+      P.netocc[w] = no0 + dnet;
+      P.nbytes[w] += nbt;  // add_replica :3148
+      D.cur_nbytes[t] = nbt;
+      D.proc_on[t] = -1;
+      D.state[t] = S_MEMORY;
+    }
+    ws_fold<LW>(D, P, S, g, K_COMPLETE, w, p, dnet, occ_regs(pf, pc, pn, no0 + dnet, durv, D.bandwidth), np0 - 1,
+                dobs);
+  }
+  // ------------------------------------------------------ releases (:3309-3314, :2444)
+  const int64_t f0 = D.dpt_ptr[t], f1 = D.dpt_ptr[t + 1];
+  if (lane == 0) {
+    if (f1 == f0 && !(D.tflags[t] & TF_WANTED)) {
+      P.nbytes[w] -= nbt;
+      D.state[t] = S_RELEASED;
+      D.holders[(size_t)t * D.WB + (w >> 6)] = 0;
+      atomicAdd((unsigned long long*)&D.g_relwait[grp_t], 1ull);
+    }
+    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+      const int d = D.dep_idx[k];
+      if (D.rel_mark[d] != (int)r) continue;
+      const int hd = D.holder_of[d];
+      P.nbytes[hd] -= nbv(D, D.res_nbytes[d]);
+      D.state[d] = S_RELEASED;
+      D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
+      atomicAdd((unsigned long long*)&D.g_relwait[D.group[d]], 1ull);
+    }
+  }
+  wbar();
+  // -------------------------------------- frontier, ascending priority (:2313-2336)
+  for (int64_t k = f0; k < f1; k++) {
+    const int x = D.dpt_idx[k];
+    if (D.fr_mark[x] != (int)r) continue;
+    if (D.tflags[x] & TF_ROOTISH) {
+      const int gi = D.group[x];
+      if (D.sat_inf) {  // decide_worker_rootish_queuing_disabled :2135-2193
+        int c = D.g_lastw[gi];
+        if (!(c >= 0 && D.g_left[gi] != 0)) {
+          const bool use_idle = g.n_idle > 0;
+          Key b = argmin_workers(D, [&](int cw, Key& kk) {
+            const double ocw = occ_of<LW>(P, D, cw, durv);  // all lanes: it shuffles
+            if (use_idle && !(P.wflags[cw] & WF_IDLE)) return false;
+            int64_t cm = 0;
+            for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++)
+              if (D.holder_of[D.dep_idx[q]] != cw) cm += nbv(D, D.res_nbytes[D.dep_idx[q]]);
+            kk.start = ocw / (double)P.nthreads[cw] + (double)cm / (double)D.bandwidth;
+            kk.nb = P.nbytes[cw];
+            kk.w = cw;
+            kk.comm = cm;
+            return true;
+          });
+          c = b.w;
+          if (lane == 0)
+            D.g_left[gi] = (int64_t)floor(((double)D.g_size[gi] / (double)D.total_nthreads) * (double)P.nthreads[c]);
+        }
+        if (lane == 0) {
+          D.g_lastw[gi] = D.g_relwait[gi] > 1 ? c : -1;
+          D.g_left[gi] -= 1;
+        }
+        wbar();
+        place_x(x, c, ROUTE_ROOTISH_NOQ, -1, true);
+      } else {  // decide_worker_rootish_queuing_enabled :2195-2245
+        const int c = itc_argmin();
+        if (c < 0) {  // -> queued (:2761): HeapSet.add, kept as a priority-sorted array
+          if (lane == 0) {
+            D.state[x] = S_QUEUED;
+            atomicAdd((unsigned long long*)&D.g_relwait[gi], (unsigned long long)-1ll);
+            long long lo = S.qhead, pos = S.qhead + S.qlen;
+            const int64_t pr = D.prio[x];
+            while (pos > lo && D.prio[D.qarr[pos - 1]] > pr) {
+              D.qarr[pos] = D.qarr[pos - 1];
+              pos--;
+            }
+            D.qarr[pos] = x;
+            S.qlen++;
+          }
+          queue_changed = true;
+          __threadfence_block();
+        } else {
+          place_x(x, c, ROUTE_ROOTISH_Q, -1, true);
+        }
+      }
+    } else if (D.dep_ptr[x + 1] > D.dep_ptr[x]) {  // decide_worker :8550-8593
+      Key b = argmin_workers(D, [&](int cw, Key& kk) {
+        const double ocw = occ_of<LW>(P, D, cw, durv);  // all lanes: it shuffles
+        bool cand = false;
+        for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1] && !cand; q++) cand = D.holder_of[D.dep_idx[q]] == cw;
+        if (!cand) return false;
+        int64_t cm = 0;
+        for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++)
+          if (D.holder_of[D.dep_idx[q]] != cw) cm += nbv(D, D.res_nbytes[D.dep_idx[q]]);
+        kk.start = ocw / (double)P.nthreads[cw] + (double)cm / (double)D.bandwidth;
+        kk.nb = P.nbytes[cw];
+        kk.w = cw;
+        kk.comm = cm;
+        if (x == D.dbg_task) {
+          double* B = D.dbgbuf + (size_t)lane * 8;
+          B[0] = cw;
+          B[1] = kk.start;
+          B[2] = (double)kk.nb;
+          B[3] = (double)cm;
+          B[4] = ocw;
+          B[5] = P.nproc[cw];
+          B[6] = (double)P.netocc[cw];
+          B[7] = (double)(P.plen[cw] & 0xff) + 100.0 * r;
+        }
+        return true;
+      });
+      if (b.w == INT32_MAX) {
+        serr(S, SERR_CAND, x);
+        break;
+      }
+      place_x(x, b.w, ROUTE_NONROOTISH, b.comm, true);
+    } else {
+      serr(S, SERR_CAND, x);
+      break;
+    }
+  }
+  // ---------------------------- Scheduler.stimulus_queue_slots_maybe_opened :4983-5023
+  if (S.qlen > 0 && !D.sat_inf) {
+    long long slots = 0;
+    for (int c = lane; c < D.W; c += 64) {
+      const int a = (int)P.cap[c] - P.nproc[c];
+      if (a > 0) slots += a;
+    }
+    slots = wsum64(slots);
+    for (long long k = 0; k < slots; k++) {
+      if (S.qlen == 0) break;
+      const int c = itc_argmin();
+      if (c < 0) continue;
+      const int q = D.qarr[S.qhead];
+      wbar();
+      if (lane == 0) {
+        S.qhead++;
+        S.qlen--;
+      }
+      wbar();
+      place_x(q, c, ROUTE_ROOTISH_Q, 0, false);
+    }
+  }
+  // the invariant local refills rely on, and whether queued tasks are interchangeable
+  {
+    bool open = false;
+    for (int c = lane; c < D.W && !D.sat_inf; c += 64) open = open || ((int)P.cap[c] - P.nproc[c] > 0);
+    const bool any_open = ballot(open) != 0;
+    if (lane == 0) S.inv_ok = (S.qlen == 0 || !any_open) ? 1 : 0;
+    if (queue_changed) {
+      const int p0 = S.qlen > 0 ? D.prefix[D.qarr[S.qhead]] : 0;
+      bool bad = false;
+      for (long long i = S.qhead + lane; i < S.qhead + S.qlen; i += 64) {
+        const int q = D.qarr[i];
+        bad = bad || D.prefix[q] != p0 || D.dep_ptr[q + 1] > D.dep_ptr[q];
+      }
+      const bool anyb = ballot(bad) != 0;
+      if (lane == 0) {
+        S.q_anon = anyb ? 0 : 1;
+        S.q_prefix = p0;
+      }
+    }
+  }
+  ws_store(S, g);
+  __threadfence_block();
+  release_slot<LW>(D, L, P, s, true);
+  Out o;
+  o.nrec = 0;
+  o.npl = npl;
+  finish_slot(D, L, s, r, o, 0, true);
+  if (lane == 0) vstore(&S.global_pending, 0);
+}
+
+template <bool LW>
+__device__ void role_exe(const Dev& D, SLds& L, const WPtr& P) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  while (true) {
+    if (vload(&S.stop)) break;
+    const unsigned m = vload(&S.ready);
+    if (!m) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    const long long sp = vload(&S.seq_pos);
+    const int rot = (int)(sp & (WIN - 1));
+    unsigned mr = rot ? ((m >> rot) | (m << (WIN - rot))) : m;
+    int cs = -1, cq = 0;
+    long long cr = -1;
+    uint32_t cf = 0;
+    bool cex = false;
+    while (mr) {
+      const int b = __builtin_ctz(mr);
+      mr &= mr - 1;
+      const int s = (rot + b) & (WIN - 1);
+      const long long r = vload(&L.sid[s]);
+      const uint32_t fl = vload(&L.flags[s]);
+      bool exact = (fl & (F_GLOBAL | F_EXACT)) != 0;
+      int qm = 0;  // 0 no refill, 1 every open slot is refilled, 2/3 the queue length decides
+      const long long ql = vload(&S.qlen);
+      if (!(fl & F_GLOBAL) && ql > 0) {
+        qm = (ql - (r - sp) * (long long)S.capmax >= (long long)S.capmax) ? 1 : 2;
+        if (qm == 2) exact = true;
+      }
+      if (exact) {
+        if (vload(&S.seq_pos) != r) continue;
+        if ((fl & F_GLOBAL) && vload(&S.walk_pos) != vload(&S.rec_len)) continue;
+        if (qm != 0) qm = 3;
+      }
+      unsigned old = 0;
+      if (lane == 0) old = atomicAnd(&S.ready, ~(1u << s));
+      old = (unsigned)__shfl((int)old, 0);
+      if (!((old >> s) & 1u)) continue;
+      cs = s;
+      cr = r;
+      cf = fl;
+      cq = qm;
+      cex = exact;
+      break;
+    }
+    if (cs < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    lds_fence();
+    if (lane == 0) atomicAdd(&S.busy_exe, 1);
+    const unsigned long long t0 = mclk();
+    if (cf & F_GLOBAL) {
+      exe_global<LW>(D, L, P, cs, cr);
+      if (lane == 0) S.prof[9]++;
+    } else if (!exe_local<LW>(D, L, P, cs, cr, cq, cex)) {
+      if (lane == 0) {
+        atomicOr(&L.flags[cs], F_EXACT);
+        atomicOr(&S.ready, 1u << cs);
+        S.prof[10]++;
+      }
+    }
+    if (lane == 0) {
+      atomicAdd(&S.prof[5], mclk() - t0);
+      atomicSub(&S.busy_exe, 1);
+    }
+  }
+}
+
+// ======================================================================== kernel
+// all threads: worker state between the engine's global arrays and the stream layout
+template <bool LW>
+__device__ void workers_io(const Dev& D, const WPtr& P, bool load) {
+  for (int c = threadIdx.x; c < D.W; c += blockDim.x) {
+    if (load) {
+      P.nproc[c] = D.w_nproc[c];
+      P.nthreads[c] = (uint16_t)D.w_nthreads[c];
+      P.cap[c] = (uint16_t)D.w_cap[c];
+      const int n = D.w_plen[c];
+      P.plen[c] = (uint32_t)n;
+      for (int i = 0; i < PMW; i++) {
+        P.pfx[(size_t)c * PMW + i] = (uint16_t)(i < n ? D.w_pfx[(size_t)c * PMAX + i] : 0);
+        P.pcnt[(size_t)c * PMW + i] = (uint16_t)(i < n ? D.w_pcnt[(size_t)c * PMAX + i] : 0);
+      }
+      P.netocc[c] = D.w_netocc[c];
+      P.nbytes[c] = D.w_nbytes[c];
+      P.mask[c] = 0;
+      P.wflags[c] = D.w_flags[c] & (WF_IDLE | WF_SAT);
+      // needs_what: the stream layout persists in gw_needs (the engine's lines stay unused)
+      for (int i = 0; i < NLW; i++) P.needs[(size_t)c * NLW + i] = D.gw_needs_saved[(size_t)c * NLW + i];
+    } else {
+      D.w_nproc[c] = P.nproc[c];
+      const int n = P.plen[c] & 0xff;
+      D.w_plen[c] = n;
+      for (int i = 0; i < PMAX; i++) {
+        D.w_pfx[(size_t)c * PMAX + i] = i < n && i < PMW ? P.pfx[(size_t)c * PMW + i] : 0;
+        D.w_pcnt[(size_t)c * PMAX + i] = i < n && i < PMW ? P.pcnt[(size_t)c * PMW + i] : 0;
+      }
+      D.w_netocc[c] = P.netocc[c];
+      D.w_nbytes[c] = P.nbytes[c];
+      const int slots = D.sat_inf ? 0 : (int)P.cap[c] - P.nproc[c];
+      const bool itc = D.sat_inf || slots > 0;
+      D.w_flags[c] = P.wflags[c] | (itc ? WF_ITC : 0);
+      D.w_itcslots[c] = itc ? slots : 0;
+      for (int i = 0; i < NLW; i++) D.gw_needs_saved[(size_t)c * NLW + i] = P.needs[(size_t)c * NLW + i];
+    }
+  }
+}
+
+template <bool LW>
+__global__ void __launch_bounds__(CTA) k_stream(const Dev* __restrict__ Dp, long long max_rounds, int snaps) {
+  const Dev& D = *Dp;
+  __shared__ SLds L;
+  SCtl& S = L.c;
+  const WPtr P = wptr<LW>(D);
+  Ctl* c = D.ctl;
+  Pos* pos = D.pos;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // ------------------------------------------------------------------ set-up
+  workers_io<LW>(D, P, true);
+  for (int i = tid; i < WIN * NE; i += blockDim.x) (&L.desc[0][0])[i] = make_uint4(0, 0, 0, 0);
+  if (tid < WIN) {
+    L.done_tag[tid] = -1;
+    L.pred[tid] = BIG;
+    L.flags[tid] = 0;
+    L.ntouch[tid] = 0;
+  }
+  // run_id / holder of the placements this engine has not sequenced (update_graph's)
+  for (long long i = pos->runid_upto + tid; i < (long long)c->n_placed; i += blockDim.x) {
+    const int tk = D.pl_task[i];
+    D.run_id[tk] = (int32_t)i;
+    D.holder_of[tk] = D.pl_worker[i];
+  }
+  if (tid == 0) {
+    S.stop = 0;
+    S.error = 0;
+    S.err_task = -1;
+    S.global_pending = 0;
+    S.busy_exe = 0;
+    S.ready = 0;
+    S.seq_pos = pos->seq;
+    S.log_len = (long long)c->n_placed;
+    S.rec_len = pos->rec_len;
+    S.walk_pos = pos->walk;
+    S.bld_pos = pos->bld;
+    S.pre_pos = pos->pre;
+    S.reg_pos = pos->reg;
+    S.qhead = c->qhead;
+    S.qlen = c->qlen;
+    S.n_tasks = c->n_tasks;
+    S.round_end = pos->round_end >= 0 ? pos->round_end : (long long)c->n_placed;
+    S.rounds_left = max_rounds > 0 ? max_rounds : -1;
+    S.prev_placed = pos->round_end >= 0 ? pos->prev_placed : (long long)c->n_placed;
+    S.rounds_nonempty = c->rounds_nonempty;
+    S.snaps = snaps;
+    S.reg_limit = (snaps || max_rounds > 0) ? S.round_end : (1ll << 62);
+    S.g_plen = min(c->g_plen, PD);
+    for (int i = 0; i < PD; i++) {
+      S.g_pfx[i] = i < c->g_plen ? c->g_pfx[i] : 0;
+      S.g_pcnt[i] = i < c->g_plen ? c->g_pcnt[i] : 0;
+    }
+    S.g_netocc = c->g_netocc;
+    for (int i = 0; i < PD; i++) S.wdur[i] = i < D.P ? D.pdur_walk[i] : -1.0;
+    S.n_idle = c->n_idle;
+    S.n_sat = c->n_sat;
+    for (int i = 0; i < 16; i++) S.prof[i] = 0;
+    S.capmax = 1;
+    S.inv_ok = 1;
+    S.q_anon = 1;
+    S.q_prefix = 0;
+  }
+  __syncthreads();
+  // queue metadata and the refill invariant (block reductions)
+  {
+    __shared__ int s_open, s_bad, s_cap;
+    if (tid == 0) {
+      s_open = 0;
+      s_bad = 0;
+      s_cap = 1;
+    }
+    __syncthreads();
+    for (int w = tid; w < D.W; w += blockDim.x) {
+      if (!D.sat_inf && (int)P.cap[w] - P.nproc[w] > 0) atomicOr(&s_open, 1);
+      atomicMax(&s_cap, (int)P.cap[w]);
+    }
+    const int p0 = S.qlen > 0 ? D.prefix[D.qarr[S.qhead]] : 0;
+    for (long long i = S.qhead + tid; i < S.qhead + S.qlen; i += blockDim.x) {
+      const int q = D.qarr[i];
+      if (D.prefix[q] != p0 || D.dep_ptr[q + 1] > D.dep_ptr[q]) atomicOr(&s_bad, 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      S.capmax = s_cap;
+      S.inv_ok = (S.qlen == 0 || !s_open) ? 1 : 0;
+      S.q_anon = s_bad ? 0 : 1;
+      S.q_prefix = p0;
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  // ------------------------------------------------------------------- roles
+  long long round_start = pos->round_start_saved;
+  if (wave == 0) {
+    if (pos->round_end < 0) round_start = 0;
+    role_seq<LW>(D, L, P, round_start);
+  } else if (wave == 1) {
+    role_bld(D, L);
+  } else if (wave == 2) {
+    role_pre(D, L);
+  } else if (wave == 3) {
+    role_reg<LW>(D, L, P);
+  } else if (wave == 4) {
+    role_wlk<LW>(D, L, P);
+  } else {
+    role_exe<LW>(D, L, P);
+  }
+  __threadfence_block();
+  __syncthreads();
+  // --------------------------------------------------------------- write-back
+  workers_io<LW>(D, P, false);
+  __shared__ long long s_itc, s_slots;
+  if (tid == 0) {
+    s_itc = 0;
+    s_slots = 0;
+  }
+  __syncthreads();
+  for (int w = tid; w < D.W; w += blockDim.x) {
+    const int slots = D.sat_inf ? 0 : (int)P.cap[w] - P.nproc[w];
+    if (D.sat_inf || slots > 0) {
+      atomicAdd((unsigned long long*)&s_itc, 1ull);
+      atomicAdd((unsigned long long*)&s_slots, (unsigned long long)(long long)(D.sat_inf ? 0 : slots));
+    }
+  }
+  __syncthreads();
+  if (wave == 0 && lane == 0) {
+    c->n_placed = (unsigned long long)S.log_len;
+    c->qhead = S.qhead;
+    c->qlen = S.qlen;
+    c->n_tasks = S.n_tasks;
+    c->n_itc = s_itc;
+    c->itc_slots = s_slots;
+    c->rounds_nonempty = S.rounds_nonempty;
+    c->g_plen = S.g_plen;
+    for (int i = 0; i < PD; i++) {
+      c->g_pfx[i] = S.g_pfx[i];
+      c->g_pcnt[i] = S.g_pcnt[i];
+    }
+    c->g_netocc = S.g_netocc;
+    c->n_idle = S.n_idle;
+    c->n_sat = S.n_sat;
+    for (int i = 0; i < PD && i < D.P; i++) D.pdur_walk[i] = S.wdur[i];
+    if (S.error && !c->error) {
+      c->error = S.error;
+      c->err_task = S.err_task;
+    }
+    for (int i = 0; i < 16; i++) c->prof2[i] = S.prof[i];
+    pos->seq = S.seq_pos;
+    pos->bld = S.bld_pos;
+    pos->pre = S.pre_pos;
+    pos->reg = S.reg_pos;
+    pos->rec_len = S.rec_len;
+    pos->walk = S.walk_pos;
+    pos->runid_upto = S.log_len;
+    pos->round_end = S.round_end;
+    pos->round_start_saved = round_start;
+    pos->prev_placed = S.prev_placed;
+    c->rec_used = 0;
+    c->walk_pos = 0;
+  }
+}
+
+}  // namespace st
+}  // namespace dgp

@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -23,6 +24,7 @@
 
 #include "../../include/dgplace.h"
 #include "dgp_device.h"
+#include "dgp_stream.h"
 
 // =================================================================== host side
 
@@ -46,6 +48,7 @@ struct dgp_engine {
   int32_t* d_batch = nullptr;
   int64_t batch_cap = 0;
   int rounds_per_sync = 16;
+  bool stream_used = false;  // the stream engine ran: the round-kernel path is no longer valid
   // timing: (start, stop) event pairs recorded around launches, resolved lazily
   bool timing = false;
   double kms[4] = {0, 0, 0, 0};
@@ -97,10 +100,13 @@ int check_device_error(dgp_engine* e, dgp::Ctl* out = nullptr) {
     static const char* names[] = {"none", "worker prefix dict overflow (PMAX)", "task without candidates",
                                   "inconsistent task state", "queue underflow", "candidate pool overflow",
                                   "global prefix dict overflow", "record log overflow", "staging overflow",
-                                  "no worker", "needs_what line overflow"};
+                                  "no worker", "needs_what line overflow", "prefix dict overflow (stream)",
+                                  "watchdog: the stream engine made no progress", "queue", "needs_what inconsistent",
+                                  "record log overflow (stream)", "task without candidates (stream)",
+                                  "descriptor ring out of order"};
     char buf[200];
     snprintf(buf, sizeof buf, "device engine error %d (%s) at task %d", c.error,
-             (c.error >= 0 && c.error <= 10) ? names[c.error] : "?", c.err_task);
+             (c.error >= 0 && c.error <= 17) ? names[c.error] : "?", c.err_task);
     return fail(e, DGP_E_DEVICE, buf);
   }
   return 0;
@@ -149,6 +155,11 @@ int timed_launch(dgp_engine* e, int kid, F&& launch) {
 
 // publish the host-side Dev (pointers, sizes, config) to the device copies the kernels read
 int sync_dev(dgp_engine* e) {
+  const char* dbg = getenv("DGP_STREAM_DEBUG");
+  e->D.dbg = dbg ? atoi(dbg) : 0;
+  const char* dt = getenv("DGP_DEBUG_TASK");
+  e->D.dbg_task = dt ? atoi(dt) : -2;
+  if (!e->D.dbgbuf) HIPCHK(e, hipMalloc((void**)&e->D.dbgbuf, 64 * 8 * sizeof(double)));
   dgp::Dev h[2] = {e->D, e->D};
   h[0].lds_workers = 0;
   h[1].lds_workers = e->D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
@@ -221,6 +232,27 @@ dgp_engine* dgp_create(int device) {
     (void)hipStreamDestroy(e->stream);
     delete e;
     return nullptr;
+  }
+  {
+    namespace S = dgp::st;
+    const size_t st = (size_t)S::WIN * S::PLC;
+    int rc = 0;
+    rc |= dalloc(e, &e->D.desc, (size_t)S::DR * S::NE, e->allocs);
+    rc |= dalloc(e, &e->D.desc_tag, (size_t)S::DR, e->allocs);
+    rc |= dalloc(e, &e->D.s2_task, st, e->allocs);
+    rc |= dalloc(e, &e->D.s2_worker, st, e->allocs);
+    rc |= dalloc(e, &e->D.s2_comm, st, e->allocs);
+    rc |= dalloc(e, &e->D.s2_start, st, e->allocs);
+    rc |= dalloc(e, &e->D.s2_wsnb, st, e->allocs);
+    rc |= dalloc(e, &e->D.s2_route, st, e->allocs);
+    rc |= dalloc(e, &e->D.srec, st, e->allocs);
+    rc |= dalloc(e, &e->D.pos, 1, e->allocs);
+    if (rc) {
+      free_list(e->allocs);
+      (void)hipStreamDestroy(e->stream);
+      delete e;
+      return nullptr;
+    }
   }
   e->D.ctl = e->ctl;
   e->D.bandwidth = 100000000;
@@ -296,6 +328,23 @@ int dgp_set_workers(dgp_engine* e, int32_t n_workers, const int32_t* nthreads) {
   rc |= dalloc(e, &D.w_itcslots, n_workers, e->allocs);
   rc |= dalloc(e, &D.w_lastcheck, n_workers, e->allocs);
   rc |= dalloc(e, &D.w_needs, (size_t)n_workers * dgp::NEEDS_W, e->allocs);
+  {
+    namespace S = dgp::st;
+    const size_t W = n_workers;
+    rc |= dalloc(e, &D.gw_nproc, W, e->allocs);
+    rc |= dalloc(e, &D.gw_nthreads, W, e->allocs);
+    rc |= dalloc(e, &D.gw_cap, W, e->allocs);
+    rc |= dalloc(e, &D.gw_plen, W, e->allocs);
+    rc |= dalloc(e, &D.gw_pfx, W * S::PMW, e->allocs);
+    rc |= dalloc(e, &D.gw_pcnt, W * S::PMW, e->allocs);
+    rc |= dalloc(e, &D.gw_netocc, W, e->allocs);
+    rc |= dalloc(e, &D.gw_nbytes, W, e->allocs);
+    rc |= dalloc(e, &D.gw_mask, W, e->allocs);
+    rc |= dalloc(e, &D.gw_needs, W * S::NLW, e->allocs);
+    rc |= dalloc(e, &D.gw_wflags, W, e->allocs);
+    rc |= dalloc(e, &D.gw_needs_ext, W * S::NXW, e->allocs);
+    rc |= dalloc(e, &D.gw_needs_saved, W * S::NLW, e->allocs);
+  }
   rc |= dalloc(e, &D.t_key, 2 * (size_t)D.Wp, e->allocs);
   rc |= dalloc(e, &D.t_idx, 2 * (size_t)D.Wp, e->allocs);
   if (rc) return DGP_E_HIP;
@@ -438,6 +487,12 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
   rc |= dalloc(e, &D.st_wsnbytes, D.st_cap, L);
   rc |= dalloc(e, &D.st_route, D.st_cap, L);
   rc |= dalloc(e, &D.ready, N, L);
+  rc |= dalloc(e, &D.run_id, N, L);
+  rc |= dalloc(e, &D.holder_of, N, L);
+  rc |= dalloc(e, &D.fr_mark, N, L);
+  rc |= dalloc(e, &D.rel_mark, N, L);
+  D.rlog_cap = 2 * N + 4096;
+  rc |= dalloc(e, &D.rlog, D.rlog_cap, L);
   if (rc) return DGP_E_HIP;
   auto up = [&](const void* dst, const void* src, size_t bytes) {
     return hipMemcpy(const_cast<void*>(dst), src, bytes, hipMemcpyHostToDevice);
@@ -487,6 +542,20 @@ int dgp_reset(dgp_engine* e) {
   HIPCHK(e, hipMemsetAsync(D.ready_key, 0, N * 8, s));
   HIPCHK(e, hipMemsetAsync(D.release_key, 0, N * 8, s));
   HIPCHK(e, hipMemsetAsync(D.cand_n, 0, N * 4, s));
+  {  // stream engine
+    namespace S = dgp::st;
+    HIPCHK(e, hipMemsetAsync(D.run_id, 0xff, N * 4, s));
+    HIPCHK(e, hipMemsetAsync(D.holder_of, 0xff, N * 4, s));
+    HIPCHK(e, hipMemsetAsync(D.fr_mark, 0xff, N * 4, s));
+    HIPCHK(e, hipMemsetAsync(D.rel_mark, 0xff, N * 4, s));
+    HIPCHK(e, hipMemsetAsync(D.desc_tag, 0xff, (size_t)S::DR * 8, s));
+    HIPCHK(e, hipMemsetAsync(D.gw_needs_ext, 0, (size_t)D.W * S::NXW * 4, s));
+    HIPCHK(e, hipMemsetAsync(D.gw_needs_saved, 0, (size_t)D.W * S::NLW * 4, s));
+    S::Pos p0{};
+    p0.round_end = -1;
+    HIPCHK(e, hipMemcpyAsync(D.pos, &p0, sizeof p0, hipMemcpyHostToDevice, s));
+    e->stream_used = false;
+  }
   std::vector<double> maxexec(D.P, -1.0);
   HIPCHK(e, hipMemcpyAsync(D.pdur_cur, e->prefix_defaults.data(), D.P * 8, hipMemcpyHostToDevice, s));
   HIPCHK(e, hipMemcpyAsync(D.pdur_walk, e->prefix_defaults.data(), D.P * 8, hipMemcpyHostToDevice, s));
@@ -532,24 +601,50 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (!e->have_results) return fail(e, DGP_E_STATE, "dgp_set_task_results first");
   HIPCHK(e, hipSetDevice(e->device));
+  if (n_rounds_out) *n_rounds_out = 0;
+  if (max_rounds == 0) return 0;
   if (int rc = sync_dev(e)) return rc;
   dgp::Ctl c;
   if (int rc = check_device_error(e, &c)) return rc;
   const long long r0 = c.rounds_nonempty;
-  // every round in one persistent workgroup (k_replay); worker state in LDS when it fits
   const dgp::Dev& D = e->D;
-  const int lds_workers = D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
-  const size_t lds = (((size_t)D.W * sizeof(int) + 15) & ~(size_t)15) +
-                     (lds_workers ? (((size_t)D.W + 3) & ~(size_t)3) * dgp::LDS_WORKER_BYTES + 64 : 0);
-  if (lds > 160 * 1024) return fail(e, DGP_E_ARG, "commit LDS exceeds 160 KiB");
-  const dgp::Dev* DPC = e->d_dev + 1;
-  const int snaps = e->snap_rounds > 0 ? 1 : 0;
-  if (int rc = timed_launch(e, 2, [&] {
-        hipLaunchKernelGGL(dgp::k_replay, dim3(1), dim3(dgp::CTA), lds, e->stream, DPC, e->d_aux, (long long)max_rounds,
-                           e->d_aux + 1, snaps);
-      }))
-    return rc;
-  if (int rc = walk(e)) return rc;
+  if (D.P <= dgp::st::PD) {
+    // the stream engine: the whole replay in one persistent workgroup (dgp_stream.h)
+    const size_t lds_w = dgp::st::lds_worker_bytes(D.W);
+    const bool lw = sizeof(dgp::st::SLds) + lds_w <= 160 * 1024;
+    const int snaps = e->snap_rounds > 0 ? 1 : 0;
+    if (lw) {
+      HIPCHK(e, hipFuncSetAttribute((const void*)dgp::st::k_stream<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds_w));
+      if (int rc = timed_launch(e, 2, [&] {
+            hipLaunchKernelGGL(dgp::st::k_stream<true>, dim3(1), dim3(dgp::CTA), lds_w, e->stream, e->d_dev,
+                               (long long)max_rounds, snaps);
+          }))
+        return rc;
+    } else {
+      if (int rc = timed_launch(e, 2, [&] {
+            hipLaunchKernelGGL(dgp::st::k_stream<false>, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev,
+                               (long long)max_rounds, snaps);
+          }))
+        return rc;
+    }
+    e->stream_used = true;
+  } else {
+    // more task prefixes than the stream descriptors carry: the round-kernel engine
+    if (e->stream_used) return fail(e, DGP_E_STATE, "engine already advanced by the stream replay");
+    const int lds_workers = D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
+    const size_t lds = (((size_t)D.W * sizeof(int) + 15) & ~(size_t)15) +
+                       (lds_workers ? (((size_t)D.W + 3) & ~(size_t)3) * dgp::LDS_WORKER_BYTES + 64 : 0);
+    if (lds > 160 * 1024) return fail(e, DGP_E_ARG, "commit LDS exceeds 160 KiB");
+    const dgp::Dev* DPC = e->d_dev + 1;
+    const int snaps = e->snap_rounds > 0 ? 1 : 0;
+    if (int rc = timed_launch(e, 2, [&] {
+          hipLaunchKernelGGL(dgp::k_replay, dim3(1), dim3(dgp::CTA), lds, e->stream, DPC, e->d_aux, (long long)max_rounds,
+                             e->d_aux + 1, snaps);
+        }))
+      return rc;
+    if (int rc = walk(e)) return rc;
+  }
   if (int rc = check_device_error(e, &c)) return rc;
   if (n_rounds_out) *n_rounds_out = c.rounds_nonempty - r0;
   return 0;
@@ -558,6 +653,7 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
 int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* tasks, const int64_t* nbytes, const double* start,
                        const double* stop) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (e->stream_used) return fail(e, DGP_E_STATE, "engine already advanced by the stream replay (dgp_reset first)");
   if (n < 0 || (n > 0 && (!tasks || !nbytes || !start || !stop))) return fail(e, DGP_E_ARG, "bad batch");
   if (n == 0) return 0;
   HIPCHK(e, hipSetDevice(e->device));
@@ -675,6 +771,12 @@ int dgp_kernel_times(dgp_engine* e, double* ms, int64_t* launches, int32_t n) {
 int dgp_set_timing(dgp_engine* e, int enabled) {
   if (!e) return DGP_E_ARG;
   e->timing = enabled != 0;
+  return 0;
+}
+
+extern "C" int dgp_debug_buf(dgp_engine* e, double* out) {
+  if (!e || !e->D.dbgbuf) return DGP_E_ARG;
+  HIPCHK(e, hipMemcpy(out, e->D.dbgbuf, 64 * 8 * sizeof(double), hipMemcpyDeviceToHost));
   return 0;
 }
 
