@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libdgplace.so")
+LIB_PATH = os.environ.get("DGP_LIB") or os.path.join(PKG, "libdgplace.so")  # DGP_LIB: debugging only
 
 _P = C.c_void_p
 _i32p = C.POINTER(C.c_int32)

@@ -36,6 +36,10 @@
 namespace dgp {
 namespace st {
 
+// the engine description every stream role reads: constant memory (scalar loads, never
+// re-fetched across the roles' fences); set by the host before each launch
+__constant__ Dev c_dev;
+
 constexpr int WIN = 32;          // in-flight stimulus slots (LDS window)
 constexpr int NE = 48;           // 16-byte descriptor entries per stimulus
 constexpr int DR = 4096;         // descriptor ring (global) — how far PRE may run ahead
@@ -55,7 +59,7 @@ constexpr int E_HDR = 7;         // header entries: 0 ids, 1 sizes/counts, 2 dur
 enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8 };
 enum : int { K_COMPLETE = 1, K_PLACE = 2 };
 enum : int { SERR_NONE = 0, SERR_PREFIX = 11, SERR_WATCHDOG = 12, SERR_QUEUE = 13, SERR_NEEDS = 14,
-             SERR_REC = 15, SERR_CAND = 16, SERR_STAGE = 17 };
+             SERR_REC = 15, SERR_CAND = 16, SERR_STAGE = 17, SERR_RANGE = 18, SERR_INV = 19 };
 
 // persistent stream position (global, survives launches)
 struct Pos {
@@ -102,7 +106,7 @@ struct SCtl {
   double g_netocc;
   double wdur[PD];  // prefix EWMA as of walk_pos (raw duration_average)
   long long n_idle, n_sat;
-  unsigned long long prof[16];
+  unsigned long long prof[32];
 };
 
 // ------------------------------------------------------------------ small helpers
@@ -145,20 +149,34 @@ __device__ __forceinline__ void vstore(T* p, T v) {
 }
 
 // ------------------------------------------------------------ worker state access
-// LW: state in LDS (dynamic carve), else in the global gw_* arrays (same layout)
+// LW: state in LDS (dynamic carve, ds_* instructions), else in the global gw_* arrays
+template <bool LW>
+struct AS {
+  template <class T>
+  using P = T*;
+};
+template <>
+struct AS<true> {
+  template <class T>
+  using P = __attribute__((address_space(3))) T*;
+};
+
+template <bool LW>
 struct WPtr {
-  int32_t* nproc;
-  uint16_t* nthreads;
-  uint16_t* cap;
-  uint32_t* plen;      // low byte: dict length
-  uint16_t* pfx;       // [W][PMW]
-  uint16_t* pcnt;      // [W][PMW]
-  int64_t* netocc;
-  int64_t* nbytes;
-  uint32_t* mask;      // in-flight slots touching the worker
-  uint32_t* needs;     // [W][NLW]: (d << 8 | count), slot NLW-1 = control (1: overflow
-                       // entries in use, NL_OVF: scan mode)
-  uint8_t* wflags;     // walker's idle / saturated bits
+  template <class T>
+  using P = typename AS<LW>::template P<T>;
+  P<int32_t> nproc;
+  P<uint16_t> nthreads;
+  P<uint16_t> cap;
+  P<uint32_t> plen;    // low byte: dict length
+  P<uint16_t> pfx;     // [W][PMW]
+  P<uint16_t> pcnt;    // [W][PMW]
+  P<int64_t> netocc;
+  P<int64_t> nbytes;
+  P<uint32_t> mask;    // in-flight slots touching the worker
+  P<uint32_t> needs;   // [W][NLW]: (d << 8 | count), slot NLW-1 = control (count << 8 | 1 when
+                       // overflow entries are in use; NL_OVF: scan mode)
+  P<uint8_t> wflags;   // walker's idle / saturated bits
 };
 
 extern __shared__ __attribute__((aligned(16))) char st_smem[];
@@ -171,22 +189,23 @@ __host__ __device__ constexpr size_t lds_worker_bytes(int W) {
 }
 
 template <bool LW>
-__device__ __forceinline__ WPtr wptr(const Dev& D) {
-  WPtr p;
-  if (LW) {
+__device__ __forceinline__ WPtr<LW> wptr(const Dev& D) {
+  WPtr<LW> p;
+  using W_ = WPtr<LW>;
+  if constexpr (LW) {
     const size_t W = D.W;
-    char* b = st_smem;
-    p.nproc = (int32_t*)b;      b += al16(W * 4);
-    p.nthreads = (uint16_t*)b;  b += al16(W * 2);
-    p.cap = (uint16_t*)b;       b += al16(W * 2);
-    p.plen = (uint32_t*)b;      b += al16(W * 4);
-    p.pfx = (uint16_t*)b;       b += al16(W * PMW * 2);
-    p.pcnt = (uint16_t*)b;      b += al16(W * PMW * 2);
-    p.netocc = (int64_t*)b;     b += al16(W * 8);
-    p.nbytes = (int64_t*)b;     b += al16(W * 8);
-    p.mask = (uint32_t*)b;      b += al16(W * 4);
-    p.needs = (uint32_t*)b;     b += al16(W * NLW * 4);
-    p.wflags = (uint8_t*)b;
+    auto b = (__attribute__((address_space(3))) char*)st_smem;
+    p.nproc = (typename W_::template P<int32_t>)b;     b += al16(W * 4);
+    p.nthreads = (typename W_::template P<uint16_t>)b; b += al16(W * 2);
+    p.cap = (typename W_::template P<uint16_t>)b;      b += al16(W * 2);
+    p.plen = (typename W_::template P<uint32_t>)b;     b += al16(W * 4);
+    p.pfx = (typename W_::template P<uint16_t>)b;      b += al16(W * PMW * 2);
+    p.pcnt = (typename W_::template P<uint16_t>)b;     b += al16(W * PMW * 2);
+    p.netocc = (typename W_::template P<int64_t>)b;    b += al16(W * 8);
+    p.nbytes = (typename W_::template P<int64_t>)b;    b += al16(W * 8);
+    p.mask = (typename W_::template P<uint32_t>)b;     b += al16(W * 4);
+    p.needs = (typename W_::template P<uint32_t>)b;    b += al16(W * NLW * 4);
+    p.wflags = (typename W_::template P<uint8_t>)b;
   } else {
     p.nproc = D.gw_nproc;
     p.nthreads = D.gw_nthreads;
@@ -201,6 +220,25 @@ __device__ __forceinline__ WPtr wptr(const Dev& D) {
     p.wflags = D.gw_wflags;
   }
   return p;
+}
+
+template <class T, class U>
+__device__ __forceinline__ T ascast(U p) {
+  return (T)p;
+}
+struct alignas(16) Q4 {  // plain 16-byte word (uint4 cannot bind an LDS lvalue)
+  uint32_t x, y, z, w;
+};
+template <class PQ>
+__device__ __forceinline__ uint4 ld4(PQ q) {
+  return make_uint4(q->x, q->y, q->z, q->w);
+}
+template <class PQ>
+__device__ __forceinline__ void st4(PQ q, const uint4& u) {
+  q->x = u.x;
+  q->y = u.y;
+  q->z = u.z;
+  q->w = u.w;
 }
 
 // LDS of the stream kernel besides the worker carve
@@ -227,10 +265,11 @@ __device__ __forceinline__ double desc_durs(const uint4& e) {
 // _calc_occupancy (:1884-1903) of worker c (per lane); durv = lane p holds the resolved
 // duration of prefix p; all lanes must be active (shuffles)
 template <bool LW>
-__device__ __forceinline__ double occ_of(const WPtr& P, const Dev& D, int c, double durv) {
+__device__ __forceinline__ double occ_of(const WPtr<LW>& P, const Dev& D, int c, double durv) {
   const uint32_t n = P.plen[c] & 0xffu;
-  const uint4 pf = *reinterpret_cast<const uint4*>(P.pfx + (size_t)c * PMW);
-  const uint4 pc = *reinterpret_cast<const uint4*>(P.pcnt + (size_t)c * PMW);
+  using U4 = typename WPtr<LW>::template P<const Q4>;
+  const uint4 pf = ld4(ascast<U4>(P.pfx + (size_t)c * PMW));
+  const uint4 pc = ld4(ascast<U4>(P.pcnt + (size_t)c * PMW));
   const uint32_t pfw[4] = {pf.x, pf.y, pf.z, pf.w};
   const uint32_t pcw[4] = {pc.x, pc.y, pc.z, pc.w};
   const int nmax = wmax((int)n);
@@ -313,7 +352,7 @@ __device__ __forceinline__ double resolve_dur(const Dev& D, double d) {  // _cal
   return d < 0 ? D.unknown_duration : d;  // max_exec_time stays -1 without heartbeats
 }
 
-__device__ void serr(SCtl& S, int code, int task) {
+__device__ __attribute__((always_inline)) void serr(SCtl& S, int code, int task) {
   if (atomicCAS(&S.error, 0, code) == 0) S.err_task = task;
   vstore(&S.stop, 1);
 }
@@ -416,7 +455,7 @@ __device__ __forceinline__ double ws_total_occ(const Dev& D, const WState& g) {
 // one record: the global-count update of its sub-step, then check_idle_saturated's idle /
 // saturated part for its worker (:2949-2991, is_unoccupied :2997). All lanes, uniform.
 template <bool LW>
-__device__ __forceinline__ void ws_fold(const Dev& D, const WPtr& P, SCtl& S, WState& g, int kind, int w, int p,
+__device__ __forceinline__ void ws_fold(const Dev& D, const WPtr<LW>& P, SCtl& S, WState& g, int kind, int w, int p,
                                         long long dnet, double occ, int nproc, double dobs) {
   const int lane = lane_id();
   if (kind == K_COMPLETE) {
@@ -452,8 +491,99 @@ __device__ __forceinline__ void ws_fold(const Dev& D, const WPtr& P, SCtl& S, WS
   }
 }
 
+__device__ __forceinline__ long long wscan_incl(long long v) {
+  const int lane = lane_id();
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// fold a batch of m records (lane i holds record i). Fast path, all records at once:
+// no prefix EWMA changes value and no prefix enters / leaves the global dict in the
+// batch, so every record's total_occupancy is a prefix sum over the lanes (integer
+// counts, integer-valued network bytes: exact in any order). Otherwise one by one.
 template <bool LW>
-__device__ void role_wlk(const Dev& D, SLds& L, const WPtr& P) {
+__device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const WPtr<LW>& P, SCtl& S, WState& g,
+                                                             const SRec& rc, int m) {
+  const int lane = lane_id();
+  const bool in = lane < m;
+  const int kind = rc.kind, w = rc.w, p = rc.p, np = rc.nproc;
+  // (a) durations unchanged: every completion's EWMA result equals the current value
+  const double cur = __shfl(g.wd, p & (PD - 1));
+  const double nw = cur < 0 ? rc.dur : 0.5 * rc.dur + 0.5 * cur;
+  bool bad = in && kind == K_COMPLETE && __double_as_longlong(nw) != __double_as_longlong(cur);
+  // (b) prefix counts stay >= 1 and every record's prefix is in the dict
+  bool found = !in;
+  long long cnt_i[PD];
+  long long tot[PD];
+#pragma unroll
+  for (int k = 0; k < PD; k++) {
+    cnt_i[k] = 0;
+    tot[k] = 0;
+    if (k >= g.n) continue;
+    const long long dl = (in && p == g.pf[k]) ? (kind == K_COMPLETE ? -1 : 1) : 0;
+    if (in && p == g.pf[k]) found = true;
+    const long long inc = wscan_incl(dl);
+    cnt_i[k] = g.cnt[k] + inc;
+    tot[k] = __shfl(inc, 63);
+    if (in && cnt_i[k] < 1) bad = true;
+  }
+  if (!found) bad = true;
+  if (ballot(bad)) {
+    for (int i = 0; i < m; i++) {
+      const double occ = mkd(rlu(dlo(rc.occ), i), rlu(dhi(rc.occ), i));
+      const long long dnet = mk64(rlu(lo32(rc.dnet), i), rlu(hi32(rc.dnet), i));
+      const double dob = mkd(rlu(dlo(rc.dur), i), rlu(dhi(rc.dur), i));
+      ws_fold<LW>(D, P, S, g, rl(kind, i), rl(w, i), rl(p, i), dnet, occ, rl(np, i), dob);
+    }
+    return;
+  }
+  const long long dn_inc = wscan_incl(in ? (long long)rc.dnet : 0);
+  const double netocc_i = g.netocc + (double)dn_inc;
+  const double rv = resolve_dur(D, g.wd);
+  double tocc = 0.0;
+#pragma unroll
+  for (int k = 0; k < PD; k++) {
+    const double dv = __shfl(rv, g.pf[k] & (PD - 1));
+    if (k < g.n) tocc += dv * (double)cnt_i[k];
+  }
+  tocc = tocc + netocc_i / (double)D.bandwidth;
+  // check_idle_saturated's idle / saturated part for the record's worker
+  const long long nt = in ? (long long)P.nthreads[w] : 1;
+  const long long pp = np;
+  const double avg = tocc / (double)D.total_nthreads;
+  bool idle = pp < nt || rc.occ < (double)nt * avg / 2;
+  bool sat = false;
+  if (!idle && pp > nt) {
+    const double pending = rc.occ * (double)(pp - nt) / (double)(pp * nt);
+    sat = 0.4 < pending && pending > 1.9 * avg;
+  }
+  // the worker's last record in the batch decides its flags
+  bool last = in;
+  for (int j = 1; j < m; j++) {
+    const int wj = rl(w, j);
+    if (lane < j && w == wj) last = false;
+  }
+  int di = 0, ds = 0;
+  if (last) {
+    const uint8_t fo = P.wflags[w];
+    const uint8_t fn = (idle ? WF_IDLE : 0) | (sat ? WF_SAT : 0);
+    di = (idle ? 1 : 0) - ((fo & WF_IDLE) ? 1 : 0);
+    ds = (sat ? 1 : 0) - ((fo & WF_SAT) ? 1 : 0);
+    if (fo != fn) P.wflags[w] = fn;
+  }
+  g.n_idle += wsum(di);
+  g.n_sat += wsum(ds);
+#pragma unroll
+  for (int k = 0; k < PD; k++)
+    if (k < g.n) g.cnt[k] += tot[k];
+  g.netocc += (double)__shfl(dn_inc, 63);
+}
+
+template <bool LW>
+__device__ __attribute__((always_inline)) void role_wlk(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
   const int lane = lane_id();
   WState g;
@@ -462,7 +592,7 @@ __device__ void role_wlk(const Dev& D, SLds& L, const WPtr& P) {
     const long long rl_ = vload(&S.rec_len);
     if (wp >= rl_) {
       if (vload(&S.stop)) break;
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(4);
       continue;
     }
     lds_fence();
@@ -471,16 +601,7 @@ __device__ void role_wlk(const Dev& D, SLds& L, const WPtr& P) {
     if (lane < m) rc = D.rlog[wp + lane];
     ws_load(S, g);
     const unsigned long long t0 = mclk();
-    for (int i = 0; i < m; i++) {
-      const int kind = rl(rc.kind, i);
-      const int w = rl(rc.w, i);
-      const int p = rl(rc.p, i);
-      const long long dnet = mk64(rlu(lo32(rc.dnet), i), rlu(hi32(rc.dnet), i));
-      const double occ = mkd(rlu(dlo(rc.occ), i), rlu(dhi(rc.occ), i));
-      const int np = rl(rc.nproc, i);
-      const double dob = mkd(rlu(dlo(rc.dur), i), rlu(dhi(rc.dur), i));
-      ws_fold<LW>(D, P, S, g, kind, w, p, dnet, occ, np, dob);
-    }
+    ws_fold_batch<LW>(D, P, S, g, rc, m);
     ws_store(S, g);
     lds_fence();
     if (lane == 0) {
@@ -492,7 +613,7 @@ __device__ void role_wlk(const Dev& D, SLds& L, const WPtr& P) {
 
 // ====================================================================== sequencer
 template <bool LW>
-__device__ void snapshot(const Dev& D, SLds& L, const WPtr& P) {
+__device__ __attribute__((always_inline)) void snapshot(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
   const int lane = lane_id();
   const long long idx = S.rounds_nonempty;
@@ -520,7 +641,7 @@ __device__ void snapshot(const Dev& D, SLds& L, const WPtr& P) {
 // every stimulus of the round is sequenced: count it, snapshot, open the next round.
 // Returns true when the replay stops here.
 template <bool LW>
-__device__ bool round_end_step(const Dev& D, SLds& L, const WPtr& P, long long& round_start) {
+__device__ __attribute__((always_inline)) bool round_end_step(const Dev& D, SLds& L, const WPtr<LW>& P, long long& round_start) {
   SCtl& S = L.c;
   const int lane = lane_id();
   if (S.round_end > round_start) {
@@ -563,7 +684,7 @@ __device__ bool round_end_step(const Dev& D, SLds& L, const WPtr& P, long long& 
 }
 
 template <bool LW>
-__device__ void role_seq(const Dev& D, SLds& L, const WPtr& P, long long& round_start) {
+__device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, const WPtr<LW>& P, long long& round_start) {
   SCtl& S = L.c;
   const int lane = lane_id();
   unsigned long long t_idle = mclk();
@@ -589,6 +710,19 @@ __device__ void role_seq(const Dev& D, SLds& L, const WPtr& P, long long& round_
       continue;
     }
     lds_fence();
+    {  // invariants of the control block (cheap; a violation names the field)
+      const long long rp = vload(&S.reg_pos);
+      const int be = vload(&S.busy_exe), gp = vload(&S.global_pending);
+      int bad = 0;
+      if (rp < sp || rp > sp + WIN) bad = 1;
+      if (be < 0 || be > 16) bad = 2;
+      if (gp < 0 || gp > 1) bad = 3;
+      if (S.qlen < 0 || S.qhead < 0) bad = 4;
+      if (bad) {
+        serr(S, SERR_INV, bad * 100000000 + (int)sp);
+        break;
+      }
+    }
     const unsigned long long t0 = mclk();
     const int s = (int)(r & (WIN - 1));
     int npl = 0, nrec = 0, npop = 0;
@@ -598,6 +732,10 @@ __device__ void role_seq(const Dev& D, SLds& L, const WPtr& P, long long& round_
       nrec = L.nrec[s];
       npop = L.npops[s];
       direct = (L.flags[s] & F_GLOBAL) != 0;
+    }
+    if (ballot(lane < m && (npl < 0 || nrec < 0 || npop < 0 || npop > npl || (!direct && (npl > PLC || nrec > PLC))))) {
+      serr(S, SERR_INV, 500000000 + (int)sp);
+      break;
     }
     int ipl = npl, irc = nrec, ipo = npop;
     for (int o = 1; o < 64; o <<= 1) {
@@ -645,62 +783,46 @@ __device__ void role_seq(const Dev& D, SLds& L, const WPtr& P, long long& round_
       S.prof[8] += 1;
     }
     lds_fence();
-    if (lane == 0) vstore(&S.seq_pos, sp + m);
+    if (lane == 0) {
+      vstore(&S.seq_pos, sp + m);
+
+    }
     t_idle = mclk();
   }
 }
 
 // ======================================================================= builder
-__device__ void role_bld(const Dev& D, SLds& L) {
-  SCtl& S = L.c;
-  const int lane = lane_id();
-  while (true) {
-    if (vload(&S.stop)) break;
-    const long long a = S.bld_pos;
-    const long long e = min(a + 64, vload(&S.log_len));
-    if (e <= a) {
-      __builtin_amdgcn_s_sleep(2);
-      continue;
+// completions [a, e) (one per lane): the waiting_on / waiters decrements
+__device__ __attribute__((always_inline)) void bld_range(const Dev& D, long long a, long long e) {
+  const long long r = a + lane_id();
+  if (r >= e) return;
+  const int t = D.pl_task[r];
+  const int w = D.pl_worker[r];
+  // the replica this completion creates (who_has, :3148)
+  atomicOr(&D.holders[(size_t)t * D.WB + (w >> 6)], 1ull << (w & 63));
+  const int64_t f0 = D.dpt_ptr[t], f1 = D.dpt_ptr[t + 1];
+  for (int64_t k = f0; k < f1; k++) {  // waiting_on.discard (:3298-3307)
+    const int x = D.dpt_idx[k];
+    if (atomicSub(&D.remaining[x], 1) == 1) {
+      int s = -1;  // the stimulus that empties waiting_on: the dependency completed last
+      for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++) s = max(s, D.run_id[D.dep_idx[q]]);
+      D.fr_mark[x] = s;
     }
-    lds_fence();
-    const unsigned long long t0 = mclk();
-    const long long r = a + lane;
-    if (r < e) {
-      const int t = D.pl_task[r];
-      const int w = D.pl_worker[r];
-      // the replica this completion creates (who_has, :3148)
-      atomicOr(&D.holders[(size_t)t * D.WB + (w >> 6)], 1ull << (w & 63));
-      const int64_t f0 = D.dpt_ptr[t], f1 = D.dpt_ptr[t + 1];
-      for (int64_t k = f0; k < f1; k++) {  // waiting_on.discard (:3298-3307)
-        const int x = D.dpt_idx[k];
-        if (atomicSub(&D.remaining[x], 1) == 1) {
-          int s = -1;  // the stimulus that empties waiting_on: the dependency completed last
-          for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++) s = max(s, D.run_id[D.dep_idx[q]]);
-          D.fr_mark[x] = s;
-        }
-      }
-      const int64_t k0 = D.dep_ptr[t], k1 = D.dep_ptr[t + 1];
-      for (int64_t k = k0; k < k1; k++) {  // waiters.discard -> release (:3309-3314)
-        const int d = D.dep_idx[k];
-        if (atomicSub(&D.waiters[d], 1) == 1 && !(D.tflags[d] & TF_WANTED)) {
-          int s = -1;
-          for (int64_t q = D.dpt_ptr[d]; q < D.dpt_ptr[d + 1]; q++) s = max(s, D.run_id[D.dpt_idx[q]]);
-          D.rel_mark[d] = s;
-        }
-      }
-    }
-    __threadfence_block();
-    wbar();
-    if (lane == 0) {
-      S.prof[1] += mclk() - t0;
-      vstore(&S.bld_pos, e);
+  }
+  const int64_t k0 = D.dep_ptr[t], k1 = D.dep_ptr[t + 1];
+  for (int64_t k = k0; k < k1; k++) {  // waiters.discard -> release (:3309-3314)
+    const int d = D.dep_idx[k];
+    if (atomicSub(&D.waiters[d], 1) == 1 && !(D.tflags[d] & TF_WANTED)) {
+      int s = -1;
+      for (int64_t q = D.dpt_ptr[d]; q < D.dpt_ptr[d + 1]; q++) s = max(s, D.run_id[D.dpt_idx[q]]);
+      D.rel_mark[d] = s;
     }
   }
 }
 
 // ==================================================================== prefetcher
 // descriptor of stimulus r (one lane): see E_HDR for the header layout
-__device__ void build_desc(const Dev& D, long long r) {
+__device__ __attribute__((always_inline)) void build_desc(const Dev& D, long long r) {
   uint4* E = D.desc + (size_t)(r & (DR - 1)) * NE;
   const int t = D.pl_task[r];
   const int w = D.pl_worker[r];
@@ -759,56 +881,80 @@ __device__ void build_desc(const Dev& D, long long r) {
   E[2] = make_uint4(dlo(dobs), dhi(dobs), 0u, 0u);
 }
 
-__device__ void role_pre(const Dev& D, SLds& L) {
+// ========================================================== builder / prefetcher
+// One wave each, in the engine workgroup (every hand-off stays on this CU: workgroup-scope
+// LDS positions, no cross-CU visibility to manage). Each takes the next range of up to 64
+// stimuli (one per lane) below its bound: BLD below the log length, PRE below BLD and
+// the descriptor ring.
+template <int KIND>  // 0 BLD, 1 PRE
+__device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L) {
   SCtl& S = L.c;
   const int lane = lane_id();
   while (true) {
     if (vload(&S.stop)) break;
-    const long long a = S.pre_pos;
-    const long long e = min(min(a + 64, vload(&S.bld_pos)), vload(&S.seq_pos) + DR);
+    const long long a = KIND == 0 ? S.bld_pos : S.pre_pos;
+    const long long hi = KIND == 0 ? vload(&S.log_len) : min(vload(&S.bld_pos), vload(&S.seq_pos) + DR);
+    const long long e = min(a + 64, hi);
     if (e <= a) {
       __builtin_amdgcn_s_sleep(2);
       continue;
     }
     lds_fence();
     const unsigned long long t0 = mclk();
-    const long long r = a + lane;
-    if (r < e) build_desc(D, r);
-    __threadfence_block();
-    if (r < e) D.desc_tag[r & (DR - 1)] = r + 1;
+    if (KIND == 0) {
+      bld_range(D, a, e);
+    } else {
+      const long long r = a + lane;
+      if (r < e) build_desc(D, r);
+    }
     __threadfence_block();
     wbar();
     if (lane == 0) {
-      S.prof[2] += mclk() - t0;
-      vstore(&S.pre_pos, e);
+      S.prof[KIND == 0 ? 1 : 2] += mclk() - t0;
+      S.prof[KIND == 0 ? 6 : 7] += 1;
+      vstore(KIND == 0 ? &S.bld_pos : &S.pre_pos, e);
     }
   }
 }
 
 // ===================================================================== registrar
 template <bool LW>
-__device__ void role_reg(const Dev& D, SLds& L, const WPtr& P) {
+__device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
   const int lane = lane_id();
   double dur = lane < D.P ? D.pdur_cur[lane] : -1.0;  // lane p: duration_average as of reg_pos
   unsigned long long t_idle = mclk();
+  constexpr int RB = 4;  // descriptors fetched per global round trip
+  uint4 EB[RB];
+  long long eb_first = -1;
+  int eb_n = 0;
+  long long pre = 0;  // cached PRE watermark: an agent-scope acquire only when exhausted
   while (true) {
     if (vload(&S.stop)) break;
     const long long r = S.reg_pos;
-    const long long lim = min(min(vload(&S.pre_pos), vload(&S.reg_limit)), vload(&S.seq_pos) + WIN);
+    if (r >= pre) pre = vload(&S.pre_pos);
+    const long long lim = min(min(pre, vload(&S.reg_limit)), vload(&S.seq_pos) + WIN);
     if (r >= lim || vload(&S.global_pending)) {
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
     lds_fence();
     const unsigned long long t0 = mclk();
-    const int s = (int)(r & (WIN - 1));
-    uint4 E = make_uint4(0, 0, 0, 0);
-    if (lane < NE) E = D.desc[(size_t)(r & (DR - 1)) * NE + lane];
-    if (D.desc_tag[r & (DR - 1)] != r + 1) {
-      serr(S, SERR_STAGE, (int)r);
-      break;
+    if (!(eb_first >= 0 && r >= eb_first && r < eb_first + eb_n)) {
+      // the descriptors of up to RB consecutive prefetched stimuli, one round trip
+      eb_first = r;
+      eb_n = (int)min((long long)RB, pre - r);
+#pragma unroll
+      for (int b = 0; b < RB; b++)
+        EB[b] = (lane < NE && b < eb_n) ? D.desc[(size_t)((r + b) & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
     }
+    uint4 E = EB[0];
+#pragma unroll
+    for (int b = 1; b < RB; b++)
+      if (r - eb_first == b) E = EB[b];
+    const int s = (int)(r & (WIN - 1));
+    unsigned long long tq = mclk();
+    if (lane == 0) S.prof[17] += tq - t0;
     // TaskPrefix.add_duration (:977-985) of the completing task's prefix
     const int p = rl((int)E.z, 0);
     const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
@@ -840,8 +986,23 @@ __device__ void role_reg(const Dev& D, SLds& L, const WPtr& P) {
       int off = E_HDR + kt + nrel;
       for (int j = 0; j < nf; j++) {
         const int kx = rl((int)E.z, off) & 0xff;
-        if (lane > off && lane <= off + kx) tw = (int)E.y;
+        if (lane > off && lane <= off + kx) tw = (int)E.y < 0 ? -2 : (int)E.y;
         off += 1 + kx;
+      }
+      if (lane >= E_HDR + kt && lane < E_HDR + kt + nrel && (int)E.x < 0) tw = -2;
+      if (ballot(tw >= D.W || (lane == 0 && w < 0) || (tw < -1))) {
+        if (D.dbgbuf) {  // post-mortem: the descriptor as registered, and where it came from
+          D.dbgbuf[lane * 8 + 0] = (double)(int)E.x;
+          D.dbgbuf[lane * 8 + 1] = (double)(int)E.y;
+          D.dbgbuf[lane * 8 + 2] = (double)(int)E.z;
+          D.dbgbuf[lane * 8 + 3] = (double)(int)E.w;
+          D.dbgbuf[lane * 8 + 4] = (double)tw;
+          D.dbgbuf[lane * 8 + 5] = (double)r;
+          D.dbgbuf[lane * 8 + 6] = (double)eb_first;
+          D.dbgbuf[lane * 8 + 7] = (double)pre;
+        }
+        serr(S, SERR_RANGE, (int)r);
+        break;
       }
       keep = tw >= 0;
       unsigned long long rem = ballot(keep);
@@ -866,18 +1027,24 @@ __device__ void role_reg(const Dev& D, SLds& L, const WPtr& P) {
       L.sid[s] = r;
     }
     lds_fence();
+    {
+      const unsigned long long n = mclk();
+      if (lane == 0) S.prof[18] += n - tq;
+      tq = n;
+    }
     const unsigned bit = 1u << s;
     int cnt = 0;
     if (flags & F_TOUCHALL) {
-      for (int c = lane; c < D.W; c += 64) cnt += __builtin_popcount(atomicOr(&P.mask[c], bit) & ~bit);
+      for (int c = lane; c < D.W; c += 64) cnt += __builtin_popcount(__hip_atomic_fetch_or(&P.mask[c], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
     } else if (keep) {
-      cnt = __builtin_popcount(atomicOr(&P.mask[tw], bit) & ~bit);
+      cnt = __builtin_popcount(__hip_atomic_fetch_or(&P.mask[tw], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
     }
     const int tot = wsum(cnt);
     if (lane == 0) {
       const int old = atomicAdd(&L.pred[s], tot - BIG);
       if (old + tot - BIG == 0) atomicOr(&S.ready, bit);
       if (flags & F_GLOBAL) vstore(&S.global_pending, 1);
+      S.prof[19] += mclk() - tq;
       S.prof[3] += mclk() - t0;
       vstore(&S.reg_pos, r + 1);
     }
@@ -901,18 +1068,18 @@ __device__ __forceinline__ bool st_needed_elsewhere(const Dev& D, int d, int w, 
 }
 
 template <bool LW>
-__device__ __forceinline__ uint32_t line_load(const WPtr& P, int c) {
+__device__ __forceinline__ uint32_t line_load(const WPtr<LW>& P, int c) {
   return lane_id() < NLW ? P.needs[(size_t)c * NLW + lane_id()] : 0u;
 }
 template <bool LW>
-__device__ __forceinline__ void line_store(const WPtr& P, int c, uint32_t nl) {
+__device__ __forceinline__ void line_store(const WPtr<LW>& P, int c, uint32_t nl) {
   if (lane_id() < NLW) P.needs[(size_t)c * NLW + lane_id()] = nl;
 }
 __device__ __forceinline__ int line_used(uint32_t nl) { return __builtin_popcountll(ballot(lane_id() < NLW - 1 && nl != 0)); }
 
 // _dec_needs_replica for dependency d (held elsewhere) of the task leaving worker c
 // (returns the bytes c no longer needs)
-__device__ int64_t needs_dec(const Dev& D, SCtl& S, int c, uint32_t& nl, int d, int64_t nb, int except) {
+__device__ __attribute__((always_inline)) int64_t needs_dec(const Dev& D, SCtl& S, int c, uint32_t& nl, int d, int64_t nb, int except) {
   const int lane = lane_id();
   const uint32_t ctl = __shfl(nl, NLW - 1);
   if (ctl == NL_OVF) return st_needed_elsewhere(D, d, c, except) ? 0 : nb;
@@ -946,7 +1113,7 @@ __device__ int64_t needs_dec(const Dev& D, SCtl& S, int c, uint32_t& nl, int d, 
 
 // _inc_needs_replica for dependency d (not held by c) of task `except` placed on c
 // (returns the bytes c newly needs)
-__device__ int64_t needs_inc(const Dev& D, SCtl& S, int c, uint32_t& nl, int d, int64_t nb, int except) {
+__device__ __attribute__((always_inline)) int64_t needs_inc(const Dev& D, SCtl& S, int c, uint32_t& nl, int d, int64_t nb, int except) {
   const int lane = lane_id();
   const uint32_t ctl = __shfl(nl, NLW - 1);
   if (ctl == NL_OVF) return st_needed_elsewhere(D, d, c, except) ? 0 : nb;
@@ -998,7 +1165,7 @@ __device__ int64_t needs_inc(const Dev& D, SCtl& S, int c, uint32_t& nl, int d, 
 }
 
 // a worker with nothing processing needs nothing (leave scan / overflow mode)
-__device__ void needs_reset(const Dev& D, int c, uint32_t& nl) {
+__device__ __attribute__((always_inline)) void needs_reset(const Dev& D, int c, uint32_t& nl) {
   const int lane = lane_id();
   const uint32_t ctl = __shfl(nl, NLW - 1);
   if (ctl == NL_OVF || (ctl >> 8) != 0) {
@@ -1045,14 +1212,16 @@ struct Out {
 
 // WorkerState.add_to_processing / remove_from_processing on the dict of c (:733-771)
 template <bool LW>
-__device__ __forceinline__ bool dict_update(const WPtr& P, int c, int p, int delta, uint4& pf, uint4& pc, uint32_t& n) {
-  pf = *reinterpret_cast<const uint4*>(P.pfx + (size_t)c * PMW);
-  pc = *reinterpret_cast<const uint4*>(P.pcnt + (size_t)c * PMW);
+__device__ __forceinline__ bool dict_update(const WPtr<LW>& P, int c, int p, int delta, uint4& pf, uint4& pc, uint32_t& n) {
+  using U4c = typename WPtr<LW>::template P<const Q4>;
+  using U4 = typename WPtr<LW>::template P<Q4>;
+  pf = ld4(ascast<U4c>(P.pfx + (size_t)c * PMW));
+  pc = ld4(ascast<U4c>(P.pcnt + (size_t)c * PMW));
   n = P.plen[c] & 0xffu;
   const bool ok = dict_add(pf, pc, n, p, delta);
   if (lane_id() == 0) {
-    *reinterpret_cast<uint4*>(P.pfx + (size_t)c * PMW) = pf;
-    *reinterpret_cast<uint4*>(P.pcnt + (size_t)c * PMW) = pc;
+    st4(ascast<U4>(P.pfx + (size_t)c * PMW), pf);
+    st4(ascast<U4>(P.pcnt + (size_t)c * PMW), pc);
     P.plen[c] = n;
   }
   return ok;
@@ -1060,12 +1229,12 @@ __device__ __forceinline__ bool dict_update(const WPtr& P, int c, int p, int del
 
 // release the workers of slot s (the waiting successors may run) — LDS state only
 template <bool LW>
-__device__ void release_slot(const Dev& D, SLds& L, const WPtr& P, int s, bool all) {
+__device__ __attribute__((always_inline)) void release_slot(const Dev& D, SLds& L, const WPtr<LW>& P, int s, bool all) {
   SCtl& S = L.c;
   const int lane = lane_id();
   const unsigned bit = 1u << s;
   auto rel = [&](int c) {
-    unsigned succ = atomicAnd(&P.mask[c], ~bit) & ~bit;
+    unsigned succ = __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit;
     while (succ) {
       const int b = __builtin_ctz(succ);
       succ &= succ - 1;
@@ -1081,7 +1250,7 @@ __device__ void release_slot(const Dev& D, SLds& L, const WPtr& P, int s, bool a
 }
 
 // stage outputs, publish counts, retire: after this SEQ may consume the slot
-__device__ void finish_slot(const Dev& D, SLds& L, int s, long long r, const Out& o, int npops, bool direct) {
+__device__ __attribute__((always_inline)) void finish_slot(const Dev& D, SLds& L, int s, long long r, const Out& o, int npops, bool direct) {
   const int lane = lane_id();
   if (!direct) {
     const size_t st0 = (size_t)s * PLC;
@@ -1140,7 +1309,7 @@ __device__ __forceinline__ Key key_at(const Key& k, int l) {
 // a stimulus whose effects stay on the workers it registered. Returns false (nothing
 // changed) when it needs every earlier stimulus retired first (needs scan mode).
 template <bool LW>
-__device__ bool exe_local(const Dev& D, SLds& L, const WPtr& P, int s, long long r, int qmode, bool exact) {
+__device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r, int qmode, bool exact) {
   SCtl& S = L.c;
   const int lane = lane_id();
   const uint4 E = lane < NE ? L.desc[s][lane] : make_uint4(0, 0, 0, 0);
@@ -1153,6 +1322,12 @@ __device__ bool exe_local(const Dev& D, SLds& L, const WPtr& P, int s, long long
   const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
   const double durv = desc_durs(E);
   const int TD = E_HDR, RL0 = E_HDR + kt, FX0 = RL0 + nrel;
+  unsigned long long tph = mclk();
+  auto phase = [&](int k) {
+    const unsigned long long n = mclk();
+    if (lane == 0) atomicAdd(&S.prof[k], n - tph);
+    tph = n;
+  };
   // ---- capacity check of the needs tables this stimulus may grow
   if (!exact) {
     int tot_new = 0, off = FX0;
@@ -1173,6 +1348,7 @@ __device__ bool exe_local(const Dev& D, SLds& L, const WPtr& P, int s, long long
   Out o;
   o.nrec = 0;
   o.npl = 0;
+  phase(11);
   // ------------------------------------------- completion: processing -> memory (:2366)
   uint4 pf, pc;
   uint32_t pn;
@@ -1199,14 +1375,15 @@ __device__ bool exe_local(const Dev& D, SLds& L, const WPtr& P, int s, long long
   const double occw = occ_regs(pf, pc, pn, no0 + dnet, durv, D.bandwidth);
   o.rec(K_COMPLETE, w, p, dnet, occw, npw, t, dobs);
   // add_replica (:3148), then the releases popped before the frontier (LIFO, :3309-3314)
-  if (lane == 0) atomicAdd((unsigned long long*)&P.nbytes[w], (unsigned long long)nbt);
+  if (lane == 0) __hip_atomic_fetch_add(&P.nbytes[w], nbt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (flags & F_SELFREL) {
-    if (lane == 0) atomicAdd((unsigned long long*)&P.nbytes[w], (unsigned long long)(-nbt));
+    if (lane == 0) __hip_atomic_fetch_add(&P.nbytes[w], -nbt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   if (lane >= RL0 && lane < RL0 + nrel) {
     const int64_t nb = mk64(E.z, E.w);
-    atomicAdd((unsigned long long*)&P.nbytes[(int)E.x], (unsigned long long)(-nb));
+    __hip_atomic_fetch_add(&P.nbytes[(int)E.x], -nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+  phase(12);
   // ------------------------------ frontier in ascending priority: decide_worker (:8550)
   int off = FX0;
   for (int j = 0; j < nf; j++) {
@@ -1285,6 +1462,10 @@ __device__ bool exe_local(const Dev& D, SLds& L, const WPtr& P, int s, long long
   int pops = 0;
   if (qmode != 0 && !D.sat_inf) {
     const int slots = (int)P.cap[w] - P.nproc[w];
+    if (slots > (int)P.cap[w] || o.npl + slots > PLC - 1) {
+      serr(S, SERR_INV, 600000000 + (int)r);
+      return true;
+    }
     if (slots > 0) {
       pops = slots;
       if (qmode == 3) pops = (int)min((long long)slots, vload(&S.qlen));
@@ -1299,6 +1480,7 @@ __device__ bool exe_local(const Dev& D, SLds& L, const WPtr& P, int s, long long
       o.rec(K_PLACE, w, S.q_prefix, 0, occ_regs(pf, pc, pn, nw, durv, D.bandwidth), np1 + 1, -1, 0.0);
     }
   }
+  phase(13);
   // ------------------------------------------------ retire: LDS state, then successors
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS writes above are performed
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -1319,7 +1501,9 @@ __device__ bool exe_local(const Dev& D, SLds& L, const WPtr& P, int s, long long
     D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
     atomicAdd((unsigned long long*)&D.g_relwait[D.group[d]], 1ull);
   }
+  phase(14);
   finish_slot(D, L, s, r, o, pops, false);
+  phase(15);
   return true;
 }
 
@@ -1350,7 +1534,7 @@ __device__ __forceinline__ Key argmin_workers(const Dev& D, F&& key_of) {
 // transition (:2366-2442, :2313-2336, :4983-5023) for any route; placements go straight
 // into the placement log, records are folded as they happen.
 template <bool LW>
-__device__ void exe_global(const Dev& D, SLds& L, const WPtr& P, int s, long long r) {
+__device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r) {
   SCtl& S = L.c;
   const int lane = lane_id();
   const uint4 E = lane < NE ? L.desc[s][lane] : make_uint4(0, 0, 0, 0);
@@ -1613,7 +1797,7 @@ __device__ void exe_global(const Dev& D, SLds& L, const WPtr& P, int s, long lon
 }
 
 template <bool LW>
-__device__ void role_exe(const Dev& D, SLds& L, const WPtr& P) {
+__device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
   const int lane = lane_id();
   while (true) {
@@ -1686,7 +1870,7 @@ __device__ void role_exe(const Dev& D, SLds& L, const WPtr& P) {
 // ======================================================================== kernel
 // all threads: worker state between the engine's global arrays and the stream layout
 template <bool LW>
-__device__ void workers_io(const Dev& D, const WPtr& P, bool load) {
+__device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WPtr<LW>& P, bool load) {
   for (int c = threadIdx.x; c < D.W; c += blockDim.x) {
     if (load) {
       P.nproc[c] = D.w_nproc[c];
@@ -1724,11 +1908,11 @@ __device__ void workers_io(const Dev& D, const WPtr& P, bool load) {
 }
 
 template <bool LW>
-__global__ void __launch_bounds__(CTA) k_stream(const Dev* __restrict__ Dp, long long max_rounds, int snaps) {
-  const Dev& D = *Dp;
+__global__ void __launch_bounds__(CTA) k_stream(long long max_rounds, int snaps) {
+  const Dev& D = c_dev;
   __shared__ SLds L;
   SCtl& S = L.c;
-  const WPtr P = wptr<LW>(D);
+  const WPtr<LW> P = wptr<LW>(D);
   Ctl* c = D.ctl;
   Pos* pos = D.pos;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1779,7 +1963,7 @@ __global__ void __launch_bounds__(CTA) k_stream(const Dev* __restrict__ Dp, long
     for (int i = 0; i < PD; i++) S.wdur[i] = i < D.P ? D.pdur_walk[i] : -1.0;
     S.n_idle = c->n_idle;
     S.n_sat = c->n_sat;
-    for (int i = 0; i < 16; i++) S.prof[i] = 0;
+    for (int i = 0; i < 32; i++) S.prof[i] = 0;
     S.capmax = 1;
     S.inv_ok = 1;
     S.q_anon = 1;
@@ -1820,9 +2004,9 @@ __global__ void __launch_bounds__(CTA) k_stream(const Dev* __restrict__ Dp, long
     if (pos->round_end < 0) round_start = 0;
     role_seq<LW>(D, L, P, round_start);
   } else if (wave == 1) {
-    role_bld(D, L);
+    role_stage<0>(D, L);
   } else if (wave == 2) {
-    role_pre(D, L);
+    role_stage<1>(D, L);
   } else if (wave == 3) {
     role_reg<LW>(D, L, P);
   } else if (wave == 4) {
@@ -1870,10 +2054,19 @@ __global__ void __launch_bounds__(CTA) k_stream(const Dev* __restrict__ Dp, long
       c->err_task = S.err_task;
     }
     for (int i = 0; i < 16; i++) c->prof2[i] = S.prof[i];
+    if (S.error) {  // pipeline state for the post-mortem (dgp_stats wave_phase*)
+      const int sl = (int)(S.seq_pos & (WIN - 1));
+      const long long dv[16] = {S.seq_pos, S.reg_pos, S.pre_pos, S.bld_pos, S.log_len,
+                                (long long)S.ready, S.busy_exe, S.global_pending, (long long)L.flags[sl], L.pred[sl],
+                                L.sid[sl], L.done_tag[sl], S.walk_pos, S.rec_len, S.qlen, S.round_end};
+      for (int i = 0; i < 16; i++) c->prof2[i] = (unsigned long long)dv[i];
+    }
+    for (int i = 0; i < 16; i++) c->prof[i < 8 ? i : 7] = i < 8 ? S.prof[16 + i] : c->prof[7];
     pos->seq = S.seq_pos;
+
+    pos->reg = S.reg_pos;
     pos->bld = S.bld_pos;
     pos->pre = S.pre_pos;
-    pos->reg = S.reg_pos;
     pos->rec_len = S.rec_len;
     pos->walk = S.walk_pos;
     pos->runid_upto = S.log_len;

@@ -103,10 +103,10 @@ int check_device_error(dgp_engine* e, dgp::Ctl* out = nullptr) {
                                   "no worker", "needs_what line overflow", "prefix dict overflow (stream)",
                                   "watchdog: the stream engine made no progress", "queue", "needs_what inconsistent",
                                   "record log overflow (stream)", "task without candidates (stream)",
-                                  "descriptor ring out of order"};
+                                  "descriptor ring out of order", "worker index out of range (stream)", "stream invariant violated"};
     char buf[200];
     snprintf(buf, sizeof buf, "device engine error %d (%s) at task %d", c.error,
-             (c.error >= 0 && c.error <= 17) ? names[c.error] : "?", c.err_task);
+             (c.error >= 0 && c.error <= 19) ? names[c.error] : "?", c.err_task);
     return fail(e, DGP_E_DEVICE, buf);
   }
   return 0;
@@ -613,21 +613,20 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
     const size_t lds_w = dgp::st::lds_worker_bytes(D.W);
     const bool lw = sizeof(dgp::st::SLds) + lds_w <= 160 * 1024;
     const int snaps = e->snap_rounds > 0 ? 1 : 0;
-    if (lw) {
-      HIPCHK(e, hipFuncSetAttribute((const void*)dgp::st::k_stream<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_w));
-      if (int rc = timed_launch(e, 2, [&] {
-            hipLaunchKernelGGL(dgp::st::k_stream<true>, dim3(1), dim3(dgp::CTA), lds_w, e->stream, e->d_dev,
-                               (long long)max_rounds, snaps);
-          }))
-        return rc;
-    } else {
-      if (int rc = timed_launch(e, 2, [&] {
-            hipLaunchKernelGGL(dgp::st::k_stream<false>, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev,
-                               (long long)max_rounds, snaps);
-          }))
-        return rc;
-    }
+    HIPCHK(e, hipMemcpyToSymbolAsync(HIP_SYMBOL(dgp::st::c_dev), &e->D, sizeof(dgp::Dev), 0, hipMemcpyHostToDevice,
+                                     e->stream));
+    long long mr = (long long)max_rounds;
+    int sn = snaps;
+    void* args[] = {&mr, &sn};
+    const void* fn = lw ? (const void*)dgp::st::k_stream<true> : (const void*)dgp::st::k_stream<false>;
+    if (lw) HIPCHK(e, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w));
+    // ONE workgroup: every hand-off between the roles stays on this CU
+    hipError_t lst = hipSuccess;
+    if (int rc = timed_launch(e, 2, [&] {
+          lst = hipLaunchKernel(fn, dim3(1), dim3(dgp::CTA), args, lw ? lds_w : 0, e->stream);
+        }))
+      return rc;
+    if (lst != hipSuccess) return fail(e, DGP_E_HIP, std::string("stream launch: ") + hipGetErrorString(lst));
     e->stream_used = true;
   } else {
     // more task prefixes than the stream descriptors carry: the round-kernel engine
@@ -788,6 +787,7 @@ int dgp_stats(dgp_engine* e, int64_t* out, int32_t n) {
                    (int64_t)c.walk_pos};
   for (int i = 0; i < 8; i++) v[6 + i] = (int64_t)c.prof[i];
   for (int i = 0; i < 16; i++) v[14 + i] = (int64_t)c.prof2[i];
+
   for (int i = 0; i < n && i < 30; i++) out[i] = v[i];
   return 0;
 }

@@ -47,7 +47,9 @@ if which in ("all", "fix"):
                 if not np.array_equal(st, exp["final_state"]):
                     bad.append("final_state")
             except Exception as ex:  # noqa: BLE001
-                bad = [f"EXC {ex}"]
+                st = e.stats()
+                bad = [f"EXC {ex}", "seq reg pre bld log ready busy gpend flags pred sid done walk rec qlen rend",
+                       [st[f"wave_phase{i}"] for i in range(16)]]
         print(f"{f:28s} {'OK ' if not bad else 'BAD'} {time.time() - t:6.2f}s {bad[:3]}", flush=True)
 if which in ("all", "rnd"):
     for n, w, sat in ((100_000, 1024, 1.1), (100_000, 1024, "inf"), (30_000, 4096, 1.1)):
