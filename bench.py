@@ -29,26 +29,21 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level param
 CONFIG = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": 1.1}
 
 
-def algorithmic_bytes(g: dict, pl_worker_of_task: np.ndarray) -> dict:
-    """Bytes each kernel must move over one full replay (DESIGN.md §3 lists the terms).
+def algorithmic_bytes(g: dict, placed_tasks: np.ndarray, n_waves: int) -> float:
+    """SURVEY.md §8(d) algorithmic bytes for placing `placed_tasks` over `n_waves` waves.
 
-    k = fan-in, f = fan-out, c = distinct candidate workers, WB = bitset words per row.
+    Per placed task t: B_t = 8 + 12 k_t + 8 k_t ceil(W/64) + 12 + 8 + 12 f_t (dep row_ptr pair,
+    dep idx + nbytes, replica bitset rows, worker + comm_bytes out, dependents row_ptr pair,
+    dependent idx + remaining RMW), plus 48 W per wave (worker vector read + write).
+    k_t / f_t are the generated graph's own fan-in / fan-out.
     """
     n = g["n_tasks"]
     W = len(g["nthreads"])
     WB = (W + 63) // 64
-    k = np.diff(g["dep_ptr"]).astype(np.int64)
-    f = np.bincount(g["dep_idx"], minlength=n).astype(np.int64)
-    src = np.repeat(np.arange(n), k)
-    holder = pl_worker_of_task[g["dep_idx"]].astype(np.int64)
-    # distinct (task, holder) pairs -> candidates per task (one replica per dependency in the replay)
-    pairs = np.unique(src.astype(np.int64) * (W + 1) + holder)
-    c = np.bincount(pairs // (W + 1), minlength=n).astype(np.int64)
-    ready_later = k > 0  # tasks released by a completion (go through k_candidate_commbytes)
-    release = (56 + 28 * (f + k)).sum() + 4 * ready_later.sum()
-    cand = (33 + k * (12 + 8 * WB) + 12 * c)[ready_later].sum()
-    commit = (64 + 25 * k + 17 * f).sum() + (96 + 52 * c + 12 * k + 33).sum()
-    return {"frontier_release": float(release), "candidate_commbytes": float(cand), "commit": float(commit)}
+    k = np.diff(g["dep_ptr"]).astype(np.int64)[placed_tasks]
+    f = np.bincount(g["dep_idx"], minlength=n).astype(np.int64)[placed_tasks]
+    per_task = 8 + 12 * k + 8 * k * WB + 12 + 8 + 12 * f
+    return float(per_task.sum() + 48 * W * n_waves)
 
 
 def main():
@@ -92,6 +87,10 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
+    # placements made by update_graph (the initial wave) precede the replay kernel's
+    eng.reset()
+    eng.update_graph()
+    n_ug = eng.num_placements()
     for _ in range(args.warmup):
         step()
     eng.set_timing(True)
@@ -129,23 +128,26 @@ def main():
                    "placements_per_step": placements},
     }
     if rank == 0:
-        pl_worker_of_task = np.empty(g["n_tasks"], np.int64)
-        pl_worker_of_task[out["pl_task"]] = out["pl_worker"]
-        ab = algorithmic_bytes(g, pl_worker_of_task)
+        n_waves = eng.stats()["rounds"]
+        # bytes of the placements each kernel makes: update_graph's initial wave, then the replay
+        ab = {"update_graph": algorithmic_bytes(g, out["pl_task"][:n_ug], 1),
+              "replay": algorithmic_bytes(g, out["pl_task"][n_ug:], max(n_waves - 1, 0))}
         kernels = {}
-        for name in ("frontier_release", "candidate_commbytes", "commit"):
+        for name, nbytes in ab.items():
             ms, n = kt_total.get(name, (0.0, 0))
             if n == 0:
                 continue
-            per_launch_bytes = ab[name] / (n / args.steps)
+            per_launch_bytes = nbytes / (n / args.steps)  # every launch of a step shares its placements
             avg_ms = ms / n
             kernels[name] = {"total_ms_per_step": ms / args.steps, "launches_per_step": n // args.steps,
-                             "avg_us": 1e3 * avg_ms, "achieved_GBs": per_launch_bytes / (avg_ms * 1e-3) / 1e9}
+                             "avg_us": 1e3 * avg_ms, "bytes_per_launch": per_launch_bytes,
+                             "achieved_GBs": per_launch_bytes / (avg_ms * 1e-3) / 1e9}
         dom = max(kernels, key=lambda k: kernels[k]["total_ms_per_step"])
         ach = kernels[dom]["achieved_GBs"]
-        result["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None}
+        result["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 4), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 8), "traffic": None}
         result["kernels"] = {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in kernels.items()}
+        result["config"]["waves"] = int(n_waves)
         if world == 1 and not args.no_cpu_baseline:
             from oracle import oracle
 

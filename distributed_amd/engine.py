@@ -25,7 +25,8 @@ DEFAULT_CONFIG = {  # distributed/distributed.yaml:13,16,24,28
     "saturation": 1.1,
 }
 
-KERNEL_NAMES = ("frontier_release", "candidate_commbytes", "commit", "other")  # ids of dgp_kernel_times
+# ids of dgp_kernel_times; id 2 is the persistent replay kernel (k_stream; k_replay when P > PD)
+KERNEL_NAMES = ("frontier_release", "candidate_commbytes", "replay", "update_graph")
 
 
 class PlacementEngine:

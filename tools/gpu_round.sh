@@ -13,5 +13,5 @@ echo "== bench"
 timeout -k 10 300 python -u bench.py "$@" > $OUT/bench.log 2>&1
 rc=$?; tail -3 $OUT/bench.log; [ $rc -ne 0 ] && exit $rc
 echo "== rocprof"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 "$@" > $OUT/prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 "$@" > $OUT/prof.log 2>&1
 rc=$?; tail -3 $OUT/prof.log; find $OUT/prof -name '*stats*' | head; exit $rc
