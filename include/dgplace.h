@@ -22,7 +22,7 @@
  *                         the tasks placed in round k-1 (tests/golden/gen_golden.py)
  *   dgp_get_placements    the compute-task decisions (_add_to_processing :3199 /
  *                         _task_to_msg :3421): task, worker, comm bytes, objective, route
- *   dgp_steal_balance     WorkStealing.balance (stealing.py:401-503, _get_thief :532)
+ *   (planned) dgp_steal_balance  WorkStealing.balance (stealing.py:401-503, _get_thief :532)
  */
 #ifndef DGPLACE_H
 #define DGPLACE_H
@@ -111,7 +111,8 @@ int dgp_get_snapshots(dgp_engine* e, int64_t* n_rounds, int32_t* nplaced, double
 int dgp_get_task_states(dgp_engine* e, uint8_t* state);
 
 /* Device timing of the engine's kernels over the work since the last reset:
- * for kernel id k (0 frontier_release, 1 candidate_commbytes, 2 commit, 3 other)
+ * for kernel id k (0 frontier_release, 1 candidate_commbytes, 2 replay = the persistent
+ * stream kernel, 3 update_graph)
  * total milliseconds (HIP events on the engine's stream) and launch count. */
 int dgp_kernel_times(dgp_engine* e, double* ms, int64_t* launches, int32_t n);
 int dgp_set_timing(dgp_engine* e, int enabled);
