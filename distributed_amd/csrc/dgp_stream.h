@@ -40,6 +40,10 @@ namespace st {
 // re-fetched across the roles' fences); set by the host before each launch
 __constant__ Dev c_dev;
 
+#ifndef DGP_PHASE_PROBES
+#define DGP_PHASE_PROBES 0  // per-phase s_memtime probes in the executors (diagnostics)
+#endif
+constexpr int SCTA = 768;        // 12 waves: 5 roles + 7 executors (168 VGPRs per wave)
 constexpr int WIN = 32;          // in-flight stimulus slots (LDS window)
 constexpr int NE = 48;           // 16-byte descriptor entries per stimulus
 constexpr int DR = 4096;         // descriptor ring (global) — how far PRE may run ahead
@@ -47,7 +51,6 @@ constexpr int PLC = 64;          // staged placements / records per stimulus
 constexpr int KT_MAX = 24;       // dependencies of the completing task in local mode
 constexpr int KX_MAX = 8;        // dependencies of a frontier task in local mode
 constexpr int PD = 8;            // prefixes whose durations ride in the descriptor
-constexpr int PMW = 8;           // prefix dict entries per worker
 constexpr int NLW = 12;          // needs_what words per worker in LDS: 11 entries + control
 constexpr int NXW = 52;          // overflow entries per worker (global) before scan mode
 constexpr int PG = 64;           // walker's global prefix dict
@@ -168,15 +171,15 @@ struct WPtr {
   P<int32_t> nproc;
   P<uint16_t> nthreads;
   P<uint16_t> cap;
-  P<uint32_t> plen;    // low byte: dict length
-  P<uint16_t> pfx;     // [W][PMW]
-  P<uint16_t> pcnt;    // [W][PMW]
+  P<uint32_t> plen;    // prefix dict insertion order (WDict::ord)
+  P<uint16_t> pcnt;    // [W][PD] prefix dict counts by prefix id (WDict::c)
   P<int64_t> netocc;
   P<int64_t> nbytes;
   P<uint32_t> mask;    // in-flight slots touching the worker
   P<uint32_t> needs;   // [W][NLW]: (d << 8 | count), slot NLW-1 = control (count << 8 | 1 when
                        // overflow entries are in use; NL_OVF: scan mode)
   P<uint8_t> wflags;   // walker's idle / saturated bits
+  P<uint16_t> stamp;   // registrar scratch: touch-set dedupe (LDS carve only)
 };
 
 extern __shared__ __attribute__((aligned(16))) char st_smem[];
@@ -184,8 +187,9 @@ extern __shared__ __attribute__((aligned(16))) char st_smem[];
 __device__ __forceinline__ size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
 __host__ __device__ constexpr size_t lds_worker_bytes(int W) {
   return ((size_t)W * 4 + 15) / 16 * 16 * 2 /* nproc plen */ + ((size_t)W * 2 + 15) / 16 * 16 * 2 +
-         ((size_t)W * PMW * 2 + 15) / 16 * 16 * 2 + ((size_t)W * 8 + 15) / 16 * 16 * 2 +
-         ((size_t)W * 4 + 15) / 16 * 16 + ((size_t)W * NLW * 4 + 15) / 16 * 16 + ((size_t)W + 15) / 16 * 16;
+         ((size_t)W * PD * 2 + 15) / 16 * 16 + ((size_t)W * 8 + 15) / 16 * 16 * 2 +
+         ((size_t)W * 4 + 15) / 16 * 16 + ((size_t)W * NLW * 4 + 15) / 16 * 16 + ((size_t)W + 15) / 16 * 16 +
+         ((size_t)W * 2 + 15) / 16 * 16 /* stamp */;
 }
 
 template <bool LW>
@@ -199,25 +203,25 @@ __device__ __forceinline__ WPtr<LW> wptr(const Dev& D) {
     p.nthreads = (typename W_::template P<uint16_t>)b; b += al16(W * 2);
     p.cap = (typename W_::template P<uint16_t>)b;      b += al16(W * 2);
     p.plen = (typename W_::template P<uint32_t>)b;     b += al16(W * 4);
-    p.pfx = (typename W_::template P<uint16_t>)b;      b += al16(W * PMW * 2);
-    p.pcnt = (typename W_::template P<uint16_t>)b;     b += al16(W * PMW * 2);
+    p.pcnt = (typename W_::template P<uint16_t>)b;     b += al16(W * PD * 2);
     p.netocc = (typename W_::template P<int64_t>)b;    b += al16(W * 8);
     p.nbytes = (typename W_::template P<int64_t>)b;    b += al16(W * 8);
     p.mask = (typename W_::template P<uint32_t>)b;     b += al16(W * 4);
     p.needs = (typename W_::template P<uint32_t>)b;    b += al16(W * NLW * 4);
-    p.wflags = (typename W_::template P<uint8_t>)b;
+    p.wflags = (typename W_::template P<uint8_t>)b;    b += al16(W);
+    p.stamp = (typename W_::template P<uint16_t>)b;
   } else {
     p.nproc = D.gw_nproc;
     p.nthreads = D.gw_nthreads;
     p.cap = D.gw_cap;
     p.plen = D.gw_plen;
-    p.pfx = D.gw_pfx;
     p.pcnt = D.gw_pcnt;
     p.netocc = D.gw_netocc;
     p.nbytes = D.gw_nbytes;
     p.mask = D.gw_mask;
     p.needs = D.gw_needs;
     p.wflags = D.gw_wflags;
+    p.stamp = nullptr;
   }
   return p;
 }
@@ -254,98 +258,89 @@ struct SLds {
   SCtl c;
 };
 
-// prefix durations of a descriptor (entries 3..6, two doubles each) -> lane p holds dur_p
-__device__ __forceinline__ double desc_durs(const uint4& e) {
-  const int lane = lane_id();
-  const int src = 3 + ((lane & (PD - 1)) >> 1);
-  const unsigned x = __shfl(e.x, src), y = __shfl(e.y, src), z = __shfl(e.z, src), w = __shfl(e.w, src);
-  return (lane & 1) ? mkd(z, w) : mkd(x, y);
-}
+__shared__ SLds st_L;  // the engine's LDS window + control block (namespace scope: the roles'
+                       // out-of-line entry functions address it directly, keeping ds_* addressing)
 
-// _calc_occupancy (:1884-1903) of worker c (per lane); durv = lane p holds the resolved
-// duration of prefix p; all lanes must be active (shuffles)
-template <bool LW>
-__device__ __forceinline__ double occ_of(const WPtr<LW>& P, const Dev& D, int c, double durv) {
-  const uint32_t n = P.plen[c] & 0xffu;
-  using U4 = typename WPtr<LW>::template P<const Q4>;
-  const uint4 pf = ld4(ascast<U4>(P.pfx + (size_t)c * PMW));
-  const uint4 pc = ld4(ascast<U4>(P.pcnt + (size_t)c * PMW));
-  const uint32_t pfw[4] = {pf.x, pf.y, pf.z, pf.w};
-  const uint32_t pcw[4] = {pc.x, pc.y, pc.z, pc.w};
-  const int nmax = wmax((int)n);
-  double res = 0.0;
-#pragma unroll
-  for (int i = 0; i < PMW; i++) {
-    if (i >= nmax) break;
-    const uint32_t pfi = (pfw[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
-    const uint32_t pci = (pcw[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
-    const double dv = __shfl(durv, (int)(pfi & (PD - 1)));
-    if ((uint32_t)i < n) res += dv * (double)pci;
-  }
-  return res + (double)P.netocc[c] / (double)D.bandwidth;
+// ---------------------------------------------------------- the per-worker prefix dict
+// WorkerState.task_prefix_count is an insertion-ordered {prefix: count} with delete on
+// zero (:733-784). With P <= PD prefixes it is held as counts indexed by prefix id
+// (8 x u16 in a uint4) plus the insertion order: 3-bit prefix ids, entry i at bits
+// 3i..3i+2, and the number of entries in bits 24..31. A prefix is present iff its
+// count is non-zero, so the pair is exactly the dict.
+struct WDict {
+  uint4 c;       // count of prefix p: 16 bits at (p & 1) * 16 of word p >> 1
+  uint32_t ord;  // insertion order
+};
+__device__ __forceinline__ uint32_t wd_n(uint32_t ord) { return ord >> 24; }
+__device__ __forceinline__ int wd_id(uint32_t ord, int i) { return (int)((ord >> (3 * i)) & 7u); }
+__device__ __forceinline__ uint32_t wd_word(const uint4& c, int p) {
+  const int wi = p >> 1;
+  return wi == 0 ? c.x : wi == 1 ? c.y : wi == 2 ? c.z : c.w;
 }
+__device__ __forceinline__ uint32_t wd_cnt(const uint4& c, int p) { return (wd_word(c, p) >> ((p & 1) * 16)) & 0xffffu; }
 
-// insertion-ordered {prefix: count} with delete-on-zero (:733-784), packed 8 x u16
-__device__ __forceinline__ bool dict_add(uint4& pf, uint4& pc, uint32_t& n, int p, int delta) {
-  uint32_t pfw[4] = {pf.x, pf.y, pf.z, pf.w};
-  uint32_t pcw[4] = {pc.x, pc.y, pc.z, pc.w};
-  auto get = [&](const uint32_t* a, int i) { return (a[i >> 1] >> ((i & 1) * 16)) & 0xffffu; };
-  auto put = [&](uint32_t* a, int i, uint32_t v) {
-    const int sh = (i & 1) * 16;
-    a[i >> 1] = (a[i >> 1] & ~(0xffffu << sh)) | ((v & 0xffffu) << sh);
-  };
-  int at = -1;
-#pragma unroll
-  for (int i = 0; i < PMW; i++)
-    if (at < 0 && (uint32_t)i < n && get(pfw, i) == (uint32_t)p) at = i;
-  bool ok = true;
+// add_to_processing (+1) / remove_from_processing (-1) of one task of prefix p
+__device__ __forceinline__ bool dict_add(WDict& d, int p, int delta) {
+  const int wi = p >> 1, sh = (p & 1) * 16;
+  uint32_t wv = wd_word(d.c, p);
+  const uint32_t cnt = (wv >> sh) & 0xffffu;
+  const uint32_t n = wd_n(d.ord);
   if (delta > 0) {
-    if (at >= 0) {
-      uint32_t v = get(pcw, at);
-      if (v == 0xffffu) ok = false;
-      else put(pcw, at, v + 1);
-    } else if (n < (uint32_t)PMW) {
-      put(pfw, (int)n, (uint32_t)p);
-      put(pcw, (int)n, 1);
-      n++;
-    } else {
-      ok = false;
-    }
-  } else if (at >= 0) {
-    uint32_t v = get(pcw, at) - 1;
-    if (v == 0) {
+    if (cnt == 0xffffu) return false;
+    if (cnt == 0) d.ord = (d.ord + (1u << 24)) | ((uint32_t)p << (3 * n));  // new key: appended
+    wv += 1u << sh;
+  } else {
+    if (cnt == 0) return true;
+    wv -= 1u << sh;
+    if (cnt == 1) {  // count reached zero: the key leaves, later keys move up
+      int k = 0;
 #pragma unroll
-      for (int i = 0; i < PMW - 1; i++)
-        if (i >= at && (uint32_t)(i + 1) < n) {
-          put(pfw, i, get(pfw, i + 1));
-          put(pcw, i, get(pcw, i + 1));
-        }
-      put(pfw, (int)n - 1, 0);
-      put(pcw, (int)n - 1, 0);
-      n--;
-    } else {
-      put(pcw, at, v);
+      for (int i = 0; i < PD; i++)
+        if ((uint32_t)i < n && wd_id(d.ord, i) == p) k = i;
+      const uint32_t ids = d.ord & 0xffffffu, lowm = (1u << (3 * k)) - 1u;
+      d.ord = (ids & lowm) | ((ids >> 3) & ~lowm) | ((n - 1) << 24);
     }
   }
-  pf = make_uint4(pfw[0], pfw[1], pfw[2], pfw[3]);
-  pc = make_uint4(pcw[0], pcw[1], pcw[2], pcw[3]);
-  return ok;
+  if (wi == 0) d.c.x = wv;
+  else if (wi == 1) d.c.y = wv;
+  else if (wi == 2) d.c.z = wv;
+  else d.c.w = wv;
+  return true;
 }
 
-// occupancy from a dict held in registers (uniform across lanes)
-__device__ __forceinline__ double occ_regs(const uint4& pf, const uint4& pc, uint32_t n, int64_t netocc,
-                                           double durv, int64_t bw) {
-  const uint32_t pfw[4] = {pf.x, pf.y, pf.z, pf.w};
-  const uint32_t pcw[4] = {pc.x, pc.y, pc.z, pc.w};
+// prefix durations: a table of PD doubles in LDS (a descriptor's entries 3..6, or the
+// walker's wdur), read by prefix id
+using DTab = const __attribute__((address_space(3))) double*;
+
+// _calc_occupancy (:1884-1903): prefix terms in dict order, then network occupancy.
+// Durations resolve as there (EWMA, else unknown-task-duration; idempotent on resolved).
+__device__ __forceinline__ double occ_dict(const WDict& d, int64_t netocc, DTab dt, const Dev& D) {
+  const uint32_t n = wd_n(d.ord);
   double res = 0.0;
 #pragma unroll
-  for (int i = 0; i < PMW; i++) {
-    if ((uint32_t)i >= n) break;
-    const uint32_t pfi = (pfw[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
-    const uint32_t pci = (pcw[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
-    res += __shfl(durv, (int)(pfi & (PD - 1))) * (double)pci;
+  for (int i = 0; i < PD; i++) {
+    if (!ballot((uint32_t)i < n)) break;
+    const int p = wd_id(d.ord, i);
+    const double dv = dt[p];
+    const double term = (dv < 0 ? D.unknown_duration : dv) * (double)wd_cnt(d.c, p);
+    if ((uint32_t)i < n) res += term;
   }
-  return res + (double)netocc / (double)bw;
+  return res + (double)netocc / (double)D.bandwidth;
+}
+
+template <bool LW>
+__device__ __forceinline__ WDict dict_load(const WPtr<LW>& P, int c) {
+  using U4 = typename WPtr<LW>::template P<const Q4>;
+  WDict d;
+  d.c = ld4(ascast<U4>(P.pcnt + (size_t)c * PD));
+  d.ord = P.plen[c];
+  return d;
+}
+
+// occupancy of worker c (per lane; any lanes)
+template <bool LW>
+__device__ __forceinline__ double occ_of(const WPtr<LW>& P, const Dev& D, int c, DTab dt) {
+  return occ_dict(dict_load<LW>(P, c), P.netocc[c], dt, D);
 }
 
 __device__ __forceinline__ double resolve_dur(const Dev& D, double d) {  // _calc_occupancy :1892-1899
@@ -527,7 +522,7 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
     if (in && p == g.pf[k]) found = true;
     const long long inc = wscan_incl(dl);
     cnt_i[k] = g.cnt[k] + inc;
-    tot[k] = __shfl(inc, 63);
+    tot[k] = rl(inc, 63);
     if (in && cnt_i[k] < 1) bad = true;
   }
   if (!found) bad = true;
@@ -579,7 +574,7 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
 #pragma unroll
   for (int k = 0; k < PD; k++)
     if (k < g.n) g.cnt[k] += tot[k];
-  g.netocc += (double)__shfl(dn_inc, 63);
+  g.netocc += (double)mk64(rlu(lo32(dn_inc), 63), rlu(hi32(dn_inc), 63));
 }
 
 template <bool LW>
@@ -618,7 +613,7 @@ __device__ __attribute__((always_inline)) void snapshot(const Dev& D, SLds& L, c
   const int lane = lane_id();
   const long long idx = S.rounds_nonempty;
   if (idx >= D.snap_cap) return;
-  const double durv = resolve_dur(D, S.wdur[lane & (PD - 1)]);
+  const DTab durv = (DTab)&S.wdur[0];
   for (int c0 = 0; c0 < D.W; c0 += 64) {
     const int c = min(c0 + lane, D.W - 1);
     const double o = occ_of<LW>(P, D, c, durv);
@@ -746,7 +741,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
         ipo += c2;
       }
     }
-    const int tpl = __shfl(ipl, 63), trc = __shfl(irc, 63), tpo = __shfl(ipo, 63);
+    const int tpl = rl(ipl, 63), trc = rl(irc, 63), tpo = rl(ipo, 63);
     const long long lb = S.log_len + (ipl - npl), rb = S.rec_len + (irc - nrec), qb = S.qhead + (ipo - npop);
     if (lane < m && !direct) {
       const size_t st0 = (size_t)s * PLC;
@@ -838,6 +833,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, long lon
   if (f1 == f0 && !(tf & TF_WANTED)) flags |= F_SELFREL;
   if (kt > KT_MAX) flags |= F_GLOBAL;
   int n = E_HDR, nrel = 0, nf = 0;
+  unsigned long long my = 0;  // entries whose .y is a worker the stimulus touches (frontier deps)
   if (!(flags & F_GLOBAL)) {
     for (int64_t k = k0; k < k1; k++) {
       const int d = D.dep_idx[k];
@@ -871,6 +867,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, long lon
     for (int64_t q = x0; q < x1; q++) {
       const int d = D.dep_idx[q];
       const int64_t nb = nbv(D, D.res_nbytes[d]);
+      my |= 1ull << n;
       E[n++] = make_uint4((unsigned)d, (unsigned)D.holder_of[d], lo32(nb), hi32(nb));
     }
   }
@@ -878,7 +875,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, long lon
   E[0] = make_uint4((unsigned)t, (unsigned)w, (unsigned)p, flags);
   E[1] = make_uint4(lo32(nbt), hi32(nbt),
                     (unsigned)(min(kt, 255) | (nrel << 8) | (min(nf, 255) << 16) | (n << 24)), (unsigned)g);
-  E[2] = make_uint4(dlo(dobs), dhi(dobs), 0u, 0u);
+  E[2] = make_uint4(dlo(dobs), dhi(dobs), lo32((int64_t)my), hi32((int64_t)my));
 }
 
 // ========================================================== builder / prefetcher
@@ -918,141 +915,148 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
 }
 
 // ===================================================================== registrar
+// In stimulus order: the prefix EWMA (TaskPrefix.add_duration :977-985) and the resolved
+// durations written into the descriptor, the slot flags, the distinct touched workers,
+// then registration (slot bit into each touched worker's mask; predecessor count = the
+// in-flight bits already there). Up to RB stimuli per poll of the shared positions.
 template <bool LW>
 __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
   const int lane = lane_id();
-  double dur = lane < D.P ? D.pdur_cur[lane] : -1.0;  // lane p: duration_average as of reg_pos
-  unsigned long long t_idle = mclk();
-  constexpr int RB = 4;  // descriptors fetched per global round trip
-  uint4 EB[RB];
-  long long eb_first = -1;
-  int eb_n = 0;
-  long long pre = 0;  // cached PRE watermark: an agent-scope acquire only when exhausted
+  // lanes 3..6 own duration_average of prefixes 2(lane-3) and 2(lane-3)+1 (the descriptor
+  // entry they fill), as of reg_pos
+  const int pa = 2 * (lane - 3);
+  const bool dl = lane >= 3 && lane < 7;
+  double dur0 = dl && pa < D.P ? D.pdur_cur[pa] : -1.0;
+  double dur1 = dl && pa + 1 < D.P ? D.pdur_cur[pa + 1] : -1.0;
+  constexpr int RB = 8;
+  long long pre = 0;  // cached PRE watermark: re-read only when exhausted
   while (true) {
     if (vload(&S.stop)) break;
-    const long long r = S.reg_pos;
-    if (r >= pre) pre = vload(&S.pre_pos);
+    const long long r0 = S.reg_pos;
+    if (r0 >= pre) pre = vload(&S.pre_pos);
     const long long lim = min(min(pre, vload(&S.reg_limit)), vload(&S.seq_pos) + WIN);
-    if (r >= lim || vload(&S.global_pending)) {
+    if (r0 >= lim || vload(&S.global_pending)) {
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
     lds_fence();
     const unsigned long long t0 = mclk();
-    if (!(eb_first >= 0 && r >= eb_first && r < eb_first + eb_n)) {
-      // the descriptors of up to RB consecutive prefetched stimuli, one round trip
-      eb_first = r;
-      eb_n = (int)min((long long)RB, pre - r);
+    const int nb = (int)min((long long)RB, lim - r0);
+    uint4 EB[RB];
 #pragma unroll
-      for (int b = 0; b < RB; b++)
-        EB[b] = (lane < NE && b < eb_n) ? D.desc[(size_t)((r + b) & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
-    }
-    uint4 E = EB[0];
+    for (int b = 0; b < RB; b++)
+      EB[b] = (lane < NE && b < nb) ? D.desc[(size_t)((r0 + b) & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
+    bool halt = false;
 #pragma unroll
-    for (int b = 1; b < RB; b++)
-      if (r - eb_first == b) E = EB[b];
-    const int s = (int)(r & (WIN - 1));
-    unsigned long long tq = mclk();
-    if (lane == 0) S.prof[17] += tq - t0;
-    // TaskPrefix.add_duration (:977-985) of the completing task's prefix
-    const int p = rl((int)E.z, 0);
-    const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
-    if (lane == p) dur = dur < 0 ? dobs : 0.5 * dobs + 0.5 * dur;
-    const double rv = resolve_dur(D, dur);
-    {
-      const int src = 2 * (max(lane - 3, 0) & 3);
-      const double a0 = __shfl(rv, src), a1 = __shfl(rv, src + 1);
-      if (lane >= 3 && lane < 7) E = make_uint4(dlo(a0), dhi(a0), dlo(a1), dhi(a1));
-    }
-    uint32_t flags = rlu(E.w, 0);
-    const int w = rl((int)E.y, 0);
-    const unsigned cnts = rlu(E.z, 1);
-    const int kt = cnts & 0xff, nrel = (cnts >> 8) & 0xff, nf = (cnts >> 16) & 0xff;
-    if (D.dbg & 1) flags |= F_EXACT;
-    if (D.dbg & 2) flags |= F_GLOBAL;
-    if (!(flags & F_GLOBAL)) {
-      const int capw = D.sat_inf ? 0 : (int)P.cap[w];
-      if (nf + capw + 1 > PLC) flags |= F_GLOBAL;
-      if (vload(&S.qlen) > 0 && (!S.inv_ok || !S.q_anon)) flags |= F_GLOBAL;
-    }
-    if (lane == 0) E.w = flags;
-    if (lane < NE) L.desc[s][lane] = E;
-    int tw = -1;
-    bool keep = false;
-    if (!(flags & F_GLOBAL)) {
-      if (lane == 0) tw = w;
-      if (lane >= E_HDR + kt && lane < E_HDR + kt + nrel) tw = (int)E.x;
-      int off = E_HDR + kt + nrel;
-      for (int j = 0; j < nf; j++) {
-        const int kx = rl((int)E.z, off) & 0xff;
-        if (lane > off && lane <= off + kx) tw = (int)E.y < 0 ? -2 : (int)E.y;
-        off += 1 + kx;
+    for (int b = 0; b < RB; b++) {
+      if (b >= nb) break;
+      const long long r = r0 + b;
+      uint4 E = EB[b];
+      const int s = (int)(r & (WIN - 1));
+      const int p = rl((int)E.z, 0);
+      const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
+      if (lane == 3 + (p >> 1)) {
+        if (p & 1) dur1 = dur1 < 0 ? dobs : 0.5 * dobs + 0.5 * dur1;
+        else dur0 = dur0 < 0 ? dobs : 0.5 * dobs + 0.5 * dur0;
       }
-      if (lane >= E_HDR + kt && lane < E_HDR + kt + nrel && (int)E.x < 0) tw = -2;
-      if (ballot(tw >= D.W || (lane == 0 && w < 0) || (tw < -1))) {
-        if (D.dbgbuf) {  // post-mortem: the descriptor as registered, and where it came from
-          D.dbgbuf[lane * 8 + 0] = (double)(int)E.x;
-          D.dbgbuf[lane * 8 + 1] = (double)(int)E.y;
-          D.dbgbuf[lane * 8 + 2] = (double)(int)E.z;
-          D.dbgbuf[lane * 8 + 3] = (double)(int)E.w;
-          D.dbgbuf[lane * 8 + 4] = (double)tw;
-          D.dbgbuf[lane * 8 + 5] = (double)r;
-          D.dbgbuf[lane * 8 + 6] = (double)eb_first;
-          D.dbgbuf[lane * 8 + 7] = (double)pre;
+      if (dl) {
+        const double a0 = resolve_dur(D, dur0), a1 = resolve_dur(D, dur1);
+        E = make_uint4(dlo(a0), dhi(a0), dlo(a1), dhi(a1));
+      }
+      uint32_t flags = rlu(E.w, 0);
+      const int w = rl((int)E.y, 0);
+      const unsigned cnts = rlu(E.z, 1);
+      const int kt = cnts & 0xff, nrel = (cnts >> 8) & 0xff, nf = (cnts >> 16) & 0xff;
+      if (D.dbg & 1) flags |= F_EXACT;
+      if (D.dbg & 2) flags |= F_GLOBAL;
+      if (!(flags & F_GLOBAL)) {
+        const int capw = D.sat_inf ? 0 : (int)P.cap[w];
+        if (nf + capw + 1 > PLC) flags |= F_GLOBAL;
+        if (vload(&S.qlen) > 0 && (!S.inv_ok || !S.q_anon)) flags |= F_GLOBAL;
+      }
+      if (lane == 0) E.w = flags;
+      if (lane < NE) L.desc[s][lane] = E;
+      int tw = -1;
+      bool keep = false;
+      if (!(flags & F_GLOBAL)) {
+        // touched workers: w (entry 0), release holders (.x), frontier dependency holders (.y)
+        const unsigned long long my = (unsigned long long)mk64(rlu(E.z, 2), rlu(E.w, 2));
+        const int RL0 = E_HDR + kt;
+        const bool isrel = lane >= RL0 && lane < RL0 + nrel;
+        const bool isfd = (my >> lane) & 1;
+        if (lane == 0) tw = w;
+        else if (isfd) tw = (int)E.y;
+        else if (isrel) tw = (int)E.x;
+        if (ballot(tw >= D.W || (lane > 0 && (isfd || isrel) && tw < 0) || (lane == 0 && w < 0))) {
+          if (D.dbgbuf) {  // post-mortem: the descriptor as registered
+            D.dbgbuf[lane * 8 + 0] = (double)(int)E.x;
+            D.dbgbuf[lane * 8 + 1] = (double)(int)E.y;
+            D.dbgbuf[lane * 8 + 2] = (double)(int)E.z;
+            D.dbgbuf[lane * 8 + 3] = (double)(int)E.w;
+            D.dbgbuf[lane * 8 + 4] = (double)tw;
+            D.dbgbuf[lane * 8 + 5] = (double)r;
+            D.dbgbuf[lane * 8 + 6] = (double)r0;
+            D.dbgbuf[lane * 8 + 7] = (double)pre;
+          }
+          serr(S, SERR_RANGE, (int)r);
+          halt = true;
+          break;
         }
-        serr(S, SERR_RANGE, (int)r);
-        break;
+        if constexpr (LW) {
+          // one representative lane per worker: every lane stamps its id, the lane that
+          // reads its own id back keeps the worker (LDS ops of one wave run in order)
+          using VP = volatile __attribute__((address_space(3))) uint16_t*;
+          if (tw >= 0) ((VP)P.stamp)[tw] = (uint16_t)lane;
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          keep = tw >= 0 && ((VP)P.stamp)[tw] == (uint16_t)lane;
+        } else {
+          keep = tw >= 0;
+          unsigned long long rem = ballot(keep);
+          while (rem) {
+            const int i = __builtin_ctzll(rem);
+            const int v = rl(tw, i);
+            const unsigned long long same = ballot(tw == v);
+            if (tw == v && lane != i) keep = false;
+            rem &= ~same;
+          }
+        }
+        const unsigned long long km = ballot(keep);
+        const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0));
+        if (keep) L.touch[s][pos] = (uint16_t)tw;
+        if (lane == 0) L.ntouch[s] = __builtin_popcountll(km);
+      } else {
+        flags |= F_TOUCHALL;
+        if (lane == 0) L.ntouch[s] = 0;
       }
-      keep = tw >= 0;
-      unsigned long long rem = ballot(keep);
-      while (rem) {  // keep the first lane of every distinct worker
-        const int i = __builtin_ctzll(rem);
-        const int v = rl(tw, i);
-        const unsigned long long same = ballot(tw == v);
-        if (tw == v && lane != i) keep = false;
-        rem &= ~same;
+      if (lane == 0) {
+        L.flags[s] = flags;
+        L.pred[s] = BIG;
+        L.sid[s] = r;
       }
-      const unsigned long long km = ballot(keep);
-      const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0));
-      if (keep) L.touch[s][pos] = (uint16_t)tw;
-      if (lane == 0) L.ntouch[s] = __builtin_popcountll(km);
-    } else {
-      flags |= F_TOUCHALL;
-      if (lane == 0) L.ntouch[s] = 0;
+      lds_fence();
+      const unsigned bit = 1u << s;
+      int cnt = 0;
+      if (flags & F_TOUCHALL) {
+        for (int c = lane; c < D.W; c += 64) cnt += __builtin_popcount(__hip_atomic_fetch_or(&P.mask[c], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
+      } else if (keep) {
+        cnt = __builtin_popcount(__hip_atomic_fetch_or(&P.mask[tw], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
+      }
+      const int tot = wsum(cnt);
+      if (lane == 0) {
+        const int old = atomicAdd(&L.pred[s], tot - BIG);
+        if (old + tot - BIG == 0) atomicOr(&S.ready, bit);
+        if (flags & F_GLOBAL) vstore(&S.global_pending, 1);
+        vstore(&S.reg_pos, r + 1);
+      }
+      if (flags & F_GLOBAL) break;  // nothing registers behind a global until it finished
     }
-    if (lane == 0) {
-      L.flags[s] = flags;
-      L.pred[s] = BIG;
-      L.sid[s] = r;
-    }
+    if (halt) break;
+    if (lane == 0) S.prof[3] += mclk() - t0;
     lds_fence();
-    {
-      const unsigned long long n = mclk();
-      if (lane == 0) S.prof[18] += n - tq;
-      tq = n;
-    }
-    const unsigned bit = 1u << s;
-    int cnt = 0;
-    if (flags & F_TOUCHALL) {
-      for (int c = lane; c < D.W; c += 64) cnt += __builtin_popcount(__hip_atomic_fetch_or(&P.mask[c], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
-    } else if (keep) {
-      cnt = __builtin_popcount(__hip_atomic_fetch_or(&P.mask[tw], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
-    }
-    const int tot = wsum(cnt);
-    if (lane == 0) {
-      const int old = atomicAdd(&L.pred[s], tot - BIG);
-      if (old + tot - BIG == 0) atomicOr(&S.ready, bit);
-      if (flags & F_GLOBAL) vstore(&S.global_pending, 1);
-      S.prof[19] += mclk() - tq;
-      S.prof[3] += mclk() - t0;
-      vstore(&S.reg_pos, r + 1);
-    }
-    lds_fence();
-    t_idle = mclk();
   }
-  (void)t_idle;
-  if (lane < D.P && lane < PD) D.pdur_cur[lane] = dur;
+  if (dl && pa < D.P) D.pdur_cur[pa] = dur0;
+  if (dl && pa + 1 < D.P) D.pdur_cur[pa + 1] = dur1;
 }
 
 // ===================================================================== executors
@@ -1081,7 +1085,7 @@ __device__ __forceinline__ int line_used(uint32_t nl) { return __builtin_popcoun
 // (returns the bytes c no longer needs)
 __device__ __attribute__((always_inline)) int64_t needs_dec(const Dev& D, SCtl& S, int c, uint32_t& nl, int d, int64_t nb, int except) {
   const int lane = lane_id();
-  const uint32_t ctl = __shfl(nl, NLW - 1);
+  const uint32_t ctl = rlu(nl, NLW - 1);
   if (ctl == NL_OVF) return st_needed_elsewhere(D, d, c, except) ? 0 : nb;
   const unsigned long long m = ballot(lane < NLW - 1 && nl != 0 && (nl >> 8) == (uint32_t)d);
   if (m) {
@@ -1115,7 +1119,7 @@ __device__ __attribute__((always_inline)) int64_t needs_dec(const Dev& D, SCtl& 
 // (returns the bytes c newly needs)
 __device__ __attribute__((always_inline)) int64_t needs_inc(const Dev& D, SCtl& S, int c, uint32_t& nl, int d, int64_t nb, int except) {
   const int lane = lane_id();
-  const uint32_t ctl = __shfl(nl, NLW - 1);
+  const uint32_t ctl = rlu(nl, NLW - 1);
   if (ctl == NL_OVF) return st_needed_elsewhere(D, d, c, except) ? 0 : nb;
   const unsigned long long m = ballot(lane < NLW - 1 && nl != 0 && (nl >> 8) == (uint32_t)d);
   if (m) {
@@ -1167,7 +1171,7 @@ __device__ __attribute__((always_inline)) int64_t needs_inc(const Dev& D, SCtl& 
 // a worker with nothing processing needs nothing (leave scan / overflow mode)
 __device__ __attribute__((always_inline)) void needs_reset(const Dev& D, int c, uint32_t& nl) {
   const int lane = lane_id();
-  const uint32_t ctl = __shfl(nl, NLW - 1);
+  const uint32_t ctl = rlu(nl, NLW - 1);
   if (ctl == NL_OVF || (ctl >> 8) != 0) {
     if (lane < NXW) __hip_atomic_store(D.gw_needs_ext + (size_t)c * NXW + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __threadfence_block();
@@ -1212,17 +1216,13 @@ struct Out {
 
 // WorkerState.add_to_processing / remove_from_processing on the dict of c (:733-771)
 template <bool LW>
-__device__ __forceinline__ bool dict_update(const WPtr<LW>& P, int c, int p, int delta, uint4& pf, uint4& pc, uint32_t& n) {
-  using U4c = typename WPtr<LW>::template P<const Q4>;
+__device__ __forceinline__ bool dict_update(const WPtr<LW>& P, int c, int p, int delta, WDict& d) {
   using U4 = typename WPtr<LW>::template P<Q4>;
-  pf = ld4(ascast<U4c>(P.pfx + (size_t)c * PMW));
-  pc = ld4(ascast<U4c>(P.pcnt + (size_t)c * PMW));
-  n = P.plen[c] & 0xffu;
-  const bool ok = dict_add(pf, pc, n, p, delta);
+  d = dict_load<LW>(P, c);
+  const bool ok = dict_add(d, p, delta);
   if (lane_id() == 0) {
-    st4(ascast<U4>(P.pfx + (size_t)c * PMW), pf);
-    st4(ascast<U4>(P.pcnt + (size_t)c * PMW), pc);
-    P.plen[c] = n;
+    st4(ascast<U4>(P.pcnt + (size_t)c * PD), d.c);
+    P.plen[c] = d.ord;
   }
   return ok;
 }
@@ -1281,7 +1281,15 @@ __device__ __attribute__((always_inline)) void finish_slot(const Dev& D, SLds& L
     L.nrec[s] = direct ? 0 : o.nrec;
     L.npops[s] = npops;
   }
+#if DGP_PHASE_PROBES
+  {
+    const unsigned long long t_a = mclk();
+    __threadfence_block();
+    if (lane == 0) atomicAdd(&L.c.prof[22], mclk() - t_a);
+  }
+#else
   __threadfence_block();
+#endif
   if (lane == 0) vstore(&L.done_tag[s], r + 1);
 }
 
@@ -1320,14 +1328,18 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   const int grp_t = rl((int)E.w, 1);
   const int kt = cnts & 0xff, nrel = (cnts >> 8) & 0xff, nf = (cnts >> 16) & 0xff;
   const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
-  const double durv = desc_durs(E);
+  const DTab durv = (DTab)(const double*)&L.desc[s][3];
   const int TD = E_HDR, RL0 = E_HDR + kt, FX0 = RL0 + nrel;
+#if DGP_PHASE_PROBES
   unsigned long long tph = mclk();
   auto phase = [&](int k) {
     const unsigned long long n = mclk();
     if (lane == 0) atomicAdd(&S.prof[k], n - tph);
     tph = n;
   };
+#else
+  auto phase = [](int) {};
+#endif
   // ---- capacity check of the needs tables this stimulus may grow
   if (!exact) {
     int tot_new = 0, off = FX0;
@@ -1349,13 +1361,33 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   o.nrec = 0;
   o.npl = 0;
   phase(11);
-  // ------------------------------------------- completion: processing -> memory (:2366)
-  uint4 pf, pc;
-  uint32_t pn;
-  const int np0 = P.nproc[w];
-  const int64_t no0 = P.netocc[w];
-  dict_update<LW>(P, w, p, -1, pf, pc, pn);
+  // ---- the touched workers' state, one lane each, in registers for the whole stimulus
+  const int nt = L.ntouch[s];
+  const bool tl = lane < nt;
+  const int cj = tl ? (int)L.touch[s][lane] : 0;
+  int np = 0, nth = 1;
+  WDict dj;
+  dj.c = make_uint4(0, 0, 0, 0);
+  dj.ord = 0;
+  int64_t net = 0, nbj = 0;
+  if (tl) {
+    np = P.nproc[cj];
+    nth = P.nthreads[cj];
+    dj = dict_load<LW>(P, cj);
+    net = P.netocc[cj];
+    nbj = P.nbytes[cj];
+  }
+  const int capw = P.cap[w];
   uint32_t nl = line_load<LW>(P, w);
+  const unsigned long long wm = ballot(tl && cj == w);
+  if (!wm) {
+    serr(S, SERR_INV, 700000000 + (int)r);
+    return true;
+  }
+  const int jw = __builtin_ctzll(wm);
+  const bool isw = lane == jw;
+  phase(16);
+  // ------------------------------------------- completion: processing -> memory (:2366)
   int64_t dnet = 0;
   for (int i = 0; i < kt; i++) {  // _dec_needs_replica for the dependencies w needed
     const int L_ = TD + i;
@@ -1365,23 +1397,25 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     const int64_t nb = mk64(rlu(E.z, L_), rlu(E.w, L_));
     dnet -= needs_dec(D, S, w, nl, d, nb, t);
   }
-  const int npw = np0 - 1;
+  const int npw = rl(np, jw) - 1;
   if (npw == 0) needs_reset(D, w, nl);
   line_store<LW>(P, w, nl);
-  if (lane == 0) {
-    P.nproc[w] = npw;
-    P.netocc[w] = no0 + dnet;
+  if (isw) {
+    dict_add(dj, p, -1);
+    np = npw;
+    net += dnet;
   }
-  const double occw = occ_regs(pf, pc, pn, no0 + dnet, durv, D.bandwidth);
-  o.rec(K_COMPLETE, w, p, dnet, occw, npw, t, dobs);
+  phase(17);
+  {
+    const double oj = occ_dict(dj, net, durv, D);
+    o.rec(K_COMPLETE, w, p, dnet, mkd(rlu(dlo(oj), jw), rlu(dhi(oj), jw)), npw, t, dobs);
+  }
   // add_replica (:3148), then the releases popped before the frontier (LIFO, :3309-3314)
-  if (lane == 0) __hip_atomic_fetch_add(&P.nbytes[w], nbt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (flags & F_SELFREL) {
-    if (lane == 0) __hip_atomic_fetch_add(&P.nbytes[w], -nbt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  if (lane >= RL0 && lane < RL0 + nrel) {
-    const int64_t nb = mk64(E.z, E.w);
-    __hip_atomic_fetch_add(&P.nbytes[(int)E.x], -nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (isw) nbj += (flags & F_SELFREL) ? 0 : nbt;
+  for (int i = 0; i < nrel; i++) {
+    const int h = rl((int)E.x, RL0 + i);
+    const int64_t nb = mk64(rlu(E.z, RL0 + i), rlu(E.w, RL0 + i));
+    if (tl && cj == h) nbj -= nb;
   }
   phase(12);
   // ------------------------------ frontier in ascending priority: decide_worker (:8550)
@@ -1389,56 +1423,59 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   for (int j = 0; j < nf; j++) {
     const int x = rl((int)E.x, off), px = rl((int)E.y, off), kx = rl((int)E.z, off) & 0xff;
     const int gx = rl((int)E.w, off);
-    const bool in = lane > off && lane <= off + kx;
-    const int h = (int)E.y;
+    // candidates = the holders of x's dependencies (each a touched lane); comm_bytes (:3136)
     int64_t comm = 0;
-    bool rep = in;
+    bool cand = false;
     for (int i = 0; i < kx; i++) {
       const int L2 = off + 1 + i;
       const int hi = rl((int)E.y, L2);
       const int64_t nbi = mk64(rlu(E.z, L2), rlu(E.w, L2));
-      if (in && hi != h) comm += nbi;
-      if (in && L2 < lane && hi == h) rep = false;
+      if (cj == hi) cand = true;
+      else comm += nbi;
     }
-    const int c = in ? h : w;
-    const double oc = occ_of<LW>(P, D, c, durv);
+    cand = cand && tl;
     Key k;
-    k.start = oc / (double)P.nthreads[c] + (double)comm / (double)D.bandwidth;
-    k.nb = P.nbytes[c];
-    k.w = c;
+    const double oc = occ_dict(dj, net, durv, D);
+    k.start = oc / (double)nth + (double)comm / (double)D.bandwidth;
+    k.nb = nbj;
+    k.w = cj;
     k.comm = comm;
-    if (x == D.dbg_task && in) {
+    if (x == D.dbg_task && cand) {
       double* B = D.dbgbuf + (size_t)lane * 8;
-      B[0] = c;
+      B[0] = cj;
       B[1] = k.start;
       B[2] = (double)k.nb;
       B[3] = (double)comm;
       B[4] = oc;
-      B[5] = P.nproc[c];
-      B[6] = (double)P.netocc[c];
-      B[7] = (double)(P.plen[c] & 0xff) + 100.0 * r;
+      B[5] = np;
+      B[6] = (double)net;
+      B[7] = (double)wd_n(dj.ord) + 100.0 * r;
     }
-    const unsigned long long reps = ballot(rep);
-    if (!reps) {
+    phase(18);
+    const unsigned long long cm = ballot(cand);
+    if (!cm) {
       serr(S, SERR_CAND, x);
       return true;
     }
-    Key best = key_at(k, __builtin_ctzll(reps));
-    for (unsigned long long rm = reps & (reps - 1); rm; rm &= rm - 1) {
-      const Key q = key_at(k, __builtin_ctzll(rm));
-      if (key_less(q, best)) best = q;
+    Key best = key_at(k, __builtin_ctzll(cm));
+    int jb = __builtin_ctzll(cm);
+    for (unsigned long long rm = cm & (cm - 1); rm; rm &= rm - 1) {
+      const int jq = __builtin_ctzll(rm);
+      const Key q = key_at(k, jq);
+      if (key_less(q, best)) {
+        best = q;
+        jb = jq;
+      }
     }
     const int cb = best.w;
+    phase(19);
     // _add_to_processing (:3199): record, WorkerState.add_to_processing, check_idle_saturated
     o.place(x, cb, best.comm, best.start, best.nb, ROUTE_NONROOTISH);
-    const int npc0 = P.nproc[cb];
-    const int64_t noc0 = P.netocc[cb];
-    if (!dict_update<LW>(P, cb, px, +1, pf, pc, pn)) serr(S, SERR_PREFIX, x);
     uint32_t nlc = line_load<LW>(P, cb);
-    int64_t dn = 0;
     if (exact) {  // scan mode reads processing_on of this stimulus' earlier placements
       __threadfence_block();
     }
+    int64_t dn = 0;
     for (int i = 0; i < kx; i++) {
       const int L2 = off + 1 + i;
       if (rl((int)E.y, L2) == cb) continue;
@@ -1447,22 +1484,31 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       dn += needs_inc(D, S, cb, nlc, d, nb, x);
     }
     line_store<LW>(P, cb, nlc);
+    const bool isb = lane == jb;
+    bool okp = true;
+    if (isb) {
+      okp = dict_add(dj, px, +1);
+      np += 1;
+      net += dn;
+    }
+    if (ballot(!okp)) serr(S, SERR_PREFIX, x);
     if (lane == 0) {
-      P.nproc[cb] = npc0 + 1;
-      P.netocc[cb] = noc0 + dn;
       D.proc_on[x] = cb;
       D.state[x] = S_PROCESSING;
       atomicAdd((unsigned long long*)&D.g_relwait[gx], (unsigned long long)-1ll);
     }
-    const double occc = occ_regs(pf, pc, pn, noc0 + dn, durv, D.bandwidth);
-    o.rec(K_PLACE, cb, px, dn, occc, npc0 + 1, x, 0.0);
+    {
+      const double oj = occ_dict(dj, net, durv, D);
+      o.rec(K_PLACE, cb, px, dn, mkd(rlu(dlo(oj), jb), rlu(dhi(oj), jb)), rl(np, jb), x, 0.0);
+    }
     off += 1 + kx;
+    phase(20);
   }
   // -------------- stimulus_queue_slots_maybe_opened (:4983): only w can have open slots
   int pops = 0;
   if (qmode != 0 && !D.sat_inf) {
-    const int slots = (int)P.cap[w] - P.nproc[w];
-    if (slots > (int)P.cap[w] || o.npl + slots > PLC - 1) {
+    const int slots = capw - rl(np, jw);
+    if (slots > capw || o.npl + slots > PLC - 1) {
       serr(S, SERR_INV, 600000000 + (int)r);
       return true;
     }
@@ -1470,21 +1516,37 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       pops = slots;
       if (qmode == 3) pops = (int)min((long long)slots, vload(&S.qlen));
     }
+    const int qp = S.q_prefix;
     for (int i = 0; i < pops; i++) {
-      const int np1 = P.nproc[w];
-      const int64_t nw = P.netocc[w];
-      const double ow = occ_of<LW>(P, D, w, durv);
-      o.place(-1, w, 0, ow / (double)P.nthreads[w] + 0.0 / (double)D.bandwidth, P.nbytes[w], ROUTE_ROOTISH_Q);
-      if (!dict_update<LW>(P, w, S.q_prefix, +1, pf, pc, pn)) serr(S, SERR_PREFIX, -1);
-      if (lane == 0) P.nproc[w] = np1 + 1;
-      o.rec(K_PLACE, w, S.q_prefix, 0, occ_regs(pf, pc, pn, nw, durv, D.bandwidth), np1 + 1, -1, 0.0);
+      const double ow = occ_dict(dj, net, durv, D);
+      const double st = ow / (double)nth + 0.0 / (double)D.bandwidth;
+      o.place(-1, w, 0, mkd(rlu(dlo(st), jw), rlu(dhi(st), jw)), mk64(rlu(lo32(nbj), jw), rlu(hi32(nbj), jw)),
+              ROUTE_ROOTISH_Q);
+      bool okq = true;
+      if (isw) {
+        okq = dict_add(dj, qp, +1);
+        np += 1;
+      }
+      if (ballot(!okq)) serr(S, SERR_PREFIX, -1);
+      const double oa = occ_dict(dj, net, durv, D);
+      o.rec(K_PLACE, w, qp, 0, mkd(rlu(dlo(oa), jw), rlu(dhi(oa), jw)), rl(np, jw), -1, 0.0);
     }
+  }
+  // ---- write the touched workers back (before the slot releases its successors)
+  if (tl) {
+    using U4 = typename WPtr<LW>::template P<Q4>;
+    P.nproc[cj] = np;
+    st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
+    P.plen[cj] = dj.ord;
+    P.netocc[cj] = net;
+    P.nbytes[cj] = nbj;
   }
   phase(13);
   // ------------------------------------------------ retire: LDS state, then successors
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS writes above are performed
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   release_slot<LW>(D, L, P, s, false);
+  phase(21);
   // replica bookkeeping in HBM (TaskState fields; the walker / globals read them later)
   if (lane == 0) {
     D.cur_nbytes[t] = nbt;
@@ -1542,7 +1604,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   const int64_t nbt = mk64(rlu(E.x, 1), rlu(E.y, 1));
   const int grp_t = rl((int)E.w, 1);
   const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
-  const double durv = desc_durs(E);
+  const DTab durv = (DTab)(const double*)&L.desc[s][3];
   WState g;
   ws_load(S, g);
   const long long lpos = S.log_len;
@@ -1569,8 +1631,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
     }
     return wsum64(v);
   };
-  uint4 pf, pc;
-  uint32_t pn;
+  WDict wd;
   // _add_to_processing (:3199) of x on c; x WAITING (frontier) or QUEUED (refill)
   auto place_x = [&](int x, int c, int route, int64_t comm, bool was_waiting) {
     if (comm < 0) comm = comm_bytes(x, c);
@@ -1579,7 +1640,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
     const int px = D.prefix[x];
     const int np0 = P.nproc[c];
     const int64_t no0 = P.netocc[c];
-    if (!dict_update<LW>(P, c, px, +1, pf, pc, pn)) serr(S, SERR_PREFIX, x);
+    if (!dict_update<LW>(P, c, px, +1, wd)) serr(S, SERR_PREFIX, x);
     uint32_t nl = line_load<LW>(P, c);
     int64_t dn = 0;
     for (int64_t k = D.dep_ptr[x]; k < D.dep_ptr[x + 1]; k++) {
@@ -1596,7 +1657,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       if (was_waiting) atomicAdd((unsigned long long*)&D.g_relwait[D.group[x]], (unsigned long long)-1ll);
     }
     __threadfence_block();
-    ws_fold<LW>(D, P, S, g, K_PLACE, c, px, dn, occ_regs(pf, pc, pn, no0 + dn, durv, D.bandwidth), np0 + 1, 0.0);
+    ws_fold<LW>(D, P, S, g, K_PLACE, c, px, dn, occ_dict(wd, no0 + dn, durv, D), np0 + 1, 0.0);
   };
   auto itc_argmin = [&]() -> int {  // decide_worker_rootish_queuing_enabled :2230-2233
     Key b = argmin_workers(D, [&](int c, Key& k) {
@@ -1614,7 +1675,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   {
     const int np0 = P.nproc[w];
     const int64_t no0 = P.netocc[w];
-    dict_update<LW>(P, w, p, -1, pf, pc, pn);
+    dict_update<LW>(P, w, p, -1, wd);
     uint32_t nl = line_load<LW>(P, w);
     int64_t dnet = 0;
     for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
@@ -1632,7 +1693,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       D.proc_on[t] = -1;
       D.state[t] = S_MEMORY;
     }
-    ws_fold<LW>(D, P, S, g, K_COMPLETE, w, p, dnet, occ_regs(pf, pc, pn, no0 + dnet, durv, D.bandwidth), np0 - 1,
+    ws_fold<LW>(D, P, S, g, K_COMPLETE, w, p, dnet, occ_dict(wd, no0 + dnet, durv, D), np0 - 1,
                 dobs);
   }
   // ------------------------------------------------------ releases (:3309-3314, :2444)
@@ -1730,7 +1791,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
           B[4] = ocw;
           B[5] = P.nproc[cw];
           B[6] = (double)P.netocc[cw];
-          B[7] = (double)(P.plen[cw] & 0xff) + 100.0 * r;
+          B[7] = (double)wd_n(P.plen[cw]) + 100.0 * r;
         }
         return true;
       });
@@ -1796,6 +1857,12 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   if (lane == 0) vstore(&S.global_pending, 0);
 }
 
+// the global path out of line: the local path keeps its own register budget
+template <bool LW>
+__device__ __attribute__((noinline)) void exe_global_entry(int s, long long r) {
+  exe_global<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r);
+}
+
 template <bool LW>
 __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
@@ -1834,7 +1901,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       }
       unsigned old = 0;
       if (lane == 0) old = atomicAnd(&S.ready, ~(1u << s));
-      old = (unsigned)__shfl((int)old, 0);
+      old = rlu(old, 0);
       if (!((old >> s) & 1u)) continue;
       cs = s;
       cr = r;
@@ -1851,7 +1918,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     if (lane == 0) atomicAdd(&S.busy_exe, 1);
     const unsigned long long t0 = mclk();
     if (cf & F_GLOBAL) {
-      exe_global<LW>(D, L, P, cs, cr);
+      exe_global_entry<LW>(cs, cr);
       if (lane == 0) S.prof[9]++;
     } else if (!exe_local<LW>(D, L, P, cs, cr, cq, cex)) {
       if (lane == 0) {
@@ -1876,12 +1943,16 @@ __device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WP
       P.nproc[c] = D.w_nproc[c];
       P.nthreads[c] = (uint16_t)D.w_nthreads[c];
       P.cap[c] = (uint16_t)D.w_cap[c];
+      // engine layout (insertion-ordered pairs) -> WDict (prefix ids < PD on this path)
       const int n = D.w_plen[c];
-      P.plen[c] = (uint32_t)n;
-      for (int i = 0; i < PMW; i++) {
-        P.pfx[(size_t)c * PMW + i] = (uint16_t)(i < n ? D.w_pfx[(size_t)c * PMAX + i] : 0);
-        P.pcnt[(size_t)c * PMW + i] = (uint16_t)(i < n ? D.w_pcnt[(size_t)c * PMAX + i] : 0);
+      uint32_t ord = (uint32_t)n << 24;
+      for (int q = 0; q < PD; q++) P.pcnt[(size_t)c * PD + q] = 0;
+      for (int i = 0; i < n; i++) {
+        const int pid = D.w_pfx[(size_t)c * PMAX + i] & (PD - 1);
+        ord |= (uint32_t)pid << (3 * i);
+        P.pcnt[(size_t)c * PD + pid] = (uint16_t)D.w_pcnt[(size_t)c * PMAX + i];
       }
+      P.plen[c] = ord;
       P.netocc[c] = D.w_netocc[c];
       P.nbytes[c] = D.w_nbytes[c];
       P.mask[c] = 0;
@@ -1890,11 +1961,13 @@ __device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WP
       for (int i = 0; i < NLW; i++) P.needs[(size_t)c * NLW + i] = D.gw_needs_saved[(size_t)c * NLW + i];
     } else {
       D.w_nproc[c] = P.nproc[c];
-      const int n = P.plen[c] & 0xff;
+      const uint32_t ord = P.plen[c];
+      const int n = (int)wd_n(ord);
       D.w_plen[c] = n;
       for (int i = 0; i < PMAX; i++) {
-        D.w_pfx[(size_t)c * PMAX + i] = i < n && i < PMW ? P.pfx[(size_t)c * PMW + i] : 0;
-        D.w_pcnt[(size_t)c * PMAX + i] = i < n && i < PMW ? P.pcnt[(size_t)c * PMW + i] : 0;
+        const int pid = wd_id(ord, i);
+        D.w_pfx[(size_t)c * PMAX + i] = i < n ? pid : 0;
+        D.w_pcnt[(size_t)c * PMAX + i] = i < n ? P.pcnt[(size_t)c * PD + pid] : 0;
       }
       D.w_netocc[c] = P.netocc[c];
       D.w_nbytes[c] = P.nbytes[c];
@@ -1907,10 +1980,23 @@ __device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WP
   }
 }
 
+
+// One call per role for the whole launch: each role is register-allocated on its own
+// (inlined into one kernel body they shared one 128-VGPR budget and spilled to scratch
+// on the executors' path).
 template <bool LW>
-__global__ void __launch_bounds__(CTA) k_stream(long long max_rounds, int snaps) {
+__device__ __attribute__((noinline)) void entry_exe() { role_exe<LW>(c_dev, st_L, wptr<LW>(c_dev)); }
+template <bool LW>
+__device__ __attribute__((noinline)) void entry_reg() { role_reg<LW>(c_dev, st_L, wptr<LW>(c_dev)); }
+template <bool LW>
+__device__ __attribute__((noinline)) void entry_wlk() { role_wlk<LW>(c_dev, st_L, wptr<LW>(c_dev)); }
+template <int KIND>
+__device__ __attribute__((noinline)) void entry_stage() { role_stage<KIND>(c_dev, st_L); }
+
+template <bool LW>
+__global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps) {
   const Dev& D = c_dev;
-  __shared__ SLds L;
+  SLds& L = st_L;
   SCtl& S = L.c;
   const WPtr<LW> P = wptr<LW>(D);
   Ctl* c = D.ctl;
@@ -2004,15 +2090,15 @@ __global__ void __launch_bounds__(CTA) k_stream(long long max_rounds, int snaps)
     if (pos->round_end < 0) round_start = 0;
     role_seq<LW>(D, L, P, round_start);
   } else if (wave == 1) {
-    role_stage<0>(D, L);
+    entry_stage<0>();
   } else if (wave == 2) {
-    role_stage<1>(D, L);
+    entry_stage<1>();
   } else if (wave == 3) {
-    role_reg<LW>(D, L, P);
+    entry_reg<LW>();
   } else if (wave == 4) {
-    role_wlk<LW>(D, L, P);
-  } else {
-    role_exe<LW>(D, L, P);
+    entry_wlk<LW>();
+  } else if (!((D.dbg >> 8) & 15) || wave - N_ROLE < ((D.dbg >> 8) & 15)) {  // dbg bits 8..11: executor count
+    entry_exe<LW>();
   }
   __threadfence_block();
   __syncthreads();

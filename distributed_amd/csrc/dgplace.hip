@@ -335,8 +335,7 @@ int dgp_set_workers(dgp_engine* e, int32_t n_workers, const int32_t* nthreads) {
     rc |= dalloc(e, &D.gw_nthreads, W, e->allocs);
     rc |= dalloc(e, &D.gw_cap, W, e->allocs);
     rc |= dalloc(e, &D.gw_plen, W, e->allocs);
-    rc |= dalloc(e, &D.gw_pfx, W * S::PMW, e->allocs);
-    rc |= dalloc(e, &D.gw_pcnt, W * S::PMW, e->allocs);
+    rc |= dalloc(e, &D.gw_pcnt, W * S::PD, e->allocs);
     rc |= dalloc(e, &D.gw_netocc, W, e->allocs);
     rc |= dalloc(e, &D.gw_nbytes, W, e->allocs);
     rc |= dalloc(e, &D.gw_mask, W, e->allocs);
@@ -623,7 +622,7 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
     // ONE workgroup: every hand-off between the roles stays on this CU
     hipError_t lst = hipSuccess;
     if (int rc = timed_launch(e, 2, [&] {
-          lst = hipLaunchKernel(fn, dim3(1), dim3(dgp::CTA), args, lw ? lds_w : 0, e->stream);
+          lst = hipLaunchKernel(fn, dim3(1), dim3(dgp::st::SCTA), args, lw ? lds_w : 0, e->stream);
         }))
       return rc;
     if (lst != hipSuccess) return fail(e, DGP_E_HIP, std::string("stream launch: ") + hipGetErrorString(lst));
