@@ -75,6 +75,7 @@ struct Ctl {
   const int32_t* round_L;         // completion list of the current round
   long long dr_steps;             // deterministic-reservation steps (diagnostics)
   unsigned long long prof2[16];   // exec_local_wave phase cycles (diagnostics)
+  unsigned long long prof3[8];    // stream engine stall counters (diagnostics)
   unsigned long long prof[8];     // k_commit phase cycles (s_memtime): setup, local steps, global
                                   // stimuli, finish, walker, max step, -, -
   long long n_global_events;
@@ -222,6 +223,7 @@ struct Dev {
   int32_t* fr_mark;          // stimulus whose completion empties the task's waiting_on
   int32_t* rel_mark;         // stimulus whose completion empties the task's waiters
   uint4* desc;               // descriptor ring [DR][NE]
+  int32_t* touch_ring;       // distinct workers each prefetched stimulus touches [DR][TMAX]
   long long* desc_tag;
   int32_t* s2_task;  // per-slot staging of placements [WIN][PLC]
   int32_t* s2_worker;

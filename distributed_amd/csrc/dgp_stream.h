@@ -51,6 +51,7 @@ constexpr int PLC = 64;          // staged placements / records per stimulus
 constexpr int KT_MAX = 24;       // dependencies of the completing task in local mode
 constexpr int KX_MAX = 8;        // dependencies of a frontier task in local mode
 constexpr int PD = 8;            // prefixes whose durations ride in the descriptor
+constexpr int TMAX = 32;         // distinct workers a local stimulus may touch (more: global)
 constexpr int NLW = 12;          // needs_what words per worker in LDS: 11 entries + control
 constexpr int NXW = 52;          // overflow entries per worker (global) before scan mode
 constexpr int PG = 64;           // walker's global prefix dict
@@ -59,7 +60,7 @@ constexpr uint32_t NL_OVF = 0xffffffffu;
 constexpr int N_ROLE = 5;        // waves 0..4 are SEQ, BLD, PRE, REG, WLK; the rest execute
 constexpr int E_HDR = 7;         // header entries: 0 ids, 1 sizes/counts, 2 duration, 3..6 durations
 
-enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8 };
+enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16 };
 enum : int { K_COMPLETE = 1, K_PLACE = 2 };
 enum : int { SERR_NONE = 0, SERR_PREFIX = 11, SERR_WATCHDOG = 12, SERR_QUEUE = 13, SERR_NEEDS = 14,
              SERR_REC = 15, SERR_CAND = 16, SERR_STAGE = 17, SERR_RANGE = 18, SERR_INV = 19 };
@@ -179,7 +180,6 @@ struct WPtr {
   P<uint32_t> needs;   // [W][NLW]: (d << 8 | count), slot NLW-1 = control (count << 8 | 1 when
                        // overflow entries are in use; NL_OVF: scan mode)
   P<uint8_t> wflags;   // walker's idle / saturated bits
-  P<uint16_t> stamp;   // registrar scratch: touch-set dedupe (LDS carve only)
 };
 
 extern __shared__ __attribute__((aligned(16))) char st_smem[];
@@ -188,8 +188,7 @@ __device__ __forceinline__ size_t al16(size_t b) { return (b + 15) & ~(size_t)15
 __host__ __device__ constexpr size_t lds_worker_bytes(int W) {
   return ((size_t)W * 4 + 15) / 16 * 16 * 2 /* nproc plen */ + ((size_t)W * 2 + 15) / 16 * 16 * 2 +
          ((size_t)W * PD * 2 + 15) / 16 * 16 + ((size_t)W * 8 + 15) / 16 * 16 * 2 +
-         ((size_t)W * 4 + 15) / 16 * 16 + ((size_t)W * NLW * 4 + 15) / 16 * 16 + ((size_t)W + 15) / 16 * 16 +
-         ((size_t)W * 2 + 15) / 16 * 16 /* stamp */;
+         ((size_t)W * 4 + 15) / 16 * 16 + ((size_t)W * NLW * 4 + 15) / 16 * 16 + ((size_t)W + 15) / 16 * 16;
 }
 
 template <bool LW>
@@ -208,8 +207,7 @@ __device__ __forceinline__ WPtr<LW> wptr(const Dev& D) {
     p.nbytes = (typename W_::template P<int64_t>)b;    b += al16(W * 8);
     p.mask = (typename W_::template P<uint32_t>)b;     b += al16(W * 4);
     p.needs = (typename W_::template P<uint32_t>)b;    b += al16(W * NLW * 4);
-    p.wflags = (typename W_::template P<uint8_t>)b;    b += al16(W);
-    p.stamp = (typename W_::template P<uint16_t>)b;
+    p.wflags = (typename W_::template P<uint8_t>)b;
   } else {
     p.nproc = D.gw_nproc;
     p.nthreads = D.gw_nthreads;
@@ -221,7 +219,6 @@ __device__ __forceinline__ WPtr<LW> wptr(const Dev& D) {
     p.mask = D.gw_mask;
     p.needs = D.gw_needs;
     p.wflags = D.gw_wflags;
-    p.stamp = nullptr;
   }
   return p;
 }
@@ -255,6 +252,7 @@ struct SLds {
   int32_t npl[WIN], npops[WIN], nrec[WIN];
   long long done_tag[WIN];
   long long sid[WIN];         // stimulus registered in each slot
+  uint16_t pre_scr[64][TMAX]; // prefetcher scratch: each lane's distinct-worker list
   SCtl c;
 };
 
@@ -682,7 +680,7 @@ template <bool LW>
 __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, const WPtr<LW>& P, long long& round_start) {
   SCtl& S = L.c;
   const int lane = lane_id();
-  unsigned long long t_idle = mclk();
+  unsigned long long t_idle = mclk(), t_sq = t_idle;
   while (true) {
     if (vload(&S.stop)) break;
     const long long sp = S.seq_pos;
@@ -697,10 +695,13 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
         t_idle = mclk();
         continue;
       }
-      if (mclk() - t_idle > WATCHDOG) {
+      const unsigned long long nw = mclk();
+      if (nw - t_idle > WATCHDOG) {
         serr(S, SERR_WATCHDOG, (int)sp);
         break;
       }
+      if (lane == 0) S.prof[30] += nw - t_sq;  // 30: sequencer waiting for the oldest slot
+      t_sq = nw;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
@@ -783,6 +784,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
 
     }
     t_idle = mclk();
+    t_sq = t_idle;
   }
 }
 
@@ -817,8 +819,22 @@ __device__ __attribute__((always_inline)) void bld_range(const Dev& D, long long
 
 // ==================================================================== prefetcher
 // descriptor of stimulus r (one lane): see E_HDR for the header layout
-__device__ __attribute__((always_inline)) void build_desc(const Dev& D, long long r) {
+__device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L, long long r) {
   uint4* E = D.desc + (size_t)(r & (DR - 1)) * NE;
+  // the distinct workers the stimulus touches, in first-touch order (lane-private LDS list)
+  auto scr = L.pre_scr[lane_id()];
+  int nt = 0;
+  bool tbad = false;
+  auto touch = [&](int c) {
+    if (c < 0 || c >= D.W) {
+      tbad = true;
+      return;
+    }
+    for (int i = 0; i < nt; i++)
+      if (scr[i] == (uint16_t)c) return;
+    if (nt < TMAX) scr[nt] = (uint16_t)c;
+    nt++;
+  };
   const int t = D.pl_task[r];
   const int w = D.pl_worker[r];
   const int p = D.prefix[t];
@@ -833,7 +849,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, long lon
   if (f1 == f0 && !(tf & TF_WANTED)) flags |= F_SELFREL;
   if (kt > KT_MAX) flags |= F_GLOBAL;
   int n = E_HDR, nrel = 0, nf = 0;
-  unsigned long long my = 0;  // entries whose .y is a worker the stimulus touches (frontier deps)
+  touch(w);
   if (!(flags & F_GLOBAL)) {
     for (int64_t k = k0; k < k1; k++) {
       const int d = D.dep_idx[k];
@@ -848,7 +864,9 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, long lon
         break;
       }
       const int64_t nb = nbv(D, D.res_nbytes[d]);
-      E[n++] = make_uint4((unsigned)D.holder_of[d], (unsigned)d, lo32(nb), hi32(nb));
+      const int hd = D.holder_of[d];
+      touch(hd);
+      E[n++] = make_uint4((unsigned)hd, (unsigned)d, lo32(nb), hi32(nb));
       nrel++;
     }
   }
@@ -867,15 +885,21 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, long lon
     for (int64_t q = x0; q < x1; q++) {
       const int d = D.dep_idx[q];
       const int64_t nb = nbv(D, D.res_nbytes[d]);
-      my |= 1ull << n;
-      E[n++] = make_uint4((unsigned)d, (unsigned)D.holder_of[d], lo32(nb), hi32(nb));
+      const int hd = D.holder_of[d];
+      touch(hd);
+      E[n++] = make_uint4((unsigned)d, (unsigned)hd, lo32(nb), hi32(nb));
     }
   }
-  if (nf > 255) flags |= F_GLOBAL;
+  if (nf > 255 || nt > TMAX) flags |= F_GLOBAL;
+  if (nf + (D.sat_inf ? 0 : D.w_cap[w]) + 1 > PLC) flags |= F_GLOBAL;  // staging room for the refill
+  if (tbad) flags |= F_GLOBAL | F_BADTOUCH;
+  if (flags & F_GLOBAL) nt = 0;
+  int32_t* T = D.touch_ring + (size_t)(r & (DR - 1)) * TMAX;
+  for (int i = 0; i < nt; i++) T[i] = scr[i];
   E[0] = make_uint4((unsigned)t, (unsigned)w, (unsigned)p, flags);
   E[1] = make_uint4(lo32(nbt), hi32(nbt),
                     (unsigned)(min(kt, 255) | (nrel << 8) | (min(nf, 255) << 16) | (n << 24)), (unsigned)g);
-  E[2] = make_uint4(dlo(dobs), dhi(dobs), lo32((int64_t)my), hi32((int64_t)my));
+  E[2] = make_uint4(dlo(dobs), dhi(dobs), (unsigned)nt, 0u);
 }
 
 // ========================================================== builder / prefetcher
@@ -902,7 +926,7 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
       bld_range(D, a, e);
     } else {
       const long long r = a + lane;
-      if (r < e) build_desc(D, r);
+      if (r < e) build_desc(D, L, r);
     }
     __threadfence_block();
     wbar();
@@ -918,7 +942,17 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
 // In stimulus order: the prefix EWMA (TaskPrefix.add_duration :977-985) and the resolved
 // durations written into the descriptor, the slot flags, the distinct touched workers,
 // then registration (slot bit into each touched worker's mask; predecessor count = the
-// in-flight bits already there). Up to RB stimuli per poll of the shared positions.
+// in-flight bits already there). A batch of up to RB stimuli per poll: phase A prepares
+// every slot of the batch; phase B registers them. The mask atomics of phase B are issued
+// back to back: one wave's LDS operations execute in order, so stimulus b sees the bits
+// of b-1 exactly as if they were registered one at a time.
+__device__ __forceinline__ int wsum_small(int v) {  // wave sum of values in [0, 64)
+  int t = 0;
+#pragma unroll
+  for (int b = 0; b < 6; b++) t += __builtin_popcountll(ballot((v >> b) & 1)) << b;
+  return t;
+}
+
 template <bool LW>
 __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
@@ -931,128 +965,183 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
   double dur1 = dl && pa + 1 < D.P ? D.pdur_cur[pa + 1] : -1.0;
   constexpr int RB = 8;
   long long pre = 0;  // cached PRE watermark: re-read only when exhausted
+  unsigned long long t_poll = mclk();
+  uint4 EB[RB];
+  int TB[RB];
+  long long eb_first = -1;
+  int eb_n = 0;
   while (true) {
     if (vload(&S.stop)) break;
     const long long r0 = S.reg_pos;
     if (r0 >= pre) pre = vload(&S.pre_pos);
-    const long long lim = min(min(pre, vload(&S.reg_limit)), vload(&S.seq_pos) + WIN);
-    if (r0 >= lim || vload(&S.global_pending)) {
+    const long long wl = vload(&S.seq_pos) + WIN;
+    const long long lim = min(min(pre, vload(&S.reg_limit)), wl);
+    const int gp = vload(&S.global_pending);
+    if (r0 >= lim || gp) {
+      // stall attribution (cycles): 24 window full, 25 descriptor not prefetched, 26 global pending
+      const unsigned long long n = mclk();
+      if (lane == 0) S.prof[gp ? 26 : (r0 >= wl ? 24 : (r0 >= pre ? 25 : 27))] += n - t_poll;
+      t_poll = n;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
     lds_fence();
     const unsigned long long t0 = mclk();
-    const int nb = (int)min((long long)RB, lim - r0);
-    uint4 EB[RB];
+    int nb = (int)min((long long)RB, lim - r0);
+    // the batch's descriptors and touch lists (prefetched by the previous iteration when
+    // it could; the loads complete while this wave polls)
+    if (eb_first == r0 && eb_n > 0) {
+      nb = min(nb, eb_n);  // use the prefetched rows; the next prefetch covers the rest
+    } else {
+      eb_first = r0;
+      eb_n = nb;
 #pragma unroll
-    for (int b = 0; b < RB; b++)
-      EB[b] = (lane < NE && b < nb) ? D.desc[(size_t)((r0 + b) & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
-    bool halt = false;
+      for (int b = 0; b < RB; b++) {
+        const size_t row = (size_t)((r0 + b) & (DR - 1));
+        EB[b] = (lane < NE && b < nb) ? D.desc[row * NE + lane] : make_uint4(0, 0, 0, 0);
+        TB[b] = (lane < TMAX && b < nb) ? D.touch_ring[row * TMAX + lane] : -1;
+      }
+    }
+    // ---------------------------------------------------------------- phase A
+    // header scalars of the whole batch first (independent of one another)
+    int pb[RB], ntb[RB];
+    uint32_t flb[RB];
+    double dob[RB];
+    const long long ql = vload(&S.qlen);  // only globals grow the queue; none runs now
+    const bool qglob = ql > 0 && (!S.inv_ok || !S.q_anon);
+    const uint32_t fadd = (qglob ? F_GLOBAL : 0u) | ((D.dbg & 1) ? F_EXACT : 0u) | ((D.dbg & 2) ? F_GLOBAL : 0u);
 #pragma unroll
     for (int b = 0; b < RB; b++) {
-      if (b >= nb) break;
+      pb[b] = rl((int)EB[b].z, 0);
+      dob[b] = mkd(rlu(EB[b].x, 2), rlu(EB[b].y, 2));
+      ntb[b] = rl((int)EB[b].z, 2);
+      flb[b] = rlu(EB[b].w, 0) | fadd;
+    }
+    // the batch ends after its first global stimulus (nothing registers behind a global)
+    int nbat = nb;
+    bool glob_end = false, halt = false;
+#pragma unroll
+    for (int b = RB - 1; b >= 0; b--) {
+      if (b < nb && (flb[b] & F_GLOBAL)) {
+        nbat = b + 1;
+        glob_end = true;
+      }
+      if (b < nb && (flb[b] & F_BADTOUCH)) halt = true;
+    }
+    if (halt) {
+      serr(S, SERR_RANGE, (int)r0);
+      break;
+    }
+    int ntmax = 0;
+    const int nloc = nbat - (glob_end ? 1 : 0);  // stimuli with touch lists
+#pragma unroll
+    for (int b = 0; b < RB; b++) {
+      if (b >= nbat) break;
       const long long r = r0 + b;
-      uint4 E = EB[b];
       const int s = (int)(r & (WIN - 1));
-      const int p = rl((int)E.z, 0);
-      const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
-      if (lane == 3 + (p >> 1)) {
-        if (p & 1) dur1 = dur1 < 0 ? dobs : 0.5 * dobs + 0.5 * dur1;
-        else dur0 = dur0 < 0 ? dobs : 0.5 * dobs + 0.5 * dur0;
+      uint4 E = EB[b];
+      const int p = pb[b];
+      if (lane == 3 + (p >> 1)) {  // TaskPrefix.add_duration, in stimulus order
+        if (p & 1) dur1 = dur1 < 0 ? dob[b] : 0.5 * dob[b] + 0.5 * dur1;
+        else dur0 = dur0 < 0 ? dob[b] : 0.5 * dob[b] + 0.5 * dur0;
       }
       if (dl) {
         const double a0 = resolve_dur(D, dur0), a1 = resolve_dur(D, dur1);
         E = make_uint4(dlo(a0), dhi(a0), dlo(a1), dhi(a1));
       }
-      uint32_t flags = rlu(E.w, 0);
-      const int w = rl((int)E.y, 0);
-      const unsigned cnts = rlu(E.z, 1);
-      const int kt = cnts & 0xff, nrel = (cnts >> 8) & 0xff, nf = (cnts >> 16) & 0xff;
-      if (D.dbg & 1) flags |= F_EXACT;
-      if (D.dbg & 2) flags |= F_GLOBAL;
-      if (!(flags & F_GLOBAL)) {
-        const int capw = D.sat_inf ? 0 : (int)P.cap[w];
-        if (nf + capw + 1 > PLC) flags |= F_GLOBAL;
-        if (vload(&S.qlen) > 0 && (!S.inv_ok || !S.q_anon)) flags |= F_GLOBAL;
-      }
-      if (lane == 0) E.w = flags;
+      const uint32_t fl = (b == nbat - 1 && glob_end) ? (flb[b] | F_TOUCHALL) : flb[b];
+      flb[b] = fl;
+      if (lane == 0) E.w = fl;
       if (lane < NE) L.desc[s][lane] = E;
-      int tw = -1;
-      bool keep = false;
-      if (!(flags & F_GLOBAL)) {
-        // touched workers: w (entry 0), release holders (.x), frontier dependency holders (.y)
-        const unsigned long long my = (unsigned long long)mk64(rlu(E.z, 2), rlu(E.w, 2));
-        const int RL0 = E_HDR + kt;
-        const bool isrel = lane >= RL0 && lane < RL0 + nrel;
-        const bool isfd = (my >> lane) & 1;
-        if (lane == 0) tw = w;
-        else if (isfd) tw = (int)E.y;
-        else if (isrel) tw = (int)E.x;
-        if (ballot(tw >= D.W || (lane > 0 && (isfd || isrel) && tw < 0) || (lane == 0 && w < 0))) {
-          if (D.dbgbuf) {  // post-mortem: the descriptor as registered
-            D.dbgbuf[lane * 8 + 0] = (double)(int)E.x;
-            D.dbgbuf[lane * 8 + 1] = (double)(int)E.y;
-            D.dbgbuf[lane * 8 + 2] = (double)(int)E.z;
-            D.dbgbuf[lane * 8 + 3] = (double)(int)E.w;
-            D.dbgbuf[lane * 8 + 4] = (double)tw;
-            D.dbgbuf[lane * 8 + 5] = (double)r;
-            D.dbgbuf[lane * 8 + 6] = (double)r0;
-            D.dbgbuf[lane * 8 + 7] = (double)pre;
-          }
-          serr(S, SERR_RANGE, (int)r);
-          halt = true;
-          break;
-        }
-        if constexpr (LW) {
-          // one representative lane per worker: every lane stamps its id, the lane that
-          // reads its own id back keeps the worker (LDS ops of one wave run in order)
-          using VP = volatile __attribute__((address_space(3))) uint16_t*;
-          if (tw >= 0) ((VP)P.stamp)[tw] = (uint16_t)lane;
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-          keep = tw >= 0 && ((VP)P.stamp)[tw] == (uint16_t)lane;
-        } else {
-          keep = tw >= 0;
-          unsigned long long rem = ballot(keep);
-          while (rem) {
-            const int i = __builtin_ctzll(rem);
-            const int v = rl(tw, i);
-            const unsigned long long same = ballot(tw == v);
-            if (tw == v && lane != i) keep = false;
-            rem &= ~same;
-          }
-        }
-        const unsigned long long km = ballot(keep);
-        const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0));
-        if (keep) L.touch[s][pos] = (uint16_t)tw;
-        if (lane == 0) L.ntouch[s] = __builtin_popcountll(km);
-      } else {
-        flags |= F_TOUCHALL;
-        if (lane == 0) L.ntouch[s] = 0;
-      }
+      // the distinct touched workers (deduplicated by the prefetcher), one lane each
+      const int nt = (b < nloc) ? ntb[b] : 0;
+      ntb[b] = nt;
+      ntmax = max(ntmax, nt);
+      if (lane < NE) L.touch[s][lane] = (uint16_t)TB[b];  // entries past nt are never read
       if (lane == 0) {
-        L.flags[s] = flags;
+        L.ntouch[s] = nt;
+        L.flags[s] = fl;
         L.pred[s] = BIG;
         L.sid[s] = r;
       }
-      lds_fence();
-      const unsigned bit = 1u << s;
-      int cnt = 0;
-      if (flags & F_TOUCHALL) {
-        for (int c = lane; c < D.W; c += 64) cnt += __builtin_popcount(__hip_atomic_fetch_or(&P.mask[c], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
-      } else if (keep) {
-        cnt = __builtin_popcount(__hip_atomic_fetch_or(&P.mask[tw], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
-      }
-      const int tot = wsum(cnt);
-      if (lane == 0) {
-        const int old = atomicAdd(&L.pred[s], tot - BIG);
-        if (old + tot - BIG == 0) atomicOr(&S.ready, bit);
-        if (flags & F_GLOBAL) vstore(&S.global_pending, 1);
-        vstore(&S.reg_pos, r + 1);
-      }
-      if (flags & F_GLOBAL) break;  // nothing registers behind a global until it finished
     }
-    if (halt) break;
-    if (lane == 0) S.prof[3] += mclk() - t0;
+    const unsigned long long tA = mclk();
+    // ---------------------------------------------------------------- phase B
+    lds_fence();  // the slots' LDS state is written before any mask bit can expose it
+    if (lane == 0) vstore(&S.reg_pos, r0 + nbat);
+    // every mask registration back to back (one wave's LDS atomics run in order); the
+    // per-lane predecessor counts packed 16 bits per stimulus
+    unsigned long long pk0 = 0, pk1 = 0;
+    int touchall_cnt = 0;
+    unsigned oldb[RB];
+#pragma unroll
+    for (int b = 0; b < RB; b++) {  // every lane issues: an inactive lane ORs 0 into its own word
+      oldb[b] = 0;
+      if (b >= nloc) break;
+      const unsigned bit = 1u << (int)((r0 + b) & (WIN - 1));
+      const bool on = lane < ntb[b];
+      oldb[b] = __hip_atomic_fetch_or(&P.mask[on ? TB[b] : lane], on ? bit : 0u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (glob_end) {
+      const unsigned bit = 1u << (int)((r0 + nbat - 1) & (WIN - 1));
+      for (int c = lane; c < D.W; c += 64)
+        touchall_cnt += __builtin_popcount(__hip_atomic_fetch_or(&P.mask[c], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
+    }
+#pragma unroll
+    for (int b = 0; b < RB; b++) {
+      const unsigned bit = 1u << (int)((r0 + b) & (WIN - 1));
+      const unsigned long long c = (b < nloc && lane < ntb[b]) ? (unsigned long long)__builtin_popcount(oldb[b] & ~bit) : 0ull;
+      if (b < 4) pk0 += c << (16 * (b & 3));
+      else pk1 += c << (16 * (b & 3));
+    }
+    unsigned long long s0 = 0, s1 = 0;
+    for (int l = 0; l < ntmax; l++) {
+      s0 += (unsigned long long)mk64(rlu(lo32((int64_t)pk0), l), rlu(hi32((int64_t)pk0), l));
+      s1 += (unsigned long long)mk64(rlu(lo32((int64_t)pk1), l), rlu(hi32((int64_t)pk1), l));
+    }
+    const int tall = glob_end ? wsum(touchall_cnt) : 0;
+    if (lane == 0) {
+      if (glob_end) vstore(&S.global_pending, 1);  // a global ends its batch
+      int oldp[RB], totb[RB];
+#pragma unroll
+      for (int b = 0; b < RB; b++) {
+        totb[b] = (int)(((b < 4 ? s0 : s1) >> (16 * (b & 3))) & 0xffffu);
+        if (b == nbat - 1 && glob_end) totb[b] = tall;
+        oldp[b] = b < nbat ? atomicAdd(&L.pred[(int)((r0 + b) & (WIN - 1))], totb[b] - BIG) : 1;
+      }
+      unsigned rdy = 0;
+#pragma unroll
+      for (int b = 0; b < RB; b++)
+        if (b < nbat && oldp[b] + totb[b] - BIG == 0) rdy |= 1u << (int)((r0 + b) & (WIN - 1));
+      if (rdy) atomicOr(&S.ready, rdy);
+    }
+    const unsigned long long tB = mclk();
+    {  // prefetch the next batch's rows while the executors run
+      const long long r1 = r0 + nbat;
+      const int n1 = (int)min((long long)RB, pre - r1);
+      if (n1 > 0) {
+        eb_first = r1;
+        eb_n = n1;
+#pragma unroll
+        for (int b = 0; b < RB; b++) {
+          const size_t row = (size_t)((r1 + b) & (DR - 1));
+          EB[b] = (lane < NE && b < n1) ? D.desc[row * NE + lane] : make_uint4(0, 0, 0, 0);
+          TB[b] = (lane < TMAX && b < n1) ? D.touch_ring[row * TMAX + lane] : -1;
+        }
+      } else {
+        eb_first = -1;
+      }
+    }
+    if (lane == 0) {
+      t_poll = mclk();
+      S.prof[3] += t_poll - t0;
+      S.prof[31] += nbat;
+      S.prof[27] += 1;            // batches
+      S.prof[17] += tA - t0;      // fetch wait + phase A
+      S.prof[18] += tB - tA;      // phase B
+      S.prof[19] += t_poll - tB;  // prefetch issue
+    }
     lds_fence();
   }
   if (dl && pa < D.P) D.pdur_cur[pa] = dur0;
@@ -1225,6 +1314,18 @@ __device__ __forceinline__ bool dict_update(const WPtr<LW>& P, int c, int p, int
     P.plen[c] = d.ord;
   }
   return ok;
+}
+
+// release one worker of slot s: clear the slot's bit; successors waiting on it count down
+template <bool LW>
+__device__ __forceinline__ void release_worker(SLds& L, const WPtr<LW>& P, int s, int c) {
+  const unsigned bit = 1u << s;
+  unsigned succ = __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit;
+  while (succ) {
+    const int b = __builtin_ctz(succ);
+    succ &= succ - 1;
+    if (atomicSub(&L.pred[b], 1) == 1) atomicOr(&L.c.ready, 1u << b);
+  }
 }
 
 // release the workers of slot s (the waiting successors may run) — LDS state only
@@ -1504,6 +1605,21 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     off += 1 + kx;
     phase(20);
   }
+  // ---- every touched worker but w is final: write back and release it now (its waiting
+  // successors may run while w takes the queue refill)
+  if (tl && !isw) {
+    using U4 = typename WPtr<LW>::template P<Q4>;
+    P.nproc[cj] = np;
+    st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
+    P.plen[cj] = dj.ord;
+    P.netocc[cj] = net;
+    P.nbytes[cj] = nbj;
+  }
+  if (nt > 1) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (tl && !isw) release_worker<LW>(L, P, s, cj);
+  }
   // -------------- stimulus_queue_slots_maybe_opened (:4983): only w can have open slots
   int pops = 0;
   if (qmode != 0 && !D.sat_inf) {
@@ -1532,8 +1648,8 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       o.rec(K_PLACE, w, qp, 0, mkd(rlu(dlo(oa), jw), rlu(dhi(oa), jw)), rl(np, jw), -1, 0.0);
     }
   }
-  // ---- write the touched workers back (before the slot releases its successors)
-  if (tl) {
+  // ---- w written back last, then released
+  if (isw) {
     using U4 = typename WPtr<LW>::template P<Q4>;
     P.nproc[cj] = np;
     st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
@@ -1541,11 +1657,11 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     P.netocc[cj] = net;
     P.nbytes[cj] = nbj;
   }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  if (lane == jw) release_worker<LW>(L, P, s, w);
   phase(13);
   // ------------------------------------------------ retire: LDS state, then successors
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS writes above are performed
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  release_slot<LW>(D, L, P, s, false);
   phase(21);
   // replica bookkeeping in HBM (TaskState fields; the walker / globals read them later)
   if (lane == 0) {
@@ -1867,10 +1983,14 @@ template <bool LW>
 __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
   const int lane = lane_id();
+  unsigned long long t_idle = mclk();
   while (true) {
     if (vload(&S.stop)) break;
     const unsigned m = vload(&S.ready);
     if (!m) {
+      const unsigned long long n = mclk();  // 28: executor idle, nothing ready
+      if (lane == 0) atomicAdd(&S.prof[28], n - t_idle);
+      t_idle = n;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
@@ -1911,6 +2031,9 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       break;
     }
     if (cs < 0) {
+      const unsigned long long n = mclk();  // 29: ready slots, none claimable (exact gating)
+      if (lane == 0) atomicAdd(&S.prof[29], n - t_idle);
+      t_idle = n;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
@@ -1931,6 +2054,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       atomicAdd(&S.prof[5], mclk() - t0);
       atomicSub(&S.busy_exe, 1);
     }
+    t_idle = mclk();
   }
 }
 
@@ -2086,6 +2210,10 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
   __syncthreads();
   // ------------------------------------------------------------------- roles
   long long round_start = pos->round_start_saved;
+  // issue priority: the in-order registrar first, then the sequencer and executors; the
+  // batch-tolerant builder / prefetcher / walker take the remaining issue slots
+  if (wave == 3) __builtin_amdgcn_s_setprio(3);
+  else if (wave == 0 || wave >= N_ROLE) __builtin_amdgcn_s_setprio(2);
   if (wave == 0) {
     if (pos->round_end < 0) round_start = 0;
     role_seq<LW>(D, L, P, round_start);
@@ -2148,6 +2276,7 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
       for (int i = 0; i < 16; i++) c->prof2[i] = (unsigned long long)dv[i];
     }
     for (int i = 0; i < 16; i++) c->prof[i < 8 ? i : 7] = i < 8 ? S.prof[16 + i] : c->prof[7];
+    for (int i = 0; i < 8; i++) c->prof3[i] = S.prof[24 + i];
     pos->seq = S.seq_pos;
 
     pos->reg = S.reg_pos;

@@ -238,6 +238,7 @@ dgp_engine* dgp_create(int device) {
     const size_t st = (size_t)S::WIN * S::PLC;
     int rc = 0;
     rc |= dalloc(e, &e->D.desc, (size_t)S::DR * S::NE, e->allocs);
+    rc |= dalloc(e, &e->D.touch_ring, (size_t)S::DR * S::TMAX, e->allocs);
     rc |= dalloc(e, &e->D.desc_tag, (size_t)S::DR, e->allocs);
     rc |= dalloc(e, &e->D.s2_task, st, e->allocs);
     rc |= dalloc(e, &e->D.s2_worker, st, e->allocs);
@@ -782,12 +783,13 @@ int dgp_stats(dgp_engine* e, int64_t* out, int32_t n) {
   if (!e || !out) return DGP_E_ARG;
   dgp::Ctl c;
   if (int rc = read_ctl(e, &c)) return rc;
-  int64_t v[30] = {(int64_t)c.n_placed, c.rounds_nonempty, c.dr_steps, c.n_global_events, (int64_t)c.rec_used,
+  int64_t v[38] = {(int64_t)c.n_placed, c.rounds_nonempty, c.dr_steps, c.n_global_events, (int64_t)c.rec_used,
                    (int64_t)c.walk_pos};
   for (int i = 0; i < 8; i++) v[6 + i] = (int64_t)c.prof[i];
   for (int i = 0; i < 16; i++) v[14 + i] = (int64_t)c.prof2[i];
+  for (int i = 0; i < 8; i++) v[30 + i] = (int64_t)c.prof3[i];
 
-  for (int i = 0; i < n && i < 30; i++) out[i] = v[i];
+  for (int i = 0; i < n && i < 38; i++) out[i] = v[i];
   return 0;
 }
 

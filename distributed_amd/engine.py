@@ -173,11 +173,11 @@ class PlacementEngine:
         self._check(self.lib.dgp_set_timing(self.h, 1 if on else 0), "dgp_set_timing")
 
     def stats(self) -> dict:
-        out = np.zeros(30, np.int64)
-        self._check(self.lib.dgp_stats(self.h, _ptr(out), 30), "dgp_stats")
+        out = np.zeros(38, np.int64)
+        self._check(self.lib.dgp_stats(self.h, _ptr(out), 38), "dgp_stats")
         return dict(zip(("placements", "rounds", "dr_steps", "global_stimuli", "records", "walk_pos",
                          "cyc_setup", "cyc_local_steps", "cyc_global", "cyc_finish", "cyc_reserve", "cyc_max_step",
-                         "cyc_exec_max", "cyc_exec_sum") + tuple(f"wave_phase{i}" for i in range(16)),
+                         "cyc_exec_max", "cyc_exec_sum") + tuple(f"wave_phase{i}" for i in range(16)) + tuple(f"stall{i}" for i in range(8)),
                         map(int, out)))
 
     def kernel_times(self) -> dict:

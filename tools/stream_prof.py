@@ -19,5 +19,10 @@ print(f"run_rounds {dt:.3f}s  {e.num_placements() / dt / 1e6:.3f} M placements/s
 for i in range(16):
     print(f"  [{i:2d}] {names[i]:28s} {P[i]:>15d}  per stimulus {P[i] / n:10.1f}")
 X = [st[k] for k in ("cyc_setup", "cyc_local_steps", "cyc_global", "cyc_finish", "cyc_reserve", "cyc_max_step", "cyc_exec_max", "cyc_exec_sum")]
-for i, nm in enumerate(["exe: w dict+line load", "exe: needs_dec", "exe: cand comm/occ/key", "exe: argmin", "exe: place commit", "exe: release_slot", "exe: finish fence", "-"]):
+for i, nm in enumerate(["exe: w dict+line load", "exe: needs_dec", "REG fetch+phase A", "REG phase B", "REG prefetch issue", "exe: release_slot", "exe: finish fence", "-"]):
     print(f"  [x{i}] {nm:28s} {X[i]:>15d}  per stimulus {X[i] / n:10.1f}")
+
+S = [st.get(f"stall{i}", 0) for i in range(8)]
+for i, nm in enumerate(["REG window full", "REG desc not prefetched", "REG global pending", "REG batches",
+                        "EXE idle (nothing ready)", "EXE ready but gated", "SEQ waits oldest slot", "REG stimuli registered"]):
+    print(f"  [s{i}] {nm:28s} {S[i]:>15d}  per stimulus {S[i] / n:10.1f}")
