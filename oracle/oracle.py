@@ -136,3 +136,68 @@ def load_fixture(path: str):
     g["name"] = meta["name"]
     exp = {k: z[k] for k in z.files if k.startswith(("pl_", "round_", "final_"))}
     return g, meta["config"], exp, meta
+
+
+# ----------------------------------------------------------------- WorkStealing
+STEAL_INPUTS = ("nthreads", "occ", "nproc", "wnbytes", "idle", "sat", "victim", "duration", "fast", "dep_ptr",
+                "dep_idx", "data_nbytes", "data_get_nbytes", "data_holder")
+
+
+def holder_csr(data_holder):
+    """who_has of each data task as CSR (a single holder, or none when released)."""
+    h = np.asarray(data_holder, np.int32)
+    ptr = np.zeros(len(h) + 1, np.int64)
+    ptr[1:] = np.cumsum(h >= 0)
+    return ptr, h[h >= 0].astype(np.int32)
+
+
+def steal_balance(p: dict) -> dict:
+    """steal_time_ratio for every task + one WorkStealing.balance() over problem ``p``
+    (the input arrays of a ``tests/golden/steal_*.npz`` fixture)."""
+    L = lib()
+    fn = L.orc_steal_balance
+    W = len(p["nthreads"])
+    T = len(p["victim"])
+    keep = []
+
+    def a(x, dt):
+        v = np.ascontiguousarray(x, dtype=dt)
+        keep.append(v)
+        return _ptr(v)
+
+    hptr, hidx = holder_csr(p["data_holder"])
+    out = dict(level=np.zeros(T, np.int8), st_task=np.zeros(T, np.int32), st_victim=np.zeros(T, np.int32),
+               st_thief=np.zeros(T, np.int32), st_level=np.zeros(T, np.int32), st_cost=np.zeros(T),
+               st_occ_victim=np.zeros(T), st_occ_thief=np.zeros(T), inflight_occ=np.zeros(W),
+               inflight_tasks=np.zeros(W, np.int32), idle_after=np.zeros(W, np.uint8), sat_after=np.zeros(W, np.uint8))
+    n = C.c_int64(0)
+    fn.restype = C.c_int
+    rc = fn(C.c_int32(W), a(p["nthreads"], np.int32), a(p["occ"], np.float64), a(p["nproc"], np.int32),
+            a(p["wnbytes"], np.int64), a(p["idle"], np.uint8), a(p["sat"], np.uint8), C.c_double(float(p["total_occ"])),
+            C.c_int64(int(p["total_nthreads"])), C.c_int64(int(p["bandwidth"])), C.c_int64(T),
+            a(p["victim"], np.int32), a(p["duration"], np.float64), a(p["fast"], np.uint8), a(p["dep_ptr"], np.int64),
+            a(p["dep_idx"], np.int32), a(p["data_nbytes"], np.int64), a(p["data_get_nbytes"], np.int64),
+            a(hptr, np.int64), a(hidx, np.int32),
+            *[_ptr(out[k]) for k in ("level", "st_task", "st_victim", "st_thief", "st_level", "st_cost",
+                                     "st_occ_victim", "st_occ_thief")],
+            C.byref(n), *[_ptr(out[k]) for k in ("inflight_occ", "inflight_tasks", "idle_after", "sat_after")])
+    if rc != 0:
+        raise RuntimeError(f"oracle steal_balance failed ({rc})")
+    k = int(n.value)
+    for key in ("st_task", "st_victim", "st_thief", "st_level", "st_cost", "st_occ_victim", "st_occ_thief"):
+        out[key] = out[key][:k]
+    return out
+
+
+def load_steal_fixture(path: str):
+    """Load a ``tests/golden/steal_*.npz`` fixture -> (problem inputs, expected outputs, meta)."""
+    import json
+
+    z = np.load(path, allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    p = {k: z[k] for k in STEAL_INPUTS}
+    for k in ("total_occ", "total_nthreads", "bandwidth"):
+        p[k] = z[k][()]
+    exp = {k: z[k] for k in ("level", "st_task", "st_level", "st_cost", "st_victim", "st_occ_victim", "st_thief",
+                             "st_occ_thief", "inflight_occ", "inflight_tasks", "idle_after", "sat_after")}
+    return p, exp, meta

@@ -15,7 +15,13 @@ def pytest_configure(config):
 
 
 def golden_files():
-    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz"))
+    """Placement replay fixtures (tests/golden/gen_golden.py)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("steal_"))
+
+
+def steal_files():
+    """WorkStealing balance fixtures (tests/golden/gen_steal.py)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("steal_") and f.endswith(".npz"))
 
 
 @pytest.fixture(scope="session")
