@@ -37,6 +37,9 @@ SIGNATURES = {
     "dgp_kernel_times": (C.c_int, [_P, _P, _P, C.c_int32]),
     "dgp_set_timing": (C.c_int, [_P, C.c_int]),
     "dgp_stats": (C.c_int, [_P, _P, C.c_int32]),
+    "dgp_steal_balance": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_int64, C.c_int64,
+                                    C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, _P, _P,
+                                    _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
 }
 
 ABI_VERSION = 1

@@ -1,0 +1,380 @@
+// dgp_steal.h — WorkStealing on MI355X: the cost levels of every processing task
+// (steal_time_ratio, /root/reference/distributed/stealing.py:241-277) and one
+// balance() call (:401-503), bit-exact with the reference (tests/golden/steal_*.npz).
+//
+// What makes balance() parallel: worker_objective (scheduler.py:3131-3146) reads the
+// plain WorkerState.occupancy, which a balance() never changes (steals are only
+// requested; in-flight occupancy is a separate account). So every examined task's
+// thief = argmin over the thief set of a key that depends only on (task, worker), and
+// the thief set only shrinks. k_best_thief evaluates that argmin for all stealable
+// tasks at once against the initial thief set (one wave per task, the thieves spread
+// over the lanes). k_balance then walks the bins in the reference's order in one wave:
+// acceptance test, in-flight accounts, thief removal, check_idle_saturated. It re-runs
+// the argmin (wave-parallel, current thief set) only when the precomputed thief has
+// since left the set — exact, because the argmin over a subset that still contains the
+// original winner is that winner.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dgp {
+namespace steal {
+
+constexpr int N_LEVELS = 15;     // len(WorkStealing.cost_multipliers) (stealing.py:83-85)
+constexpr double LATENCY = 0.1;  // stealing.py:37
+
+struct Prob {
+  int W;
+  const int32_t* nthreads;
+  const double* occ;       // WorkerState.occupancy
+  const int32_t* nproc;    // len(ws.processing)
+  const int64_t* wnbytes;  // ws.nbytes
+  const uint8_t* idle;     // membership of SchedulerState.idle
+  const uint8_t* sat;      // membership of SchedulerState.saturated
+  double total_occ;
+  int64_t total_nthreads;
+  int64_t bw;
+  int64_t T;
+  const int32_t* victim;   // processing_on
+  const double* duration;  // get_task_duration
+  const uint8_t* fast;     // prefix in fast_tasks
+  const int64_t* dep_ptr;
+  const int32_t* dep_idx;
+  const int64_t* d_nbytes;      // raw nbytes (get_comm_cost)
+  const int64_t* d_get_nbytes;  // get_nbytes() (worker_objective, steal_time_ratio)
+  const int64_t* h_ptr;         // who_has (CSR)
+  const int32_t* h_idx;
+  // work
+  int32_t* key;       // [T] level * W + victim, or N_LEVELS * W when not stealable
+  int32_t* order;     // [T] task ids sorted by key (stable)
+  int32_t* key_sorted;
+  int32_t* bin_cnt;   // [N_LEVELS * W + 1]
+  int32_t* bin_ptr;   // [N_LEVELS * W + 1] exclusive scan of bin_cnt
+  int32_t* s_best;    // [T] per sorted position: thief over the initial thief set
+  double* s_cct;      // comm cost to that thief
+  double* s_ccv;      // comm cost to the victim
+  double* s_dur;      // duration
+  // outputs
+  int8_t* level;
+  int32_t *st_task, *st_victim, *st_thief, *st_level;
+  double *st_cost, *st_occ_victim, *st_occ_thief;
+  long long* n_steals;
+  double* inflight_occ;
+  int32_t* inflight_tasks;
+  uint8_t *idle_out, *sat_out;
+};
+
+__device__ __forceinline__ bool holds(const Prob& P, int d, int w) {
+  for (int64_t k = P.h_ptr[d]; k < P.h_ptr[d + 1]; k++)
+    if (P.h_idx[k] == w) return true;
+  return false;
+}
+
+// ------------------------------------------------------------------------ levels
+// steal_time_ratio -> level (-1: not stealable) and the bin key
+__global__ void k_steal_levels(Prob P) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= P.T) return;
+  int lv;
+  if (P.fast[t]) {
+    lv = -1;                                       // :252-253
+  } else if (P.dep_ptr[t] == P.dep_ptr[t + 1]) {
+    lv = 0;                                        // :255-256
+  } else {
+    const double compute = P.duration[t];
+    if (!(compute != 0.0)) {
+      lv = -1;                                     // :260-265 long-running
+    } else {
+      int64_t nb = 0;                              // get_nbytes_deps
+      for (int64_t k = P.dep_ptr[t]; k < P.dep_ptr[t + 1]; k++) nb += P.d_get_nbytes[P.dep_idx[k]];
+      const double cm = ((double)nb / (double)P.bw + LATENCY) / compute;
+      lv = (int)rint(log2(cm) + 6.0);              // int(round(...)): half-even
+      if (lv < 1) lv = 1;
+      else if (lv >= N_LEVELS) lv = -1;
+    }
+  }
+  P.level[t] = (int8_t)lv;
+  const int k = lv >= 0 ? lv * P.W + P.victim[t] : N_LEVELS * P.W;
+  P.key[t] = k;
+  atomicAdd(&P.bin_cnt[k], 1);
+}
+
+// ------------------------------------------------------------------ objective
+struct Obj {
+  double start;
+  int64_t nb;
+  int w;
+};
+__device__ __forceinline__ bool obj_less(const Obj& a, const Obj& b) {
+  if (a.start != b.start) return a.start < b.start;
+  if (a.nb != b.nb) return a.nb < b.nb;
+  return a.w < b.w;
+}
+__device__ __forceinline__ Obj obj_shfl_xor(const Obj& o, int m) {
+  Obj r;
+  r.start = __shfl_xor(o.start, m);
+  r.nb = __shfl_xor(o.nb, m);
+  r.w = __shfl_xor(o.w, m);
+  return r;
+}
+
+// worker_objective (scheduler.py:3131-3146) of task t on worker w (+ canonical index)
+__device__ __forceinline__ Obj objective(const Prob& P, int64_t t, int w) {
+  int64_t comm = 0;
+  for (int64_t k = P.dep_ptr[t]; k < P.dep_ptr[t + 1]; k++) {
+    const int d = P.dep_idx[k];
+    if (!holds(P, d, w)) comm += P.d_get_nbytes[d];
+  }
+  const double stack = P.occ[w] / (double)P.nthreads[w];
+  return Obj{stack + (double)comm / (double)P.bw, P.wnbytes[w], w};
+}
+
+// get_comm_cost (scheduler.py:3006-3022)
+__device__ __forceinline__ double comm_cost(const Prob& P, int64_t t, int w) {
+  int64_t nb = 0;
+  for (int64_t k = P.dep_ptr[t]; k < P.dep_ptr[t + 1]; k++) {
+    const int d = P.dep_idx[k];
+    if (!holds(P, d, w)) nb += P.d_nbytes[d];
+  }
+  return (double)nb / (double)P.bw;
+}
+
+// argmin of the objective over the workers with th[w] set (one wave; all lanes return it)
+template <class TH>
+__device__ __forceinline__ Obj wave_argmin(const Prob& P, int64_t t, TH th) {
+  const int lane = threadIdx.x & 63;
+  Obj best{INFINITY, INT64_MAX, INT32_MAX};
+  for (int w = lane; w < P.W; w += 64) {
+    if (!th(w)) continue;
+    const Obj o = objective(P, t, w);
+    if (obj_less(o, best)) best = o;
+  }
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) {
+    const Obj o = obj_shfl_xor(best, m);
+    if (obj_less(o, best)) best = o;
+  }
+  return best;
+}
+
+// one wave per stealable task (sorted position i): thief over the initial thief set
+__global__ void k_best_thief(Prob P, const int32_t* n_stealable) {
+  const int i = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (i >= *n_stealable) return;
+  const int64_t t = P.order[i];
+  const Obj b = wave_argmin(P, t, [&](int w) { return P.idle[w] != 0; });
+  if ((threadIdx.x & 63) == 0) {
+    P.s_best[i] = b.w < P.W ? b.w : -1;
+    P.s_cct[i] = b.w < P.W ? comm_cost(P, t, b.w) : 0.0;
+    P.s_ccv[i] = comm_cost(P, t, P.victim[t]);
+    P.s_dur[i] = P.duration[t];
+  }
+}
+
+// ---------------------------------------------------------------------- balance
+// One wave; all per-worker balance state in LDS: occupancy, in-flight occupancy and
+// task deltas, thief / idle / saturated flags, the victim list.
+__global__ void __launch_bounds__(64) k_balance(Prob P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int W = P.W;
+  const int lane = threadIdx.x;
+  double* occ = (double*)smem;
+  double* ifo = occ + W;
+  int32_t* ift = (int32_t*)(ifo + W);
+  int32_t* vs = ift + W;                    // victims of the current level
+  uint8_t* thief = (uint8_t*)(vs + W);
+  uint8_t* idle = thief + W;
+  uint8_t* sat = idle + W;
+  uint8_t* taken = sat + W;                 // topk scratch
+  int nth_ = 0, nsat_ = 0;
+  for (int w = lane; w < W; w += 64) {
+    occ[w] = P.occ[w];
+    ifo[w] = 0.0;
+    ift[w] = 0;
+    idle[w] = P.idle[w];
+    sat[w] = P.sat[w];
+    thief[w] = P.idle[w];
+    taken[w] = 0;
+    nth_ += P.idle[w] != 0;
+    nsat_ += P.sat[w] != 0;
+  }
+  for (int m = 32; m > 0; m >>= 1) {
+    nth_ += __shfl_xor(nth_, m);
+    nsat_ += __shfl_xor(nsat_, m);
+  }
+  __syncthreads();
+  int n_thieves = nth_;
+  long long ns = 0;
+  const double avg = P.total_occ / (double)P.total_nthreads;
+  auto combined = [&](int w) { return occ[w] + ifo[w]; };                       // :505-506
+  auto is_unoccupied = [&](int w, double o, int np) {                           // scheduler.py:2997-3004
+    return np < P.nthreads[w] || o < P.nthreads[w] * avg / 2;
+  };
+  auto finish = [&]() {
+    for (int w = lane; w < W; w += 64) {
+      P.inflight_occ[w] = ifo[w];
+      P.inflight_tasks[w] = ift[w];
+      P.idle_out[w] = idle[w];
+      P.sat_out[w] = sat[w];
+    }
+    if (lane == 0) *P.n_steals = ns;
+  };
+  if (n_thieves == 0 || n_thieves == W) {  // :410-411
+    finish();
+    return;
+  }
+  // potential victims (:412-428)
+  bool live = false;
+  int npv = 0;
+  if (nsat_) {
+    if (nsat_ >= 20) {
+      live = true;
+    } else {
+      for (int w0 = 0; w0 < W; w0 += 64) {  // ascending index, then stable sort
+        const int w = w0 + lane;
+        const bool in = w < W && sat[w];
+        const unsigned long long m = __ballot(in);
+        const int pos = npv + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+        if (in) vs[pos] = w;
+        npv += __builtin_popcountll(m);
+      }
+    }
+  } else {  // topk(10, workers, key=combined occupancy): largest first, ties by index
+    for (int k = 0; k < 10 && k < W; k++) {
+      double bo = -INFINITY;
+      int bw_ = INT32_MAX;
+      for (int w = lane; w < W; w += 64) {
+        if (taken[w]) continue;
+        const double o = combined(w);
+        if (o > bo || (o == bo && w < bw_)) bo = o, bw_ = w;
+      }
+      for (int m = 32; m > 0; m >>= 1) {
+        const double o2 = __shfl_xor(bo, m);
+        const int w2 = __shfl_xor(bw_, m);
+        if (o2 > bo || (o2 == bo && w2 < bw_)) bo = o2, bw_ = w2;
+      }
+      if (bw_ >= W) break;
+      if (lane == 0) taken[bw_] = 1;
+      __syncthreads();
+      if (combined(bw_) > 0.2 && P.nproc[bw_] + ift[bw_] > P.nthreads[bw_] && !thief[bw_]) {
+        if (lane == 0) vs[npv] = bw_;
+        npv++;
+      }
+    }
+    __syncthreads();
+    if (npv == 0) {
+      finish();
+      return;
+    }
+  }
+  if (!live && lane == 0) {  // sorted(potential_victims, key=combined, reverse=True): stable
+    for (int a = 1; a < npv; a++) {
+      const int v = vs[a];
+      const double o = combined(v);
+      int b = a - 1;
+      while (b >= 0 && combined(vs[b]) < o) {
+        vs[b + 1] = vs[b];
+        b--;
+      }
+      vs[b + 1] = v;
+    }
+  }
+  __syncthreads();
+  for (int level = 0; level < N_LEVELS; level++) {  // :431
+    if (n_thieves == 0) break;
+    if (live) {  // list(potential_victims): the saturated set now, ascending index
+      npv = 0;
+      __syncthreads();
+      for (int w0 = 0; w0 < W; w0 += 64) {
+        const int w = w0 + lane;
+        const bool in = w < W && sat[w];
+        const unsigned long long m = __ballot(in);
+        const int pos = npv + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+        if (in) vs[pos] = w;
+        npv += __builtin_popcountll(m);
+      }
+      __syncthreads();
+    }
+    for (int vi = 0; vi < npv; vi++) {  // :434
+      const int v = vs[vi];
+      const int b0 = P.bin_ptr[level * W + v], b1 = P.bin_ptr[level * W + v + 1];
+      if (b0 == b1 || n_thieves == 0) continue;
+      for (int c0 = b0; c0 < b1; c0 += 64) {  // 64 tasks of the bin per load round
+        const int i = c0 + lane;
+        const bool okl = i < b1;
+        const int tq = okl ? P.order[i] : 0;
+        const int bq = okl ? P.s_best[i] : 0;
+        const double cq = okl ? P.s_cct[i] : 0.0;
+        const double vq = okl ? P.s_ccv[i] : 0.0;
+        const double dq = okl ? P.s_dur[i] : 0.0;
+        const int nq = min(64, b1 - c0);
+        for (int j = 0; j < nq; j++) {  // :439
+          if (n_thieves == 0) break;
+          const int t = __builtin_amdgcn_readlane(tq, j);
+          int th = __builtin_amdgcn_readlane(bq, j);
+          double cct = __shfl(cq, j);
+          const double ccv = __shfl(vq, j);
+          const double compute = __shfl(dq, j);
+          if (th < 0 || !thief[th]) {  // the precomputed thief left the set: argmin again
+            const Obj b = wave_argmin(P, t, [&](int w) { return thief[w] != 0; });
+            th = b.w;
+            cct = comm_cost(P, t, th);
+          }
+          const double occ_thief = combined(th);
+          const double occ_victim = combined(v);
+          if (occ_thief + cct + compute <= occ_victim - (ccv + compute) / 2) {  // :462-465
+            // move_task_request (:279-331) -> _add_to_in_flight (:191-199)
+            if (lane == 0) {
+              ifo[v] = ifo[v] - (compute + ccv);
+              ifo[th] = ifo[th] + (compute + cct);
+              ift[v] -= 1;
+              ift[th] += 1;
+              P.st_task[ns] = t;
+              P.st_victim[ns] = v;
+              P.st_thief[ns] = th;
+              P.st_level[ns] = level;
+              P.st_cost[ns] = compute + ccv;
+              P.st_occ_victim[ns] = occ_victim;
+              P.st_occ_thief[ns] = occ_thief;
+            }
+            __syncthreads();
+            ns++;
+            if (!is_unoccupied(th, combined(th), P.nproc[th] + ift[th])) {  // :487-493
+              if (lane == 0) thief[th] = 0;
+              __syncthreads();
+              n_thieves--;
+            }
+          }
+        }
+      }
+      // check_idle_saturated(victim, occ=combined) (scheduler.py:2949-2995)
+      double o = combined(v);
+      if (o < 0) o = occ[v];  // :2974-2975
+      const int p = P.nproc[v];
+      const int nc = P.nthreads[v];
+      uint8_t id = 0, sa = 0;
+      if (is_unoccupied(v, o, p)) {
+        id = 1;
+      } else if (p > nc) {
+        const double pending = o * (double)(p - nc) / (double)(p * nc);
+        if (0.4 < pending && pending > 1.9 * avg) sa = 1;
+      }
+      if (lane == 0) {
+        idle[v] = id;
+        sat[v] = sa;
+      }
+      __syncthreads();
+    }
+  }
+  finish();
+}
+
+inline size_t balance_lds_bytes(int W) { return (size_t)W * (8 + 8 + 4 + 4 + 4); }
+
+}  // namespace steal
+
+__global__ void k_iota32(int32_t* a, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = i;
+}
+}  // namespace dgp

@@ -25,6 +25,9 @@
 #include "../../include/dgplace.h"
 #include "dgp_device.h"
 #include "dgp_stream.h"
+#include "dgp_steal.h"
+
+#include <hipcub/hipcub.hpp>
 
 // =================================================================== host side
 
@@ -51,8 +54,8 @@ struct dgp_engine {
   bool stream_used = false;  // the stream engine ran: the round-kernel path is no longer valid
   // timing: (start, stop) event pairs recorded around launches, resolved lazily
   bool timing = false;
-  double kms[4] = {0, 0, 0, 0};
-  int64_t klaunch[4] = {0, 0, 0, 0};
+  double kms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t klaunch[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   std::vector<hipEvent_t> evpool;
   std::vector<int> evkind;
   size_t evused = 0;
@@ -569,7 +572,7 @@ int dgp_reset(dgp_engine* e) {
   HIPCHK(e, hipStreamSynchronize(s));
   e->graph_done = false;
   e->evused = 0;
-  for (int k = 0; k < 4; k++) {
+  for (int k = 0; k < 8; k++) {
     e->kms[k] = 0;
     e->klaunch[k] = 0;
   }
@@ -760,7 +763,7 @@ int dgp_get_task_states(dgp_engine* e, uint8_t* state) {
 int dgp_kernel_times(dgp_engine* e, double* ms, int64_t* launches, int32_t n) {
   if (!e) return DGP_E_ARG;
   if (int rc = resolve_timing(e)) return rc;
-  for (int k = 0; k < n && k < 4; k++) {
+  for (int k = 0; k < n && k < 8; k++) {
     if (ms) ms[k] = e->kms[k];
     if (launches) launches[k] = e->klaunch[k];
   }
@@ -790,6 +793,148 @@ int dgp_stats(dgp_engine* e, int64_t* out, int32_t n) {
   for (int i = 0; i < 8; i++) v[30 + i] = (int64_t)c.prof3[i];
 
   for (int i = 0; i < n && i < 38; i++) out[i] = v[i];
+  return 0;
+}
+
+
+// ------------------------------------------------------------------ WorkStealing
+// WorkStealing.balance (stealing.py:401-503) over host arrays (see include/dgplace.h).
+int dgp_steal_balance(dgp_engine* e, int32_t W, const int32_t* nthreads, const double* occ, const int32_t* nproc,
+                      const int64_t* wnbytes, const uint8_t* idle, const uint8_t* sat, double total_occ,
+                      int64_t total_nthreads, int64_t bandwidth, int64_t T, const int32_t* victim,
+                      const double* duration, const uint8_t* fast, const int64_t* dep_ptr, const int32_t* dep_idx,
+                      int64_t n_data, const int64_t* d_nbytes, const int64_t* d_get_nbytes, const int64_t* h_ptr,
+                      const int32_t* h_idx, int8_t* level_out, int32_t* st_task, int32_t* st_victim,
+                      int32_t* st_thief, int32_t* st_level, double* st_cost, double* st_occ_victim,
+                      double* st_occ_thief, int64_t* n_steals, double* inflight_occ, int32_t* inflight_tasks,
+                      uint8_t* idle_out, uint8_t* sat_out) {
+  namespace S = dgp::steal;
+  if (!e) return DGP_E_ARG;
+  if (W <= 0 || T < 0 || n_data < 0 || bandwidth <= 0 || total_nthreads <= 0 || !nthreads || !occ || !nproc ||
+      !wnbytes || !idle || !sat || !n_steals || !inflight_occ || !inflight_tasks || !idle_out || !sat_out)
+    return fail(e, DGP_E_ARG, "dgp_steal_balance: bad sizes or null pointers");
+  if (S::balance_lds_bytes(W) > 160 * 1024) return fail(e, DGP_E_ARG, "dgp_steal_balance: too many workers");
+  if ((size_t)W * S::N_LEVELS >= (1u << 30)) return fail(e, DGP_E_ARG, "dgp_steal_balance: W too large");
+  // the shapes the kernels assume, checked on the host
+  for (int32_t w = 0; w < W; w++)
+    if (nthreads[w] <= 0) return fail(e, DGP_E_ARG, "dgp_steal_balance: nthreads must be positive");
+  const int64_t E = T ? dep_ptr[T] : 0;
+  if (T && (dep_ptr[0] != 0 || E < 0)) return fail(e, DGP_E_ARG, "dgp_steal_balance: dep_ptr");
+  for (int64_t t = 0; t < T; t++) {
+    if (victim[t] < 0 || victim[t] >= W) return fail(e, DGP_E_ARG, "dgp_steal_balance: victim out of range");
+    if (dep_ptr[t + 1] < dep_ptr[t]) return fail(e, DGP_E_ARG, "dgp_steal_balance: dep_ptr not monotone");
+  }
+  for (int64_t k = 0; k < E; k++)
+    if (dep_idx[k] < 0 || dep_idx[k] >= n_data) return fail(e, DGP_E_ARG, "dgp_steal_balance: dep_idx out of range");
+  const int64_t H = n_data ? h_ptr[n_data] : 0;
+  for (int64_t d = 0; d < n_data; d++)
+    if (h_ptr[d + 1] < h_ptr[d]) return fail(e, DGP_E_ARG, "dgp_steal_balance: h_ptr not monotone");
+  for (int64_t k = 0; k < H; k++)
+    if (h_idx[k] < 0 || h_idx[k] >= W) return fail(e, DGP_E_ARG, "dgp_steal_balance: holder out of range");
+  HIPCHK(e, hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  const int NK = S::N_LEVELS * W + 1;
+  // one arena for inputs, work and outputs
+  std::vector<std::pair<void**, size_t>> parts;
+  S::Prob P{};
+  int32_t *d_nthreads, *d_nproc, *d_victim, *d_dep_idx, *d_h_idx, *d_vals;
+  double *d_occ, *d_dur, *d_ifo;
+  int64_t *d_wnb, *d_dep_ptr, *d_dnb, *d_dgnb, *d_h_ptr;
+  uint8_t *d_idle, *d_sat, *d_fast, *d_idle_o, *d_sat_o;
+  long long* d_ns;
+  void* d_tmp = nullptr;
+  size_t tmp_sort = 0, tmp_scan = 0;
+  int32_t* keys_sorted = nullptr;
+  const int Tn = (int)T;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
+                                     (int32_t*)nullptr, std::max(Tn, 1), 0, 32, s);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_scan, (int32_t*)nullptr, (int32_t*)nullptr, NK, s);
+  const size_t tmp_bytes = std::max(tmp_sort, tmp_scan);
+  auto add = [&](auto** p, size_t n) { parts.push_back({(void**)p, (n ? n : 1) * sizeof(**p)}); };
+  add(&d_nthreads, W); add(&d_occ, W); add(&d_nproc, W); add(&d_wnb, W); add(&d_idle, W); add(&d_sat, W);
+  add(&d_victim, T); add(&d_dur, T); add(&d_fast, T); add(&d_dep_ptr, T + 1); add(&d_dep_idx, E);
+  add(&d_dnb, n_data); add(&d_dgnb, n_data); add(&d_h_ptr, n_data + 1); add(&d_h_idx, H);
+  add(&P.key, T); add(&P.order, T); add(&keys_sorted, T); add(&d_vals, T); add(&P.bin_cnt, NK); add(&P.bin_ptr, NK);
+  add(&P.s_best, T); add(&P.s_cct, T); add(&P.s_ccv, T); add(&P.s_dur, T);
+  add(&P.level, T); add(&P.st_task, T); add(&P.st_victim, T); add(&P.st_thief, T); add(&P.st_level, T);
+  add(&P.st_cost, T); add(&P.st_occ_victim, T); add(&P.st_occ_thief, T); add(&d_ns, 1);
+  add(&d_ifo, W); add(&P.inflight_tasks, W); add(&d_idle_o, W); add(&d_sat_o, W);
+  size_t total = tmp_bytes + 256;
+  for (auto& pr : parts) total += (pr.second + 255) / 256 * 256;
+  char* arena = nullptr;
+  HIPCHK(e, hipMalloc(&arena, total));
+  size_t off = 0;
+  d_tmp = arena;
+  off += (tmp_bytes + 255) / 256 * 256;
+  for (auto& pr : parts) {
+    *pr.first = arena + off;
+    off += (pr.second + 255) / 256 * 256;
+  }
+  auto h2d = [&](void* dst, const void* src, size_t bytes) {
+    return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+  };
+  hipError_t st = hipSuccess;
+  auto chk = [&](hipError_t x) {
+    if (x != hipSuccess && st == hipSuccess) st = x;
+  };
+  chk(h2d(d_nthreads, nthreads, W * 4)); chk(h2d(d_occ, occ, W * 8)); chk(h2d(d_nproc, nproc, W * 4));
+  chk(h2d(d_wnb, wnbytes, W * 8)); chk(h2d(d_idle, idle, W)); chk(h2d(d_sat, sat, W));
+  chk(h2d(d_victim, victim, T * 4)); chk(h2d(d_dur, duration, T * 8)); chk(h2d(d_fast, fast, T));
+  chk(h2d(d_dep_ptr, dep_ptr, (T + 1) * 8)); chk(h2d(d_dep_idx, dep_idx, E * 4));
+  chk(h2d(d_dnb, d_nbytes, n_data * 8)); chk(h2d(d_dgnb, d_get_nbytes, n_data * 8));
+  chk(h2d(d_h_ptr, h_ptr, (n_data + 1) * 8)); chk(h2d(d_h_idx, h_idx, H * 4));
+  chk(hipMemsetAsync(P.bin_cnt, 0, NK * 4, s));
+  if (st != hipSuccess) {
+    hipFree(arena);
+    return fail(e, DGP_E_HIP, std::string("dgp_steal_balance: upload: ") + hipGetErrorString(st));
+  }
+  P.W = W; P.nthreads = d_nthreads; P.occ = d_occ; P.nproc = d_nproc; P.wnbytes = d_wnb; P.idle = d_idle;
+  P.sat = d_sat; P.total_occ = total_occ; P.total_nthreads = total_nthreads; P.bw = bandwidth; P.T = T;
+  P.victim = d_victim; P.duration = d_dur; P.fast = d_fast; P.dep_ptr = d_dep_ptr; P.dep_idx = d_dep_idx;
+  P.d_nbytes = d_dnb; P.d_get_nbytes = d_dgnb; P.h_ptr = d_h_ptr; P.h_idx = d_h_idx; P.key_sorted = keys_sorted;
+  P.n_steals = d_ns; P.inflight_occ = d_ifo; P.idle_out = d_idle_o; P.sat_out = d_sat_o;
+  int bits = 1;
+  while ((1ll << bits) < NK) bits++;
+  int rc = 0;
+  if (T > 0) {
+    rc = timed_launch(e, 4, [&] {
+      hipLaunchKernelGGL(S::k_steal_levels, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(dgp::k_iota32, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, d_vals, (int)T);
+      size_t tb = tmp_bytes;
+      hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, P.key, keys_sorted, d_vals, P.order, Tn, 0, bits, s);
+      tb = tmp_bytes;
+      hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, P.bin_cnt, P.bin_ptr, NK, s);
+    });
+    if (!rc) rc = timed_launch(e, 5, [&] {
+      hipLaunchKernelGGL(S::k_best_thief, dim3((unsigned)((T * 64 + 255) / 256)), dim3(256), 0, s, P, P.bin_ptr + NK - 1);
+    });
+  } else {
+    chk(hipMemsetAsync(P.bin_ptr, 0, NK * 4, s));
+  }
+  if (!rc) rc = timed_launch(e, 6, [&] {
+    hipLaunchKernelGGL(S::k_balance, dim3(1), dim3(64), S::balance_lds_bytes(W), s, P);
+  });
+  long long ns = 0;
+  if (!rc) {
+    chk(hipMemcpyAsync(&ns, d_ns, 8, hipMemcpyDeviceToHost, s));
+    chk(hipStreamSynchronize(s));
+  }
+  if (!rc && st == hipSuccess) {
+    *n_steals = ns;
+    auto d2h = [&](void* dst, const void* src, size_t bytes) {
+      if (dst && bytes) chk(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    };
+    d2h(level_out, P.level, T);
+    d2h(st_task, P.st_task, ns * 4); d2h(st_victim, P.st_victim, ns * 4); d2h(st_thief, P.st_thief, ns * 4);
+    d2h(st_level, P.st_level, ns * 4); d2h(st_cost, P.st_cost, ns * 8); d2h(st_occ_victim, P.st_occ_victim, ns * 8);
+    d2h(st_occ_thief, P.st_occ_thief, ns * 8);
+    d2h(inflight_occ, d_ifo, W * 8); d2h(inflight_tasks, P.inflight_tasks, W * 4);
+    d2h(idle_out, d_idle_o, W); d2h(sat_out, d_sat_o, W);
+    chk(hipStreamSynchronize(s));
+  }
+  hipFree(arena);
+  if (rc) return rc;
+  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_balance: ") + hipGetErrorString(st));
   return 0;
 }
 

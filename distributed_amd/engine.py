@@ -25,8 +25,10 @@ DEFAULT_CONFIG = {  # distributed/distributed.yaml:13,16,24,28
     "saturation": 1.1,
 }
 
-# ids of dgp_kernel_times; id 2 is the persistent replay kernel (k_stream; k_replay when P > PD)
-KERNEL_NAMES = ("frontier_release", "candidate_commbytes", "replay", "update_graph")
+# ids of dgp_kernel_times; id 2 is the persistent replay kernel (k_stream; k_replay when P > PD);
+# 4..6 are WorkStealing (levels + bins, thief argmin, balance walk)
+KERNEL_NAMES = ("frontier_release", "candidate_commbytes", "replay", "update_graph", "steal_levels",
+                "steal_thief_argmin", "steal_balance", "unused")
 
 
 class PlacementEngine:
@@ -181,7 +183,56 @@ class PlacementEngine:
                         map(int, out)))
 
     def kernel_times(self) -> dict:
-        ms = np.zeros(4)
-        n = np.zeros(4, np.int64)
-        self._check(self.lib.dgp_kernel_times(self.h, _ptr(ms), _ptr(n), 4), "dgp_kernel_times")
+        ms = np.zeros(8)
+        n = np.zeros(8, np.int64)
+        self._check(self.lib.dgp_kernel_times(self.h, _ptr(ms), _ptr(n), 8), "dgp_kernel_times")
         return {name: (float(ms[i]), int(n[i])) for i, name in enumerate(KERNEL_NAMES)}
+
+    # ------------------------------------------------------------ WorkStealing
+    def steal_balance(self, p: dict) -> dict:
+        """steal_time_ratio for every processing task + one WorkStealing.balance()
+        (distributed/stealing.py:241-277, :401-503) on the device.
+
+        ``p``: nthreads, occ, nproc, wnbytes, idle, sat (per worker); total_occ,
+        total_nthreads, bandwidth; victim, duration, fast, dep_ptr, dep_idx (per task);
+        data_nbytes, data_get_nbytes and who_has as data_holder (one worker or -1) or
+        holder_ptr / holder_idx (CSR). Returns levels, the ordered steal requests and the
+        per-worker in-flight / idle / saturated state after the call.
+        """
+        W = len(p["nthreads"])
+        T = len(p["victim"])
+        if "holder_ptr" in p:
+            hptr, hidx = np.asarray(p["holder_ptr"], np.int64), np.asarray(p["holder_idx"], np.int32)
+        else:
+            h = np.asarray(p["data_holder"], np.int32)
+            hptr = np.zeros(len(h) + 1, np.int64)
+            hptr[1:] = np.cumsum(h >= 0)
+            hidx = h[h >= 0].astype(np.int32)
+        keep = []
+
+        def a(x, dt):
+            v = np.ascontiguousarray(x, dtype=dt)
+            keep.append(v)
+            return _ptr(v)
+
+        out = dict(level=np.zeros(T, np.int8), st_task=np.zeros(T, np.int32), st_victim=np.zeros(T, np.int32),
+                   st_thief=np.zeros(T, np.int32), st_level=np.zeros(T, np.int32), st_cost=np.zeros(T),
+                   st_occ_victim=np.zeros(T), st_occ_thief=np.zeros(T), inflight_occ=np.zeros(W),
+                   inflight_tasks=np.zeros(W, np.int32), idle_after=np.zeros(W, np.uint8),
+                   sat_after=np.zeros(W, np.uint8))
+        n = C.c_int64(0)
+        nd = len(p["data_nbytes"])
+        self._check(self.lib.dgp_steal_balance(
+            self.h, W, a(p["nthreads"], np.int32), a(p["occ"], np.float64), a(p["nproc"], np.int32),
+            a(p["wnbytes"], np.int64), a(p["idle"], np.uint8), a(p["sat"], np.uint8), float(p["total_occ"]),
+            int(p["total_nthreads"]), int(p["bandwidth"]), T, a(p["victim"], np.int32), a(p["duration"], np.float64),
+            a(p["fast"], np.uint8), a(p["dep_ptr"], np.int64), a(p["dep_idx"], np.int32), nd,
+            a(p["data_nbytes"], np.int64), a(p["data_get_nbytes"], np.int64), a(hptr, np.int64), a(hidx, np.int32),
+            *[_ptr(out[k]) for k in ("level", "st_task", "st_victim", "st_thief", "st_level", "st_cost",
+                                     "st_occ_victim", "st_occ_thief")],
+            C.byref(n), *[_ptr(out[k]) for k in ("inflight_occ", "inflight_tasks", "idle_after", "sat_after")]),
+            "dgp_steal_balance")
+        k = int(n.value)
+        for key in ("st_task", "st_victim", "st_thief", "st_level", "st_cost", "st_occ_victim", "st_occ_thief"):
+            out[key] = out[key][:k]
+        return out

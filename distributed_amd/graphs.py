@@ -247,3 +247,53 @@ def check_graph(g: dict) -> None:
     for k in ("prefix_id", "group_id", "wanted", "rootish_override", "nbytes", "start", "stop"):
         if len(g[k]) != n:
             raise ValueError(f"{k} has wrong length")
+
+
+def steal_problem(n_workers: int, n_tasks: int, *, nthreads: int = 2, hot_frac: float = 0.1, seed: int = 1,
+                  n_prefixes: int = 8, zipf_a: float = 1.5) -> dict:
+    """A WorkStealing.balance() input in the shape of BASELINE.json's C4:
+    D = T/4 memory-resident dependencies (``int(lognormal(16, 3))`` bytes) on uniform
+    workers; T processing tasks with 1-2 of them (5 % dependency-free -> level 0) in
+    prefixes with durations 10 ms * 2^j, on the ``hot_frac`` "hot" workers chosen
+    ``zipf(a) mod |hot|``. Occupancy = the tasks' durations + the bytes of their remote
+    dependencies / bandwidth (each dependency once per worker); idle / saturated follow
+    ``check_idle_saturated`` (scheduler.py:2949-2995). The arrays of
+    ``PlacementEngine.steal_balance`` / ``oracle.steal_balance``."""
+    rng = np.random.default_rng(seed)
+    W, T = int(n_workers), int(n_tasks)
+    bw = 100_000_000
+    D = max(T // 4, 1)
+    hot = rng.choice(W, size=max(int(round(W * hot_frac)), 1), replace=False)
+    holder = rng.integers(0, W, D).astype(np.int32)
+    nbytes = rng.lognormal(16, 3, D).astype(np.int64)
+    pid = rng.integers(0, n_prefixes, T)
+    duration = (0.01 * 2.0 ** pid).astype(np.float64)
+    k = np.where(rng.random(T) < 0.05, 0, rng.integers(1, 3, T))
+    deps = [np.unique(rng.integers(0, D, kk)) for kk in k]
+    dep_ptr = np.zeros(T + 1, np.int64)
+    dep_ptr[1:] = np.cumsum([len(d) for d in deps])
+    dep_idx = np.concatenate(deps).astype(np.int32) if T else np.zeros(0, np.int32)
+    victim = hot[rng.zipf(zipf_a, T) % len(hot)].astype(np.int32)
+    nth = np.full(W, nthreads, np.int32)
+    nproc = np.bincount(victim, minlength=W).astype(np.int32)
+    occ = np.zeros(W)
+    np.add.at(occ, victim, duration)
+    need = {}
+    for t in range(T):
+        for d in deps[t]:
+            if holder[d] != victim[t]:
+                need.setdefault(int(victim[t]), set()).add(int(d))
+    netocc = np.zeros(W, np.int64)
+    for w, ds in need.items():
+        netocc[w] = int(nbytes[list(ds)].sum())
+    occ = occ + netocc / bw
+    wnbytes = np.bincount(holder, weights=nbytes, minlength=W).astype(np.int64)
+    total_occ = float(occ.sum())
+    tn = int(nth.sum())
+    avg = total_occ / tn
+    idle = ((nproc < nth) | (occ < nth * avg / 2)).astype(np.uint8)
+    pend = np.where(nproc > nth, occ * (nproc - nth) / np.maximum(nproc * nth, 1), 0.0)
+    sat = ((idle == 0) & (nproc > nth) & (pend > 0.4) & (pend > 1.9 * avg)).astype(np.uint8)
+    return dict(nthreads=nth, occ=occ, nproc=nproc, wnbytes=wnbytes, idle=idle, sat=sat, total_occ=total_occ,
+                total_nthreads=tn, bandwidth=bw, victim=victim, duration=duration, fast=np.zeros(T, np.uint8),
+                dep_ptr=dep_ptr, dep_idx=dep_idx, data_nbytes=nbytes, data_get_nbytes=nbytes, data_holder=holder)

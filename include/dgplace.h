@@ -22,7 +22,9 @@
  *                         the tasks placed in round k-1 (tests/golden/gen_golden.py)
  *   dgp_get_placements    the compute-task decisions (_add_to_processing :3199 /
  *                         _task_to_msg :3421): task, worker, comm bytes, objective, route
- *   (planned) dgp_steal_balance  WorkStealing.balance (stealing.py:401-503, _get_thief :532)
+ *   dgp_steal_balance     WorkStealing.steal_time_ratio (stealing.py:241-277) for every
+ *                         processing task + one WorkStealing.balance() (:401-503, _get_thief
+ *                         :532-542, move_task_request :279-331, check_idle_saturated)
  */
 #ifndef DGPLACE_H
 #define DGPLACE_H
@@ -122,6 +124,30 @@ int dgp_set_timing(dgp_engine* e, int enabled);
  * [4] record-log length, [5] record-log walker position, [6..13] commit-kernel phase
  * cycles (s_memtime): setup, local steps, global stimuli, finish, walker, longest step. */
 int dgp_stats(dgp_engine* e, int64_t* out, int32_t n);
+
+/* WorkStealing: the cost level of every processing task (steal_time_ratio,
+ * stealing.py:241-277; -1 = not stealable) and one balance() (:401-503) over a
+ * scheduler state given as host arrays. Workers: nthreads, WorkerState.occupancy,
+ * len(processing), ws.nbytes, membership of idle / saturated; the totals of
+ * SchedulerState.total_occupancy / total_nthreads and the bandwidth. Processing tasks:
+ * processing_on (victim), get_task_duration, prefix in fast_tasks, dependencies (CSR
+ * into the data arrays). Data (dependencies): raw nbytes (get_comm_cost), get_nbytes()
+ * (worker_objective, steal_time_ratio), who_has (CSR of worker ids). Tie-break: the
+ * canonical one of the golden fixtures (worker index last; bins in ascending task id;
+ * saturated in ascending worker id). Outputs: levels[T]; the ordered steal requests
+ * (task, victim, thief, level, cost = compute + victim comm cost, victim / thief combined
+ * occupancy as logged), capacity T; *n_steals; per-worker in-flight occupancy and task
+ * deltas; idle / saturated membership after the call. Kernel-time ids 4 (levels + bins),
+ * 5 (thief argmin), 6 (balance walk). */
+int dgp_steal_balance(dgp_engine* e, int32_t n_workers, const int32_t* nthreads, const double* occupancy,
+                      const int32_t* nprocessing, const int64_t* ws_nbytes, const uint8_t* idle,
+                      const uint8_t* saturated, double total_occupancy, int64_t total_nthreads, int64_t bandwidth,
+                      int64_t n_tasks, const int32_t* victim, const double* duration, const uint8_t* fast,
+                      const int64_t* dep_ptr, const int32_t* dep_idx, int64_t n_data, const int64_t* data_nbytes,
+                      const int64_t* data_get_nbytes, const int64_t* holder_ptr, const int32_t* holder_idx,
+                      int8_t* levels, int32_t* st_task, int32_t* st_victim, int32_t* st_thief, int32_t* st_level,
+                      double* st_cost, double* st_occ_victim, double* st_occ_thief, int64_t* n_steals,
+                      double* inflight_occupancy, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* saturated_out);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,55 @@
+"""HIP WorkStealing parity (needs an MI355X): levels + one balance() per problem.
+
+* every reference-generated fixture (tests/golden/steal_*.npz) is reproduced
+  bit-for-bit: levels, the ordered steal requests with their fp64 costs and logged
+  occupancies, in-flight accounts, idle / saturated sets after the call;
+* larger synthetic C4-shaped problems (distributed_amd/graphs.py:steal_problem) match
+  the oracle (oracle/steal.cpp) bit-for-bit, including 4,096 workers;
+* edge cases: no stealable task, no thief, every worker a thief.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, steal_files
+from distributed_amd import graphs
+from distributed_amd.engine import PlacementEngine
+from oracle import oracle
+from test_oracle_steal import assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = PlacementEngine(0)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("name", steal_files())
+def test_balance_matches_reference_fixture(eng, name):
+    p, exp, meta = oracle.load_steal_fixture(os.path.join(GOLDEN, name))
+    assert_same(eng.steal_balance(p), exp)
+
+
+@pytest.mark.parametrize("W,T,hot,seed", [(256, 20000, 0.1, 11), (1024, 60000, 0.05, 12), (4096, 100000, 0.1, 13),
+                                          (512, 30000, 0.3, 14)])
+def test_balance_matches_oracle_synthetic(eng, W, T, hot, seed):
+    p = graphs.steal_problem(W, T, hot_frac=hot, seed=seed)
+    out, ref = eng.steal_balance(p), oracle.steal_balance(p)
+    assert len(ref["st_task"]) > 0
+    assert_same(out, ref)
+
+
+def test_balance_edge_cases(eng):
+    p = graphs.steal_problem(64, 500, seed=3)
+    q = dict(p, idle=np.ones(64, np.uint8))  # every worker a thief: nothing to do
+    assert_same(eng.steal_balance(q), oracle.steal_balance(q))
+    q = dict(p, idle=np.zeros(64, np.uint8))  # no thief
+    assert_same(eng.steal_balance(q), oracle.steal_balance(q))
+    q = dict(p, fast=np.ones(500, np.uint8))  # nothing stealable
+    out = eng.steal_balance(q)
+    assert len(out["st_task"]) == 0 and (out["level"] == -1).all()
+    assert_same(out, oracle.steal_balance(q))
