@@ -46,6 +46,38 @@ def algorithmic_bytes(g: dict, placed_tasks: np.ndarray, n_waves: int) -> float:
     return float(per_task.sum() + 48 * W * n_waves)
 
 
+def steal_leg(eng, args, world: int) -> dict:
+    """WorkStealing.balance on a C4-shaped state: one call per
+    step, inputs uploaded by the call (the boundary hands over host arrays), device
+    kernel times from HIP events, and the oracle (oracle/steal.cpp) on the host."""
+    from distributed_amd import graphs
+
+    p = graphs.steal_problem(args.steal_workers, args.steal_tasks, seed=1)
+    eng.steal_balance(p)  # warm-up
+    eng.set_timing(True)
+    t0 = time.perf_counter()
+    n_call = 3
+    for _ in range(n_call):
+        out = eng.steal_balance(p)
+    dt = (time.perf_counter() - t0) / n_call
+    kt = eng.kernel_times()
+    eng.set_timing(False)
+    leg = {"metric": "WorkStealing.balance() calls/s", "workload": f"C4-shaped: {args.steal_workers} workers x 2 "
+           f"threads, {args.steal_tasks} processing tasks, 10% hot (zipf 1.5), 8 prefixes 10ms*2^j",
+           "ms_per_call": round(dt * 1e3, 3), "steal_requests": int(len(out["st_task"])),
+           "kernel_ms_per_call": {k: round(v[0] / n_call, 3) for k, v in kt.items() if k.startswith("steal")},
+           "reference_python_seconds_per_call_at_100k_x_4096": 242.0}
+    if world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle
+
+        t0 = time.perf_counter()
+        ref = oracle.steal_balance(p)
+        leg["cpu_baseline"] = {"ms_per_call": round((time.perf_counter() - t0) * 1e3, 1), "cores": 1, "kind": "port",
+                               "sample": "oracle/steal.cpp, one full balance() of the same problem"}
+        leg["parity"] = bool(all(np.array_equal(np.asarray(out[k]), np.asarray(ref[k])) for k in ref))
+    return leg
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -55,6 +87,9 @@ def main():
     ap.add_argument("--workers", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-steal", action="store_true", help="skip the WorkStealing.balance leg")
+    ap.add_argument("--steal-tasks", type=int, default=100_000)
+    ap.add_argument("--steal-workers", type=int, default=4096)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -162,6 +197,8 @@ def main():
                                       "sample": f"oracle/replay.cpp, full C2 replay ({n_ref} placements) x {runs}"}
             result["parity"] = bool(all(np.array_equal(out[k], ref[k]) for k in (
                 "pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")))
+        if not args.no_steal:
+            result["steal"] = steal_leg(eng, args, world)
         print(json.dumps(result), flush=True)
     eng.close()
     if dist is not None:
