@@ -848,7 +848,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   uint32_t flags = 0;
   if (f1 == f0 && !(tf & TF_WANTED)) flags |= F_SELFREL;
   if (kt > KT_MAX) flags |= F_GLOBAL;
-  int n = E_HDR, nrel = 0, nf = 0;
+  int n = E_HDR, nrel = 0, nf = 0, sumkx = 0;
   touch(w);
   if (!(flags & F_GLOBAL)) {
     for (int64_t k = k0; k < k1; k++) {
@@ -882,6 +882,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
       continue;
     }
     E[n++] = make_uint4((unsigned)x, (unsigned)D.prefix[x], (unsigned)kx, (unsigned)D.group[x]);
+    sumkx += kx;
     for (int64_t q = x0; q < x1; q++) {
       const int d = D.dep_idx[q];
       const int64_t nb = nbv(D, D.res_nbytes[d]);
@@ -899,7 +900,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   E[0] = make_uint4((unsigned)t, (unsigned)w, (unsigned)p, flags);
   E[1] = make_uint4(lo32(nbt), hi32(nbt),
                     (unsigned)(min(kt, 255) | (nrel << 8) | (min(nf, 255) << 16) | (n << 24)), (unsigned)g);
-  E[2] = make_uint4(dlo(dobs), dhi(dobs), (unsigned)nt, 0u);
+  E[2] = make_uint4(dlo(dobs), dhi(dobs), (unsigned)nt, (unsigned)sumkx);  // sumkx: needs entries it may add
 }
 
 // ========================================================== builder / prefetcher
@@ -1443,12 +1444,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
 #endif
   // ---- capacity check of the needs tables this stimulus may grow
   if (!exact) {
-    int tot_new = 0, off = FX0;
-    for (int j = 0; j < nf; j++) {
-      const int kx = rl((int)E.z, off) & 0xff;
-      tot_new += kx;
-      off += 1 + kx;
-    }
+    const int tot_new = rl((int)E.w, 2);  // the frontier's dependency count (prefetcher)
     const int ntch = L.ntouch[s];
     bool bad = false;
     if (lane < ntch) {
@@ -1507,10 +1503,11 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     net += dnet;
   }
   phase(17);
-  {
-    const double oj = occ_dict(dj, net, durv, D);
-    o.rec(K_COMPLETE, w, p, dnet, mkd(rlu(dlo(oj), jw), rlu(dhi(oj), jw)), npw, t, dobs);
-  }
+  // every lane's occupancy and stack time, kept current: only w (now) and each chosen
+  // worker (after its commit) change during the stimulus
+  double occj = occ_dict(dj, net, durv, D);
+  double stkj = occj / (double)nth;
+  o.rec(K_COMPLETE, w, p, dnet, mkd(rlu(dlo(occj), jw), rlu(dhi(occj), jw)), npw, t, dobs);
   // add_replica (:3148), then the releases popped before the frontier (LIFO, :3309-3314)
   if (isw) nbj += (flags & F_SELFREL) ? 0 : nbt;
   for (int i = 0; i < nrel; i++) {
@@ -1536,8 +1533,8 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     }
     cand = cand && tl;
     Key k;
-    const double oc = occ_dict(dj, net, durv, D);
-    k.start = oc / (double)nth + (double)comm / (double)D.bandwidth;
+    const double oc = occj;
+    k.start = stkj + (double)comm / (double)D.bandwidth;
     k.nb = nbj;
     k.w = cj;
     k.comm = comm;
@@ -1598,10 +1595,9 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       D.state[x] = S_PROCESSING;
       atomicAdd((unsigned long long*)&D.g_relwait[gx], (unsigned long long)-1ll);
     }
-    {
-      const double oj = occ_dict(dj, net, durv, D);
-      o.rec(K_PLACE, cb, px, dn, mkd(rlu(dlo(oj), jb), rlu(dhi(oj), jb)), rl(np, jb), x, 0.0);
-    }
+    occj = occ_dict(dj, net, durv, D);
+    stkj = occj / (double)nth;
+    o.rec(K_PLACE, cb, px, dn, mkd(rlu(dlo(occj), jb), rlu(dhi(occj), jb)), rl(np, jb), x, 0.0);
     off += 1 + kx;
     phase(20);
   }
@@ -1634,8 +1630,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     }
     const int qp = S.q_prefix;
     for (int i = 0; i < pops; i++) {
-      const double ow = occ_dict(dj, net, durv, D);
-      const double st = ow / (double)nth + 0.0 / (double)D.bandwidth;
+      const double st = stkj + 0.0 / (double)D.bandwidth;
       o.place(-1, w, 0, mkd(rlu(dlo(st), jw), rlu(dhi(st), jw)), mk64(rlu(lo32(nbj), jw), rlu(hi32(nbj), jw)),
               ROUTE_ROOTISH_Q);
       bool okq = true;
@@ -1644,8 +1639,9 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
         np += 1;
       }
       if (ballot(!okq)) serr(S, SERR_PREFIX, -1);
-      const double oa = occ_dict(dj, net, durv, D);
-      o.rec(K_PLACE, w, qp, 0, mkd(rlu(dlo(oa), jw), rlu(dhi(oa), jw)), rl(np, jw), -1, 0.0);
+      occj = occ_dict(dj, net, durv, D);
+      stkj = occj / (double)nth;
+      o.rec(K_PLACE, w, qp, 0, mkd(rlu(dlo(occj), jw), rlu(dhi(occj), jw)), rl(np, jw), -1, 0.0);
     }
   }
   // ---- w written back last, then released
