@@ -45,7 +45,7 @@ __constant__ Dev c_dev;
 #endif
 constexpr int SCTA = 768;        // 12 waves: 5 roles + 7 executors (168 VGPRs per wave)
 constexpr int WIN = 32;          // in-flight stimulus slots (LDS window)
-constexpr int NE = 48;           // 16-byte descriptor entries per stimulus
+constexpr int NE = 64;           // 16-byte descriptor entries per stimulus (one per lane)
 constexpr int DR = 4096;         // descriptor ring (global) — how far PRE may run ahead
 constexpr int PLC = 64;          // staged placements / records per stimulus
 constexpr int KT_MAX = 24;       // dependencies of the completing task in local mode
@@ -847,7 +847,10 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   const int kt = (int)(k1 - k0);
   uint32_t flags = 0;
   if (f1 == f0 && !(tf & TF_WANTED)) flags |= F_SELFREL;
-  if (kt > KT_MAX) flags |= F_GLOBAL;
+  if (kt > KT_MAX) {
+    flags |= F_GLOBAL;
+    atomicAdd(&L.c.prof[20], 1ull);  // diagnostics: why stimuli run global
+  }
   int n = E_HDR, nrel = 0, nf = 0, sumkx = 0;
   touch(w);
   if (!(flags & F_GLOBAL)) {
@@ -878,6 +881,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
     const int64_t x0 = D.dep_ptr[x], x1 = D.dep_ptr[x + 1];
     const int kx = (int)(x1 - x0);
     if ((D.tflags[x] & TF_ROOTISH) || kx > KX_MAX || n + 1 + kx > NE) {
+      if (!(flags & F_GLOBAL)) atomicAdd(&L.c.prof[(D.tflags[x] & TF_ROOTISH) ? 16 : 21], 1ull);
       flags |= F_GLOBAL;
       continue;
     }
@@ -891,6 +895,8 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
       E[n++] = make_uint4((unsigned)d, (unsigned)hd, lo32(nb), hi32(nb));
     }
   }
+  if (!(flags & F_GLOBAL) && (nf > 255 || nt > TMAX || nf + (D.sat_inf ? 0 : D.w_cap[w]) + 1 > PLC))
+    atomicAdd(&L.c.prof[22], 1ull);
   if (nf > 255 || nt > TMAX) flags |= F_GLOBAL;
   if (nf + (D.sat_inf ? 0 : D.w_cap[w]) + 1 > PLC) flags |= F_GLOBAL;  // staging room for the refill
   if (tbad) flags |= F_GLOBAL | F_BADTOUCH;
@@ -1013,6 +1019,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     const uint32_t fadd = (qglob ? F_GLOBAL : 0u) | ((D.dbg & 1) ? F_EXACT : 0u) | ((D.dbg & 2) ? F_GLOBAL : 0u);
 #pragma unroll
     for (int b = 0; b < RB; b++) {
+      if (lane == 0 && b < nb && qglob && !(rlu(EB[b].w, 0) & F_GLOBAL)) S.prof[23] += 1;  // diagnostics
       pb[b] = rl((int)EB[b].z, 0);
       dob[b] = mkd(rlu(EB[b].x, 2), rlu(EB[b].y, 2));
       ntb[b] = rl((int)EB[b].z, 2);
