@@ -46,6 +46,18 @@ def algorithmic_bytes(g: dict, placed_tasks: np.ndarray, n_waves: int) -> float:
     return float(per_task.sum() + 48 * W * n_waves)
 
 
+def reduce_max(x: float, dist, device: str = "cuda") -> float:
+    """The slowest rank's value (replicas only: the ranks share nothing but this and the
+    barriers; RCCL over xGMI on the GPU box, gloo in the CPU tests)."""
+    if dist is None:
+        return x
+    import torch
+
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def steal_leg(eng, args, world: int) -> dict:
     """WorkStealing.balance on a C4-shaped state: one call per
     step, inputs uploaded by the call (the boundary hands over host arrays), device
@@ -142,12 +154,7 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.set_timing(False)
     placements = eng.num_placements()
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = reduce_max(elapsed, dist)
     total_placements = placements * args.steps * world
     value = total_placements / elapsed
 
