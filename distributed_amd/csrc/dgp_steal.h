@@ -22,6 +22,7 @@ namespace steal {
 
 constexpr int N_LEVELS = 15;     // len(WorkStealing.cost_multipliers) (stealing.py:83-85)
 constexpr double LATENCY = 0.1;  // stealing.py:37
+constexpr int MAXH = 4;          // distinct dependency holders a task's fast thief search handles
 
 struct Prob {
   int W;
@@ -54,6 +55,26 @@ struct Prob {
   double* s_cct;      // comm cost to that thief
   double* s_ccv;      // comm cost to the victim
   double* s_dur;      // duration
+  // task prep per sorted position: sums of dependency sizes and the distinct holders
+  int64_t* s_cget;    // sum of get_nbytes over the dependencies
+  int64_t* s_craw;    // sum of raw nbytes
+  int32_t* s_nh;      // distinct holders (-1: more than MAXH)
+  int32_t* s_hw;      // [T][MAXH] holder worker
+  int64_t* s_hg;      // [T][MAXH] get_nbytes it holds
+  int64_t* s_hr;      // [T][MAXH] raw nbytes it holds
+  // initial thieves sorted by (stack time, ws.nbytes, index), in runs of equal stack time
+  uint64_t* tk_a;     // [W] stack-time bits (UINT64_MAX: not a thief)
+  int64_t* tk_nb;     // [W]
+  int32_t* tk_w;      // [W]
+  uint64_t* tk_a2;    // sort scratch
+  int64_t* tk_nb2;
+  int32_t* tk_w2;
+  int32_t* th_order;  // [W] thieves in key order
+  int32_t* run_start; // [W + 1]
+  double* run_a;      // [W] stack time of each run
+  int32_t* run_of_w;  // [W] run of each thief (-1: not a thief)
+  int32_t* n_runs;
+  int32_t* vs_g;      // [W] victim list (global scratch)
   // outputs
   int8_t* level;
   int32_t *st_task, *st_victim, *st_thief, *st_level;
@@ -168,7 +189,81 @@ __global__ void k_best_thief(Prob P, const int32_t* n_stealable) {
     P.s_cct[i] = b.w < P.W ? comm_cost(P, t, b.w) : 0.0;
     P.s_ccv[i] = comm_cost(P, t, P.victim[t]);
     P.s_dur[i] = P.duration[t];
+    // the task's dependency sizes and distinct holders (for the run-based thief search)
+    int64_t cg = 0, cr = 0;
+    int nh = 0;
+    int hw[MAXH];
+    int64_t hg[MAXH], hr[MAXH];
+    for (int64_t k = P.dep_ptr[t]; k < P.dep_ptr[t + 1]; k++) {
+      const int d = P.dep_idx[k];
+      const int64_t g = P.d_get_nbytes[d], rw = P.d_nbytes[d];
+      cg += g;
+      cr += rw;
+      for (int64_t q = P.h_ptr[d]; q < P.h_ptr[d + 1]; q++) {
+        const int h = P.h_idx[q];
+        int at = -1;
+        for (int j = 0; j < MAXH; j++)
+          if (j < nh && hw[j] == h) at = j;
+        if (at < 0) {
+          if (nh >= MAXH) {
+            nh = MAXH + 1;
+            break;
+          }
+          at = nh++;
+          hw[at] = h;
+          hg[at] = 0;
+          hr[at] = 0;
+        }
+        hg[at] += g;
+        hr[at] += rw;
+      }
+      if (nh > MAXH) break;
+    }
+    P.s_cget[i] = cg;
+    P.s_craw[i] = cr;
+    P.s_nh[i] = nh > MAXH ? -1 : nh;
+    for (int j = 0; j < MAXH; j++) {
+      P.s_hw[(size_t)i * MAXH + j] = j < nh && nh <= MAXH ? hw[j] : -1;
+      P.s_hg[(size_t)i * MAXH + j] = j < nh && nh <= MAXH ? hg[j] : 0;
+      P.s_hr[(size_t)i * MAXH + j] = j < nh && nh <= MAXH ? hr[j] : 0;
+    }
   }
+}
+
+// ---------------------------------------------------------------- thief order
+// sort keys of the initial thieves: stack time (ws.occupancy / nthreads, the first term of
+// worker_objective), ws.nbytes, index
+__global__ void k_thief_keys(Prob P) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= P.W) return;
+  const bool th = P.idle[w] != 0;
+  const double a = P.occ[w] / (double)P.nthreads[w];
+  P.tk_a[w] = th ? (uint64_t)__double_as_longlong(a) : ~0ull;  // a >= 0: bits order like values
+  P.tk_nb[w] = P.wnbytes[w];
+  P.tk_w[w] = w;
+}
+__global__ void k_gather_a(Prob P) {  // stack-time keys in the (nbytes, index) order
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < P.W) P.tk_a2[i] = P.tk_a[P.tk_w2[i]];
+}
+// runs of equal stack time over the sorted thieves (one thread: W steps)
+__global__ void k_runs(Prob P) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int r = 0;
+  for (int w = 0; w < P.W; w++) P.run_of_w[w] = -1;
+  int p = 0;
+  for (; p < P.W; p++) {
+    const uint64_t a = P.tk_a[p];  // tk_a holds the sorted keys here (see host sequence)
+    if (a == ~0ull) break;
+    if (p == 0 || a != P.tk_a[p - 1]) {
+      P.run_start[r] = p;
+      P.run_a[r] = __longlong_as_double((long long)a);
+      r++;
+    }
+    P.run_of_w[P.th_order[p]] = r - 1;
+  }
+  P.run_start[r] = p;
+  *P.n_runs = r;
 }
 
 // ---------------------------------------------------------------------- balance
@@ -181,11 +276,21 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   double* occ = (double*)smem;
   double* ifo = occ + W;
   int32_t* ift = (int32_t*)(ifo + W);
-  int32_t* vs = ift + W;                    // victims of the current level
-  uint8_t* thief = (uint8_t*)(vs + W);
+  int32_t* run_first = ift + W;             // first possibly-live position of each run
+  int32_t* run_alive = run_first + W;       // live thieves per run
+  int32_t* run_nxt = run_alive + W;         // next run to look at (skips emptied runs)
+  uint8_t* thief = (uint8_t*)(run_nxt + W);
   uint8_t* idle = thief + W;
   uint8_t* sat = idle + W;
   uint8_t* taken = sat + W;                 // topk scratch
+  int32_t* vs = P.vs_g;                     // victims of the current level (global scratch)
+  const int R = *P.n_runs;
+  auto run_a_g = [&](int r) { return P.run_a[r]; };
+  for (int r = lane; r < R; r += 64) {
+    run_first[r] = P.run_start[r];
+    run_alive[r] = P.run_start[r + 1] - P.run_start[r];
+    run_nxt[r] = r + 1;
+  }
   int nth_ = 0, nsat_ = 0;
   for (int w = lane; w < W; w += 64) {
     occ[w] = P.occ[w];
@@ -280,6 +385,82 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
     }
   }
   __syncthreads();
+  // the first run at or after r that still has a live thief (emptied runs are skipped
+  // through run_nxt, compressed as they are crossed)
+  auto find_run = [&](int r) {
+    int x = r;
+    while (x < R && run_alive[x] == 0) x = run_nxt[x];
+    int y = r;
+    while (y < R && y != x && run_alive[y] == 0) {
+      const int z = run_nxt[y];
+      run_nxt[y] = x;  // every lane writes the same value
+      y = z;
+    }
+    return x;
+  };
+  // _get_thief (stealing.py:532-542) over the live thieves, exact: worker_objective's start
+  // is fl(stack + comm / bw), monotone in the stack time; for a worker holding none of the
+  // task's dependencies comm is the task's whole get_nbytes sum, so the runs are scanned in
+  // order while their start can still tie the best, taking each run's first live
+  // non-holder (the run is already ordered by (nbytes, index)); the <= MAXH holders are
+  // evaluated with their own comm.
+  auto thief_from_runs = [&](int i, int64_t t, double* cct_out) -> int {
+    const int nh = P.s_nh[i];
+    if (nh < 0) {  // many holders: plain argmin
+      const Obj b = wave_argmin(P, t, [&](int w) { return thief[w] != 0; });
+      *cct_out = comm_cost(P, t, b.w);
+      return b.w;
+    }
+    int hw[MAXH];
+    int64_t hg[MAXH];
+#pragma unroll
+    for (int j = 0; j < MAXH; j++) {
+      hw[j] = P.s_hw[(size_t)i * MAXH + j];
+      hg[j] = P.s_hg[(size_t)i * MAXH + j];
+    }
+    const int64_t C = P.s_cget[i];
+    const double x = (double)C / (double)P.bw;
+    Obj best{INFINITY, INT64_MAX, INT32_MAX};
+    bool have = false;
+    for (int r = find_run(0); r < R; r = find_run(r + 1)) {
+      const double sv = run_a_g(r) + x;
+      if (have && sv > best.start) break;
+      const int pe = P.run_start[r + 1];
+      int p = run_first[r];
+      while (p < pe && !thief[P.th_order[p]]) p++;
+      run_first[r] = p;  // removed thieves are skipped for good
+      int q = p;
+      while (q < pe) {
+        const int w = P.th_order[q];
+        bool hold = false;
+#pragma unroll
+        for (int j = 0; j < MAXH; j++) hold |= j < nh && hw[j] == w;
+        if (thief[w] && !hold) break;
+        q++;
+      }
+      if (q < pe) {
+        const int w = P.th_order[q];
+        const Obj o{sv, P.wnbytes[w], w};
+        if (!have || obj_less(o, best)) best = o;
+        have = true;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MAXH; j++) {
+      if (j >= nh) break;
+      const int h = hw[j];
+      if (!thief[h]) continue;
+      const double stack = occ[h] / (double)P.nthreads[h];
+      const Obj o{stack + (double)(C - hg[j]) / (double)P.bw, P.wnbytes[h], h};
+      if (obj_less(o, best)) best = o;
+    }
+    int64_t held_raw = 0;
+#pragma unroll
+    for (int j = 0; j < MAXH; j++)
+      if (j < nh && hw[j] == best.w) held_raw = P.s_hr[(size_t)i * MAXH + j];
+    *cct_out = (double)(P.s_craw[i] - held_raw) / (double)P.bw;
+    return best.w;
+  };
   for (int level = 0; level < N_LEVELS; level++) {  // :431
     if (n_thieves == 0) break;
     if (live) {  // list(potential_victims): the saturated set now, ascending index
@@ -315,11 +496,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           double cct = __shfl(cq, j);
           const double ccv = __shfl(vq, j);
           const double compute = __shfl(dq, j);
-          if (th < 0 || !thief[th]) {  // the precomputed thief left the set: argmin again
-            const Obj b = wave_argmin(P, t, [&](int w) { return thief[w] != 0; });
-            th = b.w;
-            cct = comm_cost(P, t, th);
-          }
+          if (th < 0 || !thief[th]) th = thief_from_runs(c0 + j, t, &cct);  // the precomputed thief left
           const double occ_thief = combined(th);
           const double occ_victim = combined(v);
           if (occ_thief + cct + compute <= occ_victim - (ccv + compute) / 2) {  // :462-465
@@ -340,7 +517,10 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
             __syncthreads();
             ns++;
             if (!is_unoccupied(th, combined(th), P.nproc[th] + ift[th])) {  // :487-493
-              if (lane == 0) thief[th] = 0;
+              if (lane == 0) {
+                thief[th] = 0;
+                run_alive[P.run_of_w[th]] -= 1;
+              }
               __syncthreads();
               n_thieves--;
             }
@@ -369,7 +549,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   finish();
 }
 
-inline size_t balance_lds_bytes(int W) { return (size_t)W * (8 + 8 + 4 + 4 + 4); }
+inline size_t balance_lds_bytes(int W) { return (size_t)W * (8 + 8 + 4 + 4 + 4 + 4 + 4); }
 
 }  // namespace steal
 

@@ -849,13 +849,23 @@ int dgp_steal_balance(dgp_engine* e, int32_t W, const int32_t* nthreads, const d
   hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
                                      (int32_t*)nullptr, std::max(Tn, 1), 0, 32, s);
   hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_scan, (int32_t*)nullptr, (int32_t*)nullptr, NK, s);
-  const size_t tmp_bytes = std::max(tmp_sort, tmp_scan);
+  size_t tmp_nb = 0, tmp_a = 0;  // the two stable sorts that order the initial thieves
+  hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_nb, (int64_t*)nullptr, (int64_t*)nullptr, (int32_t*)nullptr,
+                                     (int32_t*)nullptr, W, 0, 64, s);
+  hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_a, (uint64_t*)nullptr, (uint64_t*)nullptr, (int32_t*)nullptr,
+                                     (int32_t*)nullptr, W, 0, 64, s);
+  const size_t tmp_bytes = std::max(std::max(tmp_sort, tmp_scan), std::max(tmp_nb, tmp_a));
   auto add = [&](auto** p, size_t n) { parts.push_back({(void**)p, (n ? n : 1) * sizeof(**p)}); };
   add(&d_nthreads, W); add(&d_occ, W); add(&d_nproc, W); add(&d_wnb, W); add(&d_idle, W); add(&d_sat, W);
   add(&d_victim, T); add(&d_dur, T); add(&d_fast, T); add(&d_dep_ptr, T + 1); add(&d_dep_idx, E);
   add(&d_dnb, n_data); add(&d_dgnb, n_data); add(&d_h_ptr, n_data + 1); add(&d_h_idx, H);
   add(&P.key, T); add(&P.order, T); add(&keys_sorted, T); add(&d_vals, T); add(&P.bin_cnt, NK); add(&P.bin_ptr, NK);
   add(&P.s_best, T); add(&P.s_cct, T); add(&P.s_ccv, T); add(&P.s_dur, T);
+  add(&P.s_cget, T); add(&P.s_craw, T); add(&P.s_nh, T); add(&P.s_hw, T * S::MAXH); add(&P.s_hg, T * S::MAXH);
+  add(&P.s_hr, T * S::MAXH);
+  add(&P.tk_a, W); add(&P.tk_nb, W); add(&P.tk_w, W); add(&P.tk_a2, W); add(&P.tk_nb2, W); add(&P.tk_w2, W);
+  add(&P.th_order, W); add(&P.run_start, W + 1); add(&P.run_a, W); add(&P.run_of_w, W); add(&P.n_runs, 1);
+  add(&P.vs_g, W);
   add(&P.level, T); add(&P.st_task, T); add(&P.st_victim, T); add(&P.st_thief, T); add(&P.st_level, T);
   add(&P.st_cost, T); add(&P.st_occ_victim, T); add(&P.st_occ_thief, T); add(&d_ns, 1);
   add(&d_ifo, W); add(&P.inflight_tasks, W); add(&d_idle_o, W); add(&d_sat_o, W);
@@ -906,10 +916,20 @@ int dgp_steal_balance(dgp_engine* e, int32_t W, const int32_t* nthreads, const d
       hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, P.bin_cnt, P.bin_ptr, NK, s);
     });
     if (!rc) rc = timed_launch(e, 5, [&] {
+      // initial thieves in (stack time, ws.nbytes, index) order: two stable radix sorts
+      const unsigned gw = (unsigned)((W + 255) / 256);
+      hipLaunchKernelGGL(S::k_thief_keys, dim3(gw), dim3(256), 0, s, P);
+      size_t tb = tmp_bytes;
+      hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, P.tk_nb, P.tk_nb2, P.tk_w, P.tk_w2, W, 0, 64, s);
+      hipLaunchKernelGGL(S::k_gather_a, dim3(gw), dim3(256), 0, s, P);
+      tb = tmp_bytes;
+      hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, P.tk_a2, P.tk_a, P.tk_w2, P.th_order, W, 0, 64, s);
+      hipLaunchKernelGGL(S::k_runs, dim3(1), dim3(64), 0, s, P);
       hipLaunchKernelGGL(S::k_best_thief, dim3((unsigned)((T * 64 + 255) / 256)), dim3(256), 0, s, P, P.bin_ptr + NK - 1);
     });
   } else {
     chk(hipMemsetAsync(P.bin_ptr, 0, NK * 4, s));
+    chk(hipMemsetAsync(P.n_runs, 0, 4, s));  // no thief runs are read without tasks
   }
   if (!rc) rc = timed_launch(e, 6, [&] {
     hipLaunchKernelGGL(S::k_balance, dim3(1), dim3(64), S::balance_lds_bytes(W), s, P);

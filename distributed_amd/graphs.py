@@ -250,7 +250,7 @@ def check_graph(g: dict) -> None:
 
 
 def steal_problem(n_workers: int, n_tasks: int, *, nthreads: int = 2, hot_frac: float = 0.1, seed: int = 1,
-                  n_prefixes: int = 8, zipf_a: float = 1.5) -> dict:
+                  n_prefixes: int = 8, zipf_a: float = 1.5, replicas: int = 1, occ_quantum: float = 0.0) -> dict:
     """A WorkStealing.balance() input in the shape of BASELINE.json's C4:
     D = T/4 memory-resident dependencies (``int(lognormal(16, 3))`` bytes) on uniform
     workers; T processing tasks with 1-2 of them (5 % dependency-free -> level 0) in
@@ -258,7 +258,11 @@ def steal_problem(n_workers: int, n_tasks: int, *, nthreads: int = 2, hot_frac: 
     ``zipf(a) mod |hot|``. Occupancy = the tasks' durations + the bytes of their remote
     dependencies / bandwidth (each dependency once per worker); idle / saturated follow
     ``check_idle_saturated`` (scheduler.py:2949-2995). The arrays of
-    ``PlacementEngine.steal_balance`` / ``oracle.steal_balance``."""
+    ``PlacementEngine.steal_balance`` / ``oracle.steal_balance``.
+
+    ``replicas`` > 1 gives every dependency 1..replicas distinct holders (who_has as
+    holder_ptr / holder_idx); ``occ_quantum`` > 0 rounds occupancies to that grid, so many
+    thieves tie on stack time."""
     rng = np.random.default_rng(seed)
     W, T = int(n_workers), int(n_tasks)
     bw = 100_000_000
@@ -278,16 +282,26 @@ def steal_problem(n_workers: int, n_tasks: int, *, nthreads: int = 2, hot_frac: 
     nproc = np.bincount(victim, minlength=W).astype(np.int32)
     occ = np.zeros(W)
     np.add.at(occ, victim, duration)
+    if replicas > 1:
+        extra = [rng.choice(W, size=int(rng.integers(0, replicas)), replace=False) for _ in range(D)]
+        hs = [np.unique(np.concatenate([[holder[d]], extra[d]])).astype(np.int32) for d in range(D)]
+    else:
+        hs = [holder[d:d + 1] for d in range(D)]
     need = {}
     for t in range(T):
         for d in deps[t]:
-            if holder[d] != victim[t]:
+            if victim[t] not in hs[d]:
                 need.setdefault(int(victim[t]), set()).add(int(d))
     netocc = np.zeros(W, np.int64)
     for w, ds in need.items():
         netocc[w] = int(nbytes[list(ds)].sum())
     occ = occ + netocc / bw
-    wnbytes = np.bincount(holder, weights=nbytes, minlength=W).astype(np.int64)
+    if occ_quantum > 0:
+        occ = np.round(occ / occ_quantum) * occ_quantum
+    hptr = np.zeros(D + 1, np.int64)
+    hptr[1:] = np.cumsum([len(h) for h in hs])
+    hidx = np.concatenate(hs).astype(np.int32)
+    wnbytes = np.bincount(hidx, weights=np.repeat(nbytes, np.diff(hptr)), minlength=W).astype(np.int64)
     total_occ = float(occ.sum())
     tn = int(nth.sum())
     avg = total_occ / tn
@@ -296,4 +310,5 @@ def steal_problem(n_workers: int, n_tasks: int, *, nthreads: int = 2, hot_frac: 
     sat = ((idle == 0) & (nproc > nth) & (pend > 0.4) & (pend > 1.9 * avg)).astype(np.uint8)
     return dict(nthreads=nth, occ=occ, nproc=nproc, wnbytes=wnbytes, idle=idle, sat=sat, total_occ=total_occ,
                 total_nthreads=tn, bandwidth=bw, victim=victim, duration=duration, fast=np.zeros(T, np.uint8),
-                dep_ptr=dep_ptr, dep_idx=dep_idx, data_nbytes=nbytes, data_get_nbytes=nbytes, data_holder=holder)
+                dep_ptr=dep_ptr, dep_idx=dep_idx, data_nbytes=nbytes, data_get_nbytes=nbytes, data_holder=holder,
+                **({"holder_ptr": hptr, "holder_idx": hidx} if replicas > 1 else {}))

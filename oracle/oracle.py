@@ -165,7 +165,10 @@ def steal_balance(p: dict) -> dict:
         keep.append(v)
         return _ptr(v)
 
-    hptr, hidx = holder_csr(p["data_holder"])
+    if "holder_ptr" in p:  # who_has with any number of holders
+        hptr, hidx = np.asarray(p["holder_ptr"], np.int64), np.asarray(p["holder_idx"], np.int32)
+    else:
+        hptr, hidx = holder_csr(p["data_holder"])
     out = dict(level=np.zeros(T, np.int8), st_task=np.zeros(T, np.int32), st_victim=np.zeros(T, np.int32),
                st_thief=np.zeros(T, np.int32), st_level=np.zeros(T, np.int32), st_cost=np.zeros(T),
                st_occ_victim=np.zeros(T), st_occ_thief=np.zeros(T), inflight_occ=np.zeros(W),

@@ -43,6 +43,17 @@ def test_balance_matches_oracle_synthetic(eng, W, T, hot, seed):
     assert_same(out, ref)
 
 
+@pytest.mark.parametrize("W,T,replicas,quantum,seed", [(1024, 40000, 3, 0.0, 21), (1024, 40000, 7, 0.0, 22),
+                                                       (2048, 60000, 1, 0.5, 23), (4096, 80000, 4, 0.25, 24)])
+def test_balance_thief_runs(eng, W, T, replicas, quantum, seed):
+    # the run-ordered thief search: replicated dependencies (<= MAXH distinct holders and
+    # beyond) and quantised occupancies (many thieves tied on stack time)
+    p = graphs.steal_problem(W, T, seed=seed, replicas=replicas, occ_quantum=quantum)
+    out, ref = eng.steal_balance(p), oracle.steal_balance(p)
+    assert len(ref["st_task"]) > 0
+    assert_same(out, ref)
+
+
 def test_balance_edge_cases(eng):
     p = graphs.steal_problem(64, 500, seed=3)
     q = dict(p, idle=np.ones(64, np.uint8))  # every worker a thief: nothing to do
