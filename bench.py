@@ -90,6 +90,41 @@ def steal_leg(eng, args, world: int) -> dict:
     return leg
 
 
+def c5_leg(eng_cls, local: int, args, dist, barrier) -> dict:
+    """BASELINE.json C5: the 10M-task map + tree-reduce (fan-in 8) DAG on 16,384 workers x 1
+    thread, one full replay per rank (replicas only, DESIGN.md §8: every rank replays its
+    own copy; the time is the slowest rank's). Pinned by tests/golden/c5_full_digest.json."""
+    from distributed_amd import graphs
+
+    g = graphs.map_tree_reduce(args.c5_map, args.c5_workers)
+    eng = eng_cls(local)
+    eng.load(g, CONFIG)
+    barrier()
+    t0 = time.perf_counter()
+    eng.reset()
+    eng.update_graph()
+    eng.run_rounds(-1)
+    barrier()
+    dt = reduce_max(time.perf_counter() - t0, dist)
+    out = eng.placements()
+    n = int(len(out["pl_task"]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    leg = {"metric": "task placements/sec, C5 (10M-task map + tree-reduce, 16,384 workers)",
+           "value": round(n * world / dt, 1), "unit": "placements/s", "n_gpus": world, "scaling": "weak",
+           "seconds_per_replay": round(dt, 3), "placements_per_replay": n, "n_tasks": int(g["n_tasks"]),
+           "n_workers": args.c5_workers, "parallelism": f"replicas{world}"}
+    pin = os.path.join(REPO, "tests", "golden", "c5_full_digest.json")
+    if os.path.exists(pin):
+        ref = json.load(open(pin))
+        if ref["n_map"] == args.c5_map and ref["n_workers"] == args.c5_workers:
+            leg["parity"] = graphs.placement_digest(out) == ref["digest"]
+            leg["cpu_baseline"] = {"value": round(ref["n_placements"] / ref["oracle_s"], 1), "unit": "placements/s",
+                                   "cores": 1, "kind": "port", "sample": "oracle/replay.cpp full C5 replay, timed "
+                                   "once in the build container (tools/c5_digest.py), not on this box"}
+    eng.close()
+    return leg
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -102,6 +137,9 @@ def main():
     ap.add_argument("--no-steal", action="store_true", help="skip the WorkStealing.balance leg")
     ap.add_argument("--steal-tasks", type=int, default=100_000)
     ap.add_argument("--steal-workers", type=int, default=4096)
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 (10M x 16k) leg")
+    ap.add_argument("--c5-map", type=int, default=8_750_000)
+    ap.add_argument("--c5-workers", type=int, default=16_384)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -206,8 +244,13 @@ def main():
                 "pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")))
         if not args.no_steal:
             result["steal"] = steal_leg(eng, args, world)
-        print(json.dumps(result), flush=True)
     eng.close()
+    if not args.no_c5:  # every rank takes part (barriers, max over ranks)
+        c5 = c5_leg(PlacementEngine, local, args, dist, barrier)
+        if rank == 0:
+            result["c5"] = c5
+    if rank == 0:
+        print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -230,6 +230,21 @@ def map_tree_reduce(n_map: int, n_workers: int, *, fanin: int = 8, seed: int = 3
         nthreads=np.ones(n_workers, np.int32)))
 
 
+PLACEMENT_KEYS = ("pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")
+
+
+def placement_digest(out: dict) -> str:
+    """sha256 over a placement log's six arrays (task, worker, comm bytes, fp64 start
+    bits, ws.nbytes, route), in log order: pins full-size replays whose oracle run is
+    too slow for a test (tests/golden/c5_full_digest.json)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for k in PLACEMENT_KEYS:
+        h.update(np.ascontiguousarray(out[k]).tobytes())
+    return h.hexdigest()
+
+
 def check_graph(g: dict) -> None:
     """Structural invariants the engine relies on (raise ValueError otherwise)."""
     n = g["n_tasks"]

@@ -76,3 +76,22 @@ def test_engine_matches_oracle_tree_reduce(engine_cls):
         eng.replay()
         out = eng.placements()
     assert_same(out, ref, PL_KEYS)
+
+
+def test_engine_full_c5_digest(engine_cls):
+    """BASELINE.json C5 at full size (10M tasks x 16,384 workers): the device's placement
+    log equals the oracle's, pinned by digest (tests/golden/c5_full_digest.json,
+    tools/c5_digest.py); every task is placed exactly once."""
+    import json
+
+    from distributed_amd import graphs
+
+    pin = json.load(open(os.path.join(GOLDEN, "c5_full_digest.json")))
+    g = graphs.map_tree_reduce(pin["n_map"], pin["n_workers"])
+    with engine_cls(0) as eng:
+        eng.load(g, pin["config"])
+        eng.replay()
+        out = eng.placements()
+    assert len(out["pl_task"]) == pin["n_placements"] == g["n_tasks"]
+    assert np.array_equal(np.sort(out["pl_task"]), np.arange(g["n_tasks"]))
+    assert graphs.placement_digest(out) == pin["digest"]
