@@ -237,6 +237,7 @@ struct Dev {
   st::Pos* pos;
   int32_t dbg_task;    // stream debug: dump the candidate keys of this frontier task
   double* dbgbuf;      // [64][8]
+  int32_t pre_lead;  // stream: how far (stimuli) PRE may run ahead of SEQ (<= DR)
   int32_t dbg;  // stream debug: 1 every stimulus waits for all earlier ones, 2 every stimulus global
 };
 

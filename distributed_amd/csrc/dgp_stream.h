@@ -43,7 +43,19 @@ __constant__ Dev c_dev;
 #ifndef DGP_PHASE_PROBES
 #define DGP_PHASE_PROBES 0  // per-phase s_memtime probes in the executors (diagnostics)
 #endif
-constexpr int SCTA = 768;        // 12 waves: 5 roles + 7 executors (168 VGPRs per wave)
+#ifndef DGP_EXE_SLEEP
+#define DGP_EXE_SLEEP 1  // s_sleep units (64 clocks) between an idle executor's polls
+#endif
+#ifndef DGP_REG_PROBES
+#define DGP_REG_PROBES 0  // registrar sub-phase s_memtime probes (diagnostics)
+#endif
+#ifndef DGP_RB
+#define DGP_RB 4  // registrar batch (stimuli registered per poll; 4 measured best of 2/4/8)
+#endif
+#ifndef DGP_SCTA
+#define DGP_SCTA 768
+#endif
+constexpr int SCTA = DGP_SCTA;   // 768: 12 waves = 5 roles + 7 executors (168 VGPRs per wave)
 constexpr int WIN = 32;          // in-flight stimulus slots (LDS window)
 constexpr int NE = 64;           // 16-byte descriptor entries per stimulus (one per lane)
 constexpr int DR = 4096;         // descriptor ring (global) — how far PRE may run ahead
@@ -921,7 +933,7 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
   while (true) {
     if (vload(&S.stop)) break;
     const long long a = KIND == 0 ? S.bld_pos : S.pre_pos;
-    const long long hi = KIND == 0 ? vload(&S.log_len) : min(vload(&S.bld_pos), vload(&S.seq_pos) + DR);
+    const long long hi = KIND == 0 ? vload(&S.log_len) : min(vload(&S.bld_pos), vload(&S.seq_pos) + D.pre_lead);
     const long long e = min(a + 64, hi);
     if (e <= a) {
       __builtin_amdgcn_s_sleep(2);
@@ -970,7 +982,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
   const bool dl = lane >= 3 && lane < 7;
   double dur0 = dl && pa < D.P ? D.pdur_cur[pa] : -1.0;
   double dur1 = dl && pa + 1 < D.P ? D.pdur_cur[pa + 1] : -1.0;
-  constexpr int RB = 8;
+  constexpr int RB = DGP_RB;
   long long pre = 0;  // cached PRE watermark: re-read only when exhausted
   unsigned long long t_poll = mclk();
   uint4 EB[RB];
@@ -1009,6 +1021,10 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
         TB[b] = (lane < TMAX && b < nb) ? D.touch_ring[row * TMAX + lane] : -1;
       }
     }
+#if DGP_REG_PROBES
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the batch rows are in
+    if (lane == 0) S.prof[16] += mclk() - t0;
+#endif
     // ---------------------------------------------------------------- phase A
     // header scalars of the whole batch first (independent of one another)
     int pb[RB], ntb[RB];
@@ -1040,7 +1056,6 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
       serr(S, SERR_RANGE, (int)r0);
       break;
     }
-    int ntmax = 0;
     const int nloc = nbat - (glob_end ? 1 : 0);  // stimuli with touch lists
 #pragma unroll
     for (int b = 0; b < RB; b++) {
@@ -1064,7 +1079,6 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
       // the distinct touched workers (deduplicated by the prefetcher), one lane each
       const int nt = (b < nloc) ? ntb[b] : 0;
       ntb[b] = nt;
-      ntmax = max(ntmax, nt);
       if (lane < NE) L.touch[s][lane] = (uint16_t)TB[b];  // entries past nt are never read
       if (lane == 0) {
         L.ntouch[s] = nt;
@@ -1077,9 +1091,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     // ---------------------------------------------------------------- phase B
     lds_fence();  // the slots' LDS state is written before any mask bit can expose it
     if (lane == 0) vstore(&S.reg_pos, r0 + nbat);
-    // every mask registration back to back (one wave's LDS atomics run in order); the
-    // per-lane predecessor counts packed 16 bits per stimulus
-    unsigned long long pk0 = 0, pk1 = 0;
+    // every mask registration back to back (one wave's LDS atomics run in order)
     int touchall_cnt = 0;
     unsigned oldb[RB];
 #pragma unroll
@@ -1091,30 +1103,37 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
       oldb[b] = __hip_atomic_fetch_or(&P.mask[on ? TB[b] : lane], on ? bit : 0u, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+#if DGP_REG_PROBES
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the mask atomics returned
+    const unsigned long long tM = mclk();
+    if (lane == 0) S.prof[20] += tM - tA;
+#endif
     if (glob_end) {
       const unsigned bit = 1u << (int)((r0 + nbat - 1) & (WIN - 1));
       for (int c = lane; c < D.W; c += 64)
         touchall_cnt += __builtin_popcount(__hip_atomic_fetch_or(&P.mask[c], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
     }
+    // predecessor count of stimulus b = in-flight bits already set on its workers, summed
+    // over its lanes by bit-slice ballots (counts < 32: five ballots, no lane walk)
+    int totb[RB];
 #pragma unroll
     for (int b = 0; b < RB; b++) {
       const unsigned bit = 1u << (int)((r0 + b) & (WIN - 1));
-      const unsigned long long c = (b < nloc && lane < ntb[b]) ? (unsigned long long)__builtin_popcount(oldb[b] & ~bit) : 0ull;
-      if (b < 4) pk0 += c << (16 * (b & 3));
-      else pk1 += c << (16 * (b & 3));
+      const int c = (b < nloc && lane < ntb[b]) ? __builtin_popcount(oldb[b] & ~bit) : 0;
+      int t = 0;
+#pragma unroll
+      for (int k = 0; k < 5; k++) t += __builtin_popcountll(ballot((c >> k) & 1)) << k;
+      totb[b] = t;
     }
-    unsigned long long s0 = 0, s1 = 0;
-    for (int l = 0; l < ntmax; l++) {
-      s0 += (unsigned long long)mk64(rlu(lo32((int64_t)pk0), l), rlu(hi32((int64_t)pk0), l));
-      s1 += (unsigned long long)mk64(rlu(lo32((int64_t)pk1), l), rlu(hi32((int64_t)pk1), l));
-    }
+#if DGP_REG_PROBES
+    if (lane == 0) S.prof[21] += mclk() - tM;
+#endif
     const int tall = glob_end ? wsum(touchall_cnt) : 0;
     if (lane == 0) {
       if (glob_end) vstore(&S.global_pending, 1);  // a global ends its batch
-      int oldp[RB], totb[RB];
+      int oldp[RB];
 #pragma unroll
       for (int b = 0; b < RB; b++) {
-        totb[b] = (int)(((b < 4 ? s0 : s1) >> (16 * (b & 3))) & 0xffffu);
         if (b == nbat - 1 && glob_end) totb[b] = tall;
         oldp[b] = b < nbat ? atomicAdd(&L.pred[(int)((r0 + b) & (WIN - 1))], totb[b] - BIG) : 1;
       }
@@ -1146,9 +1165,11 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
       S.prof[3] += t_poll - t0;
       S.prof[31] += nbat;
       S.prof[27] += 1;            // batches
+#if !DGP_PHASE_PROBES  // (probe builds use 16..23 for the executor phases)
       S.prof[17] += tA - t0;      // fetch wait + phase A
       S.prof[18] += tB - tA;      // phase B
       S.prof[19] += t_poll - tB;  // prefetch issue
+#endif
     }
     lds_fence();
   }
@@ -1263,6 +1284,79 @@ __device__ __attribute__((always_inline)) int64_t needs_inc(const Dev& D, SCtl& 
   // full: scan mode from here on (only reached when every earlier stimulus has retired)
   if (lane == NLW - 1) nl = NL_OVF;
   return nb;
+}
+
+// All of one task's dependency entries at once. A task's dependencies are distinct, so
+// their needs_what entries are distinct lanes of the line: each dependency is matched
+// against the line in one compare (no readlane chain through the line). Fast path only
+// when every entry of c lives in the LDS line (no overflow entries, not scan mode) and
+// the outcome needs no overflow entry; otherwise false with nl untouched, and the caller
+// takes the one-at-a-time path (needs_dec / needs_inc).
+// _dec_needs_replica (:815-823) for the dependencies in entries L0.. of E not held by c;
+// freed = the bytes c no longer needs.
+__device__ __forceinline__ bool needs_dec_all(const uint4& E, int L0, int k, int c, uint32_t& nl, int64_t& freed) {
+  const int lane = lane_id();
+  const uint32_t ctl = rlu(nl, NLW - 1);
+  if (ctl == NL_OVF || (int)(ctl >> 8) != line_used(nl)) return false;
+  const bool ent = lane < NLW - 1 && nl != 0;
+  bool hit = false, ok = true;
+  int64_t fr = 0;
+  int ngone = 0;
+  for (int i = 0; i < k; i++) {
+    const int h = rl((int)E.y, L0 + i);
+    if (h == c) continue;
+    const uint32_t d = (uint32_t)rl((int)E.x, L0 + i);
+    const bool mt = ent && (nl >> 8) == d;
+    ok = ok && ballot(mt) != 0;
+    if (ballot(mt && (nl & 0xffu) == 1u)) {
+      fr += mk64(rlu(E.z, L0 + i), rlu(E.w, L0 + i));
+      ngone++;
+    }
+    hit = hit || mt;
+  }
+  if (!ok) return false;
+  if (hit) nl = (nl & 0xffu) == 1u ? 0u : nl - 1u;
+  if (lane == NLW - 1) nl -= (uint32_t)ngone << 8;
+  freed = fr;
+  return true;
+}
+
+// _inc_needs_replica (:800-813) for the dependencies in entries L0.. of E not held by c
+// (task placed on c); added = the bytes c newly needs.
+__device__ __forceinline__ bool needs_inc_all(const uint4& E, int L0, int k, int c, uint32_t& nl, int64_t& added) {
+  const int lane = lane_id();
+  const uint32_t ctl = rlu(nl, NLW - 1);
+  if (ctl == NL_OVF || (int)(ctl >> 8) != line_used(nl)) return false;
+  const bool ent = lane < NLW - 1 && nl != 0;
+  unsigned long long em = ballot(lane < NLW - 1 && nl == 0);  // free entries
+  uint32_t nn = nl;
+  bool hit = false, ok = true;
+  int64_t ad = 0;
+  int nins = 0;
+  for (int i = 0; i < k; i++) {
+    const int h = rl((int)E.y, L0 + i);
+    if (h == c) continue;
+    const uint32_t d = (uint32_t)rl((int)E.x, L0 + i);
+    const bool mt = ent && (nl >> 8) == d;  // against the line as loaded: inserted entries hold other tasks
+    if (ballot(mt)) {
+      ok = ok && !ballot(mt && (nl & 0xffu) == 0xffu);
+      hit = hit || mt;
+    } else if (em) {
+      const int l = __builtin_ctzll(em);
+      em &= em - 1;
+      if (lane == l) nn = (d << 8) | 1u;
+      ad += mk64(rlu(E.z, L0 + i), rlu(E.w, L0 + i));
+      nins++;
+    } else {
+      ok = false;
+    }
+  }
+  if (!ok) return false;
+  if (hit) nn += 1u;
+  if (lane == NLW - 1) nn += (uint32_t)nins << 8;
+  nl = nn;
+  added = ad;
+  return true;
 }
 
 // a worker with nothing processing needs nothing (leave scan / overflow mode)
@@ -1493,7 +1587,9 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   phase(16);
   // ------------------------------------------- completion: processing -> memory (:2366)
   int64_t dnet = 0;
-  for (int i = 0; i < kt; i++) {  // _dec_needs_replica for the dependencies w needed
+  int64_t freed = 0;
+  if (needs_dec_all(E, TD, kt, w, nl, freed)) dnet = -freed;
+  else for (int i = 0; i < kt; i++) {  // _dec_needs_replica for the dependencies w needed
     const int L_ = TD + i;
     const int h = rl((int)E.y, L_);
     if (h == w) continue;
@@ -1581,7 +1677,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       __threadfence_block();
     }
     int64_t dn = 0;
-    for (int i = 0; i < kx; i++) {
+    if (!needs_inc_all(E, off + 1, kx, cb, nlc, dn)) for (int i = 0; i < kx; i++) {
       const int L2 = off + 1 + i;
       if (rl((int)E.y, L2) == cb) continue;
       const int d = rl((int)E.x, L2);
@@ -1987,14 +2083,17 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
   SCtl& S = L.c;
   const int lane = lane_id();
   unsigned long long t_idle = mclk();
+  // idle / gated ticks accumulate in registers (an LDS atomic per poll from every idle
+  // executor contends with the working waves' LDS traffic); flushed once at exit
+  unsigned long long idle28 = 0, idle29 = 0;
   while (true) {
     if (vload(&S.stop)) break;
     const unsigned m = vload(&S.ready);
     if (!m) {
       const unsigned long long n = mclk();  // 28: executor idle, nothing ready
-      if (lane == 0) atomicAdd(&S.prof[28], n - t_idle);
+      idle28 += n - t_idle;
       t_idle = n;
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(DGP_EXE_SLEEP);
       continue;
     }
     const long long sp = vload(&S.seq_pos);
@@ -2035,9 +2134,9 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     }
     if (cs < 0) {
       const unsigned long long n = mclk();  // 29: ready slots, none claimable (exact gating)
-      if (lane == 0) atomicAdd(&S.prof[29], n - t_idle);
+      idle29 += n - t_idle;
       t_idle = n;
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(DGP_EXE_SLEEP);
       continue;
     }
     lds_fence();
@@ -2058,6 +2157,10 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       atomicSub(&S.busy_exe, 1);
     }
     t_idle = mclk();
+  }
+  if (lane == 0) {
+    atomicAdd(&S.prof[28], idle28);
+    atomicAdd(&S.prof[29], idle29);
   }
 }
 

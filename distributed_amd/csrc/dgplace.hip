@@ -162,6 +162,9 @@ int sync_dev(dgp_engine* e) {
   e->D.dbg = dbg ? atoi(dbg) : 0;
   const char* dt = getenv("DGP_DEBUG_TASK");
   e->D.dbg_task = dt ? atoi(dt) : -2;
+  const char* pl = getenv("DGP_PRE_LEAD");
+  e->D.pre_lead = pl ? atoi(pl) : 4096;
+  if (e->D.pre_lead < 64 || e->D.pre_lead > dgp::st::DR) e->D.pre_lead = dgp::st::DR;
   if (!e->D.dbgbuf) HIPCHK(e, hipMalloc((void**)&e->D.dbgbuf, 64 * 8 * sizeof(double)));
   dgp::Dev h[2] = {e->D, e->D};
   h[0].lds_workers = 0;

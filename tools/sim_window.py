@@ -158,5 +158,63 @@ def main():
                 print(f"WIN {WIN:4d} L {L:4.1f}us R {Rc:4.2f}us -> {(n_stim - first) / t:8.3f} M/s")
 
 
+def simulate_ooo(ptr, wk, n_stim, WIN, E, L, Rc, first, ooo=True, frac=None):
+    """As simulate(), but a slot is freed when its stimulus finishes (out of order) when
+    ooo, else at in-order retirement. frac: early release fractions (None: at the end)."""
+    last = {}
+    reg_t = 0.0
+    execs = [0.0] * E
+    heapq.heapify(execs)
+    fin_heap = []  # finish times of registered, unfreed stimuli
+    seq_prev = 0.0
+    retire = []
+    for r in range(first, n_stim):
+        reg_t = reg_t + Rc
+        if ooo:
+            while len(fin_heap) >= WIN:
+                reg_t = max(reg_t, heapq.heappop(fin_heap))
+        elif r - WIN >= first:
+            reg_t = max(reg_t, retire[r - WIN - first])
+        st = reg_t
+        a, b = ptr[r], ptr[r + 1]
+        for i in range(a, b):
+            v = last.get(wk[i])
+            if v is not None and v > st:
+                st = v
+        ex = heapq.heappop(execs)
+        st = max(st, ex)
+        f = st + L
+        heapq.heappush(execs, f)
+        for i in range(a, b):
+            last[wk[i]] = st + L * (frac[i] if frac is not None else 1.0)
+        if ooo:
+            heapq.heappush(fin_heap, f)
+        seq_prev = max(seq_prev, f)
+        retire.append(seq_prev)
+    return seq_prev
+
+
+def main_ooo():
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 200_000
+    W = 1024
+    g = graphs.random_dag(n, W, seed=0)
+    ref = oracle.replay(g, CFG, snapshots=False)
+    pl_task, pl_worker = ref["pl_task"].astype(np.int64), ref["pl_worker"].astype(np.int64)
+    ptr, wk = touch_sets(g, pl_task, pl_worker)
+    frac = touch_roles(g, pl_task, pl_worker, ptr, wk)
+    first = 2 * W
+    n_stim = len(pl_task)
+    for L in (5.3, 4.0, 2.5):
+        for E in (7, 11):
+            for WIN in (32, 64):
+                for Rc in (0.7, 0.35):
+                    t_in = simulate_ooo(ptr, wk, n_stim, WIN, E, L, Rc, first, ooo=False, frac=frac)
+                    t_oo = simulate_ooo(ptr, wk, n_stim, WIN, E, L, Rc, first, ooo=True, frac=frac)
+                    print(f"L {L} E {E} WIN {WIN} R {Rc}: in-order {(n_stim - first) / t_in:.3f} M/s, out-of-order slots {(n_stim - first) / t_oo:.3f} M/s", flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "ooo":
+        main_ooo()
+    else:
+        main()
