@@ -78,7 +78,7 @@ def steal_leg(eng, args, world: int) -> dict:
            f"threads, {args.steal_tasks} processing tasks, 10% hot (zipf 1.5), 8 prefixes 10ms*2^j",
            "ms_per_call": round(dt * 1e3, 3), "steal_requests": int(len(out["st_task"])),
            "kernel_ms_per_call": {k: round(v[0] / n_call, 3) for k, v in kt.items() if k.startswith("steal")},
-           "reference_python_seconds_per_call_at_100k_x_4096": 242.0}
+           "reference_python_seconds_per_call_at_100k_x_4096": 242.0}  # SURVEY.md §8 a20
     if world == 1 and not args.no_cpu_baseline:
         from oracle import oracle
 
@@ -87,6 +87,43 @@ def steal_leg(eng, args, world: int) -> dict:
         leg["cpu_baseline"] = {"ms_per_call": round((time.perf_counter() - t0) * 1e3, 1), "cores": 1, "kind": "port",
                                "sample": "oracle/steal.cpp, one full balance() of the same problem"}
         leg["parity"] = bool(all(np.array_equal(np.asarray(out[k]), np.asarray(ref[k])) for k in ref))
+    return leg
+
+
+def c3_leg(eng_cls, local: int, args) -> dict:
+    """BASELINE.json C3: the P2P-shuffle-shaped graph (P inputs -> P shuffle-transfer ->
+    1 shuffle-barrier of fan-in P -> P unpack tasks with _rootish False; shuffle/_shuffle.py
+    :276-306) on 512 workers x 1 thread, placement only: one full replay per step, checked
+    bit-exact against the oracle, which is also the CPU baseline (1 core)."""
+    from distributed_amd import graphs
+
+    g = graphs.shuffle_graph(args.c3_partitions, args.c3_workers)
+    eng = eng_cls(local)
+    eng.load(g, CONFIG)
+    eng.reset()
+    eng.update_graph()
+    eng.run_rounds(-1)  # warm-up
+    n_step = 3
+    t0 = time.perf_counter()
+    for _ in range(n_step):
+        eng.reset()
+        eng.update_graph()
+        eng.run_rounds(-1)
+    dt = (time.perf_counter() - t0) / n_step
+    out = eng.placements()
+    n = int(len(out["pl_task"]))
+    leg = {"metric": "task placements/sec, C3 (P2P-shuffle-shaped graph, placement only)", "value": round(n / dt, 1),
+           "unit": "placements/s", "seconds_per_replay": round(dt, 4), "placements_per_replay": n,
+           "n_tasks": int(g["n_tasks"]), "n_partitions": args.c3_partitions, "n_workers": args.c3_workers}
+    if not args.no_cpu_baseline:
+        from oracle import oracle
+
+        ref = oracle.replay(g, CONFIG, snapshots=False)
+        leg["cpu_baseline"] = {"value": round(len(ref["pl_task"]) / ref["seconds"], 1), "unit": "placements/s",
+                               "cores": 1, "kind": "port", "sample": "oracle/replay.cpp, one full C3 replay"}
+        leg["parity"] = bool(all(np.array_equal(out[k], ref[k]) for k in (
+            "pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")))
+    eng.close()
     return leg
 
 
@@ -135,8 +172,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-steal", action="store_true", help="skip the WorkStealing.balance leg")
-    ap.add_argument("--steal-tasks", type=int, default=100_000)
+    ap.add_argument("--steal-tasks", type=int, default=500_000)
     ap.add_argument("--steal-workers", type=int, default=4096)
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 (P2P shuffle, 200k x 512) leg")
+    ap.add_argument("--c3-partitions", type=int, default=66_666)
+    ap.add_argument("--c3-workers", type=int, default=512)
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (10M x 16k) leg")
     ap.add_argument("--c5-map", type=int, default=8_750_000)
     ap.add_argument("--c5-workers", type=int, default=16_384)
@@ -245,6 +285,8 @@ def main():
         if not args.no_steal:
             result["steal"] = steal_leg(eng, args, world)
     eng.close()
+    if rank == 0 and not args.no_c3:
+        result["c3"] = c3_leg(PlacementEngine, local, args)
     if not args.no_c5:  # every rank takes part (barriers, max over ranks)
         c5 = c5_leg(PlacementEngine, local, args, dist, barrier)
         if rank == 0:

@@ -210,7 +210,7 @@ struct Dev {
   uint16_t* gw_nthreads;
   uint16_t* gw_cap;
   uint32_t* gw_plen;
-  uint16_t* gw_pcnt;
+  uint32_t* gw_pcnt;
   int64_t* gw_netocc;
   int64_t* gw_nbytes;
   uint32_t* gw_mask;

@@ -185,7 +185,7 @@ struct WPtr {
   P<uint16_t> nthreads;
   P<uint16_t> cap;
   P<uint32_t> plen;    // prefix dict insertion order (WDict::ord)
-  P<uint16_t> pcnt;    // [W][PD] prefix dict counts by prefix id (WDict::c)
+  P<uint32_t> pcnt;    // [W][PD] prefix dict counts by prefix id (WDict::c, c1)
   P<int64_t> netocc;
   P<int64_t> nbytes;
   P<uint32_t> mask;    // in-flight slots touching the worker
@@ -199,7 +199,7 @@ extern __shared__ __attribute__((aligned(16))) char st_smem[];
 __device__ __forceinline__ size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
 __host__ __device__ constexpr size_t lds_worker_bytes(int W) {
   return ((size_t)W * 4 + 15) / 16 * 16 * 2 /* nproc plen */ + ((size_t)W * 2 + 15) / 16 * 16 * 2 +
-         ((size_t)W * PD * 2 + 15) / 16 * 16 + ((size_t)W * 8 + 15) / 16 * 16 * 2 +
+         ((size_t)W * PD * 4 + 15) / 16 * 16 + ((size_t)W * 8 + 15) / 16 * 16 * 2 +
          ((size_t)W * 4 + 15) / 16 * 16 + ((size_t)W * NLW * 4 + 15) / 16 * 16 + ((size_t)W + 15) / 16 * 16;
 }
 
@@ -214,7 +214,7 @@ __device__ __forceinline__ WPtr<LW> wptr(const Dev& D) {
     p.nthreads = (typename W_::template P<uint16_t>)b; b += al16(W * 2);
     p.cap = (typename W_::template P<uint16_t>)b;      b += al16(W * 2);
     p.plen = (typename W_::template P<uint32_t>)b;     b += al16(W * 4);
-    p.pcnt = (typename W_::template P<uint16_t>)b;     b += al16(W * PD * 2);
+    p.pcnt = (typename W_::template P<uint32_t>)b;     b += al16(W * PD * 4);
     p.netocc = (typename W_::template P<int64_t>)b;    b += al16(W * 8);
     p.nbytes = (typename W_::template P<int64_t>)b;    b += al16(W * 8);
     p.mask = (typename W_::template P<uint32_t>)b;     b += al16(W * 4);
@@ -278,30 +278,48 @@ __shared__ SLds st_L;  // the engine's LDS window + control block (namespace sco
 // 3i..3i+2, and the number of entries in bits 24..31. A prefix is present iff its
 // count is non-zero, so the pair is exactly the dict.
 struct WDict {
-  uint4 c;       // count of prefix p: 16 bits at (p & 1) * 16 of word p >> 1
+  uint4 c, c1;   // count of prefix p (32 bits): word p of c (p < 4) or word p - 4 of c1
   uint32_t ord;  // insertion order
 };
 __device__ __forceinline__ uint32_t wd_n(uint32_t ord) { return ord >> 24; }
 __device__ __forceinline__ int wd_id(uint32_t ord, int i) { return (int)((ord >> (3 * i)) & 7u); }
-__device__ __forceinline__ uint32_t wd_word(const uint4& c, int p) {
-  const int wi = p >> 1;
-  return wi == 0 ? c.x : wi == 1 ? c.y : wi == 2 ? c.z : c.w;
+__device__ __forceinline__ uint32_t wd_cnt(const WDict& d, int p) {
+  switch (p & 7) {
+    case 0: return d.c.x;
+    case 1: return d.c.y;
+    case 2: return d.c.z;
+    case 3: return d.c.w;
+    case 4: return d.c1.x;
+    case 5: return d.c1.y;
+    case 6: return d.c1.z;
+    default: return d.c1.w;
+  }
 }
-__device__ __forceinline__ uint32_t wd_cnt(const uint4& c, int p) { return (wd_word(c, p) >> ((p & 1) * 16)) & 0xffffu; }
+__device__ __forceinline__ void wd_set(WDict& d, int p, uint32_t v) {
+  switch (p & 7) {
+    case 0: d.c.x = v; break;
+    case 1: d.c.y = v; break;
+    case 2: d.c.z = v; break;
+    case 3: d.c.w = v; break;
+    case 4: d.c1.x = v; break;
+    case 5: d.c1.y = v; break;
+    case 6: d.c1.z = v; break;
+    default: d.c1.w = v; break;
+  }
+}
 
 // add_to_processing (+1) / remove_from_processing (-1) of one task of prefix p
 __device__ __forceinline__ bool dict_add(WDict& d, int p, int delta) {
-  const int wi = p >> 1, sh = (p & 1) * 16;
-  uint32_t wv = wd_word(d.c, p);
-  const uint32_t cnt = (wv >> sh) & 0xffffu;
+  const uint32_t cnt = wd_cnt(d, p);
+  uint32_t wv = cnt;
   const uint32_t n = wd_n(d.ord);
   if (delta > 0) {
-    if (cnt == 0xffffu) return false;
+    if (cnt == 0xffffffffu) return false;
     if (cnt == 0) d.ord = (d.ord + (1u << 24)) | ((uint32_t)p << (3 * n));  // new key: appended
-    wv += 1u << sh;
+    wv += 1u;
   } else {
     if (cnt == 0) return true;
-    wv -= 1u << sh;
+    wv -= 1u;
     if (cnt == 1) {  // count reached zero: the key leaves, later keys move up
       int k = 0;
 #pragma unroll
@@ -311,10 +329,7 @@ __device__ __forceinline__ bool dict_add(WDict& d, int p, int delta) {
       d.ord = (ids & lowm) | ((ids >> 3) & ~lowm) | ((n - 1) << 24);
     }
   }
-  if (wi == 0) d.c.x = wv;
-  else if (wi == 1) d.c.y = wv;
-  else if (wi == 2) d.c.z = wv;
-  else d.c.w = wv;
+  wd_set(d, p, wv);
   return true;
 }
 
@@ -332,7 +347,7 @@ __device__ __forceinline__ double occ_dict(const WDict& d, int64_t netocc, DTab 
     if (!ballot((uint32_t)i < n)) break;
     const int p = wd_id(d.ord, i);
     const double dv = dt[p];
-    const double term = (dv < 0 ? D.unknown_duration : dv) * (double)wd_cnt(d.c, p);
+    const double term = (dv < 0 ? D.unknown_duration : dv) * (double)wd_cnt(d, p);
     if ((uint32_t)i < n) res += term;
   }
   return res + (double)netocc / (double)D.bandwidth;
@@ -343,6 +358,7 @@ __device__ __forceinline__ WDict dict_load(const WPtr<LW>& P, int c) {
   using U4 = typename WPtr<LW>::template P<const Q4>;
   WDict d;
   d.c = ld4(ascast<U4>(P.pcnt + (size_t)c * PD));
+  d.c1 = ld4(ascast<U4>(P.pcnt + (size_t)c * PD + 4));
   d.ord = P.plen[c];
   return d;
 }
@@ -1413,6 +1429,7 @@ __device__ __forceinline__ bool dict_update(const WPtr<LW>& P, int c, int p, int
   const bool ok = dict_add(d, p, delta);
   if (lane_id() == 0) {
     st4(ascast<U4>(P.pcnt + (size_t)c * PD), d.c);
+    st4(ascast<U4>(P.pcnt + (size_t)c * PD + 4), d.c1);
     P.plen[c] = d.ord;
   }
   return ok;
@@ -1566,6 +1583,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   int np = 0, nth = 1;
   WDict dj;
   dj.c = make_uint4(0, 0, 0, 0);
+  dj.c1 = make_uint4(0, 0, 0, 0);
   dj.ord = 0;
   int64_t net = 0, nbj = 0;
   if (tl) {
@@ -1710,6 +1728,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     using U4 = typename WPtr<LW>::template P<Q4>;
     P.nproc[cj] = np;
     st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
+    st4(ascast<U4>(P.pcnt + (size_t)cj * PD + 4), dj.c1);
     P.plen[cj] = dj.ord;
     P.netocc[cj] = net;
     P.nbytes[cj] = nbj;
@@ -1752,6 +1771,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     using U4 = typename WPtr<LW>::template P<Q4>;
     P.nproc[cj] = np;
     st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
+    st4(ascast<U4>(P.pcnt + (size_t)cj * PD + 4), dj.c1);
     P.plen[cj] = dj.ord;
     P.netocc[cj] = net;
     P.nbytes[cj] = nbj;
@@ -2180,7 +2200,7 @@ __device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WP
       for (int i = 0; i < n; i++) {
         const int pid = D.w_pfx[(size_t)c * PMAX + i] & (PD - 1);
         ord |= (uint32_t)pid << (3 * i);
-        P.pcnt[(size_t)c * PD + pid] = (uint16_t)D.w_pcnt[(size_t)c * PMAX + i];
+        P.pcnt[(size_t)c * PD + pid] = (uint32_t)D.w_pcnt[(size_t)c * PMAX + i];
       }
       P.plen[c] = ord;
       P.netocc[c] = D.w_netocc[c];

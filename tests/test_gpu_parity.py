@@ -95,3 +95,37 @@ def test_engine_full_c5_digest(engine_cls):
     assert len(out["pl_task"]) == pin["n_placements"] == g["n_tasks"]
     assert np.array_equal(np.sort(out["pl_task"]), np.arange(g["n_tasks"]))
     assert graphs.placement_digest(out) == pin["digest"]
+
+
+@pytest.mark.parametrize("sat", [1.1, "inf"])
+def test_engine_full_c3_shuffle(engine_cls, sat):
+    """BASELINE.json C3 at full size: P = 66,666 partitions (3P + 1 = 200k tasks: inputs,
+    shuffle-transfer, one barrier of fan-in P, unpack tasks with _rootish False) on 512
+    workers, bit-exact against the oracle."""
+    from distributed_amd import graphs
+
+    g = graphs.shuffle_graph(66_666, 512)
+    cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": sat}
+    ref = oracle.replay(g, cfg, snapshots=False)
+    with engine_cls(0) as eng:
+        eng.load(g, cfg)
+        eng.replay()
+        out = eng.placements()
+    assert len(out["pl_task"]) == g["n_tasks"]
+    assert_same(out, ref, PL_KEYS)
+
+
+def test_engine_full_c2(engine_cls):
+    """BASELINE.json C2 at full size (1M tasks x 1,024 workers, saturation 1.1): the whole
+    placement log bit-exact against the oracle."""
+    from distributed_amd import graphs
+
+    g = graphs.random_dag(1_000_000, 1024, seed=0)
+    cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": 1.1}
+    ref = oracle.replay(g, cfg, snapshots=False)
+    with engine_cls(0) as eng:
+        eng.load(g, cfg)
+        eng.replay()
+        out = eng.placements()
+    assert len(out["pl_task"]) == g["n_tasks"]
+    assert_same(out, ref, PL_KEYS)

@@ -64,3 +64,13 @@ def test_balance_edge_cases(eng):
     out = eng.steal_balance(q)
     assert len(out["st_task"]) == 0 and (out["level"] == -1).all()
     assert_same(out, oracle.steal_balance(q))
+
+
+def test_balance_full_c4(eng):
+    """BASELINE.json C4 at full size: WorkStealing.balance over 500k processing tasks on
+    4,096 workers x 2 threads (10% hot, zipf 1.5, eight cost-level prefixes), bit-exact
+    against the oracle."""
+    p = graphs.steal_problem(4096, 500_000, seed=1)
+    out, ref = eng.steal_balance(p), oracle.steal_balance(p)
+    assert len(ref["st_task"]) > 100_000
+    assert_same(out, ref)
