@@ -266,6 +266,14 @@ def main():
         ach = kernels[dom]["achieved_GBs"]
         result["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 4), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 8), "traffic": None}
+        # HBM bytes per launch of the replay kernel, from the committed rocprofv3 --pmc passes
+        # (tools/pmc_traffic.py); only reported for the workload they were measured on
+        tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "hbm_traffic.json")
+        if dom == "replay" and os.path.exists(tf):
+            t = json.load(open(tf))
+            if (t.get("n_tasks"), t.get("n_workers")) == (args.tasks, args.workers):
+                result["roofline"]["traffic"] = round(t["traffic_bytes_per_launch"], 1)
+                result["roofline"]["traffic_source"] = t.get("source")
         result["kernels"] = {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in kernels.items()}
         result["config"]["waves"] = int(n_waves)
         if world == 1 and not args.no_cpu_baseline:

@@ -380,6 +380,13 @@ __device__ __attribute__((always_inline)) void serr(SCtl& S, int code, int task)
 
 
 constexpr unsigned long long WATCHDOG = 40000000000ull;  // s_memtime ticks without progress (~16 s)
+// true once `now` is more than WATCHDOG ticks past `since`. The difference is taken
+// signed: a counter read that comes back below an earlier one (observed once on a C5
+// replay, where the unsigned difference wrapped and fired the watchdog 2 s in) is
+// not a stall.
+__device__ __forceinline__ bool stalled_for(unsigned long long since, unsigned long long now) {
+  return (long long)(now - since) > (long long)WATCHDOG;
+}
 
 __device__ __forceinline__ int64_t nbv(const Dev& D, int64_t v) { return v >= 0 ? v : D.default_data_size; }
 
@@ -672,7 +679,7 @@ __device__ __attribute__((always_inline)) bool round_end_step(const Dev& D, SLds
       const unsigned long long t0 = mclk();
       while (vload(&S.walk_pos) != vload(&S.rec_len) || vload(&S.busy_exe) != 0) {
         if (vload(&S.stop)) return true;
-        if (mclk() - t0 > WATCHDOG) {
+        if (stalled_for(t0, mclk())) {
           serr(S, SERR_WATCHDOG, -2);
           return true;
         }
@@ -724,7 +731,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
         continue;
       }
       const unsigned long long nw = mclk();
-      if (nw - t_idle > WATCHDOG) {
+      if (stalled_for(t_idle, nw)) {
         serr(S, SERR_WATCHDOG, (int)sp);
         break;
       }
