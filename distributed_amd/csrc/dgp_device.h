@@ -217,6 +217,7 @@ struct Dev {
   uint32_t* gw_needs;
   uint8_t* gw_wflags;
   uint32_t* gw_needs_ext;    // needs_what overflow entries [W][NXW]
+  unsigned long long* gw_held;  // [2][W] scratch of a global stimulus: held bytes, held deps per worker
   uint32_t* gw_needs_saved;  // needs_what lines between launches [W][NLW]
   int32_t* run_id;           // placement-log position of each placed task
   int32_t* holder_of;        // the worker a task runs / ran on (its single replica)

@@ -2011,6 +2011,95 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
           place_x(x, c, ROUTE_ROOTISH_Q, -1, true);
         }
       }
+    } else if (D.dep_ptr[x + 1] > D.dep_ptr[x] && D.dep_ptr[x + 1] - D.dep_ptr[x] <= 64 && x != D.dbg_task) {
+      // decide_worker :8550-8593 with the candidates = the dependency holders held in
+      // lanes (at most 64 deps): one objective per distinct holder instead of a sweep
+      // over all W workers. Same keys and the same total order as the sweep below.
+      const int64_t q0 = D.dep_ptr[x];
+      const int kx = (int)(D.dep_ptr[x + 1] - q0);
+      int hj = -1;
+      int64_t nbj = 0;
+      if (lane < kx) {
+        const int d = D.dep_idx[q0 + lane];
+        hj = D.holder_of[d];
+        nbj = nbv(D, D.res_nbytes[d]);
+      }
+      bool first = lane < kx && hj >= 0 && hj < D.W;
+      for (int j = 0; j < kx; j++) {
+        const int hh = __shfl(hj, j);
+        if (j < lane && hh == hj) first = false;
+      }
+      const unsigned long long fm = ballot(first);
+      if (!fm) {
+        serr(S, SERR_CAND, x);
+        break;
+      }
+      const int cw = first ? hj : __shfl(hj, __builtin_ctzll(fm));
+      const double ocw = occ_of<LW>(P, D, cw, durv);  // all lanes: it shuffles
+      int64_t cm = 0;
+      for (int j = 0; j < kx; j++) {
+        const int hh = __shfl(hj, j);
+        const int64_t nb = shfl64(nbj, j);
+        if (hh != cw) cm += nb;
+      }
+      Key b{INFINITY, INT64_MAX, INT32_MAX, 0};
+      if (first) {
+        b.start = ocw / (double)P.nthreads[cw] + (double)cm / (double)D.bandwidth;
+        b.nb = P.nbytes[cw];
+        b.w = cw;
+        b.comm = cm;
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        Key q;
+        q.start = __shfl_xor(b.start, o);
+        q.nb = __shfl_xor(b.nb, o);
+        q.w = __shfl_xor(b.w, o);
+        q.comm = __shfl_xor(b.comm, o);
+        if (key_less(q, b)) b = q;
+      }
+      place_x(x, b.w, ROUTE_NONROOTISH, b.comm, true);
+    } else if (D.dep_ptr[x + 1] - D.dep_ptr[x] > 64 && x != D.dbg_task) {
+      // decide_worker :8550-8593 for a wide fan-in (the shuffle barrier: P deps): one
+      // lane-parallel pass over the deps accumulates, per holder, the bytes it already
+      // holds and how many deps it holds; then comm(c) = total - held(c) (exact int64)
+      // and c is a candidate iff it holds one. Same keys as the sweep below.
+      unsigned long long* HS = D.gw_held;
+      unsigned long long* HC = D.gw_held + D.W;
+      for (int c = lane; c < D.W; c += 64) {
+        __hip_atomic_store(HS + c, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(HC + c, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __threadfence();
+      int64_t tot = 0;
+      for (int64_t q = D.dep_ptr[x] + lane; q < D.dep_ptr[x + 1]; q += 64) {
+        const int d = D.dep_idx[q];
+        const int h = D.holder_of[d];
+        const int64_t nb = nbv(D, D.res_nbytes[d]);
+        tot += nb;
+        if (h >= 0 && h < D.W) {
+          __hip_atomic_fetch_add(HS + h, (unsigned long long)nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(HC + h, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      __threadfence();
+      tot = wsum64(tot);
+      Key b = argmin_workers(D, [&](int cw, Key& kk) {
+        const double ocw = occ_of<LW>(P, D, cw, durv);  // all lanes: it shuffles
+        const unsigned long long hc = __hip_atomic_load(HC + cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t hs = (int64_t)__hip_atomic_load(HS + cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (hc == 0) return false;
+        const int64_t cm = tot - hs;
+        kk.start = ocw / (double)P.nthreads[cw] + (double)cm / (double)D.bandwidth;
+        kk.nb = P.nbytes[cw];
+        kk.w = cw;
+        kk.comm = cm;
+        return true;
+      });
+      if (b.w == INT32_MAX) {
+        serr(S, SERR_CAND, x);
+        break;
+      }
+      place_x(x, b.w, ROUTE_NONROOTISH, b.comm, true);
     } else if (D.dep_ptr[x + 1] > D.dep_ptr[x]) {  // decide_worker :8550-8593
       Key b = argmin_workers(D, [&](int cw, Key& kk) {
         const double ocw = occ_of<LW>(P, D, cw, durv);  // all lanes: it shuffles

@@ -349,6 +349,7 @@ int dgp_set_workers(dgp_engine* e, int32_t n_workers, const int32_t* nthreads) {
     rc |= dalloc(e, &D.gw_needs, W * S::NLW, e->allocs);
     rc |= dalloc(e, &D.gw_wflags, W, e->allocs);
     rc |= dalloc(e, &D.gw_needs_ext, W * S::NXW, e->allocs);
+    rc |= dalloc(e, &D.gw_held, 2 * W, e->allocs);
     rc |= dalloc(e, &D.gw_needs_saved, W * S::NLW, e->allocs);
   }
   rc |= dalloc(e, &D.t_key, 2 * (size_t)D.Wp, e->allocs);
