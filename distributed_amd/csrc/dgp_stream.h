@@ -1212,6 +1212,19 @@ __device__ __forceinline__ bool st_needed_elsewhere(const Dev& D, int d, int w, 
   return false;
 }
 
+// The bytes of deps [k0, k1) of task `except` (on worker c) that no other task on c
+// needs: in scan mode needs_inc / needs_dec return exactly these, and change nothing,
+// so the deps are taken 64 at a time (int64 sum: exact in any order).
+__device__ __forceinline__ int64_t scan_needs_sum(const Dev& D, int64_t k0, int64_t k1, int c, int except) {
+  int64_t v = 0;
+  for (int64_t q = k0 + lane_id(); q < k1; q += 64) {
+    const int d = D.dep_idx[q];
+    if (D.holder_of[d] == c) continue;
+    if (!st_needed_elsewhere(D, d, c, except)) v += nbv(D, D.res_nbytes[d]);
+  }
+  return wsum64(v);
+}
+
 template <bool LW>
 __device__ __forceinline__ uint32_t line_load(const WPtr<LW>& P, int c) {
   return lane_id() < NLW ? P.needs[(size_t)c * NLW + lane_id()] : 0u;
@@ -1886,6 +1899,10 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
     uint32_t nl = line_load<LW>(P, c);
     int64_t dn = 0;
     for (int64_t k = D.dep_ptr[x]; k < D.dep_ptr[x + 1]; k++) {
+      if (rlu(nl, NLW - 1) == NL_OVF) {  // scan mode reads only: the rest lane-parallel
+        dn += scan_needs_sum(D, k, D.dep_ptr[x + 1], c, x);
+        break;
+      }
       const int d = D.dep_idx[k];
       if (D.holder_of[d] == c) continue;
       dn += needs_inc(D, S, c, nl, d, nbv(D, D.res_nbytes[d]), x);
@@ -1921,6 +1938,10 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
     uint32_t nl = line_load<LW>(P, w);
     int64_t dnet = 0;
     for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+      if (rlu(nl, NLW - 1) == NL_OVF) {  // scan mode reads only: the rest lane-parallel
+        dnet -= scan_needs_sum(D, k, D.dep_ptr[t + 1], w, t);
+        break;
+      }
       const int d = D.dep_idx[k];
       if (D.holder_of[d] == w) continue;
       dnet -= needs_dec(D, S, w, nl, d, nbv(D, D.res_nbytes[d]), t);
