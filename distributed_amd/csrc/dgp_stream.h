@@ -1968,15 +1968,30 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       D.holders[(size_t)t * D.WB + (w >> 6)] = 0;
       atomicAdd((unsigned long long*)&D.g_relwait[grp_t], 1ull);
     }
-    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+    if constexpr (!LW) {
+      for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+        const int d = D.dep_idx[k];
+        if (D.rel_mark[d] != (int)r) continue;
+        const int hd = D.holder_of[d];
+        P.nbytes[hd] -= nbv(D, D.res_nbytes[d]);
+        D.state[d] = S_RELEASED;
+        D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
+        atomicAdd((unsigned long long*)&D.g_relwait[D.group[d]], 1ull);
+      }
+    }
+  }
+  if constexpr (LW) {  // 64 deps at a time; holders' ws.nbytes by LDS atomics (int64: exact)
+    lds_fence();
+    for (int64_t k = D.dep_ptr[t] + lane; k < D.dep_ptr[t + 1]; k += 64) {
       const int d = D.dep_idx[k];
       if (D.rel_mark[d] != (int)r) continue;
       const int hd = D.holder_of[d];
-      P.nbytes[hd] -= nbv(D, D.res_nbytes[d]);
+      __hip_atomic_fetch_add(P.nbytes + hd, -nbv(D, D.res_nbytes[d]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       D.state[d] = S_RELEASED;
       D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
       atomicAdd((unsigned long long*)&D.g_relwait[D.group[d]], 1ull);
     }
+    lds_fence();
   }
   wbar();
   // -------------------------------------- frontier, ascending priority (:2313-2336)
