@@ -1887,6 +1887,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
     return wsum64(v);
   };
   WDict wd;
+  bool skip_deps = false;  // the caller knows c holds every dependency of x
   // _add_to_processing (:3199) of x on c; x WAITING (frontier) or QUEUED (refill)
   auto place_x = [&](int x, int c, int route, int64_t comm, bool was_waiting) {
     if (comm < 0) comm = comm_bytes(x, c);
@@ -1898,7 +1899,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
     if (!dict_update<LW>(P, c, px, +1, wd)) serr(S, SERR_PREFIX, x);
     uint32_t nl = line_load<LW>(P, c);
     int64_t dn = 0;
-    for (int64_t k = D.dep_ptr[x]; k < D.dep_ptr[x + 1]; k++) {
+    for (int64_t k = skip_deps ? 0 : D.dep_ptr[x]; !skip_deps && k < D.dep_ptr[x + 1]; k++) {
       if (rlu(nl, NLW - 1) == NL_OVF) {  // scan mode reads only: the rest lane-parallel
         dn += scan_needs_sum(D, k, D.dep_ptr[x + 1], c, x);
         break;
@@ -1995,10 +1996,33 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   }
   wbar();
   // -------------------------------------- frontier, ascending priority (:2313-2336)
-  for (int64_t k = f0; k < f1; k++) {
-    const int x = D.dpt_idx[k];
-    if (D.fr_mark[x] != (int)r) continue;
-    if (D.tflags[x] & TF_ROOTISH) {
+  // 64 dependents at a time: lane j prefetches dependent j's id, frontier mark, flags and,
+  // for a single-dependency task, that dependency's holder (none of these change while
+  // the frontier is placed), so the serial walk below reads them with readlane.
+  bool fr_stop = false;
+  for (int64_t k0 = f0; k0 < f1 && !fr_stop; k0 += 64) {
+   int xl = 0, fml = -1, tfl = 0, h1l = -1;
+   if (k0 + lane < f1) {
+     xl = D.dpt_idx[k0 + lane];
+     fml = D.fr_mark[xl];
+     tfl = D.tflags[xl];
+     const int64_t a = D.dep_ptr[xl], e = D.dep_ptr[xl + 1];
+     if (e - a == 1) h1l = D.holder_of[D.dep_idx[a]];
+   }
+   const int nk = (int)min((int64_t)64, f1 - k0);
+   for (int j = 0; j < nk; j++) {
+    const int x = rl(xl, j);
+    if (rl(fml, j) != (int)r) continue;
+    const int hx = rl(h1l, j);
+    if (!(rl(tfl, j) & TF_ROOTISH) && hx >= 0 && hx < D.W && x != D.dbg_task) {
+      // decide_worker (:8550-8593) with one dependency: its holder is the only candidate
+      // and is returned directly (:8579); comm_bytes is 0 and c needs no new replica
+      skip_deps = true;
+      place_x(x, hx, ROUTE_NONROOTISH, 0, true);
+      skip_deps = false;
+      continue;
+    }
+    if (rl(tfl, j) & TF_ROOTISH) {
       const int gi = D.group[x];
       if (D.sat_inf) {  // decide_worker_rootish_queuing_disabled :2135-2193
         int c = D.g_lastw[gi];
@@ -2171,6 +2195,8 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       serr(S, SERR_CAND, x);
       break;
     }
+   }
+   if (vload(&S.error) != 0) fr_stop = true;
   }
   // ---------------------------- Scheduler.stimulus_queue_slots_maybe_opened :4983-5023
   if (S.qlen > 0 && !D.sat_inf) {
