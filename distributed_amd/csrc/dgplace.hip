@@ -163,7 +163,7 @@ int sync_dev(dgp_engine* e) {
   const char* dt = getenv("DGP_DEBUG_TASK");
   e->D.dbg_task = dt ? atoi(dt) : -2;
   const char* pl = getenv("DGP_PRE_LEAD");
-  e->D.pre_lead = pl ? atoi(pl) : 4096;
+  e->D.pre_lead = pl ? atoi(pl) : dgp::st::DR;
   if (e->D.pre_lead < 64 || e->D.pre_lead > dgp::st::DR) e->D.pre_lead = dgp::st::DR;
   if (!e->D.dbgbuf) HIPCHK(e, hipMalloc((void**)&e->D.dbgbuf, 64 * 8 * sizeof(double)));
   dgp::Dev h[2] = {e->D, e->D};
