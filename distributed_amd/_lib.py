@@ -28,7 +28,8 @@ SIGNATURES = {
     "dgp_reset": (C.c_int, [_P]),
     "dgp_update_graph": (C.c_int, [_P]),
     "dgp_run_rounds": (C.c_int, [_P, C.c_int64, _P]),
-    "dgp_tasks_finished": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P]),
+    "dgp_tasks_finished": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dgp_snapshot": (C.c_int, [_P]),
     "dgp_num_placements": (C.c_int64, [_P]),
     "dgp_get_placements": (C.c_int, [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, _P]),
     "dgp_enable_snapshots": (C.c_int, [_P, C.c_int64]),
@@ -42,7 +43,7 @@ SIGNATURES = {
                                     _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _lib = None
 
 

@@ -240,6 +240,18 @@ struct Dev {
   double* dbgbuf;      // [64][8]
   int32_t pre_lead;  // stream: how far (stimuli) PRE may run ahead of SEQ (<= DR)
   int32_t dbg;  // stream debug: 1 every stimulus waits for all earlier ones, 2 every stimulus global
+  // ---- the stimulus log the stream engine consumes. Replay mode: stimulus r completes
+  // placement r (stim_task / stim_worker alias pl_task / pl_worker, cseq aliases run_id).
+  // Service mode (dgp_tasks_finished): the accepted task-finished messages, in arrival order.
+  const int32_t* stim_task;
+  const int32_t* stim_worker;
+  int32_t* cseq;         // stimulus index of each task's completion (-1: not completed)
+  int32_t svc;           // 1: service mode (the launch ends at *svc_len)
+  long long* svc_len;    // service mode: stimulus-log length (device)
+  int32_t* sv_task;      // service-mode stimulus log [sv_cap]
+  int32_t* sv_worker;
+  int32_t* sv_cseq;      // [N]
+  int64_t sv_cap;
 };
 
 // dynamic LDS of the commit kernel: owner[W] reservation table, then (lds_workers) the

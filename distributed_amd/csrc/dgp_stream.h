@@ -59,7 +59,9 @@ constexpr int SCTA = DGP_SCTA;   // 768: 12 waves = 5 roles + 7 executors (168 V
 constexpr int WIN = 32;          // in-flight stimulus slots (LDS window)
 constexpr int NE = 64;           // 16-byte descriptor entries per stimulus (one per lane)
 #ifndef DGP_DR
-#define DGP_DR 512  // 512 x 768 B = 384 KB stays in L2: PMC read traffic 1.31 -> 0.18 GB per C2 replay, same time
+// 512 rows x (64 x 16 B descriptor + 32 x 4 B touch list) = 576 KB stays in L2: PMC read
+// traffic 1.31 -> 0.18 GB per C2 replay, same time
+#define DGP_DR 512
 #endif
 constexpr int DR = DGP_DR;       // descriptor ring (global) — how far PRE may run ahead
 constexpr int PLC = 64;          // staged placements / records per stimulus
@@ -74,6 +76,8 @@ constexpr int BIG = 1 << 24;     // registration guard of a slot's predecessor c
 constexpr uint32_t NL_OVF = 0xffffffffu;
 constexpr int N_ROLE = 5;        // waves 0..4 are SEQ, BLD, PRE, REG, WLK; the rest execute
 constexpr int E_HDR = 7;         // header entries: 0 ids, 1 sizes/counts, 2 duration, 3..6 durations
+// rows are selected with r & (DR - 1); PRE runs at most DR ahead and at least one window
+static_assert((DR & (DR - 1)) == 0 && DR >= 64 && DR >= WIN, "DGP_DR must be a power of two >= 64");
 
 enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16 };
 enum : int { K_COMPLETE = 1, K_PLACE = 2 };
@@ -115,6 +119,7 @@ struct SCtl {
   unsigned ready;      // slots whose stimulus may run
   long long seq_pos, log_len, rec_len, walk_pos, bld_pos, pre_pos, reg_pos, reg_limit;
   long long qhead, qlen, n_tasks;
+  long long stim_end;  // service mode: stimuli [seq_pos, stim_end) run in this launch
   long long round_end, rounds_left, prev_placed;
   long long rounds_nonempty, snap_idx;
   int snaps;
@@ -382,13 +387,13 @@ __device__ __attribute__((always_inline)) void serr(SCtl& S, int code, int task)
 }
 
 
-constexpr unsigned long long WATCHDOG = 40000000000ull;  // s_memtime ticks without progress (~16 s)
-// true once `now` is more than WATCHDOG ticks past `since`. The difference is taken
-// signed: a counter read that comes back below an earlier one (observed once on a C5
-// replay, where the unsigned difference wrapped and fired the watchdog 2 s in) is
-// not a stall.
+// The watchdog runs on s_memrealtime, the constant 100 MHz counter (s_memtime is the
+// shader clock: its rate follows the power state, and one read was seen to go backwards
+// during a C5 replay). 16 s without progress stops the engine with SERR_WATCHDOG.
+constexpr unsigned long long WATCHDOG = 1600000000ull;  // s_memrealtime ticks (100 MHz): 16 s
+__device__ __forceinline__ unsigned long long rclk() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ bool stalled_for(unsigned long long since, unsigned long long now) {
-  return (long long)(now - since) > (long long)WATCHDOG;
+  return now - since > WATCHDOG;
 }
 
 __device__ __forceinline__ int64_t nbv(const Dev& D, int64_t v) { return v >= 0 ? v : D.default_data_size; }
@@ -490,7 +495,8 @@ __device__ __forceinline__ void ws_fold(const Dev& D, const WPtr<LW>& P, SCtl& S
                                         long long dnet, double occ, int nproc, double dobs) {
   const int lane = lane_id();
   if (kind == K_COMPLETE) {
-    if (lane == p) g.wd = g.wd < 0 ? dobs : 0.5 * dobs + 0.5 * g.wd;
+    // no compute interval in the message (NaN): no EWMA step (TaskGroup.add_duration :1114)
+    if (lane == p && dobs == dobs) g.wd = g.wd < 0 ? dobs : 0.5 * dobs + 0.5 * g.wd;
     gdict_add(g, p, -1);
   } else if (!gdict_add(g, p, +1)) {
     serr(S, SERR_PREFIX, -1);
@@ -544,7 +550,7 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
   // (a) durations unchanged: every completion's EWMA result equals the current value
   const double cur = __shfl(g.wd, p & (PD - 1));
   const double nw = cur < 0 ? rc.dur : 0.5 * rc.dur + 0.5 * cur;
-  bool bad = in && kind == K_COMPLETE && __double_as_longlong(nw) != __double_as_longlong(cur);
+  bool bad = in && kind == K_COMPLETE && rc.dur == rc.dur && __double_as_longlong(nw) != __double_as_longlong(cur);
   // (b) prefix counts stay >= 1 and every record's prefix is in the dict
   bool found = !in;
   long long cnt_i[PD];
@@ -675,14 +681,19 @@ template <bool LW>
 __device__ __attribute__((always_inline)) bool round_end_step(const Dev& D, SLds& L, const WPtr<LW>& P, long long& round_start) {
   SCtl& S = L.c;
   const int lane = lane_id();
+  if (D.svc) {  // service mode: the launch ends with the stimulus log (no synthetic rounds)
+    round_start = S.round_end;
+    if (lane == 0) vstore(&S.stop, 1);
+    return true;
+  }
   if (S.round_end > round_start) {
     if (lane == 0) S.rounds_nonempty++;
     wbar();
     if (S.snaps) {
-      const unsigned long long t0 = mclk();
+      const unsigned long long t0 = rclk();
       while (vload(&S.walk_pos) != vload(&S.rec_len) || vload(&S.busy_exe) != 0) {
         if (vload(&S.stop)) return true;
-        if (stalled_for(t0, mclk())) {
+        if (stalled_for(t0, rclk())) {
           serr(S, SERR_WATCHDOG, -2);
           return true;
         }
@@ -718,7 +729,7 @@ template <bool LW>
 __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, const WPtr<LW>& P, long long& round_start) {
   SCtl& S = L.c;
   const int lane = lane_id();
-  unsigned long long t_idle = mclk(), t_sq = t_idle;
+  unsigned long long t_sq = mclk(), t_idle = rclk();
   while (true) {
     if (vload(&S.stop)) break;
     const long long sp = S.seq_pos;
@@ -730,11 +741,11 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
     if (m == 0) {
       if (sp == re) {
         if (round_end_step<LW>(D, L, P, round_start)) break;
-        t_idle = mclk();
+        t_idle = rclk();
         continue;
       }
       const unsigned long long nw = mclk();
-      if (stalled_for(t_idle, nw)) {
+      if (stalled_for(t_idle, rclk())) {
         serr(S, SERR_WATCHDOG, (int)sp);
         break;
       }
@@ -782,6 +793,12 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
     }
     const int tpl = rl(ipl, 63), trc = rl(irc, 63), tpo = rl(ipo, 63);
     const long long lb = S.log_len + (ipl - npl), rb = S.rec_len + (irc - nrec), qb = S.qhead + (ipo - npop);
+    // capacity first: nothing is copied past the record log (rlog_cap = 2N + 4096 covers one
+    // K_COMPLETE per completion and one K_PLACE per placement, the only record kinds)
+    if (S.rec_len + trc > D.rlog_cap || S.log_len + tpl > D.N) {
+      serr(S, SERR_REC, (int)sp);
+      break;
+    }
     if (lane < m && !direct) {
       const size_t st0 = (size_t)s * PLC;
       int popk = 0;
@@ -805,7 +822,6 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
       }
       for (int j = 0; j < nrec; j++) D.rlog[rb + j] = D.srec[st0 + j];
     }
-    if (rb + trc > D.rlog_cap) serr(S, SERR_REC, (int)sp);
     __threadfence_block();
     if (lane == 0) {
       S.log_len += tpl;
@@ -821,8 +837,8 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
       vstore(&S.seq_pos, sp + m);
 
     }
-    t_idle = mclk();
-    t_sq = t_idle;
+    t_idle = rclk();
+    t_sq = mclk();
   }
 }
 
@@ -831,8 +847,8 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
 __device__ __attribute__((always_inline)) void bld_range(const Dev& D, long long a, long long e) {
   const long long r = a + lane_id();
   if (r >= e) return;
-  const int t = D.pl_task[r];
-  const int w = D.pl_worker[r];
+  const int t = D.stim_task[r];
+  const int w = D.stim_worker[r];
   // the replica this completion creates (who_has, :3148)
   atomicOr(&D.holders[(size_t)t * D.WB + (w >> 6)], 1ull << (w & 63));
   const int64_t f0 = D.dpt_ptr[t], f1 = D.dpt_ptr[t + 1];
@@ -840,7 +856,7 @@ __device__ __attribute__((always_inline)) void bld_range(const Dev& D, long long
     const int x = D.dpt_idx[k];
     if (atomicSub(&D.remaining[x], 1) == 1) {
       int s = -1;  // the stimulus that empties waiting_on: the dependency completed last
-      for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++) s = max(s, D.run_id[D.dep_idx[q]]);
+      for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++) s = max(s, D.cseq[D.dep_idx[q]]);
       D.fr_mark[x] = s;
     }
   }
@@ -849,7 +865,7 @@ __device__ __attribute__((always_inline)) void bld_range(const Dev& D, long long
     const int d = D.dep_idx[k];
     if (atomicSub(&D.waiters[d], 1) == 1 && !(D.tflags[d] & TF_WANTED)) {
       int s = -1;
-      for (int64_t q = D.dpt_ptr[d]; q < D.dpt_ptr[d + 1]; q++) s = max(s, D.run_id[D.dpt_idx[q]]);
+      for (int64_t q = D.dpt_ptr[d]; q < D.dpt_ptr[d + 1]; q++) s = max(s, D.cseq[D.dpt_idx[q]]);
       D.rel_mark[d] = s;
     }
   }
@@ -873,8 +889,8 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
     if (nt < TMAX) scr[nt] = (uint16_t)c;
     nt++;
   };
-  const int t = D.pl_task[r];
-  const int w = D.pl_worker[r];
+  const int t = D.stim_task[r];
+  const int w = D.stim_worker[r];
   const int p = D.prefix[t];
   const int g = D.group[t];
   const uint8_t tf = D.tflags[t];
@@ -959,7 +975,10 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
   while (true) {
     if (vload(&S.stop)) break;
     const long long a = KIND == 0 ? S.bld_pos : S.pre_pos;
-    const long long hi = KIND == 0 ? vload(&S.log_len) : min(vload(&S.bld_pos), vload(&S.seq_pos) + D.pre_lead);
+    // BLD: completions up to the placement log (replay: stimulus r completes placement r)
+    // or the stimulus log (service); PRE: what BLD has built, at most pre_lead ahead of SEQ
+    const long long hi = KIND == 0 ? (D.svc ? S.stim_end : vload(&S.log_len))
+                                   : min(vload(&S.bld_pos), vload(&S.seq_pos) + D.pre_lead);
     const long long e = min(a + 64, hi);
     if (e <= a) {
       __builtin_amdgcn_s_sleep(2);
@@ -1090,7 +1109,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
       const int s = (int)(r & (WIN - 1));
       uint4 E = EB[b];
       const int p = pb[b];
-      if (lane == 3 + (p >> 1)) {  // TaskPrefix.add_duration, in stimulus order
+      if (lane == 3 + (p >> 1) && dob[b] == dob[b]) {  // TaskPrefix.add_duration, in stimulus order (NaN: none)
         if (p & 1) dur1 = dur1 < 0 ? dob[b] : 0.5 * dob[b] + 0.5 * dur1;
         else dur0 = dur0 < 0 ? dob[b] : 0.5 * dob[b] + 0.5 * dur0;
       }
@@ -2445,12 +2464,13 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     S.qhead = c->qhead;
     S.qlen = c->qlen;
     S.n_tasks = c->n_tasks;
-    S.round_end = pos->round_end >= 0 ? pos->round_end : (long long)c->n_placed;
+    S.stim_end = D.svc ? *D.svc_len : -1;
+    S.round_end = D.svc ? S.stim_end : pos->round_end >= 0 ? pos->round_end : (long long)c->n_placed;
     S.rounds_left = max_rounds > 0 ? max_rounds : -1;
     S.prev_placed = pos->round_end >= 0 ? pos->prev_placed : (long long)c->n_placed;
     S.rounds_nonempty = c->rounds_nonempty;
-    S.snaps = snaps;
-    S.reg_limit = (snaps || max_rounds > 0) ? S.round_end : (1ll << 62);
+    S.snaps = D.svc ? 0 : snaps;
+    S.reg_limit = (!D.svc && (snaps || max_rounds > 0)) ? S.round_end : (1ll << 62);
     S.g_plen = min(c->g_plen, PD);
     for (int i = 0; i < PD; i++) {
       S.g_pfx[i] = i < c->g_plen ? c->g_pfx[i] : 0;

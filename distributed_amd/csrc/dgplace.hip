@@ -26,6 +26,7 @@
 #include "dgp_device.h"
 #include "dgp_stream.h"
 #include "dgp_steal.h"
+#include "dgp_service.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -37,7 +38,9 @@ struct dgp_engine {
   std::string err;
   dgp::Dev D{};
   dgp::Ctl* ctl = nullptr;
-  long long* d_aux = nullptr;  // [0] next round start, [1] placements at the last snapshot
+  long long* d_aux = nullptr;  // [0] next round start, [1] placements at the last snapshot,
+                               // [2] service stimuli consumed by the round engine,
+                               // [3] messages one k_svc_append call answered
   dgp::Dev* d_dev = nullptr;    // [0] Dev for every kernel, [1] Dev with lds_workers for k_commit
   std::vector<void*> allocs;
   std::vector<void*> graph_allocs;
@@ -48,10 +51,14 @@ struct dgp_engine {
   std::vector<double> prefix_defaults;
   std::vector<int64_t> group_sizes;
   int64_t E = 0;
-  int32_t* d_batch = nullptr;
-  int64_t batch_cap = 0;
   int rounds_per_sync = 16;
   bool stream_used = false;  // the stream engine ran: the round-kernel path is no longer valid
+  int mode = 0;              // 0 fresh, 1 replay (dgp_run_rounds), 2 service (dgp_tasks_finished)
+  dgp::svc::Msg* d_msgs = nullptr;  // service-mode message batch (device) + status
+  int8_t* d_status = nullptr;
+  dgp::svc::Msg* h_msgs = nullptr;  // pinned staging of the batch
+  int64_t msgs_cap = 0;
+  unsigned long long last_placed = 0;  // placement-log length after the last synchronising call
   // timing: (start, stop) event pairs recorded around launches, resolved lazily
   bool timing = false;
   double kms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -180,40 +187,85 @@ int grid_for(int64_t n, int per_block, int cap) {
   return (int)b;
 }
 
-// enqueue one round (no host synchronisation); ext != nullptr: explicit completion batch
-int enqueue_round(dgp_engine* e, const int32_t* ext, int64_t ext_n) {
-  const dgp::Dev& D = e->D;
-  const dgp::Dev* DP = e->d_dev;
-  const dgp::Dev* DPC = e->d_dev + 1;
-  hipStream_t s = e->stream;
-  const int64_t N = D.N;
-  const int big = grid_for(N, 256, 128);
-  const int lds_workers = D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;  // matches sync_dev
-  const size_t lds = (((size_t)D.W * sizeof(int) + 15) & ~(size_t)15) +
-                     (lds_workers ? (((size_t)D.W + 3) & ~(size_t)3) * dgp::LDS_WORKER_BYTES + 64 : 0);
-  if (lds > 160 * 1024) return fail(e, DGP_E_ARG, "commit LDS exceeds 160 KiB");
-  hipLaunchKernelGGL(dgp::k_round_begin, dim3(1), dim3(1), 0, s, DP, e->d_aux, ext, (long long)ext_n);
+// run_id / holder_of of the placements the stream engine has not sequenced itself
+int set_runids(dgp_engine* e) {
+  hipLaunchKernelGGL(dgp::svc::k_set_runids, dim3(64), dim3(256), 0, e->stream, e->d_dev);
+  hipLaunchKernelGGL(dgp::svc::k_set_runids_done, dim3(1), dim3(64), 0, e->stream, e->d_dev);
   HIPCHK(e, hipGetLastError());
-  if (int rc = timed_launch(e, 0, [&] { hipLaunchKernelGGL(dgp::k_frontier_release, dim3(big), dim3(256), 0, s, DP); }))
-    return rc;
-  if (int rc = timed_launch(e, 1, [&] {
-        hipLaunchKernelGGL(dgp::k_candidate_commbytes, dim3(grid_for(N, 4, 256)), dim3(256), 0, s, DP);
+  return 0;
+}
+
+// the stimulus source of the stream engine for the coming launch
+void stream_source(dgp_engine* e, bool service) {
+  dgp::Dev& D = e->D;
+  D.svc = service ? 1 : 0;
+  D.stim_task = service ? D.sv_task : D.pl_task;
+  D.stim_worker = service ? D.sv_worker : D.pl_worker;
+  D.cseq = service ? D.sv_cseq : D.run_id;
+}
+
+// one launch of the stream kernel over the stimulus source set by stream_source()
+int launch_stream(dgp_engine* e, long long max_rounds, int snaps) {
+  const dgp::Dev& D = e->D;
+  const size_t lds_w = dgp::st::lds_worker_bytes(D.W);
+  const bool lw = sizeof(dgp::st::SLds) + lds_w <= 160 * 1024;
+  HIPCHK(e, hipMemcpyToSymbolAsync(HIP_SYMBOL(dgp::st::c_dev), &e->D, sizeof(dgp::Dev), 0, hipMemcpyHostToDevice,
+                                   e->stream));
+  long long mr = max_rounds;
+  int sn = snaps;
+  void* args[] = {&mr, &sn};
+  const void* fn = lw ? (const void*)dgp::st::k_stream<true> : (const void*)dgp::st::k_stream<false>;
+  if (lw) HIPCHK(e, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w));
+  // ONE workgroup: every hand-off between the roles stays on this CU
+  hipError_t lst = hipSuccess;
+  if (int rc = timed_launch(e, 2, [&] {
+        lst = hipLaunchKernel(fn, dim3(1), dim3(dgp::st::SCTA), args, lw ? lds_w : 0, e->stream);
       }))
     return rc;
-  if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_events, dim3(big), dim3(256), 0, s, DP); })) return rc;
-  if (int rc = timed_launch(e, 2, [&] { hipLaunchKernelGGL(dgp::k_commit, dim3(1), dim3(dgp::CTA), lds, s, DPC); }))
-    return rc;
-  if (e->snap_rounds > 0) {
-    hipLaunchKernelGGL(dgp::k_walk, dim3(1), dim3(64), 0, s, DP);
-    hipLaunchKernelGGL(dgp::k_snapshot, dim3(8), dim3(256), 0, s, DP, e->d_aux + 1, 1);
-    HIPCHK(e, hipGetLastError());
-  }
+  if (lst != hipSuccess) return fail(e, DGP_E_HIP, std::string("stream launch: ") + hipGetErrorString(lst));
+  e->stream_used = true;
   return 0;
 }
 
 int walk(dgp_engine* e) {
   const dgp::Dev* DP = e->d_dev;
   return timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_walk, dim3(1), dim3(64), 0, e->stream, DP); });
+}
+
+// run the stimuli appended since the last launch: the stream engine, or one round of the
+// round-kernel engine when the graph has more prefixes than the stream descriptors carry
+int run_service_stimuli(dgp_engine* e) {
+  namespace V = dgp::svc;
+  hipStream_t s = e->stream;
+  if (e->D.P <= dgp::st::PD) {
+    stream_source(e, true);
+    if (int rc = launch_stream(e, -1, 0)) return rc;
+  } else {
+    // more prefixes than the stream descriptors carry: the accepted batch is one round of
+    // the round-kernel engine (completions in message order)
+    const dgp::Dev* DP = e->d_dev;
+    const dgp::Dev* DPC = e->d_dev + 1;
+    const int64_t N = e->D.N;
+    const int big = grid_for(N, 256, 128);
+    const int lds_workers = e->D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
+    const size_t lds = (((size_t)e->D.W * sizeof(int) + 15) & ~(size_t)15) +
+                       (lds_workers ? (((size_t)e->D.W + 3) & ~(size_t)3) * dgp::LDS_WORKER_BYTES + 64 : 0);
+    if (lds > 160 * 1024) return fail(e, DGP_E_ARG, "commit LDS exceeds 160 KiB");
+    hipLaunchKernelGGL(V::k_svc_round_begin, dim3(1), dim3(64), 0, s, DP, e->d_aux + 2);
+    if (int rc = timed_launch(e, 0, [&] { hipLaunchKernelGGL(dgp::k_frontier_release, dim3(big), dim3(256), 0, s, DP); }))
+      return rc;
+    if (int rc = timed_launch(e, 1, [&] {
+          hipLaunchKernelGGL(dgp::k_candidate_commbytes, dim3(grid_for(N, 4, 256)), dim3(256), 0, s, DP);
+        }))
+      return rc;
+    if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_events, dim3(big), dim3(256), 0, s, DP); }))
+      return rc;
+    if (int rc = timed_launch(e, 2, [&] { hipLaunchKernelGGL(dgp::k_commit, dim3(1), dim3(dgp::CTA), lds, s, DPC); }))
+      return rc;
+    if (int rc = walk(e)) return rc;
+    if (int rc = set_runids(e)) return rc;
+  }
+  return 0;
 }
 
 }  // namespace
@@ -275,7 +327,9 @@ void dgp_destroy(dgp_engine* e) {
   (void)hipStreamSynchronize(e->stream);
   free_list(e->allocs);
   free_list(e->graph_allocs);
-  if (e->d_batch) (void)hipFree(e->d_batch);
+  if (e->d_msgs) (void)hipFree(e->d_msgs);
+  if (e->d_status) (void)hipFree(e->d_status);
+  if (e->h_msgs) (void)hipHostFree(e->h_msgs);
   (void)hipFree(e->ctl);
   (void)hipFree(e->d_aux);
   (void)hipFree(e->d_dev);
@@ -500,7 +554,17 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
   rc |= dalloc(e, &D.rel_mark, N, L);
   D.rlog_cap = 2 * N + 4096;
   rc |= dalloc(e, &D.rlog, D.rlog_cap, L);
+  // service mode: the stimulus log (each task completes at most once) and its length
+  D.sv_cap = N;
+  rc |= dalloc(e, &D.sv_task, N, L);
+  rc |= dalloc(e, &D.sv_worker, N, L);
+  rc |= dalloc(e, &D.sv_cseq, N, L);
+  rc |= dalloc(e, &D.svc_len, 1, L);
   if (rc) return DGP_E_HIP;
+  // completion reports default to "unknown" until dgp_set_task_results / dgp_tasks_finished
+  HIPCHK(e, hipMemset(D.res_nbytes, 0xff, N * 8));
+  HIPCHK(e, hipMemset(D.res_start, 0, N * 8));
+  HIPCHK(e, hipMemset(D.res_stop, 0, N * 8));
   auto up = [&](const void* dst, const void* src, size_t bytes) {
     return hipMemcpy(const_cast<void*>(dst), src, bytes, hipMemcpyHostToDevice);
   };
@@ -562,6 +626,10 @@ int dgp_reset(dgp_engine* e) {
     p0.round_end = -1;
     HIPCHK(e, hipMemcpyAsync(D.pos, &p0, sizeof p0, hipMemcpyHostToDevice, s));
     e->stream_used = false;
+    HIPCHK(e, hipMemsetAsync(D.svc_len, 0, sizeof(long long), s));
+    HIPCHK(e, hipMemsetAsync(D.sv_cseq, 0xff, N * 4, s));
+    e->mode = 0;
+    e->last_placed = 0;
   }
   std::vector<double> maxexec(D.P, -1.0);
   HIPCHK(e, hipMemcpyAsync(D.pdur_cur, e->prefix_defaults.data(), D.P * 8, hipMemcpyHostToDevice, s));
@@ -600,6 +668,7 @@ int dgp_update_graph(dgp_engine* e) {
     hipLaunchKernelGGL(dgp::k_snapshot, dim3(8), dim3(256), 0, s, DP, e->d_aux + 1, 0);
     HIPCHK(e, hipGetLastError());
   }
+  if (int rc = set_runids(e)) return rc;
   e->graph_done = true;
   return 0;
 }
@@ -607,7 +676,10 @@ int dgp_update_graph(dgp_engine* e) {
 int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (!e->have_results) return fail(e, DGP_E_STATE, "dgp_set_task_results first");
+  if (e->mode == 2) return fail(e, DGP_E_STATE, "engine is in service mode (dgp_tasks_finished); dgp_reset first");
   HIPCHK(e, hipSetDevice(e->device));
+  e->mode = 1;
+  stream_source(e, false);
   if (n_rounds_out) *n_rounds_out = 0;
   if (max_rounds == 0) return 0;
   if (int rc = sync_dev(e)) return rc;
@@ -617,24 +689,7 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
   const dgp::Dev& D = e->D;
   if (D.P <= dgp::st::PD) {
     // the stream engine: the whole replay in one persistent workgroup (dgp_stream.h)
-    const size_t lds_w = dgp::st::lds_worker_bytes(D.W);
-    const bool lw = sizeof(dgp::st::SLds) + lds_w <= 160 * 1024;
-    const int snaps = e->snap_rounds > 0 ? 1 : 0;
-    HIPCHK(e, hipMemcpyToSymbolAsync(HIP_SYMBOL(dgp::st::c_dev), &e->D, sizeof(dgp::Dev), 0, hipMemcpyHostToDevice,
-                                     e->stream));
-    long long mr = (long long)max_rounds;
-    int sn = snaps;
-    void* args[] = {&mr, &sn};
-    const void* fn = lw ? (const void*)dgp::st::k_stream<true> : (const void*)dgp::st::k_stream<false>;
-    if (lw) HIPCHK(e, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w));
-    // ONE workgroup: every hand-off between the roles stays on this CU
-    hipError_t lst = hipSuccess;
-    if (int rc = timed_launch(e, 2, [&] {
-          lst = hipLaunchKernel(fn, dim3(1), dim3(dgp::st::SCTA), args, lw ? lds_w : 0, e->stream);
-        }))
-      return rc;
-    if (lst != hipSuccess) return fail(e, DGP_E_HIP, std::string("stream launch: ") + hipGetErrorString(lst));
-    e->stream_used = true;
+    if (int rc = launch_stream(e, max_rounds, e->snap_rounds > 0 ? 1 : 0)) return rc;
   } else {
     // more task prefixes than the stream descriptors carry: the round-kernel engine
     if (e->stream_used) return fail(e, DGP_E_STATE, "engine already advanced by the stream replay");
@@ -656,33 +711,64 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
   return 0;
 }
 
-int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* tasks, const int64_t* nbytes, const double* start,
-                       const double* stop) {
+int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* run_id,
+                       const int64_t* nbytes, const double* start, const double* stop, int8_t* status,
+                       int64_t* n_new_placements) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
-  if (e->stream_used) return fail(e, DGP_E_STATE, "engine already advanced by the stream replay (dgp_reset first)");
-  if (n < 0 || (n > 0 && (!tasks || !nbytes || !start || !stop))) return fail(e, DGP_E_ARG, "bad batch");
-  if (n == 0) return 0;
+  if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
+  if (n < 0 || (n > 0 && (!task || !worker || !run_id || !nbytes || !start || !stop || !status)))
+    return fail(e, DGP_E_ARG, "dgp_tasks_finished: bad batch");
+  if (n_new_placements) *n_new_placements = 0;
   HIPCHK(e, hipSetDevice(e->device));
-  if (n > e->batch_cap) {
-    if (e->d_batch) (void)hipFree(e->d_batch);
-    e->d_batch = nullptr;
-    HIPCHK(e, hipMalloc((void**)&e->d_batch, n * 4));
-    e->batch_cap = n;
+  e->mode = 2;
+  if (n == 0) return 0;
+  namespace V = dgp::svc;
+  if (n > e->msgs_cap) {  // grow the pinned staging and the device batch
+    if (e->d_msgs) (void)hipFree(e->d_msgs);
+    if (e->d_status) (void)hipFree(e->d_status);
+    if (e->h_msgs) (void)hipHostFree(e->h_msgs);
+    e->d_msgs = nullptr;
+    e->d_status = nullptr;
+    e->h_msgs = nullptr;
+    e->msgs_cap = 0;
+    const int64_t cap = std::max<int64_t>(n, 1024);
+    HIPCHK(e, hipMalloc((void**)&e->d_msgs, cap * sizeof(V::Msg)));
+    HIPCHK(e, hipMalloc((void**)&e->d_status, cap));
+    HIPCHK(e, hipHostMalloc((void**)&e->h_msgs, cap * sizeof(V::Msg), hipHostMallocDefault));
+    e->msgs_cap = cap;
   }
-  std::vector<uint8_t> st(e->D.N);
-  HIPCHK(e, hipMemcpy(st.data(), e->D.state, e->D.N, hipMemcpyDeviceToHost));
-  for (int64_t i = 0; i < n; i++) {
-    if (tasks[i] < 0 || tasks[i] >= e->D.N) return fail(e, DGP_E_ARG, "task index out of range");
-    if (st[tasks[i]] != dgp::S_PROCESSING) return fail(e, DGP_E_ARG, "task-finished for a task that is not processing");
-    int32_t t = tasks[i];
-    HIPCHK(e, hipMemcpyAsync(e->D.res_nbytes + t, nbytes + i, 8, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->D.res_start + t, start + i, 8, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->D.res_stop + t, stop + i, 8, hipMemcpyHostToDevice, e->stream));
-  }
-  HIPCHK(e, hipMemcpyAsync(e->d_batch, tasks, n * 4, hipMemcpyHostToDevice, e->stream));
+  for (int64_t i = 0; i < n; i++) e->h_msgs[i] = V::Msg{task[i], worker[i], run_id[i], nbytes[i], start[i], stop[i]};
+  hipStream_t s = e->stream;
   if (int rc = sync_dev(e)) return rc;
-  if (int rc = enqueue_round(e, e->d_batch, n)) return rc;
-  if (int rc = walk(e)) return rc;
+  HIPCHK(e, hipMemcpyAsync(e->d_msgs, e->h_msgs, n * sizeof(V::Msg), hipMemcpyHostToDevice, s));
+  // the batch in segments: each ends where an answer depends on the segment's own stimuli
+  // (k_svc_append); usually the whole batch is one segment
+  long long* d_consumed = e->d_aux + 3;
+  dgp::Ctl c;
+  for (int64_t off = 0; off < n;) {
+    hipLaunchKernelGGL(V::k_svc_append, dim3(1), dim3(64), 0, s, e->d_dev, e->d_msgs + off, (long long)(n - off),
+                       e->d_status + off, d_consumed);
+    HIPCHK(e, hipGetLastError());
+    if (int rc = run_service_stimuli(e)) return rc;
+    long long k = 0;
+    HIPCHK(e, hipMemcpyAsync(&k, d_consumed, sizeof k, hipMemcpyDeviceToHost, s));
+    if (int rc = check_device_error(e, &c)) return rc;  // synchronises the stream
+    if (k <= 0) return fail(e, DGP_E_DEVICE, "dgp_tasks_finished: no progress on the batch");
+    off += k;
+  }
+  HIPCHK(e, hipMemcpy(status, e->d_status, n, hipMemcpyDeviceToHost));
+  if (n_new_placements) *n_new_placements = (int64_t)(c.n_placed - e->last_placed);
+  e->last_placed = c.n_placed;
+  return 0;
+}
+
+int dgp_snapshot(dgp_engine* e) {
+  if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (e->snap_rounds <= 0) return fail(e, DGP_E_STATE, "snapshots not enabled");
+  HIPCHK(e, hipSetDevice(e->device));
+  hipLaunchKernelGGL(dgp::svc::k_svc_snapshot_begin, dim3(1), dim3(64), 0, e->stream, e->d_dev);
+  hipLaunchKernelGGL(dgp::k_snapshot, dim3(8), dim3(256), 0, e->stream, e->d_dev, e->d_aux + 1, 0);
+  HIPCHK(e, hipGetLastError());
   return check_device_error(e);
 }
 

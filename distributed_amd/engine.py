@@ -81,7 +81,7 @@ class PlacementEngine:
         self._check(self.lib.dgp_set_workers(self.h, len(nt), _ptr(nt)), "dgp_set_workers")
         self.n_workers = len(nt)
 
-    def set_graph(self, g: dict):
+    def set_graph(self, g: dict, results: bool = True):
         arrs = {
             "dep_ptr": np.ascontiguousarray(g["dep_ptr"], np.int64),
             "dep_idx": np.ascontiguousarray(g["dep_idx"], np.int32),
@@ -98,17 +98,20 @@ class PlacementEngine:
             len(arrs["prefix_default_dur"]), _ptr(arrs["prefix_default_dur"]), _ptr(arrs["group_id"]),
             len(g["group_prefix"]), _ptr(arrs["wanted"]), _ptr(arrs["rootish_override"])), "dgp_set_graph")
         self.n_tasks = n
+        if not results:  # service mode: the task-finished messages carry nbytes / startstops
+            return
         res = [np.ascontiguousarray(g["nbytes"], np.int64), np.ascontiguousarray(g["start"], np.float64),
                np.ascontiguousarray(g["stop"], np.float64)]
         self._check(self.lib.dgp_set_task_results(self.h, *[_ptr(a) for a in res]), "dgp_set_task_results")
 
-    def load(self, g: dict, config: dict | None = None, *, snapshots: int = 0):
-        """Configure workers + config + graph in one go (the usual set-up)."""
+    def load(self, g: dict, config: dict | None = None, *, snapshots: int = 0, results: bool = True):
+        """Configure workers + config + graph in one go (the usual set-up). ``results``:
+        upload the synthetic executor's completion reports (replay mode)."""
         self.set_workers(g["nthreads"])
         self.set_config(config)
         if snapshots:
             self._check(self.lib.dgp_enable_snapshots(self.h, int(snapshots)), "dgp_enable_snapshots")
-        self.set_graph(g)
+        self.set_graph(g, results=results)
         return self
 
     # ------------------------------------------------------------------- replay
@@ -129,11 +132,33 @@ class PlacementEngine:
         self.run_rounds(-1)
         return self.num_placements()
 
-    def tasks_finished(self, tasks, nbytes, start, stop):
-        arrs = [np.ascontiguousarray(tasks, np.int32), np.ascontiguousarray(nbytes, np.int64),
-                np.ascontiguousarray(start, np.float64), np.ascontiguousarray(stop, np.float64)]
-        self._check(self.lib.dgp_tasks_finished(self.h, len(arrs[0]), *[_ptr(a) for a in arrs]),
-                    "dgp_tasks_finished")
+    # ------------------------------------------------------------- service mode
+    # answers of dgp_tasks_finished (include/dgplace.h DGP_TF_*)
+    TF_ACCEPTED, TF_FREE_KEYS, TF_ADD_KEYS, TF_RELEASE, TF_UNKNOWN_WORKER, TF_IMPOSSIBLE, TF_UNSUPPORTED = range(7)
+
+    def tasks_finished(self, task, worker, run_id, nbytes=None, start=None, stop=None):
+        """A batch of task-finished messages (Scheduler.handle_task_finished,
+        distributed/scheduler.py:5783-5797), in arrival order. ``nbytes`` < 0 means None;
+        ``start``/``stop`` is the "compute" startstop (NaN: none). Returns (status per
+        message, number of placements the batch made)."""
+        t = np.ascontiguousarray(task, np.int32).reshape(-1)
+        n = len(t)
+        w = np.ascontiguousarray(worker, np.int32).reshape(-1)
+        r = np.ascontiguousarray(run_id, np.int64).reshape(-1)
+        nb = np.ascontiguousarray(np.full(n, -1) if nbytes is None else nbytes, np.int64).reshape(-1)
+        a = np.ascontiguousarray(np.full(n, np.nan) if start is None else start, np.float64).reshape(-1)
+        b = np.ascontiguousarray(np.full(n, np.nan) if stop is None else stop, np.float64).reshape(-1)
+        if not (len(w) == len(r) == len(nb) == len(a) == len(b) == n):
+            raise ValueError("tasks_finished: all message fields need the same length")
+        st = np.zeros(n, np.int8)
+        newp = C.c_int64(0)
+        self._check(self.lib.dgp_tasks_finished(self.h, n, _ptr(t), _ptr(w), _ptr(r), _ptr(nb), _ptr(a), _ptr(b),
+                                                _ptr(st), C.byref(newp)), "dgp_tasks_finished")
+        return st, int(newp.value)
+
+    def snapshot(self):
+        """Append one per-worker snapshot (service mode round boundary)."""
+        self._check(self.lib.dgp_snapshot(self.h), "dgp_snapshot")
 
     # ------------------------------------------------------------------ results
     def num_placements(self) -> int:

@@ -16,8 +16,13 @@
  *   dgp_update_graph      the update_graph stimulus: every runnable task recommended
  *                         "waiting" in priority order and transitioned (:4600-4651, :2045)
  *   dgp_tasks_finished    Scheduler.handle_task_finished (:5783-5797) for a batch of
- *                         completions, in order: stimulus_task_finished -> _transitions
- *                         -> stimulus_queue_slots_maybe_opened (:5025, :4983)
+ *                         task-finished messages, in arrival order: the checks of
+ *                         stimulus_task_finished (:5025-5092), then for each accepted one
+ *                         _transition(key, "memory") -> _transitions ->
+ *                         stimulus_queue_slots_maybe_opened (:4983). Engine state stays
+ *                         resident between calls (service mode)
+ *   dgp_snapshot          one per-worker snapshot (occupancy, nbytes, processing, idle /
+ *                         saturated / idle_task_count, queue length) at a caller-chosen point
  *   dgp_run_rounds        the synthetic executor of the replay protocol: round k completes
  *                         the tasks placed in round k-1 (tests/golden/gen_golden.py)
  *   dgp_get_placements    the compute-task decisions (_add_to_processing :3199 /
@@ -35,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 1
+#define DGP_ABI_VERSION 2
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -96,9 +101,31 @@ int dgp_update_graph(dgp_engine* e);
  * limit) rounds ran. *n_rounds_out receives the number of rounds executed. */
 int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out);
 
-/* One batch of task-finished stimuli, processed in the given order. */
-int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* tasks, const int64_t* nbytes,
-                       const double* start, const double* stop);
+/* Answers to one task-finished message (status[i] of dgp_tasks_finished). */
+#define DGP_TF_ACCEPTED 0        /* processing on that worker with that run_id: completed (:5090) */
+#define DGP_TF_FREE_KEYS 1       /* forgotten / released / queued / no-worker, or a stale run from
+                                    another worker: reply "free-keys" (:5036-5079) */
+#define DGP_TF_ADD_KEYS 2        /* already in memory: Scheduler.add_keys (:5082-5083) */
+#define DGP_TF_RELEASE 3         /* stale run_id from the worker it is processing on: the reference
+                                    recommends "released" (:5080-5081); left to the caller */
+#define DGP_TF_UNKNOWN_WORKER 4  /* worker index not registered (:5786-5787): ignored */
+#define DGP_TF_IMPOSSIBLE 5      /* current run_id from another worker: the reference raises (:2398) */
+#define DGP_TF_UNSUPPORTED 6     /* waiting -> memory (a result for a task that is waiting again) */
+
+/* Service mode: a batch of task-finished messages (Scheduler.handle_task_finished), in
+ * arrival order. Per message: task index, worker index, the run_id of the compute-task
+ * message it answers (the placement-log position of that placement), nbytes (< 0: None)
+ * and the "compute" startstop (start/stop NaN: no compute interval). status[i] receives
+ * DGP_TF_*; the accepted ones run as stimuli in order. The batch crosses PCIe in one copy;
+ * *n_new_placements receives how many placements the batch made (read them with
+ * dgp_get_placements from the previous dgp_num_placements). */
+int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* run_id,
+                       const int64_t* nbytes, const double* start, const double* stop, int8_t* status,
+                       int64_t* n_new_placements);
+
+/* Append one worker snapshot (needs dgp_enable_snapshots): round index = number of calls
+ * (update_graph's snapshot is round 0). */
+int dgp_snapshot(dgp_engine* e);
 
 /* Placement log (run_id order). */
 int64_t dgp_num_placements(dgp_engine* e);

@@ -1,0 +1,184 @@
+"""Golden vectors for the service-mode boundary (``dgp_tasks_finished``): the reference's
+own ``Scheduler.stimulus_task_finished`` (``distributed/scheduler.py:5025-5092``) answers a
+stream of task-finished messages that mixes the genuine completions of the replay protocol
+(``gen_golden.py``) with the stale, duplicate and already-in-memory reports a live
+scheduler receives. Test infrastructure: runs only in the build container
+(python3.9 + ``_refshim``), like ``gen_golden.py``.
+
+Run (from the repo root)::
+
+    PYTHONHASHSEED=0 /opt/conda/bin/python3.9 tests/golden/gen_service.py
+
+Per message the fixture stores what the caller sends (task, worker, run_id = placement-log
+position of the compute-task it answers, nbytes, compute start/stop) and the reference's
+answer, classified as in ``include/dgplace.h`` ``DGP_TF_*``:
+
+* ``ACCEPTED``   ``_transition(key, "memory")`` ran (:5090)
+* ``FREE_KEYS``  the returned worker messages hold ``free-keys`` (:5036-5079)
+* ``ADD_KEYS``   ``Scheduler.add_keys`` was called (:5082-5083)
+* ``RELEASE``    the returned recommendations are ``{key: "released"}`` (:5080-5081); this
+  generator does not apply them, the engine leaves them to its caller as well
+* ``UNKNOWN_WORKER`` the worker is not in ``Scheduler.workers``: ``handle_task_finished``
+  returns before the stimulus (:5786-5787)
+
+Injected messages never change scheduler state (same-worker duplicates are idempotent in
+``WorkerState.add_replica`` :829-830), so the placement log and the per-round snapshots
+equal those of the plain replay; both are stored and checked.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if os.environ.get("PYTHONHASHSEED") != "0":
+    import subprocess
+
+    sys.exit(subprocess.call([sys.executable] + sys.argv, env=dict(os.environ, PYTHONHASHSEED="0")))
+sys.path.insert(0, HERE)
+
+import gen_golden as G  # noqa: E402  (installs the shim, imports the reference)
+
+import dask  # noqa: E402
+import numpy as np  # noqa: E402
+
+ACCEPTED, FREE_KEYS, ADD_KEYS, RELEASE, UNKNOWN_WORKER = 0, 1, 2, 3, 4
+
+
+def replay_service(g, cfg, seed, p_inject=0.35):
+    from distributed.scheduler import Scheduler
+
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    W = len(g["nthreads"])
+    N = g["n_tasks"]
+    addr = {i: a for a, i in widx.items()}
+    rng = np.random.default_rng(seed)
+    called = {"add_keys": 0}
+
+    def add_keys(self, worker, keys=(), stimulus_id=None):  # Scheduler.add_keys, no comms
+        called["add_keys"] += 1
+        ws = self.workers[worker]
+        for key in keys:
+            ts = self.tasks.get(key)
+            if ts is not None and ts.state == "memory":
+                self.add_replica(ts, ws)
+        return "OK"
+
+    type(s).add_keys = add_keys
+    type(s).stimulus_task_finished = Scheduler.stimulus_task_finished
+    run0 = None  # the reference's run_id counter value of placement 0
+
+    recs = {}
+    for ts in sorted(tss, key=lambda t: t.priority, reverse=True):
+        recs[ts.key] = "waiting"
+    s._transitions(recs, {}, {}, "update-graph")
+    run0 = tss[rec["task"][0]].run_id
+    msgs = {k: [] for k in ("task", "worker", "run_id", "nbytes", "start", "stop", "status")}
+    round_ptr = [0]
+    rounds, nplaced = [], []
+    done = 0
+    completed = []  # tasks accepted so far (duplicates are drawn from these)
+
+    def send(t, w, run_id, nbytes, start, stop):
+        """One task-finished message through the reference; returns its class."""
+        msgs["task"].append(t)
+        msgs["worker"].append(w)
+        msgs["run_id"].append(run_id)
+        msgs["nbytes"].append(nbytes)
+        msgs["start"].append(start)
+        msgs["stop"].append(stop)
+        if w >= W:
+            st = UNKNOWN_WORKER
+        else:
+            key = tss[t].key if t < N else ("forgotten", t)
+            ts = s.tasks.get(key)
+            before = ts.state if ts is not None else None
+            sid = f"task-finished-{len(msgs['task'])}"
+            k0 = called["add_keys"]
+            r, cm, wm = s.stimulus_task_finished(
+                key, addr[w], sid, run_id + run0, nbytes=nbytes, type=None, typename="int", metadata=None,
+                startstops=[{"action": "compute", "start": start, "stop": stop}])
+            if called["add_keys"] > k0:
+                st = ADD_KEYS
+            elif any(m.get("op") == "free-keys" for v in wm.values() for m in v):
+                st = FREE_KEYS
+            elif r == {key: "released"} and before == "processing" and ts.state == "processing":
+                st = RELEASE  # not applied (the engine leaves it to the caller)
+            else:
+                assert before == "processing" and ts.state != "processing", (key, before, ts.state, r, wm)
+                st = ACCEPTED
+                s._transitions(r, cm, wm, sid)
+                s.stimulus_queue_slots_maybe_opened(stimulus_id=sid)
+                completed.append(t)
+        msgs["status"].append(st)
+        return st
+
+    while True:
+        cur = len(rec["task"])
+        batch = list(range(done, cur))
+        rounds.append(G.snapshot(s, W, widx) + (len(s.queued),))
+        nplaced.append(cur - done)
+        done = cur
+        if not batch:
+            break
+        for pos in batch:
+            while rng.random() < p_inject:  # crafted messages before the genuine one
+                kind = int(rng.integers(0, 6))
+                proc = [ts for ts in s.tasks.values() if ts.state == "processing"]
+                if kind == 0 and completed:  # duplicate of an accepted completion, same worker
+                    t = completed[int(rng.integers(0, len(completed)))]
+                    ts = tss[t]
+                    w = int(rec["worker"][rec["task"].index(t)])  # the worker that ran it
+                    send(t, w, int(ts.run_id) - run0, 77, 0.0, 0.5)
+                elif kind == 1 and proc:  # stale run of a processing task, from another worker
+                    ts = proc[int(rng.integers(0, len(proc)))]
+                    w = (widx[ts.processing_on.address] + 1 + int(rng.integers(0, W - 1))) % W
+                    send(tidx[ts.key], w, int(ts.run_id) - run0 - 1, 5, 0.0, 0.5)
+                elif kind == 2 and s.queued:  # a queued task
+                    ts = s.queued.peek()
+                    send(tidx[ts.key], int(rng.integers(0, W)), 0, 5, 0.0, 0.5)
+                elif kind == 3:  # a key the scheduler does not know (forgotten)
+                    send(N + int(rng.integers(0, 100)), int(rng.integers(0, W)), 0, 5, 0.0, 0.5)
+                elif kind == 4:  # a worker that is not registered
+                    send(int(rng.integers(0, N)), W + int(rng.integers(0, 5)), 0, 5, 0.0, 0.5)
+                elif kind == 5 and proc:  # stale run_id from the worker it is processing on
+                    ts = proc[int(rng.integers(0, len(proc)))]
+                    send(tidx[ts.key], widx[ts.processing_on.address], int(ts.run_id) - run0 - 1, 5, 0.0, 0.5)
+            t = rec["task"][pos]
+            ts = tss[t]
+            assert ts.state == "processing", (ts.key, ts.state)
+            assert ts.run_id - run0 == pos, (ts.run_id, run0, pos)
+            st = send(t, widx[ts.processing_on.address], pos, int(g["nbytes"][t]), float(g["start"][t]),
+                      float(g["stop"][t]))
+            assert st == ACCEPTED
+        round_ptr.append(len(msgs["task"]))
+    states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
+    return rec, rounds, nplaced, states, msgs, round_ptr
+
+
+def main():
+    cases = {
+        "svc_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 64, seed=15, n_inner_prefixes=3,
+                                                          random_durations=True, nthreads="random"), 1.1, 1),
+        "svc_c2mini_satinf": (lambda: G.graphs.random_dag(2000, 32, seed=16), float("inf"), 2),
+    }
+    for name, (mk, sat, seed) in cases.items():
+        g = mk()
+        G.graphs.check_graph(g)
+        dask.config.set({"distributed.scheduler.worker-saturation": sat})
+        cfg = G.config_dict(sat)
+        rec, rounds, nplaced, states, msgs, round_ptr = replay_service(g, cfg, seed)
+        G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
+        path = os.path.join(HERE, f"{name}.npz")
+        z = dict(np.load(path, allow_pickle=False))
+        z.update(msg_task=np.array(msgs["task"], np.int32), msg_worker=np.array(msgs["worker"], np.int32),
+                 msg_runid=np.array(msgs["run_id"], np.int64), msg_nbytes=np.array(msgs["nbytes"], np.int64),
+                 msg_start=np.array(msgs["start"]), msg_stop=np.array(msgs["stop"]),
+                 msg_status=np.array(msgs["status"], np.int8), msg_round_ptr=np.array(round_ptr, np.int64))
+        np.savez_compressed(path, **z)
+        cnt = np.bincount(np.array(msgs["status"]), minlength=5)
+        print(f"{name}: {len(msgs['task'])} messages, statuses {cnt.tolist()}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,119 @@
+"""Service mode (needs an MI355X): the engine driven the way a live scheduler drives it,
+one task-finished message (or one batch) per ``dgp_tasks_finished`` call, with the device
+state resident between calls.
+
+* every golden fixture is replayed through the service entry one completion at a time and
+  one round per call: the placement log, the per-round snapshots (taken with
+  ``dgp_snapshot`` at the round boundaries) and the final task states equal the
+  reference's, bit for bit;
+* the ``svc_*`` fixtures (``tests/golden/gen_service.py``) carry the reference's own answers
+  (``Scheduler.stimulus_task_finished``, distributed/scheduler.py:5025-5092) to a message
+  stream that mixes stale, duplicate, already-in-memory, forgotten-key and unknown-worker
+  reports into the completions: the engine's status per message must equal them, and the
+  placements must be unaffected.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden_files
+from oracle import oracle
+from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def fixture_messages(g, exp):
+    """The genuine completions of the replay protocol, round by round (run_id order)."""
+    nb, a, b = g["nbytes"], g["start"], g["stop"]
+    msgs, ptr, pos = [], [0], 0
+    for n in exp["round_nplaced"]:
+        for r in range(pos, pos + int(n)):
+            t = int(exp["pl_task"][r])
+            msgs.append((t, int(exp["pl_worker"][r]), r, int(nb[t]), float(a[t]), float(b[t])))
+        pos += int(n)
+        ptr.append(len(msgs))
+    return msgs, ptr
+
+
+def drive(eng, msgs, ptr, per_message):
+    """Feed the message stream; snapshot after each round. Returns the statuses."""
+    status = []
+    for k in range(len(ptr) - 1):
+        chunk = msgs[ptr[k]:ptr[k + 1]]
+        if not chunk:
+            continue
+        groups = [[m] for m in chunk] if per_message else [chunk]
+        for grp in groups:
+            t, w, r, nb, a, b = (np.array(c) for c in zip(*grp))
+            st, _ = eng.tasks_finished(t, w, r, nb, a, b)
+            status.extend(st.tolist())
+        eng.snapshot()
+    return np.array(status, np.int8)
+
+
+def run_service(g, cfg, exp, msgs, ptr, per_message):
+    from distributed_amd.engine import PlacementEngine
+
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        status = drive(eng, msgs, ptr, per_message)
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    return out, status
+
+
+@pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])
+@pytest.mark.parametrize("name", golden_files())
+def test_service_matches_reference_fixture(name, per_message):
+    g, cfg, exp, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
+    msgs, ptr = fixture_messages(g, exp)
+    out, status = run_service(g, cfg, exp, msgs, ptr, per_message)
+    assert (status == 0).all(), np.bincount(status)
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+SVC = sorted(f for f in golden_files() if f.startswith("svc_"))
+
+
+@pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])
+@pytest.mark.parametrize("name", SVC)
+def test_service_stale_duplicate_memory(name, per_message):
+    """The reference's answers to stale / duplicate / in-memory / unknown reports."""
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    msgs = list(zip(z["msg_task"].tolist(), z["msg_worker"].tolist(), z["msg_runid"].tolist(),
+                    z["msg_nbytes"].tolist(), z["msg_start"].tolist(), z["msg_stop"].tolist()))
+    ptr = z["msg_round_ptr"].tolist()
+    out, status = run_service(g, cfg, exp, msgs, ptr, per_message)
+    want = z["msg_status"]
+    bad = np.nonzero(status != want)[0]
+    assert len(bad) == 0, f"{len(bad)} status mismatches, first message {bad[0]}: {status[bad[0]]} vs {want[bad[0]]}"
+    assert set(np.unique(want).tolist()) >= {0, 1, 2, 3, 4}  # every answer class is exercised
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+def test_service_empty_batch_and_mode_guard():
+    """An empty batch is a no-op; a replay cannot continue a service-mode engine."""
+    from distributed_amd import _lib, graphs
+    from distributed_amd.engine import PlacementEngine
+
+    g = graphs.random_dag(2000, 32, seed=3)
+    cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": 1.1}
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg)
+        eng.update_graph()
+        st, newp = eng.tasks_finished([], [], [])
+        assert len(st) == 0 and newp == 0
+        p = eng.placements(0, 1)
+        st, newp = eng.tasks_finished(p["pl_task"], p["pl_worker"], [0], [100], [0.0], [0.01])
+        assert st.tolist() == [0]
+        with pytest.raises(_lib.DgpError):
+            eng.run_rounds(-1)
