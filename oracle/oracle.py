@@ -204,3 +204,22 @@ def load_steal_fixture(path: str):
     exp = {k: z[k] for k in ("level", "st_task", "st_level", "st_cost", "st_victim", "st_occ_victim", "st_thief",
                              "st_occ_thief", "inflight_occ", "inflight_tasks", "idle_after", "sat_after")}
     return p, exp, meta
+
+
+def load_steal_problems(path: str):
+    """Load a multi-problem steal fixture (``tests/golden/steal_reftests.npz``,
+    ``gen_steal_ref.py``) -> list of (name, problem inputs, expected outputs)."""
+    import json
+
+    z = np.load(path, allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    out = []
+    for k, name in enumerate(meta["problems"]):
+        p = {key: z[f"p{k}__{key}"] for key in STEAL_INPUTS + ("holder_ptr", "holder_idx")}
+        for key in ("total_occ", "total_nthreads", "bandwidth"):
+            p[key] = z[f"p{k}__{key}"][()]
+        exp = {key: z[f"p{k}__{key}"] for key in ("level", "st_task", "st_level", "st_cost", "st_victim",
+                                                  "st_occ_victim", "st_thief", "st_occ_thief", "inflight_occ",
+                                                  "inflight_tasks", "idle_after", "sat_after")}
+        out.append((name, p, exp))
+    return out

@@ -21,7 +21,12 @@ def golden_files():
 
 def steal_files():
     """WorkStealing balance fixtures (tests/golden/gen_steal.py)."""
-    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("steal_") and f.endswith(".npz"))
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("steal_") and f.endswith(".npz")
+                  and f != STEAL_REFTESTS)
+
+
+# the reference's own balance unit scenarios, many problems in one file (gen_steal_ref.py)
+STEAL_REFTESTS = "steal_reftests.npz"
 
 
 @pytest.fixture(scope="session")

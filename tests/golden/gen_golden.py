@@ -355,7 +355,17 @@ def fixtures():
                                                    nthreads="random"), inf),
         "c2var_sat2.5": (lambda: graphs.random_dag(4000, 32, seed=7, n_inner_prefixes=2, random_durations=True,
                                                    nthreads="random", root_frac=0.3), 2.5),
+        # more task prefixes than the stream engine's descriptors carry (PD = 8): the
+        # round-kernel engine's path
+        "c2p12_sat1.1": (lambda: graphs.random_dag(3000, 64, seed=8, n_inner_prefixes=12, random_durations=True,
+                                                   nthreads="random"), 1.1),
+        "c2p12_satinf": (lambda: graphs.random_dag(2500, 48, seed=9, n_inner_prefixes=11, random_durations=True,
+                                                   nthreads="random"), inf),
         "c3mini_sat1.1": (lambda: graphs.shuffle_graph(2000, 64, seed=2), 1.1),
+        # decide_worker_non_rootish's no-dependency fast path at >= 20 and < 20 workers
+        "nodep_w24_sat1.1": (lambda: no_dep_groups(24, 30, 12, 200, seed=21), 1.1),
+        "nodep_w20_satinf": (lambda: no_dep_groups(20, 25, 9, 150, seed=22, nthreads="random"), inf),
+        "nodep_w19_sat1.1": (lambda: no_dep_groups(19, 20, 10, 120, seed=23), 1.1),
         "c5mini_sat1.1": (lambda: graphs.map_tree_reduce(50000, 1024, seed=3), 1.1),
         "sat_factor_1.1": (lambda: root_only(10, [2, 1]), 1.1),
         "sat_factor_2.5": (lambda: root_only(10, [2, 1]), 2.5),
@@ -365,6 +375,30 @@ def fixtures():
         "sat_factor_inf": (lambda: root_only(10, [2, 1]), inf),
         "occupancy_comm": (occupancy_comm_graph, 1.1),
     }
+
+
+def no_dep_groups(n_workers, n_groups, group_size, n_agg, seed, nthreads=1):
+    """The no-dependency fast path of ``decide_worker_non_rootish`` (scheduler.py:2283-2305):
+    small groups of dependency-free tasks (``len(tg) <= 2 * total_nthreads``: not root-ish)
+    placed by ``update_graph`` on ``idle or workers``; with >= 20 workers the pick is
+    ``wp_vals[n_tasks % n]``, below 20 the least-occupied worker with a round-robin start.
+    Aggregates over random loads follow."""
+    rng = np.random.default_rng(seed)
+    nl = n_groups * group_size
+    n = nl + n_agg
+    rows = [[] for _ in range(nl)] + [sorted(set(rng.integers(0, nl, 4).tolist())) for _ in range(n_agg)]
+    ptr = np.zeros(n + 1, np.int64)
+    ptr[1:] = np.cumsum([len(r) for r in rows])
+    gnames = [f"load-{k}" for k in range(n_groups)] + ["agg"]
+    gid = [t // group_size for t in range(nl)] + [n_groups] * n_agg
+    g = dict(name="nodep", dep_ptr=ptr, dep_idx=np.array([d for r in rows for d in r], np.int32),
+             prio=rng.permutation(nl).tolist() + list(range(nl, n)), prefix_id=[0] * nl + [1] * n_agg,
+             group_id=gid, prefix_names=["load", "agg"], group_names=gnames,
+             group_prefix=[0] * n_groups + [1], prefix_default_dur=[-1.0, -1.0],
+             nbytes=rng.lognormal(8, 2, n).astype(np.int64), start=np.zeros(n),
+             stop=rng.uniform(0.001, 0.2, n),
+             nthreads=(rng.integers(1, 3, n_workers) if nthreads == "random" else np.full(n_workers, nthreads)))
+    return graphs._finish(g)
 
 
 def root_only(n, nthreads):

@@ -12,7 +12,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, steal_files
+from conftest import GOLDEN, STEAL_REFTESTS, steal_files
 from distributed_amd import graphs
 from distributed_amd.engine import PlacementEngine
 from oracle import oracle
@@ -31,6 +31,16 @@ def eng():
 @pytest.mark.parametrize("name", steal_files())
 def test_balance_matches_reference_fixture(eng, name):
     p, exp, meta = oracle.load_steal_fixture(os.path.join(GOLDEN, name))
+    assert_same(eng.steal_balance(p), exp)
+
+
+REFPROBLEMS = oracle.load_steal_problems(os.path.join(GOLDEN, STEAL_REFTESTS))
+
+
+@pytest.mark.parametrize("k", range(len(REFPROBLEMS)), ids=[p[0] for p in REFPROBLEMS])
+def test_balance_matches_reference_unit_scenarios(eng, k):
+    """test_steal.py:728-777 and :1380-1565 (every permutation, multi-replica who_has)."""
+    name, p, exp = REFPROBLEMS[k]
     assert_same(eng.steal_balance(p), exp)
 
 

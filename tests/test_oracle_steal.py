@@ -15,7 +15,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, steal_files
+from conftest import GOLDEN, STEAL_REFTESTS, steal_files
 from oracle import oracle
 
 STEAL_KEYS = ("level", "st_task", "st_victim", "st_thief", "st_level", "st_cost", "st_occ_victim", "st_occ_thief",
@@ -58,3 +58,15 @@ def test_levels_cover_range():
         p, exp, meta = oracle.load_steal_fixture(os.path.join(GOLDEN, name))
         seen |= set(int(x) for x in exp["level"])
     assert 0 in seen and len(seen - {-1}) >= 10, sorted(seen)
+
+
+REFPROBLEMS = oracle.load_steal_problems(os.path.join(GOLDEN, STEAL_REFTESTS))
+
+
+@pytest.mark.parametrize("k", range(len(REFPROBLEMS)), ids=[p[0] for p in REFPROBLEMS])
+def test_oracle_matches_reference_unit_scenarios(k):
+    """The reference's own balance scenarios (test_steal.py:728-777 test_balance and the
+    dependency-balance family :1380-1565 over every worker permutation, with replicas on
+    several workers): the first balance() of each, bit-exact."""
+    name, p, exp = REFPROBLEMS[k]
+    assert_same(oracle.steal_balance(p), exp)
