@@ -134,7 +134,7 @@ def load_fixture(path: str):
     g["prefix_names"] = meta["prefix_names"]
     g["group_names"] = meta["group_names"]
     g["name"] = meta["name"]
-    exp = {k: z[k] for k in z.files if k.startswith(("pl_", "round_", "final_"))}
+    exp = {k: z[k] for k in z.files if k.startswith(("pl_", "round_", "final_", "stim_"))}
     return g, meta["config"], exp, meta
 
 

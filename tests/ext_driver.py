@@ -1,0 +1,183 @@
+"""Drives the drop-in extension (``distributed_amd/ext.py``) inside the *reference*
+scheduler state (python3.9 + ``tests/golden/_refshim.py``; build container only — the
+reference does not travel to the GPU box). Called by ``tests/test_ext.py``.
+
+For each golden fixture: the reference ``SchedulerState`` of ``gen_golden.build_state``
+(canonical tie-break instrumentation) gets a ``GPUPlacementExtension`` whose engine is a
+stand-in serving the fixture's own placement log, stimulus by stimulus
+(``stim_nplaced``): the engine outputs are fixture data, made by the reference itself.
+Then the replay protocol runs through the scheduler's real entry points:
+
+* ``update_graph``: the extension's ``SchedulerPlugin.update_graph`` hook, then the
+  scheduler's transitions (``scheduler.py:4641-4653``);
+* every completion through ``stream_handlers["task-finished"]`` -> the extension ->
+  ``Scheduler.handle_task_finished`` (``:5783-5797``).
+
+Checks: the graph the extension uploads equals the fixture graph (the TaskState -> CSR
+conversion), every placement the scheduler made came from the engine in the engine's
+order, ``validate=True`` re-derives each one with the reference's ``decide_worker*`` and
+finds it equal, and the placement records equal the fixture's. ``--diverge`` swaps two
+decisions of one stimulus: the extension must detect it, hand placement back to the
+scheduler's own decide_worker, and the records must still equal the fixture's.
+Prints one JSON line per fixture.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+if os.environ.get("PYTHONHASHSEED") != "0":
+    import subprocess
+
+    sys.exit(subprocess.call([sys.executable] + sys.argv, env=dict(os.environ, PYTHONHASHSEED="0")))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+sys.path.insert(0, REPO)
+
+import gen_golden as G  # noqa: E402  (shim + reference)
+
+import dask  # noqa: E402
+import numpy as np  # noqa: E402
+
+from distributed.scheduler import Scheduler  # noqa: E402
+from distributed_amd.ext import GPUPlacementExtension  # noqa: E402
+from oracle.oracle import load_fixture  # noqa: E402
+
+
+class FixtureEngine:
+    """The engine interface ext.py uses, serving a reference fixture's placement log."""
+
+    def __init__(self, exp, fixture_keys):
+        self.exp = exp
+        self.fkeys = fixture_keys
+        self.stim = exp["stim_nplaced"].tolist()
+        self.n = 0
+        self.k = 0
+        self.ext = None
+        self.graph = None
+        self.diverge = None  # placement index whose decision is swapped with the next one
+
+    def load(self, g, config, results=True):
+        self.graph, self.config = g, config
+
+    def update_graph(self):
+        self.n, self.k = self.stim[0], 1
+
+    def tasks_finished(self, task, worker, run_id, nbytes=None, start=None, stop=None):
+        for _ in task:  # genuine completions only in this protocol
+            self.n += self.stim[self.k]
+            self.k += 1
+        return np.zeros(len(task), np.int8), 0
+
+    def num_placements(self):
+        return self.n
+
+    def placements(self, offset=0, count=None):
+        sl = slice(offset, offset + count)
+        idx = self.ext.task_index
+        task = np.array([idx[self.fkeys[t]] for t in self.exp["pl_task"][sl]], np.int32)
+        if self.diverge is not None and offset <= self.diverge < offset + count - 1:
+            j = self.diverge - offset  # two decisions of one stimulus swapped
+            task[j], task[j + 1] = task[j + 1], task[j]
+        return {"pl_task": task, "pl_worker": self.exp["pl_worker"][sl]}
+
+    def close(self):
+        pass
+
+
+def check_upload(g_up, keys_up, g_fx, fkeys):
+    """The extension's TaskState -> CSR conversion against the fixture graph (graphs.py)."""
+    pos = {k: i for i, k in enumerate(fkeys)}
+    perm = np.array([pos[k] for k in keys_up])  # upload index -> fixture index
+    assert len(perm) == g_fx["n_tasks"]
+    for i, f in enumerate(perm):
+        up = sorted(fkeys[perm[d]] for d in g_up["dep_idx"][g_up["dep_ptr"][i]:g_up["dep_ptr"][i + 1]])
+        fx = sorted(fkeys[d] for d in g_fx["dep_idx"][g_fx["dep_ptr"][f]:g_fx["dep_ptr"][f + 1]])
+        assert up == fx, (keys_up[i], up, fx)
+    pn_up = np.array(g_up["prefix_names"])[g_up["prefix_id"]]
+    pn_fx = np.array(g_fx["prefix_names"])[g_fx["prefix_id"][perm]]
+    assert (pn_up == pn_fx).all()
+    gn_up = np.array(g_up["group_names"])[g_up["group_id"]]
+    gn_fx = np.array(g_fx["group_names"])[g_fx["group_id"][perm]]
+    assert (gn_up == gn_fx).all()
+    assert np.array_equal(g_up["wanted"], g_fx["wanted"][perm])
+    assert np.array_equal(g_up["rootish_override"], g_fx["rootish_override"][perm])
+    assert np.array_equal(g_up["nthreads"], g_fx["nthreads"])
+    # priority rank: ascending fixture priority
+    assert np.array_equal(np.argsort(g_fx["prio"][perm], kind="stable"), np.arange(len(perm)))
+    # the engine's prefix table = TaskPrefix.duration_average at upload
+    pd_fx = dict(zip(g_fx["prefix_names"], g_fx["prefix_default_dur"]))
+    assert all(pd_fx[n] == d for n, d in zip(g_up["prefix_names"], g_up["prefix_default_dur"]))
+
+
+def run(name, diverge=False):
+    g, cfg, exp, meta = load_fixture(os.path.join(HERE, "golden", name))
+    g["keys"] = None
+    sat = cfg["saturation"]
+    sat = float("inf") if sat == "inf" else float(sat)
+    dask.config.set({"distributed.scheduler.worker-saturation": sat})
+    cfg = dict(cfg, saturation=sat)
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    S = type(s)
+    S.stimulus_task_finished = Scheduler.stimulus_task_finished
+    S.handle_task_finished = Scheduler.handle_task_finished
+    S.validate_key = lambda self, key, ts=None: None
+    S.send_all = lambda self, client_msgs, worker_msgs: None
+    fkeys = [ts.key for ts in tss]
+    eng = FixtureEngine(exp, fkeys)
+    if diverge:  # first stimulus after update_graph with two or more placements
+        stim = exp["stim_nplaced"]
+        pos = np.cumsum(stim) - stim
+        k = next(i for i in range(1, len(stim)) if stim[i] >= 2 and exp["pl_task"][pos[i]] != exp["pl_task"][pos[i] + 1])
+        eng.diverge = int(pos[k])
+    ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
+    eng.ext = ext
+    s.stream_handlers = {}
+    ext._install()  # with the stream handler table in place
+    # Scheduler._create_taskstate_from_graph's tail (:4600-4653): plugin hook, then transitions
+    priority = {ts.key: ts.priority for ts in tss}
+    recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
+    ext.update_graph(s, client="client-0", keys=set(priority), tasks=list(priority), annotations={},
+                     priority=priority, dependencies={})
+    assert ext.active, ext.reason
+    check_upload(eng.graph, ext.keys, g, fkeys)
+    s._transitions(recs, {}, {}, "update-graph")
+    done = 0
+    n_msgs = 0
+    while True:
+        cur = len(rec["task"])
+        batch = rec["task"][done:cur]
+        done = cur
+        if not batch:
+            break
+        for t in batch:
+            ts = tss[t]
+            s.stream_handlers["task-finished"](
+                key=ts.key, worker=ts.processing_on.address, stimulus_id=f"tf-{t}", run_id=ts.run_id,
+                nbytes=int(g["nbytes"][t]), type=None, typename="int", metadata=None,
+                startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
+            n_msgs += 1
+    ext._end_of_stimulus("end of replay")
+    assert ext.active != diverge, ext.reason  # a divergence hands placement back to the scheduler
+    n = len(exp["pl_task"])
+    assert rec["task"] == exp["pl_task"].tolist()
+    assert rec["worker"] == exp["pl_worker"].tolist()
+    assert rec["comm"] == exp["pl_comm"].tolist()
+    assert np.array_equal(np.array(rec["start"]).view(np.int64), exp["pl_start"].view(np.int64))
+    assert rec["wsnbytes"] == exp["pl_wsnbytes"].tolist()
+    if not diverge:
+        assert ext.stats["device_decisions"] == n, (ext.stats, n)
+    return dict(fixture=name, placements=n, messages=n_msgs, device_decisions=ext.stats["device_decisions"],
+                device_queued=ext.stats["device_queued"], active=ext.active, reason=ext.reason)
+
+
+if __name__ == "__main__":
+    import warnings
+
+    warnings.filterwarnings("ignore")
+    args = sys.argv[1:]
+    diverge = "--diverge" in args
+    for nm in [a for a in args if not a.startswith("--")]:
+        print(json.dumps(run(nm, diverge)), flush=True)

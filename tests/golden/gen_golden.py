@@ -235,6 +235,7 @@ def replay(g, cfg):
     s._transitions(recs, {}, {}, "update-graph")
     rounds = []
     nplaced = []
+    stim = [len(rec["task"])]  # placements per stimulus: update_graph, then each completion
     done = 0
     while True:
         cur = len(rec["task"])
@@ -254,10 +255,13 @@ def replay(g, cfg):
                 t, "memory", sid, worker=ts.processing_on.address, nbytes=int(g["nbytes"][i]),
                 type=None, typename="int",
                 startstops=[{"action": "compute", "start": float(g["start"][i]), "stop": float(g["stop"][i])}])
+            n0 = len(rec["task"])
             s._transitions(r, cm, wm, sid)
             s.stimulus_queue_slots_maybe_opened(stimulus_id=sid)
+            stim.append(len(rec["task"]) - n0)
     secs = time.perf_counter() - t0
     states = np.array([STATE_CODES[ts.state] for ts in tss], np.uint8)
+    rec["stim"] = stim
     return s, rec, rounds, nplaced, states, secs
 
 
@@ -287,6 +291,8 @@ def save(name, g, cfg, rec, rounds, nplaced, states, secs):
         round_sat=np.stack([r[4] for r in rounds]), round_itc=np.stack([r[5] for r in rounds]),
         round_nqueued=np.array([r[6] for r in rounds], np.int32), final_state=states,
     )
+    if "stim" in rec:  # placements made by each stimulus (update_graph, then every completion)
+        out["stim_nplaced"] = np.array(rec["stim"], np.int32)
     sat = cfg["saturation"]
     meta = dict(name=name, prefix_names=list(g["prefix_names"]), group_names=list(g["group_names"]),
                 config=dict(cfg, saturation=("inf" if math.isinf(sat) else sat)),

@@ -1,0 +1,72 @@
+"""The drop-in Scheduler extension (distributed_amd/ext.py) inside the reference scheduler.
+
+Runs ``tests/ext_driver.py`` under the image's python3.9 with the reference imported from
+/root/reference (``tests/golden/_refshim.py``). Neither exists on the GPU box, so there
+these tests skip; the engine side of the same message streams is covered on the GPU by
+``tests/test_gpu_service.py`` (one dgp_tasks_finished call per message).
+"""
+import json
+import os
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+PY39 = "/opt/conda/bin/python3.9"
+DRIVER = os.path.join(REPO, "tests", "ext_driver.py")
+HAVE_REF = os.path.exists(PY39) and os.path.isdir("/root/reference/distributed")
+
+pytestmark = pytest.mark.skipif(not HAVE_REF, reason="needs the reference + python3.9 (build container only)")
+
+FIXTURES = ["c1_sat1.1.npz", "c1_satinf.npz", "c2var_sat1.1.npz", "c2var_sat2.5.npz", "c2var_satinf.npz",
+            "c2p12_sat1.1.npz", "c3mini_sat1.1.npz", "nodep_w19_sat1.1.npz", "nodep_w20_satinf.npz",
+            "nodep_w24_sat1.1.npz", "occupancy_comm.npz", "sat_factor_0.1.npz", "sat_factor_2.5.npz",
+            "sat_factor_inf.npz"]
+
+
+def drive(names, *flags):
+    env = dict(os.environ, PYTHONHASHSEED="0")
+    env.pop("PYTHONPATH", None)
+    out = subprocess.run([PY39, DRIVER, *flags, *names], capture_output=True, text=True, env=env, timeout=600,
+                         cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
+
+
+def test_extension_places_every_task_from_the_engine():
+    """Upload conversion, decision order, validate=True agreement and exact records."""
+    res = drive(FIXTURES)
+    assert [r["fixture"] for r in res] == FIXTURES
+    for r in res:
+        assert r["active"] and r["device_decisions"] == r["placements"], r
+
+
+def test_extension_hands_back_on_divergence():
+    """A decision out of order: the extension detects it at once and the scheduler's own
+    decide_worker carries on; the records are still the reference's."""
+    res = drive(["c2var_sat1.1.npz", "c1_sat1.1.npz", "c3mini_sat1.1.npz"], "--diverge")
+    for r in res:
+        assert not r["active"] and "placement order differs" in r["reason"], r
+        assert 0 < r["device_decisions"] < r["placements"], r
+
+
+def test_graph_from_tasks_layout():
+    """graph_from_tasks on plain stand-ins (no dask needed): priority order, CSR, ids."""
+    from types import SimpleNamespace as NS
+
+    from distributed_amd.ext import graph_from_tasks
+
+    P = {n: NS(name=n, duration_average=d) for n, d in (("a", -1.0), ("b", 0.5))}
+    G = {n: NS(name=n) for n in ("a-1", "b-1")}
+    t0 = NS(key="x", priority=(0, 1, 5), dependencies=[], prefix=P["a"], group=G["a-1"], who_wants=None, _rootish=None)
+    t1 = NS(key="y", priority=(0, 1, 2), dependencies=[], prefix=P["a"], group=G["a-1"], who_wants=None, _rootish=True)
+    t2 = NS(key="z", priority=(0, 1, 9), dependencies=[t0, t1], prefix=P["b"], group=G["b-1"], who_wants={1},
+            _rootish=None)
+    g, keys = graph_from_tasks([t2, t0, t1], [1, 2])
+    assert keys == ["y", "x", "z"]
+    assert g["dep_ptr"].tolist() == [0, 0, 0, 2] and g["dep_idx"].tolist() == [0, 1]
+    assert g["prefix_names"] == ["a", "b"] and g["prefix_id"].tolist() == [0, 0, 1]
+    assert g["prefix_default_dur"].tolist() == [-1.0, 0.5]
+    assert g["group_prefix"].tolist() == [0, 1]
+    assert g["wanted"].tolist() == [0, 0, 1] and g["rootish_override"].tolist() == [1, -1, -1]
