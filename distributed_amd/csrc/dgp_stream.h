@@ -361,6 +361,26 @@ __device__ __forceinline__ double occ_dict(const WDict& d, int64_t netocc, DTab 
   return res + (double)netocc / (double)D.bandwidth;
 }
 
+// The executors' form of occ_dict: the network term netocc / bandwidth is carried per
+// lane (recomputed only when netocc changes). The same fp64 operations in the same order:
+// bit-identical to occ_dict.
+__device__ __forceinline__ double occ_dict_r(const WDict& d, double net_bw, DTab dt, const Dev& D) {
+  const uint32_t n = wd_n(d.ord);
+  double res = 0.0;
+#pragma unroll
+  for (int i = 0; i < PD; i++) {
+    if (!ballot((uint32_t)i < n)) break;
+    const int p = wd_id(d.ord, i);
+    const double dv = dt[p];
+    const double term = (dv < 0 ? D.unknown_duration : dv) * (double)wd_cnt(d, p);
+    if ((uint32_t)i < n) res += term;
+  }
+  return res + net_bw;
+}
+__device__ __forceinline__ double net_bw_of(int64_t netocc, const Dev& D) {
+  return (double)netocc / (double)D.bandwidth;
+}
+
 template <bool LW>
 __device__ __forceinline__ WDict dict_load(const WPtr<LW>& P, int c) {
   using U4 = typename WPtr<LW>::template P<const Q4>;
@@ -725,6 +745,33 @@ __device__ __attribute__((always_inline)) bool round_end_step(const Dev& D, SLds
   return false;
 }
 
+// The TaskState bookkeeping of a retired local completion (one lane per slot): the
+// completed task (set_nbytes, processing_on, state; a dependent-less unwanted task is
+// released at once) and the dependencies it released (:3309-3314, :2444-2505). Only
+// exact / global stimuli and the host read these fields, and those run after every earlier
+// slot has retired.
+__device__ __forceinline__ void seq_bookkeeping(const Dev& D, SLds& L, int s) {
+  const uint4 e0 = L.desc[s][0], e1 = L.desc[s][1];
+  const int t = (int)e0.x, w = (int)e0.y;
+  const uint32_t flags = e0.w;
+  const int64_t nbt = mk64(e1.x, e1.y);
+  const int kt = e1.z & 0xff, nrel = (e1.z >> 8) & 0xff, grp_t = (int)e1.w;
+  D.cur_nbytes[t] = nbt;
+  D.proc_on[t] = -1;
+  D.state[t] = (flags & F_SELFREL) ? S_RELEASED : S_MEMORY;
+  if (flags & F_SELFREL) {
+    atomicAdd((unsigned long long*)&D.g_relwait[grp_t], 1ull);
+    D.holders[(size_t)t * D.WB + (w >> 6)] = 0;
+  }
+  for (int i = 0; i < nrel; i++) {
+    const uint4 er = L.desc[s][E_HDR + kt + i];
+    const int d = (int)er.y, hd = (int)er.x;
+    D.state[d] = S_RELEASED;
+    D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
+    atomicAdd((unsigned long long*)&D.g_relwait[D.group[d]], 1ull);
+  }
+}
+
 template <bool LW>
 __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, const WPtr<LW>& P, long long& round_start) {
   SCtl& S = L.c;
@@ -821,6 +868,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
         D.holder_of[task] = w;
       }
       for (int j = 0; j < nrec; j++) D.rlog[rb + j] = D.srec[st0 + j];
+      seq_bookkeeping(D, L, s);
     }
     __threadfence_block();
     if (lane == 0) {
@@ -1428,36 +1476,36 @@ __device__ __attribute__((always_inline)) void needs_reset(const Dev& D, int c, 
   if (lane < NLW) nl = 0;
 }
 
-// per-stimulus outputs in lanes: record k in lane k, placement q in lane q
+// per-stimulus outputs, staged as they are made: the values are wave-uniform, lane 0
+// stores each record / placement into the slot's staging rows at once (nothing is held in
+// registers until the slot retires)
 struct Out {
   int nrec, npl;
-  int r_kind, r_w, r_p, r_np, r_task;
-  int64_t r_dnet;
-  double r_occ, r_dur;
-  int q_task, q_w, q_route;
-  int64_t q_comm, q_wsnb;
-  double q_start;
-  __device__ void rec(int kind, int w, int p, int64_t dnet, double occ, int np, int task, double dur) {
-    if (lane_id() == nrec) {
-      r_kind = kind;
-      r_w = w;
-      r_p = p;
-      r_dnet = dnet;
-      r_occ = occ;
-      r_np = np;
-      r_task = task;
-      r_dur = dur;
+  size_t st0;  // the slot's staging base (slot * PLC)
+  __device__ void rec(const Dev& D, int kind, int w, int p, int64_t dnet, double occ, int np, int task, double dur) {
+    if (lane_id() == 0 && nrec < PLC) {
+      SRec rc;
+      rc.w = w;
+      rc.p = (int16_t)p;
+      rc.kind = (int8_t)kind;
+      rc.pad = 0;
+      rc.nproc = np;
+      rc.task = task;
+      rc.dnet = dnet;
+      rc.occ = occ;
+      rc.dur = dur;
+      D.srec[st0 + nrec] = rc;
     }
     nrec++;
   }
-  __device__ void place(int task, int w, int64_t comm, double start, int64_t wsnb, int route) {
-    if (lane_id() == npl) {
-      q_task = task;
-      q_w = w;
-      q_comm = comm;
-      q_start = start;
-      q_wsnb = wsnb;
-      q_route = route;
+  __device__ void place(const Dev& D, int task, int w, int64_t comm, double start, int64_t wsnb, int route) {
+    if (lane_id() == 0 && npl < PLC) {
+      D.s2_task[st0 + npl] = task;
+      D.s2_worker[st0 + npl] = w;
+      D.s2_comm[st0 + npl] = comm;
+      D.s2_start[st0 + npl] = start;
+      D.s2_wsnb[st0 + npl] = wsnb;
+      D.s2_route[st0 + npl] = (int8_t)route;
     }
     npl++;
   }
@@ -1511,33 +1559,10 @@ __device__ __attribute__((always_inline)) void release_slot(const Dev& D, SLds& 
   }
 }
 
-// stage outputs, publish counts, retire: after this SEQ may consume the slot
+// publish counts, retire: after this SEQ may consume the slot (its staging rows were
+// written as the outputs were made)
 __device__ __attribute__((always_inline)) void finish_slot(const Dev& D, SLds& L, int s, long long r, const Out& o, int npops, bool direct) {
   const int lane = lane_id();
-  if (!direct) {
-    const size_t st0 = (size_t)s * PLC;
-    if (lane < o.npl) {
-      D.s2_task[st0 + lane] = o.q_task;
-      D.s2_worker[st0 + lane] = o.q_w;
-      D.s2_comm[st0 + lane] = o.q_comm;
-      D.s2_start[st0 + lane] = o.q_start;
-      D.s2_wsnb[st0 + lane] = o.q_wsnb;
-      D.s2_route[st0 + lane] = (int8_t)o.q_route;
-    }
-    if (lane < o.nrec) {
-      SRec rc;
-      rc.w = o.r_w;
-      rc.p = (int16_t)o.r_p;
-      rc.kind = (int8_t)o.r_kind;
-      rc.pad = 0;
-      rc.nproc = o.r_np;
-      rc.task = o.r_task;
-      rc.dnet = o.r_dnet;
-      rc.occ = o.r_occ;
-      rc.dur = o.r_dur;
-      D.srec[st0 + lane] = rc;
-    }
-  }
   if (lane == 0) {
     L.npl[s] = o.npl;
     L.nrec[s] = direct ? 0 : o.nrec;
@@ -1574,6 +1599,15 @@ __device__ __forceinline__ Key key_at(const Key& k, int l) {
   o.w = rl(k.w, l);
   o.comm = mk64(rlu(lo32(k.comm), l), rlu(hi32(k.comm), l));
   return o;
+}
+
+// start time as a u64 whose unsigned order is key_less's fp64 order (+0 and -0 equal)
+__device__ __forceinline__ uint64_t start_key(double x) {
+  const uint64_t b = x == 0.0 ? 0ull : (uint64_t)__double_as_longlong(x);
+  return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+  return ((uint64_t)rlu((unsigned)(v >> 32), l) << 32) | rlu((unsigned)v, l);
 }
 
 // a stimulus whose effects stay on the workers it registered. Returns false (nothing
@@ -1617,6 +1651,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   Out o;
   o.nrec = 0;
   o.npl = 0;
+  o.st0 = (size_t)s * PLC;
   phase(11);
   // ---- the touched workers' state, one lane each, in registers for the whole stimulus
   const int nt = L.ntouch[s];
@@ -1644,6 +1679,8 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   }
   const int jw = __builtin_ctzll(wm);
   const bool isw = lane == jw;
+  double nbw = net_bw_of(net, D);            // this lane's netocc / bandwidth
+  const bool nth1 = !ballot(tl && nth != 1);  // occ / 1.0 == occ: the division is skipped
   phase(16);
   // ------------------------------------------- completion: processing -> memory (:2366)
   int64_t dnet = 0;
@@ -1665,12 +1702,13 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     np = npw;
     net += dnet;
   }
+  if (dnet != 0) nbw = net_bw_of(net, D);  // dnet is uniform
   phase(17);
   // every lane's occupancy and stack time, kept current: only w (now) and each chosen
   // worker (after its commit) change during the stimulus
-  double occj = occ_dict(dj, net, durv, D);
-  double stkj = occj / (double)nth;
-  o.rec(K_COMPLETE, w, p, dnet, mkd(rlu(dlo(occj), jw), rlu(dhi(occj), jw)), npw, t, dobs);
+  double occj = occ_dict_r(dj, nbw, durv, D);
+  double stkj = nth1 ? occj : occj / (double)nth;
+  o.rec(D, K_COMPLETE, w, p, dnet, mkd(rlu(dlo(occj), jw), rlu(dhi(occj), jw)), npw, t, dobs);
   // add_replica (:3148), then the releases popped before the frontier (LIFO, :3309-3314)
   if (isw) nbj += (flags & F_SELFREL) ? 0 : nbt;
   for (int i = 0; i < nrel; i++) {
@@ -1680,6 +1718,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   }
   phase(12);
   // ------------------------------ frontier in ascending priority: decide_worker (:8550)
+  bool released = false;  // this lane's worker was written back and released early
   int off = FX0;
   for (int j = 0; j < nf; j++) {
     const int x = rl((int)E.x, off), px = rl((int)E.y, off), kx = rl((int)E.z, off) & 0xff;
@@ -1729,9 +1768,31 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       }
     }
     const int cb = best.w;
+    if (j == nf - 1 && nt > 2) {
+      // the last frontier decision is made: every touched worker but w and the chosen one
+      // is final now (the non-chosen candidates were only read, the release holders were
+      // settled before the frontier). Write them back and release them before the commit,
+      // so stimuli waiting only on them do not wait for it.
+      const bool early = tl && !isw && lane != jb;
+      if (ballot(early)) {
+        if (early) {
+          using U4 = typename WPtr<LW>::template P<Q4>;
+          P.nproc[cj] = np;
+          st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
+          st4(ascast<U4>(P.pcnt + (size_t)cj * PD + 4), dj.c1);
+          P.plen[cj] = dj.ord;
+          P.netocc[cj] = net;
+          P.nbytes[cj] = nbj;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (early) release_worker<LW>(L, P, s, cj);
+        released = early;
+      }
+    }
     phase(19);
     // _add_to_processing (:3199): record, WorkerState.add_to_processing, check_idle_saturated
-    o.place(x, cb, best.comm, best.start, best.nb, ROUTE_NONROOTISH);
+    o.place(D, x, cb, best.comm, best.start, best.nb, ROUTE_NONROOTISH);
     uint32_t nlc = line_load<LW>(P, cb);
     if (exact) {  // scan mode reads processing_on of this stimulus' earlier placements
       __threadfence_block();
@@ -1752,21 +1813,22 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       np += 1;
       net += dn;
     }
+    if (dn != 0) nbw = isb ? net_bw_of(net, D) : nbw;  // dn is uniform
     if (ballot(!okp)) serr(S, SERR_PREFIX, x);
     if (lane == 0) {
       D.proc_on[x] = cb;
       D.state[x] = S_PROCESSING;
       atomicAdd((unsigned long long*)&D.g_relwait[gx], (unsigned long long)-1ll);
     }
-    occj = occ_dict(dj, net, durv, D);
-    stkj = occj / (double)nth;
-    o.rec(K_PLACE, cb, px, dn, mkd(rlu(dlo(occj), jb), rlu(dhi(occj), jb)), rl(np, jb), x, 0.0);
+    occj = occ_dict_r(dj, nbw, durv, D);
+    stkj = nth1 ? occj : occj / (double)nth;
+    o.rec(D, K_PLACE, cb, px, dn, mkd(rlu(dlo(occj), jb), rlu(dhi(occj), jb)), rl(np, jb), x, 0.0);
     off += 1 + kx;
     phase(20);
   }
   // ---- every touched worker but w is final: write back and release it now (its waiting
   // successors may run while w takes the queue refill)
-  if (tl && !isw) {
+  if (tl && !isw && !released) {
     using U4 = typename WPtr<LW>::template P<Q4>;
     P.nproc[cj] = np;
     st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
@@ -1778,7 +1840,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   if (nt > 1) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (tl && !isw) release_worker<LW>(L, P, s, cj);
+    if (tl && !isw && !released) release_worker<LW>(L, P, s, cj);
   }
   // -------------- stimulus_queue_slots_maybe_opened (:4983): only w can have open slots
   int pops = 0;
@@ -1795,7 +1857,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     const int qp = S.q_prefix;
     for (int i = 0; i < pops; i++) {
       const double st = stkj + 0.0 / (double)D.bandwidth;
-      o.place(-1, w, 0, mkd(rlu(dlo(st), jw), rlu(dhi(st), jw)), mk64(rlu(lo32(nbj), jw), rlu(hi32(nbj), jw)),
+      o.place(D, -1, w, 0, mkd(rlu(dlo(st), jw), rlu(dhi(st), jw)), mk64(rlu(lo32(nbj), jw), rlu(hi32(nbj), jw)),
               ROUTE_ROOTISH_Q);
       bool okq = true;
       if (isw) {
@@ -1803,9 +1865,9 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
         np += 1;
       }
       if (ballot(!okq)) serr(S, SERR_PREFIX, -1);
-      occj = occ_dict(dj, net, durv, D);
-      stkj = occj / (double)nth;
-      o.rec(K_PLACE, w, qp, 0, mkd(rlu(dlo(occj), jw), rlu(dhi(occj), jw)), rl(np, jw), -1, 0.0);
+      occj = occ_dict_r(dj, nbw, durv, D);
+      stkj = nth1 ? occj : occj / (double)nth;
+      o.rec(D, K_PLACE, w, qp, 0, mkd(rlu(dlo(occj), jw), rlu(dhi(occj), jw)), rl(np, jw), -1, 0.0);
     }
   }
   // ---- w written back last, then released
@@ -1824,22 +1886,8 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   phase(13);
   // ------------------------------------------------ retire: LDS state, then successors
   phase(21);
-  // replica bookkeeping in HBM (TaskState fields; the walker / globals read them later)
-  if (lane == 0) {
-    D.cur_nbytes[t] = nbt;
-    D.proc_on[t] = -1;
-    D.state[t] = (flags & F_SELFREL) ? S_RELEASED : S_MEMORY;
-    if (flags & F_SELFREL) {
-      atomicAdd((unsigned long long*)&D.g_relwait[grp_t], 1ull);
-      D.holders[(size_t)t * D.WB + (w >> 6)] = 0;
-    }
-  }
-  if (lane >= RL0 && lane < RL0 + nrel) {
-    const int d = (int)E.y, hd = (int)E.x;
-    D.state[d] = S_RELEASED;
-    D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
-    atomicAdd((unsigned long long*)&D.g_relwait[D.group[d]], 1ull);
-  }
+  // the completed task's and the releases' TaskState fields in HBM are written by the
+  // sequencer when it retires the slot (seq_bookkeeping): nothing reads them before
   phase(14);
   finish_slot(D, L, s, r, o, pops, false);
   phase(15);
@@ -1866,6 +1914,85 @@ __device__ __forceinline__ Key argmin_workers(const Dev& D, F&& key_of) {
     if (key_less(q, best)) best = q;
   }
   return best;
+}
+
+// A chunk of up to 64 frontier tasks (lane j: dependent j, `fr` set when stimulus r
+// releases it) that all have ONE dependency, held by the same worker c, are not root-ish
+// and share a prefix px already counted on c and in SchedulerState's global prefix dict
+// (the P2P-shuffle unpack tasks of a barrier, shuffle/_shuffle.py:276-306): decide_worker
+// returns c for each (:8579), comm is 0 and c needs no replica, so placement k differs from
+// placement 0 only by the k earlier ones in c's count of px. Lane k evaluates placement k
+// (start time from count + k, record from count + k + 1) with the serial path's exact
+// expressions; the records fold in one walker batch. Returns false (nothing done) when the
+// chunk does not qualify.
+template <bool LW>
+__device__ __attribute__((always_inline)) bool bulk_single_holder(const Dev& D, SCtl& S, const WPtr<LW>& P, WState& g,
+                                                                  DTab durv, long long r, bool fr, int xl, int tfl,
+                                                                  int h1l, long long lpos, int& npl) {
+  const int lane = lane_id();
+  const unsigned long long fm = ballot(fr);
+  if (__builtin_popcountll(fm) < 2) return false;
+  const int first = __builtin_ctzll(fm);
+  const int c = rl(h1l, first);
+  const int pxl = fr ? D.prefix[xl] : -1;
+  const int px = rl(pxl, first);
+  if (c < 0 || c >= D.W) return false;
+  if (ballot(fr && (h1l != c || pxl != px || (tfl & TF_ROOTISH) || xl == D.dbg_task))) return false;
+  const WDict d0 = dict_load<LW>(P, c);
+  const uint32_t cnt0 = wd_cnt(d0, px);
+  bool in_g = false;
+#pragma unroll
+  for (int i = 0; i < PD; i++) in_g = in_g || (i < g.n && g.pf[i] == px);
+  if (cnt0 == 0 || !in_g) return false;
+  const int m = __builtin_popcountll(fm);
+  const int rank = __builtin_popcountll(fm & ((1ull << lane) - 1));
+  const int np0 = P.nproc[c];
+  const int64_t no0 = P.netocc[c], nb0 = P.nbytes[c];
+  const double nth = (double)P.nthreads[c];
+  // lane L: c's occupancy with L (before) and L + 1 (after) of these placements made
+  WDict db = d0, da = d0;
+  wd_set(db, px, cnt0 + (uint32_t)lane);
+  wd_set(da, px, cnt0 + (uint32_t)lane + 1u);
+  const double occ_b = occ_dict(db, no0, durv, D);
+  const double occ_a = occ_dict(da, no0, durv, D);
+  const double start_l = occ_b / nth + (double)(int64_t)0 / (double)D.bandwidth;  // place_x, comm = 0
+  const double start = __shfl(start_l, rank);  // frontier lane -> its placement's start time
+  if (fr) {
+    const long long pos = lpos + npl + rank;
+    D.pl_task[pos] = xl;
+    D.pl_worker[pos] = c;
+    D.pl_comm[pos] = 0;
+    D.pl_start[pos] = start;
+    D.pl_wsnbytes[pos] = nb0;
+    D.pl_route[pos] = (int8_t)ROUTE_NONROOTISH;
+    D.run_id[xl] = (int32_t)pos;
+    D.holder_of[xl] = c;
+    D.proc_on[xl] = c;
+    D.state[xl] = S_PROCESSING;
+    atomicAdd((unsigned long long*)&D.g_relwait[D.group[xl]], (unsigned long long)-1ll);
+  }
+  if (lane == 0) {
+    using U4 = typename WPtr<LW>::template P<Q4>;
+    WDict dn = d0;
+    wd_set(dn, px, cnt0 + (uint32_t)m);
+    st4(ascast<U4>(P.pcnt + (size_t)c * PD), dn.c);
+    st4(ascast<U4>(P.pcnt + (size_t)c * PD + 4), dn.c1);
+    P.nproc[c] = np0 + m;
+  }
+  __threadfence_block();
+  // the m K_PLACE records in placement order (lane i = record i)
+  SRec rc{};
+  rc.w = c;
+  rc.p = (int16_t)px;
+  rc.kind = (int8_t)K_PLACE;
+  rc.nproc = np0 + lane + 1;
+  rc.task = -1;
+  rc.dnet = 0;
+  rc.occ = occ_a;
+  rc.dur = 0.0;
+  ws_fold_batch<LW>(D, P, S, g, rc, m);
+  npl += m;
+  return true;
 }
 
 // a stimulus that reads SchedulerState-global state: every earlier stimulus has retired,
@@ -2032,6 +2159,8 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
      if (e - a == 1) h1l = D.holder_of[D.dep_idx[a]];
    }
    const int nk = (int)min((int64_t)64, f1 - k0);
+   if (bulk_single_holder<LW>(D, S, P, g, durv, r, k0 + lane < f1 && fml == (int)r, xl, tfl, h1l, lpos, npl))
+     continue;  // the whole chunk went to one worker, placed lane-parallel
    for (int j = 0; j < nk; j++) {
     const int x = rl(xl, j);
     if (rl(fml, j) != (int)r) continue;
@@ -2268,6 +2397,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   Out o;
   o.nrec = 0;
   o.npl = npl;
+  o.st0 = (size_t)s * PLC;
   finish_slot(D, L, s, r, o, 0, true);
   if (lane == 0) vstore(&S.global_pending, 0);
 }
@@ -2278,7 +2408,10 @@ __device__ __attribute__((noinline)) void exe_global_entry(int s, long long r) {
   exe_global<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r);
 }
 
-template <bool LW>
+// G: this executor also runs the global stimuli. Only one executor wave does: a call to the
+// global path from the others' loop would make the compiler keep its clobbers out of their
+// registers (measured: +18% on the C2 replay from spills in the claim loop).
+template <bool LW, bool G>
 __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
   const int lane = lane_id();
@@ -2309,6 +2442,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       const int s = (rot + b) & (WIN - 1);
       const long long r = vload(&L.sid[s]);
       const uint32_t fl = vload(&L.flags[s]);
+      if (!G && (fl & F_GLOBAL)) continue;  // left to the global-capable executor
       bool exact = (fl & (F_GLOBAL | F_EXACT)) != 0;
       int qm = 0;  // 0 no refill, 1 every open slot is refilled, 2/3 the queue length decides
       const long long ql = vload(&S.qlen);
@@ -2342,7 +2476,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     lds_fence();
     if (lane == 0) atomicAdd(&S.busy_exe, 1);
     const unsigned long long t0 = mclk();
-    if (cf & F_GLOBAL) {
+    if (G && (cf & F_GLOBAL)) {
       exe_global_entry<LW>(cs, cr);
       if (lane == 0) S.prof[9]++;
     } else if (!exe_local<LW>(D, L, P, cs, cr, cq, cex)) {
@@ -2415,7 +2549,9 @@ __device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WP
 // (inlined into one kernel body they shared one 128-VGPR budget and spilled to scratch
 // on the executors' path).
 template <bool LW>
-__device__ __attribute__((noinline)) void entry_exe() { role_exe<LW>(c_dev, st_L, wptr<LW>(c_dev)); }
+__device__ __attribute__((noinline)) void entry_exe() { role_exe<LW, false>(c_dev, st_L, wptr<LW>(c_dev)); }
+template <bool LW>
+__device__ __attribute__((noinline)) void entry_exe_g() { role_exe<LW, true>(c_dev, st_L, wptr<LW>(c_dev)); }
 template <bool LW>
 __device__ __attribute__((noinline)) void entry_reg() { role_reg<LW>(c_dev, st_L, wptr<LW>(c_dev)); }
 template <bool LW>
@@ -2533,7 +2669,8 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
   } else if (wave == 4) {
     entry_wlk<LW>();
   } else if (!((D.dbg >> 8) & 15) || wave - N_ROLE < ((D.dbg >> 8) & 15)) {  // dbg bits 8..11: executor count
-    entry_exe<LW>();
+    if (wave == N_ROLE) entry_exe_g<LW>();  // the executor that also runs global stimuli
+    else entry_exe<LW>();
   }
   __threadfence_block();
   __syncthreads();
