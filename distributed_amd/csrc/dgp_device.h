@@ -252,6 +252,9 @@ struct Dev {
   int32_t* sv_worker;
   int32_t* sv_cseq;      // [N]
   int64_t sv_cap;
+  // DGP_TRACE builds: per-stimulus lifecycle timestamps for stimuli [trace_lo, trace_lo + trace_n)
+  unsigned long long* trace;
+  long long trace_lo, trace_n;
 };
 
 // dynamic LDS of the commit kernel: owner[W] reservation table, then (lds_workers) the

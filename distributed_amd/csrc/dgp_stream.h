@@ -53,10 +53,20 @@ __constant__ Dev c_dev;
 #define DGP_RB 4  // registrar batch (stimuli registered per poll; 4 measured best of 2/4/8)
 #endif
 #ifndef DGP_SCTA
-#define DGP_SCTA 768
+#define DGP_SCTA 1024
 #endif
-constexpr int SCTA = DGP_SCTA;   // 768: 12 waves = 5 roles + 7 executors (168 VGPRs per wave)
-constexpr int WIN = 32;          // in-flight stimulus slots (LDS window)
+constexpr int SCTA = DGP_SCTA;   // 1024: 16 waves = 5 roles + 11 executors (128 VGPRs per wave; 768/7 executors: C2 1.18 s, 1024: 1.14 s)
+#ifndef DGP_WIN
+#define DGP_WIN 32
+#endif
+constexpr int WIN = DGP_WIN;     // in-flight stimulus slots (LDS window; masks are u32: <= 32)
+#ifndef DGP_RS
+#define DGP_RS 128
+#endif
+// retire ring: stimuli registered but not yet sequenced. A slot is held only while its
+// stimulus is registered and running; a finished stimulus leaves its counts here (and its
+// outputs in the staging rows of r & (RS - 1)) until the sequencer retires it in order.
+constexpr int RS = DGP_RS;
 constexpr int NE = 64;           // 16-byte descriptor entries per stimulus (one per lane)
 #ifndef DGP_DR
 // 512 rows x (64 x 16 B descriptor + 32 x 4 B touch list) = 576 KB stays in L2: PMC read
@@ -78,6 +88,7 @@ constexpr int N_ROLE = 5;        // waves 0..4 are SEQ, BLD, PRE, REG, WLK; the 
 constexpr int E_HDR = 7;         // header entries: 0 ids, 1 sizes/counts, 2 duration, 3..6 durations
 // rows are selected with r & (DR - 1); PRE runs at most DR ahead and at least one window
 static_assert((DR & (DR - 1)) == 0 && DR >= 64 && DR >= WIN, "DGP_DR must be a power of two >= 64");
+static_assert((RS & (RS - 1)) == 0 && RS >= WIN && RS <= DR, "DGP_RS must be a power of two in [WIN, DR]");
 
 enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16 };
 enum : int { K_COMPLETE = 1, K_PLACE = 2 };
@@ -117,6 +128,7 @@ struct SCtl {
   int global_pending;  // a registered global stimulus has not finished
   int busy_exe;        // executors between claim and retirement
   unsigned ready;      // slots whose stimulus may run
+  unsigned freem;      // slots not holding a registered stimulus (REG allocates, executors free)
   long long seq_pos, log_len, rec_len, walk_pos, bld_pos, pre_pos, reg_pos, reg_limit;
   long long qhead, qlen, n_tasks;
   long long stim_end;  // service mode: stimuli [seq_pos, stim_end) run in this launch
@@ -159,7 +171,27 @@ __device__ __forceinline__ int wmax(int v) {
   return v;
 }
 __device__ __forceinline__ unsigned long long ballot(bool b) { return __ballot(b); }
-__device__ __forceinline__ unsigned long long mclk() { return __builtin_amdgcn_s_memtime(); }
+// Profiling clock and counters (dgp_stats wave_phase* / stall*): only in DGP_PROF builds.
+// s_memtime is a scalar memory read that waits on the LDS counter (lgkmcnt), so every probe
+// would drain the wave's outstanding LDS operations on the hot paths.
+#ifndef DGP_PROF
+#define DGP_PROF 0
+#endif
+__device__ __forceinline__ unsigned long long mclk() { return DGP_PROF ? __builtin_amdgcn_s_memtime() : 0ull; }
+// DGP_TRACE builds: lifecycle timestamps of sampled stimuli (tools/trace_analyze.py):
+// 0 registered, 1 ready, 2 claimed, 3 early release, 4 non-w release, 5 done, 6 retired,
+// 7 predecessor count | touched workers << 16 | executor wave << 24
+#ifndef DGP_TRACE
+#define DGP_TRACE 0
+#endif
+__device__ __forceinline__ void trace_at(const Dev& D, long long r, int k, unsigned long long v) {
+  if (DGP_TRACE && D.trace && r >= D.trace_lo && r < D.trace_lo + D.trace_n) D.trace[(r - D.trace_lo) * 8 + k] = v;
+}
+#define TR(r, k) trace_at(D, (r), (k), __builtin_amdgcn_s_memtime())
+#define PROF(stmt) \
+  do {             \
+    if (DGP_PROF) { stmt; } \
+  } while (0)
 __device__ __forceinline__ void wbar() { __builtin_amdgcn_wave_barrier(); }
 __device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
@@ -262,6 +294,12 @@ __device__ __forceinline__ void st4(PQ q, const uint4& u) {
   q->w = u.w;
 }
 
+// what the sequencer needs of a finished stimulus
+struct RMeta {
+  int32_t npl;                 // placements staged (a global stimulus: written to the log directly)
+  uint8_t nrec, npops, direct, pad;
+};
+
 // LDS of the stream kernel besides the worker carve
 struct SLds {
   uint4 desc[WIN][NE];        // descriptors of the in-flight window
@@ -269,9 +307,9 @@ struct SLds {
   int32_t ntouch[WIN];
   uint32_t flags[WIN];
   int32_t pred[WIN];
-  int32_t npl[WIN], npops[WIN], nrec[WIN];
-  long long done_tag[WIN];
   long long sid[WIN];         // stimulus registered in each slot
+  RMeta rmeta[RS];            // retire ring: counts of finished stimulus r at r & (RS - 1)
+  long long rdone[RS];        // ... and r + 1 once they are final
   uint16_t pre_scr[64][TMAX]; // prefetcher scratch: each lane's distinct-worker list
   SCtl c;
 };
@@ -662,7 +700,7 @@ __device__ __attribute__((always_inline)) void role_wlk(const Dev& D, SLds& L, c
     ws_store(S, g);
     lds_fence();
     if (lane == 0) {
-      S.prof[4] += mclk() - t0;
+      PROF(S.prof[4] += mclk() - t0);
       vstore(&S.walk_pos, wp + m);
     }
   }
@@ -750,8 +788,11 @@ __device__ __attribute__((always_inline)) bool round_end_step(const Dev& D, SLds
 // released at once) and the dependencies it released (:3309-3314, :2444-2505). Only
 // exact / global stimuli and the host read these fields, and those run after every earlier
 // slot has retired.
-__device__ __forceinline__ void seq_bookkeeping(const Dev& D, SLds& L, int s) {
-  const uint4 e0 = L.desc[s][0], e1 = L.desc[s][1];
+__device__ __forceinline__ void seq_bookkeeping(const Dev& D, long long r) {
+  // the stimulus' descriptor row in the ring: PRE rewrites it only DR stimuli later, after
+  // this one retired (its lead is bounded by seq_pos + DR)
+  const uint4* row = D.desc + (size_t)(r & (DR - 1)) * NE;
+  const uint4 e0 = row[0], e1 = row[1];
   const int t = (int)e0.x, w = (int)e0.y;
   const uint32_t flags = e0.w;
   const int64_t nbt = mk64(e1.x, e1.y);
@@ -764,7 +805,7 @@ __device__ __forceinline__ void seq_bookkeeping(const Dev& D, SLds& L, int s) {
     D.holders[(size_t)t * D.WB + (w >> 6)] = 0;
   }
   for (int i = 0; i < nrel; i++) {
-    const uint4 er = L.desc[s][E_HDR + kt + i];
+    const uint4 er = row[E_HDR + kt + i];
     const int d = (int)er.y, hd = (int)er.x;
     D.state[d] = S_RELEASED;
     D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
@@ -782,9 +823,9 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
     const long long sp = S.seq_pos;
     const long long re = S.round_end;
     const long long r = sp + lane;
-    const bool dn = lane < WIN && r < re && vload(&L.done_tag[r & (WIN - 1)]) == r + 1;
+    const bool dn = r < re && vload(&L.rdone[r & (RS - 1)]) == r + 1;
     const unsigned long long b = ballot(dn);
-    const int m = (int)__builtin_ctzll(~b);
+    const int m = b == ~0ull ? 64 : (int)__builtin_ctzll(~b);  // ctz(0) is undefined
     if (m == 0) {
       if (sp == re) {
         if (round_end_step<LW>(D, L, P, round_start)) break;
@@ -796,7 +837,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
         serr(S, SERR_WATCHDOG, (int)sp);
         break;
       }
-      if (lane == 0) S.prof[30] += nw - t_sq;  // 30: sequencer waiting for the oldest slot
+      PROF(if (lane == 0) S.prof[30] += nw - t_sq);  // 30: sequencer waiting for the oldest slot
       t_sq = nw;
       __builtin_amdgcn_s_sleep(1);
       continue;
@@ -806,7 +847,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
       const long long rp = vload(&S.reg_pos);
       const int be = vload(&S.busy_exe), gp = vload(&S.global_pending);
       int bad = 0;
-      if (rp < sp || rp > sp + WIN) bad = 1;
+      if (rp < sp || rp > sp + RS) bad = 1;
       if (be < 0 || be > 16) bad = 2;
       if (gp < 0 || gp > 1) bad = 3;
       if (S.qlen < 0 || S.qhead < 0) bad = 4;
@@ -816,14 +857,15 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
       }
     }
     const unsigned long long t0 = mclk();
-    const int s = (int)(r & (WIN - 1));
+    const int q = (int)(r & (RS - 1));  // retire-ring entry and staging rows of stimulus r
     int npl = 0, nrec = 0, npop = 0;
     bool direct = false;
     if (lane < m) {
-      npl = L.npl[s];
-      nrec = L.nrec[s];
-      npop = L.npops[s];
-      direct = (L.flags[s] & F_GLOBAL) != 0;
+      const RMeta me = L.rmeta[q];
+      npl = me.npl;
+      nrec = me.nrec;
+      npop = me.npops;
+      direct = me.direct != 0;
     }
     if (ballot(lane < m && (npl < 0 || nrec < 0 || npop < 0 || npop > npl || (!direct && (npl > PLC || nrec > PLC))))) {
       serr(S, SERR_INV, 500000000 + (int)sp);
@@ -847,7 +889,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
       break;
     }
     if (lane < m && !direct) {
-      const size_t st0 = (size_t)s * PLC;
+      const size_t st0 = (size_t)q * PLC;
       int popk = 0;
       for (int j = 0; j < npl; j++) {
         int task = D.s2_task[st0 + j];
@@ -868,7 +910,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
         D.holder_of[task] = w;
       }
       for (int j = 0; j < nrec; j++) D.rlog[rb + j] = D.srec[st0 + j];
-      seq_bookkeeping(D, L, s);
+      seq_bookkeeping(D, r);
     }
     __threadfence_block();
     if (lane == 0) {
@@ -877,12 +919,16 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
       S.qhead += tpo;
       S.qlen -= tpo;
       S.n_tasks += tpl;
-      S.prof[0] += mclk() - t0;
-      S.prof[8] += 1;
+      PROF(S.prof[0] += mclk() - t0);
+      PROF(S.prof[8] += 1);
     }
     lds_fence();
     if (lane == 0) {
       vstore(&S.seq_pos, sp + m);
+      if (DGP_TRACE) {
+        const unsigned long long tn = __builtin_amdgcn_s_memtime();
+        if (DGP_TRACE == 1) for (int i = 0; i < m; i++) trace_at(D, sp + i, 6, tn);
+      }
 
     }
     t_idle = rclk();
@@ -951,7 +997,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   if (f1 == f0 && !(tf & TF_WANTED)) flags |= F_SELFREL;
   if (kt > KT_MAX) {
     flags |= F_GLOBAL;
-    atomicAdd(&L.c.prof[20], 1ull);  // diagnostics: why stimuli run global
+    PROF(atomicAdd(&L.c.prof[20], 1ull));  // diagnostics: why stimuli run global
   }
   int n = E_HDR, nrel = 0, nf = 0, sumkx = 0;
   touch(w);
@@ -983,7 +1029,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
     const int64_t x0 = D.dep_ptr[x], x1 = D.dep_ptr[x + 1];
     const int kx = (int)(x1 - x0);
     if ((D.tflags[x] & TF_ROOTISH) || kx > KX_MAX || n + 1 + kx > NE) {
-      if (!(flags & F_GLOBAL)) atomicAdd(&L.c.prof[(D.tflags[x] & TF_ROOTISH) ? 16 : 21], 1ull);
+      if (!(flags & F_GLOBAL)) PROF(atomicAdd(&L.c.prof[(D.tflags[x] & TF_ROOTISH) ? 16 : 21], 1ull));
       flags |= F_GLOBAL;
       continue;
     }
@@ -998,7 +1044,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
     }
   }
   if (!(flags & F_GLOBAL) && (nf > 255 || nt > TMAX || nf + (D.sat_inf ? 0 : D.w_cap[w]) + 1 > PLC))
-    atomicAdd(&L.c.prof[22], 1ull);
+    PROF(atomicAdd(&L.c.prof[22], 1ull));
   if (nf > 255 || nt > TMAX) flags |= F_GLOBAL;
   if (nf + (D.sat_inf ? 0 : D.w_cap[w]) + 1 > PLC) flags |= F_GLOBAL;  // staging room for the refill
   if (tbad) flags |= F_GLOBAL | F_BADTOUCH;
@@ -1043,8 +1089,8 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
     __threadfence_block();
     wbar();
     if (lane == 0) {
-      S.prof[KIND == 0 ? 1 : 2] += mclk() - t0;
-      S.prof[KIND == 0 ? 6 : 7] += 1;
+      PROF(S.prof[KIND == 0 ? 1 : 2] += mclk() - t0);
+      PROF(S.prof[KIND == 0 ? 6 : 7] += 1);
       vstore(KIND == 0 ? &S.bld_pos : &S.pre_pos, e);
     }
   }
@@ -1086,13 +1132,14 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     if (vload(&S.stop)) break;
     const long long r0 = S.reg_pos;
     if (r0 >= pre) pre = vload(&S.pre_pos);
-    const long long wl = vload(&S.seq_pos) + WIN;
-    const long long lim = min(min(pre, vload(&S.reg_limit)), wl);
+    const long long wl = vload(&S.seq_pos) + RS;  // retire-ring capacity
+    const unsigned fm = vload(&S.freem);           // free slots (only this wave takes them)
+    const long long lim = min(min(pre, vload(&S.reg_limit)), min(wl, r0 + (long long)__builtin_popcount(fm)));
     const int gp = vload(&S.global_pending);
     if (r0 >= lim || gp) {
       // stall attribution (cycles): 24 window full, 25 descriptor not prefetched, 26 global pending
       const unsigned long long n = mclk();
-      if (lane == 0) S.prof[gp ? 26 : (r0 >= wl ? 24 : (r0 >= pre ? 25 : 27))] += n - t_poll;
+      PROF(if (lane == 0) S.prof[gp ? 26 : (r0 >= wl || !fm ? 24 : (r0 >= pre ? 25 : 27))] += n - t_poll);
       t_poll = n;
       __builtin_amdgcn_s_sleep(1);
       continue;
@@ -1116,8 +1163,18 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     }
 #if DGP_REG_PROBES
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the batch rows are in
-    if (lane == 0) S.prof[16] += mclk() - t0;
+    PROF(if (lane == 0) S.prof[16] += mclk() - t0);
 #endif
+    // the batch's slots: the lowest free ones (nb <= popcount(fm) by lim)
+    int sb[RB];
+    {
+      unsigned f = fm;
+#pragma unroll
+      for (int b = 0; b < RB; b++) {
+        sb[b] = f ? __builtin_ctz(f) : 0;
+        if (b < nb) f &= f - 1;
+      }
+    }
     // ---------------------------------------------------------------- phase A
     // header scalars of the whole batch first (independent of one another)
     int pb[RB], ntb[RB];
@@ -1128,7 +1185,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     const uint32_t fadd = (qglob ? F_GLOBAL : 0u) | ((D.dbg & 1) ? F_EXACT : 0u) | ((D.dbg & 2) ? F_GLOBAL : 0u);
 #pragma unroll
     for (int b = 0; b < RB; b++) {
-      if (lane == 0 && b < nb && qglob && !(rlu(EB[b].w, 0) & F_GLOBAL)) S.prof[23] += 1;  // diagnostics
+      PROF(if (lane == 0 && b < nb && qglob && !(rlu(EB[b].w, 0) & F_GLOBAL)) S.prof[23] += 1);  // diagnostics
       pb[b] = rl((int)EB[b].z, 0);
       dob[b] = mkd(rlu(EB[b].x, 2), rlu(EB[b].y, 2));
       ntb[b] = rl((int)EB[b].z, 2);
@@ -1154,7 +1211,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     for (int b = 0; b < RB; b++) {
       if (b >= nbat) break;
       const long long r = r0 + b;
-      const int s = (int)(r & (WIN - 1));
+      const int s = sb[b];
       uint4 E = EB[b];
       const int p = pb[b];
       if (lane == 3 + (p >> 1) && dob[b] == dob[b]) {  // TaskPrefix.add_duration, in stimulus order (NaN: none)
@@ -1183,7 +1240,14 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     const unsigned long long tA = mclk();
     // ---------------------------------------------------------------- phase B
     lds_fence();  // the slots' LDS state is written before any mask bit can expose it
-    if (lane == 0) vstore(&S.reg_pos, r0 + nbat);
+    if (lane == 0) {
+      unsigned taken = 0;
+#pragma unroll
+      for (int b = 0; b < RB; b++)
+        if (b < nbat) taken |= 1u << sb[b];
+      atomicAnd(&S.freem, ~taken);
+      vstore(&S.reg_pos, r0 + nbat);
+    }
     // every mask registration back to back (one wave's LDS atomics run in order)
     int touchall_cnt = 0;
     unsigned oldb[RB];
@@ -1191,7 +1255,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     for (int b = 0; b < RB; b++) {  // every lane issues: an inactive lane ORs 0 into its own word
       oldb[b] = 0;
       if (b >= nloc) break;
-      const unsigned bit = 1u << (int)((r0 + b) & (WIN - 1));
+      const unsigned bit = 1u << sb[b];
       const bool on = lane < ntb[b];
       oldb[b] = __hip_atomic_fetch_or(&P.mask[on ? TB[b] : lane], on ? bit : 0u, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1199,10 +1263,10 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
 #if DGP_REG_PROBES
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the mask atomics returned
     const unsigned long long tM = mclk();
-    if (lane == 0) S.prof[20] += tM - tA;
+    PROF(if (lane == 0) S.prof[20] += tM - tA);
 #endif
     if (glob_end) {
-      const unsigned bit = 1u << (int)((r0 + nbat - 1) & (WIN - 1));
+      const unsigned bit = 1u << sb[nbat - 1];
       for (int c = lane; c < D.W; c += 64)
         touchall_cnt += __builtin_popcount(__hip_atomic_fetch_or(&P.mask[c], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
     }
@@ -1211,7 +1275,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     int totb[RB];
 #pragma unroll
     for (int b = 0; b < RB; b++) {
-      const unsigned bit = 1u << (int)((r0 + b) & (WIN - 1));
+      const unsigned bit = 1u << sb[b];
       const int c = (b < nloc && lane < ntb[b]) ? __builtin_popcount(oldb[b] & ~bit) : 0;
       int t = 0;
 #pragma unroll
@@ -1219,7 +1283,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
       totb[b] = t;
     }
 #if DGP_REG_PROBES
-    if (lane == 0) S.prof[21] += mclk() - tM;
+    PROF(if (lane == 0) S.prof[21] += mclk() - tM);
 #endif
     const int tall = glob_end ? wsum(touchall_cnt) : 0;
     if (lane == 0) {
@@ -1228,13 +1292,21 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
 #pragma unroll
       for (int b = 0; b < RB; b++) {
         if (b == nbat - 1 && glob_end) totb[b] = tall;
-        oldp[b] = b < nbat ? atomicAdd(&L.pred[(int)((r0 + b) & (WIN - 1))], totb[b] - BIG) : 1;
+        oldp[b] = b < nbat ? atomicAdd(&L.pred[sb[b]], totb[b] - BIG) : 1;
       }
       unsigned rdy = 0;
 #pragma unroll
       for (int b = 0; b < RB; b++)
-        if (b < nbat && oldp[b] + totb[b] - BIG == 0) rdy |= 1u << (int)((r0 + b) & (WIN - 1));
+        if (b < nbat && oldp[b] + totb[b] - BIG == 0) rdy |= 1u << sb[b];
       if (rdy) atomicOr(&S.ready, rdy);
+      if (DGP_TRACE) {
+        for (int b = 0; b < RB; b++) {
+          if (b >= nbat) break;
+          if (DGP_TRACE == 1) TR(r0 + b, 0);
+          if (DGP_TRACE == 1 && ((rdy >> sb[b]) & 1u)) TR(r0 + b, 1);
+          trace_at(D, r0 + b, 7, (unsigned long long)(totb[b] | (ntb[b] << 16)));
+        }
+      }
     }
     const unsigned long long tB = mclk();
     {  // prefetch the next batch's rows while the executors run
@@ -1255,13 +1327,13 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     }
     if (lane == 0) {
       t_poll = mclk();
-      S.prof[3] += t_poll - t0;
-      S.prof[31] += nbat;
-      S.prof[27] += 1;            // batches
+      PROF(S.prof[3] += t_poll - t0);
+      PROF(S.prof[31] += nbat);
+      PROF(S.prof[27] += 1);            // batches
 #if !DGP_PHASE_PROBES  // (probe builds use 16..23 for the executor phases)
-      S.prof[17] += tA - t0;      // fetch wait + phase A
-      S.prof[18] += tB - tA;      // phase B
-      S.prof[19] += t_poll - tB;  // prefetch issue
+      PROF(S.prof[17] += tA - t0);      // fetch wait + phase A
+      PROF(S.prof[18] += tB - tA);      // phase B
+      PROF(S.prof[19] += t_poll - tB);  // prefetch issue
 #endif
     }
     lds_fence();
@@ -1533,7 +1605,10 @@ __device__ __forceinline__ void release_worker(SLds& L, const WPtr<LW>& P, int s
   while (succ) {
     const int b = __builtin_ctz(succ);
     succ &= succ - 1;
-    if (atomicSub(&L.pred[b], 1) == 1) atomicOr(&L.c.ready, 1u << b);
+    if (atomicSub(&L.pred[b], 1) == 1) {
+      atomicOr(&L.c.ready, 1u << b);
+      if (DGP_TRACE == 1) { const Dev& D = c_dev; TR(L.sid[b], 1); }
+    }
   }
 }
 
@@ -1548,7 +1623,10 @@ __device__ __attribute__((always_inline)) void release_slot(const Dev& D, SLds& 
     while (succ) {
       const int b = __builtin_ctz(succ);
       succ &= succ - 1;
-      if (atomicSub(&L.pred[b], 1) == 1) atomicOr(&S.ready, 1u << b);
+      if (atomicSub(&L.pred[b], 1) == 1) {
+        atomicOr(&S.ready, 1u << b);
+        if (DGP_TRACE == 1) TR(L.sid[b], 1);
+      }
     }
   };
   if (all) {
@@ -1559,25 +1637,26 @@ __device__ __attribute__((always_inline)) void release_slot(const Dev& D, SLds& 
   }
 }
 
-// publish counts, retire: after this SEQ may consume the slot (its staging rows were
-// written as the outputs were made)
+// publish the counts in the retire ring, mark the stimulus done and free its slot: the
+// sequencer retires it in order later (its staging rows were written as the outputs were made)
 __device__ __attribute__((always_inline)) void finish_slot(const Dev& D, SLds& L, int s, long long r, const Out& o, int npops, bool direct) {
   const int lane = lane_id();
+  const int q = (int)(r & (RS - 1));
   if (lane == 0) {
-    L.npl[s] = o.npl;
-    L.nrec[s] = direct ? 0 : o.nrec;
-    L.npops[s] = npops;
+    RMeta me;
+    me.npl = o.npl;
+    me.nrec = (uint8_t)(direct ? 0 : o.nrec);
+    me.npops = (uint8_t)npops;
+    me.direct = direct ? 1 : 0;
+    me.pad = 0;
+    L.rmeta[q] = me;
   }
-#if DGP_PHASE_PROBES
-  {
-    const unsigned long long t_a = mclk();
-    __threadfence_block();
-    if (lane == 0) atomicAdd(&L.c.prof[22], mclk() - t_a);
-  }
-#else
   __threadfence_block();
-#endif
-  if (lane == 0) vstore(&L.done_tag[s], r + 1);
+  if (lane == 0) {
+    vstore(&L.rdone[q], r + 1);
+    atomicOr(&L.c.freem, 1u << s);  // the slot may take the next registration
+  }
+  if (DGP_TRACE && lane == 0) TR(r, 5);
 }
 
 // objective key of lane's candidate: worker_objective (:3131-3146) + canonical index
@@ -1630,7 +1709,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   unsigned long long tph = mclk();
   auto phase = [&](int k) {
     const unsigned long long n = mclk();
-    if (lane == 0) atomicAdd(&S.prof[k], n - tph);
+    PROF(if (lane == 0) atomicAdd(&S.prof[k], n - tph));
     tph = n;
   };
 #else
@@ -1651,8 +1730,9 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   Out o;
   o.nrec = 0;
   o.npl = 0;
-  o.st0 = (size_t)s * PLC;
+  o.st0 = (size_t)(r & (RS - 1)) * PLC;
   phase(11);
+  if (DGP_TRACE == 2 && lane == 0) TR(r, 0);
   // ---- the touched workers' state, one lane each, in registers for the whole stimulus
   const int nt = L.ntouch[s];
   const bool tl = lane < nt;
@@ -1682,6 +1762,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   double nbw = net_bw_of(net, D);            // this lane's netocc / bandwidth
   const bool nth1 = !ballot(tl && nth != 1);  // occ / 1.0 == occ: the division is skipped
   phase(16);
+  if (DGP_TRACE == 2 && lane == 0) TR(r, 1);
   // ------------------------------------------- completion: processing -> memory (:2366)
   int64_t dnet = 0;
   int64_t freed = 0;
@@ -1704,6 +1785,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   }
   if (dnet != 0) nbw = net_bw_of(net, D);  // dnet is uniform
   phase(17);
+  if (DGP_TRACE == 2 && lane == 0) TR(r, 3);
   // every lane's occupancy and stack time, kept current: only w (now) and each chosen
   // worker (after its commit) change during the stimulus
   double occj = occ_dict_r(dj, nbw, durv, D);
@@ -1717,6 +1799,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     if (tl && cj == h) nbj -= nb;
   }
   phase(12);
+  if (DGP_TRACE == 2 && lane == 0) TR(r, 4);
   // ------------------------------ frontier in ascending priority: decide_worker (:8550)
   bool released = false;  // this lane's worker was written back and released early
   int off = FX0;
@@ -1788,6 +1871,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (early) release_worker<LW>(L, P, s, cj);
         released = early;
+        if (DGP_TRACE == 1 && lane == 0) TR(r, 3);
       }
     }
     phase(19);
@@ -1826,6 +1910,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     off += 1 + kx;
     phase(20);
   }
+  if (DGP_TRACE == 2 && lane == 0) TR(r, 6);
   // ---- every touched worker but w is final: write back and release it now (its waiting
   // successors may run while w takes the queue refill)
   if (tl && !isw && !released) {
@@ -1842,6 +1927,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     if (tl && !isw && !released) release_worker<LW>(L, P, s, cj);
   }
+  if (DGP_TRACE == 1 && lane == 0) TR(r, 4);
   // -------------- stimulus_queue_slots_maybe_opened (:4983): only w can have open slots
   int pops = 0;
   if (qmode != 0 && !D.sat_inf) {
@@ -2397,7 +2483,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   Out o;
   o.nrec = 0;
   o.npl = npl;
-  o.st0 = (size_t)s * PLC;
+  o.st0 = (size_t)(r & (RS - 1)) * PLC;
   finish_slot(D, L, s, r, o, 0, true);
   if (lane == 0) vstore(&S.global_pending, 0);
 }
@@ -2410,7 +2496,8 @@ __device__ __attribute__((noinline)) void exe_global_entry(int s, long long r) {
 
 // G: this executor also runs the global stimuli. Only one executor wave does: a call to the
 // global path from the others' loop would make the compiler keep its clobbers out of their
-// registers (measured: +18% on the C2 replay from spills in the claim loop).
+// registers (measured: +18% on the C2 replay from spills in the claim loop). A global-only
+// G wave (no second copy of exe_local) was measured slower: C2 1.18 -> 1.27 s.
 template <bool LW, bool G>
 __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
@@ -2429,36 +2516,50 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       __builtin_amdgcn_s_sleep(DGP_EXE_SLEEP);
       continue;
     }
+    // the ready slots in stimulus order (oldest first): lane i holds slot i's key
     const long long sp = vload(&S.seq_pos);
-    const int rot = (int)(sp & (WIN - 1));
-    unsigned mr = rot ? ((m >> rot) | (m << (WIN - rot))) : m;
+    const bool rdl = lane < WIN && ((m >> lane) & 1u);
+    const long long rsl = rdl ? vload(&L.sid[lane]) : 0;
+    const uint32_t fsl = rdl ? vload(&L.flags[lane]) : 0u;
+    unsigned key = rdl ? (unsigned)(((rsl - sp) << 5) | lane) : ~0u;  // r - sp < RS
     int cs = -1, cq = 0;
     long long cr = -1;
     uint32_t cf = 0;
     bool cex = false;
-    while (mr) {
-      const int b = __builtin_ctz(mr);
-      mr &= mr - 1;
-      const int s = (rot + b) & (WIN - 1);
-      const long long r = vload(&L.sid[s]);
-      const uint32_t fl = vload(&L.flags[s]);
-      if (!G && (fl & F_GLOBAL)) continue;  // left to the global-capable executor
-      bool exact = (fl & (F_GLOBAL | F_EXACT)) != 0;
-      int qm = 0;  // 0 no refill, 1 every open slot is refilled, 2/3 the queue length decides
-      const long long ql = vload(&S.qlen);
-      if (!(fl & F_GLOBAL) && ql > 0) {
-        qm = (ql - (r - sp) * (long long)S.capmax >= (long long)S.capmax) ? 1 : 2;
-        if (qm == 2) exact = true;
-      }
-      if (exact) {
-        if (vload(&S.seq_pos) != r) continue;
-        if ((fl & F_GLOBAL) && vload(&S.walk_pos) != vload(&S.rec_len)) continue;
-        if (qm != 0) qm = 3;
-      }
+    while (true) {
+      unsigned kmin = key;
+      for (int o = 32; o > 0; o >>= 1) kmin = min(kmin, (unsigned)__shfl_xor((int)kmin, o));
+      if (kmin == ~0u) break;
+      const int s = (int)(kmin & 31u);
+      if (lane == s) key = ~0u;  // tried
+      if (!G && (rlu(fsl, s) & F_GLOBAL)) continue;  // left to the global-capable executor
+      // claim first, then read the slot: between the scan and the claim its stimulus may
+      // have run and retired and the slot been registered again (another stimulus)
       unsigned old = 0;
       if (lane == 0) old = atomicAnd(&S.ready, ~(1u << s));
       old = rlu(old, 0);
       if (!((old >> s) & 1u)) continue;
+      lds_fence();
+      const long long r = vload(&L.sid[s]);
+      const uint32_t fl = vload(&L.flags[s]);
+      bool exact = (fl & (F_GLOBAL | F_EXACT)) != 0;
+      int qm = 0;  // 0 no refill, 1 every open slot is refilled, 2/3 the queue length decides
+      const long long ql = vload(&S.qlen);
+      const long long spn = vload(&S.seq_pos);
+      if (!(fl & F_GLOBAL) && ql > 0) {
+        qm = (ql - (r - spn) * (long long)S.capmax >= (long long)S.capmax) ? 1 : 2;
+        if (qm == 2) exact = true;
+      }
+      bool ok = G || !(fl & F_GLOBAL);
+      if (ok && exact) {
+        if (spn != r) ok = false;
+        else if ((fl & F_GLOBAL) && vload(&S.walk_pos) != vload(&S.rec_len)) ok = false;
+        if (qm != 0) qm = 3;
+      }
+      if (!ok) {  // not runnable by this executor now: give the slot back
+        if (lane == 0) atomicOr(&S.ready, 1u << s);
+        continue;
+      }
       cs = s;
       cr = r;
       cf = fl;
@@ -2475,26 +2576,31 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     }
     lds_fence();
     if (lane == 0) atomicAdd(&S.busy_exe, 1);
+    if (DGP_TRACE && lane == 0) {
+      TR(cr, 2);
+      trace_at(D, cr, 7, D.trace && cr >= D.trace_lo && cr < D.trace_lo + D.trace_n
+                             ? (D.trace[(cr - D.trace_lo) * 8 + 7] | ((unsigned long long)(threadIdx.x >> 6) << 24)) : 0);
+    }
     const unsigned long long t0 = mclk();
     if (G && (cf & F_GLOBAL)) {
       exe_global_entry<LW>(cs, cr);
-      if (lane == 0) S.prof[9]++;
+      PROF(if (lane == 0) S.prof[9]++);
     } else if (!exe_local<LW>(D, L, P, cs, cr, cq, cex)) {
       if (lane == 0) {
         atomicOr(&L.flags[cs], F_EXACT);
         atomicOr(&S.ready, 1u << cs);
-        S.prof[10]++;
+        PROF(S.prof[10]++);
       }
     }
     if (lane == 0) {
-      atomicAdd(&S.prof[5], mclk() - t0);
+      PROF(atomicAdd(&S.prof[5], mclk() - t0));
       atomicSub(&S.busy_exe, 1);
     }
     t_idle = mclk();
   }
   if (lane == 0) {
-    atomicAdd(&S.prof[28], idle28);
-    atomicAdd(&S.prof[29], idle29);
+    PROF(atomicAdd(&S.prof[28], idle28));
+    PROF(atomicAdd(&S.prof[29], idle29));
   }
 }
 
@@ -2571,8 +2677,8 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
   // ------------------------------------------------------------------ set-up
   workers_io<LW>(D, P, true);
   for (int i = tid; i < WIN * NE; i += blockDim.x) (&L.desc[0][0])[i] = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < RS; i += blockDim.x) L.rdone[i] = -1;
   if (tid < WIN) {
-    L.done_tag[tid] = -1;
     L.pred[tid] = BIG;
     L.flags[tid] = 0;
     L.ntouch[tid] = 0;
@@ -2590,6 +2696,7 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     S.global_pending = 0;
     S.busy_exe = 0;
     S.ready = 0;
+    S.freem = WIN == 32 ? 0xffffffffu : ((1u << (WIN & 31)) - 1u);
     S.seq_pos = pos->seq;
     S.log_len = (long long)c->n_placed;
     S.rec_len = pos->rec_len;
@@ -2713,10 +2820,10 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     }
     for (int i = 0; i < 16; i++) c->prof2[i] = S.prof[i];
     if (S.error) {  // pipeline state for the post-mortem (dgp_stats wave_phase*)
-      const int sl = (int)(S.seq_pos & (WIN - 1));
+      const int sl = 0;
       const long long dv[16] = {S.seq_pos, S.reg_pos, S.pre_pos, S.bld_pos, S.log_len,
                                 (long long)S.ready, S.busy_exe, S.global_pending, (long long)L.flags[sl], L.pred[sl],
-                                L.sid[sl], L.done_tag[sl], S.walk_pos, S.rec_len, S.qlen, S.round_end};
+                                L.sid[sl], (long long)S.freem, S.walk_pos, S.rec_len, S.qlen, S.round_end};
       for (int i = 0; i < 16; i++) c->prof2[i] = (unsigned long long)dv[i];
     }
     for (int i = 0; i < 16; i++) c->prof[i < 8 ? i : 7] = i < 8 ? S.prof[16 + i] : c->prof[7];

@@ -173,6 +173,17 @@ int sync_dev(dgp_engine* e) {
   e->D.pre_lead = pl ? atoi(pl) : dgp::st::DR;
   if (e->D.pre_lead < 64 || e->D.pre_lead > dgp::st::DR) e->D.pre_lead = dgp::st::DR;
   if (!e->D.dbgbuf) HIPCHK(e, hipMalloc((void**)&e->D.dbgbuf, 64 * 8 * sizeof(double)));
+  if (const char* tl = getenv("DGP_TRACE_LO")) {  // DGP_TRACE builds: sampled lifecycle trace
+    const char* tn = getenv("DGP_TRACE_N");
+    e->D.trace_lo = atoll(tl);
+    const long long n = tn ? atoll(tn) : 20000;
+    if (!e->D.trace || e->D.trace_n != n) {
+      if (e->D.trace) (void)hipFree(e->D.trace);
+      HIPCHK(e, hipMalloc((void**)&e->D.trace, n * 8 * 8));
+    }
+    e->D.trace_n = n;
+    HIPCHK(e, hipMemset(e->D.trace, 0, n * 8 * 8));
+  }
   dgp::Dev h[2] = {e->D, e->D};
   h[0].lds_workers = 0;
   h[1].lds_workers = e->D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
@@ -293,7 +304,7 @@ dgp_engine* dgp_create(int device) {
   }
   {
     namespace S = dgp::st;
-    const size_t st = (size_t)S::WIN * S::PLC;
+    const size_t st = (size_t)S::RS * S::PLC;  // staging rows of the retire ring
     int rc = 0;
     rc |= dalloc(e, &e->D.desc, (size_t)S::DR * S::NE, e->allocs);
     rc |= dalloc(e, &e->D.touch_ring, (size_t)S::DR * S::TMAX, e->allocs);
@@ -863,6 +874,12 @@ int dgp_kernel_times(dgp_engine* e, double* ms, int64_t* launches, int32_t n) {
 int dgp_set_timing(dgp_engine* e, int enabled) {
   if (!e) return DGP_E_ARG;
   e->timing = enabled != 0;
+  return 0;
+}
+
+extern "C" int dgp_debug_trace(dgp_engine* e, unsigned long long* out) {  // DGP_TRACE builds
+  if (!e || !e->D.trace) return DGP_E_ARG;
+  HIPCHK(e, hipMemcpy(out, e->D.trace, e->D.trace_n * 8 * 8, hipMemcpyDeviceToHost));
   return 0;
 }
 
