@@ -5,9 +5,11 @@ oracle CPU baseline.
 
 One step = one full replay of the workload on the device (update_graph + every
 completion round, ~1M placements), the graph already resident in HBM. For N GPUs
-(torch.distributed.run, one rank per GPU) every rank replays its own copy of the
-workload ("replicas only") and value = placements of all ranks / the
-slowest rank's time.
+(torch.distributed.run, one rank per GPU): the ordered replay does not
+partition, so every rank runs the same replay (replicated commit, outputs checked equal
+across ranks by an all-gather of digests) and value = the job's placements / the slowest
+rank's time ("strong": the work does not grow with N). The data-parallel part of the
+WorkStealing leg — the per-task thief rows — is sharded over the ranks and all-gathered.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--tasks N] [--workers W]
 """
@@ -47,8 +49,7 @@ def algorithmic_bytes(g: dict, placed_tasks: np.ndarray, n_waves: int) -> float:
 
 
 def reduce_max(x: float, dist, device: str = "cuda") -> float:
-    """The slowest rank's value (replicas only: the ranks share nothing but this and the
-    barriers; RCCL over xGMI on the GPU box, gloo in the CPU tests)."""
+    """The slowest rank's value (RCCL over xGMI on the GPU box, gloo in the CPU tests)."""
     if dist is None:
         return x
     import torch
@@ -58,25 +59,69 @@ def reduce_max(x: float, dist, device: str = "cuda") -> float:
     return float(t.item())
 
 
-def steal_leg(eng, args, world: int) -> dict:
+def link_latency_us(eng_cls, local: int, n_workers: int = 1024) -> float:
+    """The engine's link latency within a round: replays of a star (graphs.star: one
+    completion places N leaves on one worker, whose N completions then run one after
+    another) at two sizes; the slope of the replay time over N (best of 3 each)."""
+    from distributed_amd import graphs
+
+    t = {}
+    for n in (10_000, 40_000):
+        eng = eng_cls(local)
+        eng.load(graphs.star(n, n_workers), CONFIG)
+        best = float("inf")
+        for _ in range(4):
+            eng.reset()
+            eng.update_graph()
+            t0 = time.perf_counter()
+            eng.run_rounds(-1)
+            best = min(best, time.perf_counter() - t0)
+        assert eng.num_placements() == n + 1
+        eng.close()
+        t[n] = best
+    return 1e6 * (t[40_000] - t[10_000]) / 30_000
+
+
+def latency_bound(g: dict, out: dict, link_us: float, achieved_ms: float) -> dict:
+    """Latency roofline of an ordered replay: the longest chain of stimuli that share a
+    worker (dgp_conflict_depth on the engine's own placement log) times the serial link
+    latency. No engine that runs each stimulus in link_us can finish sooner."""
+    from distributed_amd.engine import conflict_depth
+
+    depth, touches = conflict_depth(g, out, 0)
+    min_ms = depth * link_us / 1e3
+    return {"bound": "latency", "critical_path_links": depth, "stimuli": int(len(out["pl_task"])),
+            "touches": touches, "link_us": round(link_us, 3), "min_ms": round(min_ms, 3),
+            "achieved_ms": round(achieved_ms, 3), "frac": round(min_ms / achieved_ms, 4)}
+
+
+def steal_leg(eng, args, world: int, dist=None, barrier=None) -> dict:
     """WorkStealing.balance on a C4-shaped state: one call per
     step, inputs uploaded by the call (the boundary hands over host arrays), device
-    kernel times from HIP events, and the oracle (oracle/steal.cpp) on the host."""
+    kernel times from HIP events, and the oracle (oracle/steal.cpp) on the host. With
+    N ranks every rank takes part: the thief rows are sharded and all-gathered
+    (distributed_amd/shard.py), the ordered walk runs on each rank."""
     from distributed_amd import graphs
 
     p = graphs.steal_problem(args.steal_workers, args.steal_tasks, seed=1)
-    eng.steal_balance(p)  # warm-up
+    group = dist.group.WORLD if dist is not None else None
+    eng.steal_balance(p, group=group)  # warm-up
     eng.set_timing(True)
+    if barrier:
+        barrier()
     t0 = time.perf_counter()
     n_call = 3
     for _ in range(n_call):
-        out = eng.steal_balance(p)
-    dt = (time.perf_counter() - t0) / n_call
+        out = eng.steal_balance(p, group=group)
+    if barrier:
+        barrier()
+    dt = reduce_max((time.perf_counter() - t0) / n_call, dist)
     kt = eng.kernel_times()
     eng.set_timing(False)
     leg = {"metric": "WorkStealing.balance() calls/s", "workload": f"C4-shaped: {args.steal_workers} workers x 2 "
            f"threads, {args.steal_tasks} processing tasks, 10% hot (zipf 1.5), 8 prefixes 10ms*2^j",
-           "ms_per_call": round(dt * 1e3, 3), "steal_requests": int(len(out["st_task"])),
+           "ms_per_call": round(dt * 1e3, 3), "steal_requests": int(len(out["st_task"])), "n_gpus": world,
+           "parallelism": "thief rows sharded + all-gather, ordered walk replicated" if world > 1 else "single",
            "kernel_ms_per_call": {k: round(v[0] / n_call, 3) for k, v in kt.items() if k.startswith("steal")},
            "reference_python_seconds_per_call_at_100k_x_4096": 242.0}  # SURVEY.md §8 a20
     if world == 1 and not args.no_cpu_baseline:
@@ -90,7 +135,7 @@ def steal_leg(eng, args, world: int) -> dict:
     return leg
 
 
-def c3_leg(eng_cls, local: int, args) -> dict:
+def c3_leg(eng_cls, local: int, args, link_us: float | None = None) -> dict:
     """BASELINE.json C3: the P2P-shuffle-shaped graph (P inputs -> P shuffle-transfer ->
     1 shuffle-barrier of fan-in P -> P unpack tasks with _rootish False; shuffle/_shuffle.py
     :276-306) on 512 workers x 1 thread, placement only: one full replay per step, checked
@@ -115,6 +160,8 @@ def c3_leg(eng_cls, local: int, args) -> dict:
     leg = {"metric": "task placements/sec, C3 (P2P-shuffle-shaped graph, placement only)", "value": round(n / dt, 1),
            "unit": "placements/s", "seconds_per_replay": round(dt, 4), "placements_per_replay": n,
            "n_tasks": int(g["n_tasks"]), "n_partitions": args.c3_partitions, "n_workers": args.c3_workers}
+    if link_us:
+        leg["latency_bound"] = latency_bound(g, out, link_us, dt * 1e3)
     if not args.no_cpu_baseline:
         from oracle import oracle
 
@@ -147,18 +194,34 @@ def c5_leg(eng_cls, local: int, args, dist, barrier) -> dict:
     n = int(len(out["pl_task"]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     leg = {"metric": "task placements/sec, C5 (10M-task map + tree-reduce, 16,384 workers)",
-           "value": round(n * world / dt, 1), "unit": "placements/s", "n_gpus": world, "scaling": "weak",
+           "value": round(n / dt, 1), "unit": "placements/s", "n_gpus": world, "scaling": "strong",
            "seconds_per_replay": round(dt, 3), "placements_per_replay": n, "n_tasks": int(g["n_tasks"]),
-           "n_workers": args.c5_workers, "parallelism": f"replicas{world}"}
+           "n_workers": args.c5_workers,
+           "parallelism": f"replicated ordered commit x{world}" if world > 1 else "single"}
+    if dist is not None:
+        from distributed_amd.shard import output_digest, replicas_agree
+
+        leg["replicas_agree"] = replicas_agree(output_digest([out["pl_task"], out["pl_worker"]]), "cuda")
     pin = os.path.join(REPO, "tests", "golden", "c5_full_digest.json")
     if os.path.exists(pin):
         ref = json.load(open(pin))
         if ref["n_map"] == args.c5_map and ref["n_workers"] == args.c5_workers:
             leg["parity"] = graphs.placement_digest(out) == ref["digest"]
-            leg["cpu_baseline"] = {"value": round(ref["n_placements"] / ref["oracle_s"], 1), "unit": "placements/s",
-                                   "cores": 1, "kind": "port", "sample": "oracle/replay.cpp full C5 replay, timed "
-                                   "once in the build container (tools/c5_digest.py), not on this box"}
     eng.close()
+    if int(os.environ.get("RANK", "0")) == 0 and world == 1 and not args.no_cpu_baseline and args.c5_cpu_map > 0:
+        # a bounded sample on this box: the same map + tree-reduce shape and worker count,
+        # fewer map tasks (the full 10M replay takes the 1-core port minutes). The port's
+        # rootish queue scan is O(W) per root (oracle/replay.cpp: argmin over idle_task_count,
+        # as scheduler.py:2195-2245), so its rate here falls with W, not with the graph.
+        from oracle import oracle
+
+        gs = graphs.map_tree_reduce(args.c5_cpu_map, args.c5_workers)
+        ref = oracle.replay(gs, CONFIG, snapshots=False)
+        leg["cpu_baseline"] = {"value": round(len(ref["pl_task"]) / ref["seconds"], 1), "unit": "placements/s",
+                               "cores": 1, "kind": "port",
+                               "sample": f"oracle/replay.cpp on this host, map {args.c5_cpu_map} + tree-reduce "
+                                         f"({len(ref['pl_task'])} placements) x {args.c5_workers} workers; the "
+                                         "rootish scan is O(W) per root, so the ratio reflects that scan"}
     return leg
 
 
@@ -180,6 +243,8 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (10M x 16k) leg")
     ap.add_argument("--c5-map", type=int, default=8_750_000)
     ap.add_argument("--c5-workers", type=int, default=16_384)
+    ap.add_argument("--c5-cpu-map", type=int, default=200_000, help="map tasks of the C5 CPU-baseline sample")
+    ap.add_argument("--no-latency", action="store_true", help="skip the link-latency chain and the latency bound")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -233,18 +298,28 @@ def main():
     eng.set_timing(False)
     placements = eng.num_placements()
     elapsed = reduce_max(elapsed, dist)
-    total_placements = placements * args.steps * world
+    total_placements = placements * args.steps  # the job's placements: every rank makes the same ones
     value = total_placements / elapsed
 
     out = eng.placements()
+    agree = None
+    if dist is not None:
+        from distributed_amd.shard import output_digest, replicas_agree
+
+        agree = replicas_agree(output_digest([out["pl_task"], out["pl_worker"], out["pl_start"]]), "cuda")
+    steal = None
+    if not args.no_steal:  # every rank takes part (sharded thief rows)
+        steal = steal_leg(eng, args, world, dist, barrier)
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "placements/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64+f64",
+        "higher_is_better": True, "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
+        "dtype": "int64+f64",
         "data": "synthetic",
         "config": {"workload": "C2: random DAG, fan-in<=4 (window 4W), lognormal(10,2) nbytes, roots N/10, "
                                "workers x 1 thread, worker-saturation 1.1; full replay per step",
-                   "n_tasks": args.tasks, "n_workers": args.workers, "parallelism": f"replicas{world}",
+                   "n_tasks": args.tasks, "n_workers": args.workers,
+                   "parallelism": f"replicated ordered commit x{world}" if world > 1 else "single",
                    "placements_per_step": placements},
     }
     if rank == 0:
@@ -274,6 +349,9 @@ def main():
             if (t.get("n_tasks"), t.get("n_workers")) == (args.tasks, args.workers):
                 result["roofline"]["traffic"] = round(t["traffic_bytes_per_launch"], 1)
                 result["roofline"]["traffic_source"] = t.get("source")
+        if not args.no_latency:
+            link_us = link_latency_us(PlacementEngine, local)
+            result["latency_bound"] = latency_bound(g, out, link_us, 1e3 * elapsed / args.steps)
         result["kernels"] = {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in kernels.items()}
         result["config"]["waves"] = int(n_waves)
         if world == 1 and not args.no_cpu_baseline:
@@ -290,11 +368,13 @@ def main():
                                       "sample": f"oracle/replay.cpp, full C2 replay ({n_ref} placements) x {runs}"}
             result["parity"] = bool(all(np.array_equal(out[k], ref[k]) for k in (
                 "pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")))
-        if not args.no_steal:
-            result["steal"] = steal_leg(eng, args, world)
+        if agree is not None:
+            result["replicas_agree"] = agree
+        if steal is not None:
+            result["steal"] = steal
     eng.close()
     if rank == 0 and not args.no_c3:
-        result["c3"] = c3_leg(PlacementEngine, local, args)
+        result["c3"] = c3_leg(PlacementEngine, local, args, result.get("latency_bound", {}).get("link_us"))
     if not args.no_c5:  # every rank takes part (barriers, max over ranks)
         c5 = c5_leg(PlacementEngine, local, args, dist, barrier)
         if rank == 0:

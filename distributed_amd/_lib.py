@@ -38,9 +38,17 @@ SIGNATURES = {
     "dgp_kernel_times": (C.c_int, [_P, _P, _P, C.c_int32]),
     "dgp_set_timing": (C.c_int, [_P, C.c_int]),
     "dgp_stats": (C.c_int, [_P, _P, C.c_int32]),
+    "dgp_conflict_depth": (C.c_int, [C.c_int64, _P, _P, _P, C.c_int64, _P, _P, C.c_int64, _P, _P]),
     "dgp_steal_balance": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_int64, C.c_int64,
                                     C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, _P, _P,
                                     _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dgp_steal_load": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_int64, C.c_int64,
+                                 C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, _P, _P, _P]),
+    "dgp_steal_thief_rows": (C.c_int, [_P, C.c_int64, C.c_int64]),
+    "dgp_steal_row_bytes": (C.c_int64, []),
+    "dgp_steal_pack_rows": (C.c_int, [_P, C.c_int64, C.c_int64, _P]),
+    "dgp_steal_unpack_rows": (C.c_int, [_P, C.c_int64, C.c_int64, _P]),
+    "dgp_steal_run": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
 }
 
 ABI_VERSION = 2
@@ -59,6 +67,15 @@ def load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise DgpError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                        " (the HIP engine has no CPU fallback)")
+    # One HIP runtime per process: torch bundles its own libamdhip64 (same soname,
+    # libamdhip64.so.7, as /opt/rocm's), and a second runtime loaded beside an
+    # initialised one sees no GPU. Importing torch first makes the engine bind to the
+    # runtime torch uses, so engine pointers and torch device tensors (the all-gather
+    # buffers of shard.py) live in one address space.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -32,6 +32,21 @@
 
 // =================================================================== host side
 
+struct StealCtx {  // WorkStealing arrays of the last dgp_steal_load (one arena)
+  char* arena = nullptr;
+  size_t cap = 0;
+  dgp::steal::Prob P{};
+  void* d_tmp = nullptr;
+  size_t tmp_bytes = 0;
+  int32_t* keys_sorted = nullptr;
+  int32_t* d_vals = nullptr;
+  int32_t W = 0;
+  int64_t T = 0;
+  int NK = 0;
+  int64_t n_stealable = 0;
+  bool loaded = false;
+};
+
 struct dgp_engine {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -66,6 +81,7 @@ struct dgp_engine {
   std::vector<hipEvent_t> evpool;
   std::vector<int> evkind;
   size_t evused = 0;
+  StealCtx steal;
 };
 
 namespace {
@@ -341,6 +357,7 @@ void dgp_destroy(dgp_engine* e) {
   if (e->d_msgs) (void)hipFree(e->d_msgs);
   if (e->d_status) (void)hipFree(e->d_status);
   if (e->h_msgs) (void)hipHostFree(e->h_msgs);
+  if (e->steal.arena) (void)hipFree(e->steal.arena);
   (void)hipFree(e->ctl);
   (void)hipFree(e->d_aux);
   (void)hipFree(e->d_dev);
@@ -889,6 +906,69 @@ extern "C" int dgp_debug_buf(dgp_engine* e, double* out) {
   return 0;
 }
 
+// Longest chain of the replay's conflict DAG (measurement; host code, no engine): stimulus r
+// completes pl_task[r] (the replay completes tasks in run_id order, SURVEY.md §8 replay
+// definition) and touches the completing worker, the holder of every dependency it
+// releases (its last dependent completed, not wanted: scheduler.py:3309-3314) and the
+// holder of every dependency of each task it makes ready (decide_worker's candidates,
+// :8550-8593). Two stimuli that touch one worker are ordered; depth = 1 + the deepest
+// earlier stimulus sharing a worker. Queue refills (rootish placements popped by a
+// completion, :4983-5023) are not modelled, so depth is a lower bound on the ordered links.
+int dgp_conflict_depth(int64_t n_tasks, const int64_t* dep_ptr, const int32_t* dep_idx, const uint8_t* wanted,
+                       int64_t n_pl, const int32_t* pl_task, const int32_t* pl_worker, int64_t first,
+                       int64_t* depth, int64_t* n_touch) {
+  if (n_tasks < 0 || n_pl < 0 || n_pl > n_tasks || first < 0 || !depth || (n_tasks && (!dep_ptr || !wanted)) ||
+      (n_pl && (!pl_task || !pl_worker)))
+    return DGP_E_ARG;
+  std::vector<int64_t> run(n_tasks, -1);
+  std::vector<int32_t> holder(n_tasks, -1);
+  int32_t wmax = 0;
+  for (int64_t r = 0; r < n_pl; r++) {
+    if (pl_task[r] < 0 || pl_task[r] >= n_tasks || pl_worker[r] < 0) return DGP_E_ARG;
+    run[pl_task[r]] = r;
+    holder[pl_task[r]] = pl_worker[r];
+    wmax = std::max(wmax, pl_worker[r]);
+  }
+  std::vector<int64_t> fr(n_tasks, -1), rel(n_tasks, -1);  // frontier / release stimulus
+  std::vector<uint8_t> has_dep(n_tasks, 0);
+  for (int64_t x = 0; x < n_tasks; x++)
+    for (int64_t j = dep_ptr[x]; j < dep_ptr[x + 1]; j++) {
+      const int32_t d = dep_idx[j];
+      fr[x] = std::max(fr[x], run[d]);
+      rel[d] = std::max(rel[d], run[x]);
+      has_dep[d] = 1;
+    }
+  std::vector<int64_t> cnt(n_pl + 1, 0);
+  for (int64_t r = 0; r < n_pl; r++) cnt[r + 1]++;
+  for (int64_t x = 0; x < n_tasks; x++) {
+    if (fr[x] >= 0) cnt[fr[x] + 1] += dep_ptr[x + 1] - dep_ptr[x];
+    if (has_dep[x] && !wanted[x] && rel[x] >= 0) cnt[rel[x] + 1]++;
+  }
+  for (int64_t r = 0; r < n_pl; r++) cnt[r + 1] += cnt[r];
+  std::vector<int32_t> tw(cnt[n_pl]);
+  std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+  for (int64_t r = 0; r < n_pl; r++) tw[pos[r]++] = pl_worker[r];
+  for (int64_t x = 0; x < n_tasks; x++) {
+    if (fr[x] >= 0)
+      for (int64_t j = dep_ptr[x]; j < dep_ptr[x + 1]; j++) tw[pos[fr[x]]++] = holder[dep_idx[j]];
+    if (has_dep[x] && !wanted[x] && rel[x] >= 0) tw[pos[rel[x]]++] = holder[x];
+  }
+  std::vector<int64_t> last(wmax + 1, 0);
+  int64_t best = 0;
+  for (int64_t r = first; r < n_pl; r++) {
+    int64_t dp = 0;
+    for (int64_t i = cnt[r]; i < cnt[r + 1]; i++)
+      if (tw[i] >= 0) dp = std::max(dp, last[tw[i]]);
+    dp += 1;
+    for (int64_t i = cnt[r]; i < cnt[r + 1]; i++)
+      if (tw[i] >= 0) last[tw[i]] = dp;
+    best = std::max(best, dp);
+  }
+  *depth = best;
+  if (n_touch) *n_touch = cnt[n_pl] - cnt[std::min(first, n_pl)];
+  return 0;
+}
+
 int dgp_stats(dgp_engine* e, int64_t* out, int32_t n) {
   if (!e || !out) return DGP_E_ARG;
   dgp::Ctl c;
@@ -906,6 +986,246 @@ int dgp_stats(dgp_engine* e, int64_t* out, int32_t n) {
 
 // ------------------------------------------------------------------ WorkStealing
 // WorkStealing.balance (stealing.py:401-503) over host arrays (see include/dgplace.h).
+// WorkStealing state resident in the engine between the phases of one balance():
+// dgp_steal_load (upload, levels, bins, thief order) -> dgp_steal_thief_rows (any
+// slice of the stealable positions; ranks of a sharded call each take one) ->
+// [dgp_steal_pack_rows / dgp_steal_unpack_rows around an all-gather] -> dgp_steal_run.
+int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const double* occ, const int32_t* nproc,
+                   const int64_t* wnbytes, const uint8_t* idle, const uint8_t* sat, double total_occ,
+                   int64_t total_nthreads, int64_t bandwidth, int64_t T, const int32_t* victim, const double* duration,
+                   const uint8_t* fast, const int64_t* dep_ptr, const int32_t* dep_idx, int64_t n_data,
+                   const int64_t* d_nbytes, const int64_t* d_get_nbytes, const int64_t* h_ptr, const int32_t* h_idx,
+                   int64_t* n_stealable) {
+  namespace S = dgp::steal;
+  if (!e) return DGP_E_ARG;
+  e->steal.loaded = false;
+  if (W <= 0 || T < 0 || n_data < 0 || bandwidth <= 0 || total_nthreads <= 0 || !nthreads || !occ || !nproc ||
+      !wnbytes || !idle || !sat || !n_stealable || (T && (!victim || !duration || !fast || !dep_ptr)) ||
+      (n_data && (!d_nbytes || !d_get_nbytes || !h_ptr)))
+    return fail(e, DGP_E_ARG, "dgp_steal_load: bad sizes or null pointers");
+  if (S::balance_lds_bytes(W) > 160 * 1024) return fail(e, DGP_E_ARG, "dgp_steal_load: too many workers");
+  if ((size_t)W * S::N_LEVELS >= (1u << 30)) return fail(e, DGP_E_ARG, "dgp_steal_load: W too large");
+  if (T >= (1ll << 31)) return fail(e, DGP_E_ARG, "dgp_steal_load: too many tasks");
+  // the shapes the kernels assume, checked on the host
+  for (int32_t w = 0; w < W; w++)
+    if (nthreads[w] <= 0) return fail(e, DGP_E_ARG, "dgp_steal_load: nthreads must be positive");
+  const int64_t E = T ? dep_ptr[T] : 0;
+  if (T && (dep_ptr[0] != 0 || E < 0)) return fail(e, DGP_E_ARG, "dgp_steal_load: dep_ptr");
+  if (E && !dep_idx) return fail(e, DGP_E_ARG, "dgp_steal_load: dep_idx");
+  for (int64_t t = 0; t < T; t++) {
+    if (victim[t] < 0 || victim[t] >= W) return fail(e, DGP_E_ARG, "dgp_steal_load: victim out of range");
+    if (dep_ptr[t + 1] < dep_ptr[t]) return fail(e, DGP_E_ARG, "dgp_steal_load: dep_ptr not monotone");
+  }
+  for (int64_t k = 0; k < E; k++)
+    if (dep_idx[k] < 0 || dep_idx[k] >= n_data) return fail(e, DGP_E_ARG, "dgp_steal_load: dep_idx out of range");
+  const int64_t H = n_data ? h_ptr[n_data] : 0;
+  if (n_data && h_ptr[0] != 0) return fail(e, DGP_E_ARG, "dgp_steal_load: h_ptr");
+  for (int64_t d = 0; d < n_data; d++)
+    if (h_ptr[d + 1] < h_ptr[d]) return fail(e, DGP_E_ARG, "dgp_steal_load: h_ptr not monotone");
+  if (H && !h_idx) return fail(e, DGP_E_ARG, "dgp_steal_load: h_idx");
+  for (int64_t k = 0; k < H; k++)
+    if (h_idx[k] < 0 || h_idx[k] >= W) return fail(e, DGP_E_ARG, "dgp_steal_load: holder out of range");
+  HIPCHK(e, hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  StealCtx& C = e->steal;
+  const int NK = S::N_LEVELS * W + 1;
+  std::vector<std::pair<void**, size_t>> parts;
+  S::Prob P{};
+  int32_t *d_nthreads, *d_nproc, *d_victim, *d_dep_idx, *d_h_idx;
+  double *d_occ, *d_dur;
+  int64_t *d_wnb, *d_dep_ptr, *d_dnb, *d_dgnb, *d_h_ptr;
+  uint8_t *d_idle, *d_sat, *d_fast;
+  const int Tn = (int)T;
+  size_t tmp_sort = 0, tmp_scan = 0, tmp_nb = 0, tmp_a = 0;
+  hipError_t st = hipSuccess;
+  auto chk = [&](hipError_t x) {
+    if (x != hipSuccess && st == hipSuccess) st = x;
+  };
+  chk(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
+                                         (int32_t*)nullptr, std::max(Tn, 1), 0, 32, s));
+  chk(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_scan, (int32_t*)nullptr, (int32_t*)nullptr, NK, s));
+  // the two stable sorts that order the initial thieves
+  chk(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_nb, (int64_t*)nullptr, (int64_t*)nullptr, (int32_t*)nullptr,
+                                         (int32_t*)nullptr, W, 0, 64, s));
+  chk(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_a, (uint64_t*)nullptr, (uint64_t*)nullptr, (int32_t*)nullptr,
+                                         (int32_t*)nullptr, W, 0, 64, s));
+  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_load: sizing: ") + hipGetErrorString(st));
+  const size_t tmp_bytes = std::max(std::max(tmp_sort, tmp_scan), std::max(tmp_nb, tmp_a));
+  auto add = [&](auto** p, size_t n) { parts.push_back({(void**)p, (n ? n : 1) * sizeof(**p)}); };
+  add(&d_nthreads, W); add(&d_occ, W); add(&d_nproc, W); add(&d_wnb, W); add(&d_idle, W); add(&d_sat, W);
+  add(&d_victim, T); add(&d_dur, T); add(&d_fast, T); add(&d_dep_ptr, T + 1); add(&d_dep_idx, E);
+  add(&d_dnb, n_data); add(&d_dgnb, n_data); add(&d_h_ptr, n_data + 1); add(&d_h_idx, H);
+  add(&P.key, T); add(&P.order, T); add(&C.keys_sorted, T); add(&C.d_vals, T); add(&P.bin_cnt, NK); add(&P.bin_ptr, NK);
+  add(&P.s_best, T); add(&P.s_cct, T); add(&P.s_ccv, T); add(&P.s_dur, T);
+  add(&P.s_cget, T); add(&P.s_craw, T); add(&P.s_nh, T); add(&P.s_hw, T * S::MAXH); add(&P.s_hg, T * S::MAXH);
+  add(&P.s_hr, T * S::MAXH);
+  add(&P.tk_a, W); add(&P.tk_nb, W); add(&P.tk_w, W); add(&P.tk_a2, W); add(&P.tk_nb2, W); add(&P.tk_w2, W);
+  add(&P.th_order, W); add(&P.run_start, W + 1); add(&P.run_a, W); add(&P.run_of_w, W); add(&P.n_runs, 1);
+  add(&P.vs_g, W);
+  add(&P.level, T); add(&P.st_task, T); add(&P.st_victim, T); add(&P.st_thief, T); add(&P.st_level, T);
+  add(&P.st_cost, T); add(&P.st_occ_victim, T); add(&P.st_occ_thief, T); add(&P.n_steals, 1);
+  add(&P.inflight_occ, W); add(&P.inflight_tasks, W); add(&P.idle_out, W); add(&P.sat_out, W);
+  size_t total = (tmp_bytes + 255) / 256 * 256;
+  for (auto& pr : parts) total += (pr.second + 255) / 256 * 256;
+  if (total > C.cap) {  // the arena grows, never shrinks, while the engine lives
+    if (C.arena) HIPCHK(e, hipFree(C.arena));
+    C.arena = nullptr;
+    C.cap = 0;
+    HIPCHK(e, hipMalloc(&C.arena, total));
+    C.cap = total;
+  }
+  size_t off = 0;
+  C.d_tmp = C.arena;
+  C.tmp_bytes = tmp_bytes;
+  off += (tmp_bytes + 255) / 256 * 256;
+  for (auto& pr : parts) {
+    *pr.first = C.arena + off;
+    off += (pr.second + 255) / 256 * 256;
+  }
+  auto h2d = [&](void* dst, const void* src, size_t bytes) {
+    return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+  };
+  chk(h2d(d_nthreads, nthreads, W * 4)); chk(h2d(d_occ, occ, W * 8)); chk(h2d(d_nproc, nproc, W * 4));
+  chk(h2d(d_wnb, wnbytes, W * 8)); chk(h2d(d_idle, idle, W)); chk(h2d(d_sat, sat, W));
+  chk(h2d(d_victim, victim, T * 4)); chk(h2d(d_dur, duration, T * 8)); chk(h2d(d_fast, fast, T));
+  chk(h2d(d_dep_ptr, dep_ptr, (T + 1) * 8)); chk(h2d(d_dep_idx, dep_idx, E * 4));
+  chk(h2d(d_dnb, d_nbytes, n_data * 8)); chk(h2d(d_dgnb, d_get_nbytes, n_data * 8));
+  chk(h2d(d_h_ptr, h_ptr, (n_data + 1) * 8)); chk(h2d(d_h_idx, h_idx, H * 4));
+  chk(hipMemsetAsync(P.bin_cnt, 0, NK * 4, s));
+  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_load: upload: ") + hipGetErrorString(st));
+  P.W = W; P.nthreads = d_nthreads; P.occ = d_occ; P.nproc = d_nproc; P.wnbytes = d_wnb; P.idle = d_idle;
+  P.sat = d_sat; P.total_occ = total_occ; P.total_nthreads = total_nthreads; P.bw = bandwidth; P.T = T;
+  P.victim = d_victim; P.duration = d_dur; P.fast = d_fast; P.dep_ptr = d_dep_ptr; P.dep_idx = d_dep_idx;
+  P.d_nbytes = d_dnb; P.d_get_nbytes = d_dgnb; P.h_ptr = d_h_ptr; P.h_idx = d_h_idx; P.key_sorted = C.keys_sorted;
+  C.P = P;
+  C.W = W;
+  C.T = T;
+  C.NK = NK;
+  int bits = 1;
+  while ((1ll << bits) < NK) bits++;
+  int rc = 0;
+  int32_t nst = 0;
+  if (T > 0) {
+    rc = timed_launch(e, 4, [&] {
+      hipLaunchKernelGGL(S::k_steal_levels, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(dgp::k_iota32, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, C.d_vals, (int)T);
+      size_t tb = tmp_bytes;
+      chk(hipcub::DeviceRadixSort::SortPairs(C.d_tmp, tb, P.key, C.keys_sorted, C.d_vals, P.order, Tn, 0, bits, s));
+      tb = tmp_bytes;
+      chk(hipcub::DeviceScan::ExclusiveSum(C.d_tmp, tb, P.bin_cnt, P.bin_ptr, NK, s));
+    });
+    if (!rc) rc = timed_launch(e, 5, [&] {
+      // initial thieves in (stack time, ws.nbytes, index) order: two stable radix sorts
+      const unsigned gw = (unsigned)((W + 255) / 256);
+      hipLaunchKernelGGL(S::k_thief_keys, dim3(gw), dim3(256), 0, s, P);
+      size_t tb = tmp_bytes;
+      chk(hipcub::DeviceRadixSort::SortPairs(C.d_tmp, tb, P.tk_nb, P.tk_nb2, P.tk_w, P.tk_w2, W, 0, 64, s));
+      hipLaunchKernelGGL(S::k_gather_a, dim3(gw), dim3(256), 0, s, P);
+      tb = tmp_bytes;
+      chk(hipcub::DeviceRadixSort::SortPairs(C.d_tmp, tb, P.tk_a2, P.tk_a, P.tk_w2, P.th_order, W, 0, 64, s));
+      hipLaunchKernelGGL(S::k_runs, dim3(1), dim3(64), 0, s, P);
+    });
+    if (!rc) chk(hipMemcpyAsync(&nst, P.bin_ptr + NK - 1, 4, hipMemcpyDeviceToHost, s));
+  } else {
+    chk(hipMemsetAsync(P.bin_ptr, 0, NK * 4, s));
+    chk(hipMemsetAsync(P.n_runs, 0, 4, s));  // no thief runs are read without tasks
+  }
+  chk(hipStreamSynchronize(s));
+  if (rc) return rc;
+  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_load: ") + hipGetErrorString(st));
+  if (nst < 0 || nst > T) return fail(e, DGP_E_STATE, "dgp_steal_load: bin scan out of range");
+  C.n_stealable = nst;
+  C.loaded = true;
+  *n_stealable = nst;
+  return 0;
+}
+
+int dgp_steal_thief_rows(dgp_engine* e, int64_t lo, int64_t hi) {
+  if (!e) return DGP_E_ARG;
+  StealCtx& C = e->steal;
+  if (!C.loaded) return fail(e, DGP_E_STATE, "dgp_steal_thief_rows: no dgp_steal_load");
+  if (lo < 0 || hi < lo || hi > C.n_stealable) return fail(e, DGP_E_ARG, "dgp_steal_thief_rows: range");
+  if (hi == lo) return 0;
+  HIPCHK(e, hipSetDevice(e->device));
+  const dgp::steal::Prob P = C.P;
+  return timed_launch(e, 5, [&] {
+    hipLaunchKernelGGL(dgp::steal::k_best_thief, dim3((unsigned)(((hi - lo) * 64 + 255) / 256)), dim3(256), 0,
+                       e->stream, P, lo, hi);
+  });
+}
+
+int64_t dgp_steal_row_bytes(void) { return (int64_t)sizeof(dgp::steal::Row); }
+
+int dgp_steal_pack_rows(dgp_engine* e, int64_t lo, int64_t hi, void* dst) {
+  if (!e) return DGP_E_ARG;
+  StealCtx& C = e->steal;
+  if (!C.loaded) return fail(e, DGP_E_STATE, "dgp_steal_pack_rows: no dgp_steal_load");
+  if (lo < 0 || hi < lo || hi > C.n_stealable || (hi > lo && !dst)) return fail(e, DGP_E_ARG, "dgp_steal_pack_rows: range");
+  if (hi == lo) return 0;
+  HIPCHK(e, hipSetDevice(e->device));
+  hipLaunchKernelGGL(dgp::steal::k_pack_rows, dim3((unsigned)((hi - lo + 255) / 256)), dim3(256), 0, e->stream, C.P,
+                     lo, hi, (dgp::steal::Row*)dst);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipStreamSynchronize(e->stream));  // the caller's collective runs on its own stream
+  return 0;
+}
+
+int dgp_steal_unpack_rows(dgp_engine* e, int64_t lo, int64_t hi, const void* src) {
+  if (!e) return DGP_E_ARG;
+  StealCtx& C = e->steal;
+  if (!C.loaded) return fail(e, DGP_E_STATE, "dgp_steal_unpack_rows: no dgp_steal_load");
+  if (lo < 0 || hi < lo || hi > C.n_stealable || (hi > lo && !src))
+    return fail(e, DGP_E_ARG, "dgp_steal_unpack_rows: range");
+  if (hi == lo) return 0;
+  HIPCHK(e, hipSetDevice(e->device));
+  hipLaunchKernelGGL(dgp::steal::k_unpack_rows, dim3((unsigned)((hi - lo + 255) / 256)), dim3(256), 0, e->stream,
+                     C.P, lo, hi, (const dgp::steal::Row*)src);
+  HIPCHK(e, hipGetLastError());
+  return 0;
+}
+
+int dgp_steal_run(dgp_engine* e, int8_t* level_out, int32_t* st_task, int32_t* st_victim, int32_t* st_thief,
+                  int32_t* st_level, double* st_cost, double* st_occ_victim, double* st_occ_thief, int64_t* n_steals,
+                  double* inflight_occ, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* sat_out) {
+  namespace S = dgp::steal;
+  if (!e) return DGP_E_ARG;
+  StealCtx& C = e->steal;
+  if (!C.loaded) return fail(e, DGP_E_STATE, "dgp_steal_run: no dgp_steal_load");
+  if (!n_steals || !inflight_occ || !inflight_tasks || !idle_out || !sat_out)
+    return fail(e, DGP_E_ARG, "dgp_steal_run: null pointers");
+  HIPCHK(e, hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  const S::Prob P = C.P;
+  const int64_t T = C.T;
+  const int32_t W = C.W;
+  int rc = timed_launch(e, 6, [&] {
+    hipLaunchKernelGGL(S::k_balance, dim3(1), dim3(64), S::balance_lds_bytes(W), s, P);
+  });
+  if (rc) return rc;
+  hipError_t st = hipSuccess;
+  auto chk = [&](hipError_t x) {
+    if (x != hipSuccess && st == hipSuccess) st = x;
+  };
+  long long ns = 0;
+  chk(hipMemcpyAsync(&ns, P.n_steals, 8, hipMemcpyDeviceToHost, s));
+  chk(hipStreamSynchronize(s));
+  if (st == hipSuccess) {
+    *n_steals = ns;
+    auto d2h = [&](void* dst, const void* src, size_t bytes) {
+      if (dst && bytes) chk(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    };
+    d2h(level_out, P.level, T);
+    d2h(st_task, P.st_task, ns * 4); d2h(st_victim, P.st_victim, ns * 4); d2h(st_thief, P.st_thief, ns * 4);
+    d2h(st_level, P.st_level, ns * 4); d2h(st_cost, P.st_cost, ns * 8); d2h(st_occ_victim, P.st_occ_victim, ns * 8);
+    d2h(st_occ_thief, P.st_occ_thief, ns * 8);
+    d2h(inflight_occ, P.inflight_occ, W * 8); d2h(inflight_tasks, P.inflight_tasks, W * 4);
+    d2h(idle_out, P.idle_out, W); d2h(sat_out, P.sat_out, W);
+    chk(hipStreamSynchronize(s));
+  }
+  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_run: ") + hipGetErrorString(st));
+  return 0;
+}
+
 int dgp_steal_balance(dgp_engine* e, int32_t W, const int32_t* nthreads, const double* occ, const int32_t* nproc,
                       const int64_t* wnbytes, const uint8_t* idle, const uint8_t* sat, double total_occ,
                       int64_t total_nthreads, int64_t bandwidth, int64_t T, const int32_t* victim,
@@ -915,154 +1235,14 @@ int dgp_steal_balance(dgp_engine* e, int32_t W, const int32_t* nthreads, const d
                       int32_t* st_thief, int32_t* st_level, double* st_cost, double* st_occ_victim,
                       double* st_occ_thief, int64_t* n_steals, double* inflight_occ, int32_t* inflight_tasks,
                       uint8_t* idle_out, uint8_t* sat_out) {
-  namespace S = dgp::steal;
-  if (!e) return DGP_E_ARG;
-  if (W <= 0 || T < 0 || n_data < 0 || bandwidth <= 0 || total_nthreads <= 0 || !nthreads || !occ || !nproc ||
-      !wnbytes || !idle || !sat || !n_steals || !inflight_occ || !inflight_tasks || !idle_out || !sat_out)
-    return fail(e, DGP_E_ARG, "dgp_steal_balance: bad sizes or null pointers");
-  if (S::balance_lds_bytes(W) > 160 * 1024) return fail(e, DGP_E_ARG, "dgp_steal_balance: too many workers");
-  if ((size_t)W * S::N_LEVELS >= (1u << 30)) return fail(e, DGP_E_ARG, "dgp_steal_balance: W too large");
-  // the shapes the kernels assume, checked on the host
-  for (int32_t w = 0; w < W; w++)
-    if (nthreads[w] <= 0) return fail(e, DGP_E_ARG, "dgp_steal_balance: nthreads must be positive");
-  const int64_t E = T ? dep_ptr[T] : 0;
-  if (T && (dep_ptr[0] != 0 || E < 0)) return fail(e, DGP_E_ARG, "dgp_steal_balance: dep_ptr");
-  for (int64_t t = 0; t < T; t++) {
-    if (victim[t] < 0 || victim[t] >= W) return fail(e, DGP_E_ARG, "dgp_steal_balance: victim out of range");
-    if (dep_ptr[t + 1] < dep_ptr[t]) return fail(e, DGP_E_ARG, "dgp_steal_balance: dep_ptr not monotone");
-  }
-  for (int64_t k = 0; k < E; k++)
-    if (dep_idx[k] < 0 || dep_idx[k] >= n_data) return fail(e, DGP_E_ARG, "dgp_steal_balance: dep_idx out of range");
-  const int64_t H = n_data ? h_ptr[n_data] : 0;
-  for (int64_t d = 0; d < n_data; d++)
-    if (h_ptr[d + 1] < h_ptr[d]) return fail(e, DGP_E_ARG, "dgp_steal_balance: h_ptr not monotone");
-  for (int64_t k = 0; k < H; k++)
-    if (h_idx[k] < 0 || h_idx[k] >= W) return fail(e, DGP_E_ARG, "dgp_steal_balance: holder out of range");
-  HIPCHK(e, hipSetDevice(e->device));
-  hipStream_t s = e->stream;
-  const int NK = S::N_LEVELS * W + 1;
-  // one arena for inputs, work and outputs
-  std::vector<std::pair<void**, size_t>> parts;
-  S::Prob P{};
-  int32_t *d_nthreads, *d_nproc, *d_victim, *d_dep_idx, *d_h_idx, *d_vals;
-  double *d_occ, *d_dur, *d_ifo;
-  int64_t *d_wnb, *d_dep_ptr, *d_dnb, *d_dgnb, *d_h_ptr;
-  uint8_t *d_idle, *d_sat, *d_fast, *d_idle_o, *d_sat_o;
-  long long* d_ns;
-  void* d_tmp = nullptr;
-  size_t tmp_sort = 0, tmp_scan = 0;
-  int32_t* keys_sorted = nullptr;
-  const int Tn = (int)T;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
-                                     (int32_t*)nullptr, std::max(Tn, 1), 0, 32, s);
-  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_scan, (int32_t*)nullptr, (int32_t*)nullptr, NK, s);
-  size_t tmp_nb = 0, tmp_a = 0;  // the two stable sorts that order the initial thieves
-  hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_nb, (int64_t*)nullptr, (int64_t*)nullptr, (int32_t*)nullptr,
-                                     (int32_t*)nullptr, W, 0, 64, s);
-  hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_a, (uint64_t*)nullptr, (uint64_t*)nullptr, (int32_t*)nullptr,
-                                     (int32_t*)nullptr, W, 0, 64, s);
-  const size_t tmp_bytes = std::max(std::max(tmp_sort, tmp_scan), std::max(tmp_nb, tmp_a));
-  auto add = [&](auto** p, size_t n) { parts.push_back({(void**)p, (n ? n : 1) * sizeof(**p)}); };
-  add(&d_nthreads, W); add(&d_occ, W); add(&d_nproc, W); add(&d_wnb, W); add(&d_idle, W); add(&d_sat, W);
-  add(&d_victim, T); add(&d_dur, T); add(&d_fast, T); add(&d_dep_ptr, T + 1); add(&d_dep_idx, E);
-  add(&d_dnb, n_data); add(&d_dgnb, n_data); add(&d_h_ptr, n_data + 1); add(&d_h_idx, H);
-  add(&P.key, T); add(&P.order, T); add(&keys_sorted, T); add(&d_vals, T); add(&P.bin_cnt, NK); add(&P.bin_ptr, NK);
-  add(&P.s_best, T); add(&P.s_cct, T); add(&P.s_ccv, T); add(&P.s_dur, T);
-  add(&P.s_cget, T); add(&P.s_craw, T); add(&P.s_nh, T); add(&P.s_hw, T * S::MAXH); add(&P.s_hg, T * S::MAXH);
-  add(&P.s_hr, T * S::MAXH);
-  add(&P.tk_a, W); add(&P.tk_nb, W); add(&P.tk_w, W); add(&P.tk_a2, W); add(&P.tk_nb2, W); add(&P.tk_w2, W);
-  add(&P.th_order, W); add(&P.run_start, W + 1); add(&P.run_a, W); add(&P.run_of_w, W); add(&P.n_runs, 1);
-  add(&P.vs_g, W);
-  add(&P.level, T); add(&P.st_task, T); add(&P.st_victim, T); add(&P.st_thief, T); add(&P.st_level, T);
-  add(&P.st_cost, T); add(&P.st_occ_victim, T); add(&P.st_occ_thief, T); add(&d_ns, 1);
-  add(&d_ifo, W); add(&P.inflight_tasks, W); add(&d_idle_o, W); add(&d_sat_o, W);
-  size_t total = tmp_bytes + 256;
-  for (auto& pr : parts) total += (pr.second + 255) / 256 * 256;
-  char* arena = nullptr;
-  HIPCHK(e, hipMalloc(&arena, total));
-  size_t off = 0;
-  d_tmp = arena;
-  off += (tmp_bytes + 255) / 256 * 256;
-  for (auto& pr : parts) {
-    *pr.first = arena + off;
-    off += (pr.second + 255) / 256 * 256;
-  }
-  auto h2d = [&](void* dst, const void* src, size_t bytes) {
-    return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
-  };
-  hipError_t st = hipSuccess;
-  auto chk = [&](hipError_t x) {
-    if (x != hipSuccess && st == hipSuccess) st = x;
-  };
-  chk(h2d(d_nthreads, nthreads, W * 4)); chk(h2d(d_occ, occ, W * 8)); chk(h2d(d_nproc, nproc, W * 4));
-  chk(h2d(d_wnb, wnbytes, W * 8)); chk(h2d(d_idle, idle, W)); chk(h2d(d_sat, sat, W));
-  chk(h2d(d_victim, victim, T * 4)); chk(h2d(d_dur, duration, T * 8)); chk(h2d(d_fast, fast, T));
-  chk(h2d(d_dep_ptr, dep_ptr, (T + 1) * 8)); chk(h2d(d_dep_idx, dep_idx, E * 4));
-  chk(h2d(d_dnb, d_nbytes, n_data * 8)); chk(h2d(d_dgnb, d_get_nbytes, n_data * 8));
-  chk(h2d(d_h_ptr, h_ptr, (n_data + 1) * 8)); chk(h2d(d_h_idx, h_idx, H * 4));
-  chk(hipMemsetAsync(P.bin_cnt, 0, NK * 4, s));
-  if (st != hipSuccess) {
-    hipFree(arena);
-    return fail(e, DGP_E_HIP, std::string("dgp_steal_balance: upload: ") + hipGetErrorString(st));
-  }
-  P.W = W; P.nthreads = d_nthreads; P.occ = d_occ; P.nproc = d_nproc; P.wnbytes = d_wnb; P.idle = d_idle;
-  P.sat = d_sat; P.total_occ = total_occ; P.total_nthreads = total_nthreads; P.bw = bandwidth; P.T = T;
-  P.victim = d_victim; P.duration = d_dur; P.fast = d_fast; P.dep_ptr = d_dep_ptr; P.dep_idx = d_dep_idx;
-  P.d_nbytes = d_dnb; P.d_get_nbytes = d_dgnb; P.h_ptr = d_h_ptr; P.h_idx = d_h_idx; P.key_sorted = keys_sorted;
-  P.n_steals = d_ns; P.inflight_occ = d_ifo; P.idle_out = d_idle_o; P.sat_out = d_sat_o;
-  int bits = 1;
-  while ((1ll << bits) < NK) bits++;
-  int rc = 0;
-  if (T > 0) {
-    rc = timed_launch(e, 4, [&] {
-      hipLaunchKernelGGL(S::k_steal_levels, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, P);
-      hipLaunchKernelGGL(dgp::k_iota32, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, d_vals, (int)T);
-      size_t tb = tmp_bytes;
-      hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, P.key, keys_sorted, d_vals, P.order, Tn, 0, bits, s);
-      tb = tmp_bytes;
-      hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, P.bin_cnt, P.bin_ptr, NK, s);
-    });
-    if (!rc) rc = timed_launch(e, 5, [&] {
-      // initial thieves in (stack time, ws.nbytes, index) order: two stable radix sorts
-      const unsigned gw = (unsigned)((W + 255) / 256);
-      hipLaunchKernelGGL(S::k_thief_keys, dim3(gw), dim3(256), 0, s, P);
-      size_t tb = tmp_bytes;
-      hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, P.tk_nb, P.tk_nb2, P.tk_w, P.tk_w2, W, 0, 64, s);
-      hipLaunchKernelGGL(S::k_gather_a, dim3(gw), dim3(256), 0, s, P);
-      tb = tmp_bytes;
-      hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, P.tk_a2, P.tk_a, P.tk_w2, P.th_order, W, 0, 64, s);
-      hipLaunchKernelGGL(S::k_runs, dim3(1), dim3(64), 0, s, P);
-      hipLaunchKernelGGL(S::k_best_thief, dim3((unsigned)((T * 64 + 255) / 256)), dim3(256), 0, s, P, P.bin_ptr + NK - 1);
-    });
-  } else {
-    chk(hipMemsetAsync(P.bin_ptr, 0, NK * 4, s));
-    chk(hipMemsetAsync(P.n_runs, 0, 4, s));  // no thief runs are read without tasks
-  }
-  if (!rc) rc = timed_launch(e, 6, [&] {
-    hipLaunchKernelGGL(S::k_balance, dim3(1), dim3(64), S::balance_lds_bytes(W), s, P);
-  });
-  long long ns = 0;
-  if (!rc) {
-    chk(hipMemcpyAsync(&ns, d_ns, 8, hipMemcpyDeviceToHost, s));
-    chk(hipStreamSynchronize(s));
-  }
-  if (!rc && st == hipSuccess) {
-    *n_steals = ns;
-    auto d2h = [&](void* dst, const void* src, size_t bytes) {
-      if (dst && bytes) chk(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
-    };
-    d2h(level_out, P.level, T);
-    d2h(st_task, P.st_task, ns * 4); d2h(st_victim, P.st_victim, ns * 4); d2h(st_thief, P.st_thief, ns * 4);
-    d2h(st_level, P.st_level, ns * 4); d2h(st_cost, P.st_cost, ns * 8); d2h(st_occ_victim, P.st_occ_victim, ns * 8);
-    d2h(st_occ_thief, P.st_occ_thief, ns * 8);
-    d2h(inflight_occ, d_ifo, W * 8); d2h(inflight_tasks, P.inflight_tasks, W * 4);
-    d2h(idle_out, d_idle_o, W); d2h(sat_out, d_sat_o, W);
-    chk(hipStreamSynchronize(s));
-  }
-  hipFree(arena);
-  if (rc) return rc;
-  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_balance: ") + hipGetErrorString(st));
-  return 0;
+  int64_t n = 0;
+  if (int rc = dgp_steal_load(e, W, nthreads, occ, nproc, wnbytes, idle, sat, total_occ, total_nthreads, bandwidth, T,
+                              victim, duration, fast, dep_ptr, dep_idx, n_data, d_nbytes, d_get_nbytes, h_ptr, h_idx,
+                              &n))
+    return rc;
+  if (int rc = dgp_steal_thief_rows(e, 0, n)) return rc;
+  return dgp_steal_run(e, level_out, st_task, st_victim, st_thief, st_level, st_cost, st_occ_victim, st_occ_thief,
+                       n_steals, inflight_occ, inflight_tasks, idle_out, sat_out);
 }
 
 }  // extern "C"

@@ -31,6 +31,24 @@ KERNEL_NAMES = ("frontier_release", "candidate_commbytes", "replay", "update_gra
                 "steal_thief_argmin", "steal_balance", "unused")
 
 
+def conflict_depth(g: dict, out: dict, first: int = 0) -> tuple[int, int]:
+    """(depth, touches): the longest chain of ordered stimuli in a replay's placement log
+    (``dgp_conflict_depth``), from stimulus ``first`` on; the critical path of the latency
+    bound bench.py reports."""
+    lib = _lib.load()
+    dp = np.ascontiguousarray(g["dep_ptr"], np.int64)
+    di = np.ascontiguousarray(g["dep_idx"], np.int32)
+    wa = np.ascontiguousarray(g["wanted"], np.uint8)
+    pt = np.ascontiguousarray(out["pl_task"], np.int32)
+    pw = np.ascontiguousarray(out["pl_worker"], np.int32)
+    d, t = C.c_int64(0), C.c_int64(0)
+    rc = lib.dgp_conflict_depth(int(g["n_tasks"]), _ptr(dp), _ptr(di), _ptr(wa), len(pt), _ptr(pt), _ptr(pw),
+                                int(first), C.byref(d), C.byref(t))
+    if rc != 0:
+        raise _lib.DgpError(f"dgp_conflict_depth: status {rc}")
+    return int(d.value), int(t.value)
+
+
 class PlacementEngine:
     """One device engine bound to HIP device ``device``."""
 
@@ -214,7 +232,7 @@ class PlacementEngine:
         return {name: (float(ms[i]), int(n[i])) for i, name in enumerate(KERNEL_NAMES)}
 
     # ------------------------------------------------------------ WorkStealing
-    def steal_balance(self, p: dict) -> dict:
+    def steal_balance(self, p: dict, group=None) -> dict:
         """steal_time_ratio for every processing task + one WorkStealing.balance()
         (distributed/stealing.py:241-277, :401-503) on the device.
 
@@ -223,7 +241,34 @@ class PlacementEngine:
         data_nbytes, data_get_nbytes and who_has as data_holder (one worker or -1) or
         holder_ptr / holder_idx (CSR). Returns levels, the ordered steal requests and the
         per-worker in-flight / idle / saturated state after the call.
+
+        ``group``: a torch.distributed group of more than one rank (one engine per GPU,
+        every rank passing the same ``p``): each rank computes its slice of the per-task
+        thief rows and one all-gather gives every rank all of them (shard.py); the
+        ordered walk then runs on every rank and gives the same result.
         """
+        inputs, outputs, out, n, keep = self._steal_args(p)
+        world = 1
+        if group is not None:
+            import torch.distributed as dist
+
+            world = dist.get_world_size(group)
+        if world == 1:
+            self._check(self.lib.dgp_steal_balance(self.h, *inputs, *outputs), "dgp_steal_balance")
+        else:
+            self._steal_sharded(inputs, outputs, group)
+        return self._steal_result(out, n)
+
+    @staticmethod
+    def _steal_result(out, n):
+        k = int(n.value)
+        for key in ("st_task", "st_victim", "st_thief", "st_level", "st_cost", "st_occ_victim", "st_occ_thief"):
+            out[key] = out[key][:k]
+        return out
+
+    def _steal_args(self, p: dict):
+        """ctypes arguments of dgp_steal_load / dgp_steal_balance (inputs) and of
+        dgp_steal_run (outputs), the output arrays, the steal count and the kept buffers."""
         W = len(p["nthreads"])
         T = len(p["victim"])
         if "holder_ptr" in p:
@@ -247,17 +292,40 @@ class PlacementEngine:
                    sat_after=np.zeros(W, np.uint8))
         n = C.c_int64(0)
         nd = len(p["data_nbytes"])
-        self._check(self.lib.dgp_steal_balance(
-            self.h, W, a(p["nthreads"], np.int32), a(p["occ"], np.float64), a(p["nproc"], np.int32),
-            a(p["wnbytes"], np.int64), a(p["idle"], np.uint8), a(p["sat"], np.uint8), float(p["total_occ"]),
-            int(p["total_nthreads"]), int(p["bandwidth"]), T, a(p["victim"], np.int32), a(p["duration"], np.float64),
-            a(p["fast"], np.uint8), a(p["dep_ptr"], np.int64), a(p["dep_idx"], np.int32), nd,
-            a(p["data_nbytes"], np.int64), a(p["data_get_nbytes"], np.int64), a(hptr, np.int64), a(hidx, np.int32),
-            *[_ptr(out[k]) for k in ("level", "st_task", "st_victim", "st_thief", "st_level", "st_cost",
-                                     "st_occ_victim", "st_occ_thief")],
-            C.byref(n), *[_ptr(out[k]) for k in ("inflight_occ", "inflight_tasks", "idle_after", "sat_after")]),
-            "dgp_steal_balance")
-        k = int(n.value)
-        for key in ("st_task", "st_victim", "st_thief", "st_level", "st_cost", "st_occ_victim", "st_occ_thief"):
-            out[key] = out[key][:k]
-        return out
+        inputs = (W, a(p["nthreads"], np.int32), a(p["occ"], np.float64), a(p["nproc"], np.int32),
+                  a(p["wnbytes"], np.int64), a(p["idle"], np.uint8), a(p["sat"], np.uint8), float(p["total_occ"]),
+                  int(p["total_nthreads"]), int(p["bandwidth"]), T, a(p["victim"], np.int32),
+                  a(p["duration"], np.float64), a(p["fast"], np.uint8), a(p["dep_ptr"], np.int64),
+                  a(p["dep_idx"], np.int32), nd, a(p["data_nbytes"], np.int64), a(p["data_get_nbytes"], np.int64),
+                  a(hptr, np.int64), a(hidx, np.int32))
+        outputs = ([_ptr(out[k]) for k in ("level", "st_task", "st_victim", "st_thief", "st_level", "st_cost",
+                                           "st_occ_victim", "st_occ_thief")] + [C.byref(n)]
+                   + [_ptr(out[k]) for k in ("inflight_occ", "inflight_tasks", "idle_after", "sat_after")])
+        return inputs, outputs, out, n, keep
+
+    def _steal_sharded(self, inputs, outputs, group):
+        """dgp_steal_load -> this rank's thief rows -> all-gather of the rows (RCCL) ->
+        dgp_steal_run (shard.py)."""
+        import torch
+        import torch.distributed as dist
+
+        from .shard import chunk_rows, gather_rows, shard_range
+
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        ns = C.c_int64(0)
+        self._check(self.lib.dgp_steal_load(self.h, *inputs, C.byref(ns)), "dgp_steal_load")
+        n = int(ns.value)
+        lo, hi = shard_range(n, rank, world)
+        self._check(self.lib.dgp_steal_thief_rows(self.h, lo, hi), "dgp_steal_thief_rows")
+        rb = int(self.lib.dgp_steal_row_bytes())
+        dev = torch.device("cuda", torch.cuda.current_device())
+        local = torch.zeros(max(chunk_rows(n, world), 0) * rb, dtype=torch.uint8, device=dev)
+        if hi > lo:
+            self._check(self.lib.dgp_steal_pack_rows(self.h, lo, hi, C.c_void_p(local.data_ptr())),
+                        "dgp_steal_pack_rows")
+        full = gather_rows(local, n, rb, group)
+        torch.cuda.synchronize()  # the all-gather ran on torch's stream, the unpack runs on the engine's
+        if n:
+            self._check(self.lib.dgp_steal_unpack_rows(self.h, 0, n, C.c_void_p(full.data_ptr())),
+                        "dgp_steal_unpack_rows")
+        self._check(self.lib.dgp_steal_run(self.h, *outputs), "dgp_steal_run")

@@ -111,6 +111,25 @@ def random_dag(n_tasks: int, n_workers: int, *, seed: int = 0, fanin: int = 4,
         nbytes=nbytes, start=np.zeros(n), stop=stop, nthreads=nth))
 
 
+def star(n_leaves: int, n_workers: int) -> dict:
+    """One root and ``n_leaves`` non-rootish leaves that depend on it: the root's completion
+    places every leaf on the root's worker (its only candidate, scheduler.py:8550-8593),
+    and the next round completes them one after another, each touching that one worker.
+    The slope of replay time over ``n_leaves`` is the engine's link latency within a round,
+    the constant of bench.py's latency bound (C3's unpack phase has the same shape)."""
+    n = int(n_leaves) + 1
+    dep_ptr = np.zeros(n + 1, np.int64)
+    dep_ptr[2:] = np.arange(1, n)
+    prefix_id = np.minimum(np.arange(n), 1).astype(np.int32)
+    return _finish(dict(
+        name=f"star_{n_leaves}x{n_workers}", dep_ptr=dep_ptr, dep_idx=np.zeros(n - 1, np.int32),
+        prio=np.arange(n, dtype=np.int64), prefix_id=prefix_id, group_id=prefix_id.copy(),
+        prefix_names=["hub", "leaf"], group_names=[f"hub-{TOKEN}", f"leaf-{TOKEN}"],
+        group_prefix=np.arange(2), prefix_default_dur=np.full(2, -1.0),
+        rootish_override=np.zeros(n, np.int8), nbytes=np.full(n, 1000, np.int64), start=np.zeros(n),
+        stop=np.full(n, 0.01), nthreads=np.ones(n_workers)))
+
+
 def shuffle_graph(n_partitions: int, n_workers: int, *, seed: int = 2) -> dict:
     """Config C3: the P2P-shuffle graph shape of ``distributed/shuffle/_shuffle.py:276-306``:
     P inputs -> P ``shuffle-transfer`` -> one ``shuffle-barrier`` (fan-in P) -> P

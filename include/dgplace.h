@@ -151,6 +151,13 @@ int dgp_set_timing(dgp_engine* e, int enabled);
  * [4] record-log length, [5] record-log walker position, [6..13] commit-kernel phase
  * cycles (s_memtime): setup, local steps, global stimuli, finish, walker, longest step. */
 int dgp_stats(dgp_engine* e, int64_t* out, int32_t n);
+/* Measurement helper (host only, no engine): the longest chain of ordered stimuli of a
+ * replay's placement log (stimulus r completes pl_task[r]; stimuli touching one worker are
+ * ordered), from stimulus `first` on. bench.py's latency bound = depth x the measured
+ * link latency. No reference counterpart (the reference runs one stimulus at a time). */
+int dgp_conflict_depth(int64_t n_tasks, const int64_t* dep_ptr, const int32_t* dep_idx, const uint8_t* wanted,
+                       int64_t n_pl, const int32_t* pl_task, const int32_t* pl_worker, int64_t first,
+                       int64_t* depth, int64_t* n_touch);
 
 /* WorkStealing: the cost level of every processing task (steal_time_ratio,
  * stealing.py:241-277; -1 = not stealable) and one balance() (:401-503) over a
@@ -175,6 +182,30 @@ int dgp_steal_balance(dgp_engine* e, int32_t n_workers, const int32_t* nthreads,
                       int8_t* levels, int32_t* st_task, int32_t* st_victim, int32_t* st_thief, int32_t* st_level,
                       double* st_cost, double* st_occ_victim, double* st_occ_thief, int64_t* n_steals,
                       double* inflight_occupancy, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* saturated_out);
+
+/* dgp_steal_balance in phases, for a balance() sharded over ranks (one engine per GPU):
+ *   dgp_steal_load       the inputs of dgp_steal_balance; levels, bins and the initial
+ *                        thief order; *n_stealable = tasks in a bin (stealing.py:220-239)
+ *   dgp_steal_thief_rows the per-task precompute of _get_thief (stealing.py:532-542:
+ *                        argmin of worker_objective over the initial thieves, comm costs,
+ *                        dependency holders) for stealable positions [lo, hi)
+ *   dgp_steal_pack_rows / dgp_steal_unpack_rows  positions [lo, hi) to / from a device
+ *                        buffer of dgp_steal_row_bytes() each (the all-gathered record)
+ *   dgp_steal_run        the ordered walk of balance() (:401-503) and the outputs of
+ *                        dgp_steal_balance. Every position must hold its row first. */
+int dgp_steal_load(dgp_engine* e, int32_t n_workers, const int32_t* nthreads, const double* occupancy,
+                   const int32_t* nprocessing, const int64_t* ws_nbytes, const uint8_t* idle, const uint8_t* saturated,
+                   double total_occupancy, int64_t total_nthreads, int64_t bandwidth, int64_t n_tasks,
+                   const int32_t* victim, const double* duration, const uint8_t* fast, const int64_t* dep_ptr,
+                   const int32_t* dep_idx, int64_t n_data, const int64_t* data_nbytes, const int64_t* data_get_nbytes,
+                   const int64_t* holder_ptr, const int32_t* holder_idx, int64_t* n_stealable);
+int dgp_steal_thief_rows(dgp_engine* e, int64_t lo, int64_t hi);
+int64_t dgp_steal_row_bytes(void);
+int dgp_steal_pack_rows(dgp_engine* e, int64_t lo, int64_t hi, void* device_dst);
+int dgp_steal_unpack_rows(dgp_engine* e, int64_t lo, int64_t hi, const void* device_src);
+int dgp_steal_run(dgp_engine* e, int8_t* levels, int32_t* st_task, int32_t* st_victim, int32_t* st_thief,
+                  int32_t* st_level, double* st_cost, double* st_occ_victim, double* st_occ_thief, int64_t* n_steals,
+                  double* inflight_occupancy, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* saturated_out);
 
 #ifdef __cplusplus
 }
