@@ -54,6 +54,8 @@ def reduce_max(x: float, dist, device: str = "cuda") -> float:
         return x
     import torch
 
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -244,6 +246,7 @@ def main():
     ap.add_argument("--c5-map", type=int, default=8_750_000)
     ap.add_argument("--c5-workers", type=int, default=16_384)
     ap.add_argument("--c5-cpu-map", type=int, default=200_000, help="map tasks of the C5 CPU-baseline sample")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--no-latency", action="store_true", help="skip the link-latency chain and the latency bound")
     args = ap.parse_args()
 
@@ -255,8 +258,11 @@ def main():
         import torch
         import torch.distributed as dist
 
+        # one GPU per rank; --dist-backend gloo rehearses the protocol with ranks sharing
+        # the GPUs there are (RCCL needs a GPU of its own per rank)
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
 
     from distributed_amd import graphs
     from distributed_amd.engine import PlacementEngine
