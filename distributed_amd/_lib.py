@@ -25,6 +25,7 @@ SIGNATURES = {
     "dgp_set_workers": (C.c_int, [_P, C.c_int32, _P]),
     "dgp_set_graph": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P]),
     "dgp_set_task_results": (C.c_int, [_P, _P, _P, _P]),
+    "dgp_set_restrictions": (C.c_int, [_P, _P, _P, _P]),
     "dgp_reset": (C.c_int, [_P]),
     "dgp_update_graph": (C.c_int, [_P]),
     "dgp_run_rounds": (C.c_int, [_P, C.c_int64, _P]),

@@ -42,6 +42,7 @@ constexpr int CTA = 1024;      // threads of the commit / dispatch workgroup
 constexpr int FL_MAX = 256;    // frontier tasks one global stimulus stages in LDS per chunk
 
 enum : uint8_t { S_RELEASED = 0, S_WAITING, S_PROCESSING, S_QUEUED, S_NO_WORKER, S_MEMORY };
+enum : uint8_t { RF_RESTRICTED = 1, RF_LOOSE = 2 };
 enum : uint8_t { TF_WANTED = 1, TF_ROOTISH = 2 };
 enum : uint8_t { WF_IDLE = 1, WF_SAT = 2, WF_ITC = 4 };
 enum : uint8_t { EV_GLOBAL = 1 };
@@ -131,6 +132,11 @@ struct Dev {
   unsigned long long* ready_key;
   unsigned long long* release_key;
   // candidate pool of newly ready tasks
+  // worker restrictions (null: none): valid_workers(ts) resolved to worker indices
+  // (scheduler.py:3043-3107), CSR ascending; restr_flags RF_RESTRICTED / RF_LOOSE
+  const int64_t* restr_ptr;
+  const int32_t* restr_idx;
+  const uint8_t* restr_flags;
   int64_t* cand_off;
   int32_t* cand_n;
   int32_t* pool_w;
@@ -295,6 +301,10 @@ __device__ __forceinline__ int64_t get_nbytes(const Dev& D, int t) {  // TaskSta
 }
 __device__ __forceinline__ bool holds(const Dev& D, int d, int w) {
   return (D.holders[(size_t)d * D.WB + (w >> 6)] >> (w & 63)) & 1ull;
+}
+// restricted and placed by decide_worker_non_rootish (a `_rootish` override wins, :2937)
+__device__ __forceinline__ bool restricted_nonrootish(const Dev& D, int x) {
+  return D.restr_flags && (D.restr_flags[x] & RF_RESTRICTED) && !(D.tflags[x] & TF_ROOTISH);
 }
 __device__ __forceinline__ void set_error(const Dev& D, int code, int task) {
   if (atomicCAS(&D.ctl->error, 0, code) == 0) D.ctl->err_task = task;
@@ -1331,7 +1341,7 @@ struct CoopShared {
   int32_t pool[32];
   int64_t pool_n;
 };
-enum : int { OP_NONE = 0, OP_ARGMIN_POOL, OP_FASTPATH, OP_KTH };
+enum : int { OP_NONE = 0, OP_ARGMIN_POOL, OP_FASTPATH, OP_KTH, OP_RESTRICTED };
 
 // eager application of a sub-step (global stimuli): what the walker would do with its record
 __device__ void apply_now(const Dev& D, int32_t kind, int t, int w, int p, int64_t dnet, const double* dur) {
@@ -1420,6 +1430,7 @@ __device__ int dispatch_prepare(const Dev& D, int x, CoopShared& S, int64_t* sta
     place_eager(D, x, D.t_idx[1], ROUTE_ROOTISH_Q, -1, stage_next, dur);
     return OP_NONE;
   }
+  if (restricted_nonrootish(D, x)) return OP_RESTRICTED;  // decide_worker with valid_workers
   if (D.dep_ptr[x + 1] > D.dep_ptr[x]) {  // decide_worker over the candidates
     int n = D.cand_n[x];
     int64_t off = D.cand_off[x];
@@ -1485,6 +1496,69 @@ __device__ __attribute__((noinline)) void dispatch_collective(const Dev& D, Coop
         D.g_lastw[gi] = D.g_relwait[gi] > 1 ? w : -1;
         D.g_left[gi] -= 1;
         place_eager(D, x, w, ROUTE_ROOTISH_NOQ, b.comm, stage_next, dur);
+      }
+    }
+  } else if (op == OP_RESTRICTED) {
+    // decide_worker (:8550-8593) with valid = valid_workers(ts) (:3043-3107; every worker
+    // runs here): candidates = who_has of the dependencies & valid; if none, valid; if
+    // that is empty too, the loose retry without restrictions (:8584-8586) or None ->
+    // no-worker (:2761-2782). The argmin of worker_objective decides (a single candidate
+    // is its own argmin).
+    const int64_t r0 = D.restr_ptr[x], r1 = D.restr_ptr[x + 1];
+    const int64_t d0 = D.dep_ptr[x], d1 = D.dep_ptr[x + 1];
+    auto held = [&](int w) {
+      for (int64_t k = d0; k < d1; k++)
+        if (holds(D, D.dep_idx[k], w)) return true;
+      return false;
+    };
+    int64_t tot = 0;
+    for (int64_t i0 = r0; i0 < r1; i0 += blockDim.x) {
+      const int64_t i = i0 + threadIdx.x;
+      int64_t t1;
+      block_excl_scan(i < r1 && held(D.restr_idx[i]) ? 1 : 0, &t1);
+      tot += t1;
+    }
+    // 0: valid & holders, 1: valid, 2: holders (loose), 3: every worker (loose), 4: none
+    int mode = tot > 0 ? 0 : (r1 > r0 ? 1 : 4);
+    if (mode == 4 && (D.restr_flags[x] & RF_LOOSE)) {
+      int64_t nh = 0;
+      for (int w0 = 0; w0 < D.W; w0 += blockDim.x) {
+        const int w = w0 + threadIdx.x;
+        int64_t t1;
+        block_excl_scan(w < D.W && held(w) ? 1 : 0, &t1);
+        nh += t1;
+      }
+      mode = nh > 0 ? 2 : 3;
+    }
+    Obj best{INFINITY, INT64_MAX, INT32_MAX};
+    int64_t bcomm = 0;
+    bool have = false;
+    auto consider = [&](int w) {
+      const int64_t cm = comm_bytes(D, x, w);
+      const Obj o = objective(D, w, cm, dur);
+      if (!have || obj_less(o, best)) {
+        best = o;
+        bcomm = cm;
+        have = true;
+      }
+    };
+    if (mode <= 1) {
+      for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
+        const int w = D.restr_idx[i];
+        if (mode == 1 || held(w)) consider(w);
+      }
+    } else if (mode <= 3) {
+      for (int w = threadIdx.x; w < D.W; w += blockDim.x)
+        if (mode == 3 || held(w)) consider(w);
+    }
+    ArgBest b = block_argmin(best, bcomm, have);
+    if (threadIdx.x == 0) {
+      if (b.o.w == INT32_MAX) {
+        D.state[x] = S_NO_WORKER;
+        atomicAdd((unsigned long long*)&D.g_relwait[D.group[x]], (unsigned long long)-1ll);
+        c->n_unrunnable++;
+      } else {
+        place_eager(D, x, b.o.w, ROUTE_NONROOTISH, b.comm, stage_next, dur);
       }
     }
   } else {  // fast path over an ordered pool
@@ -1828,7 +1902,7 @@ __device__ void candidate_body(const Dev& D, int64_t wave, int64_t nwaves) {
   for (int64_t i = wave; i < nF; i += nwaves) {
     int x = D.frontier[i];
     int64_t d0 = D.dep_ptr[x], d1 = D.dep_ptr[x + 1];
-    if (d1 == d0 || (D.tflags[x] & TF_ROOTISH)) {
+    if (d1 == d0 || (D.tflags[x] & TF_ROOTISH) || restricted_nonrootish(D, x)) {
       if (lane == 0) D.cand_n[x] = 0;
       continue;
     }
@@ -1940,7 +2014,7 @@ __device__ void events_body(const Dev& D, int64_t gtid, int64_t gthreads) {
       nf++;
       if (D.tflags[x] & TF_ROOTISH) {
         fl |= EV_GLOBAL | (D.sat_inf ? 0 : EV_MAYQUEUE);
-      } else if (D.dep_ptr[x + 1] == D.dep_ptr[x]) {
+      } else if (D.dep_ptr[x + 1] == D.dep_ptr[x] || restricted_nonrootish(D, x)) {
         fl |= EV_GLOBAL;
       } else {
         int cn = D.cand_n[x];

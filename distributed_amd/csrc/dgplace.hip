@@ -82,6 +82,8 @@ struct dgp_engine {
   std::vector<int> evkind;
   size_t evused = 0;
   StealCtx steal;
+  std::vector<uint8_t> tflags_h;           // task flags as set_graph computed them
+  std::vector<int8_t> rootish_override_h;  // TaskState._rootish per task (-1: None)
 };
 
 namespace {
@@ -261,14 +263,15 @@ int walk(dgp_engine* e) {
 
 // run the stimuli appended since the last launch: the stream engine, or one round of the
 // round-kernel engine when the graph has more prefixes than the stream descriptors carry
+// or worker restrictions
 int run_service_stimuli(dgp_engine* e) {
   namespace V = dgp::svc;
   hipStream_t s = e->stream;
-  if (e->D.P <= dgp::st::PD) {
+  if (e->D.P <= dgp::st::PD && !e->D.restr_flags) {
     stream_source(e, true);
     if (int rc = launch_stream(e, -1, 0)) return rc;
   } else {
-    // more prefixes than the stream descriptors carry: the accepted batch is one round of
+    // more prefixes than the stream descriptors carry, or restrictions: the accepted batch is one round of
     // the round-kernel engine (completions in message order)
     const dgp::Dev* DP = e->d_dev;
     const dgp::Dev* DPC = e->d_dev + 1;
@@ -608,8 +611,58 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
   HIPCHK(e, up(D.g_size, gsize.data(), n_groups * 8));
   e->prefix_defaults.assign(prefix_default_duration, prefix_default_duration + n_prefixes);
   e->group_sizes = gsize;
+  e->tflags_h = tflags;
+  e->rootish_override_h.assign(rootish_override, rootish_override + N);
+  D.restr_ptr = nullptr;  // no restrictions until dgp_set_restrictions
+  D.restr_idx = nullptr;
+  D.restr_flags = nullptr;
   e->have_graph = true;
   e->err.clear();
+  return dgp_reset(e);
+}
+
+int dgp_set_restrictions(dgp_engine* e, const int64_t* restr_ptr, const int32_t* restr_idx, const uint8_t* flags) {
+  if (!e || !e->have_graph) return fail(e, DGP_E_STATE, "graph first");
+  if (e->mode != 0 || e->stream_used) return fail(e, DGP_E_STATE, "restrictions go with the graph, before any stimulus");
+  HIPCHK(e, hipSetDevice(e->device));
+  dgp::Dev& D = e->D;
+  const int64_t N = D.N;
+  std::vector<uint8_t> tf = e->tflags_h;
+  if (flags) {
+    if (!restr_ptr || restr_ptr[0] != 0) return fail(e, DGP_E_ARG, "dgp_set_restrictions: restr_ptr");
+    for (int64_t t = 0; t < N; t++) {
+      if (restr_ptr[t + 1] < restr_ptr[t]) return fail(e, DGP_E_ARG, "dgp_set_restrictions: restr_ptr not monotone");
+      if (flags[t] & ~(dgp::RF_RESTRICTED | dgp::RF_LOOSE)) return fail(e, DGP_E_ARG, "dgp_set_restrictions: flags");
+      if (!(flags[t] & dgp::RF_RESTRICTED) && restr_ptr[t + 1] != restr_ptr[t])
+        return fail(e, DGP_E_ARG, "dgp_set_restrictions: valid workers on an unrestricted task");
+      for (int64_t k = restr_ptr[t]; k < restr_ptr[t + 1]; k++) {
+        if (restr_idx[k] < 0 || restr_idx[k] >= D.W) return fail(e, DGP_E_ARG, "dgp_set_restrictions: worker index");
+        if (k > restr_ptr[t] && restr_idx[k] <= restr_idx[k - 1])
+          return fail(e, DGP_E_ARG, "dgp_set_restrictions: valid workers must ascend");
+      }
+      // is_rootish (:2929-2947): a restricted task is not root-ish unless _rootish says so
+      if ((flags[t] & dgp::RF_RESTRICTED) && e->rootish_override_h[t] < 0) tf[t] &= (uint8_t)~dgp::TF_ROOTISH;
+    }
+  }
+  // the arrays live with the graph (freed by the next dgp_set_graph)
+  int64_t* rp = nullptr;
+  int32_t* ri = nullptr;
+  uint8_t* rf = nullptr;
+  if (flags) {
+    const int64_t K = restr_ptr[N];
+    int rc = 0;
+    rc |= dalloc(e, &rp, N + 1, e->graph_allocs);
+    rc |= dalloc(e, &ri, std::max<int64_t>(K, 1), e->graph_allocs);
+    rc |= dalloc(e, &rf, N, e->graph_allocs);
+    if (rc) return DGP_E_HIP;
+    HIPCHK(e, hipMemcpy(rp, restr_ptr, (N + 1) * 8, hipMemcpyHostToDevice));
+    if (K) HIPCHK(e, hipMemcpy(ri, restr_idx, K * 4, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(rf, flags, N, hipMemcpyHostToDevice));
+  }
+  HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), tf.data(), N, hipMemcpyHostToDevice));
+  D.restr_ptr = rp;
+  D.restr_idx = ri;
+  D.restr_flags = rf;
   return dgp_reset(e);
 }
 
@@ -715,11 +768,12 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
   if (int rc = check_device_error(e, &c)) return rc;
   const long long r0 = c.rounds_nonempty;
   const dgp::Dev& D = e->D;
-  if (D.P <= dgp::st::PD) {
+  if (D.P <= dgp::st::PD && !D.restr_flags) {
     // the stream engine: the whole replay in one persistent workgroup (dgp_stream.h)
     if (int rc = launch_stream(e, max_rounds, e->snap_rounds > 0 ? 1 : 0)) return rc;
   } else {
-    // more task prefixes than the stream descriptors carry: the round-kernel engine
+    // more task prefixes than the stream descriptors carry, or worker restrictions (decided
+    // by the global dispatch, dgp_device.h OP_RESTRICTED): the round-kernel engine
     if (e->stream_used) return fail(e, DGP_E_STATE, "engine already advanced by the stream replay");
     const int lds_workers = D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
     const size_t lds = (((size_t)D.W * sizeof(int) + 15) & ~(size_t)15) +

@@ -116,6 +116,10 @@ class PlacementEngine:
             len(arrs["prefix_default_dur"]), _ptr(arrs["prefix_default_dur"]), _ptr(arrs["group_id"]),
             len(g["group_prefix"]), _ptr(arrs["wanted"]), _ptr(arrs["rootish_override"])), "dgp_set_graph")
         self.n_tasks = n
+        if g.get("restr_flags") is not None:  # worker restrictions, resolved (graphs.restrict)
+            r = [np.ascontiguousarray(g["restr_ptr"], np.int64), np.ascontiguousarray(g["restr_idx"], np.int32),
+                 np.ascontiguousarray(g["restr_flags"], np.uint8)]
+            self._check(self.lib.dgp_set_restrictions(self.h, *[_ptr(a) for a in r]), "dgp_set_restrictions")
         if not results:  # service mode: the task-finished messages carry nbytes / startstops
             return
         res = [np.ascontiguousarray(g["nbytes"], np.int64), np.ascontiguousarray(g["start"], np.float64),

@@ -63,13 +63,19 @@ def _compute_interval(startstops):
     return math.nan, math.nan
 
 
-def graph_from_tasks(tss, nthreads):
+def graph_from_tasks(tss, nthreads, valid_workers=None, worker_index=None):
     """TaskState objects -> the engine's graph arrays (the layout of distributed_amd/graphs.py).
 
     Tasks are indexed in ascending ``TaskState.priority`` (so ``prio`` is their rank: unique
     and topological for dask.order priorities); dependencies must be among ``tss``.
     Prefixes / groups get ids in first-seen order; ``prefix_default_dur`` is each
-    ``TaskPrefix.duration_average`` now (default-task-durations or -1)."""
+    ``TaskPrefix.duration_average`` now (default-task-durations or -1).
+
+    Restrictions: with ``valid_workers`` (``SchedulerState.valid_workers``, scheduler.py
+    :3043-3107, which resolves worker / host / resource restrictions) and ``worker_index``
+    (address -> engine worker index), every task with restrictions gets its valid set as
+    ascending indices (``restr_ptr`` / ``restr_idx``) and ``restr_flags`` (1: restricted,
+    2: loose_restrictions)."""
     tss = sorted(tss, key=lambda ts: ts.priority)
     index = {ts.key: i for i, ts in enumerate(tss)}
     n = len(tss)
@@ -115,6 +121,20 @@ def graph_from_tasks(tss, nthreads):
         start=np.zeros(n),
         stop=np.zeros(n),
     )
+    if valid_workers is not None:
+        flags = np.zeros(n, np.uint8)
+        vrows = [[] for _ in range(n)]
+        for i, ts in enumerate(tss):
+            if ts.worker_restrictions or ts.host_restrictions or ts.resource_restrictions:
+                vw = valid_workers(ts)
+                if vw is None:  # restrictions that exclude nobody
+                    continue
+                flags[i] = 1 | (2 if ts.loose_restrictions else 0)
+                vrows[i] = sorted(worker_index[ws.address] for ws in vw)
+        if flags.any():
+            rp = np.zeros(n + 1, np.int64)
+            rp[1:] = np.cumsum([len(r) for r in vrows])
+            g.update(restr_ptr=rp, restr_idx=np.array([w for r in vrows for w in r], np.int32), restr_flags=flags)
     return g, [ts.key for ts in tss]
 
 
@@ -219,6 +239,12 @@ class GPUPlacementExtension(SchedulerPlugin):
         if queued or (not math.isinf(sched.WORKER_SATURATION) and sched.is_rootish(ts)):
             self.stats["device_queued"] += 1
             return None
+        # restrictions that no worker satisfies, not loose: the engine left it in
+        # no-worker (decide_worker :8584-8586 -> _transition_waiting_no_worker :2761-2782)
+        if ((ts.worker_restrictions or ts.host_restrictions or ts.resource_restrictions)
+                and not ts.loose_restrictions and sched.valid_workers(ts) == set()):
+            self.stats["device_no_worker"] += 1
+            return None
         self.fallback(f"the engine did not place {ts.key!r}")
         return _REF
 
@@ -279,7 +305,8 @@ class GPUPlacementExtension(SchedulerPlugin):
                 raise NotImplementedError("a second graph on a running engine")
             self.workers = list(s.workers)
             self.worker_index = {a: i for i, a in enumerate(self.workers)}
-            g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers])
+            g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers], s.valid_workers,
+                                        self.worker_index)
             self.keys = keys_
             self.task_index = {k: i for i, k in enumerate(keys_)}
             if self.engine_factory is not None:

@@ -111,6 +111,29 @@ def random_dag(n_tasks: int, n_workers: int, *, seed: int = 0, fanin: int = 4,
         nbytes=nbytes, start=np.zeros(n), stop=stop, nthreads=nth))
 
 
+def restrict(g: dict, frac: float, *, seed: int = 0, max_valid: int = 8, empty_frac: float = 0.1,
+             loose_frac: float = 0.5) -> dict:
+    """Worker restrictions on a fraction of the tasks (``TaskState.worker_restrictions`` /
+    ``loose_restrictions``, scheduler.py:1338-1354, :4908-4922), already resolved to the
+    valid worker indices of ``valid_workers`` (:3043-3107) as CSR ``restr_ptr`` /
+    ``restr_idx`` (ascending). ``restr_flags`` bit 0: the task is restricted; bit 1: loose.
+    A restricted task whose valid set is empty (its restriction names no worker of the
+    cluster) goes to ``no-worker`` unless loose (decide_worker :8584-8586)."""
+    rng = np.random.default_rng(seed)
+    n, W = g["n_tasks"], len(g["nthreads"])
+    flags = np.zeros(n, np.uint8)
+    rows = [[] for _ in range(n)]
+    for t in np.flatnonzero(rng.random(n) < frac):
+        flags[t] = 1 | (2 if rng.random() < loose_frac else 0)
+        if rng.random() >= empty_frac:
+            k = int(rng.integers(1, max_valid + 1))
+            rows[t] = sorted(set(rng.integers(0, W, k).tolist()))
+    ptr, idx = _csr_from_rows(rows)
+    g = dict(g)
+    g.update(restr_ptr=ptr, restr_idx=idx, restr_flags=flags)
+    return g
+
+
 def star(n_leaves: int, n_workers: int) -> dict:
     """One root and ``n_leaves`` non-rootish leaves that depend on it: the root's completion
     places every leaf on the root's worker (its only candidate, scheduler.py:8550-8593),

@@ -89,6 +89,15 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
 
 /* Per-task completion reports used by dgp_run_rounds: output nbytes and the compute
  * startstops interval of the task-finished message. */
+/* Worker restrictions of the graph's tasks (TaskState.worker_restrictions / host / resource
+ * restrictions and loose_restrictions, scheduler.py:1338-1354, :4908-4922), each resolved
+ * by the caller to its valid_workers set (:3043-3107) as ascending worker indices
+ * (CSR restr_ptr[N+1] / restr_idx). flags[t] bit 0: restricted (a non-empty restriction
+ * set; its valid set may be empty -> no-worker unless loose), bit 1: loose_restrictions.
+ * Placement follows decide_worker_non_rootish / decide_worker (:2247-2311, :8550-8593):
+ * restricted tasks are not root-ish (:2939) unless _rootish overrides. Null flags clear
+ * them. After dgp_set_graph, before any stimulus; resets the engine. */
+int dgp_set_restrictions(dgp_engine* e, const int64_t* restr_ptr, const int32_t* restr_idx, const uint8_t* flags);
 int dgp_set_task_results(dgp_engine* e, const int64_t* nbytes, const double* start, const double* stop);
 
 /* Reset all dynamic state (tasks released, workers empty, placement log cleared). */

@@ -26,7 +26,7 @@ class OrcGraph(C.Structure):
         ("wanted", _P), ("rootish_override", _P), ("nbytes", _P), ("start", _P), ("stop", _P),
         ("nthreads", _P), ("group_prefix", _P), ("prefix_default_dur", _P),
         ("bandwidth", C.c_int64), ("default_data_size", C.c_int64), ("unknown_duration", C.c_double),
-        ("saturation", C.c_double),
+        ("saturation", C.c_double), ("restr_ptr", _P), ("restr_idx", _P), ("restr_flags", _P),
     ]
 
 
@@ -89,6 +89,10 @@ def replay(g: dict, config: dict, *, snapshots: bool = True, max_rounds: int | N
         bandwidth=int(config["bandwidth"]), default_data_size=int(config["default_data_size"]),
         unknown_duration=float(config["unknown_duration"]), saturation=sat,
     )
+    if g.get("restr_flags") is not None:  # worker restrictions, resolved to indices (graphs.restrict)
+        gs.restr_ptr = _ptr(arr(g["restr_ptr"], np.int64))
+        gs.restr_idx = _ptr(arr(g["restr_idx"], np.int32))
+        gs.restr_flags = _ptr(arr(g["restr_flags"], np.uint8))
     R = int(max_rounds or (n + 2))
     out = dict(
         pl_task=np.zeros(n, np.int32), pl_worker=np.zeros(n, np.int32), pl_comm=np.zeros(n, np.int64),
@@ -130,6 +134,9 @@ def load_fixture(path: str):
     meta = json.loads(str(z["meta"]))
     g = {k: z[k] for k in ("dep_ptr", "dep_idx", "prio", "prefix_id", "group_id", "wanted", "rootish_override",
                            "nbytes", "start", "stop", "nthreads", "group_prefix", "prefix_default_dur")}
+    for k in ("restr_ptr", "restr_idx", "restr_flags"):
+        if k in z.files:
+            g[k] = z[k]
     g["n_tasks"] = len(g["prio"])
     g["prefix_names"] = meta["prefix_names"]
     g["group_names"] = meta["group_names"]

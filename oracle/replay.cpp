@@ -28,6 +28,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <iterator>
 #include <utility>
 #include <vector>
 
@@ -51,6 +52,13 @@ struct orc_graph {
   int64_t default_data_size;
   double unknown_duration;
   double saturation;  // +inf allowed
+  // worker restrictions (optional, all null = none): valid_workers(ts) (:3043-3107)
+  // resolved to worker indices (CSR, ascending), and flags bit 0 = the task has
+  // restrictions (a non-empty restriction set; its valid set may still be empty),
+  // bit 1 = loose_restrictions (:8584-8586)
+  const int64_t* restr_ptr;
+  const int32_t* restr_idx;
+  const uint8_t* restr_flags;
 };
 
 struct orc_result {
@@ -279,9 +287,13 @@ struct Replay {
   }
   double total_occupancy() const { return calc_occupancy(prefix_global, net_occ_global); }  // :1877
 
-  bool is_rootish(int32_t t) const {  // :2929-2947 (no restrictions in this replay)
+  bool restricted(int32_t t) const { return g.restr_flags && (g.restr_flags[t] & 1); }
+  bool loose(int32_t t) const { return g.restr_flags && (g.restr_flags[t] & 2); }
+
+  bool is_rootish(int32_t t) const {  // :2929-2947
     int8_t ov = g.rootish_override[t];
     if (ov >= 0) return ov != 0;
+    if (restricted(t)) return false;  // :2939-2940
     return groups[g.group_id[t]].rootish_static != 0;
   }
 
@@ -383,16 +395,28 @@ struct Replay {
     return w;
   }
 
-  int32_t decide_worker(int32_t t) {  // module-level decide_worker :8550-8593 (no restrictions)
+  // module-level decide_worker :8550-8593; valid = valid_workers(ts) or null (None)
+  int32_t decide_worker(int32_t t, const std::vector<int32_t>* valid = nullptr) {
     std::vector<int32_t> cand;
     for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++)
       for (int32_t w : who_has[g.dep_idx[k]]) cand.push_back(w);
     std::sort(cand.begin(), cand.end());
     cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
-    if (cand.empty()) {  // candidates = all_workers.copy()
-      cand.resize(W);
-      for (int32_t w = 0; w < W; w++) cand[w] = w;
+    if (!valid) {
+      if (cand.empty()) {  // candidates = all_workers.copy()
+        cand.resize(W);
+        for (int32_t w = 0; w < W; w++) cand[w] = w;
+      }
+    } else {  // candidates &= valid_workers; else valid_workers; else the loose retry
+      std::vector<int32_t> both;
+      std::set_intersection(cand.begin(), cand.end(), valid->begin(), valid->end(), std::back_inserter(both));
+      cand.swap(both);
+      if (cand.empty()) {
+        cand = *valid;
+        if (cand.empty() && loose(t)) return decide_worker(t, nullptr);
+      }
     }
+    if (cand.empty()) return -1;
     if (cand.size() == 1) return cand[0];
     Obj best = worker_objective(t, cand[0]);
     for (size_t i = 1; i < cand.size(); i++) {
@@ -404,6 +428,11 @@ struct Replay {
 
   int32_t decide_worker_non_rootish(int32_t t, Route& route) {  // :2247-2311
     if (W == 0) return -1;
+    if (restricted(t)) {  // valid_workers(ts) is not None (every worker runs here)
+      route = R_NONROOTISH;
+      std::vector<int32_t> valid(g.restr_idx + g.restr_ptr[t], g.restr_idx + g.restr_ptr[t + 1]);
+      return decide_worker(t, &valid);
+    }
     if (g.dep_ptr[t + 1] > g.dep_ptr[t]) {
       route = R_NONROOTISH;
       return decide_worker(t);

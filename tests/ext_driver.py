@@ -105,6 +105,15 @@ def check_upload(g_up, keys_up, g_fx, fkeys):
     assert np.array_equal(g_up["wanted"], g_fx["wanted"][perm])
     assert np.array_equal(g_up["rootish_override"], g_fx["rootish_override"][perm])
     assert np.array_equal(g_up["nthreads"], g_fx["nthreads"])
+    # restrictions: TaskState.worker_restrictions -> valid_workers -> indices (f1)
+    if "restr_flags" in g_fx:
+        assert np.array_equal(g_up["restr_flags"], g_fx["restr_flags"][perm])
+        for i, f in enumerate(perm):
+            up = g_up["restr_idx"][g_up["restr_ptr"][i]:g_up["restr_ptr"][i + 1]].tolist()
+            fx = g_fx["restr_idx"][g_fx["restr_ptr"][f]:g_fx["restr_ptr"][f + 1]].tolist()
+            assert up == fx, (keys_up[i], up, fx)
+    else:
+        assert "restr_flags" not in g_up
     # priority rank: ascending fixture priority
     assert np.array_equal(np.argsort(g_fx["prio"][perm], kind="stable"), np.arange(len(perm)))
     # the engine's prefix table = TaskPrefix.duration_average at upload
@@ -170,7 +179,8 @@ def run(name, diverge=False):
     if not diverge:
         assert ext.stats["device_decisions"] == n, (ext.stats, n)
     return dict(fixture=name, placements=n, messages=n_msgs, device_decisions=ext.stats["device_decisions"],
-                device_queued=ext.stats["device_queued"], active=ext.active, reason=ext.reason)
+                device_queued=ext.stats["device_queued"], device_no_worker=ext.stats["device_no_worker"],
+                active=ext.active, reason=ext.reason)
 
 
 if __name__ == "__main__":

@@ -189,6 +189,15 @@ def build_state(g, cfg):
     for t, ts in enumerate(tss):
         for d in idx[ptr[t]:ptr[t + 1]]:
             ts.add_dependency(tss[int(d)])
+    if g.get("restr_flags") is not None:  # graphs.restrict: resolved valid workers
+        rp, ri, rf = g["restr_ptr"], g["restr_idx"], g["restr_flags"]
+        for t, ts in enumerate(tss):
+            if rf[t] & 1:
+                valid = {f"tcp://w{int(w):05d}:1" for w in ri[rp[t]:rp[t + 1]]}
+                # a name no worker has: valid_workers drops it (:3059), so an otherwise
+                # empty set is still a restriction, with no valid worker
+                ts.worker_restrictions = valid | {"tcp://gone:1"}
+                ts.loose_restrictions = bool(rf[t] & 2)
     for t, ts in enumerate(tss):
         if g["wanted"][t]:
             ts.who_wants = {cs}
@@ -291,6 +300,8 @@ def save(name, g, cfg, rec, rounds, nplaced, states, secs):
         round_sat=np.stack([r[4] for r in rounds]), round_itc=np.stack([r[5] for r in rounds]),
         round_nqueued=np.array([r[6] for r in rounds], np.int32), final_state=states,
     )
+    if g.get("restr_flags") is not None:
+        out.update(restr_ptr=g["restr_ptr"], restr_idx=g["restr_idx"], restr_flags=g["restr_flags"])
     if "stim" in rec:  # placements made by each stimulus (update_graph, then every completion)
         out["stim_nplaced"] = np.array(rec["stim"], np.int32)
     sat = cfg["saturation"]
@@ -380,6 +391,17 @@ def fixtures():
         "sat_factor_0.1": (lambda: root_only(10, [2, 1]), 0.1),
         "sat_factor_inf": (lambda: root_only(10, [2, 1]), inf),
         "occupancy_comm": (occupancy_comm_graph, 1.1),
+        # worker restrictions / loose restrictions / no-worker (scheduler.py:3043-3107,
+        # :8550-8593, :2761-2782): restricted roots leave the root-ish path (:2939)
+        "restr_sat1.1": (lambda: graphs.restrict(graphs.random_dag(5000, 64, seed=51), 0.2, seed=52,
+                                                 loose_frac=1.0), 1.1),
+        "restr_satinf": (lambda: graphs.restrict(graphs.random_dag(4000, 48, seed=53, nthreads="random"), 0.25,
+                                                 seed=54, max_valid=20, empty_frac=0.0, loose_frac=0.3), inf),
+        "restr_nodep_w24": (lambda: graphs.restrict(no_dep_groups(24, 30, 12, 200, seed=55), 0.3, seed=56,
+                                                    loose_frac=1.0), 1.1),
+        # empty valid sets that are not loose: no-worker, and everything downstream waits
+        "restr_noworker_sat1.1": (lambda: graphs.restrict(graphs.random_dag(5000, 64, seed=57), 0.2, seed=58),
+                                  1.1),
     }
 
 

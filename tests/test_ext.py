@@ -22,7 +22,8 @@ pytestmark = pytest.mark.skipif(not HAVE_REF, reason="needs the reference + pyth
 FIXTURES = ["c1_sat1.1.npz", "c1_satinf.npz", "c2var_sat1.1.npz", "c2var_sat2.5.npz", "c2var_satinf.npz",
             "c2p12_sat1.1.npz", "c3mini_sat1.1.npz", "nodep_w19_sat1.1.npz", "nodep_w20_satinf.npz",
             "nodep_w24_sat1.1.npz", "occupancy_comm.npz", "sat_factor_0.1.npz", "sat_factor_2.5.npz",
-            "sat_factor_inf.npz"]
+            "sat_factor_inf.npz", "restr_sat1.1.npz", "restr_satinf.npz", "restr_nodep_w24.npz",
+            "restr_noworker_sat1.1.npz"]
 
 
 def drive(names, *flags):
@@ -40,6 +41,7 @@ def test_extension_places_every_task_from_the_engine():
     assert [r["fixture"] for r in res] == FIXTURES
     for r in res:
         assert r["active"] and r["device_decisions"] == r["placements"], r
+    assert next(r for r in res if r["fixture"] == "restr_noworker_sat1.1.npz")["device_no_worker"] > 0
 
 
 def test_extension_hands_back_on_divergence():
