@@ -41,10 +41,10 @@ SIGNATURES = {
     "dgp_stats": (C.c_int, [_P, _P, C.c_int32]),
     "dgp_conflict_depth": (C.c_int, [C.c_int64, _P, _P, _P, C.c_int64, _P, _P, C.c_int64, _P, _P]),
     "dgp_steal_balance": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_int64, C.c_int64,
-                                    C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, _P, _P,
+                                    C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, _P, _P, _P, _P, _P,
                                     _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dgp_steal_load": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_int64, C.c_int64,
-                                 C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, _P, _P, _P]),
+                                 C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dgp_steal_thief_rows": (C.c_int, [_P, C.c_int64, C.c_int64]),
     "dgp_steal_row_bytes": (C.c_int64, []),
     "dgp_steal_pack_rows": (C.c_int, [_P, C.c_int64, C.c_int64, _P]),
@@ -52,7 +52,7 @@ SIGNATURES = {
     "dgp_steal_run": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lib = None
 
 

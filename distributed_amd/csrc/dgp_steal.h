@@ -45,6 +45,11 @@ struct Prob {
   const int64_t* d_get_nbytes;  // get_nbytes() (worker_objective, steal_time_ratio)
   const int64_t* h_ptr;         // who_has (CSR)
   const int32_t* h_idx;
+  // restrictions of the processing tasks (null: none): valid_workers (scheduler.py
+  // :3043-3107) as worker indices (CSR); r_flags bit 0 restricted, bit 1 loose
+  const int64_t* r_ptr;
+  const int32_t* r_idx;
+  const uint8_t* r_flags;
   // work
   int32_t* key;       // [T] level * W + victim, or N_LEVELS * W when not stealable
   int32_t* order;     // [T] task ids sorted by key (stable)
@@ -178,6 +183,28 @@ __device__ __forceinline__ Obj wave_argmin(const Prob& P, int64_t t, TH th) {
   return best;
 }
 
+// argmin over the valid workers of restricted task t that pass th (one wave)
+template <class TH>
+__device__ __forceinline__ Obj wave_argmin_valid(const Prob& P, int64_t t, TH th) {
+  const int lane = threadIdx.x & 63;
+  Obj best{INFINITY, INT64_MAX, INT32_MAX};
+  for (int64_t k = P.r_ptr[t] + lane; k < P.r_ptr[t + 1]; k += 64) {
+    const int w = P.r_idx[k];
+    if (!th(w)) continue;
+    const Obj o = objective(P, t, w);
+    if (obj_less(o, best)) best = o;
+  }
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) {
+    const Obj o = obj_shfl_xor(best, m);
+    if (obj_less(o, best)) best = o;
+  }
+  return best;
+}
+__device__ __forceinline__ bool restricted(const Prob& P, int64_t t) { return P.r_flags && (P.r_flags[t] & 1); }
+__device__ __forceinline__ bool loose(const Prob& P, int64_t t) { return P.r_flags && (P.r_flags[t] & 2); }
+constexpr int32_t NO_THIEF = -2;  // restricted, not loose, no valid initial thief: never stolen
+
 // one wave per stealable task (sorted position i in [lo, hi)): thief over the initial
 // thief set. Rows are independent: ranks can each take a slice (dgp_steal_thief_rows)
 // and exchange them (dgp_steal_pack_rows / dgp_steal_unpack_rows).
@@ -185,9 +212,14 @@ __global__ void k_best_thief(Prob P, int64_t lo, int64_t hi) {
   const int64_t i = lo + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (i >= hi) return;
   const int64_t t = P.order[i];
-  const Obj b = wave_argmin(P, t, [&](int w) { return P.idle[w] != 0; });
+  // _get_thief (stealing.py:532-542): potential_thieves & valid_workers when restricted;
+  // with no valid thief the loose retry over every thief, or no thief at all
+  const bool rs = restricted(P, t);
+  Obj b{INFINITY, INT64_MAX, INT32_MAX};
+  if (rs) b = wave_argmin_valid(P, t, [&](int w) { return P.idle[w] != 0; });
+  if (!rs || (b.w >= P.W && loose(P, t))) b = wave_argmin(P, t, [&](int w) { return P.idle[w] != 0; });
   if ((threadIdx.x & 63) == 0) {
-    P.s_best[i] = b.w < P.W ? b.w : -1;
+    P.s_best[i] = b.w < P.W ? b.w : (rs ? NO_THIEF : -1);
     P.s_cct[i] = b.w < P.W ? comm_cost(P, t, b.w) : 0.0;
     P.s_ccv[i] = comm_cost(P, t, P.victim[t]);
     P.s_dur[i] = P.duration[t];
@@ -539,7 +571,19 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           double cct = __shfl(cq, j);
           const double ccv = __shfl(vq, j);
           const double compute = __shfl(dq, j);
-          if (th < 0 || !thief[th]) th = thief_from_runs(c0 + j, t, &cct);  // the precomputed thief left
+          if (th == NO_THIEF) continue;  // _get_thief -> None (:452-454), for good: thieves only leave
+          if (th < 0 || !thief[th]) {  // the precomputed thief left
+            th = -1;
+            if (restricted(P, t)) {
+              const Obj b = wave_argmin_valid(P, t, [&](int w) { return thief[w] != 0; });
+              if (b.w < W) {
+                th = b.w;
+                cct = comm_cost(P, t, th);
+              }
+            }
+            if (th < 0 && (!restricted(P, t) || loose(P, t))) th = thief_from_runs(c0 + j, t, &cct);
+            if (th < 0) continue;
+          }
           const double occ_thief = combined(th);
           const double occ_victim = combined(v);
           if (occ_thief + cct + compute <= occ_victim - (ccv + compute) / 2) {  // :462-465

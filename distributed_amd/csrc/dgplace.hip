@@ -1049,7 +1049,7 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
                    int64_t total_nthreads, int64_t bandwidth, int64_t T, const int32_t* victim, const double* duration,
                    const uint8_t* fast, const int64_t* dep_ptr, const int32_t* dep_idx, int64_t n_data,
                    const int64_t* d_nbytes, const int64_t* d_get_nbytes, const int64_t* h_ptr, const int32_t* h_idx,
-                   int64_t* n_stealable) {
+                   const int64_t* r_ptr, const int32_t* r_idx, const uint8_t* r_flags, int64_t* n_stealable) {
   namespace S = dgp::steal;
   if (!e) return DGP_E_ARG;
   e->steal.loaded = false;
@@ -1077,6 +1077,14 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
   for (int64_t d = 0; d < n_data; d++)
     if (h_ptr[d + 1] < h_ptr[d]) return fail(e, DGP_E_ARG, "dgp_steal_load: h_ptr not monotone");
   if (H && !h_idx) return fail(e, DGP_E_ARG, "dgp_steal_load: h_idx");
+  const int64_t RK = r_flags ? (r_ptr ? r_ptr[T] : -1) : 0;
+  if (r_flags) {
+    if (!r_ptr || r_ptr[0] != 0 || RK < 0 || (RK && !r_idx)) return fail(e, DGP_E_ARG, "dgp_steal_load: restrictions");
+    for (int64_t t = 0; t < T; t++)
+      if (r_ptr[t + 1] < r_ptr[t] || (r_flags[t] & ~3)) return fail(e, DGP_E_ARG, "dgp_steal_load: restrictions");
+    for (int64_t k = 0; k < RK; k++)
+      if (r_idx[k] < 0 || r_idx[k] >= W) return fail(e, DGP_E_ARG, "dgp_steal_load: restricted worker out of range");
+  }
   for (int64_t k = 0; k < H; k++)
     if (h_idx[k] < 0 || h_idx[k] >= W) return fail(e, DGP_E_ARG, "dgp_steal_load: holder out of range");
   HIPCHK(e, hipSetDevice(e->device));
@@ -1109,6 +1117,12 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
   add(&d_nthreads, W); add(&d_occ, W); add(&d_nproc, W); add(&d_wnb, W); add(&d_idle, W); add(&d_sat, W);
   add(&d_victim, T); add(&d_dur, T); add(&d_fast, T); add(&d_dep_ptr, T + 1); add(&d_dep_idx, E);
   add(&d_dnb, n_data); add(&d_dgnb, n_data); add(&d_h_ptr, n_data + 1); add(&d_h_idx, H);
+  int64_t* d_r_ptr = nullptr;
+  int32_t* d_r_idx = nullptr;
+  uint8_t* d_r_flags = nullptr;
+  if (r_flags) {
+    add(&d_r_ptr, T + 1); add(&d_r_idx, RK); add(&d_r_flags, T);
+  }
   add(&P.key, T); add(&P.order, T); add(&C.keys_sorted, T); add(&C.d_vals, T); add(&P.bin_cnt, NK); add(&P.bin_ptr, NK);
   add(&P.s_best, T); add(&P.s_cct, T); add(&P.s_ccv, T); add(&P.s_dur, T);
   add(&P.s_cget, T); add(&P.s_craw, T); add(&P.s_nh, T); add(&P.s_hw, T * S::MAXH); add(&P.s_hg, T * S::MAXH);
@@ -1145,8 +1159,14 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
   chk(h2d(d_dep_ptr, dep_ptr, (T + 1) * 8)); chk(h2d(d_dep_idx, dep_idx, E * 4));
   chk(h2d(d_dnb, d_nbytes, n_data * 8)); chk(h2d(d_dgnb, d_get_nbytes, n_data * 8));
   chk(h2d(d_h_ptr, h_ptr, (n_data + 1) * 8)); chk(h2d(d_h_idx, h_idx, H * 4));
+  if (r_flags) {
+    chk(h2d(d_r_ptr, r_ptr, (T + 1) * 8)); chk(h2d(d_r_idx, r_idx, RK * 4)); chk(h2d(d_r_flags, r_flags, T));
+  }
   chk(hipMemsetAsync(P.bin_cnt, 0, NK * 4, s));
   if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_load: upload: ") + hipGetErrorString(st));
+  P.r_ptr = d_r_ptr;
+  P.r_idx = d_r_idx;
+  P.r_flags = d_r_flags;
   P.W = W; P.nthreads = d_nthreads; P.occ = d_occ; P.nproc = d_nproc; P.wnbytes = d_wnb; P.idle = d_idle;
   P.sat = d_sat; P.total_occ = total_occ; P.total_nthreads = total_nthreads; P.bw = bandwidth; P.T = T;
   P.victim = d_victim; P.duration = d_dur; P.fast = d_fast; P.dep_ptr = d_dep_ptr; P.dep_idx = d_dep_idx;
@@ -1285,14 +1305,15 @@ int dgp_steal_balance(dgp_engine* e, int32_t W, const int32_t* nthreads, const d
                       int64_t total_nthreads, int64_t bandwidth, int64_t T, const int32_t* victim,
                       const double* duration, const uint8_t* fast, const int64_t* dep_ptr, const int32_t* dep_idx,
                       int64_t n_data, const int64_t* d_nbytes, const int64_t* d_get_nbytes, const int64_t* h_ptr,
-                      const int32_t* h_idx, int8_t* level_out, int32_t* st_task, int32_t* st_victim,
+                      const int32_t* h_idx, const int64_t* r_ptr, const int32_t* r_idx, const uint8_t* r_flags,
+                      int8_t* level_out, int32_t* st_task, int32_t* st_victim,
                       int32_t* st_thief, int32_t* st_level, double* st_cost, double* st_occ_victim,
                       double* st_occ_thief, int64_t* n_steals, double* inflight_occ, int32_t* inflight_tasks,
                       uint8_t* idle_out, uint8_t* sat_out) {
   int64_t n = 0;
   if (int rc = dgp_steal_load(e, W, nthreads, occ, nproc, wnbytes, idle, sat, total_occ, total_nthreads, bandwidth, T,
                               victim, duration, fast, dep_ptr, dep_idx, n_data, d_nbytes, d_get_nbytes, h_ptr, h_idx,
-                              &n))
+                              r_ptr, r_idx, r_flags, &n))
     return rc;
   if (int rc = dgp_steal_thief_rows(e, 0, n)) return rc;
   return dgp_steal_run(e, level_out, st_task, st_victim, st_thief, st_level, st_cost, st_occ_victim, st_occ_thief,

@@ -301,7 +301,9 @@ class PlacementEngine:
                   int(p["total_nthreads"]), int(p["bandwidth"]), T, a(p["victim"], np.int32),
                   a(p["duration"], np.float64), a(p["fast"], np.uint8), a(p["dep_ptr"], np.int64),
                   a(p["dep_idx"], np.int32), nd, a(p["data_nbytes"], np.int64), a(p["data_get_nbytes"], np.int64),
-                  a(hptr, np.int64), a(hidx, np.int32))
+                  a(hptr, np.int64), a(hidx, np.int32),
+                  *((a(p["restr_ptr"], np.int64), a(p["restr_idx"], np.int32), a(p["restr_flags"], np.uint8))
+                    if p.get("restr_flags") is not None else (None, None, None)))
         outputs = ([_ptr(out[k]) for k in ("level", "st_task", "st_victim", "st_thief", "st_level", "st_cost",
                                            "st_occ_victim", "st_occ_thief")] + [C.byref(n)]
                    + [_ptr(out[k]) for k in ("inflight_occ", "inflight_tasks", "idle_after", "sat_after")])

@@ -307,7 +307,8 @@ def check_graph(g: dict) -> None:
 
 
 def steal_problem(n_workers: int, n_tasks: int, *, nthreads: int = 2, hot_frac: float = 0.1, seed: int = 1,
-                  n_prefixes: int = 8, zipf_a: float = 1.5, replicas: int = 1, occ_quantum: float = 0.0) -> dict:
+                  n_prefixes: int = 8, zipf_a: float = 1.5, replicas: int = 1, occ_quantum: float = 0.0,
+                  restrict: float = 0.0) -> dict:
     """A WorkStealing.balance() input in the shape of BASELINE.json's C4:
     D = T/4 memory-resident dependencies (``int(lognormal(16, 3))`` bytes) on uniform
     workers; T processing tasks with 1-2 of them (5 % dependency-free -> level 0) in
@@ -365,7 +366,18 @@ def steal_problem(n_workers: int, n_tasks: int, *, nthreads: int = 2, hot_frac: 
     idle = ((nproc < nth) | (occ < nth * avg / 2)).astype(np.uint8)
     pend = np.where(nproc > nth, occ * (nproc - nth) / np.maximum(nproc * nth, 1), 0.0)
     sat = ((idle == 0) & (nproc > nth) & (pend > 0.4) & (pend > 1.9 * avg)).astype(np.uint8)
-    return dict(nthreads=nth, occ=occ, nproc=nproc, wnbytes=wnbytes, idle=idle, sat=sat, total_occ=total_occ,
-                total_nthreads=tn, bandwidth=bw, victim=victim, duration=duration, fast=np.zeros(T, np.uint8),
-                dep_ptr=dep_ptr, dep_idx=dep_idx, data_nbytes=nbytes, data_get_nbytes=nbytes, data_holder=holder,
-                **({"holder_ptr": hptr, "holder_idx": hidx} if replicas > 1 else {}))
+    p = dict(nthreads=nth, occ=occ, nproc=nproc, wnbytes=wnbytes, idle=idle, sat=sat, total_occ=total_occ,
+             total_nthreads=tn, bandwidth=bw, victim=victim, duration=duration, fast=np.zeros(T, np.uint8),
+             dep_ptr=dep_ptr, dep_idx=dep_idx, data_nbytes=nbytes, data_get_nbytes=nbytes, data_holder=holder,
+             **({"holder_ptr": hptr, "holder_idx": hidx} if replicas > 1 else {}))
+    if restrict > 0:  # worker restrictions on a fraction of the tasks (valid sets of 1-16, some empty / loose)
+        rr = np.random.default_rng(seed + 7)
+        flags = np.zeros(T, np.uint8)
+        rows = [[] for _ in range(T)]
+        for t in np.flatnonzero(rr.random(T) < restrict):
+            flags[t] = 1 | (2 if rr.random() < 0.5 else 0)
+            if rr.random() >= 0.1:
+                rows[t] = sorted(set(rr.integers(0, W, int(rr.integers(1, 17))).tolist()))
+        rp, ri = _csr_from_rows(rows)
+        p.update(restr_ptr=rp, restr_idx=ri, restr_flags=flags)
+    return p

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 2
+#define DGP_ABI_VERSION 3
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -180,7 +180,10 @@ int dgp_conflict_depth(int64_t n_tasks, const int64_t* dep_ptr, const int32_t* d
  * saturated in ascending worker id). Outputs: levels[T]; the ordered steal requests
  * (task, victim, thief, level, cost = compute + victim comm cost, victim / thief combined
  * occupancy as logged), capacity T; *n_steals; per-worker in-flight occupancy and task
- * deltas; idle / saturated membership after the call. Kernel-time ids 4 (levels + bins),
+ * deltas; idle / saturated membership after the call. Restrictions (nullable): each
+ * task's valid_workers as worker indices (CSR restr_ptr[T+1] / restr_idx) and flags (bit 0
+ * restricted, bit 1 loose): _get_thief (stealing.py:532-542) takes the valid thieves, the
+ * loose retry over all thieves, or skips the task. Kernel-time ids 4 (levels + bins),
  * 5 (thief argmin), 6 (balance walk). */
 int dgp_steal_balance(dgp_engine* e, int32_t n_workers, const int32_t* nthreads, const double* occupancy,
                       const int32_t* nprocessing, const int64_t* ws_nbytes, const uint8_t* idle,
@@ -188,6 +191,7 @@ int dgp_steal_balance(dgp_engine* e, int32_t n_workers, const int32_t* nthreads,
                       int64_t n_tasks, const int32_t* victim, const double* duration, const uint8_t* fast,
                       const int64_t* dep_ptr, const int32_t* dep_idx, int64_t n_data, const int64_t* data_nbytes,
                       const int64_t* data_get_nbytes, const int64_t* holder_ptr, const int32_t* holder_idx,
+                      const int64_t* restr_ptr, const int32_t* restr_idx, const uint8_t* restr_flags,
                       int8_t* levels, int32_t* st_task, int32_t* st_victim, int32_t* st_thief, int32_t* st_level,
                       double* st_cost, double* st_occ_victim, double* st_occ_thief, int64_t* n_steals,
                       double* inflight_occupancy, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* saturated_out);
@@ -207,7 +211,8 @@ int dgp_steal_load(dgp_engine* e, int32_t n_workers, const int32_t* nthreads, co
                    double total_occupancy, int64_t total_nthreads, int64_t bandwidth, int64_t n_tasks,
                    const int32_t* victim, const double* duration, const uint8_t* fast, const int64_t* dep_ptr,
                    const int32_t* dep_idx, int64_t n_data, const int64_t* data_nbytes, const int64_t* data_get_nbytes,
-                   const int64_t* holder_ptr, const int32_t* holder_idx, int64_t* n_stealable);
+                   const int64_t* holder_ptr, const int32_t* holder_idx, const int64_t* restr_ptr,
+                   const int32_t* restr_idx, const uint8_t* restr_flags, int64_t* n_stealable);
 int dgp_steal_thief_rows(dgp_engine* e, int64_t lo, int64_t hi);
 int64_t dgp_steal_row_bytes(void);
 int dgp_steal_pack_rows(dgp_engine* e, int64_t lo, int64_t hi, void* device_dst);

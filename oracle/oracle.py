@@ -188,6 +188,8 @@ def steal_balance(p: dict) -> dict:
             a(p["victim"], np.int32), a(p["duration"], np.float64), a(p["fast"], np.uint8), a(p["dep_ptr"], np.int64),
             a(p["dep_idx"], np.int32), a(p["data_nbytes"], np.int64), a(p["data_get_nbytes"], np.int64),
             a(hptr, np.int64), a(hidx, np.int32),
+            *((a(p["restr_ptr"], np.int64), a(p["restr_idx"], np.int32), a(p["restr_flags"], np.uint8))
+              if p.get("restr_flags") is not None else (None, None, None)),
             *[_ptr(out[k]) for k in ("level", "st_task", "st_victim", "st_thief", "st_level", "st_cost",
                                      "st_occ_victim", "st_occ_thief")],
             C.byref(n), *[_ptr(out[k]) for k in ("inflight_occ", "inflight_tasks", "idle_after", "sat_after")])
@@ -208,6 +210,9 @@ def load_steal_fixture(path: str):
     p = {k: z[k] for k in STEAL_INPUTS}
     for k in ("total_occ", "total_nthreads", "bandwidth"):
         p[k] = z[k][()]
+    for k in ("holder_ptr", "holder_idx", "restr_ptr", "restr_idx", "restr_flags"):
+        if k in z.files:
+            p[k] = z[k]
     exp = {k: z[k] for k in ("level", "st_task", "st_level", "st_cost", "st_victim", "st_occ_victim", "st_thief",
                              "st_occ_thief", "inflight_occ", "inflight_tasks", "idle_after", "sat_after")}
     return p, exp, meta

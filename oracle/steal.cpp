@@ -38,6 +38,11 @@ struct Problem {
   const int64_t* d_get_nbytes;  // dts.get_nbytes() (worker_objective, steal_time_ratio)
   const int64_t* h_ptr;         // who_has of each data task (CSR)
   const int32_t* h_idx;
+  // restrictions of the processing tasks (null: none): valid_workers (scheduler.py
+  // :3043-3107) as worker indices (CSR); flags bit 0 restricted, bit 1 loose
+  const int64_t* r_ptr;
+  const int32_t* r_idx;
+  const uint8_t* r_flags;
 };
 
 bool holds(const Problem& P, int d, int w) {
@@ -105,12 +110,14 @@ extern "C" int orc_steal_balance(
     const int32_t* dep_idx,
     // data (dependencies)
     const int64_t* d_nbytes, const int64_t* d_get_nbytes, const int64_t* h_ptr, const int32_t* h_idx,
+    // restrictions (nullable)
+    const int64_t* r_ptr, const int32_t* r_idx, const uint8_t* r_flags,
     // outputs
     int8_t* level_out, int32_t* st_task, int32_t* st_victim, int32_t* st_thief, int32_t* st_level, double* st_cost,
     double* st_occ_victim, double* st_occ_thief, int64_t* n_steals, double* inflight_occ, int32_t* inflight_tasks,
     uint8_t* idle_out, uint8_t* sat_out) {
   const Problem P{W, nthreads, occ, nproc, wnbytes, total_occ, total_nthreads, bandwidth, T, victim, duration,
-                  fast, dep_ptr, dep_idx, d_nbytes, d_get_nbytes, h_ptr, h_idx};
+                  fast, dep_ptr, dep_idx, d_nbytes, d_get_nbytes, h_ptr, h_idx, r_ptr, r_idx, r_flags};
   std::vector<uint8_t> idle(idle_in, idle_in + W), sat(sat_in, sat_in + W);
   std::vector<double> ifo(W, 0.0);
   std::vector<int32_t> ift(W, 0);
@@ -195,11 +202,21 @@ extern "C" int orc_steal_balance(
       for (int64_t t : bin) {  // :439
         if (!n_thieves) break;
         Obj best{0, 0, -1};  // _get_thief (:532-542): min objective over the thieves
-        for (int w = 0; w < W; w++) {
-          if (!thief[w]) continue;
-          const Obj o = objective(P, t, w);
-          if (best.w < 0 || o < best) best = o;
-        }
+        const bool rs = P.r_flags && (P.r_flags[t] & 1);
+        if (rs)  // potential_thieves & valid_workers
+          for (int64_t k = P.r_ptr[t]; k < P.r_ptr[t + 1]; k++) {
+            const int w = P.r_idx[k];
+            if (!thief[w]) continue;
+            const Obj o = objective(P, t, w);
+            if (best.w < 0 || o < best) best = o;
+          }
+        if (best.w < 0 && (!rs || (P.r_flags[t] & 2)))  // unrestricted, or loose with no valid thief
+          for (int w = 0; w < W; w++) {
+            if (!thief[w]) continue;
+            const Obj o = objective(P, t, w);
+            if (best.w < 0 || o < best) best = o;
+          }
+        if (best.w < 0) continue;  // _get_thief -> None: the task is skipped (:452-454)
         const int th = best.w;
         const double occ_thief = combined_occ(th);
         const double occ_victim = combined_occ(v);

@@ -84,3 +84,13 @@ def test_balance_full_c4(eng):
     out, ref = eng.steal_balance(p), oracle.steal_balance(p)
     assert len(ref["st_task"]) > 100_000
     assert_same(out, ref)
+
+
+@pytest.mark.parametrize("W,T,frac,seed", [(256, 20000, 0.3, 61), (4096, 80000, 0.2, 62), (1024, 40000, 0.8, 63)])
+def test_balance_restricted_matches_oracle(eng, W, T, frac, seed):
+    """_get_thief with valid_workers / loose restrictions (stealing.py:532-542) at scale;
+    the restricted reference fixtures (steal_restricted*.npz) run in the fixture test."""
+    p = graphs.steal_problem(W, T, seed=seed, restrict=frac)
+    out, ref = eng.steal_balance(p), oracle.steal_balance(p)
+    assert len(ref["st_task"]) > 0
+    assert_same(out, ref)
