@@ -42,17 +42,18 @@ SIGNATURES = {
     "dgp_conflict_depth": (C.c_int, [C.c_int64, _P, _P, _P, C.c_int64, _P, _P, C.c_int64, _P, _P]),
     "dgp_steal_balance": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_int64, C.c_int64,
                                     C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, _P, _P, _P, _P, _P,
-                                    _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+                                    _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dgp_steal_load": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_int64, C.c_int64,
-                                 C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P]),
+                                 C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, _P, _P, _P, _P, _P,
+                                 _P, _P, _P, _P]),
     "dgp_steal_thief_rows": (C.c_int, [_P, C.c_int64, C.c_int64]),
     "dgp_steal_row_bytes": (C.c_int64, []),
     "dgp_steal_pack_rows": (C.c_int, [_P, C.c_int64, C.c_int64, _P]),
     "dgp_steal_unpack_rows": (C.c_int, [_P, C.c_int64, C.c_int64, _P]),
-    "dgp_steal_run": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dgp_steal_run": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _lib = None
 
 

@@ -50,6 +50,13 @@ struct Prob {
   const int64_t* r_ptr;
   const int32_t* r_idx;
   const uint8_t* r_flags;
+  // the plugin's own state (null: fresh): levels of its stealable bins (key_stealable,
+  // stealing.py:220-239; -1 = not in a bin) and the in-flight accounts of steals not yet
+  // confirmed (in_flight_occupancy / in_flight_tasks, :191-213)
+  const int8_t* level_in;
+  const double* ifo_in;
+  const int32_t* ift_in;
+  uint8_t* checked;  // [W] out: check_idle_saturated ran on this victim (:498-500)
   // work
   int32_t* key;       // [T] level * W + victim, or N_LEVELS * W when not stealable
   int32_t* order;     // [T] task ids sorted by key (stable)
@@ -102,7 +109,9 @@ __global__ void k_steal_levels(Prob P) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= P.T) return;
   int lv;
-  if (P.fast[t]) {
+  if (P.level_in) {
+    lv = P.level_in[t] < N_LEVELS ? P.level_in[t] : -1;  // the bins as the plugin keeps them
+  } else if (P.fast[t]) {
     lv = -1;                                       // :252-253
   } else if (P.dep_ptr[t] == P.dep_ptr[t + 1]) {
     lv = 0;                                        // :255-256
@@ -366,8 +375,9 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   int nth_ = 0, nsat_ = 0;
   for (int w = lane; w < W; w += 64) {
     occ[w] = P.occ[w];
-    ifo[w] = 0.0;
-    ift[w] = 0;
+    ifo[w] = P.ifo_in ? P.ifo_in[w] : 0.0;
+    ift[w] = P.ift_in ? P.ift_in[w] : 0;
+    P.checked[w] = 0;
     idle[w] = P.idle[w];
     sat[w] = P.sat[w];
     thief[w] = P.idle[w];
@@ -629,6 +639,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
       if (lane == 0) {
         idle[v] = id;
         sat[v] = sa;
+        P.checked[v] = 1;
       }
       __syncthreads();
     }

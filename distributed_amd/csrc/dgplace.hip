@@ -1049,7 +1049,8 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
                    int64_t total_nthreads, int64_t bandwidth, int64_t T, const int32_t* victim, const double* duration,
                    const uint8_t* fast, const int64_t* dep_ptr, const int32_t* dep_idx, int64_t n_data,
                    const int64_t* d_nbytes, const int64_t* d_get_nbytes, const int64_t* h_ptr, const int32_t* h_idx,
-                   const int64_t* r_ptr, const int32_t* r_idx, const uint8_t* r_flags, int64_t* n_stealable) {
+                   const int64_t* r_ptr, const int32_t* r_idx, const uint8_t* r_flags, const int8_t* level_in,
+                   const double* ifo_in, const int32_t* ift_in, int64_t* n_stealable) {
   namespace S = dgp::steal;
   if (!e) return DGP_E_ARG;
   e->steal.loaded = false;
@@ -1078,6 +1079,9 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
     if (h_ptr[d + 1] < h_ptr[d]) return fail(e, DGP_E_ARG, "dgp_steal_load: h_ptr not monotone");
   if (H && !h_idx) return fail(e, DGP_E_ARG, "dgp_steal_load: h_idx");
   const int64_t RK = r_flags ? (r_ptr ? r_ptr[T] : -1) : 0;
+  if (level_in)
+    for (int64_t t = 0; t < T; t++)
+      if (level_in[t] < -1 || level_in[t] >= S::N_LEVELS) return fail(e, DGP_E_ARG, "dgp_steal_load: level_in");
   if (r_flags) {
     if (!r_ptr || r_ptr[0] != 0 || RK < 0 || (RK && !r_idx)) return fail(e, DGP_E_ARG, "dgp_steal_load: restrictions");
     for (int64_t t = 0; t < T; t++)
@@ -1123,6 +1127,13 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
   if (r_flags) {
     add(&d_r_ptr, T + 1); add(&d_r_idx, RK); add(&d_r_flags, T);
   }
+  int8_t* d_lv_in = nullptr;
+  double* d_ifo_in = nullptr;
+  int32_t* d_ift_in = nullptr;
+  if (level_in) add(&d_lv_in, T);
+  if (ifo_in) add(&d_ifo_in, W);
+  if (ift_in) add(&d_ift_in, W);
+  add(&P.checked, W);
   add(&P.key, T); add(&P.order, T); add(&C.keys_sorted, T); add(&C.d_vals, T); add(&P.bin_cnt, NK); add(&P.bin_ptr, NK);
   add(&P.s_best, T); add(&P.s_cct, T); add(&P.s_ccv, T); add(&P.s_dur, T);
   add(&P.s_cget, T); add(&P.s_craw, T); add(&P.s_nh, T); add(&P.s_hw, T * S::MAXH); add(&P.s_hg, T * S::MAXH);
@@ -1164,9 +1175,16 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
   }
   chk(hipMemsetAsync(P.bin_cnt, 0, NK * 4, s));
   if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_load: upload: ") + hipGetErrorString(st));
+  if (level_in) chk(h2d(d_lv_in, level_in, T));
+  if (ifo_in) chk(h2d(d_ifo_in, ifo_in, W * 8));
+  if (ift_in) chk(h2d(d_ift_in, ift_in, W * 4));
+  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_load: upload: ") + hipGetErrorString(st));
   P.r_ptr = d_r_ptr;
   P.r_idx = d_r_idx;
   P.r_flags = d_r_flags;
+  P.level_in = d_lv_in;
+  P.ifo_in = d_ifo_in;
+  P.ift_in = d_ift_in;
   P.W = W; P.nthreads = d_nthreads; P.occ = d_occ; P.nproc = d_nproc; P.wnbytes = d_wnb; P.idle = d_idle;
   P.sat = d_sat; P.total_occ = total_occ; P.total_nthreads = total_nthreads; P.bw = bandwidth; P.T = T;
   P.victim = d_victim; P.duration = d_dur; P.fast = d_fast; P.dep_ptr = d_dep_ptr; P.dep_idx = d_dep_idx;
@@ -1260,7 +1278,8 @@ int dgp_steal_unpack_rows(dgp_engine* e, int64_t lo, int64_t hi, const void* src
 
 int dgp_steal_run(dgp_engine* e, int8_t* level_out, int32_t* st_task, int32_t* st_victim, int32_t* st_thief,
                   int32_t* st_level, double* st_cost, double* st_occ_victim, double* st_occ_thief, int64_t* n_steals,
-                  double* inflight_occ, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* sat_out) {
+                  double* inflight_occ, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* sat_out,
+                  uint8_t* checked_out) {
   namespace S = dgp::steal;
   if (!e) return DGP_E_ARG;
   StealCtx& C = e->steal;
@@ -1293,7 +1312,7 @@ int dgp_steal_run(dgp_engine* e, int8_t* level_out, int32_t* st_task, int32_t* s
     d2h(st_level, P.st_level, ns * 4); d2h(st_cost, P.st_cost, ns * 8); d2h(st_occ_victim, P.st_occ_victim, ns * 8);
     d2h(st_occ_thief, P.st_occ_thief, ns * 8);
     d2h(inflight_occ, P.inflight_occ, W * 8); d2h(inflight_tasks, P.inflight_tasks, W * 4);
-    d2h(idle_out, P.idle_out, W); d2h(sat_out, P.sat_out, W);
+    d2h(idle_out, P.idle_out, W); d2h(sat_out, P.sat_out, W); d2h(checked_out, P.checked, W);
     chk(hipStreamSynchronize(s));
   }
   if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_run: ") + hipGetErrorString(st));
@@ -1306,18 +1325,19 @@ int dgp_steal_balance(dgp_engine* e, int32_t W, const int32_t* nthreads, const d
                       const double* duration, const uint8_t* fast, const int64_t* dep_ptr, const int32_t* dep_idx,
                       int64_t n_data, const int64_t* d_nbytes, const int64_t* d_get_nbytes, const int64_t* h_ptr,
                       const int32_t* h_idx, const int64_t* r_ptr, const int32_t* r_idx, const uint8_t* r_flags,
+                      const int8_t* level_in, const double* ifo_in, const int32_t* ift_in,
                       int8_t* level_out, int32_t* st_task, int32_t* st_victim,
                       int32_t* st_thief, int32_t* st_level, double* st_cost, double* st_occ_victim,
                       double* st_occ_thief, int64_t* n_steals, double* inflight_occ, int32_t* inflight_tasks,
-                      uint8_t* idle_out, uint8_t* sat_out) {
+                      uint8_t* idle_out, uint8_t* sat_out, uint8_t* checked_out) {
   int64_t n = 0;
   if (int rc = dgp_steal_load(e, W, nthreads, occ, nproc, wnbytes, idle, sat, total_occ, total_nthreads, bandwidth, T,
                               victim, duration, fast, dep_ptr, dep_idx, n_data, d_nbytes, d_get_nbytes, h_ptr, h_idx,
-                              r_ptr, r_idx, r_flags, &n))
+                              r_ptr, r_idx, r_flags, level_in, ifo_in, ift_in, &n))
     return rc;
   if (int rc = dgp_steal_thief_rows(e, 0, n)) return rc;
   return dgp_steal_run(e, level_out, st_task, st_victim, st_thief, st_level, st_cost, st_occ_victim, st_occ_thief,
-                       n_steals, inflight_occ, inflight_tasks, idle_out, sat_out);
+                       n_steals, inflight_occ, inflight_tasks, idle_out, sat_out, checked_out);
 }
 
 }  // extern "C"

@@ -293,7 +293,7 @@ class PlacementEngine:
                    st_thief=np.zeros(T, np.int32), st_level=np.zeros(T, np.int32), st_cost=np.zeros(T),
                    st_occ_victim=np.zeros(T), st_occ_thief=np.zeros(T), inflight_occ=np.zeros(W),
                    inflight_tasks=np.zeros(W, np.int32), idle_after=np.zeros(W, np.uint8),
-                   sat_after=np.zeros(W, np.uint8))
+                   sat_after=np.zeros(W, np.uint8), checked=np.zeros(W, np.uint8))
         n = C.c_int64(0)
         nd = len(p["data_nbytes"])
         inputs = (W, a(p["nthreads"], np.int32), a(p["occ"], np.float64), a(p["nproc"], np.int32),
@@ -303,10 +303,13 @@ class PlacementEngine:
                   a(p["dep_idx"], np.int32), nd, a(p["data_nbytes"], np.int64), a(p["data_get_nbytes"], np.int64),
                   a(hptr, np.int64), a(hidx, np.int32),
                   *((a(p["restr_ptr"], np.int64), a(p["restr_idx"], np.int32), a(p["restr_flags"], np.uint8))
-                    if p.get("restr_flags") is not None else (None, None, None)))
+                    if p.get("restr_flags") is not None else (None, None, None)),
+                  a(p["level_in"], np.int8) if p.get("level_in") is not None else None,
+                  a(p["inflight_occ_in"], np.float64) if p.get("inflight_occ_in") is not None else None,
+                  a(p["inflight_tasks_in"], np.int32) if p.get("inflight_tasks_in") is not None else None)
         outputs = ([_ptr(out[k]) for k in ("level", "st_task", "st_victim", "st_thief", "st_level", "st_cost",
                                            "st_occ_victim", "st_occ_thief")] + [C.byref(n)]
-                   + [_ptr(out[k]) for k in ("inflight_occ", "inflight_tasks", "idle_after", "sat_after")])
+                   + [_ptr(out[k]) for k in ("inflight_occ", "inflight_tasks", "idle_after", "sat_after", "checked")])
         return inputs, outputs, out, n, keep
 
     def _steal_sharded(self, inputs, outputs, group):

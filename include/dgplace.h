@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 3
+#define DGP_ABI_VERSION 4
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -183,7 +183,12 @@ int dgp_conflict_depth(int64_t n_tasks, const int64_t* dep_ptr, const int32_t* d
  * deltas; idle / saturated membership after the call. Restrictions (nullable): each
  * task's valid_workers as worker indices (CSR restr_ptr[T+1] / restr_idx) and flags (bit 0
  * restricted, bit 1 loose): _get_thief (stealing.py:532-542) takes the valid thieves, the
- * loose retry over all thieves, or skips the task. Kernel-time ids 4 (levels + bins),
+ * loose retry over all thieves, or skips the task. The plugin's own state (nullable):
+ * levels_in = the levels of its stealable bins (key_stealable; -1 = not in a bin; null:
+ * computed by steal_time_ratio), inflight_*_in = in_flight_occupancy / in_flight_tasks
+ * of unconfirmed steals (null: none); the in-flight outputs are then the new totals, and
+ * checked_out[w] = 1 for each victim check_idle_saturated ran on (:498-500).
+ * Kernel-time ids 4 (levels + bins),
  * 5 (thief argmin), 6 (balance walk). */
 int dgp_steal_balance(dgp_engine* e, int32_t n_workers, const int32_t* nthreads, const double* occupancy,
                       const int32_t* nprocessing, const int64_t* ws_nbytes, const uint8_t* idle,
@@ -192,9 +197,11 @@ int dgp_steal_balance(dgp_engine* e, int32_t n_workers, const int32_t* nthreads,
                       const int64_t* dep_ptr, const int32_t* dep_idx, int64_t n_data, const int64_t* data_nbytes,
                       const int64_t* data_get_nbytes, const int64_t* holder_ptr, const int32_t* holder_idx,
                       const int64_t* restr_ptr, const int32_t* restr_idx, const uint8_t* restr_flags,
+                      const int8_t* levels_in, const double* inflight_occupancy_in, const int32_t* inflight_tasks_in,
                       int8_t* levels, int32_t* st_task, int32_t* st_victim, int32_t* st_thief, int32_t* st_level,
                       double* st_cost, double* st_occ_victim, double* st_occ_thief, int64_t* n_steals,
-                      double* inflight_occupancy, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* saturated_out);
+                      double* inflight_occupancy, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* saturated_out,
+                      uint8_t* checked_out);
 
 /* dgp_steal_balance in phases, for a balance() sharded over ranks (one engine per GPU):
  *   dgp_steal_load       the inputs of dgp_steal_balance; levels, bins and the initial
@@ -212,14 +219,16 @@ int dgp_steal_load(dgp_engine* e, int32_t n_workers, const int32_t* nthreads, co
                    const int32_t* victim, const double* duration, const uint8_t* fast, const int64_t* dep_ptr,
                    const int32_t* dep_idx, int64_t n_data, const int64_t* data_nbytes, const int64_t* data_get_nbytes,
                    const int64_t* holder_ptr, const int32_t* holder_idx, const int64_t* restr_ptr,
-                   const int32_t* restr_idx, const uint8_t* restr_flags, int64_t* n_stealable);
+                   const int32_t* restr_idx, const uint8_t* restr_flags, const int8_t* levels_in,
+                   const double* inflight_occupancy_in, const int32_t* inflight_tasks_in, int64_t* n_stealable);
 int dgp_steal_thief_rows(dgp_engine* e, int64_t lo, int64_t hi);
 int64_t dgp_steal_row_bytes(void);
 int dgp_steal_pack_rows(dgp_engine* e, int64_t lo, int64_t hi, void* device_dst);
 int dgp_steal_unpack_rows(dgp_engine* e, int64_t lo, int64_t hi, const void* device_src);
 int dgp_steal_run(dgp_engine* e, int8_t* levels, int32_t* st_task, int32_t* st_victim, int32_t* st_thief,
                   int32_t* st_level, double* st_cost, double* st_occ_victim, double* st_occ_thief, int64_t* n_steals,
-                  double* inflight_occupancy, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* saturated_out);
+                  double* inflight_occupancy, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* saturated_out,
+                  uint8_t* checked_out);
 
 #ifdef __cplusplus
 }

@@ -112,20 +112,27 @@ extern "C" int orc_steal_balance(
     const int64_t* d_nbytes, const int64_t* d_get_nbytes, const int64_t* h_ptr, const int32_t* h_idx,
     // restrictions (nullable)
     const int64_t* r_ptr, const int32_t* r_idx, const uint8_t* r_flags,
+    // the plugin's bins and unconfirmed in-flight accounts (nullable)
+    const int8_t* level_in, const double* ifo_in, const int32_t* ift_in,
     // outputs
     int8_t* level_out, int32_t* st_task, int32_t* st_victim, int32_t* st_thief, int32_t* st_level, double* st_cost,
     double* st_occ_victim, double* st_occ_thief, int64_t* n_steals, double* inflight_occ, int32_t* inflight_tasks,
-    uint8_t* idle_out, uint8_t* sat_out) {
+    uint8_t* idle_out, uint8_t* sat_out, uint8_t* checked) {
   const Problem P{W, nthreads, occ, nproc, wnbytes, total_occ, total_nthreads, bandwidth, T, victim, duration,
                   fast, dep_ptr, dep_idx, d_nbytes, d_get_nbytes, h_ptr, h_idx, r_ptr, r_idx, r_flags};
   std::vector<uint8_t> idle(idle_in, idle_in + W), sat(sat_in, sat_in + W);
   std::vector<double> ifo(W, 0.0);
   std::vector<int32_t> ift(W, 0);
+  for (int w = 0; w < W; w++) {  // _combined_occupancy / _combined_nprocessing (:505-509)
+    if (ifo_in) ifo[w] = ifo_in[w];
+    if (ift_in) ift[w] = ift_in[w];
+    checked[w] = 0;
+  }
   *n_steals = 0;
   // put_key_in_stealable (stealing.py:220-230): bins per (worker, level), ascending task
   std::vector<std::vector<int64_t>> bins((size_t)W * N_LEVELS);
   for (int64_t t = 0; t < T; t++) {
-    const int lv = steal_level(P, t);
+    const int lv = level_in ? (int)level_in[t] : steal_level(P, t);
     level_out[t] = (int8_t)lv;
     if (lv >= 0) bins[(size_t)victim[t] * N_LEVELS + lv].push_back(t);
   }
@@ -244,6 +251,7 @@ extern "C" int orc_steal_balance(
         }
       }
       check_idle_saturated(v, combined_occ(v));  // :498-500
+      checked[v] = 1;
     }
   }
   return finish();

@@ -72,3 +72,19 @@ def test_graph_from_tasks_layout():
     assert g["prefix_default_dur"].tolist() == [-1.0, 0.5]
     assert g["group_prefix"].tolist() == [0, 1]
     assert g["wanted"].tolist() == [0, 0, 1] and g["rootish_override"].tolist() == [1, -1, -1]
+
+
+def test_gpu_work_stealing_matches_reference_plugin():
+    """GPUWorkStealing (distributed_amd/stealing.py) vs the reference WorkStealing on two
+    identical states, two balance() calls each: request events, metrics, in-flight
+    accounts, steal-request messages, bins and idle / saturated sets all equal
+    (tests/steal_ext_driver.py; the engine is the oracle stand-in there)."""
+    env = dict(os.environ, PYTHONHASHSEED="0")
+    env.pop("PYTHONPATH", None)
+    out = subprocess.run([PY39, os.path.join(REPO, "tests", "steal_ext_driver.py")], capture_output=True, text=True,
+                         env=env, timeout=600, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
+    assert len(res) == 4
+    for r in res:
+        assert r["differ"] == [] and r["requests"] > 0, r

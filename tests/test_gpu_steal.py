@@ -94,3 +94,19 @@ def test_balance_restricted_matches_oracle(eng, W, T, frac, seed):
     out, ref = eng.steal_balance(p), oracle.steal_balance(p)
     assert len(ref["st_task"]) > 0
     assert_same(out, ref)
+
+
+@pytest.mark.parametrize("W,T,seed", [(256, 20000, 71), (2048, 60000, 72)])
+def test_balance_plugin_state_inputs(eng, W, T, seed):
+    """levels_in (the plugin's bins) and in-flight accounts of unconfirmed steals as
+    inputs (what GPUWorkStealing passes), plus the visited-victim output."""
+    p = graphs.steal_problem(W, T, seed=seed, restrict=0.1)
+    rng = np.random.default_rng(seed)
+    lv = oracle.steal_balance(p)["level"].copy()
+    lv[rng.random(T) < 0.2] = -1  # tasks no longer in a bin
+    p["level_in"] = lv
+    p["inflight_occ_in"] = np.where(rng.random(W) < 0.3, rng.normal(0, 0.5, W), 0.0)
+    p["inflight_tasks_in"] = rng.integers(-2, 3, W).astype(np.int32)
+    out, ref = eng.steal_balance(p), oracle.steal_balance(p)
+    assert len(ref["st_task"]) > 0
+    assert_same(out, ref, keys=tuple(ref))
