@@ -121,6 +121,23 @@ def check_upload(g_up, keys_up, g_fx, fkeys):
     assert all(pd_fx[n] == d for n, d in zip(g_up["prefix_names"], g_up["prefix_default_dur"]))
 
 
+def check_messages(g, exp, sent, fkeys):
+    """The batch-built compute-task fields (distributed_amd/messages.py) against the
+    reference's own messages: key, priority, who_has, nbytes, run_id order."""
+    from distributed_amd.messages import compute_task_batch, render_messages
+
+    n = len(exp["pl_task"])
+    assert len(sent) == n, (len(sent), n)
+    batch = compute_task_batch(g, exp["pl_task"], exp["pl_worker"], 0, n, g["nbytes"])
+    addrs = [f"tcp://w{i:05d}:1" for i in range(len(g["nthreads"]))]
+    mine = render_messages(batch, fkeys, addrs, lambda t: (0, 1, int(g["prio"][t])), lambda t: 0.0)
+    for a, b in zip(mine, sent):
+        assert a["key"] == b["key"] and a["priority"] == b["priority"], (a["key"], b["key"])
+        assert {k: sorted(v) for k, v in a["who_has"].items()} == {k: sorted(v) for k, v in b["who_has"].items()}, a["key"]
+        assert a["nbytes"] == b["nbytes"], a["key"]
+    assert [m["run_id"] for m in sent] == sorted(m["run_id"] for m in sent)
+
+
 def run(name, diverge=False):
     g, cfg, exp, meta = load_fixture(os.path.join(HERE, "golden", name))
     g["keys"] = None
@@ -134,6 +151,15 @@ def run(name, diverge=False):
     S.handle_task_finished = Scheduler.handle_task_finished
     S.validate_key = lambda self, key, ts=None: None
     S.send_all = lambda self, client_msgs, worker_msgs: None
+    sent = []  # every compute-task message the reference built (_task_to_msg :3421-3450)
+    orig_msg = S._task_to_msg
+
+    def task_to_msg(self, ts, duration=-1):
+        m = orig_msg(self, ts, duration)
+        sent.append(m)
+        return m
+
+    S._task_to_msg = task_to_msg
     fkeys = [ts.key for ts in tss]
     eng = FixtureEngine(exp, fkeys)
     if diverge:  # first stimulus after update_graph with two or more placements
@@ -178,6 +204,7 @@ def run(name, diverge=False):
     assert rec["wsnbytes"] == exp["pl_wsnbytes"].tolist()
     if not diverge:
         assert ext.stats["device_decisions"] == n, (ext.stats, n)
+        check_messages(g, exp, sent, fkeys)
     return dict(fixture=name, placements=n, messages=n_msgs, device_decisions=ext.stats["device_decisions"],
                 device_queued=ext.stats["device_queued"], device_no_worker=ext.stats["device_no_worker"],
                 active=ext.active, reason=ext.reason)
