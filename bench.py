@@ -352,7 +352,14 @@ def main():
         tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "hbm_traffic.json")
         if dom == "replay" and os.path.exists(tf):
             t = json.load(open(tf))
-            if (t.get("n_tasks"), t.get("n_workers")) == (args.tasks, args.workers):
+            sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+            from pmc_traffic import engine_source_hash
+
+            if (t.get("n_tasks"), t.get("n_workers")) != (args.tasks, args.workers):
+                pass
+            elif t.get("src_sha256") != engine_source_hash():  # measured on other engine sources
+                result["roofline"]["traffic_source"] = f"stale ({t.get('source')}): engine sources changed since"
+            else:
                 result["roofline"]["traffic"] = round(t["traffic_bytes_per_launch"], 1)
                 result["roofline"]["traffic_source"] = t.get("source")
         if not args.no_latency:

@@ -161,6 +161,7 @@ struct Dev {
   // prefixes
   double* pdur_cur;   // TaskPrefix.duration_average after all committed completions
   double* pdur_walk;  // ... as of the walker position
+  double* pdur_pre;   // ... as of the stream prefetcher's position (it resolves each stimulus' durations)
   double* pmaxexec;   // TaskPrefix.max_exec_time (no heartbeats in the replay: -1)
   double* durv;       // per-round table: durations in effect at stimulus j, [n][P]
   // groups
@@ -219,7 +220,7 @@ struct Dev {
   uint32_t* gw_pcnt;
   int64_t* gw_netocc;
   int64_t* gw_nbytes;
-  uint32_t* gw_mask;
+  unsigned long long* gw_mask;  // in-flight stream slots touching each worker (bit per slot)
   uint32_t* gw_needs;
   uint8_t* gw_wflags;
   uint32_t* gw_needs_ext;    // needs_what overflow entries [W][NXW]
@@ -231,7 +232,7 @@ struct Dev {
   int32_t* rel_mark;         // stimulus whose completion empties the task's waiters
   uint4* desc;               // descriptor ring [DR][NE]
   int32_t* touch_ring;       // distinct workers each prefetched stimulus touches [DR][TMAX]
-  long long* desc_tag;
+  uint2* thdr;               // per descriptor row: (flags, touched-worker count), written by PRE for REG
   int32_t* s2_task;  // per-slot staging of placements [WIN][PLC]
   int32_t* s2_worker;
   int64_t* s2_comm;

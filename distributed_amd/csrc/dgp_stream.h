@@ -50,7 +50,7 @@ __constant__ Dev c_dev;
 #define DGP_REG_PROBES 0  // registrar sub-phase s_memtime probes (diagnostics)
 #endif
 #ifndef DGP_RB
-#define DGP_RB 4  // registrar batch (stimuli registered per poll; 4 measured best of 2/4/8)
+#define DGP_RB 8  // registrar batch (stimuli registered per poll, one lane each)
 #endif
 #ifndef DGP_SCTA
 #define DGP_SCTA 1024
@@ -59,7 +59,9 @@ constexpr int SCTA = DGP_SCTA;   // 1024: 16 waves = 5 roles + 11 executors (128
 #ifndef DGP_WIN
 #define DGP_WIN 32
 #endif
-constexpr int WIN = DGP_WIN;     // in-flight stimulus slots (LDS window; masks are u32: <= 32)
+constexpr int WIN = DGP_WIN;     // in-flight stimulus slots (LDS window; masks are u64: <= 64)
+using SMask = unsigned long long;  // a set of window slots
+static_assert(WIN >= 32 && WIN <= 64, "DGP_WIN must be in [32, 64]");
 #ifndef DGP_RS
 #define DGP_RS 128
 #endif
@@ -83,6 +85,8 @@ constexpr int NLW = 12;          // needs_what words per worker in LDS: 11 entri
 constexpr int NXW = 52;          // overflow entries per worker (global) before scan mode
 constexpr int PG = 64;           // walker's global prefix dict
 constexpr int BIG = 1 << 24;     // registration guard of a slot's predecessor count
+constexpr int T_CAND = 0x8000;   // touch-list entry flag: the worker is a frontier candidate (ids < 32768)
+constexpr int T_W = 0x7fff;
 constexpr uint32_t NL_OVF = 0xffffffffu;
 constexpr int N_ROLE = 5;        // waves 0..4 are SEQ, BLD, PRE, REG, WLK; the rest execute
 constexpr int E_HDR = 7;         // header entries: 0 ids, 1 sizes/counts, 2 duration, 3..6 durations
@@ -90,7 +94,11 @@ constexpr int E_HDR = 7;         // header entries: 0 ids, 1 sizes/counts, 2 dur
 static_assert((DR & (DR - 1)) == 0 && DR >= 64 && DR >= WIN, "DGP_DR must be a power of two >= 64");
 static_assert((RS & (RS - 1)) == 0 && RS >= WIN && RS <= DR, "DGP_RS must be a power of two in [WIN, DR]");
 
-enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16 };
+// F_SIMPLE (PRE): touches only its completing worker, empty frontier, at most one dependency
+// (held by that worker) and one release: it can be part of a single-worker run (exe_run).
+// F_RUNM (REG): F_SIMPLE and so is the stimulus just before it, on the same worker: a run
+// continues through it, so only the run-capable executor takes it
+enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16, F_SIMPLE = 32, F_RUNM = 64 };
 enum : int { K_COMPLETE = 1, K_PLACE = 2 };
 enum : int { SERR_NONE = 0, SERR_PREFIX = 11, SERR_WATCHDOG = 12, SERR_QUEUE = 13, SERR_NEEDS = 14,
              SERR_REC = 15, SERR_CAND = 16, SERR_STAGE = 17, SERR_RANGE = 18, SERR_INV = 19 };
@@ -127,8 +135,8 @@ struct SCtl {
   int capmax;          // max slot cap over workers
   int global_pending;  // a registered global stimulus has not finished
   int busy_exe;        // executors between claim and retirement
-  unsigned ready;      // slots whose stimulus may run
-  unsigned freem;      // slots not holding a registered stimulus (REG allocates, executors free)
+  SMask ready;         // slots whose stimulus may run
+  SMask freem;         // slots not holding a registered stimulus (REG allocates, executors free)
   long long seq_pos, log_len, rec_len, walk_pos, bld_pos, pre_pos, reg_pos, reg_limit;
   long long qhead, qlen, n_tasks;
   long long stim_end;  // service mode: stimuli [seq_pos, stim_end) run in this launch
@@ -228,7 +236,7 @@ struct WPtr {
   P<uint32_t> pcnt;    // [W][PD] prefix dict counts by prefix id (WDict::c, c1)
   P<int64_t> netocc;
   P<int64_t> nbytes;
-  P<uint32_t> mask;    // in-flight slots touching the worker
+  P<SMask> mask;       // in-flight slots touching the worker
   P<uint32_t> needs;   // [W][NLW]: (d << 8 | count), slot NLW-1 = control (count << 8 | 1 when
                        // overflow entries are in use; NL_OVF: scan mode)
   P<uint8_t> wflags;   // walker's idle / saturated bits
@@ -240,7 +248,7 @@ __device__ __forceinline__ size_t al16(size_t b) { return (b + 15) & ~(size_t)15
 __host__ __device__ constexpr size_t lds_worker_bytes(int W) {
   return ((size_t)W * 4 + 15) / 16 * 16 * 2 /* nproc plen */ + ((size_t)W * 2 + 15) / 16 * 16 * 2 +
          ((size_t)W * PD * 4 + 15) / 16 * 16 + ((size_t)W * 8 + 15) / 16 * 16 * 2 +
-         ((size_t)W * 4 + 15) / 16 * 16 + ((size_t)W * NLW * 4 + 15) / 16 * 16 + ((size_t)W + 15) / 16 * 16;
+         ((size_t)W * 8 + 15) / 16 * 16 + ((size_t)W * NLW * 4 + 15) / 16 * 16 + ((size_t)W + 15) / 16 * 16;
 }
 
 template <bool LW>
@@ -257,7 +265,7 @@ __device__ __forceinline__ WPtr<LW> wptr(const Dev& D) {
     p.pcnt = (typename W_::template P<uint32_t>)b;     b += al16(W * PD * 4);
     p.netocc = (typename W_::template P<int64_t>)b;    b += al16(W * 8);
     p.nbytes = (typename W_::template P<int64_t>)b;    b += al16(W * 8);
-    p.mask = (typename W_::template P<uint32_t>)b;     b += al16(W * 4);
+    p.mask = (typename W_::template P<SMask>)b;        b += al16(W * 8);
     p.needs = (typename W_::template P<uint32_t>)b;    b += al16(W * NLW * 4);
     p.wflags = (typename W_::template P<uint8_t>)b;
   } else {
@@ -302,8 +310,8 @@ struct RMeta {
 
 // LDS of the stream kernel besides the worker carve
 struct SLds {
-  uint4 desc[WIN][NE];        // descriptors of the in-flight window
-  uint16_t touch[WIN][NE];    // distinct workers each in-flight stimulus touches
+  double dur[SCTA / 64][PD];  // each executor wave: its stimulus' resolved prefix durations
+  uint16_t touch[WIN][NE];    // distinct workers each in-flight stimulus touches (| T_CAND)
   int32_t ntouch[WIN];
   uint32_t flags[WIN];
   int32_t pred[WIN];
@@ -967,20 +975,23 @@ __device__ __attribute__((always_inline)) void bld_range(const Dev& D, long long
 
 // ==================================================================== prefetcher
 // descriptor of stimulus r (one lane): see E_HDR for the header layout
-__device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L, long long r) {
+__device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L, long long r, int& p_out, double& dobs_out) {
   uint4* E = D.desc + (size_t)(r & (DR - 1)) * NE;
   // the distinct workers the stimulus touches, in first-touch order (lane-private LDS list)
   auto scr = L.pre_scr[lane_id()];
   int nt = 0;
   bool tbad = false;
-  auto touch = [&](int c) {
+  auto touch = [&](int c, bool cand) {
     if (c < 0 || c >= D.W) {
       tbad = true;
       return;
     }
-    for (int i = 0; i < nt; i++)
-      if (scr[i] == (uint16_t)c) return;
-    if (nt < TMAX) scr[nt] = (uint16_t)c;
+    for (int i = 0; i < nt && i < TMAX; i++)
+      if ((scr[i] & T_W) == c) {
+        if (cand) scr[i] |= (uint16_t)T_CAND;
+        return;
+      }
+    if (nt < TMAX) scr[nt] = (uint16_t)(c | (cand ? T_CAND : 0));
     nt++;
   };
   const int t = D.stim_task[r];
@@ -1000,12 +1011,15 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
     PROF(atomicAdd(&L.c.prof[20], 1ull));  // diagnostics: why stimuli run global
   }
   int n = E_HDR, nrel = 0, nf = 0, sumkx = 0;
-  touch(w);
+  touch(w, false);
+  int h_dep0 = -1;  // holder of the first dependency
   if (!(flags & F_GLOBAL)) {
     for (int64_t k = k0; k < k1; k++) {
       const int d = D.dep_idx[k];
       const int64_t nb = nbv(D, D.res_nbytes[d]);
-      E[n++] = make_uint4((unsigned)d, (unsigned)D.holder_of[d], lo32(nb), hi32(nb));
+      const int hd = D.holder_of[d];
+      if (k == k0) h_dep0 = hd;
+      E[n++] = make_uint4((unsigned)d, (unsigned)hd, lo32(nb), hi32(nb));
     }
     for (int64_t k = k0; k < k1; k++) {
       const int d = D.dep_idx[k];
@@ -1016,7 +1030,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
       }
       const int64_t nb = nbv(D, D.res_nbytes[d]);
       const int hd = D.holder_of[d];
-      touch(hd);
+      touch(hd, false);
       E[n++] = make_uint4((unsigned)hd, (unsigned)d, lo32(nb), hi32(nb));
       nrel++;
     }
@@ -1039,7 +1053,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
       const int d = D.dep_idx[q];
       const int64_t nb = nbv(D, D.res_nbytes[d]);
       const int hd = D.holder_of[d];
-      touch(hd);
+      touch(hd, true);
       E[n++] = make_uint4((unsigned)d, (unsigned)hd, lo32(nb), hi32(nb));
     }
   }
@@ -1048,6 +1062,9 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   if (nf > 255 || nt > TMAX) flags |= F_GLOBAL;
   if (nf + (D.sat_inf ? 0 : D.w_cap[w]) + 1 > PLC) flags |= F_GLOBAL;  // staging room for the refill
   if (tbad) flags |= F_GLOBAL | F_BADTOUCH;
+  if (!(flags & F_GLOBAL) && nt == 1 && nf == 0 && kt <= 1 && nrel <= 1 &&
+      (kt == 0 || h_dep0 == w))
+    flags |= F_SIMPLE;
   if (flags & F_GLOBAL) nt = 0;
   int32_t* T = D.touch_ring + (size_t)(r & (DR - 1)) * TMAX;
   for (int i = 0; i < nt; i++) T[i] = scr[i];
@@ -1055,6 +1072,9 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   E[1] = make_uint4(lo32(nbt), hi32(nbt),
                     (unsigned)(min(kt, 255) | (nrel << 8) | (min(nf, 255) << 16) | (n << 24)), (unsigned)g);
   E[2] = make_uint4(dlo(dobs), dhi(dobs), (unsigned)nt, (unsigned)sumkx);  // sumkx: needs entries it may add
+  D.thdr[r & (DR - 1)] = make_uint2(flags, (unsigned)nt);
+  p_out = p;
+  dobs_out = dobs;
 }
 
 // ========================================================== builder / prefetcher
@@ -1066,6 +1086,8 @@ template <int KIND>  // 0 BLD, 1 PRE
 __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L) {
   SCtl& S = L.c;
   const int lane = lane_id();
+  // PRE: lane p holds TaskPrefix.duration_average of prefix p as of pre_pos
+  double dur = (KIND == 1 && lane < PD && lane < D.P) ? D.pdur_pre[lane] : -1.0;
   while (true) {
     if (vload(&S.stop)) break;
     const long long a = KIND == 0 ? S.bld_pos : S.pre_pos;
@@ -1084,7 +1106,18 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
       bld_range(D, a, e);
     } else {
       const long long r = a + lane;
-      if (r < e) build_desc(D, L, r);
+      int pl = 0;
+      double dl = 0.0;
+      if (r < e) build_desc(D, L, r, pl, dl);
+      // TaskPrefix.add_duration (:977-985) in stimulus order; each descriptor carries the
+      // resolved durations (_calc_occupancy :1892-1899) after its own completion, entries 3..6
+      const int m = (int)(e - a);
+      for (int i = 0; i < m; i++) {
+        const int pi = rl(pl, i);
+        const double di = mkd(rlu(dlo(dl), i), rlu(dhi(dl), i));
+        if (lane == pi && di == di) dur = dur < 0 ? di : 0.5 * di + 0.5 * dur;  // NaN: no compute interval
+        if (lane < PD) ((double*)(D.desc + (size_t)((a + i) & (DR - 1)) * NE + 3))[lane] = resolve_dur(D, dur);
+      }
     }
     __threadfence_block();
     wbar();
@@ -1094,47 +1127,46 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
       vstore(KIND == 0 ? &S.bld_pos : &S.pre_pos, e);
     }
   }
+  if (KIND == 1 && lane < PD && lane < D.P) D.pdur_pre[lane] = dur;
 }
 
 // ===================================================================== registrar
-// In stimulus order: the prefix EWMA (TaskPrefix.add_duration :977-985) and the resolved
-// durations written into the descriptor, the slot flags, the distinct touched workers,
-// then registration (slot bit into each touched worker's mask; predecessor count = the
-// in-flight bits already there). A batch of up to RB stimuli per poll: phase A prepares
-// every slot of the batch; phase B registers them. The mask atomics of phase B are issued
-// back to back: one wave's LDS operations execute in order, so stimulus b sees the bits
-// of b-1 exactly as if they were registered one at a time.
-__device__ __forceinline__ int wsum_small(int v) {  // wave sum of values in [0, 64)
-  int t = 0;
-#pragma unroll
-  for (int b = 0; b < 6; b++) t += __builtin_popcountll(ballot((v >> b) & 1)) << b;
-  return t;
-}
+// In stimulus order: the slot flags, the distinct touched workers, then registration (slot
+// bit into each touched worker's mask; predecessor count = the in-flight bits already
+// there). The descriptor itself stays in the global ring (the executors read it there) and
+// PRE has already resolved its durations, so a batch of up to RB stimuli moves only the
+// touch lists and the per-slot words (lane b = stimulus b). Phase A prepares every slot of
+// the batch; phase B registers them. The mask atomics of phase B are issued back to back:
+// one wave's LDS operations execute in order, so stimulus b sees the bits of b-1 exactly as
+// if they were registered one at a time.
 
 template <bool LW>
 __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, const WPtr<LW>& P) {
   SCtl& S = L.c;
   const int lane = lane_id();
-  // lanes 3..6 own duration_average of prefixes 2(lane-3) and 2(lane-3)+1 (the descriptor
-  // entry they fill), as of reg_pos
-  const int pa = 2 * (lane - 3);
-  const bool dl = lane >= 3 && lane < 7;
-  double dur0 = dl && pa < D.P ? D.pdur_cur[pa] : -1.0;
-  double dur1 = dl && pa + 1 < D.P ? D.pdur_cur[pa + 1] : -1.0;
   constexpr int RB = DGP_RB;
   long long pre = 0;  // cached PRE watermark: re-read only when exhausted
   unsigned long long t_poll = mclk();
-  uint4 EB[RB];
-  int TB[RB];
+  int TB[RB];   // touch lists of the batch: lane i = touched worker i of stimulus r0 + b
+  uint2 HB;     // lane b: (flags, touched-worker count) of stimulus r0 + b (PRE's row header)
   long long eb_first = -1;
   int eb_n = 0;
+  int prev_simple_w = -1;  // the last registered stimulus' worker if it was F_SIMPLE, else -1
+  auto fetch = [&](long long r1, int n1) {  // the rows of stimuli [r1, r1 + n1)
+#pragma unroll
+    for (int b = 0; b < RB; b++)
+      TB[b] = (lane < TMAX && b < n1) ? D.touch_ring[(size_t)((r1 + b) & (DR - 1)) * TMAX + lane] : -1;
+    HB = lane < n1 ? D.thdr[(r1 + lane) & (DR - 1)] : make_uint2(0, 0);
+    eb_first = r1;
+    eb_n = n1;
+  };
   while (true) {
     if (vload(&S.stop)) break;
     const long long r0 = S.reg_pos;
     if (r0 >= pre) pre = vload(&S.pre_pos);
     const long long wl = vload(&S.seq_pos) + RS;  // retire-ring capacity
-    const unsigned fm = vload(&S.freem);           // free slots (only this wave takes them)
-    const long long lim = min(min(pre, vload(&S.reg_limit)), min(wl, r0 + (long long)__builtin_popcount(fm)));
+    const SMask fm = vload(&S.freem);              // free slots (only this wave takes them)
+    const long long lim = min(min(pre, vload(&S.reg_limit)), min(wl, r0 + (long long)__builtin_popcountll(fm)));
     const int gp = vload(&S.global_pending);
     if (r0 >= lim || gp) {
       // stall attribution (cycles): 24 window full, 25 descriptor not prefetched, 26 global pending
@@ -1147,117 +1179,90 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     lds_fence();
     const unsigned long long t0 = mclk();
     int nb = (int)min((long long)RB, lim - r0);
-    // the batch's descriptors and touch lists (prefetched by the previous iteration when
-    // it could; the loads complete while this wave polls)
-    if (eb_first == r0 && eb_n > 0) {
-      nb = min(nb, eb_n);  // use the prefetched rows; the next prefetch covers the rest
-    } else {
-      eb_first = r0;
-      eb_n = nb;
-#pragma unroll
-      for (int b = 0; b < RB; b++) {
-        const size_t row = (size_t)((r0 + b) & (DR - 1));
-        EB[b] = (lane < NE && b < nb) ? D.desc[row * NE + lane] : make_uint4(0, 0, 0, 0);
-        TB[b] = (lane < TMAX && b < nb) ? D.touch_ring[row * TMAX + lane] : -1;
-      }
-    }
+    // the batch's rows (prefetched by the previous iteration when it could)
+    if (eb_first == r0 && eb_n > 0) nb = min(nb, eb_n);
+    else fetch(r0, nb);
 #if DGP_REG_PROBES
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the batch rows are in
     PROF(if (lane == 0) S.prof[16] += mclk() - t0);
 #endif
-    // the batch's slots: the lowest free ones (nb <= popcount(fm) by lim)
+    // the batch's slots: the lowest free ones (nb <= popcount(fm) by lim); lane b takes sb[b]
     int sb[RB];
+    int my_s = 0;
     {
-      unsigned f = fm;
+      SMask f = fm;
 #pragma unroll
       for (int b = 0; b < RB; b++) {
-        sb[b] = f ? __builtin_ctz(f) : 0;
+        sb[b] = f ? __builtin_ctzll(f) : 0;
+        if (lane == b) my_s = sb[b];
         if (b < nb) f &= f - 1;
       }
     }
     // ---------------------------------------------------------------- phase A
-    // header scalars of the whole batch first (independent of one another)
-    int pb[RB], ntb[RB];
-    uint32_t flb[RB];
-    double dob[RB];
+    // lane b: stimulus r0 + b. Flags (PRE's, plus the queue rule and debug modes), then the
+    // batch ends after its first global stimulus (nothing registers behind a global)
     const long long ql = vload(&S.qlen);  // only globals grow the queue; none runs now
     const bool qglob = ql > 0 && (!S.inv_ok || !S.q_anon);
     const uint32_t fadd = (qglob ? F_GLOBAL : 0u) | ((D.dbg & 1) ? F_EXACT : 0u) | ((D.dbg & 2) ? F_GLOBAL : 0u);
-#pragma unroll
-    for (int b = 0; b < RB; b++) {
-      PROF(if (lane == 0 && b < nb && qglob && !(rlu(EB[b].w, 0) & F_GLOBAL)) S.prof[23] += 1);  // diagnostics
-      pb[b] = rl((int)EB[b].z, 0);
-      dob[b] = mkd(rlu(EB[b].x, 2), rlu(EB[b].y, 2));
-      ntb[b] = rl((int)EB[b].z, 2);
-      flb[b] = rlu(EB[b].w, 0) | fadd;
-    }
-    // the batch ends after its first global stimulus (nothing registers behind a global)
-    int nbat = nb;
-    bool glob_end = false, halt = false;
-#pragma unroll
-    for (int b = RB - 1; b >= 0; b--) {
-      if (b < nb && (flb[b] & F_GLOBAL)) {
-        nbat = b + 1;
-        glob_end = true;
-      }
-      if (b < nb && (flb[b] & F_BADTOUCH)) halt = true;
-    }
-    if (halt) {
+    uint32_t fl = lane < nb ? (HB.x | fadd) : 0u;
+    int nt = lane < nb ? (int)HB.y : 0;
+    PROF(if (lane < nb && qglob && !(HB.x & F_GLOBAL)) atomicAdd(&S.prof[23], 1ull));  // diagnostics
+    if (ballot(lane < nb && (fl & F_BADTOUCH))) {
       serr(S, SERR_RANGE, (int)r0);
       break;
     }
+    const unsigned long long gm = ballot(lane < nb && (fl & F_GLOBAL));
+    const bool glob_end = gm != 0;
+    const int nbat = glob_end ? __builtin_ctzll(gm) + 1 : nb;
     const int nloc = nbat - (glob_end ? 1 : 0);  // stimuli with touch lists
+    if (glob_end && lane == nbat - 1) fl |= F_TOUCHALL;
+    if (lane >= nloc) nt = 0;
+    {  // run continuations: this and the stimulus before it are F_SIMPLE on the same worker
+      int w0 = -1;
 #pragma unroll
-    for (int b = 0; b < RB; b++) {
-      if (b >= nbat) break;
-      const long long r = r0 + b;
-      const int s = sb[b];
-      uint4 E = EB[b];
-      const int p = pb[b];
-      if (lane == 3 + (p >> 1) && dob[b] == dob[b]) {  // TaskPrefix.add_duration, in stimulus order (NaN: none)
-        if (p & 1) dur1 = dur1 < 0 ? dob[b] : 0.5 * dob[b] + 0.5 * dur1;
-        else dur0 = dur0 < 0 ? dob[b] : 0.5 * dob[b] + 0.5 * dur0;
+      for (int b = 0; b < RB; b++) {
+        const int v = b < nloc ? (rl(TB[b], 0) & T_W) : -1;
+        if (lane == b) w0 = v;
       }
-      if (dl) {
-        const double a0 = resolve_dur(D, dur0), a1 = resolve_dur(D, dur1);
-        E = make_uint4(dlo(a0), dhi(a0), dlo(a1), dhi(a1));
-      }
-      const uint32_t fl = (b == nbat - 1 && glob_end) ? (flb[b] | F_TOUCHALL) : flb[b];
-      flb[b] = fl;
-      if (lane == 0) E.w = fl;
-      if (lane < NE) L.desc[s][lane] = E;
-      // the distinct touched workers (deduplicated by the prefetcher), one lane each
-      const int nt = (b < nloc) ? ntb[b] : 0;
-      ntb[b] = nt;
-      if (lane < NE) L.touch[s][lane] = (uint16_t)TB[b];  // entries past nt are never read
-      if (lane == 0) {
-        L.ntouch[s] = nt;
-        L.flags[s] = fl;
-        L.pred[s] = BIG;
-        L.sid[s] = r;
-      }
+      const bool sim = lane < nloc && (fl & F_SIMPLE);
+      int pw = __shfl_up(sim ? w0 : -1, 1);
+      if (lane == 0) pw = prev_simple_w;
+      if (sim && pw == w0) fl |= F_RUNM;
+      prev_simple_w = rl(sim ? w0 : -1, nbat - 1);
+    }
+    if (lane < nbat) {
+      L.ntouch[my_s] = nt;
+      L.flags[my_s] = fl;
+      L.pred[my_s] = BIG;
+      L.sid[my_s] = r0 + lane;
+    }
+    int ntb[RB];
+#pragma unroll
+    for (int b = 0; b < RB; b++) {  // the distinct touched workers (deduplicated by PRE), one lane each
+      ntb[b] = b < nloc ? rl(nt, b) : 0;
+      if (lane < ntb[b]) L.touch[sb[b]][lane] = (uint16_t)TB[b];
     }
     const unsigned long long tA = mclk();
     // ---------------------------------------------------------------- phase B
     lds_fence();  // the slots' LDS state is written before any mask bit can expose it
     if (lane == 0) {
-      unsigned taken = 0;
+      SMask taken = 0;
 #pragma unroll
       for (int b = 0; b < RB; b++)
-        if (b < nbat) taken |= 1u << sb[b];
+        if (b < nbat) taken |= 1ull << sb[b];
       atomicAnd(&S.freem, ~taken);
       vstore(&S.reg_pos, r0 + nbat);
+      if (glob_end) vstore(&S.global_pending, 1);  // a global ends its batch
     }
     // every mask registration back to back (one wave's LDS atomics run in order)
-    int touchall_cnt = 0;
-    unsigned oldb[RB];
+    SMask oldb[RB];
 #pragma unroll
     for (int b = 0; b < RB; b++) {  // every lane issues: an inactive lane ORs 0 into its own word
       oldb[b] = 0;
       if (b >= nloc) break;
-      const unsigned bit = 1u << sb[b];
+      const SMask bit = 1ull << sb[b];
       const bool on = lane < ntb[b];
-      oldb[b] = __hip_atomic_fetch_or(&P.mask[on ? TB[b] : lane], on ? bit : 0u, __ATOMIC_RELAXED,
+      oldb[b] = __hip_atomic_fetch_or(&P.mask[on ? (TB[b] & T_W) : lane], on ? bit : 0ull, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #if DGP_REG_PROBES
@@ -1265,65 +1270,44 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     const unsigned long long tM = mclk();
     PROF(if (lane == 0) S.prof[20] += tM - tA);
 #endif
-    if (glob_end) {
-      const unsigned bit = 1u << sb[nbat - 1];
-      for (int c = lane; c < D.W; c += 64)
-        touchall_cnt += __builtin_popcount(__hip_atomic_fetch_or(&P.mask[c], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
-    }
-    // predecessor count of stimulus b = in-flight bits already set on its workers, summed
-    // over its lanes by bit-slice ballots (counts < 32: five ballots, no lane walk)
-    int totb[RB];
+    // predecessor count of stimulus b = its workers that an earlier in-flight stimulus holds:
+    // it waits on each for the latest one only, whose release of that worker wakes it
+    // (release_worker picks the earliest successor). Each lane adds its own count to the slot
+    // (no-return LDS adds, in order after the guard)
 #pragma unroll
     for (int b = 0; b < RB; b++) {
-      const unsigned bit = 1u << sb[b];
-      const int c = (b < nloc && lane < ntb[b]) ? __builtin_popcount(oldb[b] & ~bit) : 0;
-      int t = 0;
-#pragma unroll
-      for (int k = 0; k < 5; k++) t += __builtin_popcountll(ballot((c >> k) & 1)) << k;
-      totb[b] = t;
+      if (b >= nloc) break;
+      const int c = (lane < ntb[b] && (oldb[b] & ~(1ull << sb[b])) != 0) ? 1 : 0;
+      if (c) __hip_atomic_fetch_add(&L.pred[sb[b]], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (glob_end) {  // a global stimulus waits for every in-flight stimulus on every worker
+      const int sg = sb[nbat - 1];
+      const SMask bit = 1ull << sg;
+      int cnt = 0;
+      for (int c = lane; c < D.W; c += 64)
+        cnt += (__hip_atomic_fetch_or(&P.mask[c], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit) != 0 ? 1 : 0;
+      if (cnt) __hip_atomic_fetch_add(&L.pred[sg], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #if DGP_REG_PROBES
     PROF(if (lane == 0) S.prof[21] += mclk() - tM);
 #endif
-    const int tall = glob_end ? wsum(touchall_cnt) : 0;
-    if (lane == 0) {
-      if (glob_end) vstore(&S.global_pending, 1);  // a global ends its batch
-      int oldp[RB];
-#pragma unroll
-      for (int b = 0; b < RB; b++) {
-        if (b == nbat - 1 && glob_end) totb[b] = tall;
-        oldp[b] = b < nbat ? atomicAdd(&L.pred[sb[b]], totb[b] - BIG) : 1;
-      }
-      unsigned rdy = 0;
-#pragma unroll
-      for (int b = 0; b < RB; b++)
-        if (b < nbat && oldp[b] + totb[b] - BIG == 0) rdy |= 1u << sb[b];
-      if (rdy) atomicOr(&S.ready, rdy);
+    // lane b drops slot b's registration guard; the count left is its predecessors not yet
+    // released (releases that came first were never counted)
+    if (lane < nbat) {
+      const int op = __hip_atomic_fetch_add(&L.pred[my_s], -BIG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (op == BIG) atomicOr(&S.ready, 1ull << my_s);
       if (DGP_TRACE) {
-        for (int b = 0; b < RB; b++) {
-          if (b >= nbat) break;
-          if (DGP_TRACE == 1) TR(r0 + b, 0);
-          if (DGP_TRACE == 1 && ((rdy >> sb[b]) & 1u)) TR(r0 + b, 1);
-          trace_at(D, r0 + b, 7, (unsigned long long)(totb[b] | (ntb[b] << 16)));
-        }
+        if (DGP_TRACE == 1) TR(r0 + lane, 0);
+        if (DGP_TRACE == 1 && op == BIG) TR(r0 + lane, 1);
+        trace_at(D, r0 + lane, 7, (unsigned long long)((op - BIG) | (nt << 16)));
       }
     }
     const unsigned long long tB = mclk();
     {  // prefetch the next batch's rows while the executors run
       const long long r1 = r0 + nbat;
       const int n1 = (int)min((long long)RB, pre - r1);
-      if (n1 > 0) {
-        eb_first = r1;
-        eb_n = n1;
-#pragma unroll
-        for (int b = 0; b < RB; b++) {
-          const size_t row = (size_t)((r1 + b) & (DR - 1));
-          EB[b] = (lane < NE && b < n1) ? D.desc[row * NE + lane] : make_uint4(0, 0, 0, 0);
-          TB[b] = (lane < TMAX && b < n1) ? D.touch_ring[row * TMAX + lane] : -1;
-        }
-      } else {
-        eb_first = -1;
-      }
+      if (n1 > 0) fetch(r1, n1);
+      else eb_first = -1;
     }
     if (lane == 0) {
       t_poll = mclk();
@@ -1338,8 +1322,6 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     }
     lds_fence();
   }
-  if (dl && pa < D.P) D.pdur_cur[pa] = dur0;
-  if (dl && pa + 1 < D.P) D.pdur_cur[pa + 1] = dur1;
 }
 
 // ===================================================================== executors
@@ -1597,43 +1579,45 @@ __device__ __forceinline__ bool dict_update(const WPtr<LW>& P, int c, int p, int
   return ok;
 }
 
-// release one worker of slot s: clear the slot's bit; successors waiting on it count down
-template <bool LW>
-__device__ __forceinline__ void release_worker(SLds& L, const WPtr<LW>& P, int s, int c) {
-  const unsigned bit = 1u << s;
-  unsigned succ = __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit;
-  while (succ) {
-    const int b = __builtin_ctz(succ);
-    succ &= succ - 1;
-    if (atomicSub(&L.pred[b], 1) == 1) {
-      atomicOr(&L.c.ready, 1u << b);
-      if (DGP_TRACE == 1) { const Dev& D = c_dev; TR(L.sid[b], 1); }
+// release worker c of slot s: clear the slot's bit. Every bit left on c belongs to a later
+// stimulus (an earlier one holding c would have released it before s could run); the earliest
+// of them is the one waiting for s on c, and it alone counted s (role_reg): it counts down.
+__device__ __forceinline__ void release_succ(SLds& L, SMask succ) {
+  if (!succ) return;
+  int bs = __builtin_ctzll(succ);
+  long long best = vload(&L.sid[bs]);
+  for (SMask m = succ & (succ - 1); m; m &= m - 1) {
+    const int b = __builtin_ctzll(m);
+    const long long v = vload(&L.sid[b]);
+    if (v < best) {
+      best = v;
+      bs = b;
     }
   }
+  if (atomicSub(&L.pred[bs], 1) == 1) {
+    atomicOr(&L.c.ready, 1ull << bs);
+    if (DGP_TRACE == 1) { const Dev& D = c_dev; TR(L.sid[bs], 1); }
+  }
+}
+template <bool LW>
+__device__ __forceinline__ void release_worker(SLds& L, const WPtr<LW>& P, int s, int c) {
+  const SMask bit = 1ull << s;
+  release_succ(L, __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
 }
 
 // release the workers of slot s (the waiting successors may run) — LDS state only
 template <bool LW>
 __device__ __attribute__((always_inline)) void release_slot(const Dev& D, SLds& L, const WPtr<LW>& P, int s, bool all) {
-  SCtl& S = L.c;
   const int lane = lane_id();
-  const unsigned bit = 1u << s;
+  const SMask bit = 1ull << s;
   auto rel = [&](int c) {
-    unsigned succ = __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit;
-    while (succ) {
-      const int b = __builtin_ctz(succ);
-      succ &= succ - 1;
-      if (atomicSub(&L.pred[b], 1) == 1) {
-        atomicOr(&S.ready, 1u << b);
-        if (DGP_TRACE == 1) TR(L.sid[b], 1);
-      }
-    }
+    release_succ(L, __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
   };
   if (all) {
     for (int c = lane; c < D.W; c += 64) rel(c);
   } else {
     const int nt = L.ntouch[s];
-    if (lane < nt) rel((int)L.touch[s][lane]);
+    if (lane < nt) rel((int)L.touch[s][lane] & T_W);
   }
 }
 
@@ -1654,9 +1638,19 @@ __device__ __attribute__((always_inline)) void finish_slot(const Dev& D, SLds& L
   __threadfence_block();
   if (lane == 0) {
     vstore(&L.rdone[q], r + 1);
-    atomicOr(&L.c.freem, 1u << s);  // the slot may take the next registration
+    atomicOr(&L.c.freem, 1ull << s);  // the slot may take the next registration
   }
   if (DGP_TRACE && lane == 0) TR(r, 5);
+}
+
+// wave minimum (uniform): DPP within rows of 16 lanes (quad swaps, half-row and row
+// mirrors), then the four row results
+__device__ __forceinline__ unsigned wmin_u32(unsigned v) {
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xb1, 0xf, 0xf, false));   // quad_perm(1,0,3,2)
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4e, 0xf, 0xf, false));   // quad_perm(2,3,0,1)
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xf, 0xf, false));  // row_mirror
+  return min(min(rlu(v, 0), rlu(v, 16)), min(rlu(v, 32), rlu(v, 48)));
 }
 
 // objective key of lane's candidate: worker_objective (:3131-3146) + canonical index
@@ -1689,21 +1683,31 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
   return ((uint64_t)rlu((unsigned)(v >> 32), l) << 32) | rlu((unsigned)v, l);
 }
 
+// the resolved durations of a stimulus (descriptor entries 3..6, in lanes 3..6 of E) into
+// the executor wave's LDS table, read by prefix id (one wave's LDS operations run in order)
+__device__ __forceinline__ DTab stim_durations(SLds& L, const uint4& E) {
+  const int lane = lane_id();
+  const auto t = (__attribute__((address_space(3))) double*)(double*)L.dur[threadIdx.x >> 6];
+  if (lane >= 3 && lane < 7) {
+    t[2 * (lane - 3)] = mkd(E.x, E.y);
+    t[2 * (lane - 3) + 1] = mkd(E.z, E.w);
+  }
+  return (DTab)(const double*)t;
+}
+
 // a stimulus whose effects stay on the workers it registered. Returns false (nothing
 // changed) when it needs every earlier stimulus retired first (needs scan mode).
 template <bool LW>
-__device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r, int qmode, bool exact) {
+__device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r, int qmode, bool exact, const uint4& E) {
   SCtl& S = L.c;
   const int lane = lane_id();
-  const uint4 E = lane < NE ? L.desc[s][lane] : make_uint4(0, 0, 0, 0);
+  const DTab durv = stim_durations(L, E);
   const int t = rl((int)E.x, 0), w = rl((int)E.y, 0), p = rl((int)E.z, 0);
   const uint32_t flags = rlu(E.w, 0);
   const int64_t nbt = mk64(rlu(E.x, 1), rlu(E.y, 1));
   const unsigned cnts = rlu(E.z, 1);
-  const int grp_t = rl((int)E.w, 1);
   const int kt = cnts & 0xff, nrel = (cnts >> 8) & 0xff, nf = (cnts >> 16) & 0xff;
   const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
-  const DTab durv = (DTab)(const double*)&L.desc[s][3];
   const int TD = E_HDR, RL0 = E_HDR + kt, FX0 = RL0 + nrel;
 #if DGP_PHASE_PROBES
   unsigned long long tph = mclk();
@@ -1721,7 +1725,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     const int ntch = L.ntouch[s];
     bool bad = false;
     if (lane < ntch) {
-      const int c = L.touch[s][lane];
+      const int c = L.touch[s][lane] & T_W;
       const uint32_t ctl = P.needs[(size_t)c * NLW + NLW - 1];
       bad = ctl == NL_OVF || (int)(ctl >> 8) + tot_new > NLW - 1 + NXW;
     }
@@ -1736,7 +1740,9 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   // ---- the touched workers' state, one lane each, in registers for the whole stimulus
   const int nt = L.ntouch[s];
   const bool tl = lane < nt;
-  const int cj = tl ? (int)L.touch[s][lane] : 0;
+  const int tv = tl ? (int)L.touch[s][lane] : 0;
+  const int cj = tv & T_W;
+  const bool candl = (tv & T_CAND) != 0;  // a holder of a frontier task's dependency
   int np = 0, nth = 1;
   WDict dj;
   dj.c = make_uint4(0, 0, 0, 0);
@@ -1798,10 +1804,22 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     const int64_t nb = mk64(rlu(E.z, RL0 + i), rlu(E.w, RL0 + i));
     if (tl && cj == h) nbj -= nb;
   }
+  // a release-only holder (ws.nbytes of a released dependency; no frontier candidate) is final
+  // now: written back and released before the frontier
+  bool released = false;  // this lane's worker was written back and released early
+  {
+    const bool ro = tl && !isw && !candl;
+    if (ballot(ro)) {
+      if (ro) P.nbytes[cj] = nbj;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (ro) release_worker<LW>(L, P, s, cj);
+      released = ro;
+    }
+  }
   phase(12);
   if (DGP_TRACE == 2 && lane == 0) TR(r, 4);
   // ------------------------------ frontier in ascending priority: decide_worker (:8550)
-  bool released = false;  // this lane's worker was written back and released early
   int off = FX0;
   for (int j = 0; j < nf; j++) {
     const int x = rl((int)E.x, off), px = rl((int)E.y, off), kx = rl((int)E.z, off) & 0xff;
@@ -1856,7 +1874,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       // is final now (the non-chosen candidates were only read, the release holders were
       // settled before the frontier). Write them back and release them before the commit,
       // so stimuli waiting only on them do not wait for it.
-      const bool early = tl && !isw && lane != jb;
+      const bool early = tl && !isw && lane != jb && !released;
       if (ballot(early)) {
         if (early) {
           using U4 = typename WPtr<LW>::template P<Q4>;
@@ -1870,7 +1888,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (early) release_worker<LW>(L, P, s, cj);
-        released = early;
+        released = released || early;
         if (DGP_TRACE == 1 && lane == 0) TR(r, 3);
       }
     }
@@ -1978,6 +1996,136 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   finish_slot(D, L, s, r, o, pops, false);
   phase(15);
   return true;
+}
+
+// ============================================================ single-worker runs
+// A run of consecutive stimuli r, r+1, ..., r+k-1 that each touch only worker w, place
+// nothing (empty frontier), whose dependencies w holds (no needs_what change) and whose
+// releases are on w, with the queue empty: each is the completion bookkeeping of one task
+// on w (_transition_processing_memory :2366-2442 -> _exit_processing_common :3258-3281 ->
+// WorkerState.remove_from_processing :759-771, add_replica :3148, the releases :3309-3314;
+// stimulus_queue_slots_maybe_opened :4983 finds no queued task). Each waits only for the
+// one before it on w, so one executor runs them back to back on w's state: one claim and
+// one release of w for the whole run instead of one per stimulus (the P2P-shuffle unpack
+// completions on the barrier's worker, C3). The same fp64 operations in the same order as
+// exe_local. Returns false (nothing done) when stimulus r itself is not of that form.
+template <bool LW>
+__device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r,
+                                                       const uint4& E) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  if (L.ntouch[s] != 1) return false;
+  const int w = rl((int)E.y, 0);
+  if (P.needs[(size_t)w * NLW + NLW - 1] != 0) return false;  // w needs no replica (needs_reset is a no-op)
+  // members: registered slots (guard dropped) whose stimulus r + k touches only w and waits
+  // only for its predecessor on w; lane k (k >= 1) gets the slot of r + k, k consecutive
+  const bool sl = lane < WIN && lane != s;
+  const long long offl = sl ? vload(&L.sid[lane]) - r : -1;
+  const bool el = sl && offl >= 1 && offl < 64 && vload(&L.pred[lane]) == 1 && vload(&L.ntouch[lane]) == 1 &&
+                  (L.touch[lane][0] & T_W) == w && (vload(&L.flags[lane]) & (F_GLOBAL | F_EXACT | F_SIMPLE)) == F_SIMPLE;
+  int my_slot = lane == 0 ? s : -1;
+  int n = 1;
+  while (n < 64) {
+    const unsigned long long m = ballot(el && offl == n);
+    if (!m) break;
+    if (lane == n) my_slot = __builtin_ctzll(m);
+    n++;
+  }
+  // each candidate's descriptor header (lane i: stimulus r + i); the dependency and release
+  // entries are read whether present or not (a row always holds NE entries)
+  uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0, ed = h0, er = h0, dq[4];
+  bool ok = false;
+  if (lane < n) {
+    const uint4* row = D.desc + (size_t)((r + lane) & (DR - 1)) * NE;
+    h0 = row[0];
+    h1 = row[1];
+    h2 = row[2];
+#pragma unroll
+    for (int q = 0; q < 4; q++) dq[q] = row[3 + q];
+    ed = row[E_HDR];
+    er = row[E_HDR + 1];
+  }
+  {
+    bool same = true;  // the resolved durations equal the head's (one table serves the run)
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      same = same && dq[q].x == rlu(E.x, 3 + q) && dq[q].y == rlu(E.y, 3 + q) && dq[q].z == rlu(E.z, 3 + q) &&
+             dq[q].w == rlu(E.w, 3 + q);
+    const int kt = h1.z & 0xff, nrel = (h1.z >> 8) & 0xff, nf = (h1.z >> 16) & 0xff;
+    const uint4 erel = kt == 0 ? ed : er;
+    ok = lane < n && (int)h0.y == w && !(h0.w & F_GLOBAL) && nf == 0 && kt <= 1 && nrel <= 1 &&
+         (kt == 0 || (int)ed.y == w) && (nrel == 0 || (int)erel.x == w) && same;
+    er = erel;
+  }
+  const unsigned long long bad = ballot(!ok);
+  const int k = (int)min((unsigned long long)n, (unsigned long long)__builtin_ctzll(bad | (1ull << 63)));
+  if (k == 0) return false;
+  // the members leave the window's wake-up protocol: the guard keeps them from becoming ready
+  if (lane >= 1 && lane < k) {
+    const int op = __hip_atomic_fetch_add(&L.pred[my_slot], BIG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (op != 1) serr(S, SERR_INV, 800000000 + (int)r);
+  }
+  // w's state, uniform in every lane; netocc does not change in the run
+  int np = P.nproc[w];
+  WDict dj = dict_load<LW>(P, w);
+  const int64_t net = P.netocc[w];
+  int64_t nbj = P.nbytes[w];
+  const double nbw = net_bw_of(net, D);
+  const DTab durv = stim_durations(L, E);
+  for (int i = 0; i < k; i++) {
+    const int t = rl((int)h0.x, i), p = rl((int)h0.z, i);
+    const uint32_t fl = rlu(h0.w, i);
+    const int64_t nbt = mk64(rlu(h1.x, i), rlu(h1.y, i));
+    const int nrel = (rlu(h1.z, i) >> 8) & 0xff;
+    const double dobs = mkd(rlu(h2.x, i), rlu(h2.y, i));
+    // processing -> memory: remove_from_processing, then the completion record (:2366)
+    dict_add(dj, p, -1);
+    np -= 1;
+    Out o;
+    o.nrec = 0;
+    o.npl = 0;
+    o.st0 = (size_t)((r + i) & (RS - 1)) * PLC;
+    o.rec(D, K_COMPLETE, w, p, 0, occ_dict_r(dj, nbw, durv, D), np, t, dobs);
+    // add_replica (:3148) and the release of a dependency held by w (:3309-3314)
+    nbj += (fl & F_SELFREL) ? 0 : nbt;
+    if (nrel) nbj -= mk64(rlu(er.z, i), rlu(er.w, i));
+  }
+  if (lane == 0) {
+    using U4 = typename WPtr<LW>::template P<Q4>;
+    P.nproc[w] = np;
+    st4(ascast<U4>(P.pcnt + (size_t)w * PD), dj.c);
+    st4(ascast<U4>(P.pcnt + (size_t)w * PD + 4), dj.c1);
+    P.plen[w] = dj.ord;
+    P.nbytes[w] = nbj;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): w's state is in LDS
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  // one release of w for the run: the stimulus after it on w counted one of the run's bits
+  SMask bits = 0;
+  for (int i = 0; i < k; i++) bits |= 1ull << rl(my_slot, i);
+  if (lane == 0)
+    release_succ(L, __hip_atomic_fetch_and(&P.mask[w], ~bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bits);
+  // retire every member: counts, then done, then the slots are free
+  const int q = (int)((r + lane) & (RS - 1));
+  if (lane < k) {
+    RMeta me;
+    me.npl = 0;
+    me.nrec = 1;
+    me.npops = 0;
+    me.direct = 0;
+    me.pad = 0;
+    L.rmeta[q] = me;
+  }
+  __threadfence_block();
+  if (lane < k) vstore(&L.rdone[q], r + lane + 1);
+  if (lane == 0) atomicOr(&S.freem, bits);
+  PROF(if (lane == 0) { S.prof[11] += 1; S.prof[12] += k; });
+  return true;
+}
+
+template <bool LW>
+__device__ __attribute__((noinline)) bool exe_run_entry(int s, long long r, uint4 E) {
+  return exe_run<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r, E);
 }
 
 // wave argmin over all workers of a key computed per worker (global stimuli)
@@ -2089,12 +2237,12 @@ template <bool LW>
 __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r) {
   SCtl& S = L.c;
   const int lane = lane_id();
-  const uint4 E = lane < NE ? L.desc[s][lane] : make_uint4(0, 0, 0, 0);
+  const uint4 E = lane < NE ? D.desc[(size_t)(r & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
+  const DTab durv = stim_durations(L, E);
   const int t = rl((int)E.x, 0), w = rl((int)E.y, 0), p = rl((int)E.z, 0);
   const int64_t nbt = mk64(rlu(E.x, 1), rlu(E.y, 1));
   const int grp_t = rl((int)E.w, 1);
   const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
-  const DTab durv = (DTab)(const double*)&L.desc[s][3];
   WState g;
   ws_load(S, g);
   const long long lpos = S.log_len;
@@ -2508,7 +2656,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
   unsigned long long idle28 = 0, idle29 = 0;
   while (true) {
     if (vload(&S.stop)) break;
-    const unsigned m = vload(&S.ready);
+    const SMask m = vload(&S.ready);
     if (!m) {
       const unsigned long long n = mclk();  // 28: executor idle, nothing ready
       idle28 += n - t_idle;
@@ -2518,29 +2666,33 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     }
     // the ready slots in stimulus order (oldest first): lane i holds slot i's key
     const long long sp = vload(&S.seq_pos);
-    const bool rdl = lane < WIN && ((m >> lane) & 1u);
+    const bool rdl = lane < WIN && ((m >> lane) & 1ull);
     const long long rsl = rdl ? vload(&L.sid[lane]) : 0;
     const uint32_t fsl = rdl ? vload(&L.flags[lane]) : 0u;
-    unsigned key = rdl ? (unsigned)(((rsl - sp) << 5) | lane) : ~0u;  // r - sp < RS
+    unsigned key = rdl ? (unsigned)(((rsl - sp) << 6) | lane) : ~0u;  // r - sp < RS
     int cs = -1, cq = 0;
     long long cr = -1;
     uint32_t cf = 0;
     bool cex = false;
+    uint4 E = make_uint4(0, 0, 0, 0);
     while (true) {
-      unsigned kmin = key;
-      for (int o = 32; o > 0; o >>= 1) kmin = min(kmin, (unsigned)__shfl_xor((int)kmin, o));
+      const unsigned kmin = wmin_u32(key);
       if (kmin == ~0u) break;
-      const int s = (int)(kmin & 31u);
+      const int s = (int)(kmin & 63u);
       if (lane == s) key = ~0u;  // tried
-      if (!G && (rlu(fsl, s) & F_GLOBAL)) continue;  // left to the global-capable executor
+      if (!G && (rlu(fsl, s) & (F_GLOBAL | F_RUNM))) continue;  // left to the global-capable executor
+      // the descriptor of the slot's stimulus (global ring) is in flight while the claim completes
+      const long long rs = (long long)rl64((uint64_t)rsl, s);
+      E = lane < NE ? D.desc[(size_t)(rs & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
       // claim first, then read the slot: between the scan and the claim its stimulus may
       // have run and retired and the slot been registered again (another stimulus)
-      unsigned old = 0;
-      if (lane == 0) old = atomicAnd(&S.ready, ~(1u << s));
-      old = rlu(old, 0);
-      if (!((old >> s) & 1u)) continue;
+      SMask old = 0;
+      if (lane == 0) old = atomicAnd(&S.ready, ~(1ull << s));
+      old = rl64(old, 0);
+      if (!((old >> s) & 1ull)) continue;
       lds_fence();
       const long long r = vload(&L.sid[s]);
+      if (r != rs) E = lane < NE ? D.desc[(size_t)(r & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
       const uint32_t fl = vload(&L.flags[s]);
       bool exact = (fl & (F_GLOBAL | F_EXACT)) != 0;
       int qm = 0;  // 0 no refill, 1 every open slot is refilled, 2/3 the queue length decides
@@ -2557,7 +2709,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
         if (qm != 0) qm = 3;
       }
       if (!ok) {  // not runnable by this executor now: give the slot back
-        if (lane == 0) atomicOr(&S.ready, 1u << s);
+        if (lane == 0) atomicOr(&S.ready, 1ull << s);
         continue;
       }
       cs = s;
@@ -2585,10 +2737,12 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     if (G && (cf & F_GLOBAL)) {
       exe_global_entry<LW>(cs, cr);
       PROF(if (lane == 0) S.prof[9]++);
-    } else if (!exe_local<LW>(D, L, P, cs, cr, cq, cex)) {
+    } else if (G && (cf & F_SIMPLE) && cq == 0 && !cex && exe_run_entry<LW>(cs, cr, E)) {
+      // a run of single-worker completions, back to back (only this executor calls out of line)
+    } else if (!exe_local<LW>(D, L, P, cs, cr, cq, cex, E)) {
       if (lane == 0) {
         atomicOr(&L.flags[cs], F_EXACT);
-        atomicOr(&S.ready, 1u << cs);
+        atomicOr(&S.ready, 1ull << cs);
         PROF(S.prof[10]++);
       }
     }
@@ -2676,7 +2830,6 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // ------------------------------------------------------------------ set-up
   workers_io<LW>(D, P, true);
-  for (int i = tid; i < WIN * NE; i += blockDim.x) (&L.desc[0][0])[i] = make_uint4(0, 0, 0, 0);
   for (int i = tid; i < RS; i += blockDim.x) L.rdone[i] = -1;
   if (tid < WIN) {
     L.pred[tid] = BIG;
@@ -2696,7 +2849,7 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     S.global_pending = 0;
     S.busy_exe = 0;
     S.ready = 0;
-    S.freem = WIN == 32 ? 0xffffffffu : ((1u << (WIN & 31)) - 1u);
+    S.freem = ~0ull >> (64 - WIN);
     S.seq_pos = pos->seq;
     S.log_len = (long long)c->n_placed;
     S.rec_len = pos->rec_len;
@@ -2813,7 +2966,9 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     c->g_netocc = S.g_netocc;
     c->n_idle = S.n_idle;
     c->n_sat = S.n_sat;
-    for (int i = 0; i < PD && i < D.P; i++) D.pdur_walk[i] = S.wdur[i];
+    // the durations as of the last folded record (the walker drains the record log before
+    // the launch ends): what the host-side snapshot and the next launch's globals read
+    for (int i = 0; i < PD && i < D.P; i++) D.pdur_walk[i] = D.pdur_cur[i] = S.wdur[i];
     if (S.error && !c->error) {
       c->error = S.error;
       c->err_task = S.err_task;

@@ -327,7 +327,7 @@ dgp_engine* dgp_create(int device) {
     int rc = 0;
     rc |= dalloc(e, &e->D.desc, (size_t)S::DR * S::NE, e->allocs);
     rc |= dalloc(e, &e->D.touch_ring, (size_t)S::DR * S::TMAX, e->allocs);
-    rc |= dalloc(e, &e->D.desc_tag, (size_t)S::DR, e->allocs);
+    rc |= dalloc(e, &e->D.thdr, (size_t)S::DR, e->allocs);
     rc |= dalloc(e, &e->D.s2_task, st, e->allocs);
     rc |= dalloc(e, &e->D.s2_worker, st, e->allocs);
     rc |= dalloc(e, &e->D.s2_comm, st, e->allocs);
@@ -544,6 +544,7 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
   rc |= dalloc(e, &D.frontier, N, L);
   rc |= dalloc(e, &D.pdur_cur, n_prefixes, L);
   rc |= dalloc(e, &D.pdur_walk, n_prefixes, L);
+  rc |= dalloc(e, &D.pdur_pre, n_prefixes, L);
   rc |= dalloc(e, &D.pmaxexec, n_prefixes, L);
   rc |= dalloc(e, &D.durv, (size_t)N * n_prefixes, L);
   rc |= dalloc(e, &D.g_size, n_groups, L);
@@ -700,7 +701,7 @@ int dgp_reset(dgp_engine* e) {
     HIPCHK(e, hipMemsetAsync(D.holder_of, 0xff, N * 4, s));
     HIPCHK(e, hipMemsetAsync(D.fr_mark, 0xff, N * 4, s));
     HIPCHK(e, hipMemsetAsync(D.rel_mark, 0xff, N * 4, s));
-    HIPCHK(e, hipMemsetAsync(D.desc_tag, 0xff, (size_t)S::DR * 8, s));
+    HIPCHK(e, hipMemsetAsync(D.thdr, 0, (size_t)S::DR * sizeof(uint2), s));
     HIPCHK(e, hipMemsetAsync(D.gw_needs_ext, 0, (size_t)D.W * S::NXW * 4, s));
     HIPCHK(e, hipMemsetAsync(D.gw_needs_saved, 0, (size_t)D.W * S::NLW * 4, s));
     S::Pos p0{};
@@ -715,6 +716,7 @@ int dgp_reset(dgp_engine* e) {
   std::vector<double> maxexec(D.P, -1.0);
   HIPCHK(e, hipMemcpyAsync(D.pdur_cur, e->prefix_defaults.data(), D.P * 8, hipMemcpyHostToDevice, s));
   HIPCHK(e, hipMemcpyAsync(D.pdur_walk, e->prefix_defaults.data(), D.P * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(e, hipMemcpyAsync(D.pdur_pre, e->prefix_defaults.data(), D.P * 8, hipMemcpyHostToDevice, s));
   HIPCHK(e, hipMemcpyAsync(D.pmaxexec, maxexec.data(), D.P * 8, hipMemcpyHostToDevice, s));
   HIPCHK(e, hipMemcpyAsync(D.g_relwait, e->group_sizes.data(), D.G * 8, hipMemcpyHostToDevice, s));
   HIPCHK(e, hipMemsetAsync(D.g_left, 0, D.G * 8, s));

@@ -3,30 +3,50 @@
     python tools/pmc_traffic.py gpurun_out/<tag> profiles/hbm_traffic.json [n_tasks n_workers]
 
 Reads <dir>/pmc_FETCH_SIZE/**/*counter_collection.csv and the WRITE_SIZE twin (one counter
-per pass: FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2), keeps the dispatches of `k_stream`
-and prices them per the MI355X guide's gfx950 correction: FETCH_SIZE (KiB) reports half
-the bytes of a read, so hbm = (2 * FETCH_SIZE + WRITE_SIZE) * 1024. bench.py reports the
-result as roofline.traffic when its workload matches.
+per pass: FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2), keeps the longest dispatch of
+`k_stream` (the replay; bench.py's link-latency probe launches short ones too) and prices it
+per the MI355X guide's gfx950 correction: FETCH_SIZE (KiB) reports half the bytes of a read,
+so hbm = (2 * FETCH_SIZE + WRITE_SIZE) * 1024. The engine sources' hash is recorded: bench.py
+reports the result as roofline.traffic only for the workload and the sources it was measured on.
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def engine_source_hash() -> str:
+    """sha256 over the HIP sources of libdgplace.so (bench.py computes the same)."""
+    h = hashlib.sha256()
+    csrc = os.path.join(REPO, "distributed_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".h", ".hip")):
+            h.update(f.encode())
+            h.update(open(os.path.join(csrc, f), "rb").read())
+    return h.hexdigest()
+
 
 def counter(d: str, name: str, kernel: str = "k_stream") -> list:
+    """[value] of the longest dispatch of `kernel` (one per file if several files)."""
     files = glob.glob(os.path.join(d, f"pmc_{name}", "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter csv under {d}/pmc_{name}")
-    per = {}
+    out = []
     for f in files:
+        per, dur = {}, {}
         for row in csv.DictReader(open(f)):
             if kernel not in row.get("Kernel_Name", "") or row.get("Counter_Name") != name:
                 continue
-            key = (f, row.get("Dispatch_Id") or row.get("Correlation_Id"))
+            key = row.get("Dispatch_Id") or row.get("Correlation_Id")
             per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
-    return list(per.values())
+            dur[key] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+        if per:
+            out.append(per[max(dur, key=dur.get)])
+    return out
 
 
 def main():
@@ -41,8 +61,11 @@ def main():
            "launches": {"FETCH_SIZE": len(fetch), "WRITE_SIZE": len(write)},
            "fetch_size_kib_per_launch": f_kib, "write_size_kib_per_launch": w_kib,
            "traffic_bytes_per_launch": (2 * f_kib + w_kib) * 1024,
-           "correction": "gfx950: FETCH_SIZE doubled (MI355X_MICROARCH.md HBM section)",
-           "source": os.path.relpath(d)}
+           "read_bytes_per_launch": 2 * f_kib * 1024, "write_bytes_per_launch": w_kib * 1024,
+           "correction": "gfx950: FETCH_SIZE doubled (MI355X_MICROARCH.md HBM section); calibrated on this "
+                         "kernel's own patterns in profiles/r02_calibration/calibration.json",
+           "src_sha256": engine_source_hash(),
+           "source": os.path.relpath(d, REPO) if os.path.isabs(d) else d}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
