@@ -319,6 +319,8 @@ struct SLds {
   RMeta rmeta[RS];            // retire ring: counts of finished stimulus r at r & (RS - 1)
   long long rdone[RS];        // ... and r + 1 once they are final
   uint16_t pre_scr[64][TMAX]; // prefetcher scratch: each lane's distinct-worker list
+  int32_t bld_jobs[256];      // builder: wide rows deferred to the whole wave (kind << 28 | task)
+  int32_t bld_njobs;
   SCtl c;
 };
 
@@ -945,32 +947,90 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
 }
 
 // ======================================================================= builder
-// completions [a, e) (one per lane): the waiting_on / waiters decrements
-__device__ __attribute__((always_inline)) void bld_range(const Dev& D, long long a, long long e) {
-  const long long r = a + lane_id();
-  if (r >= e) return;
-  const int t = D.stim_task[r];
-  const int w = D.stim_worker[r];
-  // the replica this completion creates (who_has, :3148)
-  atomicOr(&D.holders[(size_t)t * D.WB + (w >> 6)], 1ull << (w & 63));
-  const int64_t f0 = D.dpt_ptr[t], f1 = D.dpt_ptr[t + 1];
-  for (int64_t k = f0; k < f1; k++) {  // waiting_on.discard (:3298-3307)
-    const int x = D.dpt_idx[k];
-    if (atomicSub(&D.remaining[x], 1) == 1) {
-      int s = -1;  // the stimulus that empties waiting_on: the dependency completed last
-      for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++) s = max(s, D.cseq[D.dep_idx[q]]);
-      D.fr_mark[x] = s;
+// completions [a, e) (one per lane): the waiting_on / waiters decrements. A row wider than
+// BLD_NARROW (a completion with many dependents or dependencies: the shuffle barrier's
+// 66,666; a task whose fan-in / fan-out max is wide) would be one lane's serial chain of
+// dependent loads, so it becomes a job the whole wave takes 64 entries at a time.
+constexpr int BLD_NARROW = 32;
+constexpr int BLD_JOBS = 256;
+enum : int { BJ_COMPLETE = 0, BJ_FRMARK = 1, BJ_RELMARK = 2 };
+
+__device__ __forceinline__ bool bld_push(SLds& L, int kind, int x) {
+  const int j = atomicAdd(&L.bld_njobs, 1);
+  if (j >= BLD_JOBS) return false;  // full: the caller does it itself
+  L.bld_jobs[j] = (kind << 28) | x;
+  return true;
+}
+// the stimulus that empties x's waiting_on: its dependency completed last (one lane)
+__device__ __forceinline__ int fr_of(const Dev& D, int x) {
+  int s = -1;
+  for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++) s = max(s, D.cseq[D.dep_idx[q]]);
+  return s;
+}
+// the stimulus that empties d's waiters: its dependent completed last (one lane)
+__device__ __forceinline__ int rel_of(const Dev& D, int d) {
+  int s = -1;
+  for (int64_t q = D.dpt_ptr[d]; q < D.dpt_ptr[d + 1]; q++) s = max(s, D.cseq[D.dpt_idx[q]]);
+  return s;
+}
+// waiting_on.discard for dependent x of a completion (:3298-3307) and waiters.discard ->
+// release for dependency d (:3309-3314); the lane that empties the set marks the stimulus
+__device__ __forceinline__ void bld_dec_dependent(const Dev& D, SLds& L, int x) {
+  if (atomicSub(&D.remaining[x], 1) == 1) {
+    if (D.dep_ptr[x + 1] - D.dep_ptr[x] <= BLD_NARROW || !bld_push(L, BJ_FRMARK, x)) D.fr_mark[x] = fr_of(D, x);
+  }
+}
+__device__ __forceinline__ void bld_dec_dependency(const Dev& D, SLds& L, int d) {
+  if (atomicSub(&D.waiters[d], 1) == 1 && !(D.tflags[d] & TF_WANTED)) {
+    if (D.dpt_ptr[d + 1] - D.dpt_ptr[d] <= BLD_NARROW || !bld_push(L, BJ_RELMARK, d)) D.rel_mark[d] = rel_of(D, d);
+  }
+}
+
+__device__ __attribute__((always_inline)) void bld_range(const Dev& D, SLds& L, long long a, long long e) {
+  const int lane = lane_id();
+  const long long r = a + lane;
+  if (r < e) {
+    const int t = D.stim_task[r];
+    const int w = D.stim_worker[r];
+    // the replica this completion creates (who_has, :3148)
+    atomicOr(&D.holders[(size_t)t * D.WB + (w >> 6)], 1ull << (w & 63));
+    const int64_t f0 = D.dpt_ptr[t], f1 = D.dpt_ptr[t + 1], k0 = D.dep_ptr[t], k1 = D.dep_ptr[t + 1];
+    if ((f1 - f0 > BLD_NARROW || k1 - k0 > BLD_NARROW) && bld_push(L, BJ_COMPLETE, t)) {
+      // the wave takes it below
+    } else {
+      for (int64_t k = f0; k < f1; k++) bld_dec_dependent(D, L, D.dpt_idx[k]);
+      for (int64_t k = k0; k < k1; k++) bld_dec_dependency(D, L, D.dep_idx[k]);
     }
   }
-  const int64_t k0 = D.dep_ptr[t], k1 = D.dep_ptr[t + 1];
-  for (int64_t k = k0; k < k1; k++) {  // waiters.discard -> release (:3309-3314)
-    const int d = D.dep_idx[k];
-    if (atomicSub(&D.waiters[d], 1) == 1 && !(D.tflags[d] & TF_WANTED)) {
-      int s = -1;
-      for (int64_t q = D.dpt_ptr[d]; q < D.dpt_ptr[d + 1]; q++) s = max(s, D.cseq[D.dpt_idx[q]]);
-      D.rel_mark[d] = s;
+  // the wide rows, 64 entries at a time (jobs may add jobs: a wide completion empties a
+  // wide task)
+  lds_fence();
+  int done = 0;
+  while (true) {
+    const int nj = min(vload(&L.bld_njobs), BLD_JOBS);
+    if (done >= nj) break;
+    for (int j = done; j < nj; j++) {
+      const int code = L.bld_jobs[j];
+      const int kind = code >> 28, x = code & 0x0fffffff;
+      if (kind == BJ_COMPLETE) {
+        const int64_t f0 = D.dpt_ptr[x], f1 = D.dpt_ptr[x + 1], k0 = D.dep_ptr[x], k1 = D.dep_ptr[x + 1];
+        for (int64_t k = f0 + lane; k < f1; k += 64) bld_dec_dependent(D, L, D.dpt_idx[k]);
+        for (int64_t k = k0 + lane; k < k1; k += 64) bld_dec_dependency(D, L, D.dep_idx[k]);
+      } else {
+        const bool fr = kind == BJ_FRMARK;
+        const int64_t q0 = fr ? D.dep_ptr[x] : D.dpt_ptr[x], q1 = fr ? D.dep_ptr[x + 1] : D.dpt_ptr[x + 1];
+        int m = -1;
+        for (int64_t q = q0 + lane; q < q1; q += 64) m = max(m, D.cseq[fr ? D.dep_idx[q] : D.dpt_idx[q]]);
+        m = wmax(m);
+        if (lane == 0) (fr ? D.fr_mark : D.rel_mark)[x] = m;
+      }
+      lds_fence();
     }
+    done = nj;
   }
+  wbar();
+  if (lane == 0) L.bld_njobs = 0;
+  lds_fence();
 }
 
 // ==================================================================== prefetcher
@@ -1035,11 +1095,12 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
       nrel++;
     }
   }
-  for (int64_t k = f0; k < f1; k++) {  // dependents in ascending priority = frontier order
+  // dependents in ascending priority = frontier order; a global stimulus walks its frontier
+  // itself (exe_global), so the walk stops there
+  for (int64_t k = f0; k < f1 && !(flags & F_GLOBAL); k++) {
     const int x = D.dpt_idx[k];
     if (D.fr_mark[x] != (int)r) continue;
     nf++;
-    if (flags & F_GLOBAL) continue;
     const int64_t x0 = D.dep_ptr[x], x1 = D.dep_ptr[x + 1];
     const int kx = (int)(x1 - x0);
     if ((D.tflags[x] & TF_ROOTISH) || kx > KX_MAX || n + 1 + kx > NE) {
@@ -1103,7 +1164,7 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
     lds_fence();
     const unsigned long long t0 = mclk();
     if (KIND == 0) {
-      bld_range(D, a, e);
+      bld_range(D, L, a, e);
     } else {
       const long long r = a + lane;
       int pl = 0;
@@ -2843,6 +2904,7 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     D.holder_of[tk] = D.pl_worker[i];
   }
   if (tid == 0) {
+    L.bld_njobs = 0;
     S.stop = 0;
     S.error = 0;
     S.err_task = -1;
