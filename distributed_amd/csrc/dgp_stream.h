@@ -3061,5 +3061,73 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
   }
 }
 
+// ================================================================ steal confirmation
+// WorkStealing.move_task_confirm, the "confirm" branch (stealing.py:376-384, the finally
+// clause :396-399) on the engine state between launches (service mode): processing task t
+// leaves its worker v (WorkerState.remove_from_processing :759-771: prefix counts, the
+// needs_what of its dependencies -> network occupancy, _task_prefix_count_global) for the
+// thief h (add_to_processing :733-745), then check_idle_saturated(h) and (v) (:2949-2995)
+// with the current total occupancy. The task keeps its placement-log position as its run
+// identity (the caller maps the new compute-task's run_id to it). One wave.
+__global__ void __launch_bounds__(64) k_move_task(const Dev* __restrict__ Dp, int t, int h) {
+  const Dev& D = *Dp;
+  __shared__ SCtl S;  // needs_dec / needs_inc report inconsistencies through it
+  const int lane = lane_id();
+  if (lane == 0) {
+    S.error = 0;
+    S.err_task = -1;
+    S.stop = 0;
+  }
+  __syncthreads();
+  const int v = D.proc_on[t];
+  if (D.state[t] != S_PROCESSING || v < 0 || v >= D.W || v == h) {
+    if (lane == 0) set_error(D, ERR_BAD_STATE, t);
+    return;
+  }
+  const int p = D.prefix[t];
+  const int64_t k0 = D.dep_ptr[t], k1 = D.dep_ptr[t + 1];
+  // victim: the dependencies it needed a replica of (not held there) are needed less
+  uint32_t nl = lane < NLW ? D.gw_needs_saved[(size_t)v * NLW + lane] : 0u;
+  int64_t freed = 0;
+  for (int64_t k = k0; k < k1; k++) {
+    const int d = D.dep_idx[k];
+    if (D.holder_of[d] == v) continue;
+    freed += needs_dec(D, S, v, nl, d, nbv(D, D.res_nbytes[d]), t);
+  }
+  const int npv = D.w_nproc[v] - 1;
+  if (npv == 0) needs_reset(D, v, nl);
+  if (lane < NLW) D.gw_needs_saved[(size_t)v * NLW + lane] = nl;
+  // thief: a replica of each dependency it does not hold is needed
+  uint32_t nh = lane < NLW ? D.gw_needs_saved[(size_t)h * NLW + lane] : 0u;
+  int64_t added = 0;
+  for (int64_t k = k0; k < k1; k++) {
+    const int d = D.dep_idx[k];
+    if (D.holder_of[d] == h) continue;
+    added += needs_inc(D, S, h, nh, d, nbv(D, D.res_nbytes[d]), t);
+  }
+  if (lane < NLW) D.gw_needs_saved[(size_t)h * NLW + lane] = nh;
+  __threadfence();
+  if (lane == 0) {
+    Ctl* c = D.ctl;
+    wdict_dec(D, v, p);  // remove_from_processing: worker dict, then the global one
+    D.w_nproc[v] = npv;
+    D.w_netocc[v] -= freed;
+    gdict_dec(D, p);
+    if (!wdict_inc(D, h, p)) set_error(D, ERR_PREFIX_CAP, t);  // add_to_processing
+    D.w_nproc[h] += 1;
+    D.w_netocc[h] += added;
+    if (!gdict_inc(D, p)) set_error(D, ERR_GPREFIX_CAP, t);
+    c->g_netocc += (double)(added - freed);  // integers < 2^53: exact in any order
+    D.proc_on[t] = h;
+    D.holder_of[t] = h;
+    for (int i = 0; i < 2; i++) {  // check_idle_saturated(thief), then (victim)
+      const int w = i == 0 ? h : v;
+      walk_flags(D, w, occupancy(D, w, D.pdur_walk), D.w_nproc[w]);
+      itc_check(D, w, false);
+    }
+    if (S.error) set_error(D, S.error, S.err_task);
+  }
+}
+
 }  // namespace st
 }  // namespace dgp

@@ -846,6 +846,22 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
   return 0;
 }
 
+int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief) {
+  if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
+  if (!(e->D.P <= dgp::st::PD && !e->D.restr_flags))
+    return fail(e, DGP_E_STATE, "dgp_move_task: the round-kernel engine (more than 8 prefixes, or restrictions) "
+                                "has no steal confirmation");
+  if (task < 0 || task >= e->D.N || thief < 0 || thief >= e->D.W)
+    return fail(e, DGP_E_ARG, "dgp_move_task: task or thief out of range");
+  HIPCHK(e, hipSetDevice(e->device));
+  e->mode = 2;
+  if (int rc = sync_dev(e)) return rc;
+  hipLaunchKernelGGL(dgp::st::k_move_task, dim3(1), dim3(64), 0, e->stream, e->d_dev, task, thief);
+  HIPCHK(e, hipGetLastError());
+  return check_device_error(e);
+}
+
 int dgp_snapshot(dgp_engine* e) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->snap_rounds <= 0) return fail(e, DGP_E_STATE, "snapshots not enabled");

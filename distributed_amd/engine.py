@@ -178,6 +178,11 @@ class PlacementEngine:
                                                 _ptr(st), C.byref(newp)), "dgp_tasks_finished")
         return st, int(newp.value)
 
+    def move_task(self, task: int, thief: int):
+        """Steal confirmation (WorkStealing.move_task_confirm, distributed/stealing.py
+        :376-384): processing ``task`` moves from its worker to ``thief`` on the device."""
+        self._check(self.lib.dgp_move_task(self.h, int(task), int(thief)), "dgp_move_task")
+
     def snapshot(self):
         """Append one per-worker snapshot (service mode round boundary)."""
         self._check(self.lib.dgp_snapshot(self.h), "dgp_snapshot")

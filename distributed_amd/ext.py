@@ -22,6 +22,10 @@ How it plugs in (the reference's interfaces, ``/root/reference/distributed/``):
   ``decide_worker_rootish_queuing_enabled / _disabled`` / ``decide_worker_non_rootish``
   (``:2135-2311``); everything after the decision is the reference's own code
   (``_add_to_processing`` :3199, ``_task_to_msg`` :3421).
+* ``stream_handlers["steal-response"]`` (``stealing.py:121``): the stealing extension's
+  ``move_task_confirm`` (``:333-399``) runs as before; when it moved a processing task to
+  the thief (the "confirm" branch ``:376-384``) the engine moves it too (``dgp_move_task``),
+  so the device state follows confirmed steals.
 * ``stream_handlers["task-finished"]`` (``:3769``): each message goes to the engine first
   (``dgp_tasks_finished``: stale / duplicate checks, completion, frontier release,
   frontier placement and queue refill on the device), then to the reference
@@ -182,6 +186,49 @@ class GPUPlacementExtension(SchedulerPlugin):
         handlers = getattr(s, "stream_handlers", None)
         if handlers is not None:
             handlers["task-finished"] = self.handle_task_finished
+        self._wrap_stealing()
+
+    def _wrap_stealing(self):
+        """Follow confirmed steals: wrap the stealing extension's ``move_task_confirm``
+        (stealing.py:333-399), which is also its ``steal-response`` stream handler (:121)."""
+        s = self.scheduler
+        st = (getattr(s, "extensions", None) or {}).get("stealing")
+        if st is None or getattr(st, "_gpu_placement_wrapped", False):
+            return
+        orig = st.move_task_confirm
+
+        async def move_task_confirm(*, key, state, stimulus_id, worker=None):
+            ts = s.tasks.get(key)
+            before = ts.processing_on if ts is not None and ts.state == "processing" else None
+            try:
+                await orig(key=key, state=state, stimulus_id=stimulus_id, worker=worker)
+            finally:
+                ts = s.tasks.get(key)
+                if before is not None and ts is not None:
+                    if ts.state == "processing" and ts.processing_on is not None and ts.processing_on is not before:
+                        self.task_moved(ts, ts.processing_on)
+                    elif ts.state != "processing":  # "reschedule" (:365-376): not modelled on the device
+                        self.fallback(f"steal of {key!r} rescheduled it")
+
+        st.move_task_confirm = move_task_confirm
+        if getattr(s, "stream_handlers", None) is not None and "steal-response" in s.stream_handlers:
+            s.stream_handlers["steal-response"] = move_task_confirm
+        st._gpu_placement_wrapped = True
+
+    def task_moved(self, ts, thief):
+        """A confirmed steal moved processing ``ts`` to ``thief`` (a WorkerState)."""
+        if not self.active or self.engine is None:
+            return
+        t = self.task_index.get(ts.key)
+        w = self.worker_index.get(thief.address)
+        if t is None or w is None:
+            self.fallback(f"steal of {ts.key!r} to {thief.address}: not in the engine's tables")
+            return
+        try:
+            self.engine.move_task(t, w)
+            self.stats["steals_confirmed"] += 1
+        except Exception as e:
+            self.fallback(f"move_task: {e}")
 
     def fallback(self, reason: str):
         """Stop asking the engine; the scheduler continues on its own decisions."""

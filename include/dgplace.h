@@ -21,6 +21,8 @@
  *                         _transition(key, "memory") -> _transitions ->
  *                         stimulus_queue_slots_maybe_opened (:4983). Engine state stays
  *                         resident between calls (service mode)
+ *   dgp_move_task         WorkStealing.move_task_confirm, "confirm" branch (stealing.py:333-399,
+ *                         :376-384): a processing task moves from its worker to the thief
  *   dgp_snapshot          one per-worker snapshot (occupancy, nbytes, processing, idle /
  *                         saturated / idle_task_count, queue length) at a caller-chosen point
  *   dgp_run_rounds        the synthetic executor of the replay protocol: round k completes
@@ -40,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 4
+#define DGP_ABI_VERSION 5
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -131,6 +133,16 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out);
 int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* run_id,
                        const int64_t* nbytes, const double* start, const double* stop, int8_t* status,
                        int64_t* n_new_placements);
+
+/* Steal confirmation (WorkStealing.move_task_confirm, stealing.py:333-399, its "confirm"
+ * branch :376-384 and finally clause :396-399): processing task `task` leaves its worker
+ * (the victim: WorkerState.remove_from_processing, scheduler.py:759-771) for `thief`
+ * (add_to_processing :733-745): prefix counts, needs_what / network occupancy and the
+ * scheduler-global prefix counts, then check_idle_saturated(thief) and (victim). The task
+ * keeps its placement-log position as its run identity: its later task-finished message
+ * comes from the thief with that run_id (dgp_tasks_finished). Service mode, graphs on the
+ * stream engine (<= 8 prefixes, no restrictions); DGP_E_DEVICE if the task is not processing. */
+int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief);
 
 /* Append one worker snapshot (needs dgp_enable_snapshots): round index = number of calls
  * (update_graph's snapshot is round 0). */

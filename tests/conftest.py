@@ -15,8 +15,13 @@ def pytest_configure(config):
 
 
 def golden_files():
-    """Placement replay fixtures (tests/golden/gen_golden.py)."""
-    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("steal_"))
+    """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith(("steal_", "svc_steal_")))
+
+
+def svc_steal_files():
+    """Service-mode message streams with confirmed steals (tests/golden/gen_service.py)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svc_steal_") and f.endswith(".npz"))
 
 
 def steal_files():

@@ -24,6 +24,15 @@ answer, classified as in ``include/dgplace.h`` ``DGP_TF_*``:
 Injected messages never change scheduler state (same-worker duplicates are idempotent in
 ``WorkerState.add_replica`` :829-830), so the placement log and the per-round snapshots
 equal those of the plain replay; both are stored and checked.
+
+With ``p_steal`` (the ``svc_steal_*`` fixtures) confirmed steals are interleaved too:
+before a message, a processing task moves to another worker exactly as
+``WorkStealing.move_task_confirm``'s "confirm" branch does it (distributed/stealing.py
+:376-384 and the finally clause :396-399: remove_from_processing on the victim,
+add_to_processing on the thief, a new compute-task via ``send_task_to_worker``,
+check_idle_saturated of thief and victim). The steals change the later placements; the
+fixture stores them (``steal_msg`` = index of the message they precede, ``steal_task``,
+``steal_thief``) with the placement log and snapshots they lead to.
 """
 from __future__ import annotations
 
@@ -45,7 +54,7 @@ import numpy as np  # noqa: E402
 ACCEPTED, FREE_KEYS, ADD_KEYS, RELEASE, UNKNOWN_WORKER = 0, 1, 2, 3, 4
 
 
-def replay_service(g, cfg, seed, p_inject=0.35):
+def replay_service(g, cfg, seed, p_inject=0.35, p_steal=0.0):
     from distributed.scheduler import Scheduler
 
     s, tss, widx, rec, tidx = G.build_state(g, cfg)
@@ -78,8 +87,32 @@ def replay_service(g, cfg, seed, p_inject=0.35):
     rounds, nplaced = [], []
     done = 0
     completed = []  # tasks accepted so far (duplicates are drawn from these)
+    ran_on = {}     # task -> the worker its accepted completion came from
 
-    def send(t, w, run_id, nbytes, start, stop):
+    steals = {"msg": [], "task": [], "thief": []}
+    stolen = set()
+
+    def steal():
+        """WorkStealing.move_task_confirm, confirm branch (stealing.py:376-384, :396-399)."""
+        proc = [ts for ts in s.tasks.values() if ts.state == "processing"]
+        if not proc or W < 2:
+            return
+        ts = proc[int(rng.integers(0, len(proc)))]
+        victim = ts.processing_on
+        h = (widx[victim.address] + 1 + int(rng.integers(0, W - 1))) % W
+        thief = s.workers[addr[h]]
+        ts.processing_on = thief
+        victim.remove_from_processing(ts)
+        thief.add_to_processing(ts)
+        s._task_to_msg(ts)  # send_task_to_worker: the thief's compute-task, a new run_id
+        s.check_idle_saturated(thief)
+        s.check_idle_saturated(victim)
+        steals["msg"].append(len(msgs["task"]))
+        steals["task"].append(tidx[ts.key])
+        steals["thief"].append(h)
+        stolen.add(tidx[ts.key])
+
+    def send(t, w, run_id, nbytes, start, stop, ref_run=None):
         """One task-finished message through the reference; returns its class."""
         msgs["task"].append(t)
         msgs["worker"].append(w)
@@ -96,7 +129,7 @@ def replay_service(g, cfg, seed, p_inject=0.35):
             sid = f"task-finished-{len(msgs['task'])}"
             k0 = called["add_keys"]
             r, cm, wm = s.stimulus_task_finished(
-                key, addr[w], sid, run_id + run0, nbytes=nbytes, type=None, typename="int", metadata=None,
+                key, addr[w], sid, run_id + run0 if ref_run is None else ref_run, nbytes=nbytes, type=None, typename="int", metadata=None,
                 startstops=[{"action": "compute", "start": start, "stop": stop}])
             if called["add_keys"] > k0:
                 st = ADD_KEYS
@@ -122,18 +155,20 @@ def replay_service(g, cfg, seed, p_inject=0.35):
         if not batch:
             break
         for pos in batch:
+            while p_steal and rng.random() < p_steal:
+                steal()
             while rng.random() < p_inject:  # crafted messages before the genuine one
                 kind = int(rng.integers(0, 6))
-                proc = [ts for ts in s.tasks.values() if ts.state == "processing"]
+                proc = [ts for ts in s.tasks.values() if ts.state == "processing" and tidx[ts.key] not in stolen]
                 if kind == 0 and completed:  # duplicate of an accepted completion, same worker
                     t = completed[int(rng.integers(0, len(completed)))]
                     ts = tss[t]
-                    w = int(rec["worker"][rec["task"].index(t)])  # the worker that ran it
-                    send(t, w, int(ts.run_id) - run0, 77, 0.0, 0.5)
+                    w = ran_on[t]  # the worker that ran it
+                    send(t, w, int(rec["task"].index(t)), 77, 0.0, 0.5, ref_run=int(ts.run_id))
                 elif kind == 1 and proc:  # stale run of a processing task, from another worker
                     ts = proc[int(rng.integers(0, len(proc)))]
                     w = (widx[ts.processing_on.address] + 1 + int(rng.integers(0, W - 1))) % W
-                    send(tidx[ts.key], w, int(ts.run_id) - run0 - 1, 5, 0.0, 0.5)
+                    send(tidx[ts.key], w, rec["task"].index(tidx[ts.key]) - 1, 5, 0.0, 0.5, ref_run=int(ts.run_id) - 1)
                 elif kind == 2 and s.queued:  # a queued task
                     ts = s.queued.peek()
                     send(tidx[ts.key], int(rng.integers(0, W)), 0, 5, 0.0, 0.5)
@@ -143,31 +178,38 @@ def replay_service(g, cfg, seed, p_inject=0.35):
                     send(int(rng.integers(0, N)), W + int(rng.integers(0, 5)), 0, 5, 0.0, 0.5)
                 elif kind == 5 and proc:  # stale run_id from the worker it is processing on
                     ts = proc[int(rng.integers(0, len(proc)))]
-                    send(tidx[ts.key], widx[ts.processing_on.address], int(ts.run_id) - run0 - 1, 5, 0.0, 0.5)
+                    send(tidx[ts.key], widx[ts.processing_on.address], rec["task"].index(tidx[ts.key]) - 1, 5, 0.0, 0.5,
+                         ref_run=int(ts.run_id) - 1)
             t = rec["task"][pos]
             ts = tss[t]
             assert ts.state == "processing", (ts.key, ts.state)
-            assert ts.run_id - run0 == pos, (ts.run_id, run0, pos)
-            st = send(t, widx[ts.processing_on.address], pos, int(g["nbytes"][t]), float(g["start"][t]),
-                      float(g["stop"][t]))
+            ran_on[t] = widx[ts.processing_on.address]
+            st = send(t, ran_on[t], pos, int(g["nbytes"][t]), float(g["start"][t]), float(g["stop"][t]),
+                      ref_run=int(ts.run_id))
             assert st == ACCEPTED
         round_ptr.append(len(msgs["task"]))
     states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
-    return rec, rounds, nplaced, states, msgs, round_ptr
+    return rec, rounds, nplaced, states, msgs, round_ptr, steals
 
 
 def main():
     cases = {
         "svc_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 64, seed=15, n_inner_prefixes=3,
-                                                          random_durations=True, nthreads="random"), 1.1, 1),
-        "svc_c2mini_satinf": (lambda: G.graphs.random_dag(2000, 32, seed=16), float("inf"), 2),
+                                                          random_durations=True, nthreads="random"), 1.1, 1, 0.0),
+        "svc_c2mini_satinf": (lambda: G.graphs.random_dag(2000, 32, seed=16), float("inf"), 2, 0.0),
+        "svc_steal_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 64, seed=17, n_inner_prefixes=3,
+                                                                random_durations=True, nthreads="random"), 1.1, 3, 0.05),
+        "svc_steal_c2mini_satinf": (lambda: G.graphs.random_dag(2000, 32, seed=18), float("inf"), 4, 0.05),
     }
-    for name, (mk, sat, seed) in cases.items():
+    only = set(sys.argv[1:])
+    for name, (mk, sat, seed, p_steal) in cases.items():
+        if only and name not in only:
+            continue
         g = mk()
         G.graphs.check_graph(g)
         dask.config.set({"distributed.scheduler.worker-saturation": sat})
         cfg = G.config_dict(sat)
-        rec, rounds, nplaced, states, msgs, round_ptr = replay_service(g, cfg, seed)
+        rec, rounds, nplaced, states, msgs, round_ptr, steals = replay_service(g, cfg, seed, p_steal=p_steal)
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -175,9 +217,12 @@ def main():
                  msg_runid=np.array(msgs["run_id"], np.int64), msg_nbytes=np.array(msgs["nbytes"], np.int64),
                  msg_start=np.array(msgs["start"]), msg_stop=np.array(msgs["stop"]),
                  msg_status=np.array(msgs["status"], np.int8), msg_round_ptr=np.array(round_ptr, np.int64))
+        if p_steal:
+            z.update(steal_msg=np.array(steals["msg"], np.int64), steal_task=np.array(steals["task"], np.int32),
+                     steal_thief=np.array(steals["thief"], np.int32))
         np.savez_compressed(path, **z)
         cnt = np.bincount(np.array(msgs["status"]), minlength=5)
-        print(f"{name}: {len(msgs['task'])} messages, statuses {cnt.tolist()}")
+        print(f"{name}: {len(msgs['task'])} messages, statuses {cnt.tolist()}, {len(steals['task'])} steals")
 
 
 if __name__ == "__main__":

@@ -88,3 +88,44 @@ def test_gpu_work_stealing_matches_reference_plugin():
     assert len(res) == 4
     for r in res:
         assert r["differ"] == [] and r["requests"] > 0, r
+
+
+def test_confirmed_steal_moves_the_task_on_the_engine():
+    """The steal-response wrapper (plain stand-ins, no dask): a confirm that moved the task
+    calls engine.move_task(task index, thief index); a reschedule hands placement back."""
+    import asyncio
+    from types import SimpleNamespace as NS
+
+    from distributed_amd.ext import GPUPlacementExtension
+
+    w0, w1 = NS(address="tcp://w0"), NS(address="tcp://w1")
+    ts = NS(key="x", state="processing", processing_on=w0)
+    moved = []
+
+    class Stealing:
+        async def move_task_confirm(self, *, key, state, stimulus_id, worker=None):
+            t = sched.tasks[key]
+            if state == "ready":  # the confirm branch (stealing.py:376-384)
+                t.processing_on = w1
+            else:  # the reschedule branch (:365-376)
+                t.state = "released"
+                t.processing_on = None
+
+    class Engine:
+        def move_task(self, t, w):
+            moved.append((t, w))
+
+    st = Stealing()
+    sched = NS(tasks={"x": ts}, extensions={"stealing": st}, stream_handlers={"steal-response": st.move_task_confirm})
+    ext = GPUPlacementExtension.__new__(GPUPlacementExtension)
+    ext.scheduler, ext.active, ext.reason, ext.engine = sched, True, None, Engine()
+    ext.task_index, ext.worker_index = {"x": 3}, {"tcp://w0": 0, "tcp://w1": 1}
+    from collections import Counter, deque
+    ext.stats, ext.pending = Counter(), deque()
+    ext._wrap_stealing()
+    assert sched.stream_handlers["steal-response"] is st.move_task_confirm  # wrapped once, both places
+    asyncio.run(sched.stream_handlers["steal-response"](key="x", state="ready", stimulus_id="s1", worker="tcp://w0"))
+    assert moved == [(3, 1)] and ext.active and ext.stats["steals_confirmed"] == 1
+    ts.processing_on = w0
+    asyncio.run(sched.stream_handlers["steal-response"](key="x", state="executing", stimulus_id="s2"))
+    assert moved == [(3, 1)] and not ext.active and "rescheduled" in ext.reason

@@ -10,14 +10,18 @@ state resident between calls.
   (``Scheduler.stimulus_task_finished``, distributed/scheduler.py:5025-5092) to a message
   stream that mixes stale, duplicate, already-in-memory, forgotten-key and unknown-worker
   reports into the completions: the engine's status per message must equal them, and the
-  placements must be unaffected.
+  placements must be unaffected;
+* the ``svc_steal_*`` fixtures interleave confirmed steals (WorkStealing.move_task_confirm,
+  distributed/stealing.py:376-384) with that stream: each goes to ``dgp_move_task`` before
+  the message it preceded in the reference, and the placements, snapshots and statuses
+  that follow must still equal the reference's.
 """
 import os
 
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden_files
+from conftest import GOLDEN, golden_files, svc_steal_files
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -117,3 +121,65 @@ def test_service_empty_batch_and_mode_guard():
         assert st.tolist() == [0]
         with pytest.raises(_lib.DgpError):
             eng.run_rounds(-1)
+
+
+@pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])
+@pytest.mark.parametrize("name", svc_steal_files())
+def test_service_with_confirmed_steals(name, per_message):
+    """Steal confirmations on the device between task-finished messages."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    msgs = list(zip(z["msg_task"].tolist(), z["msg_worker"].tolist(), z["msg_runid"].tolist(),
+                    z["msg_nbytes"].tolist(), z["msg_start"].tolist(), z["msg_stop"].tolist()))
+    ptr = z["msg_round_ptr"].tolist()
+    steal_at = {}
+    for i, t, h in zip(z["steal_msg"].tolist(), z["steal_task"].tolist(), z["steal_thief"].tolist()):
+        steal_at.setdefault(i, []).append((t, h))
+    assert len(z["steal_task"]) > 50
+    R = len(exp["round_nplaced"]) + 2
+    status = []
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        for k in range(len(ptr) - 1):
+            i, e = ptr[k], ptr[k + 1]
+            while i < e:  # batches end at the next steal (per message: one message each)
+                for t, h in steal_at.get(i, ()):
+                    eng.move_task(t, h)
+                j = i + 1
+                if not per_message:
+                    while j < e and j not in steal_at:
+                        j += 1
+                t, w, r, nb, a, b = (np.array(c) for c in zip(*msgs[i:j]))
+                st, _ = eng.tasks_finished(t, w, r, nb, a, b)
+                status.extend(st.tolist())
+                i = j
+            if e > ptr[k]:
+                eng.snapshot()
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    status = np.array(status, np.int8)
+    want = z["msg_status"]
+    bad = np.nonzero(status != want)[0]
+    assert len(bad) == 0, f"{len(bad)} status mismatches, first message {bad[0]}: {status[bad[0]]} vs {want[bad[0]]}"
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+def test_move_task_rejects_a_task_not_processing():
+    from distributed_amd import _lib, graphs
+    from distributed_amd.engine import PlacementEngine
+
+    g = graphs.random_dag(2000, 32, seed=3)
+    cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": 1.1}
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, results=False)
+        eng.update_graph()
+        placed = set(eng.placements()["pl_task"].tolist())
+        waiting = next(t for t in range(g["n_tasks"]) if t not in placed)
+        with pytest.raises(_lib.DgpError):
+            eng.move_task(waiting, 0)
