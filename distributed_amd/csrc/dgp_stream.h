@@ -3129,5 +3129,135 @@ __global__ void __launch_bounds__(64) k_move_task(const Dev* __restrict__ Dp, in
   }
 }
 
+// ===================================================================== worker joins
+// Scheduler.add_worker (scheduler.py:4308-4441) on the engine state between launches
+// (service mode). The host has grown every per-worker array to W and set the new worker
+// w = W - 1's nthreads / cap; here: the empty WorkerState, check_idle_saturated(ws)
+// (:4398), then stimulus_queue_slots_maybe_opened (:4416-4420, :4983-5023): the open slots
+// of idle_task_count, each taking the queue's head through _transition_queued_processing
+// (:2797-2808) -> decide_worker_rootish_queuing_enabled (:2227-2236: argmin of
+// len(processing) / nthreads over idle_task_count, lowest index on ties) ->
+// _add_to_processing (:3199-3215: add_to_processing, check_idle_saturated, n_tasks).
+// bulk_schedule_unrunnable_after_adding_worker has nothing to schedule on this path (no
+// restrictions: no task is no-worker). One wave; *placed = the placements made.
+__global__ void __launch_bounds__(64) k_add_worker(const Dev* __restrict__ Dp, long long* placed) {
+  const Dev& D = *Dp;
+  __shared__ SCtl S;  // needs_inc reports inconsistencies through it
+  const int lane = lane_id();
+  const int w = D.W - 1;
+  Ctl* c = D.ctl;
+  if (lane == 0) {
+    S.error = 0;
+    S.err_task = -1;
+    S.stop = 0;
+    D.w_nproc[w] = 0;
+    D.w_plen[w] = 0;
+    D.w_netocc[w] = 0;
+    D.w_nbytes[w] = 0;
+    D.w_itcslots[w] = 0;
+    D.w_lastcheck[w] = ~0ull;
+    D.w_flags[w] = 0;
+    *placed = 0;
+  }
+  for (int i = lane; i < PMAX; i += 64) {
+    D.w_pfx[(size_t)w * PMAX + i] = 0;
+    D.w_pcnt[(size_t)w * PMAX + i] = 0;
+  }
+  if (lane < NLW) D.gw_needs_saved[(size_t)w * NLW + lane] = 0;
+  if (lane < NXW) D.gw_needs_ext[(size_t)w * NXW + lane] = 0;
+  __threadfence();
+  __syncthreads();
+  if (lane == 0) {  // check_idle_saturated(ws): nothing processing -> idle; idle_task_count
+    walk_flags(D, w, occupancy(D, w, D.pdur_walk), 0);
+    itc_check(D, w, false);
+  }
+  __threadfence();
+  __syncthreads();
+  // queue position and log length in registers (uniform); lane 0 writes them back at the end
+  long long qhead = c->qhead, qlen = c->qlen, pos = (long long)c->n_placed;
+  if (D.sat_inf || qlen <= 0) return;
+  // slots_available over idle_task_count, summed before any transition (:5007-5012)
+  long long slots = 0;
+  for (int i = lane; i < D.W; i += 64)
+    if (D.w_flags[i] & WF_ITC) slots += (long long)D.w_cap[i] - D.w_nproc[i];
+  slots = wsum64(slots);
+  long long n = 0;
+  for (long long k = 0; k < slots && qlen > 0; k++) {
+    // decide_worker_rootish_queuing_enabled: argmin over idle_task_count
+    double bk = INFINITY;
+    int bi = INT32_MAX;
+    for (int i = lane; i < D.W; i += 64) {
+      if (!(D.w_flags[i] & WF_ITC)) continue;
+      const double key = (double)D.w_nproc[i] / (double)D.w_nthreads[i];
+      if (key < bk) {  // ascending index per lane: the first minimum stays
+        bk = key;
+        bi = i;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const double qk = __shfl_xor(bk, o);
+      const int qi = __shfl_xor(bi, o);
+      if (qk < bk || (qk == bk && qi < bi)) {
+        bk = qk;
+        bi = qi;
+      }
+    }
+    if (bi == INT32_MAX) break;  // idle_task_count empty: the head stays queued
+    const int ws = bi;
+    const int t = D.qarr[qhead];
+    // worker_objective's comm bytes (:3136-3138) and _inc_needs_replica (:800-813) of the
+    // dependencies ws holds no replica of
+    const int64_t k0 = D.dep_ptr[t], k1 = D.dep_ptr[t + 1];
+    int64_t comm = 0, added = 0;
+    uint32_t nl = lane < NLW ? D.gw_needs_saved[(size_t)ws * NLW + lane] : 0u;
+    for (int64_t q = k0; q < k1; q++) {
+      const int d = D.dep_idx[q];
+      if (D.holder_of[d] == ws) continue;
+      const int64_t nb = nbv(D, D.res_nbytes[d]);
+      comm += nb;
+      added += needs_inc(D, S, ws, nl, d, nb, t);
+    }
+    if (lane < NLW) D.gw_needs_saved[(size_t)ws * NLW + lane] = nl;
+    __threadfence();
+    __syncthreads();
+    if (lane == 0) {
+      const double stack = occupancy(D, ws, D.pdur_walk) / (double)D.w_nthreads[ws];
+      D.pl_task[pos] = t;
+      D.pl_worker[pos] = ws;
+      D.pl_comm[pos] = comm;
+      D.pl_start[pos] = stack + (double)comm / (double)D.bandwidth;
+      D.pl_wsnbytes[pos] = D.w_nbytes[ws];
+      D.pl_route[pos] = ROUTE_ROOTISH_Q;
+      D.run_id[t] = (int32_t)pos;
+      D.holder_of[t] = ws;
+      D.state[t] = S_PROCESSING;
+      D.proc_on[t] = ws;
+      // WorkerState.add_to_processing (:733-745), the global prefix count, network occupancy
+      const int p = D.prefix[t];
+      if (!wdict_inc(D, ws, p)) set_error(D, ERR_PREFIX_CAP, t);
+      D.w_nproc[ws] += 1;
+      D.w_netocc[ws] += added;
+      if (!gdict_inc(D, p)) set_error(D, ERR_GPREFIX_CAP, t);
+      c->g_netocc += (double)added;
+      walk_flags(D, ws, occupancy(D, ws, D.pdur_walk), D.w_nproc[ws]);
+      itc_check(D, ws, false);
+      c->n_tasks += 1;
+      if (S.error) set_error(D, S.error, S.err_task);
+    }
+    __threadfence();  // the flags / counts above are read by every lane of the next scan
+    __syncthreads();
+    pos++;
+    qhead++;
+    qlen--;
+    n++;
+  }
+  if (lane == 0) {
+    c->n_placed = (unsigned long long)pos;
+    c->qhead = qhead;
+    c->qlen = qlen;
+    *placed = n;
+  }
+}
+
 }  // namespace st
 }  // namespace dgp

@@ -83,6 +83,8 @@ struct dgp_engine {
   size_t evused = 0;
   StealCtx steal;
   std::vector<uint8_t> tflags_h;           // task flags as set_graph computed them
+  std::vector<int32_t> group_h;            // TaskGroup of each task
+  std::vector<int64_t> gdep_n, gdep_len;   // per group: len(tg.dependencies), sum of their lengths
   std::vector<int8_t> rootish_override_h;  // TaskState._rootish per task (-1: None)
 };
 
@@ -106,6 +108,51 @@ int dalloc(dgp_engine* e, T** p, size_t count, std::vector<void*>& list) {
   hipError_t st = hipMalloc((void**)p, count * sizeof(T));
   if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(st));
   list.push_back((void*)*p);
+  return 0;
+}
+
+// grow a device array from n0 to n1 elements: the first n0 copied, the rest zero; the
+// allocation list entry follows the new pointer
+template <class T>
+int regrow(dgp_engine* e, T** p, size_t n0, size_t n1, std::vector<void*>& list) {
+  T* q = nullptr;
+  hipError_t st = hipMalloc((void**)&q, std::max<size_t>(n1, 1) * sizeof(T));
+  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(st));
+  HIPCHK(e, hipMemsetAsync(q, 0, std::max<size_t>(n1, 1) * sizeof(T), e->stream));
+  if (*p && n0) HIPCHK(e, hipMemcpyAsync(q, *p, std::min(n0, n1) * sizeof(T), hipMemcpyDeviceToDevice, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  bool found = false;
+  for (auto& x : list)
+    if (x == (void*)*p) {
+      x = (void*)q;
+      found = true;
+    }
+  if (*p && found) (void)hipFree(*p);
+  if (!found) list.push_back((void*)q);
+  *p = q;
+  return 0;
+}
+// re-stride a [rows][w0] device array to [rows][w1] (w1 >= w0): each row copied, the new
+// columns zero
+template <class T>
+int restride(dgp_engine* e, T** p, size_t rows, size_t w0, size_t w1, std::vector<void*>& list) {
+  T* q = nullptr;
+  hipError_t st = hipMalloc((void**)&q, std::max<size_t>(rows * w1, 1) * sizeof(T));
+  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(st));
+  HIPCHK(e, hipMemsetAsync(q, 0, std::max<size_t>(rows * w1, 1) * sizeof(T), e->stream));
+  if (*p && rows && w0)
+    HIPCHK(e, hipMemcpy2DAsync(q, w1 * sizeof(T), *p, w0 * sizeof(T), w0 * sizeof(T), rows, hipMemcpyDeviceToDevice,
+                               e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  bool found = false;
+  for (auto& x : list)
+    if (x == (void*)*p) {
+      x = (void*)q;
+      found = true;
+    }
+  if (*p && found) (void)hipFree(*p);
+  if (!found) list.push_back((void*)q);
+  *p = q;
   return 0;
 }
 
@@ -496,6 +543,8 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
   for (int64_t t = 0; t < N; t++)
     for (int64_t k = dep_ptr[t]; k < dep_ptr[t + 1]; k++) gdeps[group_id[t]].push_back(group_id[dep_idx[k]]);
   std::vector<uint8_t> grootish(n_groups, 0);
+  e->gdep_n.clear();
+  e->gdep_len.clear();
   for (int g = 0; g < n_groups; g++) {
     auto& v = gdeps[g];
     std::sort(v.begin(), v.end());
@@ -503,6 +552,8 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
     int64_t sum_len = 0;
     for (int32_t d : v) sum_len += gsize[d];
     grootish[g] = (gsize[g] > e->D.total_nthreads * 2 && (int64_t)v.size() < 5 && sum_len < 5) ? 1 : 0;
+    e->gdep_n.push_back((int64_t)v.size());
+    e->gdep_len.push_back(sum_len);
   }
   std::vector<uint8_t> tflags(N);
   for (int64_t t = 0; t < N; t++) {
@@ -613,6 +664,7 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
   e->prefix_defaults.assign(prefix_default_duration, prefix_default_duration + n_prefixes);
   e->group_sizes = gsize;
   e->tflags_h = tflags;
+  e->group_h.assign(group_id, group_id + N);
   e->rootish_override_h.assign(rootish_override, rootish_override + N);
   D.restr_ptr = nullptr;  // no restrictions until dgp_set_restrictions
   D.restr_idx = nullptr;
@@ -860,6 +912,101 @@ int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief) {
   hipLaunchKernelGGL(dgp::st::k_move_task, dim3(1), dim3(64), 0, e->stream, e->d_dev, task, thief);
   HIPCHK(e, hipGetLastError());
   return check_device_error(e);
+}
+
+int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
+  if (n_new_placements) *n_new_placements = 0;
+  if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
+  if (!(e->D.P <= dgp::st::PD && !e->D.restr_flags))
+    return fail(e, DGP_E_STATE, "dgp_add_worker: the round-kernel engine (more than 8 prefixes, or restrictions) "
+                                "has no worker addition");
+  if (nthreads <= 0 || nthreads > 65535) return fail(e, DGP_E_ARG, "dgp_add_worker: nthreads out of range");
+  if (e->D.W + 1 > 32768) return fail(e, DGP_E_ARG, "at most 32768 workers");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  namespace S = dgp::st;
+  dgp::Dev& D = e->D;
+  const size_t W0 = D.W, W1 = W0 + 1;
+  auto& A = e->allocs;
+  int rc = 0;
+  // every per-worker array one row longer (rows are per worker: a prefix copy)
+  rc |= regrow(e, &D.w_nthreads, W0, W1, A);
+  rc |= regrow(e, &D.w_cap, W0, W1, A);
+  rc |= regrow(e, &D.w_nproc, W0, W1, A);
+  rc |= regrow(e, &D.w_plen, W0, W1, A);
+  rc |= regrow(e, &D.w_pfx, W0 * dgp::PMAX, W1 * dgp::PMAX, A);
+  rc |= regrow(e, &D.w_pcnt, W0 * dgp::PMAX, W1 * dgp::PMAX, A);
+  rc |= regrow(e, &D.w_netocc, W0, W1, A);
+  rc |= regrow(e, &D.w_nbytes, W0, W1, A);
+  rc |= regrow(e, &D.w_flags, W0, W1, A);
+  rc |= regrow(e, &D.w_itcslots, W0, W1, A);
+  rc |= regrow(e, &D.w_lastcheck, W0, W1, A);
+  rc |= regrow(e, &D.w_needs, W0 * dgp::NEEDS_W, W1 * dgp::NEEDS_W, A);
+  rc |= regrow(e, &D.gw_nproc, W0, W1, A);
+  rc |= regrow(e, &D.gw_nthreads, W0, W1, A);
+  rc |= regrow(e, &D.gw_cap, W0, W1, A);
+  rc |= regrow(e, &D.gw_plen, W0, W1, A);
+  rc |= regrow(e, &D.gw_pcnt, W0 * S::PD, W1 * S::PD, A);
+  rc |= regrow(e, &D.gw_netocc, W0, W1, A);
+  rc |= regrow(e, &D.gw_nbytes, W0, W1, A);
+  rc |= regrow(e, &D.gw_mask, W0, W1, A);
+  rc |= regrow(e, &D.gw_needs, W0 * S::NLW, W1 * S::NLW, A);
+  rc |= regrow(e, &D.gw_wflags, W0, W1, A);
+  rc |= regrow(e, &D.gw_needs_ext, W0 * S::NXW, W1 * S::NXW, A);
+  rc |= regrow(e, &D.gw_held, 0, 2 * W1, A);  // [2][W] scratch of a global stimulus
+  rc |= regrow(e, &D.gw_needs_saved, W0 * S::NLW, W1 * S::NLW, A);
+  int32_t Wp = 1;
+  while ((size_t)Wp < W1) Wp <<= 1;
+  if (Wp != D.Wp) {  // the round engine's tournament tree (rebuilt before use)
+    rc |= regrow(e, &D.t_key, 0, 2 * (size_t)Wp, A);
+    rc |= regrow(e, &D.t_idx, 0, 2 * (size_t)Wp, A);
+  }
+  const int32_t WB = (int32_t)((W1 + 63) / 64);
+  if (WB != D.WB) rc |= restride(e, &D.holders, (size_t)D.N, (size_t)D.WB, (size_t)WB, e->graph_allocs);
+  if (e->snap_rounds > 0) {  // [rounds][W]: earlier rounds read 0 for the new worker
+    const size_t R = (size_t)e->snap_rounds;
+    rc |= restride(e, &D.snap_occ, R, W0, W1, A);
+    rc |= restride(e, &D.snap_nbytes, R, W0, W1, A);
+    rc |= restride(e, &D.snap_nproc, R, W0, W1, A);
+    rc |= restride(e, &D.snap_flags, R, W0, W1, A);
+  }
+  if (rc) return rc;
+  D.W = (int32_t)W1;
+  D.WB = WB;
+  D.Wp = Wp;
+  e->nthreads.push_back(nthreads);
+  D.total_nthreads += nthreads;
+  const int32_t cap = D.sat_inf ? 0 : std::max((int32_t)std::ceil(D.saturation * nthreads), (int32_t)1);
+  HIPCHK(e, hipMemcpy(D.w_nthreads + W0, &nthreads, 4, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_cap + W0, &cap, 4, hipMemcpyHostToDevice));
+  // is_rootish (:2929-2947) reads total_nthreads: the groups' flags follow the new total
+  {
+    std::vector<uint8_t> tf = e->tflags_h;
+    bool changed = false;
+    for (int64_t t = 0; t < D.N; t++) {
+      const int g = e->group_h[t];
+      const bool gr = e->group_sizes[g] > D.total_nthreads * 2 && e->gdep_n[g] < 5 && e->gdep_len[g] < 5;
+      const bool r = e->rootish_override_h[t] >= 0 ? e->rootish_override_h[t] != 0 : gr;
+      tf[t] = (uint8_t)((tf[t] & ~dgp::TF_ROOTISH) | (r ? dgp::TF_ROOTISH : 0));
+      changed = changed || tf[t] != e->tflags_h[t];
+    }
+    if (changed) {
+      HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), tf.data(), D.N, hipMemcpyHostToDevice));
+      e->tflags_h = tf;
+    }
+  }
+  e->mode = 2;
+  if (int rc2 = sync_dev(e)) return rc2;
+  hipLaunchKernelGGL(dgp::st::k_add_worker, dim3(1), dim3(64), 0, e->stream, e->d_dev, e->d_aux + 3);
+  HIPCHK(e, hipGetLastError());
+  long long placed = 0;
+  HIPCHK(e, hipMemcpyAsync(&placed, e->d_aux + 3, sizeof placed, hipMemcpyDeviceToHost, e->stream));
+  dgp::Ctl c;
+  if (int rc2 = check_device_error(e, &c)) return rc2;  // synchronises the stream
+  if (n_new_placements) *n_new_placements = placed;
+  e->last_placed = c.n_placed;
+  return 0;
 }
 
 int dgp_snapshot(dgp_engine* e) {

@@ -183,6 +183,15 @@ class PlacementEngine:
         :376-384): processing ``task`` moves from its worker to ``thief`` on the device."""
         self._check(self.lib.dgp_move_task(self.h, int(task), int(thief)), "dgp_move_task")
 
+    def add_worker(self, nthreads: int) -> int:
+        """A worker joins (Scheduler.add_worker, distributed/scheduler.py:4308-4441) with
+        index ``n_workers``: check_idle_saturated and the queue refill on the device.
+        Returns the number of placements the refill made."""
+        newp = C.c_int64(0)
+        self._check(self.lib.dgp_add_worker(self.h, int(nthreads), C.byref(newp)), "dgp_add_worker")
+        self.n_workers += 1
+        return int(newp.value)
+
     def snapshot(self):
         """Append one per-worker snapshot (service mode round boundary)."""
         self._check(self.lib.dgp_snapshot(self.h), "dgp_snapshot")

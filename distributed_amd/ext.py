@@ -370,8 +370,29 @@ class GPUPlacementExtension(SchedulerPlugin):
             self.fallback(f"update_graph: {e}")
 
     def add_worker(self, scheduler=None, worker=None):
-        if self.engine is not None and worker not in self.worker_index:
-            self.fallback(f"add_worker({worker}) after the engine started")
+        """SchedulerPlugin.add_worker (diagnostics/plugin.py): Scheduler.add_worker calls it
+        after check_idle_saturated(ws) and before bulk_schedule_unrunnable_after_adding_worker /
+        stimulus_queue_slots_maybe_opened (scheduler.py:4398-4420). The engine adds the worker
+        and makes the queue refill; the scheduler's own refill then consumes those decisions.
+        The engine's worker index order must stay the scheduler's (SortedDict address) order,
+        so only a worker whose address sorts after every known one joins on the device."""
+        if not self.active or self.engine is None or worker in self.worker_index:
+            return
+        if self.workers and worker < max(self.workers):
+            self.fallback(f"add_worker({worker}): its address sorts before a known worker's")
+            return
+        s = self.scheduler
+        try:
+            self._end_of_stimulus("the previous stimulus")
+            if not self.active:
+                return
+            self.engine.add_worker(int(s.workers[worker].nthreads))
+            self.worker_index[worker] = len(self.workers)
+            self.workers.append(worker)
+            self._fetch()
+            self.stats["workers_added"] += 1
+        except Exception as e:
+            self.fallback(f"add_worker({worker}): {e}")
 
     def remove_worker(self, scheduler=None, worker=None, **kwargs):
         if self.engine is not None and worker in self.worker_index:

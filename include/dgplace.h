@@ -23,6 +23,9 @@
  *                         resident between calls (service mode)
  *   dgp_move_task         WorkStealing.move_task_confirm, "confirm" branch (stealing.py:333-399,
  *                         :376-384): a processing task moves from its worker to the thief
+ *   dgp_add_worker        Scheduler.add_worker (scheduler.py:4308-4441): a worker joins a running
+ *                         engine: total_nthreads (:4383), check_idle_saturated (:4398), the
+ *                         queue refill stimulus_queue_slots_maybe_opened (:4416-4420)
  *   dgp_snapshot          one per-worker snapshot (occupancy, nbytes, processing, idle /
  *                         saturated / idle_task_count, queue length) at a caller-chosen point
  *   dgp_run_rounds        the synthetic executor of the replay protocol: round k completes
@@ -42,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 5
+#define DGP_ABI_VERSION 6
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -143,6 +146,19 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
  * comes from the thief with that run_id (dgp_tasks_finished). Service mode, graphs on the
  * stream engine (<= 8 prefixes, no restrictions); DGP_E_DEVICE if the task is not processing. */
 int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief);
+
+/* A worker joins (Scheduler.add_worker, scheduler.py:4308-4441) with `nthreads` threads; its
+ * index is the next one (W): the caller keeps the reference's worker order (addresses sorted,
+ * SortedDict) equal to index order, so a joining worker's address sorts after the others.
+ * On the device: the empty WorkerState, total_nthreads += nthreads (:4383; root-ish groups
+ * re-evaluated, is_rootish :2929-2947), check_idle_saturated(ws) (:4398), then
+ * stimulus_queue_slots_maybe_opened (:4416-4420, :4983-5023): queued tasks taken in queue
+ * order by decide_worker_rootish_queuing_enabled (:2227-2236) onto idle_task_count.
+ * *n_new_placements receives the placements made (read them with dgp_get_placements).
+ * Service mode, graphs on the stream engine (<= 8 prefixes, no restrictions: no task is
+ * no-worker, so bulk_schedule_unrunnable_after_adding_worker :3173-3186 has nothing to do).
+ * Snapshots taken earlier read 0 for the new worker. */
+int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements);
 
 /* Append one worker snapshot (needs dgp_enable_snapshots): round index = number of calls
  * (update_graph's snapshot is round 0). */

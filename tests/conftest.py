@@ -16,7 +16,13 @@ def pytest_configure(config):
 
 def golden_files():
     """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
-    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith(("steal_", "svc_steal_")))
+    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
+                  and not f.startswith(("steal_", "svc_steal_", "svcaddw_")))
+
+
+def svc_add_worker_files():
+    """Service-mode message streams with workers joining (tests/golden/gen_service.py add-workers)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcaddw_") and f.endswith(".npz"))
 
 
 def svc_steal_files():

@@ -83,6 +83,12 @@ class FixtureEngine:
             task[j], task[j + 1] = task[j + 1], task[j]
         return {"pl_task": task, "pl_worker": self.exp["pl_worker"][sl]}
 
+    def add_worker(self, nthreads):  # a join (the fixture's per-event placement counts)
+        k = self.stim[self.k]
+        self.n += k
+        self.k += 1
+        return k
+
     def close(self):
         pass
 
@@ -210,6 +216,77 @@ def run(name, diverge=False):
                 active=ext.active, reason=ext.reason)
 
 
+def run_joins(name):
+    """A ``svcaddw_*`` stream (gen_service.py add-workers): workers join between the
+    task-finished messages through the placement-relevant body of ``Scheduler.add_worker``
+    (scheduler.py:4370-4420: workers / running / total_nthreads, check_idle_saturated, the
+    plugins' add_worker hook, bulk_schedule_unrunnable_after_adding_worker,
+    stimulus_queue_slots_maybe_opened); the extension's hook adds the worker to the engine
+    and its queue refill decisions are the ones the scheduler then takes."""
+    from distributed.core import Status
+    from distributed.scheduler import WorkerState
+
+    path = os.path.join(HERE, "golden", name)
+    g, cfg, exp, meta = load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    g["keys"] = None
+    sat = cfg["saturation"]
+    sat = float("inf") if sat == "inf" else float(sat)
+    dask.config.set({"distributed.scheduler.worker-saturation": sat})
+    cfg = dict(cfg, saturation=sat)
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    S = type(s)
+    S.stimulus_task_finished = Scheduler.stimulus_task_finished
+    S.handle_task_finished = Scheduler.handle_task_finished
+    S.validate_key = lambda self, key, ts=None: None
+    S.send_all = lambda self, client_msgs, worker_msgs: None
+    fkeys = [ts.key for ts in tss]
+    eng = FixtureEngine(exp, fkeys)
+    ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
+    eng.ext = ext
+    s.stream_handlers = {}
+    ext._install()
+    priority = {ts.key: ts.priority for ts in tss}
+    recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
+    ext.update_graph(s, client="client-0", keys=set(priority), tasks=list(priority), annotations={},
+                     priority=priority, dependencies={})
+    assert ext.active, ext.reason
+    s._transitions(recs, {}, {}, "update-graph")
+    W0 = len(g["nthreads"])
+    joins = dict(zip(z["add_msg"].tolist(), z["add_nthreads"].tolist()))
+    k_join = 0
+    for i, (t, w) in enumerate(zip(z["msg_task"].tolist(), z["msg_worker"].tolist())):
+        if i in joins:
+            addr = f"tcp://w{W0 + k_join:05d}:1"
+            widx[addr] = W0 + k_join
+            ws = WorkerState(address=addr, status=Status.running, pid=0, name=addr, nthreads=joins[i],
+                             memory_limit=0, local_directory="", nanny=None, server_id=addr, scheduler=s)
+            s.workers[addr] = ws
+            s.running.add(ws)
+            s.aliases[addr] = addr
+            s.total_nthreads += ws.nthreads
+            s.check_idle_saturated(ws)
+            ext.add_worker(scheduler=s, worker=addr)
+            s.transitions(s.bulk_schedule_unrunnable_after_adding_worker(ws), f"add-{addr}")
+            s.stimulus_queue_slots_maybe_opened(stimulus_id=f"add-{addr}")
+            k_join += 1
+        ts = tss[t]
+        s.stream_handlers["task-finished"](
+            key=ts.key, worker=ts.processing_on.address, stimulus_id=f"tf-{t}", run_id=ts.run_id,
+            nbytes=int(g["nbytes"][t]), type=None, typename="int", metadata=None,
+            startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
+    ext._end_of_stimulus("end of stream")
+    assert ext.active, ext.reason
+    assert k_join == len(joins)
+    n = len(exp["pl_task"])
+    assert rec["task"] == exp["pl_task"].tolist()
+    assert rec["worker"] == exp["pl_worker"].tolist()
+    assert np.array_equal(np.array(rec["start"]).view(np.int64), exp["pl_start"].view(np.int64))
+    assert ext.stats["device_decisions"] == n, (ext.stats, n)
+    return dict(fixture=name, placements=n, joins=k_join, workers_added=ext.stats["workers_added"],
+                device_decisions=ext.stats["device_decisions"], active=ext.active, reason=ext.reason)
+
+
 if __name__ == "__main__":
     import warnings
 
@@ -217,4 +294,4 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     diverge = "--diverge" in args
     for nm in [a for a in args if not a.startswith("--")]:
-        print(json.dumps(run(nm, diverge)), flush=True)
+        print(json.dumps(run_joins(nm) if nm.startswith("svcaddw_") else run(nm, diverge)), flush=True)

@@ -192,7 +192,127 @@ def replay_service(g, cfg, seed, p_inject=0.35, p_steal=0.0):
     return rec, rounds, nplaced, states, msgs, round_ptr, steals
 
 
+def replay_add_workers(g, cfg, seed, n_add, max_nthreads=4):
+    """The replay protocol's completions as task-finished messages, with ``n_add`` workers
+    joining at random points of the first half of the stream, exactly as
+    ``Scheduler.add_worker`` (distributed/scheduler.py:4308-4441) changes the placement
+    state: the WorkerState enters ``workers`` / ``running`` (addresses sort after the
+    existing ones, so the new worker's index is the next one), ``total_nthreads`` grows
+    (:4383), ``check_idle_saturated(ws)`` (:4398), then
+    ``bulk_schedule_unrunnable_after_adding_worker`` and ``stimulus_queue_slots_maybe_opened``
+    (:4416-4420). Stored: ``add_msg`` (the message index each addition precedes) and
+    ``add_nthreads``; snapshots are as wide as the final worker count (0 for workers not
+    yet added)."""
+    from distributed.core import Status
+    from distributed.scheduler import Scheduler, WorkerState
+
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    W0 = len(g["nthreads"])
+    W = W0 + n_add
+    N = g["n_tasks"]
+    rng = np.random.default_rng(seed)
+    type(s).stimulus_task_finished = Scheduler.stimulus_task_finished
+    add_at = sorted(int(x) for x in rng.choice(N // 2, n_add, replace=False))
+    add_nt = [int(x) for x in rng.integers(1, max_nthreads + 1, n_add)]
+    added = {"msg": [], "nthreads": []}
+
+    def add_worker(i, nthreads):
+        addr = f"tcp://w{i:05d}:1"
+        widx[addr] = i
+        ws = WorkerState(address=addr, status=Status.running, pid=0, name=addr, nthreads=nthreads, memory_limit=0,
+                         local_directory="", nanny=None, server_id=addr, scheduler=s)
+        s.workers[addr] = ws
+        s.running.add(ws)
+        s.aliases[addr] = addr
+        s.total_nthreads += nthreads
+        s.check_idle_saturated(ws)
+        sid = f"add-worker-{i}"
+        s.transitions(s.bulk_schedule_unrunnable_after_adding_worker(ws), sid)
+        s.stimulus_queue_slots_maybe_opened(stimulus_id=sid)
+
+    recs = {}
+    for ts in sorted(tss, key=lambda t: t.priority, reverse=True):
+        recs[ts.key] = "waiting"
+    s._transitions(recs, {}, {}, "update-graph")
+    stim = [len(rec["task"])]  # placements per event: update_graph, then each join / completion
+    msgs = {k: [] for k in ("task", "worker", "run_id", "nbytes", "start", "stop", "status")}
+    round_ptr = [0]
+    rounds, nplaced = [], []
+    done = 0
+    k_add = 0
+    while True:
+        cur = len(rec["task"])
+        batch = list(range(done, cur))
+        rounds.append(G.snapshot(s, W, widx) + (len(s.queued),))
+        nplaced.append(cur - done)
+        done = cur
+        if not batch:
+            break
+        for pos in batch:
+            while k_add < n_add and add_at[k_add] <= len(msgs["task"]):
+                added["msg"].append(len(msgs["task"]))
+                added["nthreads"].append(add_nt[k_add])
+                n0 = len(rec["task"])
+                add_worker(W0 + k_add, add_nt[k_add])
+                stim.append(len(rec["task"]) - n0)
+                k_add += 1
+            t = rec["task"][pos]
+            ts = tss[t]
+            assert ts.state == "processing", (ts.key, ts.state)
+            w = widx[ts.processing_on.address]
+            sid = f"task-finished-{len(msgs['task'])}"
+            r, cm, wm = s.stimulus_task_finished(
+                ts.key, ts.processing_on.address, sid, int(ts.run_id), nbytes=int(g["nbytes"][t]), type=None,
+                typename="int", metadata=None,
+                startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
+            assert ts.state != "processing"
+            n0 = len(rec["task"])
+            s._transitions(r, cm, wm, sid)
+            s.stimulus_queue_slots_maybe_opened(stimulus_id=sid)
+            stim.append(len(rec["task"]) - n0)
+            for k, v in zip(("task", "worker", "run_id", "nbytes", "start", "stop", "status"),
+                            (t, w, pos, int(g["nbytes"][t]), float(g["start"][t]), float(g["stop"][t]), ACCEPTED)):
+                msgs[k].append(v)
+        round_ptr.append(len(msgs["task"]))
+    assert k_add == n_add, (k_add, n_add)
+    rec["stim"] = stim
+    states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
+    return rec, rounds, nplaced, states, msgs, round_ptr, added
+
+
+def main_add_workers(only):
+    cases = {
+        # 48 workers x 1-4 threads, root group of 400 tasks: root-ish (400 > 2 * total_nthreads)
+        # at the start, queued roots left when the workers join
+        "svcaddw_c2var_sat1.1": (lambda: G.graphs.random_dag(4000, 48, seed=21, n_inner_prefixes=3,
+                                                              random_durations=True, nthreads="random"), 1.1, 5, 24),
+        "svcaddw_c2mini_satinf": (lambda: G.graphs.random_dag(3000, 32, seed=22), float("inf"), 6, 12),
+        "svcaddw_c2mini_sat1.0": (lambda: G.graphs.random_dag(3000, 60, seed=23), 1.0, 7, 70),
+    }
+    for name, (mk, sat, seed, n_add) in cases.items():
+        if only and name not in only:
+            continue
+        g = mk()
+        G.graphs.check_graph(g)
+        dask.config.set({"distributed.scheduler.worker-saturation": sat})
+        cfg = G.config_dict(sat)
+        rec, rounds, nplaced, states, msgs, round_ptr, added = replay_add_workers(g, cfg, seed, n_add)
+        G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
+        path = os.path.join(HERE, f"{name}.npz")
+        z = dict(np.load(path, allow_pickle=False))
+        z.update(msg_task=np.array(msgs["task"], np.int32), msg_worker=np.array(msgs["worker"], np.int32),
+                 msg_runid=np.array(msgs["run_id"], np.int64), msg_nbytes=np.array(msgs["nbytes"], np.int64),
+                 msg_start=np.array(msgs["start"]), msg_stop=np.array(msgs["stop"]),
+                 msg_status=np.array(msgs["status"], np.int8), msg_round_ptr=np.array(round_ptr, np.int64),
+                 add_msg=np.array(added["msg"], np.int64), add_nthreads=np.array(added["nthreads"], np.int32))
+        np.savez_compressed(path, **z)
+        routes = np.bincount(np.array(rec["route"]), minlength=4).tolist()
+        print(f"{name}: {len(msgs['task'])} messages, {len(added['msg'])} workers added, routes {routes}")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "add-workers":
+        return main_add_workers(set(sys.argv[2:]))
     cases = {
         "svc_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 64, seed=15, n_inner_prefixes=3,
                                                           random_durations=True, nthreads="random"), 1.1, 1, 0.0),

@@ -44,6 +44,17 @@ def test_extension_places_every_task_from_the_engine():
     assert next(r for r in res if r["fixture"] == "restr_noworker_sat1.1.npz")["device_no_worker"] > 0
 
 
+def test_extension_follows_workers_joining():
+    """Scheduler.add_worker mid-stream: the plugin hook adds the worker to the engine, and
+    the scheduler's queue refill takes the engine's decisions (validate=True agrees)."""
+    names = ["svcaddw_c2var_sat1.1.npz", "svcaddw_c2mini_sat1.0.npz", "svcaddw_c2mini_satinf.npz"]
+    res = drive(names)
+    assert [r["fixture"] for r in res] == names
+    for r in res:
+        assert r["active"] and r["device_decisions"] == r["placements"], r
+        assert r["workers_added"] == r["joins"] > 0, r
+
+
 def test_extension_hands_back_on_divergence():
     """A decision out of order: the extension detects it at once and the scheduler's own
     decide_worker carries on; the records are still the reference's."""

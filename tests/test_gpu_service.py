@@ -11,6 +11,10 @@ state resident between calls.
   stream that mixes stale, duplicate, already-in-memory, forgotten-key and unknown-worker
   reports into the completions: the engine's status per message must equal them, and the
   placements must be unaffected;
+* the ``svcaddw_*`` fixtures have workers join mid-stream (Scheduler.add_worker,
+  distributed/scheduler.py:4308-4441): each goes to ``dgp_add_worker`` before the message it
+  preceded in the reference, and the queue refill it makes, the later placements, the
+  snapshots (as wide as the final worker count) and the task states must equal the reference's;
 * the ``svc_steal_*`` fixtures interleave confirmed steals (WorkStealing.move_task_confirm,
   distributed/stealing.py:376-384) with that stream: each goes to ``dgp_move_task`` before
   the message it preceded in the reference, and the placements, snapshots and statuses
@@ -21,7 +25,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden_files, svc_steal_files
+from conftest import GOLDEN, golden_files, svc_add_worker_files, svc_steal_files
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -183,3 +187,53 @@ def test_move_task_rejects_a_task_not_processing():
         waiting = next(t for t in range(g["n_tasks"]) if t not in placed)
         with pytest.raises(_lib.DgpError):
             eng.move_task(waiting, 0)
+
+
+@pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])
+@pytest.mark.parametrize("name", svc_add_worker_files())
+def test_service_with_workers_joining(name, per_message):
+    """Workers join a running engine (dgp_add_worker) between task-finished messages."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    msgs = list(zip(z["msg_task"].tolist(), z["msg_worker"].tolist(), z["msg_runid"].tolist(),
+                    z["msg_nbytes"].tolist(), z["msg_start"].tolist(), z["msg_stop"].tolist()))
+    ptr = z["msg_round_ptr"].tolist()
+    add_at = {}
+    for i, nt in zip(z["add_msg"].tolist(), z["add_nthreads"].tolist()):
+        add_at.setdefault(i, []).append(nt)
+    W0 = len(g["nthreads"])
+    R = len(exp["round_nplaced"]) + 2
+    status, refill = [], 0
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        for k in range(len(ptr) - 1):
+            i, e = ptr[k], ptr[k + 1]
+            while i < e:  # batches end at the next worker addition
+                for nt in add_at.get(i, ()):
+                    n0 = eng.num_placements()
+                    newp = eng.add_worker(nt)
+                    assert eng.num_placements() == n0 + newp
+                    refill += newp
+                j = i + 1
+                if not per_message:
+                    while j < e and j not in add_at:
+                        j += 1
+                t, w, r, nb, a, b = (np.array(c) for c in zip(*msgs[i:j]))
+                st, _ = eng.tasks_finished(t, w, r, nb, a, b)
+                status.extend(st.tolist())
+                i = j
+            if e > ptr[k]:
+                eng.snapshot()
+        assert eng.n_workers == W0 + len(z["add_nthreads"])
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert (np.array(status) == 0).all()
+    if cfg["saturation"] != "inf":
+        assert refill > 0  # the joins took queued tasks
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
