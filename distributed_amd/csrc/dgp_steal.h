@@ -348,22 +348,39 @@ __global__ void k_runs(Prob P) {
 }
 
 // ---------------------------------------------------------------------- balance
-// One wave; all per-worker balance state in LDS: occupancy, in-flight occupancy and
-// task deltas, thief / idle / saturated flags, the victim list.
+__device__ __forceinline__ double rl_f64(double x, int l) {  // lane l's double, via SGPRs
+  const long long b = __double_as_longlong(x);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+struct RqStage {  // 64 staged request-log entries
+  int32_t task[64], victim[64], thief[64], level[64];
+  double cost[64], occ_v[64], occ_t[64];
+};
+__host__ __device__ inline size_t balance_state_bytes(int W) { return (size_t)W * (8 + 8 + 4 + 4 + 4 + 4 + 2 + 4); }
+// One wave; all per-worker balance state in LDS: occupancy, in-flight occupancy, the
+// pending task count (len(processing) + in-flight task delta), nthreads, thief / idle /
+// saturated flags, the victim list. The walk's accept path reads nothing from global
+// memory: on gfx950 loads and stores share one in-order vmcnt, so a global load after the
+// request's log stores would wait for those stores too.
 __global__ void __launch_bounds__(64) k_balance(Prob P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int W = P.W;
   const int lane = threadIdx.x;
   double* occ = (double*)smem;
   double* ifo = occ + W;
-  int32_t* ift = (int32_t*)(ifo + W);
-  int32_t* run_first = ift + W;             // first possibly-live position of each run
+  int32_t* pend = (int32_t*)(ifo + W);      // len(processing) + in_flight_tasks
+  int32_t* run_first = pend + W;            // first possibly-live position of each run
   int32_t* run_alive = run_first + W;       // live thieves per run
   int32_t* run_nxt = run_alive + W;         // next run to look at (skips emptied runs)
-  uint8_t* thief = (uint8_t*)(run_nxt + W);
+  uint16_t* nth = (uint16_t*)(run_nxt + W);  // WorkerState.nthreads
+  uint8_t* thief = (uint8_t*)(nth + W);
   uint8_t* idle = thief + W;
   uint8_t* sat = idle + W;
   uint8_t* taken = sat + W;                 // topk scratch
+  // the request log (move_task_request's log entry, :498-500), staged 64 entries at a time
+  // and written out by the whole wave in coalesced stores
+  RqStage* rq = (RqStage*)(smem + ((balance_state_bytes(W) + 15) & ~(size_t)15));
   int32_t* vs = P.vs_g;                     // victims of the current level (global scratch)
   const int R = *P.n_runs;
   auto run_a_g = [&](int r) { return P.run_a[r]; };
@@ -376,7 +393,8 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   for (int w = lane; w < W; w += 64) {
     occ[w] = P.occ[w];
     ifo[w] = P.ifo_in ? P.ifo_in[w] : 0.0;
-    ift[w] = P.ift_in ? P.ift_in[w] : 0;
+    pend[w] = P.nproc[w] + (P.ift_in ? P.ift_in[w] : 0);
+    nth[w] = (uint16_t)P.nthreads[w];
     P.checked[w] = 0;
     idle[w] = P.idle[w];
     sat[w] = P.sat[w];
@@ -395,12 +413,29 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   const double avg = P.total_occ / (double)P.total_nthreads;
   auto combined = [&](int w) { return occ[w] + ifo[w]; };                       // :505-506
   auto is_unoccupied = [&](int w, double o, int np) {                           // scheduler.py:2997-3004
-    return np < P.nthreads[w] || o < P.nthreads[w] * avg / 2;
+    const int nt = nth[w];
+    return np < nt || o < nt * avg / 2;
+  };
+  long long ns_out = 0;  // requests already written to the output arrays
+  auto flush = [&](long long n) {  // staged requests [ns_out, n)
+    const long long k = ns_out + lane;
+    if (k < n) {
+      const int q = (int)(k & 63);
+      P.st_task[k] = rq->task[q];
+      P.st_victim[k] = rq->victim[q];
+      P.st_thief[k] = rq->thief[q];
+      P.st_level[k] = rq->level[q];
+      P.st_cost[k] = rq->cost[q];
+      P.st_occ_victim[k] = rq->occ_v[q];
+      P.st_occ_thief[k] = rq->occ_t[q];
+    }
+    ns_out = n;
   };
   auto finish = [&]() {
+    flush(ns);
     for (int w = lane; w < W; w += 64) {
       P.inflight_occ[w] = ifo[w];
-      P.inflight_tasks[w] = ift[w];
+      P.inflight_tasks[w] = pend[w] - P.nproc[w];
       P.idle_out[w] = idle[w];
       P.sat_out[w] = sat[w];
     }
@@ -443,7 +478,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
       if (bw_ >= W) break;
       if (lane == 0) taken[bw_] = 1;
       __syncthreads();
-      if (combined(bw_) > 0.2 && P.nproc[bw_] + ift[bw_] > P.nthreads[bw_] && !thief[bw_]) {
+      if (combined(bw_) > 0.2 && pend[bw_] > (int)nth[bw_] && !thief[bw_]) {
         if (lane == 0) vs[npv] = bw_;
         npv++;
       }
@@ -532,7 +567,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
       if (j >= nh) break;
       const int h = hw[j];
       if (!thief[h]) continue;
-      const double stack = occ[h] / (double)P.nthreads[h];
+      const double stack = occ[h] / (double)nth[h];
       const Obj o{stack + (double)(C - hg[j]) / (double)P.bw, P.wnbytes[h], h};
       if (obj_less(o, best)) best = o;
     }
@@ -562,6 +597,11 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
       const int v = vs[vi];
       const int b0 = P.bin_ptr[level * W + v], b1 = P.bin_ptr[level * W + v + 1];
       if (b0 == b1 || n_thieves == 0) continue;
+      // the victim's balance state in registers for its bins (it is never a thief, so only
+      // its own requests change it); WorkerState.occupancy is constant in a balance()
+      const double occ_v = occ[v];
+      double ifo_v = ifo[v];
+      int pend_v = pend[v];
       for (int c0 = b0; c0 < b1; c0 += 64) {  // 64 tasks of the bin per load round
         const int i = c0 + lane;
         const bool okl = i < b1;
@@ -576,13 +616,25 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
         // the examined tasks are accepted: 313 -> 387 ms.)
         for (int j = 0; j < nq; j++) {  // :439
           if (n_thieves == 0) break;
+          // task j's row broadcast through SGPRs (readlane: no LDS round trip)
           const int t = __builtin_amdgcn_readlane(tq, j);
           int th = __builtin_amdgcn_readlane(bq, j);
-          double cct = __shfl(cq, j);
-          const double ccv = __shfl(vq, j);
-          const double compute = __shfl(dq, j);
+          double cct = rl_f64(cq, j);
+          const double ccv = rl_f64(vq, j);
+          const double compute = rl_f64(dq, j);
           if (th == NO_THIEF) continue;  // _get_thief -> None (:452-454), for good: thieves only leave
-          if (th < 0 || !thief[th]) {  // the precomputed thief left
+          // the thief's state, read together (one LDS round trip)
+          uint8_t thf = 0;
+          double occ_th = 0.0, ifo_th = 0.0;
+          int pend_th = 0, nt_th = 1;
+          if (th >= 0) {
+            thf = thief[th];
+            occ_th = occ[th];
+            ifo_th = ifo[th];
+            pend_th = pend[th];
+            nt_th = nth[th];
+          }
+          if (th < 0 || !thf) {  // the precomputed thief left
             th = -1;
             if (restricted(P, t)) {
               const Obj b = wave_argmin_valid(P, t, [&](int w) { return thief[w] != 0; });
@@ -593,27 +645,41 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
             }
             if (th < 0 && (!restricted(P, t) || loose(P, t))) th = thief_from_runs(c0 + j, t, &cct);
             if (th < 0) continue;
+            occ_th = occ[th];
+            ifo_th = ifo[th];
+            pend_th = pend[th];
+            nt_th = nth[th];
           }
-          const double occ_thief = combined(th);
-          const double occ_victim = combined(v);
+          const double occ_thief = occ_th + ifo_th;  // combined_occupancy (:505-506)
+          const double occ_victim = occ_v + ifo_v;
           if (occ_thief + cct + compute <= occ_victim - (ccv + compute) / 2) {  // :462-465
             // move_task_request (:279-331) -> _add_to_in_flight (:191-199)
+            ifo_v = ifo_v - (compute + ccv);
+            ifo_th = ifo_th + (compute + cct);
+            pend_v -= 1;
+            pend_th += 1;
             if (lane == 0) {
-              ifo[v] = ifo[v] - (compute + ccv);
-              ifo[th] = ifo[th] + (compute + cct);
-              ift[v] -= 1;
-              ift[th] += 1;
-              P.st_task[ns] = t;
-              P.st_victim[ns] = v;
-              P.st_thief[ns] = th;
-              P.st_level[ns] = level;
-              P.st_cost[ns] = compute + ccv;
-              P.st_occ_victim[ns] = occ_victim;
-              P.st_occ_thief[ns] = occ_thief;
+              ifo[v] = ifo_v;
+              ifo[th] = ifo_th;
+              pend[v] = pend_v;
+              pend[th] = pend_th;
+              const int q = (int)(ns & 63);
+              rq->task[q] = t;
+              rq->victim[q] = v;
+              rq->thief[q] = th;
+              rq->level[q] = level;
+              rq->cost[q] = compute + ccv;
+              rq->occ_v[q] = occ_victim;
+              rq->occ_t[q] = occ_thief;
             }
-            __syncthreads();
             ns++;
-            if (!is_unoccupied(th, combined(th), P.nproc[th] + ift[th])) {  // :487-493
+            if ((ns & 63) == 0) {
+              __syncthreads();
+              flush(ns);
+            }
+            // is_unoccupied (scheduler.py:2997-3004) of the thief after the request (:487-493)
+            const double oc = occ_th + ifo_th;
+            if (!(pend_th < nt_th || oc < nt_th * avg / 2)) {
               if (lane == 0) {
                 thief[th] = 0;
                 run_alive[P.run_of_w[th]] -= 1;
@@ -624,11 +690,12 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           }
         }
       }
+      __syncthreads();
       // check_idle_saturated(victim, occ=combined) (scheduler.py:2949-2995)
       double o = combined(v);
       if (o < 0) o = occ[v];  // :2974-2975
       const int p = P.nproc[v];
-      const int nc = P.nthreads[v];
+      const int nc = nth[v];
       uint8_t id = 0, sa = 0;
       if (is_unoccupied(v, o, p)) {
         id = 1;
@@ -647,7 +714,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   finish();
 }
 
-inline size_t balance_lds_bytes(int W) { return (size_t)W * (8 + 8 + 4 + 4 + 4 + 4 + 4); }
+inline size_t balance_lds_bytes(int W) { return ((balance_state_bytes(W) + 15) & ~(size_t)15) + sizeof(RqStage); }
 
 }  // namespace steal
 

@@ -1224,6 +1224,8 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
       (n_data && (!d_nbytes || !d_get_nbytes || !h_ptr)))
     return fail(e, DGP_E_ARG, "dgp_steal_load: bad sizes or null pointers");
   if (S::balance_lds_bytes(W) > 160 * 1024) return fail(e, DGP_E_ARG, "dgp_steal_load: too many workers");
+  for (int32_t w = 0; w < W; w++)  // k_balance keeps nthreads as uint16 in LDS
+    if (nthreads[w] <= 0 || nthreads[w] > 65535) return fail(e, DGP_E_ARG, "dgp_steal_load: nthreads out of range");
   if ((size_t)W * S::N_LEVELS >= (1u << 30)) return fail(e, DGP_E_ARG, "dgp_steal_load: W too large");
   if (T >= (1ll << 31)) return fail(e, DGP_E_ARG, "dgp_steal_load: too many tasks");
   // the shapes the kernels assume, checked on the host
