@@ -348,6 +348,9 @@ __global__ void k_runs(Prob P) {
 }
 
 // ---------------------------------------------------------------------- balance
+#ifndef DGP_STEAL_PROF
+#define DGP_STEAL_PROF 0  // diagnostics: k_balance prints examined / re-evaluated / cycle counts
+#endif
 __device__ __forceinline__ double rl_f64(double x, int l) {  // lane l's double, via SGPRs
   const long long b = __double_as_longlong(x);
   const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
@@ -416,6 +419,10 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
     const int nt = nth[w];
     return np < nt || o < nt * avg / 2;
   };
+#if DGP_STEAL_PROF
+  unsigned long long pr_left = 0, pr_left_cyc = 0, pr_exam = 0;
+  const unsigned long long pr_t0 = __builtin_amdgcn_s_memtime();
+#endif
   long long ns_out = 0;  // requests already written to the output arrays
   auto flush = [&](long long n) {  // staged requests [ns_out, n)
     const long long k = ns_out + lane;
@@ -440,6 +447,11 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
       P.sat_out[w] = sat[w];
     }
     if (lane == 0) *P.n_steals = ns;
+#if DGP_STEAL_PROF
+    if (lane == 0)
+      printf("k_balance: requests %lld examined %llu thief-left %llu (%llu cycles) total %llu cycles\n", ns, pr_exam,
+             pr_left, pr_left_cyc, __builtin_amdgcn_s_memtime() - pr_t0);
+#endif
   };
   if (n_thieves == 0 || n_thieves == W) {  // :410-411
     finish();
@@ -623,6 +635,9 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           const double ccv = rl_f64(vq, j);
           const double compute = rl_f64(dq, j);
           if (th == NO_THIEF) continue;  // _get_thief -> None (:452-454), for good: thieves only leave
+#if DGP_STEAL_PROF
+          pr_exam++;
+#endif
           // the thief's state, read together (one LDS round trip)
           uint8_t thf = 0;
           double occ_th = 0.0, ifo_th = 0.0;
@@ -635,6 +650,10 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
             nt_th = nth[th];
           }
           if (th < 0 || !thf) {  // the precomputed thief left
+#if DGP_STEAL_PROF
+            const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+            pr_left++;
+#endif
             th = -1;
             if (restricted(P, t)) {
               const Obj b = wave_argmin_valid(P, t, [&](int w) { return thief[w] != 0; });
@@ -644,6 +663,9 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
               }
             }
             if (th < 0 && (!restricted(P, t) || loose(P, t))) th = thief_from_runs(c0 + j, t, &cct);
+#if DGP_STEAL_PROF
+            pr_left_cyc += __builtin_amdgcn_s_memtime() - tp0;
+#endif
             if (th < 0) continue;
             occ_th = occ[th];
             ifo_th = ifo[th];
