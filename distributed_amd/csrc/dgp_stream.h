@@ -43,6 +43,9 @@ __constant__ Dev c_dev;
 #ifndef DGP_PHASE_PROBES
 #define DGP_PHASE_PROBES 0  // per-phase s_memtime probes in the executors (diagnostics)
 #endif
+#ifndef DGP_VMPROBE
+#define DGP_VMPROBE 0  // diagnostics: store-drain time at each claim attempt (prof 11 / 12)
+#endif
 #ifndef DGP_EXE_SLEEP
 #define DGP_EXE_SLEEP 1  // s_sleep units (64 clocks) between an idle executor's polls
 #endif
@@ -2740,6 +2743,13 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       const unsigned kmin = wmin_u32(key);
       if (kmin == ~0u) break;
       const int s = (int)(kmin & 63u);
+#if DGP_VMPROBE  // diagnostics: how long this executor's earlier global stores take to drain
+      {
+        const unsigned long long ta = mclk();
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        if (lane == 0) { S.prof[11] += mclk() - ta; S.prof[12] += 1; }
+      }
+#endif
       if (lane == s) key = ~0u;  // tried
       if (!G && (rlu(fsl, s) & (F_GLOBAL | F_RUNM))) continue;  // left to the global-capable executor
       // the descriptor of the slot's stimulus (global ring) is in flight while the claim completes
