@@ -43,6 +43,9 @@ __constant__ Dev c_dev;
 #ifndef DGP_PHASE_PROBES
 #define DGP_PHASE_PROBES 0  // per-phase s_memtime probes in the executors (diagnostics)
 #endif
+#ifndef DGP_EXE_PRIO
+#define DGP_EXE_PRIO 1  // 0: fixed priority 2; 1 / 2: executors issue at priority 3 while running a stimulus, 1 / 0 while polling
+#endif
 #ifndef DGP_VMPROBE
 #define DGP_VMPROBE 0  // diagnostics: store-drain time at each claim attempt (prof 11 / 12)
 #endif
@@ -2798,6 +2801,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       continue;
     }
     lds_fence();
+    if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(3);  // busy: ahead of the polling waves
     if (lane == 0) atomicAdd(&S.busy_exe, 1);
     if (DGP_TRACE && lane == 0) {
       TR(cr, 2);
@@ -2821,6 +2825,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       PROF(atomicAdd(&S.prof[5], mclk() - t0));
       atomicSub(&S.busy_exe, 1);
     }
+    if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(DGP_EXE_PRIO == 2 ? 0 : 1);  // polling again
     t_idle = mclk();
   }
   if (lane == 0) {

@@ -288,6 +288,9 @@ def main_add_workers(only):
                                                               random_durations=True, nthreads="random"), 1.1, 5, 24),
         "svcaddw_c2mini_satinf": (lambda: G.graphs.random_dag(3000, 32, seed=22), float("inf"), 6, 12),
         "svcaddw_c2mini_sat1.0": (lambda: G.graphs.random_dag(3000, 60, seed=23), 1.0, 7, 70),
+        # 1,000 workers (worker state in LDS) growing to 1,300: the stream engine switches to
+        # its global-memory worker layout part-way through the stream
+        "svcaddw_w1000_sat1.1": (lambda: G.graphs.random_dag(30000, 1000, seed=24), 1.1, 8, 300),
     }
     for name, (mk, sat, seed, n_add) in cases.items():
         if only and name not in only:
