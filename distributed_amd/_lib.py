@@ -32,6 +32,7 @@ SIGNATURES = {
     "dgp_tasks_finished": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dgp_move_task": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "dgp_add_worker": (C.c_int, [_P, C.c_int32, _P]),
+    "dgp_add_graph": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P, _P]),
     "dgp_snapshot": (C.c_int, [_P]),
     "dgp_num_placements": (C.c_int64, [_P]),
     "dgp_get_placements": (C.c_int, [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, _P]),
@@ -55,7 +56,7 @@ SIGNATURES = {
     "dgp_steal_run": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 _lib = None
 
 

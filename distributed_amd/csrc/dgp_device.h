@@ -1707,9 +1707,10 @@ __global__ void k_init_workers(const Dev* __restrict__ Dp) {
 // update_graph, part 1 (:4600-4611 -> _transition_released_waiting :2078-2119), every
 // task in parallel: waiting_on = dependencies without a replica; waiters = dependents
 // (all of them go to waiting in the same stimulus; priorities are topological)
-__global__ void k_ug_init(const Dev* __restrict__ Dp) {
+// (tasks [lo, N): lo = 0 for the first graph, the first new task for a later one)
+__global__ void k_ug_init(const Dev* __restrict__ Dp, int lo) {
   const Dev& D = *Dp;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < D.N; t += gridDim.x * blockDim.x) {
+  for (int t = lo + blockIdx.x * blockDim.x + threadIdx.x; t < D.N; t += gridDim.x * blockDim.x) {
     int wo = 0;
     for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
       const unsigned long long* row = D.holders + (size_t)D.dep_idx[k] * D.WB;
@@ -1726,14 +1727,17 @@ __global__ void k_ug_init(const Dev* __restrict__ Dp) {
 // update_graph, part 2: the tasks that went waiting -> processing, in priority order,
 // dispatched one by one (they read global state); once idle_task_count is empty every
 // further root-ish task is queued in bulk (:2761) — order-preserving.
-__global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp) {
+// Tasks at priority positions [lo, N) (a later graph's tasks follow every earlier one in
+// priority: a new generation); its placements append to the placement log.
+__global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp, int lo) {
   const Dev& D = *Dp;
   __shared__ CoopShared S;
   __shared__ int64_t s_nr, s_pos;
   Ctl* c = D.ctl;
+  const int64_t pl0 = (int64_t)c->n_placed;  // 0 for the first graph
   // ready list in priority order
   int64_t base = 0;
-  for (int i0 = 0; i0 < D.N; i0 += blockDim.x) {
+  for (int i0 = lo; i0 < D.N; i0 += blockDim.x) {
     int i = i0 + threadIdx.x;
     int t = i < D.N ? D.order[i] : -1;
     bool r = t >= 0 && D.remaining[t] == 0;
@@ -1825,15 +1829,15 @@ __global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp)
   __syncthreads();
   int64_t np = s_np;
   for (int64_t i = threadIdx.x; i < np; i += blockDim.x) {
-    D.pl_task[i] = D.st_task[i];
-    D.pl_worker[i] = D.st_worker[i];
-    D.pl_comm[i] = D.st_comm[i];
-    D.pl_start[i] = D.st_start[i];
-    D.pl_wsnbytes[i] = D.st_wsnbytes[i];
-    D.pl_route[i] = D.st_route[i];
+    D.pl_task[pl0 + i] = D.st_task[i];
+    D.pl_worker[pl0 + i] = D.st_worker[i];
+    D.pl_comm[pl0 + i] = D.st_comm[i];
+    D.pl_start[pl0 + i] = D.st_start[i];
+    D.pl_wsnbytes[pl0 + i] = D.st_wsnbytes[i];
+    D.pl_route[pl0 + i] = D.st_route[i];
   }
   if (threadIdx.x == 0) {
-    c->n_placed = np;
+    c->n_placed = pl0 + np;
     c->round_start = 0;
     c->round_n = 0;
   }

@@ -84,6 +84,9 @@ struct dgp_engine {
   StealCtx steal;
   std::vector<uint8_t> tflags_h;           // task flags as set_graph computed them
   std::vector<int32_t> group_h;            // TaskGroup of each task
+  std::vector<int64_t> h_dep_ptr, h_prio;  // the uploaded graph (dgp_add_graph appends to it)
+  std::vector<int32_t> h_dep_idx, h_prefix;
+  std::vector<uint8_t> h_wanted;
   std::vector<int64_t> gdep_n, gdep_len;   // per group: len(tg.dependencies), sum of their lengths
   std::vector<int8_t> rootish_override_h;  // TaskState._rootish per task (-1: None)
 };
@@ -492,17 +495,19 @@ int dgp_set_workers(dgp_engine* e, int32_t n_workers, const int32_t* nthreads) {
   return dgp_set_config(e, D.bandwidth, D.default_data_size, D.unknown_duration, D.saturation);
 }
 
-int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const int32_t* dep_idx, const int64_t* prio,
-                  const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
-                  const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override) {
-  if (!e) return DGP_E_ARG;
-  if (!e->have_workers) return fail(e, DGP_E_STATE, "dgp_set_workers must come first");
+}  // extern "C"
+
+namespace {
+
+// Validate a whole graph, derive its host-side structures (dependents CSR in priority order,
+// priority order, root-ish groups, task flags) and upload it into fresh allocations on
+// e->graph_allocs. Dynamic state is left to the caller (dgp_reset, or dgp_add_graph's copy).
+int upload_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const int32_t* dep_idx, const int64_t* prio,
+                 const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
+                 const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override) {
   if (n_tasks <= 0 || n_tasks >= (1ll << 24) - 1) return fail(e, DGP_E_ARG, "n_tasks out of range (< 2^24 - 1)");
   if (n_prefixes <= 0 || n_groups <= 0) return fail(e, DGP_E_ARG, "need prefixes and groups");
   if (n_prefixes > 4096) return fail(e, DGP_E_ARG, "at most 4096 task prefixes");
-  HIPCHK(e, hipSetDevice(e->device));
-  free_list(e->graph_allocs);
-  e->have_graph = false;
   const int64_t N = n_tasks;
   const int64_t E = dep_ptr[N];
   if (dep_ptr[0] != 0 || E < 0) return fail(e, DGP_E_ARG, "bad dep_ptr");
@@ -666,9 +671,32 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
   e->tflags_h = tflags;
   e->group_h.assign(group_id, group_id + N);
   e->rootish_override_h.assign(rootish_override, rootish_override + N);
+  e->h_dep_ptr.assign(dep_ptr, dep_ptr + N + 1);
+  e->h_dep_idx.assign(dep_idx, dep_idx + E);
+  e->h_prio.assign(prio, prio + N);
+  e->h_prefix.assign(prefix_id, prefix_id + N);
+  e->h_wanted.assign(wanted, wanted + N);
   D.restr_ptr = nullptr;  // no restrictions until dgp_set_restrictions
   D.restr_idx = nullptr;
   D.restr_flags = nullptr;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const int32_t* dep_idx, const int64_t* prio,
+                  const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
+                  const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override) {
+  if (!e) return DGP_E_ARG;
+  if (!e->have_workers) return fail(e, DGP_E_STATE, "dgp_set_workers must come first");
+  HIPCHK(e, hipSetDevice(e->device));
+  free_list(e->graph_allocs);
+  e->have_graph = false;
+  if (int rc = upload_graph(e, n_tasks, dep_ptr, dep_idx, prio, prefix_id, n_prefixes, prefix_default_duration,
+                            group_id, n_groups, wanted, rootish_override))
+    return rc;
   e->have_graph = true;
   e->err.clear();
   return dgp_reset(e);
@@ -794,10 +822,10 @@ int dgp_update_graph(dgp_engine* e) {
   const dgp::Dev* DP = e->d_dev;
   hipStream_t s = e->stream;
   if (int rc = timed_launch(e, 3, [&] {
-        hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(e->D.N, 256, 2048)), dim3(256), 0, s, DP);
+        hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(e->D.N, 256, 2048)), dim3(256), 0, s, DP, 0);
       }))
     return rc;
-  if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP); }))
+  if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP, 0); }))
     return rc;
   if (e->snap_rounds > 0) {
     hipLaunchKernelGGL(dgp::k_snapshot, dim3(8), dim3(256), 0, s, DP, e->d_aux + 1, 0);
@@ -1005,6 +1033,145 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
   dgp::Ctl c;
   if (int rc2 = check_device_error(e, &c)) return rc2;  // synchronises the stream
   if (n_new_placements) *n_new_placements = placed;
+  e->last_placed = c.n_placed;
+  return 0;
+}
+
+int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx, const int64_t* prio,
+                  const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
+                  const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override,
+                  int64_t* n_new_placements) {
+  if (n_new_placements) *n_new_placements = 0;
+  if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
+  dgp::Dev& D = e->D;
+  if (D.restr_flags) return fail(e, DGP_E_STATE, "dgp_add_graph: not with worker restrictions");
+  if (n_new <= 0 || !dep_ptr || !prio || !prefix_id || !prefix_default_duration || !group_id || !wanted ||
+      !rootish_override)
+    return fail(e, DGP_E_ARG, "dgp_add_graph: bad arguments");
+  const int64_t N0 = D.N, E0 = e->E, N1 = N0 + n_new;
+  const int32_t P0 = D.P, G0 = D.G;
+  if (n_prefixes < P0 || n_groups < G0) return fail(e, DGP_E_ARG, "dgp_add_graph: prefix / group tables shrank");
+  if (n_prefixes > dgp::st::PD)
+    return fail(e, DGP_E_STATE, "dgp_add_graph: more task prefixes than the stream engine carries (8)");
+  if (dep_ptr[0] != 0) return fail(e, DGP_E_ARG, "dgp_add_graph: bad dep_ptr");
+  const int64_t En = dep_ptr[n_new];
+  for (int64_t k = 0; k < En; k++)
+    if (dep_idx[k] < 0 || dep_idx[k] >= n_new)
+      return fail(e, DGP_E_ARG, "dgp_add_graph: dependencies must be tasks of the new graph");
+  const int64_t pmax = *std::max_element(e->h_prio.begin(), e->h_prio.end());
+  for (int64_t t = 0; t < n_new; t++)
+    if (prio[t] <= pmax) return fail(e, DGP_E_ARG, "dgp_add_graph: new priorities must follow every earlier task's");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  // the whole graph, old tasks first
+  std::vector<int64_t> dp(e->h_dep_ptr), pr(e->h_prio);
+  std::vector<int32_t> di(e->h_dep_idx), pf(e->h_prefix), gr(e->group_h);
+  std::vector<uint8_t> wa(e->h_wanted);
+  std::vector<int8_t> ov(e->rootish_override_h);
+  for (int64_t t = 0; t < n_new; t++) {
+    dp.push_back(E0 + dep_ptr[t + 1]);
+    pr.push_back(prio[t]);
+    pf.push_back(prefix_id[t]);
+    gr.push_back(group_id[t]);
+    wa.push_back(wanted[t]);
+    ov.push_back(rootish_override[t]);
+  }
+  for (int64_t k = 0; k < En; k++) di.push_back((int32_t)(dep_idx[k] + N0));
+  std::vector<double> pd(e->prefix_defaults);
+  pd.resize(n_prefixes);
+  for (int32_t q = P0; q < n_prefixes; q++) pd[q] = prefix_default_duration[q];
+  // released + waiting per group after the new tasks arrive (they start released)
+  std::vector<int64_t> relwait(n_groups, 0);
+  HIPCHK(e, hipMemcpy(relwait.data(), D.g_relwait, (size_t)G0 * 8, hipMemcpyDeviceToHost));
+  for (int64_t t = 0; t < n_new; t++) relwait[group_id[t]]++;
+  const dgp::Dev old = D;
+  const int64_t old_rlog = D.rlog_cap;
+  std::vector<void*> old_allocs;
+  old_allocs.swap(e->graph_allocs);
+  e->have_graph = false;
+  if (int rc = upload_graph(e, N1, dp.data(), di.data(), pr.data(), pf.data(), n_prefixes, pd.data(), gr.data(),
+                            n_groups, wa.data(), ov.data())) {
+    free_list(e->graph_allocs);  // the engine keeps its old graph
+    e->graph_allocs.swap(old_allocs);
+    D = old;
+    return rc;
+  }
+  e->have_graph = true;
+  // the dynamic state of the old tasks carried over; the new ones as dgp_reset leaves them
+  hipStream_t s = e->stream;
+  auto carry = [&](void* dst, const void* src, size_t old_bytes, size_t new_bytes, int fill) -> hipError_t {
+    hipError_t st = hipMemsetAsync(dst, fill, new_bytes, s);
+    if (st == hipSuccess && old_bytes) st = hipMemcpyAsync(dst, src, old_bytes, hipMemcpyDeviceToDevice, s);
+    return st;
+  };
+  const size_t n0 = N0, n1 = N1;
+  HIPCHK(e, carry(D.res_nbytes, old.res_nbytes, n0 * 8, n1 * 8, 0xff));
+  HIPCHK(e, carry(D.res_start, old.res_start, n0 * 8, n1 * 8, 0));
+  HIPCHK(e, carry(D.res_stop, old.res_stop, n0 * 8, n1 * 8, 0));
+  HIPCHK(e, carry(D.state, old.state, n0, n1, 0));
+  HIPCHK(e, carry(D.remaining, old.remaining, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.waiters, old.waiters, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.proc_on, old.proc_on, n0 * 4, n1 * 4, 0xff));
+  HIPCHK(e, carry(D.cur_nbytes, old.cur_nbytes, n0 * 8, n1 * 8, 0xff));
+  HIPCHK(e, carry(D.holders, old.holders, n0 * D.WB * 8, n1 * D.WB * 8, 0));
+  HIPCHK(e, carry(D.ready_key, old.ready_key, n0 * 8, n1 * 8, 0));
+  HIPCHK(e, carry(D.release_key, old.release_key, n0 * 8, n1 * 8, 0));
+  HIPCHK(e, carry(D.cand_n, old.cand_n, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.qarr, old.qarr, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.pl_task, old.pl_task, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.pl_worker, old.pl_worker, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.pl_comm, old.pl_comm, n0 * 8, n1 * 8, 0));
+  HIPCHK(e, carry(D.pl_start, old.pl_start, n0 * 8, n1 * 8, 0));
+  HIPCHK(e, carry(D.pl_wsnbytes, old.pl_wsnbytes, n0 * 8, n1 * 8, 0));
+  HIPCHK(e, carry(D.pl_route, old.pl_route, n0, n1, 0));
+  HIPCHK(e, carry(D.run_id, old.run_id, n0 * 4, n1 * 4, 0xff));
+  HIPCHK(e, carry(D.holder_of, old.holder_of, n0 * 4, n1 * 4, 0xff));
+  HIPCHK(e, carry(D.fr_mark, old.fr_mark, n0 * 4, n1 * 4, 0xff));
+  HIPCHK(e, carry(D.rel_mark, old.rel_mark, n0 * 4, n1 * 4, 0xff));
+  HIPCHK(e, carry(D.rlog, old.rlog, (size_t)old_rlog * sizeof(dgp::st::SRec), (size_t)D.rlog_cap * sizeof(dgp::st::SRec), 0));
+  HIPCHK(e, carry(D.sv_task, old.sv_task, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.sv_worker, old.sv_worker, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.sv_cseq, old.sv_cseq, n0 * 4, n1 * 4, 0xff));
+  HIPCHK(e, carry(D.svc_len, old.svc_len, 8, 8, 0));
+  // prefixes: TaskPrefix state of the known ones kept, the new ones at their defaults
+  for (double* const* pp : {&D.pdur_cur, &D.pdur_walk, &D.pdur_pre}) {
+    HIPCHK(e, hipMemcpyAsync(*pp, pd.data(), (size_t)n_prefixes * 8, hipMemcpyHostToDevice, s));
+  }
+  HIPCHK(e, hipMemcpyAsync(D.pdur_cur, old.pdur_cur, (size_t)P0 * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(e, hipMemcpyAsync(D.pdur_walk, old.pdur_walk, (size_t)P0 * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(e, hipMemcpyAsync(D.pdur_pre, old.pdur_pre, (size_t)P0 * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(e, carry(D.pmaxexec, old.pmaxexec, (size_t)P0 * 8, (size_t)n_prefixes * 8, 0));
+  {
+    std::vector<double> mx(n_prefixes, -1.0);
+    HIPCHK(e, hipMemcpyAsync(D.pmaxexec, mx.data(), (size_t)n_prefixes * 8, hipMemcpyHostToDevice, s));
+  }
+  // groups
+  HIPCHK(e, hipMemcpyAsync(D.g_relwait, relwait.data(), (size_t)n_groups * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(e, carry(D.g_left, old.g_left, (size_t)G0 * 8, (size_t)n_groups * 8, 0));
+  HIPCHK(e, carry(D.g_lastw, old.g_lastw, (size_t)G0 * 4, (size_t)n_groups * 4, 0xff));
+  HIPCHK(e, hipStreamSynchronize(s));
+  free_list(old_allocs);
+  // the update_graph stimulus of the new tasks (:4600-4651): released -> waiting, the
+  // runnable ones (no dependency: the new graph is independent of the old) to processing
+  // or queued in priority order
+  if (int rc = sync_dev(e)) return rc;
+  dgp::Ctl c0;
+  if (int rc = read_ctl(e, &c0)) return rc;
+  const dgp::Dev* DP = e->d_dev;
+  if (int rc = timed_launch(e, 3, [&] {
+        hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(n_new, 256, 2048)), dim3(256), 0, s, DP, (int)N0);
+      }))
+    return rc;
+  if (int rc = timed_launch(e, 3, [&] {
+        hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP, (int)N0);
+      }))
+    return rc;
+  if (int rc = set_runids(e)) return rc;
+  e->mode = 2;
+  dgp::Ctl c;
+  if (int rc = check_device_error(e, &c)) return rc;
+  if (n_new_placements) *n_new_placements = (int64_t)(c.n_placed - c0.n_placed);
   e->last_placed = c.n_placed;
   return 0;
 }

@@ -192,6 +192,32 @@ class PlacementEngine:
         self.n_workers += 1
         return int(newp.value)
 
+    def add_graph(self, g: dict) -> int:
+        """A later graph submission (Scheduler.update_graph, distributed/scheduler.py
+        :4662-4751) on a running engine: ``g`` holds the new tasks only (dependencies
+        relative to it, priorities after every earlier task's, prefix / group ids and
+        ``prefix_default_dur`` / ``group_prefix`` over the engine-wide tables). Runs their
+        update_graph stimulus; returns the number of placements it made."""
+        arrs = {
+            "dep_ptr": np.ascontiguousarray(g["dep_ptr"], np.int64),
+            "dep_idx": np.ascontiguousarray(g["dep_idx"], np.int32),
+            "prio": np.ascontiguousarray(g["prio"], np.int64),
+            "prefix_id": np.ascontiguousarray(g["prefix_id"], np.int32),
+            "prefix_default_dur": np.ascontiguousarray(g["prefix_default_dur"], np.float64),
+            "group_id": np.ascontiguousarray(g["group_id"], np.int32),
+            "wanted": np.ascontiguousarray(g["wanted"], np.uint8),
+            "rootish_override": np.ascontiguousarray(g["rootish_override"], np.int8),
+        }
+        n = len(arrs["prio"])
+        newp = C.c_int64(0)
+        self._check(self.lib.dgp_add_graph(
+            self.h, n, _ptr(arrs["dep_ptr"]), _ptr(arrs["dep_idx"]), _ptr(arrs["prio"]), _ptr(arrs["prefix_id"]),
+            len(arrs["prefix_default_dur"]), _ptr(arrs["prefix_default_dur"]), _ptr(arrs["group_id"]),
+            len(g["group_prefix"]), _ptr(arrs["wanted"]), _ptr(arrs["rootish_override"]), C.byref(newp)),
+            "dgp_add_graph")
+        self.n_tasks += n
+        return int(newp.value)
+
     def snapshot(self):
         """Append one per-worker snapshot (service mode round boundary)."""
         self._check(self.lib.dgp_snapshot(self.h), "dgp_snapshot")

@@ -26,6 +26,9 @@
  *   dgp_add_worker        Scheduler.add_worker (scheduler.py:4308-4441): a worker joins a running
  *                         engine: total_nthreads (:4383), check_idle_saturated (:4398), the
  *                         queue refill stimulus_queue_slots_maybe_opened (:4416-4420)
+ *   dgp_add_graph         a later Scheduler.update_graph on a running engine (scheduler.py:4662-4751,
+ *                         _create_taskstate_from_graph :4512-4653): new tasks, then their
+ *                         update_graph stimulus
  *   dgp_snapshot          one per-worker snapshot (occupancy, nbytes, processing, idle /
  *                         saturated / idle_task_count, queue length) at a caller-chosen point
  *   dgp_run_rounds        the synthetic executor of the replay protocol: round k completes
@@ -45,7 +48,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 6
+#define DGP_ABI_VERSION 7
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -159,6 +162,22 @@ int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief);
  * no-worker, so bulk_schedule_unrunnable_after_adding_worker :3173-3186 has nothing to do).
  * Snapshots taken earlier read 0 for the new worker. */
 int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements);
+
+/* A later graph submission (Scheduler.update_graph, scheduler.py:4662-4751 ->
+ * _create_taskstate_from_graph :4512-4653) on a running engine, service mode: n_new tasks
+ * appended with indices N.. (dep_ptr / dep_idx relative to the new graph: the new graph may
+ * not depend on earlier tasks), priorities after every earlier task's (a new generation,
+ * :4713), prefix / group ids in the engine-wide tables (n_prefixes / n_groups >= the
+ * current counts; prefix_default_duration is read for the new prefixes only: a known
+ * TaskPrefix keeps its duration average). Group sizes and root-ish groups follow the grown
+ * graph (is_rootish :2929-2947). Then the update_graph stimulus of the new tasks (:4600-4651):
+ * released -> waiting, the runnable ones to processing (or queued) in priority order.
+ * *n_new_placements receives the placements made. Stream-engine graphs (<= 8 prefixes in
+ * total), no restrictions. */
+int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx, const int64_t* prio,
+                  const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
+                  const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override,
+                  int64_t* n_new_placements);
 
 /* Append one worker snapshot (needs dgp_enable_snapshots): round index = number of calls
  * (update_graph's snapshot is round 0). */

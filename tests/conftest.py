@@ -17,7 +17,12 @@ def pytest_configure(config):
 def golden_files():
     """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
-                  and not f.startswith(("steal_", "svc_steal_", "svcaddw_")))
+                  and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_")))
+
+
+def svc_second_graph_files():
+    """Service-mode message streams with a second graph submitted (gen_service.py second-graph)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcgraph_") and f.endswith(".npz"))
 
 
 def svc_add_worker_files():

@@ -48,6 +48,8 @@ sys.path.insert(0, HERE)
 
 import gen_golden as G  # noqa: E402  (installs the shim, imports the reference)
 
+import operator  # noqa: E402
+
 import dask  # noqa: E402
 import numpy as np  # noqa: E402
 
@@ -313,9 +315,139 @@ def main_add_workers(only):
         print(f"{name}: {len(msgs['task'])} messages, {len(added['msg'])} workers added, routes {routes}")
 
 
+TOKEN2 = "f9e8d7c6b5a49382716051e4d3c2b1a0"
+
+
+def replay_second_graph(g, g2, cfg, seed, at_frac):
+    """The replay protocol's completions as task-finished messages, with a second,
+    independent graph ``g2`` submitted part-way through, the way
+    ``Scheduler._create_taskstate_from_graph`` (distributed/scheduler.py:4512-4653) adds it:
+    new TaskStates (keys of their own groups ``<prefix>-TOKEN2``: the prefixes are the first
+    graph's, so each TaskPrefix keeps its duration average), priority ``(0, 2, i)`` (a later
+    generation than the first graph's ``(0, 1, i)``), dependencies, ``who_wants``, then every
+    new task recommended "waiting" in priority order. The new tasks get indices N.. in the
+    fixture; their completions follow the protocol like the others'."""
+    from distributed.scheduler import Scheduler
+
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    W = len(g["nthreads"])
+    N = g["n_tasks"]
+    type(s).stimulus_task_finished = Scheduler.stimulus_task_finished
+    recs = {}
+    for ts in sorted(tss, key=lambda t: t.priority, reverse=True):
+        recs[ts.key] = "waiting"
+    s._transitions(recs, {}, {}, "update-graph")
+    add_at = int(at_frac * N)
+    nb = list(g["nbytes"]) + list(g2["nbytes"])
+    a0 = list(g["start"]) + list(g2["start"])
+    b0 = list(g["stop"]) + list(g2["stop"])
+    cs = s.clients["client-0"]
+    run_spec = (operator.add, (), {})
+    added = {"msg": -1}
+
+    def submit():
+        keys2 = G.make_keys(g2)
+        new = []
+        for t, key in enumerate(keys2):
+            ts = s.new_task(key, run_spec, "released")
+            tidx[key] = N + t
+            ts.priority = (0, 2, int(g2["prio"][t]))
+            ov = int(g2["rootish_override"][t])
+            if ov >= 0:
+                ts._rootish = bool(ov)
+            new.append(ts)
+        ptr, idx = g2["dep_ptr"], g2["dep_idx"]
+        for t, ts in enumerate(new):
+            for d in idx[ptr[t]:ptr[t + 1]]:
+                ts.add_dependency(new[int(d)])
+            if g2["wanted"][t]:
+                ts.who_wants = {cs}
+                cs.wants_what.add(ts)
+        recs2 = {ts.key: "waiting" for ts in sorted(new, key=lambda t: t.priority, reverse=True)}
+        s._transitions(recs2, {}, {}, "update-graph-2")
+        tss.extend(new)
+
+    msgs = {k: [] for k in ("task", "worker", "run_id", "nbytes", "start", "stop", "status")}
+    stim = [len(rec["task"])]
+    round_ptr = [0]
+    rounds, nplaced = [], []
+    done = 0
+    while True:
+        cur = len(rec["task"])
+        batch = list(range(done, cur))
+        rounds.append(G.snapshot(s, W, widx) + (len(s.queued),))
+        nplaced.append(cur - done)
+        done = cur
+        if not batch:
+            break
+        for pos in batch:
+            if added["msg"] < 0 and len(msgs["task"]) >= add_at:
+                added["msg"] = len(msgs["task"])
+                n0 = len(rec["task"])
+                submit()
+                stim.append(len(rec["task"]) - n0)
+            t = rec["task"][pos]
+            ts = tss[t]
+            assert ts.state == "processing", (ts.key, ts.state)
+            w = widx[ts.processing_on.address]
+            sid = f"task-finished-{len(msgs['task'])}"
+            r, cm, wm = s.stimulus_task_finished(
+                ts.key, ts.processing_on.address, sid, int(ts.run_id), nbytes=int(nb[t]), type=None,
+                typename="int", metadata=None,
+                startstops=[{"action": "compute", "start": float(a0[t]), "stop": float(b0[t])}])
+            assert ts.state != "processing"
+            n0 = len(rec["task"])
+            s._transitions(r, cm, wm, sid)
+            s.stimulus_queue_slots_maybe_opened(stimulus_id=sid)
+            stim.append(len(rec["task"]) - n0)
+            for k, v in zip(("task", "worker", "run_id", "nbytes", "start", "stop", "status"),
+                            (t, w, pos, int(nb[t]), float(a0[t]), float(b0[t]), ACCEPTED)):
+                msgs[k].append(v)
+        round_ptr.append(len(msgs["task"]))
+    assert added["msg"] >= 0
+    rec["stim"] = stim
+    states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
+    return rec, rounds, nplaced, states, msgs, round_ptr, added["msg"]
+
+
+def main_second_graph(only):
+    cases = {
+        "svcgraph_c2var_sat1.1": (dict(n=3000, w=32, seed=31, n_inner_prefixes=3, random_durations=True,
+                                       nthreads="random"), dict(n=2000, seed=32), 1.1, 0.3),
+        "svcgraph_c2mini_satinf": (dict(n=2500, w=24, seed=33), dict(n=1500, seed=34), float("inf"), 0.5),
+    }
+    for name, (a, b, sat, frac) in cases.items():
+        if only and name not in only:
+            continue
+        kw = {k: v for k, v in a.items() if k not in ("n", "w", "seed")}
+        g = G.graphs.random_dag(a["n"], a["w"], seed=a["seed"], **kw)
+        g2 = G.graphs.random_dag(b["n"], a["w"], seed=b["seed"], **kw)
+        g2["group_names"] = [nm.replace(G.graphs.TOKEN, TOKEN2) for nm in g2["group_names"]]
+        assert g2["prefix_names"] == g["prefix_names"]
+        G.graphs.check_graph(g)
+        dask.config.set({"distributed.scheduler.worker-saturation": sat})
+        cfg = G.config_dict(sat)
+        rec, rounds, nplaced, states, msgs, round_ptr, at = replay_second_graph(g, g2, cfg, 0, frac)
+        G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
+        path = os.path.join(HERE, f"{name}.npz")
+        z = dict(np.load(path, allow_pickle=False))
+        z.update(msg_task=np.array(msgs["task"], np.int32), msg_worker=np.array(msgs["worker"], np.int32),
+                 msg_runid=np.array(msgs["run_id"], np.int64), msg_nbytes=np.array(msgs["nbytes"], np.int64),
+                 msg_start=np.array(msgs["start"]), msg_stop=np.array(msgs["stop"]),
+                 msg_status=np.array(msgs["status"], np.int8), msg_round_ptr=np.array(round_ptr, np.int64),
+                 g2_msg=np.array(at, np.int64))
+        for k in ("dep_ptr", "dep_idx", "prio", "prefix_id", "group_id", "wanted", "rootish_override"):
+            z["g2_" + k] = np.asarray(g2[k])
+        np.savez_compressed(path, **z)
+        routes = np.bincount(np.array(rec["route"]), minlength=4).tolist()
+        print(f"{name}: {len(msgs['task'])} messages, second graph of {g2['n_tasks']} at message {at}, routes {routes}")
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "add-workers":
         return main_add_workers(set(sys.argv[2:]))
+    if len(sys.argv) > 1 and sys.argv[1] == "second-graph":
+        return main_second_graph(set(sys.argv[2:]))
     cases = {
         "svc_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 64, seed=15, n_inner_prefixes=3,
                                                           random_durations=True, nthreads="random"), 1.1, 1, 0.0),

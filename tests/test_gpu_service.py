@@ -15,6 +15,9 @@ state resident between calls.
   distributed/scheduler.py:4308-4441): each goes to ``dgp_add_worker`` before the message it
   preceded in the reference, and the queue refill it makes, the later placements, the
   snapshots (as wide as the final worker count) and the task states must equal the reference's;
+* the ``svcgraph_*`` fixtures submit a second, independent graph mid-stream
+  (Scheduler.update_graph on a running scheduler, distributed/scheduler.py:4662-4751): it
+  goes to ``dgp_add_graph`` before the message it preceded in the reference;
 * the ``svc_steal_*`` fixtures interleave confirmed steals (WorkStealing.move_task_confirm,
   distributed/stealing.py:376-384) with that stream: each goes to ``dgp_move_task`` before
   the message it preceded in the reference, and the placements, snapshots and statuses
@@ -25,7 +28,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden_files, svc_add_worker_files, svc_steal_files
+from conftest import GOLDEN, golden_files, svc_add_worker_files, svc_second_graph_files, svc_steal_files
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -235,5 +238,60 @@ def test_service_with_workers_joining(name, per_message):
     assert (np.array(status) == 0).all()
     if cfg["saturation"] != "inf":
         assert refill > 0  # the joins took queued tasks
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+def second_graph(g, z):
+    """The fixture's second graph over the engine-wide tables: priorities after the first
+    graph's, its groups after the first graph's groups, the same prefixes."""
+    G1 = len(g["group_prefix"])
+    return dict(dep_ptr=z["g2_dep_ptr"], dep_idx=z["g2_dep_idx"], prio=z["g2_prio"] + int(g["prio"].max()) + 1,
+                prefix_id=z["g2_prefix_id"], group_id=z["g2_group_id"] + G1, wanted=z["g2_wanted"],
+                rootish_override=z["g2_rootish_override"], prefix_default_dur=g["prefix_default_dur"],
+                group_prefix=np.concatenate([g["group_prefix"], g["group_prefix"]]))
+
+
+@pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])
+@pytest.mark.parametrize("name", svc_second_graph_files())
+def test_service_with_a_second_graph(name, per_message):
+    """A second graph submitted to a running engine (dgp_add_graph) between messages."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    msgs = list(zip(z["msg_task"].tolist(), z["msg_worker"].tolist(), z["msg_runid"].tolist(),
+                    z["msg_nbytes"].tolist(), z["msg_start"].tolist(), z["msg_stop"].tolist()))
+    ptr = z["msg_round_ptr"].tolist()
+    at = int(z["g2_msg"])
+    g2 = second_graph(g, z)
+    R = len(exp["round_nplaced"]) + 2
+    status = []
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        for k in range(len(ptr) - 1):
+            i, e = ptr[k], ptr[k + 1]
+            while i < e:  # batches end at the submission
+                if i == at:
+                    n0 = eng.num_placements()
+                    newp = eng.add_graph(g2)
+                    assert eng.num_placements() == n0 + newp
+                j = i + 1
+                if not per_message:
+                    while j < e and j != at:
+                        j += 1
+                t, w, r, nb, a, b = (np.array(c) for c in zip(*msgs[i:j]))
+                st, _ = eng.tasks_finished(t, w, r, nb, a, b)
+                status.extend(st.tolist())
+                i = j
+            if e > ptr[k]:
+                eng.snapshot()
+        assert eng.n_tasks == g["n_tasks"] + len(g2["prio"])
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert (np.array(status) == 0).all()
     assert_same(out, exp, PL_KEYS + ROUND_KEYS)
     assert np.array_equal(out["final_state"], exp["final_state"])
