@@ -349,13 +349,19 @@ class GPUPlacementExtension(SchedulerPlugin):
             return
         try:
             if self.engine is not None:
-                raise NotImplementedError("a second graph on a running engine")
+                self._add_graph(new)
+                return
             self.workers = list(s.workers)
             self.worker_index = {a: i for i, a in enumerate(self.workers)}
             g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers], s.valid_workers,
                                         self.worker_index)
             self.keys = keys_
             self.task_index = {k: i for i, k in enumerate(keys_)}
+            self.prefix_index = {nm: i for i, nm in enumerate(g["prefix_names"])}
+            self.group_index = {nm: i for i, nm in enumerate(g["group_names"])}
+            self.prefix_dur = list(g["prefix_default_dur"])
+            self.group_prefix = list(g["group_prefix"])
+            self.max_priority = max(ts.priority for ts in new)
             if self.engine_factory is not None:
                 self.engine = self.engine_factory()
             else:
@@ -368,6 +374,45 @@ class GPUPlacementExtension(SchedulerPlugin):
             self.stats["graphs"] += 1
         except Exception as e:  # plugin errors are logged, not raised (scheduler.py:4652-4653)
             self.fallback(f"update_graph: {e}")
+
+    def _add_graph(self, new):
+        """A later update_graph (scheduler.py:4662-4751) on the running engine: the new
+        tasks must not depend on earlier ones (graph_from_tasks raises otherwise) and must
+        all follow them in priority (a new generation, :4713, with no user priority above
+        the earlier graphs'); prefixes and groups map into the engine-wide tables."""
+        s = self.scheduler
+        g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers], s.valid_workers,
+                                    self.worker_index)
+        if "restr_flags" in g:
+            raise NotImplementedError("worker restrictions in a later graph")
+        if min(ts.priority for ts in new) <= self.max_priority:
+            raise NotImplementedError("a later graph whose tasks do not all follow the earlier ones in priority")
+        pmap = np.zeros(len(g["prefix_names"]), np.int32)
+        for i, nm in enumerate(g["prefix_names"]):
+            if nm not in self.prefix_index:
+                self.prefix_index[nm] = len(self.prefix_index)
+                self.prefix_dur.append(float(g["prefix_default_dur"][i]))
+            pmap[i] = self.prefix_index[nm]
+        gmap = np.zeros(len(g["group_names"]), np.int32)
+        for i, nm in enumerate(g["group_names"]):
+            if nm not in self.group_index:
+                self.group_index[nm] = len(self.group_index)
+                self.group_prefix.append(int(pmap[g["group_prefix"][i]]))
+            gmap[i] = self.group_index[nm]
+        n0 = len(self.keys)
+        g2 = dict(dep_ptr=g["dep_ptr"], dep_idx=g["dep_idx"], prio=g["prio"] + n0, prefix_id=pmap[g["prefix_id"]],
+                  group_id=gmap[g["group_id"]], wanted=g["wanted"], rootish_override=g["rootish_override"],
+                  prefix_default_dur=np.array(self.prefix_dur, np.float64),
+                  group_prefix=np.array(self.group_prefix, np.int32))
+        self._end_of_stimulus("the previous stimulus")
+        if not self.active:
+            return
+        self.engine.add_graph(g2)
+        self.keys = self.keys + keys_
+        self.task_index.update({k: n0 + i for i, k in enumerate(keys_)})
+        self.max_priority = max(ts.priority for ts in new)
+        self._fetch()
+        self.stats["graphs"] += 1
 
     def add_worker(self, scheduler=None, worker=None):
         """SchedulerPlugin.add_worker (diagnostics/plugin.py): Scheduler.add_worker calls it

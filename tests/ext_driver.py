@@ -58,6 +58,7 @@ class FixtureEngine:
         self.ext = None
         self.graph = None
         self.diverge = None  # placement index whose decision is swapped with the next one
+        self.graphs = []
 
     def load(self, g, config, results=True):
         self.graph, self.config = g, config
@@ -82,6 +83,10 @@ class FixtureEngine:
             j = self.diverge - offset  # two decisions of one stimulus swapped
             task[j], task[j + 1] = task[j + 1], task[j]
         return {"pl_task": task, "pl_worker": self.exp["pl_worker"][sl]}
+
+    def add_graph(self, g):  # a later graph (the fixture's per-event placement counts)
+        self.graphs.append(g)
+        return self.add_worker(0)
 
     def add_worker(self, nthreads):  # a join (the fixture's per-event placement counts)
         k = self.stim[self.k]
@@ -287,6 +292,98 @@ def run_joins(name):
                 device_decisions=ext.stats["device_decisions"], active=ext.active, reason=ext.reason)
 
 
+def run_second_graph(name):
+    """A ``svcgraph_*`` stream (gen_service.py second-graph): a second, independent graph is
+    submitted mid-stream through the tail of ``_create_taskstate_from_graph``
+    (scheduler.py:4600-4653: the plugins' update_graph hook, then the transitions); the
+    extension uploads it to the engine (dgp_add_graph) and the scheduler takes the engine's
+    decisions for both graphs from then on."""
+    import operator
+
+    from gen_service import TOKEN2
+
+    path = os.path.join(HERE, "golden", name)
+    g, cfg, exp, meta = load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    g["keys"] = None
+    sat = cfg["saturation"]
+    sat = float("inf") if sat == "inf" else float(sat)
+    dask.config.set({"distributed.scheduler.worker-saturation": sat})
+    cfg = dict(cfg, saturation=sat)
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    S = type(s)
+    S.stimulus_task_finished = Scheduler.stimulus_task_finished
+    S.handle_task_finished = Scheduler.handle_task_finished
+    S.validate_key = lambda self, key, ts=None: None
+    S.send_all = lambda self, client_msgs, worker_msgs: None
+    fkeys = [ts.key for ts in tss]
+    eng = FixtureEngine(exp, fkeys)
+    ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
+    eng.ext = ext
+    s.stream_handlers = {}
+    ext._install()
+    priority = {ts.key: ts.priority for ts in tss}
+    recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
+    ext.update_graph(s, client="client-0", keys=set(priority), tasks=list(priority), annotations={},
+                     priority=priority, dependencies={})
+    assert ext.active, ext.reason
+    s._transitions(recs, {}, {}, "update-graph")
+    # the second graph, as the generator built it
+    g2 = {k[3:]: z[k] for k in z.files if k.startswith("g2_")}
+    g2["n_tasks"] = len(g2["prio"])
+    g2["prefix_names"] = g["prefix_names"]
+    g2["group_names"] = [nm.replace(G.graphs.TOKEN, TOKEN2) for nm in g["group_names"]]
+    cs = s.clients["client-0"]
+    N1 = g["n_tasks"]
+    at = int(z["g2_msg"])
+    for i, (t, w) in enumerate(zip(z["msg_task"].tolist(), z["msg_worker"].tolist())):
+        if i == at:
+            keys2 = G.make_keys(g2)
+            new = []
+            for k, key in enumerate(keys2):
+                ts = s.new_task(key, (operator.add, (), {}), "released")
+                tidx[key] = N1 + k
+                ts.priority = (0, 2, int(g2["prio"][k]))
+                new.append(ts)
+            for k, ts in enumerate(new):
+                for d in g2["dep_idx"][g2["dep_ptr"][k]:g2["dep_ptr"][k + 1]]:
+                    ts.add_dependency(new[int(d)])
+                if g2["wanted"][k]:
+                    ts.who_wants = {cs}
+                    cs.wants_what.add(ts)
+            eng.fkeys.extend(keys2)
+            tss.extend(new)
+            prio2 = {ts.key: ts.priority for ts in new}
+            ext.update_graph(s, client="client-0", keys=set(prio2), tasks=list(prio2), annotations={},
+                             priority=prio2, dependencies={})
+            assert ext.active, ext.reason
+            s._transitions({ts.key: "waiting" for ts in sorted(new, key=lambda x: x.priority, reverse=True)}, {}, {},
+                           "update-graph-2")
+        ts = tss[t]
+        s.stream_handlers["task-finished"](
+            key=ts.key, worker=ts.processing_on.address, stimulus_id=f"tf-{t}", run_id=ts.run_id,
+            nbytes=int(z["msg_nbytes"][i]), type=None, typename="int", metadata=None,
+            startstops=[{"action": "compute", "start": float(z["msg_start"][i]), "stop": float(z["msg_stop"][i])}])
+    ext._end_of_stimulus("end of stream")
+    assert ext.active, ext.reason
+    assert len(eng.graphs) == 1
+    up = eng.graphs[0]
+    assert np.array_equal(up["dep_ptr"], g2["dep_ptr"]) and np.array_equal(up["dep_idx"], g2["dep_idx"])
+    pnames = {i: nm for nm, i in ext.prefix_index.items()}
+    gnames = {i: nm for nm, i in ext.group_index.items()}
+    assert [pnames[i] for i in up["prefix_id"]] == [g2["prefix_names"][i] for i in g2["prefix_id"]]
+    assert [gnames[i] for i in up["group_id"]] == [g2["group_names"][i] for i in g2["group_id"]]
+    assert min(up["group_id"]) >= len(g["group_names"])  # new groups after the first graph's
+    assert np.array_equal(up["prio"], np.arange(g2["n_tasks"]) + N1)
+    n = len(exp["pl_task"])
+    assert rec["task"] == exp["pl_task"].tolist()
+    assert rec["worker"] == exp["pl_worker"].tolist()
+    assert np.array_equal(np.array(rec["start"]).view(np.int64), exp["pl_start"].view(np.int64))
+    assert ext.stats["device_decisions"] == n, (ext.stats, n)
+    return dict(fixture=name, placements=n, graphs=ext.stats["graphs"], device_decisions=ext.stats["device_decisions"],
+                active=ext.active, reason=ext.reason)
+
+
 if __name__ == "__main__":
     import warnings
 
@@ -294,4 +391,5 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     diverge = "--diverge" in args
     for nm in [a for a in args if not a.startswith("--")]:
-        print(json.dumps(run_joins(nm) if nm.startswith("svcaddw_") else run(nm, diverge)), flush=True)
+        fn = run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith("svcgraph_") else None
+        print(json.dumps(fn(nm) if fn else run(nm, diverge)), flush=True)

@@ -55,6 +55,16 @@ def test_extension_follows_workers_joining():
         assert r["workers_added"] == r["joins"] > 0, r
 
 
+def test_extension_follows_a_second_graph():
+    """A second, independent graph submitted to the running scheduler: the plugin hook
+    appends it to the engine (dgp_add_graph); every decision still comes from the engine."""
+    names = ["svcgraph_c2var_sat1.1.npz", "svcgraph_c2mini_satinf.npz"]
+    res = drive(names)
+    assert [r["fixture"] for r in res] == names
+    for r in res:
+        assert r["active"] and r["device_decisions"] == r["placements"] and r["graphs"] == 2, r
+
+
 def test_extension_hands_back_on_divergence():
     """A decision out of order: the extension detects it at once and the scheduler's own
     decide_worker carries on; the records are still the reference's."""
