@@ -360,7 +360,9 @@ struct RqStage {  // 64 staged request-log entries
   int32_t task[64], victim[64], thief[64], level[64];
   double cost[64], occ_v[64], occ_t[64];
 };
-__host__ __device__ inline size_t balance_state_bytes(int W) { return (size_t)W * (8 + 8 + 4 + 4 + 4 + 4 + 2 + 4); }
+__host__ __device__ inline size_t balance_state_bytes(int W) {
+  return (size_t)W * (8 + 8 + 4) + ((size_t)6 * W + 2) * 2 + (size_t)W * 4;
+}
 // One wave; all per-worker balance state in LDS: occupancy, in-flight occupancy, the
 // pending task count (len(processing) + in-flight task delta), nthreads, thief / idle /
 // saturated flags, the victim list. The walk's accept path reads nothing from global
@@ -373,11 +375,14 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   double* occ = (double*)smem;
   double* ifo = occ + W;
   int32_t* pend = (int32_t*)(ifo + W);      // len(processing) + in_flight_tasks
-  int32_t* run_first = pend + W;            // first possibly-live position of each run
-  int32_t* run_alive = run_first + W;       // live thieves per run
-  int32_t* run_nxt = run_alive + W;         // next run to look at (skips emptied runs)
-  uint16_t* nth = (uint16_t*)(run_nxt + W);  // WorkerState.nthreads
-  uint8_t* thief = (uint8_t*)(nth + W);
+  // positions, runs and counts below W (<= 4,300 here) fit 16 bits
+  uint16_t* run_first = (uint16_t*)(pend + W);  // first possibly-live position of each run
+  uint16_t* run_alive = run_first + W;          // live thieves per run
+  uint16_t* run_nxt = run_alive + W;            // next run to look at (skips emptied runs)
+  uint16_t* nth = run_nxt + W;                  // WorkerState.nthreads
+  uint16_t* tho = nth + W;                      // the thieves in key order (th_order)
+  uint16_t* rst = tho + W;                      // run_start, R + 1 entries (W + 2 reserved)
+  uint8_t* thief = (uint8_t*)(rst + W + 2);
   uint8_t* idle = thief + W;
   uint8_t* sat = idle + W;
   uint8_t* taken = sat + W;                 // topk scratch
@@ -388,10 +393,12 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   const int R = *P.n_runs;
   auto run_a_g = [&](int r) { return P.run_a[r]; };
   for (int r = lane; r < R; r += 64) {
-    run_first[r] = P.run_start[r];
-    run_alive[r] = P.run_start[r + 1] - P.run_start[r];
-    run_nxt[r] = r + 1;
+    run_first[r] = (uint16_t)P.run_start[r];
+    run_alive[r] = (uint16_t)(P.run_start[r + 1] - P.run_start[r]);
+    run_nxt[r] = (uint16_t)(r + 1);
   }
+  for (int r = lane; r <= R; r += 64) rst[r] = (uint16_t)P.run_start[r];
+  for (int q = lane; q < P.run_start[R]; q += 64) tho[q] = (uint16_t)P.th_order[q];
   int nth_ = 0, nsat_ = 0;
   for (int w = lane; w < W; w += 64) {
     occ[w] = P.occ[w];
@@ -522,7 +529,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
     int y = r;
     while (y < R && y != x && run_alive[y] == 0) {
       const int z = run_nxt[y];
-      run_nxt[y] = x;  // every lane writes the same value
+      run_nxt[y] = (uint16_t)x;  // every lane writes the same value
       y = z;
     }
     return x;
@@ -554,13 +561,13 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
     for (int r = find_run(0); r < R; r = find_run(r + 1)) {
       const double sv = run_a_g(r) + x;
       if (have && sv > best.start) break;
-      const int pe = P.run_start[r + 1];
+      const int pe = rst[r + 1];
       int p = run_first[r];
-      while (p < pe && !thief[P.th_order[p]]) p++;
-      run_first[r] = p;  // removed thieves are skipped for good
+      while (p < pe && !thief[tho[p]]) p++;
+      run_first[r] = (uint16_t)p;  // removed thieves are skipped for good
       int q = p;
       while (q < pe) {
-        const int w = P.th_order[q];
+        const int w = tho[q];
         bool hold = false;
 #pragma unroll
         for (int j = 0; j < MAXH; j++) hold |= j < nh && hw[j] == w;
@@ -568,7 +575,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
         q++;
       }
       if (q < pe) {
-        const int w = P.th_order[q];
+        const int w = tho[q];
         const Obj o{sv, P.wnbytes[w], w};
         if (!have || obj_less(o, best)) best = o;
         have = true;
