@@ -336,7 +336,27 @@ def run_second_graph(name):
     cs = s.clients["client-0"]
     N1 = g["n_tasks"]
     at = int(z["g2_msg"])
+    joins = dict(zip(z["add_msg"].tolist(), z["add_nthreads"].tolist())) if "add_msg" in z.files else {}
+    W0 = len(g["nthreads"])
+    k_join = 0
     for i, (t, w) in enumerate(zip(z["msg_task"].tolist(), z["msg_worker"].tolist())):
+        if i in joins:  # Scheduler.add_worker's placement part (see run_joins)
+            from distributed.core import Status
+            from distributed.scheduler import WorkerState
+
+            addr = f"tcp://w{W0 + k_join:05d}:1"
+            widx[addr] = W0 + k_join
+            ws = WorkerState(address=addr, status=Status.running, pid=0, name=addr, nthreads=joins[i],
+                             memory_limit=0, local_directory="", nanny=None, server_id=addr, scheduler=s)
+            s.workers[addr] = ws
+            s.running.add(ws)
+            s.aliases[addr] = addr
+            s.total_nthreads += ws.nthreads
+            s.check_idle_saturated(ws)
+            ext.add_worker(scheduler=s, worker=addr)
+            s.transitions(s.bulk_schedule_unrunnable_after_adding_worker(ws), f"add-{addr}")
+            s.stimulus_queue_slots_maybe_opened(stimulus_id=f"add-{addr}")
+            k_join += 1
         if i == at:
             keys2 = G.make_keys(g2)
             new = []

@@ -318,7 +318,7 @@ def main_add_workers(only):
 TOKEN2 = "f9e8d7c6b5a49382716051e4d3c2b1a0"
 
 
-def replay_second_graph(g, g2, cfg, seed, at_frac):
+def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0):
     """The replay protocol's completions as task-finished messages, with a second,
     independent graph ``g2`` submitted part-way through, the way
     ``Scheduler._create_taskstate_from_graph`` (distributed/scheduler.py:4512-4653) adds it:
@@ -327,10 +327,12 @@ def replay_second_graph(g, g2, cfg, seed, at_frac):
     generation than the first graph's ``(0, 1, i)``), dependencies, ``who_wants``, then every
     new task recommended "waiting" in priority order. The new tasks get indices N.. in the
     fixture; their completions follow the protocol like the others'."""
-    from distributed.scheduler import Scheduler
+    from distributed.core import Status
+    from distributed.scheduler import Scheduler, WorkerState
 
     s, tss, widx, rec, tidx = G.build_state(g, cfg)
-    W = len(g["nthreads"])
+    W0 = len(g["nthreads"])
+    W = W0 + n_add
     N = g["n_tasks"]
     type(s).stimulus_task_finished = Scheduler.stimulus_task_finished
     recs = {}
@@ -338,6 +340,24 @@ def replay_second_graph(g, g2, cfg, seed, at_frac):
         recs[ts.key] = "waiting"
     s._transitions(recs, {}, {}, "update-graph")
     add_at = int(at_frac * N)
+    # workers joining (with n_add: Scheduler.add_worker's placement part, as in replay_add_workers)
+    rng = np.random.default_rng(seed)
+    join_at = sorted(int(x) for x in rng.choice(N, n_add, replace=False)) if n_add else []
+    join_nt = [int(x) for x in rng.integers(1, 5, n_add)]
+    joins = {"msg": [], "nthreads": []}
+
+    def join(i, nthreads):
+        addr = f"tcp://w{i:05d}:1"
+        widx[addr] = i
+        ws = WorkerState(address=addr, status=Status.running, pid=0, name=addr, nthreads=nthreads, memory_limit=0,
+                         local_directory="", nanny=None, server_id=addr, scheduler=s)
+        s.workers[addr] = ws
+        s.running.add(ws)
+        s.aliases[addr] = addr
+        s.total_nthreads += nthreads
+        s.check_idle_saturated(ws)
+        s.transitions(s.bulk_schedule_unrunnable_after_adding_worker(ws), f"add-worker-{i}")
+        s.stimulus_queue_slots_maybe_opened(stimulus_id=f"add-worker-{i}")
     nb = list(g["nbytes"]) + list(g2["nbytes"])
     a0 = list(g["start"]) + list(g2["start"])
     b0 = list(g["stop"]) + list(g2["stop"])
@@ -381,6 +401,13 @@ def replay_second_graph(g, g2, cfg, seed, at_frac):
         if not batch:
             break
         for pos in batch:
+            while len(joins["msg"]) < n_add and join_at[len(joins["msg"])] <= len(msgs["task"]):
+                k = len(joins["msg"])
+                joins["msg"].append(len(msgs["task"]))
+                joins["nthreads"].append(join_nt[k])
+                n0 = len(rec["task"])
+                join(W0 + k, join_nt[k])
+                stim.append(len(rec["task"]) - n0)
             if added["msg"] < 0 and len(msgs["task"]) >= add_at:
                 added["msg"] = len(msgs["task"])
                 n0 = len(rec["task"])
@@ -404,19 +431,23 @@ def replay_second_graph(g, g2, cfg, seed, at_frac):
                             (t, w, pos, int(nb[t]), float(a0[t]), float(b0[t]), ACCEPTED)):
                 msgs[k].append(v)
         round_ptr.append(len(msgs["task"]))
-    assert added["msg"] >= 0
+    assert added["msg"] >= 0 and len(joins["msg"]) == n_add
     rec["stim"] = stim
     states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
-    return rec, rounds, nplaced, states, msgs, round_ptr, added["msg"]
+    return rec, rounds, nplaced, states, msgs, round_ptr, added["msg"], joins
 
 
 def main_second_graph(only):
     cases = {
         "svcgraph_c2var_sat1.1": (dict(n=3000, w=32, seed=31, n_inner_prefixes=3, random_durations=True,
                                        nthreads="random"), dict(n=2000, seed=32), 1.1, 0.3),
-        "svcgraph_c2mini_satinf": (dict(n=2500, w=24, seed=33), dict(n=1500, seed=34), float("inf"), 0.5),
+        "svcgraph_c2mini_satinf": (dict(n=2500, w=24, seed=33), dict(n=1500, seed=34), float("inf"), 0.5, 0),
+        # the second graph and 40 workers joining in one stream
+        "svcgraph_joins_sat1.1": (dict(n=4000, w=40, seed=35, n_inner_prefixes=2, random_durations=True,
+                                       nthreads="random"), dict(n=3000, seed=36), 1.1, 0.4, 40),
     }
-    for name, (a, b, sat, frac) in cases.items():
+    for name, (a, b, sat, frac, *nadd) in cases.items():
+        nadd = nadd[0] if nadd else 0
         if only and name not in only:
             continue
         kw = {k: v for k, v in a.items() if k not in ("n", "w", "seed")}
@@ -427,7 +458,7 @@ def main_second_graph(only):
         G.graphs.check_graph(g)
         dask.config.set({"distributed.scheduler.worker-saturation": sat})
         cfg = G.config_dict(sat)
-        rec, rounds, nplaced, states, msgs, round_ptr, at = replay_second_graph(g, g2, cfg, 0, frac)
+        rec, rounds, nplaced, states, msgs, round_ptr, at, joins = replay_second_graph(g, g2, cfg, 0, frac, nadd)
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -436,6 +467,8 @@ def main_second_graph(only):
                  msg_start=np.array(msgs["start"]), msg_stop=np.array(msgs["stop"]),
                  msg_status=np.array(msgs["status"], np.int8), msg_round_ptr=np.array(round_ptr, np.int64),
                  g2_msg=np.array(at, np.int64))
+        if nadd:
+            z.update(add_msg=np.array(joins["msg"], np.int64), add_nthreads=np.array(joins["nthreads"], np.int32))
         for k in ("dep_ptr", "dep_idx", "prio", "prefix_id", "group_id", "wanted", "rootish_override"):
             z["g2_" + k] = np.asarray(g2[k])
         np.savez_compressed(path, **z)

@@ -58,7 +58,7 @@ def test_extension_follows_workers_joining():
 def test_extension_follows_a_second_graph():
     """A second, independent graph submitted to the running scheduler: the plugin hook
     appends it to the engine (dgp_add_graph); every decision still comes from the engine."""
-    names = ["svcgraph_c2var_sat1.1.npz", "svcgraph_c2mini_satinf.npz"]
+    names = ["svcgraph_c2var_sat1.1.npz", "svcgraph_c2mini_satinf.npz", "svcgraph_joins_sat1.1.npz"]
     res = drive(names)
     assert [r["fixture"] for r in res] == names
     for r in res:

@@ -266,6 +266,10 @@ def test_service_with_a_second_graph(name, per_message):
     ptr = z["msg_round_ptr"].tolist()
     at = int(z["g2_msg"])
     g2 = second_graph(g, z)
+    joins = {}  # workers joining in the same stream (svcgraph_joins_*): before the graph
+    for m, nt in zip(z["add_msg"].tolist() if "add_msg" in z.files else [],
+                     z["add_nthreads"].tolist() if "add_nthreads" in z.files else []):
+        joins.setdefault(m, []).append(nt)
     R = len(exp["round_nplaced"]) + 2
     status = []
     with PlacementEngine(0) as eng:
@@ -273,14 +277,16 @@ def test_service_with_a_second_graph(name, per_message):
         eng.update_graph()
         for k in range(len(ptr) - 1):
             i, e = ptr[k], ptr[k + 1]
-            while i < e:  # batches end at the submission
+            while i < e:  # batches end at the submission and at each join
+                for nt in joins.get(i, ()):
+                    eng.add_worker(nt)
                 if i == at:
                     n0 = eng.num_placements()
                     newp = eng.add_graph(g2)
                     assert eng.num_placements() == n0 + newp
                 j = i + 1
                 if not per_message:
-                    while j < e and j != at:
+                    while j < e and j != at and j not in joins:
                         j += 1
                 t, w, r, nb, a, b = (np.array(c) for c in zip(*msgs[i:j]))
                 st, _ = eng.tasks_finished(t, w, r, nb, a, b)
