@@ -176,6 +176,57 @@ def c3_leg(eng_cls, local: int, args, link_us: float | None = None) -> dict:
     return leg
 
 
+def service_leg(eng_cls, local: int, args) -> dict:
+    """The drop-in boundary as a live scheduler drives it (service mode): a C2-shaped graph
+    (random DAG, fan-in 4, sat 1.1) on 1,024 workers whose completions arrive as
+    task-finished messages through dgp_tasks_finished, the replay protocol's order, with the
+    new placements read back after every call (what GPUPlacementExtension does). Two
+    granularities: one call per round (every completion of the previous round's placements)
+    and one call per message. Host-inclusive (ctypes, PCIe copies, launches, syncs);
+    checked bit-exact against the oracle's replay of the same protocol."""
+    from distributed_amd import graphs
+
+    g = graphs.random_dag(args.svc_tasks, 1024, seed=5)
+    leg = {"metric": "task-finished messages/sec through dgp_tasks_finished (service mode, host-inclusive)",
+           "workload": f"C2-shaped random DAG, {args.svc_tasks} tasks x 1024 workers, sat 1.1",
+           "n_tasks": int(g["n_tasks"])}
+    outs = {}
+    for mode in ("per_round", "per_message"):
+        eng = eng_cls(local)
+        eng.load(g, CONFIG, results=False)
+        eng.update_graph()
+        done, calls = 0, 0
+        t0 = time.perf_counter()
+        while True:
+            n = eng.num_placements()
+            if n == done:
+                break
+            p = eng.placements(done, n - done)
+            t, w = p["pl_task"], p["pl_worker"]
+            r = np.arange(done, n, dtype=np.int64)
+            nb, a, b = g["nbytes"][t], g["start"][t], g["stop"][t]
+            if mode == "per_round":
+                eng.tasks_finished(t, w, r, nb, a, b)
+                calls += 1
+            else:
+                for i in range(len(t)):
+                    eng.tasks_finished(t[i:i + 1], w[i:i + 1], r[i:i + 1], nb[i:i + 1], a[i:i + 1], b[i:i + 1])
+                    calls += 1
+            done = n
+        dt = time.perf_counter() - t0
+        outs[mode] = eng.placements()
+        eng.close()
+        leg[mode] = {"messages_per_s": round(g["n_tasks"] / dt, 1), "calls": calls,
+                     "us_per_call": round(dt / max(calls, 1) * 1e6, 1), "seconds": round(dt, 4)}
+    if not args.no_cpu_baseline:
+        from oracle import oracle
+
+        ref = oracle.replay(g, CONFIG, snapshots=False)
+        leg["parity"] = bool(all(np.array_equal(o[k], ref[k]) for o in outs.values() for k in (
+            "pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")))
+    return leg
+
+
 def c5_leg(eng_cls, local: int, args, dist, barrier) -> dict:
     """BASELINE.json C5: the 10M-task map + tree-reduce (fan-in 8) DAG on 16,384 workers x 1
     thread, one full replay per rank (replicas only, DESIGN.md §8: every rank replays its
@@ -243,6 +294,8 @@ def main():
     ap.add_argument("--c3-partitions", type=int, default=66_666)
     ap.add_argument("--c3-workers", type=int, default=512)
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (10M x 16k) leg")
+    ap.add_argument("--no-service", action="store_true", help="skip the service-mode (dgp_tasks_finished) leg")
+    ap.add_argument("--svc-tasks", type=int, default=20_000)
     ap.add_argument("--c5-map", type=int, default=8_750_000)
     ap.add_argument("--c5-workers", type=int, default=16_384)
     ap.add_argument("--c5-cpu-map", type=int, default=200_000, help="map tasks of the C5 CPU-baseline sample")
@@ -388,6 +441,8 @@ def main():
     eng.close()
     if rank == 0 and not args.no_c3:
         result["c3"] = c3_leg(PlacementEngine, local, args, result.get("latency_bound", {}).get("link_us"))
+    if rank == 0 and not args.no_service:
+        result["service"] = service_leg(PlacementEngine, local, args)
     if not args.no_c5:  # every rank takes part (barriers, max over ranks)
         c5 = c5_leg(PlacementEngine, local, args, dist, barrier)
         if rank == 0:

@@ -52,6 +52,10 @@ struct dgp_engine {
   hipStream_t stream = nullptr;
   std::string err;
   dgp::Dev D{};
+  // what the device copies of D hold (d_dev, the stream kernel's c_dev symbol) and the
+  // dynamic-LDS size last set on each stream kernel: unchanged ones are not re-sent
+  dgp::Dev dev_sent[2]{};
+  bool dev_valid = false;
   dgp::Ctl* ctl = nullptr;
   long long* d_aux = nullptr;  // [0] next round start, [1] placements at the last snapshot,
                                // [2] service stimuli consumed by the round engine,
@@ -255,7 +259,10 @@ int sync_dev(dgp_engine* e) {
   dgp::Dev h[2] = {e->D, e->D};
   h[0].lds_workers = 0;
   h[1].lds_workers = e->D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
+  if (e->dev_valid && !memcmp(h, e->dev_sent, sizeof h)) return 0;  // the device copy is current
   HIPCHK(e, hipMemcpy(e->d_dev, h, sizeof h, hipMemcpyHostToDevice));
+  memcpy(e->dev_sent, h, sizeof h);
+  e->dev_valid = true;
   return 0;
 }
 
@@ -288,13 +295,28 @@ int launch_stream(dgp_engine* e, long long max_rounds, int snaps) {
   const dgp::Dev& D = e->D;
   const size_t lds_w = dgp::st::lds_worker_bytes(D.W);
   const bool lw = sizeof(dgp::st::SLds) + lds_w <= 160 * 1024;
-  HIPCHK(e, hipMemcpyToSymbolAsync(HIP_SYMBOL(dgp::st::c_dev), &e->D, sizeof(dgp::Dev), 0, hipMemcpyHostToDevice,
-                                   e->stream));
+  // c_dev is one symbol per device, shared by every engine on it: re-sent unless it holds
+  // exactly this engine's Dev already (content compare; engines are driven from one thread)
+  static struct {
+    bool valid;
+    dgp::Dev v;
+  } sent[64];
+  auto& cs = sent[e->device & 63];
+  if (!cs.valid || memcmp(&cs.v, &e->D, sizeof(dgp::Dev))) {
+    HIPCHK(e, hipMemcpyToSymbolAsync(HIP_SYMBOL(dgp::st::c_dev), &e->D, sizeof(dgp::Dev), 0, hipMemcpyHostToDevice,
+                                     e->stream));
+    cs.v = e->D;
+    cs.valid = true;
+  }
   long long mr = max_rounds;
   int sn = snaps;
   void* args[] = {&mr, &sn};
   const void* fn = lw ? (const void*)dgp::st::k_stream<true> : (const void*)dgp::st::k_stream<false>;
-  if (lw) HIPCHK(e, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w));
+  static size_t lds_max[64];  // the kernel attribute is per device: an upper bound, raised when needed
+  if (lw && lds_max[e->device & 63] < lds_w) {
+    HIPCHK(e, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w));
+    lds_max[e->device & 63] = lds_w;
+  }
   // ONE workgroup: every hand-off between the roles stays on this CU
   hipError_t lst = hipSuccess;
   if (int rc = timed_launch(e, 2, [&] {
@@ -916,11 +938,12 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
     if (int rc = run_service_stimuli(e)) return rc;
     long long k = 0;
     HIPCHK(e, hipMemcpyAsync(&k, d_consumed, sizeof k, hipMemcpyDeviceToHost, s));
+    // the answers so far ride on the same synchronisation (the last segment's are final)
+    HIPCHK(e, hipMemcpyAsync(status, e->d_status, n, hipMemcpyDeviceToHost, s));
     if (int rc = check_device_error(e, &c)) return rc;  // synchronises the stream
     if (k <= 0) return fail(e, DGP_E_DEVICE, "dgp_tasks_finished: no progress on the batch");
     off += k;
   }
-  HIPCHK(e, hipMemcpy(status, e->d_status, n, hipMemcpyDeviceToHost));
   if (n_new_placements) *n_new_placements = (int64_t)(c.n_placed - e->last_placed);
   e->last_placed = c.n_placed;
   return 0;
@@ -1201,8 +1224,9 @@ int dgp_get_placements(dgp_engine* e, int64_t offset, int64_t count, int32_t* ta
   if (offset + count > n) return fail(e, DGP_E_ARG, "range beyond the placement log");
   if (count == 0) return 0;
   const dgp::Dev& D = e->D;
-  auto cp = [&](void* dst, const void* src, size_t sz) {
-    return dst ? hipMemcpy(dst, (const char*)src + offset * sz, count * sz, hipMemcpyDeviceToHost) : hipSuccess;
+  auto cp = [&](void* dst, const void* src, size_t sz) {  // queued on the engine's stream, one sync below
+    return dst ? hipMemcpyAsync(dst, (const char*)src + offset * sz, count * sz, hipMemcpyDeviceToHost, e->stream)
+               : hipSuccess;
   };
   HIPCHK(e, cp(task, D.pl_task, 4));
   HIPCHK(e, cp(worker, D.pl_worker, 4));
@@ -1210,6 +1234,7 @@ int dgp_get_placements(dgp_engine* e, int64_t offset, int64_t count, int32_t* ta
   HIPCHK(e, cp(start_time, D.pl_start, 8));
   HIPCHK(e, cp(ws_nbytes, D.pl_wsnbytes, 8));
   HIPCHK(e, cp(route, D.pl_route, 1));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
   return 0;
 }
 

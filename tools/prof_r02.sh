@@ -7,7 +7,7 @@ set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 T=gpurun_out/$1
 mkdir -p $T
-B="--no-cpu-baseline --no-steal --no-c3 --no-c5 --steps 1 --warmup 0"
+B="--no-cpu-baseline --no-steal --no-c3 --no-c5 --no-service --steps 1 --warmup 0"
 keep() {  # keep the k_stream rows of a pass's counter csv
   f=$(find $T/raw_$1 -name '*counter_collection.csv' | head -n 1)
   mkdir -p $T/pmc_$1
