@@ -23,13 +23,18 @@ while True:
     t_fetch += time.perf_counter() - t0
     t, w = p["pl_task"], p["pl_worker"]
     r = np.arange(done, n, dtype=np.int64)
-    for i in range(len(t)):
+    for i in range(min(len(t), int(os.environ.get("SVC_MAX_PER_ROUND", "1000000")))):
         t1 = time.perf_counter()
         eng.tasks_finished(t[i:i + 1], w[i:i + 1], r[i:i + 1], g["nbytes"][t[i:i + 1]], g["start"][t[i:i + 1]],
                            g["stop"][t[i:i + 1]])
         t_call += time.perf_counter() - t1
         calls += 1
+    if os.environ.get("SVC_MAX_PER_ROUND") and len(t) > int(os.environ["SVC_MAX_PER_ROUND"]):
+        k = int(os.environ["SVC_MAX_PER_ROUND"])
+        eng.tasks_finished(t[k:], w[k:], r[k:], g["nbytes"][t[k:]], g["start"][t[k:]], g["stop"][t[k:]])
     done = n
+    if calls >= int(os.environ.get("SVC_MAX_CALLS", "1000000000")):
+        break
 kt = eng.kernel_times()
 print(f"calls {calls}: tasks_finished {t_call / calls * 1e6:.1f} us/call, fetch {t_fetch / calls * 1e6:.1f} us/call")
 for k, (ms, nl) in kt.items():
