@@ -27,6 +27,7 @@ class OrcGraph(C.Structure):
         ("nthreads", _P), ("group_prefix", _P), ("prefix_default_dur", _P),
         ("bandwidth", C.c_int64), ("default_data_size", C.c_int64), ("unknown_duration", C.c_double),
         ("saturation", C.c_double), ("restr_ptr", _P), ("restr_idx", _P), ("restr_flags", _P),
+        ("n_joins", C.c_int64), ("join_before", _P), ("join_nthreads", _P),
     ]
 
 
@@ -34,7 +35,7 @@ class OrcResult(C.Structure):
     _fields_ = [
         ("pl_task", _P), ("pl_worker", _P), ("pl_comm", _P), ("pl_start", _P), ("pl_wsnbytes", _P),
         ("pl_route", _P), ("n_placements", C.c_int64),
-        ("max_rounds", C.c_int64), ("n_rounds", C.c_int64), ("round_nplaced", _P), ("round_occ", _P),
+        ("max_rounds", C.c_int64), ("snap_stride", C.c_int64), ("n_rounds", C.c_int64), ("round_nplaced", _P), ("round_occ", _P),
         ("round_wnbytes", _P), ("round_nproc", _P), ("round_idle", _P), ("round_sat", _P), ("round_itc", _P),
         ("round_nqueued", _P), ("final_state", _P), ("seconds", C.c_double), ("error", C.c_char * 256),
     ]
@@ -62,12 +63,16 @@ def _ptr(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def replay(g: dict, config: dict, *, snapshots: bool = True, max_rounds: int | None = None) -> dict:
+def replay(g: dict, config: dict, *, snapshots: bool = True, max_rounds: int | None = None,
+           joins: tuple | None = None) -> dict:
     """Replay graph ``g`` (graph dict, ``distributed_amd/graphs.py``) under ``config``
     ({bandwidth, default_data_size, unknown_duration, saturation}) and return the
-    placement records + per-round snapshots as numpy arrays."""
+    placement records + per-round snapshots as numpy arrays. ``joins``: (before, nthreads)
+    arrays of workers joining before the given completion (0-based, replay order); the
+    snapshots are then as wide as the final worker count."""
     n = int(g["n_tasks"])
-    w = len(g["nthreads"])
+    w0 = len(g["nthreads"])
+    w = w0 + (len(joins[0]) if joins is not None else 0)
     sat = config["saturation"]
     sat = math.inf if sat == "inf" else float(sat)
     keep = []
@@ -78,7 +83,7 @@ def replay(g: dict, config: dict, *, snapshots: bool = True, max_rounds: int | N
         return a
 
     gs = OrcGraph(
-        n_tasks=n, n_workers=w, n_prefixes=len(g["prefix_default_dur"]), n_groups=len(g["group_prefix"]),
+        n_tasks=n, n_workers=w0, n_prefixes=len(g["prefix_default_dur"]), n_groups=len(g["group_prefix"]),
         dep_ptr=_ptr(arr(g["dep_ptr"], np.int64)), dep_idx=_ptr(arr(g["dep_idx"], np.int32)),
         prio=_ptr(arr(g["prio"], np.int64)), prefix_id=_ptr(arr(g["prefix_id"], np.int32)),
         group_id=_ptr(arr(g["group_id"], np.int32)), wanted=_ptr(arr(g["wanted"], np.uint8)),
@@ -89,6 +94,10 @@ def replay(g: dict, config: dict, *, snapshots: bool = True, max_rounds: int | N
         bandwidth=int(config["bandwidth"]), default_data_size=int(config["default_data_size"]),
         unknown_duration=float(config["unknown_duration"]), saturation=sat,
     )
+    if joins is not None:
+        gs.n_joins = len(joins[0])
+        gs.join_before = _ptr(arr(joins[0], np.int64))
+        gs.join_nthreads = _ptr(arr(joins[1], np.int32))
     if g.get("restr_flags") is not None:  # worker restrictions, resolved to indices (graphs.restrict)
         gs.restr_ptr = _ptr(arr(g["restr_ptr"], np.int64))
         gs.restr_idx = _ptr(arr(g["restr_idx"], np.int32))
@@ -101,7 +110,7 @@ def replay(g: dict, config: dict, *, snapshots: bool = True, max_rounds: int | N
     )
     res = OrcResult(pl_task=_ptr(out["pl_task"]), pl_worker=_ptr(out["pl_worker"]), pl_comm=_ptr(out["pl_comm"]),
                     pl_start=_ptr(out["pl_start"]), pl_wsnbytes=_ptr(out["pl_wsnbytes"]),
-                    pl_route=_ptr(out["pl_route"]), max_rounds=R, round_nplaced=_ptr(out["round_nplaced"]),
+                    pl_route=_ptr(out["pl_route"]), max_rounds=R, snap_stride=w, round_nplaced=_ptr(out["round_nplaced"]),
                     final_state=_ptr(out["final_state"]))
     if snapshots:
         snap = dict(round_occ=np.zeros((R, w)), round_wnbytes=np.zeros((R, w), np.int64),

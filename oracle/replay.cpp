@@ -59,6 +59,12 @@ struct orc_graph {
   const int64_t* restr_ptr;
   const int32_t* restr_idx;
   const uint8_t* restr_flags;
+  // workers joining mid-replay (optional, n_joins = 0: none): join k happens before the
+  // join_before[k]-th completion (0-based, completions counted in replay order), with
+  // join_nthreads[k] threads and the next worker index (Scheduler.add_worker :4308-4441)
+  int64_t n_joins;
+  const int64_t* join_before;
+  const int32_t* join_nthreads;
 };
 
 struct orc_result {
@@ -72,6 +78,7 @@ struct orc_result {
   int64_t n_placements;
   // per round, capacity max_rounds (snapshot arrays [max_rounds][W]; may be NULL)
   int64_t max_rounds;
+  int64_t snap_stride;  // workers per snapshot row (>= n_workers + n_joins; 0: n_workers)
   int64_t n_rounds;
   int32_t* round_nplaced;
   double* round_occ;
@@ -235,19 +242,41 @@ struct Replay {
     }
     // TaskGroup.dependencies (:1474) -> is_rootish inputs (:2929-2947); total_nthreads is
     // constant during a replay, so the heuristic is static per group.
-    std::vector<std::vector<int32_t>> gdeps(g.n_groups);
+    gdeps.assign(g.n_groups, {});
     for (int64_t t = 0; t < N; t++)
       for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++) gdeps[g.group_id[t]].push_back(g.group_id[g.dep_idx[k]]);
     for (int64_t gi = 0; gi < g.n_groups; gi++) {
       auto& v = gdeps[gi];
       std::sort(v.begin(), v.end());
       v.erase(std::unique(v.begin(), v.end()), v.end());
-      int64_t sum_len = 0;
-      for (int32_t d : v) sum_len += groups[d].size;
-      groups[gi].rootish_static =
-          (groups[gi].size > total_nthreads * 2 && (int64_t)v.size() < 5 && sum_len < 5) ? 1 : 0;
     }
-    idle.init((int)W);
+    rootish_groups();
+    idle.init((int)(W + g.n_joins));  // room for the workers that join (index order = address order)
+  }
+  std::vector<std::vector<int32_t>> gdeps;  // TaskGroup.dependencies
+  void rootish_groups() {  // is_rootish's group part (:2941-2947) for the current total_nthreads
+    for (int64_t gi = 0; gi < g.n_groups; gi++) {
+      int64_t sum_len = 0;
+      for (int32_t d : gdeps[gi]) sum_len += groups[d].size;
+      groups[gi].rootish_static =
+          (groups[gi].size > total_nthreads * 2 && (int64_t)gdeps[gi].size() < 5 && sum_len < 5) ? 1 : 0;
+    }
+  }
+  // Scheduler.add_worker (:4308-4441), the placement part: the WorkerState joins workers /
+  // running with the next index, total_nthreads grows (:4383), check_idle_saturated(ws)
+  // (:4398), bulk_schedule_unrunnable_after_adding_worker (:3173-3186, nothing when no task
+  // is no-worker) and stimulus_queue_slots_maybe_opened (:4416-4420)
+  void add_worker(int32_t nthreads) {
+    ORC_CHECK(n_unrunnable == 0, "worker join with no-worker tasks: not in the replay subset");
+    Worker x;
+    x.nthreads = nthreads;
+    if (!sat_inf) x.slot_cap = std::max((int32_t)std::ceil(g.saturation * nthreads), (int32_t)1);
+    ws.push_back(x);
+    W++;
+    total_nthreads += nthreads;
+    rootish_groups();
+    check_idle_saturated((int32_t)(W - 1));
+    queue_slots_maybe_opened();
   }
 
   // ---------------------------------------------------------------- helpers
@@ -713,8 +742,10 @@ struct Replay {
   void snapshot(int64_t round, int64_t nplaced) {
     r.round_nplaced[round] = (int32_t)nplaced;
     if (r.round_occ) {
+      const int64_t stride = r.snap_stride > 0 ? r.snap_stride : W;
+      ORC_CHECK(stride >= W, "snapshot rows narrower than the worker count");
       for (int32_t w = 0; w < W; w++) {
-        int64_t o = round * W + w;
+        int64_t o = round * stride + w;
         r.round_occ[o] = occupancy(w);
         r.round_wnbytes[o] = ws[w].nbytes;
         r.round_nproc[o] = (int32_t)ws[w].nproc;
@@ -737,7 +768,7 @@ struct Replay {
     rc.items.reserve(N);
     for (int32_t t : order) rc.items.emplace_back(t, WAITING);
     transitions(std::move(rc));
-    int64_t done = 0, round = 0;
+    int64_t done = 0, round = 0, n_done = 0, k_join = 0;
     while (true) {
       int64_t cur = r.n_placements;
       ORC_CHECK(round < r.max_rounds, "too many rounds for the result buffers");
@@ -745,6 +776,8 @@ struct Replay {
       round++;
       if (cur == done) break;
       for (int64_t i = done; i < cur; i++) {  // completions in run_id order
+        while (k_join < g.n_joins && g.join_before[k_join] <= n_done) add_worker(g.join_nthreads[k_join++]);
+        n_done++;
         int32_t t = r.pl_task[i];
         ORC_CHECK(state[t] == PROCESSING, "completion of a task that is not processing");
         Recs c = t_processing_memory(t, g.nbytes[t], g.start[t], g.stop[t]);

@@ -11,7 +11,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden_files
+from conftest import GOLDEN, golden_files, svc_add_worker_files
 from oracle import oracle
 
 PL_KEYS = ("pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")
@@ -52,3 +52,18 @@ def test_scenario_occupancy_includes_communication():
     out = oracle.replay(g, cfg)
     assert out["round_occ"][1][1] == 2.5
     assert out["pl_worker"][2] == 1 and out["pl_comm"][2] == 200_000_000
+
+
+@pytest.mark.parametrize("name", svc_add_worker_files())
+def test_oracle_matches_reference_with_workers_joining(name):
+    """Workers joining mid-replay (Scheduler.add_worker, distributed/scheduler.py:4308-4441;
+    tests/golden/gen_service.py add-workers): the oracle's restatement against the
+    reference's placements, snapshots (as wide as the final worker count) and task states."""
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    z = {"add_msg": z["add_msg"], "add_nthreads": z["add_nthreads"], "msg_task": z["msg_task"],
+         "msg_nbytes": z["msg_nbytes"]}
+    assert np.array_equal(z["msg_task"], exp["pl_task"])  # messages = completions in replay order
+    out = oracle.replay(g, cfg, joins=(z["add_msg"], z["add_nthreads"]))
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
