@@ -28,6 +28,7 @@ class OrcGraph(C.Structure):
         ("bandwidth", C.c_int64), ("default_data_size", C.c_int64), ("unknown_duration", C.c_double),
         ("saturation", C.c_double), ("restr_ptr", _P), ("restr_idx", _P), ("restr_flags", _P),
         ("n_joins", C.c_int64), ("join_before", _P), ("join_nthreads", _P),
+        ("next", _P), ("next_before", C.c_int64),
     ]
 
 
@@ -64,12 +65,14 @@ def _ptr(a):
 
 
 def replay(g: dict, config: dict, *, snapshots: bool = True, max_rounds: int | None = None,
-           joins: tuple | None = None) -> dict:
+           joins: tuple | None = None, second: tuple | None = None) -> dict:
     """Replay graph ``g`` (graph dict, ``distributed_amd/graphs.py``) under ``config``
     ({bandwidth, default_data_size, unknown_duration, saturation}) and return the
     placement records + per-round snapshots as numpy arrays. ``joins``: (before, nthreads)
     arrays of workers joining before the given completion (0-based, replay order); the
-    snapshots are then as wide as the final worker count."""
+    snapshots are then as wide as the final worker count. ``second``: (graph dict, before)
+    — a later, independent graph (engine-wide prefix / group ids, priorities after ``g``'s)
+    submitted before the given completion; its tasks follow ``g``'s in the outputs."""
     n = int(g["n_tasks"])
     w0 = len(g["nthreads"])
     w = w0 + (len(joins[0]) if joins is not None else 0)
@@ -94,6 +97,21 @@ def replay(g: dict, config: dict, *, snapshots: bool = True, max_rounds: int | N
         bandwidth=int(config["bandwidth"]), default_data_size=int(config["default_data_size"]),
         unknown_duration=float(config["unknown_duration"]), saturation=sat,
     )
+    gs2 = None
+    if second is not None:
+        h, before = second
+        gs2 = OrcGraph(
+            n_tasks=len(h["prio"]), n_workers=w0, n_prefixes=len(h["prefix_default_dur"]),
+            n_groups=len(h["group_prefix"]), dep_ptr=_ptr(arr(h["dep_ptr"], np.int64)),
+            dep_idx=_ptr(arr(h["dep_idx"], np.int32)), prio=_ptr(arr(h["prio"], np.int64)),
+            prefix_id=_ptr(arr(h["prefix_id"], np.int32)), group_id=_ptr(arr(h["group_id"], np.int32)),
+            wanted=_ptr(arr(h["wanted"], np.uint8)), rootish_override=_ptr(arr(h["rootish_override"], np.int8)),
+            nbytes=_ptr(arr(h["nbytes"], np.int64)), start=_ptr(arr(h["start"], np.float64)),
+            stop=_ptr(arr(h["stop"], np.float64)), prefix_default_dur=_ptr(arr(h["prefix_default_dur"], np.float64)),
+        )
+        gs.next = C.cast(C.pointer(gs2), C.c_void_p)
+        gs.next_before = int(before)
+        n += len(h["prio"])
     if joins is not None:
         gs.n_joins = len(joins[0])
         gs.join_before = _ptr(arr(joins[0], np.int64))

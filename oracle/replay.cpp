@@ -65,6 +65,13 @@ struct orc_graph {
   int64_t n_joins;
   const int64_t* join_before;
   const int32_t* join_nthreads;
+  // a later graph submitted mid-replay (optional): its tasks get indices n_tasks.., its
+  // dependencies are relative to it (independent of this graph), priorities follow this
+  // graph's, prefix / group ids over the grown tables (n_prefixes / n_groups = the totals;
+  // prefix_default_dur read for the new prefixes). Submitted before the next_before-th
+  // completion (Scheduler.update_graph :4662-4751 -> _create_taskstate_from_graph :4512-4653)
+  const struct orc_graph* next;
+  int64_t next_before;
 };
 
 struct orc_result {
@@ -172,9 +179,40 @@ struct Recs {  // ordered dict {task: finish} with popitem() LIFO and update() k
   std::vector<std::pair<int32_t, uint8_t>> items;
 };
 
+// the graph as the replay holds it: owned copies, so that a later graph can be appended
+struct GraphArrays {
+  std::vector<int64_t> dep_ptr, prio, nbytes;
+  std::vector<int32_t> dep_idx, prefix_id, group_id;
+  std::vector<uint8_t> wanted;
+  std::vector<int8_t> rootish_override;
+  std::vector<double> start, stop, prefix_default_dur;
+  int64_t n_prefixes = 0, n_groups = 0;
+  // append graph h (dependencies relative to it) after n0 tasks
+  void append(const orc_graph& h, int64_t n0) {
+    const int64_t n = h.n_tasks, e0 = dep_ptr.empty() ? 0 : dep_ptr.back();
+    if (dep_ptr.empty()) dep_ptr.push_back(0);
+    for (int64_t t = 0; t < n; t++) {
+      dep_ptr.push_back(e0 + h.dep_ptr[t + 1]);
+      prio.push_back(h.prio[t]);
+      nbytes.push_back(h.nbytes[t]);
+      prefix_id.push_back(h.prefix_id[t]);
+      group_id.push_back(h.group_id[t]);
+      wanted.push_back(h.wanted[t]);
+      rootish_override.push_back(h.rootish_override[t]);
+      start.push_back(h.start[t]);
+      stop.push_back(h.stop[t]);
+    }
+    for (int64_t k = 0; k < h.dep_ptr[n]; k++) dep_idx.push_back((int32_t)(h.dep_idx[k] + n0));
+    for (int64_t q = n_prefixes; q < h.n_prefixes; q++) prefix_default_dur.push_back(h.prefix_default_dur[q]);
+    n_prefixes = std::max(n_prefixes, h.n_prefixes);
+    n_groups = std::max(n_groups, h.n_groups);
+  }
+};
+
 struct Replay {
   const orc_graph& g;
   orc_result& r;
+  GraphArrays G;
   int64_t N, W;
   std::vector<int64_t> dpt_ptr;
   std::vector<int32_t> dpt_idx;
@@ -207,17 +245,9 @@ struct Replay {
   std::vector<int32_t> rec_pos;
 
   Replay(const orc_graph& g_, orc_result& r_) : g(g_), r(r_), N(g_.n_tasks), W(g_.n_workers) {
+    G.append(g, 0);
     sat_inf = std::isinf(g.saturation);
-    // dependents CSR (TaskState.dependents, :1220)
-    std::vector<int64_t> deg(N + 1, 0);
-    for (int64_t t = 0; t < N; t++)
-      for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++) deg[g.dep_idx[k] + 1]++;
-    dpt_ptr.assign(N + 1, 0);
-    for (int64_t t = 0; t < N; t++) dpt_ptr[t + 1] = dpt_ptr[t] + deg[t + 1];
-    dpt_idx.resize(dpt_ptr[N]);
-    std::vector<int64_t> fill(dpt_ptr.begin(), dpt_ptr.end() - 1);
-    for (int64_t t = 0; t < N; t++)
-      for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++) dpt_idx[fill[g.dep_idx[k]]++] = (int32_t)t;
+    build_dependents();
     state.assign(N, RELEASED);
     waiting_on.assign(N, 0);
     waiters.assign(N, 0);
@@ -233,29 +263,43 @@ struct Replay {
       total_nthreads += g.nthreads[w];
       if (!sat_inf) ws[w].slot_cap = std::max((int32_t)std::ceil(g.saturation * ws[w].nthreads), (int32_t)1);
     }
-    prefixes.resize(g.n_prefixes);
-    for (int64_t p = 0; p < g.n_prefixes; p++) prefixes[p].duration_average = g.prefix_default_dur[p];
-    groups.resize(g.n_groups);
+    prefixes.resize(G.n_prefixes);
+    for (int64_t p = 0; p < G.n_prefixes; p++) prefixes[p].duration_average = G.prefix_default_dur[p];
+    groups.resize(G.n_groups);
     for (int64_t t = 0; t < N; t++) {
-      groups[g.group_id[t]].size++;
-      groups[g.group_id[t]].n_released++;
+      groups[G.group_id[t]].size++;
+      groups[G.group_id[t]].n_released++;
     }
     // TaskGroup.dependencies (:1474) -> is_rootish inputs (:2929-2947); total_nthreads is
     // constant during a replay, so the heuristic is static per group.
-    gdeps.assign(g.n_groups, {});
+    build_group_deps();
+    rootish_groups();
+    idle.init((int)(W + g.n_joins));  // room for the workers that join (index order = address order)
+  }
+  void build_dependents() {  // TaskState.dependents (:1220), over the whole graph
+    std::vector<int64_t> deg(N + 1, 0);
     for (int64_t t = 0; t < N; t++)
-      for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++) gdeps[g.group_id[t]].push_back(g.group_id[g.dep_idx[k]]);
-    for (int64_t gi = 0; gi < g.n_groups; gi++) {
+      for (int64_t k = G.dep_ptr[t]; k < G.dep_ptr[t + 1]; k++) deg[G.dep_idx[k] + 1]++;
+    dpt_ptr.assign(N + 1, 0);
+    for (int64_t t = 0; t < N; t++) dpt_ptr[t + 1] = dpt_ptr[t] + deg[t + 1];
+    dpt_idx.resize(dpt_ptr[N]);
+    std::vector<int64_t> fill(dpt_ptr.begin(), dpt_ptr.end() - 1);
+    for (int64_t t = 0; t < N; t++)
+      for (int64_t k = G.dep_ptr[t]; k < G.dep_ptr[t + 1]; k++) dpt_idx[fill[G.dep_idx[k]]++] = (int32_t)t;
+  }
+  void build_group_deps() {  // TaskGroup.dependencies (:1474)
+    gdeps.assign(G.n_groups, {});
+    for (int64_t t = 0; t < N; t++)
+      for (int64_t k = G.dep_ptr[t]; k < G.dep_ptr[t + 1]; k++) gdeps[G.group_id[t]].push_back(G.group_id[G.dep_idx[k]]);
+    for (int64_t gi = 0; gi < G.n_groups; gi++) {
       auto& v = gdeps[gi];
       std::sort(v.begin(), v.end());
       v.erase(std::unique(v.begin(), v.end()), v.end());
     }
-    rootish_groups();
-    idle.init((int)(W + g.n_joins));  // room for the workers that join (index order = address order)
   }
   std::vector<std::vector<int32_t>> gdeps;  // TaskGroup.dependencies
   void rootish_groups() {  // is_rootish's group part (:2941-2947) for the current total_nthreads
-    for (int64_t gi = 0; gi < g.n_groups; gi++) {
+    for (int64_t gi = 0; gi < G.n_groups; gi++) {
       int64_t sum_len = 0;
       for (int32_t d : gdeps[gi]) sum_len += groups[d].size;
       groups[gi].rootish_static =
@@ -266,6 +310,43 @@ struct Replay {
   // running with the next index, total_nthreads grows (:4383), check_idle_saturated(ws)
   // (:4398), bulk_schedule_unrunnable_after_adding_worker (:3173-3186, nothing when no task
   // is no-worker) and stimulus_queue_slots_maybe_opened (:4416-4420)
+  // a later, independent graph: TaskStates appended (TaskPrefix / TaskGroup shared by name
+  // through the ids), group sizes and is_rootish's group part over the grown graph, then
+  // every new task recommended "waiting" in descending priority (:4600-4651)
+  void add_graph(const orc_graph& h) {
+    ORC_CHECK(!g.restr_flags && !h.restr_flags, "a later graph with restrictions: not in the replay subset");
+    const int64_t n0 = N, n1 = N + h.n_tasks;
+    G.append(h, n0);
+    N = n1;
+    state.resize(n1, RELEASED);
+    waiting_on.resize(n1, 0);
+    waiters.resize(n1, 0);
+    processing_on.resize(n1, -1);
+    cur_nbytes.resize(n1, -1);
+    who_has.resize(n1);
+    run_id.resize(n1, -1);
+    in_queue.resize(n1, 0);
+    rec_pos.resize(n1, -1);
+    build_dependents();
+    for (int64_t p = (int64_t)prefixes.size(); p < G.n_prefixes; p++) {
+      prefixes.emplace_back();
+      prefixes.back().duration_average = G.prefix_default_dur[p];
+    }
+    groups.resize(G.n_groups);
+    for (int64_t t = n0; t < n1; t++) {
+      groups[G.group_id[t]].size++;
+      groups[G.group_id[t]].n_released++;
+    }
+    build_group_deps();
+    rootish_groups();
+    std::vector<int32_t> order;
+    for (int64_t t = n0; t < n1; t++) order.push_back((int32_t)t);
+    std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return G.prio[a] > G.prio[b]; });
+    Recs rc;
+    for (int32_t t : order) rc.items.emplace_back(t, WAITING);
+    transitions(std::move(rc));
+  }
+
   void add_worker(int32_t nthreads) {
     ORC_CHECK(n_unrunnable == 0, "worker join with no-worker tasks: not in the replay subset");
     Worker x;
@@ -289,7 +370,7 @@ struct Replay {
     return false;
   }
   void set_state(int32_t t, uint8_t s) {  // TaskState.state setter :1464-1469 (group counts)
-    Group& gr = groups[g.group_id[t]];
+    Group& gr = groups[G.group_id[t]];
     if (state[t] == RELEASED) gr.n_released--;
     if (state[t] == WAITING) gr.n_waiting--;
     if (s == RELEASED) gr.n_released++;
@@ -320,10 +401,10 @@ struct Replay {
   bool loose(int32_t t) const { return g.restr_flags && (g.restr_flags[t] & 2); }
 
   bool is_rootish(int32_t t) const {  // :2929-2947
-    int8_t ov = g.rootish_override[t];
+    int8_t ov = G.rootish_override[t];
     if (ov >= 0) return ov != 0;
     if (restricted(t)) return false;  // :2939-2940
-    return groups[g.group_id[t]].rootish_static != 0;
+    return groups[G.group_id[t]].rootish_static != 0;
   }
 
   int64_t task_slots_available(int32_t w) const {  // _task_slots_available :8762-8767
@@ -377,8 +458,8 @@ struct Replay {
   };
   Obj worker_objective(int32_t t, int32_t w) const {
     int64_t comm = 0;
-    for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++) {
-      int32_t d = g.dep_idx[k];
+    for (int64_t k = G.dep_ptr[t]; k < G.dep_ptr[t + 1]; k++) {
+      int32_t d = G.dep_idx[k];
       if (!holds(d, w)) comm += get_nbytes(d);
     }
     double stack_time = occupancy(w) / (double)ws[w].nthreads;
@@ -402,7 +483,7 @@ struct Replay {
   int32_t decide_worker_rootish_queuing_disabled(int32_t t) {  // :2135-2193
     // pool = self.idle.values() if self.idle else self.running  (all workers run here)
     bool use_idle = idle.cnt > 0;
-    Group& tg = groups[g.group_id[t]];
+    Group& tg = groups[G.group_id[t]];
     int32_t w;
     if (tg.last_worker >= 0 && tg.last_worker_tasks_left) {
       w = tg.last_worker;
@@ -427,8 +508,8 @@ struct Replay {
   // module-level decide_worker :8550-8593; valid = valid_workers(ts) or null (None)
   int32_t decide_worker(int32_t t, const std::vector<int32_t>* valid = nullptr) {
     std::vector<int32_t> cand;
-    for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++)
-      for (int32_t w : who_has[g.dep_idx[k]]) cand.push_back(w);
+    for (int64_t k = G.dep_ptr[t]; k < G.dep_ptr[t + 1]; k++)
+      for (int32_t w : who_has[G.dep_idx[k]]) cand.push_back(w);
     std::sort(cand.begin(), cand.end());
     cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
     if (!valid) {
@@ -462,7 +543,7 @@ struct Replay {
       std::vector<int32_t> valid(g.restr_idx + g.restr_ptr[t], g.restr_idx + g.restr_ptr[t + 1]);
       return decide_worker(t, &valid);
     }
-    if (g.dep_ptr[t + 1] > g.dep_ptr[t]) {
+    if (G.dep_ptr[t + 1] > G.dep_ptr[t]) {
       route = R_NONROOTISH;
       return decide_worker(t);
     }
@@ -524,11 +605,11 @@ struct Replay {
     r.pl_wsnbytes[i] = ws[w].nbytes;
     r.pl_route[i] = route;
     // WorkerState.add_to_processing :733-745
-    ws[w].prefix.inc(g.prefix_id[t]);
-    prefix_global.inc(g.prefix_id[t]);
+    ws[w].prefix.inc(G.prefix_id[t]);
+    prefix_global.inc(G.prefix_id[t]);
     ws[w].nproc++;
-    for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++) {
-      int32_t d = g.dep_idx[k];
+    for (int64_t k = G.dep_ptr[t]; k < G.dep_ptr[t + 1]; k++) {
+      int32_t d = G.dep_idx[k];
       ORC_CHECK(!who_has[d].empty(), "dependency without replica at placement");
       if (!holds(d, w)) inc_needs_replica(w, d);
     }
@@ -549,8 +630,8 @@ struct Replay {
     Recs rc;
     set_state(t, WAITING);
     int32_t wo = 0;
-    for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++) {
-      int32_t d = g.dep_idx[k];
+    for (int64_t k = G.dep_ptr[t]; k < G.dep_ptr[t + 1]; k++) {
+      int32_t d = G.dep_idx[k];
       if (who_has[d].empty()) wo++;
       if (state[d] == RELEASED)
         rec_set(rc, d, WAITING);
@@ -608,7 +689,7 @@ struct Replay {
     set_state(t, QUEUED);
     in_queue[t] = 1;
     queue_len++;
-    queue.emplace(g.prio[t], queue_inc++, t);
+    queue.emplace(G.prio[t], queue_inc++, t);
     return {};
   }
 
@@ -623,7 +704,7 @@ struct Replay {
     ORC_CHECK(w >= 0, "processing->memory without worker");
     // TaskGroup.add_duration -> TaskPrefix.add_duration :977-985 ("compute" action)
     double duration = stop - start;
-    Prefix& pf = prefixes[g.prefix_id[t]];
+    Prefix& pf = prefixes[G.prefix_id[t]];
     double old = pf.duration_average;
     if (old < 0)
       pf.duration_average = duration;
@@ -633,11 +714,11 @@ struct Replay {
     cur_nbytes[t] = nbytes;
     // _exit_processing_common :3258-3281 -> WorkerState.remove_from_processing :759-771
     processing_on[t] = -1;
-    ws[w].prefix.dec(g.prefix_id[t]);
-    prefix_global.dec(g.prefix_id[t]);
+    ws[w].prefix.dec(G.prefix_id[t]);
+    prefix_global.dec(G.prefix_id[t]);
     ws[w].nproc--;
-    for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++) {
-      int32_t d = g.dep_idx[k];
+    for (int64_t k = G.dep_ptr[t]; k < G.dep_ptr[t + 1]; k++) {
+      int32_t d = G.dep_idx[k];
       if (ws[w].needs.count(d)) dec_needs_replica(w, d);
     }
     check_idle_saturated(w);
@@ -660,18 +741,18 @@ struct Replay {
     // frontier release: dependents in descending priority
     std::vector<int32_t> deps(dpt_idx.begin() + dpt_ptr[t], dpt_idx.begin() + dpt_ptr[t + 1]);
     if (deps.size() > 1)
-      std::sort(deps.begin(), deps.end(), [&](int32_t a, int32_t b) { return g.prio[a] > g.prio[b]; });
+      std::sort(deps.begin(), deps.end(), [&](int32_t a, int32_t b) { return G.prio[a] > G.prio[b]; });
     for (int32_t x : deps) {
       if (state[x] == WAITING && waiting_on[x] > 0) {
         if (--waiting_on[x] == 0) rec_set(rc, x, PROCESSING);
       }
     }
-    for (int64_t k = g.dep_ptr[t]; k < g.dep_ptr[t + 1]; k++) {
-      int32_t d = g.dep_idx[k];
+    for (int64_t k = G.dep_ptr[t]; k < G.dep_ptr[t + 1]; k++) {
+      int32_t d = G.dep_idx[k];
       if (waiters[d] > 0) waiters[d]--;
-      if (waiters[d] == 0 && !g.wanted[d]) rec_set(rc, d, RELEASED);
+      if (waiters[d] == 0 && !G.wanted[d]) rec_set(rc, d, RELEASED);
     }
-    if (waiters[t] == 0 && !g.wanted[t]) rec_set(rc, t, RELEASED);
+    if (waiters[t] == 0 && !G.wanted[t]) rec_set(rc, t, RELEASED);
     set_state(t, MEMORY);
     return rc;
   }
@@ -682,7 +763,7 @@ struct Replay {
     who_has[t].clear();
     set_state(t, RELEASED);
     Recs rc;
-    if (g.wanted[t] || waiters[t] > 0) rec_set(rc, t, WAITING);
+    if (G.wanted[t] || waiters[t] > 0) rec_set(rc, t, WAITING);
     return rc;
   }
 
@@ -763,12 +844,13 @@ struct Replay {
     // update_graph (:4600-4611): every task recommended "waiting", descending priority
     std::vector<int32_t> order(N);
     for (int64_t t = 0; t < N; t++) order[t] = (int32_t)t;
-    std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return g.prio[a] > g.prio[b]; });
+    std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return G.prio[a] > G.prio[b]; });
     Recs rc;
     rc.items.reserve(N);
     for (int32_t t : order) rc.items.emplace_back(t, WAITING);
     transitions(std::move(rc));
     int64_t done = 0, round = 0, n_done = 0, k_join = 0;
+    bool next_done = false;
     while (true) {
       int64_t cur = r.n_placements;
       ORC_CHECK(round < r.max_rounds, "too many rounds for the result buffers");
@@ -777,10 +859,14 @@ struct Replay {
       if (cur == done) break;
       for (int64_t i = done; i < cur; i++) {  // completions in run_id order
         while (k_join < g.n_joins && g.join_before[k_join] <= n_done) add_worker(g.join_nthreads[k_join++]);
+        if (g.next && !next_done && g.next_before <= n_done) {
+          next_done = true;
+          add_graph(*g.next);
+        }
         n_done++;
         int32_t t = r.pl_task[i];
         ORC_CHECK(state[t] == PROCESSING, "completion of a task that is not processing");
-        Recs c = t_processing_memory(t, g.nbytes[t], g.start[t], g.stop[t]);
+        Recs c = t_processing_memory(t, G.nbytes[t], G.start[t], G.stop[t]);
         transitions(std::move(c));
         queue_slots_maybe_opened();
       }

@@ -25,6 +25,27 @@ def svc_second_graph_files():
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcgraph_") and f.endswith(".npz"))
 
 
+def second_graph(g, z, with_results=False):
+    """A ``svcgraph_*`` fixture's second graph over the engine-wide tables: priorities after
+    the first graph's, its groups after the first graph's groups, the same prefixes; with
+    ``with_results`` also its tasks' completion reports (from the message stream)."""
+    import numpy as np
+
+    G1 = len(g["group_prefix"])
+    h = dict(dep_ptr=z["g2_dep_ptr"], dep_idx=z["g2_dep_idx"], prio=z["g2_prio"] + int(g["prio"].max()) + 1,
+             prefix_id=z["g2_prefix_id"], group_id=z["g2_group_id"] + G1, wanted=z["g2_wanted"],
+             rootish_override=z["g2_rootish_override"], prefix_default_dur=g["prefix_default_dur"],
+             group_prefix=np.concatenate([g["group_prefix"], g["group_prefix"]]))
+    if with_results:
+        n1, n2 = g["n_tasks"], len(h["prio"])
+        nb, a, b = np.zeros(n2, np.int64), np.zeros(n2), np.zeros(n2)
+        for t, x, s0, s1 in zip(z["msg_task"], z["msg_nbytes"], z["msg_start"], z["msg_stop"]):
+            if t >= n1:
+                nb[t - n1], a[t - n1], b[t - n1] = x, s0, s1
+        h.update(nbytes=nb, start=a, stop=b)
+    return h
+
+
 def svc_add_worker_files():
     """Service-mode message streams with workers joining (tests/golden/gen_service.py add-workers)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcaddw_") and f.endswith(".npz"))

@@ -28,7 +28,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden_files, svc_add_worker_files, svc_second_graph_files, svc_steal_files
+from conftest import GOLDEN, golden_files, second_graph, svc_add_worker_files, svc_second_graph_files, svc_steal_files
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -240,16 +240,6 @@ def test_service_with_workers_joining(name, per_message):
         assert refill > 0  # the joins took queued tasks
     assert_same(out, exp, PL_KEYS + ROUND_KEYS)
     assert np.array_equal(out["final_state"], exp["final_state"])
-
-
-def second_graph(g, z):
-    """The fixture's second graph over the engine-wide tables: priorities after the first
-    graph's, its groups after the first graph's groups, the same prefixes."""
-    G1 = len(g["group_prefix"])
-    return dict(dep_ptr=z["g2_dep_ptr"], dep_idx=z["g2_dep_idx"], prio=z["g2_prio"] + int(g["prio"].max()) + 1,
-                prefix_id=z["g2_prefix_id"], group_id=z["g2_group_id"] + G1, wanted=z["g2_wanted"],
-                rootish_override=z["g2_rootish_override"], prefix_default_dur=g["prefix_default_dur"],
-                group_prefix=np.concatenate([g["group_prefix"], g["group_prefix"]]))
 
 
 @pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])

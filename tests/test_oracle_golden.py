@@ -11,7 +11,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden_files, svc_add_worker_files
+from conftest import GOLDEN, golden_files, second_graph, svc_add_worker_files, svc_second_graph_files
 from oracle import oracle
 
 PL_KEYS = ("pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")
@@ -66,4 +66,17 @@ def test_oracle_matches_reference_with_workers_joining(name):
          "msg_nbytes": z["msg_nbytes"]}
     assert np.array_equal(z["msg_task"], exp["pl_task"])  # messages = completions in replay order
     out = oracle.replay(g, cfg, joins=(z["add_msg"], z["add_nthreads"]))
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+
+
+@pytest.mark.parametrize("name", svc_second_graph_files())
+def test_oracle_matches_reference_with_a_second_graph(name):
+    """A later, independent graph submitted mid-replay (Scheduler.update_graph,
+    distributed/scheduler.py:4662-4751; tests/golden/gen_service.py second-graph), with
+    workers joining in the svcgraph_joins_* stream: the oracle against the reference."""
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = dict(np.load(path, allow_pickle=False))
+    joins = (z["add_msg"], z["add_nthreads"]) if "add_msg" in z else None
+    out = oracle.replay(g, cfg, joins=joins, second=(second_graph(g, z, with_results=True), int(z["g2_msg"])))
     assert_same(out, exp, PL_KEYS + ROUND_KEYS)
