@@ -291,3 +291,35 @@ def test_service_with_a_second_graph(name, per_message):
     assert (np.array(status) == 0).all()
     assert_same(out, exp, PL_KEYS + ROUND_KEYS)
     assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+def test_joins_and_later_graphs_reject_what_they_do_not_model():
+    """dgp_add_worker / dgp_add_graph answer with an error (the extension then hands
+    placement back to the scheduler) instead of placing wrongly."""
+    from distributed_amd import _lib, graphs
+    from distributed_amd.engine import PlacementEngine
+
+    g = graphs.random_dag(2000, 32, seed=3)
+    cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": 1.1}
+    h = graphs.random_dag(500, 32, seed=4)
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, results=False)
+        with pytest.raises(_lib.DgpError):  # before update_graph
+            eng.add_worker(2)
+        with pytest.raises(_lib.DgpError):
+            eng.add_graph(dict(h, prio=h["prio"] + g["n_tasks"]))
+        eng.update_graph()
+        with pytest.raises(_lib.DgpError):  # nthreads out of range
+            eng.add_worker(0)
+        with pytest.raises(_lib.DgpError):  # priorities not after the first graph's
+            eng.add_graph(h)
+        dep_old = dict(h, prio=h["prio"] + g["n_tasks"], dep_idx=np.asarray(h["dep_idx"]) + 10_000)
+        with pytest.raises(_lib.DgpError):  # a dependency outside the new graph
+            eng.add_graph(dep_old)
+        assert eng.add_worker(3) >= 0 and eng.n_workers == 33
+        n1 = eng.num_placements()
+        newp = eng.add_graph(dict(h, prio=h["prio"] + g["n_tasks"]))
+        assert eng.num_placements() == n1 + newp
+        assert eng.n_tasks == 2500
+        st = eng.task_states()[2000:]  # every new task went waiting, queued or processing
+        assert set(np.unique(st).tolist()) <= {1, 2, 3} and (st == 3).sum() + newp >= 50  # 50 roots
