@@ -54,9 +54,17 @@ SIGNATURES = {
     "dgp_steal_pack_rows": (C.c_int, [_P, C.c_int64, C.c_int64, _P]),
     "dgp_steal_unpack_rows": (C.c_int, [_P, C.c_int64, C.c_int64, _P]),
     "dgp_steal_run": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dgp_add_replicas": (C.c_int, [_P, C.c_int64, _P, _P]),
+    "dgp_remove_replicas": (C.c_int, [_P, C.c_int64, _P, _P]),
+    "dgp_set_worker_status": (C.c_int, [_P, C.c_int32, C.c_int32, _P]),
+    "dgp_long_running": (C.c_int, [_P, C.c_int32, C.c_double, _P]),
+    "dgp_heartbeat": (C.c_int, [_P, C.c_double, C.c_int64, _P, _P]),
+    "dgp_set_worker_flags": (C.c_int, [_P, C.c_int64, _P, _P, _P]),
+    "dgp_set_wanted": (C.c_int, [_P, C.c_int64, _P, _P]),
+    "dgp_task_erred": (C.c_int, [_P, C.c_int32, _P]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 _lib = None
 
 

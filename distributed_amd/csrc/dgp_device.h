@@ -41,14 +41,25 @@ constexpr int TOUCH_MAX = 24;  // workers one stimulus may reserve (more -> runs
 constexpr int CTA = 1024;      // threads of the commit / dispatch workgroup
 constexpr int FL_MAX = 256;    // frontier tasks one global stimulus stages in LDS per chunk
 
-enum : uint8_t { S_RELEASED = 0, S_WAITING, S_PROCESSING, S_QUEUED, S_NO_WORKER, S_MEMORY };
+enum : uint8_t { S_RELEASED = 0, S_WAITING, S_PROCESSING, S_QUEUED, S_NO_WORKER, S_MEMORY, S_ERRED };
 enum : uint8_t { RF_RESTRICTED = 1, RF_LOOSE = 2 };
 enum : uint8_t { TF_WANTED = 1, TF_ROOTISH = 2 };
-enum : uint8_t { WF_IDLE = 1, WF_SAT = 2, WF_ITC = 4 };
+// WF_PAUSED: the worker is not in SchedulerState.running (Status.paused, :5850-5883): never
+// idle / saturated / in idle_task_count, never a decide_worker candidate
+enum : uint8_t { WF_IDLE = 1, WF_SAT = 2, WF_ITC = 4, WF_PAUSED = 8 };
+// per-task dynamic flags (Dev::tdyn): TD_LR the task is in its worker's long_running
+// (add_to_long_running :747-757); TD_MULTI who_has is the task's holders bitset row (replicas
+// beyond the one completion made, add_replica / remove_replica :3148-3159), not holder_of
+enum : uint8_t { TD_LR = 1, TD_MULTI = 2 };
+// Dev::evf: which kinds of service events the engine has seen (each adds checks to the paths
+// that must honour it; the replay workloads never set any)
+enum : int32_t { EVF_MULTI = 1, EVF_LR = 2, EVF_PAUSED = 4 };
 enum : uint8_t { EV_GLOBAL = 1 };
 enum : int32_t { REC_NONE = 0, REC_COMPLETE = 1, REC_PLACE = 2 };
 enum : int { ERR_NONE = 0, ERR_PREFIX_CAP, ERR_NO_CANDIDATES, ERR_BAD_STATE, ERR_QUEUE, ERR_POOL, ERR_GPREFIX_CAP,
-             ERR_REC_CAP, ERR_STAGE_CAP, ERR_NO_WORKER, ERR_NEEDS_CAP };
+             ERR_REC_CAP, ERR_STAGE_CAP, ERR_NO_WORKER, ERR_NEEDS_CAP,
+             ERR_UNSUPPORTED = 20 };  // a service event the engine does not model (dgp_events.h);
+                                      // 11..19 are the stream engine's SERR_* codes
 enum : int { ROUTE_NONROOTISH = 0, ROUTE_ROOTISH_Q = 1, ROUTE_ROOTISH_NOQ = 2, ROUTE_FASTPATH = 3 };
 
 // device-resident control block
@@ -104,7 +115,8 @@ struct Pos;
 
 struct Dev {
   int32_t N, W, WB, P, G, Wp;
-  int64_t bandwidth, default_data_size;
+  double bandwidth;  // SchedulerState.bandwidth: the config int, then the heartbeat EWMA (:4223-4226)
+  int64_t default_data_size;
   double unknown_duration, saturation;
   int32_t sat_inf;
   int64_t total_nthreads;
@@ -227,7 +239,9 @@ struct Dev {
   unsigned long long* gw_held;  // [2][W] scratch of a global stimulus: held bytes, held deps per worker
   uint32_t* gw_needs_saved;  // needs_what lines between launches [W][NLW]
   int32_t* run_id;           // placement-log position of each placed task
-  int32_t* holder_of;        // the worker a task runs / ran on (its single replica)
+  int32_t* holder_of;        // the worker a task runs / ran on (its single replica; one of them under TD_MULTI)
+  uint8_t* tdyn;             // TD_LR / TD_MULTI per task
+  int32_t evf;               // EVF_* seen so far
   int32_t* fr_mark;          // stimulus whose completion empties the task's waiting_on
   int32_t* rel_mark;         // stimulus whose completion empties the task's waiters
   uint4* desc;               // descriptor ring [DR][NE]
@@ -302,6 +316,11 @@ __device__ __forceinline__ int64_t get_nbytes(const Dev& D, int t) {  // TaskSta
 }
 __device__ __forceinline__ bool holds(const Dev& D, int d, int w) {
   return (D.holders[(size_t)d * D.WB + (w >> 6)] >> (w & 63)) & 1ull;
+}
+// w in d.who_has on the stream engine: holder_of, or the bitset row under TD_MULTI
+__device__ __forceinline__ bool holds_any(const Dev& D, int d, int w) {
+  if ((D.evf & EVF_MULTI) && (D.tdyn[d] & TD_MULTI)) return holds(D, d, w);
+  return D.holder_of[d] == w;
 }
 // restricted and placed by decide_worker_non_rootish (a `_rootish` override wins, :2937)
 __device__ __forceinline__ bool restricted_nonrootish(const Dev& D, int x) {
@@ -401,7 +420,8 @@ __device__ void gdict_dec(const Dev& D, int p) {
 }
 
 __device__ __forceinline__ int64_t task_slots_available(const Dev& D, int w) {  // :8762-8767
-  return (int64_t)WK_cap(D)[w] - (int64_t)WK_nproc(D)[w];  // len(long_running) == 0 in the replay
+  // cap[w] counts the worker's long-running tasks on top of max(ceil(sat * nthreads), 1)
+  return (int64_t)WK_cap(D)[w] - (int64_t)WK_nproc(D)[w];
 }
 __device__ __forceinline__ bool worker_full(const Dev& D, int w) {  // :8770-8773
   if (D.sat_inf) return false;
@@ -457,8 +477,8 @@ __device__ __attribute__((noinline)) void tree_rebuild_coop(const Dev& D) {  // 
 
 // the idle_task_count part of check_idle_saturated (:2992-2995): depends only on w
 __device__ void itc_check(const Dev& D, int w, bool maintain_tree) {
-  bool on = !worker_full(D, w);
   uint8_t fl = WK_flags(D)[w];
+  bool on = !worker_full(D, w) && !(fl & WF_PAUSED);  // ... and ws.status == running (:2992)
   bool was = (fl & WF_ITC) != 0;
   if (on != was) {
     WK_flags(D)[w] = on ? (fl | WF_ITC) : (fl & ~WF_ITC);
@@ -500,13 +520,15 @@ __device__ void walk_flags(const Dev& D, int w, double occ, int64_t p) {
   uint8_t fl = WK_flags(D)[w];
   bool idle = false, sat = false;
   double avg = -1;
-  if (p < nt) {
+  if (fl & WF_PAUSED) {
+    // not running: idle.pop, saturated.discard (:2975-2977)
+  } else if (p < nt) {
     idle = true;
   } else {
     avg = total_occupancy_walk(D) / (double)D.total_nthreads;
     idle = occ < (double)nt * avg / 2;
   }
-  if (!idle && p > nt) {
+  if (!idle && p > nt && !(fl & WF_PAUSED)) {
     double pending = occ * (double)(p - nt) / (double)(p * nt);
     if (0.4 < pending) {
       if (avg < 0) avg = total_occupancy_walk(D) / (double)D.total_nthreads;

@@ -105,7 +105,9 @@ static_assert((RS & (RS - 1)) == 0 && RS >= WIN && RS <= DR, "DGP_RS must be a p
 // F_RUNM (REG): F_SIMPLE and so is the stimulus just before it, on the same worker: a run
 // continues through it, so only the run-capable executor takes it
 enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16, F_SIMPLE = 32, F_RUNM = 64 };
-enum : int { K_COMPLETE = 1, K_PLACE = 2 };
+// K_COMPLETE_LR: the completion of a long-running task (its prefix count left the worker's and
+// the global dict at add_to_long_running :747-757; remove_from_processing :764-766)
+enum : int { K_COMPLETE = 1, K_PLACE = 2, K_COMPLETE_LR = 3 };
 enum : int { SERR_NONE = 0, SERR_PREFIX = 11, SERR_WATCHDOG = 12, SERR_QUEUE = 13, SERR_NEEDS = 14,
              SERR_REC = 15, SERR_CAND = 16, SERR_STAGE = 17, SERR_RANGE = 18, SERR_INV = 19 };
 
@@ -399,8 +401,13 @@ __device__ __forceinline__ bool dict_add(WDict& d, int p, int delta) {
 // walker's wdur), read by prefix id
 using DTab = const __attribute__((address_space(3))) double*;
 
+__device__ __forceinline__ double resolve_dur(const Dev& D, double d, int p) {  // _calc_occupancy :1892-1899
+  return d < 0 ? (D.pmaxexec[p] > 0 ? 2 * D.pmaxexec[p] : D.unknown_duration) : d;
+}
+
 // _calc_occupancy (:1884-1903): prefix terms in dict order, then network occupancy.
-// Durations resolve as there (EWMA, else unknown-task-duration; idempotent on resolved).
+// Durations resolve as there (EWMA, else 2 max_exec_time, else unknown-task-duration;
+// idempotent on resolved).
 __device__ __forceinline__ double occ_dict(const WDict& d, int64_t netocc, DTab dt, const Dev& D) {
   const uint32_t n = wd_n(d.ord);
   double res = 0.0;
@@ -409,7 +416,7 @@ __device__ __forceinline__ double occ_dict(const WDict& d, int64_t netocc, DTab 
     if (!ballot((uint32_t)i < n)) break;
     const int p = wd_id(d.ord, i);
     const double dv = dt[p];
-    const double term = (dv < 0 ? D.unknown_duration : dv) * (double)wd_cnt(d, p);
+    const double term = resolve_dur(D, dv, p) * (double)wd_cnt(d, p);
     if ((uint32_t)i < n) res += term;
   }
   return res + (double)netocc / (double)D.bandwidth;
@@ -451,9 +458,6 @@ __device__ __forceinline__ double occ_of(const WPtr<LW>& P, const Dev& D, int c,
   return occ_dict(dict_load<LW>(P, c), P.netocc[c], dt, D);
 }
 
-__device__ __forceinline__ double resolve_dur(const Dev& D, double d) {  // _calc_occupancy :1892-1899
-  return d < 0 ? D.unknown_duration : d;  // max_exec_time stays -1 without heartbeats
-}
 
 __device__ __attribute__((always_inline)) void serr(SCtl& S, int code, int task) {
   if (atomicCAS(&S.error, 0, code) == 0) S.err_task = task;
@@ -552,7 +556,7 @@ __device__ __forceinline__ bool gdict_add(WState& g, int p, int delta) {
 }
 // SchedulerState.total_occupancy :1877 (prefix dict order)
 __device__ __forceinline__ double ws_total_occ(const Dev& D, const WState& g) {
-  const double rv = resolve_dur(D, g.wd);
+  const double rv = resolve_dur(D, g.wd, lane_id() & (PD - 1));
   double res = 0.0;
 #pragma unroll
   for (int i = 0; i < PD; i++) {
@@ -568,10 +572,10 @@ template <bool LW>
 __device__ __forceinline__ void ws_fold(const Dev& D, const WPtr<LW>& P, SCtl& S, WState& g, int kind, int w, int p,
                                         long long dnet, double occ, int nproc, double dobs) {
   const int lane = lane_id();
-  if (kind == K_COMPLETE) {
+  if (kind != K_PLACE) {
     // no compute interval in the message (NaN): no EWMA step (TaskGroup.add_duration :1114)
     if (lane == p && dobs == dobs) g.wd = g.wd < 0 ? dobs : 0.5 * dobs + 0.5 * g.wd;
-    gdict_add(g, p, -1);
+    if (kind == K_COMPLETE) gdict_add(g, p, -1);
   } else if (!gdict_add(g, p, +1)) {
     serr(S, SERR_PREFIX, -1);
   }
@@ -580,13 +584,16 @@ __device__ __forceinline__ void ws_fold(const Dev& D, const WPtr<LW>& P, SCtl& S
   const long long pp = nproc;
   bool idle, sat = false;
   double avg = -1.0;
-  if (pp < nt) {
+  const bool paused = (P.wflags[w] & WF_PAUSED) != 0;
+  if (paused) {
+    idle = false;  // not running: idle.pop, saturated.discard (:2975-2977)
+  } else if (pp < nt) {
     idle = true;
   } else {
     avg = ws_total_occ(D, g) / (double)D.total_nthreads;
     idle = occ < (double)nt * avg / 2;
   }
-  if (!idle && pp > nt) {
+  if (!idle && pp > nt && !paused) {
     const double pending = occ * (double)(pp - nt) / (double)(pp * nt);
     if (0.4 < pending) {
       if (avg < 0) avg = ws_total_occ(D, g) / (double)D.total_nthreads;
@@ -594,7 +601,7 @@ __device__ __forceinline__ void ws_fold(const Dev& D, const WPtr<LW>& P, SCtl& S
     }
   }
   const uint8_t fo = P.wflags[w];
-  const uint8_t fn = (idle ? WF_IDLE : 0) | (sat ? WF_SAT : 0);
+  const uint8_t fn = (fo & WF_PAUSED) | (idle ? WF_IDLE : 0) | (sat ? WF_SAT : 0);
   if (fo != fn) {
     g.n_idle += (idle ? 1 : 0) - ((fo & WF_IDLE) ? 1 : 0);
     g.n_sat += (sat ? 1 : 0) - ((fo & WF_SAT) ? 1 : 0);
@@ -624,7 +631,7 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
   // (a) durations unchanged: every completion's EWMA result equals the current value
   const double cur = __shfl(g.wd, p & (PD - 1));
   const double nw = cur < 0 ? rc.dur : 0.5 * rc.dur + 0.5 * cur;
-  bool bad = in && kind == K_COMPLETE && rc.dur == rc.dur && __double_as_longlong(nw) != __double_as_longlong(cur);
+  bool bad = in && kind != K_PLACE && rc.dur == rc.dur && __double_as_longlong(nw) != __double_as_longlong(cur);
   // (b) prefix counts stay >= 1 and every record's prefix is in the dict
   bool found = !in;
   long long cnt_i[PD];
@@ -634,7 +641,7 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
     cnt_i[k] = 0;
     tot[k] = 0;
     if (k >= g.n) continue;
-    const long long dl = (in && p == g.pf[k]) ? (kind == K_COMPLETE ? -1 : 1) : 0;
+    const long long dl = (in && p == g.pf[k]) ? (kind == K_COMPLETE ? -1 : kind == K_PLACE ? 1 : 0) : 0;
     if (in && p == g.pf[k]) found = true;
     const long long inc = wscan_incl(dl);
     cnt_i[k] = g.cnt[k] + inc;
@@ -653,7 +660,7 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
   }
   const long long dn_inc = wscan_incl(in ? (long long)rc.dnet : 0);
   const double netocc_i = g.netocc + (double)dn_inc;
-  const double rv = resolve_dur(D, g.wd);
+  const double rv = resolve_dur(D, g.wd, lane & (PD - 1));
   double tocc = 0.0;
 #pragma unroll
   for (int k = 0; k < PD; k++) {
@@ -665,9 +672,10 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
   const long long nt = in ? (long long)P.nthreads[w] : 1;
   const long long pp = np;
   const double avg = tocc / (double)D.total_nthreads;
-  bool idle = pp < nt || rc.occ < (double)nt * avg / 2;
+  const bool paused = in && (P.wflags[w] & WF_PAUSED);
+  bool idle = !paused && (pp < nt || rc.occ < (double)nt * avg / 2);
   bool sat = false;
-  if (!idle && pp > nt) {
+  if (!idle && pp > nt && !paused) {
     const double pending = rc.occ * (double)(pp - nt) / (double)(pp * nt);
     sat = 0.4 < pending && pending > 1.9 * avg;
   }
@@ -680,7 +688,7 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
   int di = 0, ds = 0;
   if (last) {
     const uint8_t fo = P.wflags[w];
-    const uint8_t fn = (idle ? WF_IDLE : 0) | (sat ? WF_SAT : 0);
+    const uint8_t fn = (fo & WF_PAUSED) | (idle ? WF_IDLE : 0) | (sat ? WF_SAT : 0);
     di = (idle ? 1 : 0) - ((fo & WF_IDLE) ? 1 : 0);
     ds = (sat ? 1 : 0) - ((fo & WF_SAT) ? 1 : 0);
     if (fo != fn) P.wflags[w] = fn;
@@ -738,7 +746,7 @@ __device__ __attribute__((always_inline)) void snapshot(const Dev& D, SLds& L, c
       D.snap_occ[k] = o;
       D.snap_nbytes[k] = P.nbytes[c];
       D.snap_nproc[k] = P.nproc[c];
-      const bool itc = D.sat_inf || (int)P.cap[c] - P.nproc[c] > 0;
+      const bool itc = !(P.wflags[c] & WF_PAUSED) && (D.sat_inf || (int)P.cap[c] - P.nproc[c] > 0);
       D.snap_flags[k] = P.wflags[c] | (itc ? WF_ITC : 0);
     }
   }
@@ -1047,11 +1055,15 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   auto scr = L.pre_scr[lane_id()];
   int nt = 0;
   bool tbad = false;
+  // service events the local path does not model make the stimulus global (exe_global):
+  // a paused worker (not in running), a replica set beyond holder_of, a long-running task
+  bool evg = false;
   auto touch = [&](int c, bool cand) {
     if (c < 0 || c >= D.W) {
       tbad = true;
       return;
     }
+    if ((D.evf & EVF_PAUSED) && (D.w_flags[c] & WF_PAUSED)) evg = true;
     for (int i = 0; i < nt && i < TMAX; i++)
       if ((scr[i] & T_W) == c) {
         if (cand) scr[i] |= (uint16_t)T_CAND;
@@ -1072,6 +1084,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   const int kt = (int)(k1 - k0);
   uint32_t flags = 0;
   if (f1 == f0 && !(tf & TF_WANTED)) flags |= F_SELFREL;
+  if ((D.evf & EVF_LR) && (D.tdyn[t] & TD_LR)) evg = true;
   if (kt > KT_MAX) {
     flags |= F_GLOBAL;
     PROF(atomicAdd(&L.c.prof[20], 1ull));  // diagnostics: why stimuli run global
@@ -1085,6 +1098,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
       const int64_t nb = nbv(D, D.res_nbytes[d]);
       const int hd = D.holder_of[d];
       if (k == k0) h_dep0 = hd;
+      if ((D.evf & EVF_MULTI) && (D.tdyn[d] & TD_MULTI)) evg = true;
       E[n++] = make_uint4((unsigned)d, (unsigned)hd, lo32(nb), hi32(nb));
     }
     for (int64_t k = k0; k < k1; k++) {
@@ -1120,6 +1134,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
       const int d = D.dep_idx[q];
       const int64_t nb = nbv(D, D.res_nbytes[d]);
       const int hd = D.holder_of[d];
+      if ((D.evf & EVF_MULTI) && (D.tdyn[d] & TD_MULTI)) evg = true;
       touch(hd, true);
       E[n++] = make_uint4((unsigned)d, (unsigned)hd, lo32(nb), hi32(nb));
     }
@@ -1129,6 +1144,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   if (nf > 255 || nt > TMAX) flags |= F_GLOBAL;
   if (nf + (D.sat_inf ? 0 : D.w_cap[w]) + 1 > PLC) flags |= F_GLOBAL;  // staging room for the refill
   if (tbad) flags |= F_GLOBAL | F_BADTOUCH;
+  if (evg) flags |= F_GLOBAL;
   if (!(flags & F_GLOBAL) && nt == 1 && nf == 0 && kt <= 1 && nrel <= 1 &&
       (kt == 0 || h_dep0 == w))
     flags |= F_SIMPLE;
@@ -1183,7 +1199,7 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
         const int pi = rl(pl, i);
         const double di = mkd(rlu(dlo(dl), i), rlu(dhi(dl), i));
         if (lane == pi && di == di) dur = dur < 0 ? di : 0.5 * di + 0.5 * dur;  // NaN: no compute interval
-        if (lane < PD) ((double*)(D.desc + (size_t)((a + i) & (DR - 1)) * NE + 3))[lane] = resolve_dur(D, dur);
+        if (lane < PD) ((double*)(D.desc + (size_t)((a + i) & (DR - 1)) * NE + 3))[lane] = resolve_dur(D, dur, lane);
       }
     }
     __threadfence_block();
@@ -1410,7 +1426,7 @@ __device__ __forceinline__ int64_t scan_needs_sum(const Dev& D, int64_t k0, int6
   int64_t v = 0;
   for (int64_t q = k0 + lane_id(); q < k1; q += 64) {
     const int d = D.dep_idx[q];
-    if (D.holder_of[d] == c) continue;
+    if (holds_any(D, d, c)) continue;
     if (!st_needed_elsewhere(D, d, c, except)) v += nbv(D, D.res_nbytes[d]);
   }
   return wsum64(v);
@@ -1456,6 +1472,9 @@ __device__ __attribute__((always_inline)) int64_t needs_dec(const Dev& D, SCtl& 
       return gone ? nb : 0;
     }
   }
+  // remove_from_processing decrements only what is in needs_what (:767-769): after replica
+  // events (add_replica deletes the entry, :831-834) an entry may be gone
+  if (D.evf & EVF_MULTI) return 0;
   serr(S, SERR_NEEDS, d);
   return 0;
 }
@@ -2296,6 +2315,27 @@ __device__ __attribute__((always_inline)) bool bulk_single_holder(const Dev& D, 
   return true;
 }
 
+// remove_all_replicas of a released dependency d (:3161-3171): every holder's ws.nbytes,
+// then who_has = None (one lane per dependency; holders may be shared: LDS / global atomics)
+template <bool LW>
+__device__ __forceinline__ void release_replicas(const Dev& D, const WPtr<LW>& P, int d) {
+  const int64_t nb = nbv(D, D.res_nbytes[d]);
+  if ((D.evf & EVF_MULTI) && (D.tdyn[d] & TD_MULTI)) {
+    for (int b = 0; b < D.WB; b++) {
+      unsigned long long m = D.holders[(size_t)d * D.WB + b];
+      D.holders[(size_t)d * D.WB + b] = 0;
+      for (; m; m &= m - 1)
+        __hip_atomic_fetch_add(P.nbytes + (b * 64 + __builtin_ctzll(m)), -nb, __ATOMIC_RELAXED,
+                               LW ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_AGENT);
+    }
+    D.tdyn[d] &= (uint8_t)~TD_MULTI;
+  } else {
+    const int hd = D.holder_of[d];
+    __hip_atomic_fetch_add(P.nbytes + hd, -nb, __ATOMIC_RELAXED, LW ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_AGENT);
+    D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
+  }
+}
+
 // a stimulus that reads SchedulerState-global state: every earlier stimulus has retired,
 // every later one waits, the walker is caught up. Exact restatement of the whole
 // transition (:2366-2442, :2313-2336, :4983-5023) for any route; placements go straight
@@ -2332,9 +2372,23 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
     int64_t v = 0;
     for (int64_t k = D.dep_ptr[x] + lane; k < D.dep_ptr[x + 1]; k += 64) {
       const int d = D.dep_idx[k];
-      if (D.holder_of[d] != c) v += nbv(D, D.res_nbytes[d]);
+      if (!holds_any(D, d, c)) v += nbv(D, D.res_nbytes[d]);
     }
     return wsum64(v);
+  };
+  const bool evp = (D.evf & EVF_PAUSED) != 0;
+  auto paused = [&](int c) { return evp && (P.wflags[c] & WF_PAUSED); };
+  // x's candidates need decide_worker's general form: a dependency with several replicas
+  // (who_has row) or a paused holder (uniform; all lanes)
+  auto gen_x = [&](int x) -> bool {
+    if (!(D.evf & (EVF_MULTI | EVF_PAUSED))) return false;
+    bool gx = false;
+    for (int64_t q = D.dep_ptr[x] + lane; q < D.dep_ptr[x + 1]; q += 64) {
+      const int d = D.dep_idx[q];
+      const int h = D.holder_of[d];
+      gx = gx || ((D.evf & EVF_MULTI) && (D.tdyn[d] & TD_MULTI)) || (h >= 0 && h < D.W && paused(h));
+    }
+    return ballot(gx) != 0;
   };
   WDict wd;
   bool skip_deps = false;  // the caller knows c holds every dependency of x
@@ -2355,7 +2409,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
         break;
       }
       const int d = D.dep_idx[k];
-      if (D.holder_of[d] == c) continue;
+      if (holds_any(D, d, c)) continue;
       dn += needs_inc(D, S, c, nl, d, nbv(D, D.res_nbytes[d]), x);
     }
     line_store<LW>(P, c, nl);
@@ -2372,6 +2426,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   auto itc_argmin = [&]() -> int {  // decide_worker_rootish_queuing_enabled :2230-2233
     Key b = argmin_workers(D, [&](int c, Key& k) {
       if (!D.sat_inf && (int)P.cap[c] - P.nproc[c] <= 0) return false;
+      if (paused(c)) return false;  // idle_task_count holds running workers only (:2992)
       k.start = (double)P.nproc[c] / (double)P.nthreads[c];
       k.nb = 0;
       k.w = c;
@@ -2385,7 +2440,10 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   {
     const int np0 = P.nproc[w];
     const int64_t no0 = P.netocc[w];
-    dict_update<LW>(P, w, p, -1, wd);
+    // a long-running task left the prefix counts at add_to_long_running (:764-766)
+    const bool lr = (D.evf & EVF_LR) && (D.tdyn[t] & TD_LR);
+    if (lr) wd = dict_load<LW>(P, w);
+    else dict_update<LW>(P, w, p, -1, wd);
     uint32_t nl = line_load<LW>(P, w);
     int64_t dnet = 0;
     for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
@@ -2394,7 +2452,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
         break;
       }
       const int d = D.dep_idx[k];
-      if (D.holder_of[d] == w) continue;
+      if (holds_any(D, d, w)) continue;
       dnet -= needs_dec(D, S, w, nl, d, nbv(D, D.res_nbytes[d]), t);
     }
     if (np0 - 1 == 0) needs_reset(D, w, nl);
@@ -2406,9 +2464,15 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       D.cur_nbytes[t] = nbt;
       D.proc_on[t] = -1;
       D.state[t] = S_MEMORY;
+      if (lr) {  // long_running.discard: the slot it held on top of the cap goes
+        P.cap[w] = (uint16_t)(P.cap[w] - 1);
+        D.w_cap[w] -= 1;
+        D.tdyn[t] &= (uint8_t)~TD_LR;
+      }
     }
-    ws_fold<LW>(D, P, S, g, K_COMPLETE, w, p, dnet, occ_dict(wd, no0 + dnet, durv, D), np0 - 1,
-                dobs);
+    __threadfence_block();
+    ws_fold<LW>(D, P, S, g, lr ? K_COMPLETE_LR : K_COMPLETE, w, p, dnet, occ_dict(wd, no0 + dnet, durv, D),
+                np0 - 1, dobs);
   }
   // ------------------------------------------------------ releases (:3309-3314, :2444)
   const int64_t f0 = D.dpt_ptr[t], f1 = D.dpt_ptr[t + 1];
@@ -2423,10 +2487,8 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
         const int d = D.dep_idx[k];
         if (D.rel_mark[d] != (int)r) continue;
-        const int hd = D.holder_of[d];
-        P.nbytes[hd] -= nbv(D, D.res_nbytes[d]);
+        release_replicas<LW>(D, P, d);
         D.state[d] = S_RELEASED;
-        D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
         atomicAdd((unsigned long long*)&D.g_relwait[D.group[d]], 1ull);
       }
     }
@@ -2436,10 +2498,8 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
     for (int64_t k = D.dep_ptr[t] + lane; k < D.dep_ptr[t + 1]; k += 64) {
       const int d = D.dep_idx[k];
       if (D.rel_mark[d] != (int)r) continue;
-      const int hd = D.holder_of[d];
-      __hip_atomic_fetch_add(P.nbytes + hd, -nbv(D, D.res_nbytes[d]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      release_replicas<LW>(D, P, d);
       D.state[d] = S_RELEASED;
-      D.holders[(size_t)d * D.WB + (hd >> 6)] = 0;
       atomicAdd((unsigned long long*)&D.g_relwait[D.group[d]], 1ull);
     }
     lds_fence();
@@ -2457,7 +2517,12 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
      fml = D.fr_mark[xl];
      tfl = D.tflags[xl];
      const int64_t a = D.dep_ptr[xl], e = D.dep_ptr[xl + 1];
-     if (e - a == 1) h1l = D.holder_of[D.dep_idx[a]];
+     if (e - a == 1) {
+       const int d1 = D.dep_idx[a];
+       h1l = D.holder_of[d1];
+       // a replica set or a paused holder: decide_worker's general form below
+       if (((D.evf & EVF_MULTI) && (D.tdyn[d1] & TD_MULTI)) || (h1l >= 0 && h1l < D.W && paused(h1l))) h1l = -1;
+     }
    }
    const int nk = (int)min((int64_t)64, f1 - k0);
    if (bulk_single_holder<LW>(D, S, P, g, durv, r, k0 + lane < f1 && fml == (int)r, xl, tfl, h1l, lpos, npl))
@@ -2478,14 +2543,15 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       const int gi = D.group[x];
       if (D.sat_inf) {  // decide_worker_rootish_queuing_disabled :2135-2193
         int c = D.g_lastw[gi];
-        if (!(c >= 0 && D.g_left[gi] != 0)) {
-          const bool use_idle = g.n_idle > 0;
+        if (!(c >= 0 && D.g_left[gi] != 0 && !paused(c))) {  // lws.status == running (:2170)
+          const bool use_idle = g.n_idle > 0;  // pool = idle or running (:2161)
           Key b = argmin_workers(D, [&](int cw, Key& kk) {
             const double ocw = occ_of<LW>(P, D, cw, durv);  // all lanes: it shuffles
             if (use_idle && !(P.wflags[cw] & WF_IDLE)) return false;
+            if (!use_idle && paused(cw)) return false;
             int64_t cm = 0;
             for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++)
-              if (D.holder_of[D.dep_idx[q]] != cw) cm += nbv(D, D.res_nbytes[D.dep_idx[q]]);
+              if (!holds_any(D, D.dep_idx[q], cw)) cm += nbv(D, D.res_nbytes[D.dep_idx[q]]);
             kk.start = ocw / (double)P.nthreads[cw] + (double)cm / (double)D.bandwidth;
             kk.nb = P.nbytes[cw];
             kk.w = cw;
@@ -2523,7 +2589,8 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
           place_x(x, c, ROUTE_ROOTISH_Q, -1, true);
         }
       }
-    } else if (D.dep_ptr[x + 1] > D.dep_ptr[x] && D.dep_ptr[x + 1] - D.dep_ptr[x] <= 64 && x != D.dbg_task) {
+    } else if (!gen_x(x) && D.dep_ptr[x + 1] > D.dep_ptr[x] && D.dep_ptr[x + 1] - D.dep_ptr[x] <= 64 &&
+               x != D.dbg_task) {
       // decide_worker :8550-8593 with the candidates = the dependency holders held in
       // lanes (at most 64 deps): one objective per distinct holder instead of a sweep
       // over all W workers. Same keys and the same total order as the sweep below.
@@ -2570,7 +2637,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
         if (key_less(q, b)) b = q;
       }
       place_x(x, b.w, ROUTE_NONROOTISH, b.comm, true);
-    } else if (D.dep_ptr[x + 1] - D.dep_ptr[x] > 64 && x != D.dbg_task) {
+    } else if (!gen_x(x) && D.dep_ptr[x + 1] - D.dep_ptr[x] > 64 && x != D.dbg_task) {
       // decide_worker :8550-8593 for a wide fan-in (the shuffle barrier: P deps): one
       // lane-parallel pass over the deps accumulates, per holder, the bytes it already
       // holds and how many deps it holds; then comm(c) = total - held(c) (exact int64)
@@ -2613,14 +2680,18 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       }
       place_x(x, b.w, ROUTE_NONROOTISH, b.comm, true);
     } else if (D.dep_ptr[x + 1] > D.dep_ptr[x]) {  // decide_worker :8550-8593
-      Key b = argmin_workers(D, [&](int cw, Key& kk) {
+      // candidates = who_has of the dependencies & running; none: every running worker
+      // (valid_workers = running when a worker is paused, decide_worker_non_rootish :2262-2266)
+      bool any_cand = true;
+      auto key_x = [&](int cw, Key& kk) {
         const double ocw = occ_of<LW>(P, D, cw, durv);  // all lanes: it shuffles
-        bool cand = false;
-        for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1] && !cand; q++) cand = D.holder_of[D.dep_idx[q]] == cw;
+        if (paused(cw)) return false;
+        bool cand = !any_cand;
+        for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1] && !cand; q++) cand = holds_any(D, D.dep_idx[q], cw);
         if (!cand) return false;
         int64_t cm = 0;
         for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++)
-          if (D.holder_of[D.dep_idx[q]] != cw) cm += nbv(D, D.res_nbytes[D.dep_idx[q]]);
+          if (!holds_any(D, D.dep_idx[q], cw)) cm += nbv(D, D.res_nbytes[D.dep_idx[q]]);
         kk.start = ocw / (double)P.nthreads[cw] + (double)cm / (double)D.bandwidth;
         kk.nb = P.nbytes[cw];
         kk.w = cw;
@@ -2637,7 +2708,12 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
           B[7] = (double)wd_n(P.plen[cw]) + 100.0 * r;
         }
         return true;
-      });
+      };
+      Key b = argmin_workers(D, key_x);
+      if (b.w == INT32_MAX && evp) {  // every holder paused
+        any_cand = false;
+        b = argmin_workers(D, key_x);
+      }
       if (b.w == INT32_MAX) {
         serr(S, SERR_CAND, x);
         break;
@@ -2655,7 +2731,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
     long long slots = 0;
     for (int c = lane; c < D.W; c += 64) {
       const int a = (int)P.cap[c] - P.nproc[c];
-      if (a > 0) slots += a;
+      if (a > 0 && !paused(c)) slots += a;  // over idle_task_count (:5007-5010)
     }
     slots = wsum64(slots);
     for (long long k = 0; k < slots; k++) {
@@ -2675,7 +2751,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   // the invariant local refills rely on, and whether queued tasks are interchangeable
   {
     bool open = false;
-    for (int c = lane; c < D.W && !D.sat_inf; c += 64) open = open || ((int)P.cap[c] - P.nproc[c] > 0);
+    for (int c = lane; c < D.W && !D.sat_inf; c += 64) open = open || ((int)P.cap[c] - P.nproc[c] > 0 && !paused(c));
     const bool any_open = ballot(open) != 0;
     if (lane == 0) S.inv_ok = (S.qlen == 0 || !any_open) ? 1 : 0;
     if (queue_changed) {
@@ -2856,7 +2932,7 @@ __device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WP
       P.netocc[c] = D.w_netocc[c];
       P.nbytes[c] = D.w_nbytes[c];
       P.mask[c] = 0;
-      P.wflags[c] = D.w_flags[c] & (WF_IDLE | WF_SAT);
+      P.wflags[c] = D.w_flags[c] & (WF_IDLE | WF_SAT | WF_PAUSED);
       // needs_what: the stream layout persists in gw_needs (the engine's lines stay unused)
       for (int i = 0; i < NLW; i++) P.needs[(size_t)c * NLW + i] = D.gw_needs_saved[(size_t)c * NLW + i];
     } else {
@@ -2872,7 +2948,7 @@ __device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WP
       D.w_netocc[c] = P.netocc[c];
       D.w_nbytes[c] = P.nbytes[c];
       const int slots = D.sat_inf ? 0 : (int)P.cap[c] - P.nproc[c];
-      const bool itc = D.sat_inf || slots > 0;
+      const bool itc = !(P.wflags[c] & WF_PAUSED) && (D.sat_inf || slots > 0);
       D.w_flags[c] = P.wflags[c] | (itc ? WF_ITC : 0);
       D.w_itcslots[c] = itc ? slots : 0;
       for (int i = 0; i < NLW; i++) D.gw_needs_saved[(size_t)c * NLW + i] = P.needs[(size_t)c * NLW + i];
@@ -2970,7 +3046,7 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     }
     __syncthreads();
     for (int w = tid; w < D.W; w += blockDim.x) {
-      if (!D.sat_inf && (int)P.cap[w] - P.nproc[w] > 0) atomicOr(&s_open, 1);
+      if (!D.sat_inf && (int)P.cap[w] - P.nproc[w] > 0 && !(P.wflags[w] & WF_PAUSED)) atomicOr(&s_open, 1);
       atomicMax(&s_cap, (int)P.cap[w]);
     }
     const int p0 = S.qlen > 0 ? D.prefix[D.qarr[S.qhead]] : 0;
@@ -3021,7 +3097,7 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
   __syncthreads();
   for (int w = tid; w < D.W; w += blockDim.x) {
     const int slots = D.sat_inf ? 0 : (int)P.cap[w] - P.nproc[w];
-    if (D.sat_inf || slots > 0) {
+    if (!(P.wflags[w] & WF_PAUSED) && (D.sat_inf || slots > 0)) {
       atomicAdd((unsigned long long*)&s_itc, 1ull);
       atomicAdd((unsigned long long*)&s_slots, (unsigned long long)(long long)(D.sat_inf ? 0 : slots));
     }
@@ -3099,6 +3175,10 @@ __global__ void __launch_bounds__(64) k_move_task(const Dev* __restrict__ Dp, in
     if (lane == 0) set_error(D, ERR_BAD_STATE, t);
     return;
   }
+  if (D.tdyn[t] & TD_LR) {  // long-running tasks leave the stealable bins (handle_long_running :5829-5831)
+    if (lane == 0) set_error(D, ERR_UNSUPPORTED, t);
+    return;
+  }
   const int p = D.prefix[t];
   const int64_t k0 = D.dep_ptr[t], k1 = D.dep_ptr[t + 1];
   // victim: the dependencies it needed a replica of (not held there) are needed less
@@ -3106,7 +3186,7 @@ __global__ void __launch_bounds__(64) k_move_task(const Dev* __restrict__ Dp, in
   int64_t freed = 0;
   for (int64_t k = k0; k < k1; k++) {
     const int d = D.dep_idx[k];
-    if (D.holder_of[d] == v) continue;
+    if (holds_any(D, d, v)) continue;
     freed += needs_dec(D, S, v, nl, d, nbv(D, D.res_nbytes[d]), t);
   }
   const int npv = D.w_nproc[v] - 1;
@@ -3117,7 +3197,7 @@ __global__ void __launch_bounds__(64) k_move_task(const Dev* __restrict__ Dp, in
   int64_t added = 0;
   for (int64_t k = k0; k < k1; k++) {
     const int d = D.dep_idx[k];
-    if (D.holder_of[d] == h) continue;
+    if (holds_any(D, d, h)) continue;
     added += needs_inc(D, S, h, nh, d, nbv(D, D.res_nbytes[d]), t);
   }
   if (lane < NLW) D.gw_needs_saved[(size_t)h * NLW + lane] = nh;
@@ -3144,54 +3224,20 @@ __global__ void __launch_bounds__(64) k_move_task(const Dev* __restrict__ Dp, in
   }
 }
 
-// ===================================================================== worker joins
-// Scheduler.add_worker (scheduler.py:4308-4441) on the engine state between launches
-// (service mode). The host has grown every per-worker array to W and set the new worker
-// w = W - 1's nthreads / cap; here: the empty WorkerState, check_idle_saturated(ws)
-// (:4398), then stimulus_queue_slots_maybe_opened (:4416-4420, :4983-5023): the open slots
-// of idle_task_count, each taking the queue's head through _transition_queued_processing
-// (:2797-2808) -> decide_worker_rootish_queuing_enabled (:2227-2236: argmin of
-// len(processing) / nthreads over idle_task_count, lowest index on ties) ->
-// _add_to_processing (:3199-3215: add_to_processing, check_idle_saturated, n_tasks).
-// bulk_schedule_unrunnable_after_adding_worker has nothing to schedule on this path (no
-// restrictions: no task is no-worker). One wave; *placed = the placements made.
-__global__ void __launch_bounds__(64) k_add_worker(const Dev* __restrict__ Dp, long long* placed) {
-  const Dev& D = *Dp;
-  __shared__ SCtl S;  // needs_inc reports inconsistencies through it
+// ============================================================= queue refill
+// Scheduler.stimulus_queue_slots_maybe_opened (:4983-5023) on the engine state between
+// launches (service mode), one wave: the open slots of idle_task_count summed before any
+// transition (:5007-5012), then each takes the queue's head through
+// _transition_queued_processing (:2797-2808) -> decide_worker_rootish_queuing_enabled
+// (:2227-2236: argmin of len(processing) / nthreads over idle_task_count, lowest index on
+// ties) -> _add_to_processing (:3199-3215: add_to_processing, check_idle_saturated,
+// n_tasks). Returns the placements made (uniform).
+__device__ long long refill_queue(const Dev& D, SCtl& S) {
   const int lane = lane_id();
-  const int w = D.W - 1;
   Ctl* c = D.ctl;
-  if (lane == 0) {
-    S.error = 0;
-    S.err_task = -1;
-    S.stop = 0;
-    D.w_nproc[w] = 0;
-    D.w_plen[w] = 0;
-    D.w_netocc[w] = 0;
-    D.w_nbytes[w] = 0;
-    D.w_itcslots[w] = 0;
-    D.w_lastcheck[w] = ~0ull;
-    D.w_flags[w] = 0;
-    *placed = 0;
-  }
-  for (int i = lane; i < PMAX; i += 64) {
-    D.w_pfx[(size_t)w * PMAX + i] = 0;
-    D.w_pcnt[(size_t)w * PMAX + i] = 0;
-  }
-  if (lane < NLW) D.gw_needs_saved[(size_t)w * NLW + lane] = 0;
-  if (lane < NXW) D.gw_needs_ext[(size_t)w * NXW + lane] = 0;
-  __threadfence();
-  __syncthreads();
-  if (lane == 0) {  // check_idle_saturated(ws): nothing processing -> idle; idle_task_count
-    walk_flags(D, w, occupancy(D, w, D.pdur_walk), 0);
-    itc_check(D, w, false);
-  }
-  __threadfence();
-  __syncthreads();
   // queue position and log length in registers (uniform); lane 0 writes them back at the end
   long long qhead = c->qhead, qlen = c->qlen, pos = (long long)c->n_placed;
-  if (D.sat_inf || qlen <= 0) return;
-  // slots_available over idle_task_count, summed before any transition (:5007-5012)
+  if (D.sat_inf || qlen <= 0) return 0;
   long long slots = 0;
   for (int i = lane; i < D.W; i += 64)
     if (D.w_flags[i] & WF_ITC) slots += (long long)D.w_cap[i] - D.w_nproc[i];
@@ -3227,7 +3273,7 @@ __global__ void __launch_bounds__(64) k_add_worker(const Dev* __restrict__ Dp, l
     uint32_t nl = lane < NLW ? D.gw_needs_saved[(size_t)ws * NLW + lane] : 0u;
     for (int64_t q = k0; q < k1; q++) {
       const int d = D.dep_idx[q];
-      if (D.holder_of[d] == ws) continue;
+      if (holds_any(D, d, ws)) continue;
       const int64_t nb = nbv(D, D.res_nbytes[d]);
       comm += nb;
       added += needs_inc(D, S, ws, nl, d, nb, t);
@@ -3270,8 +3316,57 @@ __global__ void __launch_bounds__(64) k_add_worker(const Dev* __restrict__ Dp, l
     c->n_placed = (unsigned long long)pos;
     c->qhead = qhead;
     c->qlen = qlen;
-    *placed = n;
   }
+  __threadfence();
+  __syncthreads();
+  return n;
+}
+
+// ===================================================================== worker joins
+// Scheduler.add_worker (scheduler.py:4308-4441) on the engine state between launches
+// (service mode). The host has grown every per-worker array to W and set the new worker
+// w = W - 1's nthreads / cap; here: the empty WorkerState, check_idle_saturated(ws)
+// (:4398), then stimulus_queue_slots_maybe_opened (:4416-4420, :4983-5023): the open slots
+// of idle_task_count, each taking the queue's head through _transition_queued_processing
+// (:2797-2808) -> decide_worker_rootish_queuing_enabled (:2227-2236: argmin of
+// len(processing) / nthreads over idle_task_count, lowest index on ties) ->
+// _add_to_processing (:3199-3215: add_to_processing, check_idle_saturated, n_tasks).
+// bulk_schedule_unrunnable_after_adding_worker has nothing to schedule on this path (no
+// restrictions: no task is no-worker). One wave; *placed = the placements made.
+__global__ void __launch_bounds__(64) k_add_worker(const Dev* __restrict__ Dp, long long* placed) {
+  const Dev& D = *Dp;
+  __shared__ SCtl S;  // needs_inc reports inconsistencies through it
+  const int lane = lane_id();
+  const int w = D.W - 1;
+  if (lane == 0) {
+    S.error = 0;
+    S.err_task = -1;
+    S.stop = 0;
+    D.w_nproc[w] = 0;
+    D.w_plen[w] = 0;
+    D.w_netocc[w] = 0;
+    D.w_nbytes[w] = 0;
+    D.w_itcslots[w] = 0;
+    D.w_lastcheck[w] = ~0ull;
+    D.w_flags[w] = 0;
+    *placed = 0;
+  }
+  for (int i = lane; i < PMAX; i += 64) {
+    D.w_pfx[(size_t)w * PMAX + i] = 0;
+    D.w_pcnt[(size_t)w * PMAX + i] = 0;
+  }
+  if (lane < NLW) D.gw_needs_saved[(size_t)w * NLW + lane] = 0;
+  if (lane < NXW) D.gw_needs_ext[(size_t)w * NXW + lane] = 0;
+  __threadfence();
+  __syncthreads();
+  if (lane == 0) {  // check_idle_saturated(ws): nothing processing -> idle; idle_task_count
+    walk_flags(D, w, occupancy(D, w, D.pdur_walk), 0);
+    itc_check(D, w, false);
+  }
+  __threadfence();
+  __syncthreads();
+  const long long n = refill_queue(D, S);
+  if (lane == 0) *placed = n;
 }
 
 }  // namespace st

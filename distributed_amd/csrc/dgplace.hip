@@ -25,6 +25,7 @@
 #include "../../include/dgplace.h"
 #include "dgp_device.h"
 #include "dgp_stream.h"
+#include "dgp_events.h"
 #include "dgp_steal.h"
 #include "dgp_service.h"
 
@@ -93,6 +94,9 @@ struct dgp_engine {
   std::vector<uint8_t> h_wanted;
   std::vector<int64_t> gdep_n, gdep_len;   // per group: len(tg.dependencies), sum of their lengths
   std::vector<int8_t> rootish_override_h;  // TaskState._rootish per task (-1: None)
+  std::vector<uint8_t> paused_h;           // per worker: not in SchedulerState.running
+  char* d_ev = nullptr;                    // service-event argument staging (device)
+  size_t d_ev_cap = 0;
 };
 
 namespace {
@@ -185,10 +189,11 @@ int check_device_error(dgp_engine* e, dgp::Ctl* out = nullptr) {
                                   "no worker", "needs_what line overflow", "prefix dict overflow (stream)",
                                   "watchdog: the stream engine made no progress", "queue", "needs_what inconsistent",
                                   "record log overflow (stream)", "task without candidates (stream)",
-                                  "descriptor ring out of order", "worker index out of range (stream)", "stream invariant violated"};
+                                  "descriptor ring out of order", "worker index out of range (stream)", "stream invariant violated",
+                                  "a service event the engine does not model"};
     char buf[200];
     snprintf(buf, sizeof buf, "device engine error %d (%s) at task %d", c.error,
-             (c.error >= 0 && c.error <= 19) ? names[c.error] : "?", c.err_task);
+             (c.error >= 0 && c.error <= 20) ? names[c.error] : "?", c.err_task);
     return fail(e, DGP_E_DEVICE, buf);
   }
   return 0;
@@ -432,6 +437,7 @@ void dgp_destroy(dgp_engine* e) {
   if (e->d_msgs) (void)hipFree(e->d_msgs);
   if (e->d_status) (void)hipFree(e->d_status);
   if (e->h_msgs) (void)hipHostFree(e->h_msgs);
+  if (e->d_ev) (void)hipFree(e->d_ev);
   if (e->steal.arena) (void)hipFree(e->steal.arena);
   (void)hipFree(e->ctl);
   (void)hipFree(e->d_aux);
@@ -448,7 +454,7 @@ int dgp_set_config(dgp_engine* e, int64_t bandwidth, int64_t default_data_size, 
   if (!e) return DGP_E_ARG;
   if (bandwidth <= 0 || default_data_size < 0 || !(saturation > 0))
     return fail(e, DGP_E_ARG, "bandwidth must be > 0, default_data_size >= 0, saturation > 0");
-  e->D.bandwidth = bandwidth;
+  e->D.bandwidth = (double)bandwidth;
   e->D.default_data_size = default_data_size;
   e->D.unknown_duration = unknown_duration;
   e->D.saturation = saturation;
@@ -514,7 +520,7 @@ int dgp_set_workers(dgp_engine* e, int32_t n_workers, const int32_t* nthreads) {
   if (rc) return DGP_E_HIP;
   HIPCHK(e, hipMemcpy(D.w_nthreads, nthreads, (size_t)n_workers * 4, hipMemcpyHostToDevice));
   e->have_workers = true;
-  return dgp_set_config(e, D.bandwidth, D.default_data_size, D.unknown_duration, D.saturation);
+  return dgp_set_config(e, (int64_t)D.bandwidth, D.default_data_size, D.unknown_duration, D.saturation);
 }
 
 }  // extern "C"
@@ -660,6 +666,7 @@ int upload_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const i
   rc |= dalloc(e, &D.ready, N, L);
   rc |= dalloc(e, &D.run_id, N, L);
   rc |= dalloc(e, &D.holder_of, N, L);
+  rc |= dalloc(e, &D.tdyn, N, L);
   rc |= dalloc(e, &D.fr_mark, N, L);
   rc |= dalloc(e, &D.rel_mark, N, L);
   D.rlog_cap = 2 * N + 4096;
@@ -801,6 +808,9 @@ int dgp_reset(dgp_engine* e) {
     namespace S = dgp::st;
     HIPCHK(e, hipMemsetAsync(D.run_id, 0xff, N * 4, s));
     HIPCHK(e, hipMemsetAsync(D.holder_of, 0xff, N * 4, s));
+    HIPCHK(e, hipMemsetAsync(D.tdyn, 0, N, s));
+    D.evf = 0;
+    e->paused_h.assign(D.W, 0);
     HIPCHK(e, hipMemsetAsync(D.fr_mark, 0xff, N * 4, s));
     HIPCHK(e, hipMemsetAsync(D.rel_mark, 0xff, N * 4, s));
     HIPCHK(e, hipMemsetAsync(D.thdr, 0, (size_t)S::DR * sizeof(uint2), s));
@@ -974,6 +984,7 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
                                 "has no worker addition");
   if (nthreads <= 0 || nthreads > 65535) return fail(e, DGP_E_ARG, "dgp_add_worker: nthreads out of range");
   if (e->D.W + 1 > 32768) return fail(e, DGP_E_ARG, "at most 32768 workers");
+  e->paused_h.push_back(0);
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   namespace S = dgp::st;
@@ -1069,6 +1080,8 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
   dgp::Dev& D = e->D;
   if (D.restr_flags) return fail(e, DGP_E_STATE, "dgp_add_graph: not with worker restrictions");
+  if (std::count(e->paused_h.begin(), e->paused_h.end(), 1))
+    return fail(e, DGP_E_STATE, "dgp_add_graph: not while a worker is paused");
   if (n_new <= 0 || !dep_ptr || !prio || !prefix_id || !prefix_default_duration || !group_id || !wanted ||
       !rootish_override)
     return fail(e, DGP_E_ARG, "dgp_add_graph: bad arguments");
@@ -1150,6 +1163,7 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   HIPCHK(e, carry(D.pl_route, old.pl_route, n0, n1, 0));
   HIPCHK(e, carry(D.run_id, old.run_id, n0 * 4, n1 * 4, 0xff));
   HIPCHK(e, carry(D.holder_of, old.holder_of, n0 * 4, n1 * 4, 0xff));
+  HIPCHK(e, carry(D.tdyn, old.tdyn, n0, n1, 0));
   HIPCHK(e, carry(D.fr_mark, old.fr_mark, n0 * 4, n1 * 4, 0xff));
   HIPCHK(e, carry(D.rel_mark, old.rel_mark, n0 * 4, n1 * 4, 0xff));
   HIPCHK(e, carry(D.rlog, old.rlog, (size_t)old_rlog * sizeof(dgp::st::SRec), (size_t)D.rlog_cap * sizeof(dgp::st::SRec), 0));
@@ -1197,6 +1211,186 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   if (n_new_placements) *n_new_placements = (int64_t)(c.n_placed - c0.n_placed);
   e->last_placed = c.n_placed;
   return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+// the common preconditions of a service event: the stream engine in service mode
+int event_ready(dgp_engine* e, const char* what) {
+  if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
+  if (!(e->D.P <= dgp::st::PD && !e->D.restr_flags))
+    return fail(e, DGP_E_STATE, std::string(what) + ": the round-kernel engine (more than 8 prefixes, or "
+                                                    "restrictions) has no service events");
+  HIPCHK(e, hipSetDevice(e->device));
+  e->mode = 2;
+  return 0;
+}
+
+// copy the event's argument arrays (each padded to 16 bytes) into the device staging
+int stage_args(dgp_engine* e, std::initializer_list<std::pair<const void*, size_t>> parts, std::vector<char*>& out) {
+  size_t need = 0;
+  for (auto& p : parts) need += (p.second + 15) & ~(size_t)15;
+  if (need > e->d_ev_cap) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->d_ev) (void)hipFree(e->d_ev);
+    e->d_ev = nullptr;
+    e->d_ev_cap = 0;
+    const size_t cap = std::max<size_t>(need, 4096);
+    HIPCHK(e, hipMalloc((void**)&e->d_ev, cap));
+    e->d_ev_cap = cap;
+  }
+  size_t off = 0;
+  out.clear();
+  for (auto& p : parts) {
+    out.push_back(e->d_ev + off);
+    if (p.second) HIPCHK(e, hipMemcpyAsync(e->d_ev + off, p.first, p.second, hipMemcpyHostToDevice, e->stream));
+    off += (p.second + 15) & ~(size_t)15;
+  }
+  return 0;
+}
+
+// a one-wave event kernel that may refill the queue: run it, report its placements
+template <class F>
+int event_with_refill(dgp_engine* e, F&& launch, int64_t* n_new_placements) {
+  if (int rc = sync_dev(e)) return rc;
+  launch();
+  HIPCHK(e, hipGetLastError());
+  long long placed = 0;
+  HIPCHK(e, hipMemcpyAsync(&placed, e->d_aux + 3, sizeof placed, hipMemcpyDeviceToHost, e->stream));
+  dgp::Ctl c;
+  if (int rc = check_device_error(e, &c)) return rc;  // synchronises the stream
+  if (n_new_placements) *n_new_placements = placed;
+  e->last_placed = c.n_placed;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dgp_add_replicas(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker) {
+  if (int rc = event_ready(e, "dgp_add_replicas")) return rc;
+  if (n < 0 || (n > 0 && (!task || !worker))) return fail(e, DGP_E_ARG, "dgp_add_replicas: bad batch");
+  for (int64_t i = 0; i < n; i++)
+    if (task[i] < 0 || task[i] >= e->D.N || worker[i] < 0 || worker[i] >= e->D.W)
+      return fail(e, DGP_E_ARG, "dgp_add_replicas: task or worker out of range");
+  if (n == 0) return 0;
+  std::vector<char*> a;
+  if (int rc = stage_args(e, {{task, n * 4}, {worker, n * 4}}, a)) return rc;
+  e->D.evf |= dgp::EVF_MULTI;
+  if (int rc = sync_dev(e)) return rc;
+  hipLaunchKernelGGL(dgp::ev::k_ev_add_replicas, dim3(1), dim3(64), 0, e->stream, e->d_dev, (const int32_t*)a[0],
+                     (const int32_t*)a[1], (int)n);
+  HIPCHK(e, hipGetLastError());
+  return check_device_error(e);
+}
+
+int dgp_remove_replicas(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker) {
+  if (int rc = event_ready(e, "dgp_remove_replicas")) return rc;
+  if (n < 0 || (n > 0 && (!task || !worker))) return fail(e, DGP_E_ARG, "dgp_remove_replicas: bad batch");
+  for (int64_t i = 0; i < n; i++)
+    if (task[i] < 0 || task[i] >= e->D.N || worker[i] < 0 || worker[i] >= e->D.W)
+      return fail(e, DGP_E_ARG, "dgp_remove_replicas: task or worker out of range");
+  if (n == 0) return 0;
+  std::vector<char*> a;
+  if (int rc = stage_args(e, {{task, n * 4}, {worker, n * 4}}, a)) return rc;
+  e->D.evf |= dgp::EVF_MULTI;
+  if (int rc = sync_dev(e)) return rc;
+  hipLaunchKernelGGL(dgp::ev::k_ev_remove_replicas, dim3(1), dim3(64), 0, e->stream, e->d_dev, (const int32_t*)a[0],
+                     (const int32_t*)a[1], (int)n);
+  HIPCHK(e, hipGetLastError());
+  return check_device_error(e);
+}
+
+int dgp_set_worker_status(dgp_engine* e, int32_t worker, int32_t running, int64_t* n_new_placements) {
+  if (n_new_placements) *n_new_placements = 0;
+  if (int rc = event_ready(e, "dgp_set_worker_status")) return rc;
+  if (worker < 0 || worker >= e->D.W) return fail(e, DGP_E_ARG, "dgp_set_worker_status: worker out of range");
+  const uint8_t paused = running ? 0 : 1;
+  if (e->paused_h[worker] == paused) return 0;  // ws.status == prev_status: nothing (:5858-5859)
+  e->paused_h[worker] = paused;
+  e->D.evf |= dgp::EVF_PAUSED;
+  return event_with_refill(e, [&] {
+    hipLaunchKernelGGL(dgp::ev::k_ev_worker_status, dim3(1), dim3(64), 0, e->stream, e->d_dev, worker,
+                       running ? 1 : 0, e->d_aux + 3);
+  }, n_new_placements);
+}
+
+int dgp_long_running(dgp_engine* e, int32_t task, double compute_duration, int64_t* n_new_placements) {
+  if (n_new_placements) *n_new_placements = 0;
+  if (int rc = event_ready(e, "dgp_long_running")) return rc;
+  if (task < 0 || task >= e->D.N) return fail(e, DGP_E_ARG, "dgp_long_running: task out of range");
+  e->D.evf |= dgp::EVF_LR;
+  return event_with_refill(e, [&] {
+    hipLaunchKernelGGL(dgp::ev::k_ev_long_running, dim3(1), dim3(64), 0, e->stream, e->d_dev, task,
+                       compute_duration, e->d_aux + 3);
+  }, n_new_placements);
+}
+
+int dgp_heartbeat(dgp_engine* e, double bandwidth, int64_t n, const int32_t* prefix, const double* duration) {
+  if (int rc = event_ready(e, "dgp_heartbeat")) return rc;
+  if (!(bandwidth > 0) || n < 0 || (n > 0 && (!prefix || !duration)))
+    return fail(e, DGP_E_ARG, "dgp_heartbeat: bandwidth must be > 0; prefixes and durations");
+  for (int64_t i = 0; i < n; i++)
+    if (prefix[i] < 0 || prefix[i] >= e->D.P) return fail(e, DGP_E_ARG, "dgp_heartbeat: prefix out of range");
+  e->D.bandwidth = bandwidth;
+  if (n > 0) {
+    std::vector<char*> a;
+    if (int rc = stage_args(e, {{prefix, n * 4}, {duration, n * 8}}, a)) return rc;
+    if (int rc = sync_dev(e)) return rc;
+    hipLaunchKernelGGL(dgp::ev::k_ev_heartbeat, dim3(1), dim3(64), 0, e->stream, e->d_dev, (const int32_t*)a[0],
+                       (const double*)a[1], (int)n);
+    HIPCHK(e, hipGetLastError());
+  }
+  if (int rc = sync_dev(e)) return rc;
+  return check_device_error(e);
+}
+
+int dgp_set_worker_flags(dgp_engine* e, int64_t n, const int32_t* worker, const uint8_t* idle, const uint8_t* saturated) {
+  if (int rc = event_ready(e, "dgp_set_worker_flags")) return rc;
+  if (n < 0 || (n > 0 && (!worker || !idle || !saturated))) return fail(e, DGP_E_ARG, "dgp_set_worker_flags: bad batch");
+  for (int64_t i = 0; i < n; i++) {
+    if (worker[i] < 0 || worker[i] >= e->D.W) return fail(e, DGP_E_ARG, "dgp_set_worker_flags: worker out of range");
+    if (e->paused_h[worker[i]] && (idle[i] || saturated[i]))
+      return fail(e, DGP_E_ARG, "dgp_set_worker_flags: a paused worker is neither idle nor saturated");
+  }
+  if (n == 0) return 0;
+  std::vector<char*> a;
+  if (int rc = stage_args(e, {{worker, n * 4}, {idle, (size_t)n}, {saturated, (size_t)n}}, a)) return rc;
+  if (int rc = sync_dev(e)) return rc;
+  hipLaunchKernelGGL(dgp::ev::k_ev_worker_flags, dim3(1), dim3(64), 0, e->stream, e->d_dev, (const int32_t*)a[0],
+                     (const uint8_t*)a[1], (const uint8_t*)a[2], (int)n);
+  HIPCHK(e, hipGetLastError());
+  return check_device_error(e);
+}
+
+int dgp_set_wanted(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t* wanted) {
+  if (int rc = event_ready(e, "dgp_set_wanted")) return rc;
+  if (n < 0 || (n > 0 && (!task || !wanted))) return fail(e, DGP_E_ARG, "dgp_set_wanted: bad batch");
+  for (int64_t i = 0; i < n; i++)
+    if (task[i] < 0 || task[i] >= e->D.N) return fail(e, DGP_E_ARG, "dgp_set_wanted: task out of range");
+  if (n == 0) return 0;
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  std::vector<uint8_t>& tf = e->tflags_h;
+  for (int64_t i = 0; i < n; i++) {
+    const int32_t t = task[i];
+    tf[t] = (uint8_t)((tf[t] & ~dgp::TF_WANTED) | (wanted[i] ? dgp::TF_WANTED : 0));
+    e->h_wanted[t] = wanted[i] ? 1 : 0;
+    HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(e->D.tflags) + t, &tf[t], 1, hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
+int dgp_task_erred(dgp_engine* e, int32_t task, int64_t* n_new_placements) {
+  if (n_new_placements) *n_new_placements = 0;
+  if (int rc = event_ready(e, "dgp_task_erred")) return rc;
+  if (task < 0 || task >= e->D.N) return fail(e, DGP_E_ARG, "dgp_task_erred: task out of range");
+  return event_with_refill(e, [&] {
+    hipLaunchKernelGGL(dgp::ev::k_ev_task_erred, dim3(1), dim3(64), 0, e->stream, e->d_dev, task, e->d_aux + 3);
+  }, n_new_placements);
 }
 
 int dgp_snapshot(dgp_engine* e) {

@@ -218,6 +218,61 @@ class PlacementEngine:
         self.n_tasks += n
         return int(newp.value)
 
+    # --------------------------------------------------------- service events
+    @staticmethod
+    def _arr(x, dt):
+        return np.ascontiguousarray(np.asarray(x, dtype=dt).reshape(-1))
+
+    def add_replicas(self, task, worker):
+        """SchedulerState.add_replica for each (task, worker) pair (distributed/scheduler.py
+        :3148-3153), e.g. from the add-keys stream handler (:7359-7391)."""
+        t, w = self._arr(task, np.int32), self._arr(worker, np.int32)
+        self._check(self.lib.dgp_add_replicas(self.h, len(t), _ptr(t), _ptr(w)), "dgp_add_replicas")
+
+    def remove_replicas(self, task, worker):
+        """SchedulerState.remove_replica for each pair (:3155-3159), release-worker-data."""
+        t, w = self._arr(task, np.int32), self._arr(worker, np.int32)
+        self._check(self.lib.dgp_remove_replicas(self.h, len(t), _ptr(t), _ptr(w)), "dgp_remove_replicas")
+
+    def set_worker_status(self, worker: int, running: int) -> int:
+        """handle_worker_status_change (:5850-5883); returns the placements of the refill."""
+        n = C.c_int64(0)
+        self._check(self.lib.dgp_set_worker_status(self.h, int(worker), int(running), C.byref(n)),
+                    "dgp_set_worker_status")
+        return int(n.value)
+
+    def long_running(self, task: int, compute_duration: float = math.nan) -> int:
+        """handle_long_running (:5817-5848); NaN = compute_duration None."""
+        n = C.c_int64(0)
+        self._check(self.lib.dgp_long_running(self.h, int(task), float(compute_duration), C.byref(n)),
+                    "dgp_long_running")
+        return int(n.value)
+
+    def heartbeat(self, bandwidth: float, prefixes=(), durations=()):
+        """heartbeat_worker's bandwidth EWMA result and add_exec_time per executing task's
+        prefix (:4223-4226, :4247-4252)."""
+        p, d = self._arr(prefixes, np.int32), self._arr(durations, np.float64)
+        if len(p) != len(d):
+            raise ValueError("heartbeat: one duration per prefix")
+        self._check(self.lib.dgp_heartbeat(self.h, float(bandwidth), len(p), _ptr(p), _ptr(d)), "dgp_heartbeat")
+
+    def set_worker_flags(self, workers, idle, saturated):
+        """idle / saturated membership of ``workers`` as the scheduler holds it."""
+        w, a, b = self._arr(workers, np.int32), self._arr(idle, np.uint8), self._arr(saturated, np.uint8)
+        self._check(self.lib.dgp_set_worker_flags(self.h, len(w), _ptr(w), _ptr(a), _ptr(b)), "dgp_set_worker_flags")
+
+    def set_wanted(self, task, wanted):
+        """who_wants non-empty (1) / empty (0) per task (client_desires_keys :5398-5415)."""
+        t, f = self._arr(task, np.int32), self._arr(wanted, np.uint8)
+        self._check(self.lib.dgp_set_wanted(self.h, len(t), _ptr(t), _ptr(f)), "dgp_set_wanted")
+
+    def task_erred(self, task: int) -> int:
+        """handle_task_erred (:5799-5805) of a current run with no retries left; returns the
+        placements of the refill."""
+        n = C.c_int64(0)
+        self._check(self.lib.dgp_task_erred(self.h, int(task), C.byref(n)), "dgp_task_erred")
+        return int(n.value)
+
     def snapshot(self):
         """Append one per-worker snapshot (service mode round boundary)."""
         self._check(self.lib.dgp_snapshot(self.h), "dgp_snapshot")

@@ -15,33 +15,39 @@ How it plugs in (the reference's interfaces, ``/root/reference/distributed/``):
   ``Scheduler.add_plugin`` (``scheduler.py:5940``) exactly like ``WorkStealing``
   (``stealing.py:108``): ``update_graph`` uploads the new runnable tasks (CSR dependencies,
   priorities, prefixes, groups, who_wants, ``_rootish``) and runs the engine's update_graph
-  stimulus; ``add_worker`` / ``remove_worker`` / ``restart`` keep the engine's worker table.
+  stimulus; ``add_worker`` / ``remove_worker`` / ``restart`` keep the engine's worker table;
+  ``transition`` is the catch-all described below.
 * the instance ``_TRANSITIONS_TABLE`` (the class table ``scheduler.py:2889-2913`` is read
   through ``self`` at ``:1955``): ``("waiting", "processing")`` and ``("queued",
   "processing")`` take the worker the engine chose instead of calling
   ``decide_worker_rootish_queuing_enabled / _disabled`` / ``decide_worker_non_rootish``
   (``:2135-2311``); everything after the decision is the reference's own code
   (``_add_to_processing`` :3199, ``_task_to_msg`` :3421).
-* ``stream_handlers["steal-response"]`` (``stealing.py:121``): the stealing extension's
-  ``move_task_confirm`` (``:333-399``) runs as before; when it moved a processing task to
-  the thief (the "confirm" branch ``:376-384``) the engine moves it too (``dgp_move_task``),
-  so the device state follows confirmed steals.
-* ``stream_handlers["task-finished"]`` (``:3769``): each message goes to the engine first
-  (``dgp_tasks_finished``: stale / duplicate checks, completion, frontier release,
-  frontier placement and queue refill on the device), then to the reference
+* ``stream_handlers["task-finished"]`` (``:3769``): each batch of messages goes to the
+  engine first (``dgp_tasks_finished``: stale / duplicate checks, completion, frontier
+  release, frontier placement and queue refill on the device), then to the reference
   ``Scheduler.handle_task_finished`` (``:5783-5797``), whose transitions consume the
   engine's decisions in order.
+* every other stimulus that changes a placement input (``scheduler.py:3768-3792`` worker
+  and client stream handlers, the ``heartbeat_worker`` RPC ``:4197-4252``,
+  ``set_restrictions`` ``:7702``, ``SchedulerState.add_replica`` / ``remove_replica``
+  ``:3148-3159`` from any caller, the stealing extension's ``balance`` and
+  ``move_task_confirm`` ``stealing.py:333-503``) is followed on the device when the engine
+  models it (``_ENGINE_EVENTS``) and otherwise ends GPU placement for the session, loudly.
 
-The engine replays the scheduler's own stimulus sequence, so its placements come out in
-the order the Python transitions ask for them. Every decision is checked against that
-order: a task the engine did not place, or placed in another order, means the two have
-diverged (a transition the engine does not model: worker loss, rescheduling, recompute,
-restrictions). The extension then logs it, stops asking the engine and the scheduler
-continues on its own Python decisions (``fallback``); ``validate=True`` also computes the
-reference decision for every placement and raises on any difference (tests).
+Nothing diverges silently. The engine replays the scheduler's own stimulus sequence, so its
+placements come out in the order the Python transitions ask for them, and every decision is
+checked against that order; a transition the engine does not model (worker loss, erred
+tasks, rescheduling, recompute, client releases, ...) is caught by the plugin
+``transition`` hook; a queued task the engine left queued while the scheduler has an open
+slot is a divergence too. The extension then logs it (``fallback``), stops asking the
+engine and the scheduler continues on its own Python decisions. ``validate=True`` also
+computes the reference decision for every placement and raises on any difference (tests).
 """
 from __future__ import annotations
 
+import functools
+import inspect
 import logging
 import math
 from collections import Counter, deque
@@ -56,6 +62,29 @@ except Exception:  # pragma: no cover - the GPU box has no dask
 logger = logging.getLogger("distributed_amd.ext")
 
 _REF = object()  # "no engine decision: run the reference's own transition"
+
+# transitions the engine runs itself inside a stimulus it follows (task-finished:
+# processing -> memory, the releases of dependencies, the frontier and the queue refill;
+# update_graph: released -> waiting -> processing / queued / no-worker)
+_STIMULUS_TRANSITIONS = frozenset({
+    ("processing", "memory"), ("memory", "released"), ("released", "waiting"), ("waiting", "processing"),
+    ("waiting", "queued"), ("waiting", "no-worker"), ("queued", "processing")})
+_UPDATE_GRAPH_TRANSITIONS = frozenset({
+    ("released", "waiting"), ("waiting", "processing"), ("waiting", "queued"), ("waiting", "no-worker")})
+_ADD_WORKER_TRANSITIONS = frozenset({("queued", "processing")})
+# stimulus_queue_slots_maybe_opened after long-running / a worker running again (:4983-5023)
+_REFILL_TRANSITIONS = _ADD_WORKER_TRANSITIONS
+# task-erred (:5094-5127, :2630-2720): the task erred, its waiting dependents released then
+# erred (the _transition fallback through "released", :1960-1980), dependencies nobody
+# waits for released, then the queue refill
+_ERRED_TRANSITIONS = frozenset({("processing", "erred"), ("waiting", "released"), ("released", "erred"),
+                                ("memory", "released"), ("queued", "processing")})
+
+# the placement inputs a stimulus other than task-finished / update_graph / add_worker can
+# change, and the engine method that follows each on the device (PlacementEngine); an engine
+# without the method (or one that raises) hands placement back to the scheduler
+_ENGINE_EVENTS = ("add_replicas", "remove_replicas", "set_worker_status", "long_running", "heartbeat",
+                  "set_worker_flags", "set_wanted", "task_erred")
 
 
 def _compute_interval(startstops):
@@ -159,10 +188,14 @@ class GPUPlacementExtension(SchedulerPlugin):
         self.task_index: dict = {}
         self.workers: list = []   # engine worker index -> address
         self.worker_index: dict = {}
+        self.prefix_index: dict = {}
         self.dev_run: dict = {}   # key -> placement-log position of its current placement
         self.pending: deque = deque()  # (task index, worker index) in placement order
         self.n_fetched = 0
         self.stats = Counter()
+        self._allowed: list = []  # per running wrapped stimulus: the transitions the engine follows
+        self._window = None       # (allowed transitions, keys or None) after a plugin hook's stimulus
+        self._expect_replicas: set = set()  # (key, address) replicas the running stimulus adds itself
         if hasattr(scheduler, "add_plugin"):
             scheduler.add_plugin(self, name=self.name)
         self._install()
@@ -186,11 +219,156 @@ class GPUPlacementExtension(SchedulerPlugin):
         handlers = getattr(s, "stream_handlers", None)
         if handlers is not None:
             handlers["task-finished"] = self.handle_task_finished
+            # worker stream handlers (scheduler.py:3768-3779); the transitions each may run
+            # that the engine follows itself (anything else ends GPU placement)
+            self._wrap(handlers, "add-keys", self._on_add_keys, ())
+            self._wrap(handlers, "release-worker-data", None, ())
+            self._wrap(handlers, "long-running", self._on_long_running, _REFILL_TRANSITIONS)
+            self._wrap(handlers, "worker-status-change", self._on_worker_status_change, _REFILL_TRANSITIONS)
+            self._wrap(handlers, "task-erred", self._on_task_erred, _ERRED_TRANSITIONS)
+            self._wrap(handlers, "reschedule", None, ())
+            # client stream handlers (:3781-3792)
+            self._wrap(handlers, "client-desires-keys", self._on_client_desires_keys, ())
+            self._wrap(handlers, "client-releases-keys", self._on_client_releases_keys, ())
+            self._wrap(handlers, "cancel-keys", self._on_client_releases_keys, ())
+            self._wrap(handlers, "close-client", self._on_close_client, ())
+            self._wrap(handlers, "update-data", self._on_update_data, ())
+        rpc = getattr(s, "handlers", None)
+        if isinstance(rpc, dict):
+            self._wrap(rpc, "heartbeat_worker", self._on_heartbeat, (), after=True)
+            self._wrap(rpc, "set_restrictions", self._on_set_restrictions, ())
+        self._wrap_replicas()
         self._wrap_stealing()
 
+    def _wrap(self, table, name, on_event, modelled, after=False):
+        """Route stream / RPC handler ``name`` through the extension: ``on_event(kwargs)``
+        (before the handler; with ``after`` it gets a callable that runs the handler)
+        brings the engine up to date or falls back; the handler itself then runs with
+        ``modelled`` as the transitions the engine follows for it (the plugin hook)."""
+        orig = table.get(name)
+        if orig is None or getattr(orig, "_gpu_placement", False):
+            return
+        modelled = frozenset(modelled)
+
+        def enter(kwargs):
+            self._close_window()
+            if on_event is not None and self.active and self.engine is not None:
+                try:
+                    on_event(kwargs)
+                except Exception as e:  # an engine failure ends GPU placement, never the scheduler
+                    self.fallback(f"{name}: {e}")
+            self._allowed.append(modelled)
+
+        def leave():
+            self._allowed.pop()
+            self._end_of_stimulus(name)
+
+        if inspect.iscoroutinefunction(orig):
+            @functools.wraps(orig)
+            async def wrapped(*args, **kwargs):
+                enter(kwargs)
+                try:
+                    return await orig(*args, **kwargs)
+                finally:
+                    leave()
+        elif after:
+            @functools.wraps(orig)
+            def wrapped(*args, **kwargs):
+                self._close_window()
+                box = {}
+
+                def run():
+                    self._allowed.append(modelled)
+                    try:
+                        box["r"] = orig(*args, **kwargs)
+                    finally:
+                        self._allowed.pop()
+                    return box["r"]
+
+                if on_event is not None and self.active and self.engine is not None:
+                    try:
+                        on_event(kwargs, run)
+                    except Exception as e:
+                        self.fallback(f"{name}: {e}")
+                r = box["r"] if "r" in box else run()
+                self._end_of_stimulus(name)
+                return r
+        else:
+            @functools.wraps(orig)
+            def wrapped(*args, **kwargs):
+                enter(kwargs)
+                try:
+                    return orig(*args, **kwargs)
+                finally:
+                    leave()
+        wrapped._gpu_placement = True
+        table[name] = wrapped
+
+    def _wrap_replicas(self):
+        """``SchedulerState.add_replica`` / ``remove_replica`` (scheduler.py:3148-3159) from
+        any caller (add-keys :7375, a task-finished for a task already in memory :5082,
+        release-worker-data :5813, update_data :7416, rebalance / replicate :6454, :6493):
+        who_has and ws.nbytes are inputs of decide_worker / worker_objective
+        (:8571-8593, :3131-3146). The completing task's own replica (_add_to_memory :3296)
+        is part of the task-finished stimulus the engine runs."""
+        s = self.scheduler
+        if getattr(s, "_gpu_placement_replicas", False):
+            return
+        add0, rem0 = s.add_replica, s.remove_replica
+
+        def add_replica(ts, ws):
+            k = (ts.key, ws.address)
+            if k in self._expect_replicas:
+                self._expect_replicas.discard(k)
+            elif ws not in (ts.who_has or ()):
+                self._replica_event(ts, ws, +1)
+            return add0(ts, ws)
+
+        def remove_replica(ts, ws):
+            if ws in (ts.who_has or ()):
+                self._replica_event(ts, ws, -1)
+            return rem0(ts, ws)
+
+        s.add_replica = add_replica
+        s.remove_replica = remove_replica
+        s._gpu_placement_replicas = True
+
+    def _replica_event(self, ts, ws, sign):
+        if not self.active or self.engine is None or ts.key not in self.task_index:
+            return
+        w = self.worker_index.get(ws.address)
+        what = "add_replicas" if sign > 0 else "remove_replicas"
+        if w is None:
+            self.fallback(f"{what}({ts.key!r}, {ws.address}): worker not in the engine's table")
+            return
+        self._engine_op(what, [self.task_index[ts.key]], [w])
+
+    def _engine_op(self, what, *args):
+        """Follow one placement-input change on the device; an engine without that
+        operation (or one that fails) hands placement back to the scheduler."""
+        fn = getattr(self.engine, what, None)
+        if fn is None:
+            self.fallback(f"{what}: not modelled by the engine")
+            return None
+        self._end_of_stimulus("the previous stimulus")
+        if not self.active:
+            return None
+        try:
+            r = fn(*args)
+        except Exception as e:
+            self.fallback(f"{what}: {e}")
+            return None
+        self.stats[what] += 1
+        self._fetch()  # a refill the operation made (resume, long-running)
+        return r
+
     def _wrap_stealing(self):
-        """Follow confirmed steals: wrap the stealing extension's ``move_task_confirm``
-        (stealing.py:333-399), which is also its ``steal-response`` stream handler (:121)."""
+        """Follow the stealing extension (stealing.py). ``move_task_confirm`` (:333-399, also
+        its ``steal-response`` stream handler :121): a confirmed steal moves the task on the
+        engine (``dgp_move_task``); the finally clause's check_idle_saturated of thief and
+        victim (:396-399) and ``balance``'s check_idle_saturated(victim, occ=combined
+        occupancy) (:494-496) change idle / saturated membership outside any placement,
+        which the engine takes over (``set_worker_flags``)."""
         s = self.scheduler
         st = (getattr(s, "extensions", None) or {}).get("stealing")
         if st is None or getattr(st, "_gpu_placement_wrapped", False):
@@ -200,20 +378,61 @@ class GPUPlacementExtension(SchedulerPlugin):
         async def move_task_confirm(*, key, state, stimulus_id, worker=None):
             ts = s.tasks.get(key)
             before = ts.processing_on if ts is not None and ts.state == "processing" else None
+            flags0 = self._flags_of(s)
             try:
                 await orig(key=key, state=state, stimulus_id=stimulus_id, worker=worker)
             finally:
                 ts = s.tasks.get(key)
+                moved = False
                 if before is not None and ts is not None:
                     if ts.state == "processing" and ts.processing_on is not None and ts.processing_on is not before:
                         self.task_moved(ts, ts.processing_on)
+                        moved = True
                     elif ts.state != "processing":  # "reschedule" (:365-376): not modelled on the device
                         self.fallback(f"steal of {key!r} rescheduled it")
+                if not moved:  # the reject branches re-check thief and victim (:396-399)
+                    self._sync_flags(flags0)
 
         st.move_task_confirm = move_task_confirm
         if getattr(s, "stream_handlers", None) is not None and "steal-response" in s.stream_handlers:
             s.stream_handlers["steal-response"] = move_task_confirm
+        bal = getattr(st, "balance", None)
+        if bal is not None:
+            @functools.wraps(bal)
+            def balance(*args, **kwargs):
+                flags0 = self._flags_of(s)
+                try:
+                    return bal(*args, **kwargs)
+                finally:
+                    self._sync_flags(flags0)
+
+            st.balance = balance
+            pcs = getattr(s, "periodic_callbacks", None) or {}
+            pc = pcs.get("stealing")
+            if pc is not None and getattr(pc, "callback", None) is bal:
+                pc.callback = balance
         st._gpu_placement_wrapped = True
+
+    @staticmethod
+    def _flags_of(s):
+        return set(getattr(s, "idle", {}) or {}), {ws.address for ws in (getattr(s, "saturated", ()) or ())}
+
+    def _sync_flags(self, before):
+        """Idle / saturated membership the scheduler changed outside a placement: the
+        engine's worker flags take the scheduler's (``set_worker_flags``)."""
+        if not self.active or self.engine is None:
+            return
+        s = self.scheduler
+        idle1, sat1 = self._flags_of(s)
+        idle0, sat0 = before
+        changed = sorted((idle0 ^ idle1) | (sat0 ^ sat1))
+        if not changed:
+            return
+        if any(a not in self.worker_index for a in changed):
+            self.fallback("idle / saturated change of a worker not in the engine's table")
+            return
+        self._engine_op("set_worker_flags", [self.worker_index[a] for a in changed],
+                        [1 if a in idle1 else 0 for a in changed], [1 if a in sat1 else 0 for a in changed])
 
     def task_moved(self, ts, thief):
         """A confirmed steal moved processing ``ts`` to ``thief`` (a WorkerState)."""
@@ -263,6 +482,9 @@ class GPUPlacementExtension(SchedulerPlugin):
             self.fallback(f"{what}: the engine placed {self.keys[t]!r} on {self.workers[w]} but the scheduler "
                           "did not ask for it")
 
+    def _close_window(self):
+        self._window = None
+
     # ------------------------------------------------------- placement decisions
     def _decision(self, sched, ts, queued: bool):
         """The engine's worker for ``ts`` (a WorkerState), None (the engine did not place
@@ -280,10 +502,14 @@ class GPUPlacementExtension(SchedulerPlugin):
         if any(p[0] == t for p in self.pending):
             self.fallback(f"placement order differs at {ts.key!r}")
             return _REF
-        # not placed by the engine: only a root-ish task under queuing may stay / go queued
-        # (decide_worker_rootish_queuing_enabled found no slot, :2230-2245); anything else
-        # is a transition the engine did not run
+        # not placed by the engine: only a root-ish task under queuing may stay / go queued,
+        # and only when decide_worker_rootish_queuing_enabled finds no slot, i.e.
+        # idle_task_count is empty (:2227-2229); anything else is a stimulus the engine did
+        # not run (a refill after a change it never saw)
         if queued or (not math.isinf(sched.WORKER_SATURATION) and sched.is_rootish(ts)):
+            if sched.idle_task_count:
+                self.fallback(f"the scheduler has an open slot for queued {ts.key!r} but the engine left it queued")
+                return _REF
             self.stats["device_queued"] += 1
             return None
         # restrictions that no worker satisfies, not loose: the engine left it in
@@ -337,10 +563,29 @@ class GPUPlacementExtension(SchedulerPlugin):
         return sched._add_to_processing(ts, ws, stimulus_id=stimulus_id)
 
     # ----------------------------------------------------------- plugin hooks
+    def transition(self, key, start, finish, *args, stimulus_id=None, **kwargs):
+        """SchedulerPlugin.transition (diagnostics/plugin.py:111-139), called after every
+        transition (scheduler.py:2013-2027): the catch-all. A transition outside the
+        stimuli the engine follows, or of a kind it does not model, means the scheduler's
+        state moved where the engine's did not."""
+        if not self.active or self.engine is None:
+            return
+        pair = (start, finish)
+        if self._allowed and pair in self._allowed[-1]:
+            return
+        w = self._window
+        if w is not None and pair in w[0] and (w[1] is None or key in w[1]):
+            return
+        if key not in self.task_index:
+            return  # a task the engine does not hold (scattered data, a graph it did not take)
+        self.fallback(f"transition {start} -> {finish} of {key!r} (stimulus {stimulus_id}) is not modelled "
+                      "by the engine")
+
     def update_graph(self, scheduler, *, client=None, keys=(), tasks=(), annotations=None, priority=None,
                      dependencies=None, **kwargs):
         """SchedulerPlugin.update_graph (diagnostics/plugin.py:74-109): runs before the
         scheduler transitions the new tasks (scheduler.py:4641-4653)."""
+        self._close_window()
         if not self.active:
             return
         s = self.scheduler
@@ -350,28 +595,32 @@ class GPUPlacementExtension(SchedulerPlugin):
         try:
             if self.engine is not None:
                 self._add_graph(new)
-                return
-            self.workers = list(s.workers)
-            self.worker_index = {a: i for i, a in enumerate(self.workers)}
-            g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers], s.valid_workers,
-                                        self.worker_index)
-            self.keys = keys_
-            self.task_index = {k: i for i, k in enumerate(keys_)}
-            self.prefix_index = {nm: i for i, nm in enumerate(g["prefix_names"])}
-            self.group_index = {nm: i for i, nm in enumerate(g["group_names"])}
-            self.prefix_dur = list(g["prefix_default_dur"])
-            self.group_prefix = list(g["group_prefix"])
-            self.max_priority = max(ts.priority for ts in new)
-            if self.engine_factory is not None:
-                self.engine = self.engine_factory()
             else:
-                from .engine import PlacementEngine
+                self.workers = list(s.workers)
+                self.worker_index = {a: i for i, a in enumerate(self.workers)}
+                if any(ws.status.name != "running" for ws in s.workers.values()):
+                    raise NotImplementedError("a worker is not running at the first graph")
+                g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers], s.valid_workers,
+                                            self.worker_index)
+                self.keys = keys_
+                self.task_index = {k: i for i, k in enumerate(keys_)}
+                self.prefix_index = {nm: i for i, nm in enumerate(g["prefix_names"])}
+                self.group_index = {nm: i for i, nm in enumerate(g["group_names"])}
+                self.prefix_dur = list(g["prefix_default_dur"])
+                self.group_prefix = list(g["group_prefix"])
+                self.max_priority = max(ts.priority for ts in new)
+                if self.engine_factory is not None:
+                    self.engine = self.engine_factory()
+                else:
+                    from .engine import PlacementEngine
 
-                self.engine = PlacementEngine(self.device)
-            self.engine.load(g, self._config(), results=False)
-            self.engine.update_graph()
-            self._fetch()
-            self.stats["graphs"] += 1
+                    self.engine = PlacementEngine(self.device)
+                self.engine.load(g, self._config(), results=False)
+                self.engine.update_graph()
+                self._fetch()
+                self.stats["graphs"] += 1
+            if self.active:
+                self._window = (_UPDATE_GRAPH_TRANSITIONS, {ts.key for ts in new})
         except Exception as e:  # plugin errors are logged, not raised (scheduler.py:4652-4653)
             self.fallback(f"update_graph: {e}")
 
@@ -421,6 +670,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         and makes the queue refill; the scheduler's own refill then consumes those decisions.
         The engine's worker index order must stay the scheduler's (SortedDict address) order,
         so only a worker whose address sorts after every known one joins on the device."""
+        self._close_window()
         if not self.active or self.engine is None or worker in self.worker_index:
             return
         if self.workers and worker < max(self.workers):
@@ -431,15 +681,19 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._end_of_stimulus("the previous stimulus")
             if not self.active:
                 return
+            if s.workers[worker].status.name != "running":
+                raise NotImplementedError("a worker that joins paused")
             self.engine.add_worker(int(s.workers[worker].nthreads))
             self.worker_index[worker] = len(self.workers)
             self.workers.append(worker)
             self._fetch()
             self.stats["workers_added"] += 1
+            self._window = (_ADD_WORKER_TRANSITIONS, None)
         except Exception as e:
             self.fallback(f"add_worker({worker}): {e}")
 
     def remove_worker(self, scheduler=None, worker=None, **kwargs):
+        self._close_window()
         if self.engine is not None and worker in self.worker_index:
             self.fallback(f"remove_worker({worker})")
 
@@ -455,9 +709,119 @@ class GPUPlacementExtension(SchedulerPlugin):
         self.keys, self.task_index, self.dev_run = [], {}, {}
         self.pending.clear()
         self.n_fetched = 0
+        self._window = None
 
     async def close(self):
         self.close_engine()
+
+    # -------------------------------------------- other placement-input stimuli
+    def _on_add_keys(self, kw):
+        """add-keys (Scheduler.add_keys :7359-7391): new replicas of in-memory tasks reach
+        the engine through the add_replica wrapper; nothing else changes."""
+
+    def _on_long_running(self, kw):
+        """long-running (Scheduler.handle_long_running :5817-5848): the task's prefix
+        duration average takes the reported compute duration, the task leaves its worker's
+        prefix counts (add_to_long_running :747-757) and frees a slot, then
+        check_idle_saturated and the queue refill."""
+        s = self.scheduler
+        ts = s.tasks.get(kw.get("key"))
+        if ts is None or ts.processing_on is None or ts.key not in self.task_index:
+            return
+        if ts in ts.processing_on.long_running:
+            return
+        cd = kw.get("compute_duration")
+        self._engine_op("long_running", self.task_index[ts.key], math.nan if cd is None else float(cd))
+
+    def _on_worker_status_change(self, kw):
+        """worker-status-change (Scheduler.handle_worker_status_change :5850-5883): a paused
+        (or closing) worker leaves ``running``, idle, idle_task_count and saturated; one
+        running again is checked (check_idle_saturated) and the queue refilled."""
+        s = self.scheduler
+        w = kw.get("worker")
+        ws = s.workers.get(w) if isinstance(w, str) else w
+        if ws is None:
+            return
+        st = kw.get("status")
+        name = st if isinstance(st, str) else getattr(st, "name", str(st))
+        if name == ws.status.name:
+            return
+        wi = self.worker_index.get(ws.address)
+        if wi is None:
+            self.fallback(f"worker-status-change of {ws.address}: not in the engine's table")
+            return
+        self._engine_op("set_worker_status", wi, 1 if name == "running" else 0)
+        if self.active and name == "running":
+            self._window = (_ADD_WORKER_TRANSITIONS, None)
+
+    def _on_task_erred(self, kw):
+        """task-erred (Scheduler.handle_task_erred :5799-5805 -> stimulus_task_erred
+        :5094-5127): a current run that erred with no retries left leaves its worker
+        (_exit_processing_common :3258), its waiting dependents err transitively, the
+        dependencies nobody waits for any more are released, then the queue refill. A stale
+        run, or one with retries left, reschedules: not modelled."""
+        s = self.scheduler
+        ts = s.tasks.get(kw.get("key"))
+        if ts is None or ts.state != "processing" or ts.key not in self.task_index:
+            return
+        if ts.run_id != kw.get("run_id") or ts.retries > 0:
+            self.fallback(f"task-erred of {ts.key!r} reschedules it (stale run or retries left)")
+            return
+        self._engine_op("task_erred", self.task_index[ts.key])
+
+    def _on_client_desires_keys(self, kw):
+        """client-desires-keys (:5398-5415): who_wants decides whether a finished task is
+        released (_add_to_memory :3316, _transition_memory_released)."""
+        s = self.scheduler
+        t = [self.task_index[k] for k in kw.get("keys") or () if k in self.task_index
+             and not (s.tasks.get(k) is not None and s.tasks[k].who_wants)]
+        if t:
+            self._engine_op("set_wanted", t, [1] * len(t))
+
+    def _on_client_releases_keys(self, kw):
+        """client-releases-keys / cancel-keys (:5417-5430, :5364-5396): tasks no longer
+        wanted are released or forgotten (transitions the engine does not run)."""
+        if any(k in self.task_index for k in kw.get("keys") or ()):
+            self.fallback("client-releases-keys / cancel-keys of tasks in the engine's graph")
+
+    def _on_close_client(self, kw):
+        if self.task_index:
+            self.fallback("close-client releases the client's keys (remove_client :5727)")
+
+    def _on_update_data(self, kw):
+        """update-data (:7394-7425): scattered data; a key of the engine's graph would be
+        set to memory without a transition."""
+        if any(k in self.task_index for k in (kw.get("who_has") or {})):
+            self.fallback("update-data of a task in the engine's graph")
+
+    def _on_set_restrictions(self, kw):
+        if any(k in self.task_index for k in (kw.get("worker") or {})):
+            self.fallback("set_restrictions on a task in the engine's graph")
+
+    def _on_heartbeat(self, kw, run):
+        """heartbeat_worker (:4197-4252): the bandwidth EWMA (:4223-4226) and
+        TaskPrefix.add_exec_time for the executing tasks (:4247-4252, :972-975) feed
+        _calc_occupancy (:1884-1903) and worker_objective (:3131-3146)."""
+        s = self.scheduler
+        bw0 = s.bandwidth
+        pref = {}
+        for key in (kw.get("executing") or {}):
+            ts = s.tasks.get(key)
+            if ts is not None and ts.prefix.name in self.prefix_index:
+                pref[ts.prefix.name] = ts.prefix
+        before = {nm: (p.duration_average, p.max_exec_time) for nm, p in pref.items()}
+        run()
+        after = {nm: (p.duration_average, p.max_exec_time) for nm, p in pref.items()}
+        if s.bandwidth == bw0 and before == after:
+            return
+        # each executing task's prefix in message order (add_exec_time is order-sensitive)
+        ps, ds = [], []
+        for key, dur in (kw.get("executing") or {}).items():
+            ts = s.tasks.get(key)
+            if ts is not None and ts.prefix.name in self.prefix_index:
+                ps.append(self.prefix_index[ts.prefix.name])
+                ds.append(float(dur))
+        self._engine_op("heartbeat", float(s.bandwidth), ps, ds)
 
     # ------------------------------------------------------- task-finished
     def _message_fields(self, key, worker, msg):
@@ -481,6 +845,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         then the reference handler for each, consuming the engine's decisions in order."""
         s = self.scheduler
         handler = type(s).handle_task_finished
+        self._close_window()
         self._end_of_stimulus("the previous stimulus")
         if self.active and self.engine is not None and msgs:
             fields = [self._message_fields(m["key"], m["worker"], m) for m in msgs]
@@ -494,9 +859,17 @@ class GPUPlacementExtension(SchedulerPlugin):
                 # raises; the engine does not follow those transitions
                 if np.any(status >= 3) and np.any((status != 4) & (status >= 3)):
                     self.fallback(f"task-finished answers {sorted(set(status.tolist()))} the engine does not run")
+                for m, st in zip(msgs, status.tolist()):
+                    if st == 0:  # accepted: _add_to_memory adds this replica itself (:3296)
+                        self._expect_replicas.add((m["key"], m["worker"]))
             except Exception as e:
                 self.fallback(f"tasks_finished: {e}")
-        for m in msgs:
-            m = dict(m)
-            handler(s, m.pop("key"), m.pop("worker"), m.pop("stimulus_id"), **m)
+        self._allowed.append(_STIMULUS_TRANSITIONS)
+        try:
+            for m in msgs:
+                m = dict(m)
+                handler(s, m.pop("key"), m.pop("worker"), m.pop("stimulus_id"), **m)
+        finally:
+            self._allowed.pop()
+            self._expect_replicas.clear()
         self._end_of_stimulus("task-finished")

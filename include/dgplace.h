@@ -29,6 +29,20 @@
  *   dgp_add_graph         a later Scheduler.update_graph on a running engine (scheduler.py:4662-4751,
  *                         _create_taskstate_from_graph :4512-4653): new tasks, then their
  *                         update_graph stimulus
+ *   dgp_add_replicas      SchedulerState.add_replica (scheduler.py:3148-3153), e.g. from the
+ *                         add-keys stream handler (Scheduler.add_keys :7359-7391)
+ *   dgp_remove_replicas   SchedulerState.remove_replica (:3155-3159), e.g. from
+ *                         release-worker-data (:5807-5815)
+ *   dgp_set_worker_status Scheduler.handle_worker_status_change (:5850-5883)
+ *   dgp_long_running      Scheduler.handle_long_running (:5817-5848)
+ *   dgp_heartbeat         the placement inputs of Scheduler.heartbeat_worker: the bandwidth
+ *                         EWMA (:4223-4226) and TaskPrefix.add_exec_time (:4247-4252, :972-975)
+ *   dgp_set_worker_flags  idle / saturated membership set outside a placement (the stealing
+ *                         extension's check_idle_saturated calls, stealing.py:396-399, :494-496)
+ *   dgp_set_wanted        who_wants gaining / losing its last client (client_desires_keys
+ *                         :5398-5415)
+ *   dgp_task_erred        Scheduler.handle_task_erred (:5799-5805 -> stimulus_task_erred
+ *                         :5094-5127)
  *   dgp_snapshot          one per-worker snapshot (occupancy, nbytes, processing, idle /
  *                         saturated / idle_task_count, queue length) at a caller-chosen point
  *   dgp_run_rounds        the synthetic executor of the replay protocol: round k completes
@@ -48,7 +62,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 7
+#define DGP_ABI_VERSION 8
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -69,6 +83,7 @@ extern "C" {
 #define DGP_QUEUED 3
 #define DGP_NO_WORKER 4
 #define DGP_MEMORY 5
+#define DGP_ERRED 6
 
 typedef struct dgp_engine dgp_engine;
 
@@ -178,6 +193,57 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
                   const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
                   const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override,
                   int64_t* n_new_placements);
+
+/* ---- Service events: the other placement-input stimuli of a live scheduler, in the order the
+ * scheduler handles them, between dgp_tasks_finished calls. Stream-engine graphs (<= 8 prefixes,
+ * no restrictions); DGP_E_STATE otherwise. A case the engine does not model returns
+ * DGP_E_DEVICE ("a service event the engine does not model") and the caller hands placement
+ * back to the scheduler. Those returning n_new_placements may refill the queue
+ * (stimulus_queue_slots_maybe_opened :4983-5023): read the placements with dgp_get_placements. */
+
+/* SchedulerState.add_replica(task, worker) for each pair, in order (WorkerState.add_replica
+ * :825-838: the worker's needs_what entry goes, ws.nbytes grows, who_has gains the worker:
+ * decide_worker's candidates and worker_objective's comm bytes / tie-break follow). The task
+ * must be in memory; a worker already holding it is a no-op. A worker whose needs_what is in
+ * scan mode (> 63 entries) is not modelled. */
+int dgp_add_replicas(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker);
+
+/* SchedulerState.remove_replica(task, worker) for each pair (WorkerState.remove_replica
+ * :786-798). The last replica of a task (release-worker-data then releases it to recompute,
+ * :5813-5815) is not modelled. */
+int dgp_remove_replicas(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker);
+
+/* Scheduler.handle_worker_status_change: running = 0 pauses the worker (it leaves running,
+ * idle, idle_task_count and saturated: never a decide_worker candidate, its completions are
+ * still accepted); running = 1 runs it again (check_idle_saturated, then the queue refill). */
+int dgp_set_worker_status(dgp_engine* e, int32_t worker, int32_t running, int64_t* n_new_placements);
+
+/* Scheduler.handle_long_running(task, compute_duration): the task's prefix duration average
+ * takes compute_duration (NaN: None), WorkerState.add_to_long_running (:747-757: the prefix
+ * counts, and _task_slots_available's slot :8765-8767), check_idle_saturated, the refill. */
+int dgp_long_running(dgp_engine* e, int32_t task, double compute_duration, int64_t* n_new_placements);
+
+/* Scheduler.heartbeat_worker's placement inputs: SchedulerState.bandwidth after the EWMA (a
+ * float from now on: comm and network terms divide by it) and TaskPrefix.add_exec_time for
+ * each executing task's prefix, in message order (max_exec_time; a duration above twice the
+ * duration average resets it to -1, so _calc_occupancy uses 2 max_exec_time). */
+int dgp_heartbeat(dgp_engine* e, double bandwidth, int64_t n, const int32_t* prefix, const double* duration);
+
+/* idle / saturated membership of the given workers as the scheduler holds it (a paused worker
+ * is neither). */
+int dgp_set_worker_flags(dgp_engine* e, int64_t n, const int32_t* worker, const uint8_t* idle,
+                         const uint8_t* saturated);
+
+/* who_wants of each task non-empty (1) or empty (0): a wanted task is not released when its
+ * last dependent completes (_add_to_memory :3309-3316). */
+int dgp_set_wanted(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t* wanted);
+
+/* Scheduler.handle_task_erred for a current run with no retries left: the task errs, the tasks
+ * waiting on it (and theirs, transitively) err, dependencies nobody waits for and no client
+ * wants are released, the worker leaves processing (check_idle_saturated), the queue refill.
+ * A cascade that would release a task not in memory (cancel processing or waiting work) is
+ * not modelled (nothing changes). */
+int dgp_task_erred(dgp_engine* e, int32_t task, int64_t* n_new_placements);
 
 /* Append one worker snapshot (needs dgp_enable_snapshots): round index = number of calls
  * (update_graph's snapshot is round 0). */

@@ -17,7 +17,7 @@ def pytest_configure(config):
 def golden_files():
     """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
-                  and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_")))
+                  and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcev_")))
 
 
 def svc_second_graph_files():
@@ -49,6 +49,11 @@ def second_graph(g, z, with_results=False):
 def svc_add_worker_files():
     """Service-mode message streams with workers joining (tests/golden/gen_service.py add-workers)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcaddw_") and f.endswith(".npz"))
+
+
+def svc_event_files():
+    """Service-mode streams with the other worker stimuli interleaved (gen_service.py events)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcev_") and f.endswith(".npz"))
 
 
 def svc_steal_files():

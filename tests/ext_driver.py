@@ -404,12 +404,179 @@ def run_second_graph(name):
                 active=ext.active, reason=ext.reason)
 
 
+class EventEngine(FixtureEngine):
+    """FixtureEngine with the service-event calls: each consumes the fixture's placement
+    count of its event and records what the extension passed."""
+
+    def __init__(self, exp, fixture_keys):
+        super().__init__(exp, fixture_keys)
+        self.calls = []
+
+    def _event(self, *call):
+        self.calls.append(call)
+        k = self.stim[self.k]
+        self.n += k
+        self.k += 1
+        return k
+
+    def add_replicas(self, t, w):
+        return self._event("add", [int(x) for x in t], [int(x) for x in w])
+
+    def remove_replicas(self, t, w):
+        return self._event("remove", [int(x) for x in t], [int(x) for x in w])
+
+    def set_worker_status(self, w, running):
+        return self._event("status", int(w), int(running))
+
+    def long_running(self, t, cd):
+        return self._event("long", int(t), float(cd))
+
+    def heartbeat(self, bw, ps, ds):
+        return self._event("heartbeat", float(bw), [int(x) for x in ps], [float(x) for x in ds])
+
+    def task_erred(self, t):
+        return self._event("erred", int(t))
+
+
+def run_events(name, plain=False):
+    """A ``svcev_*`` stream (gen_service.py events): every event through the scheduler's own
+    stream handler (add-keys, release-worker-data, worker-status-change, long-running,
+    task-erred) or RPC handler (heartbeat_worker's placement part), wrapped by the
+    extension, which must forward each to its engine call with the right arguments and stay
+    active; every placement comes from the engine and validate=True re-derives it."""
+    import math as _m
+
+    from gen_service import (EV_ADD_KEYS, EV_ERRED, EV_FINISHED, EV_HEARTBEAT, EV_LONG_RUNNING, EV_PAUSE,
+                             EV_RELEASE_DATA, EV_RESUME)
+
+    path = os.path.join(HERE, "golden", name)
+    g, cfg, exp, meta = load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    g["keys"] = None
+    sat = cfg["saturation"]
+    sat = float("inf") if sat == "inf" else float(sat)
+    dask.config.set({"distributed.scheduler.worker-saturation": sat})
+    cfg = dict(cfg, saturation=sat)
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    addr = {i: a for a, i in widx.items()}
+    S = type(s)
+    for nm in ("stimulus_task_finished", "handle_task_finished", "add_keys", "release_worker_data",
+               "handle_worker_status_change", "handle_long_running", "handle_task_erred", "stimulus_task_erred"):
+        setattr(S, nm, getattr(Scheduler, nm))
+    S.validate_key = lambda self, key, ts=None: None
+    S.send_all = lambda self, client_msgs, worker_msgs: None
+    S.worker_send = lambda self, worker, msg: None
+    s.extensions = {}
+
+    def heartbeat_worker(*, address, metrics, executing=None, **kw):  # Scheduler.heartbeat_worker :4223-4252
+        frac = 1 / len(s.workers)
+        s.bandwidth = s.bandwidth * (1 - frac) + metrics["bandwidth"]["total"] * frac
+        for key, duration in (executing or {}).items():
+            if key in s.tasks:
+                s.tasks[key].prefix.add_exec_time(duration)
+        return {"status": "OK"}
+
+    fkeys = [ts.key for ts in tss]
+    eng = (FixtureEngine if plain else EventEngine)(exp, fkeys)
+    ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
+    eng.ext = ext
+    s.stream_handlers = {"add-keys": s.add_keys, "release-worker-data": s.release_worker_data,
+                         "worker-status-change": s.handle_worker_status_change,
+                         "long-running": s.handle_long_running, "task-erred": s.handle_task_erred}
+    s.handlers = {"heartbeat_worker": heartbeat_worker}
+    ext._install()
+    priority = {ts.key: ts.priority for ts in tss}
+    recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
+    ext.update_graph(s, client="client-0", keys=set(priority), tasks=list(priority), annotations={},
+                     priority=priority, dependencies={})
+    assert ext.active, ext.reason
+    s._transitions(recs, {}, {}, "update-graph")
+    want = []  # the engine calls the events imply
+    hp, ht, hd = z["hb_ptr"], z["hb_task"], z["hb_dur"]
+    nbytes_bw = None
+    for i, kd in enumerate(z["ev_kind"].tolist()):
+        t, w, x = int(z["ev_task"][i]), int(z["ev_worker"][i]), float(z["ev_x"][i])
+        sid = f"ev-{i}"
+        H = s.stream_handlers
+        if kd == EV_FINISHED:
+            ts = tss[t]
+            H["task-finished"](key=ts.key, worker=addr[w], stimulus_id=sid, run_id=ts.run_id,
+                               nbytes=int(z["ev_nbytes"][i]), type=None, typename="int", metadata=None,
+                               startstops=[{"action": "compute", "start": float(z["ev_start"][i]),
+                                            "stop": float(z["ev_stop"][i])}])
+        elif kd == EV_ADD_KEYS:
+            H["add-keys"](worker=addr[w], keys=[tss[t].key], stimulus_id=sid)
+            want.append(("add", [t], [w]))
+        elif kd == EV_RELEASE_DATA:
+            H["release-worker-data"](key=tss[t].key, worker=addr[w], stimulus_id=sid)
+            want.append(("remove", [t], [w]))
+        elif kd in (EV_PAUSE, EV_RESUME):
+            H["worker-status-change"](status="running" if kd == EV_RESUME else "paused", worker=addr[w],
+                                      stimulus_id=sid)
+            want.append(("status", w, 1 if kd == EV_RESUME else 0))
+        elif kd == EV_LONG_RUNNING:
+            ts = tss[t]
+            H["long-running"](key=ts.key, worker=addr[w], compute_duration=None if _m.isnan(x) else x,
+                              stimulus_id=sid)
+            want.append(("long", t, x))
+        elif kd == EV_HEARTBEAT:
+            ex = {tss[int(q)].key: float(d) for q, d in zip(ht[hp[i]:hp[i + 1]], hd[hp[i]:hp[i + 1]])}
+            # the total that makes the reference's EWMA give the recorded bandwidth
+            frac = 1 / len(s.workers)
+            total = (x - s.bandwidth * (1 - frac)) / frac
+            bw0 = s.bandwidth
+            s.handlers["heartbeat_worker"](address=addr[w], metrics={"bandwidth": {"total": total}},
+                                           executing=ex)
+            assert s.bandwidth == x or abs(s.bandwidth - x) <= 1e-6 * x, (s.bandwidth, x)
+            ps = [int(g["prefix_id"][int(q)]) for q in ht[hp[i]:hp[i + 1]]]
+            if s.bandwidth != bw0 or ps:
+                want.append(("heartbeat", float(s.bandwidth), ps, [float(d) for d in hd[hp[i]:hp[i + 1]]]))
+            elif ext.active:
+                eng.k += 1  # nothing changed: no engine call; the fixture's count for it is 0
+        elif kd == EV_ERRED:
+            ts = tss[t]
+            H["task-erred"](key=ts.key, worker=addr[w], stimulus_id=sid, run_id=ts.run_id, exception=None,
+                            traceback=None)
+            want.append(("erred", t))
+        if plain:  # an engine without the event calls: the first event hands placement back
+            if kd != EV_FINISHED:
+                assert not ext.active and "not modelled" in ext.reason, (i, kd, ext.reason)
+            continue
+        assert ext.active, (i, kd, ext.reason)
+    ext._end_of_stimulus("end of stream")
+    n = len(exp["pl_task"])
+    if plain:  # the scheduler's own decisions from the fallback on: still the reference's
+        assert rec["task"] == exp["pl_task"].tolist() and rec["worker"] == exp["pl_worker"].tolist()
+        assert 0 < ext.stats["device_decisions"] < n, ext.stats
+        return dict(fixture=name, placements=n, device_decisions=ext.stats["device_decisions"], active=ext.active,
+                    reason=ext.reason)
+    assert ext.active, ext.reason
+    got = [c for c in eng.calls]
+    assert len(got) == len(want), (len(got), len(want))
+    for a, b in zip(got, want):
+        assert a[0] == b[0], (a, b)
+        if a[0] == "long":
+            assert a[1] == b[1] and (a[2] == b[2] or (_m.isnan(a[2]) and _m.isnan(b[2]))), (a, b)
+        elif a[0] == "heartbeat":
+            assert a[2] == b[2] and a[3] == b[3], (a, b)
+        else:
+            assert a == b, (a, b)
+    assert rec["task"] == exp["pl_task"].tolist()
+    assert rec["worker"] == exp["pl_worker"].tolist()
+    assert np.array_equal(np.array(rec["start"]).view(np.int64), exp["pl_start"].view(np.int64))
+    assert ext.stats["device_decisions"] == n, (ext.stats, n)
+    return dict(fixture=name, placements=n, events=len(want), device_decisions=ext.stats["device_decisions"],
+                active=ext.active, reason=ext.reason, calls=dict(ext.stats))
+
+
 if __name__ == "__main__":
     import warnings
 
     warnings.filterwarnings("ignore")
     args = sys.argv[1:]
     diverge = "--diverge" in args
+    plain = "--plain" in args
     for nm in [a for a in args if not a.startswith("--")]:
-        fn = run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith("svcgraph_") else None
+        fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith("svcgraph_")
+              else (lambda x: run_events(x, plain)) if nm.startswith("svcev_") else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge)), flush=True)

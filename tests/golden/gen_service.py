@@ -48,6 +48,7 @@ sys.path.insert(0, HERE)
 
 import gen_golden as G  # noqa: E402  (installs the shim, imports the reference)
 
+import math  # noqa: E402
 import operator  # noqa: E402
 
 import dask  # noqa: E402
@@ -476,11 +477,243 @@ def main_second_graph(only):
         print(f"{name}: {len(msgs['task'])} messages, second graph of {g2['n_tasks']} at message {at}, routes {routes}")
 
 
+# event kinds of the svcev_* streams (tests/test_gpu_events.py, tests/ext_driver.py)
+EV_FINISHED, EV_ADD_KEYS, EV_RELEASE_DATA, EV_PAUSE, EV_RESUME, EV_LONG_RUNNING, EV_HEARTBEAT, EV_ERRED = range(8)
+
+
+def _erred_is_simple(s, ts):
+    """The task-erred cascade of ``ts`` (stimulus_task_erred :5094 -> processing -> erred
+    :2630-2720, its waiting dependents released then erred :2579-2605 / :2508-2537) releases
+    only dependencies that are in memory: a cascade that would also cancel processing,
+    waiting or queued tasks is not generated (the engine refuses it)."""
+    closure, stack = {ts}, [ts]
+    while stack:
+        x = stack.pop()
+        for y in x.dependents:
+            if y not in closure and not y.who_has:
+                closure.add(y)
+                stack.append(y)
+    for x in closure:
+        for d in x.dependencies:
+            if d in closure:
+                continue
+            if not (d.waiters or set()) - closure and not d.who_wants and d.state != "memory":
+                return False
+    return all(x is ts or x.state == "waiting" for x in closure)
+
+
+def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_scale=0.3):
+    """The replay protocol's completions as task-finished messages, interleaved with the
+    other worker stimuli that change placement inputs, each through the reference's own
+    handler (``Scheduler.*`` borrowed onto the replay state):
+
+    * add-keys (``Scheduler.add_keys`` :7359-7391 -> ``add_replica`` :3148): a replica of an
+      in-memory task on a worker that does not hold it;
+    * release-worker-data (``Scheduler.release_worker_data`` :5807-5815): one of several
+      replicas goes (never the last: that recomputes);
+    * worker-status-change (``Scheduler.handle_worker_status_change`` :5850-5883): a running
+      worker pauses / a paused one runs again (check_idle_saturated, refill);
+    * long-running (``Scheduler.handle_long_running`` :5817-5848): a processing task
+      secedes, with a compute duration or None;
+    * heartbeat (``Scheduler.heartbeat_worker``'s placement part, restated line by line:
+      the bandwidth EWMA :4223-4226 and TaskPrefix.add_exec_time for the executing tasks
+      :4247-4252);
+    * task-erred (``Scheduler.handle_task_erred`` :5799-5805 -> ``stimulus_task_erred``
+      :5094-5127) of a current run (no retries), when its cascade releases only in-memory
+      dependencies (``_erred_is_simple``); the erred task sends no task-finished.
+
+    Stored per event (``ev_*``, in order): kind, task, worker, a float (long-running
+    compute duration, NaN for None; heartbeat: the scheduler bandwidth after it), the
+    heartbeat's executing tasks and durations (CSR ``hb_ptr`` / ``hb_task`` / ``hb_dur``), and
+    the placements each event made (``stim_nplaced``: update_graph first)."""
+    from distributed.scheduler import Scheduler
+
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    W = len(g["nthreads"])
+    N = g["n_tasks"]
+    addr = {i: a for a, i in widx.items()}
+    rng = np.random.default_rng(seed)
+    S = type(s)
+    S.stimulus_task_finished = Scheduler.stimulus_task_finished
+    S.add_keys = Scheduler.add_keys
+    S.release_worker_data = Scheduler.release_worker_data
+    S.handle_worker_status_change = Scheduler.handle_worker_status_change
+    S.handle_long_running = Scheduler.handle_long_running
+    S.handle_task_erred = Scheduler.handle_task_erred
+    S.stimulus_task_erred = Scheduler.stimulus_task_erred
+    S.send_all = lambda self, client_msgs, worker_msgs: None
+    S.worker_send = lambda self, worker, msg: None
+    s.extensions = {}
+    recs = {}
+    for ts in sorted(tss, key=lambda t: t.priority, reverse=True):
+        recs[ts.key] = "waiting"
+    s._transitions(recs, {}, {}, "update-graph")
+    ev = {k: [] for k in ("kind", "task", "worker", "x", "nbytes", "start", "stop", "runid")}
+    hb = {"ptr": [0], "task": [], "dur": []}
+    stim = [len(rec["task"])]
+    round_ptr = [0]
+    rounds, nplaced = [], []
+    done = 0
+    erred = set()
+    paused = set()
+
+    def push(kind, t=-1, w=-1, x=math.nan, nbytes=-1, start=math.nan, stop=math.nan, runid=-1):
+        for k, v in zip(ev, (kind, t, w, x, nbytes, start, stop, runid)):
+            ev[k].append(v)
+        hb["ptr"].append(len(hb["task"]))
+
+    def event():
+        kind = int(rng.choice(kinds))
+        sid = f"event-{len(ev['kind'])}"
+        n0 = len(rec["task"])
+        if kind == EV_ADD_KEYS:
+            mem = [ts for ts in tss if ts.state == "memory"]
+            if not mem:
+                return
+            ts = mem[int(rng.integers(0, len(mem)))]
+            others = [i for i in range(W) if s.workers[addr[i]] not in ts.who_has]
+            if not others:
+                return
+            w = others[int(rng.integers(0, len(others)))]
+            s.add_keys(worker=addr[w], keys=[ts.key], stimulus_id=sid)
+            push(EV_ADD_KEYS, tidx[ts.key], w)
+        elif kind == EV_RELEASE_DATA:
+            rep = [ts for ts in tss if ts.state == "memory" and len(ts.who_has) >= 2]
+            if not rep:
+                return
+            ts = rep[int(rng.integers(0, len(rep)))]
+            hs = sorted(widx[ws.address] for ws in ts.who_has)
+            w = hs[int(rng.integers(0, len(hs)))]
+            s.release_worker_data(ts.key, addr[w], sid)
+            push(EV_RELEASE_DATA, tidx[ts.key], w)
+        elif kind == EV_PAUSE:
+            run = [i for i in range(W) if i not in paused]
+            if len(run) <= max(1, W // 2):
+                return
+            w = run[int(rng.integers(0, len(run)))]
+            s.handle_worker_status_change("paused", addr[w], sid)
+            paused.add(w)
+            push(EV_PAUSE, -1, w)
+        elif kind == EV_RESUME:
+            if not paused:
+                return
+            ps = sorted(paused)
+            w = ps[int(rng.integers(0, len(ps)))]
+            s.handle_worker_status_change("running", addr[w], sid)
+            paused.discard(w)
+            push(EV_RESUME, -1, w)
+        elif kind == EV_LONG_RUNNING:
+            proc = [ts for ts in tss if ts.state == "processing" and ts not in ts.processing_on.long_running]
+            if not proc:
+                return
+            ts = proc[int(rng.integers(0, len(proc)))]
+            cd = None if rng.random() < 0.3 else float(rng.uniform(0.001, 0.05))
+            s.handle_long_running(ts.key, ts.processing_on.address, cd, sid)
+            push(EV_LONG_RUNNING, tidx[ts.key], widx[ts.processing_on.address], math.nan if cd is None else cd)
+        elif kind == EV_HEARTBEAT:
+            w = int(rng.integers(0, W))
+            ws = s.workers[addr[w]]
+            total = float(rng.uniform(1 - bw_scale, 1 + bw_scale) * 1e8)
+            # Scheduler.heartbeat_worker :4223-4226 (bandwidth EWMA)
+            frac = 1 / len(s.workers)
+            s.bandwidth = s.bandwidth * (1 - frac) + total * frac
+            # :4247-4252 (the executing tasks' prefixes see their exec time)
+            execs = [ts for ts in ws.processing]
+            execs.sort(key=lambda t: tidx[t.key])
+            k = int(rng.integers(0, min(3, len(execs)) + 1))
+            for ts in execs[:k]:
+                d = float(rng.choice([rng.uniform(0.0, 0.02), rng.uniform(0.02, 2.0)]))
+                ts.prefix.add_exec_time(d)
+                hb["task"].append(tidx[ts.key])
+                hb["dur"].append(d)
+            push(EV_HEARTBEAT, -1, w, s.bandwidth)
+        elif kind == EV_ERRED:
+            proc = [ts for ts in tss if ts.state == "processing" and _erred_is_simple(s, ts)]
+            if not proc:
+                return
+            ts = proc[int(rng.integers(0, len(proc)))]
+            w = widx[ts.processing_on.address]
+            s.handle_task_erred(key=ts.key, stimulus_id=sid, worker=addr[w], run_id=ts.run_id, exception=None,
+                                traceback=None)
+            assert ts.state == "erred", ts.state
+            erred.add(tidx[ts.key])
+            push(EV_ERRED, tidx[ts.key], w)
+        stim.append(len(rec["task"]) - n0)
+
+    while True:
+        cur = len(rec["task"])
+        batch = list(range(done, cur))
+        rounds.append(G.snapshot(s, W, widx) + (len(s.queued),))
+        nplaced.append(cur - done)
+        done = cur
+        if not batch:
+            break
+        for pos in batch:
+            while rng.random() < p_event:
+                event()
+            t = rec["task"][pos]
+            ts = tss[t]
+            if ts.state != "processing":  # erred (or a cascade released it)
+                assert ts.state == "erred", (ts.key, ts.state)
+                continue
+            w = widx[ts.processing_on.address]
+            sid = f"task-finished-{len(ev['kind'])}"
+            r, cm, wm = s.stimulus_task_finished(
+                ts.key, ts.processing_on.address, sid, int(ts.run_id), nbytes=int(g["nbytes"][t]), type=None,
+                typename="int", metadata=None,
+                startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
+            assert ts.state != "processing"
+            n0 = len(rec["task"])
+            s._transitions(r, cm, wm, sid)
+            s.stimulus_queue_slots_maybe_opened(stimulus_id=sid)
+            stim.append(len(rec["task"]) - n0)
+            push(EV_FINISHED, t, w, math.nan, int(g["nbytes"][t]), float(g["start"][t]), float(g["stop"][t]), pos)
+        round_ptr.append(len(ev["kind"]))
+    rec["stim"] = stim
+    states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
+    return rec, rounds, nplaced, states, ev, hb, round_ptr
+
+
+def main_events(only):
+    cases = {
+        # every kind, queuing on, random durations, 1-4 threads
+        "svcev_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=41, n_inner_prefixes=3,
+                                                            random_durations=True, nthreads="random"), 1.1, 41, 0.08),
+        # queuing off (root-ish co-assignment reads idle / running)
+        "svcev_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 32, seed=42), float("inf"), 42, 0.08),
+        # a denser event mix on a smaller graph
+        "svcev_dense_sat1.0": (lambda: G.graphs.random_dag(1500, 24, seed=43, n_inner_prefixes=2,
+                                                            random_durations=True), 1.0, 43, 0.3),
+    }
+    for name, (mk, sat, seed, p_event) in cases.items():
+        if only and name not in only:
+            continue
+        g = mk()
+        G.graphs.check_graph(g)
+        dask.config.set({"distributed.scheduler.worker-saturation": sat})
+        cfg = G.config_dict(sat)
+        rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(g, cfg, seed, p_event)
+        G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
+        path = os.path.join(HERE, f"{name}.npz")
+        z = dict(np.load(path, allow_pickle=False))
+        z.update(ev_kind=np.array(ev["kind"], np.int8), ev_task=np.array(ev["task"], np.int32),
+                 ev_worker=np.array(ev["worker"], np.int32), ev_x=np.array(ev["x"], np.float64),
+                 ev_nbytes=np.array(ev["nbytes"], np.int64), ev_start=np.array(ev["start"]),
+                 ev_stop=np.array(ev["stop"]), ev_runid=np.array(ev["runid"], np.int64),
+                 hb_ptr=np.array(hb["ptr"], np.int64), hb_task=np.array(hb["task"], np.int32),
+                 hb_dur=np.array(hb["dur"], np.float64), ev_round_ptr=np.array(round_ptr, np.int64))
+        np.savez_compressed(path, **z)
+        cnt = np.bincount(np.array(ev["kind"]), minlength=8).tolist()
+        print(f"{name}: {len(ev['kind'])} events (by kind {cnt}), {len(rec['task'])} placements")
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "add-workers":
         return main_add_workers(set(sys.argv[2:]))
     if len(sys.argv) > 1 and sys.argv[1] == "second-graph":
         return main_second_graph(set(sys.argv[2:]))
+    if len(sys.argv) > 1 and sys.argv[1] == "events":
+        return main_events(set(sys.argv[2:]))
     cases = {
         "svc_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 64, seed=15, n_inner_prefixes=3,
                                                           random_durations=True, nthreads="random"), 1.1, 1, 0.0),

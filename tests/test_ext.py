@@ -65,6 +65,30 @@ def test_extension_follows_a_second_graph():
         assert r["active"] and r["device_decisions"] == r["placements"] and r["graphs"] == 2, r
 
 
+EVENTS = ["svcev_c2var_sat1.1.npz", "svcev_c2mini_satinf.npz", "svcev_dense_sat1.0.npz"]
+
+
+def test_extension_follows_service_events():
+    """add-keys, release-worker-data, worker pause / resume, long-running, heartbeats and
+    task-erred through the scheduler's own handlers: the extension forwards each to its
+    engine call with the arguments the reference state implies, stays active, and every
+    placement (validate=True) is the reference's."""
+    res = drive(EVENTS)
+    assert [r["fixture"] for r in res] == EVENTS
+    for r in res:
+        assert r["active"] and r["device_decisions"] == r["placements"], r
+        for op in ("add_replicas", "remove_replicas", "set_worker_status", "long_running", "heartbeat",
+                   "task_erred"):
+            assert r["calls"].get(op, 0) > 0, (op, r)
+
+
+def test_extension_hands_back_on_unmodelled_events():
+    """An engine without the event calls: the first such event ends GPU placement loudly
+    ("not modelled") and the scheduler's own decisions carry on, equal to the reference's."""
+    res = drive(EVENTS[:1], "--plain")
+    assert not res[0]["active"] and "not modelled" in res[0]["reason"], res
+
+
 def test_extension_hands_back_on_divergence():
     """A decision out of order: the extension detects it at once and the scheduler's own
     decide_worker carries on; the records are still the reference's."""

@@ -1,0 +1,114 @@
+"""Service events (needs an MI355X): the placement-input stimuli a live scheduler handles
+besides task-finished, on the device, against the reference's own handlers.
+
+The ``svcev_*`` fixtures (``tests/golden/gen_service.py events``) run the replay protocol's
+task-finished messages through ``Scheduler.stimulus_task_finished`` with, interleaved and
+each through the reference's handler: add-keys (``Scheduler.add_keys`` -> ``add_replica``,
+distributed/scheduler.py:7359-7391, :3148), release-worker-data (:5807-5815, never the
+last replica), worker pause / resume (``handle_worker_status_change`` :5850-5883),
+long-running (``handle_long_running`` :5817-5848), heartbeats (the bandwidth EWMA
+:4223-4226 and ``TaskPrefix.add_exec_time`` :4247-4252) and task-erred
+(``handle_task_erred`` :5799-5805). Each event goes to its engine call
+(``dgp_add_replicas`` / ``dgp_remove_replicas`` / ``dgp_set_worker_status`` /
+``dgp_long_running`` / ``dgp_heartbeat`` / ``dgp_task_erred``) before the message it preceded
+in the reference; every placement (task, worker, comm bytes, objective bits, ws.nbytes,
+route), the placements each event made, the per-round snapshots and the final task states
+must equal the reference's.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, svc_event_files
+from oracle import oracle
+from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
+
+pytestmark = pytest.mark.gpu
+
+EV_FINISHED, EV_ADD_KEYS, EV_RELEASE_DATA, EV_PAUSE, EV_RESUME, EV_LONG_RUNNING, EV_HEARTBEAT, EV_ERRED = range(8)
+
+
+def drive_events(eng, g, z):
+    """Every event of a svcev_* stream through the engine, snapshot per round; returns the
+    placements each event made (update_graph's first)."""
+    kind, task, worker, x = z["ev_kind"], z["ev_task"], z["ev_worker"], z["ev_x"]
+    hp, ht, hd = z["hb_ptr"], z["hb_task"], z["hb_dur"]
+    ptr = z["ev_round_ptr"].tolist()
+    stim = [eng.num_placements()]
+    for k in range(len(ptr) - 1):
+        for i in range(ptr[k], ptr[k + 1]):
+            n0 = eng.num_placements()
+            kd, t, w = int(kind[i]), int(task[i]), int(worker[i])
+            if kd == EV_FINISHED:
+                st, _ = eng.tasks_finished([t], [w], [int(z["ev_runid"][i])], [int(z["ev_nbytes"][i])],
+                                           [float(z["ev_start"][i])], [float(z["ev_stop"][i])])
+                assert st.tolist() == [0], (i, st)
+            elif kd == EV_ADD_KEYS:
+                eng.add_replicas([t], [w])
+            elif kd == EV_RELEASE_DATA:
+                eng.remove_replicas([t], [w])
+            elif kd in (EV_PAUSE, EV_RESUME):
+                eng.set_worker_status(w, 1 if kd == EV_RESUME else 0)
+            elif kd == EV_LONG_RUNNING:
+                eng.long_running(t, float(x[i]))
+            elif kd == EV_HEARTBEAT:
+                ts = ht[hp[i]:hp[i + 1]]
+                eng.heartbeat(float(x[i]), g["prefix_id"][ts], hd[hp[i]:hp[i + 1]])
+            elif kd == EV_ERRED:
+                eng.task_erred(t)
+            else:
+                raise AssertionError(kd)
+            stim.append(eng.num_placements() - n0)
+        eng.snapshot()
+    return np.array(stim, np.int32)
+
+
+@pytest.mark.parametrize("name", svc_event_files())
+def test_service_events_match_reference(name):
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    assert set(np.unique(z["ev_kind"]).tolist()) == set(range(8))  # every event kind is exercised
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        stim = drive_events(eng, g, z)
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert np.array_equal(stim, exp["stim_nplaced"]), np.nonzero(stim != exp["stim_nplaced"])[0][:5]
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+def test_service_events_refuse_what_they_do_not_model():
+    """The last replica going, a paused worker taking a new graph, an erred cascade that
+    would cancel work: refused (DGP_E_DEVICE / DGP_E_STATE), so the extension hands
+    placement back instead of diverging."""
+    from distributed_amd import _lib, graphs
+    from distributed_amd.engine import PlacementEngine
+
+    g = graphs.random_dag(2000, 32, seed=5)
+    cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": 1.1}
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, results=False)
+        eng.update_graph()
+        p = eng.placements(0, 1)
+        t, w = int(p["pl_task"][0]), int(p["pl_worker"][0])
+        st, _ = eng.tasks_finished([t], [w], [0], [100], [0.0], [0.01])
+        assert st.tolist() == [0]
+        with pytest.raises(_lib.DgpError, match="does not model"):
+            eng.remove_replicas([t], [w])  # its only replica
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, results=False)
+        eng.update_graph()
+        eng.set_worker_status(3, 0)
+        h = dict(g2 := graphs.random_dag(200, 32, seed=6), prefix_default_dur=g["prefix_default_dur"],
+                 group_prefix=g["group_prefix"])
+        with pytest.raises(_lib.DgpError, match="paused"):
+            eng.add_graph(dict(h, prio=g2["prio"] + len(g["prio"]), group_id=g2["group_id"] + len(g["group_prefix"]),
+                               group_prefix=np.concatenate([g["group_prefix"], g2["group_prefix"]])))
