@@ -1091,7 +1091,10 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   if (n_prefixes > dgp::st::PD)
     return fail(e, DGP_E_STATE, "dgp_add_graph: more task prefixes than the stream engine carries (8)");
   if (dep_ptr[0] != 0) return fail(e, DGP_E_ARG, "dgp_add_graph: bad dep_ptr");
+  for (int64_t t = 0; t < n_new; t++)
+    if (dep_ptr[t + 1] < dep_ptr[t]) return fail(e, DGP_E_ARG, "dgp_add_graph: dep_ptr not monotone");
   const int64_t En = dep_ptr[n_new];
+  if (En > 0 && !dep_idx) return fail(e, DGP_E_ARG, "dgp_add_graph: dep_idx missing");
   for (int64_t k = 0; k < En; k++)
     if (dep_idx[k] < 0 || dep_idx[k] >= n_new)
       return fail(e, DGP_E_ARG, "dgp_add_graph: dependencies must be tasks of the new graph");

@@ -54,6 +54,7 @@ class PlacementEngine:
 
     def __init__(self, device: int = 0):
         self.lib = _lib.load()
+        self.device = int(device)
         h = self.lib.dgp_create(int(device))
         if not h:
             raise _lib.DgpError(f"dgp_create({device}) failed: no HIP device visible (no CPU fallback)")
@@ -422,8 +423,11 @@ class PlacementEngine:
         lo, hi = shard_range(n, rank, world)
         self._check(self.lib.dgp_steal_thief_rows(self.h, lo, hi), "dgp_steal_thief_rows")
         rb = int(self.lib.dgp_steal_row_bytes())
-        dev = torch.device("cuda", torch.cuda.current_device())
+        # the engine's device; the zero-fill runs on torch's stream and the pack on the
+        # engine's (a non-blocking stream): the fill must be done before the pack writes
+        dev = torch.device("cuda", self.device)
         local = torch.zeros(max(chunk_rows(n, world), 0) * rb, dtype=torch.uint8, device=dev)
+        torch.cuda.current_stream(dev).synchronize()
         if hi > lo:
             self._check(self.lib.dgp_steal_pack_rows(self.h, lo, hi, C.c_void_p(local.data_ptr())),
                         "dgp_steal_pack_rows")
