@@ -62,6 +62,12 @@ SIGNATURES = {
     "dgp_set_worker_flags": (C.c_int, [_P, C.c_int64, _P, _P, _P]),
     "dgp_set_wanted": (C.c_int, [_P, C.c_int64, _P, _P]),
     "dgp_task_erred": (C.c_int, [_P, C.c_int32, _P]),
+    "dgp_remove_worker": (C.c_int, [_P, C.c_int32]),
+    "dgp_sync_placements": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P]),
+    "dgp_sync_tasks": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dgp_sync_workers": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dgp_sync_globals": (C.c_int, [_P, C.c_int64, C.c_double, C.c_int32, _P, _P, C.c_int64, _P, _P, _P, C.c_double,
+                                   _P, _P, _P]),
 }
 
 ABI_VERSION = 8

@@ -190,6 +190,7 @@ struct Dev {
   double* pl_start;
   int64_t* pl_wsnbytes;
   int8_t* pl_route;
+  int64_t pl_cap;  // placement-log capacity (>= N; grows in service sessions that re-place tasks)
   // record log
   Rec* rec;
   int64_t rec_cap;

@@ -389,3 +389,73 @@ __global__ void __launch_bounds__(64) k_ev_task_erred(const Dev* __restrict__ Dp
 
 }  // namespace ev
 }  // namespace dgp
+
+namespace dgp {
+namespace ev {
+
+// ===================================================================== resync
+// After a stimulus the engine does not model, the scheduler decided it itself; the host then
+// hands over the scheduler's state (dgp_sync_*). Tasks: a sparse list of rows.
+struct SyncTask {
+  int32_t t, proc_on, remaining, waiters;
+  int64_t nbytes;  // TaskState.nbytes (raw: -1 = never reported)
+  int32_t hp, hn;  // who_has: holders [hp, hp + hn) of the holder list
+  uint8_t state, lr, pad0, pad1;
+  int32_t pad2;
+};
+static_assert(sizeof(SyncTask) == 40, "SyncTask layout is shared with the host");
+
+__global__ void k_sync_tasks(const Dev* __restrict__ Dp, const SyncTask* __restrict__ rows, int n,
+                             const int32_t* __restrict__ holders) {
+  const Dev& D = *Dp;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const SyncTask r = rows[i];
+    const int t = r.t;
+    D.state[t] = r.state;
+    D.remaining[t] = r.remaining;
+    D.waiters[t] = r.waiters;
+    D.proc_on[t] = r.proc_on;
+    D.res_nbytes[t] = r.nbytes;
+    D.cur_nbytes[t] = r.state == S_MEMORY ? nbv(D, r.nbytes) : -1;
+    D.fr_mark[t] = -1;
+    D.rel_mark[t] = -1;
+    for (int b = 0; b < D.WB; b++) D.holders[(size_t)t * D.WB + b] = 0;
+    int first = -1;
+    for (int k = 0; k < r.hn; k++) {
+      const int w = holders[r.hp + k];
+      D.holders[(size_t)t * D.WB + (w >> 6)] |= 1ull << (w & 63);
+      if (first < 0) first = w;
+    }
+    D.holder_of[t] = r.state == S_PROCESSING ? r.proc_on : first;
+    D.tdyn[t] = (uint8_t)((r.lr ? TD_LR : 0) | (r.hn > 1 ? TD_MULTI : 0));
+  }
+}
+
+// placements the scheduler made itself, appended to the placement log (their run identity)
+__global__ void k_sync_placements(const Dev* __restrict__ Dp, const int32_t* __restrict__ task,
+                                  const int32_t* __restrict__ worker, const int64_t* __restrict__ comm,
+                                  const double* __restrict__ start, const int64_t* __restrict__ wsnb,
+                                  const int8_t* __restrict__ route, int n) {
+  const Dev& D = *Dp;
+  const long long base = (long long)D.ctl->n_placed;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const long long pos = base + i;
+    const int t = task[i];
+    D.pl_task[pos] = t;
+    D.pl_worker[pos] = worker[i];
+    D.pl_comm[pos] = comm[i];
+    D.pl_start[pos] = start[i];
+    D.pl_wsnbytes[pos] = wsnb[i];
+    D.pl_route[pos] = route[i];
+    D.run_id[t] = (int32_t)pos;
+    D.holder_of[t] = worker[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    D.ctl->n_placed = (unsigned long long)(base + n);
+    D.pos->runid_upto = base + n;
+  }
+}
+
+}  // namespace ev
+}  // namespace dgp

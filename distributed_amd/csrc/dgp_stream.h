@@ -908,7 +908,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
     const long long lb = S.log_len + (ipl - npl), rb = S.rec_len + (irc - nrec), qb = S.qhead + (ipo - npop);
     // capacity first: nothing is copied past the record log (rlog_cap = 2N + 4096 covers one
     // K_COMPLETE per completion and one K_PLACE per placement, the only record kinds)
-    if (S.rec_len + trc > D.rlog_cap || S.log_len + tpl > D.N) {
+    if (S.rec_len + trc > D.rlog_cap || S.log_len + tpl > D.pl_cap) {
       serr(S, SERR_REC, (int)sp);
       break;
     }

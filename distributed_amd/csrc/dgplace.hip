@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -94,7 +95,9 @@ struct dgp_engine {
   std::vector<uint8_t> h_wanted;
   std::vector<int64_t> gdep_n, gdep_len;   // per group: len(tg.dependencies), sum of their lengths
   std::vector<int8_t> rootish_override_h;  // TaskState._rootish per task (-1: None)
-  std::vector<uint8_t> paused_h;           // per worker: not in SchedulerState.running
+  std::vector<uint8_t> paused_h;           // per worker: 0 running, 1 paused, 2 removed
+  int64_t log_min[3] = {0, 0, 0};          // minimum capacities of the placement / stimulus / record logs
+  int64_t sv_used = 0;                     // service stimuli appended (accepted task-finished messages)
   char* d_ev = nullptr;                    // service-event argument staging (device)
   size_t d_ev_cap = 0;
 };
@@ -194,6 +197,10 @@ int check_device_error(dgp_engine* e, dgp::Ctl* out = nullptr) {
     char buf[200];
     snprintf(buf, sizeof buf, "device engine error %d (%s) at task %d", c.error,
              (c.error >= 0 && c.error <= 20) ? names[c.error] : "?", c.err_task);
+    if (c.error == dgp::ERR_UNSUPPORTED) {  // a refused event changed nothing: the engine stays usable
+      const int zero[2] = {0, -1};
+      HIPCHK(e, hipMemcpy((char*)e->ctl + offsetof(dgp::Ctl, error), zero, sizeof zero, hipMemcpyHostToDevice));
+    }
     return fail(e, DGP_E_DEVICE, buf);
   }
   return 0;
@@ -283,6 +290,45 @@ int set_runids(dgp_engine* e) {
   hipLaunchKernelGGL(dgp::svc::k_set_runids, dim3(64), dim3(256), 0, e->stream, e->d_dev);
   hipLaunchKernelGGL(dgp::svc::k_set_runids_done, dim3(1), dim3(64), 0, e->stream, e->d_dev);
   HIPCHK(e, hipGetLastError());
+  return 0;
+}
+
+// Service sessions can place and complete a task more than once (rescheduled, recomputed
+// after a worker loss): before a call that may place up to every task and append up to
+// `stimuli` completions, the logs grow (doubling) so that one call cannot overflow them.
+int grow_logs(dgp_engine* e, int64_t stimuli) {
+  dgp::Dev& D = e->D;
+  const int64_t N = D.N, used_pl = (int64_t)e->last_placed;
+  auto& L = e->graph_allocs;
+  int rc = 0;
+  if (used_pl + N + 64 > D.pl_cap) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const int64_t cap = std::max<int64_t>(2 * D.pl_cap, used_pl + N + 64);
+    rc |= regrow(e, &D.pl_task, D.pl_cap, cap, L);
+    rc |= regrow(e, &D.pl_worker, D.pl_cap, cap, L);
+    rc |= regrow(e, &D.pl_comm, D.pl_cap, cap, L);
+    rc |= regrow(e, &D.pl_start, D.pl_cap, cap, L);
+    rc |= regrow(e, &D.pl_wsnbytes, D.pl_cap, cap, L);
+    rc |= regrow(e, &D.pl_route, D.pl_cap, cap, L);
+    if (rc) return rc;
+    D.pl_cap = cap;
+  }
+  if (e->sv_used + stimuli > D.sv_cap) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const int64_t cap = std::max<int64_t>(2 * D.sv_cap, e->sv_used + stimuli);
+    rc |= regrow(e, &D.sv_task, D.sv_cap, cap, L);
+    rc |= regrow(e, &D.sv_worker, D.sv_cap, cap, L);
+    if (rc) return rc;
+    D.sv_cap = cap;
+  }
+  // one record per placement and per completion
+  if (used_pl + N + e->sv_used + stimuli + 4096 > D.rlog_cap) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const int64_t cap = std::max<int64_t>(2 * D.rlog_cap, used_pl + N + e->sv_used + stimuli + 4096);
+    rc |= regrow(e, &D.rlog, D.rlog_cap, cap, L);
+    if (rc) return rc;
+    D.rlog_cap = cap;
+  }
   return 0;
 }
 
@@ -636,12 +682,15 @@ int upload_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const i
   rc |= dalloc(e, &D.g_left, n_groups, L);
   rc |= dalloc(e, &D.g_lastw, n_groups, L);
   rc |= dalloc(e, &D.qarr, N, L);
-  rc |= dalloc(e, &D.pl_task, N, L);
-  rc |= dalloc(e, &D.pl_worker, N, L);
-  rc |= dalloc(e, &D.pl_comm, N, L);
-  rc |= dalloc(e, &D.pl_start, N, L);
-  rc |= dalloc(e, &D.pl_wsnbytes, N, L);
-  rc |= dalloc(e, &D.pl_route, N, L);
+  // the logs: N entries (one placement / completion per task) unless a service session
+  // re-placed tasks (rescheduled, recomputed): then at least what it used (grow_logs)
+  D.pl_cap = std::max<int64_t>(N, e->log_min[0]);
+  rc |= dalloc(e, &D.pl_task, D.pl_cap, L);
+  rc |= dalloc(e, &D.pl_worker, D.pl_cap, L);
+  rc |= dalloc(e, &D.pl_comm, D.pl_cap, L);
+  rc |= dalloc(e, &D.pl_start, D.pl_cap, L);
+  rc |= dalloc(e, &D.pl_wsnbytes, D.pl_cap, L);
+  rc |= dalloc(e, &D.pl_route, D.pl_cap, L);
   int64_t capmax = 1;
   for (int32_t nt : e->nthreads) capmax = std::max<int64_t>(capmax, (int64_t)std::ceil(std::min(D.saturation, 64.0) * nt));
   D.rec_cap = 3 * N + N * std::min<int64_t>(capmax, 8) + 4096;
@@ -669,12 +718,12 @@ int upload_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const i
   rc |= dalloc(e, &D.tdyn, N, L);
   rc |= dalloc(e, &D.fr_mark, N, L);
   rc |= dalloc(e, &D.rel_mark, N, L);
-  D.rlog_cap = 2 * N + 4096;
+  D.rlog_cap = std::max<int64_t>(2 * N + 4096, e->log_min[2]);
   rc |= dalloc(e, &D.rlog, D.rlog_cap, L);
   // service mode: the stimulus log (each task completes at most once) and its length
-  D.sv_cap = N;
-  rc |= dalloc(e, &D.sv_task, N, L);
-  rc |= dalloc(e, &D.sv_worker, N, L);
+  D.sv_cap = std::max<int64_t>(N, e->log_min[1]);
+  rc |= dalloc(e, &D.sv_task, D.sv_cap, L);
+  rc |= dalloc(e, &D.sv_worker, D.sv_cap, L);
   rc |= dalloc(e, &D.sv_cseq, N, L);
   rc |= dalloc(e, &D.svc_len, 1, L);
   if (rc) return DGP_E_HIP;
@@ -824,6 +873,7 @@ int dgp_reset(dgp_engine* e) {
     HIPCHK(e, hipMemsetAsync(D.sv_cseq, 0xff, N * 4, s));
     e->mode = 0;
     e->last_placed = 0;
+    e->sv_used = 0;
   }
   std::vector<double> maxexec(D.P, -1.0);
   HIPCHK(e, hipMemcpyAsync(D.pdur_cur, e->prefix_defaults.data(), D.P * 8, hipMemcpyHostToDevice, s));
@@ -935,6 +985,7 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
   }
   for (int64_t i = 0; i < n; i++) e->h_msgs[i] = V::Msg{task[i], worker[i], run_id[i], nbytes[i], start[i], stop[i]};
   hipStream_t s = e->stream;
+  if (int rc = grow_logs(e, n)) return rc;
   if (int rc = sync_dev(e)) return rc;
   HIPCHK(e, hipMemcpyAsync(e->d_msgs, e->h_msgs, n * sizeof(V::Msg), hipMemcpyHostToDevice, s));
   // the batch in segments: each ends where an answer depends on the segment's own stimuli
@@ -956,6 +1007,7 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
   }
   if (n_new_placements) *n_new_placements = (int64_t)(c.n_placed - e->last_placed);
   e->last_placed = c.n_placed;
+  for (int64_t i = 0; i < n; i++) e->sv_used += status[i] == DGP_TF_ACCEPTED ? 1 : 0;
   return 0;
 }
 
@@ -1059,6 +1111,7 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
     }
   }
   e->mode = 2;
+  if (int rc2 = grow_logs(e, 0)) return rc2;
   if (int rc2 = sync_dev(e)) return rc2;
   hipLaunchKernelGGL(dgp::st::k_add_worker, dim3(1), dim3(64), 0, e->stream, e->d_dev, e->d_aux + 3);
   HIPCHK(e, hipGetLastError());
@@ -1080,8 +1133,8 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
   dgp::Dev& D = e->D;
   if (D.restr_flags) return fail(e, DGP_E_STATE, "dgp_add_graph: not with worker restrictions");
-  if (std::count(e->paused_h.begin(), e->paused_h.end(), 1))
-    return fail(e, DGP_E_STATE, "dgp_add_graph: not while a worker is paused");
+  if (std::count_if(e->paused_h.begin(), e->paused_h.end(), [](uint8_t v) { return v != 0; }))
+    return fail(e, DGP_E_STATE, "dgp_add_graph: not while a worker is paused or removed");
   if (n_new <= 0 || !dep_ptr || !prio || !prefix_id || !prefix_default_duration || !group_id || !wanted ||
       !rootish_override)
     return fail(e, DGP_E_ARG, "dgp_add_graph: bad arguments");
@@ -1126,6 +1179,9 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   for (int64_t t = 0; t < n_new; t++) relwait[group_id[t]]++;
   const dgp::Dev old = D;
   const int64_t old_rlog = D.rlog_cap;
+  e->log_min[0] = D.pl_cap + n_new;
+  e->log_min[1] = D.sv_cap + n_new;
+  e->log_min[2] = D.rlog_cap + 2 * n_new;
   std::vector<void*> old_allocs;
   old_allocs.swap(e->graph_allocs);
   e->have_graph = false;
@@ -1158,20 +1214,21 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   HIPCHK(e, carry(D.release_key, old.release_key, n0 * 8, n1 * 8, 0));
   HIPCHK(e, carry(D.cand_n, old.cand_n, n0 * 4, n1 * 4, 0));
   HIPCHK(e, carry(D.qarr, old.qarr, n0 * 4, n1 * 4, 0));
-  HIPCHK(e, carry(D.pl_task, old.pl_task, n0 * 4, n1 * 4, 0));
-  HIPCHK(e, carry(D.pl_worker, old.pl_worker, n0 * 4, n1 * 4, 0));
-  HIPCHK(e, carry(D.pl_comm, old.pl_comm, n0 * 8, n1 * 8, 0));
-  HIPCHK(e, carry(D.pl_start, old.pl_start, n0 * 8, n1 * 8, 0));
-  HIPCHK(e, carry(D.pl_wsnbytes, old.pl_wsnbytes, n0 * 8, n1 * 8, 0));
-  HIPCHK(e, carry(D.pl_route, old.pl_route, n0, n1, 0));
+  const size_t p0 = old.pl_cap, p1 = D.pl_cap;
+  HIPCHK(e, carry(D.pl_task, old.pl_task, p0 * 4, p1 * 4, 0));
+  HIPCHK(e, carry(D.pl_worker, old.pl_worker, p0 * 4, p1 * 4, 0));
+  HIPCHK(e, carry(D.pl_comm, old.pl_comm, p0 * 8, p1 * 8, 0));
+  HIPCHK(e, carry(D.pl_start, old.pl_start, p0 * 8, p1 * 8, 0));
+  HIPCHK(e, carry(D.pl_wsnbytes, old.pl_wsnbytes, p0 * 8, p1 * 8, 0));
+  HIPCHK(e, carry(D.pl_route, old.pl_route, p0, p1, 0));
   HIPCHK(e, carry(D.run_id, old.run_id, n0 * 4, n1 * 4, 0xff));
   HIPCHK(e, carry(D.holder_of, old.holder_of, n0 * 4, n1 * 4, 0xff));
   HIPCHK(e, carry(D.tdyn, old.tdyn, n0, n1, 0));
   HIPCHK(e, carry(D.fr_mark, old.fr_mark, n0 * 4, n1 * 4, 0xff));
   HIPCHK(e, carry(D.rel_mark, old.rel_mark, n0 * 4, n1 * 4, 0xff));
   HIPCHK(e, carry(D.rlog, old.rlog, (size_t)old_rlog * sizeof(dgp::st::SRec), (size_t)D.rlog_cap * sizeof(dgp::st::SRec), 0));
-  HIPCHK(e, carry(D.sv_task, old.sv_task, n0 * 4, n1 * 4, 0));
-  HIPCHK(e, carry(D.sv_worker, old.sv_worker, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.sv_task, old.sv_task, (size_t)old.sv_cap * 4, (size_t)D.sv_cap * 4, 0));
+  HIPCHK(e, carry(D.sv_worker, old.sv_worker, (size_t)old.sv_cap * 4, (size_t)D.sv_cap * 4, 0));
   HIPCHK(e, carry(D.sv_cseq, old.sv_cseq, n0 * 4, n1 * 4, 0xff));
   HIPCHK(e, carry(D.svc_len, old.svc_len, 8, 8, 0));
   // prefixes: TaskPrefix state of the known ones kept, the new ones at their defaults
@@ -1258,6 +1315,7 @@ int stage_args(dgp_engine* e, std::initializer_list<std::pair<const void*, size_
 // a one-wave event kernel that may refill the queue: run it, report its placements
 template <class F>
 int event_with_refill(dgp_engine* e, F&& launch, int64_t* n_new_placements) {
+  if (int rc = grow_logs(e, 0)) return rc;
   if (int rc = sync_dev(e)) return rc;
   launch();
   HIPCHK(e, hipGetLastError());
@@ -1313,6 +1371,7 @@ int dgp_set_worker_status(dgp_engine* e, int32_t worker, int32_t running, int64_
   if (int rc = event_ready(e, "dgp_set_worker_status")) return rc;
   if (worker < 0 || worker >= e->D.W) return fail(e, DGP_E_ARG, "dgp_set_worker_status: worker out of range");
   const uint8_t paused = running ? 0 : 1;
+  if (e->paused_h[worker] == 2) return fail(e, DGP_E_ARG, "dgp_set_worker_status: the worker was removed");
   if (e->paused_h[worker] == paused) return 0;  // ws.status == prev_status: nothing (:5858-5859)
   e->paused_h[worker] = paused;
   e->D.evf |= dgp::EVF_PAUSED;
@@ -1394,6 +1453,244 @@ int dgp_task_erred(dgp_engine* e, int32_t task, int64_t* n_new_placements) {
   return event_with_refill(e, [&] {
     hipLaunchKernelGGL(dgp::ev::k_ev_task_erred, dim3(1), dim3(64), 0, e->stream, e->d_dev, task, e->d_aux + 3);
   }, n_new_placements);
+}
+
+int dgp_remove_worker(dgp_engine* e, int32_t worker) {
+  if (int rc = event_ready(e, "dgp_remove_worker")) return rc;
+  if (worker < 0 || worker >= e->D.W) return fail(e, DGP_E_ARG, "dgp_remove_worker: worker out of range");
+  if (e->paused_h[worker] == 2) return 0;  // already removed ("already-removed" :5196-5197)
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  // Scheduler.remove_worker's worker table part (:5213-5231): the WorkerState leaves workers,
+  // running, idle, idle_task_count and saturated and total_nthreads; its index stays (the
+  // canonical order of the others is unchanged) as a worker that is never a candidate
+  int64_t placed = 0;
+  if (!e->paused_h[worker])
+    if (int rc = dgp_set_worker_status(e, worker, 0, &placed)) return rc;
+  e->paused_h[worker] = 2;
+  e->D.total_nthreads -= e->nthreads[worker];
+  return 0;
+}
+
+int dgp_sync_placements(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* comm_bytes,
+                        const double* start_time, const int64_t* ws_nbytes, const int8_t* route) {
+  if (int rc = event_ready(e, "dgp_sync_placements")) return rc;
+  if (n < 0 || (n > 0 && (!task || !worker || !comm_bytes || !start_time || !ws_nbytes || !route)))
+    return fail(e, DGP_E_ARG, "dgp_sync_placements: bad batch");
+  if (n == 0) return 0;
+  dgp::Ctl c;
+  if (int rc = read_ctl(e, &c)) return rc;
+  e->last_placed = c.n_placed;
+  if (int rc = grow_logs(e, 0)) return rc;
+  if ((int64_t)c.n_placed + n > e->D.pl_cap) return fail(e, DGP_E_ARG, "dgp_sync_placements: more placements than tasks");
+  for (int64_t i = 0; i < n; i++)
+    if (task[i] < 0 || task[i] >= e->D.N || worker[i] < 0 || worker[i] >= e->D.W)
+      return fail(e, DGP_E_ARG, "dgp_sync_placements: task or worker out of range");
+  std::vector<char*> a;
+  if (int rc = stage_args(e, {{task, n * 4}, {worker, n * 4}, {comm_bytes, n * 8}, {start_time, n * 8},
+                              {ws_nbytes, n * 8}, {route, (size_t)n}}, a))
+    return rc;
+  if (int rc = sync_dev(e)) return rc;
+  hipLaunchKernelGGL(dgp::ev::k_sync_placements, dim3(1), dim3(256), 0, e->stream, e->d_dev, (const int32_t*)a[0],
+                     (const int32_t*)a[1], (const int64_t*)a[2], (const double*)a[3], (const int64_t*)a[4],
+                     (const int8_t*)a[5], (int)n);
+  HIPCHK(e, hipGetLastError());
+  if (int rc = check_device_error(e, &c)) return rc;
+  e->last_placed = c.n_placed;
+  return 0;
+}
+
+int dgp_sync_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t* state, const int32_t* remaining,
+                   const int32_t* waiters, const int32_t* processing_on, const int64_t* nbytes,
+                   const uint8_t* long_running, const uint8_t* wanted, const int64_t* holder_ptr,
+                   const int32_t* holder_idx) {
+  if (int rc = event_ready(e, "dgp_sync_tasks")) return rc;
+  if (n < 0 || (n > 0 && (!task || !state || !remaining || !waiters || !processing_on || !nbytes || !long_running ||
+                          !wanted || !holder_ptr)))
+    return fail(e, DGP_E_ARG, "dgp_sync_tasks: bad rows");
+  if (n == 0) return 0;
+  const dgp::Dev& D = e->D;
+  const int64_t H = holder_ptr[n];
+  if (holder_ptr[0] != 0 || H < 0 || (H > 0 && !holder_idx)) return fail(e, DGP_E_ARG, "dgp_sync_tasks: holder_ptr");
+  std::vector<dgp::ev::SyncTask> rows(n);
+  bool lr = false, multi = false;
+  for (int64_t i = 0; i < n; i++) {
+    const int32_t t = task[i];
+    if (t < 0 || t >= D.N || state[i] > dgp::S_ERRED || holder_ptr[i + 1] < holder_ptr[i])
+      return fail(e, DGP_E_ARG, "dgp_sync_tasks: task / state / holder_ptr");
+    if (state[i] == dgp::S_PROCESSING && (processing_on[i] < 0 || processing_on[i] >= D.W))
+      return fail(e, DGP_E_ARG, "dgp_sync_tasks: processing task without a worker");
+    for (int64_t k = holder_ptr[i]; k < holder_ptr[i + 1]; k++)
+      if (holder_idx[k] < 0 || holder_idx[k] >= D.W) return fail(e, DGP_E_ARG, "dgp_sync_tasks: holder out of range");
+    auto& r = rows[i];
+    r = dgp::ev::SyncTask{};
+    r.t = t;
+    r.proc_on = state[i] == dgp::S_PROCESSING ? processing_on[i] : -1;
+    r.remaining = remaining[i];
+    r.waiters = waiters[i];
+    r.nbytes = nbytes[i];
+    r.hp = (int32_t)holder_ptr[i];
+    r.hn = (int32_t)(holder_ptr[i + 1] - holder_ptr[i]);
+    r.state = state[i];
+    r.lr = long_running[i] ? 1 : 0;
+    lr = lr || r.lr;
+    multi = multi || r.hn > 1;
+    // who_wants (TF_WANTED) rides on the host copy of the task flags
+    e->tflags_h[t] = (uint8_t)((e->tflags_h[t] & ~dgp::TF_WANTED) | (wanted[i] ? dgp::TF_WANTED : 0));
+    e->h_wanted[t] = wanted[i] ? 1 : 0;
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), e->tflags_h.data(), D.N, hipMemcpyHostToDevice));
+  std::vector<char*> a;
+  if (int rc = stage_args(e, {{rows.data(), rows.size() * sizeof(dgp::ev::SyncTask)}, {holder_idx, (size_t)H * 4}}, a))
+    return rc;
+  // every resync may leave replica rows and long-running tasks: the paths that honour them stay on
+  e->D.evf |= dgp::EVF_MULTI | (lr ? dgp::EVF_LR : 0);
+  (void)multi;
+  if (int rc = sync_dev(e)) return rc;
+  hipLaunchKernelGGL(dgp::ev::k_sync_tasks, dim3(grid_for(n, 256, 1024)), dim3(256), 0, e->stream, e->d_dev,
+                     (const dgp::ev::SyncTask*)a[0], (int)n, (const int32_t*)a[1]);
+  HIPCHK(e, hipGetLastError());
+  return check_device_error(e);
+}
+
+int dgp_sync_workers(dgp_engine* e, int32_t n_workers, const int8_t* status, const int32_t* nproc,
+                     const int32_t* n_long_running, const int32_t* plen, const int32_t* prefix, const int32_t* count,
+                     const int64_t* netocc, const int64_t* nbytes, const uint8_t* idle, const uint8_t* saturated,
+                     const int64_t* needs_ptr, const int32_t* needs_task, const int32_t* needs_count) {
+  if (int rc = event_ready(e, "dgp_sync_workers")) return rc;
+  dgp::Dev& D = e->D;
+  namespace S = dgp::st;
+  const int W = D.W;
+  if (n_workers != W || !status || !nproc || !n_long_running || !plen || !prefix || !count || !netocc || !nbytes ||
+      !idle || !saturated || !needs_ptr)
+    return fail(e, DGP_E_ARG, "dgp_sync_workers: one row per engine worker");
+  std::vector<int32_t> cap(W), pf((size_t)W * dgp::PMAX, 0), pc((size_t)W * dgp::PMAX, 0), pl(W);
+  std::vector<uint8_t> fl(W);
+  std::vector<int64_t> slots(W, 0);
+  std::vector<uint32_t> lines((size_t)W * S::NLW, 0), ext((size_t)W * S::NXW, 0);
+  int64_t n_idle = 0, n_sat = 0, n_itc = 0, itc_slots = 0;
+  bool paused_any = false, lr_any = false;
+  for (int w = 0; w < W; w++) {
+    if (status[w] < 0 || status[w] > 2) return fail(e, DGP_E_ARG, "dgp_sync_workers: status");
+    if (plen[w] < 0 || plen[w] > S::PD) return fail(e, DGP_E_ARG, "dgp_sync_workers: more than 8 prefixes on a worker");
+    const bool running = status[w] == 0;
+    if (!running && (idle[w] || saturated[w]))
+      return fail(e, DGP_E_ARG, "dgp_sync_workers: a worker that is not running is neither idle nor saturated");
+    if (status[w] == 2 && e->paused_h[w] != 2) D.total_nthreads -= e->nthreads[w];  // removed (:5217)
+    if (status[w] != 2 && e->paused_h[w] == 2) return fail(e, DGP_E_ARG, "dgp_sync_workers: a removed worker returns");
+    e->paused_h[w] = (uint8_t)status[w];
+    paused_any = paused_any || !running;
+    lr_any = lr_any || n_long_running[w] > 0;
+    const int32_t nt = std::max<int32_t>(e->nthreads[w], 1);
+    const int32_t base = D.sat_inf ? 0 : std::max((int32_t)std::ceil(D.saturation * nt), (int32_t)1);
+    cap[w] = base + (D.sat_inf ? 0 : n_long_running[w]);
+    pl[w] = plen[w];
+    for (int i = 0; i < plen[w]; i++) {
+      if (prefix[(size_t)w * S::PD + i] < 0 || prefix[(size_t)w * S::PD + i] >= D.P)
+        return fail(e, DGP_E_ARG, "dgp_sync_workers: prefix id");
+      pf[(size_t)w * dgp::PMAX + i] = prefix[(size_t)w * S::PD + i];
+      pc[(size_t)w * dgp::PMAX + i] = count[(size_t)w * S::PD + i];
+    }
+    const bool itc = running && (D.sat_inf || cap[w] - nproc[w] > 0);
+    fl[w] = (uint8_t)((idle[w] ? dgp::WF_IDLE : 0) | (saturated[w] ? dgp::WF_SAT : 0) | (itc ? dgp::WF_ITC : 0) |
+                      (running ? 0 : dgp::WF_PAUSED));
+    slots[w] = itc && !D.sat_inf ? cap[w] - nproc[w] : 0;
+    n_idle += idle[w] ? 1 : 0;
+    n_sat += saturated[w] ? 1 : 0;
+    n_itc += itc ? 1 : 0;
+    itc_slots += slots[w];
+    // needs_what: up to NLW - 1 entries in the line, then NXW overflow entries, then scan mode
+    const int64_t k0 = needs_ptr[w], k1 = needs_ptr[w + 1];
+    const int64_t m = k1 - k0;
+    if (k1 < k0 || (m > 0 && (!needs_task || !needs_count))) return fail(e, DGP_E_ARG, "dgp_sync_workers: needs_ptr");
+    uint32_t* L = lines.data() + (size_t)w * S::NLW;
+    if (m > (S::NLW - 1) + S::NXW) {
+      L[S::NLW - 1] = S::NL_OVF;
+    } else {
+      for (int64_t k = 0; k < m; k++) {
+        const int32_t d = needs_task[k0 + k], c = needs_count[k0 + k];
+        if (d < 0 || d >= D.N || c <= 0 || c > 255) return fail(e, DGP_E_ARG, "dgp_sync_workers: needs_what entry");
+        const uint32_t v = ((uint32_t)d << 8) | (uint32_t)c;
+        if (k < S::NLW - 1) L[k] = v;
+        else ext[(size_t)w * S::NXW + (k - (S::NLW - 1))] = v;
+      }
+      L[S::NLW - 1] = ((uint32_t)m << 8) | (m > S::NLW - 1 ? 1u : 0u);
+    }
+  }
+  // is_rootish (:2929-2947) follows total_nthreads
+  {
+    std::vector<uint8_t>& tf = e->tflags_h;
+    for (int64_t t = 0; t < D.N; t++) {
+      const int g = e->group_h[t];
+      const bool gr = e->group_sizes[g] > D.total_nthreads * 2 && e->gdep_n[g] < 5 && e->gdep_len[g] < 5;
+      const bool r = e->rootish_override_h[t] >= 0 ? e->rootish_override_h[t] != 0 : gr;
+      tf[t] = (uint8_t)((tf[t] & ~dgp::TF_ROOTISH) | (r ? dgp::TF_ROOTISH : 0));
+    }
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), e->tflags_h.data(), D.N, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_cap, cap.data(), (size_t)W * 4, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_nproc, nproc, (size_t)W * 4, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_plen, pl.data(), (size_t)W * 4, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_pfx, pf.data(), pf.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_pcnt, pc.data(), pc.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_netocc, netocc, (size_t)W * 8, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_nbytes, nbytes, (size_t)W * 8, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_flags, fl.data(), (size_t)W, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_itcslots, slots.data(), (size_t)W * 8, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.gw_needs_saved, lines.data(), lines.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.gw_needs_ext, ext.data(), ext.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_nthreads, e->nthreads.data(), (size_t)W * 4, hipMemcpyHostToDevice));
+  dgp::Ctl c;
+  if (int rc = read_ctl(e, &c)) return rc;
+  c.n_idle = n_idle;
+  c.n_sat = n_sat;
+  c.n_itc = n_itc;
+  c.itc_slots = itc_slots;
+  HIPCHK(e, hipMemcpy(e->ctl, &c, sizeof c, hipMemcpyHostToDevice));
+  if (paused_any) D.evf |= dgp::EVF_PAUSED;
+  if (lr_any) D.evf |= dgp::EVF_LR;
+  return sync_dev(e);
+}
+
+int dgp_sync_globals(dgp_engine* e, int64_t n_tasks_counter, double network_occ_global, int32_t g_plen,
+                     const int32_t* g_prefix, const int64_t* g_count, int64_t n_queued, const int32_t* queued,
+                     const double* duration_average, const double* max_exec_time, double bandwidth,
+                     const int64_t* group_released_waiting, const int64_t* group_left, const int32_t* group_last_worker) {
+  if (int rc = event_ready(e, "dgp_sync_globals")) return rc;
+  dgp::Dev& D = e->D;
+  if (g_plen < 0 || g_plen > dgp::PMAX_G || (g_plen > 0 && (!g_prefix || !g_count)) || n_queued < 0 ||
+      n_queued > D.N || (n_queued > 0 && !queued) || !duration_average || !max_exec_time || !(bandwidth > 0) ||
+      !group_released_waiting || !group_left || !group_last_worker)
+    return fail(e, DGP_E_ARG, "dgp_sync_globals: bad arguments");
+  for (int i = 0; i < g_plen; i++)
+    if (g_prefix[i] < 0 || g_prefix[i] >= D.P) return fail(e, DGP_E_ARG, "dgp_sync_globals: prefix id");
+  for (int64_t i = 0; i < n_queued; i++)
+    if (queued[i] < 0 || queued[i] >= D.N) return fail(e, DGP_E_ARG, "dgp_sync_globals: queued task");
+  for (int g = 0; g < D.G; g++)
+    if (group_last_worker[g] < -1 || group_last_worker[g] >= D.W) return fail(e, DGP_E_ARG, "dgp_sync_globals: last worker");
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  dgp::Ctl c;
+  if (int rc = read_ctl(e, &c)) return rc;
+  c.n_tasks = n_tasks_counter;
+  c.g_netocc = network_occ_global;
+  c.g_plen = g_plen;
+  for (int i = 0; i < dgp::PMAX_G; i++) {
+    c.g_pfx[i] = i < g_plen ? g_prefix[i] : 0;
+    c.g_pcnt[i] = i < g_plen ? g_count[i] : 0;
+  }
+  c.qhead = 0;
+  c.qlen = n_queued;
+  HIPCHK(e, hipMemcpy(e->ctl, &c, sizeof c, hipMemcpyHostToDevice));
+  if (n_queued) HIPCHK(e, hipMemcpy(D.qarr, queued, n_queued * 4, hipMemcpyHostToDevice));
+  for (double* p : {D.pdur_cur, D.pdur_walk, D.pdur_pre})
+    HIPCHK(e, hipMemcpy(p, duration_average, (size_t)D.P * 8, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.pmaxexec, max_exec_time, (size_t)D.P * 8, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.g_relwait, group_released_waiting, (size_t)D.G * 8, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.g_left, group_left, (size_t)D.G * 8, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.g_lastw, group_last_worker, (size_t)D.G * 4, hipMemcpyHostToDevice));
+  D.bandwidth = bandwidth;
+  return sync_dev(e);
 }
 
 int dgp_snapshot(dgp_engine* e) {

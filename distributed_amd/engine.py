@@ -274,6 +274,56 @@ class PlacementEngine:
         self._check(self.lib.dgp_task_erred(self.h, int(task), C.byref(n)), "dgp_task_erred")
         return int(n.value)
 
+    # ---------------------------------------------------------------- resync
+    def remove_worker(self, worker: int):
+        """Scheduler.remove_worker's worker table part (distributed/scheduler.py:5213-5231)."""
+        self._check(self.lib.dgp_remove_worker(self.h, int(worker)), "dgp_remove_worker")
+
+    def sync_placements(self, task, worker, comm, start, wsnbytes, route):
+        """Append placements the scheduler made itself (their run identity: log position)."""
+        a = [self._arr(task, np.int32), self._arr(worker, np.int32), self._arr(comm, np.int64),
+             self._arr(start, np.float64), self._arr(wsnbytes, np.int64), self._arr(route, np.int8)]
+        self._check(self.lib.dgp_sync_placements(self.h, len(a[0]), *[_ptr(x) for x in a]), "dgp_sync_placements")
+
+    def sync_tasks(self, rows: dict):
+        """``sync.task_rows`` -> dgp_sync_tasks."""
+        k = ("task", "state", "remaining", "waiters", "processing_on", "nbytes", "long_running", "wanted",
+             "holder_ptr", "holder_idx")
+        dts = (np.int32, np.uint8, np.int32, np.int32, np.int32, np.int64, np.uint8, np.uint8, np.int64, np.int32)
+        a = [self._arr(rows[n], d) for n, d in zip(k, dts)]
+        self._check(self.lib.dgp_sync_tasks(self.h, len(a[0]), *[_ptr(x) for x in a]), "dgp_sync_tasks")
+
+    def sync_workers(self, rows: dict):
+        """``sync.worker_rows`` -> dgp_sync_workers."""
+        k = ("status", "nproc", "n_long_running", "plen", "prefix", "count", "netocc", "nbytes", "idle", "saturated",
+             "needs_ptr", "needs_task", "needs_count")
+        dts = (np.int8, np.int32, np.int32, np.int32, np.int32, np.int32, np.int64, np.int64, np.uint8, np.uint8,
+               np.int64, np.int32, np.int32)
+        a = [self._arr(rows[n], d) for n, d in zip(k, dts)]
+        self._check(self.lib.dgp_sync_workers(self.h, len(a[0]), *[_ptr(x) for x in a]), "dgp_sync_workers")
+
+    def sync_globals(self, g: dict):
+        """``sync.global_rows`` -> dgp_sync_globals."""
+        gp, gc = self._arr(g["g_prefix"], np.int32), self._arr(g["g_count"], np.int64)
+        q = self._arr(g["queued"], np.int32)
+        da, mx = self._arr(g["duration_average"], np.float64), self._arr(g["max_exec_time"], np.float64)
+        rw, lf = self._arr(g["group_released_waiting"], np.int64), self._arr(g["group_left"], np.int64)
+        lw = self._arr(g["group_last_worker"], np.int32)
+        self._check(self.lib.dgp_sync_globals(
+            self.h, int(g["n_tasks"]), float(g["network_occ_global"]), len(gp), _ptr(gp), _ptr(gc), len(q), _ptr(q),
+            _ptr(da), _ptr(mx), float(g["bandwidth"]), _ptr(rw), _ptr(lf), _ptr(lw)), "dgp_sync_globals")
+
+    def sync(self, placements=None, tasks=None, workers=None, globals_=None):
+        """The whole resync, in the order include/dgplace.h prescribes."""
+        if placements is not None and len(placements["task"]):
+            self.sync_placements(*(placements[k] for k in ("task", "worker", "comm", "start", "wsnbytes", "route")))
+        if tasks is not None:
+            self.sync_tasks(tasks)
+        if workers is not None:
+            self.sync_workers(workers)
+        if globals_ is not None:
+            self.sync_globals(globals_)
+
     def snapshot(self):
         """Append one per-worker snapshot (service mode round boundary)."""
         self._check(self.lib.dgp_snapshot(self.h), "dgp_snapshot")

@@ -54,6 +54,8 @@ from collections import Counter, deque
 
 import numpy as np
 
+from . import sync
+
 try:  # the plugin base class when dask.distributed is importable; plain object otherwise
     from distributed.diagnostics.plugin import SchedulerPlugin
 except Exception:  # pragma: no cover - the GPU box has no dask
@@ -196,8 +198,18 @@ class GPUPlacementExtension(SchedulerPlugin):
         self._allowed: list = []  # per running wrapped stimulus: the transitions the engine follows
         self._window = None       # (allowed transitions, keys or None) after a plugin hook's stimulus
         self._expect_replicas: set = set()  # (key, address) replicas the running stimulus adds itself
+        # a stimulus the engine does not model: the scheduler decides it, then a resync
+        self.suspended = False
+        self.suspend_reason = None
+        self._host_pl: list = []    # placements the scheduler made meanwhile (dgp_sync_placements rows)
+        self._dirty: set = set()    # keys whose state the scheduler changed meanwhile
+        self._dirty_all = False
+        self._route = 0             # the decide_worker route of the scheduler's current decision
+        self.removed: set = set()   # addresses of removed workers (they keep their engine index)
         if hasattr(scheduler, "add_plugin"):
             scheduler.add_plugin(self, name=self.name)
+        elif isinstance(getattr(scheduler, "plugins", None), dict):  # a bare SchedulerState
+            scheduler.plugins[self.name] = self
         self._install()
 
     # ---------------------------------------------------------------- plumbing
@@ -216,6 +228,17 @@ class GPUPlacementExtension(SchedulerPlugin):
         table[("waiting", "processing")] = waiting_processing
         table[("queued", "processing")] = queued_processing
         s._TRANSITIONS_TABLE = table  # per instance: the class table stays untouched
+        if not getattr(s, "_gpu_placement_add", False):
+            ref_add = s._add_to_processing
+
+            def add_to_processing(ts, ws, stimulus_id):
+                if self.suspended and self.active and ts.key in self.task_index and ws.address in self.worker_index:
+                    self._host_pl.append((self.task_index[ts.key], self.worker_index[ws.address])
+                                         + sync.placement_record(s, ts, ws, self._route))
+                return ref_add(ts, ws, stimulus_id=stimulus_id)
+
+            s._add_to_processing = add_to_processing
+            s._gpu_placement_add = True
         handlers = getattr(s, "stream_handlers", None)
         if handlers is not None:
             handlers["task-finished"] = self.handle_task_finished
@@ -251,7 +274,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         modelled = frozenset(modelled)
 
         def enter(kwargs):
-            self._close_window()
+            self._enter()
             if on_event is not None and self.active and self.engine is not None:
                 try:
                     on_event(kwargs)
@@ -261,6 +284,8 @@ class GPUPlacementExtension(SchedulerPlugin):
 
         def leave():
             self._allowed.pop()
+            if self.suspended:
+                self._resync()
             self._end_of_stimulus(name)
 
         if inspect.iscoroutinefunction(orig):
@@ -274,7 +299,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         elif after:
             @functools.wraps(orig)
             def wrapped(*args, **kwargs):
-                self._close_window()
+                self._enter()
                 box = {}
 
                 def run():
@@ -291,6 +316,8 @@ class GPUPlacementExtension(SchedulerPlugin):
                     except Exception as e:
                         self.fallback(f"{name}: {e}")
                 r = box["r"] if "r" in box else run()
+                if self.suspended:
+                    self._resync()
                 self._end_of_stimulus(name)
                 return r
         else:
@@ -336,10 +363,19 @@ class GPUPlacementExtension(SchedulerPlugin):
     def _replica_event(self, ts, ws, sign):
         if not self.active or self.engine is None or ts.key not in self.task_index:
             return
+        if self.suspended:  # the resync carries it
+            self._dirty.add(ts.key)
+            return
         w = self.worker_index.get(ws.address)
         what = "add_replicas" if sign > 0 else "remove_replicas"
         if w is None:
-            self.fallback(f"{what}({ts.key!r}, {ws.address}): worker not in the engine's table")
+            self._suspend(f"{what}({ts.key!r}, {ws.address}): worker not in the engine's table")
+            self._dirty.add(ts.key)
+            return
+        if sign < 0 and len(ts.who_has or ()) <= 1:
+            # the last replica: release-worker-data recomputes the task (:5813-5815)
+            self._suspend(f"the last replica of {ts.key!r} leaves {ws.address}")
+            self._dirty.add(ts.key)
             return
         self._engine_op(what, [self.task_index[ts.key]], [w])
 
@@ -356,7 +392,10 @@ class GPUPlacementExtension(SchedulerPlugin):
         try:
             r = fn(*args)
         except Exception as e:
-            self.fallback(f"{what}: {e}")
+            if "does not model" in str(e):  # refused, nothing changed on the device
+                self._suspend(f"{what}: {e}")
+            else:
+                self.fallback(f"{what}: {e}")
             return None
         self.stats[what] += 1
         self._fetch()  # a refill the operation made (resume, long-running)
@@ -457,6 +496,70 @@ class GPUPlacementExtension(SchedulerPlugin):
         self.reason = reason
         self.pending.clear()
 
+    def _enter(self):
+        """A new stimulus starts: the previous one's window closes and, if the scheduler
+        decided it itself, the engine takes the scheduler's state first."""
+        self._close_window()
+        if self.suspended:
+            self._resync()
+
+    def _suspend(self, reason: str):
+        """The running stimulus is the scheduler's own (a change the engine does not model):
+        its remaining decisions come from the scheduler's Python and the engine resynchronises
+        from the scheduler's state when it ends (dgp_sync_*). An engine without the resync
+        entry points hands placement back for good (``fallback``)."""
+        if not self.active or self.engine is None:
+            return
+        if not all(hasattr(self.engine, m) for m in ("sync_placements", "sync_tasks", "sync_workers",
+                                                       "sync_globals")):
+            self.fallback(reason)
+            return
+        if not self.suspended:
+            logger.info("gpu-placement: the scheduler decides this stimulus, then the engine resynchronises: %s", reason)
+            self.suspended = True
+            self.suspend_reason = reason
+            self._host_pl = []
+            self.pending.clear()
+            self.stats["suspended"] += 1
+
+    def _mark_dirty(self, key):
+        """A task whose state changed under suspension, and the neighbours whose waiting_on /
+        waiters counts it moves."""
+        self._dirty.add(key)
+        ts = self.scheduler.tasks.get(key)
+        if ts is not None:
+            self._dirty.update(d.key for d in ts.dependencies)
+            self._dirty.update(d.key for d in ts.dependents)
+
+    def _resync(self):
+        """dgp_sync_placements / _tasks / _workers / _globals from the scheduler's state."""
+        s = self.scheduler
+        try:
+            pl = self._host_pl
+            cols = list(zip(*pl)) if pl else [[]] * 6
+            placements = dict(zip(("task", "worker", "comm", "start", "wsnbytes", "route"), cols))
+            keys = self.keys if self._dirty_all else [k for k in self._dirty if k in self.task_index]
+            widx = {a: i for i, a in enumerate(self.workers)}
+            tasks = sync.task_rows(s, keys, self.task_index, widx)
+            workers = sync.worker_rows(s, self.workers, self.prefix_index, self.task_index)
+            pnames = sorted(self.prefix_index, key=self.prefix_index.get)
+            gnames = sorted(self.group_index, key=self.group_index.get)
+            glob = sync.global_rows(s, pnames, self.prefix_dur, gnames, self.task_index, widx)
+            n0 = self.engine.num_placements()
+            self.engine.sync(placements, tasks, workers, glob)
+            for j, p in enumerate(pl):
+                self.dev_run[self.keys[p[0]]] = n0 + j
+            self.n_fetched = self.engine.num_placements()
+            self.stats["resyncs"] += 1
+            self.stats["resync_tasks"] += len(keys)
+        except Exception as e:
+            self.fallback(f"resync after '{self.suspend_reason}': {e}")
+        self.suspended = False
+        self._host_pl = []
+        self._dirty = set()
+        self._dirty_all = False
+        self.pending.clear()
+
     def _config(self):
         from distributed import scheduler as sched_mod
 
@@ -491,6 +594,9 @@ class GPUPlacementExtension(SchedulerPlugin):
         it in this stimulus: it stays / goes queued), or _REF (run the reference)."""
         if not self.active or self.engine is None:
             return _REF
+        if self.suspended:
+            self._route = self._route_of(sched, ts, queued)
+            return _REF
         t = self.task_index.get(ts.key)
         if t is None:
             self.fallback(f"{ts.key!r} is not in the engine's graph")
@@ -520,6 +626,18 @@ class GPUPlacementExtension(SchedulerPlugin):
             return None
         self.fallback(f"the engine did not place {ts.key!r}")
         return _REF
+
+    @staticmethod
+    def _route_of(sched, ts, queued: bool) -> int:
+        """The decide_worker route the scheduler's own decision takes (include/dgplace.h
+        DGP_ROUTE_*; the routes of tests/golden/gen_golden.py)."""
+        if queued:
+            return 1
+        if sched.is_rootish(ts):
+            return 2 if math.isinf(sched.WORKER_SATURATION) else 1
+        if ts.dependencies or sched.valid_workers(ts) is not None or len(sched.running) < len(sched.workers):
+            return 0
+        return 3
 
     def _reference_decision(self, sched, ts, queued: bool):
         if queued:
@@ -571,6 +689,8 @@ class GPUPlacementExtension(SchedulerPlugin):
         if not self.active or self.engine is None:
             return
         pair = (start, finish)
+        if start == finish:  # a decision that only recommends (queued / no-worker next): no change
+            return
         if self._allowed and pair in self._allowed[-1]:
             return
         w = self._window
@@ -578,14 +698,16 @@ class GPUPlacementExtension(SchedulerPlugin):
             return
         if key not in self.task_index:
             return  # a task the engine does not hold (scattered data, a graph it did not take)
-        self.fallback(f"transition {start} -> {finish} of {key!r} (stimulus {stimulus_id}) is not modelled "
-                      "by the engine")
+        if not self.suspended:
+            self._suspend(f"transition {start} -> {finish} of {key!r} (stimulus {stimulus_id}) is not modelled "
+                          "by the engine")
+        self._mark_dirty(key)
 
     def update_graph(self, scheduler, *, client=None, keys=(), tasks=(), annotations=None, priority=None,
                      dependencies=None, **kwargs):
         """SchedulerPlugin.update_graph (diagnostics/plugin.py:74-109): runs before the
         scheduler transitions the new tasks (scheduler.py:4641-4653)."""
-        self._close_window()
+        self._enter()
         if not self.active:
             return
         s = self.scheduler
@@ -670,7 +792,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         and makes the queue refill; the scheduler's own refill then consumes those decisions.
         The engine's worker index order must stay the scheduler's (SortedDict address) order,
         so only a worker whose address sorts after every known one joins on the device."""
-        self._close_window()
+        self._enter()
         if not self.active or self.engine is None or worker in self.worker_index:
             return
         if self.workers and worker < max(self.workers):
@@ -693,9 +815,27 @@ class GPUPlacementExtension(SchedulerPlugin):
             self.fallback(f"add_worker({worker}): {e}")
 
     def remove_worker(self, scheduler=None, worker=None, **kwargs):
+        """SchedulerPlugin.remove_worker: Scheduler.remove_worker calls it after its own
+        transitions (scheduler.py:5298-5302): the lost worker's processing tasks released and
+        re-placed, its lost results recomputed, all decided by the scheduler itself (the
+        plugin transition hook suspended the engine at the first of them). The engine marks
+        the worker removed (dgp_remove_worker; it keeps its index, so the canonical order of
+        the others stands) and takes the scheduler's state (dgp_sync_*)."""
         self._close_window()
-        if self.engine is not None and worker in self.worker_index:
-            self.fallback(f"remove_worker({worker})")
+        if not self.active or self.engine is None or worker not in self.worker_index:
+            return
+        self._suspend(f"remove_worker({worker})")
+        if not self.active:
+            return
+        w = self.worker_index.pop(worker)
+        self.removed.add(worker)
+        try:
+            self.engine.remove_worker(w)
+        except Exception as e:
+            self.fallback(f"remove_worker({worker}): {e}")
+            return
+        self.stats["workers_removed"] += 1
+        self._resync()
 
     def restart(self, scheduler=None):
         self.close_engine()
@@ -765,7 +905,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         if ts is None or ts.state != "processing" or ts.key not in self.task_index:
             return
         if ts.run_id != kw.get("run_id") or ts.retries > 0:
-            self.fallback(f"task-erred of {ts.key!r} reschedules it (stale run or retries left)")
+            self._suspend(f"task-erred of {ts.key!r} reschedules it (stale run or retries left)")
             return
         self._engine_op("task_erred", self.task_index[ts.key])
 
@@ -780,19 +920,27 @@ class GPUPlacementExtension(SchedulerPlugin):
 
     def _on_client_releases_keys(self, kw):
         """client-releases-keys / cancel-keys (:5417-5430, :5364-5396): tasks no longer
-        wanted are released or forgotten (transitions the engine does not run)."""
-        if any(k in self.task_index for k in kw.get("keys") or ()):
-            self.fallback("client-releases-keys / cancel-keys of tasks in the engine's graph")
+        wanted are released or forgotten, and who_wants changes even where nothing
+        transitions: the scheduler's own stimulus, then a resync of those keys."""
+        keys = [k for k in kw.get("keys") or () if k in self.task_index]
+        if keys:
+            self._suspend("client-releases-keys / cancel-keys")
+            for k in keys:
+                self._mark_dirty(k)
 
     def _on_close_client(self, kw):
         if self.task_index:
-            self.fallback("close-client releases the client's keys (remove_client :5727)")
+            self._suspend("close-client releases the client's keys (remove_client :5727)")
+            self._dirty_all = True
 
     def _on_update_data(self, kw):
-        """update-data (:7394-7425): scattered data; a key of the engine's graph would be
-        set to memory without a transition."""
-        if any(k in self.task_index for k in (kw.get("who_has") or {})):
-            self.fallback("update-data of a task in the engine's graph")
+        """update-data (:7394-7425): scattered data; a key of the engine's graph set to
+        memory without a transition: the scheduler's stimulus, then a resync."""
+        keys = [k for k in (kw.get("who_has") or {}) if k in self.task_index]
+        if keys:
+            self._suspend("update-data of tasks in the engine's graph")
+            for k in keys:
+                self._mark_dirty(k)
 
     def _on_set_restrictions(self, kw):
         if any(k in self.task_index for k in (kw.get("worker") or {})):
@@ -845,7 +993,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         then the reference handler for each, consuming the engine's decisions in order."""
         s = self.scheduler
         handler = type(s).handle_task_finished
-        self._close_window()
+        self._enter()
         self._end_of_stimulus("the previous stimulus")
         if self.active and self.engine is not None and msgs:
             fields = [self._message_fields(m["key"], m["worker"], m) for m in msgs]
@@ -872,4 +1020,6 @@ class GPUPlacementExtension(SchedulerPlugin):
         finally:
             self._allowed.pop()
             self._expect_replicas.clear()
+        if self.suspended:
+            self._resync()
         self._end_of_stimulus("task-finished")

@@ -43,6 +43,8 @@
  *                         :5398-5415)
  *   dgp_task_erred        Scheduler.handle_task_erred (:5799-5805 -> stimulus_task_erred
  *                         :5094-5127)
+ *   dgp_remove_worker     Scheduler.remove_worker's worker table (:5213-5231)
+ *   dgp_sync_*            the scheduler's state after a stimulus it decided itself
  *   dgp_snapshot          one per-worker snapshot (occupancy, nbytes, processing, idle /
  *                         saturated / idle_task_count, queue length) at a caller-chosen point
  *   dgp_run_rounds        the synthetic executor of the replay protocol: round k completes
@@ -244,6 +246,46 @@ int dgp_set_wanted(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t*
  * A cascade that would release a task not in memory (cancel processing or waiting work) is
  * not modelled (nothing changes). */
 int dgp_task_erred(dgp_engine* e, int32_t task, int64_t* n_new_placements);
+
+/* ---- Resynchronisation. A stimulus the engine does not model is decided by the scheduler's
+ * own Python (the extension hands that one stimulus back); afterwards the host passes the
+ * scheduler's state and the engine continues from it. In this order:
+ *   dgp_sync_placements  the placements the scheduler made meanwhile, appended to the placement
+ *                        log (_add_to_processing :3199: task, worker, worker_objective's comm
+ *                        bytes and start time, ws.nbytes, route): their run identity for
+ *                        dgp_tasks_finished is their log position
+ *   dgp_sync_tasks       rows of tasks whose state changed: TaskState.state, len(waiting_on),
+ *                        len(waiters), processing_on, nbytes (raw), long-running, who_wants
+ *                        non-empty, who_has (CSR of worker indices)
+ *   dgp_sync_workers     every worker: status (0 running, 1 paused, 2 removed: it keeps its
+ *                        index and is never a candidate), len(processing), len(long_running),
+ *                        task_prefix_count in insertion order (plen entries of prefix ids /
+ *                        counts, <= 8, row stride 8), _network_occ, nbytes, idle / saturated
+ *                        membership, needs_what (CSR of task indices and counts)
+ *   dgp_sync_globals     SchedulerState.n_tasks, _network_occ_global,
+ *                        _task_prefix_count_global (insertion order), queued (HeapSet order),
+ *                        TaskPrefix.duration_average / max_exec_time per prefix, bandwidth, per
+ *                        group states["released"] + states["waiting"],
+ *                        last_worker_tasks_left and last_worker (-1: None)
+ * dgp_remove_worker is the worker-table part of Scheduler.remove_worker (scheduler.py
+ * :5213-5231: the worker leaves workers / running / idle / idle_task_count / saturated and
+ * total_nthreads); the rest of that stimulus (its processing tasks released and re-placed,
+ * lost results recomputed, :5233-5300) is the scheduler's, synchronised as above. */
+int dgp_remove_worker(dgp_engine* e, int32_t worker);
+int dgp_sync_placements(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* comm_bytes,
+                        const double* start_time, const int64_t* ws_nbytes, const int8_t* route);
+int dgp_sync_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t* state, const int32_t* remaining,
+                   const int32_t* waiters, const int32_t* processing_on, const int64_t* nbytes,
+                   const uint8_t* long_running, const uint8_t* wanted, const int64_t* holder_ptr,
+                   const int32_t* holder_idx);
+int dgp_sync_workers(dgp_engine* e, int32_t n_workers, const int8_t* status, const int32_t* nproc,
+                     const int32_t* n_long_running, const int32_t* plen, const int32_t* prefix, const int32_t* count,
+                     const int64_t* netocc, const int64_t* nbytes, const uint8_t* idle, const uint8_t* saturated,
+                     const int64_t* needs_ptr, const int32_t* needs_task, const int32_t* needs_count);
+int dgp_sync_globals(dgp_engine* e, int64_t n_tasks_counter, double network_occ_global, int32_t g_plen,
+                     const int32_t* g_prefix, const int64_t* g_count, int64_t n_queued, const int32_t* queued,
+                     const double* duration_average, const double* max_exec_time, double bandwidth,
+                     const int64_t* group_released_waiting, const int64_t* group_left, const int32_t* group_last_worker);
 
 /* Append one worker snapshot (needs dgp_enable_snapshots): round index = number of calls
  * (update_graph's snapshot is round 0). */

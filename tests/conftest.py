@@ -17,7 +17,7 @@ def pytest_configure(config):
 def golden_files():
     """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
-                  and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcev_")))
+                  and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcev_", "svcrs_")))
 
 
 def svc_second_graph_files():
@@ -54,6 +54,11 @@ def svc_add_worker_files():
 def svc_event_files():
     """Service-mode streams with the other worker stimuli interleaved (gen_service.py events)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcev_") and f.endswith(".npz"))
+
+
+def svc_resync_files():
+    """Service streams with stimuli the scheduler decides itself, then resyncs (gen_service.py resync)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcrs_") and f.endswith(".npz"))
 
 
 def svc_steal_files():

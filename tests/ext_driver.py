@@ -437,6 +437,23 @@ class EventEngine(FixtureEngine):
     def task_erred(self, t):
         return self._event("erred", int(t))
 
+    # resync after a stimulus the scheduler decided itself (one fixture event)
+    def remove_worker(self, w):
+        self.calls.append(("remove", int(w)))
+
+    def sync(self, placements, tasks, workers, globals_):
+        n = len(placements["task"])
+        self.calls.append(("sync", n, tasks, workers, globals_))
+        k = self.stim[self.k]
+        assert n == k, (n, k)  # the scheduler's placements of that stimulus
+        self.n += k
+        self.k += 1
+
+    def sync_placements(self, *a):  # the extension calls sync(); these only mark the capability
+        raise AssertionError("sync() expected")
+
+    sync_tasks = sync_workers = sync_globals = sync_placements
+
 
 def run_events(name, plain=False):
     """A ``svcev_*`` stream (gen_service.py events): every event through the scheduler's own
@@ -447,7 +464,9 @@ def run_events(name, plain=False):
     import math as _m
 
     from gen_service import (EV_ADD_KEYS, EV_ERRED, EV_FINISHED, EV_HEARTBEAT, EV_LONG_RUNNING, EV_PAUSE,
-                             EV_RELEASE_DATA, EV_RESUME)
+                             EV_RELEASE_DATA, EV_RELEASE_KEYS, EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RESUME)
+
+    from distributed_amd import sync as dsync
 
     path = os.path.join(HERE, "golden", name)
     g, cfg, exp, meta = load_fixture(path)
@@ -467,6 +486,34 @@ def run_events(name, plain=False):
     S.send_all = lambda self, client_msgs, worker_msgs: None
     S.worker_send = lambda self, worker, msg: None
     s.extensions = {}
+    resyncs = bool((z["ev_kind"] >= EV_REMOVE_WORKER).any())
+    if resyncs:  # what Scheduler.remove_worker touches, as gen_service.replay_events sets it up
+        import asyncio
+        from collections import defaultdict
+        from types import SimpleNamespace as NS
+
+        from distributed.comm.addressing import get_address_host
+        from distributed.core import Status
+
+        S.remove_worker = Scheduler.remove_worker
+        S._reschedule = Scheduler._reschedule
+        S.client_releases_keys = Scheduler.client_releases_keys
+        S.remove_resources = lambda self, address: None
+        S.coerce_address = lambda self, a, resolve=True: a
+        s.status = Status.running
+        s.stream_comms = defaultdict(lambda: NS(send=lambda msg: None))
+        s.rpc = NS(remove=lambda a: None)
+        s.host_info = {}
+        for a, ws in s.workers.items():
+            hh = s.host_info.setdefault(get_address_host(a), {"addresses": set(), "nthreads": 0})
+            hh["addresses"].add(a)
+            hh["nthreads"] += ws.nthreads
+        s.total_nthreads_history = []
+        s.allowed_failures = 3
+        s.bandwidth_workers = {}
+        s.events = {}
+        s._ongoing_background_tasks = NS(closed=False, call_later=lambda *a, **k: None)
+        loop = asyncio.new_event_loop()
 
     def heartbeat_worker(*, address, metrics, executing=None, **kw):  # Scheduler.heartbeat_worker :4223-4252
         frac = 1 / len(s.workers)
@@ -480,9 +527,29 @@ def run_events(name, plain=False):
     eng = (FixtureEngine if plain else EventEngine)(exp, fkeys)
     ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
     eng.ext = ext
+    widx_all = dict(widx)
+    tix = {k: i for i, k in enumerate(fkeys)}
+    snap = {}
+
+    def full_rows():
+        return dsync.task_rows(s, fkeys, tix, widx_all)
+
+    if not plain:  # every resync must carry each task whose state changed since the suspension
+        orig_suspend = ext._suspend
+
+        def suspend(reason):
+            if not ext.suspended and "before" not in snap:
+                snap["before"] = full_rows()
+                snap["why"] = reason
+            return orig_suspend(reason)
+
+        ext._suspend = suspend
     s.stream_handlers = {"add-keys": s.add_keys, "release-worker-data": s.release_worker_data,
                          "worker-status-change": s.handle_worker_status_change,
                          "long-running": s.handle_long_running, "task-erred": s.handle_task_erred}
+    if resyncs:
+        s.stream_handlers["reschedule"] = s._reschedule
+        s.stream_handlers["client-releases-keys"] = s.client_releases_keys
     s.handlers = {"heartbeat_worker": heartbeat_worker}
     ext._install()
     priority = {ts.key: ts.priority for ts in tss}
@@ -492,6 +559,34 @@ def run_events(name, plain=False):
     assert ext.active, ext.reason
     s._transitions(recs, {}, {}, "update-graph")
     want = []  # the engine calls the events imply
+    n_sync = 0
+
+    def check_sync():
+        """The last engine call is the resync of this event: its worker / global rows equal
+        the fixture's dump, and every task that changed since the suspension is a row."""
+        nonlocal n_sync
+        c = eng.calls[-1]
+        assert c[0] == "sync", c[0]
+        _, npl, tasks, workers, glob = c
+        after = full_rows()
+        before = snap.pop("before")
+        snap["why_last"] = snap.pop("why", None)
+        fields = ("state", "remaining", "waiters", "processing_on", "nbytes", "long_running", "wanted")
+        hp_a, hi_a, hp_b, hi_b = after["holder_ptr"], after["holder_idx"], before["holder_ptr"], before["holder_idx"]
+        changed = {i for i in range(len(fkeys))
+                   if any(after[f][i] != before[f][i] for f in fields)
+                   or list(hi_a[hp_a[i]:hp_a[i + 1]]) != list(hi_b[hp_b[i]:hp_b[i + 1]])}
+        synced = set(tasks["task"].tolist())
+        miss = sorted(changed - synced)
+        assert not miss, [(t, {f: (before[f][t], after[f][t]) for f in fields}) for t in miss[:3]] + [snap.get("why_last")]
+        for i, t in enumerate(tasks["task"].tolist()):  # the rows sent are the scheduler's state
+            assert all(tasks[f][i] == after[f][t] for f in fields), t
+        for part, rows in (("workers", workers), ("globals", glob)):
+            for f, v in rows.items():
+                key = f"sync_{part}_{f}"
+                ptr = z[key + "_ptr"]
+                assert np.array_equal(np.atleast_1d(np.asarray(v)), z[key][ptr[n_sync]:ptr[n_sync + 1]]), (part, f)
+        n_sync += 1
     hp, ht, hd = z["hb_ptr"], z["hb_task"], z["hb_dur"]
     nbytes_bw = None
     for i, kd in enumerate(z["ev_kind"].tolist()):
@@ -538,6 +633,17 @@ def run_events(name, plain=False):
             H["task-erred"](key=ts.key, worker=addr[w], stimulus_id=sid, run_id=ts.run_id, exception=None,
                             traceback=None)
             want.append(("erred", t))
+        elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
+            if kd == EV_REMOVE_WORKER:
+                loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
+                want.append(("remove", w))
+            elif kd == EV_RESCHEDULE:
+                H["reschedule"](key=tss[t].key, worker=addr[w], stimulus_id=sid)
+            else:
+                H["client-releases-keys"](keys=[tss[t].key], client="client-0", stimulus_id=sid)
+            if not plain:
+                check_sync()
+                want.append(eng.calls[-1])
         if plain:  # an engine without the event calls: the first event hands placement back
             if kd != EV_FINISHED:
                 assert not ext.active and "not modelled" in ext.reason, (i, kd, ext.reason)
@@ -557,6 +663,8 @@ def run_events(name, plain=False):
         assert a[0] == b[0], (a, b)
         if a[0] == "long":
             assert a[1] == b[1] and (a[2] == b[2] or (_m.isnan(a[2]) and _m.isnan(b[2]))), (a, b)
+        elif a[0] == "sync":
+            assert a is b
         elif a[0] == "heartbeat":
             assert a[2] == b[2] and a[3] == b[3], (a, b)
         else:
@@ -564,9 +672,12 @@ def run_events(name, plain=False):
     assert rec["task"] == exp["pl_task"].tolist()
     assert rec["worker"] == exp["pl_worker"].tolist()
     assert np.array_equal(np.array(rec["start"]).view(np.int64), exp["pl_start"].view(np.int64))
-    assert ext.stats["device_decisions"] == n, (ext.stats, n)
+    # the resync stimuli's placements are the scheduler's own, every other one the engine's
+    host = sum(int(exp["stim_nplaced"][1 + i]) for i, kd in enumerate(z["ev_kind"].tolist()) if kd >= EV_REMOVE_WORKER)
+    assert ext.stats["device_decisions"] == n - host, (ext.stats, n, host)
     return dict(fixture=name, placements=n, events=len(want), device_decisions=ext.stats["device_decisions"],
-                active=ext.active, reason=ext.reason, calls=dict(ext.stats))
+                host_placements=host, resyncs=ext.stats["resyncs"], active=ext.active, reason=ext.reason,
+                calls=dict(ext.stats))
 
 
 if __name__ == "__main__":
@@ -578,5 +689,5 @@ if __name__ == "__main__":
     plain = "--plain" in args
     for nm in [a for a in args if not a.startswith("--")]:
         fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith("svcgraph_")
-              else (lambda x: run_events(x, plain)) if nm.startswith("svcev_") else None)
+              else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_")) else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge)), flush=True)

@@ -479,6 +479,38 @@ def main_second_graph(only):
 
 # event kinds of the svcev_* streams (tests/test_gpu_events.py, tests/ext_driver.py)
 EV_FINISHED, EV_ADD_KEYS, EV_RELEASE_DATA, EV_PAUSE, EV_RESUME, EV_LONG_RUNNING, EV_HEARTBEAT, EV_ERRED = range(8)
+# stimuli the engine does not model: the scheduler decides them, then the engine resyncs
+# (dgp_sync_*; the fixture stores the scheduler's state after each, distributed_amd/sync.py)
+EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS = 8, 9, 10
+RESYNC_KINDS = (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS)
+
+
+def _dump(s, g, tidx, widx, keys):
+    """The scheduler's state as the engine's resync rows (every task of the graph)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("dgp_sync", os.path.join(G.REPO, "distributed_amd", "sync.py"))
+    S = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(S)
+    workers = [a for a, _ in sorted(widx.items(), key=lambda kv: kv[1])]
+    return dict(tasks=S.task_rows(s, keys, tidx, widx),
+                workers=S.worker_rows(s, workers, {nm: i for i, nm in enumerate(g["prefix_names"])}, tidx),
+                globals=S.global_rows(s, list(g["prefix_names"]), list(g["prefix_default_dur"]),
+                                      list(g["group_names"]), tidx, widx))
+
+
+def _pack_dumps(dumps):
+    """The dumps of one fixture as arrays: sync_<part>_<field> concatenated over the dumps
+    with sync_<part>_<field>_ptr (each dump's slice)."""
+    out = {}
+    for part in ("tasks", "workers", "globals"):
+        for field in dumps[0][part]:
+            vals = [np.atleast_1d(np.asarray(d[part][field])) for d in dumps]
+            ptr = np.zeros(len(vals) + 1, np.int64)
+            ptr[1:] = np.cumsum([len(v) for v in vals])
+            out[f"sync_{part}_{field}"] = np.concatenate(vals)
+            out[f"sync_{part}_{field}_ptr"] = ptr
+    return out
 
 
 def _erred_is_simple(s, ts):
@@ -502,7 +534,7 @@ def _erred_is_simple(s, ts):
     return all(x is ts or x.state == "waiting" for x in closure)
 
 
-def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_scale=0.3):
+def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_scale=0.3, dumps=None):
     """The replay protocol's completions as task-finished messages, interleaved with the
     other worker stimuli that change placement inputs, each through the reference's own
     handler (``Scheduler.*`` borrowed onto the replay state):
@@ -544,6 +576,36 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
     S.send_all = lambda self, client_msgs, worker_msgs: None
     S.worker_send = lambda self, worker, msg: None
     s.extensions = {}
+    if EV_REMOVE_WORKER in kinds:  # what Scheduler.remove_worker touches besides placement state
+        import asyncio
+        from collections import defaultdict
+        from types import SimpleNamespace as NS
+
+        from distributed.core import Status
+        from distributed.comm.addressing import get_address_host
+
+        S.remove_worker = Scheduler.remove_worker
+        S.remove_resources = lambda self, address: None
+        S.coerce_address = lambda self, a, resolve=True: a
+        s.status = Status.running
+        s.stream_comms = defaultdict(lambda: NS(send=lambda msg: None))
+        s.rpc = NS(remove=lambda a: None)
+        s.host_info = {}
+        for a, ws in s.workers.items():
+            h = s.host_info.setdefault(get_address_host(a), {"addresses": set(), "nthreads": 0})
+            h["addresses"].add(a)
+            h["nthreads"] += ws.nthreads
+        s.total_nthreads_history = []
+        s.allowed_failures = 3
+        s.bandwidth_workers = {}
+        s.events = {}
+        s._ongoing_background_tasks = NS(closed=False, call_later=lambda *a, **k: None)
+        loop = asyncio.new_event_loop()
+    if EV_RESCHEDULE in kinds:
+        S._reschedule = Scheduler._reschedule
+    if EV_RELEASE_KEYS in kinds:
+        S.client_releases_keys = Scheduler.client_releases_keys
+    removed = set()
     recs = {}
     for ts in sorted(tss, key=lambda t: t.priority, reverse=True):
         recs[ts.key] = "waiting"
@@ -571,7 +633,7 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             if not mem:
                 return
             ts = mem[int(rng.integers(0, len(mem)))]
-            others = [i for i in range(W) if s.workers[addr[i]] not in ts.who_has]
+            others = [i for i in range(W) if i not in removed and s.workers[addr[i]] not in ts.who_has]
             if not others:
                 return
             w = others[int(rng.integers(0, len(others)))]
@@ -587,7 +649,7 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             s.release_worker_data(ts.key, addr[w], sid)
             push(EV_RELEASE_DATA, tidx[ts.key], w)
         elif kind == EV_PAUSE:
-            run = [i for i in range(W) if i not in paused]
+            run = [i for i in range(W) if i not in paused and i not in removed]
             if len(run) <= max(1, W // 2):
                 return
             w = run[int(rng.integers(0, len(run)))]
@@ -612,6 +674,8 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             push(EV_LONG_RUNNING, tidx[ts.key], widx[ts.processing_on.address], math.nan if cd is None else cd)
         elif kind == EV_HEARTBEAT:
             w = int(rng.integers(0, W))
+            if w in removed:
+                return
             ws = s.workers[addr[w]]
             total = float(rng.uniform(1 - bw_scale, 1 + bw_scale) * 1e8)
             # Scheduler.heartbeat_worker :4223-4226 (bandwidth EWMA)
@@ -627,6 +691,29 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
                 hb["task"].append(tidx[ts.key])
                 hb["dur"].append(d)
             push(EV_HEARTBEAT, -1, w, s.bandwidth)
+        elif kind == EV_REMOVE_WORKER:
+            live = [i for i in range(W) if i not in removed and i not in paused]
+            if len(live) <= max(2, W // 2):
+                return
+            w = live[int(rng.integers(0, len(live)))]
+            loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
+            removed.add(w)
+            push(EV_REMOVE_WORKER, -1, w)
+        elif kind == EV_RESCHEDULE:
+            proc = [ts for ts in tss if ts.state == "processing"]
+            if not proc:
+                return
+            ts = proc[int(rng.integers(0, len(proc)))]
+            w = widx[ts.processing_on.address]
+            s._reschedule(ts.key, addr[w], stimulus_id=sid)
+            push(EV_RESCHEDULE, tidx[ts.key], w)
+        elif kind == EV_RELEASE_KEYS:
+            wanted = [ts for ts in tss if ts.who_wants and ts.state in ("waiting", "processing", "queued")]
+            if not wanted:
+                return
+            ts = wanted[int(rng.integers(0, len(wanted)))]
+            s.client_releases_keys(keys=[ts.key], client="client-0", stimulus_id=sid)
+            push(EV_RELEASE_KEYS, tidx[ts.key], -1)
         elif kind == EV_ERRED:
             proc = [ts for ts in tss if ts.state == "processing" and _erred_is_simple(s, ts)]
             if not proc:
@@ -638,8 +725,20 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             assert ts.state == "erred", ts.state
             erred.add(tidx[ts.key])
             push(EV_ERRED, tidx[ts.key], w)
+        if kind in RESYNC_KINDS and ev["kind"] and ev["kind"][-1] == kind:
+            dumps.append(_dump(s, g, tidx, widx, [ts.key for ts in tss]))
         stim.append(len(rec["task"]) - n0)
 
+    run_of = []  # the reference run_id of each placement-log entry
+    orig_add = S._add_to_processing
+
+    def add_to_processing(self, ts, ws, stimulus_id):
+        r = orig_add(self, ts, ws, stimulus_id)
+        run_of.append(int(ts.run_id))
+        return r
+
+    S._add_to_processing = add_to_processing
+    run_of.extend([int(tss[t].run_id) for t in rec["task"]])  # update_graph's, already made
     while True:
         cur = len(rec["task"])
         batch = list(range(done, cur))
@@ -653,8 +752,9 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
                 event()
             t = rec["task"][pos]
             ts = tss[t]
-            if ts.state != "processing":  # erred (or a cascade released it)
-                assert ts.state == "erred", (ts.key, ts.state)
+            if ts.state != "processing":  # erred, released by a client, or re-placed (a later entry)
+                continue
+            if int(ts.run_id) != run_of[pos]:  # a later placement of the same task completes it
                 continue
             w = widx[ts.processing_on.address]
             sid = f"task-finished-{len(ev['kind'])}"
@@ -707,7 +807,43 @@ def main_events(only):
         print(f"{name}: {len(ev['kind'])} events (by kind {cnt}), {len(rec['task'])} placements")
 
 
+def main_resync(only):
+    """svcrs_*: the event streams plus the stimuli the engine does not model (worker removal,
+    rescheduling, client releases), each followed by the scheduler's state (resync rows)."""
+    kinds = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10)
+    cases = {
+        "svcrs_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=51, n_inner_prefixes=3,
+                                                            random_durations=True, nthreads="random"), 1.1, 51, 0.08),
+        "svcrs_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=52), float("inf"), 52, 0.08),
+    }
+    for name, (mk, sat, seed, p_event) in cases.items():
+        if only and name not in only:
+            continue
+        g = mk()
+        G.graphs.check_graph(g)
+        dask.config.set({"distributed.scheduler.worker-saturation": sat})
+        cfg = G.config_dict(sat)
+        dumps = []
+        rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(g, cfg, seed, p_event, kinds, dumps=dumps)
+        G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
+        path = os.path.join(HERE, f"{name}.npz")
+        z = dict(np.load(path, allow_pickle=False))
+        z.update(ev_kind=np.array(ev["kind"], np.int8), ev_task=np.array(ev["task"], np.int32),
+                 ev_worker=np.array(ev["worker"], np.int32), ev_x=np.array(ev["x"], np.float64),
+                 ev_nbytes=np.array(ev["nbytes"], np.int64), ev_start=np.array(ev["start"]),
+                 ev_stop=np.array(ev["stop"]), ev_runid=np.array(ev["runid"], np.int64),
+                 hb_ptr=np.array(hb["ptr"], np.int64), hb_task=np.array(hb["task"], np.int32),
+                 hb_dur=np.array(hb["dur"], np.float64), ev_round_ptr=np.array(round_ptr, np.int64))
+        z.update(_pack_dumps(dumps))
+        np.savez_compressed(path, **z)
+        cnt = np.bincount(np.array(ev["kind"]), minlength=11).tolist()
+        print(f"{name}: {len(ev['kind'])} events (by kind {cnt}), {len(dumps)} resyncs, {len(rec['task'])} placements, "
+              f"{os.path.getsize(path) / 1e3:.0f} kB")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "resync":
+        return main_resync(set(sys.argv[2:]))
     if len(sys.argv) > 1 and sys.argv[1] == "add-workers":
         return main_add_workers(set(sys.argv[2:]))
     if len(sys.argv) > 1 and sys.argv[1] == "second-graph":

@@ -82,6 +82,24 @@ def test_extension_follows_service_events():
             assert r["calls"].get(op, 0) > 0, (op, r)
 
 
+RESYNC = ["svcrs_c2var_sat1.1.npz", "svcrs_c2mini_satinf.npz"]
+
+
+def test_extension_resyncs_after_stimuli_it_does_not_model():
+    """Worker removal (Scheduler.remove_worker), rescheduling and client releases in the
+    stream: the plugin transition hook suspends the engine at the first transition it does
+    not model, the scheduler decides that stimulus, and the extension resynchronises the
+    engine (dgp_remove_worker, dgp_sync_*): the rows it sends cover every task whose state
+    changed (checked against a full dump), the worker / global rows equal the fixture's
+    dumps, the extension stays active and every other placement is the engine's
+    (validate=True)."""
+    res = drive(RESYNC)
+    assert [r["fixture"] for r in res] == RESYNC
+    for r in res:
+        assert r["active"] and r["resyncs"] > 0 and r["calls"]["workers_removed"] > 0, r
+        assert r["device_decisions"] + r["host_placements"] == r["placements"], r
+
+
 def test_extension_hands_back_on_unmodelled_events():
     """An engine without the event calls: the first such event ends GPU placement loudly
     ("not modelled") and the scheduler's own decisions carry on, equal to the reference's."""

@@ -20,22 +20,37 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, svc_event_files
+from conftest import GOLDEN, svc_event_files, svc_resync_files
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
 pytestmark = pytest.mark.gpu
 
 EV_FINISHED, EV_ADD_KEYS, EV_RELEASE_DATA, EV_PAUSE, EV_RESUME, EV_LONG_RUNNING, EV_HEARTBEAT, EV_ERRED = range(8)
+EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS = 8, 9, 10
 
 
-def drive_events(eng, g, z):
+def sync_dump(z, j):
+    """Resync rows number j of a svcrs_* fixture (gen_service.py _pack_dumps)."""
+    out = {"tasks": {}, "workers": {}, "globals": {}}
+    for k in z.files:
+        if not k.startswith("sync_") or (k.endswith("_ptr") and k[:-4] in z.files):
+            continue  # a field's per-dump offsets
+        part, field = k[5:].split("_", 1)
+        p = z[k + "_ptr"]
+        v = z[k][p[j]:p[j + 1]]
+        out[part][field] = v[0] if part == "globals" and field in ("n_tasks", "network_occ_global", "bandwidth") else v
+    return out
+
+
+def drive_events(eng, g, z, exp=None):
     """Every event of a svcev_* stream through the engine, snapshot per round; returns the
     placements each event made (update_graph's first)."""
     kind, task, worker, x = z["ev_kind"], z["ev_task"], z["ev_worker"], z["ev_x"]
     hp, ht, hd = z["hb_ptr"], z["hb_task"], z["hb_dur"]
     ptr = z["ev_round_ptr"].tolist()
     stim = [eng.num_placements()]
+    n_sync = 0
     for k in range(len(ptr) - 1):
         for i in range(ptr[k], ptr[k + 1]):
             n0 = eng.num_placements()
@@ -57,6 +72,17 @@ def drive_events(eng, g, z):
                 eng.heartbeat(float(x[i]), g["prefix_id"][ts], hd[hp[i]:hp[i + 1]])
             elif kd == EV_ERRED:
                 eng.task_erred(t)
+            elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
+                # the scheduler decided this stimulus itself: its placements, then its state
+                n = int(exp["stim_nplaced"][len(stim)])
+                sl = slice(n0, n0 + n)
+                eng.sync_placements(exp["pl_task"][sl], exp["pl_worker"][sl], exp["pl_comm"][sl], exp["pl_start"][sl],
+                                    exp["pl_wsnbytes"][sl], exp["pl_route"][sl])
+                if kd == EV_REMOVE_WORKER:
+                    eng.remove_worker(w)
+                d = sync_dump(z, n_sync)
+                n_sync += 1
+                eng.sync(None, d["tasks"], d["workers"], d["globals"])
             else:
                 raise AssertionError(kd)
             stim.append(eng.num_placements() - n0)
@@ -76,7 +102,7 @@ def test_service_events_match_reference(name):
     with PlacementEngine(0) as eng:
         eng.load(g, cfg, snapshots=R, results=False)
         eng.update_graph()
-        stim = drive_events(eng, g, z)
+        stim = drive_events(eng, g, z, exp)
         out = eng.placements()
         out.update(eng.snapshots(R))
         out["final_state"] = eng.task_states()
@@ -112,3 +138,33 @@ def test_service_events_refuse_what_they_do_not_model():
         with pytest.raises(_lib.DgpError, match="paused"):
             eng.add_graph(dict(h, prio=g2["prio"] + len(g["prio"]), group_id=g2["group_id"] + len(g["group_prefix"]),
                                group_prefix=np.concatenate([g["group_prefix"], g2["group_prefix"]])))
+
+
+@pytest.mark.parametrize("name", svc_resync_files())
+def test_service_resync_matches_reference(name):
+    """Worker removal (Scheduler.remove_worker, scheduler.py:5180-5360: processing tasks
+    released and re-placed, lost results recomputed), rescheduling (:7900-7927) and client
+    releases (:5417-5430) decided by the scheduler itself, the engine resynchronised from
+    its state (dgp_remove_worker, dgp_sync_*) after each, interleaved with every modelled
+    event: the engine's own decisions from then on, the snapshots and the final states equal
+    the reference's."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    assert set(np.unique(z["ev_kind"]).tolist()) == set(range(11))
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        stim = drive_events(eng, g, z, exp)
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert len(out["pl_task"]) > g["n_tasks"]  # re-placements: the logs grew
+    assert np.array_equal(stim, exp["stim_nplaced"]), np.nonzero(stim != exp["stim_nplaced"])[0][:5]
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    # a forgotten task (client released, :2853) leaves SchedulerState.tasks; its engine row
+    # stays, released (distributed_amd/sync.py)
+    assert np.array_equal(out["final_state"], np.where(exp["final_state"] == 7, 0, exp["final_state"]))
