@@ -43,7 +43,7 @@ constexpr int FL_MAX = 256;    // frontier tasks one global stimulus stages in L
 
 enum : uint8_t { S_RELEASED = 0, S_WAITING, S_PROCESSING, S_QUEUED, S_NO_WORKER, S_MEMORY, S_ERRED };
 enum : uint8_t { RF_RESTRICTED = 1, RF_LOOSE = 2 };
-enum : uint8_t { TF_WANTED = 1, TF_ROOTISH = 2 };
+enum : uint8_t { TF_WANTED = 1, TF_ROOTISH = 2, TF_FORGOTTEN = 4 };  // TF_FORGOTTEN: left SchedulerState.tasks (resync)
 // WF_PAUSED: the worker is not in SchedulerState.running (Status.paused, :5850-5883): never
 // idle / saturated / in idle_task_count, never a decide_worker candidate
 enum : uint8_t { WF_IDLE = 1, WF_SAT = 2, WF_ITC = 4, WF_PAUSED = 8 };

@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(64) k_ev_task_erred(const Dev* __restrict__ Dp
       for (int64_t k = D.dpt_ptr[x]; k < D.dpt_ptr[x + 1]; k++) {
         const int y = D.dpt_idx[k];
         const uint8_t sy = D.state[y];
-        if (sy == S_ERRED || sy == S_MEMORY) continue;
+        if (sy == S_ERRED || sy == S_MEMORY || (D.tflags[y] & TF_FORGOTTEN)) continue;  // not a dependent any more
         if (sy != S_WAITING) {
           ok = false;
           break;

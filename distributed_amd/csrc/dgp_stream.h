@@ -52,6 +52,9 @@ __constant__ Dev c_dev;
 #ifndef DGP_EXE_SLEEP
 #define DGP_EXE_SLEEP 1  // s_sleep units (64 clocks) between an idle executor's polls
 #endif
+#ifndef DGP_EXE_PF
+#define DGP_EXE_PF 1  // an idle executor loads the descriptor of the oldest waiting stimulus ahead of its claim
+#endif
 #ifndef DGP_REG_PROBES
 #define DGP_REG_PROBES 0  // registrar sub-phase s_memtime probes (diagnostics)
 #endif
@@ -68,6 +71,22 @@ constexpr int SCTA = DGP_SCTA;   // 1024: 16 waves = 5 roles + 11 executors (128
 constexpr int WIN = DGP_WIN;     // in-flight stimulus slots (LDS window; masks are u64: <= 64)
 using SMask = unsigned long long;  // a set of window slots
 static_assert(WIN >= 32 && WIN <= 64, "DGP_WIN must be in [32, 64]");
+#ifndef DGP_WAITC
+// 1: a stimulus is claimed once its completing worker and release holders are free and waits
+// in place for its frontier candidates (predc) just before its frontier; 0: claimed only
+// once every touched worker is free
+#define DGP_WAITC 1
+#endif
+constexpr bool WAITC = DGP_WAITC != 0;
+#ifndef DGP_WAITC_AHEAD
+#define DGP_WAITC_AHEAD 32  // a stimulus that would wait in place is claimed only this close to the oldest (32: any; 4 / 8 / 20 measured slower)
+#endif
+static_assert(!WAITC || WIN == 32, "DGP_WAITC keeps the candidate-only registrations in the masks' high half");
+// the mask bits of slot s: its registration (low half) and, with WAITC, the candidate-only
+// flag of this worker for s (high half)
+__host__ __device__ constexpr unsigned long long slot_bits(int s) {
+  return WAITC ? ((1ull << s) | (1ull << (s + 32))) : (1ull << s);
+}
 #ifndef DGP_RS
 #define DGP_RS 128
 #endif
@@ -323,6 +342,7 @@ struct SLds {
   int32_t ntouch[WIN];
   uint32_t flags[WIN];
   int32_t pred[WIN];
+  int32_t predc[WIN];         // WAITC: frontier candidates an earlier in-flight stimulus still holds
   long long sid[WIN];         // stimulus registered in each slot
   RMeta rmeta[RS];            // retire ring: counts of finished stimulus r at r & (RS - 1)
   long long rdone[RS];        // ... and r + 1 once they are final
@@ -1317,6 +1337,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
       L.ntouch[my_s] = nt;
       L.flags[my_s] = fl;
       L.pred[my_s] = BIG;
+      L.predc[my_s] = 0;
       L.sid[my_s] = r0 + lane;
     }
     int ntb[RB];
@@ -1343,8 +1364,11 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     for (int b = 0; b < RB; b++) {  // every lane issues: an inactive lane ORs 0 into its own word
       oldb[b] = 0;
       if (b >= nloc) break;
-      const SMask bit = 1ull << sb[b];
       const bool on = lane < ntb[b];
+      // entry 0 is the completing worker; a later entry flagged T_CAND is a frontier candidate
+      // (candidate-only: the stimulus waits for it in place, before its frontier)
+      const bool co = WAITC && lane > 0 && (TB[b] & T_CAND);
+      const SMask bit = co ? slot_bits(sb[b]) : (1ull << sb[b]);
       oldb[b] = __hip_atomic_fetch_or(&P.mask[on ? (TB[b] & T_W) : lane], on ? bit : 0ull, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -1361,7 +1385,8 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     for (int b = 0; b < RB; b++) {
       if (b >= nloc) break;
       const int c = (lane < ntb[b] && (oldb[b] & ~(1ull << sb[b])) != 0) ? 1 : 0;
-      if (c) __hip_atomic_fetch_add(&L.pred[sb[b]], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const bool co = WAITC && lane > 0 && (TB[b] & T_CAND);
+      if (c) __hip_atomic_fetch_add(co ? &L.predc[sb[b]] : &L.pred[sb[b]], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (glob_end) {  // a global stimulus waits for every in-flight stimulus on every worker
       const int sg = sb[nbat - 1];
@@ -1668,7 +1693,10 @@ __device__ __forceinline__ bool dict_update(const WPtr<LW>& P, int c, int p, int
 // release worker c of slot s: clear the slot's bit. Every bit left on c belongs to a later
 // stimulus (an earlier one holding c would have released it before s could run); the earliest
 // of them is the one waiting for s on c, and it alone counted s (role_reg): it counts down.
-__device__ __forceinline__ void release_succ(SLds& L, SMask succ) {
+// With WAITC the high half of the old mask says, per successor, whether it registered the
+// worker as a candidate only: its candidate count (predc) counts down instead.
+__device__ __forceinline__ void release_succ(SLds& L, SMask old) {
+  const SMask succ = WAITC ? (old & 0xffffffffull) : old;
   if (!succ) return;
   int bs = __builtin_ctzll(succ);
   long long best = vload(&L.sid[bs]);
@@ -1680,6 +1708,10 @@ __device__ __forceinline__ void release_succ(SLds& L, SMask succ) {
       bs = b;
     }
   }
+  if (WAITC && ((old >> 32) >> bs) & 1ull) {
+    __hip_atomic_fetch_add(&L.predc[bs], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
   if (atomicSub(&L.pred[bs], 1) == 1) {
     atomicOr(&L.c.ready, 1ull << bs);
     if (DGP_TRACE == 1) { const Dev& D = c_dev; TR(L.sid[bs], 1); }
@@ -1687,7 +1719,7 @@ __device__ __forceinline__ void release_succ(SLds& L, SMask succ) {
 }
 template <bool LW>
 __device__ __forceinline__ void release_worker(SLds& L, const WPtr<LW>& P, int s, int c) {
-  const SMask bit = 1ull << s;
+  const SMask bit = slot_bits(s);
   release_succ(L, __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
 }
 
@@ -1695,7 +1727,7 @@ __device__ __forceinline__ void release_worker(SLds& L, const WPtr<LW>& P, int s
 template <bool LW>
 __device__ __attribute__((always_inline)) void release_slot(const Dev& D, SLds& L, const WPtr<LW>& P, int s, bool all) {
   const int lane = lane_id();
-  const SMask bit = 1ull << s;
+  const SMask bit = slot_bits(s);
   auto rel = [&](int c) {
     release_succ(L, __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
   };
@@ -1785,6 +1817,8 @@ __device__ __forceinline__ DTab stim_durations(SLds& L, const uint4& E) {
 // changed) when it needs every earlier stimulus retired first (needs scan mode).
 template <bool LW>
 __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r, int qmode, bool exact, const uint4& E) {
+  // WAITC: the candidate-only workers (touch entries > 0 flagged T_CAND) may still be held by
+  // earlier stimuli when this one starts; their state is read after the wait before the frontier
   SCtl& S = L.c;
   const int lane = lane_id();
   const DTab durv = stim_durations(L, E);
@@ -1806,14 +1840,17 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   auto phase = [](int) {};
 #endif
   // ---- capacity check of the needs tables this stimulus may grow
+  const int tot_new = rl((int)E.w, 2);  // the frontier's dependency count (prefetcher)
   if (!exact) {
-    const int tot_new = rl((int)E.w, 2);  // the frontier's dependency count (prefetcher)
     const int ntch = L.ntouch[s];
     bool bad = false;
     if (lane < ntch) {
-      const int c = L.touch[s][lane] & T_W;
+      const int tv0 = L.touch[s][lane];
+      const int c = tv0 & T_W;
       const uint32_t ctl = P.needs[(size_t)c * NLW + NLW - 1];
-      bad = ctl == NL_OVF || (int)(ctl >> 8) + tot_new > NLW - 1 + NXW;
+      // a candidate-only worker's table may still grow by earlier stimuli's commits: margin
+      const int slack = (WAITC && lane > 0 && (tv0 & T_CAND)) ? NXW / 2 : 0;
+      bad = ctl == NL_OVF || (int)(ctl >> 8) + tot_new + slack > NLW - 1 + NXW;
     }
     if (ballot(bad)) return false;
   }
@@ -1829,15 +1866,16 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   const int tv = tl ? (int)L.touch[s][lane] : 0;
   const int cj = tv & T_W;
   const bool candl = (tv & T_CAND) != 0;  // a holder of a frontier task's dependency
+  const bool wc = WAITC && tl && lane > 0 && candl;  // candidate-only: read after the wait
   int np = 0, nth = 1;
   WDict dj;
   dj.c = make_uint4(0, 0, 0, 0);
   dj.c1 = make_uint4(0, 0, 0, 0);
   dj.ord = 0;
   int64_t net = 0, nbj = 0;
-  if (tl) {
+  if (tl) nth = P.nthreads[cj];  // static while stimuli run
+  if (tl && !wc) {
     np = P.nproc[cj];
-    nth = P.nthreads[cj];
     dj = dict_load<LW>(P, cj);
     net = P.netocc[cj];
     nbj = P.nbytes[cj];
@@ -1888,7 +1926,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   for (int i = 0; i < nrel; i++) {
     const int h = rl((int)E.x, RL0 + i);
     const int64_t nb = mk64(rlu(E.z, RL0 + i), rlu(E.w, RL0 + i));
-    if (tl && cj == h) nbj -= nb;
+    if (tl && !wc && cj == h) nbj -= nb;
   }
   // a release-only holder (ws.nbytes of a released dependency; no frontier candidate) is final
   // now: written back and released before the frontier
@@ -1901,6 +1939,44 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       if (ro) release_worker<LW>(L, P, s, cj);
       released = ro;
+    }
+  }
+  if (WAITC && ballot(wc)) {
+    // ---- the candidates: every earlier stimulus holding one has released it (release_succ
+    // counts predc down), then their state, with this stimulus' releases applied
+    if (vload(&L.predc[s]) != 0) {
+      if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(1);
+      while (vload(&L.predc[s]) != 0) __builtin_amdgcn_s_sleep(1);
+      if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(3);
+    }
+    lds_fence();
+    if (wc) {
+      np = P.nproc[cj];
+      dj = dict_load<LW>(P, cj);
+      net = P.netocc[cj];
+      nbj = P.nbytes[cj];
+    }
+    for (int i = 0; i < nrel; i++) {
+      const int h = rl((int)E.x, RL0 + i);
+      const int64_t nb = mk64(rlu(E.z, RL0 + i), rlu(E.w, RL0 + i));
+      if (wc && cj == h) nbj -= nb;
+    }
+    if (wc) {
+      nbw = net_bw_of(net, D);
+      occj = occ_dict_r(dj, nbw, durv, D);
+      stkj = nth1 ? occj : occj / (double)nth;
+    }
+    if (!exact) {  // the candidates' needs tables, exactly now (the claim checked them with a margin)
+      bool bad = false;
+      if (wc) {
+        const uint32_t ctl = P.needs[(size_t)cj * NLW + NLW - 1];
+        bad = ctl == NL_OVF || (int)(ctl >> 8) + tot_new > NLW - 1 + NXW;
+      }
+      if (ballot(bad)) {  // rare: continue as the oldest stimulus (every earlier one retired)
+        while (vload(&S.seq_pos) != r) __builtin_amdgcn_s_sleep(1);
+        lds_fence();
+        exact = true;
+      }
     }
   }
   phase(12);
@@ -2797,6 +2873,11 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
   // idle / gated ticks accumulate in registers (an LDS atomic per poll from every idle
   // executor contends with the working waves' LDS traffic); flushed once at exit
   unsigned long long idle28 = 0, idle29 = 0;
+  // DGP_EXE_PF: the descriptor of the oldest registered stimulus still waiting for its
+  // workers (slot pf_s), loaded while idle: the executor that claims it next has it in registers
+  long long pf_r = -1;
+  int pf_s = 0;
+  uint4 pfE = make_uint4(0, 0, 0, 0);
   while (true) {
     if (vload(&S.stop)) break;
     const SMask m = vload(&S.ready);
@@ -2804,6 +2885,18 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       const unsigned long long n = mclk();  // 28: executor idle, nothing ready
       idle28 += n - t_idle;
       t_idle = n;
+      if (DGP_EXE_PF && !(vload(&L.pred[pf_s]) > 0 && vload(&L.sid[pf_s]) == pf_r)) {
+        const long long sp = vload(&S.seq_pos);
+        const SMask fm = vload(&S.freem);
+        const bool wl = lane < WIN && !((fm >> lane) & 1ull) && vload(&L.pred[lane]) > 0;
+        const unsigned k = wl ? (unsigned)(((vload(&L.sid[lane]) - sp) << 6) | lane) : ~0u;
+        const unsigned kmin = wmin_u32(k);
+        if (kmin != ~0u) {
+          pf_s = (int)(kmin & 63u);
+          pf_r = sp + (long long)(kmin >> 6);
+          pfE = lane < NE ? D.desc[(size_t)(pf_r & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
+        }
+      }
       __builtin_amdgcn_s_sleep(DGP_EXE_SLEEP);
       continue;
     }
@@ -2812,7 +2905,11 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     const bool rdl = lane < WIN && ((m >> lane) & 1ull);
     const long long rsl = rdl ? vload(&L.sid[lane]) : 0;
     const uint32_t fsl = rdl ? vload(&L.flags[lane]) : 0u;
-    unsigned key = rdl ? (unsigned)(((rsl - sp) << 6) | lane) : ~0u;  // r - sp < RS
+    // WAITC: a stimulus whose candidates are final first (it never waits in place); the
+    // global-capable executor takes no other
+    const bool pcl = WAITC && rdl && vload(&L.predc[lane]) != 0;
+    const bool pskip = pcl && (G || rsl - sp >= DGP_WAITC_AHEAD);
+    unsigned key = rdl && !pskip ? (unsigned)((pcl ? 1u << 31 : 0u) | ((rsl - sp) << 6) | lane) : ~0u;  // r - sp < RS
     int cs = -1, cq = 0;
     long long cr = -1;
     uint32_t cf = 0;
@@ -2831,9 +2928,13 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
 #endif
       if (lane == s) key = ~0u;  // tried
       if (!G && (rlu(fsl, s) & (F_GLOBAL | F_RUNM))) continue;  // left to the global-capable executor
+      // WAITC: the global-capable executor never waits in place (it takes only stimuli whose
+      // candidates are final), so the oldest stimulus always finds an executor that runs it
+      if (G && WAITC && vload(&L.predc[s]) != 0) continue;  // (went non-final since the scan: cannot; kept as a guard)
       // the descriptor of the slot's stimulus (global ring) is in flight while the claim completes
       const long long rs = (long long)rl64((uint64_t)rsl, s);
-      E = lane < NE ? D.desc[(size_t)(rs & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
+      if (DGP_EXE_PF && rs == pf_r) E = pfE;
+      else E = lane < NE ? D.desc[(size_t)(rs & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
       // claim first, then read the slot: between the scan and the claim its stimulus may
       // have run and retired and the slot been registered again (another stimulus)
       SMask old = 0;

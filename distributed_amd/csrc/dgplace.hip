@@ -1515,7 +1515,7 @@ int dgp_sync_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t*
   bool lr = false, multi = false;
   for (int64_t i = 0; i < n; i++) {
     const int32_t t = task[i];
-    if (t < 0 || t >= D.N || state[i] > dgp::S_ERRED || holder_ptr[i + 1] < holder_ptr[i])
+    if (t < 0 || t >= D.N || state[i] > dgp::S_ERRED + 1 || holder_ptr[i + 1] < holder_ptr[i])
       return fail(e, DGP_E_ARG, "dgp_sync_tasks: task / state / holder_ptr");
     if (state[i] == dgp::S_PROCESSING && (processing_on[i] < 0 || processing_on[i] >= D.W))
       return fail(e, DGP_E_ARG, "dgp_sync_tasks: processing task without a worker");
@@ -1530,12 +1530,16 @@ int dgp_sync_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t*
     r.nbytes = nbytes[i];
     r.hp = (int32_t)holder_ptr[i];
     r.hn = (int32_t)(holder_ptr[i + 1] - holder_ptr[i]);
-    r.state = state[i];
+    // state 7 = forgotten (:2853): the row stays, released, flagged so that nothing walks it as
+    // a dependent any more (_propagate_forgotten drops it from its dependencies' dependents)
+    const bool forgotten = state[i] == dgp::S_ERRED + 1;
+    r.state = forgotten ? (uint8_t)dgp::S_RELEASED : state[i];
     r.lr = long_running[i] ? 1 : 0;
     lr = lr || r.lr;
     multi = multi || r.hn > 1;
     // who_wants (TF_WANTED) rides on the host copy of the task flags
-    e->tflags_h[t] = (uint8_t)((e->tflags_h[t] & ~dgp::TF_WANTED) | (wanted[i] ? dgp::TF_WANTED : 0));
+    e->tflags_h[t] = (uint8_t)((e->tflags_h[t] & ~(dgp::TF_WANTED | dgp::TF_FORGOTTEN)) |
+                               (wanted[i] ? dgp::TF_WANTED : 0) | (forgotten ? dgp::TF_FORGOTTEN : 0));
     e->h_wanted[t] = wanted[i] ? 1 : 0;
   }
   HIPCHK(e, hipStreamSynchronize(e->stream));

@@ -20,7 +20,7 @@ from __future__ import annotations
 import numpy as np
 
 STATE_CODES = {"released": 0, "waiting": 1, "processing": 2, "queued": 3, "no-worker": 4, "memory": 5, "erred": 6,
-               "forgotten": 0}
+               "forgotten": 7}
 PD = 8  # task_prefix_count entries per worker the engine carries (dgp_stream.h PD)
 
 
@@ -35,7 +35,8 @@ def task_rows(s, keys, task_index, worker_index) -> dict:
     for i, key in enumerate(keys):
         out["task"][i] = task_index[key]
         ts = s.tasks.get(key)
-        if ts is None:  # forgotten: released, nothing holds it
+        if ts is None:  # forgotten: gone from SchedulerState.tasks and from its dependencies' dependents
+            out["state"][i] = STATE_CODES["forgotten"]
             out["holder_ptr"][i + 1] = len(holders)
             continue
         out["state"][i] = STATE_CODES[ts.state]

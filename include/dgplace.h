@@ -254,7 +254,8 @@ int dgp_task_erred(dgp_engine* e, int32_t task, int64_t* n_new_placements);
  *                        log (_add_to_processing :3199: task, worker, worker_objective's comm
  *                        bytes and start time, ws.nbytes, route): their run identity for
  *                        dgp_tasks_finished is their log position
- *   dgp_sync_tasks       rows of tasks whose state changed: TaskState.state, len(waiting_on),
+ *   dgp_sync_tasks       rows of tasks whose state changed: TaskState.state (0-6 as dgp_task_states,
+ *                        7 = forgotten: left SchedulerState.tasks, :2853), len(waiting_on),
  *                        len(waiters), processing_on, nbytes (raw), long-running, who_wants
  *                        non-empty, who_has (CSR of worker indices)
  *   dgp_sync_workers     every worker: status (0 running, 1 paused, 2 removed: it keeps its
