@@ -915,6 +915,10 @@ int dgp_update_graph(dgp_engine* e) {
   }
   if (int rc = set_runids(e)) return rc;
   e->graph_done = true;
+  // dgp_tasks_finished counts its new placements from here
+  dgp::Ctl c;
+  if (int rc = read_ctl(e, &c)) return rc;
+  e->last_placed = c.n_placed;
   return 0;
 }
 

@@ -335,15 +335,17 @@ class PlacementEngine:
             self._check(-2, "dgp_num_placements")
         return int(n)
 
-    def placements(self, offset: int = 0, count: int | None = None) -> dict:
-        n = self.num_placements()
+    _PL_COLUMNS = (("pl_task", np.int32), ("pl_worker", np.int32), ("pl_comm", np.int64), ("pl_start", np.float64),
+                   ("pl_wsnbytes", np.int64), ("pl_route", np.int8))
+
+    def placements(self, offset: int = 0, count: int | None = None, columns=None) -> dict:
+        """Placement-log entries [offset, offset + count); ``columns``: only those (the
+        extension reads pl_task / pl_worker), one device round trip."""
         if count is None:
-            count = n - offset
-        out = dict(pl_task=np.zeros(count, np.int32), pl_worker=np.zeros(count, np.int32),
-                   pl_comm=np.zeros(count, np.int64), pl_start=np.zeros(count, np.float64),
-                   pl_wsnbytes=np.zeros(count, np.int64), pl_route=np.zeros(count, np.int8))
-        self._check(self.lib.dgp_get_placements(self.h, offset, count, *[_ptr(out[k]) for k in (
-            "pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")]), "dgp_get_placements")
+            count = self.num_placements() - offset
+        out = {k: np.zeros(count, dt) for k, dt in self._PL_COLUMNS if columns is None or k in columns}
+        self._check(self.lib.dgp_get_placements(self.h, offset, count, *[
+            _ptr(out[k]) if k in out else None for k, _ in self._PL_COLUMNS]), "dgp_get_placements")
         return out
 
     def snapshots(self, max_rounds: int) -> dict:

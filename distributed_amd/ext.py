@@ -46,6 +46,7 @@ computes the reference decision for every placement and raises on any difference
 """
 from __future__ import annotations
 
+import asyncio
 import functools
 import inspect
 import logging
@@ -239,6 +240,9 @@ class GPUPlacementExtension(SchedulerPlugin):
 
             s._add_to_processing = add_to_processing
             s._gpu_placement_add = True
+        if callable(getattr(s, "handle_stream", None)) and not getattr(s, "_gpu_placement_stream", False):
+            s.handle_stream = self.handle_stream  # per instance: Server.handle_stream stays untouched
+            s._gpu_placement_stream = True
         handlers = getattr(s, "stream_handlers", None)
         if handlers is not None:
             handlers["task-finished"] = self.handle_task_finished
@@ -569,14 +573,18 @@ class GPUPlacementExtension(SchedulerPlugin):
                 "unknown_duration": float(s.UNKNOWN_TASK_DURATION),
                 "saturation": "inf" if math.isinf(sat) else float(sat)}
 
-    def _fetch(self):
-        """Queue the engine's new placements (the decisions the transitions will ask for)."""
-        n = self.engine.num_placements()
+    def _fetch(self, n_new=None):
+        """Queue the engine's new placements (the decisions the transitions will ask for);
+        ``n_new``: how many the last engine call reported (saves a device round trip)."""
+        n = self.engine.num_placements() if n_new is None else self.n_fetched + n_new
         if n > self.n_fetched:
-            pl = self.engine.placements(self.n_fetched, n - self.n_fetched)
-            for j, (t, w) in enumerate(zip(pl["pl_task"].tolist(), pl["pl_worker"].tolist())):
-                self.pending.append((t, w))
-                self.dev_run[self.keys[t]] = self.n_fetched + j
+            pl = self.engine.placements(self.n_fetched, n - self.n_fetched, columns=("pl_task", "pl_worker"))
+            keys, dev_run, pending = self.keys, self.dev_run, self.pending
+            j = self.n_fetched
+            for t, w in zip(pl["pl_task"].tolist(), pl["pl_worker"].tolist()):
+                pending.append((t, w))
+                dev_run[keys[t]] = j
+                j += 1
             self.n_fetched = n
 
     def _end_of_stimulus(self, what: str):
@@ -984,6 +992,60 @@ class GPUPlacementExtension(SchedulerPlugin):
         a, b = _compute_interval(msg.get("startstops"))
         return t, w, run, -1 if nbytes is None else int(nbytes), a, b
 
+    async def handle_stream(self, comm, extra=None):
+        """``Server.handle_stream`` (core.py:1015-1065) for the scheduler's worker streams,
+        with one difference: the consecutive task-finished messages of one ``comm.read()``
+        batch go to the engine in ONE call (``handle_task_finished_batch``). The handlers
+        still run one message at a time, in arrival order, exactly as the reference loop
+        calls them; a batch from a comm is one worker's (handle_worker's ``extra``)."""
+        from distributed.comm.core import CommClosedError
+        from distributed.utils import iscoroutinefunction
+
+        extra = extra or {}
+        s = self.scheduler
+        try:
+            while True:
+                try:
+                    msgs = await comm.read()
+                except CommClosedError:
+                    logger.info("Connection to %s has been closed.", comm.peer_address)
+                    break
+                if not isinstance(msgs, (tuple, list)):
+                    msgs = (msgs,)
+                closed = False
+                run = []  # consecutive task-finished messages awaiting their engine call
+
+                def flush():
+                    if run:
+                        self.handle_task_finished_batch([{**extra, **m} for m in run])
+                        run.clear()
+
+                for msg in msgs:
+                    if msg == "OK":
+                        break
+                    op = msg.pop("op")
+                    if not op:
+                        logger.error("odd message %s", msg)
+                        continue
+                    if op == "close-stream":
+                        closed = True
+                        break
+                    handler = s.stream_handlers[op]
+                    if op == "task-finished" and handler == self.handle_task_finished:
+                        run.append(msg)
+                        continue
+                    flush()
+                    if iscoroutinefunction(handler):
+                        await handler(**{**extra, **msg})
+                    else:
+                        handler(**{**extra, **msg})
+                flush()
+                if closed:
+                    break
+                await asyncio.sleep(0)
+        finally:
+            await comm.close()
+
     def handle_task_finished(self, key=None, worker=None, stimulus_id=None, **msg):
         """Stream handler "task-finished" (scheduler.py:3769 -> :5783-5797)."""
         self.handle_task_finished_batch([dict(msg, key=key, worker=worker, stimulus_id=stimulus_id)])
@@ -999,15 +1061,15 @@ class GPUPlacementExtension(SchedulerPlugin):
             fields = [self._message_fields(m["key"], m["worker"], m) for m in msgs]
             cols = list(zip(*fields))
             try:
-                status, _ = self.engine.tasks_finished(*cols)
-                self._fetch()
+                status, n_new = self.engine.tasks_finished(*cols)
+                self._fetch(n_new)
                 self.stats["messages"] += len(msgs)
-                status = np.asarray(status)
+                status = status.tolist()
                 # DGP_TF_RELEASE / _IMPOSSIBLE / _UNSUPPORTED: the reference reschedules or
                 # raises; the engine does not follow those transitions
-                if np.any(status >= 3) and np.any((status != 4) & (status >= 3)):
-                    self.fallback(f"task-finished answers {sorted(set(status.tolist()))} the engine does not run")
-                for m, st in zip(msgs, status.tolist()):
+                if any(st >= 3 and st != 4 for st in status):
+                    self.fallback(f"task-finished answers {sorted(set(status))} the engine does not run")
+                for m, st in zip(msgs, status):
                     if st == 0:  # accepted: _add_to_memory adds this replica itself (:3296)
                         self._expect_replicas.add((m["key"], m["worker"]))
             except Exception as e:
@@ -1015,8 +1077,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         self._allowed.append(_STIMULUS_TRANSITIONS)
         try:
             for m in msgs:
-                m = dict(m)
-                handler(s, m.pop("key"), m.pop("worker"), m.pop("stimulus_id"), **m)
+                handler(s, **m)
         finally:
             self._allowed.pop()
             self._expect_replicas.clear()

@@ -153,13 +153,19 @@ def star(n_leaves: int, n_workers: int) -> dict:
         stop=np.full(n, 0.01), nthreads=np.ones(n_workers)))
 
 
-def shuffle_graph(n_partitions: int, n_workers: int, *, seed: int = 2) -> dict:
+def shuffle_graph(n_partitions: int, n_workers: int, *, seed: int = 2, restricted: bool = False) -> dict:
     """Config C3: the P2P-shuffle graph shape of ``distributed/shuffle/_shuffle.py:276-306``:
     P inputs -> P ``shuffle-transfer`` -> one ``shuffle-barrier`` (fan-in P) -> P
     ``shuffle-p2p`` unpack tasks, the unpacks forced non-rootish
     (``_ensure_output_tasks_are_non_rootish``, ``_scheduler_plugin.py:254-278``).
     Transfer outputs are ``int(lognormal(6, 1))`` bytes. Priorities follow a
     depth-first order: input i, transfer i, ..., barrier, unpack 0..P-1.
+
+    ``restricted``: each unpack task pinned to its output partition's worker, as the
+    shuffle plugin does at the barrier (``restrict_task`` / ``_set_restriction``,
+    ``_scheduler_plugin.py:101-115``, worker ``_get_worker_for_range_sharding``
+    ``_shuffle.py:612-617``: index ``W * i // P``): decide_worker's candidates (the
+    barrier's holder) miss the valid set, so each unpack goes to its pinned worker.
     """
     rng = np.random.default_rng(seed)
     p = int(n_partitions)
@@ -192,8 +198,18 @@ def shuffle_graph(n_partitions: int, n_workers: int, *, seed: int = 2) -> dict:
     rootish = np.full(n, -1, np.int8)
     rootish[unp] = 0
     group_names = [f"input-{TOKEN}", f"shuffle-transfer-{TOKEN}", "shuffle-barrier", f"shuffle-p2p-{TOKEN}"]
-    return _finish(dict(
-        name=f"shuffle_{p}x{n_workers}", dep_ptr=dep_ptr, dep_idx=dep_idx, prio=prio,
+    extra = {}
+    if restricted:
+        rrows = [[] for _ in range(n)]
+        for j in range(p):
+            rrows[unp[j]] = [int(n_workers) * j // p]
+        rptr, ridx = _csr_from_rows(rrows)
+        rflags = np.zeros(n, np.uint8)
+        rflags[unp] = 1
+        extra = dict(restr_ptr=rptr, restr_idx=ridx, restr_flags=rflags)
+    return _finish(dict(**extra,
+        name=f"shuffle_{p}x{n_workers}" + ("_restricted" if restricted else ""), dep_ptr=dep_ptr, dep_idx=dep_idx,
+        prio=prio,
         prefix_id=prefix_id, group_id=prefix_id.copy(), prefix_names=prefix_names,
         group_names=group_names, group_prefix=np.arange(4), prefix_default_dur=np.full(4, -1.0),
         rootish_override=rootish, nbytes=nbytes, start=np.zeros(n), stop=np.full(n, 0.01),

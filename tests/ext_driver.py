@@ -59,6 +59,7 @@ class FixtureEngine:
         self.graph = None
         self.diverge = None  # placement index whose decision is swapped with the next one
         self.graphs = []
+        self.calls_tf = 0  # dgp_tasks_finished calls the extension made
 
     def load(self, g, config, results=True):
         self.graph, self.config = g, config
@@ -67,15 +68,17 @@ class FixtureEngine:
         self.n, self.k = self.stim[0], 1
 
     def tasks_finished(self, task, worker, run_id, nbytes=None, start=None, stop=None):
+        self.calls_tf += 1
+        n0 = self.n
         for _ in task:  # genuine completions only in this protocol
             self.n += self.stim[self.k]
             self.k += 1
-        return np.zeros(len(task), np.int8), 0
+        return np.zeros(len(task), np.int8), self.n - n0
 
     def num_placements(self):
         return self.n
 
-    def placements(self, offset=0, count=None):
+    def placements(self, offset=0, count=None, columns=None):
         sl = slice(offset, offset + count)
         idx = self.ext.task_index
         task = np.array([idx[self.fkeys[t]] for t in self.exp["pl_task"][sl]], np.int32)
@@ -149,7 +152,38 @@ def check_messages(g, exp, sent, fkeys):
     assert [m["run_id"] for m in sent] == sorted(m["run_id"] for m in sent)
 
 
-def run(name, diverge=False):
+class FakeComm:
+    """A worker's batched stream as ``Server.handle_stream`` reads it: each ``read()`` returns
+    one batch (list of messages), then the comm closes."""
+
+    peer_address = "tcp://fake:0"
+
+    def __init__(self, batches):
+        self.batches = list(batches)
+        self.closed_ = False
+
+    async def read(self):
+        from distributed.comm.core import CommClosedError
+
+        if not self.batches:
+            raise CommClosedError("done")
+        return self.batches.pop(0)
+
+    async def close(self):
+        self.closed_ = True
+
+    def closed(self):
+        return self.closed_
+
+
+def run(name, diverge=False, stream=False, plain=False, validate=True):
+    """One fixture's replay protocol through the extension (or, ``plain``, through the
+    reference handlers alone, for timing). ``stream``: each round's messages arrive as
+    comm batches (consecutive messages of one worker per ``comm.read``) through the
+    extension's ``handle_stream``, one engine call per batch."""
+    import asyncio
+    import time as _time
+
     g, cfg, exp, meta = load_fixture(os.path.join(HERE, "golden", name))
     g["keys"] = None
     sat = cfg["saturation"]
@@ -172,13 +206,40 @@ def run(name, diverge=False):
 
     S._task_to_msg = task_to_msg
     fkeys = [ts.key for ts in tss]
+    if plain:  # the unmodified reference: its own decisions, its own handler
+        s.stream_handlers = {"task-finished": lambda **kw: Scheduler.handle_task_finished(s, **kw)}
+        if plain == "plugin":  # a SchedulerPlugin registered, as WorkStealing is in production
+            from distributed.diagnostics.plugin import SchedulerPlugin
+
+            s.plugins = {"noop": SchedulerPlugin()}
+        recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
+        s._transitions(recs, {}, {}, "update-graph")
+        done, n_msgs, t_msgs = 0, 0, 0.0
+        while True:
+            cur = len(rec["task"])
+            batch = rec["task"][done:cur]
+            done = cur
+            if not batch:
+                break
+            t0 = _time.perf_counter()
+            for t in batch:
+                ts = tss[t]
+                s.stream_handlers["task-finished"](
+                    key=ts.key, worker=ts.processing_on.address, stimulus_id=f"tf-{t}", run_id=ts.run_id,
+                    nbytes=int(g["nbytes"][t]), type=None, typename="int", metadata=None,
+                    startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
+            t_msgs += _time.perf_counter() - t0
+            n_msgs += len(batch)
+        assert rec["task"] == exp["pl_task"].tolist()
+        return dict(fixture=name, mode="plain" if plain is True else "plain+plugin", messages=n_msgs,
+                    us_per_message=round(1e6 * t_msgs / n_msgs, 2))
     eng = FixtureEngine(exp, fkeys)
     if diverge:  # first stimulus after update_graph with two or more placements
         stim = exp["stim_nplaced"]
         pos = np.cumsum(stim) - stim
         k = next(i for i in range(1, len(stim)) if stim[i] >= 2 and exp["pl_task"][pos[i]] != exp["pl_task"][pos[i] + 1])
         eng.diverge = int(pos[k])
-    ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
+    ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=validate)
     eng.ext = ext
     s.stream_handlers = {}
     ext._install()  # with the stream handler table in place
@@ -192,19 +253,39 @@ def run(name, diverge=False):
     s._transitions(recs, {}, {}, "update-graph")
     done = 0
     n_msgs = 0
+    n_reads = 0
+    t_msgs = 0.0
+    calls0 = ext.stats.get("messages", 0)
     while True:
         cur = len(rec["task"])
         batch = rec["task"][done:cur]
         done = cur
         if not batch:
             break
-        for t in batch:
+
+        def msg(t):
             ts = tss[t]
-            s.stream_handlers["task-finished"](
-                key=ts.key, worker=ts.processing_on.address, stimulus_id=f"tf-{t}", run_id=ts.run_id,
-                nbytes=int(g["nbytes"][t]), type=None, typename="int", metadata=None,
-                startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
-            n_msgs += 1
+            return dict(key=ts.key, stimulus_id=f"tf-{t}", run_id=ts.run_id, nbytes=int(g["nbytes"][t]), type=None,
+                        typename="int", metadata=None,
+                        startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
+        t0 = _time.perf_counter()
+        if stream:  # one comm.read per run of consecutive messages from one worker
+            runs = []
+            for t in batch:
+                w = tss[t].processing_on.address
+                if runs and runs[-1][0] == w:
+                    runs[-1][1].append(t)
+                else:
+                    runs.append((w, [t]))
+            for w, ts_ in runs:  # each worker's comm delivers its batch; the handler reads it
+                asyncio.run(ext.handle_stream(FakeComm([[dict(msg(t), op="task-finished") for t in ts_]]),
+                                              extra={"worker": w}))
+                n_reads += 1
+        else:
+            for t in batch:
+                s.stream_handlers["task-finished"](worker=tss[t].processing_on.address, **msg(t))
+        t_msgs += _time.perf_counter() - t0
+        n_msgs += len(batch)
     ext._end_of_stimulus("end of replay")
     assert ext.active != diverge, ext.reason  # a divergence hands placement back to the scheduler
     n = len(exp["pl_task"])
@@ -218,7 +299,8 @@ def run(name, diverge=False):
         check_messages(g, exp, sent, fkeys)
     return dict(fixture=name, placements=n, messages=n_msgs, device_decisions=ext.stats["device_decisions"],
                 device_queued=ext.stats["device_queued"], device_no_worker=ext.stats["device_no_worker"],
-                active=ext.active, reason=ext.reason)
+                active=ext.active, reason=ext.reason, engine_calls=eng.calls_tf, reads=n_reads,
+                us_per_message=round(1e6 * t_msgs / max(n_msgs, 1), 2), mode="stream" if stream else "handler")
 
 
 def run_joins(name):
@@ -436,6 +518,13 @@ class EventEngine(FixtureEngine):
 
     def task_erred(self, t):
         return self._event("erred", int(t))
+
+    # state the engine follows without a placement of its own (no fixture event)
+    def set_worker_flags(self, workers, idle, saturated):
+        self.calls.append(("flags", [int(x) for x in workers], [int(x) for x in idle], [int(x) for x in saturated]))
+
+    def set_wanted(self, task, wanted):
+        self.calls.append(("wanted", [int(x) for x in task], [int(x) for x in wanted]))
 
     # resync after a stimulus the scheduler decided itself (one fixture event)
     def remove_worker(self, w):
@@ -687,7 +776,10 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     diverge = "--diverge" in args
     plain = "--plain" in args
+    stream = "--stream" in args
     for nm in [a for a in args if not a.startswith("--")]:
         fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith("svcgraph_")
               else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_")) else None)
-        print(json.dumps(fn(nm) if fn else run(nm, diverge)), flush=True)
+        print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,
+                                               plain="plugin" if "--plugin" in args else plain,
+                                               validate="--novalidate" not in args)), flush=True)
