@@ -178,6 +178,50 @@ def c3_leg(eng_cls, local: int, args, link_us: float | None = None) -> dict:
     return leg
 
 
+def variant_legs(eng_cls, local: int, args) -> dict:
+    """The C2 and C3 workloads in the forms that used to fall off the stream engine: C2 with
+    16 task prefixes (15 inner + root; _calc_occupancy sums 16 prefix terms per worker in
+    dict order) and C3 with each unpack pinned to its output partition's worker (the
+    shuffle plugin's restrict_task, shuffle/_scheduler_plugin.py:101-115, range sharding
+    _shuffle.py:612-617). One replay per step after a warm-up, best of 2, checked bit-exact
+    against the oracle, whose run is the CPU baseline (1 core)."""
+    from distributed_amd import graphs
+
+    legs = {}
+    for name, g, what in (
+            ("c2_16prefixes", graphs.random_dag(args.tasks, args.workers, seed=0, n_inner_prefixes=15),
+             "C2 with 16 task prefixes"),
+            ("c3_restricted", graphs.shuffle_graph(args.c3_partitions, args.c3_workers, restricted=True),
+             "C3 with restricted unpacks (restrict_task)")):
+        eng = eng_cls(local)
+        eng.load(g, CONFIG)
+        ts = []
+        for _ in range(3):
+            eng.reset()
+            eng.update_graph()
+            t0 = time.perf_counter()
+            eng.run_rounds(-1)
+            ts.append(time.perf_counter() - t0)
+        dt = min(ts[1:])
+        out = eng.placements()
+        eng.close()
+        n = int(len(out["pl_task"]))
+        leg = {"metric": f"task placements/sec, {what}", "value": round(n / dt, 1), "unit": "placements/s",
+               "seconds_per_replay": round(dt, 4), "placements_per_replay": n, "n_tasks": int(g["n_tasks"]),
+               "n_prefixes": len(g["prefix_names"]),
+               "restricted_tasks": int((g["restr_flags"] != 0).sum()) if "restr_flags" in g else 0}
+        if not args.no_cpu_baseline:
+            from oracle import oracle
+
+            ref = oracle.replay(g, CONFIG, snapshots=False)
+            leg["cpu_baseline"] = {"value": round(len(ref["pl_task"]) / ref["seconds"], 1), "unit": "placements/s",
+                                   "cores": 1, "kind": "port", "sample": "oracle/replay.cpp, one full replay"}
+            leg["parity"] = bool(all(np.array_equal(out[k], ref[k]) for k in (
+                "pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")))
+        legs[name] = leg
+    return legs
+
+
 def service_leg(eng_cls, local: int, args) -> dict:
     """The drop-in boundary as a live scheduler drives it (service mode): a C2-shaped graph
     (random DAG, fan-in 4, sat 1.1) on 1,024 workers whose completions arrive as
@@ -298,6 +342,7 @@ def main():
     ap.add_argument("--c3-workers", type=int, default=512)
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (10M x 16k) leg")
     ap.add_argument("--no-service", action="store_true", help="skip the service-mode (dgp_tasks_finished) leg")
+    ap.add_argument("--no-variants", action="store_true", help="skip the 16-prefix C2 / restricted C3 legs")
     ap.add_argument("--svc-tasks", type=int, default=20_000)
     ap.add_argument("--c5-map", type=int, default=8_750_000)
     ap.add_argument("--c5-workers", type=int, default=16_384)
@@ -447,6 +492,8 @@ def main():
     eng.close()
     if rank == 0 and not args.no_c3:
         result["c3"] = c3_leg(PlacementEngine, local, args, result.get("latency_bound", {}).get("link_us"))
+    if rank == 0 and not args.no_variants:
+        result.update(variant_legs(PlacementEngine, local, args))
     if rank == 0 and not args.no_service:
         result["service"] = service_leg(PlacementEngine, local, args)
     if not args.no_c5:  # every rank takes part (barriers, max over ranks)

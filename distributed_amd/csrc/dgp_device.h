@@ -246,6 +246,7 @@ struct Dev {
   int32_t* fr_mark;          // stimulus whose completion empties the task's waiting_on
   int32_t* rel_mark;         // stimulus whose completion empties the task's waiters
   uint4* desc;               // descriptor ring [DR][NE]
+  double* dring;             // stimulus durations [DR][PX] when the graph has more prefixes than a descriptor carries
   int32_t* touch_ring;       // distinct workers each prefetched stimulus touches [DR][TMAX]
   uint2* thdr;               // per descriptor row: (flags, touched-worker count), written by PRE for REG
   int32_t* s2_task;  // per-slot staging of placements [WIN][PLC]

@@ -104,7 +104,9 @@ constexpr int DR = DGP_DR;       // descriptor ring (global) — how far PRE may
 constexpr int PLC = 64;          // staged placements / records per stimulus
 constexpr int KT_MAX = 24;       // dependencies of the completing task in local mode
 constexpr int KX_MAX = 8;        // dependencies of a frontier task in local mode
-constexpr int PD = 8;            // prefixes whose durations ride in the descriptor
+constexpr int RC_MAX = 8;        // decide_worker candidates of a restricted frontier task in local mode
+constexpr int PD = 8;            // entries of one worker's prefix dict (PMAX): the descriptor's 8 durations serve P <= PD
+constexpr int PX = 32;           // task prefixes the stream engine takes (P > PD: durations in rows of D.dring)
 constexpr int TMAX = 32;         // distinct workers a local stimulus may touch (more: global)
 constexpr int NLW = 12;          // needs_what words per worker in LDS: 11 entries + control
 constexpr int NXW = 52;          // overflow entries per worker (global) before scan mode
@@ -175,7 +177,7 @@ struct SCtl {
   int g_pfx[PG];
   long long g_pcnt[PG];
   double g_netocc;
-  double wdur[PD];  // prefix EWMA as of walk_pos (raw duration_average)
+  double wdur[PX];  // prefix EWMA as of walk_pos (raw duration_average)
   long long n_idle, n_sat;
   unsigned long long prof[32];
 };
@@ -337,7 +339,7 @@ struct RMeta {
 
 // LDS of the stream kernel besides the worker carve
 struct SLds {
-  double dur[SCTA / 64][PD];  // each executor wave: its stimulus' resolved prefix durations
+  double dur[SCTA / 64][PX];  // each executor wave: its stimulus' resolved prefix durations
   uint16_t touch[WIN][NE];    // distinct workers each in-flight stimulus touches (| T_CAND)
   int32_t ntouch[WIN];
   uint32_t flags[WIN];
@@ -357,18 +359,16 @@ __shared__ SLds st_L;  // the engine's LDS window + control block (namespace sco
 
 // ---------------------------------------------------------- the per-worker prefix dict
 // WorkerState.task_prefix_count is an insertion-ordered {prefix: count} with delete on
-// zero (:733-784). With P <= PD prefixes it is held as counts indexed by prefix id
-// (8 x u16 in a uint4) plus the insertion order: 3-bit prefix ids, entry i at bits
-// 3i..3i+2, and the number of entries in bits 24..31. A prefix is present iff its
-// count is non-zero, so the pair is exactly the dict.
+// zero (:733-784). Held as up to PD slots in insertion order, slot i = prefix id << 24 |
+// count (ids < 256, counts < 2^24) in 8 words (c: slots 0..3, c1: slots 4..7); ord >> 24
+// is the number of entries. A prefix is present iff it has a slot, so this is the dict.
 struct WDict {
-  uint4 c, c1;   // count of prefix p (32 bits): word p of c (p < 4) or word p - 4 of c1
-  uint32_t ord;  // insertion order
+  uint4 c, c1;   // the slots
+  uint32_t ord;  // entries << 24
 };
 __device__ __forceinline__ uint32_t wd_n(uint32_t ord) { return ord >> 24; }
-__device__ __forceinline__ int wd_id(uint32_t ord, int i) { return (int)((ord >> (3 * i)) & 7u); }
-__device__ __forceinline__ uint32_t wd_cnt(const WDict& d, int p) {
-  switch (p & 7) {
+__device__ __forceinline__ uint32_t wd_slot(const WDict& d, int i) {
+  switch (i & 7) {
     case 0: return d.c.x;
     case 1: return d.c.y;
     case 2: return d.c.z;
@@ -379,8 +379,8 @@ __device__ __forceinline__ uint32_t wd_cnt(const WDict& d, int p) {
     default: return d.c1.w;
   }
 }
-__device__ __forceinline__ void wd_set(WDict& d, int p, uint32_t v) {
-  switch (p & 7) {
+__device__ __forceinline__ void wd_put(WDict& d, int i, uint32_t v) {
+  switch (i & 7) {
     case 0: d.c.x = v; break;
     case 1: d.c.y = v; break;
     case 2: d.c.z = v; break;
@@ -391,34 +391,61 @@ __device__ __forceinline__ void wd_set(WDict& d, int p, uint32_t v) {
     default: d.c1.w = v; break;
   }
 }
+__device__ __forceinline__ int wd_find(const WDict& d, int p) {  // slot of prefix p, -1: absent
+  const uint32_t n = wd_n(d.ord);
+  int k = -1;
+#pragma unroll
+  for (int i = 0; i < PD; i++)
+    if ((uint32_t)i < n && (wd_slot(d, i) >> 24) == (uint32_t)p) k = i;
+  return k;
+}
+__device__ __forceinline__ uint32_t wd_cnt(const WDict& d, int p) {
+  const int k = wd_find(d, p);
+  return k < 0 ? 0u : (wd_slot(d, k) & 0xffffffu);
+}
+// count of prefix p := v > 0 (its slot, or a new one appended)
+__device__ __forceinline__ void wd_set(WDict& d, int p, uint32_t v) {
+  int k = wd_find(d, p);
+  if (k < 0) {
+    k = (int)wd_n(d.ord);
+    d.ord += 1u << 24;
+  }
+  wd_put(d, k, ((uint32_t)p << 24) | (v & 0xffffffu));
+}
 
 // add_to_processing (+1) / remove_from_processing (-1) of one task of prefix p
 __device__ __forceinline__ bool dict_add(WDict& d, int p, int delta) {
-  const uint32_t cnt = wd_cnt(d, p);
-  uint32_t wv = cnt;
+  const int k = wd_find(d, p);
   const uint32_t n = wd_n(d.ord);
   if (delta > 0) {
-    if (cnt == 0xffffffffu) return false;
-    if (cnt == 0) d.ord = (d.ord + (1u << 24)) | ((uint32_t)p << (3 * n));  // new key: appended
-    wv += 1u;
-  } else {
-    if (cnt == 0) return true;
-    wv -= 1u;
-    if (cnt == 1) {  // count reached zero: the key leaves, later keys move up
-      int k = 0;
-#pragma unroll
-      for (int i = 0; i < PD; i++)
-        if ((uint32_t)i < n && wd_id(d.ord, i) == p) k = i;
-      const uint32_t ids = d.ord & 0xffffffu, lowm = (1u << (3 * k)) - 1u;
-      d.ord = (ids & lowm) | ((ids >> 3) & ~lowm) | ((n - 1) << 24);
+    if (k >= 0) {
+      const uint32_t v = wd_slot(d, k);
+      if ((v & 0xffffffu) == 0xffffffu) return false;
+      wd_put(d, k, v + 1u);
+      return true;
     }
+    if (n >= (uint32_t)PD || p < 0 || p > 255) return false;
+    wd_put(d, (int)n, ((uint32_t)p << 24) | 1u);  // new key: appended
+    d.ord += 1u << 24;
+    return true;
   }
-  wd_set(d, p, wv);
+  if (k < 0) return true;
+  const uint32_t v = wd_slot(d, k);
+  if ((v & 0xffffffu) > 1u) {
+    wd_put(d, k, v - 1u);
+    return true;
+  }
+  // count reached zero: the key leaves, later keys move up
+#pragma unroll
+  for (int i = 0; i < PD - 1; i++)
+    if (i >= k) wd_put(d, i, wd_slot(d, i + 1));
+  wd_put(d, PD - 1, 0u);
+  d.ord -= 1u << 24;
   return true;
 }
 
-// prefix durations: a table of PD doubles in LDS (a descriptor's entries 3..6, or the
-// walker's wdur), read by prefix id
+// prefix durations: a table of PX doubles in LDS (a descriptor's entries 3..6 or a D.dring
+// row, or the walker's wdur), read by prefix id
 using DTab = const __attribute__((address_space(3))) double*;
 
 __device__ __forceinline__ double resolve_dur(const Dev& D, double d, int p) {  // _calc_occupancy :1892-1899
@@ -434,9 +461,10 @@ __device__ __forceinline__ double occ_dict(const WDict& d, int64_t netocc, DTab 
 #pragma unroll
   for (int i = 0; i < PD; i++) {
     if (!ballot((uint32_t)i < n)) break;
-    const int p = wd_id(d.ord, i);
+    const uint32_t v = wd_slot(d, i);
+    const int p = (int)(v >> 24) & (PX - 1);
     const double dv = dt[p];
-    const double term = resolve_dur(D, dv, p) * (double)wd_cnt(d, p);
+    const double term = resolve_dur(D, dv, p) * (double)(v & 0xffffffu);
     if ((uint32_t)i < n) res += term;
   }
   return res + (double)netocc / (double)D.bandwidth;
@@ -451,9 +479,9 @@ __device__ __forceinline__ double occ_dict_r(const WDict& d, double net_bw, DTab
 #pragma unroll
   for (int i = 0; i < PD; i++) {
     if (!ballot((uint32_t)i < n)) break;
-    const int p = wd_id(d.ord, i);
-    const double dv = dt[p];
-    const double term = (dv < 0 ? D.unknown_duration : dv) * (double)wd_cnt(d, p);
+    const uint32_t v = wd_slot(d, i);
+    const double dv = dt[(v >> 24) & (PX - 1)];
+    const double term = (dv < 0 ? D.unknown_duration : dv) * (double)(v & 0xffffffu);
     if ((uint32_t)i < n) res += term;
   }
   return res + net_bw;
@@ -495,29 +523,41 @@ __device__ __forceinline__ bool stalled_for(unsigned long long since, unsigned l
 }
 
 __device__ __forceinline__ int64_t nbv(const Dev& D, int64_t v) { return v >= 0 ? v : D.default_data_size; }
+// w in valid_workers(ts) (:3043-3107) as resolved on the host: task x's restriction row (ascending)
+__device__ __forceinline__ bool restr_has(const Dev& D, int x, int w) {
+  int64_t lo = D.restr_ptr[x], hi = D.restr_ptr[x + 1];
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (D.restr_idx[mid] < w) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < D.restr_ptr[x + 1] && D.restr_idx[lo] == w;
+}
 
 // ============================================================ walker (records -> flags)
-// SchedulerState globals folded in record order, held in registers (uniform over lanes;
-// lane p holds the raw duration_average of prefix p).
+// SchedulerState globals folded in record order, held in registers: the insertion-ordered
+// _task_prefix_count_global with entry i in lane i, lane p holding the raw duration_average
+// of prefix p; the rest uniform over lanes.
 struct WState {
-  int n;             // _task_prefix_count_global, insertion ordered
-  int pf[PD];
-  long long cnt[PD];
+  int n;             // _task_prefix_count_global entries (uniform)
+  int pf;            // lane i < n: prefix id of entry i
+  long long cnt;     // lane i < n: its count
   double netocc;     // _network_occ_global (holds integers < 2^53: exact in any order)
   double wd;         // lane p: TaskPrefix.duration_average
   long long n_idle, n_sat;
 };
+static_assert(PG == 64 && PX <= 64, "one lane per global dict entry / per prefix");
+
+__device__ __forceinline__ int64_t rl_i64(int64_t v, int l) { return mk64(rlu(lo32(v), l), rlu(hi32(v), l)); }
+__device__ __forceinline__ double rl_f64(double v, int l) { return mkd(rlu(dlo(v), l), rlu(dhi(v), l)); }
 
 __device__ __forceinline__ void ws_load(const SCtl& S, WState& g) {
   const int lane = lane_id();
   g.n = S.g_plen;
-#pragma unroll
-  for (int i = 0; i < PD; i++) {
-    g.pf[i] = S.g_pfx[i];
-    g.cnt[i] = S.g_pcnt[i];
-  }
+  g.pf = S.g_pfx[lane];
+  g.cnt = S.g_pcnt[lane];
   g.netocc = S.g_netocc;
-  g.wd = S.wdur[lane & (PD - 1)];
+  g.wd = S.wdur[lane & (PX - 1)];
   g.n_idle = S.n_idle;
   g.n_sat = S.n_sat;
 }
@@ -525,64 +565,58 @@ __device__ __forceinline__ void ws_store(SCtl& S, const WState& g) {
   const int lane = lane_id();
   if (lane == 0) {
     S.g_plen = g.n;
-#pragma unroll
-    for (int i = 0; i < PD; i++) {
-      S.g_pfx[i] = g.pf[i];
-      S.g_pcnt[i] = g.cnt[i];
-    }
     S.g_netocc = g.netocc;
     S.n_idle = g.n_idle;
     S.n_sat = g.n_sat;
   }
-  if (lane < PD) S.wdur[lane] = g.wd;
+  S.g_pfx[lane] = g.pf;
+  S.g_pcnt[lane] = g.cnt;
+  if (lane < PX) S.wdur[lane] = g.wd;
 }
 __device__ __forceinline__ bool gdict_add(WState& g, int p, int delta) {
-  int at = -1;
-#pragma unroll
-  for (int i = 0; i < PD; i++)
-    if (at < 0 && i < g.n && g.pf[i] == p) at = i;
+  const int lane = lane_id();
+  const unsigned long long m = ballot(lane < g.n && g.pf == p);
   if (delta > 0) {
-    if (at >= 0) {
-#pragma unroll
-      for (int i = 0; i < PD; i++)
-        if (i == at) g.cnt[i]++;
+    if (m) {
+      if (lane == __builtin_ctzll(m)) g.cnt++;
       return true;
     }
-    if (g.n >= PD) return false;
-#pragma unroll
-    for (int i = 0; i < PD; i++)
-      if (i == g.n) {
-        g.pf[i] = p;
-        g.cnt[i] = 1;
-      }
+    if (g.n >= PG) return false;
+    if (lane == g.n) {
+      g.pf = p;
+      g.cnt = 1;
+    }
     g.n++;
     return true;
   }
-  if (at < 0) return true;
-  long long v = 0;
-#pragma unroll
-  for (int i = 0; i < PD; i++)
-    if (i == at) v = --g.cnt[i];
-  if (v == 0) {
-#pragma unroll
-    for (int i = 0; i < PD - 1; i++)
-      if (i >= at && i + 1 < g.n) {
-        g.pf[i] = g.pf[i + 1];
-        g.cnt[i] = g.cnt[i + 1];
-      }
-    g.n--;
+  if (!m) return true;
+  const int at = __builtin_ctzll(m);
+  const long long v = rl_i64(g.cnt, at) - 1;
+  if (v > 0) {
+    if (lane == at) g.cnt = v;
+    return true;
   }
+  // the entry leaves: later entries move up one lane
+  const int pn = __shfl_down(g.pf, 1);
+  const long long cn = __shfl_down(g.cnt, 1);
+  if (lane >= at) {
+    g.pf = pn;
+    g.cnt = cn;
+  }
+  g.n--;
   return true;
+}
+// lane p: prefix p's duration as _calc_occupancy resolves it
+__device__ __forceinline__ double ws_lane_dur(const Dev& D, const WState& g) {
+  const int lane = lane_id();
+  return lane < D.P ? resolve_dur(D, g.wd, lane) : -1.0;
 }
 // SchedulerState.total_occupancy :1877 (prefix dict order)
 __device__ __forceinline__ double ws_total_occ(const Dev& D, const WState& g) {
-  const double rv = resolve_dur(D, g.wd, lane_id() & (PD - 1));
+  const double dv = __shfl(ws_lane_dur(D, g), g.pf & 63);  // entry lane: its prefix's duration
+  const double term = dv * (double)g.cnt;
   double res = 0.0;
-#pragma unroll
-  for (int i = 0; i < PD; i++) {
-    const double dv = __shfl(rv, g.pf[i] & (PD - 1));
-    if (i < g.n) res += dv * (double)g.cnt[i];
-  }
+  for (int i = 0; i < g.n; i++) res += rl_f64(term, i);
   return res + g.netocc / (double)D.bandwidth;
 }
 
@@ -649,24 +683,25 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
   const bool in = lane < m;
   const int kind = rc.kind, w = rc.w, p = rc.p, np = rc.nproc;
   // (a) durations unchanged: every completion's EWMA result equals the current value
-  const double cur = __shfl(g.wd, p & (PD - 1));
+  const double cur = __shfl(g.wd, p & 63);
   const double nw = cur < 0 ? rc.dur : 0.5 * rc.dur + 0.5 * cur;
   bool bad = in && kind != K_PLACE && rc.dur == rc.dur && __double_as_longlong(nw) != __double_as_longlong(cur);
-  // (b) prefix counts stay >= 1 and every record's prefix is in the dict
+  // (b) prefix counts stay >= 1 and every record's prefix is in the dict; meanwhile each
+  // record lane's prefix terms of total_occupancy in dict order (used when not bad)
   bool found = !in;
-  long long cnt_i[PD];
-  long long tot[PD];
-#pragma unroll
-  for (int k = 0; k < PD; k++) {
-    cnt_i[k] = 0;
-    tot[k] = 0;
-    if (k >= g.n) continue;
-    const long long dl = (in && p == g.pf[k]) ? (kind == K_COMPLETE ? -1 : kind == K_PLACE ? 1 : 0) : 0;
-    if (in && p == g.pf[k]) found = true;
+  long long tot_mine = 0;  // entry lane k: the batch's count change of entry k
+  const double dvl = __shfl(ws_lane_dur(D, g), g.pf & 63);  // entry lane k: its prefix's duration
+  double tocc = 0.0;
+  for (int k = 0; k < g.n; k++) {
+    const int pk = rl(g.pf, k);
+    const bool mine = in && p == pk;
+    const long long dl = mine ? (kind == K_COMPLETE ? -1 : kind == K_PLACE ? 1 : 0) : 0;
+    if (mine) found = true;
     const long long inc = wscan_incl(dl);
-    cnt_i[k] = g.cnt[k] + inc;
-    tot[k] = rl(inc, 63);
-    if (in && cnt_i[k] < 1) bad = true;
+    const long long cik = rl_i64(g.cnt, k) + inc;
+    if (lane == k) tot_mine = rl_i64(inc, 63);
+    if (in && cik < 1) bad = true;
+    tocc += rl_f64(dvl, k) * (double)cik;
   }
   if (!found) bad = true;
   if (ballot(bad)) {
@@ -680,13 +715,6 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
   }
   const long long dn_inc = wscan_incl(in ? (long long)rc.dnet : 0);
   const double netocc_i = g.netocc + (double)dn_inc;
-  const double rv = resolve_dur(D, g.wd, lane & (PD - 1));
-  double tocc = 0.0;
-#pragma unroll
-  for (int k = 0; k < PD; k++) {
-    const double dv = __shfl(rv, g.pf[k] & (PD - 1));
-    if (k < g.n) tocc += dv * (double)cnt_i[k];
-  }
   tocc = tocc + netocc_i / (double)D.bandwidth;
   // check_idle_saturated's idle / saturated part for the record's worker
   const long long nt = in ? (long long)P.nthreads[w] : 1;
@@ -715,9 +743,7 @@ __device__ __attribute__((always_inline)) void ws_fold_batch(const Dev& D, const
   }
   g.n_idle += wsum(di);
   g.n_sat += wsum(ds);
-#pragma unroll
-  for (int k = 0; k < PD; k++)
-    if (k < g.n) g.cnt[k] += tot[k];
+  if (lane < g.n) g.cnt += tot_mine;
   g.netocc += (double)mk64(rlu(lo32(dn_inc), 63), rlu(hi32(dn_inc), 63));
 }
 
@@ -1148,15 +1174,51 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
       flags |= F_GLOBAL;
       continue;
     }
-    E[n++] = make_uint4((unsigned)x, (unsigned)D.prefix[x], (unsigned)kx, (unsigned)D.group[x]);
+    // a restricted task (f1): decide_worker's candidates (:8575-8586) resolved here —
+    // holders & valid; none: the valid set; valid empty: loose -> the holders, else
+    // no-worker (global). They follow the dependency entries; the holders are not touched
+    const bool rx = restricted_nonrootish(D, x);
+    int cw[RC_MAX];
+    int nc = 0;
+    if (rx) {
+      for (int64_t q = x0; q < x1 && nc >= 0; q++) {
+        const int hd = D.holder_of[D.dep_idx[q]];
+        bool dup = false;
+        for (int i = 0; i < nc; i++) dup = dup || cw[i] == hd;
+        if (!dup && hd >= 0 && hd < D.W && restr_has(D, x, hd)) cw[nc++] = hd;
+      }
+      const int64_t r0 = D.restr_ptr[x], r1 = D.restr_ptr[x + 1];
+      if (nc == 0 && r1 > r0) {
+        if (r1 - r0 > RC_MAX) nc = -1;
+        else for (int64_t i = r0; i < r1; i++) cw[nc++] = D.restr_idx[i];
+      } else if (nc == 0) {
+        if (!(D.restr_flags[x] & RF_LOOSE)) nc = -1;  // no-worker
+        else for (int64_t q = x0; q < x1; q++) {       // decide_worker without restrictions
+          const int hd = D.holder_of[D.dep_idx[q]];
+          bool dup = false;
+          for (int i = 0; i < nc; i++) dup = dup || cw[i] == hd;
+          if (!dup) cw[nc++] = hd;
+        }
+      }
+      if (nc < 0 || n + 1 + kx + nc > NE) {
+        flags |= F_GLOBAL;
+        continue;
+      }
+    }
+    E[n++] = make_uint4((unsigned)x, (unsigned)D.prefix[x], (unsigned)(kx | (nc << 8) | (rx ? 1 << 16 : 0)),
+                        (unsigned)D.group[x]);
     sumkx += kx;
     for (int64_t q = x0; q < x1; q++) {
       const int d = D.dep_idx[q];
       const int64_t nb = nbv(D, D.res_nbytes[d]);
       const int hd = D.holder_of[d];
       if ((D.evf & EVF_MULTI) && (D.tdyn[d] & TD_MULTI)) evg = true;
-      touch(hd, true);
+      if (!rx) touch(hd, true);
       E[n++] = make_uint4((unsigned)d, (unsigned)hd, lo32(nb), hi32(nb));
+    }
+    for (int i = 0; i < nc; i++) {
+      touch(cw[i], true);
+      E[n++] = make_uint4((unsigned)cw[i], 0u, 0u, 0u);
     }
   }
   if (!(flags & F_GLOBAL) && (nf > 255 || nt > TMAX || nf + (D.sat_inf ? 0 : D.w_cap[w]) + 1 > PLC))
@@ -1166,7 +1228,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   if (tbad) flags |= F_GLOBAL | F_BADTOUCH;
   if (evg) flags |= F_GLOBAL;
   if (!(flags & F_GLOBAL) && nt == 1 && nf == 0 && kt <= 1 && nrel <= 1 &&
-      (kt == 0 || h_dep0 == w))
+      (kt == 0 || h_dep0 == w) && D.P <= PD)  // a run shares the head's descriptor durations
     flags |= F_SIMPLE;
   if (flags & F_GLOBAL) nt = 0;
   int32_t* T = D.touch_ring + (size_t)(r & (DR - 1)) * TMAX;
@@ -1190,7 +1252,7 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
   SCtl& S = L.c;
   const int lane = lane_id();
   // PRE: lane p holds TaskPrefix.duration_average of prefix p as of pre_pos
-  double dur = (KIND == 1 && lane < PD && lane < D.P) ? D.pdur_pre[lane] : -1.0;
+  double dur = (KIND == 1 && lane < PX && lane < D.P) ? D.pdur_pre[lane] : -1.0;
   while (true) {
     if (vload(&S.stop)) break;
     const long long a = KIND == 0 ? S.bld_pos : S.pre_pos;
@@ -1219,7 +1281,11 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
         const int pi = rl(pl, i);
         const double di = mkd(rlu(dlo(dl), i), rlu(dhi(dl), i));
         if (lane == pi && di == di) dur = dur < 0 ? di : 0.5 * di + 0.5 * dur;  // NaN: no compute interval
-        if (lane < PD) ((double*)(D.desc + (size_t)((a + i) & (DR - 1)) * NE + 3))[lane] = resolve_dur(D, dur, lane);
+        if (D.P <= PD) {
+          if (lane < PD) ((double*)(D.desc + (size_t)((a + i) & (DR - 1)) * NE + 3))[lane] = lane < D.P ? resolve_dur(D, dur, lane) : -1.0;
+        } else if (lane < D.P) {
+          D.dring[(size_t)((a + i) & (DR - 1)) * PX + lane] = resolve_dur(D, dur, lane);
+        }
       }
     }
     __threadfence_block();
@@ -1230,7 +1296,7 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
       vstore(KIND == 0 ? &S.bld_pos : &S.pre_pos, e);
     }
   }
-  if (KIND == 1 && lane < PD && lane < D.P) D.pdur_pre[lane] = dur;
+  if (KIND == 1 && lane < PX && lane < D.P) D.pdur_pre[lane] = dur;
 }
 
 // ===================================================================== registrar
@@ -1803,12 +1869,16 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
 
 // the resolved durations of a stimulus (descriptor entries 3..6, in lanes 3..6 of E) into
 // the executor wave's LDS table, read by prefix id (one wave's LDS operations run in order)
-__device__ __forceinline__ DTab stim_durations(SLds& L, const uint4& E) {
+__device__ __forceinline__ DTab stim_durations(const Dev& D, SLds& L, const uint4& E, long long r) {
   const int lane = lane_id();
   const auto t = (__attribute__((address_space(3))) double*)(double*)L.dur[threadIdx.x >> 6];
-  if (lane >= 3 && lane < 7) {
-    t[2 * (lane - 3)] = mkd(E.x, E.y);
-    t[2 * (lane - 3) + 1] = mkd(E.z, E.w);
+  if (D.P <= PD) {
+    if (lane >= 3 && lane < 7) {
+      t[2 * (lane - 3)] = mkd(E.x, E.y);
+      t[2 * (lane - 3) + 1] = mkd(E.z, E.w);
+    }
+  } else if (lane < D.P) {  // more prefixes than the descriptor carries: the stimulus' row
+    t[lane] = D.dring[(size_t)(r & (DR - 1)) * PX + lane];
   }
   return (DTab)(const double*)t;
 }
@@ -1821,7 +1891,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   // earlier stimuli when this one starts; their state is read after the wait before the frontier
   SCtl& S = L.c;
   const int lane = lane_id();
-  const DTab durv = stim_durations(L, E);
+  const DTab durv = stim_durations(D, L, E, r);
   const int t = rl((int)E.x, 0), w = rl((int)E.y, 0), p = rl((int)E.z, 0);
   const uint32_t flags = rlu(E.w, 0);
   const int64_t nbt = mk64(rlu(E.x, 1), rlu(E.y, 1));
@@ -1984,7 +2054,9 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   // ------------------------------ frontier in ascending priority: decide_worker (:8550)
   int off = FX0;
   for (int j = 0; j < nf; j++) {
-    const int x = rl((int)E.x, off), px = rl((int)E.y, off), kx = rl((int)E.z, off) & 0xff;
+    const int x = rl((int)E.x, off), px = rl((int)E.y, off);
+    const int hz = rl((int)E.z, off);
+    const int kx = hz & 0xff, nc = (hz >> 8) & 0xff;  // nc: a restricted task's resolved candidates
     const int gx = rl((int)E.w, off);
     // candidates = the holders of x's dependencies (each a touched lane); comm_bytes (:3136)
     int64_t comm = 0;
@@ -1995,6 +2067,10 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       const int64_t nbi = mk64(rlu(E.z, L2), rlu(E.w, L2));
       if (cj == hi) cand = true;
       else comm += nbi;
+    }
+    if (hz & (1 << 16)) {  // restricted: the candidates PRE resolved (:8575-8586)
+      cand = false;
+      for (int i = 0; i < nc; i++) cand = cand || cj == rl((int)E.x, off + 1 + kx + i);
     }
     cand = cand && tl;
     Key k;
@@ -2087,7 +2163,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     occj = occ_dict_r(dj, nbw, durv, D);
     stkj = nth1 ? occj : occj / (double)nth;
     o.rec(D, K_PLACE, cb, px, dn, mkd(rlu(dlo(occj), jb), rlu(dhi(occj), jb)), rl(np, jb), x, 0.0);
-    off += 1 + kx;
+    off += 1 + kx + nc;
     phase(20);
   }
   if (DGP_TRACE == 2 && lane == 0) TR(r, 6);
@@ -2233,7 +2309,7 @@ __device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, co
   const int64_t net = P.netocc[w];
   int64_t nbj = P.nbytes[w];
   const double nbw = net_bw_of(net, D);
-  const DTab durv = stim_durations(L, E);
+  const DTab durv = stim_durations(D, L, E, r);
   for (int i = 0; i < k; i++) {
     const int t = rl((int)h0.x, i), p = rl((int)h0.z, i);
     const uint32_t fl = rlu(h0.w, i);
@@ -2336,9 +2412,7 @@ __device__ __attribute__((always_inline)) bool bulk_single_holder(const Dev& D, 
   if (ballot(fr && (h1l != c || pxl != px || (tfl & TF_ROOTISH) || xl == D.dbg_task))) return false;
   const WDict d0 = dict_load<LW>(P, c);
   const uint32_t cnt0 = wd_cnt(d0, px);
-  bool in_g = false;
-#pragma unroll
-  for (int i = 0; i < PD; i++) in_g = in_g || (i < g.n && g.pf[i] == px);
+  const bool in_g = ballot(lane < g.n && g.pf == px) != 0;
   if (cnt0 == 0 || !in_g) return false;
   const int m = __builtin_popcountll(fm);
   const int rank = __builtin_popcountll(fm & ((1ull << lane) - 1));
@@ -2421,7 +2495,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   SCtl& S = L.c;
   const int lane = lane_id();
   const uint4 E = lane < NE ? D.desc[(size_t)(r & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
-  const DTab durv = stim_durations(L, E);
+  const DTab durv = stim_durations(D, L, E, r);
   const int t = rl((int)E.x, 0), w = rl((int)E.y, 0), p = rl((int)E.z, 0);
   const int64_t nbt = mk64(rlu(E.x, 1), rlu(E.y, 1));
   const int grp_t = rl((int)E.w, 1);
@@ -2593,7 +2667,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
      fml = D.fr_mark[xl];
      tfl = D.tflags[xl];
      const int64_t a = D.dep_ptr[xl], e = D.dep_ptr[xl + 1];
-     if (e - a == 1) {
+     if (e - a == 1 && !restricted_nonrootish(D, xl)) {
        const int d1 = D.dep_idx[a];
        h1l = D.holder_of[d1];
        // a replica set or a paused holder: decide_worker's general form below
@@ -2606,6 +2680,78 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
    for (int j = 0; j < nk; j++) {
     const int x = rl(xl, j);
     if (rl(fml, j) != (int)r) continue;
+    if (restricted_nonrootish(D, x)) {
+      // decide_worker (:8550-8593) with valid = valid_workers(ts) & running: candidates =
+      // holders & valid; none: valid; valid empty: loose -> decide_worker without
+      // restrictions (holders, else every running worker), else None -> no-worker
+      const int64_t r0 = D.restr_ptr[x], r1 = D.restr_ptr[x + 1];
+      auto held = [&](int cw) {
+        for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++)
+          if (holds_any(D, D.dep_idx[q], cw)) return true;
+        return false;
+      };
+      bool hv = false, av = false;
+      for (int64_t i = r0 + lane; i < r1; i += 64) {
+        const int cw = D.restr_idx[i];
+        if (paused(cw)) continue;
+        av = true;
+        hv = hv || held(cw);
+      }
+      int mode = ballot(hv) ? 0 : ballot(av) ? 1 : (D.restr_flags[x] & RF_LOOSE) ? 2 : 4;
+      Key b{INFINITY, INT64_MAX, INT32_MAX, 0};
+      if (mode <= 1 && r1 - r0 <= 64) {  // the candidates are in the restriction row: one lane each
+        const int cw = lane < r1 - r0 ? D.restr_idx[r0 + lane] : 0;
+        const bool in = lane < r1 - r0 && !paused(cw) && (mode == 1 || held(cw));
+        const double ocw = occ_of<LW>(P, D, cw, durv);
+        if (in) {
+          int64_t cm = 0;
+          for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++)
+            if (!holds_any(D, D.dep_idx[q], cw)) cm += nbv(D, D.res_nbytes[D.dep_idx[q]]);
+          b.start = ocw / (double)P.nthreads[cw] + (double)cm / (double)D.bandwidth;
+          b.nb = P.nbytes[cw];
+          b.w = cw;
+          b.comm = cm;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          Key q;
+          q.start = __shfl_xor(b.start, o);
+          q.nb = __shfl_xor(b.nb, o);
+          q.w = __shfl_xor(b.w, o);
+          q.comm = __shfl_xor(b.comm, o);
+          if (key_less(q, b)) b = q;
+        }
+        mode = 5;  // decided
+      }
+      for (int tr = 0; tr < 2 && mode != 4 && mode != 5; tr++) {
+        b = argmin_workers(D, [&](int cw, Key& kk) {
+          const double ocw = occ_of<LW>(P, D, cw, durv);  // all lanes: it shuffles
+          if (paused(cw)) return false;
+          if (mode <= 1 && !restr_has(D, x, cw)) return false;
+          if ((mode == 0 || mode == 2) && !held(cw)) return false;
+          int64_t cm = 0;
+          for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++)
+            if (!holds_any(D, D.dep_idx[q], cw)) cm += nbv(D, D.res_nbytes[D.dep_idx[q]]);
+          kk.start = ocw / (double)P.nthreads[cw] + (double)cm / (double)D.bandwidth;
+          kk.nb = P.nbytes[cw];
+          kk.w = cw;
+          kk.comm = cm;
+          return true;
+        });
+        if (b.w != INT32_MAX || mode != 2) break;
+        mode = 3;  // every holder paused: every running worker
+      }
+      if (b.w == INT32_MAX) {  // -> no-worker (:2761-2782)
+        if (lane == 0) {
+          D.state[x] = S_NO_WORKER;
+          atomicAdd((unsigned long long*)&D.g_relwait[D.group[x]], (unsigned long long)-1ll);
+          D.ctl->n_unrunnable++;
+        }
+        __threadfence_block();
+        continue;
+      }
+      place_x(x, b.w, ROUTE_NONROOTISH, b.comm, true);
+      continue;
+    }
     const int hx = rl(h1l, j);
     if (!(rl(tfl, j) & TF_ROOTISH) && hx >= 0 && hx < D.W && x != D.dbg_task) {
       // decide_worker (:8550-8593) with one dependency: its holder is the only candidate
@@ -3020,16 +3166,13 @@ __device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WP
       P.nproc[c] = D.w_nproc[c];
       P.nthreads[c] = (uint16_t)D.w_nthreads[c];
       P.cap[c] = (uint16_t)D.w_cap[c];
-      // engine layout (insertion-ordered pairs) -> WDict (prefix ids < PD on this path)
+      // engine layout (insertion-ordered pairs) -> WDict slots (prefix ids < PX on this path)
       const int n = D.w_plen[c];
-      uint32_t ord = (uint32_t)n << 24;
-      for (int q = 0; q < PD; q++) P.pcnt[(size_t)c * PD + q] = 0;
-      for (int i = 0; i < n; i++) {
-        const int pid = D.w_pfx[(size_t)c * PMAX + i] & (PD - 1);
-        ord |= (uint32_t)pid << (3 * i);
-        P.pcnt[(size_t)c * PD + pid] = (uint32_t)D.w_pcnt[(size_t)c * PMAX + i];
-      }
-      P.plen[c] = ord;
+      for (int q = 0; q < PD; q++)
+        P.pcnt[(size_t)c * PD + q] = q < n ? ((uint32_t)D.w_pfx[(size_t)c * PMAX + q] << 24) |
+                                                 ((uint32_t)D.w_pcnt[(size_t)c * PMAX + q] & 0xffffffu)
+                                           : 0u;
+      P.plen[c] = (uint32_t)n << 24;
       P.netocc[c] = D.w_netocc[c];
       P.nbytes[c] = D.w_nbytes[c];
       P.mask[c] = 0;
@@ -3042,9 +3185,9 @@ __device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WP
       const int n = (int)wd_n(ord);
       D.w_plen[c] = n;
       for (int i = 0; i < PMAX; i++) {
-        const int pid = wd_id(ord, i);
-        D.w_pfx[(size_t)c * PMAX + i] = i < n ? pid : 0;
-        D.w_pcnt[(size_t)c * PMAX + i] = i < n ? P.pcnt[(size_t)c * PD + pid] : 0;
+        const uint32_t v = P.pcnt[(size_t)c * PD + i];
+        D.w_pfx[(size_t)c * PMAX + i] = i < n ? (int)(v >> 24) : 0;
+        D.w_pcnt[(size_t)c * PMAX + i] = i < n ? (int)(v & 0xffffffu) : 0;
       }
       D.w_netocc[c] = P.netocc[c];
       D.w_nbytes[c] = P.nbytes[c];
@@ -3121,13 +3264,13 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     S.rounds_nonempty = c->rounds_nonempty;
     S.snaps = D.svc ? 0 : snaps;
     S.reg_limit = (!D.svc && (snaps || max_rounds > 0)) ? S.round_end : (1ll << 62);
-    S.g_plen = min(c->g_plen, PD);
-    for (int i = 0; i < PD; i++) {
+    S.g_plen = min(c->g_plen, PG);
+    for (int i = 0; i < PG; i++) {
       S.g_pfx[i] = i < c->g_plen ? c->g_pfx[i] : 0;
       S.g_pcnt[i] = i < c->g_plen ? c->g_pcnt[i] : 0;
     }
     S.g_netocc = c->g_netocc;
-    for (int i = 0; i < PD; i++) S.wdur[i] = i < D.P ? D.pdur_walk[i] : -1.0;
+    for (int i = 0; i < PX; i++) S.wdur[i] = i < D.P ? D.pdur_walk[i] : -1.0;
     S.n_idle = c->n_idle;
     S.n_sat = c->n_sat;
     for (int i = 0; i < 32; i++) S.prof[i] = 0;
@@ -3213,7 +3356,7 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     c->itc_slots = s_slots;
     c->rounds_nonempty = S.rounds_nonempty;
     c->g_plen = S.g_plen;
-    for (int i = 0; i < PD; i++) {
+    for (int i = 0; i < PG; i++) {
       c->g_pfx[i] = S.g_pfx[i];
       c->g_pcnt[i] = S.g_pcnt[i];
     }
@@ -3222,7 +3365,7 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     c->n_sat = S.n_sat;
     // the durations as of the last folded record (the walker drains the record log before
     // the launch ends): what the host-side snapshot and the next launch's globals read
-    for (int i = 0; i < PD && i < D.P; i++) D.pdur_walk[i] = D.pdur_cur[i] = S.wdur[i];
+    for (int i = 0; i < PX && i < D.P; i++) D.pdur_walk[i] = D.pdur_cur[i] = S.wdur[i];
     if (S.error && !c->error) {
       c->error = S.error;
       c->err_task = S.err_task;

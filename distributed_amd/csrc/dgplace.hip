@@ -95,6 +95,7 @@ struct dgp_engine {
   std::vector<uint8_t> h_wanted;
   std::vector<int64_t> gdep_n, gdep_len;   // per group: len(tg.dependencies), sum of their lengths
   std::vector<int8_t> rootish_override_h;  // TaskState._rootish per task (-1: None)
+  std::vector<uint8_t> restr_h;            // restriction flags per task (empty: none)
   std::vector<uint8_t> paused_h;           // per worker: 0 running, 1 paused, 2 removed
   int64_t log_min[3] = {0, 0, 0};          // minimum capacities of the placement / stimulus / record logs
   int64_t sv_used = 0;                     // service stimuli appended (accepted task-finished messages)
@@ -390,7 +391,7 @@ int walk(dgp_engine* e) {
 int run_service_stimuli(dgp_engine* e) {
   namespace V = dgp::svc;
   hipStream_t s = e->stream;
-  if (e->D.P <= dgp::st::PD && !e->D.restr_flags) {
+  if (e->D.P <= dgp::st::PX) {
     stream_source(e, true);
     if (int rc = launch_stream(e, -1, 0)) return rc;
   } else {
@@ -449,6 +450,7 @@ dgp_engine* dgp_create(int device) {
     const size_t st = (size_t)S::RS * S::PLC;  // staging rows of the retire ring
     int rc = 0;
     rc |= dalloc(e, &e->D.desc, (size_t)S::DR * S::NE, e->allocs);
+    rc |= dalloc(e, &e->D.dring, (size_t)S::DR * S::PX, e->allocs);
     rc |= dalloc(e, &e->D.touch_ring, (size_t)S::DR * S::TMAX, e->allocs);
     rc |= dalloc(e, &e->D.thdr, (size_t)S::DR, e->allocs);
     rc |= dalloc(e, &e->D.s2_task, st, e->allocs);
@@ -757,6 +759,7 @@ int upload_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const i
   D.restr_ptr = nullptr;  // no restrictions until dgp_set_restrictions
   D.restr_idx = nullptr;
   D.restr_flags = nullptr;
+  e->restr_h.clear();
   return 0;
 }
 
@@ -819,9 +822,12 @@ int dgp_set_restrictions(dgp_engine* e, const int64_t* restr_ptr, const int32_t*
     HIPCHK(e, hipMemcpy(rf, flags, N, hipMemcpyHostToDevice));
   }
   HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), tf.data(), N, hipMemcpyHostToDevice));
+  e->tflags_h = tf;
   D.restr_ptr = rp;
   D.restr_idx = ri;
   D.restr_flags = rf;
+  if (flags) e->restr_h.assign(flags, flags + N);
+  else e->restr_h.clear();
   return dgp_reset(e);
 }
 
@@ -936,7 +942,7 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
   if (int rc = check_device_error(e, &c)) return rc;
   const long long r0 = c.rounds_nonempty;
   const dgp::Dev& D = e->D;
-  if (D.P <= dgp::st::PD && !D.restr_flags) {
+  if (D.P <= dgp::st::PX) {
     // the stream engine: the whole replay in one persistent workgroup (dgp_stream.h)
     if (int rc = launch_stream(e, max_rounds, e->snap_rounds > 0 ? 1 : 0)) return rc;
   } else {
@@ -1018,8 +1024,8 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
 int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
-  if (!(e->D.P <= dgp::st::PD && !e->D.restr_flags))
-    return fail(e, DGP_E_STATE, "dgp_move_task: the round-kernel engine (more than 8 prefixes, or restrictions) "
+  if (!(e->D.P <= dgp::st::PX))
+    return fail(e, DGP_E_STATE, "dgp_move_task: the round-kernel engine (more than 32 prefixes) "
                                 "has no steal confirmation");
   if (task < 0 || task >= e->D.N || thief < 0 || thief >= e->D.W)
     return fail(e, DGP_E_ARG, "dgp_move_task: task or thief out of range");
@@ -1035,11 +1041,17 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
   if (n_new_placements) *n_new_placements = 0;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
-  if (!(e->D.P <= dgp::st::PD && !e->D.restr_flags))
-    return fail(e, DGP_E_STATE, "dgp_add_worker: the round-kernel engine (more than 8 prefixes, or restrictions) "
+  if (!(e->D.P <= dgp::st::PX))
+    return fail(e, DGP_E_STATE, "dgp_add_worker: the round-kernel engine (more than 32 prefixes) "
                                 "has no worker addition");
   if (nthreads <= 0 || nthreads > 65535) return fail(e, DGP_E_ARG, "dgp_add_worker: nthreads out of range");
   if (e->D.W + 1 > 32768) return fail(e, DGP_E_ARG, "at most 32768 workers");
+  {  // no-worker tasks would be rescheduled on the new worker (bulk_schedule_unrunnable_after_adding_worker)
+    dgp::Ctl c;
+    if (int rc = read_ctl(e, &c)) return rc;
+    if (c.n_unrunnable > 0)
+      return fail(e, DGP_E_STATE, "dgp_add_worker: no-worker tasks would be rescheduled (not modelled)");
+  }
   e->paused_h.push_back(0);
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -1105,7 +1117,8 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
     for (int64_t t = 0; t < D.N; t++) {
       const int g = e->group_h[t];
       const bool gr = e->group_sizes[g] > D.total_nthreads * 2 && e->gdep_n[g] < 5 && e->gdep_len[g] < 5;
-      const bool r = e->rootish_override_h[t] >= 0 ? e->rootish_override_h[t] != 0 : gr;
+      const bool rs = !e->restr_h.empty() && (e->restr_h[t] & dgp::RF_RESTRICTED);
+      const bool r = e->rootish_override_h[t] >= 0 ? e->rootish_override_h[t] != 0 : (gr && !rs);
       tf[t] = (uint8_t)((tf[t] & ~dgp::TF_ROOTISH) | (r ? dgp::TF_ROOTISH : 0));
       changed = changed || tf[t] != e->tflags_h[t];
     }
@@ -1136,7 +1149,6 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
   dgp::Dev& D = e->D;
-  if (D.restr_flags) return fail(e, DGP_E_STATE, "dgp_add_graph: not with worker restrictions");
   if (std::count_if(e->paused_h.begin(), e->paused_h.end(), [](uint8_t v) { return v != 0; }))
     return fail(e, DGP_E_STATE, "dgp_add_graph: not while a worker is paused or removed");
   if (n_new <= 0 || !dep_ptr || !prio || !prefix_id || !prefix_default_duration || !group_id || !wanted ||
@@ -1145,8 +1157,8 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   const int64_t N0 = D.N, E0 = e->E, N1 = N0 + n_new;
   const int32_t P0 = D.P, G0 = D.G;
   if (n_prefixes < P0 || n_groups < G0) return fail(e, DGP_E_ARG, "dgp_add_graph: prefix / group tables shrank");
-  if (n_prefixes > dgp::st::PD)
-    return fail(e, DGP_E_STATE, "dgp_add_graph: more task prefixes than the stream engine carries (8)");
+  if (n_prefixes > dgp::st::PX)
+    return fail(e, DGP_E_STATE, "dgp_add_graph: more task prefixes than the stream engine carries (32)");
   if (dep_ptr[0] != 0) return fail(e, DGP_E_ARG, "dgp_add_graph: bad dep_ptr");
   for (int64_t t = 0; t < n_new; t++)
     if (dep_ptr[t + 1] < dep_ptr[t]) return fail(e, DGP_E_ARG, "dgp_add_graph: dep_ptr not monotone");
@@ -1182,6 +1194,7 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   HIPCHK(e, hipMemcpy(relwait.data(), D.g_relwait, (size_t)G0 * 8, hipMemcpyDeviceToHost));
   for (int64_t t = 0; t < n_new; t++) relwait[group_id[t]]++;
   const dgp::Dev old = D;
+  const std::vector<uint8_t> old_tf = e->tflags_h, old_restr = e->restr_h;
   const int64_t old_rlog = D.rlog_cap;
   e->log_min[0] = D.pl_cap + n_new;
   e->log_min[1] = D.sv_cap + n_new;
@@ -1243,15 +1256,46 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   HIPCHK(e, hipMemcpyAsync(D.pdur_walk, old.pdur_walk, (size_t)P0 * 8, hipMemcpyDeviceToDevice, s));
   HIPCHK(e, hipMemcpyAsync(D.pdur_pre, old.pdur_pre, (size_t)P0 * 8, hipMemcpyDeviceToDevice, s));
   HIPCHK(e, carry(D.pmaxexec, old.pmaxexec, (size_t)P0 * 8, (size_t)n_prefixes * 8, 0));
-  {
-    std::vector<double> mx(n_prefixes, -1.0);
-    HIPCHK(e, hipMemcpyAsync(D.pmaxexec, mx.data(), (size_t)n_prefixes * 8, hipMemcpyHostToDevice, s));
+  if (n_prefixes > P0) {  // the new prefixes: no max_exec_time yet (the known ones keep theirs)
+    std::vector<double> mx(n_prefixes - P0, -1.0);
+    HIPCHK(e, hipMemcpyAsync(D.pmaxexec + P0, mx.data(), mx.size() * 8, hipMemcpyHostToDevice, s));
   }
   // groups
   HIPCHK(e, hipMemcpyAsync(D.g_relwait, relwait.data(), (size_t)n_groups * 8, hipMemcpyHostToDevice, s));
   HIPCHK(e, carry(D.g_left, old.g_left, (size_t)G0 * 8, (size_t)n_groups * 8, 0));
   HIPCHK(e, carry(D.g_lastw, old.g_lastw, (size_t)G0 * 4, (size_t)n_groups * 4, 0xff));
   HIPCHK(e, hipStreamSynchronize(s));
+  // task flags the graph upload does not know: forgotten rows (resync) and restrictions
+  for (int64_t t = 0; t < N0; t++) e->tflags_h[t] |= (uint8_t)(old_tf[t] & dgp::TF_FORGOTTEN);
+  if (old.restr_flags) {  // the earlier tasks keep their restrictions; the new ones have none
+    std::vector<int64_t> rp(N1 + 1);
+    HIPCHK(e, hipMemcpy(rp.data(), old.restr_ptr, (N0 + 1) * 8, hipMemcpyDeviceToHost));
+    const int64_t K = rp[N0];
+    for (int64_t t = N0; t < N1; t++) rp[t + 1] = K;
+    std::vector<int32_t> ri(std::max<int64_t>(K, 1), 0);
+    if (K) HIPCHK(e, hipMemcpy(ri.data(), old.restr_idx, K * 4, hipMemcpyDeviceToHost));
+    e->restr_h = old_restr;
+    e->restr_h.resize(N1, 0);
+    int64_t* rpd = nullptr;
+    int32_t* rid = nullptr;
+    uint8_t* rfd = nullptr;
+    int rc = 0;
+    rc |= dalloc(e, &rpd, N1 + 1, e->graph_allocs);
+    rc |= dalloc(e, &rid, (int64_t)ri.size(), e->graph_allocs);
+    rc |= dalloc(e, &rfd, N1, e->graph_allocs);
+    if (rc) return DGP_E_HIP;
+    HIPCHK(e, hipMemcpy(rpd, rp.data(), (N1 + 1) * 8, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(rid, ri.data(), ri.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(rfd, e->restr_h.data(), N1, hipMemcpyHostToDevice));
+    D.restr_ptr = rpd;
+    D.restr_idx = rid;
+    D.restr_flags = rfd;
+    // a restricted task is not root-ish unless _rootish says so (is_rootish :2929-2947)
+    for (int64_t t = 0; t < N0; t++)
+      if ((e->restr_h[t] & dgp::RF_RESTRICTED) && e->rootish_override_h[t] < 0)
+        e->tflags_h[t] &= (uint8_t)~dgp::TF_ROOTISH;
+  }
+  HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), e->tflags_h.data(), N1, hipMemcpyHostToDevice));
   free_list(old_allocs);
   // the update_graph stimulus of the new tasks (:4600-4651): released -> waiting, the
   // runnable ones (no dependency: the new graph is independent of the old) to processing
@@ -1285,9 +1329,9 @@ namespace {
 int event_ready(dgp_engine* e, const char* what) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
-  if (!(e->D.P <= dgp::st::PD && !e->D.restr_flags))
-    return fail(e, DGP_E_STATE, std::string(what) + ": the round-kernel engine (more than 8 prefixes, or "
-                                                    "restrictions) has no service events");
+  if (!(e->D.P <= dgp::st::PX))
+    return fail(e, DGP_E_STATE, std::string(what) + ": the round-kernel engine (more than 32 prefixes) has no "
+                                                    "service events");
   HIPCHK(e, hipSetDevice(e->device));
   e->mode = 2;
   return 0;
@@ -1631,7 +1675,8 @@ int dgp_sync_workers(dgp_engine* e, int32_t n_workers, const int8_t* status, con
     for (int64_t t = 0; t < D.N; t++) {
       const int g = e->group_h[t];
       const bool gr = e->group_sizes[g] > D.total_nthreads * 2 && e->gdep_n[g] < 5 && e->gdep_len[g] < 5;
-      const bool r = e->rootish_override_h[t] >= 0 ? e->rootish_override_h[t] != 0 : gr;
+      const bool rs = !e->restr_h.empty() && (e->restr_h[t] & dgp::RF_RESTRICTED);
+      const bool r = e->rootish_override_h[t] >= 0 ? e->rootish_override_h[t] != 0 : (gr && !rs);
       tf[t] = (uint8_t)((tf[t] & ~dgp::TF_ROOTISH) | (r ? dgp::TF_ROOTISH : 0));
     }
   }

@@ -314,7 +314,8 @@ struct Replay {
   // through the ids), group sizes and is_rootish's group part over the grown graph, then
   // every new task recommended "waiting" in descending priority (:4600-4651)
   void add_graph(const orc_graph& h) {
-    ORC_CHECK(!g.restr_flags && !h.restr_flags, "a later graph with restrictions: not in the replay subset");
+    // the earlier graph may carry restrictions (its rows stay); the later graph has none
+    ORC_CHECK(!h.restr_flags, "a later graph with restrictions: not in the replay subset");
     const int64_t n0 = N, n1 = N + h.n_tasks;
     G.append(h, n0);
     N = n1;
@@ -397,8 +398,9 @@ struct Replay {
   }
   double total_occupancy() const { return calc_occupancy(prefix_global, net_occ_global); }  // :1877
 
-  bool restricted(int32_t t) const { return g.restr_flags && (g.restr_flags[t] & 1); }
-  bool loose(int32_t t) const { return g.restr_flags && (g.restr_flags[t] & 2); }
+  // restrictions are rows of the first graph (a later graph's tasks have none)
+  bool restricted(int32_t t) const { return g.restr_flags && t < g.n_tasks && (g.restr_flags[t] & 1); }
+  bool loose(int32_t t) const { return g.restr_flags && t < g.n_tasks && (g.restr_flags[t] & 2); }
 
   bool is_rootish(int32_t t) const {  // :2929-2947
     int8_t ov = G.rootish_override[t];

@@ -294,6 +294,14 @@ def main_add_workers(only):
         # 1,000 workers (worker state in LDS) growing to 1,300: the stream engine switches to
         # its global-memory worker layout part-way through the stream
         "svcaddw_w1000_sat1.1": (lambda: G.graphs.random_dag(30000, 1000, seed=24), 1.1, 8, 300),
+        # worker restrictions (30 % of the tasks, half of them loose) and 16 task prefixes:
+        # the stream engine's restricted decisions and its 16-prefix dicts across joins
+        "svcaddw_restr_sat1.1": (lambda: G.graphs.restrict(G.graphs.random_dag(3000, 48, seed=25, n_inner_prefixes=3,
+                                                                                random_durations=True,
+                                                                                nthreads="random"),
+                                                            0.3, seed=25, empty_frac=0.0), 1.1, 9, 24),
+        "svcaddw_p16_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=26, n_inner_prefixes=15,
+                                                            random_durations=True, nthreads="random"), 1.1, 10, 24),
     }
     for name, (mk, sat, seed, n_add) in cases.items():
         if only and name not in only:
@@ -446,13 +454,18 @@ def main_second_graph(only):
         # the second graph and 40 workers joining in one stream
         "svcgraph_joins_sat1.1": (dict(n=4000, w=40, seed=35, n_inner_prefixes=2, random_durations=True,
                                        nthreads="random"), dict(n=3000, seed=36), 1.1, 0.4, 40),
+        # restrictions on the first graph (the later one has none) and 12 task prefixes
+        "svcgraph_restr_sat1.1": (dict(n=3000, w=32, seed=37, n_inner_prefixes=11, random_durations=True,
+                                       nthreads="random", restrict=0.3), dict(n=2000, seed=38), 1.1, 0.3, 8),
     }
     for name, (a, b, sat, frac, *nadd) in cases.items():
         nadd = nadd[0] if nadd else 0
         if only and name not in only:
             continue
-        kw = {k: v for k, v in a.items() if k not in ("n", "w", "seed")}
+        kw = {k: v for k, v in a.items() if k not in ("n", "w", "seed", "restrict")}
         g = G.graphs.random_dag(a["n"], a["w"], seed=a["seed"], **kw)
+        if a.get("restrict"):
+            g = G.graphs.restrict(g, a["restrict"], seed=a["seed"], empty_frac=0.0)
         g2 = G.graphs.random_dag(b["n"], a["w"], seed=b["seed"], **kw)
         g2["group_names"] = [nm.replace(G.graphs.TOKEN, TOKEN2) for nm in g2["group_names"]]
         assert g2["prefix_names"] == g["prefix_names"]

@@ -47,7 +47,8 @@ def test_extension_places_every_task_from_the_engine():
 def test_extension_follows_workers_joining():
     """Scheduler.add_worker mid-stream: the plugin hook adds the worker to the engine, and
     the scheduler's queue refill takes the engine's decisions (validate=True agrees)."""
-    names = ["svcaddw_c2var_sat1.1.npz", "svcaddw_c2mini_sat1.0.npz", "svcaddw_c2mini_satinf.npz"]
+    names = ["svcaddw_c2var_sat1.1.npz", "svcaddw_c2mini_sat1.0.npz", "svcaddw_c2mini_satinf.npz",
+             "svcaddw_restr_sat1.1.npz", "svcaddw_p16_sat1.1.npz"]
     res = drive(names)
     assert [r["fixture"] for r in res] == names
     for r in res:
@@ -58,7 +59,8 @@ def test_extension_follows_workers_joining():
 def test_extension_follows_a_second_graph():
     """A second, independent graph submitted to the running scheduler: the plugin hook
     appends it to the engine (dgp_add_graph); every decision still comes from the engine."""
-    names = ["svcgraph_c2var_sat1.1.npz", "svcgraph_c2mini_satinf.npz", "svcgraph_joins_sat1.1.npz"]
+    names = ["svcgraph_c2var_sat1.1.npz", "svcgraph_c2mini_satinf.npz", "svcgraph_joins_sat1.1.npz",
+             "svcgraph_restr_sat1.1.npz"]
     res = drive(names)
     assert [r["fixture"] for r in res] == names
     for r in res:

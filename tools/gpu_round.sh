@@ -18,7 +18,7 @@ rc=$?; tail -3 $OUT/prof.log; ls $OUT/prof; [ $rc -ne 0 ] && exit $rc
 # HBM traffic of the C2 replay: one counter per pass (FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2)
 for C in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $C"
-  timeout -k 10 240 rocprofv3 --pmc $C --output-format csv -d $OUT/pmc_$C -o run -- python3 bench.py --no-cpu-baseline --no-steal --no-c3 --no-c5 --steps 1 --warmup 0 > $OUT/pmc_$C.log 2>&1
+  timeout -k 10 240 rocprofv3 --pmc $C --output-format csv -d $OUT/pmc_$C -o run -- python3 bench.py --no-cpu-baseline --no-steal --no-c3 --no-c5 --no-variants --no-service --steps 1 --warmup 0 > $OUT/pmc_$C.log 2>&1
   rc=$?; tail -2 $OUT/pmc_$C.log; [ $rc -ne 0 ] && exit $rc
 done
 exit 0
