@@ -222,14 +222,62 @@ def variant_legs(eng_cls, local: int, args) -> dict:
     return legs
 
 
+def c_call_latency(eng_cls, local: int, g: dict) -> dict:
+    """One task-finished message per dgp_tasks_finished call through the resident kernel,
+    driven with ctypes on preallocated buffers (what a C / Cython caller pays): the replay
+    protocol over g, each call's new placements read from the mailbox (task / worker)."""
+    import ctypes as C
+
+    eng = eng_cls(local)
+    eng.load(g, CONFIG, results=False)
+    eng.set_resident(True)
+    eng.update_graph()
+    lib, h = eng.lib, eng.h
+    N = int(g["n_tasks"])
+    ptask, pworker = np.zeros(N, np.int32), np.zeros(N, np.int32)
+    m = {k: np.zeros(1, dt) for k, dt in (("t", np.int32), ("w", np.int32), ("r", np.int64), ("nb", np.int64),
+                                          ("a", np.float64), ("b", np.float64), ("st", np.int8))}
+    P = {k: v.ctypes.data_as(C.c_void_p) for k, v in m.items()}
+    newp = C.c_int64(0)
+    n = int(lib.dgp_num_placements(h))
+    lib.dgp_get_placements(h, 0, n, ptask.ctypes.data_as(C.c_void_p), pworker.ctypes.data_as(C.c_void_p),
+                           None, None, None, None)
+    done, calls = 0, 0
+    t0 = time.perf_counter()
+    while done < n:
+        t = int(ptask[done])
+        m["t"][0], m["w"][0], m["r"][0] = t, pworker[done], done
+        m["nb"][0], m["a"][0], m["b"][0] = g["nbytes"][t], g["start"][t], g["stop"][t]
+        rc = lib.dgp_tasks_finished(h, 1, P["t"], P["w"], P["r"], P["nb"], P["a"], P["b"], P["st"], C.byref(newp))
+        assert rc == 0 and m["st"][0] == 0
+        k = newp.value
+        if k:
+            lib.dgp_get_placements(h, n, k, ptask[n:].ctypes.data_as(C.c_void_p),
+                                   pworker[n:].ctypes.data_as(C.c_void_p), None, None, None, None)
+            n += k
+        done += 1
+        calls += 1
+    dt = time.perf_counter() - t0
+    eng.set_resident(False)
+    st = eng.stats()
+    eng.close()
+    k = max(st["res_requests"], 1)
+    return {"calls": calls, "us_per_call": round(dt / calls * 1e6, 2), "messages_per_s": round(calls / dt, 1),
+            "device_us_per_call": {"answer": round(st["res_append_ticks"] / k / 100, 2),
+                                   "run_stimuli": round(st["res_run_ticks"] / k / 100, 2),
+                                   "publish": round(st["res_publish_ticks"] / k / 100, 2)}}
+
+
 def service_leg(eng_cls, local: int, args) -> dict:
     """The drop-in boundary as a live scheduler drives it (service mode): a C2-shaped graph
     (random DAG, fan-in 4, sat 1.1) on 1,024 workers whose completions arrive as
     task-finished messages through dgp_tasks_finished, the replay protocol's order, with the
-    new placements read back after every call (what GPUPlacementExtension does). Two
-    granularities: one call per round (every completion of the previous round's placements)
-    and one call per message. Host-inclusive (ctypes, PCIe copies, launches, syncs);
-    checked bit-exact against the oracle's replay of the same protocol."""
+    new placements' task / worker read back after every call (what GPUPlacementExtension
+    does). Two granularities: one call per round (every completion of the previous round's
+    placements) and one call per message; each launch-per-call and through the resident
+    kernel (dgp_set_resident: mailbox in pinned host memory, no launch / copy / sync per
+    call). Host-inclusive (ctypes included); checked bit-exact against the oracle's replay
+    of the same protocol."""
     from distributed_amd import graphs
 
     g = graphs.random_dag(args.svc_tasks, 1024, seed=5)
@@ -237,30 +285,38 @@ def service_leg(eng_cls, local: int, args) -> dict:
            "workload": f"C2-shaped random DAG, {args.svc_tasks} tasks x 1024 workers, sat 1.1",
            "n_tasks": int(g["n_tasks"])}
     outs = {}
-    for mode in ("per_round", "per_message"):
+    cols = ("pl_task", "pl_worker")
+    for mode in ("per_round", "per_message", "per_round_resident", "per_message_resident"):
         eng = eng_cls(local)
         eng.load(g, CONFIG, results=False)
+        eng.set_resident(mode.endswith("resident"))
         eng.update_graph()
         done, calls = 0, 0
+        n = eng.num_placements()
         t0 = time.perf_counter()
-        while True:
-            n = eng.num_placements()
-            if n == done:
-                break
-            p = eng.placements(done, n - done)
+        while n > done:  # each batch: the previous one's new placements, completed in run_id order
+            p = eng.placements(done, n - done, columns=cols)
             t, w = p["pl_task"], p["pl_worker"]
             r = np.arange(done, n, dtype=np.int64)
             nb, a, b = g["nbytes"][t], g["start"][t], g["stop"][t]
-            if mode == "per_round":
-                eng.tasks_finished(t, w, r, nb, a, b)
+            done = n
+            if mode.startswith("per_round"):
+                _, k = eng.tasks_finished(t, w, r, nb, a, b)
+                n += k
                 calls += 1
             else:
                 for i in range(len(t)):
-                    eng.tasks_finished(t[i:i + 1], w[i:i + 1], r[i:i + 1], nb[i:i + 1], a[i:i + 1], b[i:i + 1])
+                    _, k = eng.tasks_finished(t[i:i + 1], w[i:i + 1], r[i:i + 1], nb[i:i + 1], a[i:i + 1], b[i:i + 1])
+                    n += k
                     calls += 1
-            done = n
         dt = time.perf_counter() - t0
+        eng.set_resident(False)
         outs[mode] = eng.placements()
+        if mode == "per_message_resident":
+            # the same protocol through the bare C ABI (preallocated buffers, no numpy per
+            # call): the engine's own latency per message, without the Python wrapper's
+            lat = c_call_latency(eng_cls, local, g)
+            leg["per_message_resident_c_abi"] = lat
         eng.close()
         leg[mode] = {"messages_per_s": round(g["n_tasks"] / dt, 1), "calls": calls,
                      "us_per_call": round(dt / max(calls, 1) * 1e6, 1), "seconds": round(dt, 4)}

@@ -270,6 +270,8 @@ struct Dev {
   const int32_t* stim_worker;
   int32_t* cseq;         // stimulus index of each task's completion (-1: not completed)
   int32_t svc;           // 1: service mode (the launch ends at *svc_len)
+  int32_t resident;      // service mode: the launch stays, answering requests from the mailbox
+  void* mbox;            // resident service mailbox (dgp_service.h svc::Mbox, pinned host memory)
   long long* svc_len;    // service mode: stimulus-log length (device)
   int32_t* sv_task;      // service-mode stimulus log [sv_cap]
   int32_t* sv_worker;

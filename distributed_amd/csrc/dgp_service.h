@@ -13,36 +13,10 @@
 namespace dgp {
 namespace svc {
 
-// answer to one task-finished message (the status codes of include/dgplace.h)
-enum : int8_t {
-  TF_ACCEPTED = 0,        // -> _transition(key, "memory", ...) (:5090): a completion stimulus
-  TF_FREE_KEYS = 1,       // forgotten / released / queued / no-worker task, or a stale run
-                          // from another worker (:5036-5049, :5065-5079): "free-keys" to the worker
-  TF_ADD_KEYS = 2,        // the task is already in memory (:5082-5083): Scheduler.add_keys
-  TF_RELEASE = 3,         // stale run_id from the worker the task is processing on (:5080-5081):
-                          // the reference recommends "released" (re-placement); not run by the device
-  TF_UNKNOWN_WORKER = 4,  // worker not in Scheduler.workers (:5786-5787): ignored
-  TF_IMPOSSIBLE = 5,      // processing on another worker with the current run_id: the
-                          // reference raises RuntimeError (:2398-2404)
-  TF_UNSUPPORTED = 6,     // waiting -> memory with a matching run_id (_transition_waiting_memory)
-};
-
-// one message, packed by the host so the batch crosses PCIe in one copy
-struct Msg {
-  int32_t task, worker;
-  int64_t run_id;
-  int64_t nbytes;  // < 0: None (TaskState.set_nbytes is not called, :2424-2425)
-  double start, stop;  // the "compute" startstop; NaN: none (no TaskPrefix EWMA step)
-};
-static_assert(sizeof(Msg) == 40, "Msg layout is shared with the host");
-
 // One lane, in message order: every message is answered against the state left by all
-// earlier messages. The stimuli accepted here only run after this kernel, so the first
-// message whose answer could depend on them (a task that is waiting, queued or in memory,
-// or that completed earlier in this batch: the frontier placement, the queue refill and
-// the releases of those stimuli may change its state) ends the call's batch; the host runs
-// the accepted stimuli and calls again from there. A processing task's run_id and worker
-// change only through its own completion, and released / no-worker are final here.
+// earlier messages (svc::answer, dgp_svcmsg.h). The stimuli accepted here only run after this
+// kernel, so the first message whose answer could depend on them ends the call's batch; the
+// host runs the accepted stimuli and calls again from there.
 __global__ void k_svc_append(const Dev* __restrict__ Dp, const Msg* __restrict__ msgs, long long n,
                              int8_t* __restrict__ status, long long* __restrict__ consumed) {
   const Dev& D = *Dp;
@@ -51,46 +25,8 @@ __global__ void k_svc_append(const Dev* __restrict__ Dp, const Msg* __restrict__
   long long len = len0;
   long long i = 0;
   for (; i < n; i++) {
-    const Msg m = msgs[i];
-    int8_t st;
-    if (m.worker < 0 || m.worker >= D.W) {
-      st = TF_UNKNOWN_WORKER;
-    } else if (m.task < 0 || m.task >= D.N) {
-      st = TF_FREE_KEYS;  // ts is None
-    } else {
-      const int t = m.task;
-      int s = D.state[t];
-      const bool done_here = s == S_PROCESSING && D.sv_cseq[t] >= len0;  // completed in this call
-      const bool stable = (s == S_PROCESSING && !done_here) || s == S_RELEASED || s == S_NO_WORKER;
-      if (len > len0 && !stable) break;  // answer after the accepted stimuli ran
-      if (s == S_RELEASED || s == S_QUEUED || s == S_NO_WORKER) {
-        st = TF_FREE_KEYS;
-      } else if ((int64_t)D.run_id[t] != m.run_id) {
-        const bool on_w = s == S_PROCESSING && D.proc_on[t] == m.worker;
-        st = on_w ? TF_RELEASE : TF_FREE_KEYS;
-      } else if (s == S_MEMORY) {
-        st = TF_ADD_KEYS;
-      } else if (s == S_PROCESSING) {
-        if (D.proc_on[t] != m.worker) {
-          st = TF_IMPOSSIBLE;
-        } else if (len >= D.sv_cap) {
-          st = TF_IMPOSSIBLE;
-          atomicCAS(&D.ctl->error, 0, (int)ERR_STAGE_CAP);
-        } else {
-          st = TF_ACCEPTED;
-          D.sv_task[len] = t;
-          D.sv_worker[len] = m.worker;
-          D.sv_cseq[t] = (int32_t)len;
-          D.holder_of[t] = m.worker;
-          if (m.nbytes >= 0) D.res_nbytes[t] = m.nbytes;
-          D.res_start[t] = m.start;
-          D.res_stop[t] = m.stop;
-          len++;
-        }
-      } else {
-        st = TF_UNSUPPORTED;
-      }
-    }
+    int8_t st = 0;
+    if (!answer(D, msgs[i], len0, len, st)) break;  // answer after the accepted stimuli ran
     status[i] = st;
   }
   *D.svc_len = len;

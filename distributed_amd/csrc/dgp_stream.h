@@ -33,6 +33,8 @@
 //        state in LDS; stimuli that read global state run alone, in order.
 #pragma once
 
+#include "dgp_svcmsg.h"
+
 namespace dgp {
 namespace st {
 
@@ -169,6 +171,8 @@ struct SCtl {
   long long seq_pos, log_len, rec_len, walk_pos, bld_pos, pre_pos, reg_pos, reg_limit;
   long long qhead, qlen, n_tasks;
   long long stim_end;  // service mode: stimuli [seq_pos, stim_end) run in this launch
+  long long req_n, req_off, req_pl0;  // resident service: the request's messages, consumed, first placement
+  unsigned long long req_seen;        // resident service: the last request taken
   long long round_end, rounds_left, prev_placed;
   long long rounds_nonempty, snap_idx;
   int snaps;
@@ -805,12 +809,120 @@ __device__ __attribute__((always_inline)) void snapshot(const Dev& D, SLds& L, c
 
 // every stimulus of the round is sequenced: count it, snapshot, open the next round.
 // Returns true when the replay stops here.
+// ---------------------------------------------------------- resident service mode
+// The stream kernel stays launched between dgp_tasks_finished calls: the sequencer wave,
+// once every stimulus of the request retired, publishes the answers (statuses, the log
+// length, the new placements' task / worker) into the pinned mailbox, then polls it for the
+// next request, answers its messages (svc::answer, Scheduler.stimulus_task_finished
+// :5025-5092, as k_svc_append) and raises the stimulus end: the roles continue. Returns
+// false when the kernel is to end (the host's stop, an error, or no request for a while).
+__device__ __forceinline__ unsigned long long sys_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __attribute__((noinline)) bool resident_serve(const Dev& D, SLds& L) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  svc::Mbox* mb = (svc::Mbox*)D.mbox;
+  svc::Msg* msgs = svc::mbox_msgs(mb);
+  int8_t* status = svc::mbox_status(mb);
+  while (true) {
+    if (S.req_off < S.req_n) {  // the next segment of the request in progress
+      const long long len0 = *D.svc_len;
+      long long len = len0, i = S.req_off;
+      bool cut = false;
+      while (i < S.req_n && !cut) {
+        const long long k0 = i;
+        svc::Msg m{};
+        if (k0 + lane < S.req_n) m = msgs[k0 + lane];  // 64 messages across PCIe at once
+        int8_t st = 0;
+        const int kn = (int)min((long long)64, S.req_n - k0);
+        int j = 0;
+        for (; j < kn; j++) {
+          svc::Msg mj;
+          mj.task = rl(m.task, j);
+          mj.worker = rl(m.worker, j);
+          mj.run_id = rl_i64(m.run_id, j);
+          mj.nbytes = rl_i64(m.nbytes, j);
+          mj.start = rl_f64(m.start, j);
+          mj.stop = rl_f64(m.stop, j);
+          int8_t a = 0;
+          bool take = false;
+          if (lane == 0) take = svc::answer(D, mj, len0, len, a);
+          if (__builtin_amdgcn_readfirstlane(take ? 1 : 0) == 0) {  // depends on this segment's stimuli
+            cut = true;
+            break;
+          }
+          len = rl_i64(len, 0);
+          if (lane == j) st = (int8_t)rl((int)a, 0);
+        }
+        if (lane < j) status[k0 + lane] = st;
+        i = k0 + j;
+      }
+      __threadfence();
+      if (lane == 0) {
+        *D.svc_len = len;
+        S.req_off = i;
+        S.stim_end = len;
+        S.round_end = len;
+        mb->t_app = rclk();
+      }
+      lds_fence();
+      if (len > len0) return true;  // the roles run the new stimuli; back here when they retired
+      continue;
+    }
+    if (S.req_seen != 0) {  // the request is answered: publish
+      if (lane == 0) mb->t_ret = rclk();
+      const long long n0 = S.req_pl0, n1 = S.log_len;
+      const long long cap = mb->pl_cap;
+      int32_t* pt = svc::mbox_pl_task(mb);
+      int32_t* pw = svc::mbox_pl_worker(mb);
+      if (n1 - n0 <= cap)
+        for (long long k = lane; k < n1 - n0; k += 64) {
+          pt[k] = D.pl_task[n0 + k];
+          pw[k] = D.pl_worker[n0 + k];
+        }
+      if (lane == 0) {
+        mb->pl_from = n1 - n0 <= cap ? n0 : -1;
+        mb->n_placed = n1;
+        mb->error = S.error;
+        mb->t_pub = rclk();
+      }
+      __threadfence_system();
+      if (lane == 0) __hip_atomic_store(&mb->done_seq, S.req_seen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (lane == 0) S.req_seen = 0;
+      lds_fence();
+    }
+    // the next request, the host's stop, or an idle spell (then the kernel ends; the host
+    // launches it again for the next request)
+    const unsigned long long t0 = rclk();
+    const unsigned long long last = sys_load(&mb->done_seq);
+    unsigned long long rq = 0;
+    while (true) {
+      if (vload(&S.stop) || vload(&S.error)) return false;
+      rq = sys_load(&mb->req_seq);
+      if (rq != last) break;
+      if (__hip_atomic_load(&mb->stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) return false;
+      if (rclk() - t0 > 20000000ull) return false;  // 0.2 s without a request (100 MHz clock)
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0) {
+      mb->t_seen = rclk();
+      S.req_seen = rq;
+      S.req_n = (long long)__hip_atomic_load(&mb->n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      S.req_off = 0;
+      S.req_pl0 = S.log_len;
+    }
+    lds_fence();
+  }
+}
+
 template <bool LW>
 __device__ __attribute__((always_inline)) bool round_end_step(const Dev& D, SLds& L, const WPtr<LW>& P, long long& round_start) {
   SCtl& S = L.c;
   const int lane = lane_id();
   if (D.svc) {  // service mode: the launch ends with the stimulus log (no synthetic rounds)
     round_start = S.round_end;
+    if (D.resident && resident_serve(D, L)) return false;  // the next request's stimuli
     if (lane == 0) vstore(&S.stop, 1);
     return true;
   }
@@ -3258,6 +3370,9 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     S.qlen = c->qlen;
     S.n_tasks = c->n_tasks;
     S.stim_end = D.svc ? *D.svc_len : -1;
+    S.req_n = S.req_off = 0;
+    S.req_pl0 = (long long)c->n_placed;
+    S.req_seen = 0;
     S.round_end = D.svc ? S.stim_end : pos->round_end >= 0 ? pos->round_end : (long long)c->n_placed;
     S.rounds_left = max_rounds > 0 ? max_rounds : -1;
     S.prev_placed = pos->round_end >= 0 ? pos->prev_placed : (long long)c->n_placed;

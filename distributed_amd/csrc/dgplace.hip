@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -101,6 +102,14 @@ struct dgp_engine {
   int64_t sv_used = 0;                     // service stimuli appended (accepted task-finished messages)
   char* d_ev = nullptr;                    // service-event argument staging (device)
   size_t d_ev_cap = 0;
+  // resident service mode (dgp_set_resident): the stream kernel stays launched between
+  // dgp_tasks_finished calls and takes each batch from a mailbox in pinned host memory
+  dgp::svc::Mbox* mb = nullptr;      // host address
+  dgp::svc::Mbox* mb_dev = nullptr;  // device address
+  bool resident = false;             // service calls go through the resident kernel
+  bool res_running = false;          // the resident kernel was launched (it may have ended since)
+  unsigned long long req_seq = 0;    // the last request number sent
+  int64_t res_prof[4] = {0, 0, 0, 0};  // requests answered; sums of append, run, publish (device 100 MHz ticks)
 };
 
 namespace {
@@ -204,6 +213,20 @@ int check_device_error(dgp_engine* e, dgp::Ctl* out = nullptr) {
     }
     return fail(e, DGP_E_DEVICE, buf);
   }
+  return 0;
+}
+
+// End the resident service kernel (it writes the engine state back as any launch does).
+// Every entry point but dgp_tasks_finished calls this first: nothing else may touch the
+// engine's stream or device state while it runs.
+int resident_stop(dgp_engine* e) {
+  if (!e || !e->res_running) return 0;
+  __atomic_store_n(&e->mb->stop, 1, __ATOMIC_RELEASE);
+  const hipError_t st = hipStreamSynchronize(e->stream);
+  __atomic_store_n(&e->mb->stop, 0, __ATOMIC_RELEASE);
+  e->res_running = false;
+  e->D.resident = 0;
+  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("resident kernel: ") + hipGetErrorString(st));
   return 0;
 }
 
@@ -479,7 +502,9 @@ dgp_engine* dgp_create(int device) {
 void dgp_destroy(dgp_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
+  (void)resident_stop(e);
   (void)hipStreamSynchronize(e->stream);
+  if (e->mb) (void)hipHostFree(e->mb);
   free_list(e->allocs);
   free_list(e->graph_allocs);
   if (e->d_msgs) (void)hipFree(e->d_msgs);
@@ -499,6 +524,7 @@ const char* dgp_last_error(const dgp_engine* e) { return e ? e->err.c_str() : "n
 
 int dgp_set_config(dgp_engine* e, int64_t bandwidth, int64_t default_data_size, double unknown_duration,
                    double saturation) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e) return DGP_E_ARG;
   if (bandwidth <= 0 || default_data_size < 0 || !(saturation > 0))
     return fail(e, DGP_E_ARG, "bandwidth must be > 0, default_data_size >= 0, saturation > 0");
@@ -518,6 +544,7 @@ int dgp_set_config(dgp_engine* e, int64_t bandwidth, int64_t default_data_size, 
 }
 
 int dgp_set_workers(dgp_engine* e, int32_t n_workers, const int32_t* nthreads) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || n_workers <= 0 || !nthreads) return fail(e, DGP_E_ARG, "need n_workers > 0 and nthreads");
   if (n_workers > 32768) return fail(e, DGP_E_ARG, "at most 32768 workers (commit reservation table in LDS)");
   HIPCHK(e, hipSetDevice(e->device));
@@ -770,6 +797,7 @@ extern "C" {
 int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const int32_t* dep_idx, const int64_t* prio,
                   const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
                   const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e) return DGP_E_ARG;
   if (!e->have_workers) return fail(e, DGP_E_STATE, "dgp_set_workers must come first");
   HIPCHK(e, hipSetDevice(e->device));
@@ -784,6 +812,7 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
 }
 
 int dgp_set_restrictions(dgp_engine* e, const int64_t* restr_ptr, const int32_t* restr_idx, const uint8_t* flags) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->have_graph) return fail(e, DGP_E_STATE, "graph first");
   if (e->mode != 0 || e->stream_used) return fail(e, DGP_E_STATE, "restrictions go with the graph, before any stimulus");
   HIPCHK(e, hipSetDevice(e->device));
@@ -832,6 +861,7 @@ int dgp_set_restrictions(dgp_engine* e, const int64_t* restr_ptr, const int32_t*
 }
 
 int dgp_set_task_results(dgp_engine* e, const int64_t* nbytes, const double* start, const double* stop) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->have_graph) return fail(e, DGP_E_STATE, "graph first");
   HIPCHK(e, hipSetDevice(e->device));
   size_t N = e->D.N;
@@ -843,6 +873,7 @@ int dgp_set_task_results(dgp_engine* e, const int64_t* nbytes, const double* sta
 }
 
 int dgp_reset(dgp_engine* e) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->have_graph) return fail(e, DGP_E_STATE, "graph first");
   HIPCHK(e, hipSetDevice(e->device));
   dgp::Dev& D = e->D;
@@ -903,6 +934,7 @@ int dgp_reset(dgp_engine* e) {
 }
 
 int dgp_update_graph(dgp_engine* e) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->have_graph || !e->have_config) return fail(e, DGP_E_STATE, "config, workers and graph first");
   if (e->graph_done) return fail(e, DGP_E_STATE, "update_graph already ran (dgp_reset first)");
   HIPCHK(e, hipSetDevice(e->device));
@@ -929,6 +961,7 @@ int dgp_update_graph(dgp_engine* e) {
 }
 
 int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (!e->have_results) return fail(e, DGP_E_STATE, "dgp_set_task_results first");
   if (e->mode == 2) return fail(e, DGP_E_STATE, "engine is in service mode (dgp_tasks_finished); dgp_reset first");
@@ -967,6 +1000,108 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
   return 0;
 }
 
+}  // extern "C"
+
+namespace {
+
+// dgp_tasks_finished through the resident stream kernel: the batch goes into the pinned
+// mailbox, the request number is published, and the kernel's sequencer answers it (the
+// message checks, every stimulus it accepts run to completion, the new placements copied
+// back); the host only spins on the answer. A kernel that ended on its own (no request for
+// a while) or never started is launched first; the logs grow with the kernel stopped.
+int tasks_finished_resident(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker,
+                            const int64_t* run_id, const int64_t* nbytes, const double* start, const double* stop,
+                            int8_t* status, int64_t* n_new_placements) {
+  namespace V = dgp::svc;
+  dgp::Dev& D = e->D;
+  const int64_t plc = std::min<int64_t>(std::max<int64_t>(D.N, 1024), 1 << 20);
+  if (!e->mb || e->mb->cap < n || e->mb->pl_cap < plc) {  // the mailbox, sized for this batch
+    if (int rc = resident_stop(e)) return rc;
+    if (e->mb) (void)hipHostFree(e->mb);
+    e->mb = nullptr;
+    const int64_t cap = std::max<int64_t>(n, 4096);
+    void* p = nullptr;
+    HIPCHK(e, hipHostMalloc(&p, V::mbox_bytes(cap, plc), hipHostMallocCoherent | hipHostMallocMapped));
+    memset(p, 0, 128);
+    e->mb = (V::Mbox*)p;
+    e->mb->cap = cap;
+    e->mb->pl_cap = plc;
+    e->mb->req_seq = e->mb->done_seq = e->req_seq;
+    void* pd = nullptr;
+    HIPCHK(e, hipHostGetDevicePointer(&pd, p, 0));
+    e->mb_dev = (V::Mbox*)pd;
+  }
+  // log capacity for up to every task placed once more and n completions (grow_logs), with
+  // the kernel stopped when an array must grow
+  if ((int64_t)e->last_placed + D.N + 64 > D.pl_cap || e->sv_used + n > D.sv_cap) {
+    if (int rc = resident_stop(e)) return rc;
+    if (int rc = grow_logs(e, n)) return rc;
+  }
+  V::Msg* M = V::mbox_msgs(e->mb);
+  for (int64_t i = 0; i < n; i++) M[i] = V::Msg{task[i], worker[i], run_id[i], nbytes[i], start[i], stop[i]};
+  e->mb->n = n;
+  auto launch = [&]() -> int {
+    if (int rc = sync_dev(e)) return rc;
+    stream_source(e, true);
+    D.resident = 1;
+    D.mbox = (void*)e->mb_dev;
+    if (int rc = launch_stream(e, -1, 0)) {
+      D.resident = 0;
+      return rc;
+    }
+    e->res_running = true;
+    return 0;
+  };
+  if (!e->res_running)
+    if (int rc = launch()) return rc;
+  const unsigned long long seq = ++e->req_seq;
+  __atomic_store_n(&e->mb->req_seq, seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (long spins = 0; __atomic_load_n(&e->mb->done_seq, __ATOMIC_ACQUIRE) != seq; spins++) {
+    if ((spins & 255) == 255) {
+      if (hipStreamQuery(e->stream) == hipSuccess) {  // the kernel ended: idle before this request, or an error
+        e->res_running = false;
+        D.resident = 0;
+        if (int rc = check_device_error(e)) return rc;
+        if (__atomic_load_n(&e->mb->done_seq, __ATOMIC_ACQUIRE) == seq) break;
+        if (int rc = launch()) return rc;
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+        (void)resident_stop(e);
+        return fail(e, DGP_E_DEVICE, "dgp_tasks_finished: the resident kernel did not answer within 60 s");
+      }
+    }
+  }
+  if (e->mb->error) {  // the kernel ends on a device error: report it from the control block
+    if (int rc = resident_stop(e)) return rc;
+    if (int rc = check_device_error(e)) return rc;
+  }
+  memcpy(status, V::mbox_status(e->mb), (size_t)n);
+  e->res_prof[0] += 1;
+  if (e->mb->t_app >= e->mb->t_seen && e->mb->t_ret >= e->mb->t_app && e->mb->t_pub >= e->mb->t_ret) {
+    e->res_prof[1] += (int64_t)(e->mb->t_app - e->mb->t_seen);
+    e->res_prof[2] += (int64_t)(e->mb->t_ret - e->mb->t_app);
+    e->res_prof[3] += (int64_t)(e->mb->t_pub - e->mb->t_ret);
+  }
+  const unsigned long long placed = (unsigned long long)e->mb->n_placed;
+  if (n_new_placements) *n_new_placements = (int64_t)(placed - e->last_placed);
+  e->last_placed = placed;
+  for (int64_t i = 0; i < n; i++) e->sv_used += status[i] == DGP_TF_ACCEPTED ? 1 : 0;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dgp_set_resident(dgp_engine* e, int enabled) {
+  if (!e) return DGP_E_ARG;
+  if (!enabled)
+    if (int rc = resident_stop(e)) return rc;
+  e->resident = enabled != 0;
+  return 0;
+}
+
 int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* run_id,
                        const int64_t* nbytes, const double* start, const double* stop, int8_t* status,
                        int64_t* n_new_placements) {
@@ -978,6 +1113,9 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
   HIPCHK(e, hipSetDevice(e->device));
   e->mode = 2;
   if (n == 0) return 0;
+  if (e->resident && e->D.P <= dgp::st::PX) return tasks_finished_resident(e, n, task, worker, run_id, nbytes, start, stop,
+                                                                           status, n_new_placements);
+  if (int rc = resident_stop(e)) return rc;
   namespace V = dgp::svc;
   if (n > e->msgs_cap) {  // grow the pinned staging and the device batch
     if (e->d_msgs) (void)hipFree(e->d_msgs);
@@ -1022,6 +1160,7 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
 }
 
 int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
   if (!(e->D.P <= dgp::st::PX))
@@ -1038,6 +1177,7 @@ int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief) {
 }
 
 int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
@@ -1145,6 +1285,7 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
                   const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
                   const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override,
                   int64_t* n_new_placements) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
@@ -1381,6 +1522,7 @@ int event_with_refill(dgp_engine* e, F&& launch, int64_t* n_new_placements) {
 extern "C" {
 
 int dgp_add_replicas(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_add_replicas")) return rc;
   if (n < 0 || (n > 0 && (!task || !worker))) return fail(e, DGP_E_ARG, "dgp_add_replicas: bad batch");
   for (int64_t i = 0; i < n; i++)
@@ -1398,6 +1540,7 @@ int dgp_add_replicas(dgp_engine* e, int64_t n, const int32_t* task, const int32_
 }
 
 int dgp_remove_replicas(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_remove_replicas")) return rc;
   if (n < 0 || (n > 0 && (!task || !worker))) return fail(e, DGP_E_ARG, "dgp_remove_replicas: bad batch");
   for (int64_t i = 0; i < n; i++)
@@ -1415,6 +1558,7 @@ int dgp_remove_replicas(dgp_engine* e, int64_t n, const int32_t* task, const int
 }
 
 int dgp_set_worker_status(dgp_engine* e, int32_t worker, int32_t running, int64_t* n_new_placements) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (int rc = event_ready(e, "dgp_set_worker_status")) return rc;
   if (worker < 0 || worker >= e->D.W) return fail(e, DGP_E_ARG, "dgp_set_worker_status: worker out of range");
@@ -1430,6 +1574,7 @@ int dgp_set_worker_status(dgp_engine* e, int32_t worker, int32_t running, int64_
 }
 
 int dgp_long_running(dgp_engine* e, int32_t task, double compute_duration, int64_t* n_new_placements) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (int rc = event_ready(e, "dgp_long_running")) return rc;
   if (task < 0 || task >= e->D.N) return fail(e, DGP_E_ARG, "dgp_long_running: task out of range");
@@ -1441,6 +1586,7 @@ int dgp_long_running(dgp_engine* e, int32_t task, double compute_duration, int64
 }
 
 int dgp_heartbeat(dgp_engine* e, double bandwidth, int64_t n, const int32_t* prefix, const double* duration) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_heartbeat")) return rc;
   if (!(bandwidth > 0) || n < 0 || (n > 0 && (!prefix || !duration)))
     return fail(e, DGP_E_ARG, "dgp_heartbeat: bandwidth must be > 0; prefixes and durations");
@@ -1460,6 +1606,7 @@ int dgp_heartbeat(dgp_engine* e, double bandwidth, int64_t n, const int32_t* pre
 }
 
 int dgp_set_worker_flags(dgp_engine* e, int64_t n, const int32_t* worker, const uint8_t* idle, const uint8_t* saturated) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_set_worker_flags")) return rc;
   if (n < 0 || (n > 0 && (!worker || !idle || !saturated))) return fail(e, DGP_E_ARG, "dgp_set_worker_flags: bad batch");
   for (int64_t i = 0; i < n; i++) {
@@ -1478,6 +1625,7 @@ int dgp_set_worker_flags(dgp_engine* e, int64_t n, const int32_t* worker, const 
 }
 
 int dgp_set_wanted(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t* wanted) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_set_wanted")) return rc;
   if (n < 0 || (n > 0 && (!task || !wanted))) return fail(e, DGP_E_ARG, "dgp_set_wanted: bad batch");
   for (int64_t i = 0; i < n; i++)
@@ -1495,6 +1643,7 @@ int dgp_set_wanted(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t*
 }
 
 int dgp_task_erred(dgp_engine* e, int32_t task, int64_t* n_new_placements) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (int rc = event_ready(e, "dgp_task_erred")) return rc;
   if (task < 0 || task >= e->D.N) return fail(e, DGP_E_ARG, "dgp_task_erred: task out of range");
@@ -1504,6 +1653,7 @@ int dgp_task_erred(dgp_engine* e, int32_t task, int64_t* n_new_placements) {
 }
 
 int dgp_remove_worker(dgp_engine* e, int32_t worker) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_remove_worker")) return rc;
   if (worker < 0 || worker >= e->D.W) return fail(e, DGP_E_ARG, "dgp_remove_worker: worker out of range");
   if (e->paused_h[worker] == 2) return 0;  // already removed ("already-removed" :5196-5197)
@@ -1521,6 +1671,7 @@ int dgp_remove_worker(dgp_engine* e, int32_t worker) {
 
 int dgp_sync_placements(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* comm_bytes,
                         const double* start_time, const int64_t* ws_nbytes, const int8_t* route) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_sync_placements")) return rc;
   if (n < 0 || (n > 0 && (!task || !worker || !comm_bytes || !start_time || !ws_nbytes || !route)))
     return fail(e, DGP_E_ARG, "dgp_sync_placements: bad batch");
@@ -1551,6 +1702,7 @@ int dgp_sync_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t*
                    const int32_t* waiters, const int32_t* processing_on, const int64_t* nbytes,
                    const uint8_t* long_running, const uint8_t* wanted, const int64_t* holder_ptr,
                    const int32_t* holder_idx) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_sync_tasks")) return rc;
   if (n < 0 || (n > 0 && (!task || !state || !remaining || !waiters || !processing_on || !nbytes || !long_running ||
                           !wanted || !holder_ptr)))
@@ -1609,6 +1761,7 @@ int dgp_sync_workers(dgp_engine* e, int32_t n_workers, const int8_t* status, con
                      const int32_t* n_long_running, const int32_t* plen, const int32_t* prefix, const int32_t* count,
                      const int64_t* netocc, const int64_t* nbytes, const uint8_t* idle, const uint8_t* saturated,
                      const int64_t* needs_ptr, const int32_t* needs_task, const int32_t* needs_count) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_sync_workers")) return rc;
   dgp::Dev& D = e->D;
   namespace S = dgp::st;
@@ -1710,6 +1863,7 @@ int dgp_sync_globals(dgp_engine* e, int64_t n_tasks_counter, double network_occ_
                      const int32_t* g_prefix, const int64_t* g_count, int64_t n_queued, const int32_t* queued,
                      const double* duration_average, const double* max_exec_time, double bandwidth,
                      const int64_t* group_released_waiting, const int64_t* group_left, const int32_t* group_last_worker) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_sync_globals")) return rc;
   dgp::Dev& D = e->D;
   if (g_plen < 0 || g_plen > dgp::PMAX_G || (g_plen > 0 && (!g_prefix || !g_count)) || n_queued < 0 ||
@@ -1747,6 +1901,7 @@ int dgp_sync_globals(dgp_engine* e, int64_t n_tasks_counter, double network_occ_
 }
 
 int dgp_snapshot(dgp_engine* e) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->snap_rounds <= 0) return fail(e, DGP_E_STATE, "snapshots not enabled");
   HIPCHK(e, hipSetDevice(e->device));
@@ -1758,6 +1913,8 @@ int dgp_snapshot(dgp_engine* e) {
 
 int64_t dgp_num_placements(dgp_engine* e) {
   if (!e) return -1;
+  // the resident kernel publishes the log length with every answer
+  if (e->res_running) return __atomic_load_n(&e->mb->n_placed, __ATOMIC_ACQUIRE);
   dgp::Ctl c;
   if (read_ctl(e, &c)) return -1;
   return (int64_t)c.n_placed;
@@ -1766,6 +1923,15 @@ int64_t dgp_num_placements(dgp_engine* e) {
 int dgp_get_placements(dgp_engine* e, int64_t offset, int64_t count, int32_t* task, int32_t* worker,
                        int64_t* comm_bytes, double* start_time, int64_t* ws_nbytes, int8_t* route) {
   if (!e || offset < 0 || count < 0) return fail(e, DGP_E_ARG, "bad range");
+  if (e->res_running) {  // the last answer's new placements are in the mailbox (task / worker)
+    const int64_t a = e->mb->pl_from, b = e->mb->n_placed;
+    if (a >= 0 && offset >= a && offset + count <= b && !comm_bytes && !start_time && !ws_nbytes && !route) {
+      if (task) memcpy(task, dgp::svc::mbox_pl_task(e->mb) + (offset - a), (size_t)count * 4);
+      if (worker) memcpy(worker, dgp::svc::mbox_pl_worker(e->mb) + (offset - a), (size_t)count * 4);
+      return 0;
+    }
+    if (int rc = resident_stop(e)) return rc;
+  }
   int64_t n = dgp_num_placements(e);
   if (n < 0) return DGP_E_HIP;
   if (offset + count > n) return fail(e, DGP_E_ARG, "range beyond the placement log");
@@ -1786,6 +1952,7 @@ int dgp_get_placements(dgp_engine* e, int64_t offset, int64_t count, int32_t* ta
 }
 
 int dgp_enable_snapshots(dgp_engine* e, int64_t max_rounds) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->have_workers || max_rounds <= 0) return fail(e, DGP_E_ARG, "workers first; max_rounds > 0");
   HIPCHK(e, hipSetDevice(e->device));
   dgp::Dev& D = e->D;
@@ -1806,6 +1973,7 @@ int dgp_enable_snapshots(dgp_engine* e, int64_t max_rounds) {
 int dgp_get_snapshots(dgp_engine* e, int64_t* n_rounds, int32_t* nplaced, double* occupancy, int64_t* ws_nbytes,
                       int32_t* nprocessing, uint8_t* idle, uint8_t* saturated, uint8_t* idle_task_count,
                       int32_t* nqueued) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || e->snap_rounds <= 0) return fail(e, DGP_E_STATE, "snapshots not enabled");
   const dgp::Dev& D = e->D;
   dgp::Ctl c;
@@ -1830,6 +1998,7 @@ int dgp_get_snapshots(dgp_engine* e, int64_t* n_rounds, int32_t* nplaced, double
 }
 
 int dgp_get_task_states(dgp_engine* e, uint8_t* state) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->have_graph || !state) return fail(e, DGP_E_ARG, "graph first");
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipMemcpy(state, e->D.state, e->D.N, hipMemcpyDeviceToHost));
@@ -1837,6 +2006,7 @@ int dgp_get_task_states(dgp_engine* e, uint8_t* state) {
 }
 
 int dgp_kernel_times(dgp_engine* e, double* ms, int64_t* launches, int32_t n) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e) return DGP_E_ARG;
   if (int rc = resolve_timing(e)) return rc;
   for (int k = 0; k < n && k < 8; k++) {
@@ -1847,6 +2017,7 @@ int dgp_kernel_times(dgp_engine* e, double* ms, int64_t* launches, int32_t n) {
 }
 
 int dgp_set_timing(dgp_engine* e, int enabled) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e) return DGP_E_ARG;
   e->timing = enabled != 0;
   return 0;
@@ -1859,6 +2030,7 @@ extern "C" int dgp_debug_trace(dgp_engine* e, unsigned long long* out) {  // DGP
 }
 
 extern "C" int dgp_debug_buf(dgp_engine* e, double* out) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->D.dbgbuf) return DGP_E_ARG;
   HIPCHK(e, hipMemcpy(out, e->D.dbgbuf, 64 * 8 * sizeof(double), hipMemcpyDeviceToHost));
   return 0;
@@ -1928,16 +2100,18 @@ int dgp_conflict_depth(int64_t n_tasks, const int64_t* dep_ptr, const int32_t* d
 }
 
 int dgp_stats(dgp_engine* e, int64_t* out, int32_t n) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !out) return DGP_E_ARG;
   dgp::Ctl c;
   if (int rc = read_ctl(e, &c)) return rc;
-  int64_t v[38] = {(int64_t)c.n_placed, c.rounds_nonempty, c.dr_steps, c.n_global_events, (int64_t)c.rec_used,
+  int64_t v[42] = {(int64_t)c.n_placed, c.rounds_nonempty, c.dr_steps, c.n_global_events, (int64_t)c.rec_used,
                    (int64_t)c.walk_pos};
   for (int i = 0; i < 8; i++) v[6 + i] = (int64_t)c.prof[i];
   for (int i = 0; i < 16; i++) v[14 + i] = (int64_t)c.prof2[i];
   for (int i = 0; i < 8; i++) v[30 + i] = (int64_t)c.prof3[i];
+  for (int i = 0; i < 4; i++) v[38 + i] = e->res_prof[i];
 
-  for (int i = 0; i < n && i < 38; i++) out[i] = v[i];
+  for (int i = 0; i < n && i < 42; i++) out[i] = v[i];
   return 0;
 }
 
@@ -1955,6 +2129,7 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
                    const int64_t* d_nbytes, const int64_t* d_get_nbytes, const int64_t* h_ptr, const int32_t* h_idx,
                    const int64_t* r_ptr, const int32_t* r_idx, const uint8_t* r_flags, const int8_t* level_in,
                    const double* ifo_in, const int32_t* ift_in, int64_t* n_stealable) {
+  if (int rc_ = resident_stop(e)) return rc_;
   namespace S = dgp::steal;
   if (!e) return DGP_E_ARG;
   e->steal.loaded = false;
@@ -2139,6 +2314,7 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
 }
 
 int dgp_steal_thief_rows(dgp_engine* e, int64_t lo, int64_t hi) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e) return DGP_E_ARG;
   StealCtx& C = e->steal;
   if (!C.loaded) return fail(e, DGP_E_STATE, "dgp_steal_thief_rows: no dgp_steal_load");
@@ -2155,6 +2331,7 @@ int dgp_steal_thief_rows(dgp_engine* e, int64_t lo, int64_t hi) {
 int64_t dgp_steal_row_bytes(void) { return (int64_t)sizeof(dgp::steal::Row); }
 
 int dgp_steal_pack_rows(dgp_engine* e, int64_t lo, int64_t hi, void* dst) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e) return DGP_E_ARG;
   StealCtx& C = e->steal;
   if (!C.loaded) return fail(e, DGP_E_STATE, "dgp_steal_pack_rows: no dgp_steal_load");
@@ -2169,6 +2346,7 @@ int dgp_steal_pack_rows(dgp_engine* e, int64_t lo, int64_t hi, void* dst) {
 }
 
 int dgp_steal_unpack_rows(dgp_engine* e, int64_t lo, int64_t hi, const void* src) {
+  if (int rc_ = resident_stop(e)) return rc_;
   if (!e) return DGP_E_ARG;
   StealCtx& C = e->steal;
   if (!C.loaded) return fail(e, DGP_E_STATE, "dgp_steal_unpack_rows: no dgp_steal_load");
@@ -2186,6 +2364,7 @@ int dgp_steal_run(dgp_engine* e, int8_t* level_out, int32_t* st_task, int32_t* s
                   int32_t* st_level, double* st_cost, double* st_occ_victim, double* st_occ_thief, int64_t* n_steals,
                   double* inflight_occ, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* sat_out,
                   uint8_t* checked_out) {
+  if (int rc_ = resident_stop(e)) return rc_;
   namespace S = dgp::steal;
   if (!e) return DGP_E_ARG;
   StealCtx& C = e->steal;
@@ -2236,6 +2415,7 @@ int dgp_steal_balance(dgp_engine* e, int32_t W, const int32_t* nthreads, const d
                       int32_t* st_thief, int32_t* st_level, double* st_cost, double* st_occ_victim,
                       double* st_occ_thief, int64_t* n_steals, double* inflight_occ, int32_t* inflight_tasks,
                       uint8_t* idle_out, uint8_t* sat_out, uint8_t* checked_out) {
+  if (int rc_ = resident_stop(e)) return rc_;
   int64_t n = 0;
   if (int rc = dgp_steal_load(e, W, nthreads, occ, nproc, wnbytes, idle, sat, total_occ, total_nthreads, bandwidth, T,
                               victim, duration, fast, dep_ptr, dep_idx, n_data, d_nbytes, d_get_nbytes, h_ptr, h_idx,

@@ -179,6 +179,11 @@ class PlacementEngine:
                                                 _ptr(st), C.byref(newp)), "dgp_tasks_finished")
         return st, int(newp.value)
 
+    def set_resident(self, on: bool = True):
+        """Resident service mode (dgp_set_resident): the stream kernel stays launched between
+        tasks_finished calls and takes each batch from a pinned mailbox."""
+        self._check(self.lib.dgp_set_resident(self.h, 1 if on else 0), "dgp_set_resident")
+
     def move_task(self, task: int, thief: int):
         """Steal confirmation (WorkStealing.move_task_confirm, distributed/stealing.py
         :376-384): processing ``task`` moves from its worker to ``thief`` on the device."""
@@ -370,11 +375,15 @@ class PlacementEngine:
         self._check(self.lib.dgp_set_timing(self.h, 1 if on else 0), "dgp_set_timing")
 
     def stats(self) -> dict:
-        out = np.zeros(38, np.int64)
-        self._check(self.lib.dgp_stats(self.h, _ptr(out), 38), "dgp_stats")
+        out = np.zeros(42, np.int64)
+        self._check(self.lib.dgp_stats(self.h, _ptr(out), 42), "dgp_stats")
         return dict(zip(("placements", "rounds", "dr_steps", "global_stimuli", "records", "walk_pos",
                          "cyc_setup", "cyc_local_steps", "cyc_global", "cyc_finish", "cyc_reserve", "cyc_max_step",
-                         "cyc_exec_max", "cyc_exec_sum") + tuple(f"wave_phase{i}" for i in range(16)) + tuple(f"stall{i}" for i in range(8)),
+                         "cyc_exec_max", "cyc_exec_sum") + tuple(f"wave_phase{i}" for i in range(16))
+                        + tuple(f"stall{i}" for i in range(8))
+                        # resident service requests answered and the device's 100 MHz ticks spent
+                        # answering / running / publishing them (summed)
+                        + ("res_requests", "res_append_ticks", "res_run_ticks", "res_publish_ticks"),
                         map(int, out)))
 
     def kernel_times(self) -> dict:

@@ -746,6 +746,9 @@ class GPUPlacementExtension(SchedulerPlugin):
 
                     self.engine = PlacementEngine(self.device)
                 self.engine.load(g, self._config(), results=False)
+                # task-finished batches through the resident kernel (dgp_set_resident): no
+                # launch / copy / sync per call; every other engine call ends it first
+                self.engine.set_resident(True)
                 self.engine.update_graph()
                 self._fetch()
                 self.stats["graphs"] += 1

@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 8
+#define DGP_ABI_VERSION 9
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -157,6 +157,16 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
                        const int64_t* nbytes, const double* start, const double* stop, int8_t* status,
                        int64_t* n_new_placements);
 
+/* Resident service mode (ABI 9): with `enabled`, dgp_tasks_finished keeps the stream kernel
+ * launched between calls and hands it each batch through a mailbox in pinned host memory
+ * (the kernel's sequencer answers the messages, runs their stimuli and copies the new
+ * placements' task / worker back): no launch, no copy, no synchronisation per call. The
+ * kernel ends by itself after 0.2 s without a request (the next call launches it again),
+ * and every other entry point ends it first, so the calls keep their meaning; while it
+ * runs, dgp_num_placements and dgp_get_placements of the last answer's placements (task /
+ * worker columns only) read the mailbox. */
+int dgp_set_resident(dgp_engine* e, int enabled);
+
 /* Steal confirmation (WorkStealing.move_task_confirm, stealing.py:333-399, its "confirm"
  * branch :376-384 and finally clause :396-399): processing task `task` leaves its worker
  * (the victim: WorkerState.remove_from_processing, scheduler.py:759-771) for `thief`
@@ -164,7 +174,7 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
  * scheduler-global prefix counts, then check_idle_saturated(thief) and (victim). The task
  * keeps its placement-log position as its run identity: its later task-finished message
  * comes from the thief with that run_id (dgp_tasks_finished). Service mode, graphs on the
- * stream engine (<= 8 prefixes, no restrictions); DGP_E_DEVICE if the task is not processing. */
+ * stream engine (<= 32 prefixes); DGP_E_DEVICE if the task is not processing. */
 int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief);
 
 /* A worker joins (Scheduler.add_worker, scheduler.py:4308-4441) with `nthreads` threads; its
@@ -175,8 +185,8 @@ int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief);
  * stimulus_queue_slots_maybe_opened (:4416-4420, :4983-5023): queued tasks taken in queue
  * order by decide_worker_rootish_queuing_enabled (:2227-2236) onto idle_task_count.
  * *n_new_placements receives the placements made (read them with dgp_get_placements).
- * Service mode, graphs on the stream engine (<= 8 prefixes, no restrictions: no task is
- * no-worker, so bulk_schedule_unrunnable_after_adding_worker :3173-3186 has nothing to do).
+ * Service mode, graphs on the stream engine (<= 32 prefixes); refused (DGP_E_STATE) while a
+ * task is no-worker (bulk_schedule_unrunnable_after_adding_worker :3173-3186 is not modelled).
  * Snapshots taken earlier read 0 for the new worker. */
 int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements);
 
@@ -189,16 +199,16 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements);
  * TaskPrefix keeps its duration average). Group sizes and root-ish groups follow the grown
  * graph (is_rootish :2929-2947). Then the update_graph stimulus of the new tasks (:4600-4651):
  * released -> waiting, the runnable ones to processing (or queued) in priority order.
- * *n_new_placements receives the placements made. Stream-engine graphs (<= 8 prefixes in
- * total), no restrictions. */
+ * *n_new_placements receives the placements made. Stream-engine graphs (<= 32 prefixes in
+ * total); the earlier tasks keep their restrictions, the new ones have none. */
 int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx, const int64_t* prio,
                   const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
                   const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override,
                   int64_t* n_new_placements);
 
 /* ---- Service events: the other placement-input stimuli of a live scheduler, in the order the
- * scheduler handles them, between dgp_tasks_finished calls. Stream-engine graphs (<= 8 prefixes,
- * no restrictions); DGP_E_STATE otherwise. A case the engine does not model returns
+ * scheduler handles them, between dgp_tasks_finished calls. Stream-engine graphs (<= 32 prefixes);
+ * DGP_E_STATE otherwise. A case the engine does not model returns
  * DGP_E_DEVICE ("a service event the engine does not model") and the caller hands placement
  * back to the scheduler. Those returning n_new_placements may refill the queue
  * (stimulus_queue_slots_maybe_opened :4983-5023): read the placements with dgp_get_placements. */

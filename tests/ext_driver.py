@@ -64,6 +64,9 @@ class FixtureEngine:
     def load(self, g, config, results=True):
         self.graph, self.config = g, config
 
+    def set_resident(self, on=True):  # the real engine's launch mode: nothing to serve here
+        self.resident = bool(on)
+
     def update_graph(self):
         self.n, self.k = self.stim[0], 1
 

@@ -112,6 +112,17 @@ def test_engine_returns_what_the_extension_consumes():
         assert isinstance(newp, int) and eng.num_placements() == n + newp
         more = eng.placements(n, newp)
         assert more["pl_task"].dtype == np.int32 and len(more["pl_task"]) == newp
+        # the same through the resident kernel (the extension's mode): the placements of the
+        # answer come from the mailbox, columns as the extension asks for them
+        eng.set_resident(True)
+        n1 = eng.num_placements()
+        t2, w2 = int(pl["pl_task"][1]), int(pl["pl_worker"][1])  # still processing (run_id 1)
+        st2, newp2 = eng.tasks_finished([t2], [w2], [1], [int(g["nbytes"][t2])], [0.0], [0.01])
+        assert st2.dtype == np.int8 and st2.tolist() == [0] and isinstance(newp2, int)
+        assert eng.num_placements() == n1 + newp2
+        pr = eng.placements(n1, newp2, columns=("pl_task", "pl_worker"))
+        assert set(pr) == {"pl_task", "pl_worker"} and pr["pl_task"].dtype == np.int32 and len(pr["pl_worker"]) == newp2
+        eng.set_resident(False)
         # event calls: the counts the extension's _fetch picks up afterwards
         assert eng.add_replicas([t], [(w + 1) % 16]) is None
         assert isinstance(eng.set_worker_status(3, 0), int)

@@ -64,12 +64,13 @@ def drive(eng, msgs, ptr, per_message):
     return np.array(status, np.int8)
 
 
-def run_service(g, cfg, exp, msgs, ptr, per_message):
+def run_service(g, cfg, exp, msgs, ptr, per_message, resident=False):
     from distributed_amd.engine import PlacementEngine
 
     R = len(exp["round_nplaced"]) + 2
     with PlacementEngine(0) as eng:
         eng.load(g, cfg, snapshots=R, results=False)
+        eng.set_resident(resident)
         eng.update_graph()
         status = drive(eng, msgs, ptr, per_message)
         out = eng.placements()
@@ -89,20 +90,40 @@ def test_service_matches_reference_fixture(name, per_message):
     assert np.array_equal(out["final_state"], exp["final_state"])
 
 
-SVC = sorted(f for f in golden_files() if f.startswith("svc_"))
+RESIDENT = ["c2var_sat1.1.npz", "c2mini_satinf.npz", "c3mini_sat1.1.npz", "restr_sat1.1.npz", "c2p12_sat1.1.npz",
+            "svc_c2var_sat1.1.npz"]
 
 
 @pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])
+@pytest.mark.parametrize("name", RESIDENT)
+def test_resident_service_matches_reference_fixture(name, per_message):
+    """The same message streams through the resident kernel (dgp_set_resident): each batch
+    goes through the pinned mailbox while the kernel stays launched; the snapshot between
+    rounds ends it (every other entry point does) and the next batch launches it again."""
+    g, cfg, exp, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
+    msgs, ptr = fixture_messages(g, exp)
+    out, status = run_service(g, cfg, exp, msgs, ptr, per_message, resident=True)
+    assert (status == 0).all(), np.bincount(status)
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+SVC = sorted(f for f in golden_files() if f.startswith("svc_"))
+
+
+@pytest.mark.parametrize("resident", [False, True], ids=["launch", "resident"])
+@pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])
 @pytest.mark.parametrize("name", SVC)
-def test_service_stale_duplicate_memory(name, per_message):
-    """The reference's answers to stale / duplicate / in-memory / unknown reports."""
+def test_service_stale_duplicate_memory(name, per_message, resident):
+    """The reference's answers to stale / duplicate / in-memory / unknown reports (also through
+    the resident kernel, whose answers split a batch into segments exactly as k_svc_append)."""
     path = os.path.join(GOLDEN, name)
     g, cfg, exp, meta = oracle.load_fixture(path)
     z = np.load(path, allow_pickle=False)
     msgs = list(zip(z["msg_task"].tolist(), z["msg_worker"].tolist(), z["msg_runid"].tolist(),
                     z["msg_nbytes"].tolist(), z["msg_start"].tolist(), z["msg_stop"].tolist()))
     ptr = z["msg_round_ptr"].tolist()
-    out, status = run_service(g, cfg, exp, msgs, ptr, per_message)
+    out, status = run_service(g, cfg, exp, msgs, ptr, per_message, resident)
     want = z["msg_status"]
     bad = np.nonzero(status != want)[0]
     assert len(bad) == 0, f"{len(bad)} status mismatches, first message {bad[0]}: {status[bad[0]]} vs {want[bad[0]]}"
