@@ -71,7 +71,7 @@ SIGNATURES = {
                                    _P, _P, _P]),
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 _lib = None
 
 

@@ -14,8 +14,11 @@ OUT = os.path.join(PKG, "libdgplace.so")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 # -ffp-contract=off: no fused multiply-add, so fp64 results round exactly like the
 # reference's CPython arithmetic (the parity contract is bit-exact objectives).
+# module-wide LDS lowering: the stream roles run out of line (one register budget each) and
+# reach the engine's LDS blocks at fixed addresses, not through a per-kernel offset table
+# re-read (scalar load + lgkmcnt wait) on every access.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
-         "-Wall"]
+         "-Wall", "-mllvm", "-amdgpu-lower-module-lds-strategy=module"]
 
 
 def build(force: bool = False) -> str:

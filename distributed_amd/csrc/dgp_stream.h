@@ -60,6 +60,9 @@ __constant__ Dev c_dev;
 #ifndef DGP_REG_PROBES
 #define DGP_REG_PROBES 0  // registrar sub-phase s_memtime probes (diagnostics)
 #endif
+#ifndef DGP_STAGE_PRIO
+#define DGP_STAGE_PRIO 0  // issue priority of the builder / prefetcher waves
+#endif
 #ifndef DGP_RB
 #define DGP_RB 8  // registrar batch (stimuli registered per poll, one lane each)
 #endif
@@ -3429,6 +3432,7 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
   // batch-tolerant builder / prefetcher / walker take the remaining issue slots
   if (wave == 3) __builtin_amdgcn_s_setprio(3);
   else if (wave == 0 || wave >= N_ROLE) __builtin_amdgcn_s_setprio(2);
+  else if (DGP_STAGE_PRIO && (wave == 1 || wave == 2)) __builtin_amdgcn_s_setprio(DGP_STAGE_PRIO);
   if (wave == 0) {
     if (pos->round_end < 0) round_start = 0;
     role_seq<LW>(D, L, P, round_start);

@@ -108,6 +108,7 @@ struct dgp_engine {
   dgp::svc::Mbox* mb_dev = nullptr;  // device address
   bool resident = false;             // service calls go through the resident kernel
   bool res_running = false;          // the resident kernel was launched (it may have ended since)
+  bool pending_resync = false;       // a later graph with dependencies on earlier tasks: dgp_sync_* next
   unsigned long long req_seq = 0;    // the last request number sent
   int64_t res_prof[4] = {0, 0, 0, 0};  // requests answered; sums of append, run, publish (device 100 MHz ticks)
 };
@@ -228,6 +229,14 @@ int resident_stop(dgp_engine* e) {
   e->D.resident = 0;
   if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("resident kernel: ") + hipGetErrorString(st));
   return 0;
+}
+
+// A kernel's static LDS bytes as built (the module-wide LDS lowering, build.py, allocates
+// every LDS variable its out-of-line callees use at fixed addresses in the kernel's block)
+size_t kernel_static_lds(const void* fn, size_t fallback) {
+  hipFuncAttributes a;
+  if (hipFuncGetAttributes(&a, fn) != hipSuccess) return fallback > 32 * 1024 ? fallback : 32 * 1024;
+  return a.sharedSizeBytes;
 }
 
 int resolve_timing(dgp_engine* e) {
@@ -369,7 +378,10 @@ void stream_source(dgp_engine* e, bool service) {
 int launch_stream(dgp_engine* e, long long max_rounds, int snaps) {
   const dgp::Dev& D = e->D;
   const size_t lds_w = dgp::st::lds_worker_bytes(D.W);
-  const bool lw = sizeof(dgp::st::SLds) + lds_w <= 160 * 1024;
+  // the kernel's static LDS (module-wide LDS lowering can place more than SLds in it)
+  static size_t stat_lds = 0;
+  if (!stat_lds) stat_lds = kernel_static_lds((const void*)dgp::st::k_stream<true>, sizeof(dgp::st::SLds));
+  const bool lw = stat_lds + lds_w <= 160 * 1024;
   // c_dev is one symbol per device, shared by every engine on it: re-sent unless it holds
   // exactly this engine's Dev already (content compare; engines are driven from one thread)
   static struct {
@@ -427,7 +439,8 @@ int run_service_stimuli(dgp_engine* e) {
     const int lds_workers = e->D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
     const size_t lds = (((size_t)e->D.W * sizeof(int) + 15) & ~(size_t)15) +
                        (lds_workers ? (((size_t)e->D.W + 3) & ~(size_t)3) * dgp::LDS_WORKER_BYTES + 64 : 0);
-    if (lds > 160 * 1024) return fail(e, DGP_E_ARG, "commit LDS exceeds 160 KiB");
+    if (lds + kernel_static_lds((const void*)dgp::k_replay, 0) > 160 * 1024)
+      return fail(e, DGP_E_ARG, "commit LDS exceeds 160 KiB");
     hipLaunchKernelGGL(V::k_svc_round_begin, dim3(1), dim3(64), 0, s, DP, e->d_aux + 2);
     if (int rc = timed_launch(e, 0, [&] { hipLaunchKernelGGL(dgp::k_frontier_release, dim3(big), dim3(256), 0, s, DP); }))
       return rc;
@@ -985,7 +998,8 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out) {
     const int lds_workers = D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
     const size_t lds = (((size_t)D.W * sizeof(int) + 15) & ~(size_t)15) +
                        (lds_workers ? (((size_t)D.W + 3) & ~(size_t)3) * dgp::LDS_WORKER_BYTES + 64 : 0);
-    if (lds > 160 * 1024) return fail(e, DGP_E_ARG, "commit LDS exceeds 160 KiB");
+    if (lds + kernel_static_lds((const void*)dgp::k_replay, 0) > 160 * 1024)
+      return fail(e, DGP_E_ARG, "commit LDS exceeds 160 KiB");
     const dgp::Dev* DPC = e->d_dev + 1;
     const int snaps = e->snap_rounds > 0 ? 1 : 0;
     if (int rc = timed_launch(e, 2, [&] {
@@ -1107,6 +1121,7 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
                        int64_t* n_new_placements) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
+  if (e->pending_resync) return fail(e, DGP_E_STATE, "dgp_tasks_finished: dgp_sync_* first (a later graph depends on earlier tasks)");
   if (n < 0 || (n > 0 && (!task || !worker || !run_id || !nbytes || !start || !stop || !status)))
     return fail(e, DGP_E_ARG, "dgp_tasks_finished: bad batch");
   if (n_new_placements) *n_new_placements = 0;
@@ -1166,6 +1181,7 @@ int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief) {
   if (!(e->D.P <= dgp::st::PX))
     return fail(e, DGP_E_STATE, "dgp_move_task: the round-kernel engine (more than 32 prefixes) "
                                 "has no steal confirmation");
+  if (e->pending_resync) return fail(e, DGP_E_STATE, "dgp_move_task: dgp_sync_* first (a later graph depends on earlier tasks)");
   if (task < 0 || task >= e->D.N || thief < 0 || thief >= e->D.W)
     return fail(e, DGP_E_ARG, "dgp_move_task: task or thief out of range");
   HIPCHK(e, hipSetDevice(e->device));
@@ -1181,6 +1197,7 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
   if (n_new_placements) *n_new_placements = 0;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
+  if (e->pending_resync) return fail(e, DGP_E_STATE, "dgp_add_worker: dgp_sync_* first (a later graph depends on earlier tasks)");
   if (!(e->D.P <= dgp::st::PX))
     return fail(e, DGP_E_STATE, "dgp_add_worker: the round-kernel engine (more than 32 prefixes) "
                                 "has no worker addition");
@@ -1289,6 +1306,7 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   if (n_new_placements) *n_new_placements = 0;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
+  if (e->pending_resync) return fail(e, DGP_E_STATE, "dgp_add_graph: dgp_sync_* first (a later graph depends on earlier tasks)");
   dgp::Dev& D = e->D;
   if (std::count_if(e->paused_h.begin(), e->paused_h.end(), [](uint8_t v) { return v != 0; }))
     return fail(e, DGP_E_STATE, "dgp_add_graph: not while a worker is paused or removed");
@@ -1305,9 +1323,13 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
     if (dep_ptr[t + 1] < dep_ptr[t]) return fail(e, DGP_E_ARG, "dgp_add_graph: dep_ptr not monotone");
   const int64_t En = dep_ptr[n_new];
   if (En > 0 && !dep_idx) return fail(e, DGP_E_ARG, "dgp_add_graph: dep_idx missing");
-  for (int64_t k = 0; k < En; k++)
-    if (dep_idx[k] < 0 || dep_idx[k] >= n_new)
-      return fail(e, DGP_E_ARG, "dgp_add_graph: dependencies must be tasks of the new graph");
+  // a dependency is a task of the new graph (0 .. n_new-1) or an earlier task t (-1 - t)
+  bool ext_deps = false;
+  for (int64_t k = 0; k < En; k++) {
+    if (dep_idx[k] >= n_new || (dep_idx[k] < 0 && -1 - (int64_t)dep_idx[k] >= N0))
+      return fail(e, DGP_E_ARG, "dgp_add_graph: dependency out of range");
+    ext_deps = ext_deps || dep_idx[k] < 0;
+  }
   const int64_t pmax = *std::max_element(e->h_prio.begin(), e->h_prio.end());
   for (int64_t t = 0; t < n_new; t++)
     if (prio[t] <= pmax) return fail(e, DGP_E_ARG, "dgp_add_graph: new priorities must follow every earlier task's");
@@ -1326,7 +1348,12 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
     wa.push_back(wanted[t]);
     ov.push_back(rootish_override[t]);
   }
-  for (int64_t k = 0; k < En; k++) di.push_back((int32_t)(dep_idx[k] + N0));
+  for (int64_t t = 0; t < n_new; t++) {  // rows ascending in the whole graph's numbering
+    const size_t r0 = di.size();
+    for (int64_t k = dep_ptr[t]; k < dep_ptr[t + 1]; k++)
+      di.push_back(dep_idx[k] >= 0 ? (int32_t)(dep_idx[k] + N0) : (int32_t)(-1 - (int64_t)dep_idx[k]));
+    std::sort(di.begin() + r0, di.end());
+  }
   std::vector<double> pd(e->prefix_defaults);
   pd.resize(n_prefixes);
   for (int32_t q = P0; q < n_prefixes; q++) pd[q] = prefix_default_duration[q];
@@ -1438,6 +1465,15 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   }
   HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), e->tflags_h.data(), N1, hipMemcpyHostToDevice));
   free_list(old_allocs);
+  if (ext_deps) {
+    // the new tasks stay released: the scheduler decides this update_graph stimulus itself
+    // (the new tasks' waiting_on / the earlier tasks' waiters, any placement it makes) and
+    // the caller hands over its state (dgp_sync_*) before the next stimulus
+    e->pending_resync = true;
+    e->mode = 2;
+    if (int rc = sync_dev(e)) return rc;
+    return 0;
+  }
   // the update_graph stimulus of the new tasks (:4600-4651): released -> waiting, the
   // runnable ones (no dependency: the new graph is independent of the old) to processing
   // or queued in priority order
@@ -1469,6 +1505,9 @@ namespace {
 // the common preconditions of a service event: the stream engine in service mode
 int event_ready(dgp_engine* e, const char* what) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (e->pending_resync && strncmp(what, "dgp_sync_", 9) != 0 && strcmp(what, "dgp_remove_worker") != 0)
+    return fail(e, DGP_E_STATE, std::string(what) + ": the scheduler decides the stimulus of a graph that depends on "
+                                                    "earlier tasks; dgp_sync_* first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
   if (!(e->D.P <= dgp::st::PX))
     return fail(e, DGP_E_STATE, std::string(what) + ": the round-kernel engine (more than 32 prefixes) has no "
@@ -1897,7 +1936,9 @@ int dgp_sync_globals(dgp_engine* e, int64_t n_tasks_counter, double network_occ_
   HIPCHK(e, hipMemcpy(D.g_left, group_left, (size_t)D.G * 8, hipMemcpyHostToDevice));
   HIPCHK(e, hipMemcpy(D.g_lastw, group_last_worker, (size_t)D.G * 4, hipMemcpyHostToDevice));
   D.bandwidth = bandwidth;
-  return sync_dev(e);
+  if (int rc = sync_dev(e)) return rc;
+  e->pending_resync = false;  // the resync is complete (dgp_sync_globals comes last)
+  return 0;
 }
 
 int dgp_snapshot(dgp_engine* e) {

@@ -201,9 +201,11 @@ class PlacementEngine:
     def add_graph(self, g: dict) -> int:
         """A later graph submission (Scheduler.update_graph, distributed/scheduler.py
         :4662-4751) on a running engine: ``g`` holds the new tasks only (dependencies
-        relative to it, priorities after every earlier task's, prefix / group ids and
-        ``prefix_default_dur`` / ``group_prefix`` over the engine-wide tables). Runs their
-        update_graph stimulus; returns the number of placements it made."""
+        relative to it, ``-1 - t`` for an earlier task t; priorities after every earlier
+        task's, prefix / group ids and ``prefix_default_dur`` / ``group_prefix`` over the
+        engine-wide tables). Runs their update_graph stimulus; returns the number of
+        placements it made. With dependencies on earlier tasks the stimulus is the
+        scheduler's: nothing is placed and ``sync()`` must follow (include/dgplace.h)."""
         arrs = {
             "dep_ptr": np.ascontiguousarray(g["dep_ptr"], np.int64),
             "dep_idx": np.ascontiguousarray(g["dep_idx"], np.int32),

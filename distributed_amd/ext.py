@@ -99,11 +99,13 @@ def _compute_interval(startstops):
     return math.nan, math.nan
 
 
-def graph_from_tasks(tss, nthreads, valid_workers=None, worker_index=None):
+def graph_from_tasks(tss, nthreads, valid_workers=None, worker_index=None, earlier=None):
     """TaskState objects -> the engine's graph arrays (the layout of distributed_amd/graphs.py).
 
     Tasks are indexed in ascending ``TaskState.priority`` (so ``prio`` is their rank: unique
-    and topological for dask.order priorities); dependencies must be among ``tss``.
+    and topological for dask.order priorities); dependencies must be among ``tss`` or, with
+    ``earlier`` (key -> engine index of the tasks already uploaded), earlier tasks, which a
+    row names as ``-1 - index`` (dgp_add_graph).
     Prefixes / groups get ids in first-seen order; ``prefix_default_dur`` is each
     ``TaskPrefix.duration_average`` now (default-task-durations or -1).
 
@@ -117,10 +119,16 @@ def graph_from_tasks(tss, nthreads, valid_workers=None, worker_index=None):
     n = len(tss)
     rows = []
     for ts in tss:
-        try:
-            rows.append(sorted(index[d.key] for d in ts.dependencies))
-        except KeyError as e:
-            raise ValueError(f"dependency {e} of {ts.key!r} is not in the uploaded graph") from None
+        r = []
+        for d in ts.dependencies:
+            i = index.get(d.key)
+            if i is None:
+                j = earlier.get(d.key) if earlier is not None else None
+                if j is None:
+                    raise ValueError(f"dependency {d.key!r} of {ts.key!r} is not in the uploaded graph")
+                i = -1 - j
+            r.append(i)
+        rows.append(sorted(r))
     pnames, gnames, gpref = {}, {}, []
     pid = np.zeros(n, np.int32)
     gid = np.zeros(n, np.int32)
@@ -759,12 +767,14 @@ class GPUPlacementExtension(SchedulerPlugin):
 
     def _add_graph(self, new):
         """A later update_graph (scheduler.py:4662-4751) on the running engine: the new
-        tasks must not depend on earlier ones (graph_from_tasks raises otherwise) and must
-        all follow them in priority (a new generation, :4713, with no user priority above
-        the earlier graphs'); prefixes and groups map into the engine-wide tables."""
+        tasks must all follow the earlier ones in priority (a new generation, :4713, with no
+        user priority above the earlier graphs'); prefixes and groups map into the
+        engine-wide tables. An independent graph's update_graph stimulus runs on the engine;
+        a graph that depends on earlier tasks is appended (dgp_add_graph) and its stimulus
+        is the scheduler's own, the engine resynchronised after it (``_suspend``)."""
         s = self.scheduler
         g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers], s.valid_workers,
-                                    self.worker_index)
+                                    self.worker_index, earlier=self.task_index)
         if "restr_flags" in g:
             raise NotImplementedError("worker restrictions in a later graph")
         if min(ts.priority for ts in new) <= self.max_priority:
@@ -789,12 +799,19 @@ class GPUPlacementExtension(SchedulerPlugin):
         self._end_of_stimulus("the previous stimulus")
         if not self.active:
             return
+        dependent = bool((g["dep_idx"] < 0).any())
         self.engine.add_graph(g2)
         self.keys = self.keys + keys_
         self.task_index.update({k: n0 + i for i, k in enumerate(keys_)})
         self.max_priority = max(ts.priority for ts in new)
-        self._fetch()
         self.stats["graphs"] += 1
+        if dependent:
+            self.stats["dependent_graphs"] += 1
+            self._suspend("a later graph that depends on earlier tasks")
+            for k in keys_:  # the new tasks, the earlier ones they wait on / add waiters to
+                self._mark_dirty(k)
+            return
+        self._fetch()
 
     def add_worker(self, scheduler=None, worker=None):
         """SchedulerPlugin.add_worker (diagnostics/plugin.py): Scheduler.add_worker calls it

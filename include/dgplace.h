@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 9
+#define DGP_ABI_VERSION 10
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -192,15 +192,21 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements);
 
 /* A later graph submission (Scheduler.update_graph, scheduler.py:4662-4751 ->
  * _create_taskstate_from_graph :4512-4653) on a running engine, service mode: n_new tasks
- * appended with indices N.. (dep_ptr / dep_idx relative to the new graph: the new graph may
- * not depend on earlier tasks), priorities after every earlier task's (a new generation,
+ * appended with indices N.. (dep_ptr / dep_idx relative to the new graph; dep_idx = -1 - t
+ * names the earlier task t), priorities after every earlier task's (a new generation,
  * :4713), prefix / group ids in the engine-wide tables (n_prefixes / n_groups >= the
  * current counts; prefix_default_duration is read for the new prefixes only: a known
  * TaskPrefix keeps its duration average). Group sizes and root-ish groups follow the grown
  * graph (is_rootish :2929-2947). Then the update_graph stimulus of the new tasks (:4600-4651):
  * released -> waiting, the runnable ones to processing (or queued) in priority order.
  * *n_new_placements receives the placements made. Stream-engine graphs (<= 32 prefixes in
- * total); the earlier tasks keep their restrictions, the new ones have none. */
+ * total); the earlier tasks keep their restrictions, the new ones have none.
+ * A graph with dependencies on earlier tasks is appended (the dependents rows of those tasks
+ * grow) but its update_graph stimulus is the scheduler's own (the earlier tasks' states
+ * decide the new tasks' waiting_on, :4600-4651): the new tasks stay released, no placement is
+ * made, and every stimulus call answers DGP_E_STATE until the caller hands over the
+ * scheduler's state after that stimulus (dgp_sync_placements / _tasks / _workers / _globals,
+ * below; the new tasks and the earlier tasks they depend on among the synced rows). */
 int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx, const int64_t* prio,
                   const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
                   const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override,

@@ -17,12 +17,19 @@ def pytest_configure(config):
 def golden_files():
     """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
-                  and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcev_", "svcrs_")))
+                  and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcgdep_", "svcev_",
+                                            "svcrs_")))
 
 
 def svc_second_graph_files():
     """Service-mode message streams with a second graph submitted (gen_service.py second-graph)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcgraph_") and f.endswith(".npz"))
+
+
+def svc_dep_graph_files():
+    """Service-mode streams with a later graph that depends on earlier tasks (gen_service.py
+    second-graph svcgdep_*): the scheduler decides its stimulus, the engine resyncs."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcgdep_") and f.endswith(".npz"))
 
 
 def second_graph(g, z, with_results=False):

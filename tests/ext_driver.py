@@ -92,6 +92,8 @@ class FixtureEngine:
 
     def add_graph(self, g):  # a later graph (the fixture's per-event placement counts)
         self.graphs.append(g)
+        if (np.asarray(g["dep_idx"]) < 0).any():  # dependent: appended, the scheduler's stimulus, then sync()
+            return 0
         return self.add_worker(0)
 
     def add_worker(self, nthreads):  # a join (the fixture's per-event placement counts)
@@ -382,7 +384,9 @@ def run_second_graph(name):
     submitted mid-stream through the tail of ``_create_taskstate_from_graph``
     (scheduler.py:4600-4653: the plugins' update_graph hook, then the transitions); the
     extension uploads it to the engine (dgp_add_graph) and the scheduler takes the engine's
-    decisions for both graphs from then on."""
+    decisions for both graphs from then on. ``svcgdep_*``: the second graph depends on earlier
+    tasks; the extension appends it, lets the scheduler decide that stimulus and resyncs the
+    engine (the rows it sends are the scheduler's state, the fixture's dump)."""
     import operator
 
     from gen_service import TOKEN2
@@ -402,7 +406,8 @@ def run_second_graph(name):
     S.validate_key = lambda self, key, ts=None: None
     S.send_all = lambda self, client_msgs, worker_msgs: None
     fkeys = [ts.key for ts in tss]
-    eng = FixtureEngine(exp, fkeys)
+    dep = name.startswith("svcgdep_")
+    eng = (EventEngine if dep else FixtureEngine)(exp, fkeys)
     ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
     eng.ext = ext
     s.stream_handlers = {}
@@ -452,7 +457,7 @@ def run_second_graph(name):
                 new.append(ts)
             for k, ts in enumerate(new):
                 for d in g2["dep_idx"][g2["dep_ptr"][k]:g2["dep_ptr"][k + 1]]:
-                    ts.add_dependency(new[int(d)])
+                    ts.add_dependency(new[int(d)] if d >= 0 else tss[-1 - int(d)])
                 if g2["wanted"][k]:
                     ts.who_wants = {cs}
                     cs.wants_what.add(ts)
@@ -473,7 +478,33 @@ def run_second_graph(name):
     assert ext.active, ext.reason
     assert len(eng.graphs) == 1
     up = eng.graphs[0]
-    assert np.array_equal(up["dep_ptr"], g2["dep_ptr"]) and np.array_equal(up["dep_idx"], g2["dep_idx"])
+    assert np.array_equal(up["dep_ptr"], g2["dep_ptr"])
+    for k in range(g2["n_tasks"]):  # earlier tasks by their engine index (-1 - index)
+        row = g2["dep_idx"][g2["dep_ptr"][k]:g2["dep_ptr"][k + 1]].tolist()
+        want = sorted(d if d >= 0 else -1 - ext.task_index[fkeys[-1 - d]] for d in row)
+        assert up["dep_idx"][up["dep_ptr"][k]:up["dep_ptr"][k + 1]].tolist() == want, k
+    host = 0
+    if dep:  # one resync, right after the submission: the fixture's dump
+        syncs = [c for c in eng.calls if c[0] == "sync"]
+        assert len(syncs) == 1 and ext.stats["dependent_graphs"] == 1, (len(syncs), ext.stats)
+        _, host, tasks, workers, glob = syncs[0]
+        assert host == int(z["g2_nplaced"])
+        ptr0 = {k: z[k + "_ptr"] for k in z.files if k.startswith("sync_") and k + "_ptr" in z.files}
+        dump = {k: z[k][p[0]:p[1]] for k, p in ptr0.items()}
+        row_of = {int(t): i for i, t in enumerate(dump["sync_tasks_task"].tolist())}
+        fields = ("state", "remaining", "waiters", "processing_on", "nbytes", "long_running", "wanted")
+        synced = set()
+        for i, t in enumerate(tasks["task"].tolist()):
+            f = tidx[ext.keys[t]]
+            synced.add(f)
+            assert all(tasks[fl][i] == dump["sync_tasks_" + fl][row_of[f]] for fl in fields), (t, f)
+        for k in range(g2["n_tasks"]):  # every new task and every earlier task it depends on
+            assert N1 + k in synced
+            for d in g2["dep_idx"][g2["dep_ptr"][k]:g2["dep_ptr"][k + 1]]:
+                assert (N1 + int(d) if d >= 0 else -1 - int(d)) in synced
+        for part, rows in (("workers", workers), ("globals", glob)):
+            for fl, v in rows.items():
+                assert np.array_equal(np.atleast_1d(np.asarray(v)), dump[f"sync_{part}_{fl}"]), (part, fl)
     pnames = {i: nm for nm, i in ext.prefix_index.items()}
     gnames = {i: nm for nm, i in ext.group_index.items()}
     assert [pnames[i] for i in up["prefix_id"]] == [g2["prefix_names"][i] for i in g2["prefix_id"]]
@@ -484,9 +515,9 @@ def run_second_graph(name):
     assert rec["task"] == exp["pl_task"].tolist()
     assert rec["worker"] == exp["pl_worker"].tolist()
     assert np.array_equal(np.array(rec["start"]).view(np.int64), exp["pl_start"].view(np.int64))
-    assert ext.stats["device_decisions"] == n, (ext.stats, n)
+    assert ext.stats["device_decisions"] == n - host, (ext.stats, n, host)
     return dict(fixture=name, placements=n, graphs=ext.stats["graphs"], device_decisions=ext.stats["device_decisions"],
-                active=ext.active, reason=ext.reason)
+                host_placements=host, resyncs=ext.stats["resyncs"], active=ext.active, reason=ext.reason)
 
 
 class EventEngine(FixtureEngine):
@@ -781,7 +812,7 @@ if __name__ == "__main__":
     plain = "--plain" in args
     stream = "--stream" in args
     for nm in [a for a in args if not a.startswith("--")]:
-        fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith("svcgraph_")
+        fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith(("svcgraph_", "svcgdep_"))
               else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_")) else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,
                                                plain="plugin" if "--plugin" in args else plain,

@@ -327,7 +327,7 @@ def main_add_workers(only):
 TOKEN2 = "f9e8d7c6b5a49382716051e4d3c2b1a0"
 
 
-def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0):
+def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0):
     """The replay protocol's completions as task-finished messages, with a second,
     independent graph ``g2`` submitted part-way through, the way
     ``Scheduler._create_taskstate_from_graph`` (distributed/scheduler.py:4512-4653) adds it:
@@ -335,7 +335,12 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0):
     graph's, so each TaskPrefix keeps its duration average), priority ``(0, 2, i)`` (a later
     generation than the first graph's ``(0, 1, i)``), dependencies, ``who_wants``, then every
     new task recommended "waiting" in priority order. The new tasks get indices N.. in the
-    fixture; their completions follow the protocol like the others'."""
+    fixture; their completions follow the protocol like the others'.
+
+    ``dep_frac``: that fraction of the new tasks also depends on one earlier task (in memory,
+    processing, waiting or queued when the graph arrives); the scheduler's state after the
+    submission is dumped as resync rows (the engine appends the graph, the scheduler decides
+    that stimulus, the engine resyncs)."""
     from distributed.core import Status
     from distributed.scheduler import Scheduler, WorkerState
 
@@ -373,6 +378,8 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0):
     cs = s.clients["client-0"]
     run_spec = (operator.add, (), {})
     added = {"msg": -1}
+    ext = {"ptr": None, "idx": None, "dumps": [], "nplaced": 0}
+    rng_dep = np.random.default_rng(seed + 7)
 
     def submit():
         keys2 = G.make_keys(g2)
@@ -386,14 +393,28 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0):
                 ts._rootish = bool(ov)
             new.append(ts)
         ptr, idx = g2["dep_ptr"], g2["dep_idx"]
+        earlier = [ts for ts in tss if ts.state in ("memory", "processing", "waiting", "queued")]
+        rows = []
         for t, ts in enumerate(new):
-            for d in idx[ptr[t]:ptr[t + 1]]:
-                ts.add_dependency(new[int(d)])
+            row = [int(d) for d in idx[ptr[t]:ptr[t + 1]]]
+            for d in row:
+                ts.add_dependency(new[d])
+            if dep_frac and earlier and rng_dep.random() < dep_frac:
+                o = earlier[int(rng_dep.integers(0, len(earlier)))]
+                ts.add_dependency(o)
+                row.append(-1 - tidx[o.key])
+            rows.append(row)
             if g2["wanted"][t]:
                 ts.who_wants = {cs}
                 cs.wants_what.add(ts)
+        ext["ptr"] = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
+        ext["idx"] = np.array([d for r in rows for d in r], np.int32)
         recs2 = {ts.key: "waiting" for ts in sorted(new, key=lambda t: t.priority, reverse=True)}
         s._transitions(recs2, {}, {}, "update-graph-2")
+        if dep_frac:
+            gall = dict(prefix_names=g["prefix_names"], prefix_default_dur=g["prefix_default_dur"],
+                        group_names=list(g["group_names"]) + list(g2["group_names"]))
+            ext["dumps"].append(_dump(s, gall, tidx, widx, [ts.key for ts in tss] + [ts.key for ts in new]))
         tss.extend(new)
 
     msgs = {k: [] for k in ("task", "worker", "run_id", "nbytes", "start", "stop", "status")}
@@ -422,6 +443,7 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0):
                 n0 = len(rec["task"])
                 submit()
                 stim.append(len(rec["task"]) - n0)
+                ext["nplaced"] = stim[-1]
             t = rec["task"][pos]
             ts = tss[t]
             assert ts.state == "processing", (ts.key, ts.state)
@@ -443,7 +465,7 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0):
     assert added["msg"] >= 0 and len(joins["msg"]) == n_add
     rec["stim"] = stim
     states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
-    return rec, rounds, nplaced, states, msgs, round_ptr, added["msg"], joins
+    return rec, rounds, nplaced, states, msgs, round_ptr, added["msg"], joins, ext
 
 
 def main_second_graph(only):
@@ -457,9 +479,16 @@ def main_second_graph(only):
         # restrictions on the first graph (the later one has none) and 12 task prefixes
         "svcgraph_restr_sat1.1": (dict(n=3000, w=32, seed=37, n_inner_prefixes=11, random_durations=True,
                                        nthreads="random", restrict=0.3), dict(n=2000, seed=38), 1.1, 0.3, 8),
+        # later graphs that depend on earlier tasks (the scheduler decides their stimulus, then resync)
+        "svcgdep_c2var_sat1.1": (dict(n=3000, w=32, seed=41, n_inner_prefixes=3, random_durations=True,
+                                      nthreads="random"), dict(n=2000, seed=42), 1.1, 0.3, 0, 0.2),
+        "svcgdep_c2mini_satinf": (dict(n=2500, w=24, seed=43), dict(n=1500, seed=44), float("inf"), 0.5, 0, 0.3),
+        "svcgdep_joins_sat1.0": (dict(n=3000, w=32, seed=45, n_inner_prefixes=2, random_durations=True,
+                                      nthreads="random"), dict(n=2000, seed=46), 1.0, 0.4, 12, 0.1),
     }
-    for name, (a, b, sat, frac, *nadd) in cases.items():
-        nadd = nadd[0] if nadd else 0
+    for name, (a, b, sat, frac, *more) in cases.items():
+        nadd = more[0] if more else 0
+        dep_frac = more[1] if len(more) > 1 else 0.0
         if only and name not in only:
             continue
         kw = {k: v for k, v in a.items() if k not in ("n", "w", "seed", "restrict")}
@@ -472,7 +501,8 @@ def main_second_graph(only):
         G.graphs.check_graph(g)
         dask.config.set({"distributed.scheduler.worker-saturation": sat})
         cfg = G.config_dict(sat)
-        rec, rounds, nplaced, states, msgs, round_ptr, at, joins = replay_second_graph(g, g2, cfg, 0, frac, nadd)
+        rec, rounds, nplaced, states, msgs, round_ptr, at, joins, ext = replay_second_graph(g, g2, cfg, 0, frac, nadd,
+                                                                                          dep_frac)
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -485,6 +515,9 @@ def main_second_graph(only):
             z.update(add_msg=np.array(joins["msg"], np.int64), add_nthreads=np.array(joins["nthreads"], np.int32))
         for k in ("dep_ptr", "dep_idx", "prio", "prefix_id", "group_id", "wanted", "rootish_override"):
             z["g2_" + k] = np.asarray(g2[k])
+        if dep_frac:  # dependencies on earlier tasks (-1 - t), the submission's placements, resync rows
+            z.update(g2_dep_ptr=ext["ptr"], g2_dep_idx=ext["idx"], g2_nplaced=np.array(ext["nplaced"], np.int64),
+                     **_pack_dumps(ext["dumps"]))
         np.savez_compressed(path, **z)
         routes = np.bincount(np.array(rec["route"]), minlength=4).tolist()
         print(f"{name}: {len(msgs['task'])} messages, second graph of {g2['n_tasks']} at message {at}, routes {routes}")

@@ -29,7 +29,9 @@ sys.path.insert(0, REPO)
 
 import gen_steal as GS  # noqa: E402  (shim + reference)
 
-from distributed_amd.stealing import GPUWorkStealing  # noqa: E402
+import numpy as np  # noqa: E402
+
+from distributed_amd.stealing import GPUWorkStealing, steal_problem_from_state  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 
@@ -57,6 +59,40 @@ def state_of(s, steal, events, comms):
     )
 
 
+def rows_equal(steal):
+    """The incremental task rows (StealRows) give the full rebuild's problem: identical
+    columns, and per task the same dependencies (nbytes, get_nbytes, holders) up to their
+    numbering."""
+    a, ta, _ = steal_problem_from_state(steal)
+    b, tb, _ = steal.problem()
+    assert ta == tb, "task order"
+    assert set(a) == set(b), (sorted(a), sorted(b))
+    per_dep = ("dep_idx", "data_nbytes", "data_get_nbytes", "holder_ptr", "holder_idx")
+    for k in a:
+        if k in per_dep:
+            continue
+        if isinstance(a[k], np.ndarray):
+            assert a[k].dtype == b[k].dtype and np.array_equal(a[k], b[k]), k
+        else:
+            assert a[k] == b[k], k
+
+    def deps(p):
+        out = []
+        for t in range(len(p["dep_ptr"]) - 1):
+            r = []
+            for d in p["dep_idx"][p["dep_ptr"][t]:p["dep_ptr"][t + 1]]:
+                h = tuple(p["holder_idx"][p["holder_ptr"][d]:p["holder_ptr"][d + 1]])
+                r.append((int(p["data_nbytes"][d]), int(p["data_get_nbytes"][d]), h))
+            out.append(sorted(r))
+        return out
+
+    assert deps(a) == deps(b), "dependency rows"
+    for p in (a, b):  # rows ascending (the device's dependency walks assume it)
+        for t in range(len(p["dep_ptr"]) - 1):
+            r = p["dep_idx"][p["dep_ptr"][t]:p["dep_ptr"][t + 1]]
+            assert np.all(np.diff(r) > 0), "row order"
+
+
 def run(name, case):
     out = {}
     for kind in ("reference", "gpu"):
@@ -65,13 +101,17 @@ def run(name, case):
             eng = OracleEngine()
             kw = dict(steal_base=GPUWorkStealing, steal_kwargs=dict(engine_factory=lambda: eng, validate=True))
         s, steal, widx, tidx, data, work, deps_of, events, comms = GS.build(**case, **kw)
-        steal.balance()
-        steal.balance()
+        for _ in range(2):
+            if kind == "gpu":
+                rows_equal(steal)
+            steal.balance()
         out[kind] = state_of(s, steal, events, comms)
+        if kind == "gpu":
+            rebuilt = steal.gpu_stats["rows_rebuilt"]
     ref, gpu = out["reference"], out["gpu"]
     diff = [k for k in ref if ref[k] != gpu[k]]
     n_req = sum(len(e[1]) for e in ref["events"])
-    return dict(case=name, requests=n_req, balance_events=len(ref["events"]), differ=diff)
+    return dict(case=name, requests=n_req, balance_events=len(ref["events"]), differ=diff, rows_rebuilt=rebuilt)
 
 
 CASES = {

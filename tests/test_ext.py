@@ -67,6 +67,20 @@ def test_extension_follows_a_second_graph():
         assert r["active"] and r["device_decisions"] == r["placements"] and r["graphs"] == 2, r
 
 
+def test_extension_follows_a_dependent_later_graph():
+    """A later graph whose tasks depend on earlier ones (in memory, processing, waiting or
+    queued): the extension appends it to the engine (dgp_add_graph with -1 - index rows), the
+    scheduler decides that update_graph stimulus, the engine resyncs once from the
+    scheduler's state (the rows equal the reference dump, every new task and every earlier
+    task it depends on among them) and every later decision is the engine's (validate=True)."""
+    names = ["svcgdep_c2mini_satinf.npz", "svcgdep_c2var_sat1.1.npz", "svcgdep_joins_sat1.0.npz"]
+    res = drive(names)
+    assert [r["fixture"] for r in res] == names
+    for r in res:
+        assert r["active"] and r["graphs"] == 2 and r["resyncs"] == 1, r
+        assert r["device_decisions"] + r["host_placements"] == r["placements"] and r["host_placements"] > 0, r
+
+
 EVENTS = ["svcev_c2var_sat1.1.npz", "svcev_c2mini_satinf.npz", "svcev_dense_sat1.0.npz"]
 
 
@@ -143,7 +157,8 @@ def test_gpu_work_stealing_matches_reference_plugin():
     """GPUWorkStealing (distributed_amd/stealing.py) vs the reference WorkStealing on two
     identical states, two balance() calls each: request events, metrics, in-flight
     accounts, steal-request messages, bins and idle / saturated sets all equal
-    (tests/steal_ext_driver.py; the engine is the oracle stand-in there)."""
+    (tests/steal_ext_driver.py; the engine is the oracle stand-in there). Before each
+    balance() the incrementally kept task rows (StealRows) equal a full rebuild."""
     env = dict(os.environ, PYTHONHASHSEED="0")
     env.pop("PYTHONPATH", None)
     out = subprocess.run([PY39, os.path.join(REPO, "tests", "steal_ext_driver.py")], capture_output=True, text=True,
@@ -152,7 +167,7 @@ def test_gpu_work_stealing_matches_reference_plugin():
     res = [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
     assert len(res) == 4
     for r in res:
-        assert r["differ"] == [] and r["requests"] > 0, r
+        assert r["differ"] == [] and r["requests"] > 0 and r["rows_rebuilt"] == 0, r
 
 
 def test_confirmed_steal_moves_the_task_on_the_engine():

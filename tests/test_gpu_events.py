@@ -20,7 +20,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, svc_event_files, svc_resync_files
+from conftest import GOLDEN, second_graph, svc_dep_graph_files, svc_event_files, svc_resync_files
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -168,3 +168,56 @@ def test_service_resync_matches_reference(name):
     # a forgotten task (client released, :2853) leaves SchedulerState.tasks; its engine row
     # stays, released (distributed_amd/sync.py)
     assert np.array_equal(out["final_state"], np.where(exp["final_state"] == 7, 0, exp["final_state"]))
+
+
+@pytest.mark.parametrize("name", svc_dep_graph_files())
+def test_service_dependent_later_graph_matches_reference(name):
+    """A later graph whose tasks depend on earlier ones (in memory, processing, waiting or
+    queued when it arrives): dgp_add_graph appends it (the earlier tasks' dependents rows
+    grow) without placing; the scheduler decides that update_graph stimulus (its placements
+    and state are the fixture's, gen_service.py svcgdep_*) and the engine resyncs; every later
+    placement, the snapshots and the final states are the engine's and equal the reference's."""
+    from distributed_amd import _lib
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    msgs = list(zip(z["msg_task"].tolist(), z["msg_worker"].tolist(), z["msg_runid"].tolist(),
+                    z["msg_nbytes"].tolist(), z["msg_start"].tolist(), z["msg_stop"].tolist()))
+    ptr = z["msg_round_ptr"].tolist()
+    at = int(z["g2_msg"])
+    g2 = second_graph(g, z)
+    assert (np.asarray(g2["dep_idx"]) < 0).sum() > 0
+    joins = {}
+    for m, nt in zip(z["add_msg"].tolist() if "add_msg" in z.files else [],
+                     z["add_nthreads"].tolist() if "add_nthreads" in z.files else []):
+        joins.setdefault(m, []).append(nt)
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        for k in range(len(ptr) - 1):
+            for i in range(ptr[k], ptr[k + 1]):
+                for nt in joins.get(i, ()):
+                    eng.add_worker(nt)
+                if i == at:
+                    n0 = eng.num_placements()
+                    assert eng.add_graph(g2) == 0 and eng.num_placements() == n0
+                    with pytest.raises(_lib.DgpError, match="dgp_sync"):  # nothing runs before the resync
+                        eng.tasks_finished(*[[c] for c in msgs[i]])
+                    sl = slice(n0, n0 + int(z["g2_nplaced"]))
+                    eng.sync_placements(exp["pl_task"][sl], exp["pl_worker"][sl], exp["pl_comm"][sl],
+                                        exp["pl_start"][sl], exp["pl_wsnbytes"][sl], exp["pl_route"][sl])
+                    d = sync_dump(z, 0)
+                    eng.sync(None, d["tasks"], d["workers"], d["globals"])
+                st, _ = eng.tasks_finished(*[[c] for c in msgs[i]])
+                assert st.tolist() == [0], (i, st)
+            if ptr[k + 1] > ptr[k]:
+                eng.snapshot()
+        assert eng.n_tasks == g["n_tasks"] + len(g2["prio"])
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])

@@ -8,7 +8,7 @@ mkdir -p tools/_var
 pids=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -shared $flags \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -shared -mllvm -amdgpu-lower-module-lds-strategy=module $flags \
     -o tools/_var/lib_$name.so distributed_amd/csrc/dgplace.hip 2> tools/_var/$name.err &
   pids+=($!)
 done
