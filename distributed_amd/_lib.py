@@ -37,6 +37,7 @@ SIGNATURES = {
     "dgp_snapshot": (C.c_int, [_P]),
     "dgp_num_placements": (C.c_int64, [_P]),
     "dgp_get_placements": (C.c_int, [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, _P]),
+    "dgp_task_messages": (C.c_int, [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, _P, _P]),
     "dgp_enable_snapshots": (C.c_int, [_P, C.c_int64]),
     "dgp_get_snapshots": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dgp_get_task_states": (C.c_int, [_P, _P]),
@@ -71,7 +72,7 @@ SIGNATURES = {
                                    _P, _P, _P]),
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 _lib = None
 
 

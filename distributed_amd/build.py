@@ -9,7 +9,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 SRC = [os.path.join(PKG, "csrc", "dgplace.hip")]
 DEPS = [os.path.join(PKG, "csrc", "dgp_device.h"), os.path.join(PKG, "csrc", "dgp_stream.h"),
         os.path.join(PKG, "csrc", "dgp_steal.h"), os.path.join(PKG, "csrc", "dgp_service.h"),
-        os.path.join(PKG, "csrc", "dgp_events.h"), os.path.join(PKG, "csrc", "dgp_svcmsg.h")]
+        os.path.join(PKG, "csrc", "dgp_events.h"), os.path.join(PKG, "csrc", "dgp_svcmsg.h"),
+        os.path.join(PKG, "csrc", "dgp_msgs.h")]
 OUT = os.path.join(PKG, "libdgplace.so")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 # -ffp-contract=off: no fused multiply-add, so fp64 results round exactly like the

@@ -30,6 +30,7 @@
 #include "dgp_events.h"
 #include "dgp_steal.h"
 #include "dgp_service.h"
+#include "dgp_msgs.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -102,6 +103,8 @@ struct dgp_engine {
   int64_t sv_used = 0;                     // service stimuli appended (accepted task-finished messages)
   char* d_ev = nullptr;                    // service-event argument staging (device)
   size_t d_ev_cap = 0;
+  char* d_msgbuf = nullptr;                // dgp_task_messages scratch (device)
+  size_t d_msgbuf_cap = 0;
   // resident service mode (dgp_set_resident): the stream kernel stays launched between
   // dgp_tasks_finished calls and takes each batch from a mailbox in pinned host memory
   dgp::svc::Mbox* mb = nullptr;      // host address
@@ -524,6 +527,7 @@ void dgp_destroy(dgp_engine* e) {
   if (e->d_status) (void)hipFree(e->d_status);
   if (e->h_msgs) (void)hipHostFree(e->h_msgs);
   if (e->d_ev) (void)hipFree(e->d_ev);
+  if (e->d_msgbuf) (void)hipFree(e->d_msgbuf);
   if (e->steal.arena) (void)hipFree(e->steal.arena);
   (void)hipFree(e->ctl);
   (void)hipFree(e->d_aux);
@@ -1990,6 +1994,84 @@ int dgp_get_placements(dgp_engine* e, int64_t offset, int64_t count, int32_t* ta
   HIPCHK(e, cp(route, D.pl_route, 1));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   return 0;
+}
+
+int dgp_task_messages(dgp_engine* e, int64_t offset, int64_t count, int64_t* n_deps, int64_t* n_holders,
+                      int64_t* dep_ptr, int32_t* dep_task, int64_t* dep_nbytes, int64_t* holder_ptr,
+                      int32_t* holder_idx) {
+  if (int rc_ = resident_stop(e)) return rc_;
+  if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (offset < 0 || count < 0 || !n_deps || !n_holders) return fail(e, DGP_E_ARG, "dgp_task_messages: bad arguments");
+  const int64_t n = dgp_num_placements(e);
+  if (n < 0) return DGP_E_HIP;
+  if (offset + count > n) return fail(e, DGP_E_ARG, "dgp_task_messages: range beyond the placement log");
+  if (count > INT32_MAX / 2) return fail(e, DGP_E_ARG, "dgp_task_messages: batch too large");
+  HIPCHK(e, hipSetDevice(e->device));
+  *n_deps = *n_holders = 0;
+  if (count == 0) {
+    if (dep_ptr) dep_ptr[0] = 0;
+    if (holder_ptr) holder_ptr[0] = 0;
+    return 0;
+  }
+  auto grow = [&](size_t need) -> int {
+    if (need <= e->d_msgbuf_cap) return 0;
+    if (e->d_msgbuf) (void)hipFree(e->d_msgbuf);
+    e->d_msgbuf = nullptr;
+    e->d_msgbuf_cap = 0;
+    const size_t cap = std::max(need, (size_t)1 << 20);
+    HIPCHK(e, hipMalloc((void**)&e->d_msgbuf, cap));
+    e->d_msgbuf_cap = cap;
+    return 0;
+  };
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  // pass 1: per placement, its dependencies and their holders
+  const size_t c = (size_t)count;
+  if (int rc = grow(2 * al(c * 4))) return rc;
+  int32_t* d_nd = (int32_t*)e->d_msgbuf;
+  int32_t* d_nh = (int32_t*)(e->d_msgbuf + al(c * 4));
+  hipStream_t s = e->stream;
+  if (int rc = sync_dev(e)) return rc;
+  hipLaunchKernelGGL(dgp::msg::k_msg_count, dim3((unsigned)((c + 255) / 256)), dim3(256), 0, s, e->d_dev,
+                     (long long)offset, (int)count, d_nd, d_nh);
+  HIPCHK(e, hipGetLastError());
+  std::vector<int32_t> nd(c), nh(c);
+  HIPCHK(e, hipMemcpyAsync(nd.data(), d_nd, c * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(e, hipMemcpyAsync(nh.data(), d_nh, c * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(e, hipStreamSynchronize(s));
+  std::vector<int64_t> dp(c + 1, 0), hb(c + 1, 0);
+  for (size_t j = 0; j < c; j++) {
+    dp[j + 1] = dp[j] + nd[j];
+    hb[j + 1] = hb[j] + nh[j];
+  }
+  *n_deps = dp[c];
+  *n_holders = hb[c];
+  if (!dep_ptr) return 0;  // size query
+  if (!dep_task || !dep_nbytes || !holder_ptr || (hb[c] > 0 && !holder_idx))
+    return fail(e, DGP_E_ARG, "dgp_task_messages: output arrays missing");
+  memcpy(dep_ptr, dp.data(), (c + 1) * 8);
+  const size_t E = (size_t)dp[c], H = (size_t)hb[c];
+  // pass 2: the rows, at the scanned offsets
+  const size_t o_dp = 0, o_hb = o_dp + al((c + 1) * 8), o_task = o_hb + al((c + 1) * 8), o_nb = o_task + al(E * 4),
+               o_hc = o_nb + al(E * 8), o_hi = o_hc + al(E * 4), total = o_hi + al(H * 4);
+  if (int rc = grow(total)) return rc;
+  char* B = e->d_msgbuf;
+  HIPCHK(e, hipMemcpyAsync(B + o_dp, dp.data(), (c + 1) * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(e, hipMemcpyAsync(B + o_hb, hb.data(), (c + 1) * 8, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(dgp::msg::k_msg_fill, dim3((unsigned)((c + 255) / 256)), dim3(256), 0, s, e->d_dev,
+                     (long long)offset, (int)count, (const int64_t*)(B + o_dp), (const int64_t*)(B + o_hb),
+                     (int32_t*)(B + o_task), (int64_t*)(B + o_nb), (int32_t*)(B + o_hc), (int32_t*)(B + o_hi));
+  HIPCHK(e, hipGetLastError());
+  std::vector<int32_t> hc(E);
+  if (E) {
+    HIPCHK(e, hipMemcpyAsync(dep_task, B + o_task, E * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(e, hipMemcpyAsync(dep_nbytes, B + o_nb, E * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(e, hipMemcpyAsync(hc.data(), B + o_hc, E * 4, hipMemcpyDeviceToHost, s));
+  }
+  if (H) HIPCHK(e, hipMemcpyAsync(holder_idx, B + o_hi, H * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(e, hipStreamSynchronize(s));
+  holder_ptr[0] = 0;
+  for (size_t k = 0; k < E; k++) holder_ptr[k + 1] = holder_ptr[k] + hc[k];
+  return check_device_error(e);
 }
 
 int dgp_enable_snapshots(dgp_engine* e, int64_t max_rounds) {

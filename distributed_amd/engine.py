@@ -342,6 +342,24 @@ class PlacementEngine:
             self._check(-2, "dgp_num_placements")
         return int(n)
 
+    def task_messages(self, offset: int, count: int) -> dict:
+        """who_has / nbytes of the compute-task messages of placements [offset, offset +
+        count) from the engine's state now (dgp_task_messages, _task_to_msg
+        scheduler.py:3421-3450): ``dep_ptr`` [count + 1] / ``dep_task`` / ``dep_nbytes`` per
+        dependency, ``holder_ptr`` [n_deps + 1] / ``holder_idx`` (ascending worker index)."""
+        nd, nh = C.c_int64(0), C.c_int64(0)
+        self._check(self.lib.dgp_task_messages(self.h, int(offset), int(count), C.byref(nd), C.byref(nh), None, None,
+                                               None, None, None), "dgp_task_messages")
+        out = dict(dep_ptr=np.zeros(count + 1, np.int64), dep_task=np.zeros(nd.value, np.int32),
+                   dep_nbytes=np.zeros(nd.value, np.int64), holder_ptr=np.zeros(nd.value + 1, np.int64),
+                   holder_idx=np.zeros(max(nh.value, 1), np.int32))
+        self._check(self.lib.dgp_task_messages(self.h, int(offset), int(count), C.byref(nd), C.byref(nh),
+                                               *(_ptr(out[k]) for k in ("dep_ptr", "dep_task", "dep_nbytes",
+                                                                        "holder_ptr", "holder_idx"))),
+                    "dgp_task_messages")
+        out["holder_idx"] = out["holder_idx"][:nh.value]
+        return out
+
     _PL_COLUMNS = (("pl_task", np.int32), ("pl_worker", np.int32), ("pl_comm", np.int64), ("pl_start", np.float64),
                    ("pl_wsnbytes", np.int64), ("pl_route", np.int8))
 

@@ -51,6 +51,8 @@
  *                         the tasks placed in round k-1 (tests/golden/gen_golden.py)
  *   dgp_get_placements    the compute-task decisions (_add_to_processing :3199 /
  *                         _task_to_msg :3421): task, worker, comm bytes, objective, route
+ *   dgp_task_messages     the who_has / nbytes fields of their compute-task messages
+ *                         (_task_to_msg :3421-3450)
  *   dgp_steal_balance     WorkStealing.steal_time_ratio (stealing.py:241-277) for every
  *                         processing task + one WorkStealing.balance() (:401-503, _get_thief
  *                         :532-542, move_task_request :279-331, check_idle_saturated)
@@ -64,7 +66,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 10
+#define DGP_ABI_VERSION 11
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -312,6 +314,21 @@ int dgp_snapshot(dgp_engine* e);
 int64_t dgp_num_placements(dgp_engine* e);
 int dgp_get_placements(dgp_engine* e, int64_t offset, int64_t count, int32_t* task, int32_t* worker,
                        int64_t* comm_bytes, double* start_time, int64_t* ws_nbytes, int8_t* route);
+
+/* The compute-task message fields of placements [offset, offset + count)
+ * (SchedulerState._task_to_msg, scheduler.py:3421-3450: who_has / nbytes of every
+ * dependency), from the engine's state now: call it after the engine call that made the
+ * placements and before the next stimulus, as _add_to_processing builds the message.
+ * Per placement j its dependencies dep_ptr[j] .. dep_ptr[j+1]-1 (the graph's CSR order):
+ * dep_task (task index), dep_nbytes (TaskState.nbytes as sent, -1: none reported), and their
+ * who_has holder_ptr[k] .. holder_ptr[k+1]-1 in holder_idx (ascending worker index: every
+ * replica once add-keys / dgp_add_replicas added some). *n_deps / *n_holders receive the row
+ * counts; with dep_ptr NULL the call only sizes (then call again with dep_ptr[count + 1],
+ * dep_task / dep_nbytes[n_deps], holder_ptr[n_deps + 1], holder_idx[n_holders]). Ends the
+ * resident kernel (like every call but dgp_tasks_finished). */
+int dgp_task_messages(dgp_engine* e, int64_t offset, int64_t count, int64_t* n_deps, int64_t* n_holders,
+                      int64_t* dep_ptr, int32_t* dep_task, int64_t* dep_nbytes, int64_t* holder_ptr,
+                      int32_t* holder_idx);
 
 /* Per-round worker snapshots (state after update_graph and after each round). */
 int dgp_enable_snapshots(dgp_engine* e, int64_t max_rounds);

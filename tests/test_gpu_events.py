@@ -221,3 +221,65 @@ def test_service_dependent_later_graph_matches_reference(name):
         out["final_state"] = eng.task_states()
     assert_same(out, exp, PL_KEYS + ROUND_KEYS)
     assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+@pytest.mark.parametrize("name", svc_event_files())
+def test_task_messages_follow_replicas(name):
+    """dgp_task_messages (the who_has / nbytes fields of _task_to_msg, scheduler.py
+    :3421-3450) after every event of a svcev_* stream, for the placements that event made:
+    each dependency's who_has equals a model of SchedulerState.who_has driven by the same
+    stream (the completing worker, then add-keys adding and release-worker-data removing
+    replicas), in ascending worker order, and its nbytes the size its task-finished reported."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    kind, task, worker = z["ev_kind"], z["ev_task"], z["ev_worker"]
+    hp, ht, hd = z["hb_ptr"], z["hb_task"], z["hb_dur"]
+    dp, di = g["dep_ptr"], g["dep_idx"]
+    who, nbytes = {}, {}
+    checked = multi = 0
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, results=False)
+        eng.update_graph()
+        for i in range(len(kind)):
+            n0 = eng.num_placements()
+            kd, t, w = int(kind[i]), int(task[i]), int(worker[i])
+            if kd == EV_FINISHED:
+                st, _ = eng.tasks_finished([t], [w], [int(z["ev_runid"][i])], [int(z["ev_nbytes"][i])],
+                                           [float(z["ev_start"][i])], [float(z["ev_stop"][i])])
+                assert st.tolist() == [0]
+                who[t] = {w}
+                nbytes[t] = int(z["ev_nbytes"][i])
+            elif kd == EV_ADD_KEYS:
+                eng.add_replicas([t], [w])
+                who.setdefault(t, set()).add(w)
+            elif kd == EV_RELEASE_DATA:
+                eng.remove_replicas([t], [w])
+                who[t].discard(w)
+            elif kd in (EV_PAUSE, EV_RESUME):
+                eng.set_worker_status(w, 1 if kd == EV_RESUME else 0)
+            elif kd == EV_LONG_RUNNING:
+                eng.long_running(t, float(z["ev_x"][i]))
+            elif kd == EV_HEARTBEAT:
+                ts = ht[hp[i]:hp[i + 1]]
+                eng.heartbeat(float(z["ev_x"][i]), g["prefix_id"][ts], hd[hp[i]:hp[i + 1]])
+            elif kd == EV_ERRED:
+                eng.task_erred(t)
+            n1 = eng.num_placements()
+            if n1 == n0:
+                continue
+            m = eng.task_messages(n0, n1 - n0)
+            pl = eng.placements(n0, n1 - n0)
+            for j, x in enumerate(pl["pl_task"].tolist()):
+                deps = di[dp[x]:dp[x + 1]].tolist()
+                a, b = int(m["dep_ptr"][j]), int(m["dep_ptr"][j + 1])
+                assert m["dep_task"][a:b].tolist() == deps, (i, x)
+                for k, d in zip(range(a, b), deps):
+                    hs = m["holder_idx"][m["holder_ptr"][k]:m["holder_ptr"][k + 1]].tolist()
+                    assert hs == sorted(who[d]), (i, x, d, hs, who[d])
+                    assert int(m["dep_nbytes"][k]) == nbytes[d], (i, x, d)
+                    multi += len(hs) > 1
+                checked += 1
+    assert checked > 1000 and multi > 0, (checked, multi)
