@@ -286,13 +286,14 @@ def service_leg(eng_cls, local: int, args) -> dict:
            "n_tasks": int(g["n_tasks"])}
     outs = {}
     cols = ("pl_task", "pl_worker")
-    for mode in ("per_round", "per_message", "per_round_resident", "per_message_resident"):
+    for mode in ("per_round", "per_message", "per_round_resident", "per_message_resident", "per_round_messages"):
         eng = eng_cls(local)
         eng.load(g, CONFIG, results=False)
         eng.set_resident(mode.endswith("resident"))
         eng.update_graph()
         done, calls = 0, 0
         n = eng.num_placements()
+        t_msg, n_msg, n_dep = 0.0, 0, 0
         t0 = time.perf_counter()
         while n > done:  # each batch: the previous one's new placements, completed in run_id order
             p = eng.placements(done, n - done, columns=cols)
@@ -302,6 +303,12 @@ def service_leg(eng_cls, local: int, args) -> dict:
             done = n
             if mode.startswith("per_round"):
                 _, k = eng.tasks_finished(t, w, r, nb, a, b)
+                if mode == "per_round_messages" and k:  # + the batch's compute-task who_has / nbytes
+                    tm = time.perf_counter()
+                    m = eng.task_messages(n, k)
+                    t_msg += time.perf_counter() - tm
+                    n_msg += 1
+                    n_dep += len(m["dep_task"])
                 n += k
                 calls += 1
             else:
@@ -320,6 +327,9 @@ def service_leg(eng_cls, local: int, args) -> dict:
         eng.close()
         leg[mode] = {"messages_per_s": round(g["n_tasks"] / dt, 1), "calls": calls,
                      "us_per_call": round(dt / max(calls, 1) * 1e6, 1), "seconds": round(dt, 4)}
+        if n_msg:  # dgp_task_messages (_task_to_msg fields) per batch, host-inclusive
+            leg[mode].update(task_messages_calls=n_msg, task_messages_us_per_call=round(t_msg / n_msg * 1e6, 1),
+                             task_messages_dependencies=n_dep)
     if not args.no_cpu_baseline:
         from oracle import oracle
 
