@@ -60,6 +60,9 @@ __constant__ Dev c_dev;
 #ifndef DGP_REG_PROBES
 #define DGP_REG_PROBES 0  // registrar sub-phase s_memtime probes (diagnostics)
 #endif
+#ifndef DGP_EXE_CONT
+#define DGP_EXE_CONT 0  // an executor first claims the stimulus its release of the completing worker made ready
+#endif
 #ifndef DGP_STAGE_PRIO
 #define DGP_STAGE_PRIO 0  // issue priority of the builder / prefetcher waves
 #endif
@@ -1876,9 +1879,9 @@ __device__ __forceinline__ bool dict_update(const WPtr<LW>& P, int c, int p, int
 // of them is the one waiting for s on c, and it alone counted s (role_reg): it counts down.
 // With WAITC the high half of the old mask says, per successor, whether it registered the
 // worker as a candidate only: its candidate count (predc) counts down instead.
-__device__ __forceinline__ void release_succ(SLds& L, SMask old) {
+__device__ __forceinline__ int release_succ(SLds& L, SMask old) {  // -> the slot made ready, or -1
   const SMask succ = WAITC ? (old & 0xffffffffull) : old;
-  if (!succ) return;
+  if (!succ) return -1;
   int bs = __builtin_ctzll(succ);
   long long best = vload(&L.sid[bs]);
   for (SMask m = succ & (succ - 1); m; m &= m - 1) {
@@ -1891,17 +1894,19 @@ __device__ __forceinline__ void release_succ(SLds& L, SMask old) {
   }
   if (WAITC && ((old >> 32) >> bs) & 1ull) {
     __hip_atomic_fetch_add(&L.predc[bs], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return;
+    return -1;
   }
   if (atomicSub(&L.pred[bs], 1) == 1) {
     atomicOr(&L.c.ready, 1ull << bs);
     if (DGP_TRACE == 1) { const Dev& D = c_dev; TR(L.sid[bs], 1); }
+    return bs;
   }
+  return -1;
 }
 template <bool LW>
-__device__ __forceinline__ void release_worker(SLds& L, const WPtr<LW>& P, int s, int c) {
+__device__ __forceinline__ int release_worker(SLds& L, const WPtr<LW>& P, int s, int c) {
   const SMask bit = slot_bits(s);
-  release_succ(L, __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
+  return release_succ(L, __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
 }
 
 // release the workers of slot s (the waiting successors may run) — LDS state only
@@ -2001,7 +2006,8 @@ __device__ __forceinline__ DTab stim_durations(const Dev& D, SLds& L, const uint
 // a stimulus whose effects stay on the workers it registered. Returns false (nothing
 // changed) when it needs every earlier stimulus retired first (needs scan mode).
 template <bool LW>
-__device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r, int qmode, bool exact, const uint4& E) {
+__device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r, int qmode, bool exact, const uint4& E,
+                                                         int& woke) {
   // WAITC: the candidate-only workers (touch entries > 0 flagged T_CAND) may still be held by
   // earlier stimuli when this one starts; their state is read after the wait before the frontier
   SCtl& S = L.c;
@@ -2339,7 +2345,9 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  if (lane == jw) release_worker<LW>(L, P, s, w);
+  int wk = -1;
+  if (lane == jw) wk = release_worker<LW>(L, P, s, w);
+  woke = rl(wk, jw);  // the stimulus next on w, if this release made it ready (DGP_EXE_CONT)
   phase(13);
   // ------------------------------------------------ retire: LDS state, then successors
   phase(21);
@@ -3139,6 +3147,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
   long long pf_r = -1;
   int pf_s = 0;
   uint4 pfE = make_uint4(0, 0, 0, 0);
+  int hint = -1;  // DGP_EXE_CONT
   while (true) {
     if (vload(&S.stop)) break;
     const SMask m = vload(&S.ready);
@@ -3171,6 +3180,10 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     const bool pcl = WAITC && rdl && vload(&L.predc[lane]) != 0;
     const bool pskip = pcl && (G || rsl - sp >= DGP_WAITC_AHEAD);
     unsigned key = rdl && !pskip ? (unsigned)((pcl ? 1u << 31 : 0u) | ((rsl - sp) << 6) | lane) : ~0u;  // r - sp < RS
+    // DGP_EXE_CONT: the stimulus this executor's last release of its completing worker made
+    // ready goes first (it continues the chain on that worker), unless it would wait in place
+    if (DGP_EXE_CONT && lane == hint && rdl && !pcl && !pskip) key = (unsigned)lane;
+    hint = -1;
     int cs = -1, cq = 0;
     long long cr = -1;
     uint32_t cf = 0;
@@ -3252,7 +3265,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       PROF(if (lane == 0) S.prof[9]++);
     } else if (G && (cf & F_SIMPLE) && cq == 0 && !cex && exe_run_entry<LW>(cs, cr, E)) {
       // a run of single-worker completions, back to back (only this executor calls out of line)
-    } else if (!exe_local<LW>(D, L, P, cs, cr, cq, cex, E)) {
+    } else if (!exe_local<LW>(D, L, P, cs, cr, cq, cex, E, hint)) {
       if (lane == 0) {
         atomicOr(&L.flags[cs], F_EXACT);
         atomicOr(&S.ready, 1ull << cs);
