@@ -265,7 +265,10 @@ def c_call_latency(eng_cls, local: int, g: dict) -> dict:
     return {"calls": calls, "us_per_call": round(dt / calls * 1e6, 2), "messages_per_s": round(calls / dt, 1),
             "device_us_per_call": {"answer": round(st["res_append_ticks"] / k / 100, 2),
                                    "run_stimuli": round(st["res_run_ticks"] / k / 100, 2),
-                                   "publish": round(st["res_publish_ticks"] / k / 100, 2)}}
+                                   "publish": round(st["res_publish_ticks"] / k / 100, 2)},
+            # when each role last finished a batch, after the request's stimulus was appended
+            "role_done_us_after_append": {r: round(st[f"res_role_{r}_ticks"] / k / 100, 2)
+                                          for r in ("bld", "pre", "reg", "claim", "exe", "seq", "wlk")}}
 
 
 def service_leg(eng_cls, local: int, args) -> dict:

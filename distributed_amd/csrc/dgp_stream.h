@@ -177,6 +177,7 @@ struct SCtl {
   long long seq_pos, log_len, rec_len, walk_pos, bld_pos, pre_pos, reg_pos, reg_limit;
   long long qhead, qlen, n_tasks;
   long long stim_end;  // service mode: stimuli [seq_pos, stim_end) run in this launch
+  unsigned long long t_role[8];  // resident mode: when each role last finished a batch (100 MHz clock)
   long long req_n, req_off, req_pl0;  // resident service: the request's messages, consumed, first placement
   unsigned long long req_seen;        // resident service: the last request taken
   long long round_end, rounds_left, prev_placed;
@@ -782,6 +783,7 @@ __device__ __attribute__((always_inline)) void role_wlk(const Dev& D, SLds& L, c
     if (lane == 0) {
       PROF(S.prof[4] += mclk() - t0);
       vstore(&S.walk_pos, wp + m);
+      if (D.resident) S.t_role[6] = rclk();
     }
   }
 }
@@ -891,6 +893,7 @@ __device__ __attribute__((noinline)) bool resident_serve(const Dev& D, SLds& L) 
         mb->pl_from = n1 - n0 <= cap ? n0 : -1;
         mb->n_placed = n1;
         mb->error = S.error;
+        for (int k = 0; k < 7; k++) mb->t_role[k] = S.t_role[k];
         mb->t_pub = rclk();
       }
       __threadfence_system();
@@ -1113,6 +1116,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
     lds_fence();
     if (lane == 0) {
       vstore(&S.seq_pos, sp + m);
+      if (D.resident) S.t_role[5] = rclk();
       if (DGP_TRACE) {
         const unsigned long long tn = __builtin_amdgcn_s_memtime();
         if (DGP_TRACE == 1) for (int i = 0; i < m; i++) trace_at(D, sp + i, 6, tn);
@@ -1376,7 +1380,7 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
     const long long a = KIND == 0 ? S.bld_pos : S.pre_pos;
     // BLD: completions up to the placement log (replay: stimulus r completes placement r)
     // or the stimulus log (service); PRE: what BLD has built, at most pre_lead ahead of SEQ
-    const long long hi = KIND == 0 ? (D.svc ? S.stim_end : vload(&S.log_len))
+    const long long hi = KIND == 0 ? (D.svc ? vload(&S.stim_end) : vload(&S.log_len))
                                    : min(vload(&S.bld_pos), vload(&S.seq_pos) + D.pre_lead);
     const long long e = min(a + 64, hi);
     if (e <= a) {
@@ -1412,6 +1416,7 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
       PROF(S.prof[KIND == 0 ? 1 : 2] += mclk() - t0);
       PROF(S.prof[KIND == 0 ? 6 : 7] += 1);
       vstore(KIND == 0 ? &S.bld_pos : &S.pre_pos, e);
+      if (D.resident) S.t_role[KIND] = rclk();
     }
   }
   if (KIND == 1 && lane < PX && lane < D.P) D.pdur_pre[lane] = dur;
@@ -1603,6 +1608,7 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     }
     if (lane == 0) {
       t_poll = mclk();
+      if (D.resident) S.t_role[2] = rclk();
       PROF(S.prof[3] += t_poll - t0);
       PROF(S.prof[31] += nbat);
       PROF(S.prof[27] += 1);            // batches
@@ -3260,6 +3266,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
                              ? (D.trace[(cr - D.trace_lo) * 8 + 7] | ((unsigned long long)(threadIdx.x >> 6) << 24)) : 0);
     }
     const unsigned long long t0 = mclk();
+    if (D.resident && lane == 0) S.t_role[3] = rclk();
     if (G && (cf & F_GLOBAL)) {
       exe_global_entry<LW>(cs, cr);
       PROF(if (lane == 0) S.prof[9]++);
@@ -3274,6 +3281,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     }
     if (lane == 0) {
       PROF(atomicAdd(&S.prof[5], mclk() - t0));
+      if (D.resident) S.t_role[4] = rclk();
       atomicSub(&S.busy_exe, 1);
     }
     if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(DGP_EXE_PRIO == 2 ? 0 : 1);  // polling again

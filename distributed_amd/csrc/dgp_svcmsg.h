@@ -94,17 +94,20 @@ struct Mbox {
   int error;                    // device: the engine error that ended it (0: none)
   // device (100 MHz clock) per request: taken, stimuli appended (last segment), retired, published
   unsigned long long t_seen, t_app, t_ret, t_pub;
+  // device: when each role last finished a batch (builder, prefetcher, registrar, executor
+  // claim, executor done, sequencer retire, walker), copied at publish (diagnostics)
+  unsigned long long t_role[7];
 };
 __host__ __device__ inline size_t mbox_bytes(long long cap, long long pl_cap) {
-  return 128 + (size_t)cap * sizeof(Msg) + (((size_t)cap + 15) & ~(size_t)15) + (size_t)pl_cap * 8;
+  return 256 + (size_t)cap * sizeof(Msg) + (((size_t)cap + 15) & ~(size_t)15) + (size_t)pl_cap * 8;
 }
-__host__ __device__ inline Msg* mbox_msgs(Mbox* m) { return (Msg*)((char*)m + 128); }
+__host__ __device__ inline Msg* mbox_msgs(Mbox* m) { return (Msg*)((char*)m + 256); }
 __host__ __device__ inline int8_t* mbox_status(Mbox* m) { return (int8_t*)(mbox_msgs(m) + m->cap); }
 __host__ __device__ inline int32_t* mbox_pl_task(Mbox* m) {
   return (int32_t*)((char*)mbox_status(m) + ((m->cap + 15) & ~15ll));
 }
 __host__ __device__ inline int32_t* mbox_pl_worker(Mbox* m) { return mbox_pl_task(m) + m->pl_cap; }
-static_assert(sizeof(Mbox) <= 128, "mailbox header");
+static_assert(sizeof(Mbox) <= 256, "mailbox header");
 
 }  // namespace svc
 }  // namespace dgp

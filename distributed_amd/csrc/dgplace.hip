@@ -114,6 +114,7 @@ struct dgp_engine {
   bool pending_resync = false;       // a later graph with dependencies on earlier tasks: dgp_sync_* next
   unsigned long long req_seq = 0;    // the last request number sent
   int64_t res_prof[4] = {0, 0, 0, 0};  // requests answered; sums of append, run, publish (device 100 MHz ticks)
+  int64_t res_role[7] = {0, 0, 0, 0, 0, 0, 0};  // sums of each role's last batch end after the append
 };
 
 namespace {
@@ -1100,6 +1101,9 @@ int tasks_finished_resident(dgp_engine* e, int64_t n, const int32_t* task, const
     e->res_prof[1] += (int64_t)(e->mb->t_app - e->mb->t_seen);
     e->res_prof[2] += (int64_t)(e->mb->t_ret - e->mb->t_app);
     e->res_prof[3] += (int64_t)(e->mb->t_pub - e->mb->t_ret);
+    for (int k = 0; k < 7; k++)
+      if (e->mb->t_role[k] >= e->mb->t_app && e->mb->t_role[k] <= e->mb->t_pub)
+        e->res_role[k] += (int64_t)(e->mb->t_role[k] - e->mb->t_app);
   }
   const unsigned long long placed = (unsigned long long)e->mb->n_placed;
   if (n_new_placements) *n_new_placements = (int64_t)(placed - e->last_placed);
@@ -2227,14 +2231,14 @@ int dgp_stats(dgp_engine* e, int64_t* out, int32_t n) {
   if (!e || !out) return DGP_E_ARG;
   dgp::Ctl c;
   if (int rc = read_ctl(e, &c)) return rc;
-  int64_t v[42] = {(int64_t)c.n_placed, c.rounds_nonempty, c.dr_steps, c.n_global_events, (int64_t)c.rec_used,
+  int64_t v[49] = {(int64_t)c.n_placed, c.rounds_nonempty, c.dr_steps, c.n_global_events, (int64_t)c.rec_used,
                    (int64_t)c.walk_pos};
   for (int i = 0; i < 8; i++) v[6 + i] = (int64_t)c.prof[i];
   for (int i = 0; i < 16; i++) v[14 + i] = (int64_t)c.prof2[i];
   for (int i = 0; i < 8; i++) v[30 + i] = (int64_t)c.prof3[i];
   for (int i = 0; i < 4; i++) v[38 + i] = e->res_prof[i];
-
-  for (int i = 0; i < n && i < 42; i++) out[i] = v[i];
+  for (int i = 0; i < 7; i++) v[42 + i] = e->res_role[i];
+  for (int i = 0; i < n && i < 49; i++) out[i] = v[i];
   return 0;
 }
 

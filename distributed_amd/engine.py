@@ -395,15 +395,17 @@ class PlacementEngine:
         self._check(self.lib.dgp_set_timing(self.h, 1 if on else 0), "dgp_set_timing")
 
     def stats(self) -> dict:
-        out = np.zeros(42, np.int64)
-        self._check(self.lib.dgp_stats(self.h, _ptr(out), 42), "dgp_stats")
+        out = np.zeros(49, np.int64)
+        self._check(self.lib.dgp_stats(self.h, _ptr(out), 49), "dgp_stats")
         return dict(zip(("placements", "rounds", "dr_steps", "global_stimuli", "records", "walk_pos",
                          "cyc_setup", "cyc_local_steps", "cyc_global", "cyc_finish", "cyc_reserve", "cyc_max_step",
                          "cyc_exec_max", "cyc_exec_sum") + tuple(f"wave_phase{i}" for i in range(16))
                         + tuple(f"stall{i}" for i in range(8))
                         # resident service requests answered and the device's 100 MHz ticks spent
                         # answering / running / publishing them (summed)
-                        + ("res_requests", "res_append_ticks", "res_run_ticks", "res_publish_ticks"),
+                        + ("res_requests", "res_append_ticks", "res_run_ticks", "res_publish_ticks")
+                        # when each role last finished a batch, after the request's append (summed)
+                        + tuple(f"res_role_{r}_ticks" for r in ("bld", "pre", "reg", "claim", "exe", "seq", "wlk")),
                         map(int, out)))
 
     def kernel_times(self) -> dict:

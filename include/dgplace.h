@@ -347,7 +347,11 @@ int dgp_set_timing(dgp_engine* e, int enabled);
 /* Engine counters: out[0] placements, [1] non-empty rounds, [2] deterministic-reservation
  * steps of the ordered commit, [3] stimuli that ran as global (in order, alone),
  * [4] record-log length, [5] record-log walker position, [6..13] commit-kernel phase
- * cycles (s_memtime): setup, local steps, global stimuli, finish, walker, longest step. */
+ * cycles (s_memtime): setup, local steps, global stimuli, finish, walker, longest step,
+ * [14..37] stream-kernel probes, [38] resident requests answered, [39..41] their device
+ * ticks (100 MHz) answering / running / publishing, [42..48] per request, when each role of
+ * the stream kernel last finished a batch after the request was appended (builder,
+ * prefetcher, registrar, executor claim, executor done, sequencer, walker), summed. */
 int dgp_stats(dgp_engine* e, int64_t* out, int32_t n);
 /* Measurement helper (host only, no engine): the longest chain of ordered stimuli of a
  * replay's placement log (stimulus r completes pl_task[r]; stimuli touching one worker are
