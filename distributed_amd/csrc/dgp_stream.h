@@ -60,6 +60,9 @@ __constant__ Dev c_dev;
 #ifndef DGP_REG_PROBES
 #define DGP_REG_PROBES 0  // registrar sub-phase s_memtime probes (diagnostics)
 #endif
+#ifndef DGP_OCC_BATCH
+#define DGP_OCC_BATCH 0  // executors' occupancy: every prefix duration load issued before the sum
+#endif
 #ifndef DGP_EXE_CONT
 #define DGP_EXE_CONT 0  // an executor first claims the stimulus its release of the completing worker made ready
 #endif
@@ -487,6 +490,23 @@ __device__ __forceinline__ double occ_dict(const WDict& d, int64_t netocc, DTab 
 __device__ __forceinline__ double occ_dict_r(const WDict& d, double net_bw, DTab dt, const Dev& D) {
   const uint32_t n = wd_n(d.ord);
   double res = 0.0;
+  if (DGP_OCC_BATCH) {
+    // every slot's duration load issued back to back (one LDS latency, not one per prefix),
+    // then the sum in dict insertion order: the same fp64 operations as below
+    uint32_t v[PD];
+    double dv[PD];
+#pragma unroll
+    for (int i = 0; i < PD; i++) {
+      v[i] = wd_slot(d, i);
+      dv[i] = dt[(v[i] >> 24) & (PX - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < PD; i++) {
+      const double term = (dv[i] < 0 ? D.unknown_duration : dv[i]) * (double)(v[i] & 0xffffffu);
+      if ((uint32_t)i < n) res += term;
+    }
+    return res + net_bw;
+  }
 #pragma unroll
   for (int i = 0; i < PD; i++) {
     if (!ballot((uint32_t)i < n)) break;
