@@ -444,17 +444,29 @@ __device__ void tree_update(const Dev& D, int w) {
   D.t_idx[pos] = w;
   double k = key;
   int i = w;
+  // up the path 8 levels at a time: the 8 siblings are read first (the path's writes never
+  // touch a sibling), one memory latency per 8 levels instead of one per level
   while (pos > 1) {
-    int sib = pos ^ 1;
-    double sk = D.t_key[sib];
-    int si = D.t_idx[sib];
-    if (sk < k || (sk == k && si < i)) {
-      k = sk;
-      i = si;
+    double sk[8];
+    int si[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {  // a level above the root reads node 3 (unused)
+      const int p = max(pos >> j, 2);
+      sk[j] = D.t_key[p ^ 1];
+      si[j] = D.t_idx[p ^ 1];
     }
-    pos >>= 1;
-    D.t_key[pos] = k;
-    D.t_idx[pos] = i;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (pos > 1) {
+        if (sk[j] < k || (sk[j] == k && si[j] < i)) {
+          k = sk[j];
+          i = si[j];
+        }
+        pos >>= 1;
+        D.t_key[pos] = k;
+        D.t_idx[pos] = i;
+      }
+    }
   }
 }
 __device__ __attribute__((noinline)) void tree_rebuild_coop(const Dev& D) {  // all threads of the block
@@ -1734,19 +1746,46 @@ __global__ void k_init_workers(const Dev* __restrict__ Dp) {
 // task in parallel: waiting_on = dependencies without a replica; waiters = dependents
 // (all of them go to waiting in the same stimulus; priorities are topological)
 // (tasks [lo, N): lo = 0 for the first graph, the first new task for a later one)
+// update_graph, part 1 (released -> waiting, :2078-2119): waiting_on = the dependencies not
+// in memory, waiters = the dependents. Each wave takes 64 consecutive tasks, one per lane;
+// a row wider than 32 dependencies (the P2P barrier's 66,666) is counted by the whole wave
+// afterwards instead of one lane's serial loop.
+__device__ __forceinline__ bool ug_dep_in_memory(const Dev& D, int d) {
+  const unsigned long long* row = D.holders + (size_t)d * D.WB;
+  bool any = false;
+  for (int wd = 0; wd < D.WB && !any; wd++) any = row[wd] != 0;
+  return any;
+}
 __global__ void k_ug_init(const Dev* __restrict__ Dp, int lo) {
   const Dev& D = *Dp;
-  for (int t = lo + blockIdx.x * blockDim.x + threadIdx.x; t < D.N; t += gridDim.x * blockDim.x) {
-    int wo = 0;
-    for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
-      const unsigned long long* row = D.holders + (size_t)D.dep_idx[k] * D.WB;
-      bool any = false;
-      for (int wd = 0; wd < D.WB && !any; wd++) any = row[wd] != 0;
-      wo += any ? 0 : 1;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t t0 = lo + wave * 64; t0 < D.N; t0 += nwaves * 64) {
+    const int64_t t = t0 + lane;
+    const bool in = t < D.N;
+    const int64_t a = in ? D.dep_ptr[t] : 0, b = in ? D.dep_ptr[t + 1] : 0;
+    const bool wide = b - a > 32;
+    if (in && !wide) {
+      int wo = 0;
+      for (int64_t k = a; k < b; k++) wo += ug_dep_in_memory(D, D.dep_idx[k]) ? 0 : 1;
+      D.remaining[t] = wo;
+      D.waiters[t] = (int32_t)(D.dpt_ptr[t + 1] - D.dpt_ptr[t]);
+      D.state[t] = S_WAITING;
     }
-    D.remaining[t] = wo;
-    D.waiters[t] = (int32_t)(D.dpt_ptr[t + 1] - D.dpt_ptr[t]);
-    D.state[t] = S_WAITING;
+    for (unsigned long long wm = __ballot(wide); wm; wm &= wm - 1) {
+      const int j = __builtin_ctzll(wm);
+      const int64_t tw = t0 + j;
+      const int64_t aw = __shfl(a, j), bw = __shfl(b, j);
+      int64_t wo = 0;
+      for (int64_t k = aw + lane; k < bw; k += 64) wo += ug_dep_in_memory(D, D.dep_idx[k]) ? 0 : 1;
+      wo = wave_sum64(wo);
+      if (lane == 0) {
+        D.remaining[tw] = (int32_t)wo;
+        D.waiters[tw] = (int32_t)(D.dpt_ptr[tw + 1] - D.dpt_ptr[tw]);
+        D.state[tw] = S_WAITING;
+      }
+    }
   }
 }
 
