@@ -2811,6 +2811,8 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   bool fr_stop = false;
   for (int64_t k0 = f0; k0 < f1 && !fr_stop; k0 += 64) {
    int xl = 0, fml = -1, tfl = 0, h1l = -1;
+   int rcl = -1;        // a restricted task with one dependency and one valid worker: that worker
+   int64_t rcml = 0;    // and its comm bytes (the shuffle's restricted unpacks)
    if (k0 + lane < f1) {
      xl = D.dpt_idx[k0 + lane];
      fml = D.fr_mark[xl];
@@ -2821,6 +2823,12 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
        h1l = D.holder_of[d1];
        // a replica set or a paused holder: decide_worker's general form below
        if (((D.evf & EVF_MULTI) && (D.tdyn[d1] & TD_MULTI)) || (h1l >= 0 && h1l < D.W && paused(h1l))) h1l = -1;
+     } else if (e - a == 1 && restricted_nonrootish(D, xl) && D.restr_ptr[xl + 1] - D.restr_ptr[xl] == 1) {
+       const int d1 = D.dep_idx[a];
+       if (!((D.evf & EVF_MULTI) && (D.tdyn[d1] & TD_MULTI))) {
+         rcl = D.restr_idx[D.restr_ptr[xl]];
+         rcml = D.holder_of[d1] == rcl ? 0 : nbv(D, D.res_nbytes[d1]);
+       }
      }
    }
    const int nk = (int)min((int64_t)64, f1 - k0);
@@ -2829,6 +2837,13 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
    for (int j = 0; j < nk; j++) {
     const int x = rl(xl, j);
     if (rl(fml, j) != (int)r) continue;
+    const int rc1 = rl(rcl, j);
+    if (rc1 >= 0 && rc1 < D.W && !paused(rc1) && x != D.dbg_task) {
+      // decide_worker with one valid running worker (:8575-8586): the candidates are that
+      // worker whether or not it holds the dependency (holders & valid, else valid)
+      place_x(x, rc1, ROUTE_NONROOTISH, mk64(rlu(lo32(rcml), j), rlu(hi32(rcml), j)), true);
+      continue;
+    }
     if (restricted_nonrootish(D, x)) {
       // decide_worker (:8550-8593) with valid = valid_workers(ts) & running: candidates =
       // holders & valid; none: valid; valid empty: loose -> decide_worker without

@@ -3,8 +3,8 @@ import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_amd import graphs
 from distributed_amd.engine import PlacementEngine
-if len(sys.argv) > 1 and sys.argv[1] == "c3":  # C3: P2P-shuffle shape, 66,666 partitions x 512 workers
-    g = graphs.shuffle_graph(int(sys.argv[2]) if len(sys.argv) > 2 else 66_666, 512)
+if len(sys.argv) > 1 and sys.argv[1] in ("c3", "c3r"):  # C3: P2P-shuffle shape, 66,666 partitions x 512 workers
+    g = graphs.shuffle_graph(int(sys.argv[2]) if len(sys.argv) > 2 else 66_666, 512, restricted=sys.argv[1] == "c3r")
     n = g["n_tasks"]
 else:
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
