@@ -1795,7 +1795,24 @@ __global__ void k_ug_init(const Dev* __restrict__ Dp, int lo) {
 // Tasks at priority positions [lo, N) (a later graph's tasks follow every earlier one in
 // priority: a new generation); its placements append to the placement log.
 __global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp, int lo) {
-  const Dev& D = *Dp;
+  // the dispatch is one lane's chain of dependent reads and writes of the control block
+  // (idle_task_count / idle / saturated counts, the global prefix dict, occupancy sums): the
+  // block works on an LDS copy of it (and of Dev, whose ctl points at the copy) and writes
+  // it back at the end
+  __shared__ Dev s_dev;
+  __shared__ Ctl s_ctl;
+  {
+    static_assert(sizeof(Dev) % 4 == 0 && sizeof(Ctl) % 4 == 0, "word copies");
+    const uint32_t* sd = (const uint32_t*)Dp;
+    const uint32_t* sc = (const uint32_t*)Dp->ctl;
+    for (int i = threadIdx.x; i < (int)(sizeof(Dev) / 4); i += blockDim.x) ((uint32_t*)&s_dev)[i] = sd[i];
+    for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += blockDim.x) ((uint32_t*)&s_ctl)[i] = sc[i];
+    __syncthreads();
+    if (threadIdx.x == 0) s_dev.ctl = &s_ctl;
+    __syncthreads();
+  }
+  Ctl* const ctl_g = Dp->ctl;
+  const Dev& D = s_dev;
   __shared__ CoopShared S;
   __shared__ int64_t s_nr, s_pos;
   Ctl* c = D.ctl;
@@ -1906,6 +1923,8 @@ __global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp,
     c->round_start = 0;
     c->round_n = 0;
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += blockDim.x) ((uint32_t*)ctl_g)[i] = ((const uint32_t*)&s_ctl)[i];
 }
 
 // start of a round: its completion list is the slice of the placement log made by the

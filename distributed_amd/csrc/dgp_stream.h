@@ -60,6 +60,9 @@ __constant__ Dev c_dev;
 #ifndef DGP_REG_PROBES
 #define DGP_REG_PROBES 0  // registrar sub-phase s_memtime probes (diagnostics)
 #endif
+#ifndef DGP_RUN_PAR
+#define DGP_RUN_PAR 1  // single-worker runs of one prefix: every member's record at once (lane = member)
+#endif
 #ifndef DGP_OCC_BATCH
 #define DGP_OCC_BATCH 0  // executors' occupancy: every prefix duration load issued before the sum
 #endif
@@ -2459,6 +2462,35 @@ __device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, co
   int64_t nbj = P.nbytes[w];
   const double nbw = net_bw_of(net, D);
   const DTab durv = stim_durations(D, L, E, r);
+  // members of one prefix whose count on w stays >= 1 (no dict entry leaves): member i's
+  // state is the head's with i + 1 completions applied, so every member's occupancy and
+  // record is made at once, lane i = member i (the same fp64 operations as the loop below)
+  const int p0 = rl((int)h0.z, 0);
+  const uint32_t cnt0 = wd_cnt(dj, p0);
+  if (DGP_RUN_PAR && !ballot(lane < k && (int)h0.z != p0) && cnt0 > (uint32_t)k) {
+    WDict di = dj;
+    wd_set(di, p0, cnt0 - (uint32_t)(lane + 1));
+    const double occ_i = occ_dict_r(di, nbw, durv, D);
+    int64_t dnb = 0;
+    if (lane < k) {
+      SRec rc;
+      rc.w = w;
+      rc.p = (int16_t)p0;
+      rc.kind = (int8_t)K_COMPLETE;
+      rc.pad = 0;
+      rc.nproc = np - (lane + 1);
+      rc.task = (int)h0.x;
+      rc.dnet = 0;
+      rc.occ = occ_i;
+      rc.dur = mkd(h2.x, h2.y);
+      D.srec[(size_t)((r + lane) & (RS - 1)) * PLC] = rc;
+      // add_replica (:3148) and the release of a dependency held by w (:3309-3314): integers
+      dnb = ((h0.w & F_SELFREL) ? 0 : mk64(h1.x, h1.y)) - (((h1.z >> 8) & 0xff) ? mk64(er.z, er.w) : 0);
+    }
+    nbj += wsum64(dnb);
+    wd_set(dj, p0, cnt0 - (uint32_t)k);
+    np -= k;
+  } else
   for (int i = 0; i < k; i++) {
     const int t = rl((int)h0.x, i), p = rl((int)h0.z, i);
     const uint32_t fl = rlu(h0.w, i);
