@@ -1870,10 +1870,8 @@ __global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp,
     }
     int64_t chunk = nr - pos < FL_MAX ? nr - pos : FL_MAX;
     // stop the chunk at the point where the bulk path takes over
-    if (threadIdx.x == 0) {
-      S.nlist = (int)chunk;
-      for (int64_t i = 0; i < chunk; i++) S.list[i] = D.ready[pos + i];
-    }
+    if (threadIdx.x == 0) S.nlist = (int)chunk;
+    for (int64_t i = threadIdx.x; i < chunk; i += blockDim.x) S.list[i] = D.ready[pos + i];  // every lane
     __syncthreads();
     if (threadIdx.x == 0) S.pos = 0;
     __syncthreads();
