@@ -153,6 +153,27 @@ def test_graph_from_tasks_layout():
     assert g["wanted"].tolist() == [0, 0, 1] and g["rootish_override"].tolist() == [1, -1, -1]
 
 
+def test_graph_from_tasks_names_earlier_tasks():
+    """A later graph's dependency on an already uploaded task is named -1 - its engine index
+    (dgp_add_graph); one outside both raises."""
+    from types import SimpleNamespace as NS
+
+    from distributed_amd.ext import graph_from_tasks
+
+    P = NS(name="p", duration_average=0.1)
+    G = NS(name="g")
+    old = NS(key="old", priority=(0, 1, 0), dependencies=[], prefix=P, group=G, who_wants=None, _rootish=None)
+    a = NS(key="a", priority=(0, 2, 1), dependencies=[old], prefix=P, group=G, who_wants=None, _rootish=None)
+    b = NS(key="b", priority=(0, 2, 2), dependencies=[a, old], prefix=P, group=G, who_wants=None, _rootish=None)
+    g, keys = graph_from_tasks([b, a], [1], earlier={"old": 7})
+    assert keys == ["a", "b"]
+    assert g["dep_ptr"].tolist() == [0, 1, 3] and g["dep_idx"].tolist() == [-8, -8, 0]
+    lost = NS(key="c", priority=(0, 2, 3), dependencies=[NS(key="zz")], prefix=P, group=G, who_wants=None,
+              _rootish=None)
+    with pytest.raises(ValueError, match="not in the uploaded graph"):
+        graph_from_tasks([lost], [1], earlier={"old": 7})
+
+
 def test_gpu_work_stealing_matches_reference_plugin():
     """GPUWorkStealing (distributed_amd/stealing.py) vs the reference WorkStealing on two
     identical states, two balance() calls each: request events, metrics, in-flight
