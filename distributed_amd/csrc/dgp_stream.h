@@ -60,6 +60,9 @@ __constant__ Dev c_dev;
 #ifndef DGP_REG_PROBES
 #define DGP_REG_PROBES 0  // registrar sub-phase s_memtime probes (diagnostics)
 #endif
+#ifndef DGP_BULK_RESTR
+#define DGP_BULK_RESTR 0  // global frontier: restricted single-worker tasks on distinct workers placed lane-parallel
+#endif
 #ifndef DGP_RUN_PAR
 #define DGP_RUN_PAR 1  // single-worker runs of one prefix: every member's record at once (lane = member)
 #endif
@@ -2646,6 +2649,215 @@ __device__ __attribute__((always_inline)) bool bulk_single_holder(const Dev& D, 
   return true;
 }
 
+// A chunk of frontier tasks that each have the same one dependency, the same prefix and the
+// same ONE valid worker c, running (the shuffle's restricted unpacks: restrict_task shards
+// the output partitions over the workers in contiguous ranges, so consecutive unpacks share
+// their worker): decide_worker returns c for each (:8575-8586), placement k sees c with k of
+// them made: count cnt0 + k of the prefix (its dict entry appended by the first if absent),
+// the dependency's needs_what entry made by the first (netocc grows once) or counted up.
+// The same operations as place_x one task at a time, lane L computing placement L.
+template <bool LW>
+__device__ __attribute__((always_inline)) bool bulk_restricted_same(const Dev& D, SCtl& S, const WPtr<LW>& P,
+                                                                    WState& g, DTab durv, bool fr, int xl, int rcl,
+                                                                    int rdl, bool rhl, int64_t rcml, bool evp,
+                                                                    long long lpos, int& npl) {
+  const int lane = lane_id();
+  const unsigned long long fm = ballot(fr);
+  const int m = __builtin_popcountll(fm);
+  if (m < 2) return false;
+  const int first = __builtin_ctzll(fm);
+  const int c = rl(rcl, first), d = rl(rdl, first);
+  const int pxl = fr ? D.prefix[xl] : -1;
+  const int px = rl(pxl, first);
+  const bool held = rl(rhl ? 1 : 0, first) != 0;
+  const int64_t comm = rl_i64(rcml, first);
+  if (c < 0 || c >= D.W || (evp && (P.wflags[c] & WF_PAUSED))) return false;
+  if (ballot(fr && (rcl != c || rdl != d || pxl != px || xl == D.dbg_task))) return false;
+  WDict d0 = dict_load<LW>(P, c);
+  const uint32_t cnt0 = wd_cnt(d0, px);
+  if (cnt0 == 0 && wd_n(d0.ord) >= (uint32_t)PD) return false;
+  // the dependency's needs_what entry on c (lane i holds line word i)
+  uint32_t nl = line_load<LW>(P, c);
+  int64_t dnI = 0;  // netocc added by the first placement
+  int ent = -1;
+  bool ins = false;
+  if (!held) {
+    const uint32_t ctl = rlu(nl, NLW - 1);
+    if (ctl == NL_OVF || (int)(ctl >> 8) != line_used(nl)) return false;
+    const unsigned long long hm = ballot(lane < NLW - 1 && nl != 0 && (nl >> 8) == (uint32_t)d);
+    if (hm) {
+      ent = __builtin_ctzll(hm);
+      if ((rlu(nl, ent) & 0xffu) + (uint32_t)m > 0xffu) return false;
+    } else {
+      const unsigned long long em = ballot(lane < NLW - 1 && nl == 0);
+      if (!em) return false;
+      ent = __builtin_ctzll(em);
+      ins = true;
+      dnI = comm;  // _inc_needs_replica: the bytes c newly needs (:800-813), nbytes of d
+    }
+  }
+  const int np0 = P.nproc[c];
+  const int64_t no0 = P.netocc[c], nb0 = P.nbytes[c];
+  const double nth = (double)P.nthreads[c];
+  // lane L: placement L's occupancy before (count cnt0 + L; netocc grown after the first) and after
+  WDict db = d0, da = d0;
+  if (cnt0 + (uint32_t)lane > 0) wd_set(db, px, cnt0 + (uint32_t)lane);
+  wd_set(da, px, cnt0 + (uint32_t)lane + 1u);
+  const double occ_b = occ_dict(db, lane == 0 ? no0 : no0 + dnI, durv, D);
+  const double occ_a = occ_dict(da, no0 + dnI, durv, D);
+  const double start_l = occ_b / nth + (double)comm / (double)D.bandwidth;
+  const int rank = __builtin_popcountll(fm & ((1ull << lane) - 1));
+  const double start = __shfl(start_l, rank);
+  if (fr) {
+    const long long pos = lpos + npl + rank;
+    D.pl_task[pos] = xl;
+    D.pl_worker[pos] = c;
+    D.pl_comm[pos] = comm;
+    D.pl_start[pos] = start;
+    D.pl_wsnbytes[pos] = nb0;
+    D.pl_route[pos] = (int8_t)ROUTE_NONROOTISH;
+    D.run_id[xl] = (int32_t)pos;
+    D.holder_of[xl] = c;
+    D.proc_on[xl] = c;
+    D.state[xl] = S_PROCESSING;
+    atomicAdd((unsigned long long*)&D.g_relwait[D.group[xl]], (unsigned long long)-1ll);
+  }
+  if (ent >= 0) {
+    if (lane == ent) nl = ins ? (((uint32_t)d << 8) | (uint32_t)m) : nl + (uint32_t)m;
+    if (ins && lane == NLW - 1) nl += 0x100u;
+    line_store<LW>(P, c, nl);
+  }
+  if (lane == 0) {
+    using U4 = typename WPtr<LW>::template P<Q4>;
+    WDict dn = d0;
+    wd_set(dn, px, cnt0 + (uint32_t)m);
+    st4(ascast<U4>(P.pcnt + (size_t)c * PD), dn.c);
+    st4(ascast<U4>(P.pcnt + (size_t)c * PD + 4), dn.c1);
+    P.plen[c] = dn.ord;
+    P.nproc[c] = np0 + m;
+    P.netocc[c] = no0 + dnI;
+  }
+  __threadfence_block();
+  SRec rc{};  // the m K_PLACE records in placement order (lane L = record L)
+  rc.w = c;
+  rc.p = (int16_t)px;
+  rc.kind = (int8_t)K_PLACE;
+  rc.nproc = np0 + lane + 1;
+  rc.task = -1;
+  rc.dnet = lane == 0 ? dnI : 0;
+  rc.occ = occ_a;
+  rc.dur = 0.0;
+  ws_fold_batch<LW>(D, P, S, g, rc, m);
+  npl += m;
+  return true;
+}
+
+// A chunk of frontier tasks that each have one dependency and ONE valid worker, running and
+// different for every task of the chunk (the shuffle's restricted unpacks, range-sharded
+// over the workers): decide_worker returns that worker (holders & valid, else valid,
+// :8575-8586), and the placements touch disjoint workers, so each lane makes its task's
+// placement on its own worker (occupancy before / after, the dict, needs_what, netocc, the
+// log row) and the K_PLACE records are folded in placement order at once: the same
+// operations as place_x one task at a time. False (nothing done) unless every frontier
+// lane qualifies and every worker's dict and needs line take the change in place.
+template <bool LW>
+__device__ __attribute__((always_inline)) bool bulk_restricted_distinct(const Dev& D, SCtl& S, const WPtr<LW>& P,
+                                                                        WState& g, DTab durv, bool fr, int xl, int rcl,
+                                                                        int rdl, bool rhl, int64_t rcml, bool evp,
+                                                                        long long lpos, int& npl) {
+  const int lane = lane_id();
+  const unsigned long long fm = ballot(fr);
+  const int m = __builtin_popcountll(fm);
+  if (m < 2) return false;
+  bool ok = !fr || (rcl >= 0 && rcl < D.W && !(evp && (P.wflags[rcl] & WF_PAUSED)) && xl != D.dbg_task);
+  if (ballot(!ok)) return false;
+  bool dup = false;
+  for (unsigned long long q = fm; q; q &= q - 1) {
+    const int j = __builtin_ctzll(q);
+    dup = dup || (fr && lane != j && rcl == rl(rcl, j));
+  }
+  if (ballot(dup)) return false;
+  const int c = fr ? rcl : 0;
+  const int px = fr ? D.prefix[xl] : 0;
+  WDict dc = dict_load<LW>(P, c);
+  const int np0 = P.nproc[c];
+  const int64_t no0 = P.netocc[c], nb0 = P.nbytes[c];
+  const double nth = (double)P.nthreads[c];
+  int ent = -1;  // the needs_what entry of the dependency on c (-1: c holds it)
+  bool ins = false;
+  uint32_t ctl = 0, ev = 0;
+  if (fr) {
+    if (wd_find(dc, px) < 0 && wd_n(dc.ord) >= (uint32_t)PD) ok = false;
+    if (!rhl) {
+      ctl = P.needs[(size_t)c * NLW + NLW - 1];
+      int used = 0, hit = -1, fz = -1;
+      for (int i = 0; i < NLW - 1; i++) {
+        const uint32_t e = P.needs[(size_t)c * NLW + i];
+        used += e != 0 ? 1 : 0;
+        if (e != 0 && (e >> 8) == (uint32_t)rdl) hit = i;
+        if (e == 0 && fz < 0) fz = i;
+      }
+      if (ctl == NL_OVF || (int)(ctl >> 8) != used) {
+        ok = false;
+      } else if (hit >= 0) {
+        ev = P.needs[(size_t)c * NLW + hit];
+        if ((ev & 0xffu) == 0xffu) ok = false;
+        ent = hit;
+      } else if (fz >= 0) {
+        ent = fz;
+        ins = true;
+      } else {
+        ok = false;
+      }
+    }
+  }
+  if (ballot(!ok)) return false;
+  const int rank = __builtin_popcountll(fm & ((1ull << lane) - 1));
+  const int64_t dn = ins ? rcml : 0;  // _inc_needs_replica: the bytes c newly needs (:800-813)
+  const double occ_b = occ_dict(dc, no0, durv, D);
+  const double start = occ_b / nth + (double)rcml / (double)D.bandwidth;
+  dict_add(dc, px, +1);
+  const double occ_a = occ_dict(dc, no0 + dn, durv, D);
+  if (fr) {
+    const long long pos = lpos + npl + rank;
+    D.pl_task[pos] = xl;
+    D.pl_worker[pos] = c;
+    D.pl_comm[pos] = rcml;
+    D.pl_start[pos] = start;
+    D.pl_wsnbytes[pos] = nb0;
+    D.pl_route[pos] = (int8_t)ROUTE_NONROOTISH;
+    D.run_id[xl] = (int32_t)pos;
+    D.holder_of[xl] = c;
+    using U4 = typename WPtr<LW>::template P<Q4>;
+    st4(ascast<U4>(P.pcnt + (size_t)c * PD), dc.c);
+    st4(ascast<U4>(P.pcnt + (size_t)c * PD + 4), dc.c1);
+    P.plen[c] = dc.ord;
+    P.nproc[c] = np0 + 1;
+    P.netocc[c] = no0 + dn;
+    if (ent >= 0) P.needs[(size_t)c * NLW + ent] = ins ? (((uint32_t)rdl << 8) | 1u) : ev + 1u;
+    if (ins) P.needs[(size_t)c * NLW + NLW - 1] = ctl + 0x100u;
+    D.proc_on[xl] = c;
+    D.state[xl] = S_PROCESSING;
+    atomicAdd((unsigned long long*)&D.g_relwait[D.group[xl]], (unsigned long long)-1ll);
+  }
+  __threadfence_block();
+  // the records in placement order: frontier lane -> lane rank (lanes >= m unused)
+  const int dst = (fr ? rank : 63) * 4;
+  auto push = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)v); };
+  SRec rc{};
+  rc.w = (int)push((uint32_t)c);
+  rc.p = (int16_t)push((uint32_t)px);
+  rc.kind = (int8_t)K_PLACE;
+  rc.nproc = (int)push((uint32_t)(np0 + 1));
+  rc.task = -1;
+  rc.dnet = mk64(push(lo32(dn)), push(hi32(dn)));
+  rc.occ = mkd(push(dlo(occ_a)), push(dhi(occ_a)));
+  rc.dur = 0.0;
+  ws_fold_batch<LW>(D, P, S, g, rc, m);
+  npl += m;
+  return true;
+}
+
 // remove_all_replicas of a released dependency d (:3161-3171): every holder's ws.nbytes,
 // then who_has = None (one lane per dependency; holders may be shared: LDS / global atomics)
 template <bool LW>
@@ -2843,8 +3055,10 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
   bool fr_stop = false;
   for (int64_t k0 = f0; k0 < f1 && !fr_stop; k0 += 64) {
    int xl = 0, fml = -1, tfl = 0, h1l = -1;
-   int rcl = -1;        // a restricted task with one dependency and one valid worker: that worker
-   int64_t rcml = 0;    // and its comm bytes (the shuffle's restricted unpacks)
+   int rcl = -1;        // a restricted task with one dependency and one valid worker: that worker,
+   int64_t rcml = 0;    // its comm bytes (the shuffle's restricted unpacks), the dependency
+   int rdl = -1;        // and whether the worker holds it
+   bool rhl = false;
    if (k0 + lane < f1) {
      xl = D.dpt_idx[k0 + lane];
      fml = D.fr_mark[xl];
@@ -2859,13 +3073,21 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
        const int d1 = D.dep_idx[a];
        if (!((D.evf & EVF_MULTI) && (D.tdyn[d1] & TD_MULTI))) {
          rcl = D.restr_idx[D.restr_ptr[xl]];
-         rcml = D.holder_of[d1] == rcl ? 0 : nbv(D, D.res_nbytes[d1]);
+         rdl = d1;
+         rhl = D.holder_of[d1] == rcl;
+         rcml = rhl ? 0 : nbv(D, D.res_nbytes[d1]);
        }
      }
    }
    const int nk = (int)min((int64_t)64, f1 - k0);
    if (bulk_single_holder<LW>(D, S, P, g, durv, r, k0 + lane < f1 && fml == (int)r, xl, tfl, h1l, lpos, npl))
      continue;  // the whole chunk went to one worker, placed lane-parallel
+   if (DGP_BULK_RESTR && bulk_restricted_same<LW>(D, S, P, g, durv, k0 + lane < f1 && fml == (int)r, xl, rcl, rdl, rhl,
+                                                  rcml, evp, lpos, npl))
+     continue;  // the chunk restricted to one worker, placed lane-parallel
+   if (DGP_BULK_RESTR && bulk_restricted_distinct<LW>(D, S, P, g, durv, k0 + lane < f1 && fml == (int)r, xl, rcl, rdl,
+                                                      rhl, rcml, evp, lpos, npl))
+     continue;  // one task per worker, each on its own worker, lane-parallel
    for (int j = 0; j < nk; j++) {
     const int x = rl(xl, j);
     if (rl(fml, j) != (int)r) continue;

@@ -97,14 +97,16 @@ def test_engine_full_c5_digest(engine_cls):
     assert graphs.placement_digest(out) == pin["digest"]
 
 
-@pytest.mark.parametrize("sat", [1.1, "inf"])
-def test_engine_full_c3_shuffle(engine_cls, sat):
+@pytest.mark.parametrize("sat,restricted", [(1.1, False), ("inf", False), (1.1, True)],
+                         ids=["sat1.1", "satinf", "restricted"])
+def test_engine_full_c3_shuffle(engine_cls, sat, restricted):
     """BASELINE.json C3 at full size: P = 66,666 partitions (3P + 1 = 200k tasks: inputs,
     shuffle-transfer, one barrier of fan-in P, unpack tasks with _rootish False) on 512
-    workers, bit-exact against the oracle."""
+    workers, bit-exact against the oracle; also with the unpacks restricted to their
+    range-sharded worker (restrict_task, shuffle/_scheduler_plugin.py:101-115)."""
     from distributed_amd import graphs
 
-    g = graphs.shuffle_graph(66_666, 512)
+    g = graphs.shuffle_graph(66_666, 512, restricted=restricted)
     cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": sat}
     ref = oracle.replay(g, cfg, snapshots=False)
     with engine_cls(0) as eng:
