@@ -4,7 +4,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_amd import graphs
 from distributed_amd.engine import PlacementEngine
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-for name, g in (("c2", graphs.random_dag(1_000_000, 1024, seed=0)), ("c3", graphs.shuffle_graph(66_666, 512))):
+for name, g in (("c2", graphs.random_dag(1_000_000, 1024, seed=0)), ("c3", graphs.shuffle_graph(66_666, 512)),
+                ("c3r", graphs.shuffle_graph(66_666, 512, restricted=True))):
     e = PlacementEngine(0)
     e.load(g, {"saturation": 1.1})
     ts = []
