@@ -61,7 +61,7 @@ __constant__ Dev c_dev;
 #define DGP_REG_PROBES 0  // registrar sub-phase s_memtime probes (diagnostics)
 #endif
 #ifndef DGP_BULK_RESTR
-#define DGP_BULK_RESTR 0  // global frontier: restricted single-worker tasks on distinct workers placed lane-parallel
+#define DGP_BULK_RESTR 1  // global frontier: restricted single-worker tasks on distinct workers placed lane-parallel
 #endif
 #ifndef DGP_RUN_PAR
 #define DGP_RUN_PAR 1  // single-worker runs of one prefix: every member's record at once (lane = member)
