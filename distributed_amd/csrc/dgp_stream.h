@@ -2657,25 +2657,31 @@ __device__ __attribute__((always_inline)) bool bulk_single_holder(const Dev& D, 
 // the dependency's needs_what entry made by the first (netocc grows once) or counted up.
 // The same operations as place_x one task at a time, lane L computing placement L.
 template <bool LW>
-__device__ __attribute__((always_inline)) bool bulk_restricted_same(const Dev& D, SCtl& S, const WPtr<LW>& P,
-                                                                    WState& g, DTab durv, bool fr, int xl, int rcl,
-                                                                    int rdl, bool rhl, int64_t rcml, bool evp,
-                                                                    long long lpos, int& npl) {
+__device__ __attribute__((always_inline)) unsigned long long bulk_restricted_same(const Dev& D, SCtl& S,
+                                                                                  const WPtr<LW>& P, WState& g,
+                                                                                  DTab durv, bool fr0, int from, int xl,
+                                                                                  int rcl, int rdl, bool rhl,
+                                                                                  int64_t rcml, bool evp,
+                                                                                  long long lpos, int& npl) {
+  // the run: the frontier lanes from lane `from` on, up to the first one that differs
+  // (another worker, dependency or prefix); returns the lanes placed (0: none)
   const int lane = lane_id();
-  const unsigned long long fm = ballot(fr);
-  const int m = __builtin_popcountll(fm);
-  if (m < 2) return false;
-  const int first = __builtin_ctzll(fm);
+  const int first = from;
   const int c = rl(rcl, first), d = rl(rdl, first);
-  const int pxl = fr ? D.prefix[xl] : -1;
+  const int pxl = fr0 ? D.prefix[xl] : -1;
   const int px = rl(pxl, first);
   const bool held = rl(rhl ? 1 : 0, first) != 0;
   const int64_t comm = rl_i64(rcml, first);
-  if (c < 0 || c >= D.W || (evp && (P.wflags[c] & WF_PAUSED))) return false;
-  if (ballot(fr && (rcl != c || rdl != d || pxl != px || xl == D.dbg_task))) return false;
+  if (c < 0 || c >= D.W || (evp && (P.wflags[c] & WF_PAUSED))) return 0;
+  const unsigned long long diff = ballot(fr0 && lane >= from && (rcl != c || rdl != d || pxl != px || xl == D.dbg_task));
+  const int lim = diff ? __builtin_ctzll(diff) : 64;
+  const bool fr = fr0 && lane >= from && lane < lim;
+  const unsigned long long fm = ballot(fr);
+  const int m = __builtin_popcountll(fm);
+  if (m < 2) return 0;
   WDict d0 = dict_load<LW>(P, c);
   const uint32_t cnt0 = wd_cnt(d0, px);
-  if (cnt0 == 0 && wd_n(d0.ord) >= (uint32_t)PD) return false;
+  if (cnt0 == 0 && wd_n(d0.ord) >= (uint32_t)PD) return 0;
   // the dependency's needs_what entry on c (lane i holds line word i)
   uint32_t nl = line_load<LW>(P, c);
   int64_t dnI = 0;  // netocc added by the first placement
@@ -2683,14 +2689,14 @@ __device__ __attribute__((always_inline)) bool bulk_restricted_same(const Dev& D
   bool ins = false;
   if (!held) {
     const uint32_t ctl = rlu(nl, NLW - 1);
-    if (ctl == NL_OVF || (int)(ctl >> 8) != line_used(nl)) return false;
+    if (ctl == NL_OVF || (int)(ctl >> 8) != line_used(nl)) return 0;
     const unsigned long long hm = ballot(lane < NLW - 1 && nl != 0 && (nl >> 8) == (uint32_t)d);
     if (hm) {
       ent = __builtin_ctzll(hm);
-      if ((rlu(nl, ent) & 0xffu) + (uint32_t)m > 0xffu) return false;
+      if ((rlu(nl, ent) & 0xffu) + (uint32_t)m > 0xffu) return 0;
     } else {
       const unsigned long long em = ballot(lane < NLW - 1 && nl == 0);
-      if (!em) return false;
+      if (!em) return 0;
       ent = __builtin_ctzll(em);
       ins = true;
       dnI = comm;  // _inc_needs_replica: the bytes c newly needs (:800-813), nbytes of d
@@ -2749,7 +2755,7 @@ __device__ __attribute__((always_inline)) bool bulk_restricted_same(const Dev& D
   rc.dur = 0.0;
   ws_fold_batch<LW>(D, P, S, g, rc, m);
   npl += m;
-  return true;
+  return fm;
 }
 
 // A chunk of frontier tasks that each have one dependency and ONE valid worker, running and
@@ -3082,16 +3088,22 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
    const int nk = (int)min((int64_t)64, f1 - k0);
    if (bulk_single_holder<LW>(D, S, P, g, durv, r, k0 + lane < f1 && fml == (int)r, xl, tfl, h1l, lpos, npl))
      continue;  // the whole chunk went to one worker, placed lane-parallel
-   if (DGP_BULK_RESTR && bulk_restricted_same<LW>(D, S, P, g, durv, k0 + lane < f1 && fml == (int)r, xl, rcl, rdl, rhl,
-                                                  rcml, evp, lpos, npl))
-     continue;  // the chunk restricted to one worker, placed lane-parallel
    if (DGP_BULK_RESTR && bulk_restricted_distinct<LW>(D, S, P, g, durv, k0 + lane < f1 && fml == (int)r, xl, rcl, rdl,
                                                       rhl, rcml, evp, lpos, npl))
      continue;  // one task per worker, each on its own worker, lane-parallel
+   const bool frl = k0 + lane < f1 && fml == (int)r;
    for (int j = 0; j < nk; j++) {
     const int x = rl(xl, j);
     if (rl(fml, j) != (int)r) continue;
     const int rc1 = rl(rcl, j);
+    if (DGP_BULK_RESTR && rc1 >= 0) {  // a run of restricted tasks on one worker from j on: lane-parallel
+      const unsigned long long done = bulk_restricted_same<LW>(D, S, P, g, durv, frl, j, xl, rcl, rdl, rhl, rcml, evp,
+                                                               lpos, npl);
+      if (done) {
+        j = 63 - __builtin_clzll(done);
+        continue;
+      }
+    }
     if (rc1 >= 0 && rc1 < D.W && !paused(rc1) && x != D.dbg_task) {
       // decide_worker with one valid running worker (:8575-8586): the candidates are that
       // worker whether or not it holds the dependency (holders & valid, else valid)
