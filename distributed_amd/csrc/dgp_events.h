@@ -447,10 +447,15 @@ __global__ void k_sync_placements(const Dev* __restrict__ Dp, const int32_t* __r
     D.pl_start[pos] = start[i];
     D.pl_wsnbytes[pos] = wsnb[i];
     D.pl_route[pos] = route[i];
-    D.run_id[t] = (int32_t)pos;
-    D.holder_of[t] = worker[i];
   }
   __syncthreads();
+  // run identity and holder: the last placement of each task wins (a suspended stimulus may
+  // place one task twice), so one thread walks them in log order
+  if (threadIdx.x == 0)
+    for (int i = 0; i < n; i++) {
+      D.run_id[task[i]] = (int32_t)(base + i);
+      D.holder_of[task[i]] = worker[i];
+    }
   if (threadIdx.x == 0) {
     D.ctl->n_placed = (unsigned long long)(base + n);
     D.pos->runid_upto = base + n;

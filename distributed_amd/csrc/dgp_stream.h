@@ -75,6 +75,12 @@ __constant__ Dev c_dev;
 #ifndef DGP_STAGE_PRIO
 #define DGP_STAGE_PRIO 0  // issue priority of the builder / prefetcher waves
 #endif
+#ifndef DGP_DBG_TASK
+#define DGP_DBG_TASK 0  // diagnostics: exe_local dumps the candidate keys of frontier task D.dbg_task
+#endif
+#ifndef DGP_FAST
+#define DGP_FAST 1  // F_FAST stimuli take exe_fast (0: exe_local)
+#endif
 #ifndef DGP_RB
 #define DGP_RB 8  // registrar batch (stimuli registered per poll, one lane each)
 #endif
@@ -142,7 +148,16 @@ static_assert((RS & (RS - 1)) == 0 && RS >= WIN && RS <= DR, "DGP_RS must be a p
 // (held by that worker) and one release: it can be part of a single-worker run (exe_run).
 // F_RUNM (REG): F_SIMPLE and so is the stimulus just before it, on the same worker: a run
 // continues through it, so only the run-capable executor takes it
-enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16, F_SIMPLE = 32, F_RUNM = 64 };
+// F_FAST (PRE): a local stimulus the lean executor path takes (exe_fast): at most NFF frontier
+// tasks, none restricted, at most TF touched workers, P <= PD; PRE wrote its frow rows
+enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16, F_SIMPLE = 32, F_RUNM = 64,
+                  F_FAST = 128 };
+// exe_fast's rows (D.frow, one block of FRS entries per descriptor row): row j, entry i =
+// frontier task j's comm_bytes / bandwidth and comm_bytes on touched worker i, written for its
+// candidates only (the frontier entry's .w is the candidates' touch-index mask)
+constexpr int NFF = 4;
+constexpr int TF = 16;
+constexpr int FRS = NFF * TF;
 // K_COMPLETE_LR: the completion of a long-running task (its prefix count left the worker's and
 // the global dict at add_to_long_running :747-757; remove_from_processing :764-766)
 enum : int { K_COMPLETE = 1, K_PLACE = 2, K_COMPLETE_LR = 3 };
@@ -1116,6 +1131,12 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
           task = D.qarr[qb + popk++];
           D.state[task] = S_PROCESSING;
           D.proc_on[task] = w;
+        } else {  // a frontier placement (waiting -> processing, :2313-2336): TaskState and the
+                  // group's released + waiting count, off the executors' path (only exact /
+                  // global stimuli and the host read them, after this retirement)
+          D.state[task] = S_PROCESSING;
+          D.proc_on[task] = w;
+          atomicAdd((unsigned long long*)&D.g_relwait[D.group[task]], (unsigned long long)-1ll);
         }
         D.pl_task[pos] = task;
         D.pl_worker[pos] = w;
@@ -1243,7 +1264,7 @@ __device__ __attribute__((always_inline)) void bld_range(const Dev& D, SLds& L, 
 
 // ==================================================================== prefetcher
 // descriptor of stimulus r (one lane): see E_HDR for the header layout
-__device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L, long long r, int& p_out, double& dobs_out) {
+__device__ __attribute__((always_inline)) void build_desc_seq(const Dev& D, SLds& L, long long r, int& p_out, double& dobs_out) {
   uint4* E = D.desc + (size_t)(r & (DR - 1)) * NE;
   // the distinct workers the stimulus touches, in first-touch order (lane-private LDS list)
   auto scr = L.pre_scr[lane_id()];
@@ -1252,19 +1273,19 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   // service events the local path does not model make the stimulus global (exe_global):
   // a paused worker (not in running), a replica set beyond holder_of, a long-running task
   bool evg = false;
-  auto touch = [&](int c, bool cand) {
+  auto touch = [&](int c, bool cand) -> int {  // -> its index in the touch list (-1: none)
     if (c < 0 || c >= D.W) {
       tbad = true;
-      return;
+      return -1;
     }
     if ((D.evf & EVF_PAUSED) && (D.w_flags[c] & WF_PAUSED)) evg = true;
     for (int i = 0; i < nt && i < TMAX; i++)
       if ((scr[i] & T_W) == c) {
         if (cand) scr[i] |= (uint16_t)T_CAND;
-        return;
+        return i;
       }
     if (nt < TMAX) scr[nt] = (uint16_t)(c | (cand ? T_CAND : 0));
-    nt++;
+    return nt++ < TMAX ? nt - 1 : -1;
   };
   const int t = D.stim_task[r];
   const int w = D.stim_worker[r];
@@ -1284,6 +1305,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
     PROF(atomicAdd(&L.c.prof[20], 1ull));  // diagnostics: why stimuli run global
   }
   int n = E_HDR, nrel = 0, nf = 0, sumkx = 0;
+  bool anyrx = false;  // a restricted frontier task (not on the F_FAST path)
   touch(w, false);
   int h_dep0 = -1;  // holder of the first dependency
   if (!(flags & F_GLOBAL)) {
@@ -1326,6 +1348,7 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
     // holders & valid; none: the valid set; valid empty: loose -> the holders, else
     // no-worker (global). They follow the dependency entries; the holders are not touched
     const bool rx = restricted_nonrootish(D, x);
+    anyrx = anyrx || rx;
     int cw[RC_MAX];
     int nc = 0;
     if (rx) {
@@ -1353,17 +1376,51 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
         continue;
       }
     }
-    E[n++] = make_uint4((unsigned)x, (unsigned)D.prefix[x], (unsigned)(kx | (nc << 8) | (rx ? 1 << 16 : 0)),
-                        (unsigned)D.group[x]);
+    const int nx = n++;  // the task's entry, written below with its candidates' touch mask
     sumkx += kx;
-    for (int64_t q = x0; q < x1; q++) {
-      const int d = D.dep_idx[q];
-      const int64_t nb = nbv(D, D.res_nbytes[d]);
-      const int hd = D.holder_of[d];
-      if ((D.evf & EVF_MULTI) && (D.tdyn[d] & TD_MULTI)) evg = true;
-      if (!rx) touch(hd, true);
-      E[n++] = make_uint4((unsigned)d, (unsigned)hd, lo32(nb), hi32(nb));
+    // decide_worker's candidates (:8571-8574) are the dependencies' holders; PRE resolves
+    // their state-independent objective terms for exe_fast (worker_objective :3136-3138:
+    // comm_bytes = the bytes of the dependencies the candidate does not hold, / bandwidth)
+    int tix[KX_MAX];
+    int64_t nbq[KX_MAX];
+    int64_t tot = 0;
+#pragma unroll
+    for (int q = 0; q < KX_MAX; q++) {
+      tix[q] = -1;
+      nbq[q] = 0;
+      if (q < kx) {
+        const int d = D.dep_idx[x0 + q];
+        const int64_t nb = nbv(D, D.res_nbytes[d]);
+        const int hd = D.holder_of[d];
+        if ((D.evf & EVF_MULTI) && (D.tdyn[d] & TD_MULTI)) evg = true;
+        if (!rx) tix[q] = touch(hd, true);
+        nbq[q] = nb;
+        tot += nb;
+        E[n++] = make_uint4((unsigned)d, (unsigned)hd, lo32(nb), hi32(nb));
+      }
     }
+    uint32_t cmask = 0;  // touch indices (< 32) of the candidates
+    if (!rx) {
+      const int jf = nf - 1;
+      uint4* FR = D.frow + (size_t)(r & (DR - 1)) * FRS + (size_t)jf * TF;
+#pragma unroll
+      for (int q = 0; q < KX_MAX; q++) {
+        const int i = tix[q];
+        if (q < kx && i >= 0 && i < 32 && !((cmask >> i) & 1u)) {
+          cmask |= 1u << i;
+          if (jf < NFF && i < TF) {
+            int64_t held = 0;
+#pragma unroll
+            for (int q2 = 0; q2 < KX_MAX; q2++)
+              if (q2 < kx && tix[q2] == i) held += nbq[q2];
+            const int64_t comm = tot - held;  // int64: exact in any order
+            const double cd = (double)comm / (double)D.bandwidth;
+            FR[i] = make_uint4(dlo(cd), dhi(cd), lo32(comm), hi32(comm));
+          }
+        }
+      }
+    }
+    E[nx] = make_uint4((unsigned)x, (unsigned)D.prefix[x], (unsigned)(kx | (nc << 8) | (rx ? 1 << 16 : 0)), cmask);
     for (int i = 0; i < nc; i++) {
       touch(cw[i], true);
       E[n++] = make_uint4((unsigned)cw[i], 0u, 0u, 0u);
@@ -1379,6 +1436,8 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
       (kt == 0 || h_dep0 == w) && D.P <= PD)  // a run shares the head's descriptor durations
     flags |= F_SIMPLE;
   if (flags & F_GLOBAL) nt = 0;
+  // exe_fast takes it: PRE wrote the rows of its frontier's candidates above
+  if (!(flags & F_GLOBAL) && nf <= NFF && nt <= TF && D.P <= PD && !anyrx) flags |= F_FAST;
   int32_t* T = D.touch_ring + (size_t)(r & (DR - 1)) * TMAX;
   for (int i = 0; i < nt; i++) T[i] = scr[i];
   E[0] = make_uint4((unsigned)t, (unsigned)w, (unsigned)p, flags);
@@ -1388,6 +1447,242 @@ __device__ __attribute__((always_inline)) void build_desc(const Dev& D, SLds& L,
   D.thdr[r & (DR - 1)] = make_uint2(flags, (unsigned)nt);
   p_out = p;
   dobs_out = dobs;
+}
+
+// The gathered form of build_desc: every load of one dependency level is issued before any
+// store (a store to the ring would order each later load behind it), 8 entries at a time, so
+// a lane's descriptor costs a handful of memory round trips -- the stimulus, its task, the
+// dependency ids, their fields (holders, sizes, release marks), the dependent ids and their
+// frontier marks, then per frontier task its fields, its dependencies' ids and fields --
+// instead of one or two per entry. PRE's batch is as slow as its slowest lane, so every
+// size takes this path (a completion with many dependents costs one more pair of round trips
+// per 8 of them). The descriptor, the touch list and the frow rows come out exactly as
+// build_desc_seq writes them. false (nothing written): the graph has restrictions (their
+// resolved candidates stay with build_desc_seq).
+constexpr int GC = 8;  // entries gathered per round trip
+__device__ __attribute__((always_inline)) bool build_desc_g(const Dev& D, SLds& L, long long r, int& p_out, double& dobs_out) {
+  if (D.restr_flags) return false;
+  const int t = D.stim_task[r];
+  const int w = D.stim_worker[r];
+  // ---- the completing task (one round trip)
+  const int p = D.prefix[t];
+  const int g = D.group[t];
+  const uint8_t tf = D.tflags[t];
+  const int64_t nbraw = D.res_nbytes[t];
+  const double stop = D.res_stop[t], start = D.res_start[t];
+  const int64_t k0 = D.dep_ptr[t], k1 = D.dep_ptr[t + 1];
+  const int64_t f0 = D.dpt_ptr[t], f1 = D.dpt_ptr[t + 1];
+  const uint8_t tdt = (D.evf & EVF_LR) ? D.tdyn[t] : 0;
+  const int capw = D.sat_inf ? 0 : D.w_cap[w];
+  const int kt = (int)(k1 - k0);
+  uint4* E = D.desc + (size_t)(r & (DR - 1)) * NE;
+  auto scr = L.pre_scr[lane_id()];
+  int nt = 0;
+  bool tbad = false, evg = false;
+  auto touch = [&](int c, bool cand) -> int {  // -> its index in the touch list (-1: none)
+    if (c < 0 || c >= D.W) {
+      tbad = true;
+      return -1;
+    }
+    if ((D.evf & EVF_PAUSED) && (D.w_flags[c] & WF_PAUSED)) evg = true;
+    for (int i = 0; i < nt && i < TMAX; i++)
+      if ((scr[i] & T_W) == c) {
+        if (cand) scr[i] |= (uint16_t)T_CAND;
+        return i;
+      }
+    if (nt < TMAX) scr[nt] = (uint16_t)(c | (cand ? T_CAND : 0));
+    return nt++ < TMAX ? nt - 1 : -1;
+  };
+  const int64_t nbt = nbv(D, nbraw);
+  const double dobs = stop - start;
+  uint32_t flags = 0;
+  if (f1 == f0 && !(tf & TF_WANTED)) flags |= F_SELFREL;
+  if (tdt & TD_LR) evg = true;
+  if (kt > KT_MAX) flags |= F_GLOBAL;
+  int n = E_HDR, nrel = 0, nf = 0, sumkx = 0;
+  int h_dep0 = -1;
+  touch(w, false);
+  uint32_t relm = 0;  // dependencies (< KT_MAX) released by this completion
+  if (!(flags & F_GLOBAL)) {
+    // ---- dependencies: ids, then fields, GC at a time; their entries in order
+    for (int c0 = 0; c0 < kt; c0 += GC) {
+      int dq[GC];
+#pragma unroll
+      for (int q = 0; q < GC; q++) dq[q] = c0 + q < kt ? D.dep_idx[k0 + c0 + q] : 0;
+      int64_t nbq[GC];
+      int hq[GC], rmq[GC];
+      bool mq[GC];
+#pragma unroll
+      for (int q = 0; q < GC; q++) {
+        nbq[q] = 0;
+        hq[q] = rmq[q] = -1;
+        mq[q] = false;
+        if (c0 + q < kt) {
+          nbq[q] = nbv(D, D.res_nbytes[dq[q]]);
+          hq[q] = D.holder_of[dq[q]];
+          rmq[q] = D.rel_mark[dq[q]];
+          mq[q] = (D.evf & EVF_MULTI) && (D.tdyn[dq[q]] & TD_MULTI);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < GC; q++)
+        if (c0 + q < kt) {
+          if (c0 + q == 0) h_dep0 = hq[q];
+          if (mq[q]) evg = true;
+          if (rmq[q] == (int)r) relm |= 1u << (c0 + q);
+          E[n++] = make_uint4((unsigned)dq[q], (unsigned)hq[q], lo32(nbq[q]), hi32(nbq[q]));
+        }
+    }
+    // ---- the releases (their dependency entries read back, one round trip)
+    for (uint32_t m = relm; m && !(flags & F_GLOBAL); m &= m - 1) {
+      if (n >= NE) {
+        flags |= F_GLOBAL;
+        break;
+      }
+      const uint4 er = E[E_HDR + __builtin_ctz(m)];
+      touch((int)er.y, false);
+      E[n++] = make_uint4(er.y, er.x, er.z, er.w);
+      nrel++;
+    }
+  }
+  // ---- dependents in ascending priority = frontier order (a global stimulus stops the walk)
+  uint4* FRb = D.frow + (size_t)(r & (DR - 1)) * FRS;
+  const int nd = (int)(f1 - f0);
+  for (int c0 = 0; c0 < nd && !(flags & F_GLOBAL); c0 += GC) {
+    int xq[GC];
+#pragma unroll
+    for (int q = 0; q < GC; q++) xq[q] = c0 + q < nd ? D.dpt_idx[f0 + c0 + q] : 0;
+    int frq[GC];
+#pragma unroll
+    for (int q = 0; q < GC; q++) frq[q] = c0 + q < nd ? D.fr_mark[xq[q]] : -1;
+    // the frontier tasks of this chunk: their fields at once
+    uint8_t ftf[GC];
+    int64_t fx0[GC];
+    int fkx[GC], fpx[GC];
+#pragma unroll
+    for (int q = 0; q < GC; q++) {
+      ftf[q] = 0;
+      fx0[q] = 0;
+      fkx[q] = 0;
+      fpx[q] = 0;
+      if (frq[q] == (int)r) {
+        const int x = xq[q];
+        ftf[q] = D.tflags[x];
+        fx0[q] = D.dep_ptr[x];
+        fkx[q] = (int)(D.dep_ptr[x + 1] - fx0[q]);
+        fpx[q] = D.prefix[x];
+      }
+    }
+    uint32_t fm = 0;  // the chunk's frontier tasks
+#pragma unroll
+    for (int q = 0; q < GC; q++) fm |= frq[q] == (int)r ? 1u << q : 0u;
+    static_assert(GC == 8, "DGP_SEL8");
+#define DGP_SEL8(a, q) \
+  ((q) == 0 ? a[0] : (q) == 1 ? a[1] : (q) == 2 ? a[2] : (q) == 3 ? a[3] : (q) == 4 ? a[4] : (q) == 5 ? a[5] : (q) == 6 ? a[6] : a[7])
+#pragma unroll 1
+    for (; fm && !(flags & F_GLOBAL); fm &= fm - 1) {
+      const int q = __builtin_ctz(fm);  // (lane-varying: selected without indexing the arrays)
+      const int j = nf++;
+      const int x = DGP_SEL8(xq, q), kx = DGP_SEL8(fkx, q);
+      const uint8_t ftq = DGP_SEL8(ftf, q);
+      const int64_t fxq = DGP_SEL8(fx0, q);
+      const int fpq = DGP_SEL8(fpx, q);
+      if ((ftq & TF_ROOTISH) || kx > KX_MAX || n + 1 + kx > NE) {
+        flags |= F_GLOBAL;
+        continue;
+      }
+      // its dependencies: ids, then fields
+      int dx[KX_MAX];
+#pragma unroll
+      for (int i = 0; i < KX_MAX; i++) dx[i] = i < kx ? D.dep_idx[fxq + i] : 0;
+      int64_t nbx[KX_MAX];
+      int hx[KX_MAX];
+#pragma unroll
+      for (int i = 0; i < KX_MAX; i++) {
+        nbx[i] = 0;
+        hx[i] = -1;
+        if (i < kx) {
+          nbx[i] = nbv(D, D.res_nbytes[dx[i]]);
+          hx[i] = D.holder_of[dx[i]];
+          if ((D.evf & EVF_MULTI) && (D.tdyn[dx[i]] & TD_MULTI)) evg = true;
+        }
+      }
+      const int nx = n++;
+      sumkx += kx;
+      // decide_worker's candidates (:8571-8574) are the dependencies' holders; their
+      // state-independent objective terms for exe_fast (worker_objective :3136-3138:
+      // comm_bytes = the bytes of the dependencies the candidate does not hold, / bandwidth)
+      int tix[KX_MAX];
+      int64_t tot = 0;
+#pragma unroll
+      for (int i = 0; i < KX_MAX; i++) {
+        tix[i] = -1;
+        if (i < kx) {
+          tix[i] = touch(hx[i], true);
+          tot += nbx[i];
+          E[n++] = make_uint4((unsigned)dx[i], (unsigned)hx[i], lo32(nbx[i]), hi32(nbx[i]));
+        }
+      }
+      uint32_t cmask = 0;  // touch indices (< 32) of the candidates
+#pragma unroll
+      for (int i = 0; i < KX_MAX; i++) {
+        const int ti = tix[i];
+        if (i < kx && ti >= 0 && ti < 32 && !((cmask >> ti) & 1u)) {
+          cmask |= 1u << ti;
+          if (j < NFF && ti < TF) {
+            int64_t held = 0;
+#pragma unroll
+            for (int i2 = 0; i2 < KX_MAX; i2++)
+              if (i2 < kx && tix[i2] == ti) held += nbx[i2];
+            const int64_t comm = tot - held;  // int64: exact in any order
+            const double cd = (double)comm / (double)D.bandwidth;
+            FRb[(size_t)j * TF + ti] = make_uint4(dlo(cd), dhi(cd), lo32(comm), hi32(comm));
+          }
+        }
+      }
+      E[nx] = make_uint4((unsigned)x, (unsigned)fpq, (unsigned)kx, cmask);
+    }
+#undef DGP_SEL8
+  }
+  if (nf > 255 || nt > TMAX) flags |= F_GLOBAL;
+  if (nf + capw + 1 > PLC) flags |= F_GLOBAL;  // staging room for the refill
+  if (tbad) flags |= F_GLOBAL | F_BADTOUCH;
+  if (evg) flags |= F_GLOBAL;
+  if (!(flags & F_GLOBAL) && nt == 1 && nf == 0 && kt <= 1 && nrel <= 1 && (kt == 0 || h_dep0 == w) && D.P <= PD)
+    flags |= F_SIMPLE;  // a run shares the head's descriptor durations
+  if (flags & F_GLOBAL) nt = 0;
+  if (!(flags & F_GLOBAL) && nf <= NFF && nt <= TF && D.P <= PD) flags |= F_FAST;
+  int32_t* T = D.touch_ring + (size_t)(r & (DR - 1)) * TMAX;
+  for (int i = 0; i < nt; i++) T[i] = scr[i];
+  E[0] = make_uint4((unsigned)t, (unsigned)w, (unsigned)p, flags);
+  E[1] = make_uint4(lo32(nbt), hi32(nbt),
+                    (unsigned)(min(kt, 255) | (nrel << 8) | (min(nf, 255) << 16) | (n << 24)), (unsigned)g);
+  E[2] = make_uint4(dlo(dobs), dhi(dobs), (unsigned)nt, (unsigned)sumkx);
+  D.thdr[r & (DR - 1)] = make_uint2(flags, (unsigned)nt);
+  p_out = p;
+  dobs_out = dobs;
+  return true;
+}
+struct DescOut {
+  int ok, p;
+  double dobs;
+};
+// out of line: each form gets its own register allocation (inlined together they spilled)
+__device__ __attribute__((noinline)) DescOut build_desc_g_entry(long long r) {
+  DescOut o{0, 0, 0.0};
+  o.ok = build_desc_g(c_dev, st_L, r, o.p, o.dobs) ? 1 : 0;
+  return o;
+}
+__device__ __attribute__((noinline)) DescOut build_desc_seq_entry(long long r) {
+  DescOut o{1, 0, 0.0};
+  build_desc_seq(c_dev, st_L, r, o.p, o.dobs);
+  return o;
+}
+__device__ __forceinline__ void build_desc(const Dev& D, SLds& L, long long r, int& p_out, double& dobs_out) {
+  DescOut o = build_desc_g_entry(r);
+  if (!o.ok) o = build_desc_seq_entry(r);
+  p_out = o.p;
+  dobs_out = o.dobs;
 }
 
 // ========================================================== builder / prefetcher
@@ -1959,7 +2254,8 @@ __device__ __attribute__((always_inline)) void release_slot(const Dev& D, SLds& 
 
 // publish the counts in the retire ring, mark the stimulus done and free its slot: the
 // sequencer retires it in order later (its staging rows were written as the outputs were made)
-__device__ __attribute__((always_inline)) void finish_slot(const Dev& D, SLds& L, int s, long long r, const Out& o, int npops, bool direct) {
+template <class O>
+__device__ __attribute__((always_inline)) void finish_slot(const Dev& D, SLds& L, int s, long long r, const O& o, int npops, bool direct) {
   const int lane = lane_id();
   const int q = (int)(r & (RS - 1));
   if (lane == 0) {
@@ -2210,7 +2506,6 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     const int x = rl((int)E.x, off), px = rl((int)E.y, off);
     const int hz = rl((int)E.z, off);
     const int kx = hz & 0xff, nc = (hz >> 8) & 0xff;  // nc: a restricted task's resolved candidates
-    const int gx = rl((int)E.w, off);
     // candidates = the holders of x's dependencies (each a touched lane); comm_bytes (:3136)
     int64_t comm = 0;
     bool cand = false;
@@ -2227,22 +2522,23 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     }
     cand = cand && tl;
     Key k;
-    const double oc = occj;
     k.start = stkj + (double)comm / (double)D.bandwidth;
     k.nb = nbj;
     k.w = cj;
     k.comm = comm;
+#if DGP_DBG_TASK
     if (x == D.dbg_task && cand) {
       double* B = D.dbgbuf + (size_t)lane * 8;
       B[0] = cj;
       B[1] = k.start;
       B[2] = (double)k.nb;
       B[3] = (double)comm;
-      B[4] = oc;
+      B[4] = occj;
       B[5] = np;
       B[6] = (double)net;
       B[7] = (double)wd_n(dj.ord) + 100.0 * r;
     }
+#endif
     phase(18);
     const unsigned long long cm = ballot(cand);
     if (!cm) {
@@ -2308,10 +2604,9 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     }
     if (dn != 0) nbw = isb ? net_bw_of(net, D) : nbw;  // dn is uniform
     if (ballot(!okp)) serr(S, SERR_PREFIX, x);
-    if (lane == 0) {
-      D.proc_on[x] = cb;
+    if (exact && lane == 0) {  // scan mode reads them for this stimulus' later decisions (the
+      D.proc_on[x] = cb;       // sequencer writes them, and the group count, at retirement)
       D.state[x] = S_PROCESSING;
-      atomicAdd((unsigned long long*)&D.g_relwait[gx], (unsigned long long)-1ll);
     }
     occj = occ_dict_r(dj, nbw, durv, D);
     stkj = nth1 ? occj : occj / (double)nth;
@@ -2388,6 +2683,396 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   phase(14);
   finish_slot(D, L, s, r, o, pops, false);
   phase(15);
+  return true;
+}
+
+// ============================================================ the lean local path
+// exe_fast: what exe_local does, for the F_FAST stimuli (the common local case), with the
+// state-independent work moved to PRE (its frow rows: candidate flags, comm_bytes /
+// bandwidth, lacking dependencies, released bytes per touched worker; one lane of PRE per
+// stimulus, off the chain) and the outputs staged in registers. The replay is bound by the
+// chain of stimuli sharing workers, and a wave issues about one instruction per four cycles,
+// so the latency of a stimulus is its executor's instruction count: this path keeps only the
+// state-dependent work (needs_what, the prefix dicts, occupancies, the argmin, the refill).
+
+// outputs staged in registers: placement / record k in lane k (uniform values, one select each),
+// written to the slot's staging rows with one store per field after the workers are released
+struct OutR {
+  int nrec, npl;
+  int pt, pw, pr;
+  int64_t pc, pn;
+  double ps;
+  int rw, rpk, rnp, rtk;
+  int64_t rdn;
+  double rocc, rdur;
+  __device__ __forceinline__ void init() {
+    nrec = npl = 0;
+    pt = pw = pr = 0;
+    pc = pn = 0;
+    ps = 0.0;
+    rw = rpk = rnp = rtk = 0;
+    rdn = 0;
+    rocc = rdur = 0.0;
+  }
+  __device__ __forceinline__ static int wl(int v, int l, int old) { return lane_id() == l ? v : old; }
+  __device__ __forceinline__ static int64_t wl64(int64_t v, int l, int64_t old) {
+    return mk64((unsigned)wl((int)lo32(v), l, (int)lo32(old)), (unsigned)wl((int)hi32(v), l, (int)hi32(old)));
+  }
+  __device__ __forceinline__ static double wlf(double v, int l, double old) {
+    return __longlong_as_double(wl64(__double_as_longlong(v), l, __double_as_longlong(old)));
+  }
+  __device__ __forceinline__ void place(int task, int w, int64_t comm, double start, int64_t wsnb, int route) {
+    if (npl < PLC) {
+      pt = wl(task, npl, pt);
+      pw = wl(w, npl, pw);
+      pr = wl(route, npl, pr);
+      pc = wl64(comm, npl, pc);
+      pn = wl64(wsnb, npl, pn);
+      ps = wlf(start, npl, ps);
+    }
+    npl++;
+  }
+  __device__ __forceinline__ void rec(int kind, int w, int p, int64_t dnet, double occ, int np, int task, double dur) {
+    if (nrec < PLC) {
+      rw = wl(w, nrec, rw);
+      rpk = wl((p & 0xffff) | (kind << 16), nrec, rpk);
+      rnp = wl(np, nrec, rnp);
+      rtk = wl(task, nrec, rtk);
+      rdn = wl64(dnet, nrec, rdn);
+      rocc = wlf(occ, nrec, rocc);
+      rdur = wlf(dur, nrec, rdur);
+    }
+    nrec++;
+  }
+  __device__ __forceinline__ void flush(const Dev& D, size_t st0) const {
+    const int lane = lane_id();
+    if (lane < npl && lane < PLC) {
+      D.s2_task[st0 + lane] = pt;
+      D.s2_worker[st0 + lane] = pw;
+      D.s2_comm[st0 + lane] = pc;
+      D.s2_start[st0 + lane] = ps;
+      D.s2_wsnb[st0 + lane] = pn;
+      D.s2_route[st0 + lane] = (int8_t)pr;
+    }
+    if (lane < nrec && lane < PLC) {
+      SRec rc;
+      rc.w = rw;
+      rc.p = (int16_t)(rpk & 0xffff);
+      rc.kind = (int8_t)(rpk >> 16);
+      rc.pad = 0;
+      rc.nproc = rnp;
+      rc.task = rtk;
+      rc.dnet = rdn;
+      rc.occ = rocc;
+      rc.dur = rdur;
+      D.srec[st0 + lane] = rc;
+    }
+  }
+};
+
+// minimum of a u64 over lanes 0..15 (one DPP row: quad swaps, half-row and row mirrors),
+// in every lane of row 0
+__device__ __forceinline__ uint64_t row_min_u64(uint64_t v) {
+  unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+#define DGP_MINSTEP(ctl)                                                          \
+  {                                                                               \
+    const unsigned l2 = (unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, ctl, 0xf, 0xf, false); \
+    const unsigned h2 = (unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, ctl, 0xf, 0xf, false); \
+    const bool lt = ((uint64_t)h2 << 32 | l2) < ((uint64_t)hi << 32 | lo);       \
+    lo = lt ? l2 : lo;                                                            \
+    hi = lt ? h2 : hi;                                                            \
+  }
+  DGP_MINSTEP(0xb1)   // quad_perm(1,0,3,2)
+  DGP_MINSTEP(0x4e)   // quad_perm(2,3,0,1)
+  DGP_MINSTEP(0x141)  // row_half_mirror
+  DGP_MINSTEP(0x140)  // row_mirror
+#undef DGP_MINSTEP
+  return (uint64_t)hi << 32 | lo;
+}
+
+template <bool LW>
+__device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r,
+                                                        int qmode, const uint4& E, int& woke) {
+  SCtl& S = L.c;
+  const int lane = lane_id();
+  // PRE's rows of this stimulus: in flight while the header is unpacked
+  const uint4* FRr = D.frow + (size_t)(r & (DR - 1)) * FRS;
+  const bool l16 = lane < TF;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  uint4 FJ[NFF];
+#pragma unroll
+  for (int j = 0; j < NFF; j++) FJ[j] = l16 ? FRr[j * TF + lane] : z4;
+  const DTab durv = stim_durations(D, L, E, r);
+  const int t = rl((int)E.x, 0), w = rl((int)E.y, 0), p = rl((int)E.z, 0);
+  const uint32_t flags = rlu(E.w, 0);
+  const int64_t nbt = mk64(rlu(E.x, 1), rlu(E.y, 1));
+  const unsigned cnts = rlu(E.z, 1);
+  const int kt = cnts & 0xff, nrel = (cnts >> 8) & 0xff, nf = (cnts >> 16) & 0xff;
+  const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
+  const int nt = rl((int)E.z, 2);
+  const int tot_new = rl((int)E.w, 2);  // the frontier's dependency count (prefetcher)
+  const int TD = E_HDR, RL0 = E_HDR + kt, FX0 = RL0 + nrel;
+  // the touched workers, one lane each (entry 0 = w); a candidate-only worker (WAITC) is read
+  // after the wait
+  const bool tl = lane < nt;
+  const int tv = tl ? (int)L.touch[s][lane] : 0;
+  const int cj = tv & T_W;
+  const bool candl = (tv & T_CAND) != 0;
+  const bool wc = WAITC && tl && lane > 0 && candl;
+  // ---- capacity check of the needs tables this stimulus may grow (as exe_local)
+  {
+    bool bad = false;
+    if (tl) {
+      const uint32_t ctl = P.needs[(size_t)cj * NLW + NLW - 1];
+      const int slack = wc ? NXW / 2 : 0;
+      bad = ctl == NL_OVF || (int)(ctl >> 8) + tot_new + slack > NLW - 1 + NXW;
+    }
+    if (ballot(bad)) return false;
+  }
+  OutR o;
+  o.init();
+  int np = 0, nth = 1;
+  WDict dj;
+  dj.c = z4;
+  dj.c1 = z4;
+  dj.ord = 0;
+  int64_t net = 0, nbj = 0;
+  if (tl) nth = P.nthreads[cj];  // static while stimuli run
+  if (tl && !wc) {
+    np = P.nproc[cj];
+    dj = dict_load<LW>(P, cj);
+    net = P.netocc[cj];
+    nbj = P.nbytes[cj];
+  }
+  const int capw = P.cap[w];
+  uint32_t nl = line_load<LW>(P, w);
+  if (nt < 1 || rl(cj, 0) != w) {
+    serr(S, SERR_INV, 700000000 + (int)r);
+    return true;
+  }
+  const bool isw = lane == 0;
+  double nbw = net_bw_of(net, D);
+  const bool nth1 = !ballot(tl && nth != 1);  // occ / 1.0 == occ: the division is skipped
+  // ------------------------------------------- completion: processing -> memory (:2366)
+  int64_t dnet = 0;
+  {
+    int64_t freed = 0;
+    if (needs_dec_all(E, TD, kt, w, nl, freed)) dnet = -freed;
+    else for (int i = 0; i < kt; i++) {  // _dec_needs_replica for the dependencies w needed
+      const int L_ = TD + i;
+      if (rl((int)E.y, L_) == w) continue;
+      dnet -= needs_dec(D, S, w, nl, rl((int)E.x, L_), mk64(rlu(E.z, L_), rlu(E.w, L_)), t);
+    }
+  }
+  const int npw = rl(np, 0) - 1;
+  if (npw == 0) needs_reset(D, w, nl);
+  line_store<LW>(P, w, nl);
+  if (isw) {
+    dict_add(dj, p, -1);
+    np = npw;
+    net += dnet;
+  }
+  if (dnet != 0) nbw = net_bw_of(net, D);  // dnet is uniform
+  double occj = occ_dict_r(dj, nbw, durv, D);
+  double stkj = nth1 ? occj : occj / (double)nth;
+  o.rec(K_COMPLETE, w, p, dnet, rl_f64(occj, 0), npw, t, dobs);
+  // add_replica (:3148), then the releases popped before the frontier (LIFO, :3309-3314):
+  // relsum = the released replicas' bytes this lane's worker holds
+  int64_t relsum = 0;
+  for (int i = 0; i < nrel; i++) {
+    const int h = rl((int)E.x, RL0 + i);
+    const int64_t nb = mk64(rlu(E.z, RL0 + i), rlu(E.w, RL0 + i));
+    if (cj == h) relsum += nb;
+  }
+  if (isw) nbj += (flags & F_SELFREL) ? 0 : nbt;
+  if (tl && !wc) nbj -= relsum;
+  // a release-only holder is final now: written back and released before the frontier
+  bool released = false;
+  {
+    const bool ro = tl && !isw && !candl;
+    if (ballot(ro)) {
+      if (ro) P.nbytes[cj] = nbj;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (ro) release_worker<LW>(L, P, s, cj);
+      released = ro;
+    }
+  }
+  bool exact = false;
+  if (WAITC && ballot(wc)) {
+    // the candidates: every earlier stimulus holding one has released it, then their state
+    if (vload(&L.predc[s]) != 0) {
+      if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(1);
+      while (vload(&L.predc[s]) != 0) __builtin_amdgcn_s_sleep(1);
+      if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(3);
+    }
+    lds_fence();
+    if (wc) {
+      np = P.nproc[cj];
+      dj = dict_load<LW>(P, cj);
+      net = P.netocc[cj];
+      nbj = P.nbytes[cj] - relsum;
+      nbw = net_bw_of(net, D);
+      occj = occ_dict_r(dj, nbw, durv, D);
+      stkj = nth1 ? occj : occj / (double)nth;
+    }
+    bool bad = false;  // the candidates' needs tables, exactly now
+    if (wc) {
+      const uint32_t ctl = P.needs[(size_t)cj * NLW + NLW - 1];
+      bad = ctl == NL_OVF || (int)(ctl >> 8) + tot_new > NLW - 1 + NXW;
+    }
+    if (ballot(bad)) {  // rare: continue as the oldest stimulus (every earlier one retired)
+      while (vload(&S.seq_pos) != r) __builtin_amdgcn_s_sleep(1);
+      lds_fence();
+      exact = true;
+    }
+  }
+  // ------------------------------ frontier in ascending priority: decide_worker (:8550)
+  int off = FX0;
+#pragma unroll 1
+  for (int j = 0; j < nf; j++) {
+    const uint4 FR = j == 0 ? FJ[0] : j == 1 ? FJ[1] : j == 2 ? FJ[2] : FJ[3];
+    const int x = rl((int)E.x, off), px = rl((int)E.y, off);
+    const int kx = rl((int)E.z, off) & 0xff;
+    const unsigned cmask = rlu(E.w, off);  // the candidates' touch indices (PRE)
+    // worker_objective (:3131-3146): start = occupancy / nthreads + comm_bytes / bandwidth,
+    // then (start, ws.nbytes, canonical index) minimal over the candidates
+    const bool cand = tl && ((cmask >> lane) & 1u);
+    const double cdv = cand ? mkd(FR.x, FR.y) : INFINITY;
+    const double start = stkj + cdv;
+    const uint64_t sk = cand ? start_key(start) : ~0ull;
+    const uint64_t mk = rl64(row_min_u64(sk), 0);
+    const unsigned long long eq = ballot(cand && sk == mk);
+    if (!eq) {
+      serr(S, SERR_CAND, x);
+      return true;
+    }
+    int jb = __builtin_ctzll(eq);
+    if (eq & (eq - 1)) {  // equal start times: ws.nbytes, then the worker index (key_less)
+      int64_t bn = rl_i64(nbj, jb);
+      int bw = rl(cj, jb);
+      for (unsigned long long m = eq & (eq - 1); m; m &= m - 1) {
+        const int q = __builtin_ctzll(m);
+        const int64_t nq = rl_i64(nbj, q);
+        const int wq = rl(cj, q);
+        if (nq < bn || (nq == bn && wq < bw)) {
+          jb = q;
+          bn = nq;
+          bw = wq;
+        }
+      }
+    }
+    const int cb = rl(cj, jb);
+    const double bstart = rl_f64(start, jb);
+    const int64_t bnb = rl_i64(nbj, jb);
+    const int64_t bcomm = mk64(rlu(FR.z, jb), rlu(FR.w, jb));
+    if (j == nf - 1 && nt > 2) {
+      // the last frontier decision is made: every touched worker but w and the chosen one
+      // is final now; written back and released before the commit
+      const bool early = tl && !isw && lane != jb && !released;
+      if (ballot(early)) {
+        if (early) {
+          using U4 = typename WPtr<LW>::template P<Q4>;
+          P.nproc[cj] = np;
+          st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
+          st4(ascast<U4>(P.pcnt + (size_t)cj * PD + 4), dj.c1);
+          P.plen[cj] = dj.ord;
+          P.netocc[cj] = net;
+          P.nbytes[cj] = nbj;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (early) release_worker<LW>(L, P, s, cj);
+        released = released || early;
+      }
+    }
+    // _add_to_processing (:3199): record, WorkerState.add_to_processing, check_idle_saturated
+    o.place(x, cb, bcomm, bstart, bnb, ROUTE_NONROOTISH);
+    uint32_t nlc = line_load<LW>(P, cb);
+    if (exact) __threadfence_block();
+    int64_t dn = 0;
+    if (!needs_inc_all(E, off + 1, kx, cb, nlc, dn)) for (int i = 0; i < kx; i++) {
+      const int L2 = off + 1 + i;
+      if (rl((int)E.y, L2) == cb) continue;
+      dn += needs_inc(D, S, cb, nlc, rl((int)E.x, L2), mk64(rlu(E.z, L2), rlu(E.w, L2)), x);
+    }
+    line_store<LW>(P, cb, nlc);
+    const bool isb = lane == jb;
+    bool okp = true;
+    if (isb) {
+      okp = dict_add(dj, px, +1);
+      np += 1;
+      net += dn;
+    }
+    if (dn != 0 && isb) nbw = net_bw_of(net, D);
+    if (ballot(!okp)) serr(S, SERR_PREFIX, x);
+    if (exact && lane == 0) {  // scan mode reads them for this stimulus' later decisions
+      D.proc_on[x] = cb;
+      D.state[x] = S_PROCESSING;
+    }
+    occj = occ_dict_r(dj, nbw, durv, D);
+    stkj = nth1 ? occj : occj / (double)nth;
+    o.rec(K_PLACE, cb, px, dn, rl_f64(occj, jb), rl(np, jb), x, 0.0);
+    off += 1 + kx;
+  }
+  // ---- every touched worker but w is final: written back and released
+  if (tl && !isw && !released) {
+    using U4 = typename WPtr<LW>::template P<Q4>;
+    P.nproc[cj] = np;
+    st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
+    st4(ascast<U4>(P.pcnt + (size_t)cj * PD + 4), dj.c1);
+    P.plen[cj] = dj.ord;
+    P.netocc[cj] = net;
+    P.nbytes[cj] = nbj;
+  }
+  if (nt > 1) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (tl && !isw && !released) release_worker<LW>(L, P, s, cj);
+  }
+  // -------------- stimulus_queue_slots_maybe_opened (:4983): only w can have open slots
+  int pops = 0;
+  if (qmode != 0 && !D.sat_inf) {
+    const int slots = capw - rl(np, 0);
+    if (slots > capw || o.npl + slots > PLC - 1) {
+      serr(S, SERR_INV, 600000000 + (int)r);
+      return true;
+    }
+    if (slots > 0) pops = slots;
+    const int qp = S.q_prefix;
+    const int64_t nbw0 = rl_i64(nbj, 0);
+    for (int i = 0; i < pops; i++) {
+      const double st = stkj + 0.0 / (double)D.bandwidth;
+      o.place(-1, w, 0, rl_f64(st, 0), nbw0, ROUTE_ROOTISH_Q);
+      bool okq = true;
+      if (isw) {
+        okq = dict_add(dj, qp, +1);
+        np += 1;
+      }
+      if (ballot(!okq)) serr(S, SERR_PREFIX, -1);
+      occj = occ_dict_r(dj, nbw, durv, D);
+      stkj = nth1 ? occj : occj / (double)nth;
+      o.rec(K_PLACE, w, qp, 0, rl_f64(occj, 0), rl(np, 0), -1, 0.0);
+    }
+  }
+  // ---- w written back last, then released
+  if (isw) {
+    using U4 = typename WPtr<LW>::template P<Q4>;
+    P.nproc[cj] = np;
+    st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
+    st4(ascast<U4>(P.pcnt + (size_t)cj * PD + 4), dj.c1);
+    P.plen[cj] = dj.ord;
+    P.netocc[cj] = net;
+    P.nbytes[cj] = nbj;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  int wk = -1;
+  if (isw) wk = release_worker<LW>(L, P, s, w);
+  woke = rl(wk, 0);
+  // ------------------------------------------------ outputs, then retire
+  o.flush(D, (size_t)(r & (RS - 1)) * PLC);
+  finish_slot(D, L, s, r, o, pops, false);
   return true;
 }
 
@@ -2545,6 +3230,19 @@ __device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, co
   return true;
 }
 
+// out of line, one register allocation each (inlined into the claim loop together they
+// spilled to scratch); -2: nothing changed (the stimulus goes back exact), else the slot the
+// release of w made ready (-1: none)
+template <bool LW>
+__device__ __attribute__((noinline)) int exe_fast_entry(int s, long long r, int qmode, uint4 E) {
+  int woke = -1;
+  return exe_fast<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r, qmode, E, woke) ? woke : -2;
+}
+template <bool LW>
+__device__ __attribute__((noinline)) int exe_local_entry(int s, long long r, int qmode, int exact, uint4 E) {
+  int woke = -1;
+  return exe_local<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r, qmode, exact != 0, E, woke) ? woke : -2;
+}
 template <bool LW>
 __device__ __attribute__((noinline)) bool exe_run_entry(int s, long long r, uint4 E) {
   return exe_run<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r, E);
@@ -3573,8 +4271,12 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       PROF(if (lane == 0) S.prof[9]++);
     } else if (G && (cf & F_SIMPLE) && cq == 0 && !cex && exe_run_entry<LW>(cs, cr, E)) {
       // a run of single-worker completions, back to back (only this executor calls out of line)
-    } else if (!exe_local<LW>(D, L, P, cs, cr, cq, cex, E, hint)) {
-      if (lane == 0) {
+    } else {
+      int rc = -2;
+      if (DGP_FAST && (cf & F_FAST) && !cex && cq <= 1) rc = exe_fast_entry<LW>(cs, cr, cq, E);  // the lean path
+      if (rc == -2) rc = exe_local_entry<LW>(cs, cr, cq, cex ? 1 : 0, E);
+      hint = rc >= 0 ? rc : -1;
+      if (rc == -2 && lane == 0) {
         atomicOr(&L.flags[cs], F_EXACT);
         atomicOr(&S.ready, 1ull << cs);
         PROF(S.prof[10]++);

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -111,6 +112,7 @@ struct dgp_engine {
   dgp::svc::Mbox* mb_dev = nullptr;  // device address
   bool resident = false;             // service calls go through the resident kernel
   bool res_running = false;          // the resident kernel was launched (it may have ended since)
+  bool res_hung = false;             // the resident kernel did not end when told to: the engine is unusable
   bool pending_resync = false;       // a later graph with dependencies on earlier tasks: dgp_sync_* next
   unsigned long long req_seq = 0;    // the last request number sent
   int64_t res_prof[4] = {0, 0, 0, 0};  // requests answered; sums of append, run, publish (device 100 MHz ticks)
@@ -225,6 +227,7 @@ int check_device_error(dgp_engine* e, dgp::Ctl* out = nullptr) {
 // Every entry point but dgp_tasks_finished calls this first: nothing else may touch the
 // engine's stream or device state while it runs.
 int resident_stop(dgp_engine* e) {
+  if (e && e->res_hung) return fail(e, DGP_E_DEVICE, "the resident kernel did not end: the engine is unusable");
   if (!e || !e->res_running) return 0;
   __atomic_store_n(&e->mb->stop, 1, __ATOMIC_RELEASE);
   const hipError_t st = hipStreamSynchronize(e->stream);
@@ -493,6 +496,7 @@ dgp_engine* dgp_create(int device) {
     rc |= dalloc(e, &e->D.dring, (size_t)S::DR * S::PX, e->allocs);
     rc |= dalloc(e, &e->D.touch_ring, (size_t)S::DR * S::TMAX, e->allocs);
     rc |= dalloc(e, &e->D.thdr, (size_t)S::DR, e->allocs);
+    rc |= dalloc(e, &e->D.frow, (size_t)S::DR * S::FRS, e->allocs);
     rc |= dalloc(e, &e->D.s2_task, st, e->allocs);
     rc |= dalloc(e, &e->D.s2_worker, st, e->allocs);
     rc |= dalloc(e, &e->D.s2_comm, st, e->allocs);
@@ -1041,7 +1045,7 @@ int tasks_finished_resident(dgp_engine* e, int64_t n, const int32_t* task, const
     const int64_t cap = std::max<int64_t>(n, 4096);
     void* p = nullptr;
     HIPCHK(e, hipHostMalloc(&p, V::mbox_bytes(cap, plc), hipHostMallocCoherent | hipHostMallocMapped));
-    memset(p, 0, 128);
+    memset(p, 0, sizeof(V::Mbox));  // the whole header (t_role included)
     e->mb = (V::Mbox*)p;
     e->mb->cap = cap;
     e->mb->pl_cap = plc;
@@ -1086,7 +1090,22 @@ int tasks_finished_resident(dgp_engine* e, int64_t n, const int32_t* task, const
         if (int rc = launch()) return rc;
       }
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
-        (void)resident_stop(e);
+        // told to stop, waited for a bounded time (a kernel stuck inside a request never
+        // reads the flag): never a blocking synchronisation here
+        __atomic_store_n(&e->mb->stop, 1, __ATOMIC_RELEASE);
+        const auto t1 = std::chrono::steady_clock::now();
+        hipError_t q = hipStreamQuery(e->stream);
+        while (q == hipErrorNotReady && std::chrono::steady_clock::now() - t1 < std::chrono::seconds(5)) {
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+          q = hipStreamQuery(e->stream);
+        }
+        if (q == hipErrorNotReady) {
+          e->res_hung = true;
+        } else {
+          __atomic_store_n(&e->mb->stop, 0, __ATOMIC_RELEASE);
+          e->res_running = false;
+          D.resident = 0;
+        }
         return fail(e, DGP_E_DEVICE, "dgp_tasks_finished: the resident kernel did not answer within 60 s");
       }
     }

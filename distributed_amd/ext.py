@@ -427,6 +427,9 @@ class GPUPlacementExtension(SchedulerPlugin):
         orig = st.move_task_confirm
 
         async def move_task_confirm(*, key, state, stimulus_id, worker=None):
+            # a stimulus of its own: a resync the previous one left pending runs first (the
+            # engine refuses a move while it waits for one)
+            self._enter()
             ts = s.tasks.get(key)
             before = ts.processing_on if ts is not None and ts.state == "processing" else None
             flags0 = self._flags_of(s)
@@ -451,6 +454,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         if bal is not None:
             @functools.wraps(bal)
             def balance(*args, **kwargs):
+                self._enter()  # a periodic callback: its own stimulus (a pending resync first)
                 flags0 = self._flags_of(s)
                 try:
                     return bal(*args, **kwargs)
@@ -897,6 +901,12 @@ class GPUPlacementExtension(SchedulerPlugin):
         if ts is None or ts.processing_on is None or ts.key not in self.task_index:
             return
         if ts in ts.processing_on.long_running:
+            # a repeated report: the reference still averages the prefix duration, takes the
+            # task out of the prefix counts again (add_to_long_running :747-757), then
+            # check_idle_saturated and the queue refill (:5838-5848) -- not modelled on the
+            # device: the scheduler decides this stimulus, then the engine takes its state
+            self._suspend(f"long-running reported again for {ts.key!r}")
+            self._mark_dirty(ts.key)
             return
         cd = kw.get("compute_duration")
         self._engine_op("long_running", self.task_index[ts.key], math.nan if cd is None else float(cd))

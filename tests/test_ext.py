@@ -223,6 +223,7 @@ def test_confirmed_steal_moves_the_task_on_the_engine():
     ext.task_index, ext.worker_index = {"x": 3}, {"tcp://w0": 0, "tcp://w1": 1}
     from collections import Counter, deque
     ext.stats, ext.pending = Counter(), deque()
+    ext.suspended, ext._window = False, None
     ext._wrap_stealing()
     assert sched.stream_handlers["steal-response"] is st.move_task_confirm  # wrapped once, both places
     asyncio.run(sched.stream_handlers["steal-response"](key="x", state="ready", stimulus_id="s1", worker="tcp://w0"))
