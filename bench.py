@@ -7,11 +7,12 @@ One step = one full replay of the workload on the device (update_graph + every
 completion round, ~1M placements), the graph already resident in HBM. For N GPUs
 (torch.distributed.run, one rank per GPU): the ordered replay does not
 partition (every decision reads the state the one before it left), so the placement legs
-run as replicas only — each rank one independent scheduler's replay of the workload (a
-cluster per GPU), outputs checked equal across ranks by an all-gather of digests — and
-value = the placements of all ranks / the slowest rank's time ("weak": the work per GPU is
-fixed). The data-parallel part of the WorkStealing leg — the per-task thief rows — is
-sharded over the ranks and all-gathered.
+run as independent schedulers, one per GPU: rank k replays its own C2-shaped graph (the
+generator's seed + k; rank 0's is the pinned workload), each rank checks its own replay
+bit-exact against the oracle, and value = the distinct placements all ranks made / the
+slowest rank's time ("weak": the work per GPU is fixed; per_rank_value beside it). The
+data-parallel part of the WorkStealing leg -- the per-task thief rows -- is sharded over
+the ranks and all-gathered.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--tasks N] [--workers W]
 """
@@ -60,6 +61,19 @@ def reduce_max(x: float, dist, device: str = "cuda") -> float:
         device = "cpu"
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def reduce_sum(x: float, dist, device: str = "cuda") -> float:
+    """The sum over ranks (the distinct work of independent per-GPU schedulers)."""
+    if dist is None:
+        return x
+    import torch
+
+    if dist.get_backend() == "gloo":
+        device = "cpu"
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
 
@@ -183,7 +197,8 @@ def variant_legs(eng_cls, local: int, args) -> dict:
     16 task prefixes (15 inner + root; _calc_occupancy sums 16 prefix terms per worker in
     dict order) and C3 with each unpack pinned to its output partition's worker (the
     shuffle plugin's restrict_task, shuffle/_scheduler_plugin.py:101-115, range sharding
-    _shuffle.py:612-617). One replay per step after a warm-up, best of 2, checked bit-exact
+    _shuffle.py:612-617). A step is reset + update_graph + the replay, as in the C2 / C3 legs
+(mean of 2 after a warm-up), checked bit-exact
     against the oracle, whose run is the CPU baseline (1 core)."""
     from distributed_amd import graphs
 
@@ -195,14 +210,16 @@ def variant_legs(eng_cls, local: int, args) -> dict:
              "C3 with restricted unpacks (restrict_task)")):
         eng = eng_cls(local)
         eng.load(g, CONFIG)
-        ts = []
-        for _ in range(3):
+        eng.reset()
+        eng.update_graph()
+        eng.run_rounds(-1)  # warm-up
+        n_step = 2  # a step as in the C2 / C3 legs: reset + update_graph + the replay
+        t0 = time.perf_counter()
+        for _ in range(n_step):
             eng.reset()
             eng.update_graph()
-            t0 = time.perf_counter()
             eng.run_rounds(-1)
-            ts.append(time.perf_counter() - t0)
-        dt = min(ts[1:])
+        dt = (time.perf_counter() - t0) / n_step
         out = eng.placements()
         eng.close()
         n = int(len(out["pl_task"]))
@@ -344,12 +361,13 @@ def service_leg(eng_cls, local: int, args) -> dict:
 
 def c5_leg(eng_cls, local: int, args, dist, barrier) -> dict:
     """BASELINE.json C5: the 10M-task map + tree-reduce (fan-in 8) DAG on 16,384 workers x 1
-    thread, one full replay per rank (replicas only, DESIGN.md §8: every rank replays its
-    own copy; value = all ranks' placements / the slowest rank's time). Pinned by
-    tests/golden/c5_full_digest.json."""
+    thread, one full replay per rank (one independent scheduler per GPU, rank
+    k replaying the generator's seed 3 + k; value = the placements all ranks made / the
+    slowest rank's time). Rank 0's graph is pinned by tests/golden/c5_full_digest.json."""
     from distributed_amd import graphs
 
-    g = graphs.map_tree_reduce(args.c5_map, args.c5_workers)
+    rank = int(os.environ.get("RANK", "0"))
+    g = graphs.map_tree_reduce(args.c5_map, args.c5_workers, seed=3 + rank)  # one scheduler per GPU
     eng = eng_cls(local)
     eng.load(g, CONFIG)
     barrier()
@@ -362,17 +380,15 @@ def c5_leg(eng_cls, local: int, args, dist, barrier) -> dict:
     out = eng.placements()
     n = int(len(out["pl_task"]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    n_all = reduce_sum(n, dist)
     leg = {"metric": "task placements/sec, C5 (10M-task map + tree-reduce, 16,384 workers)",
-           "value": round(n * world / dt, 1), "unit": "placements/s", "n_gpus": world, "scaling": "weak",
+           "value": round(n_all / dt, 1), "unit": "placements/s", "n_gpus": world, "scaling": "weak",
+           "per_rank_value": round(n / dt, 1),
            "seconds_per_replay": round(dt, 3), "placements_per_replay": n, "n_tasks": int(g["n_tasks"]),
            "n_workers": args.c5_workers,
-           "parallelism": f"replicas x{world} (one independent replay per GPU)" if world > 1 else "single"}
-    if dist is not None:
-        from distributed_amd.shard import output_digest, replicas_agree
-
-        leg["replicas_agree"] = replicas_agree(output_digest([out["pl_task"], out["pl_worker"]]), "cuda")
+           "parallelism": f"{world} independent schedulers (rank k: seed 3 + k)" if world > 1 else "single"}
     pin = os.path.join(REPO, "tests", "golden", "c5_full_digest.json")
-    if os.path.exists(pin):
+    if os.path.exists(pin) and rank == 0:  # rank 0 replays the pinned graph
         ref = json.load(open(pin))
         if ref["n_map"] == args.c5_map and ref["n_workers"] == args.c5_workers:
             leg["parity"] = graphs.placement_digest(out) == ref["digest"]
@@ -437,7 +453,7 @@ def main():
     from distributed_amd import graphs
     from distributed_amd.engine import PlacementEngine
 
-    g = graphs.random_dag(args.tasks, args.workers, seed=0)
+    g = graphs.random_dag(args.tasks, args.workers, seed=rank)  # one scheduler per GPU, its own graph
     eng = PlacementEngine(local)
     eng.load(g, CONFIG)
 
@@ -474,15 +490,19 @@ def main():
     eng.set_timing(False)
     placements = eng.num_placements()
     elapsed = reduce_max(elapsed, dist)
-    total_placements = placements * args.steps * world  # every rank replays its own copy (replicas)
+    total_placements = reduce_sum(placements, dist) * args.steps  # the distinct work of all ranks
     value = total_placements / elapsed
 
     out = eng.placements()
     agree = None
-    if dist is not None:
-        from distributed_amd.shard import output_digest, replicas_agree
+    if dist is not None and not args.no_cpu_baseline:
+        # every rank checks its own replay against the oracle (its own graph); all must agree
+        from oracle import oracle
 
-        agree = replicas_agree(output_digest([out["pl_task"], out["pl_worker"], out["pl_start"]]), "cuda")
+        ref = oracle.replay(g, CONFIG, snapshots=False)
+        ok = all(np.array_equal(out[k], ref[k]) for k in ("pl_task", "pl_worker", "pl_comm", "pl_start",
+                                                           "pl_wsnbytes", "pl_route"))
+        agree = reduce_sum(1.0 if ok else 0.0, dist) == world
     steal = None
     if not args.no_steal:  # every rank takes part (sharded thief rows)
         steal = steal_leg(eng, args, world, dist, barrier)
@@ -495,9 +515,11 @@ def main():
         "config": {"workload": "C2: random DAG, fan-in<=4 (window 4W), lognormal(10,2) nbytes, roots N/10, "
                                "workers x 1 thread, worker-saturation 1.1; full replay per step",
                    "n_tasks": args.tasks, "n_workers": args.workers,
-                   "parallelism": f"replicas x{world} (one independent replay per GPU)" if world > 1 else "single",
-                   "placements_per_step": placements},
+                   "parallelism": f"{world} independent schedulers, one per GPU (rank k: seed k)" if world > 1
+                   else "single", "placements_per_step": placements},
     }
+    if world > 1:
+        result["per_rank_value"] = round(placements * args.steps / elapsed, 1)
     if rank == 0:
         n_waves = eng.stats()["rounds"]
         # bytes of the placements each kernel makes: update_graph's initial wave, then the replay
@@ -555,7 +577,7 @@ def main():
             result["parity"] = bool(all(np.array_equal(out[k], ref[k]) for k in (
                 "pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")))
         if agree is not None:
-            result["replicas_agree"] = agree
+            result["parity_all_ranks"] = agree
         if steal is not None:
             result["steal"] = steal
     eng.close()

@@ -26,6 +26,8 @@ SIGNATURES = {
     "dgp_set_graph": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P]),
     "dgp_set_task_results": (C.c_int, [_P, _P, _P, _P]),
     "dgp_set_restrictions": (C.c_int, [_P, _P, _P, _P]),
+    "dgp_update_restrictions": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P]),
+    "dgp_set_rootish": (C.c_int, [_P, C.c_int64, _P, _P]),
     "dgp_reset": (C.c_int, [_P]),
     "dgp_update_graph": (C.c_int, [_P]),
     "dgp_run_rounds": (C.c_int, [_P, C.c_int64, _P]),
@@ -34,6 +36,7 @@ SIGNATURES = {
     "dgp_move_task": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "dgp_add_worker": (C.c_int, [_P, C.c_int32, _P]),
     "dgp_add_graph": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P, _P]),
+    "dgp_add_graph_deferred": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P]),
     "dgp_snapshot": (C.c_int, [_P]),
     "dgp_num_placements": (C.c_int64, [_P]),
     "dgp_get_placements": (C.c_int, [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, _P]),
@@ -72,7 +75,7 @@ SIGNATURES = {
                                    _P, _P, _P]),
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 _lib = None
 
 

@@ -149,6 +149,11 @@ struct Dev {
   const int64_t* restr_ptr;
   const int32_t* restr_idx;
   const uint8_t* restr_flags;
+  // restrictions changed after the upload (dgp_update_restrictions: Scheduler.set_restrictions,
+  // the shuffle's restrict_task): restr_ovr[t] >= 0 is task t's row in restr_pool (its length,
+  // then its valid workers ascending) in place of the CSR row; null: none changed
+  const int64_t* restr_ovr;
+  const int32_t* restr_pool;
   int64_t* cand_off;
   int32_t* cand_n;
   int32_t* pool_w;
@@ -326,6 +331,18 @@ __device__ __forceinline__ bool holds(const Dev& D, int d, int w) {
 __device__ __forceinline__ bool holds_any(const Dev& D, int d, int w) {
   if ((D.evf & EVF_MULTI) && (D.tdyn[d] & TD_MULTI)) return holds(D, d, w);
   return D.holder_of[d] == w;
+}
+// task x's valid workers (valid_workers :3043-3107 resolved on the host): idx[r0 .. r1)
+struct RRow {
+  const int32_t* idx;
+  int64_t r0, r1;
+};
+__device__ __forceinline__ RRow restr_row(const Dev& D, int x) {
+  if (D.restr_ovr) {
+    const int64_t o = D.restr_ovr[x];
+    if (o >= 0) return RRow{D.restr_pool, o + 1, o + 1 + D.restr_pool[o]};
+  }
+  return RRow{D.restr_idx, D.restr_ptr[x], D.restr_ptr[x + 1]};
 }
 // restricted and placed by decide_worker_non_rootish (a `_rootish` override wins, :2937)
 __device__ __forceinline__ bool restricted_nonrootish(const Dev& D, int x) {
@@ -1544,7 +1561,8 @@ __device__ __attribute__((noinline)) void dispatch_collective(const Dev& D, Coop
     // that is empty too, the loose retry without restrictions (:8584-8586) or None ->
     // no-worker (:2761-2782). The argmin of worker_objective decides (a single candidate
     // is its own argmin).
-    const int64_t r0 = D.restr_ptr[x], r1 = D.restr_ptr[x + 1];
+    const RRow rr = restr_row(D, x);
+    const int64_t r0 = rr.r0, r1 = rr.r1;
     const int64_t d0 = D.dep_ptr[x], d1 = D.dep_ptr[x + 1];
     auto held = [&](int w) {
       for (int64_t k = d0; k < d1; k++)
@@ -1555,7 +1573,7 @@ __device__ __attribute__((noinline)) void dispatch_collective(const Dev& D, Coop
     for (int64_t i0 = r0; i0 < r1; i0 += blockDim.x) {
       const int64_t i = i0 + threadIdx.x;
       int64_t t1;
-      block_excl_scan(i < r1 && held(D.restr_idx[i]) ? 1 : 0, &t1);
+      block_excl_scan(i < r1 && held(rr.idx[i]) ? 1 : 0, &t1);
       tot += t1;
     }
     // 0: valid & holders, 1: valid, 2: holders (loose), 3: every worker (loose), 4: none
@@ -1584,7 +1602,7 @@ __device__ __attribute__((noinline)) void dispatch_collective(const Dev& D, Coop
     };
     if (mode <= 1) {
       for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
-        const int w = D.restr_idx[i];
+        const int w = rr.idx[i];
         if (mode == 1 || held(w)) consider(w);
       }
     } else if (mode <= 3) {

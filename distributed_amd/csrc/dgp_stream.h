@@ -479,6 +479,65 @@ __device__ __forceinline__ bool dict_add(WDict& d, int p, int delta) {
   return true;
 }
 
+// add_to_processing (+1) / remove_from_processing (-1) of prefix p on lane j's dict only
+// (uniform j): lane j's slots read once, the insertion-ordered update (dict_add's) on
+// scalar registers, the slots written back to lane j (one select each)
+__device__ __forceinline__ bool dict_add_lane(WDict& d, int j, int p, int delta) {
+  uint32_t sl[PD] = {rlu(d.c.x, j), rlu(d.c.y, j), rlu(d.c.z, j), rlu(d.c.w, j),
+                     rlu(d.c1.x, j), rlu(d.c1.y, j), rlu(d.c1.z, j), rlu(d.c1.w, j)};
+  uint32_t ord = rlu(d.ord, j);
+  const uint32_t n = ord >> 24;
+  int k = -1;
+#pragma unroll
+  for (int i = 0; i < PD; i++)
+    if ((uint32_t)i < n && (sl[i] >> 24) == (uint32_t)p) k = i;
+  bool ok = true;
+  if (delta > 0) {
+    if (k >= 0) {
+#pragma unroll
+      for (int i = 0; i < PD; i++)
+        if (i == k) {
+          if ((sl[i] & 0xffffffu) == 0xffffffu) ok = false;
+          else sl[i] += 1u;
+        }
+    } else if (n >= (uint32_t)PD || p < 0 || p > 255) {
+      ok = false;
+    } else {
+#pragma unroll
+      for (int i = 0; i < PD; i++)
+        if (i == (int)n) sl[i] = ((uint32_t)p << 24) | 1u;  // new key: appended
+      ord += 1u << 24;
+    }
+  } else if (k >= 0) {
+    uint32_t ck = 0;
+#pragma unroll
+    for (int i = 0; i < PD; i++)
+      if (i == k) ck = sl[i] & 0xffffffu;
+    if (ck > 1u) {
+#pragma unroll
+      for (int i = 0; i < PD; i++)
+        if (i == k) sl[i] -= 1u;
+    } else {  // count reached zero: the key leaves, later keys move up
+#pragma unroll
+      for (int i = 0; i < PD - 1; i++)
+        if (i >= k) sl[i] = sl[i + 1];
+      sl[PD - 1] = 0u;
+      ord -= 1u << 24;
+    }
+  }
+  const bool lj = lane_id() == j;
+  d.c.x = lj ? sl[0] : d.c.x;
+  d.c.y = lj ? sl[1] : d.c.y;
+  d.c.z = lj ? sl[2] : d.c.z;
+  d.c.w = lj ? sl[3] : d.c.w;
+  d.c1.x = lj ? sl[4] : d.c1.x;
+  d.c1.y = lj ? sl[5] : d.c1.y;
+  d.c1.z = lj ? sl[6] : d.c1.z;
+  d.c1.w = lj ? sl[7] : d.c1.w;
+  d.ord = lj ? ord : d.ord;
+  return ok;
+}
+
 // prefix durations: a table of PX doubles in LDS (a descriptor's entries 3..6 or a D.dring
 // row, or the walker's wdur), read by prefix id
 using DTab = const __attribute__((address_space(3))) double*;
@@ -528,8 +587,18 @@ __device__ __forceinline__ double occ_dict_r(const WDict& d, double net_bw, DTab
     }
     return res + net_bw;
   }
+  // the first two entries' duration loads issued together (most workers hold at most two
+  // prefixes), then the rest one at a time; the same fp64 operations in dict order
+  {
+    const uint32_t v0 = d.c.x, v1 = d.c.y;
+    const double dv0 = dt[(v0 >> 24) & (PX - 1)], dv1 = dt[(v1 >> 24) & (PX - 1)];
+    const double t0 = (dv0 < 0 ? D.unknown_duration : dv0) * (double)(v0 & 0xffffffu);
+    const double t1 = (dv1 < 0 ? D.unknown_duration : dv1) * (double)(v1 & 0xffffffu);
+    if (n > 0u) res += t0;
+    if (n > 1u) res += t1;
+  }
 #pragma unroll
-  for (int i = 0; i < PD; i++) {
+  for (int i = 2; i < PD; i++) {
     if (!ballot((uint32_t)i < n)) break;
     const uint32_t v = wd_slot(d, i);
     const double dv = dt[(v >> 24) & (PX - 1)];
@@ -577,13 +646,14 @@ __device__ __forceinline__ bool stalled_for(unsigned long long since, unsigned l
 __device__ __forceinline__ int64_t nbv(const Dev& D, int64_t v) { return v >= 0 ? v : D.default_data_size; }
 // w in valid_workers(ts) (:3043-3107) as resolved on the host: task x's restriction row (ascending)
 __device__ __forceinline__ bool restr_has(const Dev& D, int x, int w) {
-  int64_t lo = D.restr_ptr[x], hi = D.restr_ptr[x + 1];
+  const RRow rr = restr_row(D, x);
+  int64_t lo = rr.r0, hi = rr.r1;
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (D.restr_idx[mid] < w) lo = mid + 1;
+    if (rr.idx[mid] < w) lo = mid + 1;
     else hi = mid;
   }
-  return lo < D.restr_ptr[x + 1] && D.restr_idx[lo] == w;
+  return lo < rr.r1 && rr.idx[lo] == w;
 }
 
 // ============================================================ walker (records -> flags)
@@ -1358,10 +1428,11 @@ __device__ __attribute__((always_inline)) void build_desc_seq(const Dev& D, SLds
         for (int i = 0; i < nc; i++) dup = dup || cw[i] == hd;
         if (!dup && hd >= 0 && hd < D.W && restr_has(D, x, hd)) cw[nc++] = hd;
       }
-      const int64_t r0 = D.restr_ptr[x], r1 = D.restr_ptr[x + 1];
+      const RRow rr = restr_row(D, x);
+      const int64_t r0 = rr.r0, r1 = rr.r1;
       if (nc == 0 && r1 > r0) {
         if (r1 - r0 > RC_MAX) nc = -1;
-        else for (int64_t i = r0; i < r1; i++) cw[nc++] = D.restr_idx[i];
+        else for (int64_t i = r0; i < r1; i++) cw[nc++] = rr.idx[i];
       } else if (nc == 0) {
         if (!(D.restr_flags[x] & RF_LOOSE)) nc = -1;  // no-worker
         else for (int64_t q = x0; q < x1; q++) {       // decide_worker without restrictions
@@ -1694,8 +1765,12 @@ template <int KIND>  // 0 BLD, 1 PRE
 __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L) {
   SCtl& S = L.c;
   const int lane = lane_id();
-  // PRE: lane p holds TaskPrefix.duration_average of prefix p as of pre_pos
+  // PRE: lane p holds TaskPrefix.duration_average of prefix p as of pre_pos, and its
+  // max_exec_time (heartbeats change it only between launches): no load in the fold loop,
+  // whose stores would otherwise each be waited for before the next iteration's load
   double dur = (KIND == 1 && lane < PX && lane < D.P) ? D.pdur_pre[lane] : -1.0;
+  const double pmx = (KIND == 1 && lane < PX && lane < D.P) ? D.pmaxexec[lane] : -1.0;
+  auto resolve = [&](double d) { return d < 0 ? (pmx > 0 ? 2 * pmx : D.unknown_duration) : d; };  // :1892-1899
   while (true) {
     if (vload(&S.stop)) break;
     const long long a = KIND == 0 ? S.bld_pos : S.pre_pos;
@@ -1725,9 +1800,9 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
         const double di = mkd(rlu(dlo(dl), i), rlu(dhi(dl), i));
         if (lane == pi && di == di) dur = dur < 0 ? di : 0.5 * di + 0.5 * dur;  // NaN: no compute interval
         if (D.P <= PD) {
-          if (lane < PD) ((double*)(D.desc + (size_t)((a + i) & (DR - 1)) * NE + 3))[lane] = lane < D.P ? resolve_dur(D, dur, lane) : -1.0;
+          if (lane < PD) ((double*)(D.desc + (size_t)((a + i) & (DR - 1)) * NE + 3))[lane] = lane < D.P ? resolve(dur) : -1.0;
         } else if (lane < D.P) {
-          D.dring[(size_t)((a + i) & (DR - 1)) * PX + lane] = resolve_dur(D, dur, lane);
+          D.dring[(size_t)((a + i) & (DR - 1)) * PX + lane] = resolve(dur);
         }
       }
     }
@@ -2076,29 +2151,33 @@ __device__ __attribute__((always_inline)) int64_t needs_inc(const Dev& D, SCtl& 
 // takes the one-at-a-time path (needs_dec / needs_inc).
 // _dec_needs_replica (:815-823) for the dependencies in entries L0.. of E not held by c;
 // freed = the bytes c no longer needs.
+// lane masks of a comparison over the (active) lanes: one v_cmp into an SGPR pair
+__device__ __forceinline__ unsigned long long lm_eq(unsigned a, unsigned b) { return __builtin_amdgcn_uicmp(a, b, 32); }
+__device__ __forceinline__ unsigned long long lm_ne(unsigned a, unsigned b) { return __builtin_amdgcn_uicmp(a, b, 33); }
+__device__ __forceinline__ bool lm_has(unsigned long long m) { return (m >> lane_id()) & 1ull; }
+constexpr unsigned long long NL_LINE = (1ull << (NLW - 1)) - 1;  // the line's entry lanes
+
 __device__ __forceinline__ bool needs_dec_all(const uint4& E, int L0, int k, int c, uint32_t& nl, int64_t& freed) {
-  const int lane = lane_id();
   const uint32_t ctl = rlu(nl, NLW - 1);
-  if (ctl == NL_OVF || (int)(ctl >> 8) != line_used(nl)) return false;
-  const bool ent = lane < NLW - 1 && nl != 0;
-  bool hit = false, ok = true;
+  const unsigned long long used = lm_ne(nl, 0u) & NL_LINE;
+  if (ctl == NL_OVF || (int)(ctl >> 8) != __builtin_popcountll(used)) return false;
+  const uint32_t key = nl >> 8;
+  const unsigned long long one = lm_eq(nl & 0xffu, 1u) & used;  // entries this decrement empties
+  unsigned long long hit = 0;
   int64_t fr = 0;
   int ngone = 0;
   for (int i = 0; i < k; i++) {
-    const int h = rl((int)E.y, L0 + i);
-    if (h == c) continue;
-    const uint32_t d = (uint32_t)rl((int)E.x, L0 + i);
-    const bool mt = ent && (nl >> 8) == d;
-    ok = ok && ballot(mt) != 0;
-    if (ballot(mt && (nl & 0xffu) == 1u)) {
+    if (rl((int)E.y, L0 + i) == c) continue;  // held by c: never needed
+    const unsigned long long m = lm_eq(key, rlu(E.x, L0 + i)) & used;
+    if (!m) return false;  // not in the line (overflow / replica events): the general path
+    hit |= m;
+    if (m & one) {
       fr += mk64(rlu(E.z, L0 + i), rlu(E.w, L0 + i));
       ngone++;
     }
-    hit = hit || mt;
   }
-  if (!ok) return false;
-  if (hit) nl = (nl & 0xffu) == 1u ? 0u : nl - 1u;
-  if (lane == NLW - 1) nl -= (uint32_t)ngone << 8;
+  if (hit) nl = lm_has(hit & one) ? 0u : (lm_has(hit) ? nl - 1u : nl);
+  if (ngone) nl = lane_id() == NLW - 1 ? nl - ((uint32_t)ngone << 8) : nl;
   freed = fr;
   return true;
 }
@@ -2106,36 +2185,34 @@ __device__ __forceinline__ bool needs_dec_all(const uint4& E, int L0, int k, int
 // _inc_needs_replica (:800-813) for the dependencies in entries L0.. of E not held by c
 // (task placed on c); added = the bytes c newly needs.
 __device__ __forceinline__ bool needs_inc_all(const uint4& E, int L0, int k, int c, uint32_t& nl, int64_t& added) {
-  const int lane = lane_id();
   const uint32_t ctl = rlu(nl, NLW - 1);
-  if (ctl == NL_OVF || (int)(ctl >> 8) != line_used(nl)) return false;
-  const bool ent = lane < NLW - 1 && nl != 0;
-  unsigned long long em = ballot(lane < NLW - 1 && nl == 0);  // free entries
+  const unsigned long long used = lm_ne(nl, 0u) & NL_LINE;
+  if (ctl == NL_OVF || (int)(ctl >> 8) != __builtin_popcountll(used)) return false;
+  const uint32_t key = nl >> 8;
+  const unsigned long long full = lm_eq(nl & 0xffu, 0xffu) & used;
+  unsigned long long freem = ~used & NL_LINE;
+  unsigned long long hit = 0;
   uint32_t nn = nl;
-  bool hit = false, ok = true;
   int64_t ad = 0;
   int nins = 0;
   for (int i = 0; i < k; i++) {
-    const int h = rl((int)E.y, L0 + i);
-    if (h == c) continue;
-    const uint32_t d = (uint32_t)rl((int)E.x, L0 + i);
-    const bool mt = ent && (nl >> 8) == d;  // against the line as loaded: inserted entries hold other tasks
-    if (ballot(mt)) {
-      ok = ok && !ballot(mt && (nl & 0xffu) == 0xffu);
-      hit = hit || mt;
-    } else if (em) {
-      const int l = __builtin_ctzll(em);
-      em &= em - 1;
-      if (lane == l) nn = (d << 8) | 1u;
+    if (rl((int)E.y, L0 + i) == c) continue;
+    const uint32_t d = rlu(E.x, L0 + i);
+    const unsigned long long m = lm_eq(key, d) & used;  // against the line as loaded (deps are distinct)
+    if (m) {
+      if (m & full) return false;
+      hit |= m;
+    } else {
+      if (!freem) return false;  // the line is full: the general path (overflow entries)
+      const int l = __builtin_ctzll(freem);
+      freem &= freem - 1;
+      nn = lane_id() == l ? (d << 8) | 1u : nn;
       ad += mk64(rlu(E.z, L0 + i), rlu(E.w, L0 + i));
       nins++;
-    } else {
-      ok = false;
     }
   }
-  if (!ok) return false;
-  if (hit) nn += 1u;
-  if (lane == NLW - 1) nn += (uint32_t)nins << 8;
+  if (hit) nn = lm_has(hit) ? nn + 1u : nn;
+  if (nins) nn = lane_id() == NLW - 1 ? nn + ((uint32_t)nins << 8) : nn;
   nl = nn;
   added = ad;
   return true;
@@ -2795,6 +2872,16 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
                                                         int qmode, const uint4& E, int& woke) {
   SCtl& S = L.c;
   const int lane = lane_id();
+#if DGP_PHASE_PROBES  // the same phase slots as exe_local's
+  unsigned long long tph = mclk();
+  auto phase = [&](int k) {
+    const unsigned long long n = mclk();
+    PROF(if (lane == 0) atomicAdd(&S.prof[k], n - tph));
+    tph = n;
+  };
+#else
+  auto phase = [](int) {};
+#endif
   // PRE's rows of this stimulus: in flight while the header is unpacked
   const uint4* FRr = D.frow + (size_t)(r & (DR - 1)) * FRS;
   const bool l16 = lane < TF;
@@ -2829,6 +2916,7 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
     }
     if (ballot(bad)) return false;
   }
+  phase(11);
   OutR o;
   o.init();
   int np = 0, nth = 1;
@@ -2853,6 +2941,7 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
   const bool isw = lane == 0;
   double nbw = net_bw_of(net, D);
   const bool nth1 = !ballot(tl && nth != 1);  // occ / 1.0 == occ: the division is skipped
+  phase(16);
   // ------------------------------------------- completion: processing -> memory (:2366)
   int64_t dnet = 0;
   {
@@ -2867,12 +2956,13 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
   const int npw = rl(np, 0) - 1;
   if (npw == 0) needs_reset(D, w, nl);
   line_store<LW>(P, w, nl);
+  dict_add_lane(dj, 0, p, -1);
   if (isw) {
-    dict_add(dj, p, -1);
     np = npw;
     net += dnet;
   }
   if (dnet != 0) nbw = net_bw_of(net, D);  // dnet is uniform
+  phase(17);
   double occj = occ_dict_r(dj, nbw, durv, D);
   double stkj = nth1 ? occj : occj / (double)nth;
   o.rec(K_COMPLETE, w, p, dnet, rl_f64(occj, 0), npw, t, dobs);
@@ -2927,6 +3017,7 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
       exact = true;
     }
   }
+  phase(12);
   // ------------------------------ frontier in ascending priority: decide_worker (:8550)
   int off = FX0;
 #pragma unroll 1
@@ -2940,6 +3031,7 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
     const bool cand = tl && ((cmask >> lane) & 1u);
     const double cdv = cand ? mkd(FR.x, FR.y) : INFINITY;
     const double start = stkj + cdv;
+    phase(18);
     const uint64_t sk = cand ? start_key(start) : ~0ull;
     const uint64_t mk = rl64(row_min_u64(sk), 0);
     const unsigned long long eq = ballot(cand && sk == mk);
@@ -2986,6 +3078,7 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
         released = released || early;
       }
     }
+    phase(19);
     // _add_to_processing (:3199): record, WorkerState.add_to_processing, check_idle_saturated
     o.place(x, cb, bcomm, bstart, bnb, ROUTE_NONROOTISH);
     uint32_t nlc = line_load<LW>(P, cb);
@@ -2998,14 +3091,13 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
     }
     line_store<LW>(P, cb, nlc);
     const bool isb = lane == jb;
-    bool okp = true;
+    const bool okp = dict_add_lane(dj, jb, px, +1);
     if (isb) {
-      okp = dict_add(dj, px, +1);
       np += 1;
       net += dn;
     }
     if (dn != 0 && isb) nbw = net_bw_of(net, D);
-    if (ballot(!okp)) serr(S, SERR_PREFIX, x);
+    if (!okp) serr(S, SERR_PREFIX, x);
     if (exact && lane == 0) {  // scan mode reads them for this stimulus' later decisions
       D.proc_on[x] = cb;
       D.state[x] = S_PROCESSING;
@@ -3014,6 +3106,7 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
     stkj = nth1 ? occj : occj / (double)nth;
     o.rec(K_PLACE, cb, px, dn, rl_f64(occj, jb), rl(np, jb), x, 0.0);
     off += 1 + kx;
+    phase(20);
   }
   // ---- every touched worker but w is final: written back and released
   if (tl && !isw && !released) {
@@ -3044,12 +3137,8 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
     for (int i = 0; i < pops; i++) {
       const double st = stkj + 0.0 / (double)D.bandwidth;
       o.place(-1, w, 0, rl_f64(st, 0), nbw0, ROUTE_ROOTISH_Q);
-      bool okq = true;
-      if (isw) {
-        okq = dict_add(dj, qp, +1);
-        np += 1;
-      }
-      if (ballot(!okq)) serr(S, SERR_PREFIX, -1);
+      if (!dict_add_lane(dj, 0, qp, +1)) serr(S, SERR_PREFIX, -1);
+      if (isw) np += 1;
       occj = occ_dict_r(dj, nbw, durv, D);
       stkj = nth1 ? occj : occj / (double)nth;
       o.rec(K_PLACE, w, qp, 0, rl_f64(occj, 0), rl(np, 0), -1, 0.0);
@@ -3070,9 +3159,11 @@ __device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, c
   int wk = -1;
   if (isw) wk = release_worker<LW>(L, P, s, w);
   woke = rl(wk, 0);
+  phase(13);
   // ------------------------------------------------ outputs, then retire
   o.flush(D, (size_t)(r & (RS - 1)) * PLC);
   finish_slot(D, L, s, r, o, pops, false);
+  phase(15);
   return true;
 }
 
@@ -3773,10 +3864,11 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
        h1l = D.holder_of[d1];
        // a replica set or a paused holder: decide_worker's general form below
        if (((D.evf & EVF_MULTI) && (D.tdyn[d1] & TD_MULTI)) || (h1l >= 0 && h1l < D.W && paused(h1l))) h1l = -1;
-     } else if (e - a == 1 && restricted_nonrootish(D, xl) && D.restr_ptr[xl + 1] - D.restr_ptr[xl] == 1) {
+     } else if (e - a == 1 && restricted_nonrootish(D, xl) && restr_row(D, xl).r1 - restr_row(D, xl).r0 == 1) {
        const int d1 = D.dep_idx[a];
        if (!((D.evf & EVF_MULTI) && (D.tdyn[d1] & TD_MULTI))) {
-         rcl = D.restr_idx[D.restr_ptr[xl]];
+         const RRow rr = restr_row(D, xl);
+         rcl = rr.idx[rr.r0];
          rdl = d1;
          rhl = D.holder_of[d1] == rcl;
          rcml = rhl ? 0 : nbv(D, D.res_nbytes[d1]);
@@ -3812,7 +3904,8 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       // decide_worker (:8550-8593) with valid = valid_workers(ts) & running: candidates =
       // holders & valid; none: valid; valid empty: loose -> decide_worker without
       // restrictions (holders, else every running worker), else None -> no-worker
-      const int64_t r0 = D.restr_ptr[x], r1 = D.restr_ptr[x + 1];
+      const RRow rr = restr_row(D, x);
+      const int64_t r0 = rr.r0, r1 = rr.r1;
       auto held = [&](int cw) {
         for (int64_t q = D.dep_ptr[x]; q < D.dep_ptr[x + 1]; q++)
           if (holds_any(D, D.dep_idx[q], cw)) return true;
@@ -3820,7 +3913,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       };
       bool hv = false, av = false;
       for (int64_t i = r0 + lane; i < r1; i += 64) {
-        const int cw = D.restr_idx[i];
+        const int cw = rr.idx[i];
         if (paused(cw)) continue;
         av = true;
         hv = hv || held(cw);
@@ -3828,7 +3921,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       int mode = ballot(hv) ? 0 : ballot(av) ? 1 : (D.restr_flags[x] & RF_LOOSE) ? 2 : 4;
       Key b{INFINITY, INT64_MAX, INT32_MAX, 0};
       if (mode <= 1 && r1 - r0 <= 64) {  // the candidates are in the restriction row: one lane each
-        const int cw = lane < r1 - r0 ? D.restr_idx[r0 + lane] : 0;
+        const int cw = lane < r1 - r0 ? rr.idx[r0 + lane] : 0;
         const bool in = lane < r1 - r0 && !paused(cw) && (mode == 1 || held(cw));
         const double ocw = occ_of<LW>(P, D, cw, durv);
         if (in) {
@@ -4273,7 +4366,10 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       // a run of single-worker completions, back to back (only this executor calls out of line)
     } else {
       int rc = -2;
-      if (DGP_FAST && (cf & F_FAST) && !cex && cq <= 1) rc = exe_fast_entry<LW>(cs, cr, cq, E);  // the lean path
+      if (DGP_FAST && (cf & F_FAST) && !cex && cq <= 1) {  // the lean path (inlined: the common case)
+        int wk = -1;
+        rc = exe_fast<LW>(D, L, P, cs, cr, cq, E, wk) ? wk : -2;
+      }
       if (rc == -2) rc = exe_local_entry<LW>(cs, cr, cq, cex ? 1 : 0, E);
       hint = rc >= 0 ? rc : -1;
       if (rc == -2 && lane == 0) {

@@ -99,6 +99,7 @@ struct dgp_engine {
   std::vector<int64_t> gdep_n, gdep_len;   // per group: len(tg.dependencies), sum of their lengths
   std::vector<int8_t> rootish_override_h;  // TaskState._rootish per task (-1: None)
   std::vector<uint8_t> restr_h;            // restriction flags per task (empty: none)
+  int64_t rpool_used = 0, rpool_cap = 0;    // dgp_update_restrictions' row pool on the device (int32s)
   std::vector<uint8_t> paused_h;           // per worker: 0 running, 1 paused, 2 removed
   int64_t log_min[3] = {0, 0, 0};          // minimum capacities of the placement / stimulus / record logs
   int64_t sv_used = 0;                     // service stimuli appended (accepted task-finished messages)
@@ -808,6 +809,9 @@ int upload_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const i
   D.restr_ptr = nullptr;  // no restrictions until dgp_set_restrictions
   D.restr_idx = nullptr;
   D.restr_flags = nullptr;
+  D.restr_ovr = nullptr;
+  D.restr_pool = nullptr;
+  e->rpool_used = e->rpool_cap = 0;
   e->restr_h.clear();
   return 0;
 }
@@ -877,9 +881,150 @@ int dgp_set_restrictions(dgp_engine* e, const int64_t* restr_ptr, const int32_t*
   D.restr_ptr = rp;
   D.restr_idx = ri;
   D.restr_flags = rf;
+  D.restr_ovr = nullptr;  // the new rows replace every earlier update
+  D.restr_pool = nullptr;
+  e->rpool_used = e->rpool_cap = 0;
   if (flags) e->restr_h.assign(flags, flags + N);
   else e->restr_h.clear();
   return dgp_reset(e);
+}
+
+namespace {
+__global__ void k_restr_scatter(int64_t* ovr, uint8_t* rf, const int32_t* task, const int64_t* off, const uint8_t* fl,
+                                int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    ovr[task[i]] = off[i];
+    rf[task[i]] = fl[i];
+  }
+}
+}  // namespace
+
+int dgp_update_restrictions(dgp_engine* e, int64_t n, const int32_t* task, const int64_t* row_ptr,
+                            const int32_t* row_idx, const uint8_t* flags) {
+  if (int rc_ = resident_stop(e)) return rc_;
+  if (!e || !e->have_graph) return fail(e, DGP_E_STATE, "graph first");
+  if (e->pending_resync) return fail(e, DGP_E_STATE, "dgp_update_restrictions: dgp_sync_* first");
+  if (n < 0 || (n && (!task || !row_ptr || !flags)) || (n && row_ptr[0] != 0))
+    return fail(e, DGP_E_ARG, "dgp_update_restrictions: arguments");
+  HIPCHK(e, hipSetDevice(e->device));
+  dgp::Dev& D = e->D;
+  const int64_t N = D.N;
+  for (int64_t i = 0; i < n; i++) {
+    if (task[i] < 0 || task[i] >= N) return fail(e, DGP_E_ARG, "dgp_update_restrictions: task index");
+    if (flags[i] & ~(dgp::RF_RESTRICTED | dgp::RF_LOOSE)) return fail(e, DGP_E_ARG, "dgp_update_restrictions: flags");
+    if (row_ptr[i + 1] < row_ptr[i]) return fail(e, DGP_E_ARG, "dgp_update_restrictions: row_ptr not monotone");
+    if (!(flags[i] & dgp::RF_RESTRICTED) && row_ptr[i + 1] != row_ptr[i])
+      return fail(e, DGP_E_ARG, "dgp_update_restrictions: valid workers on an unrestricted task");
+    for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; k++) {
+      if (row_idx[k] < 0 || row_idx[k] >= D.W) return fail(e, DGP_E_ARG, "dgp_update_restrictions: worker index");
+      if (k > row_ptr[i] && row_idx[k] <= row_idx[k - 1])
+        return fail(e, DGP_E_ARG, "dgp_update_restrictions: valid workers must ascend");
+    }
+  }
+  if (n == 0) return 0;
+  auto& A = e->graph_allocs;  // the arrays live with the graph
+  if (!D.restr_flags) {  // the graph had none: every other task keeps an empty CSR row
+    int64_t* rp = nullptr;
+    int32_t* ri = nullptr;
+    uint8_t* rf = nullptr;
+    if (dalloc(e, &rp, N + 1, A) || dalloc(e, &ri, 1, A) || dalloc(e, &rf, N, A)) return DGP_E_HIP;
+    HIPCHK(e, hipMemset(rp, 0, (N + 1) * 8));
+    HIPCHK(e, hipMemset(rf, 0, N));
+    D.restr_ptr = rp;
+    D.restr_idx = ri;
+    D.restr_flags = rf;
+    e->restr_h.assign(N, 0);
+  }
+  if (!D.restr_ovr) {
+    int64_t* ov = nullptr;
+    if (dalloc(e, &ov, N, A)) return DGP_E_HIP;
+    HIPCHK(e, hipMemset(ov, 0xff, N * 8));  // -1: the CSR row
+    D.restr_ovr = ov;
+  }
+  // the rows, appended to the pool (length, then the workers)
+  const int64_t add = n + row_ptr[n];
+  if (e->rpool_used + add > e->rpool_cap) {
+    const int64_t cap = std::max<int64_t>(std::max<int64_t>(2 * e->rpool_cap, e->rpool_used + add), 4096);
+    int32_t* np = nullptr;
+    if (dalloc(e, &np, cap, A)) return DGP_E_HIP;
+    if (e->rpool_used) HIPCHK(e, hipMemcpy(np, D.restr_pool, e->rpool_used * 4, hipMemcpyDeviceToDevice));
+    D.restr_pool = np;  // (the old pool is freed with the graph)
+    e->rpool_cap = cap;
+  }
+  std::vector<int32_t> rows((size_t)add);
+  std::vector<int64_t> off((size_t)n);
+  std::vector<uint8_t> fl(flags, flags + n);
+  int64_t q = 0;
+  std::vector<uint8_t> tf = e->tflags_h;
+  for (int64_t i = 0; i < n; i++) {
+    off[i] = e->rpool_used + q;
+    rows[q++] = (int32_t)(row_ptr[i + 1] - row_ptr[i]);
+    for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; k++) rows[q++] = row_idx[k];
+    const int t = task[i];
+    e->restr_h[t] = flags[i];
+    // is_rootish (:2929-2947): restrictions make a task non-root-ish unless _rootish says so
+    if (e->rootish_override_h[t] < 0) {
+      const int g = e->group_h[t];
+      const bool gr = e->group_sizes[g] > D.total_nthreads * 2 && e->gdep_n[g] < 5 && e->gdep_len[g] < 5;
+      const bool r = gr && !(flags[i] & dgp::RF_RESTRICTED);
+      tf[t] = (uint8_t)((tf[t] & ~dgp::TF_ROOTISH) | (r ? dgp::TF_ROOTISH : 0));
+    }
+  }
+  HIPCHK(e, hipMemcpy(const_cast<int32_t*>(D.restr_pool) + e->rpool_used, rows.data(), add * 4, hipMemcpyHostToDevice));
+  e->rpool_used += add;
+  int32_t* d_task = nullptr;
+  int64_t* d_off = nullptr;
+  uint8_t* d_fl = nullptr;
+  std::vector<void*> tmp;
+  if (dalloc(e, &d_task, n, tmp) || dalloc(e, &d_off, n, tmp) || dalloc(e, &d_fl, n, tmp)) {
+    free_list(tmp);
+    return DGP_E_HIP;
+  }
+  hipError_t st = hipMemcpy(d_task, task, n * 4, hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemcpy(d_off, off.data(), n * 8, hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemcpy(d_fl, fl.data(), n, hipMemcpyHostToDevice);
+  if (st == hipSuccess) {
+    hipLaunchKernelGGL(k_restr_scatter, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1024)), dim3(256), 0,
+                       e->stream, const_cast<int64_t*>(D.restr_ovr), const_cast<uint8_t*>(D.restr_flags), d_task,
+                       d_off, d_fl, n);
+    st = hipGetLastError();
+  }
+  if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+  free_list(tmp);
+  if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_update_restrictions: ") + hipGetErrorString(st));
+  if (tf != e->tflags_h) {
+    HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), tf.data(), N, hipMemcpyHostToDevice));
+    e->tflags_h = tf;
+  }
+  return 0;
+}
+
+int dgp_set_rootish(dgp_engine* e, int64_t n, const int32_t* task, const int8_t* value) {
+  if (int rc_ = resident_stop(e)) return rc_;
+  if (!e || !e->have_graph) return fail(e, DGP_E_STATE, "graph first");
+  if (e->pending_resync) return fail(e, DGP_E_STATE, "dgp_set_rootish: dgp_sync_* first");
+  if (n < 0 || (n && (!task || !value))) return fail(e, DGP_E_ARG, "dgp_set_rootish: arguments");
+  HIPCHK(e, hipSetDevice(e->device));
+  dgp::Dev& D = e->D;
+  for (int64_t i = 0; i < n; i++) {
+    if (task[i] < 0 || task[i] >= D.N) return fail(e, DGP_E_ARG, "dgp_set_rootish: task index");
+    if (value[i] < -1 || value[i] > 1) return fail(e, DGP_E_ARG, "dgp_set_rootish: value");
+  }
+  std::vector<uint8_t> tf = e->tflags_h;
+  for (int64_t i = 0; i < n; i++) {  // is_rootish (:2929-2947) with the new TaskState._rootish
+    const int t = task[i];
+    e->rootish_override_h[t] = value[i];
+    const int g = e->group_h[t];
+    const bool gr = e->group_sizes[g] > D.total_nthreads * 2 && e->gdep_n[g] < 5 && e->gdep_len[g] < 5;
+    const bool rs = !e->restr_h.empty() && (e->restr_h[t] & dgp::RF_RESTRICTED);
+    const bool r = value[i] >= 0 ? value[i] != 0 : (gr && !rs);
+    tf[t] = (uint8_t)((tf[t] & ~dgp::TF_ROOTISH) | (r ? dgp::TF_ROOTISH : 0));
+  }
+  if (tf != e->tflags_h) {
+    HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), tf.data(), D.N, hipMemcpyHostToDevice));
+    e->tflags_h = tf;
+  }
+  return 0;
 }
 
 int dgp_set_task_results(dgp_engine* e, const int64_t* nbytes, const double* start, const double* stop) {
@@ -1325,10 +1470,31 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
   return 0;
 }
 
+static int add_graph_impl(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx,
+                          const int64_t* prio, const int32_t* prefix_id, int32_t n_prefixes,
+                          const double* prefix_default_duration, const int32_t* group_id, int32_t n_groups,
+                          const uint8_t* wanted, const int8_t* rootish_override, int64_t* n_new_placements, bool defer);
+
 int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx, const int64_t* prio,
                   const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
                   const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override,
                   int64_t* n_new_placements) {
+  return add_graph_impl(e, n_new, dep_ptr, dep_idx, prio, prefix_id, n_prefixes, prefix_default_duration, group_id,
+                        n_groups, wanted, rootish_override, n_new_placements, false);
+}
+
+int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx,
+                           const int64_t* prio, const int32_t* prefix_id, int32_t n_prefixes,
+                           const double* prefix_default_duration, const int32_t* group_id, int32_t n_groups,
+                           const uint8_t* wanted, const int8_t* rootish_override) {
+  return add_graph_impl(e, n_new, dep_ptr, dep_idx, prio, prefix_id, n_prefixes, prefix_default_duration, group_id,
+                        n_groups, wanted, rootish_override, nullptr, true);
+}
+
+static int add_graph_impl(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx,
+                          const int64_t* prio, const int32_t* prefix_id, int32_t n_prefixes,
+                          const double* prefix_default_duration, const int32_t* group_id, int32_t n_groups,
+                          const uint8_t* wanted, const int8_t* rootish_override, int64_t* n_new_placements, bool defer) {
   if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
@@ -1390,6 +1556,7 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   for (int64_t t = 0; t < n_new; t++) relwait[group_id[t]]++;
   const dgp::Dev old = D;
   const std::vector<uint8_t> old_tf = e->tflags_h, old_restr = e->restr_h;
+  const int64_t old_rpool_used = e->rpool_used, old_rpool_cap = e->rpool_cap;
   const int64_t old_rlog = D.rlog_cap;
   e->log_min[0] = D.pl_cap + n_new;
   e->log_min[1] = D.sv_cap + n_new;
@@ -1462,6 +1629,20 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   HIPCHK(e, hipStreamSynchronize(s));
   // task flags the graph upload does not know: forgotten rows (resync) and restrictions
   for (int64_t t = 0; t < N0; t++) e->tflags_h[t] |= (uint8_t)(old_tf[t] & dgp::TF_FORGOTTEN);
+  if (old.restr_ovr) {  // rows changed after the upload: the overrides and their pool carried over
+    int64_t* ov = nullptr;
+    int32_t* pl = nullptr;
+    if (dalloc(e, &ov, N1, e->graph_allocs) || dalloc(e, &pl, std::max<int64_t>(old_rpool_cap, 1), e->graph_allocs))
+      return DGP_E_HIP;
+    HIPCHK(e, carry(ov, old.restr_ovr, (size_t)N0 * 8, (size_t)N1 * 8, 0xff));
+    if (old_rpool_used)
+      HIPCHK(e, hipMemcpyAsync(pl, old.restr_pool, (size_t)old_rpool_used * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(e, hipStreamSynchronize(s));
+    D.restr_ovr = ov;
+    D.restr_pool = pl;
+    e->rpool_used = old_rpool_used;
+    e->rpool_cap = std::max<int64_t>(old_rpool_cap, 1);
+  }
   if (old.restr_flags) {  // the earlier tasks keep their restrictions; the new ones have none
     std::vector<int64_t> rp(N1 + 1);
     HIPCHK(e, hipMemcpy(rp.data(), old.restr_ptr, (N0 + 1) * 8, hipMemcpyDeviceToHost));
@@ -1492,7 +1673,7 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
   }
   HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), e->tflags_h.data(), N1, hipMemcpyHostToDevice));
   free_list(old_allocs);
-  if (ext_deps) {
+  if (ext_deps || defer) {
     // the new tasks stay released: the scheduler decides this update_graph stimulus itself
     // (the new tasks' waiting_on / the earlier tasks' waiters, any placement it makes) and
     // the caller hands over its state (dgp_sync_*) before the next stimulus

@@ -198,14 +198,15 @@ class PlacementEngine:
         self.n_workers += 1
         return int(newp.value)
 
-    def add_graph(self, g: dict) -> int:
+    def add_graph(self, g: dict, defer: bool = False) -> int:
         """A later graph submission (Scheduler.update_graph, distributed/scheduler.py
         :4662-4751) on a running engine: ``g`` holds the new tasks only (dependencies
         relative to it, ``-1 - t`` for an earlier task t; priorities after every earlier
         task's, prefix / group ids and ``prefix_default_dur`` / ``group_prefix`` over the
         engine-wide tables). Runs their update_graph stimulus; returns the number of
         placements it made. With dependencies on earlier tasks the stimulus is the
-        scheduler's: nothing is placed and ``sync()`` must follow (include/dgplace.h)."""
+        scheduler's: nothing is placed and ``sync()`` must follow (include/dgplace.h); so
+        too with ``defer`` (dgp_add_graph_deferred: a graph with restrictions)."""
         arrs = {
             "dep_ptr": np.ascontiguousarray(g["dep_ptr"], np.int64),
             "dep_idx": np.ascontiguousarray(g["dep_idx"], np.int32),
@@ -218,6 +219,13 @@ class PlacementEngine:
         }
         n = len(arrs["prio"])
         newp = C.c_int64(0)
+        if defer:
+            self._check(self.lib.dgp_add_graph_deferred(
+                self.h, n, _ptr(arrs["dep_ptr"]), _ptr(arrs["dep_idx"]), _ptr(arrs["prio"]), _ptr(arrs["prefix_id"]),
+                len(arrs["prefix_default_dur"]), _ptr(arrs["prefix_default_dur"]), _ptr(arrs["group_id"]),
+                len(g["group_prefix"]), _ptr(arrs["wanted"]), _ptr(arrs["rootish_override"])), "dgp_add_graph_deferred")
+            self.n_tasks += n
+            return 0
         self._check(self.lib.dgp_add_graph(
             self.h, n, _ptr(arrs["dep_ptr"]), _ptr(arrs["dep_idx"]), _ptr(arrs["prio"]), _ptr(arrs["prefix_id"]),
             len(arrs["prefix_default_dur"]), _ptr(arrs["prefix_default_dur"]), _ptr(arrs["group_id"]),
@@ -268,6 +276,29 @@ class PlacementEngine:
         """idle / saturated membership of ``workers`` as the scheduler holds it."""
         w, a, b = self._arr(workers, np.int32), self._arr(idle, np.uint8), self._arr(saturated, np.uint8)
         self._check(self.lib.dgp_set_worker_flags(self.h, len(w), _ptr(w), _ptr(a), _ptr(b)), "dgp_set_worker_flags")
+
+    def update_restrictions(self, task, rows, flags):
+        """Scheduler.set_restrictions of ``task`` while the graph runs (scheduler.py
+        :7702-7707; the shuffle's restrict_task, shuffle/_scheduler_plugin.py:101-115): each
+        task's valid workers (ascending engine indices) and flags (1 restricted, 2 loose)."""
+        t, f = self._arr(task, np.int32), self._arr(flags, np.uint8)
+        rows = [sorted(int(w) for w in r) for r in rows]
+        if len(rows) != len(t) or len(f) != len(t):
+            raise ValueError("update_restrictions: one row and one flag per task")
+        rp = np.zeros(len(t) + 1, np.int64)
+        rp[1:] = np.cumsum([len(r) for r in rows])
+        ri = self._arr([w for r in rows for w in r], np.int32)
+        if len(ri) == 0:
+            ri = np.zeros(1, np.int32)
+        self._check(self.lib.dgp_update_restrictions(self.h, len(t), _ptr(t), _ptr(rp), _ptr(ri), _ptr(f)),
+                    "dgp_update_restrictions")
+
+    def set_rootish(self, task, value):
+        """TaskState._rootish per task (-1 None, 0 False, 1 True), set while the graph runs
+        (the shuffle's _ensure_output_tasks_are_non_rootish, shuffle/_scheduler_plugin.py
+        :254-278)."""
+        t, v = self._arr(task, np.int32), self._arr(value, np.int8)
+        self._check(self.lib.dgp_set_rootish(self.h, len(t), _ptr(t), _ptr(v)), "dgp_set_rootish")
 
     def set_wanted(self, task, wanted):
         """who_wants non-empty (1) / empty (0) per task (client_desires_keys :5398-5415)."""

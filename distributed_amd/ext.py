@@ -87,7 +87,7 @@ _ERRED_TRANSITIONS = frozenset({("processing", "erred"), ("waiting", "released")
 # change, and the engine method that follows each on the device (PlacementEngine); an engine
 # without the method (or one that raises) hands placement back to the scheduler
 _ENGINE_EVENTS = ("add_replicas", "remove_replicas", "set_worker_status", "long_running", "heartbeat",
-                  "set_worker_flags", "set_wanted", "task_erred")
+                  "set_worker_flags", "set_wanted", "task_erred", "update_restrictions", "set_rootish")
 
 
 def _compute_interval(startstops):
@@ -215,6 +215,8 @@ class GPUPlacementExtension(SchedulerPlugin):
         self._dirty_all = False
         self._route = 0             # the decide_worker route of the scheduler's current decision
         self.removed: set = set()   # addresses of removed workers (they keep their engine index)
+        self._rootish_h: dict = {}  # key -> the _rootish override the engine holds (-1 / 0 / 1)
+        self._restr_h: dict = {}    # key -> (restriction flags, valid worker indices) the engine holds
         if hasattr(scheduler, "add_plugin"):
             scheduler.add_plugin(self, name=self.name)
         elif isinstance(getattr(scheduler, "plugins", None), dict):  # a bare SchedulerState
@@ -271,7 +273,8 @@ class GPUPlacementExtension(SchedulerPlugin):
         rpc = getattr(s, "handlers", None)
         if isinstance(rpc, dict):
             self._wrap(rpc, "heartbeat_worker", self._on_heartbeat, (), after=True)
-            self._wrap(rpc, "set_restrictions", self._on_set_restrictions, ())
+        self._wrap_set_restrictions()
+        self._wrap_shuffle()
         self._wrap_replicas()
         self._wrap_stealing()
 
@@ -371,6 +374,105 @@ class GPUPlacementExtension(SchedulerPlugin):
         s.add_replica = add_replica
         s.remove_replica = remove_replica
         s._gpu_placement_replicas = True
+
+    def _wrap_set_restrictions(self):
+        """``Scheduler.set_restrictions`` (scheduler.py:7702-7707), both as the RPC handler
+        and as the method other extensions call -- the P2P shuffle's ``restrict_task`` ->
+        ``_set_restriction`` (shuffle/_scheduler_plugin.py:101-115, :281-293) calls
+        ``self.scheduler.set_restrictions``: a task's valid workers change outside any
+        transition, which the engine takes over (``dgp_update_restrictions``)."""
+        s = self.scheduler
+        orig = getattr(s, "set_restrictions", None)
+        if orig is None or getattr(orig, "_gpu_placement", False):
+            return
+
+        @functools.wraps(orig)
+        def set_restrictions(*args, **kwargs):
+            worker = kwargs["worker"] if "worker" in kwargs else (args[0] if args else {})
+            r = orig(*args, **kwargs)
+            self._task_inputs_changed(list(worker or {}))
+            return r
+
+        set_restrictions._gpu_placement = True
+        s.set_restrictions = set_restrictions  # per instance: other extensions call it through self
+        rpc = getattr(s, "handlers", None)
+        if isinstance(rpc, dict) and "set_restrictions" in rpc:
+            rpc["set_restrictions"] = set_restrictions
+
+    def _wrap_shuffle(self):
+        """The P2P shuffle plugin (shuffle/_scheduler_plugin.py) sets ``_rootish = False`` on
+        the barrier's dependents by plain attribute assignment when a shuffle starts
+        (``_ensure_output_tasks_are_non_rootish`` :150-151, :254-278): the engine takes the new
+        overrides after it (``dgp_set_rootish``)."""
+        s = self.scheduler
+        sh = (getattr(s, "extensions", None) or {}).get("shuffle")
+        fn = getattr(sh, "_ensure_output_tasks_are_non_rootish", None)
+        if fn is None or getattr(fn, "_gpu_placement", False):
+            return
+
+        @functools.wraps(fn)
+        def ensure_non_rootish(spec, *args, **kwargs):
+            r = fn(spec, *args, **kwargs)
+            try:
+                from distributed.shuffle._core import barrier_key
+
+                barrier = s.tasks.get(barrier_key(spec.id))
+                keys = [d.key for d in barrier.dependents] if barrier is not None else list(self.task_index)
+            except Exception:  # no barrier name: every task the engine holds
+                keys = list(self.task_index)
+            self._task_inputs_changed(keys)
+            return r
+
+        ensure_non_rootish._gpu_placement = True
+        sh._ensure_output_tasks_are_non_rootish = ensure_non_rootish
+
+    def _task_rows(self, ts):
+        """(_rootish override, restriction flags, valid worker indices) of ``ts`` as the
+        engine holds them (graph_from_tasks' resolution, valid_workers :3043-3107)."""
+        ov = -1 if ts._rootish is None else int(bool(ts._rootish))
+        if ts.worker_restrictions or ts.host_restrictions or ts.resource_restrictions:
+            vw = self.scheduler.valid_workers(ts)
+            if vw is not None:
+                row = tuple(sorted(self.worker_index[ws.address] for ws in vw if ws.address in self.worker_index))
+                return ov, 1 | (2 if ts.loose_restrictions else 0), row
+        return ov, 0, ()
+
+    def _task_inputs_changed(self, keys):
+        """TaskState._rootish / restrictions of ``keys`` may have changed outside any
+        transition: the engine takes the differences from what it holds. Under a suspension
+        the keys are marked dirty instead (the resync takes them)."""
+        if not self.active or self.engine is None:
+            return
+        keys = [k for k in keys if k in self.task_index]
+        if not keys:
+            return
+        if self.suspended:
+            self._dirty.update(keys)
+            return
+        self._push_task_inputs(keys)
+
+    def _push_task_inputs(self, keys):
+        s = self.scheduler
+        rt, rv, ut, urows, uflags = [], [], [], [], []
+        for k in keys:
+            ts = s.tasks.get(k)
+            if ts is None:
+                continue
+            t = self.task_index[k]
+            ov, fl, row = self._task_rows(ts)
+            if ov != self._rootish_h.get(k, -1):
+                rt.append(t)
+                rv.append(ov)
+                self._rootish_h[k] = ov
+            if (fl, row) != self._restr_h.get(k, (0, ())):
+                ut.append(t)
+                urows.append(row)
+                uflags.append(fl)
+                self._restr_h[k] = (fl, row)
+        if rt:
+            self._engine_op("set_rootish", rt, rv)
+        if ut:
+            self._engine_op("update_restrictions", ut, urows, uflags)
 
     def _replica_event(self, ts, ws, sign):
         if not self.active or self.engine is None or ts.key not in self.task_index:
@@ -566,6 +668,10 @@ class GPUPlacementExtension(SchedulerPlugin):
             for j, p in enumerate(pl):
                 self.dev_run[self.keys[p[0]]] = n0 + j
             self.n_fetched = self.engine.num_placements()
+            # _rootish / restrictions the scheduler changed meanwhile (set_restrictions, the
+            # shuffle's restrict_task, _ensure_output_tasks_are_non_rootish, a later graph's)
+            self.suspended = False
+            self._push_task_inputs(keys)
             self.stats["resyncs"] += 1
             self.stats["resync_tasks"] += len(keys)
         except Exception as e:
@@ -746,6 +852,7 @@ class GPUPlacementExtension(SchedulerPlugin):
                                             self.worker_index)
                 self.keys = keys_
                 self.task_index = {k: i for i, k in enumerate(keys_)}
+                self._remember_inputs(g, keys_)
                 self.prefix_index = {nm: i for i, nm in enumerate(g["prefix_names"])}
                 self.group_index = {nm: i for i, nm in enumerate(g["group_names"])}
                 self.prefix_dur = list(g["prefix_default_dur"])
@@ -769,6 +876,16 @@ class GPUPlacementExtension(SchedulerPlugin):
         except Exception as e:  # plugin errors are logged, not raised (scheduler.py:4652-4653)
             self.fallback(f"update_graph: {e}")
 
+    def _remember_inputs(self, g, keys_):
+        """What the engine holds of each uploaded task's _rootish and restrictions."""
+        for i, k in enumerate(keys_):
+            if g["rootish_override"][i] >= 0:
+                self._rootish_h[k] = int(g["rootish_override"][i])
+        if "restr_flags" in g:
+            rp, ri = g["restr_ptr"], g["restr_idx"]
+            for i in np.flatnonzero(g["restr_flags"]):
+                self._restr_h[keys_[i]] = (int(g["restr_flags"][i]), tuple(int(w) for w in ri[rp[i]:rp[i + 1]]))
+
     def _add_graph(self, new):
         """A later update_graph (scheduler.py:4662-4751) on the running engine: the new
         tasks must all follow the earlier ones in priority (a new generation, :4713, with no
@@ -779,8 +896,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         s = self.scheduler
         g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers], s.valid_workers,
                                     self.worker_index, earlier=self.task_index)
-        if "restr_flags" in g:
-            raise NotImplementedError("worker restrictions in a later graph")
+        restricted = "restr_flags" in g  # its stimulus the scheduler's, then the rows (dgp_update_restrictions)
         if min(ts.priority for ts in new) <= self.max_priority:
             raise NotImplementedError("a later graph whose tasks do not all follow the earlier ones in priority")
         pmap = np.zeros(len(g["prefix_names"]), np.int32)
@@ -804,14 +920,20 @@ class GPUPlacementExtension(SchedulerPlugin):
         if not self.active:
             return
         dependent = bool((g["dep_idx"] < 0).any())
-        self.engine.add_graph(g2)
+        if restricted:
+            self.engine.add_graph(g2, defer=True)
+        else:
+            self.engine.add_graph(g2)
         self.keys = self.keys + keys_
         self.task_index.update({k: n0 + i for i, k in enumerate(keys_)})
+        g.pop("restr_flags", None)  # the resync hands the restrictions over (the mirrors lack them)
+        self._remember_inputs(g, keys_)
         self.max_priority = max(ts.priority for ts in new)
         self.stats["graphs"] += 1
-        if dependent:
-            self.stats["dependent_graphs"] += 1
-            self._suspend("a later graph that depends on earlier tasks")
+        if dependent or restricted:
+            self.stats["dependent_graphs" if dependent else "restricted_graphs"] += 1
+            self._suspend("a later graph that depends on earlier tasks" if dependent else
+                          "a later graph with restrictions")
             for k in keys_:  # the new tasks, the earlier ones they wait on / add waiters to
                 self._mark_dirty(k)
             return
@@ -979,10 +1101,6 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._suspend("update-data of tasks in the engine's graph")
             for k in keys:
                 self._mark_dirty(k)
-
-    def _on_set_restrictions(self, kw):
-        if any(k in self.task_index for k in (kw.get("worker") or {})):
-            self.fallback("set_restrictions on a task in the engine's graph")
 
     def _on_heartbeat(self, kw, run):
         """heartbeat_worker (:4197-4252): the bandwidth EWMA (:4223-4226) and

@@ -153,7 +153,8 @@ def star(n_leaves: int, n_workers: int) -> dict:
         stop=np.full(n, 0.01), nthreads=np.ones(n_workers)))
 
 
-def shuffle_graph(n_partitions: int, n_workers: int, *, seed: int = 2, restricted: bool = False) -> dict:
+def shuffle_graph(n_partitions: int, n_workers: int, *, seed: int = 2, restricted: bool = False,
+                  live: bool = False) -> dict:
     """Config C3: the P2P-shuffle graph shape of ``distributed/shuffle/_shuffle.py:276-306``:
     P inputs -> P ``shuffle-transfer`` -> one ``shuffle-barrier`` (fan-in P) -> P
     ``shuffle-p2p`` unpack tasks, the unpacks forced non-rootish
@@ -166,6 +167,10 @@ def shuffle_graph(n_partitions: int, n_workers: int, *, seed: int = 2, restricte
     ``_scheduler_plugin.py:101-115``, worker ``_get_worker_for_range_sharding``
     ``_shuffle.py:612-617``: index ``W * i // P``): decide_worker's candidates (the
     barrier's holder) miss the valid set, so each unpack goes to its pinned worker.
+
+    ``live``: the graph as the client submits it, before the shuffle runs: the unpacks'
+    ``_rootish`` is still None (the plugin sets it False when the first transfer starts,
+    the live lifecycle of tests/golden/gen_service.py ``p2p``).
     """
     rng = np.random.default_rng(seed)
     p = int(n_partitions)
@@ -196,7 +201,8 @@ def shuffle_graph(n_partitions: int, n_workers: int, *, seed: int = 2, restricte
     prefix_id[bar] = 2
     prefix_id[unp] = 3
     rootish = np.full(n, -1, np.int8)
-    rootish[unp] = 0
+    if not live:
+        rootish[unp] = 0
     group_names = [f"input-{TOKEN}", f"shuffle-transfer-{TOKEN}", "shuffle-barrier", f"shuffle-p2p-{TOKEN}"]
     extra = {}
     if restricted:
@@ -208,7 +214,8 @@ def shuffle_graph(n_partitions: int, n_workers: int, *, seed: int = 2, restricte
         rflags[unp] = 1
         extra = dict(restr_ptr=rptr, restr_idx=ridx, restr_flags=rflags)
     return _finish(dict(**extra,
-        name=f"shuffle_{p}x{n_workers}" + ("_restricted" if restricted else ""), dep_ptr=dep_ptr, dep_idx=dep_idx,
+        name=f"shuffle_{p}x{n_workers}" + ("_restricted" if restricted else "") + ("_live" if live else ""),
+        dep_ptr=dep_ptr, dep_idx=dep_idx,
         prio=prio,
         prefix_id=prefix_id, group_id=prefix_id.copy(), prefix_names=prefix_names,
         group_names=group_names, group_prefix=np.arange(4), prefix_default_dur=np.full(4, -1.0),

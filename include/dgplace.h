@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 11
+#define DGP_ABI_VERSION 12
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -125,6 +125,18 @@ int dgp_set_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const 
  * restricted tasks are not root-ish (:2939) unless _rootish overrides. Null flags clear
  * them. After dgp_set_graph, before any stimulus; resets the engine. */
 int dgp_set_restrictions(dgp_engine* e, const int64_t* restr_ptr, const int32_t* restr_idx, const uint8_t* flags);
+/* Restrictions of n tasks changed while the graph runs: Scheduler.set_restrictions
+ * (scheduler.py:7702-7707), which the P2P shuffle's restrict_task calls for each output
+ * task (shuffle/_scheduler_plugin.py:101-115, :281-293). Task task[i] gets the valid workers
+ * row_idx[row_ptr[i] .. row_ptr[i+1]) (ascending indices) and flags[i] (as above); its
+ * root-ish flag follows (:2939). Between stimuli; keeps the engine's state. (ABI 12) */
+int dgp_update_restrictions(dgp_engine* e, int64_t n, const int32_t* task, const int64_t* row_ptr,
+                            const int32_t* row_idx, const uint8_t* flags);
+/* TaskState._rootish of n tasks set while the graph runs (-1 None, 0 False, 1 True; is_rootish
+ * :2929-2947): the shuffle plugin's _ensure_output_tasks_are_non_rootish sets False on the
+ * barrier's dependents when the shuffle starts (shuffle/_scheduler_plugin.py:150-151,
+ * :254-278). Between stimuli; keeps the engine's state. (ABI 12) */
+int dgp_set_rootish(dgp_engine* e, int64_t n, const int32_t* task, const int8_t* value);
 int dgp_set_task_results(dgp_engine* e, const int64_t* nbytes, const double* start, const double* stop);
 
 /* Reset all dynamic state (tasks released, workers empty, placement log cleared). */
@@ -213,6 +225,14 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
                   const int32_t* prefix_id, int32_t n_prefixes, const double* prefix_default_duration,
                   const int32_t* group_id, int32_t n_groups, const uint8_t* wanted, const int8_t* rootish_override,
                   int64_t* n_new_placements);
+/* dgp_add_graph whose update_graph stimulus is the scheduler's own whatever its dependencies
+ * (the appended tasks stay released, dgp_sync_* must follow): a later graph whose tasks carry
+ * restrictions (scheduler.py:4908-4922), which the caller hands over with
+ * dgp_update_restrictions after the resync. (ABI 12) */
+int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx,
+                           const int64_t* prio, const int32_t* prefix_id, int32_t n_prefixes,
+                           const double* prefix_default_duration, const int32_t* group_id, int32_t n_groups,
+                           const uint8_t* wanted, const int8_t* rootish_override);
 
 /* ---- Service events: the other placement-input stimuli of a live scheduler, in the order the
  * scheduler handles them, between dgp_tasks_finished calls. Stream-engine graphs (<= 32 prefixes);

@@ -18,7 +18,7 @@ def golden_files():
     """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
                   and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcgdep_", "svcev_",
-                                            "svcrs_")))
+                                            "svcrs_", "svcp2p_", "svcgrst_")))
 
 
 def svc_second_graph_files():
@@ -30,6 +30,12 @@ def svc_dep_graph_files():
     """Service-mode streams with a later graph that depends on earlier tasks (gen_service.py
     second-graph svcgdep_*): the scheduler decides its stimulus, the engine resyncs."""
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcgdep_") and f.endswith(".npz"))
+
+
+def svc_restr_graph_files():
+    """Service-mode streams with a later graph carrying worker restrictions (gen_service.py
+    second-graph svcgrst_*): appended deferred, the scheduler's stimulus, resync + rows."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcgrst_") and f.endswith(".npz"))
 
 
 def second_graph(g, z, with_results=False):
@@ -66,6 +72,11 @@ def svc_event_files():
 def svc_resync_files():
     """Service streams with stimuli the scheduler decides itself, then resyncs (gen_service.py resync)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcrs_") and f.endswith(".npz"))
+
+
+def svc_p2p_files():
+    """The P2P shuffle's scheduler-side lifecycle (gen_service.py p2p)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcp2p_") and f.endswith(".npz"))
 
 
 def svc_steal_files():

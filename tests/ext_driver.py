@@ -90,9 +90,9 @@ class FixtureEngine:
             task[j], task[j + 1] = task[j + 1], task[j]
         return {"pl_task": task, "pl_worker": self.exp["pl_worker"][sl]}
 
-    def add_graph(self, g):  # a later graph (the fixture's per-event placement counts)
+    def add_graph(self, g, defer=False):  # a later graph (the fixture's per-event placement counts)
         self.graphs.append(g)
-        if (np.asarray(g["dep_idx"]) < 0).any():  # dependent: appended, the scheduler's stimulus, then sync()
+        if defer or (np.asarray(g["dep_idx"]) < 0).any():  # appended, the scheduler's stimulus, then sync()
             return 0
         return self.add_worker(0)
 
@@ -406,7 +406,7 @@ def run_second_graph(name):
     S.validate_key = lambda self, key, ts=None: None
     S.send_all = lambda self, client_msgs, worker_msgs: None
     fkeys = [ts.key for ts in tss]
-    dep = name.startswith("svcgdep_")
+    dep = name.startswith(("svcgdep_", "svcgrst_"))  # the scheduler decides the submission, then a resync
     eng = (EventEngine if dep else FixtureEngine)(exp, fkeys)
     ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
     eng.ext = ext
@@ -461,6 +461,10 @@ def run_second_graph(name):
                 if g2["wanted"][k]:
                     ts.who_wants = {cs}
                     cs.wants_what.add(ts)
+                if "restr_flags" in g2 and g2["restr_flags"][k] & 1:  # as the generator set them
+                    rp, ri = g2["restr_ptr"], g2["restr_idx"]
+                    ts.worker_restrictions = {f"tcp://w{int(x):05d}:1" for x in ri[rp[k]:rp[k + 1]]} | {"tcp://gone:1"}
+                    ts.loose_restrictions = bool(g2["restr_flags"][k] & 2)
             eng.fkeys.extend(keys2)
             tss.extend(new)
             prio2 = {ts.key: ts.priority for ts in new}
@@ -486,7 +490,16 @@ def run_second_graph(name):
     host = 0
     if dep:  # one resync, right after the submission: the fixture's dump
         syncs = [c for c in eng.calls if c[0] == "sync"]
-        assert len(syncs) == 1 and ext.stats["dependent_graphs"] == 1, (len(syncs), ext.stats)
+        assert len(syncs) == 1 and ext.stats["dependent_graphs"] + ext.stats["restricted_graphs"] == 1, (
+            len(syncs), ext.stats)
+        if "restr_flags" in g2:  # the new tasks' restrictions, handed over right after the resync
+            rs = [c for c in eng.calls if c[0] == "restrict"]
+            assert len(rs) == 1 and eng.calls.index(rs[0]) == eng.calls.index(syncs[0]) + 1, eng.calls[-3:]
+            _, rt, rrows, rfl = rs[0]
+            rp, ri, rf = g2["restr_ptr"], g2["restr_idx"], g2["restr_flags"]
+            want_r = sorted((ext.task_index[fkeys[N1 + k]], ri[rp[k]:rp[k + 1]].tolist(), int(rf[k]))
+                            for k in np.flatnonzero(rf & 1))
+            assert sorted(zip(rt, rrows, rfl)) == want_r
         _, host, tasks, workers, glob = syncs[0]
         assert host == int(z["g2_nplaced"])
         ptr0 = {k: z[k + "_ptr"] for k in z.files if k.startswith("sync_") and k + "_ptr" in z.files}
@@ -553,6 +566,14 @@ class EventEngine(FixtureEngine):
     def task_erred(self, t):
         return self._event("erred", int(t))
 
+    # task inputs changed outside a transition (no placement of their own)
+    def set_rootish(self, t, v):
+        self.calls.append(("rootish", [int(x) for x in t], [int(x) for x in v]))
+
+    def update_restrictions(self, t, rows, flags):
+        self.calls.append(("restrict", [int(x) for x in t], [[int(w) for w in r] for r in rows],
+                           [int(x) for x in flags]))
+
     # state the engine follows without a placement of its own (no fixture event)
     def set_worker_flags(self, workers, idle, saturated):
         self.calls.append(("flags", [int(x) for x in workers], [int(x) for x in idle], [int(x) for x in saturated]))
@@ -587,7 +608,8 @@ def run_events(name, plain=False):
     import math as _m
 
     from gen_service import (EV_ADD_KEYS, EV_ERRED, EV_FINISHED, EV_HEARTBEAT, EV_LONG_RUNNING, EV_PAUSE,
-                             EV_RELEASE_DATA, EV_RELEASE_KEYS, EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RESUME)
+                             EV_RELEASE_DATA, EV_RELEASE_KEYS, EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RESTRICT,
+                             EV_RESUME, EV_SHUFFLE_INIT)
 
     from distributed_amd import sync as dsync
 
@@ -674,6 +696,26 @@ def run_events(name, plain=False):
         s.stream_handlers["reschedule"] = s._reschedule
         s.stream_handlers["client-releases-keys"] = s.client_releases_keys
     s.handlers = {"heartbeat_worker": heartbeat_worker}
+    plugin = spec = None
+    if (z["ev_kind"] == EV_SHUFFLE_INIT).any():  # the P2P shuffle plugin, bound to this state
+        from types import SimpleNamespace as NS2
+
+        from distributed.shuffle._core import barrier_key
+        from distributed.shuffle._scheduler_plugin import ShuffleSchedulerPlugin
+
+        S.set_restrictions = Scheduler.set_restrictions
+        bar = next(ts for ts in tss if ts.prefix.name == "shuffle-barrier")
+
+        class _View:  # what the plugin reads of its scheduler; set_restrictions goes to the (wrapped) method
+            tasks = {barrier_key("fixture"): bar}
+
+            def set_restrictions(self, worker):
+                return s.set_restrictions(worker)
+
+        plugin = ShuffleSchedulerPlugin.__new__(ShuffleSchedulerPlugin)
+        plugin.scheduler = _View()
+        spec = NS2(id="fixture")
+        s.extensions["shuffle"] = plugin
     ext._install()
     priority = {ts.key: ts.priority for ts in tss}
     recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
@@ -756,6 +798,15 @@ def run_events(name, plain=False):
             H["task-erred"](key=ts.key, worker=addr[w], stimulus_id=sid, run_id=ts.run_id, exception=None,
                             traceback=None)
             want.append(("erred", t))
+        elif kd == EV_SHUFFLE_INIT:  # the first transfer runs: _ensure_output_tasks_are_non_rootish
+            plugin._ensure_output_tasks_are_non_rootish(spec)
+            ts_ = sorted(ext.task_index[fkeys[int(q)]] for q in ht[hp[i]:hp[i + 1]])
+            want.append(("rootish", ts_, [0] * len(ts_)))
+            eng.k += 1  # the fixture's count for it (no placement)
+        elif kd == EV_RESTRICT:  # restrict_task -> _set_restriction -> Scheduler.set_restrictions
+            plugin._set_restriction(tss[t], addr[w])
+            want.append(("restrict", [ext.task_index[fkeys[t]]], [[w]], [1]))
+            eng.k += 1
         elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
             if kd == EV_REMOVE_WORKER:
                 loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
@@ -812,8 +863,8 @@ if __name__ == "__main__":
     plain = "--plain" in args
     stream = "--stream" in args
     for nm in [a for a in args if not a.startswith("--")]:
-        fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith(("svcgraph_", "svcgdep_"))
-              else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_")) else None)
+        fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_"))
+              else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcp2p_")) else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,
                                                plain="plugin" if "--plugin" in args else plain,
                                                validate="--novalidate" not in args)), flush=True)

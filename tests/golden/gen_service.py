@@ -327,7 +327,7 @@ def main_add_workers(only):
 TOKEN2 = "f9e8d7c6b5a49382716051e4d3c2b1a0"
 
 
-def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0):
+def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0, restr=False):
     """The replay protocol's completions as task-finished messages, with a second,
     independent graph ``g2`` submitted part-way through, the way
     ``Scheduler._create_taskstate_from_graph`` (distributed/scheduler.py:4512-4653) adds it:
@@ -340,7 +340,12 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0):
     ``dep_frac``: that fraction of the new tasks also depends on one earlier task (in memory,
     processing, waiting or queued when the graph arrives); the scheduler's state after the
     submission is dumped as resync rows (the engine appends the graph, the scheduler decides
-    that stimulus, the engine resyncs)."""
+    that stimulus, the engine resyncs).
+
+    ``restr``: ``g2`` carries worker restrictions (graphs.restrict rows, set on the new
+    TaskStates as build_state does): the scheduler's state after the submission is dumped as
+    resync rows too (the engine appends the graph deferred, the scheduler decides that
+    stimulus, the engine resyncs and takes the rows, dgp_update_restrictions)."""
     from distributed.core import Status
     from distributed.scheduler import Scheduler, WorkerState
 
@@ -407,11 +412,15 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0):
             if g2["wanted"][t]:
                 ts.who_wants = {cs}
                 cs.wants_what.add(ts)
+            if restr and g2["restr_flags"][t] & 1:  # as build_state sets a fixture graph's
+                rp, ri = g2["restr_ptr"], g2["restr_idx"]
+                ts.worker_restrictions = {f"tcp://w{int(w):05d}:1" for w in ri[rp[t]:rp[t + 1]]} | {"tcp://gone:1"}
+                ts.loose_restrictions = bool(g2["restr_flags"][t] & 2)
         ext["ptr"] = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
         ext["idx"] = np.array([d for r in rows for d in r], np.int32)
         recs2 = {ts.key: "waiting" for ts in sorted(new, key=lambda t: t.priority, reverse=True)}
         s._transitions(recs2, {}, {}, "update-graph-2")
-        if dep_frac:
+        if dep_frac or restr:
             gall = dict(prefix_names=g["prefix_names"], prefix_default_dur=g["prefix_default_dur"],
                         group_names=list(g["group_names"]) + list(g2["group_names"]))
             ext["dumps"].append(_dump(s, gall, tidx, widx, [ts.key for ts in tss] + [ts.key for ts in new]))
@@ -485,6 +494,11 @@ def main_second_graph(only):
         "svcgdep_c2mini_satinf": (dict(n=2500, w=24, seed=43), dict(n=1500, seed=44), float("inf"), 0.5, 0, 0.3),
         "svcgdep_joins_sat1.0": (dict(n=3000, w=32, seed=45, n_inner_prefixes=2, random_durations=True,
                                       nthreads="random"), dict(n=2000, seed=46), 1.0, 0.4, 12, 0.1),
+        # later graphs with worker restrictions (deferred append, the scheduler's stimulus, resync + rows)
+        "svcgrst_c2var_sat1.1": (dict(n=3000, w=32, seed=47, n_inner_prefixes=3, random_durations=True,
+                                      nthreads="random"), dict(n=2000, seed=48, restrict=0.3), 1.1, 0.3, 0, 0.0),
+        "svcgrst_dep_satinf": (dict(n=2500, w=24, seed=49), dict(n=1500, seed=50, restrict=0.2), float("inf"), 0.5, 0,
+                               0.2),
     }
     for name, (a, b, sat, frac, *more) in cases.items():
         nadd = more[0] if more else 0
@@ -496,13 +510,15 @@ def main_second_graph(only):
         if a.get("restrict"):
             g = G.graphs.restrict(g, a["restrict"], seed=a["seed"], empty_frac=0.0)
         g2 = G.graphs.random_dag(b["n"], a["w"], seed=b["seed"], **kw)
+        if b.get("restrict"):
+            g2 = G.graphs.restrict(g2, b["restrict"], seed=b["seed"], empty_frac=0.1)
         g2["group_names"] = [nm.replace(G.graphs.TOKEN, TOKEN2) for nm in g2["group_names"]]
         assert g2["prefix_names"] == g["prefix_names"]
         G.graphs.check_graph(g)
         dask.config.set({"distributed.scheduler.worker-saturation": sat})
         cfg = G.config_dict(sat)
-        rec, rounds, nplaced, states, msgs, round_ptr, at, joins, ext = replay_second_graph(g, g2, cfg, 0, frac, nadd,
-                                                                                          dep_frac)
+        rec, rounds, nplaced, states, msgs, round_ptr, at, joins, ext = replay_second_graph(
+            g, g2, cfg, 0, frac, nadd, dep_frac, restr=bool(b.get("restrict")))
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -515,9 +531,12 @@ def main_second_graph(only):
             z.update(add_msg=np.array(joins["msg"], np.int64), add_nthreads=np.array(joins["nthreads"], np.int32))
         for k in ("dep_ptr", "dep_idx", "prio", "prefix_id", "group_id", "wanted", "rootish_override"):
             z["g2_" + k] = np.asarray(g2[k])
-        if dep_frac:  # dependencies on earlier tasks (-1 - t), the submission's placements, resync rows
+        if dep_frac or b.get("restrict"):  # dependencies on earlier tasks (-1 - t), placements, resync rows
             z.update(g2_dep_ptr=ext["ptr"], g2_dep_idx=ext["idx"], g2_nplaced=np.array(ext["nplaced"], np.int64),
                      **_pack_dumps(ext["dumps"]))
+        if b.get("restrict"):
+            z.update(g2_restr_ptr=np.asarray(g2["restr_ptr"]), g2_restr_idx=np.asarray(g2["restr_idx"]),
+                     g2_restr_flags=np.asarray(g2["restr_flags"]))
         np.savez_compressed(path, **z)
         routes = np.bincount(np.array(rec["route"]), minlength=4).tolist()
         print(f"{name}: {len(msgs['task'])} messages, second graph of {g2['n_tasks']} at message {at}, routes {routes}")
@@ -529,6 +548,9 @@ EV_FINISHED, EV_ADD_KEYS, EV_RELEASE_DATA, EV_PAUSE, EV_RESUME, EV_LONG_RUNNING,
 # (dgp_sync_*; the fixture stores the scheduler's state after each, distributed_amd/sync.py)
 EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS = 8, 9, 10
 RESYNC_KINDS = (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS)
+# the P2P shuffle's scheduler-side lifecycle (svcp2p_*): placement inputs its plugin changes
+# outside any transition (shuffle/_scheduler_plugin.py); the tasks of an init are in hb_task
+EV_SHUFFLE_INIT, EV_RESTRICT = 11, 12
 
 
 def _dump(s, g, tidx, widx, keys):
@@ -820,6 +842,160 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
     return rec, rounds, nplaced, states, ev, hb, round_ptr
 
 
+def replay_p2p(g, cfg, dumps):
+    """The P2P shuffle's scheduler-side lifecycle on the shuffle graph as the client submits
+    it (graphs.shuffle_graph(live=True): the unpacks' _rootish None, no restrictions), each
+    step through the reference's own code (``ShuffleSchedulerPlugin`` bound to this state):
+
+    1. the transfers run; when the first one starts (shuffle_get_or_create -> ``_create``)
+       ``_ensure_output_tasks_are_non_rootish`` sets ``_rootish = False`` on every unpack
+       (shuffle/_scheduler_plugin.py:140-151, :254-278) -- EV_SHUFFLE_INIT;
+    2. the barrier completes; the unpacks go by decide_worker_non_rootish to its holder;
+    3. each unpack runs once: ``restrict_task`` -> ``_set_restriction`` ->
+       ``Scheduler.set_restrictions({key: {worker}})`` (:101-115, :281-293;
+       scheduler.py:7702-7707) with the range-sharded worker (shuffle/_shuffle.py:612-617)
+       -- EV_RESTRICT -- then raises Reschedule: ``Scheduler._reschedule`` (the "reschedule"
+       stream handler) re-places it under the restriction -- EV_RESCHEDULE, a resync dump;
+    4. the re-placed unpacks complete.
+
+    Everything else is the replay protocol (completions in placement-log order)."""
+    from types import SimpleNamespace as NS
+
+    from distributed.scheduler import Scheduler
+    from distributed.shuffle._core import barrier_key
+    from distributed.shuffle._scheduler_plugin import ShuffleSchedulerPlugin
+    from distributed.shuffle._shuffle import _get_worker_for_range_sharding
+
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    W = len(g["nthreads"])
+    N = g["n_tasks"]
+    P = (N - 1) // 3
+    addr = {i: a for a, i in widx.items()}
+    S = type(s)
+    S.stimulus_task_finished = Scheduler.stimulus_task_finished
+    S.set_restrictions = Scheduler.set_restrictions
+    S._reschedule = Scheduler._reschedule
+    S.send_all = lambda self, client_msgs, worker_msgs: None
+    S.worker_send = lambda self, worker, msg: None
+    s.extensions = {}
+    transfers = set(range(P, 2 * P))
+    bar = tss[2 * P]
+    # the plugin, bound to this state: its barrier lookup by name (barrier_key) finds the
+    # fixture's barrier task
+    sid = "fixture"
+    plugin = ShuffleSchedulerPlugin.__new__(ShuffleSchedulerPlugin)
+    plugin.scheduler = NS(tasks={barrier_key(sid): bar}, set_restrictions=s.set_restrictions)
+    spec = NS(id=sid)
+    recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
+    s._transitions(recs, {}, {}, "update-graph")
+    ev = {k: [] for k in ("kind", "task", "worker", "x", "nbytes", "start", "stop", "runid")}
+    hb = {"ptr": [0], "task": [], "dur": []}
+    stim = [len(rec["task"])]
+    round_ptr = [0]
+    rounds, nplaced = [], []
+    done = 0
+    first_run = set(range(2 * P + 1, 3 * P + 1))  # unpacks not yet restricted
+    started = False
+
+    def push(kind, t=-1, w=-1, x=math.nan, nbytes=-1, start=math.nan, stop=math.nan, runid=-1):
+        for k, v in zip(ev, (kind, t, w, x, nbytes, start, stop, runid)):
+            ev[k].append(v)
+        hb["ptr"].append(len(hb["task"]))
+
+    run_of = []
+    orig_add = S._add_to_processing
+
+    def add_to_processing(self, ts, ws, stimulus_id):
+        r = orig_add(self, ts, ws, stimulus_id)
+        run_of.append(int(ts.run_id))
+        return r
+
+    S._add_to_processing = add_to_processing
+    run_of.extend([int(tss[t].run_id) for t in rec["task"]])
+    workers = list(s.workers)  # the plugin's worker_for order (SortedDict: index order)
+    while True:
+        cur = len(rec["task"])
+        batch = list(range(done, cur))
+        rounds.append(G.snapshot(s, W, widx) + (len(s.queued),))
+        nplaced.append(cur - done)
+        done = cur
+        if not batch:
+            break
+        for pos in batch:
+            t = rec["task"][pos]
+            ts = tss[t]
+            if ts.state != "processing" or int(ts.run_id) != run_of[pos]:
+                continue
+            w = widx[ts.processing_on.address]
+            if t in transfers and not started:  # the first transfer runs: the shuffle starts
+                plugin._ensure_output_tasks_are_non_rootish(spec)
+                assert all(d._rootish is False for d in bar.dependents)
+                hb["task"].extend(sorted(tidx[d.key] for d in bar.dependents))
+                hb["dur"].extend([0.0] * len(bar.dependents))
+                push(EV_SHUFFLE_INIT)
+                stim.append(0)
+                started = True
+            if t in first_run:  # an unpack's first run: restrict_task, then Reschedule
+                first_run.discard(t)
+                j = t - (2 * P + 1)
+                wf = widx[_get_worker_for_range_sharding(P, j, workers)]
+                plugin._set_restriction(ts, addr[wf])
+                push(EV_RESTRICT, t, wf)
+                stim.append(0)
+                n0 = len(rec["task"])
+                s._reschedule(ts.key, addr[w], stimulus_id=f"reschedule-{len(ev['kind'])}")
+                push(EV_RESCHEDULE, t, w)
+                dumps.append(_dump(s, g, tidx, widx, [x.key for x in tss]))
+                stim.append(len(rec["task"]) - n0)
+                continue
+            sid_ = f"task-finished-{len(ev['kind'])}"
+            r, cm, wm = s.stimulus_task_finished(
+                ts.key, ts.processing_on.address, sid_, int(ts.run_id), nbytes=int(g["nbytes"][t]), type=None,
+                typename="int", metadata=None,
+                startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
+            n0 = len(rec["task"])
+            s._transitions(r, cm, wm, sid_)
+            s.stimulus_queue_slots_maybe_opened(stimulus_id=sid_)
+            stim.append(len(rec["task"]) - n0)
+            push(EV_FINISHED, t, w, math.nan, int(g["nbytes"][t]), float(g["start"][t]), float(g["stop"][t]), pos)
+        round_ptr.append(len(ev["kind"]))
+    assert not first_run and started
+    rec["stim"] = stim
+    states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
+    return rec, rounds, nplaced, states, ev, hb, round_ptr
+
+
+def main_p2p(only):
+    """svcp2p_*: the P2P shuffle lifecycle (replay_p2p), resync dumps after each reschedule."""
+    cases = {
+        "svcp2p_sat1.1": (lambda: G.graphs.shuffle_graph(200, 16, seed=61, live=True), 1.1),
+        "svcp2p_satinf": (lambda: G.graphs.shuffle_graph(160, 12, seed=62, live=True), float("inf")),
+    }
+    for name, (mk, sat) in cases.items():
+        if only and name not in only:
+            continue
+        g = mk()
+        G.graphs.check_graph(g)
+        dask.config.set({"distributed.scheduler.worker-saturation": sat})
+        cfg = G.config_dict(sat)
+        dumps = []
+        rec, rounds, nplaced, states, ev, hb, round_ptr = replay_p2p(g, cfg, dumps)
+        G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
+        path = os.path.join(HERE, f"{name}.npz")
+        z = dict(np.load(path, allow_pickle=False))
+        z.update(ev_kind=np.array(ev["kind"], np.int8), ev_task=np.array(ev["task"], np.int32),
+                 ev_worker=np.array(ev["worker"], np.int32), ev_x=np.array(ev["x"], np.float64),
+                 ev_nbytes=np.array(ev["nbytes"], np.int64), ev_start=np.array(ev["start"]),
+                 ev_stop=np.array(ev["stop"]), ev_runid=np.array(ev["runid"], np.int64),
+                 hb_ptr=np.array(hb["ptr"], np.int64), hb_task=np.array(hb["task"], np.int32),
+                 hb_dur=np.array(hb["dur"], np.float64), ev_round_ptr=np.array(round_ptr, np.int64))
+        z.update(_pack_dumps(dumps))
+        np.savez_compressed(path, **z)
+        cnt = np.bincount(np.array(ev["kind"]), minlength=13).tolist()
+        print(f"{name}: {len(ev['kind'])} events (by kind {cnt}), {len(dumps)} resyncs, {len(rec['task'])} placements, "
+              f"{os.path.getsize(path) / 1e3:.0f} kB")
+
+
 def main_events(only):
     cases = {
         # every kind, queuing on, random durations, 1-4 threads
@@ -890,6 +1066,8 @@ def main_resync(only):
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "resync":
         return main_resync(set(sys.argv[2:]))
+    if len(sys.argv) > 1 and sys.argv[1] == "p2p":
+        return main_p2p(set(sys.argv[2:]))
     if len(sys.argv) > 1 and sys.argv[1] == "add-workers":
         return main_add_workers(set(sys.argv[2:]))
     if len(sys.argv) > 1 and sys.argv[1] == "second-graph":

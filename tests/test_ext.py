@@ -81,6 +81,20 @@ def test_extension_follows_a_dependent_later_graph():
         assert r["device_decisions"] + r["host_placements"] == r["placements"] and r["host_placements"] > 0, r
 
 
+def test_extension_follows_a_later_graph_with_restrictions():
+    """A later graph whose tasks carry worker restrictions (scheduler.py:4908-4922): the
+    extension appends it deferred (dgp_add_graph_deferred), the scheduler decides that
+    update_graph stimulus, the engine resyncs and takes the new tasks' valid-worker rows
+    (dgp_update_restrictions) right after; every later decision is the engine's
+    (validate=True) and the extension stays active."""
+    names = ["svcgrst_c2var_sat1.1.npz", "svcgrst_dep_satinf.npz"]
+    res = drive(names)
+    assert [r["fixture"] for r in res] == names
+    for r in res:
+        assert r["active"] and r["graphs"] == 2 and r["resyncs"] == 1, r
+
+
+
 EVENTS = ["svcev_c2var_sat1.1.npz", "svcev_c2mini_satinf.npz", "svcev_dense_sat1.0.npz"]
 
 
@@ -99,6 +113,25 @@ def test_extension_follows_service_events():
 
 
 RESYNC = ["svcrs_c2var_sat1.1.npz", "svcrs_c2mini_satinf.npz"]
+P2P = ["svcp2p_sat1.1.npz", "svcp2p_satinf.npz"]
+
+
+def test_extension_follows_the_p2p_shuffle_lifecycle():
+    """The P2P shuffle as a live scheduler runs it (gen_service.py p2p), the reference's own
+    ShuffleSchedulerPlugin acting on the scheduler: when the first transfer runs,
+    _ensure_output_tasks_are_non_rootish sets _rootish False on every unpack by attribute
+    assignment (shuffle/_scheduler_plugin.py:150-151, :254-278) -- the extension's wrapper
+    hands the new overrides to the engine (dgp_set_rootish); the barrier's completion places
+    the unpacks on the device as non-rootish; each unpack's restrict_task -> set_restrictions
+    (:101-115, :281-293 -> scheduler.py:7702-7707, the *method*) reaches the engine
+    (dgp_update_restrictions); its Reschedule is the scheduler's stimulus, then a resync.
+    The extension stays active throughout; every other placement is the engine's
+    (validate=True)."""
+    res = drive(P2P)
+    assert [r["fixture"] for r in res] == P2P
+    for r in res:
+        assert r["active"] and r["resyncs"] > 0, r
+        assert r["device_decisions"] + r["host_placements"] == r["placements"], r
 
 
 def test_extension_resyncs_after_stimuli_it_does_not_model():

@@ -20,7 +20,8 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, second_graph, svc_dep_graph_files, svc_event_files, svc_resync_files
+from conftest import (GOLDEN, second_graph, svc_dep_graph_files, svc_event_files, svc_p2p_files, svc_resync_files,
+                      svc_restr_graph_files)
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -28,6 +29,7 @@ pytestmark = pytest.mark.gpu
 
 EV_FINISHED, EV_ADD_KEYS, EV_RELEASE_DATA, EV_PAUSE, EV_RESUME, EV_LONG_RUNNING, EV_HEARTBEAT, EV_ERRED = range(8)
 EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS = 8, 9, 10
+EV_SHUFFLE_INIT, EV_RESTRICT = 11, 12
 
 
 def sync_dump(z, j):
@@ -72,6 +74,11 @@ def drive_events(eng, g, z, exp=None):
                 eng.heartbeat(float(x[i]), g["prefix_id"][ts], hd[hp[i]:hp[i + 1]])
             elif kd == EV_ERRED:
                 eng.task_erred(t)
+            elif kd == EV_SHUFFLE_INIT:  # _ensure_output_tasks_are_non_rootish: the unpacks' _rootish False
+                ts = ht[hp[i]:hp[i + 1]]
+                eng.set_rootish(ts, np.zeros(len(ts), np.int8))
+            elif kd == EV_RESTRICT:  # restrict_task -> set_restrictions({key: {worker}})
+                eng.update_restrictions([t], [[w]], [1])
             elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
                 # the scheduler decided this stimulus itself: its placements, then its state
                 n = int(exp["stim_nplaced"][len(stim)])
@@ -170,7 +177,34 @@ def test_service_resync_matches_reference(name):
     assert np.array_equal(out["final_state"], np.where(exp["final_state"] == 7, 0, exp["final_state"]))
 
 
-@pytest.mark.parametrize("name", svc_dep_graph_files())
+@pytest.mark.parametrize("name", svc_p2p_files())
+def test_service_p2p_shuffle_lifecycle_matches_reference(name):
+    """The P2P shuffle's scheduler-side lifecycle (gen_service.py p2p): the unpacks' _rootish
+    set False when the first transfer runs (dgp_set_rootish), the barrier's completion
+    placing them on the device as non-rootish, each unpack's restrict_task (dgp_update_
+    restrictions) and Reschedule (the scheduler's stimulus, then dgp_sync_*), the re-placed
+    unpacks completing: every placement, snapshot and final state equals the reference's
+    ShuffleSchedulerPlugin-driven scheduler."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    assert {EV_SHUFFLE_INIT, EV_RESTRICT, EV_RESCHEDULE} <= set(np.unique(z["ev_kind"]).tolist())
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        stim = drive_events(eng, g, z, exp)
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert np.array_equal(stim, exp["stim_nplaced"]), np.nonzero(stim != exp["stim_nplaced"])[0][:5]
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+@pytest.mark.parametrize("name", svc_dep_graph_files() + svc_restr_graph_files())
 def test_service_dependent_later_graph_matches_reference(name):
     """A later graph whose tasks depend on earlier ones (in memory, processing, waiting or
     queued when it arrives): dgp_add_graph appends it (the earlier tasks' dependents rows
@@ -188,7 +222,8 @@ def test_service_dependent_later_graph_matches_reference(name):
     ptr = z["msg_round_ptr"].tolist()
     at = int(z["g2_msg"])
     g2 = second_graph(g, z)
-    assert (np.asarray(g2["dep_idx"]) < 0).sum() > 0
+    restr = "g2_restr_flags" in z.files  # svcgrst_*: worker restrictions on the later graph
+    assert restr or (np.asarray(g2["dep_idx"]) < 0).sum() > 0
     joins = {}
     for m, nt in zip(z["add_msg"].tolist() if "add_msg" in z.files else [],
                      z["add_nthreads"].tolist() if "add_nthreads" in z.files else []):
@@ -203,7 +238,7 @@ def test_service_dependent_later_graph_matches_reference(name):
                     eng.add_worker(nt)
                 if i == at:
                     n0 = eng.num_placements()
-                    assert eng.add_graph(g2) == 0 and eng.num_placements() == n0
+                    assert eng.add_graph(g2, defer=restr) == 0 and eng.num_placements() == n0
                     with pytest.raises(_lib.DgpError, match="dgp_sync"):  # nothing runs before the resync
                         eng.tasks_finished(*[[c] for c in msgs[i]])
                     sl = slice(n0, n0 + int(z["g2_nplaced"]))
@@ -211,6 +246,10 @@ def test_service_dependent_later_graph_matches_reference(name):
                                         exp["pl_start"][sl], exp["pl_wsnbytes"][sl], exp["pl_route"][sl])
                     d = sync_dump(z, 0)
                     eng.sync(None, d["tasks"], d["workers"], d["globals"])
+                    if restr:  # the new tasks' valid workers (dgp_update_restrictions)
+                        rp, ri, rf = z["g2_restr_ptr"], z["g2_restr_idx"], z["g2_restr_flags"]
+                        ts = np.flatnonzero(rf & 1)
+                        eng.update_restrictions(g["n_tasks"] + ts, [ri[rp[t]:rp[t + 1]] for t in ts], rf[ts])
                 st, _ = eng.tasks_finished(*[[c] for c in msgs[i]])
                 assert st.tolist() == [0], (i, st)
             if ptr[k + 1] > ptr[k]:
@@ -267,6 +306,11 @@ def test_task_messages_follow_replicas(name):
                 eng.heartbeat(float(z["ev_x"][i]), g["prefix_id"][ts], hd[hp[i]:hp[i + 1]])
             elif kd == EV_ERRED:
                 eng.task_erred(t)
+            elif kd == EV_SHUFFLE_INIT:  # _ensure_output_tasks_are_non_rootish: the unpacks' _rootish False
+                ts = ht[hp[i]:hp[i + 1]]
+                eng.set_rootish(ts, np.zeros(len(ts), np.int8))
+            elif kd == EV_RESTRICT:  # restrict_task -> set_restrictions({key: {worker}})
+                eng.update_restrictions([t], [[w]], [1])
             n1 = eng.num_placements()
             if n1 == n0:
                 continue

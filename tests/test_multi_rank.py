@@ -55,8 +55,9 @@ def _rank(rank, world, port, q):
         same = shard.replicas_agree(shard.output_digest([np.arange(10)]), "cpu")
         differ = shard.replicas_agree(shard.output_digest([np.arange(10) + rank]), "cpu")
         slowest = bench.reduce_max(1.0 + rank, dist, device="cpu")
+        total = bench.reduce_sum(10.0 + rank, dist, device="cpu")  # distinct per-rank work adds up
         dist.barrier()
-        q.put((rank, res, same, differ, slowest))
+        q.put((rank, res, same, differ, (slowest, total)))
     finally:
         dist.destroy_process_group()
 
@@ -76,7 +77,7 @@ def test_two_rank_row_exchange_gloo():
     for rank, merged, same, differ, slowest in res:
         assert all(merged.values()), (rank, merged)
         assert same and not differ
-        assert slowest == pytest.approx(2.0)
+        assert slowest == (pytest.approx(2.0), pytest.approx(21.0))
 
 
 @pytest.mark.parametrize("n", [0, 1, 5, 8, 9, 1000, 1001])
@@ -98,3 +99,4 @@ def test_shard_range_rejects_bad_args():
 
 def test_reduce_max_single_process():
     assert bench.reduce_max(3.5, None) == 3.5
+    assert bench.reduce_sum(3.5, None) == 3.5

@@ -24,7 +24,9 @@ print(f"run_rounds {dt:.3f}s  {e.num_placements() / dt / 1e6:.3f} M placements/s
 for i in range(16):
     print(f"  [{i:2d}] {names[i]:28s} {P[i]:>15d}  per stimulus {P[i] / n:10.1f}")
 X = [st[k] for k in ("cyc_setup", "cyc_local_steps", "cyc_global", "cyc_finish", "cyc_reserve", "cyc_max_step", "cyc_exec_max", "cyc_exec_sum")]
-for i, nm in enumerate(["global: rootish frontier", "REG fetch+phase A", "REG phase B", "REG prefetch issue", "global: kt > KT_MAX", "global: frontier kx/desc full", "global: touch/nf/staging", "global: queue rule (REG)"]):
+for i, nm in enumerate(["16 state load | global rootish", "17 compl. needs | REG fetch+A", "18 start/cand | REG phase B",
+                        "19 argmin+early | REG prefetch", "20 commit | global kt>KT_MAX", "21 | global kx/desc full",
+                        "22 | global touch/nf", "23 | global queue rule"]):
     print(f"  [x{i}] {nm:28s} {X[i]:>15d}  per stimulus {X[i] / n:10.1f}")
 
 S = [st.get(f"stall{i}", 0) for i in range(8)]
