@@ -306,10 +306,13 @@ def service_leg(eng_cls, local: int, args) -> dict:
            "n_tasks": int(g["n_tasks"])}
     outs = {}
     cols = ("pl_task", "pl_worker")
-    for mode in ("per_round", "per_message", "per_round_resident", "per_message_resident", "per_round_messages"):
+    for mode in ("per_round", "per_message", "per_round_resident", "per_message_resident", "per_round_messages",
+                 "per_message_resident_ext"):
         eng = eng_cls(local)
         eng.load(g, CONFIG, results=False)
-        eng.set_resident(mode.endswith("resident"))
+        eng.set_resident("resident" in mode)
+        if mode == "per_message_resident_ext":  # the answers carry the message fields (f3)
+            eng.set_task_messages(True)
         eng.update_graph()
         done, calls = 0, 0
         n = eng.num_placements()
@@ -332,8 +335,14 @@ def service_leg(eng_cls, local: int, args) -> dict:
                 n += k
                 calls += 1
             else:
+                ext = mode == "per_message_resident_ext"
                 for i in range(len(t)):
                     _, k = eng.tasks_finished(t[i:i + 1], w[i:i + 1], r[i:i + 1], nb[i:i + 1], a[i:i + 1], b[i:i + 1])
+                    if ext and k:  # what GPUPlacementExtension asks per message: the new placements
+                        # and their compute-task who_has / nbytes (both from the mailbox)
+                        eng.placements(n, k, columns=cols)
+                        m = eng.task_messages(n, k)
+                        n_dep += len(m["dep_task"])
                     n += k
                     calls += 1
         dt = time.perf_counter() - t0

@@ -33,6 +33,7 @@ SIGNATURES = {
     "dgp_run_rounds": (C.c_int, [_P, C.c_int64, _P]),
     "dgp_tasks_finished": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dgp_set_resident": (C.c_int, [_P, C.c_int]),
+    "dgp_set_task_messages": (C.c_int, [_P, C.c_int]),
     "dgp_move_task": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "dgp_add_worker": (C.c_int, [_P, C.c_int32, _P]),
     "dgp_add_graph": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P, _P]),
@@ -75,7 +76,7 @@ SIGNATURES = {
                                    _P, _P, _P]),
 }
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 _lib = None
 
 

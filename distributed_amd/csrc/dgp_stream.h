@@ -938,6 +938,70 @@ __device__ __attribute__((always_inline)) void snapshot(const Dev& D, SLds& L, c
 __device__ __forceinline__ unsigned long long sys_load(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// exclusive prefix sum over the wave's lanes
+__device__ __forceinline__ int wscan_excl(int v) {
+  int x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane_id() >= o) x += y;
+  }
+  return x - v;
+}
+
+// the compute-task message fields of placements [n0, n1) (_task_to_msg :3421-3450: who_has /
+// nbytes of every dependency; dgp_msgs.h's rows) into the mailbox, 64 placements per step,
+// each lane one placement; false when they exceed the mailbox's capacity (the host then asks
+// dgp_task_messages' kernels)
+__device__ __attribute__((noinline)) bool publish_messages(const Dev& D, svc::Mbox* mb, long long n0, long long n1) {
+  const int lane = lane_id();
+  int32_t* dptr = svc::mbox_m_dptr(mb);
+  int32_t* dtask = svc::mbox_m_dtask(mb);
+  int32_t* hptr = svc::mbox_m_hptr(mb);
+  int32_t* hidx = svc::mbox_m_hidx(mb);
+  int64_t* dnb = svc::mbox_m_dnb(mb);
+  const long long cap = mb->md_cap;
+  long long db = 0, hb = 0;
+  for (long long k0 = 0; k0 < n1 - n0; k0 += 64) {
+    const long long k = k0 + lane;
+    const bool act = k < n1 - n0;
+    const int t = act ? D.pl_task[n0 + k] : -1;
+    int64_t a = 0, b = 0;
+    int nh = 0;
+    if (t >= 0 && t < D.N) {
+      a = D.dep_ptr[t];
+      b = D.dep_ptr[t + 1];
+      for (int64_t q = a; q < b; q++) nh += msg::who_has_count(D, D.dep_idx[q]);
+    }
+    const int nd = (int)(b - a);
+    const int sd = wscan_excl(nd), sh = wscan_excl(nh);
+    const int td = wsum(nd), th = wsum(nh);
+    if (db + td > cap || hb + th > cap) return false;
+    if (act) {
+      dptr[k] = (int32_t)(db + sd);
+      long long e = db + sd, h = hb + sh;
+      for (int64_t q = a; q < b; q++, e++) {
+        const int d = D.dep_idx[q];
+        dtask[e] = d;
+        dnb[e] = D.cur_nbytes[d];
+        hptr[e] = (int32_t)h;
+        if (msg::multi_row(D, d)) {
+          for (int w8 = 0; w8 < D.WB; w8++)
+            for (unsigned long long m = D.holders[(size_t)d * D.WB + w8]; m; m &= m - 1) hidx[h++] = w8 * 64 + __builtin_ctzll(m);
+        } else if (D.holder_of[d] >= 0) {
+          hidx[h++] = D.holder_of[d];
+        }
+      }
+    }
+    db += td;
+    hb += th;
+  }
+  if (lane == 0) {
+    dptr[n1 - n0] = (int32_t)db;
+    hptr[db] = (int32_t)hb;
+  }
+  return true;
+}
+
 __device__ __attribute__((noinline)) bool resident_serve(const Dev& D, SLds& L) {
   SCtl& S = L.c;
   const int lane = lane_id();
@@ -1000,7 +1064,10 @@ __device__ __attribute__((noinline)) bool resident_serve(const Dev& D, SLds& L) 
           pt[k] = D.pl_task[n0 + k];
           pw[k] = D.pl_worker[n0 + k];
         }
+      const bool mok = __builtin_amdgcn_readfirstlane(mb->want_msgs) != 0 && n1 - n0 <= mb->mp_cap &&
+                       publish_messages(D, mb, n0, n1);
       if (lane == 0) {
+        mb->msg_from = mok ? n0 : -1;
         mb->pl_from = n1 - n0 <= cap ? n0 : -1;
         mb->n_placed = n1;
         mb->error = S.error;

@@ -82,7 +82,11 @@ __device__ __forceinline__ bool answer(const Dev& D, const Msg& m, long long len
 }
 
 // The resident service kernel's mailbox, in pinned, coherent host memory: the header, then
-// cap messages, cap statuses and pl_cap (task, worker) pairs of the request's new placements.
+// cap messages, cap statuses and pl_cap (task, worker) pairs of the request's new placements;
+// then, when the host asks for them (want_msgs), the compute-task message fields of those
+// placements (_task_to_msg :3421-3450, as dgp_task_messages): per placement its first
+// dependency entry (m_dptr, mp_cap + 1), per dependency entry the task, its first holder
+// (m_hptr, md_cap + 1) and nbytes, and the holders (m_hidx, md_cap).
 struct Mbox {
   unsigned long long req_seq;   // host: the request number, stored after the request
   unsigned long long done_seq;  // device: the last request answered (after its answers)
@@ -97,9 +101,17 @@ struct Mbox {
   // device: when each role last finished a batch (builder, prefetcher, registrar, executor
   // claim, executor done, sequencer retire, walker), copied at publish (diagnostics)
   unsigned long long t_role[7];
+  long long mp_cap, md_cap;     // host: capacities of the message arrays (placements, entries)
+  long long msg_from;           // device: log position of the first placement with message
+                                // fields (-1: none this request: not asked for, or too many)
+  int want_msgs;                // host: publish the message fields with the answers
 };
-__host__ __device__ inline size_t mbox_bytes(long long cap, long long pl_cap) {
-  return 256 + (size_t)cap * sizeof(Msg) + (((size_t)cap + 15) & ~(size_t)15) + (size_t)pl_cap * 8;
+__host__ __device__ inline size_t mbox_al(size_t b) { return (b + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t mbox_bytes(long long cap, long long pl_cap, long long mp_cap = 0,
+                                             long long md_cap = 0) {
+  return 256 + (size_t)cap * sizeof(Msg) + mbox_al((size_t)cap) + mbox_al((size_t)pl_cap * 8) +
+         mbox_al((size_t)(mp_cap + 1) * 4) + mbox_al((size_t)md_cap * 4) + mbox_al((size_t)(md_cap + 1) * 4) +
+         mbox_al((size_t)md_cap * 4) + (size_t)md_cap * 8;
 }
 __host__ __device__ inline Msg* mbox_msgs(Mbox* m) { return (Msg*)((char*)m + 256); }
 __host__ __device__ inline int8_t* mbox_status(Mbox* m) { return (int8_t*)(mbox_msgs(m) + m->cap); }
@@ -107,6 +119,21 @@ __host__ __device__ inline int32_t* mbox_pl_task(Mbox* m) {
   return (int32_t*)((char*)mbox_status(m) + ((m->cap + 15) & ~15ll));
 }
 __host__ __device__ inline int32_t* mbox_pl_worker(Mbox* m) { return mbox_pl_task(m) + m->pl_cap; }
+__host__ __device__ inline int32_t* mbox_m_dptr(Mbox* m) {
+  return (int32_t*)((char*)mbox_pl_task(m) + mbox_al((size_t)m->pl_cap * 8));
+}
+__host__ __device__ inline int32_t* mbox_m_dtask(Mbox* m) {
+  return (int32_t*)((char*)mbox_m_dptr(m) + mbox_al((size_t)(m->mp_cap + 1) * 4));
+}
+__host__ __device__ inline int32_t* mbox_m_hptr(Mbox* m) {
+  return (int32_t*)((char*)mbox_m_dtask(m) + mbox_al((size_t)m->md_cap * 4));
+}
+__host__ __device__ inline int32_t* mbox_m_hidx(Mbox* m) {
+  return (int32_t*)((char*)mbox_m_hptr(m) + mbox_al((size_t)(m->md_cap + 1) * 4));
+}
+__host__ __device__ inline int64_t* mbox_m_dnb(Mbox* m) {
+  return (int64_t*)((char*)mbox_m_hidx(m) + mbox_al((size_t)m->md_cap * 4));
+}
 static_assert(sizeof(Mbox) <= 256, "mailbox header");
 
 }  // namespace svc

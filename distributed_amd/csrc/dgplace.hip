@@ -27,11 +27,11 @@
 
 #include "../../include/dgplace.h"
 #include "dgp_device.h"
+#include "dgp_msgs.h"
 #include "dgp_stream.h"
 #include "dgp_events.h"
 #include "dgp_steal.h"
 #include "dgp_service.h"
-#include "dgp_msgs.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -112,6 +112,7 @@ struct dgp_engine {
   dgp::svc::Mbox* mb = nullptr;      // host address
   dgp::svc::Mbox* mb_dev = nullptr;  // device address
   bool resident = false;             // service calls go through the resident kernel
+  bool res_msgs = false;             // the resident answers carry the compute-task message fields
   bool res_running = false;          // the resident kernel was launched (it may have ended since)
   bool res_hung = false;             // the resident kernel did not end when told to: the engine is unusable
   bool pending_resync = false;       // a later graph with dependencies on earlier tasks: dgp_sync_* next
@@ -1188,12 +1189,16 @@ int tasks_finished_resident(dgp_engine* e, int64_t n, const int32_t* task, const
     if (e->mb) (void)hipHostFree(e->mb);
     e->mb = nullptr;
     const int64_t cap = std::max<int64_t>(n, 4096);
+    const int64_t mpc = std::min<int64_t>(plc, 65536), mdc = 8 * mpc;  // message fields: placements, entries
     void* p = nullptr;
-    HIPCHK(e, hipHostMalloc(&p, V::mbox_bytes(cap, plc), hipHostMallocCoherent | hipHostMallocMapped));
+    HIPCHK(e, hipHostMalloc(&p, V::mbox_bytes(cap, plc, mpc, mdc), hipHostMallocCoherent | hipHostMallocMapped));
     memset(p, 0, sizeof(V::Mbox));  // the whole header (t_role included)
     e->mb = (V::Mbox*)p;
     e->mb->cap = cap;
     e->mb->pl_cap = plc;
+    e->mb->mp_cap = mpc;
+    e->mb->md_cap = mdc;
+    e->mb->msg_from = -1;
     e->mb->req_seq = e->mb->done_seq = e->req_seq;
     void* pd = nullptr;
     HIPCHK(e, hipHostGetDevicePointer(&pd, p, 0));
@@ -1208,6 +1213,8 @@ int tasks_finished_resident(dgp_engine* e, int64_t n, const int32_t* task, const
   V::Msg* M = V::mbox_msgs(e->mb);
   for (int64_t i = 0; i < n; i++) M[i] = V::Msg{task[i], worker[i], run_id[i], nbytes[i], start[i], stop[i]};
   e->mb->n = n;
+  e->mb->want_msgs = e->res_msgs ? 1 : 0;
+  e->mb->msg_from = -1;
   auto launch = [&]() -> int {
     if (int rc = sync_dev(e)) return rc;
     stream_source(e, true);
@@ -1279,6 +1286,12 @@ int tasks_finished_resident(dgp_engine* e, int64_t n, const int32_t* task, const
 }  // namespace
 
 extern "C" {
+
+int dgp_set_task_messages(dgp_engine* e, int enabled) {
+  if (!e) return DGP_E_ARG;
+  e->res_msgs = enabled != 0;
+  return 0;
+}
 
 int dgp_set_resident(dgp_engine* e, int enabled) {
   if (!e) return DGP_E_ARG;
@@ -2203,6 +2216,30 @@ int dgp_get_placements(dgp_engine* e, int64_t offset, int64_t count, int32_t* ta
 int dgp_task_messages(dgp_engine* e, int64_t offset, int64_t count, int64_t* n_deps, int64_t* n_holders,
                       int64_t* dep_ptr, int32_t* dep_task, int64_t* dep_nbytes, int64_t* holder_ptr,
                       int32_t* holder_idx) {
+  if (e && e->res_running && n_deps && n_holders && offset >= 0 && count >= 0) {
+    // the last resident answer's placements: their fields are in the mailbox (dgp_set_task_messages)
+    namespace V = dgp::svc;
+    V::Mbox* m = e->mb;
+    const int64_t a = m->msg_from, b = m->n_placed;
+    if (a >= 0 && offset >= a && offset + count <= b) {
+      const int32_t* dp = V::mbox_m_dptr(m) + (offset - a);
+      const int32_t* hp = V::mbox_m_hptr(m);
+      const int64_t d0 = dp[0], d1 = dp[count], h0 = hp[d0], h1 = hp[d1];
+      *n_deps = d1 - d0;
+      *n_holders = h1 - h0;
+      if (!dep_ptr) return 0;  // size query
+      if (!dep_task || !dep_nbytes || !holder_ptr || (h1 > h0 && !holder_idx))
+        return fail(e, DGP_E_ARG, "dgp_task_messages: output arrays missing");
+      for (int64_t j = 0; j <= count; j++) dep_ptr[j] = dp[j] - d0;
+      for (int64_t k = d0; k <= d1; k++) holder_ptr[k - d0] = hp[k] - h0;
+      if (d1 > d0) {
+        memcpy(dep_task, V::mbox_m_dtask(m) + d0, (size_t)(d1 - d0) * 4);
+        memcpy(dep_nbytes, V::mbox_m_dnb(m) + d0, (size_t)(d1 - d0) * 8);
+      }
+      if (h1 > h0) memcpy(holder_idx, V::mbox_m_hidx(m) + h0, (size_t)(h1 - h0) * 4);
+      return 0;
+    }
+  }
   if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
   if (offset < 0 || count < 0 || !n_deps || !n_holders) return fail(e, DGP_E_ARG, "dgp_task_messages: bad arguments");

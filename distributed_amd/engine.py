@@ -184,6 +184,11 @@ class PlacementEngine:
         tasks_finished calls and takes each batch from a pinned mailbox."""
         self._check(self.lib.dgp_set_resident(self.h, 1 if on else 0), "dgp_set_resident")
 
+    def set_task_messages(self, on: bool = True):
+        """Resident answers carry their placements' compute-task message fields
+        (dgp_set_task_messages): task_messages of the last answer reads the mailbox."""
+        self._check(self.lib.dgp_set_task_messages(self.h, 1 if on else 0), "dgp_set_task_messages")
+
     def move_task(self, task: int, thief: int):
         """Steal confirmation (WorkStealing.move_task_confirm, distributed/stealing.py
         :376-384): processing ``task`` moves from its worker to ``thief`` on the device."""

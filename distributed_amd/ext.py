@@ -90,6 +90,20 @@ _ENGINE_EVENTS = ("add_replicas", "remove_replicas", "set_worker_status", "long_
                   "set_worker_flags", "set_wanted", "task_erred", "update_restrictions", "set_rootish")
 
 
+_SM = None
+
+
+def _sched_mod():
+    """distributed.scheduler, imported once (the compute-task message's TaskState run_id
+    counter, time and ToPickle)."""
+    global _SM
+    if _SM is None:
+        from distributed import scheduler
+
+        _SM = scheduler
+    return _SM
+
+
 def _compute_interval(startstops):
     """The "compute" startstop of a task-finished message (TaskGroup.add_duration is fed
     every startstop; only "compute" moves TaskPrefix.duration_average, :977-985)."""
@@ -217,6 +231,11 @@ class GPUPlacementExtension(SchedulerPlugin):
         self.removed: set = set()   # addresses of removed workers (they keep their engine index)
         self._rootish_h: dict = {}  # key -> the _rootish override the engine holds (-1 / 0 / 1)
         self._restr_h: dict = {}    # key -> (restriction flags, valid worker indices) the engine holds
+        # key -> (message batch, row): the who_has / nbytes of the compute-task message of an
+        # engine placement not yet sent (dgp_task_messages, fetched with the placements)
+        self._msg_of: dict = {}
+        self.engine_messages = True
+        self.n_engine_messages = 0
         if hasattr(scheduler, "add_plugin"):
             scheduler.add_plugin(self, name=self.name)
         elif isinstance(getattr(scheduler, "plugins", None), dict):  # a bare SchedulerState
@@ -250,6 +269,17 @@ class GPUPlacementExtension(SchedulerPlugin):
 
             s._add_to_processing = add_to_processing
             s._gpu_placement_add = True
+        if not getattr(s, "_gpu_placement_msg", False) and callable(getattr(s, "_task_to_msg", None)):
+            ref_msg = s._task_to_msg
+
+            def task_to_msg(ts, duration=-1):
+                m = self._msg_of.pop(ts.key, None)
+                if m is None or not self.active:
+                    return ref_msg(ts, duration)
+                return self._engine_task_msg(ts, duration, *m)
+
+            s._task_to_msg = task_to_msg
+            s._gpu_placement_msg = True
         if callable(getattr(s, "handle_stream", None)) and not getattr(s, "_gpu_placement_stream", False):
             s.handle_stream = self.handle_stream  # per instance: Server.handle_stream stays untouched
             s._gpu_placement_stream = True
@@ -691,21 +721,75 @@ class GPUPlacementExtension(SchedulerPlugin):
                 "unknown_duration": float(s.UNKNOWN_TASK_DURATION),
                 "saturation": "inf" if math.isinf(sat) else float(sat)}
 
-    def _fetch(self, n_new=None):
+    def _fetch(self, n_new=None, messages=True):
         """Queue the engine's new placements (the decisions the transitions will ask for);
-        ``n_new``: how many the last engine call reported (saves a device round trip)."""
+        ``n_new``: how many the last engine call reported (saves a device round trip).
+        ``messages``: also take their compute-task messages' who_has / nbytes from the
+        engine (dgp_task_messages: its replica state after the call, which is the state each
+        message is built in when the call was one stimulus, or several whose later members
+        add no replica of an earlier one's dependencies)."""
         n = self.engine.num_placements() if n_new is None else self.n_fetched + n_new
         if n > self.n_fetched:
-            pl = self.engine.placements(self.n_fetched, n - self.n_fetched, columns=("pl_task", "pl_worker"))
+            n0 = self.n_fetched
+            pl = self.engine.placements(n0, n - n0, columns=("pl_task", "pl_worker"))
             keys, dev_run, pending = self.keys, self.dev_run, self.pending
-            j = self.n_fetched
-            for t, w in zip(pl["pl_task"].tolist(), pl["pl_worker"].tolist()):
+            j = n0
+            tasks = pl["pl_task"].tolist()
+            for t, w in zip(tasks, pl["pl_worker"].tolist()):
                 pending.append((t, w))
                 dev_run[keys[t]] = j
                 j += 1
             self.n_fetched = n
+            if messages and self.engine_messages and hasattr(self.engine, "task_messages"):
+                m = self.engine.task_messages(n0, n - n0)
+                batch = tuple(m[k].tolist() for k in ("dep_ptr", "dep_task", "dep_nbytes", "holder_ptr", "holder_idx"))
+                msg_of = self._msg_of
+                for i, t in enumerate(tasks):
+                    msg_of[keys[t]] = (batch, i)
+
+    def _engine_task_msg(self, ts, duration, batch, i):
+        """``SchedulerState._task_to_msg`` (scheduler.py:3421-3450) for a placement the engine
+        made, its ``who_has`` / ``nbytes`` from the engine's batch (dgp_task_messages: the
+        dependencies in CSR order, their holders ascending by worker index) instead of a
+        walk over the dependencies' replica sets; every other field as there."""
+        sm = _sched_mod()
+        dep_ptr, dep_task, dep_nbytes, holder_ptr, holder_idx = batch
+        keys, addrs = self.keys, self.workers
+        who_has, nbytes = {}, {}
+        for k in range(dep_ptr[i], dep_ptr[i + 1]):
+            dk = keys[dep_task[k]]
+            h0, h1 = holder_ptr[k], holder_ptr[k + 1]
+            who_has[dk] = [addrs[holder_idx[h0]]] if h1 == h0 + 1 else [addrs[h] for h in holder_idx[h0:h1]]
+            nbytes[dk] = dep_nbytes[k]
+        if self.validate:
+            ref_who = {d.key: sorted(ws.address for ws in d.who_has or ()) for d in ts.dependencies}
+            ref_nb = {d.key: d.nbytes for d in ts.dependencies}
+            if {k: sorted(v) for k, v in who_has.items()} != ref_who or nbytes != ref_nb:
+                raise AssertionError(f"gpu-placement: compute-task message of {ts.key!r}: engine who_has "
+                                     f"{who_has} nbytes {nbytes}, the reference {ref_who} {ref_nb}")
+        if duration < 0:
+            duration = self.scheduler.get_task_duration(ts)
+        ts.run_id = next(sm.TaskState._run_id_iterator)
+        assert ts.priority, ts
+        self.n_engine_messages += 1
+        return {
+            "op": "compute-task",
+            "key": ts.key,
+            "run_id": ts.run_id,
+            "priority": ts.priority,
+            "duration": duration,
+            "stimulus_id": f"compute-task-{sm.time()}",
+            "who_has": who_has,
+            "nbytes": nbytes,
+            "run_spec": sm.ToPickle(ts.run_spec),
+            "resource_restrictions": ts.resource_restrictions,
+            "actor": ts.actor,
+            "annotations": ts.annotations or {},
+            "span_id": ts.group.span_id,
+        }
 
     def _end_of_stimulus(self, what: str):
+        self._msg_of.clear()
         if self.active and self.pending:
             t, w = self.pending[0]
             self.fallback(f"{what}: the engine placed {self.keys[t]!r} on {self.workers[w]} but the scheduler "
@@ -868,6 +952,9 @@ class GPUPlacementExtension(SchedulerPlugin):
                 # task-finished batches through the resident kernel (dgp_set_resident): no
                 # launch / copy / sync per call; every other engine call ends it first
                 self.engine.set_resident(True)
+                if self.engine_messages and hasattr(self.engine, "set_task_messages"):
+                    # ... and their answers carry the compute-task message fields (f3)
+                    self.engine.set_task_messages(True)
                 self.engine.update_graph()
                 self._fetch()
                 self.stats["graphs"] += 1
@@ -1210,9 +1297,12 @@ class GPUPlacementExtension(SchedulerPlugin):
             cols = list(zip(*fields))
             try:
                 status, n_new = self.engine.tasks_finished(*cols)
-                self._fetch(n_new)
-                self.stats["messages"] += len(msgs)
                 status = status.tolist()
+                # an already-in-memory report (add_keys) adds a replica after the placements
+                # of the messages before it: those compute-task messages take who_has from
+                # the scheduler, as built at their time (the reference's own _task_to_msg)
+                self._fetch(n_new, messages=len(status) == 1 or 2 not in status)
+                self.stats["messages"] += len(msgs)
                 # DGP_TF_RELEASE / _IMPOSSIBLE / _UNSUPPORTED: the reference reschedules or
                 # raises; the engine does not follow those transitions
                 if any(st >= 3 and st != 4 for st in status):

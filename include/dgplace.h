@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 12
+#define DGP_ABI_VERSION 13
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -180,6 +180,14 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
  * runs, dgp_num_placements and dgp_get_placements of the last answer's placements (task /
  * worker columns only) read the mailbox. */
 int dgp_set_resident(dgp_engine* e, int enabled);
+
+/* (ABI 13) With `enabled`, every resident answer also carries the compute-task message
+ * fields of its new placements (who_has / nbytes per dependency, as dgp_task_messages; the
+ * kernel's sequencer writes them into the mailbox before it publishes the answer), and
+ * dgp_task_messages of those placements reads the mailbox: no kernel stop, no launch, no
+ * copy. Replaces the per-placement walk of SchedulerState._task_to_msg (scheduler.py
+ * :3421-3450) over the dependencies' who_has sets for the extension's batches. */
+int dgp_set_task_messages(dgp_engine* e, int enabled);
 
 /* Steal confirmation (WorkStealing.move_task_confirm, stealing.py:333-399, its "confirm"
  * branch :376-384 and finally clause :396-399): processing task `task` leaves its worker

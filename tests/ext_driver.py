@@ -35,6 +35,7 @@ if os.environ.get("PYTHONHASHSEED") != "0":
     sys.exit(subprocess.call([sys.executable] + sys.argv, env=dict(os.environ, PYTHONHASHSEED="0")))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
 
 import gen_golden as G  # noqa: E402  (shim + reference)
 
@@ -63,9 +64,21 @@ class FixtureEngine:
 
     def load(self, g, config, results=True):
         self.graph, self.config = g, config
+        self.deps = []  # engine index -> its dependencies' engine indices (CSR order)
+        self._append_deps(g)
+        self.who, self.nb = {}, {}  # replicas / reported sizes as the engine holds them
+
+    def _append_deps(self, g):
+        base = len(self.deps)
+        dp, di = np.asarray(g["dep_ptr"]), np.asarray(g["dep_idx"])
+        for i in range(len(dp) - 1):
+            self.deps.append([int(d) + base if d >= 0 else -1 - int(d) for d in di[dp[i]:dp[i + 1]]])
 
     def set_resident(self, on=True):  # the real engine's launch mode: nothing to serve here
         self.resident = bool(on)
+
+    def set_task_messages(self, on=True):  # the real engine's mailbox message fields: task_messages below
+        self.task_msgs = bool(on)
 
     def update_graph(self):
         self.n, self.k = self.stim[0], 1
@@ -73,10 +86,27 @@ class FixtureEngine:
     def tasks_finished(self, task, worker, run_id, nbytes=None, start=None, stop=None):
         self.calls_tf += 1
         n0 = self.n
-        for _ in task:  # genuine completions only in this protocol
+        for i, t in enumerate(task):  # genuine completions only in this protocol
             self.n += self.stim[self.k]
             self.k += 1
+            self.who[int(t)] = {int(worker[i])}
+            self.nb[int(t)] = -1 if nbytes is None else int(nbytes[i])
         return np.zeros(len(task), np.int8), self.n - n0
+
+    def task_messages(self, offset, count):
+        """dgp_task_messages' arrays from the replicas this stand-in tracked (the placement
+        log's tasks from placements(); holders ascending)."""
+        tasks = self.placements(offset, count)["pl_task"].tolist()
+        ptr, dt, dn, hp, hi = [0], [], [], [0], []
+        for t in tasks:
+            for d in self.deps[t]:
+                dt.append(d)
+                dn.append(self.nb.get(d, -1))
+                hi.extend(sorted(self.who.get(d, ())))
+                hp.append(len(hi))
+            ptr.append(len(dt))
+        return dict(dep_ptr=np.array(ptr, np.int64), dep_task=np.array(dt, np.int32), dep_nbytes=np.array(dn, np.int64),
+                    holder_ptr=np.array(hp, np.int64), holder_idx=np.array(hi, np.int32))
 
     def num_placements(self):
         return self.n
@@ -92,6 +122,7 @@ class FixtureEngine:
 
     def add_graph(self, g, defer=False):  # a later graph (the fixture's per-event placement counts)
         self.graphs.append(g)
+        self._append_deps(g)
         if defer or (np.asarray(g["dep_idx"]) < 0).any():  # appended, the scheduler's stimulus, then sync()
             return 0
         return self.add_worker(0)
@@ -141,9 +172,9 @@ def check_upload(g_up, keys_up, g_fx, fkeys):
 
 
 def check_messages(g, exp, sent, fkeys):
-    """The batch-built compute-task fields (distributed_amd/messages.py) against the
+    """The host-model compute-task fields (tests/msg_model.py) against the
     reference's own messages: key, priority, who_has, nbytes, run_id order."""
-    from distributed_amd.messages import compute_task_batch, render_messages
+    from msg_model import compute_task_batch, render_messages
 
     n = len(exp["pl_task"])
     assert len(sent) == n, (len(sent), n)
@@ -244,10 +275,28 @@ def run(name, diverge=False, stream=False, plain=False, validate=True):
         pos = np.cumsum(stim) - stim
         k = next(i for i in range(1, len(stim)) if stim[i] >= 2 and exp["pl_task"][pos[i]] != exp["pl_task"][pos[i] + 1])
         eng.diverge = int(pos[k])
+    S._task_to_msg = orig_msg  # the extension wraps the instance's: every message recorded below
+    eng.t_engine = 0.0
+    for nm_ in ("tasks_finished", "placements", "task_messages", "num_placements"):
+        def timed(*a, _f=getattr(eng, nm_), **k):
+            t0_ = _time.perf_counter()
+            try:
+                return _f(*a, **k)
+            finally:
+                eng.t_engine += _time.perf_counter() - t0_
+        setattr(eng, nm_, timed)
     ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=validate)
     eng.ext = ext
     s.stream_handlers = {}
     ext._install()  # with the stream handler table in place
+    ext_msg = s._task_to_msg
+
+    def record_msg(ts, duration=-1):
+        m = ext_msg(ts, duration)
+        sent.append(m)
+        return m
+
+    s._task_to_msg = record_msg
     # Scheduler._create_taskstate_from_graph's tail (:4600-4653): plugin hook, then transitions
     priority = {ts.key: ts.priority for ts in tss}
     recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
@@ -301,8 +350,14 @@ def run(name, diverge=False, stream=False, plain=False, validate=True):
     assert rec["wsnbytes"] == exp["pl_wsnbytes"].tolist()
     if not diverge:
         assert ext.stats["device_decisions"] == n, (ext.stats, n)
+        # every compute-task message built from the engine's batch (dgp_task_messages)
+        assert ext.n_engine_messages == n, (ext.n_engine_messages, n)
         check_messages(g, exp, sent, fkeys)
     return dict(fixture=name, placements=n, messages=n_msgs, device_decisions=ext.stats["device_decisions"],
+                engine_messages=ext.n_engine_messages,
+                # the extension and the reference handler without the stand-in engine's own time
+                # (on the box the engine call replaces it: bench.py service leg)
+                us_per_message_host=round(1e6 * (t_msgs - eng.t_engine) / max(n_msgs, 1), 2),
                 device_queued=ext.stats["device_queued"], device_no_worker=ext.stats["device_no_worker"],
                 active=ext.active, reason=ext.reason, engine_calls=eng.calls_tf, reads=n_reads,
                 us_per_message=round(1e6 * t_msgs / max(n_msgs, 1), 2), mode="stream" if stream else "handler")
@@ -549,9 +604,13 @@ class EventEngine(FixtureEngine):
         return k
 
     def add_replicas(self, t, w):
+        for a, b in zip(t, w):
+            self.who.setdefault(int(a), set()).add(int(b))
         return self._event("add", [int(x) for x in t], [int(x) for x in w])
 
     def remove_replicas(self, t, w):
+        for a, b in zip(t, w):
+            self.who.get(int(a), set()).discard(int(b))
         return self._event("remove", [int(x) for x in t], [int(x) for x in w])
 
     def set_worker_status(self, w, running):
@@ -592,6 +651,13 @@ class EventEngine(FixtureEngine):
         assert n == k, (n, k)  # the scheduler's placements of that stimulus
         self.n += k
         self.k += 1
+        # the replicas as the scheduler holds them after its stimulus (what the sync carries)
+        e = self.ext
+        for key, i in e.task_index.items():
+            ts = e.scheduler.tasks.get(key)
+            if ts is not None:
+                self.who[i] = {e.worker_index[ws.address] for ws in ts.who_has or ()}
+                self.nb[i] = ts.nbytes
 
     def sync_placements(self, *a):  # the extension calls sync(); these only mark the capability
         raise AssertionError("sync() expected")

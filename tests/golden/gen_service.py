@@ -807,6 +807,30 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
 
     S._add_to_processing = add_to_processing
     run_of.extend([int(tss[t].run_id) for t in rec["task"]])  # update_graph's, already made
+    # the compute-task messages the reference builds from here on (_task_to_msg :3421-3450),
+    # one per placement-log entry: who_has (holder indices, ascending) and nbytes per
+    # dependency, in the graph's dep_idx order
+    n_ug = len(rec["task"])
+    tm = {"task": [], "dep_ptr": [0], "dep_task": [], "dep_nbytes": [], "hold_ptr": [0], "hold_idx": []}
+    orig_msg = S._task_to_msg
+    dp, di = g["dep_ptr"], g["dep_idx"]
+
+    def task_to_msg(self, ts, duration=-1):
+        m = orig_msg(self, ts, duration)
+        t = tidx[ts.key]
+        deps = di[dp[t]:dp[t + 1]].tolist()
+        assert sorted(tidx[k] for k in m["who_has"]) == sorted(deps) == sorted(tidx[k] for k in m["nbytes"])
+        tm["task"].append(t)
+        for d in deps:
+            k = tss[d].key
+            tm["dep_task"].append(d)
+            tm["dep_nbytes"].append(int(m["nbytes"][k]))
+            tm["hold_idx"].extend(sorted(widx[a] for a in m["who_has"][k]))
+            tm["hold_ptr"].append(len(tm["hold_idx"]))
+        tm["dep_ptr"].append(len(tm["dep_task"]))
+        return m
+
+    S._task_to_msg = task_to_msg
     while True:
         cur = len(rec["task"])
         batch = list(range(done, cur))
@@ -838,8 +862,19 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             push(EV_FINISHED, t, w, math.nan, int(g["nbytes"][t]), float(g["start"][t]), float(g["stop"][t]), pos)
         round_ptr.append(len(ev["kind"]))
     rec["stim"] = stim
+    S._task_to_msg = orig_msg
+    assert len(tm["task"]) == len(rec["task"]) - n_ug and tm["task"] == rec["task"][n_ug:]
+    ev["tm"] = dict(tm, first=n_ug)
     states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
     return rec, rounds, nplaced, states, ev, hb, round_ptr
+
+
+def _tm_arrays(tm):
+    """The recorded compute-task messages as fixture arrays (tm_*)."""
+    return dict(tm_first=np.int64(tm["first"]), tm_task=np.array(tm["task"], np.int32),
+                tm_dep_ptr=np.array(tm["dep_ptr"], np.int64), tm_dep_task=np.array(tm["dep_task"], np.int32),
+                tm_dep_nbytes=np.array(tm["dep_nbytes"], np.int64), tm_hold_ptr=np.array(tm["hold_ptr"], np.int64),
+                tm_hold_idx=np.array(tm["hold_idx"], np.int32))
 
 
 def replay_p2p(g, cfg, dumps):
@@ -1024,6 +1059,7 @@ def main_events(only):
                  ev_stop=np.array(ev["stop"]), ev_runid=np.array(ev["runid"], np.int64),
                  hb_ptr=np.array(hb["ptr"], np.int64), hb_task=np.array(hb["task"], np.int32),
                  hb_dur=np.array(hb["dur"], np.float64), ev_round_ptr=np.array(round_ptr, np.int64))
+        z.update(_tm_arrays(ev["tm"]))
         np.savez_compressed(path, **z)
         cnt = np.bincount(np.array(ev["kind"]), minlength=8).tolist()
         print(f"{name}: {len(ev['kind'])} events (by kind {cnt}), {len(rec['task'])} placements")

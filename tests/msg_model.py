@@ -1,4 +1,6 @@
-"""compute-task messages for a batch of the engine's placements.
+"""Host-side model of the compute-task message fields of a batch of placements (test
+infrastructure: the checker of tests/ext_driver.py and tests/test_messages.py; the
+product builds them from dgp_task_messages, distributed_amd/ext.py _engine_task_msg).
 
 The reference builds one dict per placement in ``SchedulerState._task_to_msg``
 (scheduler.py:3421-3450): ``who_has`` / ``nbytes`` of every dependency, the task's

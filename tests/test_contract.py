@@ -115,6 +115,7 @@ def test_engine_returns_what_the_extension_consumes():
         # the same through the resident kernel (the extension's mode): the placements of the
         # answer come from the mailbox, columns as the extension asks for them
         eng.set_resident(True)
+        eng.set_task_messages(True)
         n1 = eng.num_placements()
         t2, w2 = int(pl["pl_task"][1]), int(pl["pl_worker"][1])  # still processing (run_id 1)
         st2, newp2 = eng.tasks_finished([t2], [w2], [1], [int(g["nbytes"][t2])], [0.0], [0.01])
@@ -122,6 +123,11 @@ def test_engine_returns_what_the_extension_consumes():
         assert eng.num_placements() == n1 + newp2
         pr = eng.placements(n1, newp2, columns=("pl_task", "pl_worker"))
         assert set(pr) == {"pl_task", "pl_worker"} and pr["pl_task"].dtype == np.int32 and len(pr["pl_worker"]) == newp2
+        # ext.py _fetch: the answer's compute-task message fields (from the mailbox)
+        m = eng.task_messages(n1, newp2)
+        assert m["dep_ptr"].dtype == np.int64 and len(m["dep_ptr"]) == newp2 + 1
+        assert m["dep_task"].dtype == np.int32 and len(m["dep_task"]) == m["dep_ptr"][-1] == len(m["dep_nbytes"])
+        assert m["holder_ptr"][-1] == len(m["holder_idx"])
         eng.set_resident(False)
         # event calls: the counts the extension's _fetch picks up afterwards
         assert eng.add_replicas([t], [(w + 1) % 16]) is None

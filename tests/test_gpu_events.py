@@ -262,8 +262,9 @@ def test_service_dependent_later_graph_matches_reference(name):
     assert np.array_equal(out["final_state"], exp["final_state"])
 
 
+@pytest.mark.parametrize("resident", [False, True], ids=["launch", "resident"])
 @pytest.mark.parametrize("name", svc_event_files())
-def test_task_messages_follow_replicas(name):
+def test_task_messages_follow_replicas(name, resident):
     """dgp_task_messages (the who_has / nbytes fields of _task_to_msg, scheduler.py
     :3421-3450) after every event of a svcev_* stream, for the placements that event made:
     each dependency's who_has equals a model of SchedulerState.who_has driven by the same
@@ -278,9 +279,12 @@ def test_task_messages_follow_replicas(name):
     hp, ht, hd = z["hb_ptr"], z["hb_task"], z["hb_dur"]
     dp, di = g["dep_ptr"], g["dep_idx"]
     who, nbytes = {}, {}
-    checked = multi = 0
+    checked = multi = pinned = 0
     with PlacementEngine(0) as eng:
         eng.load(g, cfg, results=False)
+        if resident:  # the task-finished answers carry the message fields (dgp_set_task_messages)
+            eng.set_resident(True)
+            eng.set_task_messages(True)
         eng.update_graph()
         for i in range(len(kind)):
             n0 = eng.num_placements()
@@ -315,15 +319,28 @@ def test_task_messages_follow_replicas(name):
             if n1 == n0:
                 continue
             m = eng.task_messages(n0, n1 - n0)
-            pl = eng.placements(n0, n1 - n0)
+            pl = eng.placements(n0, n1 - n0, columns=("pl_task", "pl_worker"))  # (the mailbox, resident)
             for j, x in enumerate(pl["pl_task"].tolist()):
                 deps = di[dp[x]:dp[x + 1]].tolist()
                 a, b = int(m["dep_ptr"][j]), int(m["dep_ptr"][j + 1])
                 assert m["dep_task"][a:b].tolist() == deps, (i, x)
+                # the reference's own message for this placement (gen_service.py records
+                # _task_to_msg's who_has / nbytes per placement after update_graph)
+                r = n0 + j - int(z["tm_first"])
+                if r >= 0:
+                    assert int(z["tm_task"][r]) == x, (i, x)
+                    ra = int(z["tm_dep_ptr"][r])
+                    assert z["tm_dep_task"][ra:ra + b - a].tolist() == deps
                 for k, d in zip(range(a, b), deps):
                     hs = m["holder_idx"][m["holder_ptr"][k]:m["holder_ptr"][k + 1]].tolist()
                     assert hs == sorted(who[d]), (i, x, d, hs, who[d])
                     assert int(m["dep_nbytes"][k]) == nbytes[d], (i, x, d)
+                    if r >= 0:
+                        rk = ra + k - a
+                        rh = z["tm_hold_idx"][z["tm_hold_ptr"][rk]:z["tm_hold_ptr"][rk + 1]].tolist()
+                        assert hs == rh, (i, x, d, hs, rh)
+                        assert int(m["dep_nbytes"][k]) == int(z["tm_dep_nbytes"][rk]), (i, x, d)
+                        pinned += 1
                     multi += len(hs) > 1
                 checked += 1
-    assert checked > 1000 and multi > 0, (checked, multi)
+    assert checked > 1000 and multi > 0 and pinned > 1000, (checked, multi, pinned)
