@@ -356,9 +356,17 @@ __device__ __forceinline__ double rl_f64(double x, int l) {  // lane l's double,
   const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
-struct RqStage {  // 64 staged request-log entries
-  int32_t task[64], victim[64], thief[64], level[64];
-  double cost[64], occ_v[64], occ_t[64];
+__device__ __forceinline__ int64_t rl_i64s(int64_t x, int l) {  // lane l's int64, via SGPRs
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)x, l), hi = __builtin_amdgcn_readlane((unsigned)(x >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// one task's thief-search rows (k_best_thief's prep, per sorted position), uniform: holders
+// (<= MAXH), the get_nbytes / raw nbytes each holds, each holder's ws.nbytes
+struct TRow {
+  int nh;
+  int64_t cget, craw;
+  int hw[MAXH];
+  int64_t hg[MAXH], hr[MAXH], hn[MAXH];
 };
 __host__ __device__ inline size_t balance_state_bytes(int W) {
   return (size_t)W * (8 + 8 + 4) + ((size_t)6 * W + 2) * 2 + (size_t)W * 4;
@@ -386,9 +394,6 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   uint8_t* idle = thief + W;
   uint8_t* sat = idle + W;
   uint8_t* taken = sat + W;                 // topk scratch
-  // the request log (move_task_request's log entry, :498-500), staged 64 entries at a time
-  // and written out by the whole wave in coalesced stores
-  RqStage* rq = (RqStage*)(smem + ((balance_state_bytes(W) + 15) & ~(size_t)15));
   int32_t* vs = P.vs_g;                     // victims of the current level (global scratch)
   const int R = *P.n_runs;
   auto run_a_g = [&](int r) { return P.run_a[r]; };
@@ -427,26 +432,11 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
     return np < nt || o < nt * avg / 2;
   };
 #if DGP_STEAL_PROF
-  unsigned long long pr_left = 0, pr_left_cyc = 0, pr_exam = 0;
+  unsigned long long pr_left = 0, pr_left_cyc = 0, pr_exam = 0, pr_pro = 0, pr_loop = 0, pr_epi = 0, pr_chunks = 0;
+  unsigned long long pr_many = 0, pr_win = 0, pr_wcyc = 0;
   const unsigned long long pr_t0 = __builtin_amdgcn_s_memtime();
 #endif
-  long long ns_out = 0;  // requests already written to the output arrays
-  auto flush = [&](long long n) {  // staged requests [ns_out, n)
-    const long long k = ns_out + lane;
-    if (k < n) {
-      const int q = (int)(k & 63);
-      P.st_task[k] = rq->task[q];
-      P.st_victim[k] = rq->victim[q];
-      P.st_thief[k] = rq->thief[q];
-      P.st_level[k] = rq->level[q];
-      P.st_cost[k] = rq->cost[q];
-      P.st_occ_victim[k] = rq->occ_v[q];
-      P.st_occ_thief[k] = rq->occ_t[q];
-    }
-    ns_out = n;
-  };
   auto finish = [&]() {
-    flush(ns);
     for (int w = lane; w < W; w += 64) {
       P.inflight_occ[w] = ifo[w];
       P.inflight_tasks[w] = pend[w] - P.nproc[w];
@@ -456,8 +446,10 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
     if (lane == 0) *P.n_steals = ns;
 #if DGP_STEAL_PROF
     if (lane == 0)
-      printf("k_balance: requests %lld examined %llu thief-left %llu (%llu cycles) total %llu cycles\n", ns, pr_exam,
-             pr_left, pr_left_cyc, __builtin_amdgcn_s_memtime() - pr_t0);
+      printf("k_balance: requests %lld examined %llu thief-left %llu (%llu cycles) total %llu cycles; chunks %llu "
+             "prologue %llu loop %llu epilogue %llu; many-holder %llu windows %llu (%llu cycles)\n", ns, pr_exam,
+             pr_left, pr_left_cyc, __builtin_amdgcn_s_memtime() - pr_t0, pr_chunks, pr_pro, pr_loop, pr_epi, pr_many,
+             pr_win, pr_wcyc);
 #endif
   };
   if (n_thieves == 0 || n_thieves == W) {  // :410-411
@@ -536,65 +528,77 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   };
   // _get_thief (stealing.py:532-542) over the live thieves, exact: worker_objective's start
   // is fl(stack + comm / bw), monotone in the stack time; for a worker holding none of the
-  // task's dependencies comm is the task's whole get_nbytes sum, so the runs are scanned in
-  // order while their start can still tie the best, taking each run's first live
-  // non-holder (the run is already ordered by (nbytes, index)); the <= MAXH holders are
-  // evaluated with their own comm.
-  auto thief_from_runs = [&](int i, int64_t t, double* cct_out) -> int {
-    const int nh = P.s_nh[i];
+  // task's dependencies comm is the task's whole get_nbytes sum, so each run (ordered by
+  // (nbytes, index)) offers its first live non-holder, and the runs are taken 64 at a time,
+  // one per lane, while a window can still tie the best; the <= MAXH holders are evaluated
+  // with their own comm. The task's rows come from the chunk's registers (TRow: no global
+  // round trip on this path but the runs' stack times and ws.nbytes, one per window).
+  auto thief_from_runs = [&](int i, int64_t t, const TRow& tr, double* cct_out) -> int {
+    const int nh = tr.nh;
     if (nh < 0) {  // many holders: plain argmin
+#if DGP_STEAL_PROF
+      pr_many++;
+#endif
       const Obj b = wave_argmin(P, t, [&](int w) { return thief[w] != 0; });
       *cct_out = comm_cost(P, t, b.w);
       return b.w;
     }
-    int hw[MAXH];
-    int64_t hg[MAXH];
-#pragma unroll
-    for (int j = 0; j < MAXH; j++) {
-      hw[j] = P.s_hw[(size_t)i * MAXH + j];
-      hg[j] = P.s_hg[(size_t)i * MAXH + j];
-    }
-    const int64_t C = P.s_cget[i];
-    const double x = (double)C / (double)P.bw;
+    const double x = (double)tr.cget / (double)P.bw;
     Obj best{INFINITY, INT64_MAX, INT32_MAX};
-    bool have = false;
-    for (int r = find_run(0); r < R; r = find_run(r + 1)) {
-      const double sv = run_a_g(r) + x;
-      if (have && sv > best.start) break;
-      const int pe = rst[r + 1];
-      int p = run_first[r];
-      while (p < pe && !thief[tho[p]]) p++;
-      run_first[r] = (uint16_t)p;  // removed thieves are skipped for good
-      int q = p;
-      while (q < pe) {
-        const int w = tho[q];
-        bool hold = false;
+#if DGP_STEAL_PROF
+    unsigned long long q0 = __builtin_amdgcn_s_memtime();
+#endif
+    for (int r0 = find_run(0); r0 < R; r0 = find_run(r0 + 64)) {
+#if DGP_STEAL_PROF
+      pr_win++;
+#endif
+      const int r = r0 + lane;
+      Obj o{INFINITY, INT64_MAX, INT32_MAX};
+      if (r < R && run_alive[r] != 0) {
+        const int pe = rst[r + 1];
+        int p = run_first[r];
+        while (p < pe && !thief[tho[p]]) p++;
+        run_first[r] = (uint16_t)p;  // removed thieves are skipped for good
+        int q = p;
+        while (q < pe) {
+          const int w = tho[q];
+          bool hold = false;
 #pragma unroll
-        for (int j = 0; j < MAXH; j++) hold |= j < nh && hw[j] == w;
-        if (thief[w] && !hold) break;
-        q++;
+          for (int j = 0; j < MAXH; j++) hold |= j < nh && tr.hw[j] == w;
+          if (thief[w] && !hold) break;
+          q++;
+        }
+        if (q < pe) {
+          const int w = tho[q];
+          o = Obj{run_a_g(r) + x, P.wnbytes[w], w};
+        }
       }
-      if (q < pe) {
-        const int w = tho[q];
-        const Obj o{sv, P.wnbytes[w], w};
-        if (!have || obj_less(o, best)) best = o;
-        have = true;
+#pragma unroll
+      for (int m = 32; m > 0; m >>= 1) {
+        const Obj o2 = obj_shfl_xor(o, m);
+        if (obj_less(o2, o)) o = o2;
       }
+      if (obj_less(o, best)) best = o;
+      // every later window's start is at least its last run's (the stack times ascend)
+      if (best.w != INT32_MAX && run_a_g(min(r0 + 63, R - 1)) + x > best.start) break;
     }
+#if DGP_STEAL_PROF
+    pr_wcyc += __builtin_amdgcn_s_memtime() - q0;
+#endif
 #pragma unroll
     for (int j = 0; j < MAXH; j++) {
       if (j >= nh) break;
-      const int h = hw[j];
+      const int h = tr.hw[j];
       if (!thief[h]) continue;
       const double stack = occ[h] / (double)nth[h];
-      const Obj o{stack + (double)(C - hg[j]) / (double)P.bw, P.wnbytes[h], h};
+      const Obj o{stack + (double)(tr.cget - tr.hg[j]) / (double)P.bw, tr.hn[j], h};
       if (obj_less(o, best)) best = o;
     }
     int64_t held_raw = 0;
 #pragma unroll
     for (int j = 0; j < MAXH; j++)
-      if (j < nh && hw[j] == best.w) held_raw = P.s_hr[(size_t)i * MAXH + j];
-    *cct_out = (double)(P.s_craw[i] - held_raw) / (double)P.bw;
+      if (j < nh && tr.hw[j] == best.w) held_raw = tr.hr[j];
+    *cct_out = (double)(tr.craw - held_raw) / (double)P.bw;
     return best.w;
   };
   for (int level = 0; level < N_LEVELS; level++) {  // :431
@@ -622,93 +626,213 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
       double ifo_v = ifo[v];
       int pend_v = pend[v];
       for (int c0 = b0; c0 < b1; c0 += 64) {  // 64 tasks of the bin per load round
+#if DGP_STEAL_PROF
+        unsigned long long pc0 = __builtin_amdgcn_s_memtime();
+        pr_chunks++;
+#endif
         const int i = c0 + lane;
         const bool okl = i < b1;
         const int tq = okl ? P.order[i] : 0;
-        const int bq = okl ? P.s_best[i] : 0;
+        const int thL = okl ? P.s_best[i] : NO_THIEF;  // each lane's task: its precomputed thief
         const double cq = okl ? P.s_cct[i] : 0.0;
         const double vq = okl ? P.s_ccv[i] : 0.0;
         const double dq = okl ? P.s_dur[i] : 0.0;
+        // the thief search's rows of the lane's task (used when its thief left)
+        const int nhL = okl ? P.s_nh[i] : -1;
+        const int64_t cgL = okl ? P.s_cget[i] : 0, crL = okl ? P.s_craw[i] : 0;
+        int hwL[MAXH];
+        int64_t hgL[MAXH], hrL[MAXH], hnL[MAXH];
+#pragma unroll
+        for (int j = 0; j < MAXH; j++) {
+          const bool hj = okl && j < nhL;
+          hwL[j] = hj ? P.s_hw[(size_t)i * MAXH + j] : 0;
+          hgL[j] = hj ? P.s_hg[(size_t)i * MAXH + j] : 0;
+          hrL[j] = hj ? P.s_hr[(size_t)i * MAXH + j] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < MAXH; j++) hnL[j] = okl && j < nhL ? P.wnbytes[hwL[j]] : 0;
         const int nq = min(64, b1 - c0);
-        // (Testing the 64 tasks together and skipping to the first accepted one is exact
-        // -- a rejection changes nothing -- but was measured slower on C4, where 89% of
-        // the examined tasks are accepted: 313 -> 387 ms.)
-        for (int j = 0; j < nq; j++) {  // :439
-          if (n_thieves == 0) break;
-          // task j's row broadcast through SGPRs (readlane: no LDS round trip)
-          const int t = __builtin_amdgcn_readlane(tq, j);
-          int th = __builtin_amdgcn_readlane(bq, j);
-          double cct = rl_f64(cq, j);
-          const double ccv = rl_f64(vq, j);
-          const double compute = rl_f64(dq, j);
-          if (th == NO_THIEF) continue;  // _get_thief -> None (:452-454), for good: thieves only leave
+        // each lane's thief's balance state, gathered at once (the lanes of one thief hold the
+        // same values); the walk works on one "current" thief in uniform registers and puts
+        // its state back into those lanes and into LDS when it moves to another one
+        const bool hasL = thL >= 0;
+        int aliveL = hasL && thief[thL] ? 1 : 0;
+        const double occL = hasL ? occ[thL] : 0.0;
+        double ifoL = hasL ? ifo[thL] : 0.0;
+        int pendL = hasL ? pend[thL] : 0;
+        const int ntL = hasL ? (int)nth[thL] : 1;
+        // the state-free terms of each task's test and request (the same fp64 operations)
+        const double hvL = (vq + dq) / 2;  // (ccv + compute) / 2
+        const double dvL = dq + vq;        // compute + ccv
+        const double dtL = dq + cq;        // compute + cct
+        const double limL = ntL * avg / 2;  // is_unoccupied's occupancy bound of the thief
+        // this chunk's requests (the log entry of move_task_request :498-500): in the lane of
+        // the accepted task, written out together
+        int accL = 0, thO = 0;
+        double ovO = 0.0, otO = 0.0;
+        const long long ns0 = ns;
 #if DGP_STEAL_PROF
+        __builtin_amdgcn_s_waitcnt(0);
+        unsigned long long pc1 = __builtin_amdgcn_s_memtime();
+        pr_pro += pc1 - pc0;
+#endif
+        // The walk in windows: from task j up to the next task whose precomputed thief left
+        // (d), one serial pass carries the victim's and each thief's in-flight accounts as if
+        // every task were accepted (two fp64 operations per task, the reference's order),
+        // recording in each task's lane the state it sees; then every task's test and the
+        // thief's is_unoccupied run in parallel. The first rejection, or the task after the
+        // first one that fills its thief, ends the accepted prefix [j, b); if b falls inside
+        // the window the accounts are replayed over [j, b) from the window's start. Task d
+        // takes the thief search and runs on its own.
+        int j = 0;
+        while (j < nq && n_thieves > 0) {
+          const bool todo = lane >= j && lane < nq && thL != NO_THIEF;
+          const unsigned long long needs = __ballot(todo && !(hasL && aliveL));
+          const int d = needs ? (int)__builtin_ctzll(needs) : nq;
+          const double ifo_vS = ifo_v;
+          const double ifoS = ifoL;
+          const int pendS = pendL;
+          double vb = 0.0, tb = 0.0;
+          int pb = 0;
+          for (int k = j; k < d; k++) {
+            const int thk = __builtin_amdgcn_readlane(thL, k);
+            if (thk == NO_THIEF) continue;
+            vb = lane == k ? ifo_v : vb;
+            ifo_v = ifo_v - rl_f64(dvL, k);
+            const double tbk = rl_f64(ifoL, k);
+            const int pbk = __builtin_amdgcn_readlane(pendL, k);
+            tb = lane == k ? tbk : tb;
+            pb = lane == k ? pbk : pb;
+            const double tnew = tbk + rl_f64(dtL, k);
+            const bool mine = thL == thk;
+            ifoL = mine ? tnew : ifoL;
+            pendL = mine ? pbk + 1 : pendL;
+          }
+          const bool inw = todo && lane < d;
+          const double ot = occL + tb;          // combined_occupancy of the thief (:505-506)
+          const double ov = occ_v + vb;         // ... and of the victim
+          const bool acc = ot + cq + dq <= ov - hvL;  // :462-465
+          const bool full = acc && !((pb + 1) < ntL || occL + (tb + dtL) < limL);  // :487-493
+          const unsigned long long bad = __ballot(inw && !acc), fil = __ballot(inw && full);
+          const int fb = bad ? (int)__builtin_ctzll(bad) : 64;
+          const int ff = fil ? (int)__builtin_ctzll(fil) : 64;
+          const int b = min(min(fb, ff + 1), d);
+#if DGP_STEAL_PROF
+          pr_exam += __builtin_popcountll(__ballot(inw && lane < b));
+#endif
+          if (b < d) {  // the accounts of the accepted prefix only
+            ifo_v = ifo_vS;
+            ifoL = ifoS;
+            pendL = pendS;
+            for (int k = j; k < b; k++) {
+              const int thk = __builtin_amdgcn_readlane(thL, k);
+              if (thk == NO_THIEF) continue;
+              ifo_v = ifo_v - rl_f64(dvL, k);
+              const double tnew = rl_f64(ifoL, k) + rl_f64(dtL, k);
+              const int pbk = __builtin_amdgcn_readlane(pendL, k);
+              const bool mine = thL == thk;
+              ifoL = mine ? tnew : ifoL;
+              pendL = mine ? pbk + 1 : pendL;
+            }
+          }
+          // move_task_request (:279-331) for the accepted prefix
+          const bool com = inw && lane < b;
+          const unsigned long long cm = __ballot(com);
+          if (com) {
+            accL = 1;
+            thO = thL;
+            ovO = ov;
+            otO = ot;
+          }
+          ns += __builtin_popcountll(cm);
+          pend_v -= __builtin_popcountll(cm);
+          if (ff < b) {  // task ff filled its thief: no longer a thief (:487-493)
+            const int x = __builtin_amdgcn_readlane(thL, ff);
+            if (thL == x) aliveL = 0;
+            if (lane == 0) {
+              thief[x] = 0;
+              run_alive[P.run_of_w[x]] -= 1;
+            }
+            __syncthreads();
+            n_thieves--;
+          }
+          // a rejected task changes nothing (:462-465); one after a fill is tested again
+          j = (fb <= ff && b == fb) ? b + 1 : b;
+          if (b != d || d >= nq || n_thieves == 0) continue;
+          // task d: its precomputed thief left (or it had none): the live state into LDS, then
+          // a new search over the live thieves, and the task on its own
+#if DGP_STEAL_PROF
+          const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+          pr_left++;
           pr_exam++;
 #endif
-          // the thief's state, read together (one LDS round trip)
-          uint8_t thf = 0;
-          double occ_th = 0.0, ifo_th = 0.0;
-          int pend_th = 0, nt_th = 1;
-          if (th >= 0) {
-            thf = thief[th];
-            occ_th = occ[th];
-            ifo_th = ifo[th];
-            pend_th = pend[th];
-            nt_th = nth[th];
+          j = d + 1;
+          if (hasL) {  // every lane of one thief holds the same values
+            ifo[thL] = ifoL;
+            pend[thL] = pendL;
           }
-          if (th < 0 || !thf) {  // the precomputed thief left
-#if DGP_STEAL_PROF
-            const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
-            pr_left++;
-#endif
-            th = -1;
-            if (restricted(P, t)) {
-              const Obj b = wave_argmin_valid(P, t, [&](int w) { return thief[w] != 0; });
-              if (b.w < W) {
-                th = b.w;
-                cct = comm_cost(P, t, th);
-              }
+          __syncthreads();
+          // (the lane index through an empty asm: these reads stay on this path instead of
+          // being hoisted into the windows)
+          int jj = d;
+          asm volatile("" : "+s"(jj));
+          const int t = __builtin_amdgcn_readlane(tq, jj);
+          double cct = rl_f64(cq, jj);
+          const double compute = rl_f64(dq, jj);
+          int th = -1;
+          if (restricted(P, t)) {
+            const Obj bo = wave_argmin_valid(P, t, [&](int w) { return thief[w] != 0; });
+            if (bo.w < W) {
+              th = bo.w;
+              cct = comm_cost(P, t, th);
             }
-            if (th < 0 && (!restricted(P, t) || loose(P, t))) th = thief_from_runs(c0 + j, t, &cct);
-#if DGP_STEAL_PROF
-            pr_left_cyc += __builtin_amdgcn_s_memtime() - tp0;
-#endif
-            if (th < 0) continue;
-            occ_th = occ[th];
-            ifo_th = ifo[th];
-            pend_th = pend[th];
-            nt_th = nth[th];
           }
-          const double occ_thief = occ_th + ifo_th;  // combined_occupancy (:505-506)
+          if (th < 0 && (!restricted(P, t) || loose(P, t))) {
+            TRow tr;
+            tr.nh = __builtin_amdgcn_readlane(nhL, jj);
+            tr.cget = rl_i64s(cgL, jj);
+            tr.craw = rl_i64s(crL, jj);
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) {
+              tr.hw[q] = __builtin_amdgcn_readlane(hwL[q], jj);
+              tr.hg[q] = rl_i64s(hgL[q], jj);
+              tr.hr[q] = rl_i64s(hrL[q], jj);
+              tr.hn[q] = rl_i64s(hnL[q], jj);
+            }
+            th = thief_from_runs(c0 + jj, t, tr, &cct);
+          }
+#if DGP_STEAL_PROF
+          pr_left_cyc += __builtin_amdgcn_s_memtime() - tp0;
+#endif
+          if (th < 0) continue;
+          const double occ_th = occ[th];
+          double ifo_th = ifo[th];
+          int pend_th = pend[th];
+          const int nt_th = nth[th];
+          const double occ_thief = occ_th + ifo_th;
           const double occ_victim = occ_v + ifo_v;
-          if (occ_thief + cct + compute <= occ_victim - (ccv + compute) / 2) {  // :462-465
-            // move_task_request (:279-331) -> _add_to_in_flight (:191-199)
-            ifo_v = ifo_v - (compute + ccv);
+          if (occ_thief + cct + compute <= occ_victim - rl_f64(hvL, jj)) {
+            ifo_v = ifo_v - rl_f64(dvL, jj);
             ifo_th = ifo_th + (compute + cct);
             pend_v -= 1;
             pend_th += 1;
+            if (thL == th) {
+              ifoL = ifo_th;
+              pendL = pend_th;
+            }
             if (lane == 0) {
-              ifo[v] = ifo_v;
               ifo[th] = ifo_th;
-              pend[v] = pend_v;
               pend[th] = pend_th;
-              const int q = (int)(ns & 63);
-              rq->task[q] = t;
-              rq->victim[q] = v;
-              rq->thief[q] = th;
-              rq->level[q] = level;
-              rq->cost[q] = compute + ccv;
-              rq->occ_v[q] = occ_victim;
-              rq->occ_t[q] = occ_thief;
+            }
+            if (lane == jj) {
+              accL = 1;
+              thO = th;
+              ovO = occ_victim;
+              otO = occ_thief;
             }
             ns++;
-            if ((ns & 63) == 0) {
-              __syncthreads();
-              flush(ns);
-            }
-            // is_unoccupied (scheduler.py:2997-3004) of the thief after the request (:487-493)
-            const double oc = occ_th + ifo_th;
-            if (!(pend_th < nt_th || oc < nt_th * avg / 2)) {
+            if (!(pend_th < nt_th || occ_th + ifo_th < nt_th * avg / 2)) {
+              if (thL == th) aliveL = 0;
               if (lane == 0) {
                 thief[th] = 0;
                 run_alive[P.run_of_w[th]] -= 1;
@@ -718,6 +842,33 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
             }
           }
         }
+        if (hasL) {
+          ifo[thL] = ifoL;
+          pend[thL] = pendL;
+        }
+#if DGP_STEAL_PROF
+        unsigned long long pc2 = __builtin_amdgcn_s_memtime();
+        pr_loop += pc2 - pc1;
+#endif
+        const unsigned long long am = __ballot(accL != 0);
+        if (accL) {
+          const long long k = ns0 + __builtin_amdgcn_mbcnt_hi((unsigned)(am >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)am, 0));
+          P.st_task[k] = tq;
+          P.st_victim[k] = v;
+          P.st_thief[k] = thO;
+          P.st_level[k] = level;
+          P.st_cost[k] = dvL;
+          P.st_occ_victim[k] = ovO;
+          P.st_occ_thief[k] = otO;
+        }
+        __syncthreads();
+#if DGP_STEAL_PROF
+        pr_epi += __builtin_amdgcn_s_memtime() - pc2;
+#endif
+      }
+      if (lane == 0) {
+        ifo[v] = ifo_v;
+        pend[v] = pend_v;
       }
       __syncthreads();
       // check_idle_saturated(victim, occ=combined) (scheduler.py:2949-2995)
@@ -743,7 +894,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   finish();
 }
 
-inline size_t balance_lds_bytes(int W) { return ((balance_state_bytes(W) + 15) & ~(size_t)15) + sizeof(RqStage); }
+inline size_t balance_lds_bytes(int W) { return (balance_state_bytes(W) + 15) & ~(size_t)15; }
 
 }  // namespace steal
 
