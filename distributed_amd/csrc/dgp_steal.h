@@ -348,6 +348,9 @@ __global__ void k_runs(Prob P) {
 }
 
 // ---------------------------------------------------------------------- balance
+#ifndef DGP_STEAL_WCACHE
+#define DGP_STEAL_WCACHE 1  // the thief search's first-window cache (run stack times, ws.nbytes)
+#endif
 #ifndef DGP_STEAL_PROF
 #define DGP_STEAL_PROF 0  // diagnostics: k_balance prints examined / re-evaluated / cycle counts
 #endif
@@ -360,14 +363,6 @@ __device__ __forceinline__ int64_t rl_i64s(int64_t x, int l) {  // lane l's int6
   const unsigned lo = __builtin_amdgcn_readlane((unsigned)x, l), hi = __builtin_amdgcn_readlane((unsigned)(x >> 32), l);
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-// one task's thief-search rows (k_best_thief's prep, per sorted position), uniform: holders
-// (<= MAXH), the get_nbytes / raw nbytes each holds, each holder's ws.nbytes
-struct TRow {
-  int nh;
-  int64_t cget, craw;
-  int hw[MAXH];
-  int64_t hg[MAXH], hr[MAXH], hn[MAXH];
-};
 __host__ __device__ inline size_t balance_state_bytes(int W) {
   return (size_t)W * (8 + 8 + 4) + ((size_t)6 * W + 2) * 2 + (size_t)W * 4;
 }
@@ -396,7 +391,6 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   uint8_t* taken = sat + W;                 // topk scratch
   int32_t* vs = P.vs_g;                     // victims of the current level (global scratch)
   const int R = *P.n_runs;
-  auto run_a_g = [&](int r) { return P.run_a[r]; };
   for (int r = lane; r < R; r += 64) {
     run_first[r] = (uint16_t)P.run_start[r];
     run_alive[r] = (uint16_t)(P.run_start[r + 1] - P.run_start[r]);
@@ -526,81 +520,10 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
     }
     return x;
   };
-  // _get_thief (stealing.py:532-542) over the live thieves, exact: worker_objective's start
-  // is fl(stack + comm / bw), monotone in the stack time; for a worker holding none of the
-  // task's dependencies comm is the task's whole get_nbytes sum, so each run (ordered by
-  // (nbytes, index)) offers its first live non-holder, and the runs are taken 64 at a time,
-  // one per lane, while a window can still tie the best; the <= MAXH holders are evaluated
-  // with their own comm. The task's rows come from the chunk's registers (TRow: no global
-  // round trip on this path but the runs' stack times and ws.nbytes, one per window).
-  auto thief_from_runs = [&](int i, int64_t t, const TRow& tr, double* cct_out) -> int {
-    const int nh = tr.nh;
-    if (nh < 0) {  // many holders: plain argmin
-#if DGP_STEAL_PROF
-      pr_many++;
-#endif
-      const Obj b = wave_argmin(P, t, [&](int w) { return thief[w] != 0; });
-      *cct_out = comm_cost(P, t, b.w);
-      return b.w;
-    }
-    const double x = (double)tr.cget / (double)P.bw;
-    Obj best{INFINITY, INT64_MAX, INT32_MAX};
-#if DGP_STEAL_PROF
-    unsigned long long q0 = __builtin_amdgcn_s_memtime();
-#endif
-    for (int r0 = find_run(0); r0 < R; r0 = find_run(r0 + 64)) {
-#if DGP_STEAL_PROF
-      pr_win++;
-#endif
-      const int r = r0 + lane;
-      Obj o{INFINITY, INT64_MAX, INT32_MAX};
-      if (r < R && run_alive[r] != 0) {
-        const int pe = rst[r + 1];
-        int p = run_first[r];
-        while (p < pe && !thief[tho[p]]) p++;
-        run_first[r] = (uint16_t)p;  // removed thieves are skipped for good
-        int q = p;
-        while (q < pe) {
-          const int w = tho[q];
-          bool hold = false;
-#pragma unroll
-          for (int j = 0; j < MAXH; j++) hold |= j < nh && tr.hw[j] == w;
-          if (thief[w] && !hold) break;
-          q++;
-        }
-        if (q < pe) {
-          const int w = tho[q];
-          o = Obj{run_a_g(r) + x, P.wnbytes[w], w};
-        }
-      }
-#pragma unroll
-      for (int m = 32; m > 0; m >>= 1) {
-        const Obj o2 = obj_shfl_xor(o, m);
-        if (obj_less(o2, o)) o = o2;
-      }
-      if (obj_less(o, best)) best = o;
-      // every later window's start is at least its last run's (the stack times ascend)
-      if (best.w != INT32_MAX && run_a_g(min(r0 + 63, R - 1)) + x > best.start) break;
-    }
-#if DGP_STEAL_PROF
-    pr_wcyc += __builtin_amdgcn_s_memtime() - q0;
-#endif
-#pragma unroll
-    for (int j = 0; j < MAXH; j++) {
-      if (j >= nh) break;
-      const int h = tr.hw[j];
-      if (!thief[h]) continue;
-      const double stack = occ[h] / (double)nth[h];
-      const Obj o{stack + (double)(tr.cget - tr.hg[j]) / (double)P.bw, tr.hn[j], h};
-      if (obj_less(o, best)) best = o;
-    }
-    int64_t held_raw = 0;
-#pragma unroll
-    for (int j = 0; j < MAXH; j++)
-      if (j < nh && tr.hw[j] == best.w) held_raw = tr.hr[j];
-    *cct_out = (double)(tr.craw - held_raw) / (double)P.bw;
-    return best.w;
-  };
+  // the run stack times from the first live run, one lane each, kept across searches while
+  // that start stays (the batch search below reads them by shuffle)
+  int wc_r0 = -1;
+  double wc_a = 0.0;
   for (int level = 0; level < N_LEVELS; level++) {  // :431
     if (n_thieves == 0) break;
     if (live) {  // list(potential_victims): the saturated set now, ascending index
@@ -633,8 +556,8 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
         const int i = c0 + lane;
         const bool okl = i < b1;
         const int tq = okl ? P.order[i] : 0;
-        const int thL = okl ? P.s_best[i] : NO_THIEF;  // each lane's task: its precomputed thief
-        const double cq = okl ? P.s_cct[i] : 0.0;
+        int thL = okl ? P.s_best[i] : NO_THIEF;  // each lane's task: its precomputed thief
+        double cq = okl ? P.s_cct[i] : 0.0;
         const double vq = okl ? P.s_ccv[i] : 0.0;
         const double dq = okl ? P.s_dur[i] : 0.0;
         // the thief search's rows of the lane's task (used when its thief left)
@@ -651,21 +574,26 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
         }
 #pragma unroll
         for (int j = 0; j < MAXH; j++) hnL[j] = okl && j < nhL ? P.wnbytes[hwL[j]] : 0;
+        // the search's comm terms (worker_objective :3136-3138), computed once per task
+        const double xL = (double)cgL / (double)P.bw;
+        double hcL[MAXH];
+#pragma unroll
+        for (int j = 0; j < MAXH; j++) hcL[j] = (double)(cgL - hgL[j]) / (double)P.bw;
         const int nq = min(64, b1 - c0);
         // each lane's thief's balance state, gathered at once (the lanes of one thief hold the
         // same values); the walk works on one "current" thief in uniform registers and puts
         // its state back into those lanes and into LDS when it moves to another one
-        const bool hasL = thL >= 0;
+        bool hasL = thL >= 0;
         int aliveL = hasL && thief[thL] ? 1 : 0;
-        const double occL = hasL ? occ[thL] : 0.0;
+        double occL = hasL ? occ[thL] : 0.0;
         double ifoL = hasL ? ifo[thL] : 0.0;
         int pendL = hasL ? pend[thL] : 0;
-        const int ntL = hasL ? (int)nth[thL] : 1;
+        int ntL = hasL ? (int)nth[thL] : 1;
         // the state-free terms of each task's test and request (the same fp64 operations)
         const double hvL = (vq + dq) / 2;  // (ccv + compute) / 2
         const double dvL = dq + vq;        // compute + ccv
-        const double dtL = dq + cq;        // compute + cct
-        const double limL = ntL * avg / 2;  // is_unoccupied's occupancy bound of the thief
+        double dtL = dq + cq;              // compute + cct
+        double limL = ntL * avg / 2;        // is_unoccupied's occupancy bound of the thief
         // this chunk's requests (the log entry of move_task_request :498-500): in the lane of
         // the accepted task, written out together
         int accL = 0, thO = 0;
@@ -759,88 +687,158 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           // a rejected task changes nothing (:462-465); one after a fill is tested again
           j = (fb <= ff && b == fb) ? b + 1 : b;
           if (b != d || d >= nq || n_thieves == 0) continue;
-          // task d: its precomputed thief left (or it had none): the live state into LDS, then
-          // a new search over the live thieves, and the task on its own
+          // task d's precomputed thief left (or it had none): every task from d on whose thief
+          // left gets a new one now, in parallel (one lane each). _get_thief's argmin reads
+          // only the thief set and the plain occupancies (worker_objective :3131-3146), and the
+          // set only shrinks, so a winner found now is the winner when the task's turn comes
+          // as long as it is still a thief; one that leaves by then is searched again.
 #if DGP_STEAL_PROF
           const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
           pr_left++;
-          pr_exam++;
 #endif
-          j = d + 1;
-          if (hasL) {  // every lane of one thief holds the same values
+          if (hasL) {  // the live accounts into LDS (every lane of one thief holds the same values)
             ifo[thL] = ifoL;
             pend[thL] = pendL;
           }
           __syncthreads();
-          // (the lane index through an empty asm: these reads stay on this path instead of
-          // being hoisted into the windows)
-          int jj = d;
-          asm volatile("" : "+s"(jj));
-          const int t = __builtin_amdgcn_readlane(tq, jj);
-          double cct = rl_f64(cq, jj);
-          const double compute = rl_f64(dq, jj);
-          int th = -1;
-          if (restricted(P, t)) {
-            const Obj bo = wave_argmin_valid(P, t, [&](int w) { return thief[w] != 0; });
-            if (bo.w < W) {
-              th = bo.w;
-              cct = comm_cost(P, t, th);
+          const bool sl = lane >= d && lane < nq && thL != NO_THIEF && !(hasL && aliveL);
+          // restricted tasks (valid_workers): the plain argmin over their live valid thieves,
+          // one task at a time (a loose one with none falls through to the general search)
+          bool gen = sl;
+          if (P.r_flags) {
+            unsigned long long rm = __ballot(sl && restricted(P, tq));
+            for (; rm; rm &= rm - 1) {
+              const int k = (int)__builtin_ctzll(rm);
+              const int tk = __builtin_amdgcn_readlane(tq, k);
+              const Obj bo = wave_argmin_valid(P, tk, [&](int w) { return thief[w] != 0; });
+              const bool lo_ = loose(P, tk);
+              const int nth_k = bo.w < W ? bo.w : (lo_ ? -1 : NO_THIEF);
+              const double cc = bo.w < W ? comm_cost(P, tk, bo.w) : 0.0;
+              if (lane == k && nth_k != -1) {
+                thL = nth_k;
+                cq = cc;
+                gen = false;
+              }
             }
           }
-          if (th < 0 && (!restricted(P, t) || loose(P, t))) {
-            TRow tr;
-            tr.nh = __builtin_amdgcn_readlane(nhL, jj);
-            tr.cget = rl_i64s(cgL, jj);
-            tr.craw = rl_i64s(crL, jj);
-#pragma unroll
-            for (int q = 0; q < MAXH; q++) {
-              tr.hw[q] = __builtin_amdgcn_readlane(hwL[q], jj);
-              tr.hg[q] = rl_i64s(hgL[q], jj);
-              tr.hr[q] = rl_i64s(hrL[q], jj);
-              tr.hn[q] = rl_i64s(hnL[q], jj);
+          // many holders (more than MAXH): the plain argmin, one task at a time
+          {
+            unsigned long long mm = __ballot(gen && nhL < 0);
+            for (; mm; mm &= mm - 1) {
+              const int k = (int)__builtin_ctzll(mm);
+              const int tk = __builtin_amdgcn_readlane(tq, k);
+              const Obj bo = wave_argmin(P, tk, [&](int w) { return thief[w] != 0; });
+              const double cc = comm_cost(P, tk, bo.w);
+              if (lane == k) {
+                thL = bo.w;
+                cq = cc;
+                gen = false;
+              }
             }
-            th = thief_from_runs(c0 + jj, t, tr, &cct);
+          }
+          // the general search, each lane its own task: the runs of equal stack time in
+          // order, each offering its first live non-holder (ordered by (ws.nbytes, index));
+          // the first run with one gives the least start, later runs only while their start
+          // ties; then the <= MAXH holders with their own comm. ws.nbytes is read only to break
+          // a tie of starts.
+          {
+            const int rf = find_run(0);
+            if (!DGP_STEAL_WCACHE || rf != wc_r0) {  // the window of run stack times from rf
+              wc_r0 = rf;
+              wc_a = rf + lane < R ? P.run_a[rf + lane] : INFINITY;
+            }
+            int r = rf;
+            bool act = gen;
+            double bs = INFINITY;   // best start
+            int bw_ = INT32_MAX;    // best worker
+            int64_t bn = -1;        // its ws.nbytes (-1: not read yet)
+            auto nb_of = [&](int w) { return P.wnbytes[w]; };
+            while (__ballot(act)) {
+              // this lane's run r: its stack time from the window (a shuffle every lane runs)
+              const int off = r - wc_r0;
+              const bool inw_ = off >= 0 && off < 64;
+              double ra = __shfl(wc_a, inw_ ? off : 0);
+              if (act) {
+                if (!inw_) ra = P.run_a[r];
+                const double sv = ra + xL;
+                if (bw_ != INT32_MAX && sv > bs) {
+                  act = false;
+                } else {
+                  const int pe = rst[r + 1];
+                  int p = run_first[r];
+                  while (p < pe && !thief[tho[p]]) p++;
+                  run_first[r] = (uint16_t)p;  // the same value from every lane that scans it
+                  int q = p;
+                  while (q < pe) {
+                    const int w = tho[q];
+                    bool hold = false;
+#pragma unroll
+                    for (int jh = 0; jh < MAXH; jh++) hold |= jh < nhL && hwL[jh] == w;
+                    if (thief[w] && !hold) break;
+                    q++;
+                  }
+                  if (q < pe) {
+                    const int w = tho[q];
+                    if (bw_ == INT32_MAX) {
+                      bs = sv;
+                      bw_ = w;
+                    } else if (sv == bs) {  // a tie of starts: ws.nbytes, then the index
+                      if (bn < 0) bn = nb_of(bw_);
+                      const int64_t nw = nb_of(w);
+                      if (nw < bn || (nw == bn && w < bw_)) {
+                        bw_ = w;
+                        bn = nw;
+                      }
+                    }
+                  }
+                  // the next run with a live thief (run_nxt links, compressed as crossed)
+                  int x = r + 1;
+                  while (x < R && run_alive[x] == 0) x = run_nxt[x];
+                  r = x;
+                  if (r >= R) act = false;
+                }
+              }
+            }
+            if (gen) {
+#pragma unroll
+              for (int jh = 0; jh < MAXH; jh++) {
+                if (jh >= nhL) break;
+                const int h = hwL[jh];
+                if (!thief[h]) continue;
+                const double st = occ[h] / (double)nth[h] + hcL[jh];
+                bool better = bw_ == INT32_MAX || st < bs;
+                if (!better && st == bs) {
+                  if (bn < 0) bn = nb_of(bw_);
+                  better = hnL[jh] < bn || (hnL[jh] == bn && h < bw_);
+                }
+                if (better) {
+                  bs = st;
+                  bw_ = h;
+                  bn = hnL[jh];
+                }
+              }
+              int64_t held_raw = 0;
+#pragma unroll
+              for (int jh = 0; jh < MAXH; jh++)
+                if (jh < nhL && hwL[jh] == bw_) held_raw = hrL[jh];
+              thL = bw_ < W ? bw_ : NO_THIEF;
+              cq = (double)(crL - held_raw) / (double)P.bw;
+            }
+          }
+          // the searched lanes take their new thief's accounts
+          if (sl) {
+            hasL = thL >= 0;
+            aliveL = hasL ? 1 : 0;
+            occL = hasL ? occ[thL] : 0.0;
+            ifoL = hasL ? ifo[thL] : 0.0;
+            pendL = hasL ? pend[thL] : 0;
+            ntL = hasL ? (int)nth[thL] : 1;
+            dtL = dq + cq;
+            limL = ntL * avg / 2;
           }
 #if DGP_STEAL_PROF
           pr_left_cyc += __builtin_amdgcn_s_memtime() - tp0;
 #endif
-          if (th < 0) continue;
-          const double occ_th = occ[th];
-          double ifo_th = ifo[th];
-          int pend_th = pend[th];
-          const int nt_th = nth[th];
-          const double occ_thief = occ_th + ifo_th;
-          const double occ_victim = occ_v + ifo_v;
-          if (occ_thief + cct + compute <= occ_victim - rl_f64(hvL, jj)) {
-            ifo_v = ifo_v - rl_f64(dvL, jj);
-            ifo_th = ifo_th + (compute + cct);
-            pend_v -= 1;
-            pend_th += 1;
-            if (thL == th) {
-              ifoL = ifo_th;
-              pendL = pend_th;
-            }
-            if (lane == 0) {
-              ifo[th] = ifo_th;
-              pend[th] = pend_th;
-            }
-            if (lane == jj) {
-              accL = 1;
-              thO = th;
-              ovO = occ_victim;
-              otO = occ_thief;
-            }
-            ns++;
-            if (!(pend_th < nt_th || occ_th + ifo_th < nt_th * avg / 2)) {
-              if (thL == th) aliveL = 0;
-              if (lane == 0) {
-                thief[th] = 0;
-                run_alive[P.run_of_w[th]] -= 1;
-              }
-              __syncthreads();
-              n_thieves--;
-            }
-          }
         }
         if (hasL) {
           ifo[thL] = ifoL;
