@@ -37,6 +37,7 @@ SIGNATURES = {
     "dgp_move_task": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "dgp_add_worker": (C.c_int, [_P, C.c_int32, _P]),
     "dgp_add_graph": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P, _P]),
+    "dgp_set_priorities": (C.c_int, [_P, _P]),
     "dgp_add_graph_deferred": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P]),
     "dgp_snapshot": (C.c_int, [_P]),
     "dgp_num_placements": (C.c_int64, [_P]),
@@ -76,7 +77,7 @@ SIGNATURES = {
                                    _P, _P, _P]),
 }
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 _lib = None
 
 

@@ -1496,6 +1496,56 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
                         n_groups, wanted, rootish_override, n_new_placements, false);
 }
 
+int dgp_set_priorities(dgp_engine* e, const int64_t* prio) {
+  if (int rc_ = resident_stop(e)) return rc_;
+  if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
+  if (!prio) return fail(e, DGP_E_ARG, "dgp_set_priorities: prio missing");
+  dgp::Dev& D = e->D;
+  const int64_t N = D.N;
+  const std::vector<int64_t>& dp = e->h_dep_ptr;
+  const std::vector<int32_t>& di = e->h_dep_idx;
+  std::vector<int32_t> order(N);
+  std::iota(order.begin(), order.end(), 0);
+  std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return prio[a] < prio[b]; });
+  for (int64_t i = 1; i < N; i++)
+    if (prio[order[i]] == prio[order[i - 1]]) return fail(e, DGP_E_ARG, "dgp_set_priorities: priorities must be unique");
+  for (int64_t t = 0; t < N; t++)
+    for (int64_t k = dp[t]; k < dp[t + 1]; k++)
+      if (prio[di[k]] >= prio[t]) return fail(e, DGP_E_ARG, "dgp_set_priorities: priorities must be topological");
+  // the dependents rows in the new order (the frontier order of _add_to_memory)
+  const int64_t E = dp[N];
+  std::vector<int64_t> dpt_ptr(N + 1, 0);
+  for (int64_t k = 0; k < E; k++) dpt_ptr[di[k] + 1]++;
+  for (int64_t t = 0; t < N; t++) dpt_ptr[t + 1] += dpt_ptr[t];
+  std::vector<int32_t> dpt_idx(E > 0 ? E : 1);
+  {
+    std::vector<int64_t> fill(dpt_ptr.begin(), dpt_ptr.end() - 1);
+    for (int64_t t = 0; t < N; t++)
+      for (int64_t k = dp[t]; k < dp[t + 1]; k++) dpt_idx[fill[di[k]]++] = (int32_t)t;
+    for (int64_t t = 0; t < N; t++)
+      if (dpt_ptr[t + 1] - dpt_ptr[t] > 1)
+        std::sort(dpt_idx.begin() + dpt_ptr[t], dpt_idx.begin() + dpt_ptr[t + 1],
+                  [&](int32_t a, int32_t b) { return prio[a] < prio[b]; });
+  }
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, hipMemcpy(const_cast<int64_t*>(D.prio), prio, (size_t)N * 8, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(const_cast<int32_t*>(D.order), order.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+  if (E > 0) HIPCHK(e, hipMemcpy(const_cast<int32_t*>(D.dpt_idx), dpt_idx.data(), (size_t)E * 4, hipMemcpyHostToDevice));
+  // the queue (qarr[qhead, qhead + qlen), ascending priority) re-sorted
+  dgp::Ctl c;
+  if (int rc = read_ctl(e, &c)) return rc;
+  if (c.qlen > 1) {
+    std::vector<int32_t> q((size_t)c.qlen);
+    HIPCHK(e, hipMemcpy(q.data(), D.qarr + c.qhead, q.size() * 4, hipMemcpyDeviceToHost));
+    std::stable_sort(q.begin(), q.end(), [&](int32_t a, int32_t b) { return prio[a] < prio[b]; });
+    HIPCHK(e, hipMemcpy(D.qarr + c.qhead, q.data(), q.size() * 4, hipMemcpyHostToDevice));
+  }
+  e->h_prio.assign(prio, prio + N);
+  return sync_dev(e);
+}
+
 int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx,
                            const int64_t* prio, const int32_t* prefix_id, int32_t n_prefixes,
                            const double* prefix_default_duration, const int32_t* group_id, int32_t n_groups,

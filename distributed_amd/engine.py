@@ -239,6 +239,14 @@ class PlacementEngine:
         self.n_tasks += n
         return int(newp.value)
 
+    def set_priorities(self, prio):
+        """Every task's priority anew (dgp_set_priorities): the merged ranks after a later
+        graph whose user priority outranks earlier tasks (appended with ``defer``)."""
+        p = np.ascontiguousarray(prio, np.int64).reshape(-1)
+        if len(p) != self.n_tasks:
+            raise ValueError(f"set_priorities: {len(p)} priorities for {self.n_tasks} tasks")
+        self._check(self.lib.dgp_set_priorities(self.h, _ptr(p)), "dgp_set_priorities")
+
     # --------------------------------------------------------- service events
     @staticmethod
     def _arr(x, dt):

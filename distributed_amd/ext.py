@@ -942,6 +942,7 @@ class GPUPlacementExtension(SchedulerPlugin):
                 self.prefix_dur = list(g["prefix_default_dur"])
                 self.group_prefix = list(g["group_prefix"])
                 self.max_priority = max(ts.priority for ts in new)
+                self.prio_of = [s.tasks[k].priority for k in keys_]  # engine index -> TaskState.priority
                 if self.engine_factory is not None:
                     self.engine = self.engine_factory()
                 else:
@@ -974,17 +975,22 @@ class GPUPlacementExtension(SchedulerPlugin):
                 self._restr_h[keys_[i]] = (int(g["restr_flags"][i]), tuple(int(w) for w in ri[rp[i]:rp[i + 1]]))
 
     def _add_graph(self, new):
-        """A later update_graph (scheduler.py:4662-4751) on the running engine: the new
-        tasks must all follow the earlier ones in priority (a new generation, :4713, with no
-        user priority above the earlier graphs'); prefixes and groups map into the
-        engine-wide tables. An independent graph's update_graph stimulus runs on the engine;
-        a graph that depends on earlier tasks is appended (dgp_add_graph) and its stimulus
-        is the scheduler's own, the engine resynchronised after it (``_suspend``)."""
+        """A later update_graph (scheduler.py:4662-4751) on the running engine; prefixes and
+        groups map into the engine-wide tables. An independent graph whose tasks follow the
+        earlier ones in priority (a new generation, :4713) runs its update_graph stimulus on
+        the engine. A graph that depends on earlier tasks, carries restrictions, or whose
+        user priority outranks earlier tasks (then every task's merged rank goes to the
+        engine, dgp_set_priorities) is appended without placing and its stimulus is the
+        scheduler's own, the engine resynchronised after it (``_suspend``)."""
         s = self.scheduler
         g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers], s.valid_workers,
                                     self.worker_index, earlier=self.task_index)
         restricted = "restr_flags" in g  # its stimulus the scheduler's, then the rows (dgp_update_restrictions)
-        if min(ts.priority for ts in new) <= self.max_priority:
+        # a user priority that outranks earlier tasks (_set_priorities :4934-4981): the engine
+        # takes every task's rank in the merged order (dgp_set_priorities) and the stimulus is
+        # the scheduler's, then a resync
+        outranks = min(ts.priority for ts in new) <= self.max_priority
+        if outranks and not hasattr(self.engine, "set_priorities"):
             raise NotImplementedError("a later graph whose tasks do not all follow the earlier ones in priority")
         pmap = np.zeros(len(g["prefix_names"]), np.int32)
         for i, nm in enumerate(g["prefix_names"]):
@@ -1007,20 +1013,28 @@ class GPUPlacementExtension(SchedulerPlugin):
         if not self.active:
             return
         dependent = bool((g["dep_idx"] < 0).any())
-        if restricted:
+        if restricted or outranks:
             self.engine.add_graph(g2, defer=True)
         else:
             self.engine.add_graph(g2)
         self.keys = self.keys + keys_
         self.task_index.update({k: n0 + i for i, k in enumerate(keys_)})
+        self.prio_of = self.prio_of + [s.tasks[k].priority for k in keys_]
+        if outranks:  # every task's rank in the merged order (forgotten tasks keep theirs)
+            order = sorted(range(len(self.prio_of)), key=self.prio_of.__getitem__)
+            rank = np.empty(len(order), np.int64)
+            rank[order] = np.arange(len(order))
+            self.engine.set_priorities(rank)
+            self.stats["reranked_graphs"] += 1
         g.pop("restr_flags", None)  # the resync hands the restrictions over (the mirrors lack them)
         self._remember_inputs(g, keys_)
-        self.max_priority = max(ts.priority for ts in new)
+        self.max_priority = max(self.max_priority, max(ts.priority for ts in new))
         self.stats["graphs"] += 1
-        if dependent or restricted:
-            self.stats["dependent_graphs" if dependent else "restricted_graphs"] += 1
+        if dependent or restricted or outranks:
+            if not outranks:
+                self.stats["dependent_graphs" if dependent else "restricted_graphs"] += 1
             self._suspend("a later graph that depends on earlier tasks" if dependent else
-                          "a later graph with restrictions")
+                          "a later graph with restrictions" if restricted else "a later graph that outranks earlier tasks")
             for k in keys_:  # the new tasks, the earlier ones they wait on / add waiters to
                 self._mark_dirty(k)
             return

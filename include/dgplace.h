@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 13
+#define DGP_ABI_VERSION 14
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -241,6 +241,14 @@ int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr,
                            const int64_t* prio, const int32_t* prefix_id, int32_t n_prefixes,
                            const double* prefix_default_duration, const int32_t* group_id, int32_t n_groups,
                            const uint8_t* wanted, const int8_t* rootish_override);
+
+/* (ABI 14) Every task's priority anew (n_tasks entries, unique and topological): a later
+ * graph submitted with a user priority that outranks earlier tasks (Scheduler.update_graph's
+ * _set_priorities, scheduler.py:4934-4981: -user priority first in the tuple) — appended
+ * with dgp_add_graph_deferred, then the merged ranks here, then dgp_sync_* as for any
+ * deferred graph. The dependents rows (the frontier order of _add_to_memory) and the queue
+ * are re-sorted in the new order. */
+int dgp_set_priorities(dgp_engine* e, const int64_t* prio);
 
 /* ---- Service events: the other placement-input stimuli of a live scheduler, in the order the
  * scheduler handles them, between dgp_tasks_finished calls. Stream-engine graphs (<= 32 prefixes);

@@ -18,7 +18,7 @@ def golden_files():
     """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
                   and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcgdep_", "svcev_",
-                                            "svcrs_", "svcp2p_", "svcgrst_")))
+                                            "svcrs_", "svcp2p_", "svcgrst_", "svcgprio_")))
 
 
 def svc_second_graph_files():
@@ -36,6 +36,12 @@ def svc_restr_graph_files():
     """Service-mode streams with a later graph carrying worker restrictions (gen_service.py
     second-graph svcgrst_*): appended deferred, the scheduler's stimulus, resync + rows."""
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcgrst_") and f.endswith(".npz"))
+
+
+def svc_prio_graph_files():
+    """Service-mode streams with a later graph whose user priority outranks the earlier tasks
+    (gen_service.py second-graph svcgprio_*): appended deferred, re-ranked, resynced."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcgprio_") and f.endswith(".npz"))
 
 
 def second_graph(g, z, with_results=False):

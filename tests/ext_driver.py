@@ -461,7 +461,10 @@ def run_second_graph(name):
     S.validate_key = lambda self, key, ts=None: None
     S.send_all = lambda self, client_msgs, worker_msgs: None
     fkeys = [ts.key for ts in tss]
-    dep = name.startswith(("svcgdep_", "svcgrst_"))  # the scheduler decides the submission, then a resync
+    # the scheduler decides the submission, then a resync (svcgprio_: a user priority above the
+    # earlier tasks', the engine takes the merged ranks first)
+    dep = name.startswith(("svcgdep_", "svcgrst_", "svcgprio_"))
+    user_prio = int(z["g2_user_prio"]) if "g2_user_prio" in z.files else 0
     eng = (EventEngine if dep else FixtureEngine)(exp, fkeys)
     ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
     eng.ext = ext
@@ -508,7 +511,7 @@ def run_second_graph(name):
             for k, key in enumerate(keys2):
                 ts = s.new_task(key, (operator.add, (), {}), "released")
                 tidx[key] = N1 + k
-                ts.priority = (0, 2, int(g2["prio"][k]))
+                ts.priority = (-user_prio, 2, int(g2["prio"][k]))
                 new.append(ts)
             for k, ts in enumerate(new):
                 for d in g2["dep_idx"][g2["dep_ptr"][k]:g2["dep_ptr"][k + 1]]:
@@ -545,8 +548,13 @@ def run_second_graph(name):
     host = 0
     if dep:  # one resync, right after the submission: the fixture's dump
         syncs = [c for c in eng.calls if c[0] == "sync"]
-        assert len(syncs) == 1 and ext.stats["dependent_graphs"] + ext.stats["restricted_graphs"] == 1, (
-            len(syncs), ext.stats)
+        assert len(syncs) == 1 and (ext.stats["dependent_graphs"] + ext.stats["restricted_graphs"]
+                                    + ext.stats["reranked_graphs"]) == 1, (len(syncs), ext.stats)
+        if user_prio:  # every task's merged rank, handed over before the resync
+            ps = [c for c in eng.calls if c[0] == "prio"]
+            assert len(ps) == 1 and eng.calls.index(ps[0]) < eng.calls.index(syncs[0]), eng.calls[-3:]
+            want_p = [int(z["g2_prio_all"][tidx[k]]) for k in ext.keys]
+            assert ps[0][1] == want_p
         if "restr_flags" in g2:  # the new tasks' restrictions, handed over right after the resync
             rs = [c for c in eng.calls if c[0] == "restrict"]
             assert len(rs) == 1 and eng.calls.index(rs[0]) == eng.calls.index(syncs[0]) + 1, eng.calls[-3:]
@@ -626,6 +634,9 @@ class EventEngine(FixtureEngine):
         return self._event("erred", int(t))
 
     # task inputs changed outside a transition (no placement of their own)
+    def set_priorities(self, prio):
+        self.calls.append(("prio", [int(x) for x in prio]))
+
     def set_rootish(self, t, v):
         self.calls.append(("rootish", [int(x) for x in t], [int(x) for x in v]))
 
@@ -929,7 +940,7 @@ if __name__ == "__main__":
     plain = "--plain" in args
     stream = "--stream" in args
     for nm in [a for a in args if not a.startswith("--")]:
-        fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_"))
+        fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_"))
               else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcp2p_")) else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,
                                                plain="plugin" if "--plugin" in args else plain,

@@ -327,7 +327,7 @@ def main_add_workers(only):
 TOKEN2 = "f9e8d7c6b5a49382716051e4d3c2b1a0"
 
 
-def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0, restr=False):
+def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0, restr=False, user_prio=0):
     """The replay protocol's completions as task-finished messages, with a second,
     independent graph ``g2`` submitted part-way through, the way
     ``Scheduler._create_taskstate_from_graph`` (distributed/scheduler.py:4512-4653) adds it:
@@ -345,7 +345,12 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0, restr=
     ``restr``: ``g2`` carries worker restrictions (graphs.restrict rows, set on the new
     TaskStates as build_state does): the scheduler's state after the submission is dumped as
     resync rows too (the engine appends the graph deferred, the scheduler decides that
-    stimulus, the engine resyncs and takes the rows, dgp_update_restrictions)."""
+    stimulus, the engine resyncs and takes the rows, dgp_update_restrictions).
+
+    ``user_prio``: the later graph is submitted with that user priority (``_set_priorities``
+    :4934-4981 puts ``-priority`` first in the tuple), so its tasks outrank every earlier one:
+    the resync rows are dumped after the submission and the fixture holds every task's rank
+    in the merged order (``g2_prio_all``, the engine's re-rank: dgp_set_priorities)."""
     from distributed.core import Status
     from distributed.scheduler import Scheduler, WorkerState
 
@@ -392,7 +397,7 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0, restr=
         for t, key in enumerate(keys2):
             ts = s.new_task(key, run_spec, "released")
             tidx[key] = N + t
-            ts.priority = (0, 2, int(g2["prio"][t]))
+            ts.priority = (-user_prio, 2, int(g2["prio"][t]))
             ov = int(g2["rootish_override"][t])
             if ov >= 0:
                 ts._rootish = bool(ov)
@@ -420,11 +425,13 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0, restr=
         ext["idx"] = np.array([d for r in rows for d in r], np.int32)
         recs2 = {ts.key: "waiting" for ts in sorted(new, key=lambda t: t.priority, reverse=True)}
         s._transitions(recs2, {}, {}, "update-graph-2")
-        if dep_frac or restr:
+        if dep_frac or restr or user_prio:
             gall = dict(prefix_names=g["prefix_names"], prefix_default_dur=g["prefix_default_dur"],
                         group_names=list(g["group_names"]) + list(g2["group_names"]))
             ext["dumps"].append(_dump(s, gall, tidx, widx, [ts.key for ts in tss] + [ts.key for ts in new]))
         tss.extend(new)
+        ext["prio_all"] = np.empty(len(tss), np.int64)
+        ext["prio_all"][sorted(range(len(tss)), key=lambda t: tss[t].priority)] = np.arange(len(tss))
 
     msgs = {k: [] for k in ("task", "worker", "run_id", "nbytes", "start", "stop", "status")}
     stim = [len(rec["task"])]
@@ -499,10 +506,15 @@ def main_second_graph(only):
                                       nthreads="random"), dict(n=2000, seed=48, restrict=0.3), 1.1, 0.3, 0, 0.0),
         "svcgrst_dep_satinf": (dict(n=2500, w=24, seed=49), dict(n=1500, seed=50, restrict=0.2), float("inf"), 0.5, 0,
                                0.2),
+        # later graphs submitted with a user priority: they outrank the earlier tasks (re-rank)
+        "svcgprio_c2var_sat1.1": (dict(n=3000, w=32, seed=53, n_inner_prefixes=3, random_durations=True,
+                                       nthreads="random"), dict(n=2000, seed=54), 1.1, 0.3, 0, 0.0, 1),
+        "svcgprio_c2mini_satinf": (dict(n=2500, w=24, seed=55), dict(n=1500, seed=56), float("inf"), 0.5, 0, 0.0, 1),
     }
     for name, (a, b, sat, frac, *more) in cases.items():
         nadd = more[0] if more else 0
         dep_frac = more[1] if len(more) > 1 else 0.0
+        user_prio = more[2] if len(more) > 2 else 0
         if only and name not in only:
             continue
         kw = {k: v for k, v in a.items() if k not in ("n", "w", "seed", "restrict")}
@@ -518,7 +530,7 @@ def main_second_graph(only):
         dask.config.set({"distributed.scheduler.worker-saturation": sat})
         cfg = G.config_dict(sat)
         rec, rounds, nplaced, states, msgs, round_ptr, at, joins, ext = replay_second_graph(
-            g, g2, cfg, 0, frac, nadd, dep_frac, restr=bool(b.get("restrict")))
+            g, g2, cfg, 0, frac, nadd, dep_frac, restr=bool(b.get("restrict")), user_prio=user_prio)
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -531,7 +543,9 @@ def main_second_graph(only):
             z.update(add_msg=np.array(joins["msg"], np.int64), add_nthreads=np.array(joins["nthreads"], np.int32))
         for k in ("dep_ptr", "dep_idx", "prio", "prefix_id", "group_id", "wanted", "rootish_override"):
             z["g2_" + k] = np.asarray(g2[k])
-        if dep_frac or b.get("restrict"):  # dependencies on earlier tasks (-1 - t), placements, resync rows
+        if user_prio:  # the merged ranks of every task (fixture order: the first graph's, then the later one's)
+            z.update(g2_user_prio=np.array(user_prio, np.int64), g2_prio_all=ext["prio_all"])
+        if dep_frac or b.get("restrict") or user_prio:  # dependencies on earlier tasks (-1 - t), placements, resync rows
             z.update(g2_dep_ptr=ext["ptr"], g2_dep_idx=ext["idx"], g2_nplaced=np.array(ext["nplaced"], np.int64),
                      **_pack_dumps(ext["dumps"]))
         if b.get("restrict"):

@@ -94,6 +94,18 @@ def test_extension_follows_a_later_graph_with_restrictions():
         assert r["active"] and r["graphs"] == 2 and r["resyncs"] == 1, r
 
 
+def test_extension_follows_a_later_graph_that_outranks_earlier_tasks():
+    """A later graph submitted with a user priority (_set_priorities, scheduler.py:4934-4981):
+    its tasks outrank every earlier one. The extension appends it deferred, hands the engine
+    every task's rank in the merged order (dgp_set_priorities), the scheduler decides that
+    update_graph stimulus and the engine resyncs; every later decision is the engine's
+    (validate=True) and the extension stays active."""
+    names = ["svcgprio_c2mini_satinf.npz", "svcgprio_c2var_sat1.1.npz"]
+    res = drive(names)
+    assert [r["fixture"] for r in res] == names
+    for r in res:
+        assert r["active"] and r["graphs"] == 2 and r["resyncs"] == 1, r
+
 
 EVENTS = ["svcev_c2var_sat1.1.npz", "svcev_c2mini_satinf.npz", "svcev_dense_sat1.0.npz"]
 

@@ -20,8 +20,8 @@ import os
 import numpy as np
 import pytest
 
-from conftest import (GOLDEN, second_graph, svc_dep_graph_files, svc_event_files, svc_p2p_files, svc_resync_files,
-                      svc_restr_graph_files)
+from conftest import (GOLDEN, second_graph, svc_dep_graph_files, svc_event_files, svc_p2p_files, svc_prio_graph_files,
+                      svc_resync_files, svc_restr_graph_files)
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -204,7 +204,7 @@ def test_service_p2p_shuffle_lifecycle_matches_reference(name):
     assert np.array_equal(out["final_state"], exp["final_state"])
 
 
-@pytest.mark.parametrize("name", svc_dep_graph_files() + svc_restr_graph_files())
+@pytest.mark.parametrize("name", svc_dep_graph_files() + svc_restr_graph_files() + svc_prio_graph_files())
 def test_service_dependent_later_graph_matches_reference(name):
     """A later graph whose tasks depend on earlier ones (in memory, processing, waiting or
     queued when it arrives): dgp_add_graph appends it (the earlier tasks' dependents rows
@@ -223,7 +223,8 @@ def test_service_dependent_later_graph_matches_reference(name):
     at = int(z["g2_msg"])
     g2 = second_graph(g, z)
     restr = "g2_restr_flags" in z.files  # svcgrst_*: worker restrictions on the later graph
-    assert restr or (np.asarray(g2["dep_idx"]) < 0).sum() > 0
+    rerank = "g2_prio_all" in z.files  # svcgprio_*: a user priority above the earlier tasks'
+    assert restr or rerank or (np.asarray(g2["dep_idx"]) < 0).sum() > 0
     joins = {}
     for m, nt in zip(z["add_msg"].tolist() if "add_msg" in z.files else [],
                      z["add_nthreads"].tolist() if "add_nthreads" in z.files else []):
@@ -238,7 +239,9 @@ def test_service_dependent_later_graph_matches_reference(name):
                     eng.add_worker(nt)
                 if i == at:
                     n0 = eng.num_placements()
-                    assert eng.add_graph(g2, defer=restr) == 0 and eng.num_placements() == n0
+                    assert eng.add_graph(g2, defer=restr or rerank) == 0 and eng.num_placements() == n0
+                    if rerank:  # every task's rank in the merged order (dgp_set_priorities)
+                        eng.set_priorities(z["g2_prio_all"])
                     with pytest.raises(_lib.DgpError, match="dgp_sync"):  # nothing runs before the resync
                         eng.tasks_finished(*[[c] for c in msgs[i]])
                     sl = slice(n0, n0 + int(z["g2_nplaced"]))
