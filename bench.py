@@ -138,7 +138,12 @@ def steal_leg(eng, args, world: int, dist=None, barrier=None) -> dict:
     eng.set_timing(False)
     leg = {"metric": "WorkStealing.balance() calls/s", "workload": f"C4-shaped: {args.steal_workers} workers x 2 "
            f"threads, {args.steal_tasks} processing tasks, 10% hot (zipf 1.5), 8 prefixes 10ms*2^j",
-           "ms_per_call": round(dt * 1e3, 3), "steal_requests": int(len(out["st_task"])), "n_gpus": world,
+           # GPUWorkStealing.balance()'s device path with a scheduler-free stand-in: the problem
+           # as host arrays in, dgp_steal_balance (upload, levels, bins, thief rows, the ordered
+           # walk), the ordered requests and per-worker accounts back; host-inclusive
+           "ms_per_call": round(dt * 1e3, 3), "fits_100ms_interval": bool(dt <= 0.1),
+           "boundary": "host arrays -> dgp_steal_balance -> request arrays (host-inclusive, ctypes included)",
+           "steal_requests": int(len(out["st_task"])), "n_gpus": world,
            "parallelism": "thief rows sharded + all-gather, ordered walk replicated" if world > 1 else "single",
            "kernel_ms_per_call": {k: round(v[0] / n_call, 3) for k, v in kt.items() if k.startswith("steal")},
            "reference_python_seconds_per_call_at_100k_x_4096": 242.0}
@@ -416,6 +421,16 @@ def c5_leg(eng_cls, local: int, args, dist, barrier) -> dict:
                                "sample": f"oracle/replay.cpp on this host, map {args.c5_cpu_map} + tree-reduce "
                                          f"({len(ref['pl_task'])} placements) x {args.c5_workers} workers; the "
                                          "rootish scan is O(W) per root, so the ratio reflects that scan"}
+    # the 1-core port on the FULL graph (tools/c5_cpu_full.py, minutes: run once per round on
+    # the GPU box's host and committed under profiles/), reported beside the sample
+    import glob
+
+    full = sorted(glob.glob(os.path.join(REPO, "profiles", "*_c5_cpu_full.json")))
+    if full and rank == 0:
+        f = json.load(open(full[-1]))
+        leg["cpu_baseline_full"] = {"value": f["placements_per_s"], "unit": "placements/s", "cores": 1, "kind": "port",
+                                    "seconds": f["seconds"], "digest_matches_gpu_pin": f["digest_matches_gpu_pin"],
+                                    "source": os.path.relpath(full[-1], REPO)}
     return leg
 
 
