@@ -79,7 +79,14 @@ __constant__ Dev c_dev;
 #define DGP_DBG_TASK 0  // diagnostics: exe_local dumps the candidate keys of frontier task D.dbg_task
 #endif
 #ifndef DGP_FAST
-#define DGP_FAST 1  // F_FAST stimuli take exe_fast (0: exe_local)
+#define DGP_FAST 0  // F_FAST stimuli take exe_fast (0: exe_local). Measured (profiles/r04ab): with exe_local
+                    // inlined and no exe_fast, C2 1.021 s vs 1.003-1.01 s and C3 0.118 vs 0.129 s
+#endif
+#ifndef DGP_LOCAL_INLINE
+#define DGP_LOCAL_INLINE 1  // exe_local inlined into the claim loop (else out of line, its own registers)
+#endif
+#ifndef DGP_DESC_G
+#define DGP_DESC_G 1  // PRE's gathered descriptor build first (0: the sequential form only)
 #endif
 #ifndef DGP_RB
 #define DGP_RB 8  // registrar batch (stimuli registered per poll, one lane each)
@@ -1817,7 +1824,8 @@ __device__ __attribute__((noinline)) DescOut build_desc_seq_entry(long long r) {
   return o;
 }
 __device__ __forceinline__ void build_desc(const Dev& D, SLds& L, long long r, int& p_out, double& dobs_out) {
-  DescOut o = build_desc_g_entry(r);
+  DescOut o{0, 0, 0.0};
+  if (DGP_DESC_G) o = build_desc_g_entry(r);
   if (!o.ok) o = build_desc_seq_entry(r);
   p_out = o.p;
   dobs_out = o.dobs;
@@ -4437,7 +4445,14 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
         int wk = -1;
         rc = exe_fast<LW>(D, L, P, cs, cr, cq, E, wk) ? wk : -2;
       }
-      if (rc == -2) rc = exe_local_entry<LW>(cs, cr, cq, cex ? 1 : 0, E);
+      if (rc == -2) {
+        if (DGP_LOCAL_INLINE) {
+          int wk = -1;
+          rc = exe_local<LW>(D, L, P, cs, cr, cq, cex, E, wk) ? wk : -2;
+        } else {
+          rc = exe_local_entry<LW>(cs, cr, cq, cex ? 1 : 0, E);
+        }
+      }
       hint = rc >= 0 ? rc : -1;
       if (rc == -2 && lane == 0) {
         atomicOr(&L.flags[cs], F_EXACT);
