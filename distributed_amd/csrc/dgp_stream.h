@@ -1553,7 +1553,7 @@ __device__ __attribute__((always_inline)) void build_desc_seq(const Dev& D, SLds
         const int i = tix[q];
         if (q < kx && i >= 0 && i < 32 && !((cmask >> i) & 1u)) {
           cmask |= 1u << i;
-          if (jf < NFF && i < TF) {
+          if (DGP_FAST && jf < NFF && i < TF) {  // exe_fast's rows (only it reads them)
             int64_t held = 0;
 #pragma unroll
             for (int q2 = 0; q2 < KX_MAX; q2++)
@@ -1774,7 +1774,7 @@ __device__ __attribute__((always_inline)) bool build_desc_g(const Dev& D, SLds& 
         const int ti = tix[i];
         if (i < kx && ti >= 0 && ti < 32 && !((cmask >> ti) & 1u)) {
           cmask |= 1u << ti;
-          if (j < NFF && ti < TF) {
+          if (DGP_FAST && j < NFF && ti < TF) {  // exe_fast's rows (only it reads them)
             int64_t held = 0;
 #pragma unroll
             for (int i2 = 0; i2 < KX_MAX; i2++)
