@@ -31,7 +31,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <cstddef>
 #include <cstdint>
 
 namespace dgp {
@@ -114,38 +113,6 @@ struct SRec;
 struct Pos;
 }  // namespace st
 
-// One task's dynamic fields in one 32-byte record: a stimulus dirties one line per task it
-// touches instead of one per field (the separate arrays wrote ~16x the placement payload).
-struct TRec {
-  int32_t remaining;  // |waiting_on|
-  int32_t waiters;    // |waiters|
-  int32_t proc_on;    // processing_on, -1 when not processing
-  int32_t run_id;     // placement-log position of each placed task
-  int32_t holder_of;  // the worker a task runs / ran on (its single replica; one of them under TD_MULTI)
-  int32_t fr_mark;    // stimulus whose completion empties the task's waiting_on
-  int32_t rel_mark;   // stimulus whose completion empties the task's waiters
-  uint8_t state;
-  uint8_t tdyn;       // TD_LR / TD_MULTI
-  uint8_t pad0, pad1;
-};
-static_assert(sizeof(TRec) == 32, "one task record per 32 bytes");
-// field OFF of every task's record, indexed like the array it replaces
-template <class T, size_t OFF>
-struct TF {
-  TRec* r;
-  __host__ __device__ __forceinline__ T& operator[](int64_t i) const {
-    return *reinterpret_cast<T*>(reinterpret_cast<char*>(r + i) + OFF);
-  }
-};
-// an int32 per task at a stride: a plain array, or a record field
-struct I32V {
-  char* p;
-  int32_t stride;
-  __host__ __device__ __forceinline__ int32_t& operator[](int64_t i) const {
-    return *reinterpret_cast<int32_t*>(p + i * stride);
-  }
-};
-
 struct Dev {
   int32_t N, W, WB, P, G, Wp;
   double bandwidth;  // SchedulerState.bandwidth: the config int, then the heartbeat EWMA (:4223-4226)
@@ -167,12 +134,11 @@ struct Dev {
   int64_t* res_nbytes;
   double* res_start;
   double* res_stop;
-  // task state: the TRec fields (one record per task)
-  TRec* trec;
-  TF<uint8_t, offsetof(TRec, state)> state;
-  TF<int32_t, offsetof(TRec, remaining)> remaining;
-  TF<int32_t, offsetof(TRec, waiters)> waiters;
-  TF<int32_t, offsetof(TRec, proc_on)> proc_on;
+  // task state
+  uint8_t* state;
+  int32_t* remaining;  // |waiting_on|
+  int32_t* waiters;    // |waiters|
+  int32_t* proc_on;    // processing_on, -1 when not processing
   int64_t* cur_nbytes;
   unsigned long long* holders;  // who_has bitsets [N][WB]
   unsigned long long* ready_key;
@@ -278,12 +244,12 @@ struct Dev {
   uint32_t* gw_needs_ext;    // needs_what overflow entries [W][NXW]
   unsigned long long* gw_held;  // [2][W] scratch of a global stimulus: held bytes, held deps per worker
   uint32_t* gw_needs_saved;  // needs_what lines between launches [W][NLW]
-  TF<int32_t, offsetof(TRec, run_id)> run_id;
-  TF<int32_t, offsetof(TRec, holder_of)> holder_of;
-  TF<uint8_t, offsetof(TRec, tdyn)> tdyn;
+  int32_t* run_id;           // placement-log position of each placed task
+  int32_t* holder_of;        // the worker a task runs / ran on (its single replica; one of them under TD_MULTI)
+  uint8_t* tdyn;             // TD_LR / TD_MULTI per task
   int32_t evf;               // EVF_* seen so far
-  TF<int32_t, offsetof(TRec, fr_mark)> fr_mark;
-  TF<int32_t, offsetof(TRec, rel_mark)> rel_mark;
+  int32_t* fr_mark;          // stimulus whose completion empties the task's waiting_on
+  int32_t* rel_mark;         // stimulus whose completion empties the task's waiters
   uint4* desc;               // descriptor ring [DR][NE]
   double* dring;             // stimulus durations [DR][PX] when the graph has more prefixes than a descriptor carries
   int32_t* touch_ring;       // distinct workers each prefetched stimulus touches [DR][TMAX]
@@ -308,7 +274,7 @@ struct Dev {
   // Service mode (dgp_tasks_finished): the accepted task-finished messages, in arrival order.
   const int32_t* stim_task;
   const int32_t* stim_worker;
-  I32V cseq;             // stimulus index of each task's completion (-1: not completed)
+  int32_t* cseq;         // stimulus index of each task's completion (-1: not completed)
   int32_t svc;           // 1: service mode (the launch ends at *svc_len)
   int32_t resident;      // service mode: the launch stays, answering requests from the mailbox
   void* mbox;            // resident service mailbox (dgp_service.h svc::Mbox, pinned host memory)
@@ -351,33 +317,6 @@ __device__ __forceinline__ char* lds_field(int W, int k) {
 #define WK_itcslots(D) WK_(D, w_itcslots, 8, int64_t)
 #define WK_lastcheck(D) WK_(D, w_lastcheck, 9, unsigned long long)
 #define WK_flags(D) WK_(D, w_flags, 10, uint8_t)
-
-// the task records' initial values (dgp_reset; the new tasks of dgp_add_graph)
-__global__ void k_trec_init(TRec* r, int64_t lo, int64_t hi) {
-  const int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= hi) return;
-  TRec t;
-  t.remaining = 0;
-  t.waiters = 0;
-  t.proc_on = -1;
-  t.run_id = -1;
-  t.holder_of = -1;
-  t.fr_mark = -1;
-  t.rel_mark = -1;
-  t.state = 0;
-  t.tdyn = 0;
-  t.pad0 = t.pad1 = 0;
-  r[i] = t;
-}
-// every task's state byte (dgp_get_task_states)
-__global__ void k_trec_state(const TRec* r, uint8_t* out, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = r[i].state;
-}
-__host__ inline void set_trec_views(Dev& D) {
-  D.state.r = D.remaining.r = D.waiters.r = D.proc_on.r = D.trec;
-  D.run_id.r = D.holder_of.r = D.fr_mark.r = D.rel_mark.r = D.tdyn.r = D.trec;
-}
 
 // ============================================================== small helpers
 

@@ -1395,10 +1395,7 @@ __device__ __attribute__((always_inline)) void bld_range(const Dev& D, SLds& L, 
         int m = -1;
         for (int64_t q = q0 + lane; q < q1; q += 64) m = max(m, D.cseq[fr ? D.dep_idx[q] : D.dpt_idx[q]]);
         m = wmax(m);
-        if (lane == 0) {
-          if (fr) D.fr_mark[x] = m;
-          else D.rel_mark[x] = m;
-        }
+        if (lane == 0) (fr ? D.fr_mark : D.rel_mark)[x] = m;
       }
       lds_fence();
     }

@@ -380,7 +380,7 @@ void stream_source(dgp_engine* e, bool service) {
   D.svc = service ? 1 : 0;
   D.stim_task = service ? D.sv_task : D.pl_task;
   D.stim_worker = service ? D.sv_worker : D.pl_worker;
-  D.cseq = service ? dgp::I32V{(char*)D.sv_cseq, 4} : dgp::I32V{(char*)&D.trec->run_id, (int32_t)sizeof(dgp::TRec)};
+  D.cseq = service ? D.sv_cseq : D.run_id;
 }
 
 // one launch of the stream kernel over the stimulus source set by stream_source()
@@ -711,8 +711,10 @@ int upload_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const i
   rc |= dalloc(e, &D.res_nbytes, N, L);
   rc |= dalloc(e, &D.res_start, N, L);
   rc |= dalloc(e, &D.res_stop, N, L);
-  rc |= dalloc(e, &D.trec, N, L);
-  dgp::set_trec_views(D);
+  rc |= dalloc(e, &D.state, N, L);
+  rc |= dalloc(e, &D.remaining, N, L);
+  rc |= dalloc(e, &D.waiters, N, L);
+  rc |= dalloc(e, &D.proc_on, N, L);
   rc |= dalloc(e, &D.cur_nbytes, N, L);
   rc |= dalloc(e, &D.holders, (size_t)N * D.WB, L);
   rc |= dalloc(e, &D.ready_key, N, L);
@@ -764,6 +766,11 @@ int upload_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const i
   rc |= dalloc(e, &D.st_wsnbytes, D.st_cap, L);
   rc |= dalloc(e, &D.st_route, D.st_cap, L);
   rc |= dalloc(e, &D.ready, N, L);
+  rc |= dalloc(e, &D.run_id, N, L);
+  rc |= dalloc(e, &D.holder_of, N, L);
+  rc |= dalloc(e, &D.tdyn, N, L);
+  rc |= dalloc(e, &D.fr_mark, N, L);
+  rc |= dalloc(e, &D.rel_mark, N, L);
   D.rlog_cap = std::max<int64_t>(2 * N + 4096, e->log_min[2]);
   rc |= dalloc(e, &D.rlog, D.rlog_cap, L);
   // service mode: the stimulus log (each task completes at most once) and its length
@@ -1042,8 +1049,10 @@ int dgp_reset(dgp_engine* e) {
   hipStream_t s = e->stream;
   HIPCHK(e, hipMemsetAsync(e->ctl, 0, sizeof(dgp::Ctl), s));
   HIPCHK(e, hipMemsetAsync(e->d_aux, 0, 4 * sizeof(long long), s));
-  hipLaunchKernelGGL(dgp::k_trec_init, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, D.trec, (int64_t)0, (int64_t)N);
-  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipMemsetAsync(D.state, 0, N, s));
+  HIPCHK(e, hipMemsetAsync(D.remaining, 0, N * 4, s));
+  HIPCHK(e, hipMemsetAsync(D.waiters, 0, N * 4, s));
+  HIPCHK(e, hipMemsetAsync(D.proc_on, 0xff, N * 4, s));
   HIPCHK(e, hipMemsetAsync(D.cur_nbytes, 0xff, N * 8, s));
   HIPCHK(e, hipMemsetAsync(D.holders, 0, N * D.WB * 8, s));
   HIPCHK(e, hipMemsetAsync(D.ready_key, 0, N * 8, s));
@@ -1051,8 +1060,13 @@ int dgp_reset(dgp_engine* e) {
   HIPCHK(e, hipMemsetAsync(D.cand_n, 0, N * 4, s));
   {  // stream engine
     namespace S = dgp::st;
+    HIPCHK(e, hipMemsetAsync(D.run_id, 0xff, N * 4, s));
+    HIPCHK(e, hipMemsetAsync(D.holder_of, 0xff, N * 4, s));
+    HIPCHK(e, hipMemsetAsync(D.tdyn, 0, N, s));
     D.evf = 0;
     e->paused_h.assign(D.W, 0);
+    HIPCHK(e, hipMemsetAsync(D.fr_mark, 0xff, N * 4, s));
+    HIPCHK(e, hipMemsetAsync(D.rel_mark, 0xff, N * 4, s));
     HIPCHK(e, hipMemsetAsync(D.thdr, 0, (size_t)S::DR * sizeof(uint2), s));
     HIPCHK(e, hipMemsetAsync(D.gw_needs_ext, 0, (size_t)D.W * S::NXW * 4, s));
     HIPCHK(e, hipMemsetAsync(D.gw_needs_saved, 0, (size_t)D.W * S::NLW * 4, s));
@@ -1632,11 +1646,10 @@ static int add_graph_impl(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, 
   HIPCHK(e, carry(D.res_nbytes, old.res_nbytes, n0 * 8, n1 * 8, 0xff));
   HIPCHK(e, carry(D.res_start, old.res_start, n0 * 8, n1 * 8, 0));
   HIPCHK(e, carry(D.res_stop, old.res_stop, n0 * 8, n1 * 8, 0));
-  // the task records: the old tasks' carried, the new ones initial
-  if (n0) HIPCHK(e, hipMemcpyAsync(D.trec, old.trec, n0 * sizeof(dgp::TRec), hipMemcpyDeviceToDevice, s));
-  hipLaunchKernelGGL(dgp::k_trec_init, dim3((unsigned)((n1 - n0 + 255) / 256)), dim3(256), 0, s, D.trec, (int64_t)n0,
-                     (int64_t)n1);
-  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, carry(D.state, old.state, n0, n1, 0));
+  HIPCHK(e, carry(D.remaining, old.remaining, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.waiters, old.waiters, n0 * 4, n1 * 4, 0));
+  HIPCHK(e, carry(D.proc_on, old.proc_on, n0 * 4, n1 * 4, 0xff));
   HIPCHK(e, carry(D.cur_nbytes, old.cur_nbytes, n0 * 8, n1 * 8, 0xff));
   HIPCHK(e, carry(D.holders, old.holders, n0 * D.WB * 8, n1 * D.WB * 8, 0));
   HIPCHK(e, carry(D.ready_key, old.ready_key, n0 * 8, n1 * 8, 0));
@@ -1650,6 +1663,11 @@ static int add_graph_impl(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, 
   HIPCHK(e, carry(D.pl_start, old.pl_start, p0 * 8, p1 * 8, 0));
   HIPCHK(e, carry(D.pl_wsnbytes, old.pl_wsnbytes, p0 * 8, p1 * 8, 0));
   HIPCHK(e, carry(D.pl_route, old.pl_route, p0, p1, 0));
+  HIPCHK(e, carry(D.run_id, old.run_id, n0 * 4, n1 * 4, 0xff));
+  HIPCHK(e, carry(D.holder_of, old.holder_of, n0 * 4, n1 * 4, 0xff));
+  HIPCHK(e, carry(D.tdyn, old.tdyn, n0, n1, 0));
+  HIPCHK(e, carry(D.fr_mark, old.fr_mark, n0 * 4, n1 * 4, 0xff));
+  HIPCHK(e, carry(D.rel_mark, old.rel_mark, n0 * 4, n1 * 4, 0xff));
   HIPCHK(e, carry(D.rlog, old.rlog, (size_t)old_rlog * sizeof(dgp::st::SRec), (size_t)D.rlog_cap * sizeof(dgp::st::SRec), 0));
   HIPCHK(e, carry(D.sv_task, old.sv_task, (size_t)old.sv_cap * 4, (size_t)D.sv_cap * 4, 0));
   HIPCHK(e, carry(D.sv_worker, old.sv_worker, (size_t)old.sv_cap * 4, (size_t)D.sv_cap * 4, 0));
@@ -2397,14 +2415,7 @@ int dgp_get_task_states(dgp_engine* e, uint8_t* state) {
   if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->have_graph || !state) return fail(e, DGP_E_ARG, "graph first");
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  uint8_t* d = nullptr;
-  HIPCHK(e, hipMalloc((void**)&d, std::max<int64_t>(e->D.N, 1)));
-  hipLaunchKernelGGL(dgp::k_trec_state, dim3((unsigned)((e->D.N + 255) / 256)), dim3(256), 0, e->stream, e->D.trec, d,
-                     (int64_t)e->D.N);
-  hipError_t st = hipStreamSynchronize(e->stream);
-  if (st == hipSuccess) st = hipMemcpy(state, d, e->D.N, hipMemcpyDeviceToHost);
-  (void)hipFree(d);
-  HIPCHK(e, st);
+  HIPCHK(e, hipMemcpy(state, e->D.state, e->D.N, hipMemcpyDeviceToHost));
   return 0;
 }
 
