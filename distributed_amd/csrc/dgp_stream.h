@@ -85,6 +85,9 @@ __constant__ Dev c_dev;
 #ifndef DGP_LOCAL_INLINE
 #define DGP_LOCAL_INLINE 1  // exe_local inlined into the claim loop (else out of line, its own registers)
 #endif
+#ifndef DGP_STAGE_DELAY
+#define DGP_STAGE_DELAY 0  // diagnostics: 1 / 2 delay every BLD / PRE batch (4 x s_sleep 127, ~32k cycles)
+#endif
 #ifndef DGP_DESC_G
 #define DGP_DESC_G 1  // PRE's gathered descriptor build first (0: the sequential form only)
 #endif
@@ -1883,6 +1886,8 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
     }
     __threadfence_block();
     wbar();
+    if (DGP_STAGE_DELAY && KIND == DGP_STAGE_DELAY - 1)  // diagnostics: is this stage on the critical path?
+      for (int k = 0; k < 4; k++) __builtin_amdgcn_s_sleep(127);
     if (lane == 0) {
       PROF(S.prof[KIND == 0 ? 1 : 2] += mclk() - t0);
       PROF(S.prof[KIND == 0 ? 6 : 7] += 1);
