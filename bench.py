@@ -581,6 +581,28 @@ def main():
             else:
                 result["roofline"]["traffic"] = round(t["traffic_bytes_per_launch"], 1)
                 result["roofline"]["traffic_source"] = t.get("source")
+        # a measured copy peak beside the 8 TB/s datasheet figure: a 2 GiB
+        # device-to-device copy, read + written bytes over its event-timed duration
+        try:
+            import torch
+
+            src = torch.empty(1 << 31, dtype=torch.uint8, device=f"cuda:{local}")
+            dst = torch.empty_like(src)
+            dst.copy_(src)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            best = None
+            for _ in range(5):
+                e0.record()
+                dst.copy_(src)
+                e1.record()
+                torch.cuda.synchronize()
+                ms_c = e0.elapsed_time(e1)
+                best = ms_c if best is None else min(best, ms_c)
+            result["roofline"]["copy_peak_measured"] = round(2 * src.numel() / (best * 1e-3) / 1e9, 1)
+            del src, dst
+            torch.cuda.empty_cache()
+        except Exception as ex:  # reported, never fatal
+            result["roofline"]["copy_peak_measured"] = f"unavailable: {ex}"
         if not args.no_latency:
             link_us = link_latency_us(PlacementEngine, local)
             result["latency_bound"] = latency_bound(g, out, link_us, 1e3 * elapsed / args.steps)

@@ -131,39 +131,48 @@ def graph_from_tasks(tss, nthreads, valid_workers=None, worker_index=None, earli
     tss = sorted(tss, key=lambda ts: ts.priority)
     index = {ts.key: i for i, ts in enumerate(tss)}
     n = len(tss)
-    rows = []
-    for ts in tss:
-        r = []
-        for d in ts.dependencies:
-            i = index.get(d.key)
-            if i is None:
-                j = earlier.get(d.key) if earlier is not None else None
-                if j is None:
-                    raise ValueError(f"dependency {d.key!r} of {ts.key!r} is not in the uploaded graph")
-                i = -1 - j
-            r.append(i)
-        rows.append(sorted(r))
+    # the dependency edges in bulk: every row's keys flattened, mapped to indices (an earlier
+    # task as -1 - its engine index), then each row sorted by one lexsort
+    counts = np.fromiter((len(ts.dependencies) for ts in tss), np.int64, n)
+    dkeys = [d.key for ts in tss for d in ts.dependencies]
+    none = -(1 << 40)
+    if earlier is None:
+        didx = np.fromiter((index.get(k, none) for k in dkeys), np.int64, len(dkeys))
+    else:
+        didx = np.fromiter((index[k] if k in index else -1 - earlier.get(k, -none) for k in dkeys), np.int64,
+                           len(dkeys))
+    bad = (didx == none) | (didx <= -1 + none)
+    if bad.any():
+        k = int(np.flatnonzero(bad)[0])
+        row = int(np.searchsorted(np.cumsum(counts), k, side="right"))
+        raise ValueError(f"dependency {dkeys[k]!r} of {tss[row].key!r} is not in the uploaded graph")
+    rowid = np.repeat(np.arange(n, dtype=np.int64), counts)
+    didx = didx[np.lexsort((didx, rowid))]
     pnames, gnames, gpref = {}, {}, []
-    pid = np.zeros(n, np.int32)
-    gid = np.zeros(n, np.int32)
     pdur = []
-    for i, ts in enumerate(tss):
-        p = ts.prefix.name
-        if p not in pnames:
-            pnames[p] = len(pnames)
-            pdur.append(float(ts.prefix.duration_average))
-        g = ts.group.name
-        if g not in gnames:
-            gnames[g] = len(gnames)
-            gpref.append(pnames[p])
-        pid[i] = pnames[p]
-        gid[i] = gnames[g]
+    pid = np.empty(n, np.int32)
+    gid = np.empty(n, np.int32)
+    pl = [ts.prefix for ts in tss]
+    gl = [ts.group.name for ts in tss]
+    for i in range(n):
+        p = pl[i].name
+        q = pnames.get(p)
+        if q is None:
+            q = pnames[p] = len(pnames)
+            pdur.append(float(pl[i].duration_average))
+        pid[i] = q
+        gn = gl[i]
+        h = gnames.get(gn)
+        if h is None:
+            h = gnames[gn] = len(gnames)
+            gpref.append(q)
+        gid[i] = h
     ptr = np.zeros(n + 1, np.int64)
-    ptr[1:] = np.cumsum([len(r) for r in rows])
+    np.cumsum(counts, out=ptr[1:])
     g = dict(
         n_tasks=n,
         dep_ptr=ptr,
-        dep_idx=np.array([d for r in rows for d in r], np.int32),
+        dep_idx=didx.astype(np.int32),
         prio=np.arange(n, dtype=np.int64),
         prefix_id=pid,
         group_id=gid,
