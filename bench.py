@@ -311,13 +311,16 @@ def service_leg(eng_cls, local: int, args) -> dict:
            "n_tasks": int(g["n_tasks"])}
     outs = {}
     cols = ("pl_task", "pl_worker")
+    window = args.svc_window_us * 1e-6
     for mode in ("per_round", "per_message", "per_round_resident", "per_message_resident", "per_round_messages",
-                 "per_message_resident_ext"):
+                 "per_message_resident_ext", "per_message_overlap_ext"):
         eng = eng_cls(local)
         eng.load(g, CONFIG, results=False)
         eng.set_resident("resident" in mode)
-        if mode == "per_message_resident_ext":  # the answers carry the message fields (f3)
+        if mode.endswith("_ext"):  # the answers carry the message fields (f3)
             eng.set_task_messages(True)
+        if mode == "per_message_overlap_ext":
+            eng.set_resident(True)
         eng.update_graph()
         done, calls = 0, 0
         n = eng.num_placements()
@@ -339,6 +342,23 @@ def service_leg(eng_cls, local: int, args) -> dict:
                     n_dep += len(m["dep_task"])
                 n += k
                 calls += 1
+            elif mode == "per_message_overlap_ext":
+                # GPUPlacementExtension's path: post the message, run the reference handler's
+                # Python up to its first decision (stood in for by `window` of host work: the
+                # overlap window tests/ext_driver.py measures), then the answer, the new
+                # placements and their message fields through engine.answer
+                tl, wl, rl, nbl, al, bl = t.tolist(), w.tolist(), r.tolist(), nb.tolist(), a.tolist(), b.tolist()
+                for i in range(len(tl)):
+                    eng.tasks_finished_post((tl[i],), (wl[i],), (rl[i],), (nbl[i],), (al[i],), (bl[i],))
+                    t_end = time.perf_counter() + window
+                    while time.perf_counter() < t_end:
+                        pass
+                    _, k = eng.tasks_finished_wait()
+                    if k:
+                        m = eng.answer(n, k, True)[2]
+                        n_dep += len(m[1])
+                    n += k
+                    calls += 1
             else:
                 ext = mode == "per_message_resident_ext"
                 for i in range(len(t)):
@@ -361,6 +381,9 @@ def service_leg(eng_cls, local: int, args) -> dict:
         eng.close()
         leg[mode] = {"messages_per_s": round(g["n_tasks"] / dt, 1), "calls": calls,
                      "us_per_call": round(dt / max(calls, 1) * 1e6, 1), "seconds": round(dt, 4)}
+        if mode == "per_message_overlap_ext":  # what the drop-in adds to the handler's own time
+            leg[mode].update(host_window_us=args.svc_window_us,
+                             exposed_us_per_call=round(dt / max(calls, 1) * 1e6 - args.svc_window_us, 1))
         if n_msg:  # dgp_task_messages (_task_to_msg fields) per batch, host-inclusive
             leg[mode].update(task_messages_calls=n_msg, task_messages_us_per_call=round(t_msg / n_msg * 1e6, 1),
                              task_messages_dependencies=n_dep)
@@ -453,6 +476,9 @@ def main():
     ap.add_argument("--no-service", action="store_true", help="skip the service-mode (dgp_tasks_finished) leg")
     ap.add_argument("--no-variants", action="store_true", help="skip the 16-prefix C2 / restricted C3 legs")
     ap.add_argument("--svc-tasks", type=int, default=20_000)
+    ap.add_argument("--svc-window-us", type=float, default=50.0,
+                    help="host work between post and wait in the overlapped service leg (the extension's "
+                         "window before its first decision: tests/ext_driver.py us_overlap_window)")
     ap.add_argument("--c5-map", type=int, default=8_750_000)
     ap.add_argument("--c5-workers", type=int, default=16_384)
     ap.add_argument("--c5-cpu-map", type=int, default=200_000, help="map tasks of the C5 CPU-baseline sample")

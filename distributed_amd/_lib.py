@@ -34,6 +34,8 @@ SIGNATURES = {
     "dgp_tasks_finished": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dgp_set_resident": (C.c_int, [_P, C.c_int]),
     "dgp_set_task_messages": (C.c_int, [_P, C.c_int]),
+    "dgp_tasks_finished_post": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P]),
+    "dgp_tasks_finished_wait": (C.c_int, [_P, _P, _P]),
     "dgp_move_task": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "dgp_add_worker": (C.c_int, [_P, C.c_int32, _P]),
     "dgp_add_graph": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P, _P]),
@@ -77,7 +79,7 @@ SIGNATURES = {
                                    _P, _P, _P]),
 }
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 _lib = None
 
 

@@ -117,6 +117,11 @@ struct dgp_engine {
   bool res_hung = false;             // the resident kernel did not end when told to: the engine is unusable
   bool pending_resync = false;       // a later graph with dependencies on earlier tasks: dgp_sync_* next
   unsigned long long req_seq = 0;    // the last request number sent
+  // dgp_tasks_finished_post: 0 nothing posted, 1 a batch in the resident mailbox awaiting its
+  // answer, 2 answered at the post (launch per call) and kept for dgp_tasks_finished_wait
+  int posted = 0;
+  int64_t posted_n = 0, posted_new = 0;
+  std::vector<int8_t> posted_status;
   int64_t res_prof[4] = {0, 0, 0, 0};  // requests answered; sums of append, run, publish (device 100 MHz ticks)
   int64_t res_role[7] = {0, 0, 0, 0, 0, 0, 0};  // sums of each role's last batch end after the append
 };
@@ -230,6 +235,7 @@ int check_device_error(dgp_engine* e, dgp::Ctl* out = nullptr) {
 // engine's stream or device state while it runs.
 int resident_stop(dgp_engine* e) {
   if (e && e->res_hung) return fail(e, DGP_E_DEVICE, "the resident kernel did not end: the engine is unusable");
+  if (e && e->posted) return fail(e, DGP_E_STATE, "a posted task-finished batch: dgp_tasks_finished_wait first");
   if (!e || !e->res_running) return 0;
   __atomic_store_n(&e->mb->stop, 1, __ATOMIC_RELEASE);
   const hipError_t st = hipStreamSynchronize(e->stream);
@@ -239,6 +245,8 @@ int resident_stop(dgp_engine* e) {
   if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("resident kernel: ") + hipGetErrorString(st));
   return 0;
 }
+
+int resident_wait(dgp_engine* e, int8_t* status, int64_t* n_new_placements);  // below
 
 // A kernel's static LDS bytes as built (the module-wide LDS lowering, build.py, allocates
 // every LDS variable its out-of-line callees use at fixed addresses in the kernel's block)
@@ -525,6 +533,11 @@ dgp_engine* dgp_create(int device) {
 void dgp_destroy(dgp_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
+  if (e->posted == 1) {  // a posted batch: its answer first (the kernel is inside the request)
+    std::vector<int8_t> st((size_t)std::max<int64_t>(e->posted_n, 1));
+    (void)resident_wait(e, st.data(), nullptr);
+  }
+  e->posted = 0;
   (void)resident_stop(e);
   (void)hipStreamSynchronize(e->stream);
   if (e->mb) (void)hipHostFree(e->mb);
@@ -1178,9 +1191,24 @@ namespace {
 // message checks, every stimulus it accepts run to completion, the new placements copied
 // back); the host only spins on the answer. A kernel that ended on its own (no request for
 // a while) or never started is launched first; the logs grow with the kernel stopped.
-int tasks_finished_resident(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker,
-                            const int64_t* run_id, const int64_t* nbytes, const double* start, const double* stop,
-                            int8_t* status, int64_t* n_new_placements) {
+// resident_post returns as soon as the request is published (dgp_tasks_finished_post: the
+// caller's own work overlaps the device's), resident_wait takes the answer.
+int resident_launch(dgp_engine* e) {
+  dgp::Dev& D = e->D;
+  if (int rc = sync_dev(e)) return rc;
+  stream_source(e, true);
+  D.resident = 1;
+  D.mbox = (void*)e->mb_dev;
+  if (int rc = launch_stream(e, -1, 0)) {
+    D.resident = 0;
+    return rc;
+  }
+  e->res_running = true;
+  return 0;
+}
+
+int resident_post(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* run_id,
+                  const int64_t* nbytes, const double* start, const double* stop) {
   namespace V = dgp::svc;
   dgp::Dev& D = e->D;
   const int64_t plc = std::min<int64_t>(std::max<int64_t>(D.N, 1024), 1 << 20);
@@ -1215,22 +1243,21 @@ int tasks_finished_resident(dgp_engine* e, int64_t n, const int32_t* task, const
   e->mb->n = n;
   e->mb->want_msgs = e->res_msgs ? 1 : 0;
   e->mb->msg_from = -1;
-  auto launch = [&]() -> int {
-    if (int rc = sync_dev(e)) return rc;
-    stream_source(e, true);
-    D.resident = 1;
-    D.mbox = (void*)e->mb_dev;
-    if (int rc = launch_stream(e, -1, 0)) {
-      D.resident = 0;
-      return rc;
-    }
-    e->res_running = true;
-    return 0;
-  };
   if (!e->res_running)
-    if (int rc = launch()) return rc;
+    if (int rc = resident_launch(e)) return rc;
   const unsigned long long seq = ++e->req_seq;
   __atomic_store_n(&e->mb->req_seq, seq, __ATOMIC_RELEASE);
+  e->posted = 1;
+  e->posted_n = n;
+  return 0;
+}
+
+int resident_wait(dgp_engine* e, int8_t* status, int64_t* n_new_placements) {
+  namespace V = dgp::svc;
+  dgp::Dev& D = e->D;
+  const int64_t n = e->posted_n;
+  const unsigned long long seq = e->req_seq;
+  e->posted = 0;  // answered or failed below: the engine's other entry points are open again
   const auto t0 = std::chrono::steady_clock::now();
   for (long spins = 0; __atomic_load_n(&e->mb->done_seq, __ATOMIC_ACQUIRE) != seq; spins++) {
     if ((spins & 255) == 255) {
@@ -1239,7 +1266,7 @@ int tasks_finished_resident(dgp_engine* e, int64_t n, const int32_t* task, const
         D.resident = 0;
         if (int rc = check_device_error(e)) return rc;
         if (__atomic_load_n(&e->mb->done_seq, __ATOMIC_ACQUIRE) == seq) break;
-        if (int rc = launch()) return rc;
+        if (int rc = resident_launch(e)) return rc;
       }
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
         // told to stop, waited for a bounded time (a kernel stuck inside a request never
@@ -1301,20 +1328,31 @@ int dgp_set_resident(dgp_engine* e, int enabled) {
   return 0;
 }
 
-int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* run_id,
-                       const int64_t* nbytes, const double* start, const double* stop, int8_t* status,
-                       int64_t* n_new_placements) {
+}  // extern "C"
+
+namespace {
+
+// the preconditions of dgp_tasks_finished / dgp_tasks_finished_post
+int tf_check(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* run_id,
+             const int64_t* nbytes, const double* start, const double* stop) {
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (e->posted) return fail(e, DGP_E_STATE, "a posted task-finished batch: dgp_tasks_finished_wait first");
   if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
   if (e->pending_resync) return fail(e, DGP_E_STATE, "dgp_tasks_finished: dgp_sync_* first (a later graph depends on earlier tasks)");
-  if (n < 0 || (n > 0 && (!task || !worker || !run_id || !nbytes || !start || !stop || !status)))
+  if (n < 0 || (n > 0 && (!task || !worker || !run_id || !nbytes || !start || !stop)))
     return fail(e, DGP_E_ARG, "dgp_tasks_finished: bad batch");
-  if (n_new_placements) *n_new_placements = 0;
   HIPCHK(e, hipSetDevice(e->device));
   e->mode = 2;
-  if (n == 0) return 0;
-  if (e->resident && e->D.P <= dgp::st::PX) return tasks_finished_resident(e, n, task, worker, run_id, nbytes, start, stop,
-                                                                           status, n_new_placements);
+  return 0;
+}
+
+bool tf_resident(const dgp_engine* e) { return e->resident && e->D.P <= dgp::st::PX; }
+
+// dgp_tasks_finished launched per call: the batch copied to the device, the service kernels,
+// the answers copied back
+int tasks_finished_launch(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker,
+                          const int64_t* run_id, const int64_t* nbytes, const double* start, const double* stop,
+                          int8_t* status, int64_t* n_new_placements) {
   if (int rc = resident_stop(e)) return rc;
   namespace V = dgp::svc;
   if (n > e->msgs_cap) {  // grow the pinned staging and the device batch
@@ -1356,6 +1394,52 @@ int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int3
   if (n_new_placements) *n_new_placements = (int64_t)(c.n_placed - e->last_placed);
   e->last_placed = c.n_placed;
   for (int64_t i = 0; i < n; i++) e->sv_used += status[i] == DGP_TF_ACCEPTED ? 1 : 0;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* run_id,
+                       const int64_t* nbytes, const double* start, const double* stop, int8_t* status,
+                       int64_t* n_new_placements) {
+  if (int rc = tf_check(e, n, task, worker, run_id, nbytes, start, stop)) return rc;
+  if (n > 0 && !status) return fail(e, DGP_E_ARG, "dgp_tasks_finished: bad batch");
+  if (n_new_placements) *n_new_placements = 0;
+  if (n == 0) return 0;
+  if (tf_resident(e)) {
+    if (int rc = resident_post(e, n, task, worker, run_id, nbytes, start, stop)) return rc;
+    return resident_wait(e, status, n_new_placements);
+  }
+  return tasks_finished_launch(e, n, task, worker, run_id, nbytes, start, stop, status, n_new_placements);
+}
+
+int dgp_tasks_finished_post(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker,
+                            const int64_t* run_id, const int64_t* nbytes, const double* start, const double* stop) {
+  if (int rc = tf_check(e, n, task, worker, run_id, nbytes, start, stop)) return rc;
+  if (n > 0 && tf_resident(e)) return resident_post(e, n, task, worker, run_id, nbytes, start, stop);
+  // launch per call: answered here, kept for the wait
+  e->posted_status.assign((size_t)std::max<int64_t>(n, 1), 0);
+  e->posted_new = 0;
+  if (n > 0)
+    if (int rc = tasks_finished_launch(e, n, task, worker, run_id, nbytes, start, stop, e->posted_status.data(),
+                                       &e->posted_new))
+      return rc;
+  e->posted = 2;
+  e->posted_n = n;
+  return 0;
+}
+
+int dgp_tasks_finished_wait(dgp_engine* e, int8_t* status, int64_t* n_new_placements) {
+  if (!e) return DGP_E_ARG;
+  if (!e->posted) return fail(e, DGP_E_STATE, "dgp_tasks_finished_wait: no batch posted");
+  if (e->posted_n > 0 && !status) return fail(e, DGP_E_ARG, "dgp_tasks_finished_wait: no status array");
+  if (n_new_placements) *n_new_placements = 0;
+  if (e->posted == 1) return resident_wait(e, status, n_new_placements);
+  if (e->posted_n > 0) memcpy(status, e->posted_status.data(), (size_t)e->posted_n);
+  if (n_new_placements) *n_new_placements = e->posted_new;
+  e->posted = 0;
   return 0;
 }
 
@@ -2225,6 +2309,10 @@ int dgp_snapshot(dgp_engine* e) {
 
 int64_t dgp_num_placements(dgp_engine* e) {
   if (!e) return -1;
+  if (e->posted) {
+    fail(e, DGP_E_STATE, "a posted task-finished batch: dgp_tasks_finished_wait first");
+    return -1;
+  }
   // the resident kernel publishes the log length with every answer
   if (e->res_running) return __atomic_load_n(&e->mb->n_placed, __ATOMIC_ACQUIRE);
   dgp::Ctl c;
@@ -2235,6 +2323,7 @@ int64_t dgp_num_placements(dgp_engine* e) {
 int dgp_get_placements(dgp_engine* e, int64_t offset, int64_t count, int32_t* task, int32_t* worker,
                        int64_t* comm_bytes, double* start_time, int64_t* ws_nbytes, int8_t* route) {
   if (!e || offset < 0 || count < 0) return fail(e, DGP_E_ARG, "bad range");
+  if (e->posted) return fail(e, DGP_E_STATE, "a posted task-finished batch: dgp_tasks_finished_wait first");
   if (e->res_running) {  // the last answer's new placements are in the mailbox (task / worker)
     const int64_t a = e->mb->pl_from, b = e->mb->n_placed;
     if (a >= 0 && offset >= a && offset + count <= b && !comm_bytes && !start_time && !ws_nbytes && !route) {
@@ -2266,6 +2355,7 @@ int dgp_get_placements(dgp_engine* e, int64_t offset, int64_t count, int32_t* ta
 int dgp_task_messages(dgp_engine* e, int64_t offset, int64_t count, int64_t* n_deps, int64_t* n_holders,
                       int64_t* dep_ptr, int32_t* dep_task, int64_t* dep_nbytes, int64_t* holder_ptr,
                       int32_t* holder_idx) {
+  if (e && e->posted) return fail(e, DGP_E_STATE, "a posted task-finished batch: dgp_tasks_finished_wait first");
   if (e && e->res_running && n_deps && n_holders && offset >= 0 && count >= 0) {
     // the last resident answer's placements: their fields are in the mailbox (dgp_set_task_messages)
     namespace V = dgp::svc;

@@ -62,6 +62,14 @@ class PlacementEngine:
         self.n_tasks = 0
         self.n_workers = 0
         self._keep = []
+        self._posted_n = 0
+        # per-call buffers of the extension's service path (tasks_finished_post / _wait, answer)
+        self._one = None
+        self._st = np.zeros(64, np.int8)
+        self._st_ptr = _ptr(self._st)
+        self._newp, self._nd, self._nh = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+        self._newp_ref, self._nd_ref, self._nh_ref = C.byref(self._newp), C.byref(self._nd), C.byref(self._nh)
+        self._ans = None
 
     # ------------------------------------------------------------------ plumbing
     def _check(self, rc: int, what: str):
@@ -159,11 +167,8 @@ class PlacementEngine:
     # answers of dgp_tasks_finished (include/dgplace.h DGP_TF_*)
     TF_ACCEPTED, TF_FREE_KEYS, TF_ADD_KEYS, TF_RELEASE, TF_UNKNOWN_WORKER, TF_IMPOSSIBLE, TF_UNSUPPORTED = range(7)
 
-    def tasks_finished(self, task, worker, run_id, nbytes=None, start=None, stop=None):
-        """A batch of task-finished messages (Scheduler.handle_task_finished,
-        distributed/scheduler.py:5783-5797), in arrival order. ``nbytes`` < 0 means None;
-        ``start``/``stop`` is the "compute" startstop (NaN: none). Returns (status per
-        message, number of placements the batch made)."""
+    @staticmethod
+    def _tf_batch(task, worker, run_id, nbytes, start, stop):
         t = np.ascontiguousarray(task, np.int32).reshape(-1)
         n = len(t)
         w = np.ascontiguousarray(worker, np.int32).reshape(-1)
@@ -173,11 +178,90 @@ class PlacementEngine:
         b = np.ascontiguousarray(np.full(n, np.nan) if stop is None else stop, np.float64).reshape(-1)
         if not (len(w) == len(r) == len(nb) == len(a) == len(b) == n):
             raise ValueError("tasks_finished: all message fields need the same length")
+        return n, (t, w, r, nb, a, b)
+
+    def tasks_finished(self, task, worker, run_id, nbytes=None, start=None, stop=None):
+        """A batch of task-finished messages (Scheduler.handle_task_finished,
+        distributed/scheduler.py:5783-5797), in arrival order. ``nbytes`` < 0 means None;
+        ``start``/``stop`` is the "compute" startstop (NaN: none). Returns (status per
+        message, number of placements the batch made)."""
+        n, cols = self._tf_batch(task, worker, run_id, nbytes, start, stop)
         st = np.zeros(n, np.int8)
         newp = C.c_int64(0)
-        self._check(self.lib.dgp_tasks_finished(self.h, n, _ptr(t), _ptr(w), _ptr(r), _ptr(nb), _ptr(a), _ptr(b),
-                                                _ptr(st), C.byref(newp)), "dgp_tasks_finished")
+        self._check(self.lib.dgp_tasks_finished(self.h, n, *map(_ptr, cols), _ptr(st), C.byref(newp)),
+                    "dgp_tasks_finished")
         return st, int(newp.value)
+
+    def tasks_finished_post(self, task, worker, run_id, nbytes=None, start=None, stop=None):
+        """The first half of ``tasks_finished`` (dgp_tasks_finished_post): the batch goes to
+        the device and the call returns; ``tasks_finished_wait`` takes the answer. In
+        between, the caller's own work runs while the device decides. A one-message batch
+        goes through preallocated buffers (the extension's per-message case)."""
+        if len(task) == 1 and nbytes is not None and start is not None and stop is not None:
+            one = self._one
+            if one is None:
+                one = self._one = tuple(np.zeros(1, dt) for dt in (np.int32, np.int32, np.int64, np.int64,
+                                                                    np.float64, np.float64))
+                self._one_ptrs = tuple(_ptr(x) for x in one)
+            one[0][0], one[1][0], one[2][0], one[3][0], one[4][0], one[5][0] = (
+                task[0], worker[0], run_id[0], nbytes[0], start[0], stop[0])
+            rc = self.lib.dgp_tasks_finished_post(self.h, 1, *self._one_ptrs)
+            n = 1
+        else:
+            n, cols = self._tf_batch(task, worker, run_id, nbytes, start, stop)
+            rc = self.lib.dgp_tasks_finished_post(self.h, n, *map(_ptr, cols))
+        self._check(rc, "dgp_tasks_finished_post")
+        self._posted_n = n
+
+    def tasks_finished_wait(self):
+        """(status per message, number of new placements) of the posted batch."""
+        n = self._posted_n
+        if n > len(self._st):
+            self._st = np.zeros(max(n, 2 * len(self._st)), np.int8)
+            self._st_ptr = _ptr(self._st)
+        self._check(self.lib.dgp_tasks_finished_wait(self.h, self._st_ptr, self._newp_ref), "dgp_tasks_finished_wait")
+        return self._st[:n].copy(), int(self._newp.value)
+
+    @staticmethod
+    def _ans_grow(b, d, h):
+        if d > b["dcap"]:
+            b["dcap"] = max(d, 2 * b["dcap"])
+            b.update(dt=np.zeros(b["dcap"], np.int32), dn=np.zeros(b["dcap"], np.int64),
+                     hp=np.zeros(b["dcap"] + 1, np.int64))
+            b.update(pdt=_ptr(b["dt"]), pdn=_ptr(b["dn"]), php=_ptr(b["hp"]))
+        if h > b["hcap"]:
+            b["hcap"] = max(h, 2 * b["hcap"])
+            b["hi"] = np.zeros(b["hcap"], np.int32)
+            b["phi"] = _ptr(b["hi"])
+
+    def answer(self, offset: int, count: int, messages: bool = True):
+        """What the extension takes after an answer, in one go and as Python lists: the task
+        and worker of placements [offset, offset + count) (dgp_get_placements) and, with
+        ``messages``, their compute-task fields (dgp_task_messages: dep_ptr, dep_task,
+        dep_nbytes, holder_ptr, holder_idx) -- or None. Preallocated buffers, no numpy
+        allocation per call."""
+        b = self._ans
+        if b is None or b["cap"] < count:
+            cap = max(count, 64, 2 * (b["cap"] if b else 0))
+            b = self._ans = dict(cap=cap, pt=np.zeros(cap, np.int32), pw=np.zeros(cap, np.int32),
+                                 dp=np.zeros(cap + 1, np.int64), dcap=0, hcap=0)
+            b.update(ppt=_ptr(b["pt"]), ppw=_ptr(b["pw"]), pdp=_ptr(b["dp"]))
+            self._ans_grow(b, 256, 256)
+        self._check(self.lib.dgp_get_placements(self.h, offset, count, b["ppt"], b["ppw"], None, None, None, None),
+                    "dgp_get_placements")
+        tasks, workers = b["pt"][:count].tolist(), b["pw"][:count].tolist()
+        if not messages:
+            return tasks, workers, None
+        nd, nh = self._nd, self._nh
+        self._check(self.lib.dgp_task_messages(self.h, offset, count, self._nd_ref, self._nh_ref, None, None, None,
+                                               None, None), "dgp_task_messages")
+        d, h = nd.value, nh.value
+        if d > b["dcap"] or h > b["hcap"]:
+            self._ans_grow(b, d, h)
+        self._check(self.lib.dgp_task_messages(self.h, offset, count, self._nd_ref, self._nh_ref, b["pdp"], b["pdt"],
+                                               b["pdn"], b["php"], b["phi"]), "dgp_task_messages")
+        return tasks, workers, (b["dp"][:count + 1].tolist(), b["dt"][:d].tolist(), b["dn"][:d].tolist(),
+                                b["hp"][:d + 1].tolist(), b["hi"][:h].tolist())
 
     def set_resident(self, on: bool = True):
         """Resident service mode (dgp_set_resident): the stream kernel stays launched between

@@ -245,6 +245,13 @@ class GPUPlacementExtension(SchedulerPlugin):
         self._msg_of: dict = {}
         self.engine_messages = True
         self.n_engine_messages = 0
+        # a task-finished batch the device is answering while the reference's handler runs
+        # (dgp_tasks_finished_post): its messages, their (key, worker) pairs, and the replica
+        # additions seen before the answer came (classified by _settle)
+        self.overlap = True
+        self._posted = None
+        self._posted_pairs = ()
+        self._deferred_adds: list = []
         if hasattr(scheduler, "add_plugin"):
             scheduler.add_plugin(self, name=self.name)
         elif isinstance(getattr(scheduler, "plugins", None), dict):  # a bare SchedulerState
@@ -282,6 +289,8 @@ class GPUPlacementExtension(SchedulerPlugin):
             ref_msg = s._task_to_msg
 
             def task_to_msg(ts, duration=-1):
+                if self._posted is not None:
+                    self._settle()
                 m = self._msg_of.pop(ts.key, None)
                 if m is None or not self.active:
                     return ref_msg(ts, duration)
@@ -399,6 +408,11 @@ class GPUPlacementExtension(SchedulerPlugin):
 
         def add_replica(ts, ws):
             k = (ts.key, ws.address)
+            if self._posted is not None:
+                if k in self._posted_pairs:  # the batch's own completion: classified by the answer
+                    self._deferred_adds.append((ts, ws, ws in (ts.who_has or ())))
+                    return add0(ts, ws)
+                self._settle()
             if k in self._expect_replicas:
                 self._expect_replicas.discard(k)
             elif ws not in (ts.who_has or ()):
@@ -406,6 +420,8 @@ class GPUPlacementExtension(SchedulerPlugin):
             return add0(ts, ws)
 
         def remove_replica(ts, ws):
+            if self._posted is not None:
+                self._settle()
             if ws in (ts.who_has or ()):
                 self._replica_event(ts, ws, -1)
             return rem0(ts, ws)
@@ -535,6 +551,8 @@ class GPUPlacementExtension(SchedulerPlugin):
     def _engine_op(self, what, *args):
         """Follow one placement-input change on the device; an engine without that
         operation (or one that fails) hands placement back to the scheduler."""
+        if self._posted is not None:
+            self._settle()
         fn = getattr(self.engine, what, None)
         if fn is None:
             self.fallback(f"{what}: not modelled by the engine")
@@ -740,18 +758,24 @@ class GPUPlacementExtension(SchedulerPlugin):
         n = self.engine.num_placements() if n_new is None else self.n_fetched + n_new
         if n > self.n_fetched:
             n0 = self.n_fetched
-            pl = self.engine.placements(n0, n - n0, columns=("pl_task", "pl_worker"))
+            want = messages and self.engine_messages and hasattr(self.engine, "task_messages")
+            if hasattr(self.engine, "answer"):  # one call, preallocated buffers
+                tasks, workers, batch = self.engine.answer(n0, n - n0, want)
+            else:
+                pl = self.engine.placements(n0, n - n0, columns=("pl_task", "pl_worker"))
+                tasks, workers, batch = pl["pl_task"].tolist(), pl["pl_worker"].tolist(), None
+                if want:
+                    m = self.engine.task_messages(n0, n - n0)
+                    batch = tuple(m[k].tolist() for k in ("dep_ptr", "dep_task", "dep_nbytes", "holder_ptr",
+                                                          "holder_idx"))
             keys, dev_run, pending = self.keys, self.dev_run, self.pending
             j = n0
-            tasks = pl["pl_task"].tolist()
-            for t, w in zip(tasks, pl["pl_worker"].tolist()):
+            for t, w in zip(tasks, workers):
                 pending.append((t, w))
                 dev_run[keys[t]] = j
                 j += 1
             self.n_fetched = n
-            if messages and self.engine_messages and hasattr(self.engine, "task_messages"):
-                m = self.engine.task_messages(n0, n - n0)
-                batch = tuple(m[k].tolist() for k in ("dep_ptr", "dep_task", "dep_nbytes", "holder_ptr", "holder_idx"))
+            if batch is not None:
                 msg_of = self._msg_of
                 for i, t in enumerate(tasks):
                     msg_of[keys[t]] = (batch, i)
@@ -798,6 +822,8 @@ class GPUPlacementExtension(SchedulerPlugin):
         }
 
     def _end_of_stimulus(self, what: str):
+        if self._posted is not None:
+            self._settle()
         self._msg_of.clear()
         if self.active and self.pending:
             t, w = self.pending[0]
@@ -811,6 +837,8 @@ class GPUPlacementExtension(SchedulerPlugin):
     def _decision(self, sched, ts, queued: bool):
         """The engine's worker for ``ts`` (a WorkerState), None (the engine did not place
         it in this stimulus: it stays / goes queued), or _REF (run the reference)."""
+        if self._posted is not None:  # the batch's answer, which the device computed meanwhile
+            self._settle()
         if not self.active or self.engine is None:
             return _REF
         if self.suspended:
@@ -912,6 +940,10 @@ class GPUPlacementExtension(SchedulerPlugin):
             return
         if self._allowed and pair in self._allowed[-1]:
             return
+        if self._posted is not None:
+            self._settle()
+            if not self.active:
+                return
         w = self._window
         if w is not None and pair in w[0] and (w[1] is None or key in w[1]):
             return
@@ -1306,11 +1338,16 @@ class GPUPlacementExtension(SchedulerPlugin):
 
     def handle_task_finished(self, key=None, worker=None, stimulus_id=None, **msg):
         """Stream handler "task-finished" (scheduler.py:3769 -> :5783-5797)."""
-        self.handle_task_finished_batch([dict(msg, key=key, worker=worker, stimulus_id=stimulus_id)])
+        msg["key"], msg["worker"], msg["stimulus_id"] = key, worker, stimulus_id
+        self.handle_task_finished_batch((msg,))
 
     def handle_task_finished_batch(self, msgs):
         """Several task-finished messages in arrival order: ONE engine call (one PCIe copy),
-        then the reference handler for each, consuming the engine's decisions in order."""
+        then the reference handler for each, consuming the engine's decisions in order. The
+        call is posted (dgp_tasks_finished_post) and its answer taken at the first decision
+        the handler's transitions ask for (``_settle``): the reference's Python up to there
+        (stimulus_task_finished :5025-5090, _transition_processing_memory :2366-2420) runs
+        while the device decides."""
         s = self.scheduler
         handler = type(s).handle_task_finished
         self._enter()
@@ -1319,20 +1356,12 @@ class GPUPlacementExtension(SchedulerPlugin):
             fields = [self._message_fields(m["key"], m["worker"], m) for m in msgs]
             cols = list(zip(*fields))
             try:
-                status, n_new = self.engine.tasks_finished(*cols)
-                status = status.tolist()
-                # an already-in-memory report (add_keys) adds a replica after the placements
-                # of the messages before it: those compute-task messages take who_has from
-                # the scheduler, as built at their time (the reference's own _task_to_msg)
-                self._fetch(n_new, messages=len(status) == 1 or 2 not in status)
-                self.stats["messages"] += len(msgs)
-                # DGP_TF_RELEASE / _IMPOSSIBLE / _UNSUPPORTED: the reference reschedules or
-                # raises; the engine does not follow those transitions
-                if any(st >= 3 and st != 4 for st in status):
-                    self.fallback(f"task-finished answers {sorted(set(status))} the engine does not run")
-                for m, st in zip(msgs, status):
-                    if st == 0:  # accepted: _add_to_memory adds this replica itself (:3296)
-                        self._expect_replicas.add((m["key"], m["worker"]))
+                if self.overlap and hasattr(self.engine, "tasks_finished_post"):
+                    self.engine.tasks_finished_post(*cols)
+                    self._posted = msgs
+                    self._posted_pairs = {(m["key"], m["worker"]) for m in msgs}
+                else:
+                    self._answer(msgs, *self.engine.tasks_finished(*cols))
             except Exception as e:
                 self.fallback(f"tasks_finished: {e}")
         self._allowed.append(_STIMULUS_TRANSITIONS)
@@ -1341,7 +1370,46 @@ class GPUPlacementExtension(SchedulerPlugin):
                 handler(s, **m)
         finally:
             self._allowed.pop()
+            self._settle()  # a batch whose transitions asked for no decision
             self._expect_replicas.clear()
         if self.suspended:
             self._resync()
         self._end_of_stimulus("task-finished")
+
+    def _answer(self, msgs, status, n_new):
+        status = status.tolist()
+        # an already-in-memory report (add_keys) adds a replica after the placements of the
+        # messages before it: those compute-task messages take who_has from the scheduler, as
+        # built at their time (the reference's own _task_to_msg)
+        self._fetch(n_new, messages=len(status) == 1 or 2 not in status)
+        self.stats["messages"] += len(msgs)
+        expect, bad = self._expect_replicas, False
+        for m, st in zip(msgs, status):
+            if st == 0:  # accepted: _add_to_memory adds this replica itself (:3296)
+                expect.add((m["key"], m["worker"]))
+            elif st >= 3 and st != 4:
+                bad = True
+        # DGP_TF_RELEASE / _IMPOSSIBLE / _UNSUPPORTED: the reference reschedules or raises;
+        # the engine does not follow those transitions
+        if bad:
+            self.fallback(f"task-finished answers {sorted(set(status))} the engine does not run")
+
+    def _settle(self):
+        """The posted batch's answer (dgp_tasks_finished_wait), then the replica additions
+        the handler made before it, classified as add_replica would have at the time."""
+        msgs = self._posted
+        if msgs is None:
+            return
+        self._posted = None
+        self._posted_pairs = ()
+        try:
+            self._answer(msgs, *self.engine.tasks_finished_wait())
+        except Exception as e:
+            self.fallback(f"tasks_finished: {e}")
+        adds, self._deferred_adds = self._deferred_adds, []
+        for ts, ws, had in adds:
+            k = (ts.key, ws.address)
+            if k in self._expect_replicas:
+                self._expect_replicas.discard(k)
+            elif not had:
+                self._replica_event(ts, ws, +1)

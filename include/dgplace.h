@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 14
+#define DGP_ABI_VERSION 15
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -188,6 +188,21 @@ int dgp_set_resident(dgp_engine* e, int enabled);
  * copy. Replaces the per-placement walk of SchedulerState._task_to_msg (scheduler.py
  * :3421-3450) over the dependencies' who_has sets for the extension's batches. */
 int dgp_set_task_messages(dgp_engine* e, int enabled);
+
+/* (ABI 15) dgp_tasks_finished in two halves, so that the caller's own work overlaps the
+ * device's: _post takes the batch (arguments and checks as dgp_tasks_finished) and returns
+ * as soon as the resident kernel has the request (launch per call: the batch is answered
+ * here and the answer kept); _wait spins on the answer and returns what dgp_tasks_finished
+ * would (status[i] for the posted n messages, *n_new_placements). In between, every entry
+ * point that touches the device or the mailbox fails with DGP_E_STATE (the kernel is inside
+ * the request); dgp_destroy waits for the answer. The extension posts a task-finished batch before it runs
+ * the reference's Scheduler.handle_task_finished (scheduler.py:5783-5797) and waits at the
+ * first decision that batch's transitions ask for (_transition_waiting_processing :2313,
+ * _transition_queued_processing :2797): _transition_processing_memory's Python (:2366-2420)
+ * runs while the device decides. */
+int dgp_tasks_finished_post(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker,
+                            const int64_t* run_id, const int64_t* nbytes, const double* start, const double* stop);
+int dgp_tasks_finished_wait(dgp_engine* e, int8_t* status, int64_t* n_new_placements);
 
 /* Steal confirmation (WorkStealing.move_task_confirm, stealing.py:333-399, its "confirm"
  * branch :376-384 and finally clause :396-399): processing task `task` leaves its worker

@@ -26,6 +26,7 @@ from __future__ import annotations
 import json
 import os
 import sys
+import time as _time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -61,6 +62,9 @@ class FixtureEngine:
         self.diverge = None  # placement index whose decision is swapped with the next one
         self.graphs = []
         self.calls_tf = 0  # dgp_tasks_finished calls the extension made
+        self._posted = None
+        self.t_window = 0.0
+        self.windows = []
 
     def load(self, g, config, results=True):
         self.graph, self.config = g, config
@@ -84,6 +88,23 @@ class FixtureEngine:
         self.n, self.k = self.stim[0], 1
 
     def tasks_finished(self, task, worker, run_id, nbytes=None, start=None, stop=None):
+        return self._finished(task, worker, run_id, nbytes, start, stop)
+
+    def tasks_finished_post(self, *args):  # dgp_tasks_finished_post: answered at the wait
+        assert self._posted is None, "a batch posted twice"
+        self._posted = args
+        self._t_post = _time.perf_counter()
+
+    def tasks_finished_wait(self):
+        # the host time between post and wait: the window the device's answer overlaps
+        dt_ = _time.perf_counter() - self._t_post
+        self.t_window += dt_
+        self.windows.append(dt_)
+        args, self._posted = self._posted, None
+        assert args is not None, "no batch posted"
+        return self._finished(*args)
+
+    def _finished(self, task, worker, run_id, nbytes=None, start=None, stop=None):
         self.calls_tf += 1
         n0 = self.n
         for i, t in enumerate(task):  # genuine completions only in this protocol
@@ -108,10 +129,20 @@ class FixtureEngine:
         return dict(dep_ptr=np.array(ptr, np.int64), dep_task=np.array(dt, np.int32), dep_nbytes=np.array(dn, np.int64),
                     holder_ptr=np.array(hp, np.int64), holder_idx=np.array(hi, np.int32))
 
+    def answer(self, offset, count, messages=True):  # PlacementEngine.answer from the two calls it fuses
+        pl = self.placements(offset, count)
+        batch = None
+        if messages:
+            m = self.task_messages(offset, count)
+            batch = tuple(m[k].tolist() for k in ("dep_ptr", "dep_task", "dep_nbytes", "holder_ptr", "holder_idx"))
+        return pl["pl_task"].tolist(), pl["pl_worker"].tolist(), batch
+
     def num_placements(self):
+        assert self._posted is None, "num_placements while a batch is posted"
         return self.n
 
     def placements(self, offset=0, count=None, columns=None):
+        assert self._posted is None, "placements while a batch is posted"
         sl = slice(offset, offset + count)
         idx = self.ext.task_index
         task = np.array([idx[self.fkeys[t]] for t in self.exp["pl_task"][sl]], np.int32)
@@ -128,6 +159,7 @@ class FixtureEngine:
         return self.add_worker(0)
 
     def add_worker(self, nthreads):  # a join (the fixture's per-event placement counts)
+        assert self._posted is None, "add_worker while a batch is posted"
         k = self.stim[self.k]
         self.n += k
         self.k += 1
@@ -250,14 +282,14 @@ def run(name, diverge=False, stream=False, plain=False, validate=True):
             s.plugins = {"noop": SchedulerPlugin()}
         recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
         s._transitions(recs, {}, {}, "update-graph")
-        done, n_msgs, t_msgs = 0, 0, 0.0
+        done, n_msgs, t_msgs, c_msgs = 0, 0, 0.0, 0.0
         while True:
             cur = len(rec["task"])
             batch = rec["task"][done:cur]
             done = cur
             if not batch:
                 break
-            t0 = _time.perf_counter()
+            t0, c0 = _time.perf_counter(), _time.process_time()
             for t in batch:
                 ts = tss[t]
                 s.stream_handlers["task-finished"](
@@ -265,10 +297,12 @@ def run(name, diverge=False, stream=False, plain=False, validate=True):
                     nbytes=int(g["nbytes"][t]), type=None, typename="int", metadata=None,
                     startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
             t_msgs += _time.perf_counter() - t0
+            c_msgs += _time.process_time() - c0
             n_msgs += len(batch)
         assert rec["task"] == exp["pl_task"].tolist()
         return dict(fixture=name, mode="plain" if plain is True else "plain+plugin", messages=n_msgs,
-                    us_per_message=round(1e6 * t_msgs / n_msgs, 2))
+                    us_per_message=round(1e6 * t_msgs / n_msgs, 2),
+                    cpu_us_per_message=round(1e6 * c_msgs / n_msgs, 2))
     eng = FixtureEngine(exp, fkeys)
     if diverge:  # first stimulus after update_graph with two or more placements
         stim = exp["stim_nplaced"]
@@ -276,16 +310,19 @@ def run(name, diverge=False, stream=False, plain=False, validate=True):
         k = next(i for i in range(1, len(stim)) if stim[i] >= 2 and exp["pl_task"][pos[i]] != exp["pl_task"][pos[i] + 1])
         eng.diverge = int(pos[k])
     S._task_to_msg = orig_msg  # the extension wraps the instance's: every message recorded below
-    eng.t_engine = 0.0
-    for nm_ in ("tasks_finished", "placements", "task_messages", "num_placements"):
+    eng.t_engine = eng.c_engine = 0.0
+    for nm_ in ("tasks_finished", "tasks_finished_post", "tasks_finished_wait", "placements", "task_messages",
+                "num_placements"):
         def timed(*a, _f=getattr(eng, nm_), **k):
-            t0_ = _time.perf_counter()
+            t0_, c0_ = _time.perf_counter(), _time.process_time()
             try:
                 return _f(*a, **k)
             finally:
                 eng.t_engine += _time.perf_counter() - t0_
+                eng.c_engine += _time.process_time() - c0_
         setattr(eng, nm_, timed)
     ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=validate)
+    ext.overlap = "--nooverlap" not in sys.argv
     eng.ext = ext
     s.stream_handlers = {}
     ext._install()  # with the stream handler table in place
@@ -308,7 +345,7 @@ def run(name, diverge=False, stream=False, plain=False, validate=True):
     done = 0
     n_msgs = 0
     n_reads = 0
-    t_msgs = 0.0
+    t_msgs = c_msgs = 0.0
     calls0 = ext.stats.get("messages", 0)
     while True:
         cur = len(rec["task"])
@@ -322,7 +359,7 @@ def run(name, diverge=False, stream=False, plain=False, validate=True):
             return dict(key=ts.key, stimulus_id=f"tf-{t}", run_id=ts.run_id, nbytes=int(g["nbytes"][t]), type=None,
                         typename="int", metadata=None,
                         startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
-        t0 = _time.perf_counter()
+        t0, c0 = _time.perf_counter(), _time.process_time()
         if stream:  # one comm.read per run of consecutive messages from one worker
             runs = []
             for t in batch:
@@ -339,6 +376,7 @@ def run(name, diverge=False, stream=False, plain=False, validate=True):
             for t in batch:
                 s.stream_handlers["task-finished"](worker=tss[t].processing_on.address, **msg(t))
         t_msgs += _time.perf_counter() - t0
+        c_msgs += _time.process_time() - c0
         n_msgs += len(batch)
     ext._end_of_stimulus("end of replay")
     assert ext.active != diverge, ext.reason  # a divergence hands placement back to the scheduler
@@ -358,6 +396,11 @@ def run(name, diverge=False, stream=False, plain=False, validate=True):
                 # the extension and the reference handler without the stand-in engine's own time
                 # (on the box the engine call replaces it: bench.py service leg)
                 us_per_message_host=round(1e6 * (t_msgs - eng.t_engine) / max(n_msgs, 1), 2),
+                cpu_us_per_message_host=round(1e6 * (c_msgs - eng.c_engine) / max(n_msgs, 1), 2),
+                # between the post and the first decision: the device answers meanwhile
+                us_overlap_window=round(1e6 * eng.t_window / max(eng.calls_tf, 1), 2),
+                us_overlap_window_p10_p50=[round(1e6 * float(np.percentile(eng.windows, q)), 1) for q in (10, 50)]
+                if eng.windows else None,
                 device_queued=ext.stats["device_queued"], device_no_worker=ext.stats["device_no_worker"],
                 active=ext.active, reason=ext.reason, engine_calls=eng.calls_tf, reads=n_reads,
                 us_per_message=round(1e6 * t_msgs / max(n_msgs, 1), 2), mode="stream" if stream else "handler")
@@ -605,6 +648,7 @@ class EventEngine(FixtureEngine):
         self.calls = []
 
     def _event(self, *call):
+        assert self._posted is None, f"{call[0]} while a task-finished batch is posted"  # the engine refuses it
         self.calls.append(call)
         k = self.stim[self.k]
         self.n += k

@@ -132,6 +132,98 @@ def test_service_stale_duplicate_memory(name, per_message, resident):
     assert np.array_equal(out["final_state"], exp["final_state"])
 
 
+def drive_posted(eng, msgs, ptr):
+    """``drive`` one message per dgp_tasks_finished_post / _wait (GPUPlacementExtension's
+    overlapped path): the entry points that touch the device refuse while a batch is posted,
+    and each answer's new placements and message fields through ``engine.answer`` equal
+    placements() + task_messages() of the same range."""
+    from distributed_amd import _lib
+
+    status, n, refused = [], eng.num_placements(), 0
+    for k in range(len(ptr) - 1):
+        chunk = msgs[ptr[k]:ptr[k + 1]]
+        if not chunk:
+            continue
+        for m in chunk:
+            eng.tasks_finished_post(*[(x,) for x in m])
+            if refused < 2:  # the kernel is inside the request: no other call meanwhile
+                with pytest.raises(_lib.DgpError, match="posted"):
+                    eng.num_placements() if refused == 0 else eng.placements(0, 1)
+                refused += 1
+            st, new = eng.tasks_finished_wait()
+            status.extend(st.tolist())
+            if new:
+                tasks, workers, fields = eng.answer(n, new, True)
+                p = eng.placements(n, new, columns=("pl_task", "pl_worker"))
+                tm = eng.task_messages(n, new)
+                assert tasks == p["pl_task"].tolist() and workers == p["pl_worker"].tolist()
+                for got, key in zip(fields, ("dep_ptr", "dep_task", "dep_nbytes", "holder_ptr", "holder_idx")):
+                    assert got == tm[key].tolist(), key
+                n += new
+        eng.snapshot()
+    return np.array(status, np.int8)
+
+
+@pytest.mark.parametrize("resident", [False, True], ids=["launch", "resident"])
+@pytest.mark.parametrize("name", ["c2var_sat1.1.npz", "c3mini_sat1.1.npz", "svc_c2var_sat1.1.npz"])
+def test_posted_service_matches_reference_fixture(name, resident):
+    """dgp_tasks_finished_post / _wait (ABI 15) give what dgp_tasks_finished gives: the
+    reference's statuses, placements, snapshots and final states, launch per call and
+    through the resident kernel (with the mailbox's message fields)."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    if name.startswith("svc_"):
+        z = np.load(path, allow_pickle=False)
+        msgs = list(zip(z["msg_task"].tolist(), z["msg_worker"].tolist(), z["msg_runid"].tolist(),
+                        z["msg_nbytes"].tolist(), z["msg_start"].tolist(), z["msg_stop"].tolist()))
+        ptr, want = z["msg_round_ptr"].tolist(), z["msg_status"]
+    else:
+        msgs, ptr = fixture_messages(g, exp)
+        want = np.zeros(len(msgs), np.int8)
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.set_resident(resident)
+        eng.set_task_messages(resident)
+        eng.update_graph()
+        status = drive_posted(eng, msgs, ptr)
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert np.array_equal(status, want)
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+def test_posted_batch_guards():
+    """A wait with nothing posted and a second post are refused; closing the engine with a
+    batch posted waits for its answer."""
+    from distributed_amd import _lib, graphs
+    from distributed_amd.engine import PlacementEngine
+
+    g = graphs.random_dag(2000, 32, seed=3)
+    cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": 1.1}
+    for resident in (False, True):
+        eng = PlacementEngine(0)
+        eng.load(g, cfg)
+        eng.set_resident(resident)
+        eng.update_graph()
+        with pytest.raises(_lib.DgpError, match="no batch posted"):
+            eng.tasks_finished_wait()
+        p = eng.placements(0, 2)
+        eng.tasks_finished_post(p["pl_task"][:1], p["pl_worker"][:1], [0], [100], [0.0], [0.01])
+        with pytest.raises(_lib.DgpError, match="posted"):
+            eng.tasks_finished_post(p["pl_task"][1:], p["pl_worker"][1:], [1], [100], [0.0], [0.01])
+        with pytest.raises(_lib.DgpError, match="posted"):
+            eng.tasks_finished(p["pl_task"][1:], p["pl_worker"][1:], [1], [100], [0.0], [0.01])
+        st, _ = eng.tasks_finished_wait()
+        assert st.tolist() == [0]
+        eng.tasks_finished_post(p["pl_task"][1:], p["pl_worker"][1:], [1], [100], [0.0], [0.01])
+        eng.close()  # waits for the posted answer first
+
+
 def test_service_empty_batch_and_mode_guard():
     """An empty batch is a no-op; a replay cannot continue a service-mode engine."""
     from distributed_amd import _lib, graphs
