@@ -785,11 +785,12 @@ class GPUPlacementExtension(SchedulerPlugin):
         made, its ``who_has`` / ``nbytes`` from the engine's batch (dgp_task_messages: the
         dependencies in CSR order, their holders ascending by worker index) instead of a
         walk over the dependencies' replica sets; every other field as there."""
-        sm = _sched_mod()
+        sm = _SM or _sched_mod()
         dep_ptr, dep_task, dep_nbytes, holder_ptr, holder_idx = batch
         keys, addrs = self.keys, self.workers
         who_has, nbytes = {}, {}
-        for k in range(dep_ptr[i], dep_ptr[i + 1]):
+        d0, d1 = dep_ptr[i], dep_ptr[i + 1]
+        for k in range(d0, d1) if d1 > d0 else ():
             dk = keys[dep_task[k]]
             h0, h1 = holder_ptr[k], holder_ptr[k + 1]
             who_has[dk] = [addrs[holder_idx[h0]]] if h1 == h0 + 1 else [addrs[h] for h in holder_idx[h0:h1]]
@@ -844,6 +845,11 @@ class GPUPlacementExtension(SchedulerPlugin):
         if self.suspended:
             self._route = self._route_of(sched, ts, queued)
             return _REF
+        pending = self.pending
+        if pending and self.keys[pending[0][0]] == ts.key:  # the common case: the engine's next placement
+            _, w = pending.popleft()
+            self.stats["device_decisions"] += 1
+            return sched.workers[self.workers[w]]
         t = self.task_index.get(ts.key)
         if t is None:
             self.fallback(f"{ts.key!r} is not in the engine's graph")
@@ -908,7 +914,8 @@ class GPUPlacementExtension(SchedulerPlugin):
         ws = self._decision(sched, ts, False)
         if ws is _REF:
             return ref(sched, key, stimulus_id)
-        self._check(sched, ts, ws, False)
+        if self.validate:
+            self._check(sched, ts, ws, False)
         if ws is None:
             if sched.is_rootish(ts) and not math.isinf(sched.WORKER_SATURATION):
                 return {ts.key: "queued"}, {}, {}
@@ -921,7 +928,8 @@ class GPUPlacementExtension(SchedulerPlugin):
         ws = self._decision(sched, ts, True)
         if ws is _REF:
             return ref(sched, key, stimulus_id)
-        self._check(sched, ts, ws, True)
+        if self.validate:
+            self._check(sched, ts, ws, True)
         if ws is None:
             return {}, {}, {}
         sched.queued.discard(ts)
@@ -933,12 +941,12 @@ class GPUPlacementExtension(SchedulerPlugin):
         transition (scheduler.py:2013-2027): the catch-all. A transition outside the
         stimuli the engine follows, or of a kind it does not model, means the scheduler's
         state moved where the engine's did not."""
+        pair = (start, finish)
+        if self._allowed and pair in self._allowed[-1]:  # the running stimulus' own transitions
+            return
         if not self.active or self.engine is None:
             return
-        pair = (start, finish)
         if start == finish:  # a decision that only recommends (queued / no-worker next): no change
-            return
-        if self._allowed and pair in self._allowed[-1]:
             return
         if self._posted is not None:
             self._settle()
@@ -1350,11 +1358,17 @@ class GPUPlacementExtension(SchedulerPlugin):
         while the device decides."""
         s = self.scheduler
         handler = type(s).handle_task_finished
-        self._enter()
-        self._end_of_stimulus("the previous stimulus")
+        self._window = None  # _enter
+        if self.suspended:
+            self._resync()
+        if self.pending or self._msg_of or self._posted is not None:
+            self._end_of_stimulus("the previous stimulus")
         if self.active and self.engine is not None and msgs:
-            fields = [self._message_fields(m["key"], m["worker"], m) for m in msgs]
-            cols = list(zip(*fields))
+            if len(msgs) == 1:
+                m = msgs[0]
+                cols = [(x,) for x in self._message_fields(m["key"], m["worker"], m)]
+            else:
+                cols = list(zip(*[self._message_fields(m["key"], m["worker"], m) for m in msgs]))
             try:
                 if self.overlap and hasattr(self.engine, "tasks_finished_post"):
                     self.engine.tasks_finished_post(*cols)
@@ -1374,7 +1388,8 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._expect_replicas.clear()
         if self.suspended:
             self._resync()
-        self._end_of_stimulus("task-finished")
+        if self.pending or self._msg_of:
+            self._end_of_stimulus("task-finished")
 
     def _answer(self, msgs, status, n_new):
         status = status.tolist()

@@ -406,6 +406,99 @@ def run(name, diverge=False, stream=False, plain=False, validate=True):
                 us_per_message=round(1e6 * t_msgs / max(n_msgs, 1), 2), mode="stream" if stream else "handler")
 
 
+def run_ab(name):
+    """Timing A/B of the drop-in: the reference (its own handler, a SchedulerPlugin
+    registered) and the extension (overlapped engine call; the stand-in engine's time
+    subtracted) on two independent states of the same fixture in ONE process, fed the same
+    task-finished messages alternately (which side goes first alternates too). Each message's
+    handler time is taken on both sides under the same machine conditions, so the per-message
+    difference cancels what other tenants of the machine do; reported with its 95 % interval."""
+    from distributed.diagnostics.plugin import SchedulerPlugin
+
+    g, cfg, exp, meta = load_fixture(os.path.join(HERE, "golden", name))
+    g["keys"] = None
+    sat = cfg["saturation"]
+    sat = float("inf") if sat == "inf" else float(sat)
+    dask.config.set({"distributed.scheduler.worker-saturation": sat})
+    cfg = dict(cfg, saturation=sat)
+    sides = {}
+    for mode in ("reference", "extension"):
+        s, tss, widx, rec, tidx = G.build_state(g, cfg)  # a class of its own per state
+        S = type(s)
+        S.stimulus_task_finished = Scheduler.stimulus_task_finished
+        S.handle_task_finished = Scheduler.handle_task_finished
+        S.validate_key = lambda self, key, ts=None: None
+        S.send_all = lambda self, client_msgs, worker_msgs: None
+        recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
+        eng = None
+        if mode == "reference":
+            s.plugins = {"noop": SchedulerPlugin()}
+            handler = (lambda _s: lambda **kw: Scheduler.handle_task_finished(_s, **kw))(s)
+        else:
+            eng = FixtureEngine(exp, [ts.key for ts in tss])
+            eng.t_engine = 0.0
+            for nm_ in ("tasks_finished", "tasks_finished_post", "tasks_finished_wait", "placements",
+                        "task_messages", "num_placements"):
+                def timed(*a, _f=getattr(eng, nm_), **k):
+                    t0_ = _time.perf_counter()
+                    try:
+                        return _f(*a, **k)
+                    finally:
+                        eng.t_engine += _time.perf_counter() - t0_
+                setattr(eng, nm_, timed)
+            ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=False)
+            eng.ext = ext
+            s.stream_handlers = {}
+            ext._install()
+            priority = {ts.key: ts.priority for ts in tss}
+            ext.update_graph(s, client="client-0", keys=set(priority), tasks=list(priority), annotations={},
+                             priority=priority, dependencies={})
+            assert ext.active, ext.reason
+            handler = s.stream_handlers["task-finished"]
+        s._transitions(recs, {}, {}, "update-graph")
+        sides[mode] = (tss, rec, handler, eng)
+    rec0 = sides["reference"][1]
+    diffs, tot = [], {"reference": 0.0, "extension": 0.0}
+    done, i = 0, 0
+    while True:
+        cur = len(rec0["task"])
+        batch = rec0["task"][done:cur]
+        done = cur
+        if not batch:
+            break
+        for t in batch:
+            dt = {}
+            for mode in (("reference", "extension") if i % 2 == 0 else ("extension", "reference")):
+                tss, rec, handler, eng = sides[mode]
+                ts = tss[t]
+                kw = dict(key=ts.key, worker=ts.processing_on.address, stimulus_id=f"tf-{t}", run_id=ts.run_id,
+                          nbytes=int(g["nbytes"][t]), type=None, typename="int", metadata=None,
+                          startstops=[{"action": "compute", "start": float(g["start"][t]),
+                                       "stop": float(g["stop"][t])}])
+                e0 = eng.t_engine if eng else 0.0
+                t0 = _time.perf_counter()
+                handler(**kw)
+                d = _time.perf_counter() - t0
+                if eng:
+                    d -= eng.t_engine - e0
+                dt[mode] = d
+                tot[mode] += d
+            diffs.append(dt["extension"] - dt["reference"])
+            i += 1
+    ext = sides["extension"][3].ext
+    ext._end_of_stimulus("end of replay")
+    for mode in sides:
+        assert sides[mode][1]["task"] == exp["pl_task"].tolist(), mode
+    assert ext.active and ext.stats["device_decisions"] == len(exp["pl_task"]), (ext.reason, ext.stats)
+    d = np.array(diffs) * 1e6
+    half = 1.96 * d.std(ddof=1) / np.sqrt(len(d))
+    return dict(fixture=name, mode="ab", messages=i,
+                reference_us_per_message=round(1e6 * tot["reference"] / i, 2),
+                extension_host_us_per_message=round(1e6 * tot["extension"] / i, 2),
+                diff_us_per_message=round(float(d.mean()), 2), diff_ci95_us=round(float(half), 2),
+                diff_median_us=round(float(np.median(d)), 2))
+
+
 def run_joins(name):
     """A ``svcaddw_*`` stream (gen_service.py add-workers): workers join between the
     task-finished messages through the placement-relevant body of ``Scheduler.add_worker``
@@ -984,6 +1077,9 @@ if __name__ == "__main__":
     plain = "--plain" in args
     stream = "--stream" in args
     for nm in [a for a in args if not a.startswith("--")]:
+        if "--ab" in args:
+            print(json.dumps(run_ab(nm)), flush=True)
+            continue
         fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_"))
               else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcp2p_")) else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,

@@ -21,10 +21,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PY39 = "/opt/conda/bin/python3.9"
 
 
-def start(fixture, *flags):
+def start(fixture, *flags, core=None):
     env = dict(os.environ, PYTHONHASHSEED="0")
     env.pop("PYTHONPATH", None)
-    return subprocess.Popen([PY39, os.path.join(REPO, "tests", "ext_driver.py"), *flags, fixture],
+    pin = ["taskset", "-c", str(core)] if core is not None else []  # one core each: no migrations
+    return subprocess.Popen([*pin, PY39, os.path.join(REPO, "tests", "ext_driver.py"), *flags, fixture],
                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=REPO)
 
 
@@ -51,7 +52,7 @@ def main():
         plain, ext, win, p10 = [], [], [], []
         for _ in range(reps):
             # the pair runs at the same time: whatever else loads the machine loads both
-            pp, pe = start(fx, "--plain", "--plugin"), start(fx, "--novalidate")
+            pp, pe = start(fx, "--plain", "--plugin", core=2), start(fx, "--novalidate", core=5)
             plain.append(result(pp)[key])
             r = result(pe)
             ext.append(r[key.replace("message", "message_host")])
