@@ -436,18 +436,48 @@ def run_ab(name):
             handler = (lambda _s: lambda **kw: Scheduler.handle_task_finished(_s, **kw))(s)
         else:
             eng = FixtureEngine(exp, [ts.key for ts in tss])
-            eng.t_engine = 0.0
-            for nm_ in ("tasks_finished", "tasks_finished_post", "tasks_finished_wait", "placements",
+            eng.t_engine, eng.n_timed, depth = 0.0, 0, [0]
+            # the stand-in's time leaves the extension's: every outermost call into it is
+            # timed (the real engine's Python wrappers and device time are bench.py's
+            # service.per_message_overlap_ext.exposed_us_per_call instead)
+            for nm_ in ("tasks_finished", "tasks_finished_post", "tasks_finished_wait", "answer", "placements",
                         "task_messages", "num_placements"):
                 def timed(*a, _f=getattr(eng, nm_), **k):
+                    if depth[0]:
+                        return _f(*a, **k)
+                    depth[0] = 1
                     t0_ = _time.perf_counter()
                     try:
                         return _f(*a, **k)
                     finally:
                         eng.t_engine += _time.perf_counter() - t0_
+                        eng.n_timed += 1
+                        depth[0] = 0
                 setattr(eng, nm_, timed)
+
+            def _noop():
+                pass
+
+            def _timed_noop(*a, _f=_noop, **k):  # the wrapper's own cost, taken off per timed call
+                if depth[0]:
+                    return _f(*a, **k)
+                depth[0] = 1
+                t0_ = _time.perf_counter()
+                try:
+                    return _f(*a, **k)
+                finally:
+                    eng.t_engine += _time.perf_counter() - t0_
+                    eng.n_timed += 1
+                    depth[0] = 0
+            t_cal = _time.perf_counter()
+            for _ in range(200_000):
+                _timed_noop()
+            eng.wrap_s = (_time.perf_counter() - t_cal) / 200_000
+            eng.t_engine, eng.n_timed = 0.0, 0
             ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=False)
             eng.ext = ext
+            ext.overlap = os.environ.get("AB_OVERLAP", "1") == "1"  # knobs for attributing the difference
+            ext.engine_messages = os.environ.get("AB_MESSAGES", "1") == "1"
             s.stream_handlers = {}
             ext._install()
             priority = {ts.key: ts.priority for ts in tss}
@@ -459,6 +489,18 @@ def run_ab(name):
         sides[mode] = (tss, rec, handler, eng)
     rec0 = sides["reference"][1]
     diffs, tot = [], {"reference": 0.0, "extension": 0.0}
+    import gc
+
+    profs = {}
+    if os.environ.get("AB_PROFILE"):  # one cProfile per side: call counts and times side by side
+        import cProfile
+
+        profs = {"reference": cProfile.Profile(), "extension": cProfile.Profile()}
+    gc.collect()
+    if os.environ.get("AB_GC") == "freeze":  # the states built above leave the collector's scans
+        gc.freeze()
+    elif os.environ.get("AB_GC") == "off":
+        gc.disable()
     done, i = 0, 0
     while True:
         cur = len(rec0["task"])
@@ -475,12 +517,17 @@ def run_ab(name):
                           nbytes=int(g["nbytes"][t]), type=None, typename="int", metadata=None,
                           startstops=[{"action": "compute", "start": float(g["start"][t]),
                                        "stop": float(g["stop"][t])}])
-                e0 = eng.t_engine if eng else 0.0
+                e0, n0 = (eng.t_engine, eng.n_timed) if eng else (0.0, 0)
+                prof = profs.get(mode)
+                if prof:
+                    prof.enable()
                 t0 = _time.perf_counter()
                 handler(**kw)
                 d = _time.perf_counter() - t0
+                if prof:
+                    prof.disable()
                 if eng:
-                    d -= eng.t_engine - e0
+                    d -= eng.t_engine - e0 + (eng.n_timed - n0) * eng.wrap_s
                 dt[mode] = d
                 tot[mode] += d
             diffs.append(dt["extension"] - dt["reference"])
@@ -490,6 +537,9 @@ def run_ab(name):
     for mode in sides:
         assert sides[mode][1]["task"] == exp["pl_task"].tolist(), mode
     assert ext.active and ext.stats["device_decisions"] == len(exp["pl_task"]), (ext.reason, ext.stats)
+    assert ext.n_engine_messages == (len(exp["pl_task"]) if ext.engine_messages else 0)
+    for mode, prof in profs.items():
+        prof.dump_stats(os.path.join(os.environ["AB_PROFILE"], f"ab_{mode}.prof"))
     d = np.array(diffs) * 1e6
     half = 1.96 * d.std(ddof=1) / np.sqrt(len(d))
     return dict(fixture=name, mode="ab", messages=i,
