@@ -1116,23 +1116,30 @@ class GPUPlacementExtension(SchedulerPlugin):
 
     def remove_worker(self, scheduler=None, worker=None, **kwargs):
         """SchedulerPlugin.remove_worker: Scheduler.remove_worker calls it after its own
-        transitions (scheduler.py:5298-5302): the lost worker's processing tasks released and
-        re-placed, its lost results recomputed, all decided by the scheduler itself (the
-        plugin transition hook suspended the engine at the first of them). The engine marks
-        the worker removed (dgp_remove_worker; it keeps its index, so the canonical order of
-        the others stands) and takes the scheduler's state (dgp_sync_*)."""
+        transitions (scheduler.py:5298-5302). The engine marks the worker removed
+        (dgp_remove_worker: it leaves running / idle / saturated and total_nthreads and keeps
+        its index, so the canonical order of the others stands). A worker that leaves with
+        nothing processing and no last replica (retire_workers' drained worker: paused, its
+        data copied elsewhere) runs no transition; its replicas went through the replica hook
+        (dgp_remove_replicas) and the engine follows the removal on the device. Otherwise its
+        processing tasks were released and re-placed and its lost results recomputed by the
+        scheduler itself (the transition hook suspended the engine at the first of them), and
+        the engine takes the scheduler's state (dgp_sync_*)."""
         self._close_window()
         if not self.active or self.engine is None or worker not in self.worker_index:
             return
-        self._suspend(f"remove_worker({worker})")
-        if not self.active:
-            return
+        on_device = not self.suspended
         w = self.worker_index.pop(worker)
         self.removed.add(worker)
         try:
             self.engine.remove_worker(w)
         except Exception as e:
             self.fallback(f"remove_worker({worker}): {e}")
+            return
+        if on_device:
+            self.stats["workers_removed_on_device"] += 1
+            self._fetch()  # none expected: a removal frees no slot
+            self._end_of_stimulus(f"remove_worker({worker})")
             return
         self.stats["workers_removed"] += 1
         self._resync()

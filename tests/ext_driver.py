@@ -873,7 +873,7 @@ def run_events(name, plain=False):
 
     from gen_service import (EV_ADD_KEYS, EV_ERRED, EV_FINISHED, EV_HEARTBEAT, EV_LONG_RUNNING, EV_PAUSE,
                              EV_RELEASE_DATA, EV_RELEASE_KEYS, EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RESTRICT,
-                             EV_RESUME, EV_SHUFFLE_INIT)
+                             EV_RESUME, EV_RETIRE, EV_RETIRE_REPLICA, EV_SHUFFLE_INIT)
 
     from distributed_amd import sync as dsync
 
@@ -1071,6 +1071,14 @@ def run_events(name, plain=False):
             plugin._set_restriction(tss[t], addr[w])
             want.append(("restrict", [ext.task_index[fkeys[t]]], [[w]], [1]))
             eng.k += 1
+        elif kd == EV_RETIRE_REPLICA:  # made by the EV_RETIRE that follows (remove_worker's replica drops)
+            want.append(("remove", [t], [w]))
+        elif kd == EV_RETIRE:  # a drained worker leaves: no transition, followed on the device
+            rs0 = ext.stats["resyncs"]
+            loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
+            want.append(("remove", w))
+            assert ext.stats["resyncs"] == rs0 and not ext.suspended, (i, ext.stats)
+            eng.k += 1  # the fixture's count for it (no placement)
         elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
             if kd == EV_REMOVE_WORKER:
                 loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
@@ -1131,7 +1139,7 @@ if __name__ == "__main__":
             print(json.dumps(run_ab(nm)), flush=True)
             continue
         fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_"))
-              else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcp2p_")) else None)
+              else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcrt_", "svcp2p_")) else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,
                                                plain="plugin" if "--plugin" in args else plain,
                                                validate="--novalidate" not in args)), flush=True)

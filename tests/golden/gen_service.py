@@ -565,6 +565,11 @@ RESYNC_KINDS = (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS)
 # the P2P shuffle's scheduler-side lifecycle (svcp2p_*): placement inputs its plugin changes
 # outside any transition (shuffle/_scheduler_plugin.py); the tasks of an init are in hb_task
 EV_SHUFFLE_INIT, EV_RESTRICT = 11, 12
+# a drained worker retires (svcrt_*): retire_workers' shape -- paused, its processing done, its
+# sole replicas copied elsewhere by add-keys -- then Scheduler.remove_worker, which runs no
+# transition; EV_RETIRE_REPLICA records each replica remove_worker drops there (has_what
+# order), EV_RETIRE the removal itself. The engine follows it without a resync.
+EV_RETIRE, EV_RETIRE_REPLICA = 13, 14
 
 
 def _dump(s, g, tidx, widx, keys):
@@ -658,7 +663,7 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
     S.send_all = lambda self, client_msgs, worker_msgs: None
     S.worker_send = lambda self, worker, msg: None
     s.extensions = {}
-    if EV_REMOVE_WORKER in kinds:  # what Scheduler.remove_worker touches besides placement state
+    if EV_REMOVE_WORKER in kinds or EV_RETIRE in kinds:  # what Scheduler.remove_worker touches besides placement state
         import asyncio
         from collections import defaultdict
         from types import SimpleNamespace as NS
@@ -781,6 +786,28 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
             removed.add(w)
             push(EV_REMOVE_WORKER, -1, w)
+        elif kind == EV_RETIRE:
+            cand = [i for i in sorted(paused) if i not in removed and not s.workers[addr[i]].processing]
+            live = [i for i in range(W) if i not in removed and i not in paused]
+            if not cand or len(live) <= max(2, W // 2):
+                return
+            w = cand[int(rng.integers(0, len(cand)))]
+            ws = s.workers[addr[w]]
+            for ts in list(ws.has_what):  # retire_workers' replicate step: no last replica leaves
+                if len(ts.who_has) == 1:
+                    w2 = live[int(rng.integers(0, len(live)))]
+                    s.add_keys(worker=addr[w2], keys=[ts.key], stimulus_id=sid)
+                    push(EV_ADD_KEYS, tidx[ts.key], w2)
+                    stim.append(0)
+            held = [tidx[ts.key] for ts in ws.has_what]
+            loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
+            assert len(rec["task"]) == n0  # no transition ran, nothing was placed
+            removed.add(w)
+            paused.discard(w)
+            for t in held:
+                push(EV_RETIRE_REPLICA, t, w)
+                stim.append(0)
+            push(EV_RETIRE, -1, w)
         elif kind == EV_RESCHEDULE:
             proc = [ts for ts in tss if ts.state == "processing"]
             if not proc:
@@ -1087,6 +1114,10 @@ def main_resync(only):
         "svcrs_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=51, n_inner_prefixes=3,
                                                             random_durations=True, nthreads="random"), 1.1, 51, 0.08),
         "svcrs_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=52), float("inf"), 52, 0.08),
+        # drained workers retiring among the other events, no resync stimulus
+        "svcrt_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=53, n_inner_prefixes=3,
+                                                            random_durations=True, nthreads="random"), 1.1, 53, 0.1),
+        "svcrt_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=54), float("inf"), 54, 0.1),
     }
     for name, (mk, sat, seed, p_event) in cases.items():
         if only and name not in only:
@@ -1096,7 +1127,8 @@ def main_resync(only):
         dask.config.set({"distributed.scheduler.worker-saturation": sat})
         cfg = G.config_dict(sat)
         dumps = []
-        rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(g, cfg, seed, p_event, kinds, dumps=dumps)
+        kinds_ = (1, 2, 3, 4, 5, 6, 7, EV_RETIRE, EV_RETIRE, EV_PAUSE) if name.startswith("svcrt_") else kinds
+        rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(g, cfg, seed, p_event, kinds_, dumps=dumps)
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -1106,7 +1138,8 @@ def main_resync(only):
                  ev_stop=np.array(ev["stop"]), ev_runid=np.array(ev["runid"], np.int64),
                  hb_ptr=np.array(hb["ptr"], np.int64), hb_task=np.array(hb["task"], np.int32),
                  hb_dur=np.array(hb["dur"], np.float64), ev_round_ptr=np.array(round_ptr, np.int64))
-        z.update(_pack_dumps(dumps))
+        if dumps:
+            z.update(_pack_dumps(dumps))
         np.savez_compressed(path, **z)
         cnt = np.bincount(np.array(ev["kind"]), minlength=11).tolist()
         print(f"{name}: {len(ev['kind'])} events (by kind {cnt}), {len(dumps)} resyncs, {len(rec['task'])} placements, "

@@ -161,6 +161,20 @@ def test_extension_resyncs_after_stimuli_it_does_not_model():
         assert r["device_decisions"] + r["host_placements"] == r["placements"], r
 
 
+def test_extension_follows_retiring_workers_on_the_device():
+    """Drained workers retire (svcrt_*: paused, nothing processing, sole replicas copied
+    elsewhere first): Scheduler.remove_worker runs no transition, so the extension drops the
+    worker's replicas (dgp_remove_replicas through the replica hook) and removes it on the
+    device (dgp_remove_worker) with no resync; every placement is the engine's
+    (validate=True) and the extension stays active."""
+    names = ["svcrt_c2var_sat1.1.npz", "svcrt_c2mini_satinf.npz"]
+    res = drive(names)
+    assert [r["fixture"] for r in res] == names
+    for r in res:
+        assert r["active"] and r["resyncs"] == 0 and r["calls"]["workers_removed_on_device"] > 0, r
+        assert r["device_decisions"] == r["placements"], r
+
+
 def test_extension_hands_back_on_unmodelled_events():
     """An engine without the event calls: the first such event ends GPU placement loudly
     ("not modelled") and the scheduler's own decisions carry on, equal to the reference's."""

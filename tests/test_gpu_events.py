@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 
 from conftest import (GOLDEN, second_graph, svc_dep_graph_files, svc_event_files, svc_p2p_files, svc_prio_graph_files,
-                      svc_resync_files, svc_restr_graph_files)
+                      svc_resync_files, svc_restr_graph_files, svc_retire_files)
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -30,6 +30,7 @@ pytestmark = pytest.mark.gpu
 EV_FINISHED, EV_ADD_KEYS, EV_RELEASE_DATA, EV_PAUSE, EV_RESUME, EV_LONG_RUNNING, EV_HEARTBEAT, EV_ERRED = range(8)
 EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS = 8, 9, 10
 EV_SHUFFLE_INIT, EV_RESTRICT = 11, 12
+EV_RETIRE, EV_RETIRE_REPLICA = 13, 14
 
 
 def sync_dump(z, j):
@@ -79,6 +80,10 @@ def drive_events(eng, g, z, exp=None):
                 eng.set_rootish(ts, np.zeros(len(ts), np.int8))
             elif kd == EV_RESTRICT:  # restrict_task -> set_restrictions({key: {worker}})
                 eng.update_restrictions([t], [[w]], [1])
+            elif kd == EV_RETIRE_REPLICA:  # remove_worker drops the retiring worker's replicas (:5263-5265)
+                eng.remove_replicas([t], [w])
+            elif kd == EV_RETIRE:  # then the worker itself, no transition: no resync
+                eng.remove_worker(w)
             elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
                 # the scheduler decided this stimulus itself: its placements, then its state
                 n = int(exp["stim_nplaced"][len(stim)])
@@ -145,6 +150,34 @@ def test_service_events_refuse_what_they_do_not_model():
         with pytest.raises(_lib.DgpError, match="paused"):
             eng.add_graph(dict(h, prio=g2["prio"] + len(g["prio"]), group_id=g2["group_id"] + len(g["group_prefix"]),
                                group_prefix=np.concatenate([g["group_prefix"], g2["group_prefix"]])))
+
+
+@pytest.mark.parametrize("name", svc_retire_files())
+def test_service_retiring_workers_match_reference(name):
+    """Drained workers retire (Scheduler.remove_worker, scheduler.py:5180-5360, of a paused
+    worker with nothing processing whose sole replicas were first copied elsewhere by
+    add-keys, as retire_workers does): remove_worker runs no transition, so the engine
+    follows it on the device -- its replicas dropped (dgp_remove_replicas), the worker
+    removed (dgp_remove_worker) -- with no resync; every later placement, the snapshots and
+    the final states equal the reference's."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    kinds = set(np.unique(z["ev_kind"]).tolist())
+    assert {EV_RETIRE, EV_RETIRE_REPLICA} <= kinds and not kinds & {EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS}
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        stim = drive_events(eng, g, z, exp)
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert np.array_equal(stim, exp["stim_nplaced"]), np.nonzero(stim != exp["stim_nplaced"])[0][:5]
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
 
 
 @pytest.mark.parametrize("name", svc_resync_files())
