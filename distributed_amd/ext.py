@@ -1290,7 +1290,11 @@ class GPUPlacementExtension(SchedulerPlugin):
         if ts is not None and key in self.dev_run and msg.get("run_id") == ts.run_id:
             run = self.dev_run[key]
         nbytes = msg.get("nbytes")
-        a, b = _compute_interval(msg.get("startstops"))
+        ss = msg.get("startstops")
+        if ss and len(ss) == 1 and ss[0].get("action") == "compute":  # the usual message
+            a, b = float(ss[0]["start"]), float(ss[0]["stop"])
+        else:
+            a, b = _compute_interval(ss)
         return t, w, run, -1 if nbytes is None else int(nbytes), a, b
 
     async def handle_stream(self, comm, extra=None):
@@ -1348,9 +1352,34 @@ class GPUPlacementExtension(SchedulerPlugin):
             await comm.close()
 
     def handle_task_finished(self, key=None, worker=None, stimulus_id=None, **msg):
-        """Stream handler "task-finished" (scheduler.py:3769 -> :5783-5797)."""
-        msg["key"], msg["worker"], msg["stimulus_id"] = key, worker, stimulus_id
-        self.handle_task_finished_batch((msg,))
+        """Stream handler "task-finished" (scheduler.py:3769 -> :5783-5797). The common case
+        -- engine active, nothing left from the previous stimulus -- inline:
+        ``handle_task_finished_batch`` of one message."""
+        eng = self.engine
+        post = getattr(eng, "tasks_finished_post", None)
+        if (post is None or not self.active or not self.overlap or self.suspended or self.pending or self._msg_of
+                or self._posted is not None):
+            msg["key"], msg["worker"], msg["stimulus_id"] = key, worker, stimulus_id
+            return self.handle_task_finished_batch((msg,))
+        self._window = None
+        s = self.scheduler
+        try:
+            post(*[(x,) for x in self._message_fields(key, worker, msg)])
+        except Exception as e:
+            self.fallback(f"tasks_finished: {e}")
+        else:
+            self._posted = self._posted_pairs = [(key, worker)]
+        self._allowed.append(_STIMULUS_TRANSITIONS)
+        try:
+            type(s).handle_task_finished(s, key=key, worker=worker, stimulus_id=stimulus_id, **msg)
+        finally:
+            self._allowed.pop()
+            self._settle()  # a message whose transitions asked for no decision
+            self._expect_replicas.clear()
+        if self.suspended:
+            self._resync()
+        if self.pending or self._msg_of:
+            self._end_of_stimulus("task-finished")
 
     def handle_task_finished_batch(self, msgs):
         """Several task-finished messages in arrival order: ONE engine call (one PCIe copy),
@@ -1375,11 +1404,11 @@ class GPUPlacementExtension(SchedulerPlugin):
             try:
                 if self.overlap and hasattr(self.engine, "tasks_finished_post"):
                     self.engine.tasks_finished_post(*cols)
-                    self._posted = msgs
-                    self._posted_pairs = (((m["key"], m["worker"]),) if len(msgs) == 1
-                                          else {(m["key"], m["worker"]) for m in msgs})
+                    pairs = [(m["key"], m["worker"]) for m in msgs]
+                    self._posted = pairs
+                    self._posted_pairs = pairs if len(pairs) == 1 else set(pairs)
                 else:
-                    self._answer(msgs, *self.engine.tasks_finished(*cols))
+                    self._answer([(m["key"], m["worker"]) for m in msgs], *self.engine.tasks_finished(*cols))
             except Exception as e:
                 self.fallback(f"tasks_finished: {e}")
         self._allowed.append(_STIMULUS_TRANSITIONS)
@@ -1395,17 +1424,17 @@ class GPUPlacementExtension(SchedulerPlugin):
         if self.pending or self._msg_of:
             self._end_of_stimulus("task-finished")
 
-    def _answer(self, msgs, status, n_new):
+    def _answer(self, pairs, status, n_new):
         status = status.tolist()
         # an already-in-memory report (add_keys) adds a replica after the placements of the
         # messages before it: those compute-task messages take who_has from the scheduler, as
         # built at their time (the reference's own _task_to_msg)
         self._fetch(n_new, messages=len(status) == 1 or 2 not in status)
-        self.stats["messages"] += len(msgs)
+        self.stats["messages"] += len(pairs)
         expect, bad = self._expect_replicas, False
-        for m, st in zip(msgs, status):
+        for kw, st in zip(pairs, status):
             if st == 0:  # accepted: _add_to_memory adds this replica itself (:3296)
-                expect.add((m["key"], m["worker"]))
+                expect.add(kw)
             elif st >= 3 and st != 4:
                 bad = True
         # DGP_TF_RELEASE / _IMPOSSIBLE / _UNSUPPORTED: the reference reschedules or raises;
@@ -1416,13 +1445,13 @@ class GPUPlacementExtension(SchedulerPlugin):
     def _settle(self):
         """The posted batch's answer (dgp_tasks_finished_wait), then the replica additions
         the handler made before it, classified as add_replica would have at the time."""
-        msgs = self._posted
-        if msgs is None:
+        pairs = self._posted
+        if pairs is None:
             return
         self._posted = None
         self._posted_pairs = ()
         try:
-            self._answer(msgs, *self.engine.tasks_finished_wait())
+            self._answer(pairs, *self.engine.tasks_finished_wait())
         except Exception as e:
             self.fallback(f"tasks_finished: {e}")
         adds, self._deferred_adds = self._deferred_adds, []
