@@ -44,6 +44,23 @@ def test_extension_places_every_task_from_the_engine():
     assert next(r for r in res if r["fixture"] == "restr_noworker_sat1.1.npz")["device_no_worker"] > 0
 
 
+def test_extension_batches_and_synchronous_calls():
+    """The other two ways the task-finished messages reach the engine: a comm.read batch of
+    one worker's consecutive messages through handle_stream (one posted call for several
+    messages, the answer taken at the first decision), and the engine call made
+    synchronously before the handler (overlap off). Same decisions, validate=True."""
+    names = ["c2var_sat1.1.npz", "c3mini_sat1.1.npz", "restr_sat1.1.npz", "nodep_w24_sat1.1.npz"]
+    for flags in (("--stream",), ("--nooverlap",)):
+        res = drive(names, *flags)
+        assert [r["fixture"] for r in res] == names
+        for r in res:
+            assert r["active"] and r["device_decisions"] == r["placements"], (flags, r)
+            if flags == ("--stream",):
+                assert r["engine_calls"] == r["reads"] <= r["messages"], r
+            else:
+                assert r["us_overlap_window"] == 0.0, r
+
+
 def test_extension_follows_workers_joining():
     """Scheduler.add_worker mid-stream: the plugin hook adds the worker to the engine, and
     the scheduler's queue refill takes the engine's decisions (validate=True agrees)."""
