@@ -301,8 +301,11 @@ def service_leg(eng_cls, local: int, args) -> dict:
     does). Two granularities: one call per round (every completion of the previous round's
     placements) and one call per message; each launch-per-call and through the resident
     kernel (dgp_set_resident: mailbox in pinned host memory, no launch / copy / sync per
-    call). Host-inclusive (ctypes included); checked bit-exact against the oracle's replay
-    of the same protocol."""
+    call). ``per_message_overlap_ext`` is the extension's own path: each message posted
+    (dgp_tasks_finished_post), ``--svc-window-us`` of host work standing in for the reference
+    handler's Python before its first decision, then the wait and ``engine.answer``; its
+    ``exposed_us_per_call`` is what the engine adds to the handler. Host-inclusive (ctypes
+    included); checked bit-exact against the oracle's replay of the same protocol."""
     from distributed_amd import graphs
 
     g = graphs.random_dag(args.svc_tasks, 1024, seed=5)
