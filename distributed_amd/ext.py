@@ -1429,7 +1429,8 @@ class GPUPlacementExtension(SchedulerPlugin):
         # an already-in-memory report (add_keys) adds a replica after the placements of the
         # messages before it: those compute-task messages take who_has from the scheduler, as
         # built at their time (the reference's own _task_to_msg)
-        self._fetch(n_new, messages=len(status) == 1 or 2 not in status)
+        if n_new:
+            self._fetch(n_new, messages=len(status) == 1 or 2 not in status)
         self.stats["messages"] += len(pairs)
         expect, bad = self._expect_replicas, False
         for kw, st in zip(pairs, status):
@@ -1454,6 +1455,8 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._answer(pairs, *self.engine.tasks_finished_wait())
         except Exception as e:
             self.fallback(f"tasks_finished: {e}")
+        if not self._deferred_adds:
+            return
         adds, self._deferred_adds = self._deferred_adds, []
         for ts, ws, had in adds:
             k = (ts.key, ws.address)
