@@ -61,6 +61,16 @@ def test_extension_batches_and_synchronous_calls():
                 assert r["us_overlap_window"] == 0.0, r
 
 
+def test_ab_timing_harness():
+    """ext_driver.py --ab (DESIGN §7's per-message A/B): both sides of one process make the
+    reference's placements from the same messages, every placement on the extension's side
+    comes from the engine, and the report carries the difference with its interval."""
+    r = drive(["c2var_sat1.1.npz"], "--ab")[0]
+    assert r["mode"] == "ab" and r["messages"] > 1000, r
+    for k in ("reference_us_per_message", "extension_host_us_per_message", "diff_us_per_message", "diff_ci95_us"):
+        assert isinstance(r[k], float) and r[k] == r[k], (k, r)
+
+
 def test_extension_follows_workers_joining():
     """Scheduler.add_worker mid-stream: the plugin hook adds the worker to the engine, and
     the scheduler's queue refill takes the engine's decisions (validate=True agrees)."""
