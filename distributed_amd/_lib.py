@@ -11,6 +11,9 @@ import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DGP_LIB") or os.path.join(PKG, "libdgplace.so")  # DGP_LIB: debugging only
+# the same sources built with a 64-slot stimulus window and no wait-in-place claims
+# (-DDGP_WIN=64 -DDGP_WAITC=0, build.py): what graphs with restrictions run
+LIB_W64_PATH = os.path.join(PKG, "libdgplace_w64.so")
 
 _P = C.c_void_p
 _i32p = C.POINTER(C.c_int32)
@@ -80,20 +83,20 @@ SIGNATURES = {
 }
 
 ABI_VERSION = 15
-_lib = None
+_libs: dict = {}
 
 
 class DgpError(RuntimeError):
     pass
 
 
-def load() -> C.CDLL:
-    """Load libdgplace.so (raises if it was not built)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise DgpError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+def load(window: int = 32) -> C.CDLL:
+    """Load libdgplace.so (``window`` 64: libdgplace_w64.so); raises if it was not built."""
+    path = LIB_PATH if window == 32 else LIB_W64_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise DgpError(f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                        " (the HIP engine has no CPU fallback)")
     # One HIP runtime per process: torch bundles its own libamdhip64 (same soname,
     # libamdhip64.so.7, as /opt/rocm's), and a second runtime loaded beside an
@@ -104,12 +107,12 @@ def load() -> C.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
-    lib = C.CDLL(LIB_PATH)
+    lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     if lib.dgp_abi_version() != ABI_VERSION:
-        raise DgpError(f"libdgplace ABI {lib.dgp_abi_version()} != {ABI_VERSION}")
-    _lib = lib
+        raise DgpError(f"{os.path.basename(path)} ABI {lib.dgp_abi_version()} != {ABI_VERSION}")
+    _libs[path] = lib
     return lib

@@ -12,6 +12,10 @@ DEPS = [os.path.join(PKG, "csrc", "dgp_device.h"), os.path.join(PKG, "csrc", "dg
         os.path.join(PKG, "csrc", "dgp_events.h"), os.path.join(PKG, "csrc", "dgp_svcmsg.h"),
         os.path.join(PKG, "csrc", "dgp_msgs.h")]
 OUT = os.path.join(PKG, "libdgplace.so")
+# the same sources with a 64-slot stimulus window and no wait-in-place claims: graphs with
+# restrictions run this build (engine.py PlacementEngine.load)
+OUT_W64 = os.path.join(PKG, "libdgplace_w64.so")
+W64_FLAGS = ["-DDGP_WIN=64", "-DDGP_WAITC=0"]
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 # -ffp-contract=off: no fused multiply-add, so fp64 results round exactly like the
 # reference's CPython arithmetic (the parity contract is bit-exact objectives).
@@ -23,12 +27,17 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fn
 
 
 def build(force: bool = False) -> str:
+    """Both builds, compiled side by side; returns the default library's path."""
     newest = max(os.path.getmtime(p) for p in SRC + DEPS + [os.path.join(PKG, "..", "include", "dgplace.h")])
-    if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= newest:
-        return OUT
-    tmp = OUT + ".tmp"
-    subprocess.check_call([HIPCC, *FLAGS, "-o", tmp, *SRC])
-    os.replace(tmp, OUT)
+    jobs = []
+    for out, extra in ((OUT, []), (OUT_W64, W64_FLAGS)):
+        if not force and os.path.exists(out) and os.path.getmtime(out) >= newest:
+            continue
+        jobs.append((out, subprocess.Popen([HIPCC, *FLAGS, *extra, "-o", out + ".tmp", *SRC])))
+    for out, proc in jobs:
+        if proc.wait() != 0:
+            raise subprocess.CalledProcessError(proc.returncode, f"hipcc -> {out}")
+        os.replace(out + ".tmp", out)
     return OUT
 
 

@@ -52,8 +52,13 @@ def conflict_depth(g: dict, out: dict, first: int = 0) -> tuple[int, int]:
 class PlacementEngine:
     """One device engine bound to HIP device ``device``."""
 
-    def __init__(self, device: int = 0):
-        self.lib = _lib.load()
+    def __init__(self, device: int = 0, window: int | str = "auto"):
+        """``window``: the stream kernel's in-flight stimulus window -- 32 (wait-in-place
+        claims, libdgplace.so), 64 (no wait-in-place, libdgplace_w64.so) or "auto": 64 for a
+        graph with restrictions, chosen at ``load`` (the restricted unpacks'
+        completions are window-bound; the C2 chain needs wait-in-place)."""
+        self.window = window
+        self.lib = _lib.load(64 if window == 64 else 32)
         self.device = int(device)
         h = self.lib.dgp_create(int(device))
         if not h:
@@ -138,12 +143,26 @@ class PlacementEngine:
     def load(self, g: dict, config: dict | None = None, *, snapshots: int = 0, results: bool = True):
         """Configure workers + config + graph in one go (the usual set-up). ``results``:
         upload the synthetic executor's completion reports (replay mode)."""
+        if self.window == "auto" and self.n_tasks == 0:
+            rf = g.get("restr_flags")
+            self._use_lib(64 if rf is not None and np.asarray(rf).any() else 32)
         self.set_workers(g["nthreads"])
         self.set_config(config)
         if snapshots:
             self._check(self.lib.dgp_enable_snapshots(self.h, int(snapshots)), "dgp_enable_snapshots")
         self.set_graph(g, results=results)
         return self
+
+    def _use_lib(self, window: int):
+        """A fresh engine on the build with that window (before anything was uploaded)."""
+        lib = _lib.load(window)
+        if lib is self.lib:
+            return
+        h = lib.dgp_create(self.device)
+        if not h:
+            raise _lib.DgpError(f"dgp_create({self.device}) failed: no HIP device visible (no CPU fallback)")
+        self.lib.dgp_destroy(self.h)
+        self.lib, self.h = lib, h
 
     # ------------------------------------------------------------------- replay
     def reset(self):

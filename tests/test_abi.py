@@ -17,8 +17,9 @@ def declared():
     return sorted(set(re.findall(r"\b(dgp_[a-z_]+)\s*\(", src)))
 
 
-def test_library_exports_every_declared_symbol():
-    lib = _lib.load()
+@pytest.mark.parametrize("window", [32, 64])
+def test_library_exports_every_declared_symbol(window):
+    lib = _lib.load(window)  # libdgplace.so and the 64-slot window build libdgplace_w64.so
     names = declared()
     assert len(names) >= 15
     missing = [n for n in names if not hasattr(lib, n)]
@@ -31,6 +32,7 @@ def test_binding_covers_header():
 
 def test_abi_version():
     assert _lib.load().dgp_abi_version() == _lib.ABI_VERSION
+    assert _lib.load(64).dgp_abi_version() == _lib.ABI_VERSION
 
 
 def test_create_without_gpu_returns_null_or_engine():
