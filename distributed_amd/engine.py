@@ -54,9 +54,9 @@ class PlacementEngine:
 
     def __init__(self, device: int = 0, window: int | str = "auto"):
         """``window``: the stream kernel's in-flight stimulus window -- 32 (wait-in-place
-        claims, libdgplace.so), 64 (no wait-in-place, libdgplace_w64.so) or "auto": 64 for a
-        graph with restrictions, chosen at ``load`` (the restricted unpacks'
-        completions are window-bound; the C2 chain needs wait-in-place)."""
+        claims, libdgplace.so), 64 (no wait-in-place, libdgplace_w64.so) or "auto": chosen at
+        ``load`` by ``auto_window`` (the unpacks' completions after a wide
+        frontier are window-bound; the C2 chain needs wait-in-place)."""
         self.window = window
         self.lib = _lib.load(64 if window == 64 else 32)
         self.device = int(device)
@@ -144,14 +144,28 @@ class PlacementEngine:
         """Configure workers + config + graph in one go (the usual set-up). ``results``:
         upload the synthetic executor's completion reports (replay mode)."""
         if self.window == "auto" and self.n_tasks == 0:
-            rf = g.get("restr_flags")
-            self._use_lib(64 if rf is not None and np.asarray(rf).any() else 32)
+            self._use_lib(self.auto_window(g))
         self.set_workers(g["nthreads"])
         self.set_config(config)
         if snapshots:
             self._check(self.lib.dgp_enable_snapshots(self.h, int(snapshots)), "dgp_enable_snapshots")
         self.set_graph(g, results=results)
         return self
+
+    WIDE_FRONTIER = 4096  # dependents of one task from which the 64-slot build is chosen
+
+    @classmethod
+    def auto_window(cls, g: dict) -> int:
+        """64 for a graph with restrictions or a wide frontier (a task with at least
+        WIDE_FRONTIER dependents: the P2P barrier, whose completion readies every unpack at
+        once), else 32."""
+        rf = g.get("restr_flags")
+        if rf is not None and np.asarray(rf).any():
+            return 64
+        di = np.asarray(g["dep_idx"])
+        if len(di) and int(np.bincount(di[di >= 0]).max()) >= cls.WIDE_FRONTIER:
+            return 64
+        return 32
 
     def _use_lib(self, window: int):
         """A fresh engine on the build with that window (before anything was uploaded)."""
