@@ -10,10 +10,15 @@ import ctypes as C
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("DGP_LIB") or os.path.join(PKG, "libdgplace.so")  # DGP_LIB: debugging only
+# DGP_LIB (debugging / A-B runs only): a variant build used for BOTH windows, unless
+# DGP_LIB_W64 names the 64-slot variant too -- a variant is never silently paired with the
+# packaged build of the other window.
+LIB_PATH = os.environ.get("DGP_LIB") or os.path.join(PKG, "libdgplace.so")
 # the same sources built with a 64-slot stimulus window and no wait-in-place claims
 # (-DDGP_WIN=64 -DDGP_WAITC=0, build.py): what graphs with restrictions run
-LIB_W64_PATH = os.path.join(PKG, "libdgplace_w64.so")
+LIB_W64_PATH = (os.environ.get("DGP_LIB_W64") or os.environ.get("DGP_LIB")
+                or os.path.join(PKG, "libdgplace_w64.so"))
+WINDOWS = (32, 64)
 
 _P = C.c_void_p
 _i32p = C.POINTER(C.c_int32)
@@ -92,6 +97,8 @@ class DgpError(RuntimeError):
 
 def load(window: int = 32) -> C.CDLL:
     """Load libdgplace.so (``window`` 64: libdgplace_w64.so); raises if it was not built."""
+    if window not in WINDOWS:
+        raise ValueError(f"window must be one of {WINDOWS}, not {window!r}")
     path = LIB_PATH if window == 32 else LIB_W64_PATH
     if path in _libs:
         return _libs[path]

@@ -10,7 +10,7 @@ SRC = [os.path.join(PKG, "csrc", "dgplace.hip")]
 DEPS = [os.path.join(PKG, "csrc", "dgp_device.h"), os.path.join(PKG, "csrc", "dgp_stream.h"),
         os.path.join(PKG, "csrc", "dgp_steal.h"), os.path.join(PKG, "csrc", "dgp_service.h"),
         os.path.join(PKG, "csrc", "dgp_events.h"), os.path.join(PKG, "csrc", "dgp_svcmsg.h"),
-        os.path.join(PKG, "csrc", "dgp_msgs.h")]
+        os.path.join(PKG, "csrc", "dgp_msgs.h"), os.path.join(PKG, "csrc", "dgp_exev.h")]
 OUT = os.path.join(PKG, "libdgplace.so")
 # the same sources with a 64-slot stimulus window and no wait-in-place claims: graphs with
 # restrictions run this build (engine.py PlacementEngine.load)
@@ -33,11 +33,26 @@ def build(force: bool = False) -> str:
     for out, extra in ((OUT, []), (OUT_W64, W64_FLAGS)):
         if not force and os.path.exists(out) and os.path.getmtime(out) >= newest:
             continue
-        jobs.append((out, subprocess.Popen([HIPCC, *FLAGS, *extra, "-o", out + ".tmp", *SRC])))
-    for out, proc in jobs:
-        if proc.wait() != 0:
-            raise subprocess.CalledProcessError(proc.returncode, f"hipcc -> {out}")
+        log = open(out + ".log", "w")  # one diagnostics file per job: the two never interleave
+        jobs.append((out, log, subprocess.Popen([HIPCC, *FLAGS, *extra, "-o", out + ".tmp", *SRC],
+                                                stdout=log, stderr=subprocess.STDOUT)))
+    failed = []
+    for out, log, proc in jobs:  # every job is waited for before anything is raised
+        rc = proc.wait()
+        log.close()
+        if rc != 0:
+            failed.append((out, rc))
+    for out, log, proc in jobs:
+        if any(out == f for f, _ in failed):
+            if os.path.exists(out + ".tmp"):
+                os.remove(out + ".tmp")
+            continue
         os.replace(out + ".tmp", out)
+        os.remove(out + ".log")
+    if failed:
+        out, rc = failed[0]
+        msg = open(out + ".log").read()[-4000:]
+        raise subprocess.CalledProcessError(rc, f"hipcc -> {out}", output=msg)
     return OUT
 
 

@@ -82,6 +82,10 @@ __constant__ Dev c_dev;
 #define DGP_FAST 0  // F_FAST stimuli take exe_fast (0: exe_local). Measured (profiles/r04ab): with exe_local
                     // inlined and no exe_fast, C2 1.021 s vs 1.003-1.01 s and C3 0.118 vs 0.129 s
 #endif
+#ifndef DGP_EXEV
+#define DGP_EXEV 0  // 1: F_FAST stimuli on the LDS worker layout take exe_v (dgp_exev.h), the vector form: measured
+                    // 30% slower per stimulus than exe_local (profiles/r05/exev_*), kept off
+#endif
 #ifndef DGP_LOCAL_INLINE
 #define DGP_LOCAL_INLINE 1  // exe_local inlined into the claim loop (else out of line, its own registers)
 #endif
@@ -262,12 +266,21 @@ __device__ __forceinline__ unsigned long long ballot(bool b) { return __ballot(b
 __device__ __forceinline__ unsigned long long mclk() { return DGP_PROF ? __builtin_amdgcn_s_memtime() : 0ull; }
 // DGP_TRACE builds: lifecycle timestamps of sampled stimuli (tools/trace_analyze.py):
 // 0 registered, 1 ready, 2 claimed, 3 early release, 4 non-w release, 5 done, 6 retired,
-// 7 predecessor count | touched workers << 16 | executor wave << 24
+// 7 predecessor count | touched workers << 16 | executor wave << 24.
+// DGP_TRACE=3: those, plus the executor's phases and who made the stimulus ready
+// (tools/link_profile.py): 8 precheck, 9 state loaded, 10 completion needs, 11 before the
+// wait, 12 after the wait, 13 first frontier keys, 14 argmin + early release, 15 first commit,
+// 16 frontier done, 17 refill done, 18 w released, 19 the stimulus whose release made it
+// ready, 20 candidates final (predc 0), 21 the stimulus whose release did that,
+// 22 nf | kt << 8 | nrel << 16 | nt << 24, 23 predc at the claim. One row is DGP_TSTR words.
 #ifndef DGP_TRACE
 #define DGP_TRACE 0
 #endif
+constexpr int TSTR = 32;
+constexpr bool TRL = DGP_TRACE == 1 || DGP_TRACE == 3;  // lifecycle events
+constexpr bool TR3 = DGP_TRACE == 3;                     // executor phases
 __device__ __forceinline__ void trace_at(const Dev& D, long long r, int k, unsigned long long v) {
-  if (DGP_TRACE && D.trace && r >= D.trace_lo && r < D.trace_lo + D.trace_n) D.trace[(r - D.trace_lo) * 8 + k] = v;
+  if (DGP_TRACE && D.trace && r >= D.trace_lo && r < D.trace_lo + D.trace_n) D.trace[(r - D.trace_lo) * TSTR + k] = v;
 }
 #define TR(r, k) trace_at(D, (r), (k), __builtin_amdgcn_s_memtime())
 #define PROF(stmt) \
@@ -1313,7 +1326,7 @@ __device__ __attribute__((always_inline)) void role_seq(const Dev& D, SLds& L, c
       if (D.resident) S.t_role[5] = rclk();
       if (DGP_TRACE) {
         const unsigned long long tn = __builtin_amdgcn_s_memtime();
-        if (DGP_TRACE == 1) for (int i = 0; i < m; i++) trace_at(D, sp + i, 6, tn);
+        if (TRL) for (int i = 0; i < m; i++) trace_at(D, sp + i, 6, tn);
       }
 
     }
@@ -1556,7 +1569,7 @@ __device__ __attribute__((always_inline)) void build_desc_seq(const Dev& D, SLds
         const int i = tix[q];
         if (q < kx && i >= 0 && i < 32 && !((cmask >> i) & 1u)) {
           cmask |= 1u << i;
-          if (DGP_FAST && jf < NFF && i < TF) {  // exe_fast's rows (only it reads them)
+          if ((DGP_FAST || DGP_EXEV) && jf < NFF && i < TF) {  // exe_fast's / exe_v's rows
             int64_t held = 0;
 #pragma unroll
             for (int q2 = 0; q2 < KX_MAX; q2++)
@@ -1777,7 +1790,7 @@ __device__ __attribute__((always_inline)) bool build_desc_g(const Dev& D, SLds& 
         const int ti = tix[i];
         if (i < kx && ti >= 0 && ti < 32 && !((cmask >> ti) & 1u)) {
           cmask |= 1u << ti;
-          if (DGP_FAST && j < NFF && ti < TF) {  // exe_fast's rows (only it reads them)
+          if ((DGP_FAST || DGP_EXEV) && j < NFF && ti < TF) {  // exe_fast's / exe_v's rows
             int64_t held = 0;
 #pragma unroll
             for (int i2 = 0; i2 < KX_MAX; i2++)
@@ -2070,8 +2083,8 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
       const int op = __hip_atomic_fetch_add(&L.pred[my_s], -BIG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (op == BIG) atomicOr(&S.ready, 1ull << my_s);
       if (DGP_TRACE) {
-        if (DGP_TRACE == 1) TR(r0 + lane, 0);
-        if (DGP_TRACE == 1 && op == BIG) TR(r0 + lane, 1);
+        if (TRL) TR(r0 + lane, 0);
+        if (TRL && op == BIG) TR(r0 + lane, 1);
         trace_at(D, r0 + lane, 7, (unsigned long long)((op - BIG) | (nt << 16)));
       }
     }
@@ -2363,7 +2376,7 @@ __device__ __forceinline__ bool dict_update(const WPtr<LW>& P, int c, int p, int
 // of them is the one waiting for s on c, and it alone counted s (role_reg): it counts down.
 // With WAITC the high half of the old mask says, per successor, whether it registered the
 // worker as a candidate only: its candidate count (predc) counts down instead.
-__device__ __forceinline__ int release_succ(SLds& L, SMask old) {  // -> the slot made ready, or -1
+__device__ __forceinline__ int release_succ(SLds& L, SMask old, int from = -1) {  // -> the slot made ready, or -1
   const SMask succ = WAITC ? (old & 0xffffffffull) : old;
   if (!succ) return -1;
   int bs = __builtin_ctzll(succ);
@@ -2377,12 +2390,21 @@ __device__ __forceinline__ int release_succ(SLds& L, SMask old) {  // -> the slo
     }
   }
   if (WAITC && ((old >> 32) >> bs) & 1ull) {
-    __hip_atomic_fetch_add(&L.predc[bs], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int pc = __hip_atomic_fetch_add(&L.predc[bs], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (TR3 && pc == 1) {
+      const Dev& D = c_dev;
+      TR(L.sid[bs], 20);
+      if (from >= 0) trace_at(D, L.sid[bs], 21, (unsigned long long)L.sid[from]);
+    }
     return -1;
   }
   if (atomicSub(&L.pred[bs], 1) == 1) {
     atomicOr(&L.c.ready, 1ull << bs);
-    if (DGP_TRACE == 1) { const Dev& D = c_dev; TR(L.sid[bs], 1); }
+    if (TRL) {
+      const Dev& D = c_dev;
+      TR(L.sid[bs], 1);
+      if (TR3 && from >= 0) trace_at(D, L.sid[bs], 19, (unsigned long long)L.sid[from]);
+    }
     return bs;
   }
   return -1;
@@ -2390,7 +2412,8 @@ __device__ __forceinline__ int release_succ(SLds& L, SMask old) {  // -> the slo
 template <bool LW>
 __device__ __forceinline__ int release_worker(SLds& L, const WPtr<LW>& P, int s, int c) {
   const SMask bit = slot_bits(s);
-  return release_succ(L, __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
+  return release_succ(L, __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit,
+                      DGP_TRACE ? s : -1);
 }
 
 // release the workers of slot s (the waiting successors may run) — LDS state only
@@ -2399,7 +2422,8 @@ __device__ __attribute__((always_inline)) void release_slot(const Dev& D, SLds& 
   const int lane = lane_id();
   const SMask bit = slot_bits(s);
   auto rel = [&](int c) {
-    release_succ(L, __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit);
+    release_succ(L, __hip_atomic_fetch_and(&P.mask[c], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~bit,
+                 DGP_TRACE ? s : -1);
   };
   if (all) {
     for (int c = lane; c < D.W; c += 64) rel(c);
@@ -2536,6 +2560,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   o.st0 = (size_t)(r & (RS - 1)) * PLC;
   phase(11);
   if (DGP_TRACE == 2 && lane == 0) TR(r, 0);
+  if (TR3 && lane == 0) TR(r, 8);
   // ---- the touched workers' state, one lane each, in registers for the whole stimulus
   const int nt = L.ntouch[s];
   const bool tl = lane < nt;
@@ -2569,6 +2594,11 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   const bool nth1 = !ballot(tl && nth != 1);  // occ / 1.0 == occ: the division is skipped
   phase(16);
   if (DGP_TRACE == 2 && lane == 0) TR(r, 1);
+  if (TR3 && lane == 0) {
+    TR(r, 9);
+    trace_at(D, r, 22, (unsigned long long)(nf | kt << 8 | nrel << 16 | nt << 24));
+    trace_at(D, r, 23, (unsigned long long)vload(&L.predc[s]));
+  }
   // ------------------------------------------- completion: processing -> memory (:2366)
   int64_t dnet = 0;
   int64_t freed = 0;
@@ -2592,6 +2622,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   if (dnet != 0) nbw = net_bw_of(net, D);  // dnet is uniform
   phase(17);
   if (DGP_TRACE == 2 && lane == 0) TR(r, 3);
+  if (TR3 && lane == 0) TR(r, 10);
   // every lane's occupancy and stack time, kept current: only w (now) and each chosen
   // worker (after its commit) change during the stimulus
   double occj = occ_dict_r(dj, nbw, durv, D);
@@ -2617,6 +2648,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       released = ro;
     }
   }
+  if (TR3 && lane == 0) TR(r, 11);
   if (WAITC && ballot(wc)) {
     // ---- the candidates: every earlier stimulus holding one has released it (release_succ
     // counts predc down), then their state, with this stimulus' releases applied
@@ -2657,6 +2689,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   }
   phase(12);
   if (DGP_TRACE == 2 && lane == 0) TR(r, 4);
+  if (TR3 && lane == 0) TR(r, 12);
   // ------------------------------ frontier in ascending priority: decide_worker (:8550)
   int off = FX0;
   for (int j = 0; j < nf; j++) {
@@ -2697,6 +2730,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     }
 #endif
     phase(18);
+    if (TR3 && lane == 0 && j == 0) TR(r, 13);
     const unsigned long long cm = ballot(cand);
     if (!cm) {
       serr(S, SERR_CAND, x);
@@ -2733,10 +2767,11 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (early) release_worker<LW>(L, P, s, cj);
         released = released || early;
-        if (DGP_TRACE == 1 && lane == 0) TR(r, 3);
+        if (TRL && lane == 0) TR(r, 3);
       }
     }
     phase(19);
+    if (TR3 && lane == 0 && j == 0) TR(r, 14);
     // _add_to_processing (:3199): record, WorkerState.add_to_processing, check_idle_saturated
     o.place(D, x, cb, best.comm, best.start, best.nb, ROUTE_NONROOTISH);
     uint32_t nlc = line_load<LW>(P, cb);
@@ -2770,8 +2805,10 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     o.rec(D, K_PLACE, cb, px, dn, mkd(rlu(dlo(occj), jb), rlu(dhi(occj), jb)), rl(np, jb), x, 0.0);
     off += 1 + kx + nc;
     phase(20);
+    if (TR3 && lane == 0 && j == 0) TR(r, 15);
   }
   if (DGP_TRACE == 2 && lane == 0) TR(r, 6);
+  if (TR3 && lane == 0) TR(r, 16);
   // ---- every touched worker but w is final: write back and release it now (its waiting
   // successors may run while w takes the queue refill)
   if (tl && !isw && !released) {
@@ -2788,7 +2825,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     if (tl && !isw && !released) release_worker<LW>(L, P, s, cj);
   }
-  if (DGP_TRACE == 1 && lane == 0) TR(r, 4);
+  if (TRL && lane == 0) TR(r, 4);
   // -------------- stimulus_queue_slots_maybe_opened (:4983): only w can have open slots
   int pops = 0;
   if (qmode != 0 && !D.sat_inf) {
@@ -2817,6 +2854,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
       o.rec(D, K_PLACE, w, qp, 0, mkd(rlu(dlo(occj), jw), rlu(dhi(occj), jw)), rl(np, jw), -1, 0.0);
     }
   }
+  if (TR3 && lane == 0) TR(r, 17);
   // ---- w written back last, then released
   if (isw) {
     using U4 = typename WPtr<LW>::template P<Q4>;
@@ -2831,6 +2869,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   int wk = -1;
   if (lane == jw) wk = release_worker<LW>(L, P, s, w);
+  if (TR3 && lane == 0) TR(r, 18);
   woke = rl(wk, jw);  // the stimulus next on w, if this release made it ready (DGP_EXE_CONT)
   phase(13);
   // ------------------------------------------------ retire: LDS state, then successors
@@ -3400,6 +3439,8 @@ __device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, co
   PROF(if (lane == 0) { S.prof[11] += 1; S.prof[12] += k; });
   return true;
 }
+
+#include "dgp_exev.h"
 
 // out of line, one register allocation each (inlined into the claim loop together they
 // spilled to scratch); -2: nothing changed (the stimulus goes back exact), else the slot the
@@ -4435,7 +4476,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     if (DGP_TRACE && lane == 0) {
       TR(cr, 2);
       trace_at(D, cr, 7, D.trace && cr >= D.trace_lo && cr < D.trace_lo + D.trace_n
-                             ? (D.trace[(cr - D.trace_lo) * 8 + 7] | ((unsigned long long)(threadIdx.x >> 6) << 24)) : 0);
+                             ? (D.trace[(cr - D.trace_lo) * TSTR + 7] | ((unsigned long long)(threadIdx.x >> 6) << 24)) : 0);
     }
     const unsigned long long t0 = mclk();
     if (D.resident && lane == 0) S.t_role[3] = rclk();
@@ -4446,7 +4487,11 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       // a run of single-worker completions, back to back (only this executor calls out of line)
     } else {
       int rc = -2;
-      if (DGP_FAST && (cf & F_FAST) && !cex && cq <= 1) {  // the lean path (inlined: the common case)
+      if (LW && DGP_EXEV && (cf & F_FAST) && !cex && cq <= 1) {  // the vector form (the common case)
+        int wk = -1;
+        rc = exe_v<LW>(D, L, P, cs, cr, cq, E, wk) ? wk : -2;
+      }
+      if (rc == -2 && DGP_FAST && (cf & F_FAST) && !cex && cq <= 1) {  // the lean path (inlined: the common case)
         int wk = -1;
         rc = exe_fast<LW>(D, L, P, cs, cr, cq, E, wk) ? wk : -2;
       }

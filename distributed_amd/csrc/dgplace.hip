@@ -313,10 +313,10 @@ int sync_dev(dgp_engine* e) {
     const long long n = tn ? atoll(tn) : 20000;
     if (!e->D.trace || e->D.trace_n != n) {
       if (e->D.trace) (void)hipFree(e->D.trace);
-      HIPCHK(e, hipMalloc((void**)&e->D.trace, n * 8 * 8));
+      HIPCHK(e, hipMalloc((void**)&e->D.trace, n * 32 * 8));
     }
     e->D.trace_n = n;
-    HIPCHK(e, hipMemset(e->D.trace, 0, n * 8 * 8));
+    HIPCHK(e, hipMemset(e->D.trace, 0, n * 32 * 8));
   }
   dgp::Dev h[2] = {e->D, e->D};
   h[0].lds_workers = 0;
@@ -2529,7 +2529,7 @@ int dgp_set_timing(dgp_engine* e, int enabled) {
 
 extern "C" int dgp_debug_trace(dgp_engine* e, unsigned long long* out) {  // DGP_TRACE builds
   if (!e || !e->D.trace) return DGP_E_ARG;
-  HIPCHK(e, hipMemcpy(out, e->D.trace, e->D.trace_n * 8 * 8, hipMemcpyDeviceToHost));
+  HIPCHK(e, hipMemcpy(out, e->D.trace, e->D.trace_n * 32 * 8, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -57,7 +57,10 @@ class PlacementEngine:
         claims, libdgplace.so), 64 (no wait-in-place, libdgplace_w64.so) or "auto": chosen at
         ``load`` by ``auto_window`` (the unpacks' completions after a wide
         frontier are window-bound; the C2 chain needs wait-in-place)."""
+        if window not in (*_lib.WINDOWS, "auto"):
+            raise ValueError(f"window must be 32, 64 or 'auto', not {window!r}")
         self.window = window
+        self._configured = False  # set_timing / set_resident / ... ran: the handle may not be replaced
         self.lib = _lib.load(64 if window == 64 else 32)
         self.device = int(device)
         h = self.lib.dgp_create(int(device))
@@ -168,10 +171,15 @@ class PlacementEngine:
         return 32
 
     def _use_lib(self, window: int):
-        """A fresh engine on the build with that window (before anything was uploaded)."""
+        """A fresh engine on the build with that window (before anything was uploaded).
+        On an "auto" engine, ``load`` must therefore be the first call: anything configured
+        on the handle before it would be lost with the handle, so that raises."""
         lib = _lib.load(window)
         if lib is self.lib:
             return
+        if self._configured:
+            raise _lib.DgpError("load() must come first on an engine with window='auto': the handle was already "
+                                "configured (set_timing / set_resident / set_task_messages / enable_snapshots)")
         h = lib.dgp_create(self.device)
         if not h:
             raise _lib.DgpError(f"dgp_create({self.device}) failed: no HIP device visible (no CPU fallback)")
@@ -299,11 +307,13 @@ class PlacementEngine:
     def set_resident(self, on: bool = True):
         """Resident service mode (dgp_set_resident): the stream kernel stays launched between
         tasks_finished calls and takes each batch from a pinned mailbox."""
+        self._configured = True
         self._check(self.lib.dgp_set_resident(self.h, 1 if on else 0), "dgp_set_resident")
 
     def set_task_messages(self, on: bool = True):
         """Resident answers carry their placements' compute-task message fields
         (dgp_set_task_messages): task_messages of the last answer reads the mailbox."""
+        self._configured = True
         self._check(self.lib.dgp_set_task_messages(self.h, 1 if on else 0), "dgp_set_task_messages")
 
     def move_task(self, task: int, thief: int):
@@ -553,6 +563,7 @@ class PlacementEngine:
         return st
 
     def set_timing(self, on: bool = True):
+        self._configured = True
         self._check(self.lib.dgp_set_timing(self.h, 1 if on else 0), "dgp_set_timing")
 
     def stats(self) -> dict:

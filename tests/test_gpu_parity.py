@@ -131,3 +131,34 @@ def test_engine_full_c2(engine_cls):
         out = eng.placements()
     assert len(out["pl_task"]) == g["n_tasks"]
     assert_same(out, ref, PL_KEYS)
+
+
+@pytest.mark.parametrize("window", [32, 64])
+@pytest.mark.parametrize("name", ["c2mini_sat1.1.npz", "c2var_sat1.1.npz", "restr_sat1.1.npz", "c3mini_sat1.1.npz"])
+def test_both_window_builds_match_fixture(engine_cls, name, window):
+    """Each fixture on BOTH builds, forced (libdgplace.so: 32-slot window with wait-in-place
+    claims; libdgplace_w64.so: 64 slots, no wait-in-place): the auto choice runs restricted
+    graphs only on the 64-slot build and C2-shaped ones only on the 32-slot one, so each
+    build also runs the other's shapes here."""
+    g, cfg, exp, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
+    R = len(exp["round_nplaced"]) + 2
+    with engine_cls(0, window=window) as eng:
+        eng.load(g, cfg, snapshots=R)
+        eng.replay()
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+
+
+@pytest.mark.parametrize("window", [32, 64])
+def test_both_window_builds_match_oracle_c3_restricted(engine_cls, window):
+    from distributed_amd import graphs
+
+    g = graphs.shuffle_graph(6_000, 128, restricted=True)
+    cfg = {"bandwidth": 100_000_000, "default_data_size": 1024, "unknown_duration": 0.5, "saturation": 1.1}
+    ref = oracle.replay(g, cfg, snapshots=False)
+    with engine_cls(0, window=window) as eng:
+        eng.load(g, cfg)
+        eng.replay()
+        out = eng.placements()
+    assert_same(out, ref, PL_KEYS)

@@ -22,10 +22,10 @@ e.load(g, {"saturation": 1.1})
 e.reset()
 e.update_graph()
 e.run_rounds(-1)
-buf = np.zeros(n * 8, np.uint64)
+buf = np.zeros(n * 32, np.uint64)
 e.lib.dgp_debug_trace.argtypes = [C.c_void_p, C.c_void_p]
 assert e.lib.dgp_debug_trace(e.h, buf.ctypes.data_as(C.c_void_p)) == 0
-T = buf.reshape(n, 8).astype(np.int64)
+T = buf.reshape(n, 32).astype(np.int64)
 ok = (T[:, 0] > 0) & (T[:, 1] > 0) & (T[:, 2] > 0) & (T[:, 5] > 0) & (T[:, 6] > 0)
 T = T[ok]
 pred = T[:, 7] & 0xFFFF

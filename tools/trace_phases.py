@@ -20,10 +20,10 @@ e.load(g, {"saturation": 1.1})
 e.reset()
 e.update_graph()
 e.run_rounds(-1)
-buf = np.zeros(n * 8, np.uint64)
+buf = np.zeros(n * 32, np.uint64)
 e.lib.dgp_debug_trace.argtypes = [C.c_void_p, C.c_void_p]
 assert e.lib.dgp_debug_trace(e.h, buf.ctypes.data_as(C.c_void_p)) == 0
-T = buf.reshape(n, 8).astype(np.int64)
+T = buf.reshape(n, 32).astype(np.int64)
 T = T[(T[:, 2] > 0) & (T[:, 5] > 0) & (T[:, 0] > 0) & (T[:, 1] > 0) & (T[:, 3] > 0) & (T[:, 4] > 0) & (T[:, 6] > 0)]
 seq = [("claimed -> precheck", 2, 0), ("precheck -> state loaded", 0, 1), ("loaded -> completion needs", 1, 3),
        ("needs -> occupancy + releases", 3, 4), ("releases -> frontier done", 4, 6), ("frontier -> done", 6, 5),
