@@ -460,6 +460,29 @@ def c5_leg(eng_cls, local: int, args, dist, barrier) -> dict:
     return leg
 
 
+REF_PY_C2 = 22_615.0  # reference placement-only throughput at C2, 1 core
+
+
+def ref_python_summary(value):
+    """The committed timings of the reference's own Python (profiles/ref_python_*.json)."""
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+    out = {"baseline_md_placements_per_s": REF_PY_C2, "multiple_of_baseline_md": round(value / REF_PY_C2, 2)}
+    for cfg in ("c2", "c3", "c4"):
+        f = os.path.join(here, f"ref_python_{cfg}.json")
+        if not os.path.exists(f):
+            continue
+        r = json.load(open(f))
+        keep = {k: r[k] for k in ("placements", "placement_only_s", "replay_s", "balance_s", "steal_requests", "cores",
+                                  "python", "dask") if k in r}
+        if "placement_only_s" in r:
+            keep["placements_per_placement_only_s"] = round(r["placements"] / r["placement_only_s"], 1)
+        out[cfg] = keep
+    if "c2" in out and "placements_per_placement_only_s" in out["c2"]:
+        out["multiple_of_measured_c2"] = round(value / out["c2"]["placements_per_placement_only_s"], 2)
+    out["source"] = "tools/ref_python_time.py (build container, /root/reference under python3.9, 1 core)"
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -651,6 +674,12 @@ def main():
                                       "sample": f"oracle/replay.cpp, full C2 replay ({n_ref} placements) x {runs}"}
             result["parity"] = bool(all(np.array_equal(out[k], ref[k]) for k in (
                 "pl_task", "pl_worker", "pl_comm", "pl_start", "pl_wsnbytes", "pl_route")))
+        # the reference's own Python (22,615 placements/s placement-only, C2, one
+        # core) is the north_star's "reference CPU placement throughput": vs_baseline is the
+        # multiple of it; profiles/ref_python_*.json are this container's own timings of the
+        # reference (tools/ref_python_time.py: it never travels to the GPU box)
+        result["vs_baseline"] = round(value / REF_PY_C2, 2)
+        result["reference_python"] = ref_python_summary(value)
         if agree is not None:
             result["parity_all_ranks"] = agree
         if steal is not None:

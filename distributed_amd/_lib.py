@@ -46,6 +46,7 @@ SIGNATURES = {
     "dgp_tasks_finished_wait": (C.c_int, [_P, _P, _P]),
     "dgp_move_task": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "dgp_add_worker": (C.c_int, [_P, C.c_int32, _P]),
+    "dgp_add_worker_at": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, _P]),
     "dgp_add_graph": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P, _P]),
     "dgp_set_priorities": (C.c_int, [_P, _P]),
     "dgp_add_graph_deferred": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P]),
@@ -87,7 +88,7 @@ SIGNATURES = {
                                    _P, _P, _P]),
 }
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 _libs: dict = {}
 
 

@@ -4947,12 +4947,14 @@ __device__ long long refill_queue(const Dev& D, SCtl& S) {
 // len(processing) / nthreads over idle_task_count, lowest index on ties) ->
 // _add_to_processing (:3199-3215: add_to_processing, check_idle_saturated, n_tasks).
 // bulk_schedule_unrunnable_after_adding_worker has nothing to schedule on this path (no
-// restrictions: no task is no-worker). One wave; *placed = the placements made.
-__global__ void __launch_bounds__(64) k_add_worker(const Dev* __restrict__ Dp, long long* placed) {
+// restrictions: no task is no-worker). One wave; *placed = the placements made. The worker
+// is w (its index in address order; the host opened its rows). A worker that joins paused
+// (not in running, :4368-4369) is neither idle nor saturated nor in idle_task_count
+// (check_idle_saturated :2980-2995) and takes no refill (:4416).
+__global__ void __launch_bounds__(64) k_add_worker(const Dev* __restrict__ Dp, long long* placed, int w, int running) {
   const Dev& D = *Dp;
   __shared__ SCtl S;  // needs_inc reports inconsistencies through it
   const int lane = lane_id();
-  const int w = D.W - 1;
   if (lane == 0) {
     S.error = 0;
     S.err_task = -1;
@@ -4974,6 +4976,10 @@ __global__ void __launch_bounds__(64) k_add_worker(const Dev* __restrict__ Dp, l
   if (lane < NXW) D.gw_needs_ext[(size_t)w * NXW + lane] = 0;
   __threadfence();
   __syncthreads();
+  if (!running) {
+    if (lane == 0) D.w_flags[w] = WF_PAUSED;
+    return;
+  }
   if (lane == 0) {  // check_idle_saturated(ws): nothing processing -> idle; idle_task_count
     walk_flags(D, w, occupancy(D, w, D.pdur_walk), 0);
     itc_check(D, w, false);

@@ -194,6 +194,19 @@ int restride(dgp_engine* e, T** p, size_t rows, size_t w0, size_t w1, std::vecto
   return 0;
 }
 
+// open row `pos` of a [W0 + 1][row] device array whose rows 0..W0-1 are in use: rows
+// pos..W0-1 move up by one, row pos zero (a worker inserted at index pos)
+template <class T>
+int shift_rows(dgp_engine* e, T* p, size_t W0, size_t row, size_t pos) {
+  if (!p || pos >= W0) return 0;
+  std::vector<T> h((W0 + 1) * row);
+  HIPCHK(e, hipMemcpy(h.data(), p, h.size() * sizeof(T), hipMemcpyDeviceToHost));
+  std::memmove(h.data() + (pos + 1) * row, h.data() + pos * row, (W0 - pos) * row * sizeof(T));
+  std::fill(h.data() + pos * row, h.data() + (pos + 1) * row, T{});
+  HIPCHK(e, hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
 void free_list(std::vector<void*>& l) {
   for (void* p : l) (void)hipFree(p);
   l.clear();
@@ -1461,7 +1474,40 @@ int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief) {
   return check_device_error(e);
 }
 
+}  // extern "C"
+
+namespace {
+// a worker inserted at index pos: every worker index >= pos held per task moves up by one
+// (holder_of, processing_on) and each who_has bitset row gains a zero bit at pos
+__global__ void k_insert_worker_remap(int32_t* holder_of, int32_t* proc_on, unsigned long long* holders, int64_t N,
+                                      int32_t WB, int32_t pos) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < N; t += (int64_t)gridDim.x * blockDim.x) {
+    if (holder_of[t] >= pos) holder_of[t] += 1;
+    if (proc_on[t] >= pos) proc_on[t] += 1;
+    unsigned long long* row = holders + (size_t)t * WB;
+    const int k0 = pos >> 6, b0 = pos & 63;
+    const unsigned long long low = b0 ? ((1ull << b0) - 1) : 0ull;  // bits below pos stay
+    unsigned long long carry = 0;  // the top bit of the previous word, moving into this one
+    for (int k = k0; k < WB; k++) {
+      const unsigned long long v = row[k];
+      row[k] = k == k0 ? ((v & low) | ((v & ~low) << 1)) : ((v << 1) | carry);
+      carry = v >> 63;
+    }
+  }
+}
+__global__ void k_remap_range(int32_t* a, int64_t n, int32_t pos) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (a[i] >= pos) a[i] += 1;
+}
+}  // namespace
+
+extern "C" {
+
 int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
+  return dgp_add_worker_at(e, nthreads, 1, e ? e->D.W : 0, n_new_placements);
+}
+
+int dgp_add_worker_at(dgp_engine* e, int32_t nthreads, int32_t running, int32_t position, int64_t* n_new_placements) {
   if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
@@ -1472,15 +1518,22 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
                                 "has no worker addition");
   if (nthreads <= 0 || nthreads > 65535) return fail(e, DGP_E_ARG, "dgp_add_worker: nthreads out of range");
   if (e->D.W + 1 > 32768) return fail(e, DGP_E_ARG, "at most 32768 workers");
+  if (position < 0 || position > e->D.W) return fail(e, DGP_E_ARG, "dgp_add_worker_at: position out of range");
   {  // no-worker tasks would be rescheduled on the new worker (bulk_schedule_unrunnable_after_adding_worker)
     dgp::Ctl c;
     if (int rc = read_ctl(e, &c)) return rc;
     if (c.n_unrunnable > 0)
       return fail(e, DGP_E_STATE, "dgp_add_worker: no-worker tasks would be rescheduled (not modelled)");
   }
-  e->paused_h.push_back(0);
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (position < e->D.W) {  // the stream positions must be settled: no descriptor or record waits with old indices
+    dgp::st::Pos ps;
+    HIPCHK(e, hipMemcpy(&ps, e->D.pos, sizeof ps, hipMemcpyDeviceToHost));
+    if (ps.pre > ps.seq || ps.walk != ps.rec_len)
+      return fail(e, DGP_E_STATE, "dgp_add_worker_at: the stream engine has prefetched stimuli or unfolded records");
+  }
+  e->paused_h.insert(e->paused_h.begin() + position, (uint8_t)(running ? 0 : 1));
   namespace S = dgp::st;
   dgp::Dev& D = e->D;
   const size_t W0 = D.W, W1 = W0 + 1;
@@ -1531,11 +1584,80 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
   D.W = (int32_t)W1;
   D.WB = WB;
   D.Wp = Wp;
-  e->nthreads.push_back(nthreads);
+  const size_t pos = (size_t)position;
+  if (pos < W0) {
+    // Scheduler.workers is a SortedDict by address (:3746, inserted at :4353) and the canonical
+    // worker order is its order: the new worker takes index pos, every later one moves up
+    rc |= shift_rows(e, D.w_nthreads, W0, 1, pos);
+    rc |= shift_rows(e, D.w_cap, W0, 1, pos);
+    rc |= shift_rows(e, D.w_nproc, W0, 1, pos);
+    rc |= shift_rows(e, D.w_plen, W0, 1, pos);
+    rc |= shift_rows(e, D.w_pfx, W0, dgp::PMAX, pos);
+    rc |= shift_rows(e, D.w_pcnt, W0, dgp::PMAX, pos);
+    rc |= shift_rows(e, D.w_netocc, W0, 1, pos);
+    rc |= shift_rows(e, D.w_nbytes, W0, 1, pos);
+    rc |= shift_rows(e, D.w_flags, W0, 1, pos);
+    rc |= shift_rows(e, D.w_itcslots, W0, 1, pos);
+    rc |= shift_rows(e, D.w_lastcheck, W0, 1, pos);
+    rc |= shift_rows(e, D.w_needs, W0, dgp::NEEDS_W, pos);
+    rc |= shift_rows(e, D.gw_nproc, W0, 1, pos);
+    rc |= shift_rows(e, D.gw_nthreads, W0, 1, pos);
+    rc |= shift_rows(e, D.gw_cap, W0, 1, pos);
+    rc |= shift_rows(e, D.gw_plen, W0, 1, pos);
+    rc |= shift_rows(e, D.gw_pcnt, W0, S::PD, pos);
+    rc |= shift_rows(e, D.gw_netocc, W0, 1, pos);
+    rc |= shift_rows(e, D.gw_nbytes, W0, 1, pos);
+    rc |= shift_rows(e, D.gw_mask, W0, 1, pos);
+    rc |= shift_rows(e, D.gw_needs, W0, S::NLW, pos);
+    rc |= shift_rows(e, D.gw_wflags, W0, 1, pos);
+    rc |= shift_rows(e, D.gw_needs_ext, W0, S::NXW, pos);
+    rc |= shift_rows(e, D.gw_needs_saved, W0, S::NLW, pos);
+    if (rc) return rc;
+    // worker indices held per task: holder_of, processing_on, the who_has bitsets
+    hipLaunchKernelGGL(k_insert_worker_remap, dim3((unsigned)std::min<int64_t>((D.N + 255) / 256, 4096)), dim3(256), 0,
+                       e->stream, D.holder_of, D.proc_on, D.holders, (int64_t)D.N, WB, (int32_t)pos);
+    HIPCHK(e, hipGetLastError());
+    {  // placements the stream engine has not sequenced carry their worker into holder_of at its start
+      dgp::st::Pos ps;
+      dgp::Ctl c0;
+      HIPCHK(e, hipMemcpy(&ps, D.pos, sizeof ps, hipMemcpyDeviceToHost));
+      if (int rc2 = read_ctl(e, &c0)) return rc2;
+      const int64_t a = ps.runid_upto, b = (int64_t)c0.n_placed;
+      if (b > a)
+        hipLaunchKernelGGL(k_remap_range, dim3(64), dim3(256), 0, e->stream, D.pl_worker + a, b - a, (int32_t)pos);
+      HIPCHK(e, hipGetLastError());
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    // the groups' last_worker and the restriction rows (valid workers stay ascending)
+    auto remap_host = [&](int32_t* dptr, size_t n) -> int {
+      if (!dptr || !n) return 0;
+      std::vector<int32_t> h(n);
+      HIPCHK(e, hipMemcpy(h.data(), dptr, n * 4, hipMemcpyDeviceToHost));
+      for (auto& v : h) v += v >= (int32_t)pos ? 1 : 0;
+      HIPCHK(e, hipMemcpy(dptr, h.data(), n * 4, hipMemcpyHostToDevice));
+      return 0;
+    };
+    if (int rc2 = remap_host(D.g_lastw, (size_t)D.G)) return rc2;
+    if (D.restr_ptr) {
+      int64_t K = 0;
+      HIPCHK(e, hipMemcpy(&K, D.restr_ptr + D.N, 8, hipMemcpyDeviceToHost));
+      if (int rc2 = remap_host(const_cast<int32_t*>(D.restr_idx), (size_t)K)) return rc2;
+    }
+    if (D.restr_pool && e->rpool_used) {  // rows [len, workers...]: only the workers move
+      std::vector<int32_t> h((size_t)e->rpool_used);
+      HIPCHK(e, hipMemcpy(h.data(), D.restr_pool, h.size() * 4, hipMemcpyDeviceToHost));
+      for (size_t q = 0; q < h.size();) {
+        const int32_t len = h[q++];
+        for (int32_t i = 0; i < len; i++, q++) h[q] += h[q] >= (int32_t)pos ? 1 : 0;
+      }
+      HIPCHK(e, hipMemcpy(const_cast<int32_t*>(D.restr_pool), h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    }
+  }
+  e->nthreads.insert(e->nthreads.begin() + pos, nthreads);
   D.total_nthreads += nthreads;
   const int32_t cap = D.sat_inf ? 0 : std::max((int32_t)std::ceil(D.saturation * nthreads), (int32_t)1);
-  HIPCHK(e, hipMemcpy(D.w_nthreads + W0, &nthreads, 4, hipMemcpyHostToDevice));
-  HIPCHK(e, hipMemcpy(D.w_cap + W0, &cap, 4, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_nthreads + pos, &nthreads, 4, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.w_cap + pos, &cap, 4, hipMemcpyHostToDevice));
   // is_rootish (:2929-2947) reads total_nthreads: the groups' flags follow the new total
   {
     std::vector<uint8_t> tf = e->tflags_h;
@@ -1556,7 +1678,10 @@ int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements) {
   e->mode = 2;
   if (int rc2 = grow_logs(e, 0)) return rc2;
   if (int rc2 = sync_dev(e)) return rc2;
-  hipLaunchKernelGGL(dgp::st::k_add_worker, dim3(1), dim3(64), 0, e->stream, e->d_dev, e->d_aux + 3);
+  if (!running) D.evf |= dgp::EVF_PAUSED;
+  if (int rc2 = sync_dev(e)) return rc2;
+  hipLaunchKernelGGL(dgp::st::k_add_worker, dim3(1), dim3(64), 0, e->stream, e->d_dev, e->d_aux + 3, (int32_t)pos,
+                     running ? 1 : 0);
   HIPCHK(e, hipGetLastError());
   long long placed = 0;
   HIPCHK(e, hipMemcpyAsync(&placed, e->d_aux + 3, sizeof placed, hipMemcpyDeviceToHost, e->stream));

@@ -321,12 +321,16 @@ class PlacementEngine:
         :376-384): processing ``task`` moves from its worker to ``thief`` on the device."""
         self._check(self.lib.dgp_move_task(self.h, int(task), int(thief)), "dgp_move_task")
 
-    def add_worker(self, nthreads: int) -> int:
-        """A worker joins (Scheduler.add_worker, distributed/scheduler.py:4308-4441) with
-        index ``n_workers``: check_idle_saturated and the queue refill on the device.
-        Returns the number of placements the refill made."""
+    def add_worker(self, nthreads: int, *, running: bool = True, position: int | None = None) -> int:
+        """A worker joins (Scheduler.add_worker, distributed/scheduler.py:4308-4441):
+        check_idle_saturated and the queue refill on the device. ``position``: its index in
+        the address order of the engine's workers (default: after all of them); every later
+        worker's index moves up by one (dgp_add_worker_at). ``running`` False: it joins
+        paused (no refill). Returns the number of placements the refill made."""
         newp = C.c_int64(0)
-        self._check(self.lib.dgp_add_worker(self.h, int(nthreads), C.byref(newp)), "dgp_add_worker")
+        pos = self.n_workers if position is None else int(position)
+        self._check(self.lib.dgp_add_worker_at(self.h, int(nthreads), 1 if running else 0, pos, C.byref(newp)),
+                    "dgp_add_worker_at")
         self.n_workers += 1
         return int(newp.value)
 

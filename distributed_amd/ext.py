@@ -47,6 +47,7 @@ computes the reference decision for every placement and raises on any difference
 from __future__ import annotations
 
 import asyncio
+import bisect
 import functools
 import inspect
 import logging
@@ -75,6 +76,9 @@ _STIMULUS_TRANSITIONS = frozenset({
 _UPDATE_GRAPH_TRANSITIONS = frozenset({
     ("released", "waiting"), ("waiting", "processing"), ("waiting", "queued"), ("waiting", "no-worker")})
 _ADD_WORKER_TRANSITIONS = frozenset({("queued", "processing")})
+# a removed worker keeps its engine index under this suffix: it sorts right after its address
+# (no address has a NUL), so the list stays in address order if the address joins again
+_REMOVED = "\x00removed"
 # stimulus_queue_slots_maybe_opened after long-running / a worker running again (:4983-5023)
 _REFILL_TRANSITIONS = _ADD_WORKER_TRANSITIONS
 # task-erred (:5094-5127, :2630-2720): the task erred, its waiting dependents released then
@@ -1028,8 +1032,8 @@ class GPUPlacementExtension(SchedulerPlugin):
         engine, dgp_set_priorities) is appended without placing and its stimulus is the
         scheduler's own, the engine resynchronised after it (``_suspend``)."""
         s = self.scheduler
-        g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers], s.valid_workers,
-                                    self.worker_index, earlier=self.task_index)
+        g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads if a in s.workers else 1 for a in self.workers],
+                                    s.valid_workers, self.worker_index, earlier=self.task_index)
         restricted = "restr_flags" in g  # its stimulus the scheduler's, then the rows (dgp_update_restrictions)
         # a user priority that outranks earlier tasks (_set_priorities :4934-4981): the engine
         # takes every task's rank in the merged order (dgp_set_priorities) and the stimulus is
@@ -1090,26 +1094,34 @@ class GPUPlacementExtension(SchedulerPlugin):
         after check_idle_saturated(ws) and before bulk_schedule_unrunnable_after_adding_worker /
         stimulus_queue_slots_maybe_opened (scheduler.py:4398-4420). The engine adds the worker
         and makes the queue refill; the scheduler's own refill then consumes those decisions.
-        The engine's worker index order must stay the scheduler's (SortedDict address) order,
-        so only a worker whose address sorts after every known one joins on the device."""
+        The engine's worker index order is the scheduler's (SortedDict by address, :3746,
+        :4353): the worker takes its address's place and every later index moves up by one on
+        the device (dgp_add_worker_at); a worker that joins paused takes no refill."""
         self._enter()
         if not self.active or self.engine is None or worker in self.worker_index:
-            return
-        if self.workers and worker < max(self.workers):
-            self.fallback(f"add_worker({worker}): its address sorts before a known worker's")
             return
         s = self.scheduler
         try:
             self._end_of_stimulus("the previous stimulus")
             if not self.active:
                 return
-            if s.workers[worker].status.name != "running":
-                raise NotImplementedError("a worker that joins paused")
-            self.engine.add_worker(int(s.workers[worker].nthreads))
-            self.worker_index[worker] = len(self.workers)
-            self.workers.append(worker)
+            ws = s.workers[worker]
+            running = ws.status.name == "running"
+            # the engine's workers in address order (a removed one keeps its place, under a
+            # name that sorts right after its address)
+            pos = bisect.bisect_left(self.workers, worker)
+            self.engine.add_worker(int(ws.nthreads), running=running, position=pos)
+            self.workers.insert(pos, worker)
+            if pos < len(self.workers) - 1:  # later workers moved up by one
+                self.worker_index = {a: i for i, a in enumerate(self.workers) if not a.endswith(_REMOVED)}
+                self._restr_h = {k: (fl, tuple(v + (v >= pos) for v in row)) for k, (fl, row) in self._restr_h.items()}
+                self.stats["workers_inserted"] += 1
+            else:
+                self.worker_index[worker] = pos
             self._fetch()
             self.stats["workers_added"] += 1
+            if not running:
+                self.stats["workers_added_paused"] += 1
             self._window = (_ADD_WORKER_TRANSITIONS, None)
         except Exception as e:
             self.fallback(f"add_worker({worker}): {e}")
@@ -1131,6 +1143,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         on_device = not self.suspended
         w = self.worker_index.pop(worker)
         self.removed.add(worker)
+        self.workers[w] = worker + _REMOVED  # keeps its index and its place in address order
         try:
             self.engine.remove_worker(w)
         except Exception as e:

@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 15
+#define DGP_ABI_VERSION 16
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -226,6 +226,19 @@ int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief);
  * task is no-worker (bulk_schedule_unrunnable_after_adding_worker :3173-3186 is not modelled).
  * Snapshots taken earlier read 0 for the new worker. */
 int dgp_add_worker(dgp_engine* e, int32_t nthreads, int64_t* n_new_placements);
+/* dgp_add_worker_at: Scheduler.add_worker (scheduler.py:4308-4441) for a worker whose address
+ * sorts anywhere among the known ones: SchedulerState.workers is a SortedDict keyed by address
+ * (:3746, the insertion :4353) and the engine's worker index is that order (the canonical
+ * tie-break and the no-dependency round robin over workers.values(), :2286-2305). The new
+ * worker takes index `position` (the number of engine workers, removed ones included, whose
+ * address sorts before it); every worker index >= position held by the engine -- per-worker
+ * state, holder_of / processing_on, who_has bitset columns, restriction rows, the groups'
+ * last_worker -- moves up by one on the device. `running` 0: the worker joins paused (status
+ * paused, :4368-4369): total_nthreads grows, it is neither running, idle, saturated nor in
+ * idle_task_count, and no queue refill follows (:4416). dgp_add_worker(e, n, p) ==
+ * dgp_add_worker_at(e, n, 1, W, p). Needs the stream engine settled (no stimulus prefetched
+ * beyond the sequenced ones): true between service calls. */
+int dgp_add_worker_at(dgp_engine* e, int32_t nthreads, int32_t running, int32_t position, int64_t* n_new_placements);
 
 /* A later graph submission (Scheduler.update_graph, scheduler.py:4662-4751 ->
  * _create_taskstate_from_graph :4512-4653) on a running engine, service mode: n_new tasks

@@ -65,6 +65,7 @@ class FixtureEngine:
         self._posted = None
         self.t_window = 0.0
         self.windows = []
+        self.joins = []  # add_worker calls: (nthreads, running, position)
 
     def load(self, g, config, results=True):
         self.graph, self.config = g, config
@@ -158,8 +159,11 @@ class FixtureEngine:
             return 0
         return self.add_worker(0)
 
-    def add_worker(self, nthreads):  # a join (the fixture's per-event placement counts)
+    def add_worker(self, nthreads, running=True, position=None):  # a join (the fixture's per-event placement counts)
         assert self._posted is None, "add_worker while a batch is posted"
+        self.joins.append((int(nthreads), bool(running), position))
+        if position is not None:  # dgp_add_worker_at: every later worker index moves up by one
+            self.who = {t: {w + (w >= position) for w in ws} for t, ws in self.who.items()}
         k = self.stim[self.k]
         self.n += k
         self.k += 1
@@ -555,7 +559,10 @@ def run_joins(name):
     (scheduler.py:4370-4420: workers / running / total_nthreads, check_idle_saturated, the
     plugins' add_worker hook, bulk_schedule_unrunnable_after_adding_worker,
     stimulus_queue_slots_maybe_opened); the extension's hook adds the worker to the engine
-    and its queue refill decisions are the ones the scheduler then takes."""
+    and its queue refill decisions are the ones the scheduler then takes. ``svcaddw_order_*``:
+    the addresses sort among the known ones (the extension must insert each at its SortedDict
+    place, dgp_add_worker_at) and some join paused, resuming later through the scheduler's
+    worker-status-change handler."""
     from distributed.core import Status
     from distributed.scheduler import WorkerState
 
@@ -567,17 +574,21 @@ def run_joins(name):
     sat = float("inf") if sat == "inf" else float(sat)
     dask.config.set({"distributed.scheduler.worker-saturation": sat})
     cfg = dict(cfg, saturation=sat)
-    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    step = int(z["addr_step"]) if "addr_step" in z.files else 0
+    s, tss, widx, rec, tidx = G.build_state(g, cfg, (lambda i: f"tcp://w{step * i:07d}:1") if step else None)
     S = type(s)
     S.stimulus_task_finished = Scheduler.stimulus_task_finished
     S.handle_task_finished = Scheduler.handle_task_finished
+    S.handle_worker_status_change = Scheduler.handle_worker_status_change
     S.validate_key = lambda self, key, ts=None: None
     S.send_all = lambda self, client_msgs, worker_msgs: None
+    s.extensions = {}
     fkeys = [ts.key for ts in tss]
-    eng = FixtureEngine(exp, fkeys)
+    eng = EventEngine(exp, fkeys)
+    eng.joins = []
     ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
     eng.ext = ext
-    s.stream_handlers = {}
+    s.stream_handlers = {"worker-status-change": s.handle_worker_status_change}
     ext._install()
     priority = {ts.key: ts.priority for ts in tss}
     recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
@@ -586,37 +597,62 @@ def run_joins(name):
     assert ext.active, ext.reason
     s._transitions(recs, {}, {}, "update-graph")
     W0 = len(g["nthreads"])
-    joins = dict(zip(z["add_msg"].tolist(), z["add_nthreads"].tolist()))
-    k_join = 0
+    joins = {}
+    n_add = len(z["add_nthreads"])
+    addrs = z["add_addr"].tolist() if "add_addr" in z.files else [f"tcp://w{W0 + k:05d}:1" for k in range(n_add)]
+    running = z["add_running"].tolist() if "add_running" in z.files else [1] * n_add
+    pos = z["add_pos"].tolist() if "add_pos" in z.files else [W0 + k for k in range(n_add)]
+    for k, (i, nt) in enumerate(zip(z["add_msg"].tolist(), z["add_nthreads"].tolist())):
+        joins.setdefault(i, []).append(k)
+    resumes = {}
+    for i, w in zip(*((z["res_msg"].tolist(), z["res_worker"].tolist()) if "res_msg" in z.files else ((), ()))):
+        resumes.setdefault(i, []).append(w)
+    k_join = n_res = 0
     for i, (t, w) in enumerate(zip(z["msg_task"].tolist(), z["msg_worker"].tolist())):
-        if i in joins:
-            addr = f"tcp://w{W0 + k_join:05d}:1"
-            widx[addr] = W0 + k_join
-            ws = WorkerState(address=addr, status=Status.running, pid=0, name=addr, nthreads=joins[i],
-                             memory_limit=0, local_directory="", nanny=None, server_id=addr, scheduler=s)
+        for k in joins.get(i, ()):
+            addr = addrs[k]
+            run_ = bool(running[k])
+            ws = WorkerState(address=addr, status=Status.running if run_ else Status.paused, pid=0, name=addr,
+                             nthreads=int(z["add_nthreads"][k]), memory_limit=0, local_directory="", nanny=None,
+                             server_id=addr, scheduler=s)
             s.workers[addr] = ws
-            s.running.add(ws)
+            for r_, a in enumerate(s.workers):  # the canonical index is the SortedDict rank
+                widx[a] = r_
+            assert widx[addr] == pos[k], (addr, widx[addr], pos[k])
+            if run_:
+                s.running.add(ws)
             s.aliases[addr] = addr
             s.total_nthreads += ws.nthreads
             s.check_idle_saturated(ws)
             ext.add_worker(scheduler=s, worker=addr)
-            s.transitions(s.bulk_schedule_unrunnable_after_adding_worker(ws), f"add-{addr}")
-            s.stimulus_queue_slots_maybe_opened(stimulus_id=f"add-{addr}")
+            assert ext.worker_index[addr] == pos[k] and eng.joins[-1] == (ws.nthreads, run_, pos[k]), \
+                (ext.worker_index.get(addr), eng.joins[-1], pos[k])
+            if run_:
+                s.transitions(s.bulk_schedule_unrunnable_after_adding_worker(ws), f"add-{addr}")
+                s.stimulus_queue_slots_maybe_opened(stimulus_id=f"add-{addr}")
             k_join += 1
+        for w_ in resumes.get(i, ()):  # a paused joiner resumes: the scheduler's own stream handler
+            a = next(x for x, r_ in widx.items() if r_ == w_ and x in s.workers)
+            s.stream_handlers["worker-status-change"](status="running", worker=a, stimulus_id=f"resume-{a}")
+            assert eng.calls[-1] == ("status", w_, 1), eng.calls[-1:]
+            n_res += 1
         ts = tss[t]
+        assert widx[ts.processing_on.address] == w  # the message's worker index is the SortedDict rank
         s.stream_handlers["task-finished"](
             key=ts.key, worker=ts.processing_on.address, stimulus_id=f"tf-{t}", run_id=ts.run_id,
             nbytes=int(g["nbytes"][t]), type=None, typename="int", metadata=None,
             startstops=[{"action": "compute", "start": float(g["start"][t]), "stop": float(g["stop"][t])}])
     ext._end_of_stimulus("end of stream")
     assert ext.active, ext.reason
-    assert k_join == len(joins)
+    assert k_join == n_add
+    assert ext.workers == sorted(s.workers), "the engine's worker order is the SortedDict's"
     n = len(exp["pl_task"])
     assert rec["task"] == exp["pl_task"].tolist()
     assert rec["worker"] == exp["pl_worker"].tolist()
     assert np.array_equal(np.array(rec["start"]).view(np.int64), exp["pl_start"].view(np.int64))
     assert ext.stats["device_decisions"] == n, (ext.stats, n)
-    return dict(fixture=name, placements=n, joins=k_join, workers_added=ext.stats["workers_added"],
+    return dict(fixture=name, placements=n, joins=k_join, resumes=n_res, workers_added=ext.stats["workers_added"],
+                workers_inserted=ext.stats["workers_inserted"], workers_added_paused=ext.stats["workers_added_paused"],
                 device_decisions=ext.stats["device_decisions"], active=ext.active, reason=ext.reason)
 
 

@@ -89,8 +89,11 @@ def make_keys(g):
     return keys
 
 
-def build_state(g, cfg):
-    """Create the reference SchedulerState for graph ``g`` (no transitions yet)."""
+def build_state(g, cfg, addr_of=None):
+    """Create the reference SchedulerState for graph ``g`` (no transitions yet). ``addr_of``:
+    worker index -> address (default ``tcp://w{i:05d}:1``; any form whose order is the index
+    order)."""
+    addr_of = addr_of or (lambda i: f"tcp://w{i:05d}:1")
     from sortedcontainers import SortedDict
 
     from distributed.collections import HeapSet
@@ -159,7 +162,7 @@ def build_state(g, cfg):
     s.saturated = IdxSet()
     assert s.bandwidth == cfg["bandwidth"]
     for i in range(W):
-        addr = f"tcp://w{i:05d}:1"
+        addr = addr_of(i)
         widx[addr] = i
         ws = WorkerState(address=addr, status=Status.running, pid=0, name=addr,
                          nthreads=int(g["nthreads"][i]), memory_limit=0, local_directory="",
@@ -193,7 +196,7 @@ def build_state(g, cfg):
         rp, ri, rf = g["restr_ptr"], g["restr_idx"], g["restr_flags"]
         for t, ts in enumerate(tss):
             if rf[t] & 1:
-                valid = {f"tcp://w{int(w):05d}:1" for w in ri[rp[t]:rp[t + 1]]}
+                valid = {addr_of(int(w)) for w in ri[rp[t]:rp[t + 1]]}
                 # a name no worker has: valid_workers drops it (:3059), so an otherwise
                 # empty set is still a restriction, with no valid worker
                 ts.worker_restrictions = valid | {"tcp://gone:1"}

@@ -195,43 +195,66 @@ def replay_service(g, cfg, seed, p_inject=0.35, p_steal=0.0):
     return rec, rounds, nplaced, states, msgs, round_ptr, steals
 
 
-def replay_add_workers(g, cfg, seed, n_add, max_nthreads=4):
+def replay_add_workers(g, cfg, seed, n_add, max_nthreads=4, interleave=False, n_paused=0):
     """The replay protocol's completions as task-finished messages, with ``n_add`` workers
     joining at random points of the first half of the stream, exactly as
     ``Scheduler.add_worker`` (distributed/scheduler.py:4308-4441) changes the placement
-    state: the WorkerState enters ``workers`` / ``running`` (addresses sort after the
-    existing ones, so the new worker's index is the next one), ``total_nthreads`` grows
-    (:4383), ``check_idle_saturated(ws)`` (:4398), then
+    state: the WorkerState enters ``workers`` (a SortedDict by address, :3746, :4353) /
+    ``running``, ``total_nthreads`` grows (:4383), ``check_idle_saturated(ws)`` (:4398), then
     ``bulk_schedule_unrunnable_after_adding_worker`` and ``stimulus_queue_slots_maybe_opened``
-    (:4416-4420). Stored: ``add_msg`` (the message index each addition precedes) and
-    ``add_nthreads``; snapshots are as wide as the final worker count (0 for workers not
-    yet added)."""
+    (:4416-4420). Addresses sort after the existing ones (the new worker's index is the next
+    one), or with ``interleave`` anywhere among them: the canonical worker index is always
+    the SortedDict rank, so every later worker's index moves up by one at such a join.
+    ``n_paused`` of the joining workers join paused (status paused: not running, no refill,
+    :4368-4369, :4416) and resume later through ``Scheduler.handle_worker_status_change``
+    (:5850-5883). Stored: ``add_msg`` (the message index each addition precedes),
+    ``add_nthreads``, ``add_pos`` (its index at the join), ``add_running``; ``res_msg`` /
+    ``res_worker`` (the resumes: message index, the worker's index then); messages, placements
+    and snapshots carry the index of their time; snapshots are as wide as the final worker
+    count (0 for workers not yet added)."""
     from distributed.core import Status
     from distributed.scheduler import Scheduler, WorkerState
 
-    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    addr_of = (lambda i: f"tcp://w{100 * i:07d}:1") if interleave else None
+    s, tss, widx, rec, tidx = G.build_state(g, cfg, addr_of)
     W0 = len(g["nthreads"])
     W = W0 + n_add
     N = g["n_tasks"]
     rng = np.random.default_rng(seed)
     type(s).stimulus_task_finished = Scheduler.stimulus_task_finished
+    type(s).handle_worker_status_change = Scheduler.handle_worker_status_change
+    type(s).send_all = lambda self, client_msgs, worker_msgs: None
+    s.extensions = {}
     add_at = sorted(int(x) for x in rng.choice(N // 2, n_add, replace=False))
     add_nt = [int(x) for x in rng.integers(1, max_nthreads + 1, n_add)]
-    added = {"msg": [], "nthreads": []}
+    add_near = [int(x) for x in rng.integers(0, W0, n_add)]  # interleave: the address follows worker j's
+    paused_k = set(int(x) for x in rng.choice(n_add, n_paused, replace=False)) if n_paused else set()
+    added = {"msg": [], "nthreads": [], "pos": [], "running": [], "addr": []}
+    resumes = {"msg": [], "worker": []}
+    res_at = {}  # message index -> address to resume
 
-    def add_worker(i, nthreads):
-        addr = f"tcp://w{i:05d}:1"
-        widx[addr] = i
-        ws = WorkerState(address=addr, status=Status.running, pid=0, name=addr, nthreads=nthreads, memory_limit=0,
-                         local_directory="", nanny=None, server_id=addr, scheduler=s)
+    def add_worker(k, nthreads):
+        addr = f"tcp://w{100 * add_near[k] + 1 + k:07d}:1" if interleave else f"tcp://w{W0 + k:05d}:1"
+        running = k not in paused_k
+        ws = WorkerState(address=addr, status=Status.running if running else Status.paused, pid=0, name=addr,
+                         nthreads=nthreads, memory_limit=0, local_directory="", nanny=None, server_id=addr,
+                         scheduler=s)
         s.workers[addr] = ws
-        s.running.add(ws)
+        for i, a in enumerate(s.workers):  # the SortedDict rank is the canonical index
+            widx[a] = i
+        if running:
+            s.running.add(ws)
         s.aliases[addr] = addr
         s.total_nthreads += nthreads
         s.check_idle_saturated(ws)
-        sid = f"add-worker-{i}"
-        s.transitions(s.bulk_schedule_unrunnable_after_adding_worker(ws), sid)
-        s.stimulus_queue_slots_maybe_opened(stimulus_id=sid)
+        sid = f"add-worker-{k}"
+        if running:
+            s.transitions(s.bulk_schedule_unrunnable_after_adding_worker(ws), sid)
+            s.stimulus_queue_slots_maybe_opened(stimulus_id=sid)
+        else:  # resumes somewhere in the rest of the stream
+            res_at.setdefault(int(rng.integers(len(msgs["task"]) + 1, N)), []).append(addr)
+        added["addr"].append(addr)
+        return widx[addr], running
 
     recs = {}
     for ts in sorted(tss, key=lambda t: t.priority, reverse=True):
@@ -256,9 +279,17 @@ def replay_add_workers(g, cfg, seed, n_add, max_nthreads=4):
                 added["msg"].append(len(msgs["task"]))
                 added["nthreads"].append(add_nt[k_add])
                 n0 = len(rec["task"])
-                add_worker(W0 + k_add, add_nt[k_add])
+                p, running = add_worker(k_add, add_nt[k_add])
+                added["pos"].append(p)
+                added["running"].append(int(running))
                 stim.append(len(rec["task"]) - n0)
                 k_add += 1
+            for a in res_at.pop(len(msgs["task"]), ()):
+                resumes["msg"].append(len(msgs["task"]))
+                resumes["worker"].append(widx[a])
+                n0 = len(rec["task"])
+                s.handle_worker_status_change("running", a, f"resume-{a}")
+                stim.append(len(rec["task"]) - n0)
             t = rec["task"][pos]
             ts = tss[t]
             assert ts.state == "processing", (ts.key, ts.state)
@@ -278,8 +309,10 @@ def replay_add_workers(g, cfg, seed, n_add, max_nthreads=4):
                 msgs[k].append(v)
         round_ptr.append(len(msgs["task"]))
     assert k_add == n_add, (k_add, n_add)
+    assert not res_at or min(res_at) >= len(msgs["task"]), res_at  # resumes past the stream's end are dropped
     rec["stim"] = stim
     states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
+    added["resumes"] = resumes
     return rec, rounds, nplaced, states, msgs, round_ptr, added
 
 
@@ -302,15 +335,24 @@ def main_add_workers(only):
                                                             0.3, seed=25, empty_frac=0.0), 1.1, 9, 24),
         "svcaddw_p16_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=26, n_inner_prefixes=15,
                                                             random_durations=True, nthreads="random"), 1.1, 10, 24),
+        # addresses that sort among the known ones (a real cluster's tcp://host:<port>): every
+        # later worker's canonical index moves up at each join; 4 of them join paused and
+        # resume later
+        "svcaddw_order_sat1.1": (lambda: G.graphs.random_dag(4000, 40, seed=27, n_inner_prefixes=3,
+                                                              random_durations=True, nthreads="random"), 1.1, 11, 24,
+                                 dict(interleave=True, n_paused=4)),
+        "svcaddw_order_satinf": (lambda: G.graphs.random_dag(3000, 32, seed=28), float("inf"), 12, 16,
+                                 dict(interleave=True, n_paused=3)),
     }
-    for name, (mk, sat, seed, n_add) in cases.items():
+    for name, (mk, sat, seed, n_add, *kw) in cases.items():
         if only and name not in only:
             continue
         g = mk()
         G.graphs.check_graph(g)
         dask.config.set({"distributed.scheduler.worker-saturation": sat})
         cfg = G.config_dict(sat)
-        rec, rounds, nplaced, states, msgs, round_ptr, added = replay_add_workers(g, cfg, seed, n_add)
+        rec, rounds, nplaced, states, msgs, round_ptr, added = replay_add_workers(g, cfg, seed, n_add,
+                                                                                 **(kw[0] if kw else {}))
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -318,7 +360,12 @@ def main_add_workers(only):
                  msg_runid=np.array(msgs["run_id"], np.int64), msg_nbytes=np.array(msgs["nbytes"], np.int64),
                  msg_start=np.array(msgs["start"]), msg_stop=np.array(msgs["stop"]),
                  msg_status=np.array(msgs["status"], np.int8), msg_round_ptr=np.array(round_ptr, np.int64),
-                 add_msg=np.array(added["msg"], np.int64), add_nthreads=np.array(added["nthreads"], np.int32))
+                 add_msg=np.array(added["msg"], np.int64), add_nthreads=np.array(added["nthreads"], np.int32),
+                 add_pos=np.array(added["pos"], np.int32), add_running=np.array(added["running"], np.int8),
+                 res_msg=np.array(added["resumes"]["msg"], np.int64),
+                 res_worker=np.array(added["resumes"]["worker"], np.int32),
+                 add_addr=np.array(added["addr"], dtype="U32"),
+                 addr_step=np.array(100 if (kw and kw[0].get("interleave")) else 0, np.int32))
         np.savez_compressed(path, **z)
         routes = np.bincount(np.array(rec["route"]), minlength=4).tolist()
         print(f"{name}: {len(msgs['task'])} messages, {len(added['msg'])} workers added, routes {routes}")

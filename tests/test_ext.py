@@ -83,6 +83,19 @@ def test_extension_follows_workers_joining():
         assert r["workers_added"] == r["joins"] > 0, r
 
 
+def test_extension_follows_workers_joining_in_address_order():
+    """Workers join at addresses that sort among the known ones (SortedDict order, scheduler.py
+    :3746 / :4353) and some join paused, resuming later: the extension inserts each at its
+    place (dgp_add_worker_at, every later index moves up) and stays active; every decision
+    is the engine's and validate=True agrees."""
+    names = ["svcaddw_order_sat1.1.npz", "svcaddw_order_satinf.npz"]
+    res = drive(names)
+    for r in res:
+        assert r["active"] and r["device_decisions"] == r["placements"], r
+        assert r["workers_added"] == r["joins"] > 0 and r["workers_inserted"] > 0, r
+        assert r["workers_added_paused"] > 0 and r["resumes"] > 0, r
+
+
 def test_extension_follows_a_second_graph():
     """A second, independent graph submitted to the running scheduler: the plugin hook
     appends it to the engine (dgp_add_graph); every decision still comes from the engine."""

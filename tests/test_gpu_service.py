@@ -308,7 +308,9 @@ def test_move_task_rejects_a_task_not_processing():
 @pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])
 @pytest.mark.parametrize("name", svc_add_worker_files())
 def test_service_with_workers_joining(name, per_message):
-    """Workers join a running engine (dgp_add_worker) between task-finished messages."""
+    """Workers join a running engine (dgp_add_worker_at) between task-finished messages; in
+    the svcaddw_order_* fixtures at addresses that sort among the known ones (every later
+    worker's index moves up on the device) and some of them paused, resuming later."""
     from distributed_amd.engine import PlacementEngine
 
     path = os.path.join(GOLDEN, name)
@@ -317,9 +319,14 @@ def test_service_with_workers_joining(name, per_message):
     msgs = list(zip(z["msg_task"].tolist(), z["msg_worker"].tolist(), z["msg_runid"].tolist(),
                     z["msg_nbytes"].tolist(), z["msg_start"].tolist(), z["msg_stop"].tolist()))
     ptr = z["msg_round_ptr"].tolist()
-    add_at = {}
-    for i, nt in zip(z["add_msg"].tolist(), z["add_nthreads"].tolist()):
-        add_at.setdefault(i, []).append(nt)
+    add_at = {}  # message index -> the joins before it: (nthreads, position, running)
+    n_add = len(z["add_nthreads"])
+    pos = z["add_pos"].tolist() if "add_pos" in z else [None] * n_add
+    run = z["add_running"].tolist() if "add_running" in z else [1] * n_add
+    for i, nt, p_, r_ in zip(z["add_msg"].tolist(), z["add_nthreads"].tolist(), pos, run):
+        add_at.setdefault(i, []).append((nt, p_, r_))
+    for i, w in zip(*((z["res_msg"].tolist(), z["res_worker"].tolist()) if "res_msg" in z else ((), ()))):
+        add_at.setdefault(i, []).append((0, w, 2))  # a paused joiner resumes (worker-status-change)
     W0 = len(g["nthreads"])
     R = len(exp["round_nplaced"]) + 2
     status, refill = [], 0
@@ -329,9 +336,12 @@ def test_service_with_workers_joining(name, per_message):
         for k in range(len(ptr) - 1):
             i, e = ptr[k], ptr[k + 1]
             while i < e:  # batches end at the next worker addition
-                for nt in add_at.get(i, ()):
+                for nt, p_, r_ in add_at.get(i, ()):
                     n0 = eng.num_placements()
-                    newp = eng.add_worker(nt)
+                    if r_ == 2:
+                        newp = eng.set_worker_status(p_, 1)
+                    else:
+                        newp = eng.add_worker(nt, running=bool(r_), position=p_)
                     assert eng.num_placements() == n0 + newp
                     refill += newp
                 j = i + 1

@@ -62,6 +62,13 @@ def test_oracle_matches_reference_with_workers_joining(name):
     path = os.path.join(GOLDEN, name)
     g, cfg, exp, meta = oracle.load_fixture(path)
     z = np.load(path, allow_pickle=False)
+    if "add_pos" in z.files and (not z["add_running"].all() or
+                                 (z["add_pos"] != len(g["nthreads"]) + np.arange(len(z["add_pos"]))).any()):
+        # svcaddw_order_*: joins among the known addresses and paused joins. The oracle's
+        # restatement appends workers and has no paused workers (check_idle_saturated's
+        # paused branch, :2980-2981); these fixtures pin the engine directly against the
+        # reference's own placements (tests/test_gpu_service.py, tests/ext_driver.py)
+        pytest.skip("insertion / paused joins: pinned against the reference on the GPU, not restated by the oracle")
     z = {"add_msg": z["add_msg"], "add_nthreads": z["add_nthreads"], "msg_task": z["msg_task"],
          "msg_nbytes": z["msg_nbytes"]}
     assert np.array_equal(z["msg_task"], exp["pl_task"])  # messages = completions in replay order
