@@ -1813,7 +1813,9 @@ __global__ void k_ug_init(const Dev* __restrict__ Dp, int lo) {
 // further root-ish task is queued in bulk (:2761) — order-preserving.
 // Tasks at priority positions [lo, N) (a later graph's tasks follow every earlier one in
 // priority: a new generation); its placements append to the placement log.
-__global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp, int lo) {
+// scan_lo: the first priority position scanned; task_lo: the first task of the graph (a later
+// graph whose user priority outranks earlier tasks: its tasks sit anywhere in the order)
+__global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp, int scan_lo, int task_lo) {
   // the dispatch is one lane's chain of dependent reads and writes of the control block
   // (idle_task_count / idle / saturated counts, the global prefix dict, occupancy sums): the
   // block works on an LDS copy of it (and of Dev, whose ctl points at the copy) and writes
@@ -1838,10 +1840,10 @@ __global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp,
   const int64_t pl0 = (int64_t)c->n_placed;  // 0 for the first graph
   // ready list in priority order
   int64_t base = 0;
-  for (int i0 = lo; i0 < D.N; i0 += blockDim.x) {
+  for (int i0 = scan_lo; i0 < D.N; i0 += blockDim.x) {
     int i = i0 + threadIdx.x;
     int t = i < D.N ? D.order[i] : -1;
-    bool r = t >= 0 && D.remaining[t] == 0;
+    bool r = t >= task_lo && D.remaining[t] == 0;
     int64_t tot;
     int64_t pos = block_excl_scan(r ? 1 : 0, &tot);
     if (r) D.ready[base + pos] = t;

@@ -23,6 +23,7 @@
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/dgplace.h"
@@ -116,6 +117,7 @@ struct dgp_engine {
   bool res_running = false;          // the resident kernel was launched (it may have ended since)
   bool res_hung = false;             // the resident kernel did not end when told to: the engine is unusable
   bool pending_resync = false;       // a later graph with dependencies on earlier tasks: dgp_sync_* next
+  int64_t pending_lo = -1;           // ... its first task (dgp_graph_stimulus may run its stimulus instead)
   unsigned long long req_seq = 0;    // the last request number sent
   // dgp_tasks_finished_post: 0 nothing posted, 1 a batch in the resident mailbox awaiting its
   // answer, 2 answered at the post (launch per call) and kept for dgp_tasks_finished_wait
@@ -930,7 +932,7 @@ int dgp_update_restrictions(dgp_engine* e, int64_t n, const int32_t* task, const
                             const int32_t* row_idx, const uint8_t* flags) {
   if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->have_graph) return fail(e, DGP_E_STATE, "graph first");
-  if (e->pending_resync) return fail(e, DGP_E_STATE, "dgp_update_restrictions: dgp_sync_* first");
+  // (while an appended graph's stimulus is pending: its tasks' rows go in before dgp_graph_stimulus)
   if (n < 0 || (n && (!task || !row_ptr || !flags)) || (n && row_ptr[0] != 0))
     return fail(e, DGP_E_ARG, "dgp_update_restrictions: arguments");
   HIPCHK(e, hipSetDevice(e->device));
@@ -1029,7 +1031,7 @@ int dgp_update_restrictions(dgp_engine* e, int64_t n, const int32_t* task, const
 int dgp_set_rootish(dgp_engine* e, int64_t n, const int32_t* task, const int8_t* value) {
   if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->have_graph) return fail(e, DGP_E_STATE, "graph first");
-  if (e->pending_resync) return fail(e, DGP_E_STATE, "dgp_set_rootish: dgp_sync_* first");
+  // (while an appended graph's stimulus is pending: its tasks' flags go in before dgp_graph_stimulus)
   if (n < 0 || (n && (!task || !value))) return fail(e, DGP_E_ARG, "dgp_set_rootish: arguments");
   HIPCHK(e, hipSetDevice(e->device));
   dgp::Dev& D = e->D;
@@ -1139,7 +1141,7 @@ int dgp_update_graph(dgp_engine* e) {
         hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(e->D.N, 256, 2048)), dim3(256), 0, s, DP, 0);
       }))
     return rc;
-  if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP, 0); }))
+  if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP, 0, 0); }))
     return rc;
   if (e->snap_rounds > 0) {
     hipLaunchKernelGGL(dgp::k_snapshot, dim3(8), dim3(256), 0, s, DP, e->d_aux + 1, 0);
@@ -1763,6 +1765,113 @@ int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr,
                         n_groups, wanted, rootish_override, nullptr, true);
 }
 
+}  // extern "C"
+
+namespace {
+int stage_args(dgp_engine* e, std::initializer_list<std::pair<const void*, size_t>> parts, std::vector<char*>& out);
+// every earlier task a new one depends on gains it as a waiter (_transition_released_waiting
+// :2094-2099: dts.waiters.add(ts) for a dependency that is not released)
+__global__ void k_add_waiters(int32_t* waiters, const int32_t* dep, const int32_t* cnt, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    waiters[dep[i]] += cnt[i];
+}
+// the later graph's tasks that are ready at once with dependencies (every one an earlier task
+// in memory) go to decide_worker over their dependencies' holders: they become the frontier
+// k_candidate_commbytes computes the candidates and comm bytes of
+__global__ void k_ug_frontier(const dgp::Dev* __restrict__ Dp, int lo) {
+  const dgp::Dev& D = *Dp;
+  for (int64_t t = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < D.N; t += (int64_t)gridDim.x * blockDim.x)
+    if (D.remaining[t] == 0 && D.dep_ptr[t + 1] > D.dep_ptr[t]) D.frontier[atomicAdd(&D.ctl->n_frontier, 1ull)] = (int)t;
+}
+__global__ void k_ug_frontier_reset(const dgp::Dev* __restrict__ Dp) {
+  if (threadIdx.x == 0) {
+    Dp->ctl->n_frontier = 0;
+    Dp->ctl->pool_used = 0;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int dgp_graph_stimulus(dgp_engine* e, int64_t* n_new_placements) {
+  if (int rc_ = resident_stop(e)) return rc_;
+  if (n_new_placements) *n_new_placements = 0;
+  if (!e || !e->pending_resync || e->pending_lo < 0)
+    return fail(e, DGP_E_STATE, "dgp_graph_stimulus: no appended graph (dgp_add_graph_deferred first)");
+  dgp::Dev& D = e->D;
+  const int64_t lo = e->pending_lo, N = D.N;
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  // the earlier tasks the new ones depend on: in memory (a replica), or waiting / queued /
+  // processing (the new task waits on it); one released, erred or forgotten would be
+  // recomputed or fail the new task (:2082-2097), which the engine leaves to the scheduler
+  std::vector<uint8_t> st((size_t)lo);
+  HIPCHK(e, hipMemcpy(st.data(), D.state, (size_t)lo, hipMemcpyDeviceToHost));
+  std::unordered_map<int32_t, int32_t> add;
+  const std::vector<int64_t>& dp = e->h_dep_ptr;
+  const std::vector<int32_t>& di = e->h_dep_idx;
+  for (int64_t t = lo; t < N; t++)
+    for (int64_t k = dp[t]; k < dp[t + 1]; k++) {
+      const int32_t d = di[k];
+      if (d >= lo) continue;
+      const uint8_t sd = st[d];
+      if (sd == dgp::S_RELEASED || sd == dgp::S_ERRED || (e->tflags_h[d] & dgp::TF_FORGOTTEN))
+        return fail(e, DGP_E_UNSUPPORTED, "dgp_graph_stimulus: an earlier dependency is released, erred or "
+                                          "forgotten (recomputed by the scheduler): dgp_sync_* instead");
+      add[d] += 1;
+    }
+  if (!add.empty()) {
+    std::vector<int32_t> dd, cc;
+    for (auto& kv : add) {
+      dd.push_back(kv.first);
+      cc.push_back(kv.second);
+    }
+    std::vector<char*> a;
+    if (int rc = stage_args(e, {{dd.data(), dd.size() * 4}, {cc.data(), cc.size() * 4}}, a)) return rc;
+    hipLaunchKernelGGL(k_add_waiters, dim3((unsigned)std::min<size_t>((dd.size() + 255) / 256, 1024)), dim3(256), 0,
+                       e->stream, D.waiters, (const int32_t*)a[0], (const int32_t*)a[1], (int64_t)dd.size());
+    HIPCHK(e, hipGetLastError());
+  }
+  e->pending_resync = false;
+  e->pending_lo = -1;
+  e->mode = 2;
+  // the priority positions to scan: the new tasks follow every earlier one unless a user
+  // priority outranks them (dgp_set_priorities re-ranked every task: scan them all)
+  int64_t pmax_old = -1;
+  for (int64_t t = 0; t < lo; t++) pmax_old = std::max(pmax_old, e->h_prio[t]);
+  bool follows = true;
+  for (int64_t t = lo; t < N && follows; t++) follows = e->h_prio[t] > pmax_old;
+  if (int rc = grow_logs(e, 0)) return rc;
+  if (int rc = sync_dev(e)) return rc;
+  dgp::Ctl c0;
+  if (int rc = read_ctl(e, &c0)) return rc;
+  const dgp::Dev* DP = e->d_dev;
+  hipStream_t s = e->stream;
+  if (int rc = timed_launch(e, 3, [&] {
+        hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(N - lo, 256, 2048)), dim3(256), 0, s, DP, (int)lo);
+        hipLaunchKernelGGL(k_ug_frontier_reset, dim3(1), dim3(64), 0, s, DP);
+        hipLaunchKernelGGL(k_ug_frontier, dim3(grid_for(N - lo, 256, 2048)), dim3(256), 0, s, DP, (int)lo);
+        hipLaunchKernelGGL(dgp::k_candidate_commbytes, dim3(grid_for(N - lo, 256, 2048)), dim3(256), 0, s, DP);
+      }))
+    return rc;
+  if (int rc = timed_launch(e, 3, [&] {
+        hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP, follows ? (int)lo : 0, (int)lo);
+      }))
+    return rc;
+  if (int rc = set_runids(e)) return rc;
+  dgp::Ctl c;
+  if (int rc = check_device_error(e, &c)) return rc;
+  if (!follows && c.qlen > 1) {  // the queue (HeapSet by priority) with the new root-ish tasks in their place
+    std::vector<int32_t> q((size_t)c.qlen);
+    HIPCHK(e, hipMemcpy(q.data(), D.qarr + c.qhead, q.size() * 4, hipMemcpyDeviceToHost));
+    std::stable_sort(q.begin(), q.end(), [&](int32_t a, int32_t b) { return e->h_prio[a] < e->h_prio[b]; });
+    HIPCHK(e, hipMemcpy(D.qarr + c.qhead, q.data(), q.size() * 4, hipMemcpyHostToDevice));
+  }
+  if (n_new_placements) *n_new_placements = (int64_t)(c.n_placed - c0.n_placed);
+  e->last_placed = c.n_placed;
+  return 0;
+}
+
 static int add_graph_impl(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const int32_t* dep_idx,
                           const int64_t* prio, const int32_t* prefix_id, int32_t n_prefixes,
                           const double* prefix_default_duration, const int32_t* group_id, int32_t n_groups,
@@ -1950,6 +2059,7 @@ static int add_graph_impl(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, 
     // (the new tasks' waiting_on / the earlier tasks' waiters, any placement it makes) and
     // the caller hands over its state (dgp_sync_*) before the next stimulus
     e->pending_resync = true;
+    e->pending_lo = N0;
     e->mode = 2;
     if (int rc = sync_dev(e)) return rc;
     return 0;
@@ -1966,7 +2076,7 @@ static int add_graph_impl(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, 
       }))
     return rc;
   if (int rc = timed_launch(e, 3, [&] {
-        hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP, (int)N0);
+        hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP, (int)N0, (int)N0);
       }))
     return rc;
   if (int rc = set_runids(e)) return rc;
@@ -2418,6 +2528,7 @@ int dgp_sync_globals(dgp_engine* e, int64_t n_tasks_counter, double network_occ_
   D.bandwidth = bandwidth;
   if (int rc = sync_dev(e)) return rc;
   e->pending_resync = false;  // the resync is complete (dgp_sync_globals comes last)
+  e->pending_lo = -1;
   return 0;
 }
 

@@ -370,6 +370,21 @@ class PlacementEngine:
         self.n_tasks += n
         return int(newp.value)
 
+    UNSUPPORTED = -5  # DGP_E_UNSUPPORTED: a case the engine leaves to the caller, nothing changed
+
+    def graph_stimulus(self) -> int | None:
+        """The update_graph stimulus of the graph ``add_graph(defer=True)`` appended, on the
+        device (dgp_graph_stimulus): dependent, restricted (rows first, update_restrictions)
+        or outranking (ranks first, set_priorities) later graphs. Returns its placements, or
+        None when the engine leaves it to the scheduler (an earlier dependency is released /
+        erred / forgotten): then the scheduler's stimulus and ``sync()`` follow as before."""
+        newp = C.c_int64(0)
+        rc = self.lib.dgp_graph_stimulus(self.h, C.byref(newp))
+        if rc == self.UNSUPPORTED:
+            return None
+        self._check(rc, "dgp_graph_stimulus")
+        return int(newp.value)
+
     def set_priorities(self, prio):
         """Every task's priority anew (dgp_set_priorities): the merged ranks after a later
         graph whose user priority outranks earlier tasks (appended with ``defer``)."""

@@ -1029,8 +1029,10 @@ class GPUPlacementExtension(SchedulerPlugin):
         earlier ones in priority (a new generation, :4713) runs its update_graph stimulus on
         the engine. A graph that depends on earlier tasks, carries restrictions, or whose
         user priority outranks earlier tasks (then every task's merged rank goes to the
-        engine, dgp_set_priorities) is appended without placing and its stimulus is the
-        scheduler's own, the engine resynchronised after it (``_suspend``)."""
+        engine, dgp_set_priorities) is appended without placing, its tasks' valid workers
+        go in, and its stimulus runs on the engine too (dgp_graph_stimulus); only when an
+        earlier dependency is released / erred / forgotten (recomputed by the scheduler) is
+        the stimulus the scheduler's own, the engine resynchronised after it (``_suspend``)."""
         s = self.scheduler
         g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads if a in s.workers else 1 for a in self.workers],
                                     s.valid_workers, self.worker_index, earlier=self.task_index)
@@ -1075,13 +1077,21 @@ class GPUPlacementExtension(SchedulerPlugin):
             rank[order] = np.arange(len(order))
             self.engine.set_priorities(rank)
             self.stats["reranked_graphs"] += 1
-        g.pop("restr_flags", None)  # the resync hands the restrictions over (the mirrors lack them)
+        g.pop("restr_flags", None)  # the rows go to the engine below (dgp_update_restrictions)
         self._remember_inputs(g, keys_)
         self.max_priority = max(self.max_priority, max(ts.priority for ts in new))
         self.stats["graphs"] += 1
         if dependent or restricted or outranks:
             if not outranks:
                 self.stats["dependent_graphs" if dependent else "restricted_graphs"] += 1
+            # the stimulus on the device (dgp_graph_stimulus), the new tasks' valid workers first
+            if hasattr(self.engine, "graph_stimulus"):
+                if restricted:
+                    self._push_task_inputs(keys_)
+                if self.active and self.engine.graph_stimulus() is not None:
+                    self.stats["graph_stimuli_on_device"] += 1
+                    self._fetch()
+                    return
             self._suspend("a later graph that depends on earlier tasks" if dependent else
                           "a later graph with restrictions" if restricted else "a later graph that outranks earlier tasks")
             for k in keys_:  # the new tasks, the earlier ones they wait on / add waiters to

@@ -73,6 +73,7 @@ extern "C" {
 #define DGP_E_HIP -2     /* HIP runtime error (no device, OOM, launch failure) */
 #define DGP_E_STATE -3   /* call out of order (e.g. rounds before update_graph) */
 #define DGP_E_DEVICE -4  /* the device engine detected an inconsistent state */
+#define DGP_E_UNSUPPORTED -5  /* a case the engine leaves to the caller; nothing changed (ABI 16) */
 
 /* placement routes (which reference decide_worker path produced it) */
 #define DGP_ROUTE_NONROOTISH 0   /* decide_worker_non_rootish -> decide_worker (:2247, :8550) */
@@ -269,6 +270,19 @@ int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr,
                            const int64_t* prio, const int32_t* prefix_id, int32_t n_prefixes,
                            const double* prefix_default_duration, const int32_t* group_id, int32_t n_groups,
                            const uint8_t* wanted, const int8_t* rootish_override);
+/* (ABI 16) The update_graph stimulus (Scheduler.update_graph :4662-4751 ->
+ * _transition_released_waiting :2078-2119 -> decide_worker / queued) of the graph the last
+ * dgp_add_graph_deferred appended, on the device: for a later graph whose tasks depend on
+ * earlier ones (each earlier dependency in memory, or waiting / queued / processing: the new
+ * task waits on it and it gains the new task as a waiter), carries worker restrictions (its
+ * rows given first with dgp_update_restrictions) or outranks earlier tasks by user priority
+ * (every task's rank given first with dgp_set_priorities; new root-ish tasks queue in their
+ * priority place). Ends the pending state of the append (no dgp_sync_* needed). An earlier
+ * dependency that is released, erred or forgotten (recomputed or failed by the scheduler,
+ * :2082-2097) returns DGP_E_UNSUPPORTED with nothing changed: the scheduler decides that
+ * stimulus and the caller resynchronises as before. Replaces the scheduler's Python for that
+ * stimulus (scheduler.py:4600-4653). */
+int dgp_graph_stimulus(dgp_engine* e, int64_t* n_new_placements);
 
 /* (ABI 14) Every task's priority anew (n_tasks entries, unique and topological): a later
  * graph submitted with a user priority that outranks earlier tasks (Scheduler.update_graph's

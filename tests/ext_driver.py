@@ -656,7 +656,7 @@ def run_joins(name):
                 device_decisions=ext.stats["device_decisions"], active=ext.active, reason=ext.reason)
 
 
-def run_second_graph(name):
+def run_second_graph(name, resync=False):
     """A ``svcgraph_*`` stream (gen_service.py second-graph): a second, independent graph is
     submitted mid-stream through the tail of ``_create_taskstate_from_graph``
     (scheduler.py:4600-4653: the plugins' update_graph hook, then the transitions); the
@@ -687,7 +687,9 @@ def run_second_graph(name):
     # earlier tasks', the engine takes the merged ranks first)
     dep = name.startswith(("svcgdep_", "svcgrst_", "svcgprio_"))
     user_prio = int(z["g2_user_prio"]) if "g2_user_prio" in z.files else 0
-    eng = (EventEngine if dep else FixtureEngine)(exp, fkeys)
+    # the engine runs that stimulus (dgp_graph_stimulus) unless ``resync``: the engine of
+    # rounds 3-4 without it, the scheduler deciding and a resync after it
+    eng = ((EventEngine if resync else GraphStimulusEngine) if dep else FixtureEngine)(exp, fkeys)
     ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
     eng.ext = ext
     s.stream_handlers = {}
@@ -768,7 +770,23 @@ def run_second_graph(name):
         want = sorted(d if d >= 0 else -1 - ext.task_index[fkeys[-1 - d]] for d in row)
         assert up["dep_idx"][up["dep_ptr"][k]:up["dep_ptr"][k + 1]].tolist() == want, k
     host = 0
-    if dep:  # one resync, right after the submission: the fixture's dump
+    if dep and not resync:  # the stimulus on the device: its inputs handed over first, no resync
+        gst = [c for c in eng.calls if c[0] == "gstim"]
+        assert len(gst) == 1 and not [c for c in eng.calls if c[0] == "sync"], eng.calls[-4:]
+        assert ext.stats["graph_stimuli_on_device"] == 1 and ext.stats["resyncs"] == 0, ext.stats
+        if user_prio:  # every task's merged rank, before the stimulus
+            ps = [c for c in eng.calls if c[0] == "prio"]
+            assert len(ps) == 1 and eng.calls.index(ps[0]) < eng.calls.index(gst[0]), eng.calls[-3:]
+            assert ps[0][1] == [int(z["g2_prio_all"][tidx[k]]) for k in ext.keys]
+        if "restr_flags" in g2:  # the new tasks' valid workers, right before the stimulus
+            rs = [c for c in eng.calls if c[0] == "restrict"]
+            assert len(rs) == 1 and eng.calls.index(rs[0]) == eng.calls.index(gst[0]) - 1, eng.calls[-3:]
+            _, rt, rrows, rfl = rs[0]
+            rp, ri, rf = g2["restr_ptr"], g2["restr_idx"], g2["restr_flags"]
+            want_r = sorted((ext.task_index[fkeys[N1 + k]], ri[rp[k]:rp[k + 1]].tolist(), int(rf[k]))
+                            for k in np.flatnonzero(rf & 1))
+            assert sorted(zip(rt, rrows, rfl)) == want_r
+    if dep and resync:  # one resync, right after the submission: the fixture's dump
         syncs = [c for c in eng.calls if c[0] == "sync"]
         assert len(syncs) == 1 and (ext.stats["dependent_graphs"] + ext.stats["restricted_graphs"]
                                     + ext.stats["reranked_graphs"]) == 1, (len(syncs), ext.stats)
@@ -815,7 +833,8 @@ def run_second_graph(name):
     assert np.array_equal(np.array(rec["start"]).view(np.int64), exp["pl_start"].view(np.int64))
     assert ext.stats["device_decisions"] == n - host, (ext.stats, n, host)
     return dict(fixture=name, placements=n, graphs=ext.stats["graphs"], device_decisions=ext.stats["device_decisions"],
-                host_placements=host, resyncs=ext.stats["resyncs"], active=ext.active, reason=ext.reason)
+                host_placements=host, resyncs=ext.stats["resyncs"], active=ext.active, reason=ext.reason,
+                graph_stimuli_on_device=ext.stats["graph_stimuli_on_device"])
 
 
 class EventEngine(FixtureEngine):
@@ -897,6 +916,14 @@ class EventEngine(FixtureEngine):
         raise AssertionError("sync() expected")
 
     sync_tasks = sync_workers = sync_globals = sync_placements
+
+
+class GraphStimulusEngine(EventEngine):
+    """EventEngine that runs a later graph's update_graph stimulus itself (dgp_graph_stimulus):
+    the fixture's placement count of that event."""
+
+    def graph_stimulus(self):
+        return self._event("gstim")
 
 
 def run_events(name, plain=False):
@@ -1174,7 +1201,8 @@ if __name__ == "__main__":
         if "--ab" in args:
             print(json.dumps(run_ab(nm)), flush=True)
             continue
-        fn = (run_joins if nm.startswith("svcaddw_") else run_second_graph if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_"))
+        fn = (run_joins if nm.startswith("svcaddw_") else (lambda x: run_second_graph(x, "--resync" in args))
+              if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_"))
               else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcrt_", "svcp2p_")) else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,
                                                plain="plugin" if "--plugin" in args else plain,

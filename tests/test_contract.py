@@ -42,7 +42,7 @@ def _double_methods():
     tree = ast.parse(open(os.path.join(HERE, "ext_driver.py")).read())
     out = {}
     for node in tree.body:
-        if isinstance(node, ast.ClassDef) and node.name in ("FixtureEngine", "EventEngine"):
+        if isinstance(node, ast.ClassDef) and node.name in ("FixtureEngine", "EventEngine", "GraphStimulusEngine"):
             ms = {}
             for f in node.body:
                 if isinstance(f, ast.FunctionDef):
@@ -80,6 +80,8 @@ def test_extension_calls_exist_on_engine_and_doubles():
         n_req = sum(1 for p in ps if p.default is p.empty)
         # the double the extension is driven with in tests/test_ext.py: EventEngine covers all
         d = doubles["EventEngine"].get(name, "missing")
+        if name == "graph_stimulus":  # EventEngine drives the resync path; this double runs the stimulus
+            d = doubles["GraphStimulusEngine"].get(name, "missing")
         if name in ("move_task",):  # steal confirmations: tests/steal_ext_driver.py drives the real oracle
             continue
         assert d != "missing", f"EventEngine has no {name}()"

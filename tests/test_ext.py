@@ -107,44 +107,35 @@ def test_extension_follows_a_second_graph():
         assert r["active"] and r["device_decisions"] == r["placements"] and r["graphs"] == 2, r
 
 
-def test_extension_follows_a_dependent_later_graph():
+LATER = ["svcgdep_c2mini_satinf.npz", "svcgdep_c2var_sat1.1.npz", "svcgdep_joins_sat1.0.npz",
+         "svcgrst_c2var_sat1.1.npz", "svcgrst_dep_satinf.npz", "svcgprio_c2mini_satinf.npz", "svcgprio_c2var_sat1.1.npz"]
+
+
+def test_extension_runs_later_graph_stimuli_on_the_engine():
     """A later graph whose tasks depend on earlier ones (in memory, processing, waiting or
-    queued): the extension appends it to the engine (dgp_add_graph with -1 - index rows), the
-    scheduler decides that update_graph stimulus, the engine resyncs once from the
-    scheduler's state (the rows equal the reference dump, every new task and every earlier
-    task it depends on among them) and every later decision is the engine's (validate=True)."""
-    names = ["svcgdep_c2mini_satinf.npz", "svcgdep_c2var_sat1.1.npz", "svcgdep_joins_sat1.0.npz"]
-    res = drive(names)
-    assert [r["fixture"] for r in res] == names
+    queued), carry worker restrictions (scheduler.py:4908-4922) or outrank earlier tasks by a
+    user priority (_set_priorities :4934-4981): the extension appends it (dgp_add_graph /
+    _deferred), hands the engine the new tasks' valid workers (dgp_update_restrictions) or
+    every task's merged rank (dgp_set_priorities), and the engine runs that update_graph
+    stimulus itself (dgp_graph_stimulus): no resync, every decision the engine's
+    (validate=True), the extension active."""
+    res = drive(LATER)
+    assert [r["fixture"] for r in res] == LATER
+    for r in res:
+        assert r["active"] and r["graphs"] == 2 and r["resyncs"] == 0, r
+        assert r["graph_stimuli_on_device"] == 1 and r["device_decisions"] == r["placements"], r
+
+
+def test_extension_resyncs_later_graphs_without_the_engine_stimulus():
+    """The same streams with an engine that has no dgp_graph_stimulus (--resync): the
+    scheduler decides that stimulus, the engine resyncs once from its state (the rows equal
+    the reference dump, every new task and every earlier task it depends on among them) and
+    every later decision is the engine's (validate=True). The path the extension keeps for an
+    earlier dependency that is released, erred or forgotten."""
+    res = drive(LATER, "--resync")
     for r in res:
         assert r["active"] and r["graphs"] == 2 and r["resyncs"] == 1, r
-        assert r["device_decisions"] + r["host_placements"] == r["placements"] and r["host_placements"] > 0, r
-
-
-def test_extension_follows_a_later_graph_with_restrictions():
-    """A later graph whose tasks carry worker restrictions (scheduler.py:4908-4922): the
-    extension appends it deferred (dgp_add_graph_deferred), the scheduler decides that
-    update_graph stimulus, the engine resyncs and takes the new tasks' valid-worker rows
-    (dgp_update_restrictions) right after; every later decision is the engine's
-    (validate=True) and the extension stays active."""
-    names = ["svcgrst_c2var_sat1.1.npz", "svcgrst_dep_satinf.npz"]
-    res = drive(names)
-    assert [r["fixture"] for r in res] == names
-    for r in res:
-        assert r["active"] and r["graphs"] == 2 and r["resyncs"] == 1, r
-
-
-def test_extension_follows_a_later_graph_that_outranks_earlier_tasks():
-    """A later graph submitted with a user priority (_set_priorities, scheduler.py:4934-4981):
-    its tasks outrank every earlier one. The extension appends it deferred, hands the engine
-    every task's rank in the merged order (dgp_set_priorities), the scheduler decides that
-    update_graph stimulus and the engine resyncs; every later decision is the engine's
-    (validate=True) and the extension stays active."""
-    names = ["svcgprio_c2mini_satinf.npz", "svcgprio_c2var_sat1.1.npz"]
-    res = drive(names)
-    assert [r["fixture"] for r in res] == names
-    for r in res:
-        assert r["active"] and r["graphs"] == 2 and r["resyncs"] == 1, r
+        assert r["device_decisions"] + r["host_placements"] == r["placements"], r
 
 
 EVENTS = ["svcev_c2var_sat1.1.npz", "svcev_c2mini_satinf.npz", "svcev_dense_sat1.0.npz"]

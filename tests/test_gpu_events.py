@@ -298,6 +298,68 @@ def test_service_dependent_later_graph_matches_reference(name):
     assert np.array_equal(out["final_state"], exp["final_state"])
 
 
+@pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])
+@pytest.mark.parametrize("name", svc_dep_graph_files() + svc_restr_graph_files() + svc_prio_graph_files())
+def test_later_graph_stimulus_on_the_engine(name, per_message):
+    """The same later graphs with their update_graph stimulus decided by the engine
+    (dgp_graph_stimulus): appended deferred, the new tasks' valid workers
+    (dgp_update_restrictions) or every task's merged rank (dgp_set_priorities) first, then
+    the stimulus on the device -- the earlier tasks gain the new ones as waiters, the new ones
+    wait on the earlier ones not in memory, the runnable ones go to processing / queued in
+    priority order. Its placements and every later one, the snapshots and the final states
+    equal the reference's; no resync."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    msgs = list(zip(z["msg_task"].tolist(), z["msg_worker"].tolist(), z["msg_runid"].tolist(),
+                    z["msg_nbytes"].tolist(), z["msg_start"].tolist(), z["msg_stop"].tolist()))
+    ptr = z["msg_round_ptr"].tolist()
+    at = int(z["g2_msg"])
+    g2 = second_graph(g, z)
+    restr = "g2_restr_flags" in z.files
+    rerank = "g2_prio_all" in z.files
+    joins = {}
+    for m, nt in zip(z["add_msg"].tolist() if "add_msg" in z.files else [],
+                     z["add_nthreads"].tolist() if "add_nthreads" in z.files else []):
+        joins.setdefault(m, []).append(nt)
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        for k in range(len(ptr) - 1):
+            i, e = ptr[k], ptr[k + 1]
+            while i < e:
+                for nt in joins.get(i, ()):
+                    eng.add_worker(nt)
+                if i == at:
+                    n0 = eng.num_placements()
+                    assert eng.add_graph(g2, defer=True) == 0 and eng.num_placements() == n0
+                    if rerank:
+                        eng.set_priorities(z["g2_prio_all"])
+                    if restr:
+                        rp, ri, rf = z["g2_restr_ptr"], z["g2_restr_idx"], z["g2_restr_flags"]
+                        ts = np.flatnonzero(rf & 1)
+                        eng.update_restrictions(g["n_tasks"] + ts, [ri[rp[t]:rp[t + 1]] for t in ts], rf[ts])
+                    newp = eng.graph_stimulus()
+                    assert newp == int(z["g2_nplaced"]) and eng.num_placements() == n0 + newp, (newp, z["g2_nplaced"])
+                j = i + 1
+                if not per_message:
+                    while j < e and j not in joins and j != at:
+                        j += 1
+                st, _ = eng.tasks_finished(*(np.array(c) for c in zip(*msgs[i:j])))
+                assert (st == 0).all(), (i, st)
+                i = j
+            if e > ptr[k]:
+                eng.snapshot()
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
 @pytest.mark.parametrize("resident", [False, True], ids=["launch", "resident"])
 @pytest.mark.parametrize("name", svc_event_files())
 def test_task_messages_follow_replicas(name, resident):
