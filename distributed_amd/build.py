@@ -26,8 +26,27 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fn
          "-Wall", "-mllvm", "-amdgpu-lower-module-lds-strategy=module"]
 
 
+# the extension's graph ingestion pass (host C against the stable Python ABI; ext.py loads
+# it with ctypes.PyDLL): one build for any CPython >= 3.9
+INGEST_SRC = os.path.join(PKG, "csrc", "dgp_ingest.c")
+INGEST_OUT = os.path.join(PKG, "libdgpingest.so")
+
+
+def build_ingest(force: bool = False) -> str:
+    import sysconfig
+
+    if force or not os.path.exists(INGEST_OUT) or os.path.getmtime(INGEST_OUT) < os.path.getmtime(INGEST_SRC):
+        subprocess.run([shutil.which("gcc") or "cc", "-O2", "-Wall", "-shared", "-fPIC",
+                        "-I" + sysconfig.get_paths()["include"], "-o", INGEST_OUT + ".tmp", INGEST_SRC],
+                       check=True, capture_output=True, text=True)
+        os.replace(INGEST_OUT + ".tmp", INGEST_OUT)
+    return INGEST_OUT
+
+
 def build(force: bool = False) -> str:
-    """Both builds, compiled side by side; returns the default library's path."""
+    """Both builds, compiled side by side (and the ingestion pass); returns the default
+    library's path."""
+    build_ingest(force)
     newest = max(os.path.getmtime(p) for p in SRC + DEPS + [os.path.join(PKG, "..", "include", "dgplace.h")])
     jobs = []
     for out, extra in ((OUT, []), (OUT_W64, W64_FLAGS)):

@@ -53,6 +53,8 @@ import inspect
 import logging
 import math
 from collections import Counter, deque
+from itertools import chain, islice, repeat
+from operator import attrgetter, lt, truth
 
 import numpy as np
 
@@ -117,6 +119,96 @@ def _compute_interval(startstops):
     return math.nan, math.nan
 
 
+_PRIO, _KEY, _DEPS = attrgetter("priority"), attrgetter("key"), attrgetter("dependencies")
+_GROUP, _PREFIX, _WANTS, _ROOTISH = attrgetter("group"), attrgetter("prefix"), attrgetter("who_wants"), attrgetter("_rootish")
+_RESTR = (attrgetter("worker_restrictions"), attrgetter("host_restrictions"), attrgetter("resource_restrictions"))
+_ROOTISH_CODE = {None: -1, False: 0, True: 1}
+
+
+_FORCE_PY_INGEST = False  # tests: the Python passes even where the C library is built
+_INGEST = []  # [ctypes function or None]: libdgpingest.so's dgp_ingest_columns, loaded once
+
+
+def _ingest_lib():
+    """dgp_ingest_columns (csrc/dgp_ingest.c, built by distributed_amd/build.py) through
+    ctypes.PyDLL (the GIL stays held, its Python errors propagate); None when the library
+    is not built (graph_from_tasks then runs its Python passes)."""
+    if not _INGEST:
+        import ctypes
+        import os
+
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdgpingest.so")
+        fn = None
+        if os.path.exists(path):
+            fn = ctypes.PyDLL(path).dgp_ingest_columns
+            P = ctypes.c_void_p
+            fn.argtypes = [ctypes.py_object, ctypes.py_object, P, P, ctypes.c_int64, P, P, P, P, P, P, P, P]
+            fn.restype = ctypes.c_int64
+        _INGEST.append(fn)
+    return _INGEST[0]
+
+
+def _columns_c(fn, tss):
+    """The per-task columns in one C pass (dgp_ingest_columns): (dependency counts, flat
+    dependency ids in set order (-1 - m: misses[m], outside ``tss``), misses, prefix ids,
+    first task per prefix, group ids, first task per group, wanted, rootish code,
+    restriction bits)."""
+    n = len(tss)
+    cnt = np.empty(n, np.int64)
+    pid, gid = np.empty(n, np.int32), np.empty(n, np.int32)
+    pfirst, gfirst = np.empty(max(n, 1), np.int32), np.empty(max(n, 1), np.int32)
+    nid = np.zeros(2, np.int32)
+    wanted, rootish, restr = np.empty(n, np.uint8), np.empty(n, np.int8), np.empty(n, np.uint8)
+    cap = 4 * n + 16
+    while True:
+        misses = []
+        dflat = np.empty(cap, np.int64)
+        e = fn(tss, misses, cnt.ctypes.data, dflat.ctypes.data, cap, pid.ctypes.data, gid.ctypes.data,
+               pfirst.ctypes.data, gfirst.ctypes.data, nid.ctypes.data, wanted.ctypes.data, rootish.ctypes.data,
+               restr.ctypes.data)
+        if e <= cap:
+            break
+        cap = e
+    return (cnt, dflat[:e], misses, pid, pfirst[:nid[0]], gid, gfirst[:nid[1]], wanted, rootish, restr)
+
+
+def _columns_py(tss):
+    """_columns_c's result with Python passes (one C-level map per column)."""
+    n = len(tss)
+    deps = list(map(_DEPS, tss))
+    cnt = np.fromiter(map(len, deps), np.int64, n)
+    tid = dict(zip(map(id, tss), range(n)))
+    flat = list(chain.from_iterable(deps))
+    none = -(1 << 40)
+    dflat = np.fromiter(map(tid.get, map(id, flat), repeat(none)), np.int64, len(flat))
+    misses, mid = [], {}
+    for k in np.flatnonzero(dflat == none).tolist():
+        d = flat[k]
+        m = mid.get(id(d))
+        if m is None:
+            m = mid[id(d)] = len(misses)
+            misses.append(d)
+        dflat[k] = -1 - m
+    pid, pfirst = _first_seen(list(map(_PREFIX, tss)))
+    gid, gfirst = _first_seen(list(map(_GROUP, tss)))
+    restr = np.zeros(n, np.uint8)
+    for b, get in enumerate(_RESTR):
+        restr |= np.fromiter(map(truth, map(get, tss)), np.uint8, n) << b
+    return (cnt, dflat, misses, pid, pfirst, gid, gfirst, np.fromiter(map(truth, map(_WANTS, tss)), np.uint8, n),
+            np.fromiter(map(_ROOTISH_CODE.__getitem__, map(_ROOTISH, tss)), np.int8, n), restr)
+
+
+def _first_seen(objs):
+    """(ids of ``objs`` in first-seen order, the first position of each id); identity
+    hashing (TaskGroup / TaskPrefix define no __hash__)."""
+    ids = np.fromiter(map(dict(zip(map(id, reversed(objs)), range(len(objs) - 1, -1, -1))).__getitem__,
+                          map(id, objs)), np.int64, len(objs))
+    first = np.unique(ids)  # positions of first occurrences, ascending = first-seen order
+    rank = np.zeros(len(objs), np.int32)
+    rank[first] = np.arange(len(first), dtype=np.int32)
+    return rank[ids], first.astype(np.int32)
+
+
 def graph_from_tasks(tss, nthreads, valid_workers=None, worker_index=None, earlier=None):
     """TaskState objects -> the engine's graph arrays (the layout of distributed_amd/graphs.py).
 
@@ -131,48 +223,41 @@ def graph_from_tasks(tss, nthreads, valid_workers=None, worker_index=None, earli
     :3043-3107, which resolves worker / host / resource restrictions) and ``worker_index``
     (address -> engine worker index), every task with restrictions gets its valid set as
     ascending indices (``restr_ptr`` / ``restr_idx``) and ``restr_flags`` (1: restricted,
-    2: loose_restrictions)."""
-    tss = sorted(tss, key=lambda ts: ts.priority)
-    index = {ts.key: i for i, ts in enumerate(tss)}
+    2: loose_restrictions).
+
+    Every per-task column is one C-level pass (``map`` over attribute getters into
+    ``np.fromiter``): no Python frame and no container allocation per task (a Python loop
+    here costs ~10 us per task, mostly the collector walking the scheduler's heap); only
+    restricted tasks and dependencies on earlier graphs are visited one by one. Returns
+    (graph, keys in engine order, their priorities)."""
+    prio = list(map(_PRIO, tss))
+    if not all(map(lt, prio, islice(prio, 1, None))):  # not already in ascending priority
+        tss = sorted(tss, key=_PRIO)
+        prio = list(map(_PRIO, tss))
     n = len(tss)
-    # the dependency edges in bulk: every row's keys flattened, mapped to indices (an earlier
-    # task as -1 - its engine index), then each row sorted by one lexsort
-    counts = np.fromiter((len(ts.dependencies) for ts in tss), np.int64, n)
-    dkeys = [d.key for ts in tss for d in ts.dependencies]
+    keys = list(map(_KEY, tss))
+    fn = _ingest_lib()
+    use_c = fn is not None and not _FORCE_PY_INGEST
+    cnt, didx, misses, pid, pfirst, gid, gfirst, wanted, rootish, restr = (
+        _columns_c(fn, tss) if use_c else _columns_py(tss))
+    # a dependency outside the graph: an earlier task (engine index e -> -1 - e), else an error
     none = -(1 << 40)
-    if earlier is None:
-        didx = np.fromiter((index.get(k, none) for k in dkeys), np.int64, len(dkeys))
-    else:
-        didx = np.fromiter((index[k] if k in index else -1 - earlier.get(k, -none) for k in dkeys), np.int64,
-                           len(dkeys))
-    bad = (didx == none) | (didx <= -1 + none)
-    if bad.any():
-        k = int(np.flatnonzero(bad)[0])
-        row = int(np.searchsorted(np.cumsum(counts), k, side="right"))
-        raise ValueError(f"dependency {dkeys[k]!r} of {tss[row].key!r} is not in the uploaded graph")
-    rowid = np.repeat(np.arange(n, dtype=np.int64), counts)
-    didx = didx[np.lexsort((didx, rowid))]
-    pnames, gnames, gpref = {}, {}, []
-    pdur = []
-    pid = np.empty(n, np.int32)
-    gid = np.empty(n, np.int32)
-    pl = [ts.prefix for ts in tss]
-    gl = [ts.group.name for ts in tss]
-    for i in range(n):
-        p = pl[i].name
-        q = pnames.get(p)
-        if q is None:
-            q = pnames[p] = len(pnames)
-            pdur.append(float(pl[i].duration_average))
-        pid[i] = q
-        gn = gl[i]
-        h = gnames.get(gn)
-        if h is None:
-            h = gnames[gn] = len(gnames)
-            gpref.append(q)
-        gid[i] = h
+    if misses:
+        eidx = np.fromiter(map((earlier or {}).get, map(_KEY, misses), repeat(none)), np.int64, len(misses))
+        lost = np.flatnonzero(eidx == none)
+        if len(lost):
+            m = int(lost[0])
+            k = int(np.flatnonzero(didx == -1 - m)[0])
+            row = int(np.searchsorted(np.cumsum(cnt), k, side="right"))
+            raise ValueError(f"dependency {misses[m].key!r} of {keys[row]!r} is not in the uploaded graph")
+        out = didx < 0
+        didx[out] = -1 - eidx[-1 - didx[out]]
+    if misses or not use_c:  # each row ascending (one lexsort over the flat edges; the C pass sorted them)
+        rowid = np.repeat(np.arange(n, dtype=np.int64), cnt)
+        didx = didx[np.lexsort((didx, rowid))]
+    prefixes = [tss[i].prefix for i in pfirst.tolist()]
     ptr = np.zeros(n + 1, np.int64)
-    np.cumsum(counts, out=ptr[1:])
+    np.cumsum(cnt, out=ptr[1:])
     g = dict(
         n_tasks=n,
         dep_ptr=ptr,
@@ -180,33 +265,37 @@ def graph_from_tasks(tss, nthreads, valid_workers=None, worker_index=None, earli
         prio=np.arange(n, dtype=np.int64),
         prefix_id=pid,
         group_id=gid,
-        prefix_names=list(pnames),
-        group_names=list(gnames),
-        group_prefix=np.array(gpref, np.int32),
-        prefix_default_dur=np.array(pdur, np.float64),
-        wanted=np.array([1 if ts.who_wants else 0 for ts in tss], np.uint8),
-        rootish_override=np.array([-1 if ts._rootish is None else int(bool(ts._rootish)) for ts in tss], np.int8),
+        prefix_names=[p.name for p in prefixes],
+        group_names=[tss[i].group.name for i in gfirst.tolist()],
+        group_prefix=pid[gfirst].astype(np.int32),
+        prefix_default_dur=np.array([float(p.duration_average) for p in prefixes], np.float64),
+        wanted=wanted,
+        rootish_override=rootish,
         nthreads=np.asarray(nthreads, np.int32),
         # completion reports arrive with the task-finished messages (service mode)
         nbytes=np.full(n, -1, np.int64),
         start=np.zeros(n),
         stop=np.zeros(n),
     )
-    if valid_workers is not None:
+    if valid_workers is not None and restr.any():
         flags = np.zeros(n, np.uint8)
-        vrows = [[] for _ in range(n)]
-        for i, ts in enumerate(tss):
-            if ts.worker_restrictions or ts.host_restrictions or ts.resource_restrictions:
-                vw = valid_workers(ts)
-                if vw is None:  # restrictions that exclude nobody
-                    continue
-                flags[i] = 1 | (2 if ts.loose_restrictions else 0)
-                vrows[i] = sorted(worker_index[ws.address] for ws in vw)
-        if flags.any():
+        vrows = {}
+        for i in np.flatnonzero(restr).tolist():
+            ts = tss[i]
+            vw = valid_workers(ts)
+            if vw is None:  # restrictions that exclude nobody
+                continue
+            flags[i] = 1 | (2 if ts.loose_restrictions else 0)
+            vrows[i] = sorted(worker_index[ws.address] for ws in vw)
+        if vrows:
+            rc = np.zeros(n, np.int64)
+            for i, r in vrows.items():
+                rc[i] = len(r)
             rp = np.zeros(n + 1, np.int64)
-            rp[1:] = np.cumsum([len(r) for r in vrows])
-            g.update(restr_ptr=rp, restr_idx=np.array([w for r in vrows for w in r], np.int32), restr_flags=flags)
-    return g, [ts.key for ts in tss]
+            np.cumsum(rc, out=rp[1:])
+            g.update(restr_ptr=rp, restr_idx=np.array([w for i in sorted(vrows) for w in vrows[i]], np.int32),
+                     restr_flags=flags)
+    return g, keys, prio
 
 
 class GPUPlacementExtension(SchedulerPlugin):
@@ -970,28 +1059,36 @@ class GPUPlacementExtension(SchedulerPlugin):
         if not self.active:
             return
         s = self.scheduler
-        new = [s.tasks[k] for k in (priority or {}) if k in s.tasks and k not in self.task_index]
+        # Scheduler.update_graph fills ``priority`` in descending TaskState.priority
+        # (scheduler.py:4601-4611): reversed, the tasks arrive in engine order
+        try:
+            new = list(map(s.tasks.__getitem__, reversed(priority or {})))
+        except KeyError:  # a key the scheduler no longer holds
+            new = [ts for ts in map(s.tasks.get, reversed(priority or {})) if ts is not None]
+        if self.task_index:
+            ti = self.task_index
+            new = [ts for ts in new if ts.key not in ti]
         if not new:
             return
         try:
             if self.engine is not None:
-                self._add_graph(new)
+                keys_ = self._add_graph(new)
             else:
                 self.workers = list(s.workers)
                 self.worker_index = {a: i for i, a in enumerate(self.workers)}
                 if any(ws.status.name != "running" for ws in s.workers.values()):
                     raise NotImplementedError("a worker is not running at the first graph")
-                g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers], s.valid_workers,
-                                            self.worker_index)
+                g, keys_, prio_ = graph_from_tasks(new, [s.workers[a].nthreads for a in self.workers],
+                                                   s.valid_workers, self.worker_index)
                 self.keys = keys_
-                self.task_index = {k: i for i, k in enumerate(keys_)}
+                self.task_index = dict(zip(keys_, range(len(keys_))))
                 self._remember_inputs(g, keys_)
                 self.prefix_index = {nm: i for i, nm in enumerate(g["prefix_names"])}
                 self.group_index = {nm: i for i, nm in enumerate(g["group_names"])}
                 self.prefix_dur = list(g["prefix_default_dur"])
                 self.group_prefix = list(g["group_prefix"])
-                self.max_priority = max(ts.priority for ts in new)
-                self.prio_of = [s.tasks[k].priority for k in keys_]  # engine index -> TaskState.priority
+                self.max_priority = prio_[-1]
+                self.prio_of = prio_  # engine index -> TaskState.priority
                 if self.engine_factory is not None:
                     self.engine = self.engine_factory()
                 else:
@@ -1008,16 +1105,17 @@ class GPUPlacementExtension(SchedulerPlugin):
                 self.engine.update_graph()
                 self._fetch()
                 self.stats["graphs"] += 1
-            if self.active:
-                self._window = (_UPDATE_GRAPH_TRANSITIONS, {ts.key for ts in new})
+            if self.active and keys_ is not None:  # the first graph's keys: the index's key view
+                self._window = (_UPDATE_GRAPH_TRANSITIONS,
+                                self.task_index.keys() if len(keys_) == len(self.task_index) else set(keys_))
         except Exception as e:  # plugin errors are logged, not raised (scheduler.py:4652-4653)
             self.fallback(f"update_graph: {e}")
 
     def _remember_inputs(self, g, keys_):
         """What the engine holds of each uploaded task's _rootish and restrictions."""
-        for i, k in enumerate(keys_):
-            if g["rootish_override"][i] >= 0:
-                self._rootish_h[k] = int(g["rootish_override"][i])
+        ro = g["rootish_override"]
+        for i in np.flatnonzero(ro >= 0).tolist():
+            self._rootish_h[keys_[i]] = int(ro[i])
         if "restr_flags" in g:
             rp, ri = g["restr_ptr"], g["restr_idx"]
             for i in np.flatnonzero(g["restr_flags"]):
@@ -1034,13 +1132,13 @@ class GPUPlacementExtension(SchedulerPlugin):
         earlier dependency is released / erred / forgotten (recomputed by the scheduler) is
         the stimulus the scheduler's own, the engine resynchronised after it (``_suspend``)."""
         s = self.scheduler
-        g, keys_ = graph_from_tasks(new, [s.workers[a].nthreads if a in s.workers else 1 for a in self.workers],
+        g, keys_, prio_ = graph_from_tasks(new, [s.workers[a].nthreads if a in s.workers else 1 for a in self.workers],
                                     s.valid_workers, self.worker_index, earlier=self.task_index)
         restricted = "restr_flags" in g  # its stimulus the scheduler's, then the rows (dgp_update_restrictions)
         # a user priority that outranks earlier tasks (_set_priorities :4934-4981): the engine
         # takes every task's rank in the merged order (dgp_set_priorities) and the stimulus is
         # the scheduler's, then a resync
-        outranks = min(ts.priority for ts in new) <= self.max_priority
+        outranks = prio_[0] <= self.max_priority
         if outranks and not hasattr(self.engine, "set_priorities"):
             raise NotImplementedError("a later graph whose tasks do not all follow the earlier ones in priority")
         pmap = np.zeros(len(g["prefix_names"]), np.int32)
@@ -1062,15 +1160,15 @@ class GPUPlacementExtension(SchedulerPlugin):
                   group_prefix=np.array(self.group_prefix, np.int32))
         self._end_of_stimulus("the previous stimulus")
         if not self.active:
-            return
+            return None
         dependent = bool((g["dep_idx"] < 0).any())
         if restricted or outranks:
             self.engine.add_graph(g2, defer=True)
         else:
             self.engine.add_graph(g2)
         self.keys = self.keys + keys_
-        self.task_index.update({k: n0 + i for i, k in enumerate(keys_)})
-        self.prio_of = self.prio_of + [s.tasks[k].priority for k in keys_]
+        self.task_index.update(zip(keys_, range(n0, n0 + len(keys_))))
+        self.prio_of = self.prio_of + prio_
         if outranks:  # every task's rank in the merged order (forgotten tasks keep theirs)
             order = sorted(range(len(self.prio_of)), key=self.prio_of.__getitem__)
             rank = np.empty(len(order), np.int64)
@@ -1079,7 +1177,7 @@ class GPUPlacementExtension(SchedulerPlugin):
             self.stats["reranked_graphs"] += 1
         g.pop("restr_flags", None)  # the rows go to the engine below (dgp_update_restrictions)
         self._remember_inputs(g, keys_)
-        self.max_priority = max(self.max_priority, max(ts.priority for ts in new))
+        self.max_priority = max(self.max_priority, prio_[-1])
         self.stats["graphs"] += 1
         if dependent or restricted or outranks:
             if not outranks:
@@ -1091,13 +1189,14 @@ class GPUPlacementExtension(SchedulerPlugin):
                 if self.active and self.engine.graph_stimulus() is not None:
                     self.stats["graph_stimuli_on_device"] += 1
                     self._fetch()
-                    return
+                    return keys_
             self._suspend("a later graph that depends on earlier tasks" if dependent else
                           "a later graph with restrictions" if restricted else "a later graph that outranks earlier tasks")
             for k in keys_:  # the new tasks, the earlier ones they wait on / add waiters to
                 self._mark_dirty(k)
-            return
+            return keys_
         self._fetch()
+        return keys_
 
     def add_worker(self, scheduler=None, worker=None):
         """SchedulerPlugin.add_worker (diagnostics/plugin.py): Scheduler.add_worker calls it

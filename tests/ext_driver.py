@@ -1189,6 +1189,60 @@ def run_events(name, plain=False):
                 calls=dict(ext.stats))
 
 
+class NullEngine:
+    """The engine interface with nothing behind it: times the extension's own graph
+    ingestion (TaskState -> the engine's arrays) apart from any engine."""
+
+    def load(self, g, config, results=True):
+        self.graph = g
+
+    def set_resident(self, on=True):
+        pass
+
+    def set_task_messages(self, on=True):
+        pass
+
+    def update_graph(self):
+        return 0
+
+    def num_placements(self):
+        return 0
+
+    def close(self):
+        pass
+
+
+def run_ingest(n, workers=1024, repeat=3):
+    """f4 ingestion: the extension's update_graph hook on an n-task C2-shaped graph of
+    reference TaskStates (graph_from_tasks: ordering, dependency CSR, prefix / group /
+    wanted / _rootish / restriction columns, and the extension's own index tables), with an
+    engine that does nothing; the upload is checked against the graph it was built from."""
+    from distributed_amd import graphs
+
+    g = graphs.random_dag(n, workers, seed=5)
+    g["keys"] = None
+    s, tss, widx, rec, tidx = G.build_state(g, {"bandwidth": 100_000_000})
+    fkeys = [ts.key for ts in tss]
+    # as Scheduler.update_graph hands it to the plugins: descending priority (:4601-4611)
+    priority = {ts.key: ts.priority for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
+    best = None
+    for _ in range(repeat):
+        eng = NullEngine()
+        ext = GPUPlacementExtension(s, engine_factory=lambda: eng)
+        s.stream_handlers = {}
+        ext._install()
+        t0, c0 = _time.perf_counter(), _time.process_time()
+        ext.update_graph(s, client="client-0", keys=set(priority), tasks=list(priority), annotations={},
+                         priority=priority, dependencies={})
+        dt, dc = _time.perf_counter() - t0, _time.process_time() - c0
+        assert ext.active, ext.reason
+        check_upload(eng.graph, ext.keys, g, fkeys)
+        best = min(best or (dt, dc), (dt, dc))
+    return dict(mode="ingest", n_tasks=n, n_workers=workers, n_edges=int(g["dep_ptr"][-1]),
+                seconds=round(best[0], 4), us_per_task=round(1e6 * best[0] / n, 3),
+                cpu_us_per_task=round(1e6 * best[1] / n, 3))
+
+
 if __name__ == "__main__":
     import warnings
 
@@ -1198,6 +1252,9 @@ if __name__ == "__main__":
     plain = "--plain" in args
     stream = "--stream" in args
     for nm in [a for a in args if not a.startswith("--")]:
+        if "--ingest" in args:
+            print(json.dumps(run_ingest(int(nm))), flush=True)
+            continue
         if "--ab" in args:
             print(json.dumps(run_ab(nm)), flush=True)
             continue

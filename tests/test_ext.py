@@ -9,6 +9,7 @@ import json
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 from conftest import REPO
@@ -42,6 +43,16 @@ def test_extension_places_every_task_from_the_engine():
     for r in res:
         assert r["active"] and r["device_decisions"] == r["placements"], r
     assert next(r for r in res if r["fixture"] == "restr_noworker_sat1.1.npz")["device_no_worker"] > 0
+
+
+def test_extension_ingests_a_200k_graph_in_bulk():
+    """f4 ingestion (ext_driver.py --ingest): the extension's update_graph hook turns a 200k-task
+    C2-shaped graph of reference TaskStates into the engine's arrays (checked against the
+    graph they were built from) in about 2 us per task on this container; the bound here is
+    loose (shared CPU), the measured figure goes to DESIGN §7."""
+    (r,) = drive(["200000"], "--ingest")
+    assert r["n_tasks"] == 200000 and r["n_edges"] > 600000, r
+    assert r["us_per_task"] < 4.0, r
 
 
 def test_extension_batches_and_synchronous_calls():
@@ -222,10 +233,27 @@ def test_extension_hands_back_on_divergence():
         assert 0 < r["device_decisions"] < r["placements"], r
 
 
-def test_graph_from_tasks_layout():
-    """graph_from_tasks on plain stand-ins (no dask needed): priority order, CSR, ids."""
-    from types import SimpleNamespace as NS
+class NS:
+    """A plain object with identity hashing, like TaskState / TaskGroup / TaskPrefix."""
 
+    def __init__(self, **kw):
+        self.worker_restrictions = self.host_restrictions = self.resource_restrictions = None
+        self.__dict__.update(kw)
+
+
+@pytest.fixture(params=["c", "python"])
+def ingest(request, monkeypatch):
+    """graph_from_tasks through the C pass (libdgpingest.so) and through the Python passes."""
+    from distributed_amd import ext
+
+    if request.param == "c" and ext._ingest_lib() is None:
+        pytest.skip("libdgpingest.so not built")
+    monkeypatch.setattr(ext, "_FORCE_PY_INGEST", request.param == "python")
+    return request.param
+
+
+def test_graph_from_tasks_layout(ingest):
+    """graph_from_tasks on plain stand-ins (no dask needed): priority order, CSR, ids."""
     from distributed_amd.ext import graph_from_tasks
 
     P = {n: NS(name=n, duration_average=d) for n, d in (("a", -1.0), ("b", 0.5))}
@@ -234,8 +262,8 @@ def test_graph_from_tasks_layout():
     t1 = NS(key="y", priority=(0, 1, 2), dependencies=[], prefix=P["a"], group=G["a-1"], who_wants=None, _rootish=True)
     t2 = NS(key="z", priority=(0, 1, 9), dependencies=[t0, t1], prefix=P["b"], group=G["b-1"], who_wants={1},
             _rootish=None)
-    g, keys = graph_from_tasks([t2, t0, t1], [1, 2])
-    assert keys == ["y", "x", "z"]
+    g, keys, prio = graph_from_tasks([t2, t0, t1], [1, 2])
+    assert keys == ["y", "x", "z"] and prio == [(0, 1, 2), (0, 1, 5), (0, 1, 9)]
     assert g["dep_ptr"].tolist() == [0, 0, 0, 2] and g["dep_idx"].tolist() == [0, 1]
     assert g["prefix_names"] == ["a", "b"] and g["prefix_id"].tolist() == [0, 0, 1]
     assert g["prefix_default_dur"].tolist() == [-1.0, 0.5]
@@ -243,11 +271,54 @@ def test_graph_from_tasks_layout():
     assert g["wanted"].tolist() == [0, 0, 1] and g["rootish_override"].tolist() == [1, -1, -1]
 
 
-def test_graph_from_tasks_names_earlier_tasks():
+def test_graph_from_tasks_c_pass_equals_python_passes(monkeypatch):
+    """The C ingestion pass (csrc/dgp_ingest.c) and the Python passes give the same graph on
+    random stand-ins: shuffled input order, shared prefixes / groups, dependencies on
+    earlier tasks, wanted / _rootish / restricted rows."""
+    from distributed_amd import ext
+
+    if ext._ingest_lib() is None:
+        pytest.skip("libdgpingest.so not built")
+    rng = np.random.default_rng(4)
+    P = [NS(name=f"p{i}", duration_average=float(i) - 1) for i in range(5)]
+    G = [NS(name=f"g{i}", prefix=P[i % 5]) for i in range(12)]
+    earlier = {f"old{i}": 100 + i for i in range(20)}
+    olds = [NS(key=k) for k in earlier]
+    tss = []
+    for i in range(400):
+        gi = int(rng.integers(12))
+        deps = {tss[int(j)] for j in rng.integers(0, i, int(rng.integers(0, 5)))} if i else set()
+        deps |= {olds[int(j)] for j in rng.integers(0, 20, int(rng.integers(0, 2)))}
+        t = NS(key=f"t{i}", priority=(0, 1, i), dependencies=deps, prefix=G[gi].prefix, group=G[gi],
+               who_wants={1} if rng.random() < 0.1 else None,
+               _rootish=[None, True, False][int(rng.integers(3))],
+               loose_restrictions=bool(rng.random() < 0.5))
+        if rng.random() < 0.1:
+            t.worker_restrictions = {f"w{int(rng.integers(8))}"}
+        tss.append(t)
+    order = [tss[int(i)] for i in rng.permutation(len(tss))]
+    workers = [NS(address=f"w{i}") for i in range(8)]
+    widx = {ws.address: i for i, ws in enumerate(workers)}
+
+    def valid_workers(ts):
+        return {ws for ws in workers if ws.address in ts.worker_restrictions}
+
+    out = {}
+    for mode in ("c", "python"):
+        monkeypatch.setattr(ext, "_FORCE_PY_INGEST", mode == "python")
+        out[mode] = ext.graph_from_tasks(order, [1] * 8, valid_workers, widx, earlier=earlier)
+    (gc_, kc, pc), (gp, kp, pp) = out["c"], out["python"]
+    assert kc == kp == [f"t{i}" for i in range(400)] and pc == pp
+    assert set(gc_) == set(gp) and "restr_flags" in gc_
+    for k in gc_:
+        a, b = gc_[k], gp[k]
+        assert (np.array_equal(a, b) if isinstance(a, np.ndarray) else a == b), k
+    assert (gc_["dep_idx"] < 0).any()
+
+
+def test_graph_from_tasks_names_earlier_tasks(ingest):
     """A later graph's dependency on an already uploaded task is named -1 - its engine index
     (dgp_add_graph); one outside both raises."""
-    from types import SimpleNamespace as NS
-
     from distributed_amd.ext import graph_from_tasks
 
     P = NS(name="p", duration_average=0.1)
@@ -255,7 +326,7 @@ def test_graph_from_tasks_names_earlier_tasks():
     old = NS(key="old", priority=(0, 1, 0), dependencies=[], prefix=P, group=G, who_wants=None, _rootish=None)
     a = NS(key="a", priority=(0, 2, 1), dependencies=[old], prefix=P, group=G, who_wants=None, _rootish=None)
     b = NS(key="b", priority=(0, 2, 2), dependencies=[a, old], prefix=P, group=G, who_wants=None, _rootish=None)
-    g, keys = graph_from_tasks([b, a], [1], earlier={"old": 7})
+    g, keys, _ = graph_from_tasks([b, a], [1], earlier={"old": 7})
     assert keys == ["a", "b"]
     assert g["dep_ptr"].tolist() == [0, 1, 3] and g["dep_idx"].tolist() == [-8, -8, 0]
     lost = NS(key="c", priority=(0, 2, 3), dependencies=[NS(key="zz")], prefix=P, group=G, who_wants=None,
