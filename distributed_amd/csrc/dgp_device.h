@@ -50,7 +50,8 @@ enum : uint8_t { WF_IDLE = 1, WF_SAT = 2, WF_ITC = 4, WF_PAUSED = 8 };
 // per-task dynamic flags (Dev::tdyn): TD_LR the task is in its worker's long_running
 // (add_to_long_running :747-757); TD_MULTI who_has is the task's holders bitset row (replicas
 // beyond the one completion made, add_replica / remove_replica :3148-3159), not holder_of
-enum : uint8_t { TD_LR = 1, TD_MULTI = 2 };
+// TD_READD / TD_REWAIT / TD_WHELD: marks of one worker-loss cascade (dgp_events.h), cleared by it
+enum : uint8_t { TD_LR = 1, TD_MULTI = 2, TD_READD = 4, TD_REWAIT = 8, TD_WHELD = 16 };
 // Dev::evf: which kinds of service events the engine has seen (each adds checks to the paths
 // that must honour it; the replay workloads never set any)
 enum : int32_t { EVF_MULTI = 1, EVF_LR = 2, EVF_PAUSED = 4 };
@@ -229,6 +230,7 @@ struct Dev {
   uint8_t* snap_flags;
   int32_t* snap_nqueued;
   int32_t lds_workers;  // commit kernel: worker state lives in dynamic LDS
+  int32_t needs_stream;  // needs_what lives in the stream engine's layout (gw_needs_saved / gw_needs_ext)
   Ctl* ctl;
   // ---- stream engine (dgp_stream.h)
   int32_t* gw_nproc;  // worker state in the stream layout when it does not fit in LDS
@@ -637,8 +639,111 @@ __device__ __forceinline__ uint32_t* needs_line(const Dev& D, int w) { return D.
 __device__ __forceinline__ bool needs_overflowed(const Dev& D, int w) {
   return needs_line(D, w)[NEEDS_W - 1] == NEEDS_OVF;
 }
+// The same operations on the stream engine's layout (dgp_stream.h needs_inc / needs_dec /
+// needs_reset, one lane instead of a wave): gw_needs_saved[w] = SNLW - 1 entries
+// (d << 8 | count) and a control word (entry count << 8, or SNL_OVF: scan mode), the rest in
+// gw_needs_ext[w] (SNXW entries). The update_graph dispatcher and the service-event
+// cascades place with these when the stream engine owns the worker state.
+constexpr int SNLW = 12, SNXW = 52;
+constexpr uint32_t SNL_OVF = 0xffffffffu;
+__device__ __forceinline__ int64_t res_nb(const Dev& D, int d) {
+  const int64_t v = D.res_nbytes[d];
+  return v >= 0 ? v : D.default_data_size;
+}
+__device__ int64_t sneeds_inc(const Dev& D, int w, int d, int t) {
+  uint32_t* L = D.gw_needs_saved + (size_t)w * SNLW;
+  uint32_t* X = D.gw_needs_ext + (size_t)w * SNXW;
+  const int64_t nb = res_nb(D, d);
+  const uint32_t ctl = L[SNLW - 1];
+  if (ctl == SNL_OVF) return needed_elsewhere(D, d, w, t) ? 0 : nb;
+  int used = 0, empty = -1;
+  for (int i = 0; i < SNLW - 1; i++) {
+    const uint32_t e = L[i];
+    if (e != 0 && (e >> 8) == (uint32_t)d) {
+      if ((e & 0xffu) == 0xffu) {
+        set_error(D, ERR_BAD_STATE, d);
+        return 0;
+      }
+      L[i] = e + 1;
+      return 0;
+    }
+    if (e != 0) used++;
+    else if (empty < 0) empty = i;
+  }
+  const int ext = (int)(ctl >> 8) - used;
+  int xempty = 0;
+  if (ext > 0) {
+    xempty = -1;
+    for (int i = 0; i < SNXW; i++) {
+      const uint32_t e = X[i];
+      if (e != 0 && (e >> 8) == (uint32_t)d) {
+        if ((e & 0xffu) == 0xffu) {
+          set_error(D, ERR_BAD_STATE, d);
+          return 0;
+        }
+        X[i] = e + 1;
+        return 0;
+      }
+      if (e == 0 && xempty < 0) xempty = i;
+    }
+  }
+  if (empty >= 0) {
+    L[empty] = ((uint32_t)d << 8) | 1u;
+    L[SNLW - 1] = ctl + 0x100u;
+    return nb;
+  }
+  if (ext < SNXW) {
+    X[xempty] = ((uint32_t)d << 8) | 1u;
+    L[SNLW - 1] = ctl + 0x100u;
+    return nb;
+  }
+  L[SNLW - 1] = SNL_OVF;  // full: scan mode
+  return nb;
+}
+__device__ int64_t sneeds_dec(const Dev& D, int w, int d, int t) {
+  uint32_t* L = D.gw_needs_saved + (size_t)w * SNLW;
+  uint32_t* X = D.gw_needs_ext + (size_t)w * SNXW;
+  const int64_t nb = res_nb(D, d);
+  const uint32_t ctl = L[SNLW - 1];
+  if (ctl == SNL_OVF) return needed_elsewhere(D, d, w, t) ? 0 : nb;
+  int used = 0;
+  for (int i = 0; i < SNLW - 1; i++) {
+    const uint32_t e = L[i];
+    if (e != 0 && (e >> 8) == (uint32_t)d) {
+      const uint32_t v = e - 1;
+      const bool gone = (v & 0xffu) == 0;
+      L[i] = gone ? 0u : v;
+      if (gone) L[SNLW - 1] = ctl - 0x100u;
+      return gone ? nb : 0;
+    }
+    used += e != 0;
+  }
+  if ((int)(ctl >> 8) - used > 0)
+    for (int i = 0; i < SNXW; i++) {
+      const uint32_t e = X[i];
+      if (e != 0 && (e >> 8) == (uint32_t)d) {
+        const uint32_t v = e - 1;
+        const bool gone = (v & 0xffu) == 0;
+        X[i] = gone ? 0u : v;
+        if (gone) L[SNLW - 1] = ctl - 0x100u;
+        return gone ? nb : 0;
+      }
+    }
+  if (D.evf & EVF_MULTI) return 0;  // a replica event may have removed the entry (add_replica :831-834)
+  set_error(D, ERR_BAD_STATE, d);
+  return 0;
+}
+__device__ void sneeds_reset(const Dev& D, int w) {  // a worker with nothing processing needs nothing
+  uint32_t* L = D.gw_needs_saved + (size_t)w * SNLW;
+  const uint32_t ctl = L[SNLW - 1];
+  if (ctl == SNL_OVF || (ctl >> 8) != 0)
+    for (int i = 0; i < SNXW; i++) D.gw_needs_ext[(size_t)w * SNXW + i] = 0u;
+  for (int i = 0; i < SNLW; i++) L[i] = 0u;
+}
+
 // _inc_needs_replica: bytes w newly needs (0 if d was needed already); t = task being placed
 __device__ int64_t needs_inc(const Dev& D, int w, int d, int t) {
+  if (D.needs_stream) return sneeds_inc(D, w, d, t);
   uint32_t* line = needs_line(D, w);
   if (line[NEEDS_W - 1] != NEEDS_OVF) {
     const uint32_t key = (uint32_t)d << 8;
@@ -669,6 +774,7 @@ __device__ int64_t needs_inc(const Dev& D, int w, int d, int t) {
 }
 // _dec_needs_replica (only when d is in needs_what); t = task leaving w (processing_on cleared)
 __device__ int64_t needs_dec(const Dev& D, int w, int d, int t) {
+  if (D.needs_stream) return sneeds_dec(D, w, d, t);
   uint32_t* line = needs_line(D, w);
   if (line[NEEDS_W - 1] != NEEDS_OVF) {
     const uint32_t key = (uint32_t)d << 8;
@@ -689,6 +795,10 @@ __device__ int64_t needs_dec(const Dev& D, int w, int d, int t) {
 }
 // a worker with nothing processing needs nothing: leave scan mode
 __device__ __forceinline__ void needs_maybe_reset(const Dev& D, int w) {
+  if (D.needs_stream) {
+    if (WK_nproc(D)[w] == 0) sneeds_reset(D, w);
+    return;
+  }
   uint32_t* line = needs_line(D, w);
   if (line[NEEDS_W - 1] == NEEDS_OVF && WK_nproc(D)[w] == 0)
     for (int i = 0; i < NEEDS_W; i++) line[i] = 0;
@@ -1373,7 +1483,7 @@ __device__ int64_t gather_pool(const Dev& D, bool use_idle, int32_t* list, int c
   int64_t base = 0;
   for (int w0 = 0; w0 < D.W; w0 += blockDim.x) {
     int w = w0 + threadIdx.x;
-    bool in = w < D.W && (!use_idle || (WK_flags(D)[w] & WF_IDLE));
+    bool in = w < D.W && (use_idle ? (WK_flags(D)[w] & WF_IDLE) : !(WK_flags(D)[w] & WF_PAUSED));
     int64_t tot;
     int64_t pos = block_excl_scan(in ? 1 : 0, &tot);
     if (in && base + pos < cap) list[base + pos] = w;
@@ -1468,7 +1578,8 @@ __device__ int dispatch_prepare(const Dev& D, int x, CoopShared& S, int64_t* sta
   if (D.tflags[x] & TF_ROOTISH) {
     if (D.sat_inf) {  // decide_worker_rootish_queuing_disabled :2135-2193
       int gi = D.group[x];
-      if (D.g_lastw[gi] >= 0 && D.g_left[gi] != 0) {
+      // last_worker, while it has tasks left and still runs (:2168-2171)
+      if (D.g_lastw[gi] >= 0 && D.g_left[gi] != 0 && !(WK_flags(D)[D.g_lastw[gi]] & WF_PAUSED)) {
         int w = D.g_lastw[gi];
         D.g_lastw[gi] = D.g_relwait[gi] > 1 ? w : -1;
         D.g_left[gi] -= 1;
@@ -1511,8 +1622,9 @@ __device__ int dispatch_prepare(const Dev& D, int x, CoopShared& S, int64_t* sta
     place_eager(D, x, best, ROUTE_NONROOTISH, bcomm, stage_next, dur);
     return OP_NONE;
   }
-  // no-dependency fast path :2283-2305
+  // no-dependency fast path :2283-2305 (pool = idle, else running)
   bool use_idle = c->n_idle > 0;
+  if (!use_idle && (D.evf & EVF_PAUSED)) return OP_KTH;  // a paused / removed worker: the pool is counted there
   int64_t n = use_idle ? c->n_idle : D.W;
   if (n >= 20 && !use_idle) {
     place_eager(D, x, (int)(c->n_tasks % n), ROUTE_FASTPATH, -1, stage_next, dur);
@@ -1531,7 +1643,7 @@ __device__ __attribute__((noinline)) void dispatch_collective(const Dev& D, Coop
     int64_t bcomm = 0;
     bool have = false;
     for (int w = threadIdx.x; w < D.W; w += blockDim.x) {
-      if (use_idle && !(WK_flags(D)[w] & WF_IDLE)) continue;
+      if (use_idle ? !(WK_flags(D)[w] & WF_IDLE) : (WK_flags(D)[w] & WF_PAUSED)) continue;  // idle, else running
       int64_t cm = comm_bytes(D, x, w);
       Obj o = objective(D, w, cm, dur);
       if (!have || obj_less(o, best)) {
@@ -1569,21 +1681,30 @@ __device__ __attribute__((noinline)) void dispatch_collective(const Dev& D, Coop
         if (holds(D, D.dep_idx[k], w)) return true;
       return false;
     };
+    // valid_workers & running: a paused / removed worker is never valid (:3099-3105)
+    auto run = [&](int w) { return !(WK_flags(D)[w] & WF_PAUSED); };
+    int64_t nval = 0;
+    for (int64_t i0 = r0; i0 < r1; i0 += blockDim.x) {
+      const int64_t i = i0 + threadIdx.x;
+      int64_t t1;
+      block_excl_scan(i < r1 && run(rr.idx[i]) ? 1 : 0, &t1);
+      nval += t1;
+    }
     int64_t tot = 0;
     for (int64_t i0 = r0; i0 < r1; i0 += blockDim.x) {
       const int64_t i = i0 + threadIdx.x;
       int64_t t1;
-      block_excl_scan(i < r1 && held(rr.idx[i]) ? 1 : 0, &t1);
+      block_excl_scan(i < r1 && run(rr.idx[i]) && held(rr.idx[i]) ? 1 : 0, &t1);
       tot += t1;
     }
     // 0: valid & holders, 1: valid, 2: holders (loose), 3: every worker (loose), 4: none
-    int mode = tot > 0 ? 0 : (r1 > r0 ? 1 : 4);
+    int mode = tot > 0 ? 0 : (nval > 0 ? 1 : 4);
     if (mode == 4 && (D.restr_flags[x] & RF_LOOSE)) {
       int64_t nh = 0;
       for (int w0 = 0; w0 < D.W; w0 += blockDim.x) {
         const int w = w0 + threadIdx.x;
         int64_t t1;
-        block_excl_scan(w < D.W && held(w) ? 1 : 0, &t1);
+        block_excl_scan(w < D.W && run(w) && held(w) ? 1 : 0, &t1);
         nh += t1;
       }
       mode = nh > 0 ? 2 : 3;
@@ -1603,11 +1724,11 @@ __device__ __attribute__((noinline)) void dispatch_collective(const Dev& D, Coop
     if (mode <= 1) {
       for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
         const int w = rr.idx[i];
-        if (mode == 1 || held(w)) consider(w);
+        if (run(w) && (mode == 1 || held(w))) consider(w);
       }
     } else if (mode <= 3) {
       for (int w = threadIdx.x; w < D.W; w += blockDim.x)
-        if (mode == 3 || held(w)) consider(w);
+        if (run(w) && (mode == 3 || held(w))) consider(w);
     }
     ArgBest b = block_argmin(best, bcomm, have);
     if (threadIdx.x == 0) {
@@ -1622,14 +1743,20 @@ __device__ __attribute__((noinline)) void dispatch_collective(const Dev& D, Coop
   } else {  // fast path over an ordered pool
     bool use_idle = c->n_idle > 0;
     int64_t n = gather_pool(D, use_idle, S.pool, 32);
-    if (op == OP_KTH) {
+    if (n == 0) {  // no running worker: no-worker (:2289-2290)
+      if (threadIdx.x == 0) {
+        D.state[x] = S_NO_WORKER;
+        atomicAdd((unsigned long long*)&D.g_relwait[D.group[x]], (unsigned long long)-1ll);
+        c->n_unrunnable++;
+      }
+    } else if (op == OP_KTH && n >= 20) {
       // pool[n_tasks % n] — n >= 20 idle workers: find the k-th idle worker
       int64_t k = c->n_tasks % n;
       int64_t base = 0;
       __shared__ int s_kth;
       for (int w0 = 0; w0 < D.W; w0 += blockDim.x) {
         int w = w0 + threadIdx.x;
-        bool in = w < D.W && (WK_flags(D)[w] & WF_IDLE);
+        bool in = w < D.W && (use_idle ? (WK_flags(D)[w] & WF_IDLE) : !(WK_flags(D)[w] & WF_PAUSED));
         int64_t tot;
         int64_t pos = block_excl_scan(in ? 1 : 0, &tot);
         if (in && base + pos == k) s_kth = w;
@@ -2004,15 +2131,14 @@ __global__ void k_frontier_release(const Dev* __restrict__ Dp) {
 
 // one wave per newly ready task: candidate workers (OR of the dependencies' replica
 // bitsets) and, per candidate, the exact comm bytes (total minus what it holds)
-__device__ void candidate_body(const Dev& D, int64_t wave, int64_t nwaves) {
+// one wave: task x's candidates (pool entries from ctl->pool_used on)
+__device__ void candidate_row(const Dev& D, int x) {
   const int lane = threadIdx.x & 63;
-  const int64_t nF = (int64_t)D.ctl->n_frontier;
-  for (int64_t i = wave; i < nF; i += nwaves) {
-    int x = D.frontier[i];
+  {
     int64_t d0 = D.dep_ptr[x], d1 = D.dep_ptr[x + 1];
     if (d1 == d0 || (D.tflags[x] & TF_ROOTISH) || restricted_nonrootish(D, x)) {
       if (lane == 0) D.cand_n[x] = 0;
-      continue;
+      return;
     }
     int64_t tot = 0;
     for (int64_t k = d0 + lane; k < d1; k += 64) tot += get_nbytes(D, D.dep_idx[k]);
@@ -2033,7 +2159,7 @@ __device__ void candidate_body(const Dev& D, int64_t wave, int64_t nwaves) {
       if (base + total_c > D.pool_cap) set_error(D, ERR_POOL, x);
     }
     base = __shfl(base, 0);
-    if (base + total_c > D.pool_cap) continue;
+    if (base + total_c > D.pool_cap) return;
     int64_t pos = base;
     for (int wd0 = 0; wd0 < D.WB; wd0 += 64) {
       int wd = wd0 + lane;
@@ -2068,6 +2194,10 @@ __device__ void candidate_body(const Dev& D, int64_t wave, int64_t nwaves) {
       D.cand_n[x] = total_c;
     }
   }
+}
+__device__ void candidate_body(const Dev& D, int64_t wave, int64_t nwaves) {
+  const int64_t nF = (int64_t)D.ctl->n_frontier;
+  for (int64_t i = wave; i < nF; i += nwaves) candidate_row(D, D.frontier[i]);
 }
 
 __global__ void k_candidate_commbytes(const Dev* __restrict__ Dp) {

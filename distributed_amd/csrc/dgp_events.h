@@ -387,6 +387,285 @@ __global__ void __launch_bounds__(64) k_ev_task_erred(const Dev* __restrict__ Dp
   if (lane == 0) *placed = n;
 }
 
+// ================================================================= worker loss (f2)
+// Scheduler.remove_worker (scheduler.py:5180-5303) of a worker with processing tasks or
+// sole replicas, decided here instead of by the scheduler. The host passes the worker's
+// processing tasks in the order the scheduler iterates ws.processing and its replicas in
+// ws.has_what order (the recommendations' order, :5235-5278). Then, as the reference:
+//   * the worker leaves running / idle / idle_task_count / saturated (:5226-5231);
+//   * remove_replica for each replica (:5270-5271): a task left with none is lost;
+//   * recommendations {processing task: released, ..., lost task: released, ...} run
+//     through SchedulerState._transitions (:2045-2076): a dict popped LIFO, each
+//     transition's recommendations merged with dict.update (a key already present keeps its
+//     place). The transitions a loss reaches are restated one by one:
+//       processing -> released  _transition_processing_released :2606-2628
+//                               (_exit_processing_common :3258-3281, _propagate_released
+//                               :3337-3357); -> waiting goes through released (:1961-1984)
+//       released -> waiting     _transition_released_waiting :2078-2119
+//       memory -> released      _transition_memory_released :2444-2505 (a lost task)
+//       waiting -> processing   decide_worker* + _add_to_processing: the update_graph
+//                               dispatcher's own (dispatch_prepare / dispatch_collective)
+//     A case outside these (a dependency to recompute, a queued or no-worker dependent, a
+//     task nobody needs any more) is reported as ERR_UNSUPPORTED; the host checks for them
+//     before it calls (dgp_lose_worker), so this is a guard.
+// One CTA: lane 0 runs the recommendation machine; a placement takes wave 0 (candidates)
+// and, for its collectives, the whole block. Scratch: D.frontier / D.ready = the
+// recommendation stack (task, finish), D.ready_key = each task's place in it (-1: absent,
+// set by the host before the launch), D.release_key = the tasks marked TD_READD / TD_REWAIT
+// (the round engine's key, unused by the stream engine).
+enum : int { RC_RELEASED = 0, RC_WAITING = 1, RC_PROCESSING = 2 };
+
+__device__ __forceinline__ void loss_mark(const Dev& D, long long& nmark, int t, uint8_t m) {
+  if (!(D.tdyn[t] & (TD_READD | TD_REWAIT))) D.release_key[nmark++] = (unsigned long long)t;
+  D.tdyn[t] |= m;
+}
+
+__device__ __forceinline__ void rec_push(const Dev& D, long long& sp, int t, int v) {
+  long long* at = (long long*)D.ready_key;
+  const long long p = at[t];
+  if (p >= 0) {  // dict.update on a present key: the value changes, the place stays
+    D.ready[p] = v;
+    return;
+  }
+  at[t] = sp;
+  D.frontier[sp] = t;
+  D.ready[sp] = v;
+  sp++;
+}
+
+// WorkerState.remove_from_processing (:759-771) of t on its worker x, then (a current
+// worker) check_idle_saturated (:3278). needs_what membership is the line's (the removed
+// worker's replicas are gone already: TD_WHELD names what it held, for scan mode).
+__device__ void loss_exit_processing(const Dev& D, int t, int lost_w) {
+  const int x = D.proc_on[t];
+  const int p = D.prefix[t];
+  uint32_t* L = D.gw_needs_saved + (size_t)x * SNLW;
+  int64_t freed = 0;
+  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+    const int d = D.dep_idx[k];
+    if (L[SNLW - 1] == SNL_OVF) {  // scan mode: needed iff not held and nobody else on x needs it
+      const bool held = x == lost_w ? (D.tdyn[d] & TD_WHELD) != 0 : holds_any(D, d, x);
+      if (!held && !needed_elsewhere(D, d, x, t)) freed += res_nb(D, d);
+      continue;
+    }
+    bool present = false;  // "if dts in self.needs_what" (:770)
+    for (int i = 0; i < SNLW - 1 && !present; i++) present = L[i] != 0 && (L[i] >> 8) == (uint32_t)d;
+    if (!present && (int)(L[SNLW - 1] >> 8) > 0)
+      for (int i = 0; i < SNXW && !present; i++) {
+        const uint32_t e = D.gw_needs_ext[(size_t)x * SNXW + i];
+        present = e != 0 && (e >> 8) == (uint32_t)d;
+      }
+    if (present) freed += sneeds_dec(D, x, d, t);
+  }
+  const int npw = D.w_nproc[x] - 1;
+  if (npw == 0) sneeds_reset(D, x);
+  if (D.tdyn[t] & TD_LR) {
+    D.w_cap[x] -= 1;
+    D.tdyn[t] &= (uint8_t)~TD_LR;
+  } else {
+    wdict_dec(D, x, p);
+    gdict_dec(D, p);
+  }
+  D.w_nproc[x] = npw;
+  D.w_netocc[x] -= freed;
+  D.ctl->g_netocc -= (double)freed;
+  D.proc_on[t] = -1;
+  if (x != lost_w) {  // _exit_processing_common: a removed worker is not checked (:3275-3276)
+    walk_flags(D, x, occupancy(D, x, D.pdur_walk), D.w_nproc[x]);
+    itc_check(D, x, true);
+  }
+}
+
+// _transition_released_waiting (:2078-2119) of t: waiting_on = the dependencies without a
+// replica; a dependency it (re-)joins as a waiter gains one (a lost task recomputed had left
+// its dependencies' waiters when it completed: TD_READD)
+__device__ void loss_released_waiting(const Dev& D, long long& sp, long long& nmark, int t) {
+  int wo = 0;
+  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+    const int d = D.dep_idx[k];
+    const uint8_t sd = D.state[d];
+    bool any = false;
+    for (int b = 0; b < D.WB && !any; b++) any = D.holders[(size_t)d * D.WB + b] != 0;
+    wo += any ? 0 : 1;
+    if (sd == S_RELEASED && (D.tdyn[d] & TD_READD)) {  // a result lost here, recomputed: its rec (:2105-2106)
+      rec_push(D, sp, d, RC_WAITING);
+      continue;
+    }
+    if (sd == S_RELEASED || sd == S_ERRED || (D.tflags[d] & TF_FORGOTTEN)) {  // a recompute chain / lost dependency
+      set_error(D, ERR_UNSUPPORTED, t);
+      return;
+    }
+    if (D.tdyn[t] & TD_READD) D.waiters[d] += 1;  // dts.waiters.add(ts) (:2108-2110)
+  }
+  D.state[t] = S_WAITING;
+  D.remaining[t] = wo;
+  loss_mark(D, nmark, t, TD_REWAIT);
+  D.tdyn[t] &= (uint8_t)~TD_READD;
+  if (wo == 0) rec_push(D, sp, t, RC_PROCESSING);
+}
+
+// lane 0: pop recommendations until one is a placement (returns its task) or none is left
+// (-1). ERR_UNSUPPORTED stops the machine.
+__device__ int loss_machine(const Dev& D, long long& sp, long long& nmark, int lost_w) {
+  long long* at = (long long*)D.ready_key;
+  while (sp > 0 && D.ctl->error == 0) {
+    sp--;
+    const int t = D.frontier[sp];
+    const int v = D.ready[sp];
+    at[t] = -1;
+    const uint8_t st = D.state[t];
+    if ((v == RC_RELEASED && st == S_RELEASED) || (v == RC_WAITING && st == S_WAITING) ||
+        (v == RC_PROCESSING && st == S_PROCESSING))
+      continue;  // start == finish (:1936-1937)
+    const bool needed = D.waiters[t] > 0 || (D.tflags[t] & TF_WANTED);
+    if (st == S_PROCESSING && (v == RC_RELEASED || v == RC_WAITING)) {
+      loss_exit_processing(D, t, lost_w);
+      D.state[t] = S_RELEASED;
+      atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], 1ull);
+      if (!needed) {  // _propagate_released would release its dependencies (:3346-3353)
+        set_error(D, ERR_UNSUPPORTED, t);
+        break;
+      }
+      rec_push(D, sp, t, RC_WAITING);  // :3343-3344
+      if (v == RC_WAITING) loss_released_waiting(D, sp, nmark, t);  // through released (:1961-1984)
+      continue;
+    }
+    if (st == S_RELEASED && v == RC_WAITING) {
+      loss_released_waiting(D, sp, nmark, t);
+      continue;
+    }
+    if (st == S_MEMORY && v == RC_RELEASED) {  // a lost result (:2444-2505): no replica is left
+      D.state[t] = S_RELEASED;
+      D.holder_of[t] = -1;
+      atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], 1ull);
+      if (needed) {
+        rec_push(D, sp, t, RC_WAITING);
+        loss_mark(D, nmark, t, TD_READD);
+      }
+      for (int64_t k = D.dpt_ptr[t]; k < D.dpt_ptr[t + 1]; k++) {  // its waiters (:2494-2500)
+        const int y = D.dpt_idx[k];
+        const uint8_t sy = D.state[y];
+        if (sy == S_PROCESSING) {
+          rec_push(D, sp, y, RC_WAITING);
+        } else if (sy == S_WAITING) {
+          if (!(D.tdyn[y] & TD_REWAIT)) D.remaining[y] += 1;  // waiting_on.add (a set)
+        } else if (sy == S_QUEUED || sy == S_NO_WORKER) {
+          set_error(D, ERR_UNSUPPORTED, y);
+          break;
+        }
+      }
+      continue;
+    }
+    if (st == S_WAITING && v == RC_PROCESSING) return t;  // decide_worker + _add_to_processing
+    set_error(D, ERR_UNSUPPORTED, t);
+  }
+  return -1;
+}
+
+__global__ void __launch_bounds__(CTA) k_ev_lose_worker(const Dev* __restrict__ Dp, int w, const int32_t* __restrict__ proc,
+                                                        int n_proc, const int32_t* __restrict__ held, int n_held,
+                                                        long long* placed) {
+  __shared__ Dev s_dev;  // Dev and Ctl in LDS, as the update_graph dispatcher works on them
+  __shared__ Ctl s_ctl;
+  {
+    const uint32_t* sd = (const uint32_t*)Dp;
+    const uint32_t* sc = (const uint32_t*)Dp->ctl;
+    for (int i = threadIdx.x; i < (int)(sizeof(Dev) / 4); i += blockDim.x) ((uint32_t*)&s_dev)[i] = sd[i];
+    for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += blockDim.x) ((uint32_t*)&s_ctl)[i] = sc[i];
+    __syncthreads();
+    if (threadIdx.x == 0) s_dev.ctl = &s_ctl;
+    __syncthreads();
+  }
+  Ctl* const ctl_g = Dp->ctl;
+  const Dev& D = s_dev;
+  Ctl* c = D.ctl;
+  __shared__ CoopShared S;
+  __shared__ long long s_sp, s_nmark;
+  __shared__ int s_x;
+  const int64_t pl0 = (int64_t)c->n_placed;
+  const double* dur = D.pdur_cur;
+  if (threadIdx.x == 0) {
+    // the worker table part (:5226-5231): out of running / idle / idle_task_count / saturated
+    D.w_flags[w] |= WF_PAUSED;
+    walk_flags(D, w, occupancy(D, w, D.pdur_walk), D.w_nproc[w]);
+    itc_check(D, w, false);
+    // remove_replica for every replica the worker holds (:5270-5271), in has_what order
+    for (int i = 0; i < n_held; i++) {
+      const int t = held[i];
+      unsigned long long* row = D.holders + (size_t)t * D.WB;
+      row[w >> 6] &= ~(1ull << (w & 63));
+      D.w_nbytes[w] -= res_nb(D, t);
+      D.tdyn[t] |= TD_WHELD;
+      if (D.holder_of[t] == w) {
+        int h = -1;
+        for (int b = 0; b < D.WB && h < 0; b++)
+          if (row[b]) h = b * 64 + __builtin_ctzll(row[b]);
+        D.holder_of[t] = h;
+      }
+    }
+    // the recommendations (:5235-5278): processing tasks, then the lost results
+    long long sp = 0;
+    for (int i = 0; i < n_proc; i++) rec_push(D, sp, proc[i], RC_RELEASED);
+    for (int i = 0; i < n_held; i++) {
+      const int t = held[i];
+      bool any = false;
+      for (int b = 0; b < D.WB && !any; b++) any = D.holders[(size_t)t * D.WB + b] != 0;
+      if (!any) rec_push(D, sp, t, RC_RELEASED);
+    }
+    s_sp = sp;
+    s_nmark = 0;
+  }
+  __syncthreads();
+  tree_rebuild_coop(D);
+  int64_t stage_next = 0;  // lane 0's staging cursor
+  while (true) {
+    if (threadIdx.x == 0) {
+      long long sp = s_sp, nmark = s_nmark;
+      s_x = loss_machine(D, sp, nmark, w);
+      s_sp = sp;
+      s_nmark = nmark;
+      c->pool_used = 0;
+    }
+    __syncthreads();
+    const int x = s_x;
+    if (x < 0) break;
+    if (threadIdx.x < 64) candidate_row(D, x);  // decide_worker's candidates (who_has rows)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      S.op = dispatch_prepare(D, x, S, &stage_next, dur);
+      S.x = x;
+    }
+    __syncthreads();
+    if (S.op != OP_NONE) dispatch_collective(D, S, &stage_next, dur);
+    __syncthreads();
+  }
+  // the cascade's marks go; its placements become the placement log's tail (run_id order)
+  __shared__ int64_t s_np;
+  if (threadIdx.x == 0) s_np = stage_next;
+  __syncthreads();
+  const long long nmark = s_nmark;
+  for (long long i = threadIdx.x; i < nmark; i += blockDim.x) {
+    const int t = (int)D.release_key[i];
+    D.tdyn[t] &= (uint8_t)~(TD_READD | TD_REWAIT);
+  }
+  for (int i = threadIdx.x; i < n_held; i += blockDim.x) D.tdyn[held[i]] &= (uint8_t)~TD_WHELD;
+  const int64_t np = s_np;
+  for (int64_t i = threadIdx.x; i < np; i += blockDim.x) {
+    D.pl_task[pl0 + i] = D.st_task[i];
+    D.pl_worker[pl0 + i] = D.st_worker[i];
+    D.pl_comm[pl0 + i] = D.st_comm[i];
+    D.pl_start[pl0 + i] = D.st_start[i];
+    D.pl_wsnbytes[pl0 + i] = D.st_wsnbytes[i];
+    D.pl_route[pl0 + i] = D.st_route[i];
+  }
+  if (threadIdx.x == 0) {
+    c->n_placed = pl0 + np;
+    *placed = np;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += blockDim.x) ((uint32_t*)ctl_g)[i] = ((const uint32_t*)&s_ctl)[i];
+}
+
 }  // namespace ev
 }  // namespace dgp
 

@@ -152,6 +152,7 @@ constexpr int BIG = 1 << 24;     // registration guard of a slot's predecessor c
 constexpr int T_CAND = 0x8000;   // touch-list entry flag: the worker is a frontier candidate (ids < 32768)
 constexpr int T_W = 0x7fff;
 constexpr uint32_t NL_OVF = 0xffffffffu;
+static_assert(NLW == SNLW && NXW == SNXW && NL_OVF == SNL_OVF, "dgp_device.h's one-lane needs_what ops use this layout");
 constexpr int N_ROLE = 5;        // waves 0..4 are SEQ, BLD, PRE, REG, WLK; the rest execute
 constexpr int E_HDR = 7;         // header entries: 0 ids, 1 sizes/counts, 2 duration, 3..6 durations
 // rows are selected with r & (DR - 1); PRE runs at most DR ahead and at least one window

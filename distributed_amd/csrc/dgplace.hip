@@ -333,6 +333,8 @@ int sync_dev(dgp_engine* e) {
     e->D.trace_n = n;
     HIPCHK(e, hipMemset(e->D.trace, 0, n * 32 * 8));
   }
+  // the stream engine owns the worker state (and its needs_what layout) whenever it runs
+  e->D.needs_stream = e->D.gw_needs_saved && e->D.P <= dgp::st::PX ? 1 : 0;
   dgp::Dev h[2] = {e->D, e->D};
   h[0].lds_workers = 0;
   h[1].lds_workers = e->D.W <= dgp::LDS_WORKERS_MAX ? 1 : 0;
@@ -1769,6 +1771,25 @@ int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr,
 
 namespace {
 int stage_args(dgp_engine* e, std::initializer_list<std::pair<const void*, size_t>> parts, std::vector<char*>& out);
+// is_rootish (:2929-2947) reads total_nthreads: the groups' flags follow a new total
+int refresh_rootish(dgp_engine* e) {
+  dgp::Dev& D = e->D;
+  std::vector<uint8_t> tf = e->tflags_h;
+  bool changed = false;
+  for (int64_t t = 0; t < D.N; t++) {
+    const int g = e->group_h[t];
+    const bool gr = e->group_sizes[g] > D.total_nthreads * 2 && e->gdep_n[g] < 5 && e->gdep_len[g] < 5;
+    const bool rs = !e->restr_h.empty() && (e->restr_h[t] & dgp::RF_RESTRICTED);
+    const bool r = e->rootish_override_h[t] >= 0 ? e->rootish_override_h[t] != 0 : (gr && !rs);
+    tf[t] = (uint8_t)((tf[t] & ~dgp::TF_ROOTISH) | (r ? dgp::TF_ROOTISH : 0));
+    changed = changed || tf[t] != e->tflags_h[t];
+  }
+  if (changed) {
+    HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), tf.data(), D.N, hipMemcpyHostToDevice));
+    e->tflags_h = tf;
+  }
+  return 0;
+}
 // every earlier task a new one depends on gains it as a waiter (_transition_released_waiting
 // :2094-2099: dts.waiters.add(ts) for a dependency that is not released)
 __global__ void k_add_waiters(int32_t* waiters, const int32_t* dep, const int32_t* cnt, int64_t n) {
@@ -2295,6 +2316,56 @@ int dgp_remove_worker(dgp_engine* e, int32_t worker) {
     if (int rc = dgp_set_worker_status(e, worker, 0, &placed)) return rc;
   e->paused_h[worker] = 2;
   e->D.total_nthreads -= e->nthreads[worker];
+  return refresh_rootish(e);
+}
+
+int dgp_lose_worker(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing, int64_t n_held,
+                    const int32_t* held, int64_t* n_new_placements) {
+  if (int rc_ = resident_stop(e)) return rc_;
+  if (n_new_placements) *n_new_placements = 0;
+  if (int rc = event_ready(e, "dgp_lose_worker")) return rc;
+  dgp::Dev& D = e->D;
+  if (worker < 0 || worker >= D.W) return fail(e, DGP_E_ARG, "dgp_lose_worker: worker out of range");
+  if (e->paused_h[worker] == 2) return fail(e, DGP_E_ARG, "dgp_lose_worker: the worker was removed");
+  if (n_processing < 0 || n_held < 0 || n_processing > D.N || n_held > D.N || (n_processing && !processing) ||
+      (n_held && !held))
+    return fail(e, DGP_E_ARG, "dgp_lose_worker: bad task lists");
+  for (int64_t i = 0; i < n_processing; i++)
+    if (processing[i] < 0 || processing[i] >= D.N) return fail(e, DGP_E_ARG, "dgp_lose_worker: task out of range");
+  for (int64_t i = 0; i < n_held; i++)
+    if (held[i] < 0 || held[i] >= D.N) return fail(e, DGP_E_ARG, "dgp_lose_worker: task out of range");
+  // decide_worker_non_rootish takes valid_workers = running when a worker is paused
+  // (:2262-2266): the dispatcher's candidates are the who_has rows, so no other worker may be
+  // paused (a removed one holds nothing)
+  for (int32_t v = 0; v < D.W; v++)
+    if (v != worker && e->paused_h[v] == 1)
+      return fail(e, DGP_E_UNSUPPORTED, "dgp_lose_worker: another worker is paused: dgp_sync_* instead");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  // Scheduler.remove_worker's host part (:5217-5218): total_nthreads, which is_rootish reads
+  e->paused_h[worker] = 2;
+  D.total_nthreads -= e->nthreads[worker];
+  D.evf |= dgp::EVF_PAUSED;
+  if (int rc = refresh_rootish(e)) return rc;
+  HIPCHK(e, hipMemsetAsync(D.ready_key, 0xff, (size_t)D.N * 8, e->stream));  // the recommendation dict: empty
+  std::vector<char*> a;
+  if (int rc = stage_args(e, {{processing, (size_t)n_processing * 4}, {held, (size_t)n_held * 4}}, a)) return rc;
+  if (int rc = grow_logs(e, 0)) return rc;
+  if (int rc = sync_dev(e)) return rc;
+  hipLaunchKernelGGL(dgp::ev::k_ev_lose_worker, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev, worker,
+                     (const int32_t*)a[0], (int)n_processing, (const int32_t*)a[1], (int)n_held, e->d_aux + 3);
+  HIPCHK(e, hipGetLastError());
+  if (int rc = set_runids(e)) return rc;
+  long long placed = 0;
+  HIPCHK(e, hipMemcpyAsync(&placed, e->d_aux + 3, sizeof placed, hipMemcpyDeviceToHost, e->stream));
+  dgp::Ctl c;
+  if (int rc = check_device_error(e, &c)) {
+    // the cascade stopped part-way: the engine's state is the scheduler's to hand over
+    e->pending_resync = true;
+    return c.error == dgp::ERR_UNSUPPORTED ? fail(e, DGP_E_UNSUPPORTED, std::string(e->err)) : rc;
+  }
+  if (n_new_placements) *n_new_placements = placed;
+  e->last_placed = c.n_placed;
   return 0;
 }
 

@@ -381,6 +381,7 @@ class PlacementEngine:
         newp = C.c_int64(0)
         rc = self.lib.dgp_graph_stimulus(self.h, C.byref(newp))
         if rc == self.UNSUPPORTED:
+            self.refusal = (self.lib.dgp_last_error(self.h) or b"").decode()
             return None
         self._check(rc, "dgp_graph_stimulus")
         return int(newp.value)
@@ -475,6 +476,22 @@ class PlacementEngine:
     def remove_worker(self, worker: int):
         """Scheduler.remove_worker's worker table part (distributed/scheduler.py:5213-5231)."""
         self._check(self.lib.dgp_remove_worker(self.h, int(worker)), "dgp_remove_worker")
+
+    def lose_worker(self, worker: int, processing, held) -> int | None:
+        """The whole Scheduler.remove_worker stimulus (distributed/scheduler.py:5180-5303) on
+        the device (dgp_lose_worker): ``processing`` = the worker's processing tasks in the
+        order the scheduler iterates them, ``held`` = its replicas in ws.has_what order.
+        Returns the placements it made, or None when the engine leaves the stimulus to the
+        scheduler (another worker paused, or a cascade it does not restate); after a refusal
+        from the device the scheduler's state follows by ``sync()`` as after remove_worker."""
+        p, h = self._arr(processing, np.int32), self._arr(held, np.int32)
+        newp = C.c_int64(0)
+        rc = self.lib.dgp_lose_worker(self.h, int(worker), len(p), _ptr(p), len(h), _ptr(h), C.byref(newp))
+        if rc == self.UNSUPPORTED:
+            self.refusal = (self.lib.dgp_last_error(self.h) or b"").decode()
+            return None
+        self._check(rc, "dgp_lose_worker")
+        return int(newp.value)
 
     def sync_placements(self, task, worker, comm, start, wsnbytes, route):
         """Append placements the scheduler made itself (their run identity: log position)."""

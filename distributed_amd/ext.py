@@ -88,6 +88,11 @@ _REFILL_TRANSITIONS = _ADD_WORKER_TRANSITIONS
 # waits for released, then the queue refill
 _ERRED_TRANSITIONS = frozenset({("processing", "erred"), ("waiting", "released"), ("released", "erred"),
                                 ("memory", "released"), ("queued", "processing")})
+# a worker lost with processing tasks / sole replicas (Scheduler.remove_worker :5233-5303):
+# processing -> released (-> waiting through released, :1961-1984), memory -> released for the
+# lost results, released -> waiting, then decide_worker
+_LOSS_TRANSITIONS = frozenset({("processing", "released"), ("released", "waiting"), ("memory", "released"),
+                               ("waiting", "processing"), ("waiting", "queued"), ("waiting", "no-worker")})
 
 # the placement inputs a stimulus other than task-finished / update_graph / add_worker can
 # change, and the engine method that follows each on the device (PlacementEngine); an engine
@@ -331,6 +336,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         self._dirty_all = False
         self._route = 0             # the decide_worker route of the scheduler's current decision
         self.removed: set = set()   # addresses of removed workers (they keep their engine index)
+        self._losing = None         # the worker whose loss the engine decided (its replica drops are the engine's)
         self._rootish_h: dict = {}  # key -> the _rootish override the engine holds (-1 / 0 / 1)
         self._restr_h: dict = {}    # key -> (restriction flags, valid worker indices) the engine holds
         # key -> (message batch, row): the who_has / nbytes of the compute-task message of an
@@ -414,6 +420,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         self._wrap_shuffle()
         self._wrap_replicas()
         self._wrap_stealing()
+        self._wrap_remove_worker()
 
     def _wrap(self, table, name, on_event, modelled, after=False):
         """Route stream / RPC handler ``name`` through the extension: ``on_event(kwargs)``
@@ -482,6 +489,100 @@ class GPUPlacementExtension(SchedulerPlugin):
                     leave()
         wrapped._gpu_placement = True
         table[name] = wrapped
+
+    def _wrap_remove_worker(self):
+        """``Scheduler.remove_worker`` (scheduler.py:5180-5362), from any caller (the
+        "unregister" RPC, heartbeat timeouts, retire_workers, close_worker): when the worker
+        still has processing tasks or sole replicas, the whole stimulus -- its processing
+        tasks released and re-placed, its lost results recomputed -- is the engine's
+        (dgp_lose_worker, ``_lose_worker``) before the scheduler's own code runs; its
+        transitions then take the engine's decisions (validated like any other). A loss the
+        engine does not restate keeps the old path: the scheduler decides, then a resync."""
+        s = self.scheduler
+        orig = getattr(s, "remove_worker", None)
+        if orig is None or getattr(orig, "_gpu_placement", False) or not inspect.iscoroutinefunction(orig):
+            return
+
+        @functools.wraps(orig)
+        async def remove_worker(*args, **kwargs):
+            self._enter()
+            address = args[0] if args else kwargs.get("address")
+            lost = False
+            if self.active and self.engine is not None:
+                try:
+                    lost = self._lose_worker(address, bool(kwargs.get("safe", False)))
+                except Exception as e:  # an engine failure ends GPU placement, never the scheduler
+                    self.fallback(f"remove_worker({address}): {e}")
+            self._allowed.append(_LOSS_TRANSITIONS if lost else frozenset())
+            try:
+                return await orig(*args, **kwargs)
+            finally:
+                self._allowed.pop()
+                self._losing = None
+
+        remove_worker._gpu_placement = True
+        s.remove_worker = remove_worker  # per instance: every self.remove_worker call goes through it
+        rpc = getattr(s, "handlers", None)
+        if isinstance(rpc, dict) and "unregister" in rpc:
+            rpc["unregister"] = remove_worker
+
+    @staticmethod
+    def _loss_supported(s, ws, proc, held, safe) -> bool:
+        """The losses dgp_lose_worker restates: no other worker paused, no processing task
+        that errs (KilledWorker, :5239-5265) or that nobody needs, and every lost result that
+        is needed has its dependencies in memory elsewhere and no queued / no-worker waiter."""
+        if len(s.running) < len(s.workers):
+            return False
+        for ts in proc:
+            if (not safe and ts.suspicious + 1 > s.allowed_failures) or not (ts.waiters or ts.who_wants):
+                return False
+            if ts.actor or ts.has_lost_dependencies:
+                return False
+        for ts in held:
+            if ts.who_has != {ws}:
+                continue
+            if not ts.run_spec or ts.actor or ts.has_lost_dependencies:
+                return False
+            if ts.who_wants or ts.waiters:
+                for d in ts.dependencies:
+                    if d.state != "memory" or d.who_has == {ws}:
+                        return False
+            for d in ts.waiters or ():
+                if d.state in ("queued", "no-worker"):
+                    return False
+                if d.state == "processing" and not (d.waiters or d.who_wants):
+                    return False
+        return True
+
+    def _lose_worker(self, address, safe) -> bool:
+        """The engine's half of a worker loss (see ``_wrap_remove_worker``): True when the
+        engine decided the stimulus (its placements are queued for the transitions)."""
+        s = self.scheduler
+        ws = s.workers.get(address)
+        if ws is None or address not in self.worker_index or self.suspended:
+            return False
+        if not hasattr(self.engine, "lose_worker"):
+            return False
+        proc, held = list(ws.processing), list(ws.has_what)  # the orders remove_worker iterates (:5236, :5270)
+        if not proc and not any(ts.who_has == {ws} for ts in held):
+            return False  # a drained worker: no transition (the plugin hook follows it)
+        ti = self.task_index
+        if (any(ts.key not in ti for ts in proc) or any(ts.who_has == {ws} and ts.key not in ti for ts in held)
+                or not self._loss_supported(s, ws, proc, held, safe)):
+            self.stats["losses_left_to_scheduler"] += 1
+            return False
+        self._end_of_stimulus("the previous stimulus")
+        if not self.active:
+            return False
+        n = self.engine.lose_worker(self.worker_index[address], [ti[ts.key] for ts in proc],
+                                    [ti[ts.key] for ts in held if ts.key in ti])
+        if n is None:  # refused: the scheduler decides, the engine resyncs after
+            self._suspend(f"remove_worker({address}): {getattr(self.engine, 'refusal', 'refused by the engine')}")
+            return False
+        self._losing = address
+        self.stats["workers_lost_on_device"] += 1
+        self._fetch(n)
+        return True
 
     def _wrap_replicas(self):
         """``SchedulerState.add_replica`` / ``remove_replica`` (scheduler.py:3148-3159) from
@@ -623,6 +724,8 @@ class GPUPlacementExtension(SchedulerPlugin):
             return
         if self.suspended:  # the resync carries it
             self._dirty.add(ts.key)
+            return
+        if sign < 0 and ws.address == self._losing:  # dgp_lose_worker dropped the lost worker's replicas
             return
         w = self.worker_index.get(ws.address)
         what = "add_replicas" if sign > 0 else "remove_replicas"
@@ -1243,9 +1346,11 @@ class GPUPlacementExtension(SchedulerPlugin):
         nothing processing and no last replica (retire_workers' drained worker: paused, its
         data copied elsewhere) runs no transition; its replicas went through the replica hook
         (dgp_remove_replicas) and the engine follows the removal on the device. Otherwise its
-        processing tasks were released and re-placed and its lost results recomputed by the
-        scheduler itself (the transition hook suspended the engine at the first of them), and
-        the engine takes the scheduler's state (dgp_sync_*)."""
+        processing tasks were released and re-placed and its lost results recomputed: by the
+        engine (dgp_lose_worker, decided in ``_wrap_remove_worker`` before the scheduler's
+        own code ran, whose transitions took those decisions), or, for a loss the engine does
+        not restate, by the scheduler itself (the transition hook suspended the engine at the
+        first of them) after which the engine takes the scheduler's state (dgp_sync_*)."""
         self._close_window()
         if not self.active or self.engine is None or worker not in self.worker_index:
             return
@@ -1253,6 +1358,9 @@ class GPUPlacementExtension(SchedulerPlugin):
         w = self.worker_index.pop(worker)
         self.removed.add(worker)
         self.workers[w] = worker + _REMOVED  # keeps its index and its place in address order
+        if worker == self._losing and on_device:  # dgp_lose_worker decided the whole stimulus
+            self._end_of_stimulus(f"remove_worker({worker})")
+            return
         try:
             self.engine.remove_worker(w)
         except Exception as e:

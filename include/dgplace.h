@@ -44,6 +44,8 @@
  *   dgp_task_erred        Scheduler.handle_task_erred (:5799-5805 -> stimulus_task_erred
  *                         :5094-5127)
  *   dgp_remove_worker     Scheduler.remove_worker's worker table (:5213-5231)
+ *   dgp_lose_worker       the whole Scheduler.remove_worker stimulus (:5180-5303): processing
+ *                         tasks released and re-placed, lost results recomputed (ABI 17)
  *   dgp_sync_*            the scheduler's state after a stimulus it decided itself
  *   dgp_snapshot          one per-worker snapshot (occupancy, nbytes, processing, idle /
  *                         saturated / idle_task_count, queue length) at a caller-chosen point
@@ -66,7 +68,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 16
+#define DGP_ABI_VERSION 17
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -369,6 +371,19 @@ int dgp_task_erred(dgp_engine* e, int32_t task, int64_t* n_new_placements);
  * total_nthreads); the rest of that stimulus (its processing tasks released and re-placed,
  * lost results recomputed, :5233-5300) is the scheduler's, synchronised as above. */
 int dgp_remove_worker(dgp_engine* e, int32_t worker);
+/* dgp_lose_worker: Scheduler.remove_worker (scheduler.py:5180-5303) of a worker that still
+ * has processing tasks or sole replicas, decided on the device: the worker leaves the tables,
+ * every replica it holds is removed (held: ws.has_what in its order), and the recommendations
+ * {processing[i]: released..., lost results: released...} run through the transitions
+ * (processing -> released -> waiting, memory -> released -> waiting, waiting -> processing
+ * with decide_worker), LIFO as SchedulerState._transitions pops them. processing: the
+ * worker's tasks in the order the scheduler iterates ws.processing. The placements append to
+ * the placement log (*n_new_placements). DGP_E_UNSUPPORTED: another worker is paused, or the
+ * cascade reaches a case the engine does not restate (a dependency to recompute, a queued or
+ * no-worker dependent, a task nobody needs); after a refusal from the device the engine
+ * takes the scheduler's state (dgp_sync_*) as after dgp_remove_worker. */
+int dgp_lose_worker(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing, int64_t n_held,
+                    const int32_t* held, int64_t* n_new_placements);
 int dgp_sync_placements(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* comm_bytes,
                         const double* start_time, const int64_t* ws_nbytes, const int8_t* route);
 int dgp_sync_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t* state, const int32_t* remaining,

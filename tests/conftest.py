@@ -18,7 +18,7 @@ def golden_files():
     """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
                   and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcgdep_", "svcev_",
-                                            "svcrs_", "svcrt_", "svcp2p_", "svcgrst_", "svcgprio_")))
+                                            "svcrs_", "svcrt_", "svcwl_", "svcp2p_", "svcgrst_", "svcgprio_")))
 
 
 def svc_second_graph_files():
@@ -83,6 +83,12 @@ def svc_resync_files():
 def svc_retire_files():
     """Service streams where drained workers retire, followed on the device (gen_service.py resync svcrt_*)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcrt_") and f.endswith(".npz"))
+
+
+def svc_loss_files():
+    """Service streams where workers with processing tasks / sole replicas are lost, decided
+    on the device (gen_service.py resync svcwl_*)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcwl_") and f.endswith(".npz"))
 
 
 def svc_p2p_files():

@@ -866,6 +866,11 @@ class EventEngine(FixtureEngine):
     def set_worker_status(self, w, running):
         return self._event("status", int(w), int(running))
 
+    def lose_worker(self, w, processing, held):  # dgp_lose_worker: the fixture's placements of that event
+        for s_ in self.who.values():
+            s_.discard(int(w))
+        return self._event("lose", int(w), [int(x) for x in processing], [int(x) for x in held])
+
     def long_running(self, t, cd):
         return self._event("long", int(t), float(cd))
 
@@ -936,7 +941,7 @@ def run_events(name, plain=False):
 
     from gen_service import (EV_ADD_KEYS, EV_ERRED, EV_FINISHED, EV_HEARTBEAT, EV_LONG_RUNNING, EV_PAUSE,
                              EV_RELEASE_DATA, EV_RELEASE_KEYS, EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RESTRICT,
-                             EV_RESUME, EV_RETIRE, EV_RETIRE_REPLICA, EV_SHUFFLE_INIT)
+                             EV_RESUME, EV_RETIRE, EV_RETIRE_REPLICA, EV_SHUFFLE_INIT, EV_LOSE_WORKER)
 
     from distributed_amd import sync as dsync
 
@@ -1052,6 +1057,7 @@ def run_events(name, plain=False):
     s._transitions(recs, {}, {}, "update-graph")
     want = []  # the engine calls the events imply
     n_sync = 0
+    on_device = set()  # EV_REMOVE_WORKER events the engine decided (dgp_lose_worker)
 
     def check_sync():
         """The last engine call is the resync of this event: its worker / global rows equal
@@ -1142,9 +1148,24 @@ def run_events(name, plain=False):
             want.append(("remove", w))
             assert ext.stats["resyncs"] == rs0 and not ext.suspended, (i, ext.stats)
             eng.k += 1  # the fixture's count for it (no placement)
+        elif kd == EV_LOSE_WORKER:  # a worker lost with work on it: the engine decides the stimulus
+            rs0, lw0 = ext.stats["resyncs"], ext.stats["workers_lost_on_device"]
+            lst = [int(q) for q in ht[hp[i]:hp[i + 1]]]
+            loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
+            want.append(("lose", w, lst[:int(x)], lst[int(x):]))
+            assert ext.stats["resyncs"] == rs0 and ext.stats["workers_lost_on_device"] == lw0 + 1, (i, ext.stats)
+            assert not ext.suspended, (i, ext.suspend_reason)
         elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
             if kd == EV_REMOVE_WORKER:
+                lw0 = ext.stats["workers_lost_on_device"]
                 loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
+                if ext.stats["workers_lost_on_device"] > lw0:  # a loss the engine restates: decided there
+                    assert eng.calls[-1][:2] == ("lose", w), eng.calls[-1]
+                    want.append(eng.calls[-1])
+                    on_device.add(i)
+                    n_sync += 1  # the fixture's resync rows of this event are not needed
+                    snap.pop("before", None)
+                    continue
                 want.append(("remove", w))
             elif kd == EV_RESCHEDULE:
                 H["reschedule"](key=tss[t].key, worker=addr[w], stimulus_id=sid)
@@ -1182,7 +1203,8 @@ def run_events(name, plain=False):
     assert rec["worker"] == exp["pl_worker"].tolist()
     assert np.array_equal(np.array(rec["start"]).view(np.int64), exp["pl_start"].view(np.int64))
     # the resync stimuli's placements are the scheduler's own, every other one the engine's
-    host = sum(int(exp["stim_nplaced"][1 + i]) for i, kd in enumerate(z["ev_kind"].tolist()) if kd >= EV_REMOVE_WORKER)
+    host = sum(int(exp["stim_nplaced"][1 + i]) for i, kd in enumerate(z["ev_kind"].tolist())
+               if kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS) and i not in on_device)
     assert ext.stats["device_decisions"] == n - host, (ext.stats, n, host)
     return dict(fixture=name, placements=n, events=len(want), device_decisions=ext.stats["device_decisions"],
                 host_placements=host, resyncs=ext.stats["resyncs"], active=ext.active, reason=ext.reason,
@@ -1260,7 +1282,8 @@ if __name__ == "__main__":
             continue
         fn = (run_joins if nm.startswith("svcaddw_") else (lambda x: run_second_graph(x, "--resync" in args))
               if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_"))
-              else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcrt_", "svcp2p_")) else None)
+              else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcrt_", "svcwl_", "svcp2p_"))
+              else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,
                                                plain="plugin" if "--plugin" in args else plain,
                                                validate="--novalidate" not in args)), flush=True)

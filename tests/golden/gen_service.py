@@ -617,6 +617,38 @@ EV_SHUFFLE_INIT, EV_RESTRICT = 11, 12
 # transition; EV_RETIRE_REPLICA records each replica remove_worker drops there (has_what
 # order), EV_RETIRE the removal itself. The engine follows it without a resync.
 EV_RETIRE, EV_RETIRE_REPLICA = 13, 14
+# a worker with processing tasks or sole replicas is lost (svcwl_*): Scheduler.remove_worker
+# releases and re-places its processing tasks and recomputes its lost results; the engine
+# decides the whole stimulus (dgp_lose_worker). hb_task holds the worker's processing tasks
+# in ws.processing iteration order (ev_x of them), then its replicas in ws.has_what order.
+EV_LOSE_WORKER = 15
+
+
+def _loss_is_supported(s, ws):
+    """The worker losses the engine decides itself (dgp_lose_worker; the extension checks the
+    same before it asks): no other worker paused, no processing task that errs
+    (KilledWorker) or that nobody needs, and every lost result that is needed has its
+    dependencies in memory elsewhere and no queued / no-worker dependent."""
+    if len(s.running) < len(s.workers):
+        return False
+    for ts in ws.processing:
+        if ts.suspicious + 1 > s.allowed_failures or not (ts.waiters or ts.who_wants) or ts.has_lost_dependencies:
+            return False
+    for ts in ws.has_what:
+        if ts.who_has != {ws}:
+            continue
+        if not ts.run_spec or ts.has_lost_dependencies:
+            return False
+        if ts.who_wants or ts.waiters:
+            for d in ts.dependencies:
+                if d.state != "memory" or d.who_has == {ws}:
+                    return False
+        for d in ts.waiters or ():
+            if d.state in ("queued", "no-worker"):
+                return False
+            if d.state == "processing" and not (d.waiters or d.who_wants):
+                return False
+    return True
 
 
 def _dump(s, g, tidx, widx, keys):
@@ -710,7 +742,7 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
     S.send_all = lambda self, client_msgs, worker_msgs: None
     S.worker_send = lambda self, worker, msg: None
     s.extensions = {}
-    if EV_REMOVE_WORKER in kinds or EV_RETIRE in kinds:  # what Scheduler.remove_worker touches besides placement state
+    if EV_REMOVE_WORKER in kinds or EV_RETIRE in kinds or EV_LOSE_WORKER in kinds:  # what Scheduler.remove_worker touches besides placement state
         import asyncio
         from collections import defaultdict
         from types import SimpleNamespace as NS
@@ -833,6 +865,28 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
             removed.add(w)
             push(EV_REMOVE_WORKER, -1, w)
+        elif kind == EV_LOSE_WORKER:
+            live = [i for i in range(W) if i not in removed]
+            if len(live) <= max(2, W // 2):
+                return
+            cand = []
+            for i in live:
+                ws = s.workers[addr[i]]
+                busy = bool(ws.processing) or any(ts.who_has == {ws} for ts in ws.has_what)
+                if busy and _loss_is_supported(s, ws):
+                    cand.append(i)
+            if not cand:
+                return
+            w = cand[int(rng.integers(0, len(cand)))]
+            ws = s.workers[addr[w]]
+            proc = [tidx[ts.key] for ts in ws.processing]  # the order remove_worker iterates (:5236)
+            held = [tidx[ts.key] for ts in ws.has_what]  # ... and :5270
+            loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
+            removed.add(w)
+            paused.discard(w)
+            hb["task"].extend(proc + held)
+            hb["dur"].extend([0.0] * (len(proc) + len(held)))
+            push(EV_LOSE_WORKER, -1, w, float(len(proc)))
         elif kind == EV_RETIRE:
             cand = [i for i in sorted(paused) if i not in removed and not s.workers[addr[i]].processing]
             live = [i for i in range(W) if i not in removed and i not in paused]
@@ -1165,6 +1219,10 @@ def main_resync(only):
         "svcrt_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=53, n_inner_prefixes=3,
                                                             random_durations=True, nthreads="random"), 1.1, 53, 0.1),
         "svcrt_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=54), float("inf"), 54, 0.1),
+        # workers lost with processing tasks / sole replicas, decided by the engine
+        "svcwl_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=55, n_inner_prefixes=3,
+                                                            random_durations=True, nthreads="random"), 1.1, 55, 0.1),
+        "svcwl_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=56), float("inf"), 56, 0.1),
     }
     for name, (mk, sat, seed, p_event) in cases.items():
         if only and name not in only:
@@ -1174,7 +1232,8 @@ def main_resync(only):
         dask.config.set({"distributed.scheduler.worker-saturation": sat})
         cfg = G.config_dict(sat)
         dumps = []
-        kinds_ = (1, 2, 3, 4, 5, 6, 7, EV_RETIRE, EV_RETIRE, EV_PAUSE) if name.startswith("svcrt_") else kinds
+        kinds_ = ((1, 2, 3, 4, 5, 6, 7, EV_RETIRE, EV_RETIRE, EV_PAUSE) if name.startswith("svcrt_") else
+                  (1, 2, 3, 4, 5, 6, 7, EV_LOSE_WORKER, EV_LOSE_WORKER, EV_RESUME) if name.startswith("svcwl_") else kinds)
         rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(g, cfg, seed, p_event, kinds_, dumps=dumps)
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
@@ -1188,7 +1247,7 @@ def main_resync(only):
         if dumps:
             z.update(_pack_dumps(dumps))
         np.savez_compressed(path, **z)
-        cnt = np.bincount(np.array(ev["kind"]), minlength=11).tolist()
+        cnt = np.bincount(np.array(ev["kind"]), minlength=16).tolist()
         print(f"{name}: {len(ev['kind'])} events (by kind {cnt}), {len(dumps)} resyncs, {len(rec['task'])} placements, "
               f"{os.path.getsize(path) / 1e3:.0f} kB")
 

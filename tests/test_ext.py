@@ -200,6 +200,7 @@ def test_extension_resyncs_after_stimuli_it_does_not_model():
     assert [r["fixture"] for r in res] == RESYNC
     for r in res:
         assert r["active"] and r["resyncs"] > 0 and r["calls"]["workers_removed"] > 0, r
+        assert r["calls"]["workers_lost_on_device"] > 0, r  # the losses the engine restates: decided there
         assert r["device_decisions"] + r["host_placements"] == r["placements"], r
 
 
@@ -214,6 +215,21 @@ def test_extension_follows_retiring_workers_on_the_device():
     assert [r["fixture"] for r in res] == names
     for r in res:
         assert r["active"] and r["resyncs"] == 0 and r["calls"]["workers_removed_on_device"] > 0, r
+        assert r["device_decisions"] == r["placements"], r
+
+
+def test_extension_runs_worker_losses_on_the_engine():
+    """Workers lost with processing tasks and sole replicas (svcwl_*): the extension's
+    remove_worker wrapper hands the whole stimulus to the engine (dgp_lose_worker, with the
+    worker's processing tasks and replicas in the scheduler's own iteration order) before
+    Scheduler.remove_worker runs; its transitions (processing tasks released and re-placed,
+    lost results recomputed, their processing dependents released to wait) take the engine's
+    decisions, validate=True re-derives each; no resync, every placement the engine's."""
+    names = ["svcwl_c2var_sat1.1.npz", "svcwl_c2mini_satinf.npz"]
+    res = drive(names)
+    assert [r["fixture"] for r in res] == names
+    for r in res:
+        assert r["active"] and r["resyncs"] == 0 and r["calls"]["workers_lost_on_device"] >= 10, r
         assert r["device_decisions"] == r["placements"], r
 
 

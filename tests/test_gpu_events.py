@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 
 from conftest import (GOLDEN, second_graph, svc_dep_graph_files, svc_event_files, svc_p2p_files, svc_prio_graph_files,
-                      svc_resync_files, svc_restr_graph_files, svc_retire_files)
+                      svc_loss_files, svc_resync_files, svc_restr_graph_files, svc_retire_files)
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -31,6 +31,7 @@ EV_FINISHED, EV_ADD_KEYS, EV_RELEASE_DATA, EV_PAUSE, EV_RESUME, EV_LONG_RUNNING,
 EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS = 8, 9, 10
 EV_SHUFFLE_INIT, EV_RESTRICT = 11, 12
 EV_RETIRE, EV_RETIRE_REPLICA = 13, 14
+EV_LOSE_WORKER = 15
 
 
 def sync_dump(z, j):
@@ -84,6 +85,10 @@ def drive_events(eng, g, z, exp=None):
                 eng.remove_replicas([t], [w])
             elif kd == EV_RETIRE:  # then the worker itself, no transition: no resync
                 eng.remove_worker(w)
+            elif kd == EV_LOSE_WORKER:  # the whole remove_worker stimulus on the device
+                lst = ht[hp[i]:hp[i + 1]]
+                npr = int(x[i])
+                assert eng.lose_worker(w, lst[:npr], lst[npr:]) is not None, (i, eng.refusal)
             elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
                 # the scheduler decided this stimulus itself: its placements, then its state
                 n = int(exp["stim_nplaced"][len(stim)])
@@ -175,6 +180,35 @@ def test_service_retiring_workers_match_reference(name):
         out = eng.placements()
         out.update(eng.snapshots(R))
         out["final_state"] = eng.task_states()
+    assert np.array_equal(stim, exp["stim_nplaced"]), np.nonzero(stim != exp["stim_nplaced"])[0][:5]
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
+@pytest.mark.parametrize("name", svc_loss_files())
+def test_service_worker_loss_on_the_engine(name):
+    """Workers lost with processing tasks and sole replicas (Scheduler.remove_worker,
+    scheduler.py:5180-5303: processing tasks released and re-placed, lost results
+    recomputed, their processing dependents released to wait for them), decided by the
+    engine (dgp_lose_worker) with no resync, interleaved with every modelled event: the
+    placements each loss made, every later decision, the snapshots and the final states
+    equal the reference's."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    kinds = set(np.unique(z["ev_kind"]).tolist())
+    assert EV_LOSE_WORKER in kinds and not kinds & {EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS}
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        stim = drive_events(eng, g, z, exp)
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert len(out["pl_task"]) > g["n_tasks"]  # re-placements and recomputes: the logs grew
     assert np.array_equal(stim, exp["stim_nplaced"]), np.nonzero(stim != exp["stim_nplaced"])[0][:5]
     assert_same(out, exp, PL_KEYS + ROUND_KEYS)
     assert np.array_equal(out["final_state"], exp["final_state"])
