@@ -1508,7 +1508,7 @@ struct CoopShared {
   int32_t pool[32];
   int64_t pool_n;
 };
-enum : int { OP_NONE = 0, OP_ARGMIN_POOL, OP_FASTPATH, OP_KTH, OP_RESTRICTED };
+enum : int { OP_NONE = 0, OP_ARGMIN_POOL, OP_FASTPATH, OP_KTH, OP_RESTRICTED, OP_RUNNING };
 
 // eager application of a sub-step (global stimuli): what the walker would do with its record
 __device__ void apply_now(const Dev& D, int32_t kind, int t, int w, int p, int64_t dnet, const double* dur) {
@@ -1603,6 +1603,9 @@ __device__ int dispatch_prepare(const Dev& D, int x, CoopShared& S, int64_t* sta
     int n = D.cand_n[x];
     int64_t off = D.cand_off[x];
     if (n <= 0) {
+      // every holder paused: valid_workers = running (:2262-2266), candidates & valid empty ->
+      // candidates = valid (:8575-8582)
+      if (D.evf & EVF_PAUSED) return OP_RUNNING;
       set_error(D, ERR_NO_CANDIDATES, x);
       return OP_NONE;
     }
@@ -1637,7 +1640,31 @@ __device__ int dispatch_prepare(const Dev& D, int x, CoopShared& S, int64_t* sta
 __device__ __attribute__((noinline)) void dispatch_collective(const Dev& D, CoopShared& S, int64_t* stage_next, const double* dur) {
   int op = S.op, x = S.x;
   Ctl* c = D.ctl;
-  if (op == OP_ARGMIN_POOL) {
+  if (op == OP_RUNNING) {  // decide_worker's argmin over every running worker
+    Obj best{INFINITY, INT64_MAX, INT32_MAX};
+    int64_t bcomm = 0;
+    bool have = false;
+    for (int w = threadIdx.x; w < D.W; w += blockDim.x) {
+      if (WK_flags(D)[w] & WF_PAUSED) continue;
+      const int64_t cm = comm_bytes(D, x, w);
+      const Obj o = objective(D, w, cm, dur);
+      if (!have || obj_less(o, best)) {
+        best = o;
+        bcomm = cm;
+        have = true;
+      }
+    }
+    ArgBest b = block_argmin(best, bcomm, have);
+    if (threadIdx.x == 0) {
+      if (b.o.w == INT32_MAX) {  // no running worker: no-worker
+        D.state[x] = S_NO_WORKER;
+        atomicAdd((unsigned long long*)&D.g_relwait[D.group[x]], (unsigned long long)-1ll);
+        c->n_unrunnable++;
+      } else {
+        place_eager(D, x, b.o.w, ROUTE_NONROOTISH, b.comm, stage_next, dur);
+      }
+    }
+  } else if (op == OP_ARGMIN_POOL) {
     bool use_idle = c->n_idle > 0;
     Obj best{INFINITY, INT64_MAX, INT32_MAX};
     int64_t bcomm = 0;
@@ -2143,12 +2170,22 @@ __device__ void candidate_row(const Dev& D, int x) {
     int64_t tot = 0;
     for (int64_t k = d0 + lane; k < d1; k += 64) tot += get_nbytes(D, D.dep_idx[k]);
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    // candidates = who_has of the dependencies & running (a paused worker is not valid,
+    // decide_worker_non_rootish :2262-2266)
+    auto running_bits = [&](int wd) {
+      unsigned long long m = 0;
+      if (D.evf & EVF_PAUSED)
+        for (int b = 0; b < 64 && wd * 64 + b < D.W; b++) m |= (WK_flags(D)[wd * 64 + b] & WF_PAUSED) ? 1ull << b : 0ull;
+      return ~m;
+    };
     int total_c = 0;
     for (int wd0 = 0; wd0 < D.WB; wd0 += 64) {
       int wd = wd0 + lane;
       unsigned long long acc = 0;
-      if (wd < D.WB)
+      if (wd < D.WB) {
         for (int64_t k = d0; k < d1; k++) acc |= D.holders[(size_t)D.dep_idx[k] * D.WB + wd];
+        acc &= running_bits(wd);
+      }
       int cnt = __popcll(acc);
       for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
       total_c += cnt;
@@ -2164,8 +2201,10 @@ __device__ void candidate_row(const Dev& D, int x) {
     for (int wd0 = 0; wd0 < D.WB; wd0 += 64) {
       int wd = wd0 + lane;
       unsigned long long acc = 0;
-      if (wd < D.WB)
+      if (wd < D.WB) {
         for (int64_t k = d0; k < d1; k++) acc |= D.holders[(size_t)D.dep_idx[k] * D.WB + wd];
+        acc &= running_bits(wd);
+      }
       int cnt = __popcll(acc);
       int incl = cnt;
       for (int o = 1; o < 64; o <<= 1) {

@@ -2334,12 +2334,6 @@ int dgp_lose_worker(dgp_engine* e, int32_t worker, int64_t n_processing, const i
     if (processing[i] < 0 || processing[i] >= D.N) return fail(e, DGP_E_ARG, "dgp_lose_worker: task out of range");
   for (int64_t i = 0; i < n_held; i++)
     if (held[i] < 0 || held[i] >= D.N) return fail(e, DGP_E_ARG, "dgp_lose_worker: task out of range");
-  // decide_worker_non_rootish takes valid_workers = running when a worker is paused
-  // (:2262-2266): the dispatcher's candidates are the who_has rows, so no other worker may be
-  // paused (a removed one holds nothing)
-  for (int32_t v = 0; v < D.W; v++)
-    if (v != worker && e->paused_h[v] == 1)
-      return fail(e, DGP_E_UNSUPPORTED, "dgp_lose_worker: another worker is paused: dgp_sync_* instead");
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   // Scheduler.remove_worker's host part (:5217-5218): total_nthreads, which is_rootish reads

@@ -528,11 +528,9 @@ class GPUPlacementExtension(SchedulerPlugin):
 
     @staticmethod
     def _loss_supported(s, ws, proc, held, safe) -> bool:
-        """The losses dgp_lose_worker restates: no other worker paused, no processing task
+        """The losses dgp_lose_worker restates: no processing task
         that errs (KilledWorker, :5239-5265) or that nobody needs, and every lost result that
         is needed has its dependencies in memory elsewhere and no queued / no-worker waiter."""
-        if len(s.running) < len(s.workers):
-            return False
         for ts in proc:
             if (not safe and ts.suspicious + 1 > s.allowed_failures) or not (ts.waiters or ts.who_wants):
                 return False

@@ -626,11 +626,9 @@ EV_LOSE_WORKER = 15
 
 def _loss_is_supported(s, ws):
     """The worker losses the engine decides itself (dgp_lose_worker; the extension checks the
-    same before it asks): no other worker paused, no processing task that errs
+    same before it asks): no processing task that errs
     (KilledWorker) or that nobody needs, and every lost result that is needed has its
     dependencies in memory elsewhere and no queued / no-worker dependent."""
-    if len(s.running) < len(s.workers):
-        return False
     for ts in ws.processing:
         if ts.suspicious + 1 > s.allowed_failures or not (ts.waiters or ts.who_wants) or ts.has_lost_dependencies:
             return False
