@@ -147,6 +147,8 @@ def steal_leg(eng, args, world: int, dist=None, barrier=None) -> dict:
            "parallelism": "thief rows sharded + all-gather, ordered walk replicated" if world > 1 else "single",
            "kernel_ms_per_call": {k: round(v[0] / n_call, 3) for k, v in kt.items() if k.startswith("steal")},
            "reference_python_seconds_per_call_at_100k_x_4096": 242.0}
+    if world == 1:
+        leg["plugin_path"] = steal_plugin_leg(eng, p, out)
     if world == 1 and not args.no_cpu_baseline:
         from oracle import oracle
 
@@ -155,6 +157,52 @@ def steal_leg(eng, args, world: int, dist=None, barrier=None) -> dict:
         leg["cpu_baseline"] = {"ms_per_call": round((time.perf_counter() - t0) * 1e3, 1), "cores": 1, "kind": "port",
                                "sample": "oracle/steal.cpp, one full balance() of the same problem"}
         leg["parity"] = bool(all(np.array_equal(np.asarray(out[k]), np.asarray(ref[k])) for k in ref))
+    return leg
+
+
+def steal_plugin_leg(eng, p, out_dev) -> dict:
+    """GPUWorkStealing.balance() end to end from the plugin's state (stealing.py
+    ``balance_plan``): the StealRows the transition hooks keep -> problem arrays (numpy over
+    the rows; the dependencies' who_has kept by the replica hooks) -> dgp_steal_order +
+    dgp_steal_balance -> the ordered requests as arrays, on a scheduler-free stand-in of the
+    plugin state at the same C4 problem (distributed_amd/steal_standin.py; the tasks in the
+    bins the device's levels give). Everything of balance() before move_task_request, which
+    is the reference's own code (its per-request cost, measured in the reference, beside)."""
+    from distributed_amd.steal_standin import plugin_from_problem
+    from distributed_amd.stealing import balance_plan
+
+    plugin, slot_task = plugin_from_problem(p, out_dev["level"])
+    balance_plan(plugin, eng)  # warm-up
+    n_call = 3
+    t_prob = []
+    t0 = time.perf_counter()
+    for _ in range(n_call):
+        t1 = time.perf_counter()
+        plugin.rows.problem(plugin)  # the host half alone, for the breakdown
+        t_prob.append(time.perf_counter() - t1)
+    t_host = (time.perf_counter() - t0) / n_call
+    t0 = time.perf_counter()
+    for _ in range(n_call):
+        plan = balance_plan(plugin, eng)
+        out, rows, wss = plan
+        req = slot_task[rows[out["st_task"]]]  # the request list: task of each request, in order
+    dt = (time.perf_counter() - t0) / n_call
+    parity = bool(np.array_equal(req, out_dev["st_task"]) and all(
+        np.array_equal(out[k], out_dev[k]) for k in ("st_victim", "st_thief", "st_level", "st_cost", "st_occ_victim",
+                                                   "st_occ_thief", "inflight_occ", "inflight_tasks", "idle_after",
+                                                   "sat_after", "checked")))
+    leg = {"metric": "GPUWorkStealing.balance() from plugin state, ms per call",
+           "ms_per_call": round(dt * 1e3, 3), "fits_100ms_interval": bool(dt <= 0.1),
+           "host_problem_ms": round(min(t_prob) * 1e3, 3), "host_problem_ms_mean": round(t_host * 1e3, 3),
+           "stealable_tasks": int(len(slot_task)), "steal_requests": int(len(req)),
+           "boundary": "StealRows (plugin state) -> balance_plan -> request arrays; move_task_request excluded",
+           "parity_with_device_leg": parity}
+    ref = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "ref_python_c4.json")
+    if os.path.exists(ref):
+        r = json.load(open(ref))
+        if "move_task_request_us" in r:
+            leg["reference_move_task_request_us_per_request"] = r["move_task_request_us"]
+            leg["reference_apply_ms_for_these_requests"] = round(r["move_task_request_us"] * len(req) / 1e3, 1)
     return leg
 
 

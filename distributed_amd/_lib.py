@@ -83,6 +83,7 @@ SIGNATURES = {
     "dgp_task_erred": (C.c_int, [_P, C.c_int32, _P]),
     "dgp_remove_worker": (C.c_int, [_P, C.c_int32]),
     "dgp_lose_worker": (C.c_int, [_P, C.c_int32, C.c_int64, _P, C.c_int64, _P, _P]),
+    "dgp_steal_order": (C.c_int, [_P, C.c_int64, _P, _P]),
     "dgp_sync_placements": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P]),
     "dgp_sync_tasks": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dgp_sync_workers": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -90,7 +91,7 @@ SIGNATURES = {
                                    _P, _P, _P]),
 }
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 _libs: dict = {}
 
 

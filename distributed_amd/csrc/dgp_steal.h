@@ -364,7 +364,7 @@ __device__ __forceinline__ int64_t rl_i64s(int64_t x, int l) {  // lane l's int6
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 __host__ __device__ inline size_t balance_state_bytes(int W) {
-  return (size_t)W * (8 + 8 + 4) + ((size_t)6 * W + 2) * 2 + (size_t)W * 4;
+  return (size_t)W * (8 + 8 + 4) + ((size_t)6 * W + 2) * 2 + (size_t)W * 4 + (size_t)W;
 }
 // One wave; all per-worker balance state in LDS: occupancy, in-flight occupancy, the
 // pending task count (len(processing) + in-flight task delta), nthreads, thief / idle /
@@ -389,6 +389,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
   uint8_t* idle = thief + W;
   uint8_t* sat = idle + W;
   uint8_t* taken = sat + W;                 // topk scratch
+  uint8_t* own = taken + W;                 // a window's lane per thief (does a thief repeat in it?)
   int32_t* vs = P.vs_g;                     // victims of the current level (global scratch)
   const int R = *P.n_runs;
   for (int r = lane; r < R; r += 64) {
@@ -441,7 +442,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
 #if DGP_STEAL_PROF
     if (lane == 0)
       printf("k_balance: requests %lld examined %llu thief-left %llu (%llu cycles) total %llu cycles; chunks %llu "
-             "prologue %llu loop %llu epilogue %llu; many-holder %llu windows %llu (%llu cycles)\n", ns, pr_exam,
+             "prologue %llu loop %llu epilogue %llu; windows with a repeated thief %llu, windows %llu (chain / serial pass %llu cycles)\n", ns, pr_exam,
              pr_left, pr_left_cyc, __builtin_amdgcn_s_memtime() - pr_t0, pr_chunks, pr_pro, pr_loop, pr_epi, pr_many,
              pr_win, pr_wcyc);
 #endif
@@ -548,6 +549,19 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
       const double occ_v = occ[v];
       double ifo_v = ifo[v];
       int pend_v = pend[v];
+      // each chunk's task rows, loaded one chunk ahead (the walk of chunk c hides the loads of c + 1)
+      int ntq = 0, nthL = NO_THIEF;
+      double ncq = 0.0, nvq = 0.0, ndq = 0.0;
+      auto load_rows = [&](int c) {
+        const int i = c + lane;
+        const bool ok = i < b1;
+        ntq = ok ? P.order[i] : 0;
+        nthL = ok ? P.s_best[i] : NO_THIEF;  // each lane's task: its precomputed thief
+        ncq = ok ? P.s_cct[i] : 0.0;
+        nvq = ok ? P.s_ccv[i] : 0.0;
+        ndq = ok ? P.s_dur[i] : 0.0;
+      };
+      load_rows(b0);
       for (int c0 = b0; c0 < b1; c0 += 64) {  // 64 tasks of the bin per load round
 #if DGP_STEAL_PROF
         unsigned long long pc0 = __builtin_amdgcn_s_memtime();
@@ -555,34 +569,49 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
 #endif
         const int i = c0 + lane;
         const bool okl = i < b1;
-        const int tq = okl ? P.order[i] : 0;
-        int thL = okl ? P.s_best[i] : NO_THIEF;  // each lane's task: its precomputed thief
-        double cq = okl ? P.s_cct[i] : 0.0;
-        const double vq = okl ? P.s_ccv[i] : 0.0;
-        const double dq = okl ? P.s_dur[i] : 0.0;
-        // the thief search's rows of the lane's task (used when its thief left)
-        const int nhL = okl ? P.s_nh[i] : -1;
-        const int64_t cgL = okl ? P.s_cget[i] : 0, crL = okl ? P.s_craw[i] : 0;
+        const int tq = ntq;
+        int thL = nthL;
+        double cq = ncq;
+        const double vq = nvq;
+        const double dq = ndq;
+        if (c0 + 64 < b1) load_rows(c0 + 64);
+        // the thief search's rows of the lane's task, read the first time a search needs them
+        bool have_rows = false;
+        int nhL = -1;
+        int64_t cgL = 0, crL = 0;
         int hwL[MAXH];
         int64_t hgL[MAXH], hrL[MAXH], hnL[MAXH];
-#pragma unroll
-        for (int j = 0; j < MAXH; j++) {
-          const bool hj = okl && j < nhL;
-          hwL[j] = hj ? P.s_hw[(size_t)i * MAXH + j] : 0;
-          hgL[j] = hj ? P.s_hg[(size_t)i * MAXH + j] : 0;
-          hrL[j] = hj ? P.s_hr[(size_t)i * MAXH + j] : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < MAXH; j++) hnL[j] = okl && j < nhL ? P.wnbytes[hwL[j]] : 0;
-        // the search's comm terms (worker_objective :3136-3138), computed once per task
-        const double xL = (double)cgL / (double)P.bw;
+        double xL = 0.0;
         double hcL[MAXH];
 #pragma unroll
-        for (int j = 0; j < MAXH; j++) hcL[j] = (double)(cgL - hgL[j]) / (double)P.bw;
+        for (int q = 0; q < MAXH; q++) {
+          hwL[q] = 0;
+          hgL[q] = hrL[q] = hnL[q] = 0;
+          hcL[q] = 0.0;
+        }
+        auto search_rows = [&]() {
+          if (have_rows) return;
+          have_rows = true;
+          nhL = okl ? P.s_nh[i] : -1;
+          cgL = okl ? P.s_cget[i] : 0;
+          crL = okl ? P.s_craw[i] : 0;
+#pragma unroll
+          for (int q = 0; q < MAXH; q++) {
+            const bool hj = okl && q < nhL;
+            hwL[q] = hj ? P.s_hw[(size_t)i * MAXH + q] : 0;
+            hgL[q] = hj ? P.s_hg[(size_t)i * MAXH + q] : 0;
+            hrL[q] = hj ? P.s_hr[(size_t)i * MAXH + q] : 0;
+          }
+#pragma unroll
+          for (int q = 0; q < MAXH; q++) hnL[q] = okl && q < nhL ? P.wnbytes[hwL[q]] : 0;
+          // the search's comm terms (worker_objective :3136-3138), computed once per task
+          xL = (double)cgL / (double)P.bw;
+#pragma unroll
+          for (int q = 0; q < MAXH; q++) hcL[q] = (double)(cgL - hgL[q]) / (double)P.bw;
+        };
         const int nq = min(64, b1 - c0);
         // each lane's thief's balance state, gathered at once (the lanes of one thief hold the
-        // same values); the walk works on one "current" thief in uniform registers and puts
-        // its state back into those lanes and into LDS when it moves to another one
+        // same values); LDS holds every thief's accounts as of the last committed window
         bool hasL = thL >= 0;
         int aliveL = hasL && thief[thL] ? 1 : 0;
         double occL = hasL ? occ[thL] : 0.0;
@@ -605,38 +634,68 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
         pr_pro += pc1 - pc0;
 #endif
         // The walk in windows: from task j up to the next task whose precomputed thief left
-        // (d), one serial pass carries the victim's and each thief's in-flight accounts as if
-        // every task were accepted (two fp64 operations per task, the reference's order),
-        // recording in each task's lane the state it sees; then every task's test and the
-        // thief's is_unoccupied run in parallel. The first rejection, or the task after the
-        // first one that fills its thief, ends the accepted prefix [j, b); if b falls inside
-        // the window the accounts are replayed over [j, b) from the window's start. Task d
-        // takes the thief search and runs on its own.
+        // (d), every task's test and the thief's is_unoccupied run in parallel, each lane with
+        // the accounts it would see if every earlier task of the window were accepted; the
+        // first rejection, or the task after the first one that fills its thief, ends the
+        // accepted prefix [j, b). The victim's in-flight occupancy is one fp64 chain over the
+        // window (the reference's order); a thief's accounts are the lane's own unless the
+        // thief repeats in the window -- then one serial pass carries them task by task (and
+        // replays the accepted prefix if b falls inside). The accepted prefix writes its
+        // thieves' accounts to LDS; every lane re-reads its thief's. Task d takes the thief
+        // search and runs on its own.
         int j = 0;
         while (j < nq && n_thieves > 0) {
           const bool todo = lane >= j && lane < nq && thL != NO_THIEF;
           const unsigned long long needs = __ballot(todo && !(hasL && aliveL));
           const int d = needs ? (int)__builtin_ctzll(needs) : nq;
-          const double ifo_vS = ifo_v;
-          const double ifoS = ifoL;
-          const int pendS = pendL;
-          double vb = 0.0, tb = 0.0;
-          int pb = 0;
-          for (int k = j; k < d; k++) {
-            const int thk = __builtin_amdgcn_readlane(thL, k);
-            if (thk == NO_THIEF) continue;
-            vb = lane == k ? ifo_v : vb;
-            ifo_v = ifo_v - rl_f64(dvL, k);
-            const double tbk = rl_f64(ifoL, k);
-            const int pbk = __builtin_amdgcn_readlane(pendL, k);
-            tb = lane == k ? tbk : tb;
-            pb = lane == k ? pbk : pb;
-            const double tnew = tbk + rl_f64(dtL, k);
-            const bool mine = thL == thk;
-            ifoL = mine ? tnew : ifoL;
-            pendL = mine ? pbk + 1 : pendL;
-          }
           const bool inw = todo && lane < d;
+          if (inw) own[thL] = (uint8_t)lane;
+          __syncthreads();
+          const bool repeats = __ballot(inw && own[thL] != (uint8_t)lane) != 0;
+#if DGP_STEAL_PROF
+          if (repeats) pr_many++;
+          const unsigned long long wc0 = __builtin_amdgcn_s_memtime();
+#endif
+          // the victim's chain over the window; a lane without a thief subtracts +0.0 (exact)
+          double vb = 0.0;
+          {
+            const double dvz = inw ? dvL : 0.0;
+            for (int k = j; k < d; k++) {
+              vb = lane == k ? ifo_v : vb;
+              ifo_v = ifo_v - rl_f64(dvz, k);
+            }
+          }
+          // each task's thief accounts as they would be after the window's earlier tasks:
+          // the lane's own unless its thief repeats in the window; then the chain of that
+          // thief's tasks (prev = the nearest earlier one) is resolved link by link, all
+          // thieves at once (one fp64 add per link, the reference's order)
+          double tb = ifoL;
+          int pb = pendL;
+          int prv = -1, nxt = 64;  // nearest earlier / later lane of the window with the same thief
+          if (repeats) {
+            for (int m = j; m < d; m++) {
+              const int thm = __builtin_amdgcn_readlane(thL, m);
+              const bool same = inw && thL == thm;
+              prv = same && lane > m ? m : prv;
+              nxt = same && lane < m && nxt == 64 ? m : nxt;
+            }
+            const int src = prv >= 0 ? prv : lane;
+            const double pdt = __shfl(dtL, src);
+            bool done = prv < 0;
+            while (__ballot(inw && !done)) {
+              const double ptb = __shfl(tb, src);
+              const int ppb = __shfl(pb, src);
+              const bool pdone = __shfl((int)done, src) != 0;
+              if (!done && pdone) {
+                tb = ptb + pdt;
+                pb = ppb + 1;
+                done = true;
+              }
+            }
+          }
+#if DGP_STEAL_PROF
+          pr_wcyc += __builtin_amdgcn_s_memtime() - wc0;
+#endif
           const double ot = occL + tb;          // combined_occupancy of the thief (:505-506)
           const double ov = occ_v + vb;         // ... and of the victim
           const bool acc = ot + cq + dq <= ov - hvL;  // :462-465
@@ -647,25 +706,21 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           const int b = min(min(fb, ff + 1), d);
 #if DGP_STEAL_PROF
           pr_exam += __builtin_popcountll(__ballot(inw && lane < b));
+          pr_win++;
 #endif
-          if (b < d) {  // the accounts of the accepted prefix only
-            ifo_v = ifo_vS;
-            ifoL = ifoS;
-            pendL = pendS;
-            for (int k = j; k < b; k++) {
-              const int thk = __builtin_amdgcn_readlane(thL, k);
-              if (thk == NO_THIEF) continue;
-              ifo_v = ifo_v - rl_f64(dvL, k);
-              const double tnew = rl_f64(ifoL, k) + rl_f64(dtL, k);
-              const int pbk = __builtin_amdgcn_readlane(pendL, k);
-              const bool mine = thL == thk;
-              ifoL = mine ? tnew : ifoL;
-              pendL = mine ? pbk + 1 : pendL;
-            }
-          }
           // move_task_request (:279-331) for the accepted prefix
           const bool com = inw && lane < b;
           const unsigned long long cm = __ballot(com);
+          if (b < d) ifo_v = rl_f64(vb, b);  // the victim's chain up to the prefix's end
+          if (com && nxt >= b) {  // each thief takes the account of its last accepted task (:327-331)
+            ifo[thL] = tb + dtL;
+            pend[thL] = pb + 1;
+          }
+          __syncthreads();
+          if (cm && hasL) {
+            ifoL = ifo[thL];
+            pendL = pend[thL];
+          }
           if (com) {
             accL = 1;
             thO = thL;
@@ -696,11 +751,7 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
           pr_left++;
 #endif
-          if (hasL) {  // the live accounts into LDS (every lane of one thief holds the same values)
-            ifo[thL] = ifoL;
-            pend[thL] = pendL;
-          }
-          __syncthreads();
+          search_rows();
           const bool sl = lane >= d && lane < nq && thL != NO_THIEF && !(hasL && aliveL);
           // restricted tasks (valid_workers): the plain argmin over their live valid thieves,
           // one task at a time (a loose one with none falls through to the general search)
@@ -840,10 +891,6 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           pr_left_cyc += __builtin_amdgcn_s_memtime() - tp0;
 #endif
         }
-        if (hasL) {
-          ifo[thL] = ifoL;
-          pend[thL] = pendL;
-        }
 #if DGP_STEAL_PROF
         unsigned long long pc2 = __builtin_amdgcn_s_memtime();
         pr_loop += pc2 - pc1;
@@ -890,6 +937,20 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
     }
   }
   finish();
+}
+
+// dgp_steal_order's sort helpers: int64 keys as order-preserving uint64, gathers by permutation
+__global__ void k_flip_sign(uint64_t* k, int64_t n) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) k[i] ^= 1ull << 63;
+}
+__global__ void k_gather_u64(const uint64_t* __restrict__ src, const int32_t* __restrict__ perm, uint64_t* dst, int64_t n) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[perm[i]];
+}
+__global__ void k_gather_i32(const int32_t* __restrict__ src, const int32_t* __restrict__ perm, int32_t* dst, int64_t n) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[perm[i]];
 }
 
 inline size_t balance_lds_bytes(int W) { return (balance_state_bytes(W) + 15) & ~(size_t)15; }

@@ -51,6 +51,8 @@ struct StealCtx {  // WorkStealing arrays of the last dgp_steal_load (one arena)
   int NK = 0;
   int64_t n_stealable = 0;
   bool loaded = false;
+  // dgp_steal_order for the next load: the tasks' (priority, arrival) keys (host)
+  std::vector<int64_t> order_prio, order_arr;
 };
 
 struct dgp_engine {
@@ -3001,8 +3003,14 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
                                          (int32_t*)nullptr, W, 0, 64, s));
   chk(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_a, (uint64_t*)nullptr, (uint64_t*)nullptr, (int32_t*)nullptr,
                                          (int32_t*)nullptr, W, 0, 64, s));
+  // dgp_steal_order: the tasks' (priority, arrival) order, two stable 64-bit sorts
+  const bool ordered = (int64_t)e->steal.order_prio.size() == T && T > 0;
+  size_t tmp_ord = 0;
+  if (ordered)
+    chk(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_ord, (uint64_t*)nullptr, (uint64_t*)nullptr, (int32_t*)nullptr,
+                                           (int32_t*)nullptr, Tn, 0, 64, s));
   if (st != hipSuccess) return fail(e, DGP_E_HIP, std::string("dgp_steal_load: sizing: ") + hipGetErrorString(st));
-  const size_t tmp_bytes = std::max(std::max(tmp_sort, tmp_scan), std::max(tmp_nb, tmp_a));
+  const size_t tmp_bytes = std::max(std::max(std::max(tmp_sort, tmp_scan), std::max(tmp_nb, tmp_a)), tmp_ord);
   auto add = [&](auto** p, size_t n) { parts.push_back({(void**)p, (n ? n : 1) * sizeof(**p)}); };
   add(&d_nthreads, W); add(&d_occ, W); add(&d_nproc, W); add(&d_wnb, W); add(&d_idle, W); add(&d_sat, W);
   add(&d_victim, T); add(&d_dur, T); add(&d_fast, T); add(&d_dep_ptr, T + 1); add(&d_dep_idx, E);
@@ -3020,6 +3028,11 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
   if (ifo_in) add(&d_ifo_in, W);
   if (ift_in) add(&d_ift_in, W);
   add(&P.checked, W);
+  uint64_t *d_ok1 = nullptr, *d_ok2 = nullptr, *d_ok3 = nullptr;
+  int32_t *d_perm1 = nullptr, *d_perm2 = nullptr;
+  if (ordered) {
+    add(&d_ok1, T); add(&d_ok2, T); add(&d_ok3, T); add(&d_perm1, T); add(&d_perm2, T);
+  }
   add(&P.key, T); add(&P.order, T); add(&C.keys_sorted, T); add(&C.d_vals, T); add(&P.bin_cnt, NK); add(&P.bin_ptr, NK);
   add(&P.s_best, T); add(&P.s_cct, T); add(&P.s_ccv, T); add(&P.s_dur, T);
   add(&P.s_cget, T); add(&P.s_craw, T); add(&P.s_nh, T); add(&P.s_hw, T * S::MAXH); add(&P.s_hg, T * S::MAXH);
@@ -3086,9 +3099,29 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
   if (T > 0) {
     rc = timed_launch(e, 4, [&] {
       hipLaunchKernelGGL(S::k_steal_levels, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, P);
-      hipLaunchKernelGGL(dgp::k_iota32, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, C.d_vals, (int)T);
+      int32_t* key_in = P.key;
+      if (ordered) {
+        // ascending (priority, arrival): arrival first, then priority, both stable; the bin
+        // sort below then keeps that order inside each bin. Keys go through the sign bit
+        // flipped (int64 order as uint64).
+        const unsigned gt = (unsigned)((T + 255) / 256);
+        chk(hipMemcpyAsync(d_ok1, C.order_prio.data(), T * 8, hipMemcpyHostToDevice, s));
+        chk(hipMemcpyAsync(d_ok2, C.order_arr.data(), T * 8, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(S::k_flip_sign, dim3(gt), dim3(256), 0, s, d_ok1, T);
+        hipLaunchKernelGGL(S::k_flip_sign, dim3(gt), dim3(256), 0, s, d_ok2, T);
+        hipLaunchKernelGGL(dgp::k_iota32, dim3(gt), dim3(256), 0, s, d_perm1, (int)T);
+        size_t tb = tmp_bytes;
+        chk(hipcub::DeviceRadixSort::SortPairs(C.d_tmp, tb, d_ok2, d_ok3, d_perm1, d_perm2, Tn, 0, 64, s));
+        hipLaunchKernelGGL(S::k_gather_u64, dim3(gt), dim3(256), 0, s, d_ok1, d_perm2, d_ok3, T);
+        tb = tmp_bytes;
+        chk(hipcub::DeviceRadixSort::SortPairs(C.d_tmp, tb, d_ok3, d_ok2, d_perm2, C.d_vals, Tn, 0, 64, s));
+        hipLaunchKernelGGL(S::k_gather_i32, dim3(gt), dim3(256), 0, s, P.key, C.d_vals, d_perm1, T);
+        key_in = d_perm1;  // the bin keys in that order, the task ids (C.d_vals) beside them
+      } else {
+        hipLaunchKernelGGL(dgp::k_iota32, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, C.d_vals, (int)T);
+      }
       size_t tb = tmp_bytes;
-      chk(hipcub::DeviceRadixSort::SortPairs(C.d_tmp, tb, P.key, C.keys_sorted, C.d_vals, P.order, Tn, 0, bits, s));
+      chk(hipcub::DeviceRadixSort::SortPairs(C.d_tmp, tb, key_in, C.keys_sorted, C.d_vals, P.order, Tn, 0, bits, s));
       tb = tmp_bytes;
       chk(hipcub::DeviceScan::ExclusiveSum(C.d_tmp, tb, P.bin_cnt, P.bin_ptr, NK, s));
     });
@@ -3114,7 +3147,17 @@ int dgp_steal_load(dgp_engine* e, int32_t W, const int32_t* nthreads, const doub
   if (nst < 0 || nst > T) return fail(e, DGP_E_STATE, "dgp_steal_load: bin scan out of range");
   C.n_stealable = nst;
   C.loaded = true;
+  C.order_prio.clear();
+  C.order_arr.clear();
   *n_stealable = nst;
+  return 0;
+}
+
+int dgp_steal_order(dgp_engine* e, int64_t n_tasks, const int64_t* priority, const int64_t* arrival) {
+  if (!e) return DGP_E_ARG;
+  if (n_tasks < 0 || (n_tasks && (!priority || !arrival))) return fail(e, DGP_E_ARG, "dgp_steal_order: bad arrays");
+  e->steal.order_prio.assign(priority, priority + n_tasks);
+  e->steal.order_arr.assign(arrival, arrival + n_tasks);
   return 0;
 }
 

@@ -630,8 +630,10 @@ class PlacementEngine:
         ``p``: nthreads, occ, nproc, wnbytes, idle, sat (per worker); total_occ,
         total_nthreads, bandwidth; victim, duration, fast, dep_ptr, dep_idx (per task);
         data_nbytes, data_get_nbytes and who_has as data_holder (one worker or -1) or
-        holder_ptr / holder_idx (CSR). Returns levels, the ordered steal requests and the
-        per-worker in-flight / idle / saturated state after the call.
+        holder_ptr / holder_idx (CSR); optionally task_prio / task_arrival (int64 per task):
+        the tasks are then walked in ascending (priority, arrival) rather than input order
+        (dgp_steal_order, sorted on the device). Returns levels, the ordered steal requests
+        and the per-worker in-flight / idle / saturated state after the call.
 
         ``group``: a torch.distributed group of more than one rank (one engine per GPU,
         every rank passing the same ``p``): each rank computes its slice of the per-task
@@ -697,6 +699,9 @@ class PlacementEngine:
         outputs = ([_ptr(out[k]) for k in ("level", "st_task", "st_victim", "st_thief", "st_level", "st_cost",
                                            "st_occ_victim", "st_occ_thief")] + [C.byref(n)]
                    + [_ptr(out[k]) for k in ("inflight_occ", "inflight_tasks", "idle_after", "sat_after", "checked")])
+        if p.get("task_prio") is not None:  # rows in arrival slots: the device orders them (dgp_steal_order)
+            self._check(self.lib.dgp_steal_order(self.h, T, a(p["task_prio"], np.int64), a(p["task_arrival"], np.int64)),
+                        "dgp_steal_order")
         return inputs, outputs, out, n, keep
 
     def _steal_sharded(self, inputs, outputs, group):

@@ -8,7 +8,8 @@ stealable bins the ``transition`` hook keeps (:175-239), ``move_task_request`` /
 ``extensions["stealing"]`` keeps its contract for the rest of the scheduler.
 
 One balance() = one ``dgp_steal_balance`` call (PlacementEngine.steal_balance) on the
-plugin's current state (the task rows kept incrementally, ``StealRows``): workers
+plugin's current state (the task rows and their dependencies' who_has kept incrementally,
+``StealRows``; ``balance_plan``): workers
 (occupancy, processing, nbytes, idle / saturated), the
 tasks of its bins with their levels, their dependencies and who_has, worker
 restrictions (``valid_workers``), and the in-flight accounts of unconfirmed steals. The
@@ -16,7 +17,8 @@ device returns the ordered steal requests; they are applied here exactly as bala
 does: ``move_task_request`` per request, the log entry and both metrics, then
 ``check_idle_saturated(victim, occ=combined)`` for every victim the walk visited.
 
-Order: within a bin the device takes tasks in ascending ``TaskState.priority`` and
+Order: within a bin the device takes tasks in ascending ``TaskState.priority`` (then
+arrival in the bin; the rows go unsorted, the device sorts them: dgp_steal_order) and
 victims in ascending worker address (the reference iterates Python sets, whose order
 is hash-dependent; the golden fixtures pin the same canonical order).
 """
@@ -69,54 +71,82 @@ def steal_problem_from_state(plugin) -> tuple[dict, list, list]:
         holder_ptr=hptr, holder_idx=np.array([w for h in holders for w in h], np.int32),
         level_in=np.array([plugin.key_stealable[ts][1] for ts in tasks], np.int8),
     )
-    _restriction_rows(p, s, tasks, widx)
+    _restriction_rows(p, s, list(enumerate(tasks)), T, widx)
     return p, tasks, wss
 
 
+def pack_priority(pr):
+    """``TaskState.priority`` = (-user priority, generation, dask.order position)
+    (scheduler.py:4719-4724) as one int64 of the same order, or None when it does not fit
+    (then the host orders the rows)."""
+    try:
+        a, b, c = pr
+    except (TypeError, ValueError):
+        return None
+    if type(a) is int and type(b) is int and type(c) is int and -(1 << 15) <= a < (1 << 15) and 0 <= b < (1 << 20) \
+            and 0 <= c < (1 << 27):
+        return ((a + (1 << 15)) << 47) | (b << 27) | c
+    return None
+
+
 class StealRows:
-    """The task rows of the steal problem, kept as the plugin's transition hook fills and
-    empties its bins (``put_key_in_stealable`` / ``remove_key_from_stealable``,
-    stealing.py:218-239), so one ``balance()`` gathers them instead of rebuilding them: per
-    task (one numpy row slot) its bin worker, level, fast flag, prefix and dependency ids
-    (ascending, into a refcounted table of the dependency TaskStates), ordered by
-    (priority, arrival). Read at balance time, as the full rebuild does: durations (per
-    prefix), restrictions and the dependencies' nbytes / holders (one pass over the
-    distinct dependencies)."""
+    """The steal problem's rows, kept as the plugin's hooks change its state, so that one
+    ``balance()`` gathers them with numpy instead of visiting TaskStates:
+
+    * task rows (one slot each, filled and emptied by ``put_key_in_stealable`` /
+      ``remove_key_from_stealable``, stealing.py:218-239): bin worker, level, fast flag,
+      prefix, dependency ids (into the dependency table), the packed priority and arrival
+      (the device orders the rows by them, dgp_steal_order), a restrictions flag;
+    * the dependency table (refcounted by the task rows): nbytes, get_nbytes() and who_has
+      as worker-address codes, kept by the scheduler's replica hooks (add_replica /
+      remove_replica / remove_all_replicas, scheduler.py:3148-3171, wrapped by the plugin).
+
+    Read at balance time: worker columns, durations (per prefix), restrictions (restricted
+    rows only)."""
 
     KD = 4  # dependency ids held in the slot row; longer rows keep the rest in ``more``
+    HM = 8  # holders held in the dependency row; more in ``hmore``
 
     def __init__(self):
-        from sortedcontainers import SortedList
-
         self.slot = {}  # TaskState -> row slot
-        self.task, self.key, self.free = [], [], []
-        self.order = SortedList()  # (priority, arrival, slot): ties in arrival order
+        self.task, self.free = [], []
         self.arrival = 0
         cap = 1024
+        self.live = np.zeros(cap, bool)
         self.lvl = np.zeros(cap, np.int8)
         self.fst = np.zeros(cap, np.uint8)
         self.pfx = np.zeros(cap, np.int32)
         self.vic = np.zeros(cap, np.int32)
         self.nd = np.zeros(cap, np.int32)
         self.dmat = np.zeros((cap, self.KD), np.int64)
+        self.pk = np.zeros(cap, np.int64)
+        self.arr = np.zeros(cap, np.int64)
+        self.rst = np.zeros(cap, np.uint8)
         self.more = {}  # slot -> dependency ids beyond the first KD
+        self.pk_bad = {}  # slot -> a priority pack_priority cannot hold
         self.data_id, self.data, self.data_ref, self.data_free = {}, [], [], []
+        dcap = 1024
+        self.dnb = np.zeros(dcap, np.int64)
+        self.dgnb = np.zeros(dcap, np.int64)
+        self.hold = np.zeros((dcap, self.HM), np.int32)
+        self.hcnt = np.zeros(dcap, np.int32)
+        self.hmore = {}  # data slot -> holder codes beyond HM
         self.prefix_id, self.prefixes = {}, []  # TaskPrefix name -> code, code -> TaskPrefix
         self.addr_id, self.addrs = {}, []  # worker address -> code
 
     def __len__(self):
         return len(self.slot)
 
+    @staticmethod
+    def _grown(a, cap):
+        b = np.zeros((cap,) + a.shape[1:], a.dtype)
+        b[:len(a)] = a
+        return b
+
     def _grow(self):
         cap = 2 * len(self.lvl)
-        for nm in ("lvl", "fst", "pfx", "vic", "nd"):
-            a = getattr(self, nm)
-            b = np.zeros(cap, a.dtype)
-            b[:len(a)] = a
-            setattr(self, nm, b)
-        d = np.zeros((cap, self.KD), np.int64)
-        d[:len(self.dmat)] = self.dmat
-        self.dmat = d
+        for nm in ("live", "lvl", "fst", "pfx", "vic", "nd", "dmat", "pk", "arr", "rst"):
+            setattr(self, nm, self._grown(getattr(self, nm), cap))
 
     def _code(self, table, items, key, obj):
         c = table.get(key)
@@ -125,6 +155,80 @@ class StealRows:
             items.append(obj)
         return c
 
+    # ------------------------------------------------------------- dependency table
+    def _new_data(self, dts):
+        if self.data_free:
+            j = self.data_free.pop()
+            self.data[j] = dts
+            self.data_ref[j] = 0
+        else:
+            j = len(self.data)
+            self.data.append(dts)
+            self.data_ref.append(0)
+            if j >= len(self.dnb):
+                cap = 2 * len(self.dnb)
+                for nm in ("dnb", "dgnb", "hold", "hcnt"):
+                    setattr(self, nm, self._grown(getattr(self, nm), cap))
+        self.data_id[dts] = j
+        self.dnb[j] = dts.nbytes
+        self.dgnb[j] = dts.get_nbytes()
+        self.hcnt[j] = 0
+        self.hmore.pop(j, None)
+        for ws in dts.who_has or ():
+            self._hold_add(j, self._code(self.addr_id, self.addrs, ws.address, ws.address))
+        return j
+
+    def _hold_add(self, j, c):
+        n = int(self.hcnt[j])
+        if c in self.hold[j, :min(n, self.HM)] or c in self.hmore.get(j, ()):
+            return
+        if n < self.HM:
+            self.hold[j, n] = c
+        else:
+            self.hmore.setdefault(j, []).append(c)
+        self.hcnt[j] = n + 1
+
+    def _hold_remove(self, j, c):
+        n = int(self.hcnt[j])
+        ex = self.hmore.get(j)
+        row = self.hold[j]
+        for q in range(min(n, self.HM)):
+            if row[q] == c:  # the last holder takes its place
+                if ex:
+                    row[q] = ex.pop()
+                    if not ex:
+                        del self.hmore[j]
+                else:
+                    row[q] = row[n - 1]
+                self.hcnt[j] = n - 1
+                return
+        if ex and c in ex:
+            ex.remove(c)
+            if not ex:
+                del self.hmore[j]
+            self.hcnt[j] = n - 1
+
+    def replica(self, ts, address, sign):
+        """SchedulerState.add_replica / remove_replica of (ts, worker) (the plugin's hooks)."""
+        j = self.data_id.get(ts)
+        if j is None:
+            return
+        c = self._code(self.addr_id, self.addrs, address, address)
+        if sign > 0:
+            self.dnb[j] = ts.nbytes
+            self.dgnb[j] = ts.get_nbytes()
+            self._hold_add(j, c)
+        else:
+            self._hold_remove(j, c)
+
+    def replicas_cleared(self, ts):
+        """SchedulerState.remove_all_replicas(ts)."""
+        j = self.data_id.get(ts)
+        if j is not None:
+            self.hcnt[j] = 0
+            self.hmore.pop(j, None)
+
+    # ------------------------------------------------------------------ task rows
     def put(self, ts, worker: str, level: int) -> None:
         if ts in self.slot:
             self.remove(ts)
@@ -132,15 +236,7 @@ class StealRows:
         for dts in ts.dependencies:
             j = self.data_id.get(dts)
             if j is None:
-                if self.data_free:
-                    j = self.data_free.pop()
-                    self.data[j] = dts
-                    self.data_ref[j] = 0
-                else:
-                    j = len(self.data)
-                    self.data.append(dts)
-                    self.data_ref.append(0)
-                self.data_id[dts] = j
+                j = self._new_data(dts)
             self.data_ref[j] += 1
             ids.append(j)
         ids.sort()
@@ -149,12 +245,10 @@ class StealRows:
         else:
             i = len(self.task)
             self.task.append(None)
-            self.key.append(None)
             if i >= len(self.lvl):
                 self._grow()
-        key = (ts.priority, self.arrival, i)
-        self.arrival += 1
-        self.task[i], self.key[i] = ts, key
+        self.task[i] = ts
+        self.live[i] = True
         self.lvl[i] = level
         pf = ts.prefix
         self.fst[i] = 1 if pf.name in fast_tasks else 0
@@ -165,68 +259,145 @@ class StealRows:
         self.dmat[i, :k] = ids[:k]
         if len(ids) > self.KD:
             self.more[i] = ids[self.KD:]
+        pk = pack_priority(ts.priority)
+        if pk is None:
+            self.pk_bad[i] = ts.priority
+            pk = 0
+        self.pk[i] = pk
+        self.arr[i] = self.arrival
+        self.arrival += 1
+        self.rst[i] = 1 if (ts.worker_restrictions or ts.host_restrictions or ts.resource_restrictions) else 0
         self.slot[ts] = i
-        self.order.add(key)
 
     def remove(self, ts) -> None:
         i = self.slot.pop(ts, None)
         if i is None:
             return
-        self.order.remove(self.key[i])
         n = int(self.nd[i])
         for j in self.dmat[i, :min(n, self.KD)].tolist() + self.more.pop(i, []):
             self.data_ref[j] -= 1
             if self.data_ref[j] == 0:
                 del self.data_id[self.data[j]]
                 self.data[j] = None
+                self.hcnt[j] = 0
+                self.hmore.pop(j, None)
                 self.data_free.append(j)
-        self.task[i] = self.key[i] = None
+        self.pk_bad.pop(i, None)
+        self.live[i] = False
+        self.task[i] = None
         self.free.append(i)
 
     def clear(self) -> None:
         self.__init__()
 
-    def problem(self, plugin) -> tuple[dict, list, list]:
-        """Same result as ``steal_problem_from_state(plugin)`` (up to the numbering of the
-        dependencies, which the device does not order by)."""
+    def problem(self, plugin) -> tuple[dict, np.ndarray, list]:
+        """The dgp_steal_balance inputs of the current state -> (problem dict, the row slot
+        of each problem task, workers in device order). The rows go in slot order with
+        their (priority, arrival) keys; the device orders them (dgp_steal_order)."""
         s = plugin.scheduler
         wss = list(s.workers.values())
         widx = {ws.address: i for i, ws in enumerate(wss)}
-        T = len(self.order)
-        rows = np.fromiter((k[2] for k in self.order), np.int64, T)
-        tasks = [self.task[i] for i in rows.tolist()]
+        n = len(self.task)
+        rows = np.flatnonzero(self.live[:n])
+        T = len(rows)
+        sel = slice(0, n) if T == n else rows  # no free slot: the columns are read as views
         p = _worker_columns(plugin, s, wss)
         amap = np.array([widx.get(a, -1) for a in self.addrs] or [0], np.int32)
-        p["victim"] = amap[self.vic[rows]]
+        p["victim"] = amap[self.vic[sel]]
         # get_task_duration (scheduler.py:3024-3041) per prefix; its unknown_durations side
         # effect for the tasks of prefixes without a duration
         pd = np.array([pf.duration_average for pf in self.prefixes] or [0.0], np.float64)
-        dur = pd[self.pfx[rows]]
+        dur = pd[self.pfx[sel]]
         for k in np.flatnonzero(~(dur >= 0)).tolist():
-            dur[k] = s.get_task_duration(tasks[k])
+            dur[k] = s.get_task_duration(self.task[int(rows[k])])
         p["duration"] = dur
-        p["fast"] = self.fst[rows]
-        p["level_in"] = self.lvl[rows]
-        cnt = self.nd[rows].astype(np.int64)
+        p["fast"] = self.fst[sel]
+        p["level_in"] = self.lvl[sel]
+        cnt = self.nd[sel].astype(np.int64)
         dep_ptr = np.zeros(T + 1, np.int64)
         np.cumsum(cnt, out=dep_ptr[1:])
-        gids = np.empty(int(dep_ptr[-1]), np.int64)
-        r_, j_ = np.nonzero(np.arange(self.KD)[None, :] < np.minimum(cnt, self.KD)[:, None])
-        gids[dep_ptr[r_] + j_] = self.dmat[rows[r_], j_]
-        for r in np.flatnonzero(cnt > self.KD).tolist():
-            ex = self.more[int(rows[r])]
-            gids[dep_ptr[r] + self.KD:dep_ptr[r + 1]] = ex
-        uniq, inv = np.unique(gids, return_inverse=True)  # monotone: rows stay ascending
-        data = [self.data[j] for j in uniq.tolist()]
-        holders = [sorted(widx[ws.address] for ws in (dts.who_has or ())) for dts in data]
-        hptr = np.zeros(len(data) + 1, np.int64)
-        np.cumsum([len(h) for h in holders], out=hptr[1:])
-        p.update(dep_ptr=dep_ptr, dep_idx=inv.astype(np.int32).reshape(-1),
-                 data_nbytes=np.array([dts.nbytes for dts in data], np.int64),
-                 data_get_nbytes=np.array([dts.get_nbytes() for dts in data], np.int64),
-                 holder_ptr=hptr, holder_idx=np.array([w for h in holders for w in h], np.int32))
-        _restriction_rows(p, s, tasks, widx)
-        return p, tasks, wss
+        inrow = np.arange(self.KD)[None, :] < np.minimum(cnt, self.KD)[:, None]
+        if not self.more:  # every row in its slot: the row-major selection is the CSR
+            gids = self.dmat[sel][inrow]
+        else:
+            gids = np.empty(int(dep_ptr[-1]), np.int64)
+            r_, j_ = np.nonzero(inrow)
+            gids[dep_ptr[r_] + j_] = self.dmat[rows[r_], j_]
+            for r in np.flatnonzero(cnt > self.KD).tolist():
+                gids[dep_ptr[r] + self.KD:dep_ptr[r + 1]] = self.more[int(rows[r])]
+        nd_ = len(self.data)
+        hc = self.hcnt[:nd_].astype(np.int64)
+        hptr = np.zeros(nd_ + 1, np.int64)
+        np.cumsum(hc, out=hptr[1:])
+        inline = np.minimum(hc, self.HM)
+        m = np.arange(self.HM)[None, :] < inline[:, None]
+        hm = np.where(m, amap[self.hold[:nd_]], np.iinfo(np.int32).max)
+        if self.hmore:  # rows with more holders than HM: their full lists
+            hidx = np.empty(int(hptr[-1]), np.int32)
+            big = np.zeros(nd_, bool)
+            big[list(self.hmore)] = True
+            mm = m & ~big[:, None]
+            hm_small = np.sort(np.where(mm, hm, np.iinfo(np.int32).max), axis=1)
+            rr, cc = np.nonzero(np.arange(self.HM)[None, :] < np.where(big, 0, inline)[:, None])
+            hidx[hptr[rr] + cc] = hm_small[rr, cc]
+            for j, ex in self.hmore.items():
+                hidx[hptr[j]:hptr[j + 1]] = np.sort(np.concatenate([hm[j, :self.HM], amap[np.asarray(ex, np.int64)]]))
+        else:
+            hm.sort(axis=1)
+            hidx = hm[m]
+        p.update(dep_ptr=dep_ptr, dep_idx=gids.astype(np.int32), data_nbytes=self.dnb[:nd_],
+                 data_get_nbytes=self.dgnb[:nd_], holder_ptr=hptr, holder_idx=hidx.astype(np.int32))
+        if self.pk_bad:  # priorities that do not pack: the rows' ranks in the host's order
+            keys = [(self.pk_bad[i] if i in self.pk_bad else self.task[i].priority, int(self.arr[i]))
+                    for i in rows.tolist()]
+            order = sorted(range(T), key=keys.__getitem__)
+            rank = np.empty(T, np.int64)
+            rank[order] = np.arange(T)
+            p["task_prio"], p["task_arrival"] = rank, np.zeros(T, np.int64)
+        else:
+            p["task_prio"], p["task_arrival"] = self.pk[sel], self.arr[sel]
+        rpos = np.flatnonzero(self.rst[sel]).tolist()
+        if rpos:
+            _restriction_rows(p, s, [(k, self.task[int(rows[k])]) for k in rpos], T, widx)
+        return p, rows, wss
+
+
+def ordered_problem(p, slots):
+    """A StealRows problem (rows in slot order with their task_prio / task_arrival keys) with
+    its tasks put in the device's walk order (ascending priority, then arrival) -- the
+    layout of steal_problem_from_state; for tests and checks. Returns (problem, slots)."""
+    perm = np.lexsort((p["task_arrival"], p["task_prio"]))
+    q = {k: v for k, v in p.items() if k not in ("task_prio", "task_arrival")}
+    for k in ("victim", "duration", "fast", "level_in"):
+        q[k] = p[k][perm]
+    cnt = np.diff(p["dep_ptr"])[perm]
+    dp = np.zeros(len(perm) + 1, np.int64)
+    np.cumsum(cnt, out=dp[1:])
+    q["dep_ptr"] = dp
+    q["dep_idx"] = np.concatenate([p["dep_idx"][p["dep_ptr"][t]:p["dep_ptr"][t + 1]] for t in perm] or
+                                  [np.zeros(0, np.int32)]).astype(np.int32)
+    if p.get("restr_flags") is not None:
+        rc = np.diff(p["restr_ptr"])[perm]
+        rp = np.zeros(len(perm) + 1, np.int64)
+        np.cumsum(rc, out=rp[1:])
+        q["restr_ptr"] = rp
+        q["restr_idx"] = np.concatenate([p["restr_idx"][p["restr_ptr"][t]:p["restr_ptr"][t + 1]] for t in perm] or
+                                        [np.zeros(0, np.int32)]).astype(np.int32)
+        q["restr_flags"] = p["restr_flags"][perm]
+    return q, np.asarray(slots)[perm]
+
+
+def balance_plan(plugin, engine):
+    """GPUWorkStealing.balance()'s decisions from the plugin's state, before any of them is
+    applied: (device outputs, each output row's StealRows slot, workers in device order), or
+    None for balance()'s early exits (stealing.py:409-411). ``plugin``: the plugin (or a
+    stand-in with its attributes: scheduler, rows, in_flight_occupancy / in_flight_tasks)."""
+    s = plugin.scheduler
+    if not s.idle or len(s.idle) == len(s.workers):
+        return None
+    p, rows, wss = plugin.rows.problem(plugin)
+    out = engine.steal_balance(p)
+    return out, rows, wss
 
 
 def _worker_columns(plugin, s, wss) -> dict:
@@ -243,12 +414,12 @@ def _worker_columns(plugin, s, wss) -> dict:
     )
 
 
-def _restriction_rows(p, s, tasks, widx) -> None:
-    """valid_workers (scheduler.py:3043-3107) of the restricted tasks, read at balance time."""
-    T = len(tasks)
+def _restriction_rows(p, s, at, T, widx) -> None:
+    """valid_workers (scheduler.py:3043-3107) of the restricted tasks, read at balance time.
+    ``at``: (problem position, TaskState) of the tasks that may be restricted."""
     flags = np.zeros(T, np.uint8)
     vrows = {}
-    for i, ts in enumerate(tasks):
+    for i, ts in at:
         if ts.worker_restrictions or ts.host_restrictions or ts.resource_restrictions:
             vw = s.valid_workers(ts)
             if vw is None:
@@ -279,6 +450,34 @@ class GPUWorkStealing(WorkStealing):
         self.gpu_stats = Counter()
         self.rows = StealRows()  # before the reference __init__: its hooks may fill the bins
         super().__init__(scheduler)
+        self._wrap_replicas()
+
+    def _wrap_replicas(self):
+        """who_has of the dependencies in the rows follows SchedulerState.add_replica /
+        remove_replica / remove_all_replicas (scheduler.py:3148-3171; every replica change
+        goes through them), so balance() reads no TaskState."""
+        s = self.scheduler
+        add, rem, clr = (getattr(s, n, None) for n in ("add_replica", "remove_replica", "remove_all_replicas"))
+        if add is None or rem is None or clr is None or getattr(s, "_gpu_steal_replicas", None) is self:
+            return
+
+        def add_replica(ts, ws):
+            r = add(ts, ws)
+            self.rows.replica(ts, ws.address, +1)
+            return r
+
+        def remove_replica(ts, ws):
+            r = rem(ts, ws)
+            self.rows.replica(ts, ws.address, -1)
+            return r
+
+        def remove_all_replicas(ts):
+            r = clr(ts)
+            self.rows.replicas_cleared(ts)
+            return r
+
+        s.add_replica, s.remove_replica, s.remove_all_replicas = add_replica, remove_replica, remove_all_replicas
+        s._gpu_steal_replicas = self
 
     # the bins' task rows follow the reference hooks (stealing.py:218-239, :511-516)
     def put_key_in_stealable(self, ts) -> None:
@@ -295,15 +494,18 @@ class GPUWorkStealing(WorkStealing):
         super().restart(scheduler)
         self.rows.clear()
 
-    def problem(self):
-        """The dgp_steal_balance inputs of the current state (the incremental rows; rebuilt
-        from the bins if anything changed them outside the hooks)."""
+    def _rows_current(self):
+        """The rows, rebuilt from the bins if anything changed the bins outside the hooks."""
         if len(self.rows) != len(self.key_stealable):
             self.gpu_stats["rows_rebuilt"] += 1
             self.rows.clear()
             for ts, (worker, level) in self.key_stealable.items():
                 self.rows.put(ts, worker, level)
-        return self.rows.problem(self)
+        return self.rows
+
+    def problem(self):
+        """The dgp_steal_balance inputs of the current state: (problem, row slots, workers)."""
+        return self._rows_current().problem(self)
 
     def _engine(self):
         if self.engine is None:
@@ -318,14 +520,16 @@ class GPUWorkStealing(WorkStealing):
     def balance(self) -> None:
         s = self.scheduler
         start = time()
-        # the early exits of balance() (stealing.py:409-411): no thief, or every worker one
-        if not s.idle or len(s.idle) == len(s.workers):
+        self._rows_current()
+        plan = balance_plan(self, self._engine())  # the early exits of balance() (:409-411) inside
+        if plan is None:
             return
-        p, tasks, wss = self.problem()
-        out = self._engine().steal_balance(p)
+        out, rows, wss = plan
+        task = self.rows.task
+        slots = rows[out["st_task"]].tolist()
         log = []
-        for k in range(len(out["st_task"])):
-            ts = tasks[int(out["st_task"][k])]
+        for k, sl in enumerate(slots):
+            ts = task[sl]
             victim, thief = wss[int(out["st_victim"][k])], wss[int(out["st_thief"][k])]
             level = int(out["st_level"][k])
             cost = float(out["st_cost"][k])

@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 17
+#define DGP_ABI_VERSION 18
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -489,6 +489,12 @@ int dgp_steal_balance(dgp_engine* e, int32_t n_workers, const int32_t* nthreads,
                       double* inflight_occupancy, int32_t* inflight_tasks, uint8_t* idle_out, uint8_t* saturated_out,
                       uint8_t* checked_out);
 
+/* dgp_steal_order: the next dgp_steal_load / dgp_steal_balance takes its tasks in ascending
+ * (priority, arrival) instead of their input order (the order the bins are walked in,
+ * stealing.py:441-461 with the canonical tie-break), sorted on the device; n_tasks must be
+ * that call's n_tasks. The plugin keeps its task rows in arrival slots (no host sort per
+ * balance() call). Outputs still index the tasks in input order. (ABI 18) */
+int dgp_steal_order(dgp_engine* e, int64_t n_tasks, const int64_t* priority, const int64_t* arrival);
 /* dgp_steal_balance in phases, for a balance() sharded over ranks (one engine per GPU):
  *   dgp_steal_load       the inputs of dgp_steal_balance; levels, bins and the initial
  *                        thief order; *n_stealable = tasks in a bin (stealing.py:220-239)

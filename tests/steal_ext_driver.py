@@ -31,7 +31,7 @@ import gen_steal as GS  # noqa: E402  (shim + reference)
 
 import numpy as np  # noqa: E402
 
-from distributed_amd.stealing import GPUWorkStealing, steal_problem_from_state  # noqa: E402
+from distributed_amd.stealing import GPUWorkStealing, ordered_problem, steal_problem_from_state  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 
@@ -40,8 +40,20 @@ class OracleEngine:
         self.calls = 0
 
     def steal_balance(self, p):
+        """The oracle on the problem in the device's walk order (dgp_steal_order's sort of
+        the rows by (task_prio, task_arrival)); the outputs index the rows as given."""
         self.calls += 1
-        return oracle.steal_balance(p)
+        if p.get("task_prio") is None:
+            return oracle.steal_balance(p)
+        perm = np.lexsort((p["task_arrival"], p["task_prio"]))
+        q, _ = ordered_problem(p, perm)
+        out = dict(oracle.steal_balance(q))
+        out["st_task"] = perm[np.asarray(out["st_task"], np.int64)].astype(np.int32)
+        if "level" in out:
+            lv = np.empty_like(np.asarray(out["level"]))
+            lv[perm] = out["level"]
+            out["level"] = lv
+        return out
 
 
 def state_of(s, steal, events, comms):
@@ -64,7 +76,9 @@ def rows_equal(steal):
     columns, and per task the same dependencies (nbytes, get_nbytes, holders) up to their
     numbering."""
     a, ta, _ = steal_problem_from_state(steal)
-    b, tb, _ = steal.problem()
+    b, slots, _ = steal.problem()
+    b, slots = ordered_problem(b, slots)  # the device's walk order
+    tb = [steal.rows.task[int(i)] for i in slots]
     assert ta == tb, "task order"
     assert set(a) == set(b), (sorted(a), sorted(b))
     per_dep = ("dep_idx", "data_nbytes", "data_get_nbytes", "holder_ptr", "holder_idx")

@@ -6,7 +6,7 @@ unknown_durations side effect), restrictions. The reference-plugin version of th
 check runs in tests/steal_ext_driver.py before every balance()."""
 import numpy as np
 
-from distributed_amd.stealing import StealRows, steal_problem_from_state
+from distributed_amd.stealing import StealRows, ordered_problem, steal_problem_from_state
 
 
 class NS:  # a plain stand-in, hashed by identity like TaskState / WorkerState
@@ -73,7 +73,9 @@ def test_incremental_rows_equal_the_full_rebuild():
 
     def check():
         a, ta, _ = steal_problem_from_state(plugin)
-        b, tb, _ = rows.problem(plugin)
+        b, slots, _ = rows.problem(plugin)
+        b, slots = ordered_problem(b, slots)  # the device's walk order
+        tb = [rows.task[int(i)] for i in slots]
         assert ta == tb
         assert set(a) == set(b)
         for k in a:
@@ -105,6 +107,27 @@ def test_incremental_rows_equal_the_full_rebuild():
         put(ts)
     for ts in tasks[1:1500:7]:  # a task put again (a recalculated cost) moves to the end of its ties
         put(ts)
+    check()
+    # who_has changes through the scheduler's replica hooks (add_replica / remove_replica /
+    # remove_all_replicas), which the plugin forwards to the rows
+    for i, d in enumerate(data[:60]):
+        ws = wss[(i * 5) % 16]
+        if i % 3 == 0 and len(d.who_has) > 1:
+            h = sorted(d.who_has, key=lambda w: w.address)[0]
+            d.who_has.discard(h)
+            rows.replica(d, h.address, -1)
+        elif i % 3 == 1:
+            d.who_has.add(ws)
+            rows.replica(d, ws.address, +1)
+        else:
+            for w in wss[:12]:  # more holders than a dependency row keeps inline
+                d.who_has.add(w)
+                rows.replica(d, w.address, +1)
+    check()
+    for d in data[60:70]:
+        for w in list(d.who_has):
+            d.who_has.discard(w)
+        rows.replicas_cleared(d)
     check()
     assert "p2" in s.unknown_durations
     rows.clear()

@@ -2,7 +2,7 @@
 /root/reference through tests/golden/_refshim.py; the reference never travels to the GPU
 box). One process, one core (the scheduler is single-threaded), PYTHONHASHSEED=0.
 
-    PYTHONHASHSEED=0 taskset -c 2 /opt/conda/bin/python3.9 tools/ref_python_time.py c2|c3|c4 [--out FILE]
+    PYTHONHASHSEED=0 taskset -c 2 /opt/conda/bin/python3.9 tools/ref_python_time.py c2|c3|c4|c4mtr [--out FILE]
 
 c2 / c3: the BASELINE.json C2 (1M-task random DAG x 1,024 workers, saturation 1.1) and
 C3 (P2P-shuffle shape, 66,666 partitions x 512 workers) graphs of distributed_amd/graphs.py,
@@ -175,6 +175,21 @@ def main():
         res = dict(config=f"C4: gen_steal.build(4096 workers, {T} tasks, nthreads 2, hot 10%, seed 1)",
                    balance_s=secs, steal_requests=n_req, state_build_s=built,
                    move_task_request_note="included: the reference's balance() sends each request itself")
+    elif which == "c4mtr":  # the reference's own WorkStealing.move_task_request, per request
+        import gen_steal as GS
+
+        T = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 100_000
+        s, steal, widx, tidx, data, work, deps_of, events, comms = GS.build(4096, T, 2, 0.1, 1)
+        tasks = sorted(steal.key_stealable, key=lambda ts: ts.priority)
+        thieves = sorted(s.idle.values(), key=lambda ws: ws.address)
+        n = min(20_000, len(tasks))
+        a = time.perf_counter()
+        for i, ts in enumerate(tasks[:n]):
+            steal.move_task_request(ts, ts.processing_on, thieves[i % len(thieves)])
+        secs = time.perf_counter() - a
+        res = dict(config=f"C4: gen_steal.build(4096 workers, {T} tasks, nthreads 2, hot 10%, seed 1); "
+                          f"move_task_request for the first {n} stealable tasks (priority order), thieves round-robin",
+                   move_task_request_us=round(1e6 * secs / n, 2), requests=n)
     else:
         raise SystemExit(f"unknown config {which}")
     res.update(reference="/root/reference (fjetter/distributed) SchedulerState / WorkStealing, unmodified, via "
