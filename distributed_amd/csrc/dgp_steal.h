@@ -649,9 +649,17 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           const unsigned long long needs = __ballot(todo && !(hasL && aliveL));
           const int d = needs ? (int)__builtin_ctzll(needs) : nq;
           const bool inw = todo && lane < d;
+          // which thieves repeat in the window: every lane of the window writes its lane to
+          // its thief's slot, a lane that finds another's marks the slot (0xff)
           if (inw) own[thL] = (uint8_t)lane;
           __syncthreads();
-          const bool repeats = __ballot(inw && own[thL] != (uint8_t)lane) != 0;
+          const bool lost_race = inw && own[thL] != (uint8_t)lane;
+          __syncthreads();
+          if (lost_race) own[thL] = 0xff;
+          __syncthreads();
+          const bool rep = inw && own[thL] == 0xff;
+          const unsigned long long repm = __ballot(rep);
+          const bool repeats = repm != 0;
 #if DGP_STEAL_PROF
           if (repeats) pr_many++;
           const unsigned long long wc0 = __builtin_amdgcn_s_memtime();
@@ -671,26 +679,22 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           // thieves at once (one fp64 add per link, the reference's order)
           double tb = ifoL;
           int pb = pendL;
-          int prv = -1, nxt = 64;  // nearest earlier / later lane of the window with the same thief
-          if (repeats) {
-            for (int m = j; m < d; m++) {
-              const int thm = __builtin_amdgcn_readlane(thL, m);
-              const bool same = inw && thL == thm;
-              prv = same && lane > m ? m : prv;
-              nxt = same && lane < m && nxt == 64 ? m : nxt;
+          unsigned long long mym = 0;  // the window's lanes of this lane's thief when it repeats
+          for (unsigned long long rm = repm; rm;) {  // one chain per repeated thief, in task order
+            const int k0 = (int)__builtin_ctzll(rm);
+            const int x = __builtin_amdgcn_readlane(thL, k0);
+            const unsigned long long mx = __ballot(inw && thL == x);
+            rm &= ~mx;
+            double cur = rl_f64(ifoL, k0);  // every lane of a thief holds its accounts
+            const int p0 = __builtin_amdgcn_readlane(pendL, k0);
+            for (unsigned long long q = mx; q; q &= q - 1) {
+              const int k = (int)__builtin_ctzll(q);
+              tb = lane == k ? cur : tb;
+              cur = cur + rl_f64(dtL, k);
             }
-            const int src = prv >= 0 ? prv : lane;
-            const double pdt = __shfl(dtL, src);
-            bool done = prv < 0;
-            while (__ballot(inw && !done)) {
-              const double ptb = __shfl(tb, src);
-              const int ppb = __shfl(pb, src);
-              const bool pdone = __shfl((int)done, src) != 0;
-              if (!done && pdone) {
-                tb = ptb + pdt;
-                pb = ppb + 1;
-                done = true;
-              }
+            if ((mx >> lane) & 1ull) {
+              mym = mx;
+              pb = p0 + __builtin_popcountll(mx & ((1ull << lane) - 1ull));
             }
           }
 #if DGP_STEAL_PROF
@@ -712,7 +716,9 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           const bool com = inw && lane < b;
           const unsigned long long cm = __ballot(com);
           if (b < d) ifo_v = rl_f64(vb, b);  // the victim's chain up to the prefix's end
-          if (com && nxt >= b) {  // each thief takes the account of its last accepted task (:327-331)
+          // the last accepted task of each thief carries its accounts (:327-331)
+          const unsigned long long later = mym & ~((2ull << lane) - 1ull) & (b >= 64 ? ~0ull : ((1ull << b) - 1ull));
+          if (com && later == 0) {
             ifo[thL] = tb + dtL;
             pend[thL] = pb + 1;
           }
