@@ -10,7 +10,7 @@ SRC = [os.path.join(PKG, "csrc", "dgplace.hip")]
 DEPS = [os.path.join(PKG, "csrc", "dgp_device.h"), os.path.join(PKG, "csrc", "dgp_stream.h"),
         os.path.join(PKG, "csrc", "dgp_steal.h"), os.path.join(PKG, "csrc", "dgp_service.h"),
         os.path.join(PKG, "csrc", "dgp_events.h"), os.path.join(PKG, "csrc", "dgp_svcmsg.h"),
-        os.path.join(PKG, "csrc", "dgp_msgs.h"), os.path.join(PKG, "csrc", "dgp_exev.h")]
+        os.path.join(PKG, "csrc", "dgp_msgs.h")]
 OUT = os.path.join(PKG, "libdgplace.so")
 # the same sources with a 64-slot stimulus window and no wait-in-place claims: graphs with
 # restrictions run this build (engine.py PlacementEngine.load)

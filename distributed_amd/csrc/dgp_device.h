@@ -256,7 +256,6 @@ struct Dev {
   double* dring;             // stimulus durations [DR][PX] when the graph has more prefixes than a descriptor carries
   int32_t* touch_ring;       // distinct workers each prefetched stimulus touches [DR][TMAX]
   uint2* thdr;               // per descriptor row: (flags, touched-worker count), written by PRE for REG
-  uint4* frow;               // F_FAST stimuli: PRE's frontier-candidate rows [DR][NFF][TF] (dgp_stream.h)
   int32_t* s2_task;  // per-slot staging of placements [WIN][PLC]
   int32_t* s2_worker;
   int64_t* s2_comm;

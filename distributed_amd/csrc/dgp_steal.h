@@ -659,9 +659,8 @@ __global__ void __launch_bounds__(64) k_balance(Prob P) {
           __syncthreads();
           const bool rep = inw && own[thL] == 0xff;
           const unsigned long long repm = __ballot(rep);
-          const bool repeats = repm != 0;
 #if DGP_STEAL_PROF
-          if (repeats) pr_many++;
+          if (repm) pr_many++;
           const unsigned long long wc0 = __builtin_amdgcn_s_memtime();
 #endif
           // the victim's chain over the window; a lane without a thief subtracts +0.0 (exact)

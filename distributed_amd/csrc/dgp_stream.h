@@ -48,9 +48,6 @@ __constant__ Dev c_dev;
 #ifndef DGP_EXE_PRIO
 #define DGP_EXE_PRIO 1  // 0: fixed priority 2; 1 / 2: executors issue at priority 3 while running a stimulus, 1 / 0 while polling
 #endif
-#ifndef DGP_VMPROBE
-#define DGP_VMPROBE 0  // diagnostics: store-drain time at each claim attempt (prof 11 / 12)
-#endif
 #ifndef DGP_EXE_SLEEP
 #define DGP_EXE_SLEEP 1  // s_sleep units (64 clocks) between an idle executor's polls
 #endif
@@ -65,35 +62,6 @@ __constant__ Dev c_dev;
 #endif
 #ifndef DGP_RUN_PAR
 #define DGP_RUN_PAR 1  // single-worker runs of one prefix: every member's record at once (lane = member)
-#endif
-#ifndef DGP_OCC_BATCH
-#define DGP_OCC_BATCH 0  // executors' occupancy: every prefix duration load issued before the sum
-#endif
-#ifndef DGP_EXE_CONT
-#define DGP_EXE_CONT 0  // an executor first claims the stimulus its release of the completing worker made ready
-#endif
-#ifndef DGP_STAGE_PRIO
-#define DGP_STAGE_PRIO 0  // issue priority of the builder / prefetcher waves
-#endif
-#ifndef DGP_DBG_TASK
-#define DGP_DBG_TASK 0  // diagnostics: exe_local dumps the candidate keys of frontier task D.dbg_task
-#endif
-#ifndef DGP_FAST
-#define DGP_FAST 0  // F_FAST stimuli take exe_fast (0: exe_local). Measured (profiles/r04ab): with exe_local
-                    // inlined and no exe_fast, C2 1.021 s vs 1.003-1.01 s and C3 0.118 vs 0.129 s
-#endif
-#ifndef DGP_EXEV
-#define DGP_EXEV 0  // 1: F_FAST stimuli on the LDS worker layout take exe_v (dgp_exev.h), the vector form: measured
-                    // 30% slower per stimulus than exe_local (profiles/r05/exev_*), kept off
-#endif
-#ifndef DGP_LOCAL_INLINE
-#define DGP_LOCAL_INLINE 1  // exe_local inlined into the claim loop (else out of line, its own registers)
-#endif
-#ifndef DGP_STAGE_DELAY
-#define DGP_STAGE_DELAY 0  // diagnostics: 1 / 2 delay every BLD / PRE batch (4 x s_sleep 127, ~32k cycles)
-#endif
-#ifndef DGP_DESC_G
-#define DGP_DESC_G 1  // PRE's gathered descriptor build first (0: the sequential form only)
 #endif
 #ifndef DGP_RB
 #define DGP_RB 8  // registrar batch (stimuli registered per poll, one lane each)
@@ -115,9 +83,6 @@ static_assert(WIN >= 32 && WIN <= 64, "DGP_WIN must be in [32, 64]");
 #define DGP_WAITC 1
 #endif
 constexpr bool WAITC = DGP_WAITC != 0;
-#ifndef DGP_WAITC_AHEAD
-#define DGP_WAITC_AHEAD 32  // a stimulus that would wait in place is claimed only this close to the oldest (32: any; 4 / 8 / 20 measured slower)
-#endif
 static_assert(!WAITC || WIN == 32, "DGP_WAITC keeps the candidate-only registrations in the masks' high half");
 // the mask bits of slot s: its registration (low half) and, with WAITC, the candidate-only
 // flag of this worker for s (high half)
@@ -163,16 +128,7 @@ static_assert((RS & (RS - 1)) == 0 && RS >= WIN && RS <= DR, "DGP_RS must be a p
 // (held by that worker) and one release: it can be part of a single-worker run (exe_run).
 // F_RUNM (REG): F_SIMPLE and so is the stimulus just before it, on the same worker: a run
 // continues through it, so only the run-capable executor takes it
-// F_FAST (PRE): a local stimulus the lean executor path takes (exe_fast): at most NFF frontier
-// tasks, none restricted, at most TF touched workers, P <= PD; PRE wrote its frow rows
-enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16, F_SIMPLE = 32, F_RUNM = 64,
-                  F_FAST = 128 };
-// exe_fast's rows (D.frow, one block of FRS entries per descriptor row): row j, entry i =
-// frontier task j's comm_bytes / bandwidth and comm_bytes on touched worker i, written for its
-// candidates only (the frontier entry's .w is the candidates' touch-index mask)
-constexpr int NFF = 4;
-constexpr int TF = 16;
-constexpr int FRS = NFF * TF;
+enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16, F_SIMPLE = 32, F_RUNM = 64 };
 // K_COMPLETE_LR: the completion of a long-running task (its prefix count left the worker's and
 // the global dict at add_to_long_running :747-757; remove_from_processing :764-766)
 enum : int { K_COMPLETE = 1, K_PLACE = 2, K_COMPLETE_LR = 3 };
@@ -594,23 +550,6 @@ __device__ __forceinline__ double occ_dict(const WDict& d, int64_t netocc, DTab 
 __device__ __forceinline__ double occ_dict_r(const WDict& d, double net_bw, DTab dt, const Dev& D) {
   const uint32_t n = wd_n(d.ord);
   double res = 0.0;
-  if (DGP_OCC_BATCH) {
-    // every slot's duration load issued back to back (one LDS latency, not one per prefix),
-    // then the sum in dict insertion order: the same fp64 operations as below
-    uint32_t v[PD];
-    double dv[PD];
-#pragma unroll
-    for (int i = 0; i < PD; i++) {
-      v[i] = wd_slot(d, i);
-      dv[i] = dt[(v[i] >> 24) & (PX - 1)];
-    }
-#pragma unroll
-    for (int i = 0; i < PD; i++) {
-      const double term = (dv[i] < 0 ? D.unknown_duration : dv[i]) * (double)(v[i] & 0xffffffu);
-      if ((uint32_t)i < n) res += term;
-    }
-    return res + net_bw;
-  }
   // the first two entries' duration loads issued together (most workers hold at most two
   // prefixes), then the rest one at a time; the same fp64 operations in dict order
   {
@@ -1466,7 +1405,6 @@ __device__ __attribute__((always_inline)) void build_desc_seq(const Dev& D, SLds
     PROF(atomicAdd(&L.c.prof[20], 1ull));  // diagnostics: why stimuli run global
   }
   int n = E_HDR, nrel = 0, nf = 0, sumkx = 0;
-  bool anyrx = false;  // a restricted frontier task (not on the F_FAST path)
   touch(w, false);
   int h_dep0 = -1;  // holder of the first dependency
   if (!(flags & F_GLOBAL)) {
@@ -1509,7 +1447,6 @@ __device__ __attribute__((always_inline)) void build_desc_seq(const Dev& D, SLds
     // holders & valid; none: the valid set; valid empty: loose -> the holders, else
     // no-worker (global). They follow the dependency entries; the holders are not touched
     const bool rx = restricted_nonrootish(D, x);
-    anyrx = anyrx || rx;
     int cw[RC_MAX];
     int nc = 0;
     if (rx) {
@@ -1540,46 +1477,27 @@ __device__ __attribute__((always_inline)) void build_desc_seq(const Dev& D, SLds
     }
     const int nx = n++;  // the task's entry, written below with its candidates' touch mask
     sumkx += kx;
-    // decide_worker's candidates (:8571-8574) are the dependencies' holders; PRE resolves
-    // their state-independent objective terms for exe_fast (worker_objective :3136-3138:
-    // comm_bytes = the bytes of the dependencies the candidate does not hold, / bandwidth)
+    // decide_worker's candidates (:8571-8574) are the dependencies' holders: their touch
+    // indices, the mask the executor's argmin takes
     int tix[KX_MAX];
-    int64_t nbq[KX_MAX];
-    int64_t tot = 0;
 #pragma unroll
     for (int q = 0; q < KX_MAX; q++) {
       tix[q] = -1;
-      nbq[q] = 0;
       if (q < kx) {
         const int d = D.dep_idx[x0 + q];
         const int64_t nb = nbv(D, D.res_nbytes[d]);
         const int hd = D.holder_of[d];
         if ((D.evf & EVF_MULTI) && (D.tdyn[d] & TD_MULTI)) evg = true;
         if (!rx) tix[q] = touch(hd, true);
-        nbq[q] = nb;
-        tot += nb;
         E[n++] = make_uint4((unsigned)d, (unsigned)hd, lo32(nb), hi32(nb));
       }
     }
     uint32_t cmask = 0;  // touch indices (< 32) of the candidates
     if (!rx) {
-      const int jf = nf - 1;
-      uint4* FR = D.frow + (size_t)(r & (DR - 1)) * FRS + (size_t)jf * TF;
 #pragma unroll
       for (int q = 0; q < KX_MAX; q++) {
         const int i = tix[q];
-        if (q < kx && i >= 0 && i < 32 && !((cmask >> i) & 1u)) {
-          cmask |= 1u << i;
-          if ((DGP_FAST || DGP_EXEV) && jf < NFF && i < TF) {  // exe_fast's / exe_v's rows
-            int64_t held = 0;
-#pragma unroll
-            for (int q2 = 0; q2 < KX_MAX; q2++)
-              if (q2 < kx && tix[q2] == i) held += nbq[q2];
-            const int64_t comm = tot - held;  // int64: exact in any order
-            const double cd = (double)comm / (double)D.bandwidth;
-            FR[i] = make_uint4(dlo(cd), dhi(cd), lo32(comm), hi32(comm));
-          }
-        }
+        if (q < kx && i >= 0 && i < 32) cmask |= 1u << i;
       }
     }
     E[nx] = make_uint4((unsigned)x, (unsigned)D.prefix[x], (unsigned)(kx | (nc << 8) | (rx ? 1 << 16 : 0)), cmask);
@@ -1598,8 +1516,6 @@ __device__ __attribute__((always_inline)) void build_desc_seq(const Dev& D, SLds
       (kt == 0 || h_dep0 == w) && D.P <= PD)  // a run shares the head's descriptor durations
     flags |= F_SIMPLE;
   if (flags & F_GLOBAL) nt = 0;
-  // exe_fast takes it: PRE wrote the rows of its frontier's candidates above
-  if (!(flags & F_GLOBAL) && nf <= NFF && nt <= TF && D.P <= PD && !anyrx) flags |= F_FAST;
   int32_t* T = D.touch_ring + (size_t)(r & (DR - 1)) * TMAX;
   for (int i = 0; i < nt; i++) T[i] = scr[i];
   E[0] = make_uint4((unsigned)t, (unsigned)w, (unsigned)p, flags);
@@ -1618,7 +1534,7 @@ __device__ __attribute__((always_inline)) void build_desc_seq(const Dev& D, SLds
 // frontier marks, then per frontier task its fields, its dependencies' ids and fields --
 // instead of one or two per entry. PRE's batch is as slow as its slowest lane, so every
 // size takes this path (a completion with many dependents costs one more pair of round trips
-// per 8 of them). The descriptor, the touch list and the frow rows come out exactly as
+// per 8 of them). The descriptor and the touch list come out exactly as
 // build_desc_seq writes them. false (nothing written): the graph has restrictions (their
 // resolved candidates stay with build_desc_seq).
 constexpr int GC = 8;  // entries gathered per round trip
@@ -1708,7 +1624,6 @@ __device__ __attribute__((always_inline)) bool build_desc_g(const Dev& D, SLds& 
     }
   }
   // ---- dependents in ascending priority = frontier order (a global stimulus stops the walk)
-  uint4* FRb = D.frow + (size_t)(r & (DR - 1)) * FRS;
   const int nd = (int)(f1 - f0);
   for (int c0 = 0; c0 < nd && !(flags & F_GLOBAL); c0 += GC) {
     int xq[GC];
@@ -1744,7 +1659,7 @@ __device__ __attribute__((always_inline)) bool build_desc_g(const Dev& D, SLds& 
 #pragma unroll 1
     for (; fm && !(flags & F_GLOBAL); fm &= fm - 1) {
       const int q = __builtin_ctz(fm);  // (lane-varying: selected without indexing the arrays)
-      const int j = nf++;
+      nf++;
       const int x = DGP_SEL8(xq, q), kx = DGP_SEL8(fkx, q);
       const uint8_t ftq = DGP_SEL8(ftf, q);
       const int64_t fxq = DGP_SEL8(fx0, q);
@@ -1771,17 +1686,14 @@ __device__ __attribute__((always_inline)) bool build_desc_g(const Dev& D, SLds& 
       }
       const int nx = n++;
       sumkx += kx;
-      // decide_worker's candidates (:8571-8574) are the dependencies' holders; their
-      // state-independent objective terms for exe_fast (worker_objective :3136-3138:
-      // comm_bytes = the bytes of the dependencies the candidate does not hold, / bandwidth)
+      // decide_worker's candidates (:8571-8574) are the dependencies' holders: their touch
+      // indices, the mask the executor's argmin takes
       int tix[KX_MAX];
-      int64_t tot = 0;
 #pragma unroll
       for (int i = 0; i < KX_MAX; i++) {
         tix[i] = -1;
         if (i < kx) {
           tix[i] = touch(hx[i], true);
-          tot += nbx[i];
           E[n++] = make_uint4((unsigned)dx[i], (unsigned)hx[i], lo32(nbx[i]), hi32(nbx[i]));
         }
       }
@@ -1789,18 +1701,7 @@ __device__ __attribute__((always_inline)) bool build_desc_g(const Dev& D, SLds& 
 #pragma unroll
       for (int i = 0; i < KX_MAX; i++) {
         const int ti = tix[i];
-        if (i < kx && ti >= 0 && ti < 32 && !((cmask >> ti) & 1u)) {
-          cmask |= 1u << ti;
-          if ((DGP_FAST || DGP_EXEV) && j < NFF && ti < TF) {  // exe_fast's / exe_v's rows
-            int64_t held = 0;
-#pragma unroll
-            for (int i2 = 0; i2 < KX_MAX; i2++)
-              if (i2 < kx && tix[i2] == ti) held += nbx[i2];
-            const int64_t comm = tot - held;  // int64: exact in any order
-            const double cd = (double)comm / (double)D.bandwidth;
-            FRb[(size_t)j * TF + ti] = make_uint4(dlo(cd), dhi(cd), lo32(comm), hi32(comm));
-          }
-        }
+        if (i < kx && ti >= 0 && ti < 32) cmask |= 1u << ti;
       }
       E[nx] = make_uint4((unsigned)x, (unsigned)fpq, (unsigned)kx, cmask);
     }
@@ -1813,7 +1714,6 @@ __device__ __attribute__((always_inline)) bool build_desc_g(const Dev& D, SLds& 
   if (!(flags & F_GLOBAL) && nt == 1 && nf == 0 && kt <= 1 && nrel <= 1 && (kt == 0 || h_dep0 == w) && D.P <= PD)
     flags |= F_SIMPLE;  // a run shares the head's descriptor durations
   if (flags & F_GLOBAL) nt = 0;
-  if (!(flags & F_GLOBAL) && nf <= NFF && nt <= TF && D.P <= PD) flags |= F_FAST;
   int32_t* T = D.touch_ring + (size_t)(r & (DR - 1)) * TMAX;
   for (int i = 0; i < nt; i++) T[i] = scr[i];
   E[0] = make_uint4((unsigned)t, (unsigned)w, (unsigned)p, flags);
@@ -1842,7 +1742,7 @@ __device__ __attribute__((noinline)) DescOut build_desc_seq_entry(long long r) {
 }
 __device__ __forceinline__ void build_desc(const Dev& D, SLds& L, long long r, int& p_out, double& dobs_out) {
   DescOut o{0, 0, 0.0};
-  if (DGP_DESC_G) o = build_desc_g_entry(r);
+  o = build_desc_g_entry(r);
   if (!o.ok) o = build_desc_seq_entry(r);
   p_out = o.p;
   dobs_out = o.dobs;
@@ -1900,8 +1800,6 @@ __device__ __attribute__((always_inline)) void role_stage(const Dev& D, SLds& L)
     }
     __threadfence_block();
     wbar();
-    if (DGP_STAGE_DELAY && KIND == DGP_STAGE_DELAY - 1)  // diagnostics: is this stage on the critical path?
-      for (int k = 0; k < 4; k++) __builtin_amdgcn_s_sleep(127);
     if (lane == 0) {
       PROF(S.prof[KIND == 0 ? 1 : 2] += mclk() - t0);
       PROF(S.prof[KIND == 0 ? 6 : 7] += 1);
@@ -2717,19 +2615,6 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     k.nb = nbj;
     k.w = cj;
     k.comm = comm;
-#if DGP_DBG_TASK
-    if (x == D.dbg_task && cand) {
-      double* B = D.dbgbuf + (size_t)lane * 8;
-      B[0] = cj;
-      B[1] = k.start;
-      B[2] = (double)k.nb;
-      B[3] = (double)comm;
-      B[4] = occj;
-      B[5] = np;
-      B[6] = (double)net;
-      B[7] = (double)wd_n(dj.ord) + 100.0 * r;
-    }
-#endif
     phase(18);
     if (TR3 && lane == 0 && j == 0) TR(r, 13);
     const unsigned long long cm = ballot(cand);
@@ -2871,417 +2756,13 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   int wk = -1;
   if (lane == jw) wk = release_worker<LW>(L, P, s, w);
   if (TR3 && lane == 0) TR(r, 18);
-  woke = rl(wk, jw);  // the stimulus next on w, if this release made it ready (DGP_EXE_CONT)
+  woke = rl(wk, jw);  // the stimulus next on w, if this release made it ready
   phase(13);
   // ------------------------------------------------ retire: LDS state, then successors
   phase(21);
   // the completed task's and the releases' TaskState fields in HBM are written by the
   // sequencer when it retires the slot (seq_bookkeeping): nothing reads them before
   phase(14);
-  finish_slot(D, L, s, r, o, pops, false);
-  phase(15);
-  return true;
-}
-
-// ============================================================ the lean local path
-// exe_fast: what exe_local does, for the F_FAST stimuli (the common local case), with the
-// state-independent work moved to PRE (its frow rows: candidate flags, comm_bytes /
-// bandwidth, lacking dependencies, released bytes per touched worker; one lane of PRE per
-// stimulus, off the chain) and the outputs staged in registers. The replay is bound by the
-// chain of stimuli sharing workers, and a wave issues about one instruction per four cycles,
-// so the latency of a stimulus is its executor's instruction count: this path keeps only the
-// state-dependent work (needs_what, the prefix dicts, occupancies, the argmin, the refill).
-
-// outputs staged in registers: placement / record k in lane k (uniform values, one select each),
-// written to the slot's staging rows with one store per field after the workers are released
-struct OutR {
-  int nrec, npl;
-  int pt, pw, pr;
-  int64_t pc, pn;
-  double ps;
-  int rw, rpk, rnp, rtk;
-  int64_t rdn;
-  double rocc, rdur;
-  __device__ __forceinline__ void init() {
-    nrec = npl = 0;
-    pt = pw = pr = 0;
-    pc = pn = 0;
-    ps = 0.0;
-    rw = rpk = rnp = rtk = 0;
-    rdn = 0;
-    rocc = rdur = 0.0;
-  }
-  __device__ __forceinline__ static int wl(int v, int l, int old) { return lane_id() == l ? v : old; }
-  __device__ __forceinline__ static int64_t wl64(int64_t v, int l, int64_t old) {
-    return mk64((unsigned)wl((int)lo32(v), l, (int)lo32(old)), (unsigned)wl((int)hi32(v), l, (int)hi32(old)));
-  }
-  __device__ __forceinline__ static double wlf(double v, int l, double old) {
-    return __longlong_as_double(wl64(__double_as_longlong(v), l, __double_as_longlong(old)));
-  }
-  __device__ __forceinline__ void place(int task, int w, int64_t comm, double start, int64_t wsnb, int route) {
-    if (npl < PLC) {
-      pt = wl(task, npl, pt);
-      pw = wl(w, npl, pw);
-      pr = wl(route, npl, pr);
-      pc = wl64(comm, npl, pc);
-      pn = wl64(wsnb, npl, pn);
-      ps = wlf(start, npl, ps);
-    }
-    npl++;
-  }
-  __device__ __forceinline__ void rec(int kind, int w, int p, int64_t dnet, double occ, int np, int task, double dur) {
-    if (nrec < PLC) {
-      rw = wl(w, nrec, rw);
-      rpk = wl((p & 0xffff) | (kind << 16), nrec, rpk);
-      rnp = wl(np, nrec, rnp);
-      rtk = wl(task, nrec, rtk);
-      rdn = wl64(dnet, nrec, rdn);
-      rocc = wlf(occ, nrec, rocc);
-      rdur = wlf(dur, nrec, rdur);
-    }
-    nrec++;
-  }
-  __device__ __forceinline__ void flush(const Dev& D, size_t st0) const {
-    const int lane = lane_id();
-    if (lane < npl && lane < PLC) {
-      D.s2_task[st0 + lane] = pt;
-      D.s2_worker[st0 + lane] = pw;
-      D.s2_comm[st0 + lane] = pc;
-      D.s2_start[st0 + lane] = ps;
-      D.s2_wsnb[st0 + lane] = pn;
-      D.s2_route[st0 + lane] = (int8_t)pr;
-    }
-    if (lane < nrec && lane < PLC) {
-      SRec rc;
-      rc.w = rw;
-      rc.p = (int16_t)(rpk & 0xffff);
-      rc.kind = (int8_t)(rpk >> 16);
-      rc.pad = 0;
-      rc.nproc = rnp;
-      rc.task = rtk;
-      rc.dnet = rdn;
-      rc.occ = rocc;
-      rc.dur = rdur;
-      D.srec[st0 + lane] = rc;
-    }
-  }
-};
-
-// minimum of a u64 over lanes 0..15 (one DPP row: quad swaps, half-row and row mirrors),
-// in every lane of row 0
-__device__ __forceinline__ uint64_t row_min_u64(uint64_t v) {
-  unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
-#define DGP_MINSTEP(ctl)                                                          \
-  {                                                                               \
-    const unsigned l2 = (unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, ctl, 0xf, 0xf, false); \
-    const unsigned h2 = (unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, ctl, 0xf, 0xf, false); \
-    const bool lt = ((uint64_t)h2 << 32 | l2) < ((uint64_t)hi << 32 | lo);       \
-    lo = lt ? l2 : lo;                                                            \
-    hi = lt ? h2 : hi;                                                            \
-  }
-  DGP_MINSTEP(0xb1)   // quad_perm(1,0,3,2)
-  DGP_MINSTEP(0x4e)   // quad_perm(2,3,0,1)
-  DGP_MINSTEP(0x141)  // row_half_mirror
-  DGP_MINSTEP(0x140)  // row_mirror
-#undef DGP_MINSTEP
-  return (uint64_t)hi << 32 | lo;
-}
-
-template <bool LW>
-__device__ __attribute__((always_inline)) bool exe_fast(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r,
-                                                        int qmode, const uint4& E, int& woke) {
-  SCtl& S = L.c;
-  const int lane = lane_id();
-#if DGP_PHASE_PROBES  // the same phase slots as exe_local's
-  unsigned long long tph = mclk();
-  auto phase = [&](int k) {
-    const unsigned long long n = mclk();
-    PROF(if (lane == 0) atomicAdd(&S.prof[k], n - tph));
-    tph = n;
-  };
-#else
-  auto phase = [](int) {};
-#endif
-  // PRE's rows of this stimulus: in flight while the header is unpacked
-  const uint4* FRr = D.frow + (size_t)(r & (DR - 1)) * FRS;
-  const bool l16 = lane < TF;
-  const uint4 z4 = make_uint4(0, 0, 0, 0);
-  uint4 FJ[NFF];
-#pragma unroll
-  for (int j = 0; j < NFF; j++) FJ[j] = l16 ? FRr[j * TF + lane] : z4;
-  const DTab durv = stim_durations(D, L, E, r);
-  const int t = rl((int)E.x, 0), w = rl((int)E.y, 0), p = rl((int)E.z, 0);
-  const uint32_t flags = rlu(E.w, 0);
-  const int64_t nbt = mk64(rlu(E.x, 1), rlu(E.y, 1));
-  const unsigned cnts = rlu(E.z, 1);
-  const int kt = cnts & 0xff, nrel = (cnts >> 8) & 0xff, nf = (cnts >> 16) & 0xff;
-  const double dobs = mkd(rlu(E.x, 2), rlu(E.y, 2));
-  const int nt = rl((int)E.z, 2);
-  const int tot_new = rl((int)E.w, 2);  // the frontier's dependency count (prefetcher)
-  const int TD = E_HDR, RL0 = E_HDR + kt, FX0 = RL0 + nrel;
-  // the touched workers, one lane each (entry 0 = w); a candidate-only worker (WAITC) is read
-  // after the wait
-  const bool tl = lane < nt;
-  const int tv = tl ? (int)L.touch[s][lane] : 0;
-  const int cj = tv & T_W;
-  const bool candl = (tv & T_CAND) != 0;
-  const bool wc = WAITC && tl && lane > 0 && candl;
-  // ---- capacity check of the needs tables this stimulus may grow (as exe_local)
-  {
-    bool bad = false;
-    if (tl) {
-      const uint32_t ctl = P.needs[(size_t)cj * NLW + NLW - 1];
-      const int slack = wc ? NXW / 2 : 0;
-      bad = ctl == NL_OVF || (int)(ctl >> 8) + tot_new + slack > NLW - 1 + NXW;
-    }
-    if (ballot(bad)) return false;
-  }
-  phase(11);
-  OutR o;
-  o.init();
-  int np = 0, nth = 1;
-  WDict dj;
-  dj.c = z4;
-  dj.c1 = z4;
-  dj.ord = 0;
-  int64_t net = 0, nbj = 0;
-  if (tl) nth = P.nthreads[cj];  // static while stimuli run
-  if (tl && !wc) {
-    np = P.nproc[cj];
-    dj = dict_load<LW>(P, cj);
-    net = P.netocc[cj];
-    nbj = P.nbytes[cj];
-  }
-  const int capw = P.cap[w];
-  uint32_t nl = line_load<LW>(P, w);
-  if (nt < 1 || rl(cj, 0) != w) {
-    serr(S, SERR_INV, 700000000 + (int)r);
-    return true;
-  }
-  const bool isw = lane == 0;
-  double nbw = net_bw_of(net, D);
-  const bool nth1 = !ballot(tl && nth != 1);  // occ / 1.0 == occ: the division is skipped
-  phase(16);
-  // ------------------------------------------- completion: processing -> memory (:2366)
-  int64_t dnet = 0;
-  {
-    int64_t freed = 0;
-    if (needs_dec_all(E, TD, kt, w, nl, freed)) dnet = -freed;
-    else for (int i = 0; i < kt; i++) {  // _dec_needs_replica for the dependencies w needed
-      const int L_ = TD + i;
-      if (rl((int)E.y, L_) == w) continue;
-      dnet -= needs_dec(D, S, w, nl, rl((int)E.x, L_), mk64(rlu(E.z, L_), rlu(E.w, L_)), t);
-    }
-  }
-  const int npw = rl(np, 0) - 1;
-  if (npw == 0) needs_reset(D, w, nl);
-  line_store<LW>(P, w, nl);
-  dict_add_lane(dj, 0, p, -1);
-  if (isw) {
-    np = npw;
-    net += dnet;
-  }
-  if (dnet != 0) nbw = net_bw_of(net, D);  // dnet is uniform
-  phase(17);
-  double occj = occ_dict_r(dj, nbw, durv, D);
-  double stkj = nth1 ? occj : occj / (double)nth;
-  o.rec(K_COMPLETE, w, p, dnet, rl_f64(occj, 0), npw, t, dobs);
-  // add_replica (:3148), then the releases popped before the frontier (LIFO, :3309-3314):
-  // relsum = the released replicas' bytes this lane's worker holds
-  int64_t relsum = 0;
-  for (int i = 0; i < nrel; i++) {
-    const int h = rl((int)E.x, RL0 + i);
-    const int64_t nb = mk64(rlu(E.z, RL0 + i), rlu(E.w, RL0 + i));
-    if (cj == h) relsum += nb;
-  }
-  if (isw) nbj += (flags & F_SELFREL) ? 0 : nbt;
-  if (tl && !wc) nbj -= relsum;
-  // a release-only holder is final now: written back and released before the frontier
-  bool released = false;
-  {
-    const bool ro = tl && !isw && !candl;
-    if (ballot(ro)) {
-      if (ro) P.nbytes[cj] = nbj;
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      if (ro) release_worker<LW>(L, P, s, cj);
-      released = ro;
-    }
-  }
-  bool exact = false;
-  if (WAITC && ballot(wc)) {
-    // the candidates: every earlier stimulus holding one has released it, then their state
-    if (vload(&L.predc[s]) != 0) {
-      if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(1);
-      while (vload(&L.predc[s]) != 0) __builtin_amdgcn_s_sleep(1);
-      if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(3);
-    }
-    lds_fence();
-    if (wc) {
-      np = P.nproc[cj];
-      dj = dict_load<LW>(P, cj);
-      net = P.netocc[cj];
-      nbj = P.nbytes[cj] - relsum;
-      nbw = net_bw_of(net, D);
-      occj = occ_dict_r(dj, nbw, durv, D);
-      stkj = nth1 ? occj : occj / (double)nth;
-    }
-    bool bad = false;  // the candidates' needs tables, exactly now
-    if (wc) {
-      const uint32_t ctl = P.needs[(size_t)cj * NLW + NLW - 1];
-      bad = ctl == NL_OVF || (int)(ctl >> 8) + tot_new > NLW - 1 + NXW;
-    }
-    if (ballot(bad)) {  // rare: continue as the oldest stimulus (every earlier one retired)
-      while (vload(&S.seq_pos) != r) __builtin_amdgcn_s_sleep(1);
-      lds_fence();
-      exact = true;
-    }
-  }
-  phase(12);
-  // ------------------------------ frontier in ascending priority: decide_worker (:8550)
-  int off = FX0;
-#pragma unroll 1
-  for (int j = 0; j < nf; j++) {
-    const uint4 FR = j == 0 ? FJ[0] : j == 1 ? FJ[1] : j == 2 ? FJ[2] : FJ[3];
-    const int x = rl((int)E.x, off), px = rl((int)E.y, off);
-    const int kx = rl((int)E.z, off) & 0xff;
-    const unsigned cmask = rlu(E.w, off);  // the candidates' touch indices (PRE)
-    // worker_objective (:3131-3146): start = occupancy / nthreads + comm_bytes / bandwidth,
-    // then (start, ws.nbytes, canonical index) minimal over the candidates
-    const bool cand = tl && ((cmask >> lane) & 1u);
-    const double cdv = cand ? mkd(FR.x, FR.y) : INFINITY;
-    const double start = stkj + cdv;
-    phase(18);
-    const uint64_t sk = cand ? start_key(start) : ~0ull;
-    const uint64_t mk = rl64(row_min_u64(sk), 0);
-    const unsigned long long eq = ballot(cand && sk == mk);
-    if (!eq) {
-      serr(S, SERR_CAND, x);
-      return true;
-    }
-    int jb = __builtin_ctzll(eq);
-    if (eq & (eq - 1)) {  // equal start times: ws.nbytes, then the worker index (key_less)
-      int64_t bn = rl_i64(nbj, jb);
-      int bw = rl(cj, jb);
-      for (unsigned long long m = eq & (eq - 1); m; m &= m - 1) {
-        const int q = __builtin_ctzll(m);
-        const int64_t nq = rl_i64(nbj, q);
-        const int wq = rl(cj, q);
-        if (nq < bn || (nq == bn && wq < bw)) {
-          jb = q;
-          bn = nq;
-          bw = wq;
-        }
-      }
-    }
-    const int cb = rl(cj, jb);
-    const double bstart = rl_f64(start, jb);
-    const int64_t bnb = rl_i64(nbj, jb);
-    const int64_t bcomm = mk64(rlu(FR.z, jb), rlu(FR.w, jb));
-    if (j == nf - 1 && nt > 2) {
-      // the last frontier decision is made: every touched worker but w and the chosen one
-      // is final now; written back and released before the commit
-      const bool early = tl && !isw && lane != jb && !released;
-      if (ballot(early)) {
-        if (early) {
-          using U4 = typename WPtr<LW>::template P<Q4>;
-          P.nproc[cj] = np;
-          st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
-          st4(ascast<U4>(P.pcnt + (size_t)cj * PD + 4), dj.c1);
-          P.plen[cj] = dj.ord;
-          P.netocc[cj] = net;
-          P.nbytes[cj] = nbj;
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (early) release_worker<LW>(L, P, s, cj);
-        released = released || early;
-      }
-    }
-    phase(19);
-    // _add_to_processing (:3199): record, WorkerState.add_to_processing, check_idle_saturated
-    o.place(x, cb, bcomm, bstart, bnb, ROUTE_NONROOTISH);
-    uint32_t nlc = line_load<LW>(P, cb);
-    if (exact) __threadfence_block();
-    int64_t dn = 0;
-    if (!needs_inc_all(E, off + 1, kx, cb, nlc, dn)) for (int i = 0; i < kx; i++) {
-      const int L2 = off + 1 + i;
-      if (rl((int)E.y, L2) == cb) continue;
-      dn += needs_inc(D, S, cb, nlc, rl((int)E.x, L2), mk64(rlu(E.z, L2), rlu(E.w, L2)), x);
-    }
-    line_store<LW>(P, cb, nlc);
-    const bool isb = lane == jb;
-    const bool okp = dict_add_lane(dj, jb, px, +1);
-    if (isb) {
-      np += 1;
-      net += dn;
-    }
-    if (dn != 0 && isb) nbw = net_bw_of(net, D);
-    if (!okp) serr(S, SERR_PREFIX, x);
-    if (exact && lane == 0) {  // scan mode reads them for this stimulus' later decisions
-      D.proc_on[x] = cb;
-      D.state[x] = S_PROCESSING;
-    }
-    occj = occ_dict_r(dj, nbw, durv, D);
-    stkj = nth1 ? occj : occj / (double)nth;
-    o.rec(K_PLACE, cb, px, dn, rl_f64(occj, jb), rl(np, jb), x, 0.0);
-    off += 1 + kx;
-    phase(20);
-  }
-  // ---- every touched worker but w is final: written back and released
-  if (tl && !isw && !released) {
-    using U4 = typename WPtr<LW>::template P<Q4>;
-    P.nproc[cj] = np;
-    st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
-    st4(ascast<U4>(P.pcnt + (size_t)cj * PD + 4), dj.c1);
-    P.plen[cj] = dj.ord;
-    P.netocc[cj] = net;
-    P.nbytes[cj] = nbj;
-  }
-  if (nt > 1) {
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (tl && !isw && !released) release_worker<LW>(L, P, s, cj);
-  }
-  // -------------- stimulus_queue_slots_maybe_opened (:4983): only w can have open slots
-  int pops = 0;
-  if (qmode != 0 && !D.sat_inf) {
-    const int slots = capw - rl(np, 0);
-    if (slots > capw || o.npl + slots > PLC - 1) {
-      serr(S, SERR_INV, 600000000 + (int)r);
-      return true;
-    }
-    if (slots > 0) pops = slots;
-    const int qp = S.q_prefix;
-    const int64_t nbw0 = rl_i64(nbj, 0);
-    for (int i = 0; i < pops; i++) {
-      const double st = stkj + 0.0 / (double)D.bandwidth;
-      o.place(-1, w, 0, rl_f64(st, 0), nbw0, ROUTE_ROOTISH_Q);
-      if (!dict_add_lane(dj, 0, qp, +1)) serr(S, SERR_PREFIX, -1);
-      if (isw) np += 1;
-      occj = occ_dict_r(dj, nbw, durv, D);
-      stkj = nth1 ? occj : occj / (double)nth;
-      o.rec(K_PLACE, w, qp, 0, rl_f64(occj, 0), rl(np, 0), -1, 0.0);
-    }
-  }
-  // ---- w written back last, then released
-  if (isw) {
-    using U4 = typename WPtr<LW>::template P<Q4>;
-    P.nproc[cj] = np;
-    st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
-    st4(ascast<U4>(P.pcnt + (size_t)cj * PD + 4), dj.c1);
-    P.plen[cj] = dj.ord;
-    P.netocc[cj] = net;
-    P.nbytes[cj] = nbj;
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  int wk = -1;
-  if (isw) wk = release_worker<LW>(L, P, s, w);
-  woke = rl(wk, 0);
-  phase(13);
-  // ------------------------------------------------ outputs, then retire
-  o.flush(D, (size_t)(r & (RS - 1)) * PLC);
   finish_slot(D, L, s, r, o, pops, false);
   phase(15);
   return true;
@@ -3441,21 +2922,8 @@ __device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, co
   return true;
 }
 
-#include "dgp_exev.h"
-
 // out of line, one register allocation each (inlined into the claim loop together they
-// spilled to scratch); -2: nothing changed (the stimulus goes back exact), else the slot the
-// release of w made ready (-1: none)
-template <bool LW>
-__device__ __attribute__((noinline)) int exe_fast_entry(int s, long long r, int qmode, uint4 E) {
-  int woke = -1;
-  return exe_fast<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r, qmode, E, woke) ? woke : -2;
-}
-template <bool LW>
-__device__ __attribute__((noinline)) int exe_local_entry(int s, long long r, int qmode, int exact, uint4 E) {
-  int woke = -1;
-  return exe_local<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r, qmode, exact != 0, E, woke) ? woke : -2;
-}
+// spilled to scratch)
 template <bool LW>
 __device__ __attribute__((noinline)) bool exe_run_entry(int s, long long r, uint4 E) {
   return exe_run<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r, E);
@@ -4367,7 +3835,6 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
   long long pf_r = -1;
   int pf_s = 0;
   uint4 pfE = make_uint4(0, 0, 0, 0);
-  int hint = -1;  // DGP_EXE_CONT
   while (true) {
     if (vload(&S.stop)) break;
     const SMask m = vload(&S.ready);
@@ -4398,12 +3865,8 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     // WAITC: a stimulus whose candidates are final first (it never waits in place); the
     // global-capable executor takes no other
     const bool pcl = WAITC && rdl && vload(&L.predc[lane]) != 0;
-    const bool pskip = pcl && (G || rsl - sp >= DGP_WAITC_AHEAD);
+    const bool pskip = pcl && G;
     unsigned key = rdl && !pskip ? (unsigned)((pcl ? 1u << 31 : 0u) | ((rsl - sp) << 6) | lane) : ~0u;  // r - sp < RS
-    // DGP_EXE_CONT: the stimulus this executor's last release of its completing worker made
-    // ready goes first (it continues the chain on that worker), unless it would wait in place
-    if (DGP_EXE_CONT && lane == hint && rdl && !pcl && !pskip) key = (unsigned)lane;
-    hint = -1;
     int cs = -1, cq = 0;
     long long cr = -1;
     uint32_t cf = 0;
@@ -4413,13 +3876,6 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
       const unsigned kmin = wmin_u32(key);
       if (kmin == ~0u) break;
       const int s = (int)(kmin & 63u);
-#if DGP_VMPROBE  // diagnostics: how long this executor's earlier global stores take to drain
-      {
-        const unsigned long long ta = mclk();
-        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-        if (lane == 0) { S.prof[11] += mclk() - ta; S.prof[12] += 1; }
-      }
-#endif
       if (lane == s) key = ~0u;  // tried
       if (!G && (rlu(fsl, s) & (F_GLOBAL | F_RUNM))) continue;  // left to the global-capable executor
       // WAITC: the global-capable executor never waits in place (it takes only stimuli whose
@@ -4487,24 +3943,8 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     } else if (G && (cf & F_SIMPLE) && cq == 0 && !cex && exe_run_entry<LW>(cs, cr, E)) {
       // a run of single-worker completions, back to back (only this executor calls out of line)
     } else {
-      int rc = -2;
-      if (LW && DGP_EXEV && (cf & F_FAST) && !cex && cq <= 1) {  // the vector form (the common case)
-        int wk = -1;
-        rc = exe_v<LW>(D, L, P, cs, cr, cq, E, wk) ? wk : -2;
-      }
-      if (rc == -2 && DGP_FAST && (cf & F_FAST) && !cex && cq <= 1) {  // the lean path (inlined: the common case)
-        int wk = -1;
-        rc = exe_fast<LW>(D, L, P, cs, cr, cq, E, wk) ? wk : -2;
-      }
-      if (rc == -2) {
-        if (DGP_LOCAL_INLINE) {
-          int wk = -1;
-          rc = exe_local<LW>(D, L, P, cs, cr, cq, cex, E, wk) ? wk : -2;
-        } else {
-          rc = exe_local_entry<LW>(cs, cr, cq, cex ? 1 : 0, E);
-        }
-      }
-      hint = rc >= 0 ? rc : -1;
+      int wk = -1;
+      const int rc = exe_local<LW>(D, L, P, cs, cr, cq, cex, E, wk) ? wk : -2;  // inlined: the common case
       if (rc == -2 && lane == 0) {
         atomicOr(&L.flags[cs], F_EXACT);
         atomicOr(&S.ready, 1ull << cs);
@@ -4685,7 +4125,6 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
   // batch-tolerant builder / prefetcher / walker take the remaining issue slots
   if (wave == 3) __builtin_amdgcn_s_setprio(3);
   else if (wave == 0 || wave >= N_ROLE) __builtin_amdgcn_s_setprio(2);
-  else if (DGP_STAGE_PRIO && (wave == 1 || wave == 2)) __builtin_amdgcn_s_setprio(DGP_STAGE_PRIO);
   if (wave == 0) {
     if (pos->round_end < 0) round_start = 0;
     role_seq<LW>(D, L, P, round_start);

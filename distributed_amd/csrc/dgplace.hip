@@ -525,7 +525,6 @@ dgp_engine* dgp_create(int device) {
     rc |= dalloc(e, &e->D.dring, (size_t)S::DR * S::PX, e->allocs);
     rc |= dalloc(e, &e->D.touch_ring, (size_t)S::DR * S::TMAX, e->allocs);
     rc |= dalloc(e, &e->D.thdr, (size_t)S::DR, e->allocs);
-    rc |= dalloc(e, &e->D.frow, (size_t)S::DR * S::FRS, e->allocs);
     rc |= dalloc(e, &e->D.s2_task, st, e->allocs);
     rc |= dalloc(e, &e->D.s2_worker, st, e->allocs);
     rc |= dalloc(e, &e->D.s2_comm, st, e->allocs);

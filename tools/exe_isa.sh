@@ -4,7 +4,7 @@ cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contrac
   -mllvm -amdgpu-lower-module-lds-strategy=module --offload-device-only $@ -o /tmp/dev.co /root/repo/distributed_amd/csrc/dgplace.hip 2>/dev/null
 /opt/rocm/lib/llvm/bin/clang-offload-bundler --unbundle --type=o --input=/tmp/dev.co --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output=/tmp/dev950.o
 /opt/rocm/lib/llvm/bin/llvm-objdump -d --mcpu=gfx950 /tmp/dev950.o > /tmp/dev.s
-for f in entry_exeILb1EEEvv exe_fast_entryILb1EEEiixi15HIP_vector_typeIjLj4EE exe_local_entryILb1EEEiixii15HIP_vector_typeIjLj4EE \
+for f in entry_exeILb1EEEvv \
          exe_run_entryILb1EEEbix15HIP_vector_typeIjLj4EE build_desc_g_entryEx build_desc_seq_entryEx \
          entry_regILb1EEEvv entry_wlkILb1EEEvv entry_stageILi0EEEvv entry_stageILi1EEEvv; do
   a=$(grep -n "${f}>:" /tmp/dev.s | head -1 | cut -d: -f1)
