@@ -83,6 +83,9 @@ static_assert(WIN >= 32 && WIN <= 64, "DGP_WIN must be in [32, 64]");
 #define DGP_WAITC 1
 #endif
 constexpr bool WAITC = DGP_WAITC != 0;
+// a stimulus that would wait in place is claimed only within this many stimuli of the oldest
+// (stimuli in flight span up to RS; 4 / 8 / 16 / 20 measured slower, profiles/r04knob)
+constexpr int WAITC_AHEAD = 32;
 static_assert(!WAITC || WIN == 32, "DGP_WAITC keeps the candidate-only registrations in the masks' high half");
 // the mask bits of slot s: its registration (low half) and, with WAITC, the candidate-only
 // flag of this worker for s (high half)
@@ -3865,7 +3868,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     // WAITC: a stimulus whose candidates are final first (it never waits in place); the
     // global-capable executor takes no other
     const bool pcl = WAITC && rdl && vload(&L.predc[lane]) != 0;
-    const bool pskip = pcl && G;
+    const bool pskip = pcl && (G || rsl - sp >= WAITC_AHEAD);
     unsigned key = rdl && !pskip ? (unsigned)((pcl ? 1u << 31 : 0u) | ((rsl - sp) << 6) | lane) : ~0u;  // r - sp < RS
     int cs = -1, cq = 0;
     long long cr = -1;
