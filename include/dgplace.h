@@ -378,7 +378,8 @@ int dgp_remove_worker(dgp_engine* e, int32_t worker);
  * (processing -> released -> waiting, memory -> released -> waiting, waiting -> processing
  * with decide_worker), LIFO as SchedulerState._transitions pops them. processing: the
  * worker's tasks in the order the scheduler iterates ws.processing. The placements append to
- * the placement log (*n_new_placements). DGP_E_UNSUPPORTED: another worker is paused, or the
+ * the placement log (*n_new_placements); paused workers may be present (decide_worker's
+ * candidates are then the running holders, or every running worker). DGP_E_UNSUPPORTED: the
  * cascade reaches a case the engine does not restate (a dependency to recompute, a queued or
  * no-worker dependent, a task nobody needs); after a refusal from the device the engine
  * takes the scheduler's state (dgp_sync_*) as after dgp_remove_worker. */
