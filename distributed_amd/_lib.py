@@ -10,14 +10,9 @@ import ctypes as C
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-# DGP_LIB (debugging / A-B runs only): a variant build used for BOTH windows, unless
-# DGP_LIB_W64 names the 64-slot variant too -- a variant is never silently paired with the
-# packaged build of the other window.
+# DGP_LIB (debugging / A-B runs only): a variant build of the same sources
 LIB_PATH = os.environ.get("DGP_LIB") or os.path.join(PKG, "libdgplace.so")
-# the same sources built with a 64-slot stimulus window and no wait-in-place claims
-# (-DDGP_WIN=64 -DDGP_WAITC=0, build.py): what graphs with restrictions run
-LIB_W64_PATH = (os.environ.get("DGP_LIB_W64") or os.environ.get("DGP_LIB")
-                or os.path.join(PKG, "libdgplace_w64.so"))
+# the stream kernel's two window builds, both in the library (dgp_set_window, ABI 19)
 WINDOWS = (32, 64)
 
 _P = C.c_void_p
@@ -84,6 +79,8 @@ SIGNATURES = {
     "dgp_remove_worker": (C.c_int, [_P, C.c_int32]),
     "dgp_lose_worker": (C.c_int, [_P, C.c_int32, C.c_int64, _P, C.c_int64, _P, _P]),
     "dgp_steal_order": (C.c_int, [_P, C.c_int64, _P, _P]),
+    "dgp_set_window": (C.c_int, [_P, C.c_int32]),
+    "dgp_get_window": (C.c_int, [_P]),
     "dgp_sync_placements": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P]),
     "dgp_sync_tasks": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dgp_sync_workers": (C.c_int, [_P, C.c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -91,7 +88,7 @@ SIGNATURES = {
                                    _P, _P, _P]),
 }
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 _libs: dict = {}
 
 
@@ -99,11 +96,9 @@ class DgpError(RuntimeError):
     pass
 
 
-def load(window: int = 32) -> C.CDLL:
-    """Load libdgplace.so (``window`` 64: libdgplace_w64.so); raises if it was not built."""
-    if window not in WINDOWS:
-        raise ValueError(f"window must be one of {WINDOWS}, not {window!r}")
-    path = LIB_PATH if window == 32 else LIB_W64_PATH
+def load() -> C.CDLL:
+    """Load libdgplace.so; raises if it was not built."""
+    path = LIB_PATH
     if path in _libs:
         return _libs[path]
     if not os.path.exists(path):

@@ -12,10 +12,6 @@ DEPS = [os.path.join(PKG, "csrc", "dgp_device.h"), os.path.join(PKG, "csrc", "dg
         os.path.join(PKG, "csrc", "dgp_events.h"), os.path.join(PKG, "csrc", "dgp_svcmsg.h"),
         os.path.join(PKG, "csrc", "dgp_msgs.h")]
 OUT = os.path.join(PKG, "libdgplace.so")
-# the same sources with a 64-slot stimulus window and no wait-in-place claims: graphs with
-# restrictions run this build (engine.py PlacementEngine.load)
-OUT_W64 = os.path.join(PKG, "libdgplace_w64.so")
-W64_FLAGS = ["-DDGP_WIN=64", "-DDGP_WAITC=0"]
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 # -ffp-contract=off: no fused multiply-add, so fp64 results round exactly like the
 # reference's CPython arithmetic (the parity contract is bit-exact objectives).
@@ -44,34 +40,21 @@ def build_ingest(force: bool = False) -> str:
 
 
 def build(force: bool = False) -> str:
-    """Both builds, compiled side by side (and the ingestion pass); returns the default
-    library's path."""
+    """The engine library (both stream-window builds in one: dgp_stream.h is included twice)
+    and the ingestion pass; returns the library's path."""
     build_ingest(force)
+    stale = os.path.join(PKG, "libdgplace_w64.so")  # the separate 64-slot build of ABI <= 18
+    if os.path.exists(stale):
+        os.remove(stale)
     newest = max(os.path.getmtime(p) for p in SRC + DEPS + [os.path.join(PKG, "..", "include", "dgplace.h")])
-    jobs = []
-    for out, extra in ((OUT, []), (OUT_W64, W64_FLAGS)):
-        if not force and os.path.exists(out) and os.path.getmtime(out) >= newest:
-            continue
-        log = open(out + ".log", "w")  # one diagnostics file per job: the two never interleave
-        jobs.append((out, log, subprocess.Popen([HIPCC, *FLAGS, *extra, "-o", out + ".tmp", *SRC],
-                                                stdout=log, stderr=subprocess.STDOUT)))
-    failed = []
-    for out, log, proc in jobs:  # every job is waited for before anything is raised
-        rc = proc.wait()
-        log.close()
-        if rc != 0:
-            failed.append((out, rc))
-    for out, log, proc in jobs:
-        if any(out == f for f, _ in failed):
-            if os.path.exists(out + ".tmp"):
-                os.remove(out + ".tmp")
-            continue
-        os.replace(out + ".tmp", out)
-        os.remove(out + ".log")
-    if failed:
-        out, rc = failed[0]
-        msg = open(out + ".log").read()[-4000:]
-        raise subprocess.CalledProcessError(rc, f"hipcc -> {out}", output=msg)
+    if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= newest:
+        return OUT
+    r = subprocess.run([HIPCC, *FLAGS, "-o", OUT + ".tmp", *SRC], capture_output=True, text=True)
+    if r.returncode != 0:
+        if os.path.exists(OUT + ".tmp"):
+            os.remove(OUT + ".tmp")
+        raise subprocess.CalledProcessError(r.returncode, f"hipcc -> {OUT}", output=(r.stdout + r.stderr)[-4000:])
+    os.replace(OUT + ".tmp", OUT)
     return OUT
 
 

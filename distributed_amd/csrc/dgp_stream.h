@@ -31,12 +31,35 @@
 //        the idle / saturated sets of check_idle_saturated (:2949).
 //   EXE  executors (the other waves): pick any ready stimulus and run it on the worker
 //        state in LDS; stimuli that read global state run alone, in order.
-#pragma once
+//
+// Included twice by dgplace.hip: namespace st with the 32-slot window and wait-in-place
+// claims (DGP_WIN 32, DGP_WAITC 1), namespace st64 with 64 slots and no wait-in-place
+// (DGP_ST_NS st64, DGP_WIN 64, DGP_WAITC 0). The engine picks one per graph (dgp_set_window).
 
 #include "dgp_svcmsg.h"
 
+#ifndef DGP_ST_NS
+#define DGP_ST_NS st
+#endif
+
+#ifndef DGP_STREAM_SHARED_DEFINED
+#define DGP_STREAM_SHARED_DEFINED
+#define DGP_ST_PRIMARY 1  // the first inclusion also defines the window-independent kernels
 namespace dgp {
-namespace st {
+// the stream kernel's static LDS block (SLds), one allocation for both window builds in the
+// module-wide LDS struct, sized for the 64-slot one (each namespace checks its SLds fits)
+constexpr size_t ST_LDS_BYTES = 22608;
+__shared__ __attribute__((aligned(16))) char st_lds_raw[ST_LDS_BYTES];
+// the per-worker LDS carve (dynamic LDS, sized at launch)
+extern __shared__ __attribute__((aligned(16))) char st_smem[];
+}  // namespace dgp
+#else
+#undef DGP_ST_PRIMARY
+#define DGP_ST_PRIMARY 0
+#endif
+
+namespace dgp {
+namespace DGP_ST_NS {
 
 // the engine description every stream role reads: constant memory (scalar loads, never
 // re-fetched across the roles' fences); set by the host before each launch
@@ -138,6 +161,7 @@ enum : int { K_COMPLETE = 1, K_PLACE = 2, K_COMPLETE_LR = 3 };
 enum : int { SERR_NONE = 0, SERR_PREFIX = 11, SERR_WATCHDOG = 12, SERR_QUEUE = 13, SERR_NEEDS = 14,
              SERR_REC = 15, SERR_CAND = 16, SERR_STAGE = 17, SERR_RANGE = 18, SERR_INV = 19 };
 
+#if DGP_ST_PRIMARY  // Dev points at these (dgp_device.h): one type for both builds
 // persistent stream position (global, survives launches)
 struct Pos {
   long long seq, bld, pre, reg;  // stimuli sequenced / built / prefetched / registered
@@ -160,6 +184,10 @@ struct SRec {
   double occ;
   double dur;  // completion: the observed duration (stop - start) for the prefix EWMA
 };
+#else
+using st::Pos;
+using st::SRec;
+#endif
 
 // LDS control block
 struct SCtl {
@@ -289,7 +317,6 @@ struct WPtr {
   P<uint8_t> wflags;   // walker's idle / saturated bits
 };
 
-extern __shared__ __attribute__((aligned(16))) char st_smem[];
 
 __device__ __forceinline__ size_t al16(size_t b) { return (b + 15) & ~(size_t)15; }
 __host__ __device__ constexpr size_t lds_worker_bytes(int W) {
@@ -372,8 +399,10 @@ struct SLds {
   SCtl c;
 };
 
-__shared__ SLds st_L;  // the engine's LDS window + control block (namespace scope: the roles'
-                       // out-of-line entry functions address it directly, keeping ds_* addressing)
+static_assert(sizeof(SLds) <= ST_LDS_BYTES, "ST_LDS_BYTES must hold the 64-slot window's SLds");
+// the engine's LDS window + control block (namespace scope: the roles' out-of-line entry
+// functions address it directly, keeping ds_* addressing)
+__device__ __forceinline__ SLds& st_L() { return *reinterpret_cast<SLds*>(st_lds_raw); }
 
 // ---------------------------------------------------------- the per-worker prefix dict
 // WorkerState.task_prefix_count is an insertion-ordered {prefix: count} with delete on
@@ -1735,12 +1764,12 @@ struct DescOut {
 // out of line: each form gets its own register allocation (inlined together they spilled)
 __device__ __attribute__((noinline)) DescOut build_desc_g_entry(long long r) {
   DescOut o{0, 0, 0.0};
-  o.ok = build_desc_g(c_dev, st_L, r, o.p, o.dobs) ? 1 : 0;
+  o.ok = build_desc_g(c_dev, st_L(), r, o.p, o.dobs) ? 1 : 0;
   return o;
 }
 __device__ __attribute__((noinline)) DescOut build_desc_seq_entry(long long r) {
   DescOut o{1, 0, 0.0};
-  build_desc_seq(c_dev, st_L, r, o.p, o.dobs);
+  build_desc_seq(c_dev, st_L(), r, o.p, o.dobs);
   return o;
 }
 __device__ __forceinline__ void build_desc(const Dev& D, SLds& L, long long r, int& p_out, double& dobs_out) {
@@ -2929,7 +2958,7 @@ __device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, co
 // spilled to scratch)
 template <bool LW>
 __device__ __attribute__((noinline)) bool exe_run_entry(int s, long long r, uint4 E) {
-  return exe_run<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r, E);
+  return exe_run<LW>(c_dev, st_L(), wptr<LW>(c_dev), s, r, E);
 }
 
 // wave argmin over all workers of a key computed per worker (global stimuli)
@@ -3818,7 +3847,7 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
 // the global path out of line: the local path keeps its own register budget
 template <bool LW>
 __device__ __attribute__((noinline)) void exe_global_entry(int s, long long r) {
-  exe_global<LW>(c_dev, st_L, wptr<LW>(c_dev), s, r);
+  exe_global<LW>(c_dev, st_L(), wptr<LW>(c_dev), s, r);
 }
 
 // G: this executor also runs the global stimuli. Only one executor wave does: a call to the
@@ -4016,20 +4045,20 @@ __device__ __attribute__((always_inline)) void workers_io(const Dev& D, const WP
 // (inlined into one kernel body they shared one 128-VGPR budget and spilled to scratch
 // on the executors' path).
 template <bool LW>
-__device__ __attribute__((noinline)) void entry_exe() { role_exe<LW, false>(c_dev, st_L, wptr<LW>(c_dev)); }
+__device__ __attribute__((noinline)) void entry_exe() { role_exe<LW, false>(c_dev, st_L(), wptr<LW>(c_dev)); }
 template <bool LW>
-__device__ __attribute__((noinline)) void entry_exe_g() { role_exe<LW, true>(c_dev, st_L, wptr<LW>(c_dev)); }
+__device__ __attribute__((noinline)) void entry_exe_g() { role_exe<LW, true>(c_dev, st_L(), wptr<LW>(c_dev)); }
 template <bool LW>
-__device__ __attribute__((noinline)) void entry_reg() { role_reg<LW>(c_dev, st_L, wptr<LW>(c_dev)); }
+__device__ __attribute__((noinline)) void entry_reg() { role_reg<LW>(c_dev, st_L(), wptr<LW>(c_dev)); }
 template <bool LW>
-__device__ __attribute__((noinline)) void entry_wlk() { role_wlk<LW>(c_dev, st_L, wptr<LW>(c_dev)); }
+__device__ __attribute__((noinline)) void entry_wlk() { role_wlk<LW>(c_dev, st_L(), wptr<LW>(c_dev)); }
 template <int KIND>
-__device__ __attribute__((noinline)) void entry_stage() { role_stage<KIND>(c_dev, st_L); }
+__device__ __attribute__((noinline)) void entry_stage() { role_stage<KIND>(c_dev, st_L()); }
 
 template <bool LW>
 __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps) {
   const Dev& D = c_dev;
-  SLds& L = st_L;
+  SLds& L = st_L();
   SCtl& S = L.c;
   const WPtr<LW> P = wptr<LW>(D);
   Ctl* c = D.ctl;
@@ -4210,6 +4239,7 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
   }
 }
 
+#if DGP_ST_PRIMARY  // the event kernels below do not depend on the window: defined once, in st
 // ================================================================ steal confirmation
 // WorkStealing.move_task_confirm, the "confirm" branch (stealing.py:376-384, the finally
 // clause :396-399) on the engine state between launches (service mode): processing task t
@@ -4433,5 +4463,7 @@ __global__ void __launch_bounds__(64) k_add_worker(const Dev* __restrict__ Dp, l
   if (lane == 0) *placed = n;
 }
 
-}  // namespace st
+#endif  // DGP_ST_PRIMARY
+
+}  // namespace DGP_ST_NS
 }  // namespace dgp

@@ -29,6 +29,13 @@
 #include "../../include/dgplace.h"
 #include "dgp_device.h"
 #include "dgp_msgs.h"
+#include "dgp_stream.h"  // dgp::st: the 32-slot window with wait-in-place claims
+#undef DGP_ST_NS
+#undef DGP_WIN
+#undef DGP_WAITC
+#define DGP_ST_NS st64  // dgp::st64: the same stream kernel with 64 slots, no wait-in-place
+#define DGP_WIN 64
+#define DGP_WAITC 0
 #include "dgp_stream.h"
 #include "dgp_events.h"
 #include "dgp_steal.h"
@@ -60,6 +67,7 @@ struct dgp_engine {
   hipStream_t stream = nullptr;
   std::string err;
   dgp::Dev D{};
+  int window = 32;  // the stream kernel build the next launch runs (dgp_set_window): 32 or 64
   // what the device copies of D hold (d_dev, the stream kernel's c_dev symbol) and the
   // dynamic-LDS size last set on each stream kernel: unchanged ones are not re-sent
   dgp::Dev dev_sent[2]{};
@@ -410,31 +418,49 @@ void stream_source(dgp_engine* e, bool service) {
   D.cseq = service ? D.sv_cseq : D.run_id;
 }
 
+// the two builds of the stream kernel (dgp_stream.h included as dgp::st and dgp::st64)
+struct StreamW32 {
+  static const void* kernel(bool lw) {
+    return lw ? (const void*)dgp::st::k_stream<true> : (const void*)dgp::st::k_stream<false>;
+  }
+  static hipError_t send(const dgp::Dev& d, hipStream_t s) {
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(dgp::st::c_dev), &d, sizeof(dgp::Dev), 0, hipMemcpyHostToDevice, s);
+  }
+};
+struct StreamW64 {
+  static const void* kernel(bool lw) {
+    return lw ? (const void*)dgp::st64::k_stream<true> : (const void*)dgp::st64::k_stream<false>;
+  }
+  static hipError_t send(const dgp::Dev& d, hipStream_t s) {
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(dgp::st64::c_dev), &d, sizeof(dgp::Dev), 0, hipMemcpyHostToDevice, s);
+  }
+};
+
 // one launch of the stream kernel over the stimulus source set by stream_source()
-int launch_stream(dgp_engine* e, long long max_rounds, int snaps) {
+template <class B>
+int launch_stream_build(dgp_engine* e, long long max_rounds, int snaps) {
   const dgp::Dev& D = e->D;
   const size_t lds_w = dgp::st::lds_worker_bytes(D.W);
   // the kernel's static LDS (module-wide LDS lowering can place more than SLds in it)
   static size_t stat_lds = 0;
-  if (!stat_lds) stat_lds = kernel_static_lds((const void*)dgp::st::k_stream<true>, sizeof(dgp::st::SLds));
+  if (!stat_lds) stat_lds = kernel_static_lds(B::kernel(true), dgp::ST_LDS_BYTES);
   const bool lw = stat_lds + lds_w <= 160 * 1024;
-  // c_dev is one symbol per device, shared by every engine on it: re-sent unless it holds
-  // exactly this engine's Dev already (content compare; engines are driven from one thread)
+  // c_dev is one symbol per device and build, shared by every engine on it: re-sent unless it
+  // holds exactly this engine's Dev already (content compare; engines are driven from one thread)
   static struct {
     bool valid;
     dgp::Dev v;
   } sent[64];
   auto& cs = sent[e->device & 63];
   if (!cs.valid || memcmp(&cs.v, &e->D, sizeof(dgp::Dev))) {
-    HIPCHK(e, hipMemcpyToSymbolAsync(HIP_SYMBOL(dgp::st::c_dev), &e->D, sizeof(dgp::Dev), 0, hipMemcpyHostToDevice,
-                                     e->stream));
+    HIPCHK(e, B::send(e->D, e->stream));
     cs.v = e->D;
     cs.valid = true;
   }
   long long mr = max_rounds;
   int sn = snaps;
   void* args[] = {&mr, &sn};
-  const void* fn = lw ? (const void*)dgp::st::k_stream<true> : (const void*)dgp::st::k_stream<false>;
+  const void* fn = B::kernel(lw);
   static size_t lds_max[64];  // the kernel attribute is per device: an upper bound, raised when needed
   if (lw && lds_max[e->device & 63] < lds_w) {
     HIPCHK(e, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w));
@@ -449,6 +475,11 @@ int launch_stream(dgp_engine* e, long long max_rounds, int snaps) {
   if (lst != hipSuccess) return fail(e, DGP_E_HIP, std::string("stream launch: ") + hipGetErrorString(lst));
   e->stream_used = true;
   return 0;
+}
+
+int launch_stream(dgp_engine* e, long long max_rounds, int snaps) {
+  return e->window == 64 ? launch_stream_build<StreamW64>(e, max_rounds, snaps)
+                         : launch_stream_build<StreamW32>(e, max_rounds, snaps);
 }
 
 int walk(dgp_engine* e) {
@@ -1460,6 +1491,16 @@ int dgp_tasks_finished_wait(dgp_engine* e, int8_t* status, int64_t* n_new_placem
   e->posted = 0;
   return 0;
 }
+
+int dgp_set_window(dgp_engine* e, int32_t window) {
+  if (!e) return DGP_E_ARG;
+  if (window != 32 && window != 64) return fail(e, DGP_E_ARG, "dgp_set_window: window must be 32 or 64");
+  if (int rc_ = resident_stop(e)) return rc_;  // the next launch takes the other build
+  e->window = window;
+  return 0;
+}
+
+int dgp_get_window(dgp_engine* e) { return e ? e->window : 0; }
 
 int dgp_move_task(dgp_engine* e, int32_t task, int32_t thief) {
   if (int rc_ = resident_stop(e)) return rc_;

@@ -54,19 +54,21 @@ class PlacementEngine:
 
     def __init__(self, device: int = 0, window: int | str = "auto"):
         """``window``: the stream kernel's in-flight stimulus window -- 32 (wait-in-place
-        claims, libdgplace.so), 64 (no wait-in-place, libdgplace_w64.so) or "auto": chosen at
-        ``load`` by ``auto_window`` (the unpacks' completions after a wide
-        frontier are window-bound; the C2 chain needs wait-in-place)."""
+        claims), 64 (no wait-in-place) or "auto": chosen per graph by ``auto_window`` at
+        ``load`` and at each later graph (the unpacks' completions after a wide
+        frontier are window-bound; the C2 chain needs wait-in-place). Both builds are in the
+        one library (``dgp_set_window``) and make identical placements."""
         if window not in (*_lib.WINDOWS, "auto"):
             raise ValueError(f"window must be 32, 64 or 'auto', not {window!r}")
         self.window = window
-        self._configured = False  # set_timing / set_resident / ... ran: the handle may not be replaced
-        self.lib = _lib.load(64 if window == 64 else 32)
+        self.lib = _lib.load()
         self.device = int(device)
         h = self.lib.dgp_create(int(device))
         if not h:
             raise _lib.DgpError(f"dgp_create({device}) failed: no HIP device visible (no CPU fallback)")
         self.h = h
+        if window != "auto":
+            self.set_window(window)
         self.n_tasks = 0
         self.n_workers = 0
         self._keep = []
@@ -146,8 +148,8 @@ class PlacementEngine:
     def load(self, g: dict, config: dict | None = None, *, snapshots: int = 0, results: bool = True):
         """Configure workers + config + graph in one go (the usual set-up). ``results``:
         upload the synthetic executor's completion reports (replay mode)."""
-        if self.window == "auto" and self.n_tasks == 0:
-            self._use_lib(self.auto_window(g))
+        if self.window == "auto":
+            self.set_window(self.auto_window(g))
         self.set_workers(g["nthreads"])
         self.set_config(config)
         if snapshots:
@@ -170,21 +172,18 @@ class PlacementEngine:
             return 64
         return 32
 
-    def _use_lib(self, window: int):
-        """A fresh engine on the build with that window (before anything was uploaded).
-        On an "auto" engine, ``load`` must therefore be the first call: anything configured
-        on the handle before it would be lost with the handle, so that raises."""
-        lib = _lib.load(window)
-        if lib is self.lib:
-            return
-        if self._configured:
-            raise _lib.DgpError("load() must come first on an engine with window='auto': the handle was already "
-                                "configured (set_timing / set_resident / set_task_messages / enable_snapshots)")
-        h = lib.dgp_create(self.device)
-        if not h:
-            raise _lib.DgpError(f"dgp_create({self.device}) failed: no HIP device visible (no CPU fallback)")
-        self.lib.dgp_destroy(self.h)
-        self.lib, self.h = lib, h
+    def set_window(self, window: int):
+        """The stream kernel build the next launches run (32 or 64 slots, ABI 19)."""
+        self._check(self.lib.dgp_set_window(self.h, int(window)), "dgp_set_window")
+
+    def get_window(self) -> int:
+        return int(self.lib.dgp_get_window(self.h))
+
+    def later_graph_window(self, g: dict):
+        """A later graph on an "auto" engine: the 64-slot build from the first graph that
+        wants it (restrictions or a wide frontier) on; a 32-slot engine stays unless so."""
+        if self.window == "auto" and self.get_window() != 64 and self.auto_window(g) == 64:
+            self.set_window(64)
 
     # ------------------------------------------------------------------- replay
     def reset(self):
@@ -307,13 +306,11 @@ class PlacementEngine:
     def set_resident(self, on: bool = True):
         """Resident service mode (dgp_set_resident): the stream kernel stays launched between
         tasks_finished calls and takes each batch from a pinned mailbox."""
-        self._configured = True
         self._check(self.lib.dgp_set_resident(self.h, 1 if on else 0), "dgp_set_resident")
 
     def set_task_messages(self, on: bool = True):
         """Resident answers carry their placements' compute-task message fields
         (dgp_set_task_messages): task_messages of the last answer reads the mailbox."""
-        self._configured = True
         self._check(self.lib.dgp_set_task_messages(self.h, 1 if on else 0), "dgp_set_task_messages")
 
     def move_task(self, task: int, thief: int):
@@ -343,6 +340,7 @@ class PlacementEngine:
         placements it made. With dependencies on earlier tasks the stimulus is the
         scheduler's: nothing is placed and ``sync()`` must follow (include/dgplace.h); so
         too with ``defer`` (dgp_add_graph_deferred: a graph with restrictions)."""
+        self.later_graph_window(g)
         arrs = {
             "dep_ptr": np.ascontiguousarray(g["dep_ptr"], np.int64),
             "dep_idx": np.ascontiguousarray(g["dep_idx"], np.int32),
@@ -450,6 +448,8 @@ class PlacementEngine:
         ri = self._arr([w for r in rows for w in r], np.int32)
         if len(ri) == 0:
             ri = np.zeros(1, np.int32)
+        if self.window == "auto" and f.any() and self.get_window() != 64:
+            self.set_window(64)  # restrictions from now on: the 64-slot build (auto_window)
         self._check(self.lib.dgp_update_restrictions(self.h, len(t), _ptr(t), _ptr(rp), _ptr(ri), _ptr(f)),
                     "dgp_update_restrictions")
 
@@ -599,7 +599,6 @@ class PlacementEngine:
         return st
 
     def set_timing(self, on: bool = True):
-        self._configured = True
         self._check(self.lib.dgp_set_timing(self.h, 1 if on else 0), "dgp_set_timing")
 
     def stats(self) -> dict:

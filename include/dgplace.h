@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 18
+#define DGP_ABI_VERSION 19
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -173,6 +173,16 @@ int dgp_run_rounds(dgp_engine* e, int64_t max_rounds, int64_t* n_rounds_out);
 int dgp_tasks_finished(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* run_id,
                        const int64_t* nbytes, const double* start, const double* stop, int8_t* status,
                        int64_t* n_new_placements);
+
+/* (ABI 19) The stream kernel's in-flight stimulus window for the launches from now on: 32
+ * slots with wait-in-place claims (the default; the ordered C2 chain needs them) or 64 slots
+ * without (graphs with worker restrictions or a wide frontier: their replay is window-bound,
+ * DESIGN.md §9). Both builds live in this library and make identical placements; only speed
+ * differs, so a caller may switch per graph (PlacementEngine does at load and at each later
+ * graph). Ends a resident kernel (the next call relaunches it with the new window).
+ * dgp_get_window returns the current one. */
+int dgp_set_window(dgp_engine* e, int32_t window);
+int dgp_get_window(dgp_engine* e);
 
 /* Resident service mode (ABI 9): with `enabled`, dgp_tasks_finished keeps the stream kernel
  * launched between calls and hands it each batch through a mailbox in pinned host memory

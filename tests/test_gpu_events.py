@@ -319,7 +319,10 @@ def test_service_dependent_later_graph_matches_reference(name):
                     if restr:  # the new tasks' valid workers (dgp_update_restrictions)
                         rp, ri, rf = z["g2_restr_ptr"], z["g2_restr_idx"], z["g2_restr_flags"]
                         ts = np.flatnonzero(rf & 1)
+                        w0 = eng.get_window()
                         eng.update_restrictions(g["n_tasks"] + ts, [ri[rp[t]:rp[t + 1]] for t in ts], rf[ts])
+                        # the first restricted graph moves an "auto" engine to the 64-slot build
+                        assert (w0, eng.get_window()) == (eng.auto_window(g), 64)
                 st, _ = eng.tasks_finished(*[[c] for c in msgs[i]])
                 assert st.tolist() == [0], (i, st)
             if ptr[k + 1] > ptr[k]:

@@ -136,10 +136,10 @@ def test_engine_full_c2(engine_cls):
 @pytest.mark.parametrize("window", [32, 64])
 @pytest.mark.parametrize("name", ["c2mini_sat1.1.npz", "c2var_sat1.1.npz", "restr_sat1.1.npz", "c3mini_sat1.1.npz"])
 def test_both_window_builds_match_fixture(engine_cls, name, window):
-    """Each fixture on BOTH builds, forced (libdgplace.so: 32-slot window with wait-in-place
-    claims; libdgplace_w64.so: 64 slots, no wait-in-place): the auto choice runs restricted
-    graphs only on the 64-slot build and C2-shaped ones only on the 32-slot one, so each
-    build also runs the other's shapes here."""
+    """Each fixture on BOTH stream-kernel builds, forced (dgp_set_window: 32-slot window with
+    wait-in-place claims; 64 slots, no wait-in-place): the auto choice runs restricted graphs
+    only on the 64-slot build and C2-shaped ones only on the 32-slot one, so each build also
+    runs the other's shapes here."""
     g, cfg, exp, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
     R = len(exp["round_nplaced"]) + 2
     with engine_cls(0, window=window) as eng:

@@ -108,6 +108,43 @@ def test_resident_service_matches_reference_fixture(name, per_message):
     assert np.array_equal(out["final_state"], exp["final_state"])
 
 
+@pytest.mark.parametrize("resident", [False, True], ids=["launch", "resident"])
+@pytest.mark.parametrize("name", ["c2var_sat1.1.npz", "restr_sat1.1.npz", "c3mini_sat1.1.npz"])
+def test_window_switched_between_calls(name, resident):
+    """Both stream-kernel builds on ONE engine (dgp_set_window, ABI 19): the window alternates
+    32 / 64 every call, so consecutive batches run on different builds over the same resident
+    state; the placements, snapshots and final states still equal the reference's."""
+    from distributed_amd.engine import PlacementEngine
+
+    g, cfg, exp, meta = oracle.load_fixture(os.path.join(GOLDEN, name))
+    msgs, ptr = fixture_messages(g, exp)
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.set_resident(resident)
+        eng.update_graph()
+        status, calls = [], 0
+        for k in range(len(ptr) - 1):
+            chunk = msgs[ptr[k]:ptr[k + 1]]
+            if not chunk:
+                continue
+            for i in range(0, len(chunk), 7):  # batches of 7 messages
+                eng.set_window(64 if calls % 2 else 32)
+                assert eng.get_window() == (64 if calls % 2 else 32)
+                t, w, r, nb, a, b = (np.array(c) for c in zip(*chunk[i:i + 7]))
+                st, _ = eng.tasks_finished(t, w, r, nb, a, b)
+                status.extend(st.tolist())
+                calls += 1
+            eng.snapshot()
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert calls > 10
+    assert (np.array(status) == 0).all()
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
+
+
 SVC = sorted(f for f in golden_files() if f.startswith("svc_"))
 
 
