@@ -151,7 +151,8 @@ static_assert((DR & (DR - 1)) == 0 && DR >= 64 && DR >= WIN, "DGP_DR must be a p
 static_assert((RS & (RS - 1)) == 0 && RS >= WIN && RS <= DR, "DGP_RS must be a power of two in [WIN, DR]");
 
 // F_SIMPLE (PRE): touches only its completing worker, empty frontier, at most one dependency
-// (held by that worker) and one release: it can be part of a single-worker run (exe_run).
+// (held by that worker, or by another one and not released) and one release: it can be part
+// of a single-worker run (exe_run).
 // F_RUNM (REG): F_SIMPLE and so is the stimulus just before it, on the same worker: a run
 // continues through it, so only the run-capable executor takes it
 enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16, F_SIMPLE = 32, F_RUNM = 64 };
@@ -1545,7 +1546,7 @@ __device__ __attribute__((always_inline)) void build_desc_seq(const Dev& D, SLds
   if (tbad) flags |= F_GLOBAL | F_BADTOUCH;
   if (evg) flags |= F_GLOBAL;
   if (!(flags & F_GLOBAL) && nt == 1 && nf == 0 && kt <= 1 && nrel <= 1 &&
-      (kt == 0 || h_dep0 == w) && D.P <= PD)  // a run shares the head's descriptor durations
+      (kt == 0 || h_dep0 >= 0) && D.P <= PD)  // a run shares the head's descriptor durations
     flags |= F_SIMPLE;
   if (flags & F_GLOBAL) nt = 0;
   int32_t* T = D.touch_ring + (size_t)(r & (DR - 1)) * TMAX;
@@ -1743,7 +1744,7 @@ __device__ __attribute__((always_inline)) bool build_desc_g(const Dev& D, SLds& 
   if (nf + capw + 1 > PLC) flags |= F_GLOBAL;  // staging room for the refill
   if (tbad) flags |= F_GLOBAL | F_BADTOUCH;
   if (evg) flags |= F_GLOBAL;
-  if (!(flags & F_GLOBAL) && nt == 1 && nf == 0 && kt <= 1 && nrel <= 1 && (kt == 0 || h_dep0 == w) && D.P <= PD)
+  if (!(flags & F_GLOBAL) && nt == 1 && nf == 0 && kt <= 1 && nrel <= 1 && (kt == 0 || h_dep0 >= 0) && D.P <= PD)
     flags |= F_SIMPLE;  // a run shares the head's descriptor durations
   if (flags & F_GLOBAL) nt = 0;
   int32_t* T = D.touch_ring + (size_t)(r & (DR - 1)) * TMAX;
@@ -2802,8 +2803,10 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
 
 // ============================================================ single-worker runs
 // A run of consecutive stimuli r, r+1, ..., r+k-1 that each touch only worker w, place
-// nothing (empty frontier), whose dependencies w holds (no needs_what change) and whose
-// releases are on w, with the queue empty: each is the completion bookkeeping of one task
+// nothing (empty frontier), whose dependency w holds or needs from elsewhere (then the same
+// dependency d0 for every such member, whose needs_what entry on w stays >= 1: a count
+// decrement, no network-occupancy change) and whose releases are on w, with the queue
+// empty: each is the completion bookkeeping of one task
 // on w (_transition_processing_memory :2366-2442 -> _exit_processing_common :3258-3281 ->
 // WorkerState.remove_from_processing :759-771, add_replica :3148, the releases :3309-3314;
 // stimulus_queue_slots_maybe_opened :4983 finds no queued task). Each waits only for the
@@ -2818,7 +2821,6 @@ __device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, co
   const int lane = lane_id();
   if (L.ntouch[s] != 1) return false;
   const int w = rl((int)E.y, 0);
-  if (P.needs[(size_t)w * NLW + NLW - 1] != 0) return false;  // w needs no replica (needs_reset is a no-op)
   // members: registered slots (guard dropped) whose stimulus r + k touches only w and waits
   // only for its predecessor on w; lane k (k >= 1) gets the slot of r + k, k consecutive
   const bool sl = lane < WIN && lane != s;
@@ -2836,7 +2838,7 @@ __device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, co
   // each candidate's descriptor header (lane i: stimulus r + i); the dependency and release
   // entries are read whether present or not (a row always holds NE entries)
   uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0, ed = h0, er = h0, dq[4];
-  bool ok = false;
+  bool ok = false, needs_m = false;
   if (lane < n) {
     const uint4* row = D.desc + (size_t)((r + lane) & (DR - 1)) * NE;
     h0 = row[0];
@@ -2856,12 +2858,40 @@ __device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, co
     const int kt = h1.z & 0xff, nrel = (h1.z >> 8) & 0xff, nf = (h1.z >> 16) & 0xff;
     const uint4 erel = kt == 0 ? ed : er;
     ok = lane < n && (int)h0.y == w && !(h0.w & F_GLOBAL) && nf == 0 && kt <= 1 && nrel <= 1 &&
-         (kt == 0 || (int)ed.y == w) && (nrel == 0 || (int)erel.x == w) && same;
+         (nrel == 0 || (int)erel.x == w) && same;
     er = erel;
+    needs_m = ok && kt == 1 && (int)ed.y != w;  // _dec_needs_replica (:767-769) of a dependency held elsewhere
   }
-  const unsigned long long bad = ballot(!ok);
-  const int k = (int)min((unsigned long long)n, (unsigned long long)__builtin_ctzll(bad | (1ull << 63)));
-  if (k == 0) return false;
+  // the members that need a dependency from elsewhere all need the same one, d0, whose entry
+  // in w's LDS needs_what line keeps a count >= 1 through the run (no entry leaves, so
+  // netocc and the occupancy's network term stay as they are)
+  const unsigned long long nm = ballot(needs_m);
+  const uint32_t nl = line_load<LW>(P, w);
+  const uint32_t ctl = rlu(nl, NLW - 1);
+  if (ctl == NL_OVF) return false;  // scan mode: exe_local
+  unsigned long long cut = ballot(!ok);
+  int d_ml = -1;  // the line lane of d0's entry
+  if (nm) {
+    const uint32_t d0 = rlu(ed.x, __builtin_ctzll(nm));
+    cut |= ballot(needs_m && ed.x != d0);
+    const unsigned long long em = ballot(lane < NLW - 1 && nl != 0 && (nl >> 8) == d0);
+    if (!em) {
+      cut |= nm & (0ull - nm);  // d0 not in the line: the run ends before its first member
+    } else {
+      d_ml = __builtin_ctzll(em);
+      const int c0 = (int)(rlu(nl, d_ml) & 0xffu);
+      // the member whose decrement would empty the entry ends the run (exe_local takes it)
+      unsigned long long mm = nm;
+      for (int i = 1; i < c0 && mm; i++) mm &= mm - 1;
+      if (mm) cut |= mm & (0ull - mm);
+    }
+  }
+  int k = (int)min((unsigned long long)n, (unsigned long long)__builtin_ctzll(cut | (1ull << 63)));
+  // a needs line with entries belongs to tasks still processing on w: w keeps one (no
+  // needs_reset), as it does when the line is empty only if nothing else is processing
+  if (ctl != 0) k = min(k, P.nproc[w] - 1);
+  if (k <= 0) return false;
+  const int n_dec = __builtin_popcountll(nm & ((k >= 64 ? 0ull : (1ull << k)) - 1ull));
   // the members leave the window's wake-up protocol: the guard keeps them from becoming ready
   if (lane >= 1 && lane < k) {
     const int op = __hip_atomic_fetch_add(&L.pred[my_slot], BIG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2929,6 +2959,7 @@ __device__ __attribute__((always_inline)) bool exe_run(const Dev& D, SLds& L, co
     P.plen[w] = dj.ord;
     P.nbytes[w] = nbj;
   }
+  if (n_dec && lane == d_ml) P.needs[(size_t)w * NLW + d_ml] = nl - (uint32_t)n_dec;
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): w's state is in LDS
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   // one release of w for the run: the stimulus after it on w counted one of the run's bits
