@@ -1961,6 +1961,67 @@ __global__ void k_ug_init(const Dev* __restrict__ Dp, int lo) {
   }
 }
 
+// k_ug_dispatch's dynamic LDS: the tournament tree and the worker arrays its lane-0 chain of
+// dependent reads and writes walks per placement, staged in LDS when they fit (bit k of
+// `mask`: array k, in this order; the host picks the prefix that fits its LDS budget). The
+// dispatch's LDS copy of Dev points at the staged copies, so every callee uses them as is.
+constexpr int UG_NF = 15;
+__host__ __device__ inline size_t ug_field_bytes(int k, int W, int Wp, int P) {
+  switch (k) {
+    case 13: case 14: return (size_t)P * sizeof(double);  // pdur_cur, pdur_walk
+    case 0: return 2 * (size_t)Wp * sizeof(double);   // t_key
+    case 1: return 2 * (size_t)Wp * sizeof(int32_t);  // t_idx
+    case 2: case 3: case 4: case 5: return (size_t)W * 4;  // nproc, nthreads, cap, plen
+    case 6: return (size_t)W;                                  // flags
+    case 7: case 8: case 9: case 10: return (size_t)W * 8;     // itcslots, netocc, nbytes, lastcheck
+    default: return (size_t)W * PMAX * 4;                      // pfx, pcnt
+  }
+}
+__host__ __device__ inline size_t ug_field_off(int k, int W, int Wp, int P, uint32_t mask) {  // 16-aligned
+  size_t o = 0;
+  for (int j = 0; j < k; j++)
+    if (mask >> j & 1) o += (ug_field_bytes(j, W, Wp, P) + 15) & ~(size_t)15;
+  return o;
+}
+__device__ inline void** ug_field_ptr(Dev& d, int k) {
+  switch (k) {
+    case 0: return (void**)&d.t_key;
+    case 1: return (void**)&d.t_idx;
+    case 2: return (void**)&d.w_nproc;
+    case 3: return (void**)&d.w_nthreads;
+    case 4: return (void**)&d.w_cap;
+    case 5: return (void**)&d.w_plen;
+    case 6: return (void**)&d.w_flags;
+    case 7: return (void**)&d.w_itcslots;
+    case 8: return (void**)&d.w_netocc;
+    case 9: return (void**)&d.w_nbytes;
+    case 10: return (void**)&d.w_lastcheck;
+    case 11: return (void**)&d.w_pfx;
+    case 12: return (void**)&d.w_pcnt;
+    case 13: return (void**)&d.pdur_cur;
+    default: return (void**)&d.pdur_walk;
+  }
+}
+// dir 0: global -> LDS (and the Dev copy points at LDS); 1: LDS -> global (g: the global Dev)
+__device__ inline void ug_stage(Dev& d, const Dev& g, uint32_t mask, int dir) {
+  for (int k = 0; k < UG_NF; k++) {
+    if (!(mask >> k & 1)) continue;
+    const size_t nb = ug_field_bytes(k, d.W, d.Wp, d.P);
+    char* l = dgp_smem + ug_field_off(k, d.W, d.Wp, d.P, mask);
+    char* gp = (char*)*ug_field_ptr(const_cast<Dev&>(g), k);
+    char* src = dir == 0 ? gp : l;
+    char* dst = dir == 0 ? l : gp;
+    const size_t nw = nb / 4;
+    for (size_t i = threadIdx.x; i < nw; i += blockDim.x) ((uint32_t*)dst)[i] = ((const uint32_t*)src)[i];
+    for (size_t i = nw * 4 + threadIdx.x; i < nb; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  if (dir == 0 && threadIdx.x == 0)
+    for (int k = 0; k < UG_NF; k++)
+      if (mask >> k & 1) *ug_field_ptr(d, k) = dgp_smem + ug_field_off(k, d.W, d.Wp, d.P, mask);
+  __syncthreads();
+}
+
 // update_graph, part 2: the tasks that went waiting -> processing, in priority order,
 // dispatched one by one (they read global state); once idle_task_count is empty every
 // further root-ish task is queued in bulk (:2761) — order-preserving.
@@ -1968,7 +2029,8 @@ __global__ void k_ug_init(const Dev* __restrict__ Dp, int lo) {
 // priority: a new generation); its placements append to the placement log.
 // scan_lo: the first priority position scanned; task_lo: the first task of the graph (a later
 // graph whose user priority outranks earlier tasks: its tasks sit anywhere in the order)
-__global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp, int scan_lo, int task_lo) {
+__global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp, int scan_lo, int task_lo,
+                                                     uint32_t lds_mask) {
   // the dispatch is one lane's chain of dependent reads and writes of the control block
   // (idle_task_count / idle / saturated counts, the global prefix dict, occupancy sums): the
   // block works on an LDS copy of it (and of Dev, whose ctl points at the copy) and writes
@@ -1984,6 +2046,7 @@ __global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp,
     __syncthreads();
     if (threadIdx.x == 0) s_dev.ctl = &s_ctl;
     __syncthreads();
+    if (lds_mask) ug_stage(s_dev, *Dp, lds_mask, 0);
   }
   Ctl* const ctl_g = Dp->ctl;
   const Dev& D = s_dev;
@@ -2097,6 +2160,7 @@ __global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp,
   }
   __syncthreads();
   for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += blockDim.x) ((uint32_t*)ctl_g)[i] = ((const uint32_t*)&s_ctl)[i];
+  if (lds_mask) ug_stage(s_dev, *Dp, lds_mask, 1);
 }
 
 // start of a round: its completion list is the slice of the placement log made by the

@@ -3746,14 +3746,30 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       }
       __threadfence();
       int64_t tot = 0;
-      for (int64_t q = D.dep_ptr[x] + lane; q < D.dep_ptr[x + 1]; q += 64) {
-        const int d = D.dep_idx[q];
-        const int h = D.holder_of[d];
-        const int64_t nb = nbv(D, D.res_nbytes[d]);
-        tot += nb;
-        if (h >= 0 && h < D.W) {
-          __hip_atomic_fetch_add(HS + h, (unsigned long long)nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_add(HC + h, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // 8 dependencies per lane per step: their loads are all in flight before the atomics
+      // (one dependent chain dep_idx -> holder_of / res_nbytes per step, not per dependency)
+      constexpr int UW = 8;
+      const int64_t q1 = D.dep_ptr[x + 1];
+      for (int64_t q0 = D.dep_ptr[x]; q0 < q1; q0 += 64 * UW) {
+        int dq[UW], hq[UW];
+        int64_t nq[UW];
+#pragma unroll
+        for (int u = 0; u < UW; u++) {
+          const int64_t q = q0 + u * 64 + lane;
+          dq[u] = q < q1 ? D.dep_idx[q] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < UW; u++) {
+          hq[u] = dq[u] >= 0 ? D.holder_of[dq[u]] : -1;
+          nq[u] = dq[u] >= 0 ? nbv(D, D.res_nbytes[dq[u]]) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < UW; u++) {
+          tot += nq[u];
+          if (hq[u] >= 0 && hq[u] < D.W) {
+            __hip_atomic_fetch_add(HS + hq[u], (unsigned long long)nq[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(HC + hq[u], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
       }
       __threadfence();

@@ -410,6 +410,42 @@ int grow_logs(dgp_engine* e, int64_t stimuli) {
 }
 
 // the stimulus source of the stream engine for the coming launch
+// k_ug_dispatch: which of its arrays go to dynamic LDS (in the order below, while they fit
+// beside the kernel's static LDS), and that many bytes
+void ug_lds_plan(const dgp::Dev& D, uint32_t* mask, size_t* bytes) {
+  static size_t stat = 0;
+  if (!stat) stat = kernel_static_lds((const void*)dgp::k_ug_dispatch, 48 * 1024);
+  const size_t budget = 160 * 1024 > stat + 1024 ? 160 * 1024 - stat - 1024 : 0;
+  uint32_t m = 0;
+  size_t used = 0;
+  // the prefix durations first (a few hundred bytes, read by every occupancy), then the
+  // list in order while it fits
+  const int order[dgp::UG_NF] = {13, 14, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12};
+  for (int k : order) {
+    const size_t b = (dgp::ug_field_bytes(k, D.W, D.Wp, D.P) + 15) & ~(size_t)15;
+    if (used + b > budget) break;
+    used += b;
+    m |= 1u << k;
+  }
+  *mask = m;
+  *bytes = used;
+}
+
+int launch_ug_dispatch(dgp_engine* e, int scan_lo, int task_lo) {
+  uint32_t mask = 0;
+  size_t bytes = 0;
+  ug_lds_plan(e->D, &mask, &bytes);
+  static size_t attr_set[64];
+  if (bytes > attr_set[e->device & 63]) {
+    HIPCHK(e, hipFuncSetAttribute((const void*)dgp::k_ug_dispatch, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    attr_set[e->device & 63] = bytes;
+  }
+  const dgp::Dev* DP = e->d_dev;
+  return timed_launch(e, 3, [&] {
+    hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), bytes, e->stream, DP, scan_lo, task_lo, mask);
+  });
+}
+
 void stream_source(dgp_engine* e, bool service) {
   dgp::Dev& D = e->D;
   D.svc = service ? 1 : 0;
@@ -1175,8 +1211,7 @@ int dgp_update_graph(dgp_engine* e) {
         hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(e->D.N, 256, 2048)), dim3(256), 0, s, DP, 0);
       }))
     return rc;
-  if (int rc = timed_launch(e, 3, [&] { hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP, 0, 0); }))
-    return rc;
+  if (int rc = launch_ug_dispatch(e, 0, 0)) return rc;
   if (e->snap_rounds > 0) {
     hipLaunchKernelGGL(dgp::k_snapshot, dim3(8), dim3(256), 0, s, DP, e->d_aux + 1, 0);
     HIPCHK(e, hipGetLastError());
@@ -1917,10 +1952,7 @@ int dgp_graph_stimulus(dgp_engine* e, int64_t* n_new_placements) {
         hipLaunchKernelGGL(dgp::k_candidate_commbytes, dim3(grid_for(N - lo, 256, 2048)), dim3(256), 0, s, DP);
       }))
     return rc;
-  if (int rc = timed_launch(e, 3, [&] {
-        hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP, follows ? (int)lo : 0, (int)lo);
-      }))
-    return rc;
+  if (int rc = launch_ug_dispatch(e, follows ? (int)lo : 0, (int)lo)) return rc;
   if (int rc = set_runids(e)) return rc;
   dgp::Ctl c;
   if (int rc = check_device_error(e, &c)) return rc;
@@ -2138,10 +2170,7 @@ static int add_graph_impl(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, 
         hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(n_new, 256, 2048)), dim3(256), 0, s, DP, (int)N0);
       }))
     return rc;
-  if (int rc = timed_launch(e, 3, [&] {
-        hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), 0, s, DP, (int)N0, (int)N0);
-      }))
-    return rc;
+  if (int rc = launch_ug_dispatch(e, (int)N0, (int)N0)) return rc;
   if (int rc = set_runids(e)) return rc;
   e->mode = 2;
   dgp::Ctl c;
