@@ -230,7 +230,8 @@ def c3_leg(eng_cls, local: int, args, link_us: float | None = None) -> dict:
     n = int(len(out["pl_task"]))
     leg = {"metric": "task placements/sec, C3 (P2P-shuffle-shaped graph, placement only)", "value": round(n / dt, 1),
            "unit": "placements/s", "seconds_per_replay": round(dt, 4), "placements_per_replay": n,
-           "n_tasks": int(g["n_tasks"]), "n_partitions": args.c3_partitions, "n_workers": args.c3_workers}
+           "n_tasks": int(g["n_tasks"]), "n_partitions": args.c3_partitions, "n_workers": args.c3_workers,
+           "stream_window": eng.get_window()}
     if link_us:
         leg["latency_bound"] = latency_bound(g, out, link_us, dt * 1e3)
     if not args.no_cpu_baseline:
@@ -274,10 +275,12 @@ def variant_legs(eng_cls, local: int, args) -> dict:
             eng.run_rounds(-1)
         dt = (time.perf_counter() - t0) / n_step
         out = eng.placements()
+        window = eng.get_window()
         eng.close()
         n = int(len(out["pl_task"]))
         leg = {"metric": f"task placements/sec, {what}", "value": round(n / dt, 1), "unit": "placements/s",
                "seconds_per_replay": round(dt, 4), "placements_per_replay": n, "n_tasks": int(g["n_tasks"]),
+               "stream_window": window,
                "n_prefixes": len(g["prefix_names"]),
                "restricted_tasks": int((g["restr_flags"] != 0).sum()) if "restr_flags" in g else 0}
         if not args.no_cpu_baseline:
@@ -708,6 +711,7 @@ def main():
             result["latency_bound"] = latency_bound(g, out, link_us, 1e3 * elapsed / args.steps)
         result["kernels"] = {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in kernels.items()}
         result["config"]["waves"] = int(n_waves)
+        result["config"]["stream_window"] = eng.get_window()  # the stream-kernel build that ran (32 / 64)
         if world == 1 and not args.no_cpu_baseline:
             from oracle import oracle
 
