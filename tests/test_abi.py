@@ -64,3 +64,56 @@ def test_window_is_validated(bad):
 
     with pytest.raises(ValueError):
         PE(0, window=bad)
+
+
+class _WindowLib:
+    """dgp_set_window / dgp_get_window of a library handle, recorded (no GPU)."""
+
+    def __init__(self, window):
+        self.window, self.calls = window, []
+
+    def dgp_set_window(self, h, w):
+        self.calls.append(w)
+        self.window = w
+        return 0
+
+    def dgp_get_window(self, h):
+        return self.window
+
+    def dgp_update_restrictions(self, *a):
+        return 0
+
+
+def _engine_with(window, current):
+    from distributed_amd.engine import PlacementEngine as PE
+
+    e = object.__new__(PE)  # the host logic only: no device handle
+    e.window, e.lib, e.h, e.n_tasks = window, _WindowLib(current), 1, 100
+    return e
+
+
+def test_later_graph_moves_an_auto_engine_to_the_64_slot_build():
+    """engine.py later_graph_window / update_restrictions: the first later graph (or run-time
+    restriction update) that wants the 64-slot build moves an "auto" engine there, once; a
+    forced window never moves."""
+    from distributed_amd import graphs
+
+    plain = graphs.random_dag(2_000, 16, seed=1)
+    restricted = graphs.restrict(plain, 0.1, seed=1)
+    e = _engine_with("auto", 32)
+    e.later_graph_window(plain)
+    assert e.lib.calls == []
+    e.later_graph_window(restricted)
+    assert e.lib.calls == [64]
+    e.later_graph_window(restricted)  # already there
+    assert e.lib.calls == [64]
+    e = _engine_with("auto", 32)
+    e.update_restrictions([5], [[1, 2]], [1])
+    assert e.lib.calls == [64]
+    e = _engine_with("auto", 32)
+    e.update_restrictions([5], [[1, 2]], [0])  # flags 0: nothing restricted
+    assert e.lib.calls == []
+    e = _engine_with(32, 32)  # forced
+    e.later_graph_window(restricted)
+    e.update_restrictions([5], [[1, 2]], [1])
+    assert e.lib.calls == []
