@@ -77,6 +77,9 @@ __constant__ Dev c_dev;
 #ifndef DGP_EXE_PF
 #define DGP_EXE_PF 1  // an idle executor loads the descriptor of the oldest waiting stimulus ahead of its claim
 #endif
+#ifndef DGP_PROF_GLOBAL
+#define DGP_PROF_GLOBAL 0  // diagnostics (with DGP_PROF): prof[9] / [22] take cycles of global stimuli / wide fan-ins
+#endif
 #ifndef DGP_REG_PROBES
 #define DGP_REG_PROBES 0  // registrar sub-phase s_memtime probes (diagnostics)
 #endif
@@ -3746,6 +3749,9 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
       }
       __threadfence();
       int64_t tot = 0;
+#if DGP_PROF_GLOBAL
+      const unsigned long long tw0 = mclk();
+#endif
       // 8 dependencies per lane per step: their loads are all in flight before the atomics
       // (one dependent chain dep_idx -> holder_of / res_nbytes per step, not per dependency)
       constexpr int UW = 8;
@@ -3773,6 +3779,9 @@ __device__ __attribute__((always_inline)) void exe_global(const Dev& D, SLds& L,
         }
       }
       __threadfence();
+#if DGP_PROF_GLOBAL
+      PROF(if (lane == 0) S.prof[22] += mclk() - tw0);  // diagnostics: the wide fan-in's holder sums
+#endif
       tot = wsum64(tot);
       Key b = argmin_workers(D, [&](int cw, Key& kk) {
         const double ocw = occ_of<LW>(P, D, cw, durv);  // all lanes: it shuffles
@@ -4018,7 +4027,11 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     if (D.resident && lane == 0) S.t_role[3] = rclk();
     if (G && (cf & F_GLOBAL)) {
       exe_global_entry<LW>(cs, cr);
+#if DGP_PROF_GLOBAL  // diagnostics: cycles in global stimuli instead of their count
+      PROF(if (lane == 0) S.prof[9] += mclk() - t0);
+#else
       PROF(if (lane == 0) S.prof[9]++);
+#endif
     } else if (G && (cf & F_SIMPLE) && cq == 0 && !cex && exe_run_entry<LW>(cs, cr, E)) {
       // a run of single-worker completions, back to back (only this executor calls out of line)
     } else {
