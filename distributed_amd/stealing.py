@@ -343,7 +343,9 @@ class StealRows:
             for j, ex in self.hmore.items():
                 hidx[hptr[j]:hptr[j + 1]] = np.sort(np.concatenate([hm[j, :self.HM], amap[np.asarray(ex, np.int64)]]))
         else:
-            hm.sort(axis=1)
+            multi = np.flatnonzero(inline > 1)  # most data have one holder: sort only the others
+            if len(multi):
+                hm[multi] = np.sort(hm[multi], axis=1)
             hidx = hm[m]
         p.update(dep_ptr=dep_ptr, dep_idx=gids.astype(np.int32), data_nbytes=self.dnb[:nd_],
                  data_get_nbytes=self.dgnb[:nd_], holder_ptr=hptr, holder_idx=hidx.astype(np.int32))
