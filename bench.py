@@ -168,8 +168,9 @@ def steal_plugin_leg(eng, p, out_dev) -> dict:
     plugin state at the same C4 problem (distributed_amd/steal_standin.py; the tasks in the
     bins the device's levels give). Everything of balance() before move_task_request, which
     is the reference's own code (its per-request cost, measured in the reference, beside)."""
-    from distributed_amd.steal_standin import plugin_from_problem
-    from distributed_amd.stealing import balance_plan
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    from steal_standin import plugin_from_problem
+    from distributed_amd.stealing import apply_requests, balance_plan
 
     plugin, slot_task = plugin_from_problem(p, out_dev["level"])
     balance_plan(plugin, eng)  # warm-up
@@ -187,6 +188,17 @@ def steal_plugin_leg(eng, p, out_dev) -> dict:
         out, rows, wss = plan
         req = slot_task[rows[out["st_task"]]]  # the request list: task of each request, in order
     dt = (time.perf_counter() - t0) / n_call
+    # the whole product path once: balance_plan, then the requests applied in bulk (bins,
+    # steal-request messages, in-flight records and accounts, log, metrics; apply_requests)
+    t0 = time.perf_counter()
+    out_a, rows_a, wss_a = balance_plan(plugin, eng)
+    t1 = time.perf_counter()
+    log = apply_requests(plugin, out_a, plugin._last_problem, rows_a, wss_a, t0)
+    t_full = time.perf_counter() - t0
+    t_apply = time.perf_counter() - t1
+    nmsg = sum(len(c.buffer) for c in plugin.scheduler.stream_comms.values())
+    applied_ok = bool(len(log) == len(plugin.in_flight) == nmsg == len(req)
+                      and all(len(plugin.key_stealable) + len(req) == len(slot_task) for _ in (0,)))
     parity = bool(np.array_equal(req, out_dev["st_task"]) and all(
         np.array_equal(out[k], out_dev[k]) for k in ("st_victim", "st_thief", "st_level", "st_cost", "st_occ_victim",
                                                    "st_occ_thief", "inflight_occ", "inflight_tasks", "idle_after",
@@ -195,7 +207,12 @@ def steal_plugin_leg(eng, p, out_dev) -> dict:
            "ms_per_call": round(dt * 1e3, 3), "fits_100ms_interval": bool(dt <= 0.1),
            "host_problem_ms": round(min(t_prob) * 1e3, 3), "host_problem_ms_mean": round(t_host * 1e3, 3),
            "stealable_tasks": int(len(slot_task)), "steal_requests": int(len(req)),
-           "boundary": "StealRows (plugin state) -> balance_plan -> request arrays; move_task_request excluded",
+           "boundary": "StealRows (plugin state) -> balance_plan -> request arrays",
+           "with_requests_applied_ms": round(t_full * 1e3, 3), "apply_requests_ms": round(t_apply * 1e3, 3),
+           "with_requests_boundary": "balance_plan + apply_requests (bulk move_task_request: bins, steal-request "
+                                     "messages per victim, in_flight, accounts, log, metrics); the scheduler's "
+                                     "check_idle_saturated of the visited victims excluded",
+           "requests_applied_consistent": applied_ok,
            "parity_with_device_leg": parity}
     ref = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "ref_python_c4.json")
     if os.path.exists(ref):

@@ -1614,7 +1614,8 @@ int dgp_add_worker_at(dgp_engine* e, int32_t nthreads, int32_t running, int32_t 
     if (ps.pre > ps.seq || ps.walk != ps.rec_len)
       return fail(e, DGP_E_STATE, "dgp_add_worker_at: the stream engine has prefetched stimuli or unfolded records");
   }
-  e->paused_h.insert(e->paused_h.begin() + position, (uint8_t)(running ? 0 : 1));
+  if (position < e->D.W && e->snap_rounds > 0)  // [rounds][W] snapshot columns would belong to the wrong worker
+    return fail(e, DGP_E_STATE, "dgp_add_worker_at: a mid-list insertion with replay snapshots recorded");
   namespace S = dgp::st;
   dgp::Dev& D = e->D;
   const size_t W0 = D.W, W1 = W0 + 1;
@@ -1734,6 +1735,8 @@ int dgp_add_worker_at(dgp_engine* e, int32_t nthreads, int32_t running, int32_t 
       HIPCHK(e, hipMemcpy(const_cast<int32_t*>(D.restr_pool), h.data(), h.size() * 4, hipMemcpyHostToDevice));
     }
   }
+  // the host mirrors follow only once every device step above succeeded
+  e->paused_h.insert(e->paused_h.begin() + position, (uint8_t)(running ? 0 : 1));
   e->nthreads.insert(e->nthreads.begin() + pos, nthreads);
   D.total_nthreads += nthreads;
   const int32_t cap = D.sat_inf ? 0 : std::max((int32_t)std::ceil(D.saturation * nthreads), (int32_t)1);

@@ -337,6 +337,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         self._route = 0             # the decide_worker route of the scheduler's current decision
         self.removed: set = set()   # addresses of removed workers (they keep their engine index)
         self._losing = None         # the worker whose loss the engine decided (its replica drops are the engine's)
+        self._loss_token = None     # the open remove_worker window: (its transitions, address)
         self._rootish_h: dict = {}  # key -> the _rootish override the engine holds (-1 / 0 / 1)
         self._restr_h: dict = {}    # key -> (restriction flags, valid worker indices) the engine holds
         # key -> (message batch, row): the who_has / nbytes of the compute-task message of an
@@ -508,23 +509,55 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._enter()
             address = args[0] if args else kwargs.get("address")
             lost = False
-            if self.active and self.engine is not None:
+            # the reference returns "already-removed" before any transition when the scheduler
+            # is closed or the (coerced) address is not a worker (:5193-5199): no engine call then
+            live = self._removable(address)
+            if live is not None and self.active and self.engine is not None:
                 try:
-                    lost = self._lose_worker(address, bool(kwargs.get("safe", False)))
+                    lost = self._lose_worker(live, bool(kwargs.get("safe", False)))
                 except Exception as e:  # an engine failure ends GPU placement, never the scheduler
                     self.fallback(f"remove_worker({address}): {e}")
-            self._allowed.append(_LOSS_TRANSITIONS if lost else frozenset())
+            # the loss window closes in the plugin hook (``remove_worker`` below), which the
+            # reference calls synchronously right after its transitions (:5298-5317), not across
+            # the await of the plugins' awaitables that follows
+            token = (_LOSS_TRANSITIONS if lost else frozenset(), live)
+            self._loss_token = token
+            self._allowed.append(token[0])
             try:
                 return await orig(*args, **kwargs)
             finally:
-                self._allowed.pop()
-                self._losing = None
+                self._close_loss(token)
 
         remove_worker._gpu_placement = True
         s.remove_worker = remove_worker  # per instance: every self.remove_worker call goes through it
         rpc = getattr(s, "handlers", None)
         if isinstance(rpc, dict) and "unregister" in rpc:
             rpc["unregister"] = remove_worker
+
+    def _removable(self, address):
+        """The address ``Scheduler.remove_worker`` would act on, or None when it returns
+        "already-removed" without a transition (scheduler closed, not a worker)."""
+        s = self.scheduler
+        st = getattr(s, "status", None)
+        if getattr(st, "name", st) == "closed":
+            return None
+        coerce = getattr(s, "coerce_address", None)
+        if callable(coerce):
+            try:
+                address = coerce(address)
+            except Exception:
+                return None
+        return address if address in getattr(s, "workers", {}) else None
+
+    def _close_loss(self, token):
+        """End the window a ``remove_worker`` stimulus opened (once: the plugin hook or,
+        when the reference returned early, the wrapper's ``finally``)."""
+        if getattr(self, "_loss_token", None) is not token:
+            return
+        self._loss_token = None
+        if self._allowed and self._allowed[-1] is token[0]:
+            self._allowed.pop()
+        self._losing = None
 
     @staticmethod
     def _loss_supported(s, ws, proc, held, safe) -> bool:
@@ -1350,13 +1383,17 @@ class GPUPlacementExtension(SchedulerPlugin):
         not restate, by the scheduler itself (the transition hook suspended the engine at the
         first of them) after which the engine takes the scheduler's state (dgp_sync_*)."""
         self._close_window()
+        losing = self._losing
+        token = getattr(self, "_loss_token", None)
+        if token is not None and token[1] == worker:
+            self._close_loss(token)  # the stimulus' transitions are over (:5298): close its window now
         if not self.active or self.engine is None or worker not in self.worker_index:
             return
         on_device = not self.suspended
         w = self.worker_index.pop(worker)
         self.removed.add(worker)
         self.workers[w] = worker + _REMOVED  # keeps its index and its place in address order
-        if worker == self._losing and on_device:  # dgp_lose_worker decided the whole stimulus
+        if worker == losing and on_device:  # dgp_lose_worker decided the whole stimulus
             self._end_of_stimulus(f"remove_worker({worker})")
             return
         try:

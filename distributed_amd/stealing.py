@@ -24,7 +24,10 @@ is hash-dependent; the golden fixtures pin the same canonical order).
 """
 from __future__ import annotations
 
+import gc
+import itertools
 import math
+import operator
 from collections import Counter
 from time import time
 
@@ -124,8 +127,9 @@ class StealRows:
         self.rst = np.zeros(cap, np.uint8)
         self.more = {}  # slot -> dependency ids beyond the first KD
         self.pk_bad = {}  # slot -> a priority pack_priority cannot hold
-        self.data_id, self.data, self.data_ref, self.data_free = {}, [], [], []
+        self.data_id, self.data, self.data_free = {}, [], []
         dcap = 1024
+        self.data_ref = np.zeros(dcap, np.int64)  # task rows referencing each dependency
         self.dnb = np.zeros(dcap, np.int64)
         self.dgnb = np.zeros(dcap, np.int64)
         self.hold = np.zeros((dcap, self.HM), np.int32)
@@ -164,11 +168,11 @@ class StealRows:
         else:
             j = len(self.data)
             self.data.append(dts)
-            self.data_ref.append(0)
             if j >= len(self.dnb):
                 cap = 2 * len(self.dnb)
-                for nm in ("dnb", "dgnb", "hold", "hcnt"):
+                for nm in ("data_ref", "dnb", "dgnb", "hold", "hcnt"):
                     setattr(self, nm, self._grown(getattr(self, nm), cap))
+            self.data_ref[j] = 0
         self.data_id[dts] = j
         self.dnb[j] = dts.nbytes
         self.dgnb[j] = dts.get_nbytes()
@@ -287,6 +291,42 @@ class StealRows:
         self.task[i] = None
         self.free.append(i)
 
+    def remove_many(self, tss, slots) -> None:
+        """``remove`` of many rows at once (the requested tasks of one balance()): ``slots``
+        their row slots, in the order of ``tss``."""
+        slots = np.asarray(slots, np.int64)
+        if not len(slots):
+            return
+        pop = self.slot.pop
+        for ts in tss:
+            pop(ts, None)
+        n = self.nd[slots].astype(np.int64)
+        inrow = np.arange(self.KD)[None, :] < np.minimum(n, self.KD)[:, None]
+        ids = [self.dmat[slots][inrow]]
+        if self.more:
+            more = self.more
+            ids += [np.asarray(more.pop(i), np.int64) for i in slots[n > self.KD].tolist() if i in more]
+        ids = np.concatenate(ids)
+        dec = np.bincount(ids, minlength=len(self.data))
+        touched = np.flatnonzero(dec)
+        self.data_ref[touched] -= dec[touched]
+        for j in touched[self.data_ref[touched] == 0].tolist():
+            del self.data_id[self.data[j]]
+            self.data[j] = None
+            self.hmore.pop(j, None)
+            self.data_free.append(j)
+        gone = touched[self.data_ref[touched] == 0]
+        self.hcnt[gone] = 0
+        if self.pk_bad:
+            for i in slots.tolist():
+                self.pk_bad.pop(i, None)
+        self.live[slots] = False
+        task = self.task
+        sl = slots.tolist()
+        for i in sl:
+            task[i] = None
+        self.free.extend(sl)
+
     def clear(self) -> None:
         self.__init__()
 
@@ -389,6 +429,121 @@ def ordered_problem(p, slots):
     return q, np.asarray(slots)[perm]
 
 
+def thief_comm_bytes(p, prow, thief) -> np.ndarray:
+    """Per request: the bytes of its task's dependencies the thief does not hold --
+    ``get_comm_cost(ts, thief)``'s sum (scheduler.py:3006-3022, raw ``nbytes``) -- from the
+    problem arrays (``prow``: each request's problem row, ``thief``: its thief's index)."""
+    dp, di = p["dep_ptr"], p["dep_idx"]
+    a, b = dp[prow], dp[prow + 1]
+    cnt = (b - a).astype(np.int64)
+    K = len(prow)
+    if not K or not cnt.sum():
+        return np.zeros(K, np.int64)
+    k_of = np.repeat(np.arange(K), cnt)  # one entry per (request, dependency)
+    first = np.cumsum(cnt) - cnt
+    d = di[np.repeat(a, cnt) + (np.arange(len(k_of)) - np.repeat(first, cnt))].astype(np.int64)
+    hp, hi = p["holder_ptr"], p["holder_idx"]
+    hn = (hp[d + 1] - hp[d]).astype(np.int64)
+    e_of = np.repeat(np.arange(len(d)), hn)  # one entry per (dependency entry, holder)
+    hfirst = np.cumsum(hn) - hn
+    h = hi[np.repeat(hp[d], hn) + (np.arange(len(e_of)) - np.repeat(hfirst, hn))]
+    held = np.zeros(len(d), bool)
+    held[e_of[h == thief[k_of[e_of]]]] = True
+    nb = np.where(held, 0, p["data_nbytes"][d]).astype(np.int64)
+    out = np.zeros(K, np.int64)
+    np.add.at(out, k_of, nb)
+    return out
+
+
+def apply_requests(plugin, out, p, rows, wss, start) -> list:
+    """The requests of one balance(), applied in bulk -- what ``move_task_request`` does per
+    request (stealing.py:279-321: the task leaves its bin, a ``steal-request`` message to the
+    victim, the in-flight record and accounts, ``_add_to_in_flight`` :191-199), the log entry
+    and both metrics (:466-480) -- with the same results. The in-flight accounts are the
+    device's (its walk carried them in the reference's operation order: ``inflight_occ`` /
+    ``inflight_tasks``); each request's thief duration is ``get_task_duration +
+    get_comm_cost(ts, thief)`` from the problem arrays; the victim duration is the device's
+    ``st_cost`` (the same two terms). Messages go per victim in request order (one
+    ``BatchedSend.send(*msgs)``). Returns the ``("request", log)`` entries."""
+    st_task = np.asarray(out["st_task"], np.int64)
+    if not len(st_task):
+        return []
+    # the bulk allocations (in-flight records, messages, log entries) would trigger the cyclic
+    # collector again and again over the scheduler's whole heap; none of them forms a cycle
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        return _apply_requests(plugin, out, p, rows, wss, start, st_task)
+    finally:
+        if was:
+            gc.enable()
+
+
+def _apply_requests(plugin, out, p, rows, wss, start, st_task) -> list:
+    s = plugin.scheduler
+    K = len(st_task)
+    slots = np.asarray(rows)[st_task]
+    tss = _gather(plugin.rows.task, slots.tolist())
+    vi, ti = np.asarray(out["st_victim"], np.int64), np.asarray(out["st_thief"], np.int64)
+    lv = np.asarray(out["st_level"], np.int64)
+    cost = np.asarray(out["st_cost"], np.float64)
+    thief_dur = np.asarray(p["duration"], np.float64)[st_task] + thief_comm_bytes(p, st_task, ti) / s.bandwidth
+    c0 = plugin._request_counter
+    plugin._request_counter = c0 + K
+    sids = [f"steal-{c}" for c in range(c0, c0 + K)]
+    A = [ws.address for ws in wss]
+    per_victim = [None] * len(wss)
+    ks_pop, bins, slot_pop = plugin.key_stealable.pop, plugin.stealable, plugin.rows.slot.pop
+    inflight = plugin.in_flight
+    log = []
+    log_append = log.append
+    # one pass over the requests, each TaskState touched once: its bin (remove_key_from_stealable
+    # :230-239), its row slot, the steal-request message (:306-308), the in-flight record
+    # (:309-320, _add_to_in_flight :192) and the log entry (:468-478)
+    for ts, sid, w, t_, l_, c, vd, td, ov, ot in zip(tss, sids, vi.tolist(), ti.tolist(), lv.tolist(), cost.tolist(),
+                                                     cost.tolist(), thief_dur.tolist(),
+                                                     np.asarray(out["st_occ_victim"]).tolist(),
+                                                     np.asarray(out["st_occ_thief"]).tolist()):
+        r = ks_pop(ts, None)
+        if r is not None:
+            bins[r[0]][r[1]].discard(ts)
+        slot_pop(ts, None)
+        key = ts.key
+        m = per_victim[w]
+        if m is None:
+            m = per_victim[w] = []
+        m.append({"op": "steal-request", "key": key, "stimulus_id": sid})
+        v, t = wss[w], wss[t_]
+        inflight[ts] = {"victim": v, "thief": t, "victim_duration": vd, "thief_duration": td, "stimulus_id": sid}
+        log_append((start, l_, key, c, A[w], ov, A[t_], ot))
+    plugin.rows.remove_many((), slots)  # the slots themselves (their TaskStates left above)
+    comms = getattr(s, "stream_comms", {})
+    for w, msgs in enumerate(per_victim):
+        if msgs:
+            comms[A[w]].send(*msgs)
+    plugin._in_flight_event.clear()
+    iocc, itsk = out["inflight_occ"], out["inflight_tasks"]
+    io, it = plugin.in_flight_occupancy, plugin.in_flight_tasks
+    for i in np.unique(np.concatenate([vi, ti])).tolist():
+        io[wss[i]] = float(iocc[i])
+        it[wss[i]] = int(itsk[i])
+    # metrics (:479-480): counts per level, and the costs summed per level in request order
+    # (np.cumsum adds sequentially, as the reference's += does)
+    mc, mt = plugin.metrics["request_count_total"], plugin.metrics["request_cost_total"]
+    for l_ in np.unique(lv).tolist():
+        sel = cost[lv == l_]
+        mc[l_] += int(len(sel))
+        mt[l_] = float(np.cumsum(np.concatenate([[mt[l_]], sel]))[-1])
+    return log
+
+def _gather(seq, idx):
+    """[seq[i] for i in idx] in one C call (operator.itemgetter); a tuple."""
+    if not idx:
+        return ()
+    if len(idx) == 1:
+        return (seq[idx[0]],)
+    return operator.itemgetter(*idx)(seq)
+
 def balance_plan(plugin, engine):
     """GPUWorkStealing.balance()'s decisions from the plugin's state, before any of them is
     applied: (device outputs, each output row's StealRows slot, workers in device order), or
@@ -399,6 +554,7 @@ def balance_plan(plugin, engine):
         return None
     p, rows, wss = plugin.rows.problem(plugin)
     out = engine.steal_balance(p)
+    plugin._last_problem = p  # apply_requests reads its dependency rows (thief durations)
     return out, rows, wss
 
 
@@ -444,10 +600,12 @@ class GPUWorkStealing(WorkStealing):
     ``device``); ``validate``: after applying, check that the plugin's in-flight accounts
     and the scheduler's idle / saturated sets equal the device's."""
 
-    def __init__(self, scheduler, *, device: int = 0, engine_factory=None, validate: bool = False):
+    def __init__(self, scheduler, *, device: int = 0, engine_factory=None, validate: bool = False,
+                 bulk: bool = True):
         self.device = device
         self.engine_factory = engine_factory
         self.validate = validate
+        self.bulk = bulk  # requests applied in bulk (apply_requests); False: move_task_request each
         self.engine = None
         self.gpu_stats = Counter()
         self.rows = StealRows()  # before the reference __init__: its hooks may fill the bins
@@ -527,19 +685,10 @@ class GPUWorkStealing(WorkStealing):
         if plan is None:
             return
         out, rows, wss = plan
-        task = self.rows.task
-        slots = rows[out["st_task"]].tolist()
-        log = []
-        for k, sl in enumerate(slots):
-            ts = task[sl]
-            victim, thief = wss[int(out["st_victim"][k])], wss[int(out["st_thief"][k])]
-            level = int(out["st_level"][k])
-            cost = float(out["st_cost"][k])
-            self.move_task_request(ts, victim, thief)  # :466
-            log.append((start, level, ts.key, cost, victim.address, float(out["st_occ_victim"][k]), thief.address,
-                        float(out["st_occ_thief"][k])))
-            self.metrics["request_count_total"][level] += 1  # :479-480
-            self.metrics["request_cost_total"][level] += cost
+        if self.bulk and self._comms_open(out, wss):
+            log = apply_requests(self, out, self._last_problem, rows, wss, start)
+        else:
+            log = self._apply_one_by_one(out, rows, wss, start)
         for i in np.flatnonzero(out["checked"]):  # check_idle_saturated(victim, occ=combined) :498-500
             ws = wss[int(i)]
             s.check_idle_saturated(ws, occ=self._combined_occupancy(ws))
@@ -553,6 +702,34 @@ class GPUWorkStealing(WorkStealing):
         stop = time()
         if s.digests:
             s.digests["steal-duration"].add(stop - start)
+
+    def _comms_open(self, out, wss) -> bool:
+        """Every victim's stream is open: a closed one makes move_task_request skip that
+        request's in-flight record (:322-324), which only the per-request path restates."""
+        comms = getattr(self.scheduler, "stream_comms", {})
+        for i in np.unique(np.asarray(out["st_victim"])).tolist():
+            c = comms.get(wss[i].address)
+            comm = getattr(c, "comm", None)
+            if c is None or (comm is not None and comm.closed()):
+                return False
+        return True
+
+    def _apply_one_by_one(self, out, rows, wss, start) -> list:
+        """The requests through the reference's own ``move_task_request``, one at a time."""
+        task = self.rows.task
+        slots = rows[out["st_task"]].tolist()
+        log = []
+        for k, sl in enumerate(slots):
+            ts = task[sl]
+            victim, thief = wss[int(out["st_victim"][k])], wss[int(out["st_thief"][k])]
+            level = int(out["st_level"][k])
+            cost = float(out["st_cost"][k])
+            self.move_task_request(ts, victim, thief)  # :466
+            log.append((start, level, ts.key, cost, victim.address, float(out["st_occ_victim"][k]), thief.address,
+                        float(out["st_occ_thief"][k])))
+            self.metrics["request_count_total"][level] += 1  # :479-480
+            self.metrics["request_cost_total"][level] += cost
+        return log
 
     def _validate(self, out, wss):
         s = self.scheduler

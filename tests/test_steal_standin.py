@@ -1,12 +1,16 @@
 """bench.py's C4 balance() leg runs GPUWorkStealing's product path (``balance_plan``: the
 plugin's StealRows -> problem -> device) on a scheduler-free stand-in of the plugin state
-(distributed_amd/steal_standin.py). On CPU: the stand-in's problem, put in the device's walk
+(tools/steal_standin.py). On CPU: the stand-in's problem, put in the device's walk
 order (dgp_steal_order's sort), is the C4 problem itself, and the oracle gives the same
 requests on both (the task index of each request mapped through the row slots)."""
+import os
+import sys
+
 import numpy as np
 
-from distributed_amd import graphs
-from distributed_amd.steal_standin import plugin_from_problem
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+from distributed_amd import graphs  # noqa: E402
+from steal_standin import plugin_from_problem  # noqa: E402
 from distributed_amd.stealing import ordered_problem
 from oracle import oracle
 

@@ -6,15 +6,22 @@ the in-flight accounts -- and a few scheduler fields (workers, idle / saturated,
 bandwidth, get_task_duration / valid_workers). The GPU box has no ``distributed``, so the
 bench builds these from a C4 problem (graphs.steal_problem) with plain objects carrying
 exactly the attributes balance() reads, fills the rows through ``StealRows.put`` as the
-hooks would, and times ``balance_plan`` -- plugin state to the ordered request arrays, the
-product code path of ``GPUWorkStealing.balance`` before ``move_task_request`` is applied
-(the reference's own per-request cost, reported beside it).
+hooks would, with the reference plugin's bins (``stealable`` / ``key_stealable``) and
+in-flight fields, and times ``GPUWorkStealing.balance``'s product path on it:
+``balance_plan`` (plugin state to the ordered request arrays) and ``apply_requests`` (the
+requests applied in bulk: bins, messages, in-flight records and accounts, log, metrics).
+Test / bench scaffolding (tools/, not the product package).
 """
 from __future__ import annotations
 
+import os
+import sys
+from collections import defaultdict
+
 import numpy as np
 
-from .stealing import StealRows
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_amd.stealing import StealRows  # noqa: E402
 
 
 class Obj:
@@ -22,6 +29,25 @@ class Obj:
 
     def __init__(self, **kw):
         self.__dict__.update(kw)
+
+
+class Comm:
+    """BatchedSend's send(*msgs) (batched.py:150-159), buffering."""
+
+    def __init__(self):
+        self.buffer = []
+        self.comm = None
+
+    def send(self, *msgs):
+        self.buffer.extend(msgs)
+
+
+class Event:
+    def clear(self):
+        pass
+
+    def set(self):
+        pass
 
 
 class Sched:
@@ -35,6 +61,7 @@ class Sched:
         self.total_nthreads = total_nthreads
         self.bandwidth = bandwidth
         self.unknown_durations = {}
+        self.stream_comms = {a: Comm() for a in workers}
 
     def get_task_duration(self, ts):  # scheduler.py:3024-3041
         d = ts.prefix.duration_average
@@ -72,7 +99,10 @@ def plugin_from_problem(p: dict, levels) -> tuple:
     data = [_data(nb, gnb, {wl[int(h)] for h in hs})
             for nb, gnb, hs in zip(p["data_nbytes"].tolist(), p["data_get_nbytes"].tolist(), holders)]
     prefixes = {d: Obj(name=f"p{j}", duration_average=float(d)) for j, d in enumerate(sorted(set(p["duration"].tolist())))}
-    plugin = Obj(scheduler=s, rows=StealRows(), in_flight_occupancy={}, in_flight_tasks={})
+    plugin = Obj(scheduler=s, rows=StealRows(), in_flight_occupancy=defaultdict(int), in_flight_tasks=defaultdict(int),
+                 in_flight={}, _request_counter=0, _in_flight_event=Event(), key_stealable={},
+                 stealable={a: [set() for _ in range(15)] for a in addr},
+                 metrics={"request_count_total": defaultdict(int), "request_cost_total": defaultdict(float)})
     dp, di = p["dep_ptr"], p["dep_idx"]
     lv = np.asarray(levels)
     slot_task = []
@@ -82,6 +112,9 @@ def plugin_from_problem(p: dict, levels) -> tuple:
         ts = Obj(key=("t", t), priority=(0, 1, t), dependencies=[data[int(d)] for d in di[dp[t]:dp[t + 1]]],
                  prefix=prefixes[float(p["duration"][t])], worker_restrictions=None, host_restrictions=None,
                  resource_restrictions=None, loose_restrictions=False)
-        plugin.rows.put(ts, addr[int(p["victim"][t])], int(lv[t]))
+        a, level = addr[int(p["victim"][t])], int(lv[t])
+        plugin.stealable[a][level].add(ts)  # put_key_in_stealable (stealing.py:220-228)
+        plugin.key_stealable[ts] = (a, level)
+        plugin.rows.put(ts, a, level)
         slot_task.append(t)
     return plugin, np.array(slot_task, np.int64)
