@@ -2022,6 +2022,251 @@ __device__ inline void ug_stage(Dev& d, const Dev& g, uint32_t mask, int dir) {
   __syncthreads();
 }
 
+// update_graph's root-ish dispatch with queuing (decide_worker_rootish_queuing_enabled
+// :2195-2245, then _add_to_processing :3199-3256 as place_eager does it) for a run of
+// consecutive dependency-free root-ish ready tasks of one prefix, every pick at once.
+// The pick is the idle_task_count worker of least len(processing) / nthreads (ties: the
+// canonical index); a pick changes only the picked worker's count. With one nthreads over
+// idle_task_count the picks are therefore the pairs (v, m) -- worker v at processing count
+// m, nproc_v <= m < nproc_v + slots_v -- in ascending (m, v) order: pair (v, m)'s rank is
+// the pairs of the levels below m plus the workers before v at level m, and pick r takes
+// ready[pos + r]. For such tasks (no comm bytes, no needs_what, one prefix p) everything
+// place_eager does at pick r on v (the k-th on v) is a function of (v, k, r) and the state
+// before the run: v's dict with p counted k (+1 after), nproc_v + k, the global dict with p
+// counted r + 1 (total_occupancy for check_idle_saturated's idle / saturated test). So the
+// picks are one thread each, the workers' end states (dict, nproc, idle / saturated of
+// their last pick, idle_task_count) one thread per worker, and the tree is rebuilt after.
+// All threads; returns the picks made, 0 when the run does not qualify (the serial path
+// takes the task and raises any capacity error as before).
+constexpr int UG_FILL_LEVELS = 64;
+__device__ __attribute__((noinline)) int64_t ug_fill_rootish(const Dev& D, int64_t pos, int64_t nr, int64_t stage0,
+                                                             const double* dur) {
+  __shared__ int64_t f_lvl[UG_FILL_LEVELS + 1];  // pairs below each level (exclusive prefix)
+  __shared__ int f_ok, f_nth, f_mlo, f_mhi, f_run;
+  __shared__ int64_t f_stot, f_M;
+  Ctl* c = D.ctl;
+  const int tid = threadIdx.x;
+  const int x0 = D.ready[pos];
+  const int p = D.prefix[x0];
+  if (tid == 0) {
+    f_ok = (D.tflags[x0] & TF_ROOTISH) && D.dep_ptr[x0 + 1] == D.dep_ptr[x0] && p >= 0 && p < D.P ? 1 : 0;
+    f_nth = -1;
+    f_mlo = INT32_MAX;
+    f_mhi = -1;
+    f_run = INT32_MAX;
+    f_stot = 0;
+  }
+  __syncthreads();
+  if (!f_ok) return 0;
+  // the run: consecutive ready tasks from pos that are root-ish, dependency-free, of prefix p
+  for (int64_t i0 = pos; i0 < nr && f_run == INT32_MAX; i0 += blockDim.x) {
+    const int64_t i = i0 + tid;
+    if (i < nr) {
+      const int x = D.ready[i];
+      if (!((D.tflags[x] & TF_ROOTISH) && D.dep_ptr[x + 1] == D.dep_ptr[x] && D.prefix[x] == p))
+        atomicMin(&f_run, (int)(i - pos));
+    }
+    __syncthreads();
+  }
+  const int64_t M = f_run == INT32_MAX ? nr - pos : (int64_t)f_run;
+  // idle_task_count: one nthreads, the level span, the slots; every picked worker's dict
+  // must hold p or have room for it (else the serial path raises ERR_PREFIX_CAP)
+  for (int v = tid; v < D.W; v += blockDim.x) {
+    if (!(WK_flags(D)[v] & WF_ITC)) continue;
+    const int nt = WK_nthreads(D)[v];
+    const int np = WK_nproc(D)[v];
+    const int64_t sl = task_slots_available(D, v);
+    if (sl <= 0 || nt <= 0) {
+      f_ok = 0;
+      continue;
+    }
+    if (atomicCAS(&f_nth, -1, nt) != -1 && f_nth != nt) f_ok = 0;
+    atomicMin(&f_mlo, np);
+    atomicMax(&f_mhi, (int)(np + sl - 1));
+    atomicAdd((unsigned long long*)&f_stot, (unsigned long long)sl);
+    const int n = WK_plen(D)[v];
+    bool has = false;
+    for (int i = 0; i < n; i++) has = has || WK_pfx(D)[(size_t)v * PMAX + i] == p;
+    if (!has && n >= PMAX) f_ok = 0;
+  }
+  __syncthreads();
+  if (!f_ok || f_nth <= 0 || f_stot <= 0 || f_mhi - f_mlo + 1 > UG_FILL_LEVELS) return 0;
+  const int64_t Mp = M < f_stot ? M : f_stot;
+  bool gdict_room = false;
+  for (int i = 0; i < c->g_plen; i++) gdict_room = gdict_room || c->g_pfx[i] == p;
+  if ((!gdict_room && c->g_plen >= PMAX_G) || stage0 + Mp > D.st_cap) return 0;
+  const int mlo = f_mlo, L = f_mhi - f_mlo + 1;
+  // pairs per level, then their exclusive prefix over the levels
+  if (tid <= L) f_lvl[tid] = 0;
+  __syncthreads();
+  for (int v = tid; v < D.W; v += blockDim.x) {
+    if (!(WK_flags(D)[v] & WF_ITC)) continue;
+    const int np = WK_nproc(D)[v];
+    const int64_t sl = task_slots_available(D, v);
+    for (int64_t k = 0; k < sl; k++) atomicAdd((unsigned long long*)&f_lvl[np + k - mlo + 1], 1ull);
+  }
+  __syncthreads();
+  if (tid == 0)
+    for (int l = 1; l <= L; l++) f_lvl[l] += f_lvl[l - 1];
+  __syncthreads();
+  // ranks: per level, the workers in index order (a block scan over the workers); pick r of
+  // worker v (its k-th) records v in the staging row and k in st_comm (0 once placed)
+  // scratch (the tree is rebuilt after): each worker's last pick, its rank and its k
+  int32_t* last = D.t_idx;
+  double* last_k = D.t_key;
+  for (int v = tid; v < D.W; v += blockDim.x) last[v] = -1;
+  __syncthreads();
+  for (int l = 0; l < L; l++) {
+    const int m = mlo + l;
+    if (f_lvl[l] >= Mp) break;
+    int64_t base = 0;
+    for (int v0 = 0; v0 < D.W; v0 += blockDim.x) {
+      const int v = v0 + tid;
+      bool in = false;
+      if (v < D.W && (WK_flags(D)[v] & WF_ITC)) {
+        const int np = WK_nproc(D)[v];
+        in = np <= m && m < np + task_slots_available(D, v);
+      }
+      int64_t tot;
+      const int64_t o = block_excl_scan(in ? 1 : 0, &tot);
+      const int64_t r = f_lvl[l] + base + o;
+      if (in && r < Mp) {
+        D.st_worker[stage0 + r] = v;
+        D.st_comm[stage0 + r] = m - WK_nproc(D)[v];
+        last[v] = (int32_t)r;  // levels ascend: the last level written is the worker's last pick
+        last_k[v] = (double)(m - WK_nproc(D)[v]);
+      }
+      base += tot;
+    }
+  }
+  __syncthreads();
+  __threadfence_block();
+  // the picks, one thread each: the placement record (worker_objective's start before the
+  // pick, ws.nbytes) and the task's TaskState
+  const double bw = (double)D.bandwidth;
+  auto occ_k = [&](int v, int64_t k) {  // v's occupancy with p counted k more times (:1884-1903)
+    double res = 0.0;
+    const int n = WK_plen(D)[v];
+    const int* pf = WK_pfx(D) + (size_t)v * PMAX;
+    const int* pc = WK_pcnt(D) + (size_t)v * PMAX;
+    bool has = false;
+    for (int i = 0; i < n; i++) {
+      const int64_t cnt = pc[i] + (pf[i] == p ? k : 0);
+      has = has || pf[i] == p;
+      res += prefix_duration(D, dur, pf[i]) * (double)cnt;
+    }
+    if (!has && k > 0) res += prefix_duration(D, dur, p) * (double)k;  // appended at the first pick
+    return res + (double)WK_netocc(D)[v] / bw;
+  };
+  for (int64_t r = tid; r < Mp; r += blockDim.x) {
+    const int v = D.st_worker[stage0 + r];
+    const int64_t k = D.st_comm[stage0 + r];
+    const int x = D.ready[pos + r];
+    const double stack = occ_k(v, k) / (double)WK_nthreads(D)[v];
+    D.st_task[stage0 + r] = x;
+    D.st_comm[stage0 + r] = 0;
+    D.st_start[stage0 + r] = stack + (double)0 / bw;
+    D.st_wsnbytes[stage0 + r] = WK_nbytes(D)[v];
+    D.st_route[stage0 + r] = (int8_t)ROUTE_ROOTISH_Q;
+    D.proc_on[x] = v;
+    if (D.state[x] == S_WAITING) atomicAdd((unsigned long long*)&D.g_relwait[D.group[x]], (unsigned long long)-1ll);
+    D.state[x] = S_PROCESSING;
+  }
+  // total_occupancy after pick r (the global dict with p counted r + 1 more, :1877)
+  int gi = -1;
+  for (int i = 0; i < c->g_plen; i++)
+    if (c->g_pfx[i] == p) gi = i;
+  auto total_occ = [&](int64_t r) {
+    double res = 0.0;
+    for (int i = 0; i < c->g_plen; i++)
+      res += prefix_duration(D, D.pdur_walk, c->g_pfx[i]) * (double)(c->g_pcnt[i] + (i == gi ? r + 1 : 0));
+    if (gi < 0) res += prefix_duration(D, D.pdur_walk, p) * (double)(r + 1);
+    return res + c->g_netocc / bw;
+  };
+  __syncthreads();
+  // the workers' end states, one thread each: check_idle_saturated of its last pick
+  // (walk_flags' rule), its dict / nproc, then idle_task_count (itc_check without the tree)
+  __shared__ long long f_didle, f_dsat, f_ditc, f_dslots;
+  if (tid == 0) f_didle = f_dsat = f_ditc = f_dslots = 0;
+  __syncthreads();
+  for (int v = tid; v < D.W; v += blockDim.x) {
+    const int32_t rl = last[v];
+    if (rl < 0) continue;
+    const int64_t npk = (int64_t)last_k[v] + 1;  // its picks: k = 0 .. the last one's
+    // dict and nproc after npk picks of prefix p (wdict_inc's append on the first)
+    int* pf = WK_pfx(D) + (size_t)v * PMAX;
+    int* pc = WK_pcnt(D) + (size_t)v * PMAX;
+    const int n = WK_plen(D)[v];
+    int hi = -1;
+    for (int i = 0; i < n; i++)
+      if (pf[i] == p) hi = i;
+    if (hi >= 0) {
+      pc[hi] += (int)npk;
+    } else {
+      pf[n] = p;
+      pc[n] = (int)npk;
+      WK_plen(D)[v] = n + 1;
+    }
+    WK_nproc(D)[v] += (int32_t)npk;
+    // idle / saturated of the last pick (walk_flags, with total_occupancy after pick rl)
+    {
+      const int64_t pn = WK_nproc(D)[v];
+      const int64_t nt = WK_nthreads(D)[v];
+      const uint8_t fl = WK_flags(D)[v];
+      const double occ = occ_k(v, 0);
+      bool idle = false, sat = false;
+      double avg = -1;
+      if (fl & WF_PAUSED) {
+      } else if (pn < nt) {
+        idle = true;
+      } else {
+        avg = total_occ(rl) / (double)D.total_nthreads;
+        idle = occ < (double)nt * avg / 2;
+      }
+      if (!idle && pn > nt && !(fl & WF_PAUSED)) {
+        const double pending = occ * (double)(pn - nt) / (double)(pn * nt);
+        if (0.4 < pending) {
+          if (avg < 0) avg = total_occ(rl) / (double)D.total_nthreads;
+          sat = pending > 1.9 * avg;
+        }
+      }
+      if (idle != ((fl & WF_IDLE) != 0)) atomicAdd((unsigned long long*)&f_didle, idle ? 1ull : (unsigned long long)-1ll);
+      if (sat != ((fl & WF_SAT) != 0)) atomicAdd((unsigned long long*)&f_dsat, sat ? 1ull : (unsigned long long)-1ll);
+      uint8_t nf = (fl & ~(WF_IDLE | WF_SAT)) | (idle ? WF_IDLE : 0) | (sat ? WF_SAT : 0);
+      // idle_task_count (itc_check)
+      const bool on = !worker_full(D, v) && !(nf & WF_PAUSED);
+      if (on != ((nf & WF_ITC) != 0)) {
+        nf = on ? (nf | WF_ITC) : (nf & ~WF_ITC);
+        atomicAdd((unsigned long long*)&f_ditc, on ? 1ull : (unsigned long long)-1ll);
+      }
+      const int64_t contrib = on ? task_slots_available(D, v) : 0;
+      const int64_t delta = contrib - WK_itcslots(D)[v];
+      if (delta) atomicAdd((unsigned long long*)&f_dslots, (unsigned long long)delta);
+      WK_itcslots(D)[v] = contrib;
+      WK_flags(D)[v] = nf;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    c->n_idle += f_didle;
+    c->n_sat += f_dsat;
+    c->n_itc += f_ditc;
+    c->itc_slots += f_dslots;
+    c->n_tasks += Mp;
+    if (gi >= 0) {
+      c->g_pcnt[gi] += Mp;
+    } else {
+      c->g_pfx[c->g_plen] = p;
+      c->g_pcnt[c->g_plen] = Mp;
+      c->g_plen++;
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  tree_rebuild_coop(D);
+  return Mp;
+}
+
 // update_graph, part 2: the tasks that went waiting -> processing, in priority order,
 // dispatched one by one (they read global state); once idle_task_count is empty every
 // further root-ish task is queued in bulk (:2761) — order-preserving.
@@ -2104,6 +2349,20 @@ __global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp,
       }
       bulk_done = true;
       continue;
+    }
+    // a run of root-ish tasks while idle_task_count has room: every pick at once
+    if (!D.sat_inf && c->n_itc > 0 && (D.tflags[D.ready[pos]] & TF_ROOTISH)) {
+      __shared__ int64_t s_stage;
+      if (threadIdx.x == 0) s_stage = stage_next;
+      __syncthreads();
+      const int64_t nf = ug_fill_rootish(D, pos, nr, s_stage, dur);
+      if (nf > 0) {
+        if (threadIdx.x == 0) {
+          stage_next += nf;
+          s_pos = pos + nf;
+        }
+        continue;
+      }
     }
     int64_t chunk = nr - pos < FL_MAX ? nr - pos : FL_MAX;
     // stop the chunk at the point where the bulk path takes over

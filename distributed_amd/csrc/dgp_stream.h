@@ -48,7 +48,7 @@
 namespace dgp {
 // the stream kernel's static LDS block (SLds), one allocation for both window builds in the
 // module-wide LDS struct, sized for the 64-slot one (each namespace checks its SLds fits)
-constexpr size_t ST_LDS_BYTES = 22624;
+constexpr size_t ST_LDS_BYTES = 22608;
 __shared__ __attribute__((aligned(16))) char st_lds_raw[ST_LDS_BYTES];
 // the per-worker LDS carve (dynamic LDS, sized at launch)
 extern __shared__ __attribute__((aligned(16))) char st_smem[];
@@ -73,15 +73,6 @@ __constant__ Dev c_dev;
 #endif
 #ifndef DGP_EXE_SLEEP
 #define DGP_EXE_SLEEP 1  // s_sleep units (64 clocks) between an idle executor's polls
-#endif
-#ifndef DGP_PARK
-// 1: a stimulus whose frontier candidates are still held after DGP_PARK_SPIN polls is parked
-// (its completing worker's state written back to LDS, the slot flagged in S.parkm) and the
-// executor claims other work; any executor resumes it once its candidates are free
-#define DGP_PARK 1
-#endif
-#ifndef DGP_PARK_SPIN
-#define DGP_PARK_SPIN 8  // polls (s_sleep 1 each) waited in place before parking
 #endif
 #ifndef DGP_EXE_PF
 #define DGP_EXE_PF 1  // an idle executor loads the descriptor of the oldest waiting stimulus ahead of its claim
@@ -167,9 +158,7 @@ static_assert((RS & (RS - 1)) == 0 && RS >= WIN && RS <= DR, "DGP_RS must be a p
 // of a single-worker run (exe_run).
 // F_RUNM (REG): F_SIMPLE and so is the stimulus just before it, on the same worker: a run
 // continues through it, so only the run-capable executor takes it
-// F_PQ1 (executor): a parked stimulus refills every open slot on resume (its claim's queue mode 1)
-enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16, F_SIMPLE = 32, F_RUNM = 64,
-                  F_PQ1 = 128 };
+enum : uint32_t { F_GLOBAL = 1, F_SELFREL = 2, F_EXACT = 4, F_TOUCHALL = 8, F_BADTOUCH = 16, F_SIMPLE = 32, F_RUNM = 64 };
 // K_COMPLETE_LR: the completion of a long-running task (its prefix count left the worker's and
 // the global dict at add_to_long_running :747-757; remove_from_processing :764-766)
 enum : int { K_COMPLETE = 1, K_PLACE = 2, K_COMPLETE_LR = 3 };
@@ -215,7 +204,6 @@ struct SCtl {
   int busy_exe;        // executors between claim and retirement
   SMask ready;         // slots whose stimulus may run
   SMask freem;         // slots not holding a registered stimulus (REG allocates, executors free)
-  SMask parkm;         // DGP_PARK: slots whose stimulus is parked before its frontier (no executor holds it)
   long long seq_pos, log_len, rec_len, walk_pos, bld_pos, pre_pos, reg_pos, reg_limit;
   long long qhead, qlen, n_tasks;
   long long stim_end;  // service mode: stimuli [seq_pos, stim_end) run in this launch
@@ -2461,14 +2449,9 @@ __device__ __forceinline__ DTab stim_durations(const Dev& D, SLds& L, const uint
 
 // a stimulus whose effects stay on the workers it registered. Returns false (nothing
 // changed) when it needs every earlier stimulus retired first (needs scan mode).
-// DGP_PARK: woke = WOKE_PARKED when the stimulus parked (slot in S.parkm); `resume` continues
-// a parked stimulus at its frontier: the completion, the releases and the release-only holders'
-// write-back were done before it parked, its completing worker's state is in LDS, and its
-// records so far are the one completion record (o.nrec = 1, o.npl = 0)
-constexpr int WOKE_PARKED = -3;
 template <bool LW>
 __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, const WPtr<LW>& P, int s, long long r, int qmode, bool exact, const uint4& E,
-                                                         int& woke, bool resume = false) {
+                                                         int& woke) {
   // WAITC: the candidate-only workers (touch entries > 0 flagged T_CAND) may still be held by
   // earlier stimuli when this one starts; their state is read after the wait before the frontier
   SCtl& S = L.c;
@@ -2493,7 +2476,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
 #endif
   // ---- capacity check of the needs tables this stimulus may grow
   const int tot_new = rl((int)E.w, 2);  // the frontier's dependency count (prefetcher)
-  if (!exact && !resume) {
+  if (!exact) {
     const int ntch = L.ntouch[s];
     bool bad = false;
     if (lane < ntch) {
@@ -2520,15 +2503,6 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   const int cj = tv & T_W;
   const bool candl = (tv & T_CAND) != 0;  // a holder of a frontier task's dependency
   const bool wc = WAITC && tl && lane > 0 && candl;  // candidate-only: read after the wait
-  const unsigned long long wm = ballot(tl && cj == w);
-  if (!wm) {
-    serr(S, SERR_INV, 700000000 + (int)r);
-    return true;
-  }
-  const int jw = __builtin_ctzll(wm);
-  const bool isw = lane == jw;
-  // a release-only holder (no frontier candidate) is final after the releases: released early
-  const bool ro = tl && !isw && !candl;
   int np = 0, nth = 1;
   WDict dj;
   dj.c = make_uint4(0, 0, 0, 0);
@@ -2536,14 +2510,21 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   dj.ord = 0;
   int64_t net = 0, nbj = 0;
   if (tl) nth = P.nthreads[cj];  // static while stimuli run
-  if (tl && !wc && !(resume && ro)) {
+  if (tl && !wc) {
     np = P.nproc[cj];
     dj = dict_load<LW>(P, cj);
     net = P.netocc[cj];
     nbj = P.nbytes[cj];
   }
   const int capw = P.cap[w];
-  uint32_t nl = resume ? 0u : line_load<LW>(P, w);
+  uint32_t nl = line_load<LW>(P, w);
+  const unsigned long long wm = ballot(tl && cj == w);
+  if (!wm) {
+    serr(S, SERR_INV, 700000000 + (int)r);
+    return true;
+  }
+  const int jw = __builtin_ctzll(wm);
+  const bool isw = lane == jw;
   double nbw = net_bw_of(net, D);            // this lane's netocc / bandwidth
   const bool nth1 = !ballot(tl && nth != 1);  // occ / 1.0 == occ: the division is skipped
   phase(16);
@@ -2553,9 +2534,6 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     trace_at(D, r, 22, (unsigned long long)(nf | kt << 8 | nrel << 16 | nt << 24));
     trace_at(D, r, 23, (unsigned long long)vload(&L.predc[s]));
   }
-  double occj = 0.0, stkj = 0.0;
-  bool released = false;  // this lane's worker was written back and released early
-  if (!resume) {
   // ------------------------------------------- completion: processing -> memory (:2366)
   int64_t dnet = 0;
   int64_t freed = 0;
@@ -2582,8 +2560,8 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   if (TR3 && lane == 0) TR(r, 10);
   // every lane's occupancy and stack time, kept current: only w (now) and each chosen
   // worker (after its commit) change during the stimulus
-  occj = occ_dict_r(dj, nbw, durv, D);
-  stkj = nth1 ? occj : occj / (double)nth;
+  double occj = occ_dict_r(dj, nbw, durv, D);
+  double stkj = nth1 ? occj : occj / (double)nth;
   o.rec(D, K_COMPLETE, w, p, dnet, mkd(rlu(dlo(occj), jw), rlu(dhi(occj), jw)), npw, t, dobs);
   // add_replica (:3148), then the releases popped before the frontier (LIFO, :3309-3314)
   if (isw) nbj += (flags & F_SELFREL) ? 0 : nbt;
@@ -2594,18 +2572,16 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
   }
   // a release-only holder (ws.nbytes of a released dependency; no frontier candidate) is final
   // now: written back and released before the frontier
-  if (ballot(ro)) {
-    if (ro) P.nbytes[cj] = nbj;
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (ro) release_worker<LW>(L, P, s, cj);
-    released = ro;
-  }
-  } else {  // resumed: w's state as it parked (the same fp64 values: pure functions of it)
-    o.nrec = 1;
-    occj = occ_dict_r(dj, nbw, durv, D);
-    stkj = nth1 ? occj : occj / (double)nth;
-    released = ro;
+  bool released = false;  // this lane's worker was written back and released early
+  {
+    const bool ro = tl && !isw && !candl;
+    if (ballot(ro)) {
+      if (ro) P.nbytes[cj] = nbj;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (ro) release_worker<LW>(L, P, s, cj);
+      released = ro;
+    }
   }
   if (TR3 && lane == 0) TR(r, 11);
   if (WAITC && ballot(wc)) {
@@ -2613,30 +2589,7 @@ __device__ __attribute__((always_inline)) bool exe_local(const Dev& D, SLds& L, 
     // counts predc down), then their state, with this stimulus' releases applied
     if (vload(&L.predc[s]) != 0) {
       if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(1);
-      int spins = 0;
-      while (vload(&L.predc[s]) != 0) {
-        if (DGP_PARK && !exact && qmode <= 1 && ++spins > DGP_PARK_SPIN) {
-          // park: w (the only lane this stimulus still holds in registers: every other
-          // non-candidate lane was released above) back into LDS, then the slot in parkm.
-          // predc only counts down from here, so the executor that finds it 0 resumes it
-          if (isw) {
-            using U4 = typename WPtr<LW>::template P<Q4>;
-            P.nproc[cj] = np;
-            st4(ascast<U4>(P.pcnt + (size_t)cj * PD), dj.c);
-            st4(ascast<U4>(P.pcnt + (size_t)cj * PD + 4), dj.c1);
-            P.plen[cj] = dj.ord;
-            P.netocc[cj] = net;
-            P.nbytes[cj] = nbj;
-          }
-          if (lane == 0 && qmode == 1) atomicOr(&L.flags[s], F_PQ1);
-          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the state above is in LDS
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-          if (lane == 0) atomicOr(&S.parkm, 1ull << s);
-          woke = WOKE_PARKED;
-          return true;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
+      while (vload(&L.predc[s]) != 0) __builtin_amdgcn_s_sleep(1);
       if (DGP_EXE_PRIO) __builtin_amdgcn_s_setprio(3);
     }
     lds_fence();
@@ -3973,8 +3926,7 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
   while (true) {
     if (vload(&S.stop)) break;
     const SMask m = vload(&S.ready);
-    const SMask pk = DGP_PARK ? vload(&S.parkm) : 0ull;  // parked: resumable once predc is 0
-    if (!m && !pk) {
+    if (!m) {
       const unsigned long long n = mclk();  // 28: executor idle, nothing ready
       idle28 += n - t_idle;
       t_idle = n;
@@ -3996,43 +3948,23 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
     // the ready slots in stimulus order (oldest first): lane i holds slot i's key
     const long long sp = vload(&S.seq_pos);
     const bool rdl = lane < WIN && ((m >> lane) & 1ull);
-    const bool pkl = DGP_PARK && lane < WIN && ((pk >> lane) & 1ull) && vload(&L.predc[lane]) == 0;
-    const long long rsl = (rdl || pkl) ? vload(&L.sid[lane]) : 0;
+    const long long rsl = rdl ? vload(&L.sid[lane]) : 0;
     const uint32_t fsl = rdl ? vload(&L.flags[lane]) : 0u;
     // WAITC: a stimulus whose candidates are final first (it never waits in place); the
     // global-capable executor takes no other
     const bool pcl = WAITC && rdl && vload(&L.predc[lane]) != 0;
     const bool pskip = pcl && (G || rsl - sp >= WAITC_AHEAD);
-    unsigned key = (rdl && !pskip) || pkl ? (unsigned)((pcl ? 1u << 31 : 0u) | ((rsl - sp) << 6) | lane) : ~0u;  // r - sp < RS
+    unsigned key = rdl && !pskip ? (unsigned)((pcl ? 1u << 31 : 0u) | ((rsl - sp) << 6) | lane) : ~0u;  // r - sp < RS
     int cs = -1, cq = 0;
     long long cr = -1;
     uint32_t cf = 0;
-    bool cex = false, cres = false;
+    bool cex = false;
     uint4 E = make_uint4(0, 0, 0, 0);
     while (true) {
       const unsigned kmin = wmin_u32(key);
       if (kmin == ~0u) break;
       const int s = (int)(kmin & 63u);
       if (lane == s) key = ~0u;  // tried
-      if (DGP_PARK && rlu(pkl ? 1u : 0u, s)) {  // a parked stimulus whose candidates are free: resume it
-        const long long rs = (long long)rl64((uint64_t)rsl, s);
-        E = lane < NE ? D.desc[(size_t)(rs & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
-        SMask old = 0;
-        if (lane == 0) old = atomicAnd(&S.parkm, ~(1ull << s));
-        old = rl64(old, 0);
-        if (!((old >> s) & 1ull)) continue;
-        lds_fence();
-        const long long r = vload(&L.sid[s]);  // (a parked slot is not re-registered: r == rs)
-        if (r != rs) E = lane < NE ? D.desc[(size_t)(r & (DR - 1)) * NE + lane] : make_uint4(0, 0, 0, 0);
-        const uint32_t fl = vload(&L.flags[s]);
-        cs = s;
-        cr = r;
-        cf = fl;
-        cq = (fl & F_PQ1) ? 1 : 0;
-        cex = false;
-        cres = true;
-        break;
-      }
       if (!G && (rlu(fsl, s) & (F_GLOBAL | F_RUNM))) continue;  // left to the global-capable executor
       // WAITC: the global-capable executor never waits in place (it takes only stimuli whose
       // candidates are final), so the oldest stimulus always finds an executor that runs it
@@ -4100,11 +4032,11 @@ __device__ __attribute__((always_inline)) void role_exe(const Dev& D, SLds& L, c
 #else
       PROF(if (lane == 0) S.prof[9]++);
 #endif
-    } else if (G && !cres && (cf & F_SIMPLE) && cq == 0 && !cex && exe_run_entry<LW>(cs, cr, E)) {
+    } else if (G && (cf & F_SIMPLE) && cq == 0 && !cex && exe_run_entry<LW>(cs, cr, E)) {
       // a run of single-worker completions, back to back (only this executor calls out of line)
     } else {
       int wk = -1;
-      const int rc = exe_local<LW>(D, L, P, cs, cr, cq, cex, E, wk, cres) ? wk : -2;  // inlined: the common case
+      const int rc = exe_local<LW>(D, L, P, cs, cr, cq, cex, E, wk) ? wk : -2;  // inlined: the common case
       if (rc == -2 && lane == 0) {
         atomicOr(&L.flags[cs], F_EXACT);
         atomicOr(&S.ready, 1ull << cs);
@@ -4214,7 +4146,6 @@ __global__ void __launch_bounds__(SCTA) k_stream(long long max_rounds, int snaps
     S.global_pending = 0;
     S.busy_exe = 0;
     S.ready = 0;
-    S.parkm = 0;
     S.freem = ~0ull >> (64 - WIN);
     S.seq_pos = pos->seq;
     S.log_len = (long long)c->n_placed;

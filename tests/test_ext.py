@@ -409,3 +409,27 @@ def test_confirmed_steal_moves_the_task_on_the_engine():
     ts.processing_on = w0
     asyncio.run(sched.stream_handlers["steal-response"](key="x", state="executing", stimulus_id="s2"))
     assert moved == [(3, 1)] and not ext.active and "rescheduled" in ext.reason
+
+
+def test_drop_ins_install_from_dask_config():
+    """distributed.scheduler.gpu-placement.* (distributed_amd/config.py) in a real reference
+    Scheduler, started: off by default (the reference's extensions untouched); installed by
+    the ``distributed_amd.preload`` preload or by ``scheduler_extensions()`` as
+    ``extensions=`` (scheduler.py:3890-3897's rule: GPUWorkStealing replaces WorkStealing,
+    and no stealing at all when distributed.scheduler.work-stealing is off)."""
+    env = dict(os.environ, PYTHONHASHSEED="0")
+    env.pop("PYTHONPATH", None)
+    out = subprocess.run([PY39, os.path.join(REPO, "tests", "config_driver.py")], capture_output=True, text=True,
+                         env=env, timeout=600, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = {r["case"]: r for r in (json.loads(x) for x in out.stdout.splitlines() if x.startswith("{"))}
+    d = res["default"]
+    assert d["stealing"] == "WorkStealing" and d["placement"] == "NoneType" and "gpu-placement" not in d["extensions"]
+    assert d["task_finished"] == "Scheduler.handle_task_finished"
+    for c in ("preload", "extensions"):
+        r = res[c]
+        assert r["stealing"] == "GPUWorkStealing" and r["placement"] == "GPUPlacementExtension", r
+        assert "WorkStealing" not in r["plugins"] and "GPUWorkStealing" in r["plugins"], r
+        assert r["stealing_callback"] and r["task_finished"] == "GPUPlacementExtension.handle_task_finished", r
+    n = res["no_stealing"]
+    assert n["stealing"] is None and not n["stealing_callback"] and n["placement"] == "GPUPlacementExtension", n
