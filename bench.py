@@ -109,8 +109,10 @@ def latency_bound(g: dict, out: dict, link_us: float, achieved_ms: float) -> dic
     depth, touches = conflict_depth(g, out, 0)
     min_ms = depth * link_us / 1e3
     return {"bound": "latency", "critical_path_links": depth, "stimuli": int(len(out["pl_task"])),
+            "average_parallelism": round(len(out["pl_task"]) / max(1, depth), 2),
             "touches": touches, "link_us": round(link_us, 3), "min_ms": round(min_ms, 3),
-            "achieved_ms": round(achieved_ms, 3), "frac": round(min_ms / achieved_ms, 4)}
+            "achieved_ms": round(achieved_ms, 3), "achieved_us_per_link": round(1e3 * achieved_ms / max(1, depth), 3),
+            "frac": round(min_ms / achieved_ms, 4)}
 
 
 def steal_leg(eng, args, world: int, dist=None, barrier=None) -> dict:
@@ -501,6 +503,10 @@ def c5_leg(eng_cls, local: int, args, dist, barrier) -> dict:
         if ref["n_map"] == args.c5_map and ref["n_workers"] == args.c5_workers:
             leg["parity"] = graphs.placement_digest(out) == ref["digest"]
     eng.close()
+    if rank == 0 and world == 1 and not args.no_latency:
+        # the chain of this replay (dgp_conflict_depth over its placement log) x the link of
+        # the global worker-state path (the star at 16,384 workers)
+        leg["latency_bound"] = latency_bound(g, out, link_latency_us(eng_cls, local, args.c5_workers), dt * 1e3)
     if int(os.environ.get("RANK", "0")) == 0 and world == 1 and not args.no_cpu_baseline and args.c5_cpu_map > 0:
         # a bounded sample on this box: the same map + tree-reduce shape and worker count,
         # fewer map tasks (the full 10M replay takes the 1-core port minutes). The port's

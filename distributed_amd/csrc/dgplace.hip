@@ -1614,8 +1614,6 @@ int dgp_add_worker_at(dgp_engine* e, int32_t nthreads, int32_t running, int32_t 
     if (ps.pre > ps.seq || ps.walk != ps.rec_len)
       return fail(e, DGP_E_STATE, "dgp_add_worker_at: the stream engine has prefetched stimuli or unfolded records");
   }
-  if (position < e->D.W && e->snap_rounds > 0)  // [rounds][W] snapshot columns would belong to the wrong worker
-    return fail(e, DGP_E_STATE, "dgp_add_worker_at: a mid-list insertion with replay snapshots recorded");
   namespace S = dgp::st;
   dgp::Dev& D = e->D;
   const size_t W0 = D.W, W1 = W0 + 1;
@@ -1655,7 +1653,11 @@ int dgp_add_worker_at(dgp_engine* e, int32_t nthreads, int32_t running, int32_t 
   }
   const int32_t WB = (int32_t)((W1 + 63) / 64);
   if (WB != D.WB) rc |= restride(e, &D.holders, (size_t)D.N, (size_t)D.WB, (size_t)WB, e->graph_allocs);
-  if (e->snap_rounds > 0) {  // [rounds][W]: earlier rounds read 0 for the new worker
+  // [rounds][W] snapshots: a round's row holds the worker indices of its time (the SortedDict
+  // rank then), padded with zeros to the current width -- the layout the reference-generated
+  // fixtures record (tests/golden/gen_service.py, add_worker streams) -- so the new column is
+  // appended, not inserted at `position`
+  if (e->snap_rounds > 0) {
     const size_t R = (size_t)e->snap_rounds;
     rc |= restride(e, &D.snap_occ, R, W0, W1, A);
     rc |= restride(e, &D.snap_nbytes, R, W0, W1, A);

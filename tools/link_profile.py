@@ -1,6 +1,6 @@
 """Per-link breakdown of the C2 replay's critical chain (GPU, a DGP_TRACE=3 build):
     tools/build_variants.sh trace3 "-DDGP_TRACE=3"
-    DGP_LIB=tools/_var/lib_trace3.so python tools/link_profile.py [lo] [n] [c3] [--out file.json]
+    DGP_LIB=tools/_var/lib_trace3.so python tools/link_profile.py [lo] [n] [c3|c5] [--out file.json]
 
 Every traced stimulus records its executor's phases (s_memtime ticks) and which earlier
 stimulus' release made it ready (its completing worker / release holders free: `pred` 0)
@@ -27,7 +27,9 @@ from distributed_amd import graphs  # noqa: E402
 from distributed_amd.engine import PlacementEngine  # noqa: E402
 
 c3 = "c3" in args
-g = graphs.shuffle_graph(66_666, 512) if c3 else graphs.random_dag(1_000_000, 1024, seed=0)
+c5 = "c5" in args  # C5-shaped: map 1M + tree-reduce on 16,384 workers (the global worker-state path)
+g = (graphs.shuffle_graph(66_666, 512) if c3 else graphs.map_tree_reduce(1_000_000, 16_384) if c5
+     else graphs.random_dag(1_000_000, 1024, seed=0))
 e = PlacementEngine(0, window=32)
 e.load(g, {"saturation": 1.1})
 e.reset()
@@ -75,8 +77,9 @@ res["ready_to_claim"] = pct(rc[ok])
 SUB = [(14, 24, "place stores"), (24, 25, "line_load cb"), (25, 26, "needs_inc"), (26, 27, "line_store+dict_add"),
        (27, 28, "net_bw + ballot"), (28, 29, "occ_dict_r"), (29, 15, "rec stores")]
 sel = (L[:, 24] > 0) & (L[:, 29] > 0) & (nf > 0)
-print("  first commit, split:")
-for a, b, nm in SUB:
+if sel.any():
+    print("  first commit, split:")
+for a, b, nm in (SUB if sel.any() else ()):  # (only the commit-split probe build records these)
     d = L[sel, b] - L[sel, a]
     res["phases"]["commit:" + nm] = pct(d)
     print(f"    {nm:22s} mean {d.mean():8.0f} p50 {np.percentile(d, 50):8.0f}")
