@@ -44,6 +44,7 @@ SIGNATURES = {
     "dgp_add_worker_at": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, _P]),
     "dgp_add_graph": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P, _P]),
     "dgp_set_priorities": (C.c_int, [_P, _P]),
+    "dgp_remap_prefixes": (C.c_int, [_P, C.c_int32, _P, _P]),
     "dgp_graph_stimulus": (C.c_int, [_P, _P]),
     "dgp_add_graph_deferred": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P]),
     "dgp_snapshot": (C.c_int, [_P]),
@@ -88,7 +89,7 @@ SIGNATURES = {
                                    _P, _P, _P]),
 }
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 _libs: dict = {}
 
 

@@ -1791,6 +1791,58 @@ int dgp_add_graph(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, const in
                         n_groups, wanted, rootish_override, n_new_placements, false);
 }
 
+// (ABI 20) The task prefix table anew: the stream engine carries at most PX prefixes, a
+// long-lived scheduler meets more over its session (TaskPrefix objects are per key_split
+// name, scheduler.py:923-1031). The caller gives every task a slot in a table of
+// n_prefixes live prefixes (the prefixes whose tasks are released / waiting / queued /
+// processing / no-worker or in a worker's or the global task_prefix_count, :733-784,
+// :1884-1903; a task of a prefix left out is in memory / erred / forgotten and its slot is
+// never read) with each slot's default duration; the per-prefix state and every structure
+// holding prefix ids (the workers' and the global dicts, the durations, the queue) then come
+// from dgp_sync_workers / dgp_sync_globals (pending until dgp_sync_globals).
+int dgp_remap_prefixes(dgp_engine* e, int32_t n_prefixes, const int32_t* task_prefix,
+                       const double* prefix_default_duration) {
+  if (int rc_ = resident_stop(e)) return rc_;
+  if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");
+  if (e->mode == 1) return fail(e, DGP_E_STATE, "engine advanced by a replay (dgp_run_rounds); dgp_reset first");
+  if (e->posted) return fail(e, DGP_E_STATE, "a posted task-finished batch: dgp_tasks_finished_wait first");
+  dgp::Dev& D = e->D;
+  if (n_prefixes <= 0 || n_prefixes > dgp::st::PX || !task_prefix || !prefix_default_duration)
+    return fail(e, DGP_E_ARG, "dgp_remap_prefixes: 1 .. 32 prefixes, every task's slot and each slot's default");
+  for (int64_t t = 0; t < D.N; t++)
+    if (task_prefix[t] < 0 || task_prefix[t] >= n_prefixes) return fail(e, DGP_E_ARG, "dgp_remap_prefixes: slot out of range");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  {  // no descriptor, duration row or record of the old numbering may be pending
+    dgp::st::Pos ps;
+    HIPCHK(e, hipMemcpy(&ps, D.pos, sizeof ps, hipMemcpyDeviceToHost));
+    if (ps.pre > ps.seq || ps.walk != ps.rec_len)
+      return fail(e, DGP_E_STATE, "dgp_remap_prefixes: the stream engine has prefetched stimuli or unfolded records");
+  }
+  if (n_prefixes > D.P) {  // per-prefix arrays one slot each (the round engine's table [N][P] too)
+    int rc = 0;
+    rc |= dalloc(e, &D.pdur_cur, n_prefixes, e->graph_allocs);
+    rc |= dalloc(e, &D.pdur_walk, n_prefixes, e->graph_allocs);
+    rc |= dalloc(e, &D.pdur_pre, n_prefixes, e->graph_allocs);
+    rc |= dalloc(e, &D.pmaxexec, n_prefixes, e->graph_allocs);
+    rc |= dalloc(e, &D.durv, (size_t)D.N * n_prefixes, e->graph_allocs);
+    if (rc) return rc;
+  }
+  HIPCHK(e, hipMemcpy(const_cast<int32_t*>(D.prefix), task_prefix, (size_t)D.N * 4, hipMemcpyHostToDevice));
+  e->h_prefix.assign(task_prefix, task_prefix + D.N);
+  e->prefix_defaults.assign(prefix_default_duration, prefix_default_duration + n_prefixes);
+  // placeholders until dgp_sync_globals brings each slot's TaskPrefix state
+  std::vector<double> mx(n_prefixes, -1.0);
+  for (double* p : {D.pdur_cur, D.pdur_walk, D.pdur_pre})
+    HIPCHK(e, hipMemcpy(p, prefix_default_duration, (size_t)n_prefixes * 8, hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(D.pmaxexec, mx.data(), (size_t)n_prefixes * 8, hipMemcpyHostToDevice));
+  D.P = n_prefixes;
+  if (int rc = sync_dev(e)) return rc;
+  e->pending_resync = true;  // the dicts hold the old numbering: dgp_sync_workers / _globals next
+  e->mode = 2;
+  return 0;
+}
+
 int dgp_set_priorities(dgp_engine* e, const int64_t* prio) {
   if (int rc_ = resident_stop(e)) return rc_;
   if (!e || !e->graph_done) return fail(e, DGP_E_STATE, "dgp_update_graph first");

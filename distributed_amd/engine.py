@@ -392,6 +392,16 @@ class PlacementEngine:
             raise ValueError(f"set_priorities: {len(p)} priorities for {self.n_tasks} tasks")
         self._check(self.lib.dgp_set_priorities(self.h, _ptr(p)), "dgp_set_priorities")
 
+    def remap_prefixes(self, task_prefix, prefix_default_duration):
+        """The task prefix table anew (dgp_remap_prefixes): every task's slot in a table of
+        at most 32 live prefixes and each slot's default duration; ``sync(workers=...,
+        globals_=...)`` in the new numbering must follow before any other stimulus."""
+        t = np.ascontiguousarray(task_prefix, np.int32).reshape(-1)
+        d = np.ascontiguousarray(prefix_default_duration, np.float64).reshape(-1)
+        if len(t) != self.n_tasks:
+            raise ValueError(f"remap_prefixes: {len(t)} slots for {self.n_tasks} tasks")
+        self._check(self.lib.dgp_remap_prefixes(self.h, len(d), _ptr(t), _ptr(d)), "dgp_remap_prefixes")
+
     # --------------------------------------------------------- service events
     @staticmethod
     def _arr(x, dt):

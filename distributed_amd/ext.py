@@ -58,7 +58,7 @@ from operator import attrgetter, lt, truth
 
 import numpy as np
 
-from . import sync
+from . import prefixes, sync
 
 try:  # the plugin base class when dask.distributed is importable; plain object otherwise
     from distributed.diagnostics.plugin import SchedulerPlugin
@@ -320,7 +320,15 @@ class GPUPlacementExtension(SchedulerPlugin):
         self.task_index: dict = {}
         self.workers: list = []   # engine worker index -> address
         self.worker_index: dict = {}
-        self.prefix_index: dict = {}
+        self.prefix_index: dict = {}  # prefix name -> the engine's slot (at most prefixes.PX live at once)
+        # every engine task's prefix (an index into pnames, stable for the session), each
+        # name's default duration, and the tasks whose device slot is a placeholder since a
+        # compaction left their (then dead) prefix out (prefixes.py)
+        self.pnames: list = []
+        self.pname_id: dict = {}
+        self.pname_dur: dict = {}
+        self.task_pname = np.zeros(0, np.int32)
+        self._stale: set = set()
         self.dev_run: dict = {}   # key -> placement-log position of its current placement
         self.pending: deque = deque()  # (task index, worker index) in placement order
         self.n_fetched = 0
@@ -599,6 +607,8 @@ class GPUPlacementExtension(SchedulerPlugin):
             return False  # a drained worker: no transition (the plugin hook follows it)
         ti = self.task_index
         if (any(ts.key not in ti for ts in proc) or any(ts.who_has == {ws} and ts.key not in ti for ts in held)
+                or any(ts.who_has == {ws} and (ts.prefix.name not in self.prefix_index or ti[ts.key] in self._stale)
+                       for ts in held)
                 or not self._loss_supported(s, ws, proc, held, safe)):
             self.stats["losses_left_to_scheduler"] += 1
             return False
@@ -937,6 +947,8 @@ class GPUPlacementExtension(SchedulerPlugin):
             cols = list(zip(*pl)) if pl else [[]] * 6
             placements = dict(zip(("task", "worker", "comm", "start", "wsnbytes", "route"), cols))
             keys = self.keys if self._dirty_all else [k for k in self._dirty if k in self.task_index]
+            if hasattr(self.engine, "remap_prefixes") and not self._prefixes_current(keys):
+                self._compact_prefixes([], resync=False)  # the rows below come in the new numbering
             widx = {a: i for i, a in enumerate(self.workers)}
             tasks = sync.task_rows(s, keys, self.task_index, widx)
             workers = sync.worker_rows(s, self.workers, self.prefix_index, self.task_index)
@@ -1220,6 +1232,7 @@ class GPUPlacementExtension(SchedulerPlugin):
                 self.prefix_index = {nm: i for i, nm in enumerate(g["prefix_names"])}
                 self.group_index = {nm: i for i, nm in enumerate(g["group_names"])}
                 self.prefix_dur = list(g["prefix_default_dur"])
+                self._note_prefixes(g)
                 self.group_prefix = list(g["group_prefix"])
                 self.max_priority = prio_[-1]
                 self.prio_of = prio_  # engine index -> TaskState.priority
@@ -1244,6 +1257,57 @@ class GPUPlacementExtension(SchedulerPlugin):
                                 self.task_index.keys() if len(keys_) == len(self.task_index) else set(keys_))
         except Exception as e:  # plugin errors are logged, not raised (scheduler.py:4652-4653)
             self.fallback(f"update_graph: {e}")
+
+    def _note_prefixes(self, g):
+        """Each new engine task's prefix name (session-stable ids) and the names' defaults."""
+        ids = []
+        for nm, d in zip(g["prefix_names"], g["prefix_default_dur"]):
+            if nm not in self.pname_id:
+                self.pname_id[nm] = len(self.pnames)
+                self.pnames.append(nm)
+                self.pname_dur[nm] = float(d)
+            ids.append(self.pname_id[nm])
+        lut = np.array(ids or [0], np.int32)
+        self.task_pname = np.concatenate([self.task_pname, lut[np.asarray(g["prefix_id"], np.int64)]]).astype(np.int32)
+
+    def _compact_prefixes(self, extra, resync: bool):
+        """The engine's prefix table compacted to the live prefixes + ``extra``
+        (prefixes.py): dgp_remap_prefixes, then (``resync``) the workers' and global rows in
+        the new numbering; otherwise the caller's resync follows."""
+        s = self.scheduler
+        table = prefixes.compacted(self.prefix_index, prefixes.live_prefixes(s), extra)
+        if table is None:
+            raise NotImplementedError(f"more than {prefixes.PX} live task prefixes")
+        old_names = sorted(self.prefix_index, key=self.prefix_index.get)
+        slots, stale = prefixes.task_slots(self.task_pname, self.pnames, table)
+        names = sorted(table, key=table.get)
+        defaults = [self.pname_dur.get(nm, -1.0) for nm in names]
+        self.engine.remap_prefixes(slots, defaults)
+        self.prefix_index = table
+        self.prefix_dur = defaults
+        self.group_prefix = [table.get(old_names[p], 0) if 0 <= p < len(old_names) else 0 for p in self.group_prefix]
+        self._stale = set(stale.tolist())
+        self.stats["prefix_compactions"] += 1
+        if resync:
+            widx = {a: i for i, a in enumerate(self.workers)}
+            workers = sync.worker_rows(s, self.workers, self.prefix_index, self.task_index)
+            gnames = sorted(self.group_index, key=self.group_index.get)
+            glob = sync.global_rows(s, names, self.prefix_dur, gnames, self.task_index, widx)
+            self.engine.sync(None, None, workers, glob)
+
+    def _prefixes_current(self, keys) -> bool:
+        """Every live prefix has a slot and no live task among ``keys`` (the resync's) holds a
+        placeholder slot (its prefix was dead at a compaction, then recomputed)."""
+        s = self.scheduler
+        if not set(prefixes.live_prefixes(s)) <= set(self.prefix_index):
+            return False
+        if self._stale:
+            ti = self.task_index
+            for k in keys:
+                ts = s.tasks.get(k)
+                if ts is not None and ti[k] in self._stale and ts.state in prefixes.LIVE_STATES:
+                    return False
+        return True
 
     def _remember_inputs(self, g, keys_):
         """What the engine holds of each uploaded task's _rootish and restrictions."""
@@ -1275,6 +1339,13 @@ class GPUPlacementExtension(SchedulerPlugin):
         outranks = prio_[0] <= self.max_priority
         if outranks and not hasattr(self.engine, "set_priorities"):
             raise NotImplementedError("a later graph whose tasks do not all follow the earlier ones in priority")
+        if len(self.prefix_index) + sum(nm not in self.prefix_index for nm in g["prefix_names"]) > prefixes.PX:
+            # more task prefixes over the session than the engine's table: the live ones and
+            # this graph's in a compacted table (dgp_remap_prefixes + the dicts' resync)
+            self._end_of_stimulus("the previous stimulus")
+            if not self.active:
+                return None
+            self._compact_prefixes(list(g["prefix_names"]), resync=True)
         pmap = np.zeros(len(g["prefix_names"]), np.int32)
         for i, nm in enumerate(g["prefix_names"]):
             if nm not in self.prefix_index:
@@ -1301,6 +1372,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         else:
             self.engine.add_graph(g2)
         self.keys = self.keys + keys_
+        self._note_prefixes(g)
         self.task_index.update(zip(keys_, range(n0, n0 + len(keys_))))
         self.prio_of = self.prio_of + prio_
         if outranks:  # every task's rank in the merged order (forgotten tasks keep theirs)

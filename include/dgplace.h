@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 19
+#define DGP_ABI_VERSION 20
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -295,6 +295,19 @@ int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr,
  * stimulus and the caller resynchronises as before. Replaces the scheduler's Python for that
  * stimulus (scheduler.py:4600-4653). */
 int dgp_graph_stimulus(dgp_engine* e, int64_t* n_new_placements);
+
+/* (ABI 20) The task prefix table anew (the stream engine carries at most 32 prefixes; a
+ * long-lived scheduler meets more: TaskPrefix objects per key_split name, scheduler.py:923-1031).
+ * task_prefix: every task's slot in a table of n_prefixes (<= 32) live prefixes -- those of
+ * the tasks released / waiting / queued / processing / no-worker and of the workers' and
+ * the global task_prefix_count (:733-784, :1884-1903); a task of a prefix left out is in
+ * memory / erred / forgotten and the engine never reads its slot. prefix_default_duration:
+ * each slot's default-task-durations entry (-1: none). Replaces the PX-prefix ceiling of
+ * dgp_add_graph for a session: the caller compacts the table when a later graph would pass
+ * it. Pending until dgp_sync_workers + dgp_sync_globals bring the dicts, durations and
+ * queue in the new numbering (as after dgp_add_graph_deferred). Between stimuli. */
+int dgp_remap_prefixes(dgp_engine* e, int32_t n_prefixes, const int32_t* task_prefix,
+                       const double* prefix_default_duration);
 
 /* (ABI 14) Every task's priority anew (n_tasks entries, unique and topological): a later
  * graph submitted with a user priority that outranks earlier tasks (Scheduler.update_graph's

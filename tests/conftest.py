@@ -18,7 +18,7 @@ def golden_files():
     """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
                   and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcgdep_", "svcev_",
-                                            "svcrs_", "svcrt_", "svcwl_", "svcp2p_", "svcgrst_", "svcgprio_")))
+                                            "svcrs_", "svcrt_", "svcwl_", "svcp2p_", "svcgrst_", "svcgprio_", "svcpfx_")))
 
 
 def svc_second_graph_files():

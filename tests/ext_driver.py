@@ -837,6 +837,124 @@ def run_second_graph(name, resync=False):
                 graph_stimuli_on_device=ext.stats["graph_stimuli_on_device"])
 
 
+def run_prefixes(name):
+    """A ``svcpfx_*`` stream (gen_service.py prefixes): six later graphs, each with task
+    prefixes of its own (75 over the stream), submitted through the plugins' update_graph
+    hook. Where a graph would pass the engine's table (prefixes.PX) the extension compacts it
+    (``_compact_prefixes``: dgp_remap_prefixes, then the dicts' resync) and stays active:
+    every placement comes from the engine, validate=True re-derives each, and the remaps and
+    resync rows equal the ones the generator recorded (the same prefixes.py on the reference
+    state)."""
+    import operator
+
+    path = os.path.join(HERE, "golden", name)
+    g, cfg, exp, meta = load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    g["keys"] = None
+    sat = cfg["saturation"]
+    sat = float("inf") if sat == "inf" else float(sat)
+    dask.config.set({"distributed.scheduler.worker-saturation": sat})
+    cfg = dict(cfg, saturation=sat)
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    S = type(s)
+    S.stimulus_task_finished = Scheduler.stimulus_task_finished
+    S.handle_task_finished = Scheduler.handle_task_finished
+    S.validate_key = lambda self, key, ts=None: None
+    S.send_all = lambda self, client_msgs, worker_msgs: None
+    fkeys = [ts.key for ts in tss]
+    eng = EventEngine(exp, fkeys)
+    ext = GPUPlacementExtension(s, engine_factory=lambda: eng, validate=True)
+    eng.ext = ext
+    s.stream_handlers = {}
+    ext._install()
+    priority = {ts.key: ts.priority for ts in tss}
+    recs = {ts.key: "waiting" for ts in sorted(tss, key=lambda t: t.priority, reverse=True)}
+    ext.update_graph(s, client="client-0", keys=set(priority), tasks=list(priority), annotations={},
+                     priority=priority, dependencies={})
+    assert ext.active, ext.reason
+    s._transitions(recs, {}, {}, "update-graph")
+    cs = s.clients["client-0"]
+    K = int(z["gk_n"])
+    at = {int(z[f"g{k}_msg"]): k for k in range(K)}
+    remaps_seen = 0
+    for i, (t, w) in enumerate(zip(z["msg_task"].tolist(), z["msg_worker"].tolist())):
+        if i in at:
+            k = at[i]
+            p = f"g{k}_"
+            gk = dict(prefix_id=z[p + "prefix_local"], group_id=z[p + "group_local"],
+                      prefix_names=z[p + "prefix_names"].tolist(), group_names=z[p + "group_names"].tolist(),
+                      n_tasks=len(z[p + "prio"]))
+            keys_k = G.make_keys(gk)
+            base = len(tss)
+            new = []
+            for j, key in enumerate(keys_k):
+                ts = s.new_task(key, (operator.add, (), {}), "released")
+                tidx[key] = base + j
+                ts.priority = (0, 2 + k, int(z[p + "prio"][j]))
+                new.append(ts)
+            dp, di = z[p + "dep_ptr"], z[p + "dep_idx"]
+            for j, ts in enumerate(new):
+                for d in di[dp[j]:dp[j + 1]]:
+                    ts.add_dependency(new[int(d)])
+                if z[p + "wanted"][j]:
+                    ts.who_wants = {cs}
+                    cs.wants_what.add(ts)
+            eng.fkeys.extend(keys_k)
+            tss.extend(new)
+            n_calls = len(eng.calls)
+            prio_k = {ts.key: ts.priority for ts in new}
+            ext.update_graph(s, client="client-0", keys=set(prio_k), tasks=list(prio_k), annotations={},
+                             priority=prio_k, dependencies={})
+            assert ext.active, ext.reason
+            rm = [c for c in eng.calls[n_calls:] if c[0] == "remap"]
+            if p + "remap_slots" in z.files:  # the generator's remap and resync rows, the extension's too
+                assert len(rm) == 1, eng.calls[n_calls:]
+                remaps_seen += 1
+                _, slots, defaults = rm[0]
+                assert np.array_equal(slots, z[p + "remap_slots"]), k
+                assert np.array_equal(np.asarray(defaults), z[p + "remap_defaults"]), k
+                rows = [c for c in eng.calls[n_calls:] if c[0] == "sync_rows"]
+                assert len(rows) == 1
+                j0 = int(z[p + "remap_dump"])
+                # group-indexed rows by group name (the fixture numbers groups in its graphs'
+                # order, the extension in the order its ingestion meets them)
+                fx_groups = list(meta["group_names"]) + [nm for kk in range(k) for nm in z[f"g{kk}_group_names"].tolist()]
+                ext_groups = sorted(ext.group_index, key=ext.group_index.get)
+                for part, got in (("workers", rows[0][1]), ("globals", rows[0][2])):
+                    for fl, v in got.items():
+                        pp = z[f"sync_{part}_{fl}_ptr"]
+                        want = z[f"sync_{part}_{fl}"][pp[j0]:pp[j0 + 1]]
+                        v = np.atleast_1d(np.asarray(v))
+                        if fl.startswith("group_"):
+                            eg = ext_groups[:len(v)]  # (the graph's own groups join after the resync)
+                            assert len(eg) == len(fx_groups) == len(want), (k, fl)
+                            v = dict(zip(eg, v.tolist()))
+                            want = dict(zip(fx_groups, want.tolist()))
+                            assert v == want, (k, part, fl)
+                        else:
+                            assert np.array_equal(v, want), (k, part, fl)
+            else:
+                assert not rm, (k, rm)
+            s._transitions({ts.key: "waiting" for ts in sorted(new, key=lambda x: x.priority, reverse=True)}, {}, {},
+                           f"update-graph-{k + 2}")
+        ts = tss[t]
+        s.stream_handlers["task-finished"](
+            key=ts.key, worker=ts.processing_on.address, stimulus_id=f"tf-{t}", run_id=ts.run_id,
+            nbytes=int(z["msg_nbytes"][i]), type=None, typename="int", metadata=None,
+            startstops=[{"action": "compute", "start": float(z["msg_start"][i]), "stop": float(z["msg_stop"][i])}])
+    ext._end_of_stimulus("end of stream")
+    assert ext.active, ext.reason
+    n = len(exp["pl_task"])
+    assert rec["task"] == exp["pl_task"].tolist()
+    assert rec["worker"] == exp["pl_worker"].tolist()
+    assert np.array_equal(np.array(rec["start"]).view(np.int64), exp["pl_start"].view(np.int64))
+    assert ext.stats["device_decisions"] == n, (ext.stats, n)
+    return dict(fixture=name, placements=n, graphs=ext.stats["graphs"], device_decisions=ext.stats["device_decisions"],
+                prefix_compactions=ext.stats["prefix_compactions"], remaps_checked=remaps_seen,
+                prefixes_seen=len(ext.pnames), table=len(ext.prefix_index), resyncs=ext.stats["resyncs"],
+                active=ext.active, reason=ext.reason)
+
+
 class EventEngine(FixtureEngine):
     """FixtureEngine with the service-event calls: each consumes the fixture's placement
     count of its event and records what the extension passed."""
@@ -902,7 +1020,14 @@ class EventEngine(FixtureEngine):
     def remove_worker(self, w):
         self.calls.append(("remove", int(w)))
 
+    def remap_prefixes(self, task_prefix, prefix_default_duration):  # dgp_remap_prefixes: no placement
+        self.calls.append(("remap", np.array(task_prefix, np.int32), [float(x) for x in prefix_default_duration]))
+
     def sync(self, placements, tasks, workers, globals_):
+        if placements is None:  # the dicts in a compacted prefix numbering: no stimulus of its own
+            assert tasks is None
+            self.calls.append(("sync_rows", workers, globals_))
+            return
         n = len(placements["task"])
         self.calls.append(("sync", n, tasks, workers, globals_))
         k = self.stim[self.k]
@@ -1283,6 +1408,7 @@ if __name__ == "__main__":
         fn = (run_joins if nm.startswith("svcaddw_") else (lambda x: run_second_graph(x, "--resync" in args))
               if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_"))
               else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcrt_", "svcwl_", "svcp2p_"))
+              else run_prefixes if nm.startswith("svcpfx_")
               else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,
                                                plain="plugin" if "--plugin" in args else plain,

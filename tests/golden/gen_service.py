@@ -603,6 +603,234 @@ def main_second_graph(only):
         print(f"{name}: {len(msgs['task'])} messages, second graph of {g2['n_tasks']} at message {at}, routes {routes}")
 
 
+def _load_repo_module(name):
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(f"dgp_{name}", os.path.join(G.REPO, "distributed_amd", f"{name}.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def later_graph(k, n, w, seed, n_prefixes):
+    """Later graph k of a svcpfx_* stream: a C2-shaped random DAG whose task prefixes are its
+    own (``g{k}root``, ``g{k}in{j}``: key_split keeps them) and whose groups carry a token of
+    their own."""
+    gk = G.graphs.random_dag(n, w, seed=seed, n_inner_prefixes=n_prefixes - 1, random_durations=True,
+                             nthreads="random")
+    names = [f"g{k}root"] + [f"g{k}in{j}" for j in range(n_prefixes - 1)]
+    tok = f"{k:02d}" + TOKEN2[2:]
+    gk["prefix_names"] = names
+    gk["group_names"] = [f"{nm}-{tok}" for nm in names]
+    return gk
+
+
+def replay_later_graphs(g, later, cfg, at_fracs):
+    """The replay protocol's completions as task-finished messages, with the independent
+    graphs ``later`` submitted at the messages ``at_fracs`` of the first graph's size (as
+    replay_second_graph submits one: new TaskStates of priority ``(0, 2 + k, i)``, then every
+    new task recommended "waiting"). Each graph brings task prefixes of its own, so over the
+    stream the session meets more of them than the engine's table holds (prefixes.PX). The
+    engine's table follows the extension's rule (distributed_amd/prefixes.py, run here on the
+    reference state at the point the extension's update_graph hook runs: the new TaskStates
+    exist, released): a graph that fits appends its new names; one that does not compacts the
+    table to the live prefixes, recorded as the remap (every earlier task's slot, each slot's
+    default) plus the workers' and global resync rows in the new numbering."""
+    P = _load_repo_module("prefixes")
+    S = _load_repo_module("sync")
+    s, tss, widx, rec, tidx = G.build_state(g, cfg)
+    W = len(g["nthreads"])
+    N = g["n_tasks"]
+    type(s).stimulus_task_finished = Scheduler_stimulus_task_finished()
+    recs = {}
+    for ts in sorted(tss, key=lambda t: t.priority, reverse=True):
+        recs[ts.key] = "waiting"
+    s._transitions(recs, {}, {}, "update-graph")
+    nb, a0, b0 = list(g["nbytes"]), list(g["start"]), list(g["stop"])
+    for gk in later:
+        nb += list(gk["nbytes"])
+        a0 += list(gk["start"])
+        b0 += list(gk["stop"])
+    cs = s.clients["client-0"]
+    run_spec = (operator.add, (), {})
+    # the extension's prefix bookkeeping (ext.py _note_prefixes / _add_graph / _compact_prefixes)
+    slot_of = {nm: i for i, nm in enumerate(g["prefix_names"])}
+    pnames = list(g["prefix_names"])
+    pname_dur = {nm: float(d) for nm, d in zip(g["prefix_names"], g["prefix_default_dur"])}
+    task_pname = np.asarray(g["prefix_id"], np.int32).copy()
+    group_names = list(g["group_names"])
+    at_msgs = [int(f * N) for f in at_fracs]
+    subs = []  # per later graph: message index, its prefix ids (engine slots), the table's defaults, the remap
+
+    def submit(k):
+        nonlocal slot_of, task_pname
+        gk = later[k]
+        base = len(tss)
+        keys_k = G.make_keys(gk)
+        new = []
+        for t, key in enumerate(keys_k):
+            ts = s.new_task(key, run_spec, "released")
+            tidx[key] = base + t
+            ts.priority = (0, 2 + k, int(gk["prio"][t]))
+            new.append(ts)
+        ptr, idx = gk["dep_ptr"], gk["dep_idx"]
+        for t, ts in enumerate(new):
+            for d in idx[ptr[t]:ptr[t + 1]]:
+                ts.add_dependency(new[int(d)])
+            if gk["wanted"][t]:
+                ts.who_wants = {cs}
+                cs.wants_what.add(ts)
+        # the extension's hook: the graph's names in the order its ingestion meets them (the
+        # new tasks in priority order), then the table
+        order = np.argsort(np.asarray(gk["prio"]), kind="stable")
+        first = []
+        for t in order.tolist():
+            nm = gk["prefix_names"][int(gk["prefix_id"][t])]
+            if nm not in first:
+                first.append(nm)
+        sub = {"msg": None, "remap": None}
+        if len(slot_of) + sum(nm not in slot_of for nm in first) > P.PX:
+            live = P.live_prefixes(s)
+            table = P.compacted(slot_of, live, first)
+            assert table is not None, f"more than PX live prefixes: {len(live)} live + {first}"
+            slots, stale = P.task_slots(task_pname, pnames, table)
+            names = sorted(table, key=table.get)
+            defaults = [pname_dur.get(nm, -1.0) for nm in names]
+            keys_old = [ts.key for ts in tss]
+            workers = [a for a, _ in sorted(widx.items(), key=lambda kv: kv[1])]
+            sub["remap"] = dict(slots=slots, defaults=np.array(defaults, np.float64),
+                                workers=S.worker_rows(s, workers, table, {k_: tidx[k_] for k_ in keys_old}),
+                                globals=S.global_rows(s, names, defaults, group_names,
+                                                      {k_: tidx[k_] for k_ in keys_old}, widx))
+            slot_of = table
+        for nm in first:
+            if nm not in slot_of:
+                slot_of[nm] = len(slot_of)
+        for nm, d in zip(gk["prefix_names"], gk["prefix_default_dur"]):
+            if nm not in pname_dur:
+                pname_dur[nm] = float(d)
+                pnames.append(nm)
+        names_now = sorted(slot_of, key=slot_of.get)
+        sub["prefix_id"] = np.array([slot_of[gk["prefix_names"][int(p)]] for p in gk["prefix_id"]], np.int32)
+        sub["defaults"] = np.array([pname_dur.get(nm, -1.0) for nm in names_now], np.float64)
+        sub["group_base"] = len(group_names)
+        group_names.extend(gk["group_names"])
+        pid = {nm: i for i, nm in enumerate(pnames)}
+        task_pname = np.concatenate([task_pname, np.array([pid[gk["prefix_names"][int(p)]] for p in gk["prefix_id"]],
+                                                          np.int32)])
+        recs2 = {ts.key: "waiting" for ts in sorted(new, key=lambda t: t.priority, reverse=True)}
+        s._transitions(recs2, {}, {}, f"update-graph-{k + 2}")
+        tss.extend(new)
+        subs.append(sub)
+
+    msgs = {k: [] for k in ("task", "worker", "run_id", "nbytes", "start", "stop", "status")}
+    stim = [len(rec["task"])]
+    round_ptr = [0]
+    rounds, nplaced = [], []
+    done = 0
+    nsub = 0
+    while True:
+        cur = len(rec["task"])
+        batch = list(range(done, cur))
+        rounds.append(G.snapshot(s, W, widx) + (len(s.queued),))
+        nplaced.append(cur - done)
+        done = cur
+        if not batch:
+            break
+        for pos in batch:
+            while nsub < len(later) and len(msgs["task"]) >= at_msgs[nsub]:
+                n0 = len(rec["task"])
+                submit(nsub)
+                subs[-1]["msg"] = len(msgs["task"])
+                subs[-1]["nplaced"] = len(rec["task"]) - n0
+                stim.append(len(rec["task"]) - n0)
+                nsub += 1
+            t = rec["task"][pos]
+            ts = tss[t]
+            assert ts.state == "processing", (ts.key, ts.state)
+            w = widx[ts.processing_on.address]
+            sid = f"task-finished-{len(msgs['task'])}"
+            r, cm, wm = s.stimulus_task_finished(
+                ts.key, ts.processing_on.address, sid, int(ts.run_id), nbytes=int(nb[t]), type=None,
+                typename="int", metadata=None,
+                startstops=[{"action": "compute", "start": float(a0[t]), "stop": float(b0[t])}])
+            n0 = len(rec["task"])
+            s._transitions(r, cm, wm, sid)
+            s.stimulus_queue_slots_maybe_opened(stimulus_id=sid)
+            stim.append(len(rec["task"]) - n0)
+            for k, v in zip(("task", "worker", "run_id", "nbytes", "start", "stop", "status"),
+                            (t, w, pos, int(nb[t]), float(a0[t]), float(b0[t]), ACCEPTED)):
+                msgs[k].append(v)
+        round_ptr.append(len(msgs["task"]))
+    assert nsub == len(later), (nsub, len(later))
+    rec["stim"] = stim
+    states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
+    return rec, rounds, nplaced, states, msgs, round_ptr, subs, len(pnames)
+
+
+def Scheduler_stimulus_task_finished():
+    from distributed.scheduler import Scheduler
+
+    return Scheduler.stimulus_task_finished
+
+
+def main_prefixes(only):
+    """svcpfx_*: later graphs with task prefixes of their own, more over the stream than the
+    engine's table (prefixes.PX) -- the table compacts to the live prefixes."""
+    cases = {
+        # 3 + 6 x 12 = 75 task prefixes over the stream, at most ~27 live at once
+        "svcpfx_c2var_sat1.1": (dict(n=3000, w=32, seed=61, n_inner_prefixes=2), 6, 500, 12, 1.1),
+        "svcpfx_c2var_satinf": (dict(n=2500, w=24, seed=62, n_inner_prefixes=2), 6, 400, 12, float("inf")),
+    }
+    for name, (a, K, nk, pk, sat) in cases.items():
+        if only and name not in only:
+            continue
+        g = G.graphs.random_dag(a["n"], a["w"], seed=a["seed"], n_inner_prefixes=a["n_inner_prefixes"],
+                                random_durations=True, nthreads="random")
+        later = [later_graph(k, nk, a["w"], a["seed"] * 10 + k, pk) for k in range(K)]
+        G.graphs.check_graph(g)
+        dask.config.set({"distributed.scheduler.worker-saturation": sat})
+        cfg = G.config_dict(sat)
+        at = [0.1 + 0.3 * k for k in range(K)]  # message indices (x the first graph's size)
+        rec, rounds, nplaced, states, msgs, round_ptr, subs, n_names = replay_later_graphs(g, later, cfg, at)
+        G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
+        path = os.path.join(HERE, f"{name}.npz")
+        z = dict(np.load(path, allow_pickle=False))
+        z.update(msg_task=np.array(msgs["task"], np.int32), msg_worker=np.array(msgs["worker"], np.int32),
+                 msg_runid=np.array(msgs["run_id"], np.int64), msg_nbytes=np.array(msgs["nbytes"], np.int64),
+                 msg_start=np.array(msgs["start"]), msg_stop=np.array(msgs["stop"]),
+                 msg_status=np.array(msgs["status"], np.int8), msg_round_ptr=np.array(round_ptr, np.int64),
+                 gk_n=np.array(K, np.int64), gk_prefix_names_total=np.array(n_names, np.int64))
+        dumps = []
+        for k, (gk, sub) in enumerate(zip(later, subs)):
+            p = f"g{k}_"
+            for f in ("dep_ptr", "dep_idx", "prio", "group_id", "wanted", "rootish_override", "nbytes", "start",
+                      "stop"):
+                z[p + f] = np.asarray(gk[f])
+            z[p + "prefix_id"] = sub["prefix_id"]  # the engine's slots
+            z[p + "prefix_local"] = np.asarray(gk["prefix_id"], np.int32)  # into its own names
+            z[p + "prefix_names"] = np.array(gk["prefix_names"])
+            z[p + "group_names"] = np.array(gk["group_names"])
+            z[p + "group_local"] = np.asarray(gk["group_id"], np.int32)
+            z[p + "group_id"] = np.asarray(gk["group_id"], np.int32) + sub["group_base"]
+            z[p + "defaults"] = sub["defaults"]
+            z[p + "msg"] = np.array(sub["msg"], np.int64)
+            z[p + "nplaced"] = np.array(sub["nplaced"], np.int64)
+            z[p + "n_groups"] = np.array(sub["group_base"] + len(gk["group_names"]), np.int64)
+            if sub["remap"] is not None:
+                z[p + "remap_slots"] = sub["remap"]["slots"]
+                z[p + "remap_defaults"] = sub["remap"]["defaults"]
+                z[p + "remap_dump"] = np.array(len(dumps), np.int64)
+                dumps.append(dict(tasks=dict(task=np.zeros(0, np.int32)), workers=sub["remap"]["workers"],
+                                  globals=sub["remap"]["globals"]))
+        if dumps:
+            z.update({k_: v for k_, v in _pack_dumps(dumps).items() if not k_.startswith("sync_tasks")})
+        np.savez_compressed(path, **z)
+        nrm = sum(sub["remap"] is not None for sub in subs)
+        print(f"{name}: {len(msgs['task'])} messages, {K} later graphs, {n_names} task prefixes, {nrm} remaps, "
+              f"{len(rec['task'])} placements")
+
+
 # event kinds of the svcev_* streams (tests/test_gpu_events.py, tests/ext_driver.py)
 EV_FINISHED, EV_ADD_KEYS, EV_RELEASE_DATA, EV_PAUSE, EV_RESUME, EV_LONG_RUNNING, EV_HEARTBEAT, EV_ERRED = range(8)
 # stimuli the engine does not model: the scheduler decides them, then the engine resyncs
@@ -1261,6 +1489,8 @@ def main():
         return main_second_graph(set(sys.argv[2:]))
     if len(sys.argv) > 1 and sys.argv[1] == "events":
         return main_events(set(sys.argv[2:]))
+    if len(sys.argv) > 1 and sys.argv[1] == "prefixes":
+        return main_prefixes(set(sys.argv[2:]))
     cases = {
         "svc_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 64, seed=15, n_inner_prefixes=3,
                                                           random_durations=True, nthreads="random"), 1.1, 1, 0.0),

@@ -433,3 +433,19 @@ def test_drop_ins_install_from_dask_config():
         assert r["stealing_callback"] and r["task_finished"] == "GPUPlacementExtension.handle_task_finished", r
     n = res["no_stealing"]
     assert n["stealing"] is None and not n["stealing_callback"] and n["placement"] == "GPUPlacementExtension", n
+
+
+def test_extension_compacts_the_prefix_table():
+    """svcpfx_*: six later graphs with task prefixes of their own (75 over the stream, more
+    than the engine's table of 32): the extension compacts the table to the live prefixes
+    (prefixes.py; dgp_remap_prefixes + the dicts' resync) wherever a graph would not fit,
+    stays active, and every placement comes from the engine (validate=True). Its remaps and
+    resync rows equal the ones the generator recorded on the reference state, which the GPU
+    test replays through the C ABI (tests/test_gpu_events.py)."""
+    names = ["svcpfx_c2var_sat1.1.npz", "svcpfx_c2var_satinf.npz"]
+    res = drive(names)
+    assert [r["fixture"] for r in res] == names
+    for r in res:
+        assert r["active"] and r["device_decisions"] == r["placements"], r
+        assert r["prefixes_seen"] > 64 and r["prefix_compactions"] >= 3, r
+        assert r["remaps_checked"] == r["prefix_compactions"] and r["table"] <= 32, r

@@ -479,3 +479,77 @@ def test_task_messages_follow_replicas(name, resident):
                     multi += len(hs) > 1
                 checked += 1
     assert checked > 1000 and multi > 0 and pinned > 1000, (checked, multi, pinned)
+
+
+def svc_prefix_files():
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcpfx_") and f.endswith(".npz"))
+
+
+def later_graph_of(z, k, pmax):
+    """Later graph k of a svcpfx_* fixture over the engine-wide tables: priorities after every
+    earlier task's, its prefix ids the engine's slots, its groups after the earlier ones."""
+    p = f"g{k}_"
+    return dict(dep_ptr=z[p + "dep_ptr"], dep_idx=z[p + "dep_idx"], prio=z[p + "prio"] + pmax + 1,
+                prefix_id=z[p + "prefix_id"], group_id=z[p + "group_id"], wanted=z[p + "wanted"],
+                rootish_override=z[p + "rootish_override"], prefix_default_dur=z[p + "defaults"],
+                group_prefix=np.zeros(int(z[p + "n_groups"]), np.int32))
+
+
+@pytest.mark.parametrize("per_message", [True, False], ids=["per-message", "per-round"])
+@pytest.mark.parametrize("name", svc_prefix_files())
+def test_service_prefix_table_compacts(name, per_message):
+    """A session meeting more task prefixes than the engine's table (svcpfx_*: six later
+    graphs with prefixes of their own, 75 over the stream): where a graph would not fit, the
+    table is compacted to the live prefixes (dgp_remap_prefixes with every earlier task's slot,
+    then the workers' and global rows in the new numbering, distributed_amd/prefixes.py run on
+    the reference state), then the graph goes in (dgp_add_graph). Every placement, the
+    per-round snapshots and the final task states equal the reference's."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    msgs = list(zip(z["msg_task"].tolist(), z["msg_worker"].tolist(), z["msg_runid"].tolist(),
+                    z["msg_nbytes"].tolist(), z["msg_start"].tolist(), z["msg_stop"].tolist()))
+    ptr = z["msg_round_ptr"].tolist()
+    K = int(z["gk_n"])
+    assert int(z["gk_prefix_names_total"]) > 64
+    at = {int(z[f"g{k}_msg"]): k for k in range(K)}
+    R = len(exp["round_nplaced"]) + 2
+    status, remaps = [], 0
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        pmax = int(np.max(g["prio"]))
+        for kk in range(len(ptr) - 1):
+            i, e = ptr[kk], ptr[kk + 1]
+            while i < e:  # batches end at each submission
+                if i in at:
+                    k = at[i]
+                    if f"g{k}_remap_slots" in z.files:
+                        d = sync_dump(z, int(z[f"g{k}_remap_dump"]))
+                        eng.remap_prefixes(z[f"g{k}_remap_slots"], z[f"g{k}_remap_defaults"])
+                        eng.sync(None, None, d["workers"], d["globals"])
+                        remaps += 1
+                    gk = later_graph_of(z, k, pmax)
+                    pmax = int(gk["prio"].max())
+                    n0 = eng.num_placements()
+                    newp = eng.add_graph(gk)
+                    assert newp == int(z[f"g{k}_nplaced"]) and eng.num_placements() == n0 + newp
+                j = i + 1
+                if not per_message:
+                    while j < e and j not in at:
+                        j += 1
+                t, w, r, nb, a, b = (np.array(c) for c in zip(*msgs[i:j]))
+                st, _ = eng.tasks_finished(t, w, r, nb, a, b)
+                status.extend(st.tolist())
+                i = j
+            if e > ptr[kk]:
+                eng.snapshot()
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert remaps >= 3
+    assert (np.array(status) == 0).all()
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
