@@ -1923,11 +1923,16 @@ __global__ void k_init_workers(const Dev* __restrict__ Dp) {
 // a row wider than 32 dependencies (the P2P barrier's 66,666) is counted by the whole wave
 // afterwards instead of one lane's serial loop.
 __device__ __forceinline__ bool ug_dep_in_memory(const Dev& D, int d) {
+  // every word loaded independently (no exit on the first set bit: the loads issue back to
+  // back, one memory round trip per row instead of one per word)
   const unsigned long long* row = D.holders + (size_t)d * D.WB;
-  bool any = false;
-  for (int wd = 0; wd < D.WB && !any; wd++) any = row[wd] != 0;
-  return any;
+  unsigned long long any = 0;
+  for (int wd = 0; wd < D.WB; wd++) any |= row[wd];
+  return any != 0;
 }
+// a row wider than this is counted by k_ug_init_wide's grid (the host launches it for each
+// such task, dgplace.hip launch_ug_init); k_ug_init leaves it at 0
+constexpr int64_t UG_WIDE = 2048;
 __global__ void k_ug_init(const Dev* __restrict__ Dp, int lo) {
   const Dev& D = *Dp;
   const int lane = threadIdx.x & 63;
@@ -1950,7 +1955,8 @@ __global__ void k_ug_init(const Dev* __restrict__ Dp, int lo) {
       const int64_t tw = t0 + j;
       const int64_t aw = __shfl(a, j), bw = __shfl(b, j);
       int64_t wo = 0;
-      for (int64_t k = aw + lane; k < bw; k += 64) wo += ug_dep_in_memory(D, D.dep_idx[k]) ? 0 : 1;
+      if (bw - aw <= UG_WIDE)
+        for (int64_t k = aw + lane; k < bw; k += 64) wo += ug_dep_in_memory(D, D.dep_idx[k]) ? 0 : 1;
       wo = wave_sum64(wo);
       if (lane == 0) {
         D.remaining[tw] = (int32_t)wo;
@@ -1959,6 +1965,57 @@ __global__ void k_ug_init(const Dev* __restrict__ Dp, int lo) {
       }
     }
   }
+}
+
+// the dependencies not in memory of one row wider than UG_WIDE (the P2P barrier's 66,666),
+// over the whole grid: k_ug_init left remaining[t] at 0 and this adds each block's count
+__global__ void k_ug_init_wide(const Dev* __restrict__ Dp, int t, int64_t a, int64_t b) {
+  const Dev& D = *Dp;
+  int cnt = 0;
+  for (int64_t k = a + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < b; k += (int64_t)gridDim.x * blockDim.x)
+    cnt += ug_dep_in_memory(D, D.dep_idx[k]) ? 0 : 1;
+  cnt = (int)wave_sum64(cnt);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&D.remaining[t], cnt);
+}
+
+// update_graph's ready list (the tasks of order[scan_lo, N) from task_lo on with no
+// remaining dependency, in priority order) over many workgroups: each takes a tile of
+// RDY_TILE order entries, counts its ready tasks (k_ready_count), then writes them at the
+// sum of the earlier tiles' counts (k_ready_scatter); the last tile writes the total, which
+// k_ug_dispatch takes as its list length
+constexpr int RDY_TILE = 4 * CTA;
+__global__ void __launch_bounds__(CTA) k_ready_count(const Dev* __restrict__ Dp, int scan_lo, int task_lo, int64_t* cnt) {
+  const Dev& D = *Dp;
+  const int64_t base = scan_lo + (int64_t)blockIdx.x * RDY_TILE;
+  int c = 0;
+  for (int j = 0; j < RDY_TILE / CTA; j++) {
+    const int64_t i = base + (int64_t)j * CTA + threadIdx.x;
+    const int t = i < D.N ? D.order[i] : -1;
+    c += (t >= task_lo && D.remaining[t] == 0) ? 1 : 0;
+  }
+  int64_t tot;
+  block_excl_scan(c, &tot);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(CTA) k_ready_scatter(const Dev* __restrict__ Dp, int scan_lo, int task_lo,
+                                                       const int64_t* cnt, int64_t* total) {
+  const Dev& D = *Dp;
+  int64_t off = 0;
+  for (int k = threadIdx.x; k < (int)blockIdx.x; k += CTA) off += cnt[k];
+  int64_t off_tot;
+  block_excl_scan(off, &off_tot);
+  const int64_t base = scan_lo + (int64_t)blockIdx.x * RDY_TILE;
+  int64_t run = off_tot;
+  for (int j = 0; j < RDY_TILE / CTA; j++) {
+    const int64_t i = base + (int64_t)j * CTA + threadIdx.x;
+    const int t = i < D.N ? D.order[i] : -1;
+    const bool r = t >= task_lo && D.remaining[t] == 0;
+    int64_t tot;
+    const int64_t pos = block_excl_scan(r ? 1 : 0, &tot);
+    if (r) D.ready[run + pos] = t;
+    run += tot;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *total = run;
 }
 
 // k_ug_dispatch's dynamic LDS: the tournament tree and the worker arrays its lane-0 chain of
@@ -2274,8 +2331,8 @@ __device__ __attribute__((noinline)) int64_t ug_fill_rootish(const Dev& D, int64
 // priority: a new generation); its placements append to the placement log.
 // scan_lo: the first priority position scanned; task_lo: the first task of the graph (a later
 // graph whose user priority outranks earlier tasks: its tasks sit anywhere in the order)
-__global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp, int scan_lo, int task_lo,
-                                                     uint32_t lds_mask) {
+__global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp, const int64_t* __restrict__ ready_n,
+                                                     int task_lo, uint32_t lds_mask) {
   // the dispatch is one lane's chain of dependent reads and writes of the control block
   // (idle_task_count / idle / saturated counts, the global prefix dict, occupancy sums): the
   // block works on an LDS copy of it (and of Dev, whose ctl points at the copy) and writes
@@ -2299,19 +2356,10 @@ __global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp,
   __shared__ int64_t s_nr, s_pos;
   Ctl* c = D.ctl;
   const int64_t pl0 = (int64_t)c->n_placed;  // 0 for the first graph
-  // ready list in priority order
-  int64_t base = 0;
-  for (int i0 = scan_lo; i0 < D.N; i0 += blockDim.x) {
-    int i = i0 + threadIdx.x;
-    int t = i < D.N ? D.order[i] : -1;
-    bool r = t >= task_lo && D.remaining[t] == 0;
-    int64_t tot;
-    int64_t pos = block_excl_scan(r ? 1 : 0, &tot);
-    if (r) D.ready[base + pos] = t;
-    base += tot;
-  }
+  // the ready list in priority order: D.ready[0, *ready_n) (k_ready_count / k_ready_scatter)
+  (void)task_lo;
   if (threadIdx.x == 0) {
-    s_nr = base;
+    s_nr = *ready_n;
     s_pos = 0;
   }
   tree_rebuild_coop(D);

@@ -105,6 +105,9 @@ struct dgp_engine {
   std::vector<uint8_t> tflags_h;           // task flags as set_graph computed them
   std::vector<int32_t> group_h;            // TaskGroup of each task
   std::vector<int64_t> h_dep_ptr, h_prio;  // the uploaded graph (dgp_add_graph appends to it)
+  std::vector<int32_t> h_wide;             // tasks with more than UG_WIDE dependencies (k_ug_init_wide)
+  int64_t* d_rdy = nullptr;                // update_graph's ready-list pass: per-tile counts, then the total
+  int64_t rdy_cap = 0;
   std::vector<int32_t> h_dep_idx, h_prefix;
   std::vector<uint8_t> h_wanted;
   std::vector<int64_t> gdep_n, gdep_len;   // per group: len(tg.dependencies), sum of their lengths
@@ -431,6 +434,21 @@ void ug_lds_plan(const dgp::Dev& D, uint32_t* mask, size_t* bytes) {
   *bytes = used;
 }
 
+// update_graph part 1 over tasks [lo, N): k_ug_init, then k_ug_init_wide for each row wider
+// than UG_WIDE (counted across a grid instead of one wave's serial loop)
+int launch_ug_init(dgp_engine* e, int64_t lo) {
+  const dgp::Dev* DP = e->d_dev;
+  hipStream_t s = e->stream;
+  const int64_t N = e->D.N;
+  hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(N - lo, 256, 2048)), dim3(256), 0, s, DP, (int)lo);
+  for (int32_t t : e->h_wide) {
+    if (t < lo) continue;
+    const int64_t a = e->h_dep_ptr[t], b = e->h_dep_ptr[t + 1];
+    hipLaunchKernelGGL(dgp::k_ug_init_wide, dim3(grid_for(b - a, 1024, 256)), dim3(256), 0, s, DP, (int)t, a, b);
+  }
+  return 0;
+}
+
 int launch_ug_dispatch(dgp_engine* e, int scan_lo, int task_lo) {
   uint32_t mask = 0;
   size_t bytes = 0;
@@ -440,9 +458,30 @@ int launch_ug_dispatch(dgp_engine* e, int scan_lo, int task_lo) {
     HIPCHK(e, hipFuncSetAttribute((const void*)dgp::k_ug_dispatch, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     attr_set[e->device & 63] = bytes;
   }
+  // the ready list's tiles: a count per tile, then the total
+  const int64_t n_scan = std::max<int64_t>(0, (int64_t)e->D.N - scan_lo);
+  const int64_t tiles = (n_scan + dgp::RDY_TILE - 1) / dgp::RDY_TILE;
+  if (tiles + 1 > e->rdy_cap) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->d_rdy) HIPCHK(e, hipFree(e->d_rdy));
+    e->d_rdy = nullptr;
+    e->rdy_cap = 0;
+    const int64_t cap = std::max<int64_t>(tiles + 1, 1024);
+    HIPCHK(e, hipMalloc((void**)&e->d_rdy, (size_t)cap * 8));
+    e->rdy_cap = cap;
+  }
+  int64_t* total = e->d_rdy + tiles;
   const dgp::Dev* DP = e->d_dev;
+  hipStream_t s = e->stream;
   return timed_launch(e, 3, [&] {
-    hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), bytes, e->stream, DP, scan_lo, task_lo, mask);
+    if (tiles == 0) {
+      (void)hipMemsetAsync(total, 0, 8, s);
+    } else {
+      hipLaunchKernelGGL(dgp::k_ready_count, dim3((unsigned)tiles), dim3(dgp::CTA), 0, s, DP, scan_lo, task_lo, e->d_rdy);
+      hipLaunchKernelGGL(dgp::k_ready_scatter, dim3((unsigned)tiles), dim3(dgp::CTA), 0, s, DP, scan_lo, task_lo,
+                         (const int64_t*)e->d_rdy, total);
+    }
+    hipLaunchKernelGGL(dgp::k_ug_dispatch, dim3(1), dim3(dgp::CTA), bytes, s, DP, (const int64_t*)total, task_lo, mask);
   });
 }
 
@@ -637,6 +676,7 @@ void dgp_destroy(dgp_engine* e) {
   (void)hipFree(e->ctl);
   (void)hipFree(e->d_aux);
   (void)hipFree(e->d_dev);
+  if (e->d_rdy) (void)hipFree(e->d_rdy);
   for (hipEvent_t ev : e->evpool) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
   delete e;
@@ -901,6 +941,9 @@ int upload_graph(dgp_engine* e, int64_t n_tasks, const int64_t* dep_ptr, const i
   e->group_h.assign(group_id, group_id + N);
   e->rootish_override_h.assign(rootish_override, rootish_override + N);
   e->h_dep_ptr.assign(dep_ptr, dep_ptr + N + 1);
+  e->h_wide.clear();
+  for (int64_t t = 0; t < N; t++)
+    if (dep_ptr[t + 1] - dep_ptr[t] > dgp::UG_WIDE) e->h_wide.push_back((int32_t)t);
   e->h_dep_idx.assign(dep_idx, dep_idx + E);
   e->h_prio.assign(prio, prio + N);
   e->h_prefix.assign(prefix_id, prefix_id + N);
@@ -1208,7 +1251,7 @@ int dgp_update_graph(dgp_engine* e) {
   const dgp::Dev* DP = e->d_dev;
   hipStream_t s = e->stream;
   if (int rc = timed_launch(e, 3, [&] {
-        hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(e->D.N, 256, 2048)), dim3(256), 0, s, DP, 0);
+        launch_ug_init(e, 0);
       }))
     return rc;
   if (int rc = launch_ug_dispatch(e, 0, 0)) return rc;
@@ -2003,7 +2046,7 @@ int dgp_graph_stimulus(dgp_engine* e, int64_t* n_new_placements) {
   const dgp::Dev* DP = e->d_dev;
   hipStream_t s = e->stream;
   if (int rc = timed_launch(e, 3, [&] {
-        hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(N - lo, 256, 2048)), dim3(256), 0, s, DP, (int)lo);
+        launch_ug_init(e, lo);
         hipLaunchKernelGGL(k_ug_frontier_reset, dim3(1), dim3(64), 0, s, DP);
         hipLaunchKernelGGL(k_ug_frontier, dim3(grid_for(N - lo, 256, 2048)), dim3(256), 0, s, DP, (int)lo);
         hipLaunchKernelGGL(dgp::k_candidate_commbytes, dim3(grid_for(N - lo, 256, 2048)), dim3(256), 0, s, DP);
@@ -2224,7 +2267,7 @@ static int add_graph_impl(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr, 
   if (int rc = read_ctl(e, &c0)) return rc;
   const dgp::Dev* DP = e->d_dev;
   if (int rc = timed_launch(e, 3, [&] {
-        hipLaunchKernelGGL(dgp::k_ug_init, dim3(grid_for(n_new, 256, 2048)), dim3(256), 0, s, DP, (int)N0);
+        launch_ug_init(e, N0);
       }))
     return rc;
   if (int rc = launch_ug_dispatch(e, (int)N0, (int)N0)) return rc;
