@@ -2384,7 +2384,18 @@ __global__ void __launch_bounds__(CTA) k_ug_dispatch(const Dev* __restrict__ Dp,
         if (q) {
           D.qarr[qb + queued + oq] = x;
           D.state[x] = S_QUEUED;
-          atomicAdd((unsigned long long*)&D.g_relwait[D.group[x]], (unsigned long long)-1ll);
+        }
+        // released + waiting of each queued task's group, one atomic per group a wave holds
+        // (a root-ish run is mostly one group: per-task atomics on one address serialised)
+        {
+          const int g = q ? D.group[x] : -1;
+          for (unsigned long long m = __ballot(q); m;) {
+            const int g0 = __shfl(g, __builtin_ctzll(m));
+            const unsigned long long mg = __ballot(q && g == g0);
+            if ((threadIdx.x & 63) == __builtin_ctzll(m))
+              atomicAdd((unsigned long long*)&D.g_relwait[g0], (unsigned long long)-(long long)__builtin_popcountll(mg));
+            m &= ~mg;
+          }
         }
         if (k) D.ready[pos + kept + ok] = x;
         queued += tq;
