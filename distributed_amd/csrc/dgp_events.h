@@ -415,6 +415,32 @@ __global__ void __launch_bounds__(64) k_ev_task_erred(const Dev* __restrict__ Dp
 // (the round engine's key, unused by the stream engine).
 enum : int { RC_RELEASED = 0, RC_WAITING = 1, RC_PROCESSING = 2 };
 
+// The scheduler's iteration orders the cascade follows where the engine's own (index order)
+// differs: row i names task[i] and what it iterates, kind 0 its dependencies
+// (_transition_released_waiting :2101, a set), kind 1 its waiters (_transition_memory_released
+// :2494, a set); rows sorted by (task, kind), checked by the host (dgp_lose_worker_ordered).
+enum : int { LO_DEPS = 0, LO_WAITERS = 1 };
+struct LossOrder {
+  const int32_t* task;
+  const int8_t* kind;
+  const int64_t* ptr;
+  const int32_t* idx;
+  int n;
+  // the row of (t, k) as [*a, *b) of idx, or false (binary search: a loss names a few tasks)
+  __device__ bool row(int t, int k, int64_t* a, int64_t* b) const {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if (task[m] < t || (task[m] == t && kind[m] < k)) lo = m + 1;
+      else hi = m;
+    }
+    if (lo >= n || task[lo] != t || kind[lo] != k) return false;
+    *a = ptr[lo];
+    *b = ptr[lo + 1];
+    return true;
+  }
+};
+
 __device__ __forceinline__ void loss_mark(const Dev& D, long long& nmark, int t, uint8_t m) {
   if (!(D.tdyn[t] & (TD_READD | TD_REWAIT))) D.release_key[nmark++] = (unsigned long long)t;
   D.tdyn[t] |= m;
@@ -477,28 +503,47 @@ __device__ void loss_exit_processing(const Dev& D, int t, int lost_w) {
 }
 
 // _transition_released_waiting (:2078-2119) of t: waiting_on = the dependencies without a
-// replica; a dependency it (re-)joins as a waiter gains one (a lost task recomputed had left
-// its dependencies' waiters when it completed: TD_READD)
-__device__ void loss_released_waiting(const Dev& D, long long& sp, long long& nmark, int t) {
+// replica; a released dependency is recommended to waiting in turn (:2105-2106: a result lost
+// here, or one released earlier -- a recompute chain; either left its own dependencies'
+// waiters when it completed, so it is marked TD_READD), every other dependency gains t as a
+// waiter when t had left it (TD_READD, :2108-2110). ts.waiters becomes the waiting
+// dependents (:2112), recounted for a recomputed task (any other one never left them); a
+// dependent still processing counts too: its own processing -> released -> waiting comes
+// later in the cascade and adds it then (a task it never left, so the engine does not add
+// it again).
+__device__ void loss_released_waiting(const Dev& D, const LossOrder& O, long long& sp, long long& nmark, int t) {
   int wo = 0;
-  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
-    const int d = D.dep_idx[k];
+  int64_t a = D.dep_ptr[t], b = D.dep_ptr[t + 1];
+  const int32_t* row = D.dep_idx;
+  if (O.row(t, LO_DEPS, &a, &b)) row = O.idx;  // the scheduler's set order
+  const bool readd = (D.tdyn[t] & TD_READD) != 0;
+  for (int64_t k = a; k < b; k++) {
+    const int d = row[k];
     const uint8_t sd = D.state[d];
-    bool any = false;
-    for (int b = 0; b < D.WB && !any; b++) any = D.holders[(size_t)d * D.WB + b] != 0;
-    wo += any ? 0 : 1;
-    if (sd == S_RELEASED && (D.tdyn[d] & TD_READD)) {  // a result lost here, recomputed: its rec (:2105-2106)
-      rec_push(D, sp, d, RC_WAITING);
-      continue;
-    }
-    if (sd == S_RELEASED || sd == S_ERRED || (D.tflags[d] & TF_FORGOTTEN)) {  // a recompute chain / lost dependency
+    if (sd == S_ERRED || (D.tflags[d] & TF_FORGOTTEN)) {  // a lost / erred dependency
       set_error(D, ERR_UNSUPPORTED, t);
       return;
     }
-    if (D.tdyn[t] & TD_READD) D.waiters[d] += 1;  // dts.waiters.add(ts) (:2108-2110)
+    bool any = false;
+    for (int w = 0; w < D.WB && !any; w++) any = D.holders[(size_t)d * D.WB + w] != 0;
+    wo += any ? 0 : 1;
+    if (sd == S_RELEASED) {  // recomputed: its recommendation (:2105-2106)
+      loss_mark(D, nmark, d, TD_READD);
+      rec_push(D, sp, d, RC_WAITING);
+      continue;
+    }
+    if (readd) D.waiters[d] += 1;  // dts.waiters.add(ts) (:2108-2110)
   }
   D.state[t] = S_WAITING;
   D.remaining[t] = wo;
+  if (readd) {
+    int nw = 0;
+    for (int64_t k = D.dpt_ptr[t]; k < D.dpt_ptr[t + 1]; k++) {
+      const uint8_t sy = D.state[D.dpt_idx[k]];
+      nw += (sy == S_WAITING || sy == S_PROCESSING) ? 1 : 0;
+    }
+    D.waiters[t] = nw;
+  }
   loss_mark(D, nmark, t, TD_REWAIT);
   D.tdyn[t] &= (uint8_t)~TD_READD;
   if (wo == 0) rec_push(D, sp, t, RC_PROCESSING);
@@ -506,7 +551,7 @@ __device__ void loss_released_waiting(const Dev& D, long long& sp, long long& nm
 
 // lane 0: pop recommendations until one is a placement (returns its task) or none is left
 // (-1). ERR_UNSUPPORTED stops the machine.
-__device__ int loss_machine(const Dev& D, long long& sp, long long& nmark, int lost_w) {
+__device__ int loss_machine(const Dev& D, const LossOrder& O, long long& sp, long long& nmark, int lost_w) {
   long long* at = (long long*)D.ready_key;
   while (sp > 0 && D.ctl->error == 0) {
     sp--;
@@ -527,11 +572,11 @@ __device__ int loss_machine(const Dev& D, long long& sp, long long& nmark, int l
         break;
       }
       rec_push(D, sp, t, RC_WAITING);  // :3343-3344
-      if (v == RC_WAITING) loss_released_waiting(D, sp, nmark, t);  // through released (:1961-1984)
+      if (v == RC_WAITING) loss_released_waiting(D, O, sp, nmark, t);  // through released (:1961-1984)
       continue;
     }
     if (st == S_RELEASED && v == RC_WAITING) {
-      loss_released_waiting(D, sp, nmark, t);
+      loss_released_waiting(D, O, sp, nmark, t);
       continue;
     }
     if (st == S_MEMORY && v == RC_RELEASED) {  // a lost result (:2444-2505): no replica is left
@@ -542,8 +587,11 @@ __device__ int loss_machine(const Dev& D, long long& sp, long long& nmark, int l
         rec_push(D, sp, t, RC_WAITING);
         loss_mark(D, nmark, t, TD_READD);
       }
-      for (int64_t k = D.dpt_ptr[t]; k < D.dpt_ptr[t + 1]; k++) {  // its waiters (:2494-2500)
-        const int y = D.dpt_idx[k];
+      int64_t a = D.dpt_ptr[t], b = D.dpt_ptr[t + 1];
+      const int32_t* row = D.dpt_idx;
+      if (O.row(t, LO_WAITERS, &a, &b)) row = O.idx;  // the scheduler's set order of ts.waiters
+      for (int64_t k = a; k < b; k++) {  // its waiters (:2494-2500)
+        const int y = row[k];
         const uint8_t sy = D.state[y];
         if (sy == S_PROCESSING) {
           rec_push(D, sp, y, RC_WAITING);
@@ -564,7 +612,7 @@ __device__ int loss_machine(const Dev& D, long long& sp, long long& nmark, int l
 
 __global__ void __launch_bounds__(CTA) k_ev_lose_worker(const Dev* __restrict__ Dp, int w, const int32_t* __restrict__ proc,
                                                         int n_proc, const int32_t* __restrict__ held, int n_held,
-                                                        long long* placed) {
+                                                        LossOrder O, long long* placed) {
   __shared__ Dev s_dev;  // Dev and Ctl in LDS, as the update_graph dispatcher works on them
   __shared__ Ctl s_ctl;
   {
@@ -621,7 +669,7 @@ __global__ void __launch_bounds__(CTA) k_ev_lose_worker(const Dev* __restrict__ 
   while (true) {
     if (threadIdx.x == 0) {
       long long sp = s_sp, nmark = s_nmark;
-      s_x = loss_machine(D, sp, nmark, w);
+      s_x = loss_machine(D, O, sp, nmark, w);
       s_sp = sp;
       s_nmark = nmark;
       c->pool_used = 0;

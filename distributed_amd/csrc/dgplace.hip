@@ -2492,9 +2492,49 @@ int dgp_remove_worker(dgp_engine* e, int32_t worker) {
 
 int dgp_lose_worker(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing, int64_t n_held,
                     const int32_t* held, int64_t* n_new_placements) {
+  return dgp_lose_worker_ordered(e, worker, n_processing, processing, n_held, held, 0, nullptr, nullptr, nullptr, nullptr,
+                                 n_new_placements);
+}
+
+int dgp_lose_worker_ordered(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing,
+                            int64_t n_held, const int32_t* held, int64_t n_order, const int32_t* order_task,
+                            const int8_t* order_kind, const int64_t* order_ptr, const int32_t* order_idx,
+                            int64_t* n_new_placements) {
   if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (int rc = event_ready(e, "dgp_lose_worker")) return rc;
+  {  // the order rows: sorted by (task, kind); kind 0 a permutation of the task's dependencies,
+     // kind 1 distinct dependents of it
+    const dgp::Dev& D = e->D;
+    if (n_order < 0 || n_order > 2 * D.N || (n_order && (!order_task || !order_kind || !order_ptr || !order_idx)))
+      return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: bad order rows");
+    if (n_order && order_ptr[0] != 0) return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: order_ptr[0] != 0");
+    const std::vector<int64_t>& dp = e->h_dep_ptr;
+    const std::vector<int32_t>& di = e->h_dep_idx;
+    for (int64_t i = 0; i < n_order; i++) {
+      const int32_t t = order_task[i];
+      const int k = order_kind[i];
+      if (t < 0 || t >= D.N || (k != dgp::ev::LO_DEPS && k != dgp::ev::LO_WAITERS) || order_ptr[i + 1] < order_ptr[i])
+        return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: bad order row");
+      if (i > 0 && (order_task[i - 1] > t || (order_task[i - 1] == t && order_kind[i - 1] >= k)))
+        return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: order rows not sorted by (task, kind)");
+      std::vector<int32_t> r(order_idx + order_ptr[i], order_idx + order_ptr[i + 1]);
+      for (int32_t x : r)
+        if (x < 0 || x >= D.N) return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: task out of range");
+      std::sort(r.begin(), r.end());
+      if (std::adjacent_find(r.begin(), r.end()) != r.end())
+        return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: a task twice in one row");
+      if (k == dgp::ev::LO_DEPS) {
+        std::vector<int32_t> own(di.begin() + dp[t], di.begin() + dp[t + 1]);
+        std::sort(own.begin(), own.end());
+        if (own != r) return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: a dependency row is not the task's dependencies");
+      } else {
+        for (int32_t y : r)
+          if (std::find(di.begin() + dp[y], di.begin() + dp[y + 1], t) == di.begin() + dp[y + 1])
+            return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: a waiters row names a task that does not depend on it");
+      }
+    }
+  }
   dgp::Dev& D = e->D;
   if (worker < 0 || worker >= D.W) return fail(e, DGP_E_ARG, "dgp_lose_worker: worker out of range");
   if (e->paused_h[worker] == 2) return fail(e, DGP_E_ARG, "dgp_lose_worker: the worker was removed");
@@ -2514,11 +2554,18 @@ int dgp_lose_worker(dgp_engine* e, int32_t worker, int64_t n_processing, const i
   if (int rc = refresh_rootish(e)) return rc;
   HIPCHK(e, hipMemsetAsync(D.ready_key, 0xff, (size_t)D.N * 8, e->stream));  // the recommendation dict: empty
   std::vector<char*> a;
-  if (int rc = stage_args(e, {{processing, (size_t)n_processing * 4}, {held, (size_t)n_held * 4}}, a)) return rc;
+  const int64_t n_oidx = n_order ? order_ptr[n_order] : 0;
+  if (int rc = stage_args(e, {{processing, (size_t)n_processing * 4}, {held, (size_t)n_held * 4},
+                              {order_task, (size_t)n_order * 4}, {order_kind, (size_t)n_order},
+                              {order_ptr, n_order ? (size_t)(n_order + 1) * 8 : 0}, {order_idx, (size_t)n_oidx * 4}},
+                          a))
+    return rc;
+  dgp::ev::LossOrder O{(const int32_t*)a[2], (const int8_t*)a[3], (const int64_t*)a[4], (const int32_t*)a[5],
+                       (int)n_order};
   if (int rc = grow_logs(e, 0)) return rc;
   if (int rc = sync_dev(e)) return rc;
   hipLaunchKernelGGL(dgp::ev::k_ev_lose_worker, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev, worker,
-                     (const int32_t*)a[0], (int)n_processing, (const int32_t*)a[1], (int)n_held, e->d_aux + 3);
+                     (const int32_t*)a[0], (int)n_processing, (const int32_t*)a[1], (int)n_held, O, e->d_aux + 3);
   HIPCHK(e, hipGetLastError());
   if (int rc = set_runids(e)) return rc;
   long long placed = 0;

@@ -58,7 +58,7 @@ from operator import attrgetter, lt, truth
 
 import numpy as np
 
-from . import prefixes, sync
+from . import loss, prefixes, sync
 
 try:  # the plugin base class when dask.distributed is importable; plain object otherwise
     from distributed.diagnostics.plugin import SchedulerPlugin
@@ -567,32 +567,6 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._allowed.pop()
         self._losing = None
 
-    @staticmethod
-    def _loss_supported(s, ws, proc, held, safe) -> bool:
-        """The losses dgp_lose_worker restates: no processing task
-        that errs (KilledWorker, :5239-5265) or that nobody needs, and every lost result that
-        is needed has its dependencies in memory elsewhere and no queued / no-worker waiter."""
-        for ts in proc:
-            if (not safe and ts.suspicious + 1 > s.allowed_failures) or not (ts.waiters or ts.who_wants):
-                return False
-            if ts.actor or ts.has_lost_dependencies:
-                return False
-        for ts in held:
-            if ts.who_has != {ws}:
-                continue
-            if not ts.run_spec or ts.actor or ts.has_lost_dependencies:
-                return False
-            if ts.who_wants or ts.waiters:
-                for d in ts.dependencies:
-                    if d.state != "memory" or d.who_has == {ws}:
-                        return False
-            for d in ts.waiters or ():
-                if d.state in ("queued", "no-worker"):
-                    return False
-                if d.state == "processing" and not (d.waiters or d.who_wants):
-                    return False
-        return True
-
     def _lose_worker(self, address, safe) -> bool:
         """The engine's half of a worker loss (see ``_wrap_remove_worker``): True when the
         engine decided the stimulus (its placements are queued for the transitions)."""
@@ -606,17 +580,20 @@ class GPUPlacementExtension(SchedulerPlugin):
         if not proc and not any(ts.who_has == {ws} for ts in held):
             return False  # a drained worker: no transition (the plugin hook follows it)
         ti = self.task_index
-        if (any(ts.key not in ti for ts in proc) or any(ts.who_has == {ws} and ts.key not in ti for ts in held)
-                or any(ts.who_has == {ws} and (ts.prefix.name not in self.prefix_index or ti[ts.key] in self._stale)
-                       for ts in held)
-                or not self._loss_supported(s, ws, proc, held, safe)):
+        chain = None
+        if not (any(ts.key not in ti for ts in proc) or any(ts.who_has == {ws} and ts.key not in ti for ts in held)):
+            chain = loss.supported(s, ws, proc, held, safe)
+        # every task the cascade may re-wait or place is the engine's, with its prefix's slot
+        if chain is None or any(ts.key not in ti or ts.prefix.name not in self.prefix_index or ti[ts.key] in self._stale
+                                for ts in chain + loss.lost_results(ws, held)):
             self.stats["losses_left_to_scheduler"] += 1
             return False
         self._end_of_stimulus("the previous stimulus")
         if not self.active:
             return False
+        order = loss.loss_orders(chain, lambda ts: ti[ts.key])
         n = self.engine.lose_worker(self.worker_index[address], [ti[ts.key] for ts in proc],
-                                    [ti[ts.key] for ts in held if ts.key in ti])
+                                    [ti[ts.key] for ts in held if ts.key in ti], order)
         if n is None:  # refused: the scheduler decides, the engine resyncs after
             self._suspend(f"remove_worker({address}): {getattr(self.engine, 'refusal', 'refused by the engine')}")
             return False

@@ -7,10 +7,11 @@ prefixes matter to placement: those of the tasks that are waiting, queued, proce
 no-worker and those counted in a worker's or the global ``task_prefix_count``
 (``_calc_occupancy`` :1884-1903 sums exactly these). A task of any other prefix is released,
 in memory, erred or forgotten: nothing reads its prefix until it is recomputed, and every
-recompute the engine does not run itself (a later graph that needs a released task, a loss
-with a recompute chain) is the scheduler's stimulus followed by a resync, which makes the
-table current again first (``GPUPlacementExtension._prefixes_current``); the recompute the
-engine runs itself (``dgp_lose_worker``) is only offered for tasks whose prefix has its slot.
+recompute the engine does not run itself (a later graph that needs a released task) is the
+scheduler's stimulus followed by a resync, which makes the table current again first
+(``GPUPlacementExtension._prefixes_current``); the recomputes the engine runs itself
+(``dgp_lose_worker_ordered``, recompute chains included) are only offered when every task of
+the cascade has its prefix's slot.
 
 So when a later graph would pass ``PX`` prefixes, the table is compacted: the live prefixes
 keep their relative order, the new graph's follow, and ``dgp_remap_prefixes`` gives every

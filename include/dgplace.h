@@ -45,7 +45,9 @@
  *                         :5094-5127)
  *   dgp_remove_worker     Scheduler.remove_worker's worker table (:5213-5231)
  *   dgp_lose_worker       the whole Scheduler.remove_worker stimulus (:5180-5303): processing
- *                         tasks released and re-placed, lost results recomputed (ABI 17)
+ *                         tasks released and re-placed, lost results recomputed (ABI 17),
+ *                         with recompute chains in the scheduler's set orders
+ *                         (dgp_lose_worker_ordered, ABI 21)
  *   dgp_sync_*            the scheduler's state after a stimulus it decided itself
  *   dgp_snapshot          one per-worker snapshot (occupancy, nbytes, processing, idle /
  *                         saturated / idle_task_count, queue length) at a caller-chosen point
@@ -68,7 +70,7 @@
 extern "C" {
 #endif
 
-#define DGP_ABI_VERSION 20
+#define DGP_ABI_VERSION 21
 
 #define DGP_OK 0
 #define DGP_E_ARG -1     /* invalid argument / shape */
@@ -403,11 +405,24 @@ int dgp_remove_worker(dgp_engine* e, int32_t worker);
  * worker's tasks in the order the scheduler iterates ws.processing. The placements append to
  * the placement log (*n_new_placements); paused workers may be present (decide_worker's
  * candidates are then the running holders, or every running worker). DGP_E_UNSUPPORTED: the
- * cascade reaches a case the engine does not restate (a dependency to recompute, a queued or
- * no-worker dependent, a task nobody needs); after a refusal from the device the engine
+ * cascade reaches a case the engine does not restate (a released dependency: see
+ * dgp_lose_worker_ordered; a queued or no-worker dependent, a task nobody needs); after a refusal from the device the engine
  * takes the scheduler's state (dgp_sync_*) as after dgp_remove_worker. */
 int dgp_lose_worker(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing, int64_t n_held,
                     const int32_t* held, int64_t* n_new_placements);
+/* dgp_lose_worker_ordered (ABI 21): dgp_lose_worker, and a released dependency of a task the
+ * cascade re-waits is recomputed in turn (_transition_released_waiting :2101-2106: a chain of
+ * recomputes back to results still in memory). Where the recommendations' order follows a
+ * Python set, the caller passes the scheduler's iteration order: rows i = 0..n_order-1,
+ * sorted by (order_task, order_kind), name order_idx[order_ptr[i], order_ptr[i+1]) as
+ * order_task[i]'s dependencies (kind 0: ts.dependencies, a permutation of its row) or its
+ * waiters (kind 1: ts.waiters of a lost result, dependents of it); a task without a row
+ * iterates in index order. dgp_lose_worker is this call with no rows. DGP_E_UNSUPPORTED as
+ * there (KilledWorker, a queued / no-worker dependent, an erred or forgotten dependency). */
+int dgp_lose_worker_ordered(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing,
+                            int64_t n_held, const int32_t* held, int64_t n_order, const int32_t* order_task,
+                            const int8_t* order_kind, const int64_t* order_ptr, const int32_t* order_idx,
+                            int64_t* n_new_placements);
 int dgp_sync_placements(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* comm_bytes,
                         const double* start_time, const int64_t* ws_nbytes, const int8_t* route);
 int dgp_sync_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t* state, const int32_t* remaining,

@@ -962,6 +962,7 @@ class EventEngine(FixtureEngine):
     def __init__(self, exp, fixture_keys):
         super().__init__(exp, fixture_keys)
         self.calls = []
+        self.loss_orders = []  # the order rows of each lose_worker call
 
     def _event(self, *call):
         assert self._posted is None, f"{call[0]} while a task-finished batch is posted"  # the engine refuses it
@@ -984,9 +985,10 @@ class EventEngine(FixtureEngine):
     def set_worker_status(self, w, running):
         return self._event("status", int(w), int(running))
 
-    def lose_worker(self, w, processing, held):  # dgp_lose_worker: the fixture's placements of that event
+    def lose_worker(self, w, processing, held, order=()):  # dgp_lose_worker_ordered: the fixture's placements
         for s_ in self.who.values():
             s_.discard(int(w))
+        self.loss_orders.append([(int(t), int(k), [int(q) for q in seq]) for t, k, seq in order])
         return self._event("lose", int(w), [int(x) for x in processing], [int(x) for x in held])
 
     def long_running(self, t, cd):
@@ -1280,6 +1282,11 @@ def run_events(name, plain=False):
             want.append(("lose", w, lst[:int(x)], lst[int(x):]))
             assert ext.stats["resyncs"] == rs0 and ext.stats["workers_lost_on_device"] == lw0 + 1, (i, ext.stats)
             assert not ext.suspended, (i, ext.suspend_reason)
+            if "lo_evptr" in z.files:  # the extension's set orders are the generator's (same hash seed)
+                ep, rp, li = z["lo_evptr"], z["lo_rowptr"], z["lo_idx"]
+                rows = [(int(z["lo_task"][r]), int(z["lo_kind"][r]), li[rp[r]:rp[r + 1]].tolist())
+                        for r in range(ep[i], ep[i + 1])]
+                assert sorted(eng.loss_orders[-1]) == sorted(rows), (i, eng.loss_orders[-1], rows)
         elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
             if kd == EV_REMOVE_WORKER:
                 lw0 = ext.stats["workers_lost_on_device"]

@@ -926,7 +926,7 @@ def _erred_is_simple(s, ts):
     return all(x is ts or x.state == "waiting" for x in closure)
 
 
-def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_scale=0.3, dumps=None):
+def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_scale=0.3, dumps=None, chains=False):
     """The replay protocol's completions as task-finished messages, interleaved with the
     other worker stimuli that change placement inputs, each through the reference's own
     handler (``Scheduler.*`` borrowed onto the replay state):
@@ -949,7 +949,12 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
     Stored per event (``ev_*``, in order): kind, task, worker, a float (long-running
     compute duration, NaN for None; heartbeat: the scheduler bandwidth after it), the
     heartbeat's executing tasks and durations (CSR ``hb_ptr`` / ``hb_task`` / ``hb_dur``), and
-    the placements each event made (``stim_nplaced``: update_graph first)."""
+    the placements each event made (``stim_nplaced``: update_graph first).
+
+    ``chains``: worker losses may recompute released dependencies (distributed_amd/loss.py);
+    each loss event's order rows (the set orders the cascade follows, as loss_orders gives
+    them in this process) go to ``hb["lo"]``: CSR over events (``evptr``) into rows (``task``,
+    ``kind``, ``rowptr`` into ``idx``)."""
     from distributed.scheduler import Scheduler
 
     s, tss, widx, rec, tidx = G.build_state(g, cfg)
@@ -1004,6 +1009,9 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
     s._transitions(recs, {}, {}, "update-graph")
     ev = {k: [] for k in ("kind", "task", "worker", "x", "nbytes", "start", "stop", "runid")}
     hb = {"ptr": [0], "task": [], "dur": []}
+    lo = {"evptr": [0], "task": [], "kind": [], "rowptr": [0], "idx": []}
+    hb["lo"] = lo
+    LS = _load_repo_module("loss") if chains else None
     stim = [len(rec["task"])]
     round_ptr = [0]
     rounds, nplaced = [], []
@@ -1015,6 +1023,7 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
         for k, v in zip(ev, (kind, t, w, x, nbytes, start, stop, runid)):
             ev[k].append(v)
         hb["ptr"].append(len(hb["task"]))
+        lo["evptr"].append(len(lo["task"]))
 
     def event():
         kind = int(rng.choice(kinds))
@@ -1095,16 +1104,32 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             live = [i for i in range(W) if i not in removed]
             if len(live) <= max(2, W // 2):
                 return
-            cand = []
+            cand, chained, casc = [], [], {}
             for i in live:
                 ws = s.workers[addr[i]]
                 busy = bool(ws.processing) or any(ts.who_has == {ws} for ts in ws.has_what)
-                if busy and _loss_is_supported(s, ws):
+                if not busy:
+                    continue
+                if chains:
+                    c = LS.supported(s, ws, list(ws.processing), list(ws.has_what), False)
+                    if c is not None:
+                        cand.append(i)
+                        casc[i] = c
+                        if any(t.state == "released" for t in c):  # recomputes a released dependency
+                            chained.append(i)
+                elif _loss_is_supported(s, ws):
                     cand.append(i)
             if not cand:
                 return
-            w = cand[int(rng.integers(0, len(cand)))]
+            pick = chained if chained and rng.random() < 0.75 else cand
+            w = pick[int(rng.integers(0, len(pick)))]
             ws = s.workers[addr[w]]
+            if chains:
+                for t, k, seq in LS.loss_orders(casc[w], lambda ts: tidx[ts.key]):
+                    lo["task"].append(t)
+                    lo["kind"].append(k)
+                    lo["idx"].extend(seq)
+                    lo["rowptr"].append(len(lo["idx"]))
             proc = [tidx[ts.key] for ts in ws.processing]  # the order remove_worker iterates (:5236)
             held = [tidx[ts.key] for ts in ws.has_what]  # ... and :5270
             loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
@@ -1293,6 +1318,9 @@ def replay_p2p(g, cfg, dumps):
     s._transitions(recs, {}, {}, "update-graph")
     ev = {k: [] for k in ("kind", "task", "worker", "x", "nbytes", "start", "stop", "runid")}
     hb = {"ptr": [0], "task": [], "dur": []}
+    lo = {"evptr": [0], "task": [], "kind": [], "rowptr": [0], "idx": []}
+    hb["lo"] = lo
+    LS = _load_repo_module("loss") if chains else None
     stim = [len(rec["task"])]
     round_ptr = [0]
     rounds, nplaced = [], []
@@ -1449,6 +1477,10 @@ def main_resync(only):
         "svcwl_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=55, n_inner_prefixes=3,
                                                             random_durations=True, nthreads="random"), 1.1, 55, 0.1),
         "svcwl_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=56), float("inf"), 56, 0.1),
+        # ... whose lost results recompute released dependencies (recompute chains)
+        "svcwl_chain_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=57, n_inner_prefixes=3,
+                                                                  random_durations=True, nthreads="random"), 1.1, 57, 0.1),
+        "svcwl_chain_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=58), float("inf"), 58, 0.1),
     }
     for name, (mk, sat, seed, p_event) in cases.items():
         if only and name not in only:
@@ -1460,7 +1492,8 @@ def main_resync(only):
         dumps = []
         kinds_ = ((1, 2, 3, 4, 5, 6, 7, EV_RETIRE, EV_RETIRE, EV_PAUSE) if name.startswith("svcrt_") else
                   (1, 2, 3, 4, 5, 6, 7, EV_LOSE_WORKER, EV_LOSE_WORKER, EV_RESUME) if name.startswith("svcwl_") else kinds)
-        rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(g, cfg, seed, p_event, kinds_, dumps=dumps)
+        rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(g, cfg, seed, p_event, kinds_, dumps=dumps,
+                                                                        chains=name.startswith("svcwl_chain_"))
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -1472,10 +1505,15 @@ def main_resync(only):
                  hb_dur=np.array(hb["dur"], np.float64), ev_round_ptr=np.array(round_ptr, np.int64))
         if dumps:
             z.update(_pack_dumps(dumps))
+        lo = hb["lo"]
+        if lo["task"]:
+            z.update(lo_evptr=np.array(lo["evptr"], np.int64), lo_task=np.array(lo["task"], np.int32),
+                     lo_kind=np.array(lo["kind"], np.int8), lo_rowptr=np.array(lo["rowptr"], np.int64),
+                     lo_idx=np.array(lo["idx"], np.int32))
         np.savez_compressed(path, **z)
         cnt = np.bincount(np.array(ev["kind"]), minlength=16).tolist()
         print(f"{name}: {len(ev['kind'])} events (by kind {cnt}), {len(dumps)} resyncs, {len(rec['task'])} placements, "
-              f"{os.path.getsize(path) / 1e3:.0f} kB")
+              f"{len(lo['task'])} order rows, {os.path.getsize(path) / 1e3:.0f} kB")
 
 
 def main():

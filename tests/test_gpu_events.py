@@ -47,6 +47,15 @@ def sync_dump(z, j):
     return out
 
 
+def loss_order_rows(z, i):
+    """The set-order rows of loss event i (svcwl_chain_*: gen_service.py records what
+    distributed_amd.loss.loss_orders gave in the generating process), as (task, kind, tasks)."""
+    if "lo_evptr" not in z.files:
+        return ()
+    ep, rp, idx = z["lo_evptr"], z["lo_rowptr"], z["lo_idx"]
+    return [(int(z["lo_task"][r]), int(z["lo_kind"][r]), idx[rp[r]:rp[r + 1]].tolist()) for r in range(ep[i], ep[i + 1])]
+
+
 def drive_events(eng, g, z, exp=None):
     """Every event of a svcev_* stream through the engine, snapshot per round; returns the
     placements each event made (update_graph's first)."""
@@ -88,7 +97,7 @@ def drive_events(eng, g, z, exp=None):
             elif kd == EV_LOSE_WORKER:  # the whole remove_worker stimulus on the device
                 lst = ht[hp[i]:hp[i + 1]]
                 npr = int(x[i])
-                assert eng.lose_worker(w, lst[:npr], lst[npr:]) is not None, (i, eng.refusal)
+                assert eng.lose_worker(w, lst[:npr], lst[npr:], loss_order_rows(z, i)) is not None, (i, eng.refusal)
             elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
                 # the scheduler decided this stimulus itself: its placements, then its state
                 n = int(exp["stim_nplaced"][len(stim)])
@@ -192,7 +201,8 @@ def test_service_worker_loss_on_the_engine(name):
     recomputed, their processing dependents released to wait for them), decided by the
     engine (dgp_lose_worker) with no resync, interleaved with every modelled event: the
     placements each loss made, every later decision, the snapshots and the final states
-    equal the reference's."""
+    equal the reference's. svcwl_chain_*: the lost results recompute released dependencies
+    in turn (recompute chains, in the scheduler's set orders: dgp_lose_worker_ordered)."""
     from distributed_amd.engine import PlacementEngine
 
     path = os.path.join(GOLDEN, name)
