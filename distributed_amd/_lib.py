@@ -79,7 +79,8 @@ SIGNATURES = {
     "dgp_task_erred": (C.c_int, [_P, C.c_int32, _P]),
     "dgp_remove_worker": (C.c_int, [_P, C.c_int32]),
     "dgp_lose_worker": (C.c_int, [_P, C.c_int32, C.c_int64, _P, C.c_int64, _P, _P]),
-    "dgp_lose_worker_ordered": (C.c_int, [_P, C.c_int32, C.c_int64, _P, C.c_int64, _P, C.c_int64, _P, _P, _P, _P, _P]),
+    "dgp_lose_worker_ordered": (C.c_int, [_P, C.c_int32, C.c_int64, _P, _P, C.c_int64, _P, C.c_int64, _P, _P, _P, _P,
+                                          _P]),
     "dgp_steal_order": (C.c_int, [_P, C.c_int64, _P, _P]),
     "dgp_set_window": (C.c_int, [_P, C.c_int32]),
     "dgp_get_window": (C.c_int, [_P]),

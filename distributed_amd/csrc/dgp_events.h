@@ -34,6 +34,11 @@ using st::NL_OVF;
 using st::SCtl;
 using st::nbv;
 
+// An erred task left its dependencies' waiters (:2593-2598) but the stream engine's builder
+// counts every completion down on every dependent: a count no completion takes to zero
+// keeps it off the frontier when a dependency is recomputed later
+constexpr int32_t ERRED_REMAINING = 1 << 30;
+
 __device__ __forceinline__ void ev_init(SCtl& S) {
   if (lane_id() == 0) {
     S.error = 0;
@@ -322,7 +327,10 @@ __global__ void __launch_bounds__(64) k_ev_task_erred(const Dev* __restrict__ Dp
     s_ok = ok ? 1 : 0;
     if (ok) {
       // waiting -> released -> erred for the closure but t (TaskGroup states :1464-1469)
-      for (long long i = 1; i < qn; i++) atomicAdd((unsigned long long*)&D.g_relwait[D.group[Q[i]]], (unsigned long long)-1ll);
+      for (long long i = 1; i < qn; i++) {
+        atomicAdd((unsigned long long*)&D.g_relwait[D.group[Q[i]]], (unsigned long long)-1ll);
+        D.remaining[Q[i]] = ERRED_REMAINING;  // (see ERRED_REMAINING)
+      }
       D.ready_key[0] = (unsigned long long)rn;  // the releases, applied after the worker's part
     }
   }
@@ -413,13 +421,14 @@ __global__ void __launch_bounds__(64) k_ev_task_erred(const Dev* __restrict__ Dp
 // recommendation stack (task, finish), D.ready_key = each task's place in it (-1: absent,
 // set by the host before the launch), D.release_key = the tasks marked TD_READD / TD_REWAIT
 // (the round engine's key, unused by the stream engine).
-enum : int { RC_RELEASED = 0, RC_WAITING = 1, RC_PROCESSING = 2 };
+enum : int { RC_RELEASED = 0, RC_WAITING = 1, RC_PROCESSING = 2, RC_ERRED = 3 };
 
 // The scheduler's iteration orders the cascade follows where the engine's own (index order)
 // differs: row i names task[i] and what it iterates, kind 0 its dependencies
 // (_transition_released_waiting :2101, a set), kind 1 its waiters (_transition_memory_released
-// :2494, a set); rows sorted by (task, kind), checked by the host (dgp_lose_worker_ordered).
-enum : int { LO_DEPS = 0, LO_WAITERS = 1 };
+// :2494 / :2711, a set), kind 2 its dependents (_transition_released_erred :2519, a set);
+// rows sorted by (task, kind), checked by the host (dgp_lose_worker_ordered).
+enum : int { LO_DEPS = 0, LO_WAITERS = 1, LO_DEPENDENTS = 2 };
 struct LossOrder {
   const int32_t* task;
   const int8_t* kind;
@@ -549,6 +558,52 @@ __device__ void loss_released_waiting(const Dev& D, const LossOrder& O, long lon
   if (wo == 0) rec_push(D, sp, t, RC_PROCESSING);
 }
 
+// dts.waiters.discard(ts) for each dependency of ts that is not erred, and a release
+// recommended for one left without waiters and not wanted (:2715-2718, :2593-2598): only a
+// dependency in memory is restated (its release frees its replicas)
+__device__ bool loss_discard_waiter(const Dev& D, const LossOrder& O, long long& sp, int t) {
+  int64_t a = D.dep_ptr[t], b = D.dep_ptr[t + 1];
+  const int32_t* row = D.dep_idx;
+  if (O.row(t, LO_DEPS, &a, &b)) row = O.idx;
+  for (int64_t k = a; k < b; k++) {
+    const int d = row[k];
+    if (D.state[d] == S_ERRED) continue;  // an erred task has no waiters (:2720)
+    if (D.waiters[d] > 0) D.waiters[d] -= 1;
+    if (D.waiters[d] == 0 && !(D.tflags[d] & TF_WANTED)) {
+      if (D.state[d] != S_MEMORY) {  // the cascade would release a waiting / processing task
+        set_error(D, ERR_UNSUPPORTED, d);
+        return false;
+      }
+      rec_push(D, sp, d, RC_RELEASED);
+    }
+  }
+  return true;
+}
+
+// Scheduler.remove_worker's KilledWorker (:5239-5265): processing -> erred of t at once, in
+// the processing loop (:2630-2720): it leaves the removed worker, its waiters are recommended
+// to erred, its dependencies drop it as a waiter
+__device__ bool loss_killed(const Dev& D, const LossOrder& O, long long& sp, int t, int lost_w) {
+  loss_exit_processing(D, t, lost_w);
+  D.state[t] = S_ERRED;
+  int64_t a = D.dpt_ptr[t], b = D.dpt_ptr[t + 1];
+  const int32_t* row = D.dpt_idx;
+  if (O.row(t, LO_WAITERS, &a, &b)) row = O.idx;  // ts.waiters' set order
+  for (int64_t k = a; k < b; k++) {
+    const int y = row[k];
+    const uint8_t sy = D.state[y];
+    if (sy == S_WAITING) {
+      rec_push(D, sp, y, RC_ERRED);
+    } else if (!(sy == S_MEMORY || sy == S_ERRED || sy == S_RELEASED || (D.tflags[y] & TF_FORGOTTEN))) {
+      set_error(D, ERR_UNSUPPORTED, y);  // a processing / queued / no-worker dependent
+      return false;
+    }
+  }
+  if (!loss_discard_waiter(D, O, sp, t)) return false;
+  D.waiters[t] = 0;  // ts.waiters = None
+  return true;
+}
+
 // lane 0: pop recommendations until one is a placement (returns its task) or none is left
 // (-1). ERR_UNSUPPORTED stops the machine.
 __device__ int loss_machine(const Dev& D, const LossOrder& O, long long& sp, long long& nmark, int lost_w) {
@@ -560,8 +615,28 @@ __device__ int loss_machine(const Dev& D, const LossOrder& O, long long& sp, lon
     at[t] = -1;
     const uint8_t st = D.state[t];
     if ((v == RC_RELEASED && st == S_RELEASED) || (v == RC_WAITING && st == S_WAITING) ||
-        (v == RC_PROCESSING && st == S_PROCESSING))
+        (v == RC_PROCESSING && st == S_PROCESSING) || (v == RC_ERRED && st == S_ERRED))
       continue;  // start == finish (:1936-1937)
+    if (st == S_WAITING && v == RC_ERRED) {
+      // waiting -> released (:2579-2605: its dependencies drop it; exception_blame is set, so
+      // no recommendation for itself and ts.waiters = None), then released -> erred
+      // (:2507-2537: every dependent without a replica is recommended to erred)
+      if (!loss_discard_waiter(D, O, sp, t)) break;
+      D.waiters[t] = 0;
+      D.remaining[t] = ERRED_REMAINING;
+      D.state[t] = S_ERRED;
+      atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], (unsigned long long)-1ll);
+      int64_t a = D.dpt_ptr[t], b = D.dpt_ptr[t + 1];
+      const int32_t* row = D.dpt_idx;
+      if (O.row(t, LO_DEPENDENTS, &a, &b)) row = O.idx;  // ts.dependents' set order
+      for (int64_t k = a; k < b; k++) {
+        const int y = row[k];
+        bool held = false;
+        for (int w = 0; w < D.WB && !held; w++) held = D.holders[(size_t)y * D.WB + w] != 0;
+        if (!held && !(D.tflags[y] & TF_FORGOTTEN)) rec_push(D, sp, y, RC_ERRED);
+      }
+      continue;
+    }
     const bool needed = D.waiters[t] > 0 || (D.tflags[t] & TF_WANTED);
     if (st == S_PROCESSING && (v == RC_RELEASED || v == RC_WAITING)) {
       loss_exit_processing(D, t, lost_w);
@@ -579,7 +654,26 @@ __device__ int loss_machine(const Dev& D, const LossOrder& O, long long& sp, lon
       loss_released_waiting(D, O, sp, nmark, t);
       continue;
     }
-    if (st == S_MEMORY && v == RC_RELEASED) {  // a lost result (:2444-2505): no replica is left
+    if (st == S_NO_WORKER && v == RC_WAITING) {  // through released: _transition_no_worker_released :2747-2759
+      D.ctl->n_unrunnable--;  // unrunnable.remove
+      D.state[t] = S_RELEASED;
+      atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], 1ull);
+      if (!needed) {  // _propagate_released would release its dependencies (:3346-3353)
+        set_error(D, ERR_UNSUPPORTED, t);
+        break;
+      }
+      rec_push(D, sp, t, RC_WAITING);
+      loss_released_waiting(D, O, sp, nmark, t);
+      continue;
+    }
+    if (st == S_MEMORY && v == RC_RELEASED) {  // :2444-2505: a lost result, or a release
+      // remove_all_replicas (:2475): the holders left (none for a lost result)
+      for (int w = 0; w < D.WB; w++) {
+        unsigned long long m = D.holders[(size_t)t * D.WB + w];
+        D.holders[(size_t)t * D.WB + w] = 0;
+        for (; m; m &= m - 1) D.w_nbytes[w * 64 + __builtin_ctzll(m)] -= res_nb(D, t);
+      }
+      D.tdyn[t] &= (uint8_t)~TD_MULTI;
       D.state[t] = S_RELEASED;
       D.holder_of[t] = -1;
       atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], 1ull);
@@ -590,6 +684,7 @@ __device__ int loss_machine(const Dev& D, const LossOrder& O, long long& sp, lon
       int64_t a = D.dpt_ptr[t], b = D.dpt_ptr[t + 1];
       const int32_t* row = D.dpt_idx;
       if (O.row(t, LO_WAITERS, &a, &b)) row = O.idx;  // the scheduler's set order of ts.waiters
+      if (D.waiters[t] == 0) b = a;                   // ts.waiters is empty
       for (int64_t k = a; k < b; k++) {  // its waiters (:2494-2500)
         const int y = row[k];
         const uint8_t sy = D.state[y];
@@ -597,7 +692,11 @@ __device__ int loss_machine(const Dev& D, const LossOrder& O, long long& sp, lon
           rec_push(D, sp, y, RC_WAITING);
         } else if (sy == S_WAITING) {
           if (!(D.tdyn[y] & TD_REWAIT)) D.remaining[y] += 1;  // waiting_on.add (a set)
-        } else if (sy == S_QUEUED || sy == S_NO_WORKER) {
+        } else if (sy == S_NO_WORKER) {
+          rec_push(D, sp, y, RC_WAITING);
+        } else if (sy == S_QUEUED) {
+          // stays queued (:2494-2500 names neither) but no longer in ts.waiters once t is
+          // re-waited, while its completion would still count down the engine's count
           set_error(D, ERR_UNSUPPORTED, y);
           break;
         }
@@ -611,8 +710,9 @@ __device__ int loss_machine(const Dev& D, const LossOrder& O, long long& sp, lon
 }
 
 __global__ void __launch_bounds__(CTA) k_ev_lose_worker(const Dev* __restrict__ Dp, int w, const int32_t* __restrict__ proc,
-                                                        int n_proc, const int32_t* __restrict__ held, int n_held,
-                                                        LossOrder O, long long* placed) {
+                                                        int n_proc, const int8_t* __restrict__ killed,
+                                                        const int32_t* __restrict__ held, int n_held, LossOrder O,
+                                                        long long* placed) {
   __shared__ Dev s_dev;  // Dev and Ctl in LDS, as the update_graph dispatcher works on them
   __shared__ Ctl s_ctl;
   {
@@ -653,7 +753,10 @@ __global__ void __launch_bounds__(CTA) k_ev_lose_worker(const Dev* __restrict__ 
     }
     // the recommendations (:5235-5278): processing tasks, then the lost results
     long long sp = 0;
-    for (int i = 0; i < n_proc; i++) rec_push(D, sp, proc[i], RC_RELEASED);
+    for (int i = 0; i < n_proc && D.ctl->error == 0; i++) {
+      if (killed && killed[i]) loss_killed(D, O, sp, proc[i], w);  // KilledWorker: erred at once
+      else rec_push(D, sp, proc[i], RC_RELEASED);
+    }
     for (int i = 0; i < n_held; i++) {
       const int t = held[i];
       bool any = false;

@@ -2492,14 +2492,14 @@ int dgp_remove_worker(dgp_engine* e, int32_t worker) {
 
 int dgp_lose_worker(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing, int64_t n_held,
                     const int32_t* held, int64_t* n_new_placements) {
-  return dgp_lose_worker_ordered(e, worker, n_processing, processing, n_held, held, 0, nullptr, nullptr, nullptr, nullptr,
-                                 n_new_placements);
+  return dgp_lose_worker_ordered(e, worker, n_processing, processing, nullptr, n_held, held, 0, nullptr, nullptr,
+                                 nullptr, nullptr, n_new_placements);
 }
 
 int dgp_lose_worker_ordered(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing,
-                            int64_t n_held, const int32_t* held, int64_t n_order, const int32_t* order_task,
-                            const int8_t* order_kind, const int64_t* order_ptr, const int32_t* order_idx,
-                            int64_t* n_new_placements) {
+                            const int8_t* killed, int64_t n_held, const int32_t* held, int64_t n_order,
+                            const int32_t* order_task, const int8_t* order_kind, const int64_t* order_ptr,
+                            const int32_t* order_idx, int64_t* n_new_placements) {
   if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (int rc = event_ready(e, "dgp_lose_worker")) return rc;
@@ -2514,7 +2514,7 @@ int dgp_lose_worker_ordered(dgp_engine* e, int32_t worker, int64_t n_processing,
     for (int64_t i = 0; i < n_order; i++) {
       const int32_t t = order_task[i];
       const int k = order_kind[i];
-      if (t < 0 || t >= D.N || (k != dgp::ev::LO_DEPS && k != dgp::ev::LO_WAITERS) || order_ptr[i + 1] < order_ptr[i])
+      if (t < 0 || t >= D.N || k < dgp::ev::LO_DEPS || k > dgp::ev::LO_DEPENDENTS || order_ptr[i + 1] < order_ptr[i])
         return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: bad order row");
       if (i > 0 && (order_task[i - 1] > t || (order_task[i - 1] == t && order_kind[i - 1] >= k)))
         return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: order rows not sorted by (task, kind)");
@@ -2531,7 +2531,7 @@ int dgp_lose_worker_ordered(dgp_engine* e, int32_t worker, int64_t n_processing,
       } else {
         for (int32_t y : r)
           if (std::find(di.begin() + dp[y], di.begin() + dp[y + 1], t) == di.begin() + dp[y + 1])
-            return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: a waiters row names a task that does not depend on it");
+            return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: a waiters / dependents row names a task that does not depend on it");
       }
     }
   }
@@ -2557,7 +2557,8 @@ int dgp_lose_worker_ordered(dgp_engine* e, int32_t worker, int64_t n_processing,
   const int64_t n_oidx = n_order ? order_ptr[n_order] : 0;
   if (int rc = stage_args(e, {{processing, (size_t)n_processing * 4}, {held, (size_t)n_held * 4},
                               {order_task, (size_t)n_order * 4}, {order_kind, (size_t)n_order},
-                              {order_ptr, n_order ? (size_t)(n_order + 1) * 8 : 0}, {order_idx, (size_t)n_oidx * 4}},
+                              {order_ptr, n_order ? (size_t)(n_order + 1) * 8 : 0}, {order_idx, (size_t)n_oidx * 4},
+                              {killed, killed ? (size_t)n_processing : 0}},
                           a))
     return rc;
   dgp::ev::LossOrder O{(const int32_t*)a[2], (const int8_t*)a[3], (const int64_t*)a[4], (const int32_t*)a[5],
@@ -2565,7 +2566,8 @@ int dgp_lose_worker_ordered(dgp_engine* e, int32_t worker, int64_t n_processing,
   if (int rc = grow_logs(e, 0)) return rc;
   if (int rc = sync_dev(e)) return rc;
   hipLaunchKernelGGL(dgp::ev::k_ev_lose_worker, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev, worker,
-                     (const int32_t*)a[0], (int)n_processing, (const int32_t*)a[1], (int)n_held, O, e->d_aux + 3);
+                     (const int32_t*)a[0], (int)n_processing, killed ? (const int8_t*)a[6] : nullptr,
+                     (const int32_t*)a[1], (int)n_held, O, e->d_aux + 3);
   HIPCHK(e, hipGetLastError());
   if (int rc = set_runids(e)) return rc;
   long long placed = 0;

@@ -487,26 +487,37 @@ class PlacementEngine:
         """Scheduler.remove_worker's worker table part (distributed/scheduler.py:5213-5231)."""
         self._check(self.lib.dgp_remove_worker(self.h, int(worker)), "dgp_remove_worker")
 
-    def lose_worker(self, worker: int, processing, held, order=()) -> int | None:
+    def lose_worker(self, worker: int, processing, held, order=(), killed=None) -> int | None:
         """The whole Scheduler.remove_worker stimulus (distributed/scheduler.py:5180-5303) on
         the device (dgp_lose_worker_ordered): ``processing`` = the worker's processing tasks in
         the order the scheduler iterates them, ``held`` = its replicas in ws.has_what order,
         ``order`` = (task, kind, tasks) rows: the scheduler's iteration order of a task's
-        dependencies (kind 0) or waiters (kind 1) where the cascade follows a set
-        (``distributed_amd.loss.loss_orders``). Returns the placements it made, or None when
+        dependencies (kind 0), waiters (kind 1) or dependents (kind 2) where the cascade
+        follows a set (``distributed_amd.loss.loss_orders``), ``killed`` = a flag per
+        processing task that ran out of retries (KilledWorker: erred at once). Returns the
+        placements it made, or None when
         the engine leaves the stimulus to the scheduler (a cascade it does not restate);
         after a refusal from the device the scheduler's state follows by ``sync()`` as after
         remove_worker."""
         p, h = self._arr(processing, np.int32), self._arr(held, np.int32)
-        rows = sorted((int(t), int(k), list(map(int, seq))) for t, k, seq in order)
+        rows, seen = [], set()
+        for t, k, seq in order:  # one row per (task, kind): the first
+            if (int(t), int(k)) not in seen:
+                seen.add((int(t), int(k)))
+                rows.append((int(t), int(k), list(map(int, seq))))
+        rows.sort()
+        kf = None if killed is None or not any(killed) else self._arr(killed, np.int8)
+        if kf is not None and len(kf) != len(p):
+            raise ValueError("killed: one flag per processing task")
         ot = np.array([r[0] for r in rows], np.int32)
         ok = np.array([r[1] for r in rows], np.int8)
         op = np.zeros(len(rows) + 1, np.int64)
         op[1:] = np.cumsum([len(r[2]) for r in rows]) if rows else []
         oi = np.array([x for r in rows for x in r[2]], np.int32)
         newp = C.c_int64(0)
-        rc = self.lib.dgp_lose_worker_ordered(self.h, int(worker), len(p), _ptr(p), len(h), _ptr(h), len(rows),
-                                              _ptr(ot), _ptr(ok), _ptr(op), _ptr(oi), C.byref(newp))
+        rc = self.lib.dgp_lose_worker_ordered(self.h, int(worker), len(p), _ptr(p), None if kf is None else _ptr(kf),
+                                              len(h), _ptr(h), len(rows), _ptr(ot), _ptr(ok), _ptr(op), _ptr(oi),
+                                              C.byref(newp))
         if rc == self.UNSUPPORTED:
             self.refusal = (self.lib.dgp_last_error(self.h) or b"").decode()
             return None

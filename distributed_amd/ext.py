@@ -90,9 +90,11 @@ _ERRED_TRANSITIONS = frozenset({("processing", "erred"), ("waiting", "released")
                                 ("memory", "released"), ("queued", "processing")})
 # a worker lost with processing tasks / sole replicas (Scheduler.remove_worker :5233-5303):
 # processing -> released (-> waiting through released, :1961-1984), memory -> released for the
-# lost results, released -> waiting, then decide_worker
+# lost results and the recompute chains' released dependencies, released -> waiting, then
+# decide_worker; a no-worker waiter through released; a KilledWorker's erred cascade
 _LOSS_TRANSITIONS = frozenset({("processing", "released"), ("released", "waiting"), ("memory", "released"),
-                               ("waiting", "processing"), ("waiting", "queued"), ("waiting", "no-worker")})
+                               ("waiting", "processing"), ("waiting", "queued"), ("waiting", "no-worker"),
+                               ("no-worker", "released")}) | _ERRED_TRANSITIONS - {("queued", "processing")}
 
 # the placement inputs a stimulus other than task-finished / update_graph / add_worker can
 # change, and the engine method that follows each on the device (PlacementEngine); an engine
@@ -580,20 +582,22 @@ class GPUPlacementExtension(SchedulerPlugin):
         if not proc and not any(ts.who_has == {ws} for ts in held):
             return False  # a drained worker: no transition (the plugin hook follows it)
         ti = self.task_index
-        chain = None
+        plan = None
         if not (any(ts.key not in ti for ts in proc) or any(ts.who_has == {ws} and ts.key not in ti for ts in held)):
-            chain = loss.supported(s, ws, proc, held, safe)
-        # every task the cascade may re-wait or place is the engine's, with its prefix's slot
-        if chain is None or any(ts.key not in ti or ts.prefix.name not in self.prefix_index or ti[ts.key] in self._stale
-                                for ts in chain + loss.lost_results(ws, held)):
+            plan = loss.supported(s, ws, proc, held, safe)
+        # every task the cascade may re-wait, place or err is the engine's, with its prefix's slot
+        if plan is None or any(ts.key not in ti or ts.prefix.name not in self.prefix_index or ti[ts.key] in self._stale
+                               for ts in plan[0] + plan[1] + loss.lost_results(ws, held)):
             self.stats["losses_left_to_scheduler"] += 1
             return False
         self._end_of_stimulus("the previous stimulus")
         if not self.active:
             return False
-        order = loss.loss_orders(chain, lambda ts: ti[ts.key])
+        chain, erred = plan
+        killed = loss.killed_flags(s, proc, safe)
+        order = loss.loss_orders(chain, lambda ts: ti[ts.key], erred, sum(killed))
         n = self.engine.lose_worker(self.worker_index[address], [ti[ts.key] for ts in proc],
-                                    [ti[ts.key] for ts in held if ts.key in ti], order)
+                                    [ti[ts.key] for ts in held if ts.key in ti], order, killed)
         if n is None:  # refused: the scheduler decides, the engine resyncs after
             self._suspend(f"remove_worker({address}): {getattr(self.engine, 'refusal', 'refused by the engine')}")
             return False

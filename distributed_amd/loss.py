@@ -9,7 +9,8 @@ task re-waited there recomputes each released dependency in turn
 chain. Those recommendations enter the dict in ``ts.dependencies`` order -- a set, hashed by
 key -- and the dict is popped LIFO, so the order in which the chain's tasks are placed is the
 set's. The host passes that order for every task of the cascade with two or more
-dependencies (``loss_orders``).
+dependencies (``loss_orders``). A processing task out of retries errs at once
+(KilledWorker, :5239-5265), and its waiting dependents with it (``erred_closure``).
 
 Pure Python over duck-typed scheduler objects: the extension calls it on the live
 scheduler, ``tests/golden/gen_service.py`` on the reference, so the fixtures' order rows are
@@ -17,7 +18,40 @@ the extension's.
 """
 from __future__ import annotations
 
-LO_DEPS, LO_WAITERS = 0, 1  # dgp_events.h LossOrder kinds
+LO_DEPS, LO_WAITERS, LO_DEPENDENTS = 0, 1, 2  # dgp_events.h LossOrder kinds
+
+
+def killed_flags(s, proc, safe) -> list:
+    """Per processing task: it runs out of retries with this loss (KilledWorker,
+    scheduler.py:5239-5265: suspicious + 1 > allowed_failures when not safe)."""
+    return [bool(not safe and ts.suspicious + 1 > s.allowed_failures) for ts in proc]
+
+
+def erred_closure(killed, lost=frozenset()) -> list | None:
+    """The tasks the KilledWorker transitions err (each killed task, then every dependent
+    without a replica, transitively: :2711-2713, :2518-2521), killed ones first; None when the
+    engine does not restate that cascade -- a member besides the killed ones that is not
+    waiting, or a dependency it would release that is not in memory (its waiters all erred,
+    not wanted) or is a lost result (``lost``: recomputed first, then released by the erred
+    waiter -- a cascade the engine refuses)."""
+    out, seen, stack = list(killed), set(killed), list(killed)
+    while stack:
+        x = stack.pop()
+        for y in x.dependents:
+            if y not in seen and not y.who_has:
+                seen.add(y)
+                out.append(y)
+                stack.append(y)
+    for x in out[len(killed):]:
+        if x.state != "waiting":
+            return None
+    for x in out:
+        for d in x.dependencies:
+            if d in seen:
+                continue
+            if not (d.waiters or set()) - seen and not d.who_wants and (d.state != "memory" or d in lost):
+                return None
+    return out
 
 
 def lost_results(ws, held) -> list:
@@ -25,16 +59,16 @@ def lost_results(ws, held) -> list:
     return [ts for ts in held if ts.who_has == {ws}]
 
 
-def cascade(ws, proc, held):
+def cascade(ws, proc, held, killed=()):
     """The tasks whose ``released -> waiting`` the loss may run -- the processing tasks, the
-    lost results that are needed, their processing waiters, and every released or lost
+    lost results that are needed, their processing / no-worker waiters, and every released or lost
     dependency those recompute, transitively -- in discovery order; None when one of them is
     a case the engine does not restate (an erred or forgotten dependency, a chain task without
     run_spec or with lost dependencies, an actor)."""
     lost = lost_results(ws, held)
     lostset = set(lost)
-    stack = list(proc) + [ts for ts in lost if ts.who_wants or ts.waiters]
-    stack += [y for ts in lost for y in (ts.waiters or ()) if y.state == "processing"]
+    stack = [ts for ts in proc if ts not in killed] + [ts for ts in lost if ts.who_wants or ts.waiters]
+    stack += [y for ts in lost for y in (ts.waiters or ()) if y.state in ("processing", "no-worker") and y not in killed]
     out, seen = [], set()
     while stack:
         t = stack.pop()
@@ -52,32 +86,51 @@ def cascade(ws, proc, held):
     return out
 
 
-def supported(s, ws, proc, held, safe) -> list | None:
-    """The cascade (see ``cascade``) when dgp_lose_worker_ordered restates the loss, else None:
-    no processing task that errs (KilledWorker, :5239-5265) or that nobody needs, no lost
-    result without run_spec or with a queued / no-worker waiter."""
-    for ts in proc:
-        if (not safe and ts.suspicious + 1 > s.allowed_failures) or not (ts.waiters or ts.who_wants):
-            return None
+def supported(s, ws, proc, held, safe) -> tuple | None:
+    """(the re-wait cascade, the erred closure) when dgp_lose_worker_ordered restates the
+    loss (see ``cascade`` / ``erred_closure``), else None: no processing task that nobody
+    needs, no KilledWorker cascade outside ``erred_closure``, no lost result without run_spec,
+    with a queued waiter, or with a processing / no-worker waiter nobody needs (its release
+    would release its own dependencies)."""
+    kf = killed_flags(s, proc, safe)
+    killed = [ts for ts, k in zip(proc, kf) if k]
+    for ts, k in zip(proc, kf):
         if ts.actor or ts.has_lost_dependencies:
             return None
+        if not k and not (ts.waiters or ts.who_wants):
+            return None
+    ks = set(killed)
     for ts in lost_results(ws, held):
         if not ts.run_spec or ts.actor or ts.has_lost_dependencies:
             return None
         for d in ts.waiters or ():
-            if d.state in ("queued", "no-worker"):
+            if d in ks:
+                continue
+            if d.state == "queued":  # leaves ts.waiters at the recompute yet stays queued
                 return None
-            if d.state == "processing" and not (d.waiters or d.who_wants):
+            if d.state in ("processing", "no-worker") and not (d.waiters or d.who_wants):
                 return None
-    return cascade(ws, proc, held)
+    erred = erred_closure(killed, set(lost_results(ws, held))) if killed else []
+    if erred is None:
+        return None
+    chain = cascade(ws, proc, held, ks)
+    if chain is None or set(chain) & set(erred):
+        return None
+    return chain, erred
 
 
-def loss_orders(tasks, index_of) -> list:
-    """(task, LO_DEPS, dependencies) rows in the engine's numbering for every task of the
-    cascade with two or more dependencies, in the order this process iterates the sets."""
+def loss_orders(tasks, index_of, erred=(), n_killed=0) -> list:
+    """The (task, kind, tasks) rows in the engine's numbering, in the order this process
+    iterates the sets: LO_DEPS for every task of the re-wait cascade and of the erred closure
+    with two or more dependencies; for the erred closure also LO_WAITERS of each killed task
+    (its first ``n_killed``) and LO_DEPENDENTS of the others, with two or more members."""
     rows = []
-    for t in tasks:
+    for t in list(tasks) + list(erred):
         deps = t.dependencies
         if len(deps) >= 2:
             rows.append((index_of(t), LO_DEPS, [index_of(d) for d in deps]))
+    for i, t in enumerate(erred):
+        kin = (LO_WAITERS, t.waiters or ()) if i < n_killed else (LO_DEPENDENTS, t.dependents)
+        if len(kin[1]) >= 2:
+            rows.append((index_of(t), kin[0], [index_of(y) for y in kin[1]]))
     return rows

@@ -410,19 +410,26 @@ int dgp_remove_worker(dgp_engine* e, int32_t worker);
  * takes the scheduler's state (dgp_sync_*) as after dgp_remove_worker. */
 int dgp_lose_worker(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing, int64_t n_held,
                     const int32_t* held, int64_t* n_new_placements);
-/* dgp_lose_worker_ordered (ABI 21): dgp_lose_worker, and a released dependency of a task the
- * cascade re-waits is recomputed in turn (_transition_released_waiting :2101-2106: a chain of
- * recomputes back to results still in memory). Where the recommendations' order follows a
- * Python set, the caller passes the scheduler's iteration order: rows i = 0..n_order-1,
- * sorted by (order_task, order_kind), name order_idx[order_ptr[i], order_ptr[i+1]) as
- * order_task[i]'s dependencies (kind 0: ts.dependencies, a permutation of its row) or its
- * waiters (kind 1: ts.waiters of a lost result, dependents of it); a task without a row
- * iterates in index order. dgp_lose_worker is this call with no rows. DGP_E_UNSUPPORTED as
- * there (KilledWorker, a queued / no-worker dependent, an erred or forgotten dependency). */
+/* dgp_lose_worker_ordered (ABI 21): dgp_lose_worker, and
+ *  - a released dependency of a task the cascade re-waits is recomputed in turn
+ *    (_transition_released_waiting :2101-2106: a chain of recomputes back to results still in
+ *    memory); a no-worker waiter of a lost result is re-waited like a processing one;
+ *  - killed[i] != 0 (NULL: none): processing[i] ran out of retries (KilledWorker, :5239-5265):
+ *    processing -> erred at once in the processing loop (:2630-2720), its waiting dependents
+ *    erred in turn (waiting -> released -> erred :2579-2605, :2507-2537) and a dependency in
+ *    memory that nobody waits for any more released with its replicas (:2444-2505).
+ * Where the recommendations' order follows a Python set, the caller passes the scheduler's
+ * iteration order: rows i = 0..n_order-1, sorted by (order_task, order_kind), name
+ * order_idx[order_ptr[i], order_ptr[i+1]) as order_task[i]'s dependencies (kind 0:
+ * ts.dependencies, a permutation of its row), its waiters (kind 1: ts.waiters, dependents of
+ * it) or its dependents (kind 2: ts.dependents); a task without a row iterates in index
+ * order. dgp_lose_worker is this call with no rows and nothing killed. DGP_E_UNSUPPORTED as
+ * there (a queued waiter of a lost result; an erred cascade that reaches a processing / queued
+ * task or would release one that is not in memory; an erred or forgotten dependency). */
 int dgp_lose_worker_ordered(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing,
-                            int64_t n_held, const int32_t* held, int64_t n_order, const int32_t* order_task,
-                            const int8_t* order_kind, const int64_t* order_ptr, const int32_t* order_idx,
-                            int64_t* n_new_placements);
+                            const int8_t* killed, int64_t n_held, const int32_t* held, int64_t n_order,
+                            const int32_t* order_task, const int8_t* order_kind, const int64_t* order_ptr,
+                            const int32_t* order_idx, int64_t* n_new_placements);
 int dgp_sync_placements(dgp_engine* e, int64_t n, const int32_t* task, const int32_t* worker, const int64_t* comm_bytes,
                         const double* start_time, const int64_t* ws_nbytes, const int8_t* route);
 int dgp_sync_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t* state, const int32_t* remaining,

@@ -963,6 +963,7 @@ class EventEngine(FixtureEngine):
         super().__init__(exp, fixture_keys)
         self.calls = []
         self.loss_orders = []  # the order rows of each lose_worker call
+        self.loss_killed = []  # ... and its killed processing tasks
 
     def _event(self, *call):
         assert self._posted is None, f"{call[0]} while a task-finished batch is posted"  # the engine refuses it
@@ -985,10 +986,11 @@ class EventEngine(FixtureEngine):
     def set_worker_status(self, w, running):
         return self._event("status", int(w), int(running))
 
-    def lose_worker(self, w, processing, held, order=()):  # dgp_lose_worker_ordered: the fixture's placements
-        for s_ in self.who.values():
+    def lose_worker(self, w, processing, held, order=(), killed=None):  # dgp_lose_worker_ordered
+        for s_ in self.who.values():  # (the fixture's placements of that event)
             s_.discard(int(w))
         self.loss_orders.append([(int(t), int(k), [int(q) for q in seq]) for t, k, seq in order])
+        self.loss_killed.append(sorted(int(t) for t, k in zip(processing, killed or ()) if k))
         return self._event("lose", int(w), [int(x) for x in processing], [int(x) for x in held])
 
     def long_running(self, t, cd):
@@ -1100,6 +1102,7 @@ def run_events(name, plain=False):
         from distributed.core import Status
 
         S.remove_worker = Scheduler.remove_worker
+        S.transition = Scheduler.transition  # a KilledWorker's processing -> erred (:5249-5256)
         S._reschedule = Scheduler._reschedule
         S.client_releases_keys = Scheduler.client_releases_keys
         S.remove_resources = lambda self, address: None
@@ -1113,7 +1116,8 @@ def run_events(name, plain=False):
             hh["addresses"].add(a)
             hh["nthreads"] += ws.nthreads
         s.total_nthreads_history = []
-        s.allowed_failures = 3
+        nm_ = os.path.basename(path)  # as gen_service.loss_allowed_failures
+        s.allowed_failures = 0 if nm_.startswith("svcwl_killed0_") else 1 if nm_.startswith("svcwl_killed_") else 3
         s.bandwidth_workers = {}
         s.events = {}
         s._ongoing_background_tasks = NS(closed=False, call_later=lambda *a, **k: None)
@@ -1286,7 +1290,10 @@ def run_events(name, plain=False):
                 ep, rp, li = z["lo_evptr"], z["lo_rowptr"], z["lo_idx"]
                 rows = [(int(z["lo_task"][r]), int(z["lo_kind"][r]), li[rp[r]:rp[r + 1]].tolist())
                         for r in range(ep[i], ep[i + 1])]
-                assert sorted(eng.loss_orders[-1]) == sorted(rows), (i, eng.loss_orders[-1], rows)
+                assert sorted(set((t, k, tuple(q)) for t, k, q in eng.loss_orders[-1])) == \
+                    sorted(set((t, k, tuple(q)) for t, k, q in rows)), (i, eng.loss_orders[-1], rows)
+                kp = z["lo_kptr"]
+                assert eng.loss_killed[-1] == sorted(z["lo_ktask"][kp[i]:kp[i + 1]].tolist()), i
         elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
             if kd == EV_REMOVE_WORKER:
                 lw0 = ext.stats["workers_lost_on_device"]

@@ -926,7 +926,8 @@ def _erred_is_simple(s, ts):
     return all(x is ts or x.state == "waiting" for x in closure)
 
 
-def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_scale=0.3, dumps=None, chains=False):
+def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_scale=0.3, dumps=None, chains=False,
+                  allowed_failures=3):
     """The replay protocol's completions as task-finished messages, interleaved with the
     other worker stimuli that change placement inputs, each through the reference's own
     handler (``Scheduler.*`` borrowed onto the replay state):
@@ -951,10 +952,11 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
     heartbeat's executing tasks and durations (CSR ``hb_ptr`` / ``hb_task`` / ``hb_dur``), and
     the placements each event made (``stim_nplaced``: update_graph first).
 
-    ``chains``: worker losses may recompute released dependencies (distributed_amd/loss.py);
-    each loss event's order rows (the set orders the cascade follows, as loss_orders gives
-    them in this process) go to ``hb["lo"]``: CSR over events (``evptr``) into rows (``task``,
-    ``kind``, ``rowptr`` into ``idx``)."""
+    ``chains``: worker losses may recompute released dependencies and err tasks out of retries
+    (KilledWorker: ``allowed_failures``), as distributed_amd/loss.py accepts them; each loss
+    event's order rows (the set orders the cascade follows, as loss_orders gives them in this
+    process) go to ``hb["lo"]``: CSR over events (``evptr``) into rows (``task``, ``kind``,
+    ``rowptr`` into ``idx``), and its killed processing tasks (``kptr`` into ``ktask``)."""
     from distributed.scheduler import Scheduler
 
     s, tss, widx, rec, tidx = G.build_state(g, cfg)
@@ -982,6 +984,7 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
         from distributed.comm.addressing import get_address_host
 
         S.remove_worker = Scheduler.remove_worker
+        S.transition = Scheduler.transition  # a KilledWorker's processing -> erred (:5249-5256)
         S.remove_resources = lambda self, address: None
         S.coerce_address = lambda self, a, resolve=True: a
         s.status = Status.running
@@ -993,7 +996,7 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             h["addresses"].add(a)
             h["nthreads"] += ws.nthreads
         s.total_nthreads_history = []
-        s.allowed_failures = 3
+        s.allowed_failures = allowed_failures
         s.bandwidth_workers = {}
         s.events = {}
         s._ongoing_background_tasks = NS(closed=False, call_later=lambda *a, **k: None)
@@ -1009,7 +1012,7 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
     s._transitions(recs, {}, {}, "update-graph")
     ev = {k: [] for k in ("kind", "task", "worker", "x", "nbytes", "start", "stop", "runid")}
     hb = {"ptr": [0], "task": [], "dur": []}
-    lo = {"evptr": [0], "task": [], "kind": [], "rowptr": [0], "idx": []}
+    lo = {"evptr": [0], "task": [], "kind": [], "rowptr": [0], "idx": [], "kptr": [0], "ktask": []}
     hb["lo"] = lo
     LS = _load_repo_module("loss") if chains else None
     stim = [len(rec["task"])]
@@ -1024,6 +1027,7 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             ev[k].append(v)
         hb["ptr"].append(len(hb["task"]))
         lo["evptr"].append(len(lo["task"]))
+        lo["kptr"].append(len(lo["ktask"]))
 
     def event():
         kind = int(rng.choice(kinds))
@@ -1115,7 +1119,8 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
                     if c is not None:
                         cand.append(i)
                         casc[i] = c
-                        if any(t.state == "released" for t in c):  # recomputes a released dependency
+                        # recomputes a released dependency, or errs a task out of retries
+                        if any(t.state == "released" for t in c[0]) or c[1]:
                             chained.append(i)
                 elif _loss_is_supported(s, ws):
                     cand.append(i)
@@ -1125,19 +1130,32 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             w = pick[int(rng.integers(0, len(pick)))]
             ws = s.workers[addr[w]]
             if chains:
-                for t, k, seq in LS.loss_orders(casc[w], lambda ts: tidx[ts.key]):
+                kf = LS.killed_flags(s, list(ws.processing), False)
+                for t, k, seq in LS.loss_orders(casc[w][0], lambda ts: tidx[ts.key], casc[w][1], sum(kf)):
                     lo["task"].append(t)
                     lo["kind"].append(k)
                     lo["idx"].extend(seq)
                     lo["rowptr"].append(len(lo["idx"]))
+                lo["ktask"].extend(tidx[ts.key] for ts, k in zip(ws.processing, kf) if k)
             proc = [tidx[ts.key] for ts in ws.processing]  # the order remove_worker iterates (:5236)
             held = [tidx[ts.key] for ts in ws.has_what]  # ... and :5270
+            if os.environ.get("DGP_DEBUG_STATES"):
+                watch = [int(x) for x in os.environ["DGP_DEBUG_STATES"].split(",") if x]
+                before = {t: (tss[t].state, sorted(widx[h.address] for h in tss[t].who_has or ()),
+                              len(tss[t].waiters or ())) for t in watch}
             loop.run_until_complete(s.remove_worker(addr[w], stimulus_id=sid))
+            if os.environ.get("DGP_DEBUG_STATES"):
+                print("LOSS", len(hb.get("dbg", [])), "worker", w, "proc", proc, "held", held, flush=True)
+                for t in watch:
+                    print("   ", t, before[t], "->", (tss[t].state, sorted(widx[h.address] for h in tss[t].who_has or ()),
+                                                     len(tss[t].waiters or ())), flush=True)
             removed.add(w)
             paused.discard(w)
             hb["task"].extend(proc + held)
             hb["dur"].extend([0.0] * (len(proc) + len(held)))
             push(EV_LOSE_WORKER, -1, w, float(len(proc)))
+            if os.environ.get("DGP_DEBUG_STATES"):  # diagnostics: the states after each loss
+                hb.setdefault("dbg", []).append(np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8))
         elif kind == EV_RETIRE:
             cand = [i for i in sorted(paused) if i not in removed and not s.workers[addr[i]].processing]
             live = [i for i in range(W) if i not in removed and i not in paused]
@@ -1318,7 +1336,7 @@ def replay_p2p(g, cfg, dumps):
     s._transitions(recs, {}, {}, "update-graph")
     ev = {k: [] for k in ("kind", "task", "worker", "x", "nbytes", "start", "stop", "runid")}
     hb = {"ptr": [0], "task": [], "dur": []}
-    lo = {"evptr": [0], "task": [], "kind": [], "rowptr": [0], "idx": []}
+    lo = {"evptr": [0], "task": [], "kind": [], "rowptr": [0], "idx": [], "kptr": [0], "ktask": []}
     hb["lo"] = lo
     LS = _load_repo_module("loss") if chains else None
     stim = [len(rec["task"])]
@@ -1461,6 +1479,11 @@ def main_events(only):
         print(f"{name}: {len(ev['kind'])} events (by kind {cnt}), {len(rec['task'])} placements")
 
 
+def loss_allowed_failures(name):
+    """Scheduler.allowed_failures of a loss stream (tests/ext_driver.py sets the same)."""
+    return 0 if name.startswith("svcwl_killed0_") else 1 if name.startswith("svcwl_killed_") else 3
+
+
 def main_resync(only):
     """svcrs_*: the event streams plus the stimuli the engine does not model (worker removal,
     rescheduling, client releases), each followed by the scheduler's state (resync rows)."""
@@ -1481,6 +1504,13 @@ def main_resync(only):
         "svcwl_chain_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=57, n_inner_prefixes=3,
                                                                   random_durations=True, nthreads="random"), 1.1, 57, 0.1),
         "svcwl_chain_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=58), float("inf"), 58, 0.1),
+        # ... and tasks out of retries (allowed_failures 1: a task on its second lost worker errs)
+        "svcwl_killed_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=59, n_inner_prefixes=3,
+                                                                   random_durations=True, nthreads="random"), 1.1, 59, 0.12),
+        "svcwl_killed_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=60), float("inf"), 60, 0.12),
+        # allowed_failures 0: every processing task of a lost worker errs
+        "svcwl_killed0_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=61, n_inner_prefixes=3,
+                                                                    random_durations=True, nthreads="random"), 1.1, 61, 0.12),
     }
     for name, (mk, sat, seed, p_event) in cases.items():
         if only and name not in only:
@@ -1492,8 +1522,9 @@ def main_resync(only):
         dumps = []
         kinds_ = ((1, 2, 3, 4, 5, 6, 7, EV_RETIRE, EV_RETIRE, EV_PAUSE) if name.startswith("svcrt_") else
                   (1, 2, 3, 4, 5, 6, 7, EV_LOSE_WORKER, EV_LOSE_WORKER, EV_RESUME) if name.startswith("svcwl_") else kinds)
-        rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(g, cfg, seed, p_event, kinds_, dumps=dumps,
-                                                                        chains=name.startswith("svcwl_chain_"))
+        rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(
+            g, cfg, seed, p_event, kinds_, dumps=dumps, chains=name.startswith(("svcwl_chain_", "svcwl_killed")),
+            allowed_failures=loss_allowed_failures(name))
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -1506,14 +1537,17 @@ def main_resync(only):
         if dumps:
             z.update(_pack_dumps(dumps))
         lo = hb["lo"]
-        if lo["task"]:
+        if lo["task"] or lo["ktask"]:
             z.update(lo_evptr=np.array(lo["evptr"], np.int64), lo_task=np.array(lo["task"], np.int32),
                      lo_kind=np.array(lo["kind"], np.int8), lo_rowptr=np.array(lo["rowptr"], np.int64),
-                     lo_idx=np.array(lo["idx"], np.int32))
+                     lo_idx=np.array(lo["idx"], np.int32), lo_kptr=np.array(lo["kptr"], np.int64),
+                     lo_ktask=np.array(lo["ktask"], np.int32))
         np.savez_compressed(path, **z)
+        if hb.get("dbg"):
+            np.save(os.path.join(HERE, f"_dbg_{name}.npy"), np.stack(hb["dbg"]))
         cnt = np.bincount(np.array(ev["kind"]), minlength=16).tolist()
         print(f"{name}: {len(ev['kind'])} events (by kind {cnt}), {len(dumps)} resyncs, {len(rec['task'])} placements, "
-              f"{len(lo['task'])} order rows, {os.path.getsize(path) / 1e3:.0f} kB")
+              f"{len(lo['task'])} order rows, {len(lo['ktask'])} killed, {os.path.getsize(path) / 1e3:.0f} kB")
 
 
 def main():

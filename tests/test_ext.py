@@ -230,9 +230,11 @@ def test_extension_runs_worker_losses_on_the_engine():
     decisions, validate=True re-derives each; no resync, every placement the engine's.
     svcwl_chain_*: lost results whose dependencies were released recompute them in turn; the
     extension passes the set orders the cascade follows (distributed_amd/loss.py), equal to
-    the ones the fixture recorded."""
+    the ones the fixture recorded. svcwl_killed_*: a task on its second lost worker errs at once
+    (KilledWorker, allowed_failures 1), its waiting dependents with it."""
     names = ["svcwl_c2var_sat1.1.npz", "svcwl_c2mini_satinf.npz", "svcwl_chain_c2var_sat1.1.npz",
-             "svcwl_chain_c2mini_satinf.npz"]
+             "svcwl_chain_c2mini_satinf.npz", "svcwl_killed_c2var_sat1.1.npz", "svcwl_killed_c2mini_satinf.npz",
+             "svcwl_killed0_c2var_sat1.1.npz"]
     res = drive(names)
     assert [r["fixture"] for r in res] == names
     for r in res:

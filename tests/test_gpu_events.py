@@ -56,6 +56,14 @@ def loss_order_rows(z, i):
     return [(int(z["lo_task"][r]), int(z["lo_kind"][r]), idx[rp[r]:rp[r + 1]].tolist()) for r in range(ep[i], ep[i + 1])]
 
 
+def loss_killed(z, i, proc):
+    """Per processing task of loss event i: it ran out of retries (svcwl_killed_*)."""
+    if "lo_kptr" not in z.files:
+        return None
+    k = set(z["lo_ktask"][z["lo_kptr"][i]:z["lo_kptr"][i + 1]].tolist())
+    return [int(t) in k for t in proc]
+
+
 def drive_events(eng, g, z, exp=None):
     """Every event of a svcev_* stream through the engine, snapshot per round; returns the
     placements each event made (update_graph's first)."""
@@ -97,7 +105,8 @@ def drive_events(eng, g, z, exp=None):
             elif kd == EV_LOSE_WORKER:  # the whole remove_worker stimulus on the device
                 lst = ht[hp[i]:hp[i + 1]]
                 npr = int(x[i])
-                assert eng.lose_worker(w, lst[:npr], lst[npr:], loss_order_rows(z, i)) is not None, (i, eng.refusal)
+                assert eng.lose_worker(w, lst[:npr], lst[npr:], loss_order_rows(z, i),
+                                       loss_killed(z, i, lst[:npr])) is not None, (i, eng.refusal)
             elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
                 # the scheduler decided this stimulus itself: its placements, then its state
                 n = int(exp["stim_nplaced"][len(stim)])
@@ -202,7 +211,9 @@ def test_service_worker_loss_on_the_engine(name):
     engine (dgp_lose_worker) with no resync, interleaved with every modelled event: the
     placements each loss made, every later decision, the snapshots and the final states
     equal the reference's. svcwl_chain_*: the lost results recompute released dependencies
-    in turn (recompute chains, in the scheduler's set orders: dgp_lose_worker_ordered)."""
+    in turn (recompute chains, in the scheduler's set orders: dgp_lose_worker_ordered).
+    svcwl_killed_*: allowed_failures 1, so a task on its second lost worker errs at once
+    (KilledWorker) with its waiting dependents."""
     from distributed_amd.engine import PlacementEngine
 
     path = os.path.join(GOLDEN, name)
