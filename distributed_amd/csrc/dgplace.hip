@@ -1991,7 +1991,24 @@ __global__ void k_ug_frontier_reset(const dgp::Dev* __restrict__ Dp) {
 
 extern "C" {
 
+static int graph_stimulus_impl(dgp_engine* e, bool ordered, int64_t n_order, const int32_t* order_task,
+                               const int8_t* order_kind, const int64_t* order_ptr, const int32_t* order_idx,
+                               int64_t* n_new_placements);
+static int graph_stimulus_recompute(dgp_engine* e, int64_t n_order, const int32_t* order_task, const int8_t* order_kind,
+                                    const int64_t* order_ptr, const int32_t* order_idx, int64_t* n_new_placements);
+
 int dgp_graph_stimulus(dgp_engine* e, int64_t* n_new_placements) {
+  return graph_stimulus_impl(e, false, 0, nullptr, nullptr, nullptr, nullptr, n_new_placements);
+}
+
+int dgp_graph_stimulus_ordered(dgp_engine* e, int64_t n_order, const int32_t* order_task, const int8_t* order_kind,
+                               const int64_t* order_ptr, const int32_t* order_idx, int64_t* n_new_placements) {
+  return graph_stimulus_impl(e, true, n_order, order_task, order_kind, order_ptr, order_idx, n_new_placements);
+}
+
+static int graph_stimulus_impl(dgp_engine* e, bool ordered, int64_t n_order, const int32_t* order_task,
+                               const int8_t* order_kind, const int64_t* order_ptr, const int32_t* order_idx,
+                               int64_t* n_new_placements) {
   if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (!e || !e->pending_resync || e->pending_lo < 0)
@@ -2001,23 +2018,29 @@ int dgp_graph_stimulus(dgp_engine* e, int64_t* n_new_placements) {
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   // the earlier tasks the new ones depend on: in memory (a replica), or waiting / queued /
-  // processing (the new task waits on it); one released, erred or forgotten would be
-  // recomputed or fail the new task (:2082-2097), which the engine leaves to the scheduler
+  // processing (the new task waits on it); one released is recomputed (:2105-2106: the
+  // recommendation machine with the scheduler's set orders, dgp_graph_stimulus_ordered); one
+  // erred or forgotten would fail the new task (:4613-4618), which the engine leaves to the
+  // scheduler
   std::vector<uint8_t> st((size_t)lo);
   HIPCHK(e, hipMemcpy(st.data(), D.state, (size_t)lo, hipMemcpyDeviceToHost));
   std::unordered_map<int32_t, int32_t> add;
   const std::vector<int64_t>& dp = e->h_dep_ptr;
   const std::vector<int32_t>& di = e->h_dep_idx;
+  bool recompute = false;
   for (int64_t t = lo; t < N; t++)
     for (int64_t k = dp[t]; k < dp[t + 1]; k++) {
       const int32_t d = di[k];
       if (d >= lo) continue;
       const uint8_t sd = st[d];
-      if (sd == dgp::S_RELEASED || sd == dgp::S_ERRED || (e->tflags_h[d] & dgp::TF_FORGOTTEN))
+      if (sd == dgp::S_ERRED || (e->tflags_h[d] & dgp::TF_FORGOTTEN) || (sd == dgp::S_RELEASED && !ordered))
         return fail(e, DGP_E_UNSUPPORTED, "dgp_graph_stimulus: an earlier dependency is released, erred or "
                                           "forgotten (recomputed by the scheduler): dgp_sync_* instead");
+      recompute = recompute || sd == dgp::S_RELEASED;
       add[d] += 1;
     }
+  if (recompute) return graph_stimulus_recompute(e, n_order, order_task, order_kind, order_ptr, order_idx,
+                                                 n_new_placements);
   if (!add.empty()) {
     std::vector<int32_t> dd, cc;
     for (auto& kv : add) {
@@ -2490,6 +2513,97 @@ int dgp_remove_worker(dgp_engine* e, int32_t worker) {
   return refresh_rootish(e);
 }
 
+// the order rows of dgp_lose_worker_ordered / dgp_graph_stimulus_ordered: sorted by (task,
+// kind); kind 0 a permutation of the task's dependencies, kinds 1 / 2 distinct dependents
+static int check_order_rows(dgp_engine* e, int64_t n_order, const int32_t* order_task, const int8_t* order_kind,
+                            const int64_t* order_ptr, const int32_t* order_idx, const char* what) {
+  const dgp::Dev& D = e->D;
+  if (n_order < 0 || n_order > 2 * D.N || (n_order && (!order_task || !order_kind || !order_ptr || !order_idx)))
+    return fail(e, DGP_E_ARG, std::string(what) + ": bad order rows");
+  if (n_order && order_ptr[0] != 0) return fail(e, DGP_E_ARG, std::string(what) + ": order_ptr[0] != 0");
+  const std::vector<int64_t>& dp = e->h_dep_ptr;
+  const std::vector<int32_t>& di = e->h_dep_idx;
+  for (int64_t i = 0; i < n_order; i++) {
+    const int32_t t = order_task[i];
+    const int k = order_kind[i];
+    if (t < 0 || t >= D.N || k < dgp::ev::LO_DEPS || k > dgp::ev::LO_DEPENDENTS || order_ptr[i + 1] < order_ptr[i])
+      return fail(e, DGP_E_ARG, std::string(what) + ": bad order row");
+    if (i > 0 && (order_task[i - 1] > t || (order_task[i - 1] == t && order_kind[i - 1] >= k)))
+      return fail(e, DGP_E_ARG, std::string(what) + ": order rows not sorted by (task, kind)");
+    std::vector<int32_t> r(order_idx + order_ptr[i], order_idx + order_ptr[i + 1]);
+    for (int32_t x : r)
+      if (x < 0 || x >= D.N) return fail(e, DGP_E_ARG, std::string(what) + ": task out of range");
+    std::sort(r.begin(), r.end());
+    if (std::adjacent_find(r.begin(), r.end()) != r.end())
+      return fail(e, DGP_E_ARG, std::string(what) + ": a task twice in one row");
+    if (k == dgp::ev::LO_DEPS) {
+      std::vector<int32_t> own(di.begin() + dp[t], di.begin() + dp[t + 1]);
+      std::sort(own.begin(), own.end());
+      if (own != r) return fail(e, DGP_E_ARG, std::string(what) + ": a dependency row is not the task's dependencies");
+    } else {
+      for (int32_t y : r)
+        if (std::find(di.begin() + dp[y], di.begin() + dp[y + 1], t) == di.begin() + dp[y + 1])
+          return fail(e, DGP_E_ARG, std::string(what) + ": a waiters / dependents row names a task that does not depend on it");
+    }
+  }
+  return 0;
+}
+
+// a later graph's update_graph stimulus that recomputes released earlier dependencies
+// (:4598-4611 -> _transitions): the runnable new tasks recommended waiting in the dict's
+// order (priority descending, popped LIFO), through the worker-loss recommendation machine
+// (k_ev_lose_worker with no worker), every set order the cascade follows from the host
+static int graph_stimulus_recompute(dgp_engine* e, int64_t n_order, const int32_t* order_task, const int8_t* order_kind,
+                                    const int64_t* order_ptr, const int32_t* order_idx, int64_t* n_new_placements) {
+  if (int rc = check_order_rows(e, n_order, order_task, order_kind, order_ptr, order_idx, "dgp_graph_stimulus_ordered"))
+    return rc;
+  dgp::Dev& D = e->D;
+  const int64_t lo = e->pending_lo, N = D.N;
+  std::vector<int32_t> recs;
+  for (int64_t t = lo; t < N; t++) recs.push_back((int32_t)t);
+  std::stable_sort(recs.begin(), recs.end(), [&](int32_t a, int32_t b) { return e->h_prio[a] > e->h_prio[b]; });
+  int64_t pmax_old = -1;
+  for (int64_t t = 0; t < lo; t++) pmax_old = std::max(pmax_old, e->h_prio[t]);
+  bool follows = true;
+  for (int64_t t = lo; t < N && follows; t++) follows = e->h_prio[t] > pmax_old;
+  e->pending_resync = false;
+  e->pending_lo = -1;
+  e->mode = 2;
+  HIPCHK(e, hipMemsetAsync(D.ready_key, 0xff, (size_t)D.N * 8, e->stream));  // the recommendation dict: empty
+  std::vector<char*> a;
+  const int64_t n_oidx = n_order ? order_ptr[n_order] : 0;
+  if (int rc = stage_args(e, {{recs.data(), recs.size() * 4}, {order_task, (size_t)n_order * 4},
+                              {order_kind, (size_t)n_order}, {order_ptr, n_order ? (size_t)(n_order + 1) * 8 : 0},
+                              {order_idx, (size_t)n_oidx * 4}},
+                          a))
+    return rc;
+  dgp::ev::LossOrder O{(const int32_t*)a[1], (const int8_t*)a[2], (const int64_t*)a[3], (const int32_t*)a[4],
+                       (int)n_order};
+  if (int rc = grow_logs(e, 0)) return rc;
+  if (int rc = sync_dev(e)) return rc;
+  dgp::Ctl c0;
+  if (int rc = read_ctl(e, &c0)) return rc;
+  hipLaunchKernelGGL(dgp::ev::k_ev_lose_worker, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev, -1,
+                     (const int32_t*)a[0], (int)recs.size(), (const int8_t*)nullptr, (const int32_t*)nullptr, 0, O,
+                     e->d_aux + 3);
+  HIPCHK(e, hipGetLastError());
+  if (int rc = set_runids(e)) return rc;
+  dgp::Ctl c;
+  if (int rc = check_device_error(e, &c)) {
+    e->pending_resync = true;  // the cascade stopped part-way: the scheduler's state is handed over
+    return c.error == dgp::ERR_UNSUPPORTED ? fail(e, DGP_E_UNSUPPORTED, std::string(e->err)) : rc;
+  }
+  if (!follows && c.qlen > 1) {  // the queue (HeapSet by priority) with the new root-ish tasks in their place
+    std::vector<int32_t> q((size_t)c.qlen);
+    HIPCHK(e, hipMemcpy(q.data(), D.qarr + c.qhead, q.size() * 4, hipMemcpyDeviceToHost));
+    std::stable_sort(q.begin(), q.end(), [&](int32_t x, int32_t y) { return e->h_prio[x] < e->h_prio[y]; });
+    HIPCHK(e, hipMemcpy(D.qarr + c.qhead, q.data(), q.size() * 4, hipMemcpyHostToDevice));
+  }
+  if (n_new_placements) *n_new_placements = (int64_t)(c.n_placed - c0.n_placed);
+  e->last_placed = c.n_placed;
+  return 0;
+}
+
 int dgp_lose_worker(dgp_engine* e, int32_t worker, int64_t n_processing, const int32_t* processing, int64_t n_held,
                     const int32_t* held, int64_t* n_new_placements) {
   return dgp_lose_worker_ordered(e, worker, n_processing, processing, nullptr, n_held, held, 0, nullptr, nullptr,
@@ -2503,38 +2617,8 @@ int dgp_lose_worker_ordered(dgp_engine* e, int32_t worker, int64_t n_processing,
   if (int rc_ = resident_stop(e)) return rc_;
   if (n_new_placements) *n_new_placements = 0;
   if (int rc = event_ready(e, "dgp_lose_worker")) return rc;
-  {  // the order rows: sorted by (task, kind); kind 0 a permutation of the task's dependencies,
-     // kind 1 distinct dependents of it
-    const dgp::Dev& D = e->D;
-    if (n_order < 0 || n_order > 2 * D.N || (n_order && (!order_task || !order_kind || !order_ptr || !order_idx)))
-      return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: bad order rows");
-    if (n_order && order_ptr[0] != 0) return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: order_ptr[0] != 0");
-    const std::vector<int64_t>& dp = e->h_dep_ptr;
-    const std::vector<int32_t>& di = e->h_dep_idx;
-    for (int64_t i = 0; i < n_order; i++) {
-      const int32_t t = order_task[i];
-      const int k = order_kind[i];
-      if (t < 0 || t >= D.N || k < dgp::ev::LO_DEPS || k > dgp::ev::LO_DEPENDENTS || order_ptr[i + 1] < order_ptr[i])
-        return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: bad order row");
-      if (i > 0 && (order_task[i - 1] > t || (order_task[i - 1] == t && order_kind[i - 1] >= k)))
-        return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: order rows not sorted by (task, kind)");
-      std::vector<int32_t> r(order_idx + order_ptr[i], order_idx + order_ptr[i + 1]);
-      for (int32_t x : r)
-        if (x < 0 || x >= D.N) return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: task out of range");
-      std::sort(r.begin(), r.end());
-      if (std::adjacent_find(r.begin(), r.end()) != r.end())
-        return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: a task twice in one row");
-      if (k == dgp::ev::LO_DEPS) {
-        std::vector<int32_t> own(di.begin() + dp[t], di.begin() + dp[t + 1]);
-        std::sort(own.begin(), own.end());
-        if (own != r) return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: a dependency row is not the task's dependencies");
-      } else {
-        for (int32_t y : r)
-          if (std::find(di.begin() + dp[y], di.begin() + dp[y + 1], t) == di.begin() + dp[y + 1])
-            return fail(e, DGP_E_ARG, "dgp_lose_worker_ordered: a waiters / dependents row names a task that does not depend on it");
-      }
-    }
-  }
+  if (int rc = check_order_rows(e, n_order, order_task, order_kind, order_ptr, order_idx, "dgp_lose_worker_ordered"))
+    return rc;
   dgp::Dev& D = e->D;
   if (worker < 0 || worker >= D.W) return fail(e, DGP_E_ARG, "dgp_lose_worker: worker out of range");
   if (e->paused_h[worker] == 2) return fail(e, DGP_E_ARG, "dgp_lose_worker: the worker was removed");

@@ -370,14 +370,22 @@ class PlacementEngine:
 
     UNSUPPORTED = -5  # DGP_E_UNSUPPORTED: a case the engine leaves to the caller, nothing changed
 
-    def graph_stimulus(self) -> int | None:
+    def graph_stimulus(self, order=None) -> int | None:
         """The update_graph stimulus of the graph ``add_graph(defer=True)`` appended, on the
         device (dgp_graph_stimulus): dependent, restricted (rows first, update_restrictions)
-        or outranking (ranks first, set_priorities) later graphs. Returns its placements, or
-        None when the engine leaves it to the scheduler (an earlier dependency is released /
-        erred / forgotten): then the scheduler's stimulus and ``sync()`` follow as before."""
+        or outranking (ranks first, set_priorities) later graphs. ``order``: (task, kind,
+        tasks) rows of the set orders a recompute of released earlier dependencies follows
+        (``distributed_amd.loss.graph_orders``; given, even empty, the engine recomputes
+        them: dgp_graph_stimulus_ordered). Returns its placements, or None when the engine
+        leaves it to the scheduler (an earlier dependency released without ``order``, erred
+        or forgotten): then the scheduler's stimulus and ``sync()`` follow as before."""
         newp = C.c_int64(0)
-        rc = self.lib.dgp_graph_stimulus(self.h, C.byref(newp))
+        if order is not None:
+            ot, ok, op, oi = self._order_rows(order)
+            rc = self.lib.dgp_graph_stimulus_ordered(self.h, len(ot), _ptr(ot), _ptr(ok), _ptr(op), _ptr(oi),
+                                                     C.byref(newp))
+        else:
+            rc = self.lib.dgp_graph_stimulus(self.h, C.byref(newp))
         if rc == self.UNSUPPORTED:
             self.refusal = (self.lib.dgp_last_error(self.h) or b"").decode()
             return None
@@ -487,6 +495,22 @@ class PlacementEngine:
         """Scheduler.remove_worker's worker table part (distributed/scheduler.py:5213-5231)."""
         self._check(self.lib.dgp_remove_worker(self.h, int(worker)), "dgp_remove_worker")
 
+    @staticmethod
+    def _order_rows(order):
+        """(task, kind, tasks) rows as the C ABI's sorted CSR (one row per (task, kind): the first)."""
+        rows, seen = [], set()
+        for t, k, seq in order:
+            if (int(t), int(k)) not in seen:
+                seen.add((int(t), int(k)))
+                rows.append((int(t), int(k), list(map(int, seq))))
+        rows.sort()
+        ot = np.array([r[0] for r in rows], np.int32)
+        ok = np.array([r[1] for r in rows], np.int8)
+        op = np.zeros(len(rows) + 1, np.int64)
+        op[1:] = np.cumsum([len(r[2]) for r in rows]) if rows else []
+        oi = np.array([x for r in rows for x in r[2]], np.int32)
+        return ot, ok, op, oi
+
     def lose_worker(self, worker: int, processing, held, order=(), killed=None) -> int | None:
         """The whole Scheduler.remove_worker stimulus (distributed/scheduler.py:5180-5303) on
         the device (dgp_lose_worker_ordered): ``processing`` = the worker's processing tasks in
@@ -500,23 +524,13 @@ class PlacementEngine:
         after a refusal from the device the scheduler's state follows by ``sync()`` as after
         remove_worker."""
         p, h = self._arr(processing, np.int32), self._arr(held, np.int32)
-        rows, seen = [], set()
-        for t, k, seq in order:  # one row per (task, kind): the first
-            if (int(t), int(k)) not in seen:
-                seen.add((int(t), int(k)))
-                rows.append((int(t), int(k), list(map(int, seq))))
-        rows.sort()
+        ot, ok, op, oi = self._order_rows(order)
         kf = None if killed is None or not any(killed) else self._arr(killed, np.int8)
         if kf is not None and len(kf) != len(p):
             raise ValueError("killed: one flag per processing task")
-        ot = np.array([r[0] for r in rows], np.int32)
-        ok = np.array([r[1] for r in rows], np.int8)
-        op = np.zeros(len(rows) + 1, np.int64)
-        op[1:] = np.cumsum([len(r[2]) for r in rows]) if rows else []
-        oi = np.array([x for r in rows for x in r[2]], np.int32)
         newp = C.c_int64(0)
         rc = self.lib.dgp_lose_worker_ordered(self.h, int(worker), len(p), _ptr(p), None if kf is None else _ptr(kf),
-                                              len(h), _ptr(h), len(rows), _ptr(ot), _ptr(ok), _ptr(op), _ptr(oi),
+                                              len(h), _ptr(h), len(ot), _ptr(ot), _ptr(ok), _ptr(op), _ptr(oi),
                                               C.byref(newp))
         if rc == self.UNSUPPORTED:
             self.refusal = (self.lib.dgp_last_error(self.h) or b"").decode()

@@ -335,6 +335,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         self.pending: deque = deque()  # (task index, worker index) in placement order
         self.n_fetched = 0
         self.stats = Counter()
+        self._recomputed = set()  # earlier tasks a later graph's stimulus recomputed on the device
         self._allowed: list = []  # per running wrapped stimulus: the transitions the engine follows
         self._window = None       # (allowed transitions, keys or None) after a plugin hook's stimulus
         self._expect_replicas: set = set()  # (key, address) replicas the running stimulus adds itself
@@ -1234,8 +1235,11 @@ class GPUPlacementExtension(SchedulerPlugin):
                 self._fetch()
                 self.stats["graphs"] += 1
             if self.active and keys_ is not None:  # the first graph's keys: the index's key view
+                # (a later graph's stimulus that recomputed earlier tasks: theirs too)
                 self._window = (_UPDATE_GRAPH_TRANSITIONS,
-                                self.task_index.keys() if len(keys_) == len(self.task_index) else set(keys_))
+                                self.task_index.keys() if len(keys_) == len(self.task_index)
+                                else set(keys_) | self._recomputed)
+            self._recomputed = set()
         except Exception as e:  # plugin errors are logged, not raised (scheduler.py:4652-4653)
             self.fallback(f"update_graph: {e}")
 
@@ -1373,7 +1377,20 @@ class GPUPlacementExtension(SchedulerPlugin):
             if hasattr(self.engine, "graph_stimulus"):
                 if restricted:
                     self._push_task_inputs(keys_)
-                if self.active and self.engine.graph_stimulus() is not None:
+                # released earlier dependencies are recomputed on the device when the engine
+                # takes the scheduler's set orders (dgp_graph_stimulus_ordered)
+                chain = loss.graph_cascade(new) if dependent else []
+                ti = self.task_index
+                order = None
+                if chain and all(ts.key in ti and ts.prefix.name in self.prefix_index and ti[ts.key] not in self._stale
+                                 for ts in chain):
+                    order = loss.graph_orders(new, chain, lambda ts: ti[ts.key])
+                    self.stats["graph_recomputes_on_device"] += 1
+                stim = (self.engine.graph_stimulus(order) if order is not None else self.engine.graph_stimulus()) \
+                    if self.active else None
+                if stim is not None:
+                    if order is not None:
+                        self._recomputed = {ts.key for ts in chain}
                     self.stats["graph_stimuli_on_device"] += 1
                     self._fetch()
                     return keys_

@@ -134,3 +134,37 @@ def loss_orders(tasks, index_of, erred=(), n_killed=0) -> list:
         if len(kin[1]) >= 2:
             rows.append((index_of(t), kin[0], [index_of(y) for y in kin[1]]))
     return rows
+
+
+def graph_cascade(new) -> list | None:
+    """A later graph's update_graph stimulus (scheduler.py:4598-4611): the earlier tasks its
+    runnable ``new`` tasks recompute -- released dependencies, transitively back to results in
+    memory (:2105-2106) -- in discovery order; None when the engine does not restate the
+    stimulus (an erred, forgotten or blamed dependency: the new task errs, :4613-4618; a task
+    to recompute without run_spec, with lost dependencies or an actor)."""
+    newset = set(new)
+    out, seen, stack = [], set(), list(new)
+    while stack:
+        t = stack.pop()
+        for d in t.dependencies:
+            if d in newset or d in seen:
+                continue
+            if d.state in ("erred", "forgotten") or d.exception_blame:
+                return None
+            if d.state == "released":
+                if not d.run_spec or d.actor or d.has_lost_dependencies:
+                    return None
+                seen.add(d)
+                out.append(d)
+                stack.append(d)
+    return out
+
+
+def graph_orders(new, chain, index_of) -> list:
+    """(task, LO_DEPS, dependencies) rows for the tasks of a later graph's stimulus whose
+    recommendations follow a set: a new or recomputed task with two or more dependencies that
+    are recomputed (the others are either in the dict already -- the new ones, whose place
+    stays -- or only gain it as a waiter)."""
+    cs = set(chain)
+    return [(index_of(t), LO_DEPS, [index_of(d) for d in t.dependencies])
+            for t in list(new) + list(chain) if sum(d in cs for d in t.dependencies) >= 2]

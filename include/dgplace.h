@@ -297,6 +297,15 @@ int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr,
  * stimulus and the caller resynchronises as before. Replaces the scheduler's Python for that
  * stimulus (scheduler.py:4600-4653). */
 int dgp_graph_stimulus(dgp_engine* e, int64_t* n_new_placements);
+/* dgp_graph_stimulus_ordered (ABI 21): dgp_graph_stimulus, and an earlier dependency that is
+ * released is recomputed (_transition_released_waiting :2101-2106, back to results in
+ * memory): the runnable new tasks are recommended waiting in the dict's order (priority
+ * descending, popped LIFO) and run through the worker-loss recommendation machine; the
+ * scheduler's set orders the cascade follows come as order rows, as for
+ * dgp_lose_worker_ordered (distributed_amd/loss.py graph_orders). An erred or forgotten
+ * earlier dependency still returns DGP_E_UNSUPPORTED with nothing changed. */
+int dgp_graph_stimulus_ordered(dgp_engine* e, int64_t n_order, const int32_t* order_task, const int8_t* order_kind,
+                               const int64_t* order_ptr, const int32_t* order_idx, int64_t* n_new_placements);
 
 /* (ABI 20) The task prefix table anew (the stream engine carries at most 32 prefixes; a
  * long-lived scheduler meets more: TaskPrefix objects per key_split name, scheduler.py:923-1031).

@@ -18,7 +18,8 @@ def golden_files():
     """Placement replay fixtures (tests/golden/gen_golden.py, gen_service.py)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
                   and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcgdep_", "svcev_",
-                                            "svcrs_", "svcrt_", "svcwl_", "svcp2p_", "svcgrst_", "svcgprio_", "svcpfx_")))
+                                            "svcrs_", "svcrt_", "svcwl_", "svcp2p_", "svcgrst_", "svcgprio_", "svcpfx_",
+                                            "svcgrec_")))
 
 
 def svc_second_graph_files():
@@ -28,8 +29,8 @@ def svc_second_graph_files():
 
 def svc_dep_graph_files():
     """Service-mode streams with a later graph that depends on earlier tasks (gen_service.py
-    second-graph svcgdep_*): the scheduler decides its stimulus, the engine resyncs."""
-    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcgdep_") and f.endswith(".npz"))
+    second-graph svcgdep_*; svcgrec_*: some of them released, recomputed by that stimulus)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith(("svcgdep_", "svcgrec_")) and f.endswith(".npz"))
 
 
 def svc_restr_graph_files():

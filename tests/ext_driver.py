@@ -685,7 +685,7 @@ def run_second_graph(name, resync=False):
     fkeys = [ts.key for ts in tss]
     # the scheduler decides the submission, then a resync (svcgprio_: a user priority above the
     # earlier tasks', the engine takes the merged ranks first)
-    dep = name.startswith(("svcgdep_", "svcgrst_", "svcgprio_"))
+    dep = name.startswith(("svcgdep_", "svcgrst_", "svcgprio_", "svcgrec_"))
     user_prio = int(z["g2_user_prio"]) if "g2_user_prio" in z.files else 0
     # the engine runs that stimulus (dgp_graph_stimulus) unless ``resync``: the engine of
     # rounds 3-4 without it, the scheduler deciding and a resync after it
@@ -774,6 +774,13 @@ def run_second_graph(name, resync=False):
         gst = [c for c in eng.calls if c[0] == "gstim"]
         assert len(gst) == 1 and not [c for c in eng.calls if c[0] == "sync"], eng.calls[-4:]
         assert ext.stats["graph_stimuli_on_device"] == 1 and ext.stats["resyncs"] == 0, ext.stats
+        if "g2_lo_task" in z.files:  # a recompute: the extension's set orders are the generator's
+            rp, li = z["g2_lo_rowptr"], z["g2_lo_idx"]
+            want = sorted((int(t), int(k), tuple(li[rp[r]:rp[r + 1]].tolist()))
+                          for r, (t, k) in enumerate(zip(z["g2_lo_task"].tolist(), z["g2_lo_kind"].tolist())))
+            got = eng.graph_orders[-1]
+            assert got is not None and sorted((t, k, tuple(q)) for t, k, q in got) == want
+            assert ext.stats["graph_recomputes_on_device"] == 1, ext.stats
         if user_prio:  # every task's merged rank, before the stimulus
             ps = [c for c in eng.calls if c[0] == "prio"]
             assert len(ps) == 1 and eng.calls.index(ps[0]) < eng.calls.index(gst[0]), eng.calls[-3:]
@@ -964,6 +971,7 @@ class EventEngine(FixtureEngine):
         self.calls = []
         self.loss_orders = []  # the order rows of each lose_worker call
         self.loss_killed = []  # ... and its killed processing tasks
+        self.graph_orders = []  # the order rows of each graph_stimulus call (None: plain)
 
     def _event(self, *call):
         assert self._posted is None, f"{call[0]} while a task-finished batch is posted"  # the engine refuses it
@@ -1056,7 +1064,8 @@ class GraphStimulusEngine(EventEngine):
     """EventEngine that runs a later graph's update_graph stimulus itself (dgp_graph_stimulus):
     the fixture's placement count of that event."""
 
-    def graph_stimulus(self):
+    def graph_stimulus(self, order=None):
+        self.graph_orders.append(order)
         return self._event("gstim")
 
 
@@ -1420,7 +1429,7 @@ if __name__ == "__main__":
             print(json.dumps(run_ab(nm)), flush=True)
             continue
         fn = (run_joins if nm.startswith("svcaddw_") else (lambda x: run_second_graph(x, "--resync" in args))
-              if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_"))
+              if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_", "svcgrec_"))
               else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcrt_", "svcwl_", "svcp2p_"))
               else run_prefixes if nm.startswith("svcpfx_")
               else None)

@@ -374,7 +374,7 @@ def main_add_workers(only):
 TOKEN2 = "f9e8d7c6b5a49382716051e4d3c2b1a0"
 
 
-def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0, restr=False, user_prio=0):
+def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0, restr=False, user_prio=0, recompute=False):
     """The replay protocol's completions as task-finished messages, with a second,
     independent graph ``g2`` submitted part-way through, the way
     ``Scheduler._create_taskstate_from_graph`` (distributed/scheduler.py:4512-4653) adds it:
@@ -450,7 +450,8 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0, restr=
                 ts._rootish = bool(ov)
             new.append(ts)
         ptr, idx = g2["dep_ptr"], g2["dep_idx"]
-        earlier = [ts for ts in tss if ts.state in ("memory", "processing", "waiting", "queued")]
+        live = ("memory", "processing", "waiting", "queued") + (("released",) if recompute else ())
+        earlier = [ts for ts in tss if ts.state in live]
         rows = []
         for t, ts in enumerate(new):
             row = [int(d) for d in idx[ptr[t]:ptr[t + 1]]]
@@ -471,6 +472,16 @@ def replay_second_graph(g, g2, cfg, seed, at_frac, n_add=0, dep_frac=0.0, restr=
         ext["ptr"] = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
         ext["idx"] = np.array([d for r in rows for d in r], np.int32)
         recs2 = {ts.key: "waiting" for ts in sorted(new, key=lambda t: t.priority, reverse=True)}
+        if recompute:  # the set orders the recompute follows (distributed_amd/loss.py, as the extension passes them)
+            LS = _load_repo_module("loss")
+            chain = LS.graph_cascade(new)
+            assert chain, "no released earlier dependency"
+            rows = LS.graph_orders(new, chain, lambda ts: tidx[ts.key])
+            ext["lo_task"] = np.array([r[0] for r in rows], np.int32)
+            ext["lo_kind"] = np.array([r[1] for r in rows], np.int8)
+            ext["lo_rowptr"] = np.concatenate([[0], np.cumsum([len(r[2]) for r in rows])]).astype(np.int64)
+            ext["lo_idx"] = np.array([x for r in rows for x in r[2]], np.int32)
+            ext["n_recomputed"] = len(chain)
         s._transitions(recs2, {}, {}, "update-graph-2")
         if dep_frac or restr or user_prio:
             gall = dict(prefix_names=g["prefix_names"], prefix_default_dur=g["prefix_default_dur"],
@@ -557,11 +568,17 @@ def main_second_graph(only):
         "svcgprio_c2var_sat1.1": (dict(n=3000, w=32, seed=53, n_inner_prefixes=3, random_durations=True,
                                        nthreads="random"), dict(n=2000, seed=54), 1.1, 0.3, 0, 0.0, 1),
         "svcgprio_c2mini_satinf": (dict(n=2500, w=24, seed=55), dict(n=1500, seed=56), float("inf"), 0.5, 0, 0.0, 1),
+        # later graphs that depend on released earlier tasks: recomputed (recompute chains)
+        "svcgrec_c2var_sat1.1": (dict(n=3000, w=32, seed=57, n_inner_prefixes=3, random_durations=True,
+                                      nthreads="random"), dict(n=2000, seed=58), 1.1, 0.5, 0, 0.2, 0, True),
+        "svcgrec_c2mini_satinf": (dict(n=2500, w=24, seed=59), dict(n=1500, seed=60), float("inf"), 0.6, 0, 0.3, 0,
+                                  True),
     }
     for name, (a, b, sat, frac, *more) in cases.items():
         nadd = more[0] if more else 0
         dep_frac = more[1] if len(more) > 1 else 0.0
         user_prio = more[2] if len(more) > 2 else 0
+        recompute = bool(more[3]) if len(more) > 3 else False
         if only and name not in only:
             continue
         kw = {k: v for k, v in a.items() if k not in ("n", "w", "seed", "restrict")}
@@ -577,7 +594,7 @@ def main_second_graph(only):
         dask.config.set({"distributed.scheduler.worker-saturation": sat})
         cfg = G.config_dict(sat)
         rec, rounds, nplaced, states, msgs, round_ptr, at, joins, ext = replay_second_graph(
-            g, g2, cfg, 0, frac, nadd, dep_frac, restr=bool(b.get("restrict")), user_prio=user_prio)
+            g, g2, cfg, 0, frac, nadd, dep_frac, restr=bool(b.get("restrict")), user_prio=user_prio, recompute=recompute)
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -598,6 +615,10 @@ def main_second_graph(only):
         if b.get("restrict"):
             z.update(g2_restr_ptr=np.asarray(g2["restr_ptr"]), g2_restr_idx=np.asarray(g2["restr_idx"]),
                      g2_restr_flags=np.asarray(g2["restr_flags"]))
+        if recompute:  # the set-order rows of the recompute (distributed_amd/loss.py graph_orders)
+            z.update(g2_lo_task=ext["lo_task"], g2_lo_kind=ext["lo_kind"], g2_lo_rowptr=ext["lo_rowptr"],
+                     g2_lo_idx=ext["lo_idx"], g2_n_recomputed=np.array(ext["n_recomputed"], np.int64))
+            print(f"{name}: {ext['n_recomputed']} earlier tasks recomputed, {len(ext['lo_task'])} order rows")
         np.savez_compressed(path, **z)
         routes = np.bincount(np.array(rec["route"]), minlength=4).tolist()
         print(f"{name}: {len(msgs['task'])} messages, second graph of {g2['n_tasks']} at message {at}, routes {routes}")

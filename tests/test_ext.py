@@ -120,7 +120,8 @@ def test_extension_follows_a_second_graph():
 
 
 LATER = ["svcgdep_c2mini_satinf.npz", "svcgdep_c2var_sat1.1.npz", "svcgdep_joins_sat1.0.npz",
-         "svcgrst_c2var_sat1.1.npz", "svcgrst_dep_satinf.npz", "svcgprio_c2mini_satinf.npz", "svcgprio_c2var_sat1.1.npz"]
+         "svcgrst_c2var_sat1.1.npz", "svcgrst_dep_satinf.npz", "svcgprio_c2mini_satinf.npz", "svcgprio_c2var_sat1.1.npz",
+         "svcgrec_c2var_sat1.1.npz", "svcgrec_c2mini_satinf.npz"]
 
 
 def test_extension_runs_later_graph_stimuli_on_the_engine():

@@ -56,6 +56,15 @@ def loss_order_rows(z, i):
     return [(int(z["lo_task"][r]), int(z["lo_kind"][r]), idx[rp[r]:rp[r + 1]].tolist()) for r in range(ep[i], ep[i + 1])]
 
 
+def graph_order_rows(z):
+    """The set-order rows of a svcgrec_* later graph's recompute (None: a plain stimulus)."""
+    if "g2_lo_task" not in z.files:
+        return None
+    rp, idx = z["g2_lo_rowptr"], z["g2_lo_idx"]
+    return [(int(t), int(k), idx[rp[r]:rp[r + 1]].tolist())
+            for r, (t, k) in enumerate(zip(z["g2_lo_task"].tolist(), z["g2_lo_kind"].tolist()))]
+
+
 def loss_killed(z, i, proc):
     """Per processing task of loss event i: it ran out of retries (svcwl_killed_*)."""
     if "lo_kptr" not in z.files:
@@ -364,8 +373,10 @@ def test_later_graph_stimulus_on_the_engine(name, per_message):
     (dgp_update_restrictions) or every task's merged rank (dgp_set_priorities) first, then
     the stimulus on the device -- the earlier tasks gain the new ones as waiters, the new ones
     wait on the earlier ones not in memory, the runnable ones go to processing / queued in
-    priority order. Its placements and every later one, the snapshots and the final states
-    equal the reference's; no resync."""
+    priority order. svcgrec_*: some earlier dependencies are released and recomputed by that
+    stimulus (recompute chains through the recommendation machine, in the scheduler's set
+    orders: dgp_graph_stimulus_ordered). Its placements and every later one, the snapshots and
+    the final states equal the reference's; no resync."""
     from distributed_amd.engine import PlacementEngine
 
     path = os.path.join(GOLDEN, name)
@@ -400,7 +411,7 @@ def test_later_graph_stimulus_on_the_engine(name, per_message):
                         rp, ri, rf = z["g2_restr_ptr"], z["g2_restr_idx"], z["g2_restr_flags"]
                         ts = np.flatnonzero(rf & 1)
                         eng.update_restrictions(g["n_tasks"] + ts, [ri[rp[t]:rp[t + 1]] for t in ts], rf[ts])
-                    newp = eng.graph_stimulus()
+                    newp = eng.graph_stimulus(graph_order_rows(z))
                     assert newp == int(z["g2_nplaced"]) and eng.num_placements() == n0 + newp, (newp, z["g2_nplaced"])
                 j = i + 1
                 if not per_message:
