@@ -709,11 +709,15 @@ __device__ int loss_machine(const Dev& D, const LossOrder& O, long long& sp, lon
   return -1;
 }
 
-// w >= 0: Scheduler.remove_worker of w (proc: its processing tasks, recommended released).
-// w < 0: a later graph's update_graph stimulus whose tasks recompute released earlier
-// dependencies (:4598-4611, dgp_graph_stimulus): proc = the runnable new tasks in the
-// recommendation dict's order, each recommended waiting (none is in a waiters set yet: TD_READD)
-__global__ void __launch_bounds__(CTA) k_ev_lose_worker(const Dev* __restrict__ Dp, int w, const int32_t* __restrict__ proc,
+// mode LM_LOSS: Scheduler.remove_worker of w (proc: its processing tasks, recommended released).
+// LM_GRAPH (w < 0): a later graph's update_graph stimulus whose tasks recompute released
+// earlier dependencies (:4598-4611, dgp_graph_stimulus): proc = the runnable new tasks in the
+// recommendation dict's order, each recommended waiting (none is in a waiters set yet: TD_READD).
+// LM_RELEASE (w < 0): Scheduler._reschedule (:7900-7924): transitions({key: "released"}) of
+// each processing task in proc
+enum : int { LM_LOSS = 0, LM_GRAPH = 1, LM_RELEASE = 2 };
+__global__ void __launch_bounds__(CTA) k_ev_lose_worker(const Dev* __restrict__ Dp, int mode, int w,
+                                                        const int32_t* __restrict__ proc,
                                                         int n_proc, const int8_t* __restrict__ killed,
                                                         const int32_t* __restrict__ held, int n_held, LossOrder O,
                                                         long long* placed) {
@@ -736,7 +740,7 @@ __global__ void __launch_bounds__(CTA) k_ev_lose_worker(const Dev* __restrict__ 
   __shared__ int s_x;
   const int64_t pl0 = (int64_t)c->n_placed;
   const double* dur = D.pdur_cur;
-  if (threadIdx.x == 0 && w >= 0) {
+  if (threadIdx.x == 0 && mode == LM_LOSS) {
     // the worker table part (:5226-5231): out of running / idle / idle_task_count / saturated
     D.w_flags[w] |= WF_PAUSED;
     walk_flags(D, w, occupancy(D, w, D.pdur_walk), D.w_nproc[w]);
@@ -761,9 +765,12 @@ __global__ void __launch_bounds__(CTA) k_ev_lose_worker(const Dev* __restrict__ 
     // graph's runnable tasks
     long long sp = 0, nmark = 0;
     for (int i = 0; i < n_proc && D.ctl->error == 0; i++) {
-      if (w < 0) {
+      if (mode == LM_GRAPH) {
         loss_mark(D, nmark, proc[i], TD_READD);
         rec_push(D, sp, proc[i], RC_WAITING);
+      } else if (mode == LM_RELEASE) {
+        if (D.state[proc[i]] != S_PROCESSING) set_error(D, ERR_BAD_STATE, proc[i]);
+        else rec_push(D, sp, proc[i], RC_RELEASED);
       } else if (killed && killed[i]) {
         loss_killed(D, O, sp, proc[i], w);  // KilledWorker: erred at once
       } else {

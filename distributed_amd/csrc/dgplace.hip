@@ -2583,8 +2583,8 @@ static int graph_stimulus_recompute(dgp_engine* e, int64_t n_order, const int32_
   if (int rc = sync_dev(e)) return rc;
   dgp::Ctl c0;
   if (int rc = read_ctl(e, &c0)) return rc;
-  hipLaunchKernelGGL(dgp::ev::k_ev_lose_worker, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev, -1,
-                     (const int32_t*)a[0], (int)recs.size(), (const int8_t*)nullptr, (const int32_t*)nullptr, 0, O,
+  hipLaunchKernelGGL(dgp::ev::k_ev_lose_worker, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev, (int)dgp::ev::LM_GRAPH,
+                     -1, (const int32_t*)a[0], (int)recs.size(), (const int8_t*)nullptr, (const int32_t*)nullptr, 0, O,
                      e->d_aux + 3);
   HIPCHK(e, hipGetLastError());
   if (int rc = set_runids(e)) return rc;
@@ -2598,6 +2598,37 @@ static int graph_stimulus_recompute(dgp_engine* e, int64_t n_order, const int32_
     HIPCHK(e, hipMemcpy(q.data(), D.qarr + c.qhead, q.size() * 4, hipMemcpyDeviceToHost));
     std::stable_sort(q.begin(), q.end(), [&](int32_t x, int32_t y) { return e->h_prio[x] < e->h_prio[y]; });
     HIPCHK(e, hipMemcpy(D.qarr + c.qhead, q.data(), q.size() * 4, hipMemcpyHostToDevice));
+  }
+  if (n_new_placements) *n_new_placements = (int64_t)(c.n_placed - c0.n_placed);
+  e->last_placed = c.n_placed;
+  return 0;
+}
+
+int dgp_reschedule(dgp_engine* e, int32_t task, int64_t* n_new_placements) {
+  if (int rc_ = resident_stop(e)) return rc_;
+  if (n_new_placements) *n_new_placements = 0;
+  if (int rc = event_ready(e, "dgp_reschedule")) return rc;
+  dgp::Dev& D = e->D;
+  if (task < 0 || task >= D.N) return fail(e, DGP_E_ARG, "dgp_reschedule: task out of range");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, hipMemsetAsync(D.ready_key, 0xff, (size_t)D.N * 8, e->stream));  // the recommendation dict: empty
+  std::vector<char*> a;
+  if (int rc = stage_args(e, {{&task, 4}}, a)) return rc;
+  if (int rc = grow_logs(e, 0)) return rc;
+  if (int rc = sync_dev(e)) return rc;
+  dgp::Ctl c0;
+  if (int rc = read_ctl(e, &c0)) return rc;
+  const dgp::ev::LossOrder O{nullptr, nullptr, nullptr, nullptr, 0};
+  hipLaunchKernelGGL(dgp::ev::k_ev_lose_worker, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev,
+                     (int)dgp::ev::LM_RELEASE, -1, (const int32_t*)a[0], 1, (const int8_t*)nullptr,
+                     (const int32_t*)nullptr, 0, O, e->d_aux + 3);
+  HIPCHK(e, hipGetLastError());
+  if (int rc = set_runids(e)) return rc;
+  dgp::Ctl c;
+  if (int rc = check_device_error(e, &c)) {
+    e->pending_resync = true;  // the cascade stopped part-way: the scheduler's state is handed over
+    return c.error == dgp::ERR_UNSUPPORTED ? fail(e, DGP_E_UNSUPPORTED, std::string(e->err)) : rc;
   }
   if (n_new_placements) *n_new_placements = (int64_t)(c.n_placed - c0.n_placed);
   e->last_placed = c.n_placed;
@@ -2649,7 +2680,8 @@ int dgp_lose_worker_ordered(dgp_engine* e, int32_t worker, int64_t n_processing,
                        (int)n_order};
   if (int rc = grow_logs(e, 0)) return rc;
   if (int rc = sync_dev(e)) return rc;
-  hipLaunchKernelGGL(dgp::ev::k_ev_lose_worker, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev, worker,
+  hipLaunchKernelGGL(dgp::ev::k_ev_lose_worker, dim3(1), dim3(dgp::CTA), 0, e->stream, e->d_dev, (int)dgp::ev::LM_LOSS,
+                     worker,
                      (const int32_t*)a[0], (int)n_processing, killed ? (const int8_t*)a[6] : nullptr,
                      (const int32_t*)a[1], (int)n_held, O, e->d_aux + 3);
   HIPCHK(e, hipGetLastError());

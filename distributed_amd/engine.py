@@ -495,6 +495,19 @@ class PlacementEngine:
         """Scheduler.remove_worker's worker table part (distributed/scheduler.py:5213-5231)."""
         self._check(self.lib.dgp_remove_worker(self.h, int(worker)), "dgp_remove_worker")
 
+    def reschedule(self, task: int) -> int | None:
+        """Scheduler._reschedule (distributed/scheduler.py:7900-7924) of a processing task on
+        the device (dgp_reschedule): released from its worker, waiting again, placed again.
+        Returns the placements it made (0 or 1), or None when the engine leaves it to the
+        scheduler (a task nobody needs); then ``sync()`` follows as after remove_worker."""
+        newp = C.c_int64(0)
+        rc = self.lib.dgp_reschedule(self.h, int(task), C.byref(newp))
+        if rc == self.UNSUPPORTED:
+            self.refusal = (self.lib.dgp_last_error(self.h) or b"").decode()
+            return None
+        self._check(rc, "dgp_reschedule")
+        return int(newp.value)
+
     @staticmethod
     def _order_rows(order):
         """(task, kind, tasks) rows as the C ABI's sorted CSR (one row per (task, kind): the first)."""

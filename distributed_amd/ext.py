@@ -88,6 +88,10 @@ _REFILL_TRANSITIONS = _ADD_WORKER_TRANSITIONS
 # waits for released, then the queue refill
 _ERRED_TRANSITIONS = frozenset({("processing", "erred"), ("waiting", "released"), ("released", "erred"),
                                 ("memory", "released"), ("queued", "processing")})
+# reschedule (Scheduler._reschedule :7900-7924): processing -> released -> waiting, then
+# decide_worker (dgp_reschedule)
+_RESCHEDULE_TRANSITIONS = frozenset({("processing", "released"), ("released", "waiting"), ("waiting", "processing"),
+                                     ("waiting", "queued"), ("waiting", "no-worker")})
 # a worker lost with processing tasks / sole replicas (Scheduler.remove_worker :5233-5303):
 # processing -> released (-> waiting through released, :1961-1984), memory -> released for the
 # lost results and the recompute chains' released dependencies, released -> waiting, then
@@ -418,7 +422,7 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._wrap(handlers, "long-running", self._on_long_running, _REFILL_TRANSITIONS)
             self._wrap(handlers, "worker-status-change", self._on_worker_status_change, _REFILL_TRANSITIONS)
             self._wrap(handlers, "task-erred", self._on_task_erred, _ERRED_TRANSITIONS)
-            self._wrap(handlers, "reschedule", None, ())
+            self._wrap(handlers, "reschedule", self._on_reschedule, _RESCHEDULE_TRANSITIONS)
             # client stream handlers (:3781-3792)
             self._wrap(handlers, "client-desires-keys", self._on_client_desires_keys, ())
             self._wrap(handlers, "client-releases-keys", self._on_client_releases_keys, ())
@@ -1541,6 +1545,29 @@ class GPUPlacementExtension(SchedulerPlugin):
         self._engine_op("set_worker_status", wi, 1 if name == "running" else 0)
         if self.active and name == "running":
             self._window = (_ADD_WORKER_TRANSITIONS, None)
+
+    def _on_reschedule(self, kw):
+        """reschedule (Scheduler._reschedule :7900-7924, the worker's Reschedule): a processing
+        task released and placed again -- on the device (dgp_reschedule) when something needs
+        it; otherwise (its release would release its dependencies) the scheduler decides and
+        the engine resynchronises."""
+        s = self.scheduler
+        ts = s.tasks.get(kw.get("key"))
+        if ts is None or ts.state != "processing":  # the reference returns without a transition
+            return
+        w = kw.get("worker")
+        if w and ts.processing_on is not None and ts.processing_on.address != w:
+            return
+        if ts.key not in self.task_index:
+            return
+        if not (ts.waiters or ts.who_wants) or ts.has_lost_dependencies or ts.actor or \
+                not hasattr(self.engine, "reschedule"):
+            self._suspend(f"reschedule of {ts.key!r} is not restated by the engine")
+            self._mark_dirty(ts.key)
+            return
+        if self._engine_op("reschedule", self.task_index[ts.key]) is None and self.active:
+            self._suspend(f"reschedule of {ts.key!r}: {getattr(self.engine, 'refusal', 'refused by the engine')}")
+            self._mark_dirty(ts.key)
 
     def _on_task_erred(self, kw):
         """task-erred (Scheduler.handle_task_erred :5799-5805 -> stimulus_task_erred

@@ -297,6 +297,14 @@ int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr,
  * stimulus and the caller resynchronises as before. Replaces the scheduler's Python for that
  * stimulus (scheduler.py:4600-4653). */
 int dgp_graph_stimulus(dgp_engine* e, int64_t* n_new_placements);
+/* dgp_reschedule (ABI 21): Scheduler._reschedule (scheduler.py:7900-7924) of a processing task
+ * -- transitions({key: "released"}): it leaves its worker (check_idle_saturated), is
+ * recommended waiting when something needs it and placed again by decide_worker, through the
+ * worker-loss recommendation machine. *n_new_placements: 0 or 1. DGP_E_UNSUPPORTED (a task
+ * nobody needs: its release would release its dependencies) leaves the engine to be
+ * resynchronised as after dgp_lose_worker; DGP_E_STATE (ERR_BAD_STATE) for a task that is not
+ * processing. */
+int dgp_reschedule(dgp_engine* e, int32_t task, int64_t* n_new_placements);
 /* dgp_graph_stimulus_ordered (ABI 21): dgp_graph_stimulus, and an earlier dependency that is
  * released is recomputed (_transition_released_waiting :2101-2106, back to results in
  * memory): the runnable new tasks are recommended waiting in the dict's order (priority

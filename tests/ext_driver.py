@@ -1004,6 +1004,9 @@ class EventEngine(FixtureEngine):
     def long_running(self, t, cd):
         return self._event("long", int(t), float(cd))
 
+    def reschedule(self, t):  # dgp_reschedule: the fixture's placements of that event
+        return self._event("resched", int(t))
+
     def heartbeat(self, bw, ps, ds):
         return self._event("heartbeat", float(bw), [int(x) for x in ps], [float(x) for x in ds])
 
@@ -1197,7 +1200,7 @@ def run_events(name, plain=False):
     s._transitions(recs, {}, {}, "update-graph")
     want = []  # the engine calls the events imply
     n_sync = 0
-    on_device = set()  # EV_REMOVE_WORKER events the engine decided (dgp_lose_worker)
+    on_device = set()  # EV_REMOVE_WORKER / EV_RESCHEDULE events the engine decided (dgp_lose_worker, dgp_reschedule)
 
     def check_sync():
         """The last engine call is the resync of this event: its worker / global rows equal
@@ -1316,7 +1319,15 @@ def run_events(name, plain=False):
                     continue
                 want.append(("remove", w))
             elif kd == EV_RESCHEDULE:
+                rs0 = ext.stats["reschedule"]
                 H["reschedule"](key=tss[t].key, worker=addr[w], stimulus_id=sid)
+                if ext.stats["reschedule"] > rs0:  # decided by the engine (dgp_reschedule): no resync
+                    assert eng.calls[-1] == ("resched", ext.task_index[fkeys[t]]), eng.calls[-1]
+                    want.append(eng.calls[-1])
+                    on_device.add(i)
+                    n_sync += 1  # the fixture's resync rows of this event are not needed
+                    snap.pop("before", None)
+                    continue
             else:
                 H["client-releases-keys"](keys=[tss[t].key], client="client-0", stimulus_id=sid)
             if not plain:

@@ -180,14 +180,14 @@ def test_extension_follows_the_p2p_shuffle_lifecycle():
     hands the new overrides to the engine (dgp_set_rootish); the barrier's completion places
     the unpacks on the device as non-rootish; each unpack's restrict_task -> set_restrictions
     (:101-115, :281-293 -> scheduler.py:7702-7707, the *method*) reaches the engine
-    (dgp_update_restrictions); its Reschedule is the scheduler's stimulus, then a resync.
-    The extension stays active throughout; every other placement is the engine's
-    (validate=True)."""
+    (dgp_update_restrictions); its Reschedule runs on the engine too (dgp_reschedule: the
+    unpack released from its worker and placed again on its restriction). The extension stays
+    active throughout with no resync; every placement is the engine's (validate=True)."""
     res = drive(P2P)
     assert [r["fixture"] for r in res] == P2P
     for r in res:
-        assert r["active"] and r["resyncs"] > 0, r
-        assert r["device_decisions"] + r["host_placements"] == r["placements"], r
+        assert r["active"] and r["resyncs"] == 0 and r["calls"]["reschedule"] > 0, r
+        assert r["device_decisions"] == r["placements"], r
 
 
 def test_extension_resyncs_after_stimuli_it_does_not_model():

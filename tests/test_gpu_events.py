@@ -73,7 +73,7 @@ def loss_killed(z, i, proc):
     return [int(t) in k for t in proc]
 
 
-def drive_events(eng, g, z, exp=None):
+def drive_events(eng, g, z, exp=None, device_resched=False):
     """Every event of a svcev_* stream through the engine, snapshot per round; returns the
     placements each event made (update_graph's first)."""
     kind, task, worker, x = z["ev_kind"], z["ev_task"], z["ev_worker"], z["ev_x"]
@@ -116,6 +116,8 @@ def drive_events(eng, g, z, exp=None):
                 npr = int(x[i])
                 assert eng.lose_worker(w, lst[:npr], lst[npr:], loss_order_rows(z, i),
                                        loss_killed(z, i, lst[:npr])) is not None, (i, eng.refusal)
+            elif kd == EV_RESCHEDULE and device_resched and eng.reschedule(t) is not None:
+                n_sync += 1  # decided on the device (dgp_reschedule): the fixture's resync rows unused
             elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
                 # the scheduler decided this stimulus itself: its placements, then its state
                 n = int(exp["stim_nplaced"][len(stim)])
@@ -245,13 +247,16 @@ def test_service_worker_loss_on_the_engine(name):
 
 
 @pytest.mark.parametrize("name", svc_resync_files())
-def test_service_resync_matches_reference(name):
+@pytest.mark.parametrize("device_resched", [False, True], ids=["resync", "resched-on-device"])
+def test_service_resync_matches_reference(name, device_resched):
     """Worker removal (Scheduler.remove_worker, scheduler.py:5180-5360: processing tasks
     released and re-placed, lost results recomputed), rescheduling (:7900-7927) and client
     releases (:5417-5430) decided by the scheduler itself, the engine resynchronised from
     its state (dgp_remove_worker, dgp_sync_*) after each, interleaved with every modelled
     event: the engine's own decisions from then on, the snapshots and the final states equal
-    the reference's."""
+    the reference's. resched-on-device: each reschedule decided by the engine instead
+    (dgp_reschedule: released, waiting again, decide_worker), the scheduler's stimulus and
+    resync only when it refuses (a task nobody needs)."""
     from distributed_amd.engine import PlacementEngine
 
     path = os.path.join(GOLDEN, name)
@@ -262,7 +267,7 @@ def test_service_resync_matches_reference(name):
     with PlacementEngine(0) as eng:
         eng.load(g, cfg, snapshots=R, results=False)
         eng.update_graph()
-        stim = drive_events(eng, g, z, exp)
+        stim = drive_events(eng, g, z, exp, device_resched=device_resched)
         out = eng.placements()
         out.update(eng.snapshots(R))
         out["final_state"] = eng.task_states()
@@ -275,13 +280,14 @@ def test_service_resync_matches_reference(name):
 
 
 @pytest.mark.parametrize("name", svc_p2p_files())
-def test_service_p2p_shuffle_lifecycle_matches_reference(name):
+@pytest.mark.parametrize("device_resched", [False, True], ids=["resync", "resched-on-device"])
+def test_service_p2p_shuffle_lifecycle_matches_reference(name, device_resched):
     """The P2P shuffle's scheduler-side lifecycle (gen_service.py p2p): the unpacks' _rootish
     set False when the first transfer runs (dgp_set_rootish), the barrier's completion
     placing them on the device as non-rootish, each unpack's restrict_task (dgp_update_
-    restrictions) and Reschedule (the scheduler's stimulus, then dgp_sync_*), the re-placed
-    unpacks completing: every placement, snapshot and final state equals the reference's
-    ShuffleSchedulerPlugin-driven scheduler."""
+    restrictions) and Reschedule (the scheduler's stimulus, then dgp_sync_*; resched-on-device:
+    dgp_reschedule, no resync), the re-placed unpacks completing: every placement, snapshot
+    and final state equals the reference's ShuffleSchedulerPlugin-driven scheduler."""
     from distributed_amd.engine import PlacementEngine
 
     path = os.path.join(GOLDEN, name)
@@ -292,7 +298,7 @@ def test_service_p2p_shuffle_lifecycle_matches_reference(name):
     with PlacementEngine(0) as eng:
         eng.load(g, cfg, snapshots=R, results=False)
         eng.update_graph()
-        stim = drive_events(eng, g, z, exp)
+        stim = drive_events(eng, g, z, exp, device_resched=device_resched)
         out = eng.placements()
         out.update(eng.snapshots(R))
         out["final_state"] = eng.task_states()
