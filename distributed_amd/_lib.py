@@ -48,6 +48,7 @@ SIGNATURES = {
     "dgp_graph_stimulus": (C.c_int, [_P, _P]),
     "dgp_graph_stimulus_ordered": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, _P]),
     "dgp_reschedule": (C.c_int, [_P, C.c_int32, _P]),
+    "dgp_release_tasks": (C.c_int, [_P, C.c_int64, _P, _P, _P]),
     "dgp_add_graph_deferred": (C.c_int, [_P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32, _P, _P]),
     "dgp_snapshot": (C.c_int, [_P]),
     "dgp_num_placements": (C.c_int64, [_P]),

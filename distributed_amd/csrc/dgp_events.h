@@ -395,6 +395,41 @@ __global__ void __launch_bounds__(64) k_ev_task_erred(const Dev* __restrict__ Dp
   if (lane == 0) *placed = n;
 }
 
+// client-releases-keys (:5417-5430) whose transitions touch only results in memory (or
+// released): each listed task memory -> released (remove_all_replicas :3161-3171, its
+// holders' ws.nbytes) or, flagged, on to forgotten (_propagate_forgotten :3359-3398; the
+// row stays, released, TF_FORGOTTEN: the host sets the flags), then the queue refill
+// (stimulus_queue_slots_maybe_opened :5430). The host lists the closure the scheduler's
+// transitions reach (distributed_amd/loss.py release_plan); the effects commute.
+__global__ void __launch_bounds__(64) k_ev_release_tasks(const Dev* __restrict__ Dp, const int32_t* __restrict__ task,
+                                                           int n, long long* placed) {
+  const Dev& D = *Dp;
+  __shared__ SCtl S;
+  ev_init(S);
+  const int lane = lane_id();
+  if (lane == 0) {
+    *placed = 0;
+    for (int i = 0; i < n; i++) {
+      const int t = task[i];
+      if (D.state[t] != S_MEMORY) continue;  // released already: nothing held
+      const int64_t nb = nbv(D, D.res_nbytes[t]);
+      for (int b = 0; b < D.WB; b++) {
+        unsigned long long m = D.holders[(size_t)t * D.WB + b];
+        D.holders[(size_t)t * D.WB + b] = 0;
+        for (; m; m &= m - 1) D.w_nbytes[b * 64 + __builtin_ctzll(m)] -= nb;
+      }
+      D.tdyn[t] &= (uint8_t)~TD_MULTI;
+      D.holder_of[t] = -1;
+      D.state[t] = S_RELEASED;
+      atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], 1ull);
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  const long long m = st::refill_queue(D, S);
+  if (lane == 0) *placed = m;
+}
+
 // ================================================================= worker loss (f2)
 // Scheduler.remove_worker (scheduler.py:5180-5303) of a worker with processing tasks or
 // sole replicas, decided here instead of by the scheduler. The host passes the worker's

@@ -2429,6 +2429,38 @@ int dgp_long_running(dgp_engine* e, int32_t task, double compute_duration, int64
   }, n_new_placements);
 }
 
+int dgp_release_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t* forget, int64_t* n_new_placements) {
+  if (int rc_ = resident_stop(e)) return rc_;
+  if (n_new_placements) *n_new_placements = 0;
+  if (int rc = event_ready(e, "dgp_release_tasks")) return rc;
+  dgp::Dev& D = e->D;
+  if (n < 0 || (n > 0 && (!task || !forget))) return fail(e, DGP_E_ARG, "dgp_release_tasks: bad batch");
+  for (int64_t i = 0; i < n; i++)
+    if (task[i] < 0 || task[i] >= D.N) return fail(e, DGP_E_ARG, "dgp_release_tasks: task out of range");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  // only results in memory or released: anything else (a cancellation) is the scheduler's
+  std::vector<uint8_t> st((size_t)D.N);
+  HIPCHK(e, hipMemcpy(st.data(), D.state, (size_t)D.N, hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < n; i++)
+    if ((st[task[i]] != dgp::S_MEMORY && st[task[i]] != dgp::S_RELEASED) || (e->tflags_h[task[i]] & dgp::TF_FORGOTTEN))
+      return fail(e, DGP_E_UNSUPPORTED, "dgp_release_tasks: a task that is not in memory or released (a "
+                                        "cancellation: the scheduler decides, then dgp_sync_*)");
+  // who_wants emptied; forgotten ones leave SchedulerState.tasks (their rows stay, flagged)
+  for (int64_t i = 0; i < n; i++) {
+    const int32_t t = task[i];
+    e->tflags_h[t] = (uint8_t)((e->tflags_h[t] & ~dgp::TF_WANTED) | (forget[i] ? dgp::TF_FORGOTTEN : 0));
+    e->h_wanted[t] = 0;
+  }
+  HIPCHK(e, hipMemcpy(const_cast<uint8_t*>(D.tflags), e->tflags_h.data(), D.N, hipMemcpyHostToDevice));
+  std::vector<char*> a;
+  if (int rc = stage_args(e, {{task, (size_t)n * 4}}, a)) return rc;
+  return event_with_refill(e, [&] {
+    hipLaunchKernelGGL(dgp::ev::k_ev_release_tasks, dim3(1), dim3(64), 0, e->stream, e->d_dev, (const int32_t*)a[0],
+                       (int)n, e->d_aux + 3);
+  }, n_new_placements);
+}
+
 int dgp_heartbeat(dgp_engine* e, double bandwidth, int64_t n, const int32_t* prefix, const double* duration) {
   if (int rc_ = resident_stop(e)) return rc_;
   if (int rc = event_ready(e, "dgp_heartbeat")) return rc;

@@ -508,6 +508,22 @@ class PlacementEngine:
         self._check(rc, "dgp_reschedule")
         return int(newp.value)
 
+    def release_tasks(self, task, forget) -> int | None:
+        """client-releases-keys (distributed/scheduler.py:5417-5430) that reaches only results in
+        memory or released (dgp_release_tasks): each task released with its replicas, forgotten
+        where flagged, then the queue refill. Returns its placements, or None when the engine
+        leaves it to the scheduler (a cancellation), with nothing changed."""
+        t, f = self._arr(task, np.int32), self._arr(forget, np.uint8)
+        if len(t) != len(f):
+            raise ValueError("one forget flag per task")
+        newp = C.c_int64(0)
+        rc = self.lib.dgp_release_tasks(self.h, len(t), _ptr(t), _ptr(f), C.byref(newp))
+        if rc == self.UNSUPPORTED:
+            self.refusal = (self.lib.dgp_last_error(self.h) or b"").decode()
+            return None
+        self._check(rc, "dgp_release_tasks")
+        return int(newp.value)
+
     @staticmethod
     def _order_rows(order):
         """(task, kind, tasks) rows as the C ABI's sorted CSR (one row per (task, kind): the first)."""

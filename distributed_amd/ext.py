@@ -88,6 +88,10 @@ _REFILL_TRANSITIONS = _ADD_WORKER_TRANSITIONS
 # waits for released, then the queue refill
 _ERRED_TRANSITIONS = frozenset({("processing", "erred"), ("waiting", "released"), ("released", "erred"),
                                 ("memory", "released"), ("queued", "processing")})
+# client-releases-keys of results in memory (:5417-5430): memory -> released / forgotten,
+# released -> forgotten (dgp_release_tasks), then the queue refill
+_RELEASE_TRANSITIONS = frozenset({("memory", "released"), ("memory", "forgotten"), ("released", "forgotten"),
+                                  ("queued", "processing")})
 # reschedule (Scheduler._reschedule :7900-7924): processing -> released -> waiting, then
 # decide_worker (dgp_reschedule)
 _RESCHEDULE_TRANSITIONS = frozenset({("processing", "released"), ("released", "waiting"), ("waiting", "processing"),
@@ -425,8 +429,8 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._wrap(handlers, "reschedule", self._on_reschedule, _RESCHEDULE_TRANSITIONS)
             # client stream handlers (:3781-3792)
             self._wrap(handlers, "client-desires-keys", self._on_client_desires_keys, ())
-            self._wrap(handlers, "client-releases-keys", self._on_client_releases_keys, ())
-            self._wrap(handlers, "cancel-keys", self._on_client_releases_keys, ())
+            self._wrap(handlers, "client-releases-keys", self._on_client_releases_keys, _RELEASE_TRANSITIONS)
+            self._wrap(handlers, "cancel-keys", self._on_cancel_keys, ())
             self._wrap(handlers, "close-client", self._on_close_client, ())
             self._wrap(handlers, "update-data", self._on_update_data, ())
         rpc = getattr(s, "handlers", None)
@@ -1163,7 +1167,7 @@ class GPUPlacementExtension(SchedulerPlugin):
         stimuli the engine follows, or of a kind it does not model, means the scheduler's
         state moved where the engine's did not."""
         pair = (start, finish)
-        if self._allowed and pair in self._allowed[-1]:  # the running stimulus' own transitions
+        if self._allowed and pair in self._allowed[-1] and not self.suspended:  # the stimulus' own, followed
             return
         if not self.active or self.engine is None:
             return
@@ -1594,12 +1598,34 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._engine_op("set_wanted", t, [1] * len(t))
 
     def _on_client_releases_keys(self, kw):
-        """client-releases-keys / cancel-keys (:5417-5430, :5364-5396): tasks no longer
-        wanted are released or forgotten, and who_wants changes even where nothing
-        transitions: the scheduler's own stimulus, then a resync of those keys."""
+        """client-releases-keys (:5417-5430): tasks no longer wanted are released or
+        forgotten. When its transitions reach only results in memory (or released), the engine
+        follows on the device (dgp_release_tasks: replicas, who_wants, forgotten rows, the
+        queue refill); otherwise (a cancellation) the scheduler's own stimulus, then a resync
+        of those keys."""
+        s = self.scheduler
+        keys = [k for k in kw.get("keys") or () if k in self.task_index]
+        if not keys:
+            return
+        plan = None
+        if hasattr(self.engine, "release_tasks"):
+            plan = loss.release_plan(s, kw.get("client"), keys)
+        ti = self.task_index
+        if plan is not None and all(ts.key in ti for ts, _ in plan):
+            if not plan:
+                return  # who_wants of another client only: nothing transitions
+            if self._engine_op("release_tasks", [ti[ts.key] for ts, _ in plan], [1 if f else 0 for _, f in plan]) \
+                    is not None or not self.active:
+                return
+        self._suspend("client-releases-keys")
+        for k in keys:
+            self._mark_dirty(k)
+
+    def _on_cancel_keys(self, kw):
+        """cancel-keys (:5364-5396): the scheduler's own stimulus, then a resync of those keys."""
         keys = [k for k in kw.get("keys") or () if k in self.task_index]
         if keys:
-            self._suspend("client-releases-keys / cancel-keys")
+            self._suspend("cancel-keys")
             for k in keys:
                 self._mark_dirty(k)
 

@@ -168,3 +168,48 @@ def graph_orders(new, chain, index_of) -> list:
     cs = set(chain)
     return [(index_of(t), LO_DEPS, [index_of(d) for d in t.dependencies])
             for t in list(new) + list(chain) if sum(d in cs for d in t.dependencies) >= 2]
+
+
+def release_plan(s, client, keys) -> list | None:
+    """client-releases-keys (scheduler.py:5417-5430): the tasks its transitions reach, each
+    with its forget flag -- the keys no other client wants (_client_releases_keys
+    :3400-3419: forgotten without dependents, else released when nothing waits on them), then
+    every dependency _propagate_forgotten forgets (:3378-3385: no dependent left, not wanted)
+    -- when all of them are results in memory or released (dgp_release_tasks); None when
+    the release reaches anything else (a cancellation, an erred or actor task, a forgotten
+    task with dependents still live): the scheduler's stimulus, then a resync."""
+    cs = s.clients.get(client)
+    if cs is None:
+        return []
+    recs, seen = [], set()
+    for key in keys:
+        ts = s.tasks.get(key)
+        if ts is None or ts in seen or ts not in (cs.wants_what or ()):
+            continue
+        seen.add(ts)
+        if (ts.who_wants or set()) - {cs}:
+            continue  # still wanted by another client: who_wants changes, nothing transitions
+        if not ts.dependents:
+            recs.append((ts, True))
+        elif ts.state != "erred" and not ts.waiters:
+            recs.append((ts, False))
+    plan, forgotten, stack = {}, set(), list(recs)
+    while stack:
+        ts, forget = stack.pop()
+        if ts.state not in ("memory", "released") or ts.actor:
+            return None
+        if not forget and (not ts.run_spec or ts.has_lost_dependencies):
+            forget = True  # memory -> released of pure data / lost dependencies: forgotten (:2485-2488)
+        if not forget:
+            plan.setdefault(ts, False)
+            continue
+        if ts in forgotten:
+            continue
+        forgotten.add(ts)
+        plan[ts] = True
+        if any(d not in forgotten for d in ts.dependents):
+            return None  # its dependents would be forgotten or flagged with lost dependencies
+        for dts in ts.dependencies:
+            if not any(x not in forgotten for x in dts.dependents) and not dts.who_wants:
+                stack.append((dts, True))
+    return list(plan.items())

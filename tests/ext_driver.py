@@ -1007,6 +1007,9 @@ class EventEngine(FixtureEngine):
     def reschedule(self, t):  # dgp_reschedule: the fixture's placements of that event
         return self._event("resched", int(t))
 
+    def release_tasks(self, t, f):  # dgp_release_tasks: the fixture's placements of that event
+        return self._event("release", [int(x) for x in t], [int(x) for x in f])
+
     def heartbeat(self, bw, ps, ds):
         return self._event("heartbeat", float(bw), [int(x) for x in ps], [float(x) for x in ds])
 
@@ -1329,7 +1332,20 @@ def run_events(name, plain=False):
                     snap.pop("before", None)
                     continue
             else:
+                rl0 = ext.stats["release_tasks"]
                 H["client-releases-keys"](keys=[tss[t].key], client="client-0", stimulus_id=sid)
+                if ext.stats["release_tasks"] > rl0:  # followed by the engine (dgp_release_tasks): no resync
+                    c = eng.calls[-1]
+                    assert c[0] == "release", c
+                    if "rk_evptr" in z.files:  # the extension's closure is the generator's
+                        rp = z["rk_evptr"]
+                        want_t = [ext.task_index[fkeys[q]] for q in z["rk_task"][rp[i]:rp[i + 1]].tolist()]
+                        assert sorted(zip(c[1], c[2])) == sorted(zip(want_t, z["rk_forget"][rp[i]:rp[i + 1]].tolist())), i
+                    want.append(c)
+                    on_device.add(i)
+                    n_sync += 1
+                    snap.pop("before", None)
+                    continue
             if not plain:
                 check_sync()
                 want.append(eng.calls[-1])
@@ -1441,7 +1457,7 @@ if __name__ == "__main__":
             continue
         fn = (run_joins if nm.startswith("svcaddw_") else (lambda x: run_second_graph(x, "--resync" in args))
               if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_", "svcgrec_"))
-              else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcrt_", "svcwl_", "svcp2p_"))
+              else (lambda x: run_events(x, plain)) if nm.startswith(("svcev_", "svcrs_", "svcrt_", "svcwl_", "svcp2p_", "svcrel_"))
               else run_prefixes if nm.startswith("svcpfx_")
               else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,

@@ -948,7 +948,7 @@ def _erred_is_simple(s, ts):
 
 
 def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_scale=0.3, dumps=None, chains=False,
-                  allowed_failures=3):
+                  allowed_failures=3, release_memory=False):
     """The replay protocol's completions as task-finished messages, interleaved with the
     other worker stimuli that change placement inputs, each through the reference's own
     handler (``Scheduler.*`` borrowed onto the replay state):
@@ -1033,7 +1033,8 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
     s._transitions(recs, {}, {}, "update-graph")
     ev = {k: [] for k in ("kind", "task", "worker", "x", "nbytes", "start", "stop", "runid")}
     hb = {"ptr": [0], "task": [], "dur": []}
-    lo = {"evptr": [0], "task": [], "kind": [], "rowptr": [0], "idx": [], "kptr": [0], "ktask": []}
+    lo = {"evptr": [0], "task": [], "kind": [], "rowptr": [0], "idx": [], "kptr": [0], "ktask": [],
+          "rptr": [0], "rtask": [], "rforget": []}
     hb["lo"] = lo
     LS = _load_repo_module("loss") if chains else None
     stim = [len(rec["task"])]
@@ -1049,6 +1050,7 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
         hb["ptr"].append(len(hb["task"]))
         lo["evptr"].append(len(lo["task"]))
         lo["kptr"].append(len(lo["ktask"]))
+        lo["rptr"].append(len(lo["rtask"]))
 
     def event():
         kind = int(rng.choice(kinds))
@@ -1208,10 +1210,18 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             s._reschedule(ts.key, addr[w], stimulus_id=sid)
             push(EV_RESCHEDULE, tidx[ts.key], w)
         elif kind == EV_RELEASE_KEYS:
-            wanted = [ts for ts in tss if ts.who_wants and ts.state in ("waiting", "processing", "queued")]
+            states = ("memory",) if release_memory else ("waiting", "processing", "queued")
+            wanted = [ts for ts in tss if ts.who_wants and ts.state in states]
             if not wanted:
                 return
             ts = wanted[int(rng.integers(0, len(wanted)))]
+            if release_memory:  # what the engine takes (distributed_amd/loss.py release_plan, as the extension)
+                LR = _load_repo_module("loss")
+                plan = LR.release_plan(s, "client-0", [ts.key])
+                assert plan is not None, ts.key
+                for x, f in plan:
+                    lo["rtask"].append(tidx[x.key])
+                    lo["rforget"].append(1 if f else 0)
             s.client_releases_keys(keys=[ts.key], client="client-0", stimulus_id=sid)
             push(EV_RELEASE_KEYS, tidx[ts.key], -1)
         elif kind == EV_ERRED:
@@ -1357,7 +1367,8 @@ def replay_p2p(g, cfg, dumps):
     s._transitions(recs, {}, {}, "update-graph")
     ev = {k: [] for k in ("kind", "task", "worker", "x", "nbytes", "start", "stop", "runid")}
     hb = {"ptr": [0], "task": [], "dur": []}
-    lo = {"evptr": [0], "task": [], "kind": [], "rowptr": [0], "idx": [], "kptr": [0], "ktask": []}
+    lo = {"evptr": [0], "task": [], "kind": [], "rowptr": [0], "idx": [], "kptr": [0], "ktask": [],
+          "rptr": [0], "rtask": [], "rforget": []}
     hb["lo"] = lo
     LS = _load_repo_module("loss") if chains else None
     stim = [len(rec["task"])]
@@ -1529,6 +1540,10 @@ def main_resync(only):
         "svcwl_killed_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=59, n_inner_prefixes=3,
                                                                    random_durations=True, nthreads="random"), 1.1, 59, 0.12),
         "svcwl_killed_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=60), float("inf"), 60, 0.12),
+        # clients release results in memory (forgotten / released, the dependencies they forget)
+        "svcrel_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=63, n_inner_prefixes=3,
+                                                             random_durations=True, nthreads="random"), 1.1, 63, 0.12),
+        "svcrel_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=64), float("inf"), 64, 0.12),
         # allowed_failures 0: every processing task of a lost worker errs
         "svcwl_killed0_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=61, n_inner_prefixes=3,
                                                                     random_durations=True, nthreads="random"), 1.1, 61, 0.12),
@@ -1542,10 +1557,11 @@ def main_resync(only):
         cfg = G.config_dict(sat)
         dumps = []
         kinds_ = ((1, 2, 3, 4, 5, 6, 7, EV_RETIRE, EV_RETIRE, EV_PAUSE) if name.startswith("svcrt_") else
-                  (1, 2, 3, 4, 5, 6, 7, EV_LOSE_WORKER, EV_LOSE_WORKER, EV_RESUME) if name.startswith("svcwl_") else kinds)
+                  (1, 2, 3, 4, 5, 6, 7, EV_LOSE_WORKER, EV_LOSE_WORKER, EV_RESUME) if name.startswith("svcwl_") else
+                  (1, 2, 3, 4, 5, 6, 7, EV_RELEASE_KEYS, EV_RELEASE_KEYS) if name.startswith("svcrel_") else kinds)
         rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(
             g, cfg, seed, p_event, kinds_, dumps=dumps, chains=name.startswith(("svcwl_chain_", "svcwl_killed")),
-            allowed_failures=loss_allowed_failures(name))
+            allowed_failures=loss_allowed_failures(name), release_memory=name.startswith("svcrel_"))
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))
@@ -1558,6 +1574,9 @@ def main_resync(only):
         if dumps:
             z.update(_pack_dumps(dumps))
         lo = hb["lo"]
+        if lo["rtask"]:
+            z.update(rk_evptr=np.array(lo["rptr"], np.int64), rk_task=np.array(lo["rtask"], np.int32),
+                     rk_forget=np.array(lo["rforget"], np.uint8))
         if lo["task"] or lo["ktask"]:
             z.update(lo_evptr=np.array(lo["evptr"], np.int64), lo_task=np.array(lo["task"], np.int32),
                      lo_kind=np.array(lo["kind"], np.int8), lo_rowptr=np.array(lo["rowptr"], np.int64),

@@ -243,6 +243,20 @@ def test_extension_runs_worker_losses_on_the_engine():
         assert r["device_decisions"] == r["placements"], r
 
 
+def test_extension_follows_client_releases_on_the_engine():
+    """Clients release results in memory (svcrel_*): the extension computes what the
+    scheduler's transitions will reach (loss.release_plan: the keys forgotten or released, the
+    dependencies forgotten with them) and the engine follows on the device
+    (dgp_release_tasks) before the handler runs; the closures equal the generator's, no
+    resync, every placement the engine's (validate=True)."""
+    names = ["svcrel_c2var_sat1.1.npz", "svcrel_c2mini_satinf.npz"]
+    res = drive(names)
+    assert [r["fixture"] for r in res] == names
+    for r in res:
+        assert r["active"] and r["resyncs"] == 0 and r["calls"]["release_tasks"] >= 50, r
+        assert r["device_decisions"] == r["placements"], r
+
+
 def test_extension_hands_back_on_unmodelled_events():
     """An engine without the event calls: the first such event ends GPU placement loudly
     ("not modelled") and the scheduler's own decisions carry on, equal to the reference's."""

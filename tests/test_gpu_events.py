@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 
 from conftest import (GOLDEN, second_graph, svc_dep_graph_files, svc_event_files, svc_p2p_files, svc_prio_graph_files,
-                      svc_loss_files, svc_resync_files, svc_restr_graph_files, svc_retire_files)
+                      svc_loss_files, svc_release_files, svc_resync_files, svc_restr_graph_files, svc_retire_files)
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -73,7 +73,7 @@ def loss_killed(z, i, proc):
     return [int(t) in k for t in proc]
 
 
-def drive_events(eng, g, z, exp=None, device_resched=False):
+def drive_events(eng, g, z, exp=None, device_resched=False, device_release=False):
     """Every event of a svcev_* stream through the engine, snapshot per round; returns the
     placements each event made (update_graph's first)."""
     kind, task, worker, x = z["ev_kind"], z["ev_task"], z["ev_worker"], z["ev_x"]
@@ -118,6 +118,11 @@ def drive_events(eng, g, z, exp=None, device_resched=False):
                                        loss_killed(z, i, lst[:npr])) is not None, (i, eng.refusal)
             elif kd == EV_RESCHEDULE and device_resched and eng.reschedule(t) is not None:
                 n_sync += 1  # decided on the device (dgp_reschedule): the fixture's resync rows unused
+            elif kd == EV_RELEASE_KEYS and device_release:
+                rp = z["rk_evptr"]  # the release's closure (loss.release_plan in the generator)
+                rows = slice(rp[i], rp[i + 1])
+                assert eng.release_tasks(z["rk_task"][rows], z["rk_forget"][rows]) is not None, (i, eng.refusal)
+                n_sync += 1
             elif kd in (EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS):
                 # the scheduler decided this stimulus itself: its placements, then its state
                 n = int(exp["stim_nplaced"][len(stim)])
@@ -276,6 +281,34 @@ def test_service_resync_matches_reference(name, device_resched):
     assert_same(out, exp, PL_KEYS + ROUND_KEYS)
     # a forgotten task (client released, :2853) leaves SchedulerState.tasks; its engine row
     # stays, released (distributed_amd/sync.py)
+    assert np.array_equal(out["final_state"], np.where(exp["final_state"] == 7, 0, exp["final_state"]))
+
+
+@pytest.mark.parametrize("device_release", [False, True], ids=["resync", "release-on-device"])
+@pytest.mark.parametrize("name", svc_release_files())
+def test_service_client_releases(name, device_release):
+    """Clients release results in memory (client-releases-keys, scheduler.py:5417-5430): the
+    keys forgotten or released with their replicas, the dependencies nobody needs any more
+    forgotten (_propagate_forgotten :3359-3398), then the queue refill -- on the device
+    (dgp_release_tasks, the closure loss.release_plan gives) or, for comparison, decided by
+    the scheduler and resynchronised. Every placement, snapshot and final state equals the
+    reference's (a forgotten task's row stays, released)."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    assert EV_RELEASE_KEYS in set(np.unique(z["ev_kind"]).tolist())
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        stim = drive_events(eng, g, z, exp, device_release=device_release)
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert np.array_equal(stim, exp["stim_nplaced"]), np.nonzero(stim != exp["stim_nplaced"])[0][:5]
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
     assert np.array_equal(out["final_state"], np.where(exp["final_state"] == 7, 0, exp["final_state"]))
 
 
