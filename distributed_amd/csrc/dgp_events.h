@@ -299,6 +299,22 @@ __global__ void __launch_bounds__(64) k_ev_task_erred(const Dev* __restrict__ Dp
         Q[qn++] = y;
       }
     }
+    // a member that is a dependency of another member and that nobody else wants: the other
+    // member's waiting -> released (:2587-2592) recommends it released, which overrides its
+    // "erred" when it is popped later (the dict keeps the place, the value changes), so it
+    // ends released or erred by the recommendation dict's order: not restated here
+    for (long long i = 1; i < qn && ok; i++) {
+      const int y = Q[i];
+      for (int64_t k = D.dep_ptr[y]; k < D.dep_ptr[y + 1] && ok; k++) {
+        const int d = D.dep_idx[k];
+        if (d == t || D.state[d] != S_ERRED || (D.tflags[d] & TF_WANTED)) continue;
+        for (long long j = 1; j < qn; j++)
+          if (Q[j] == d) {
+            ok = false;
+            break;
+          }
+      }
+    }
     // waiters.discard for every dependency outside the closure (:2711-2715, :2593-2598)
     const bool dec = ok;
     for (long long i = 0; i < qn && dec; i++) {
@@ -395,41 +411,6 @@ __global__ void __launch_bounds__(64) k_ev_task_erred(const Dev* __restrict__ Dp
   if (lane == 0) *placed = n;
 }
 
-// client-releases-keys (:5417-5430) whose transitions touch only results in memory (or
-// released): each listed task memory -> released (remove_all_replicas :3161-3171, its
-// holders' ws.nbytes) or, flagged, on to forgotten (_propagate_forgotten :3359-3398; the
-// row stays, released, TF_FORGOTTEN: the host sets the flags), then the queue refill
-// (stimulus_queue_slots_maybe_opened :5430). The host lists the closure the scheduler's
-// transitions reach (distributed_amd/loss.py release_plan); the effects commute.
-__global__ void __launch_bounds__(64) k_ev_release_tasks(const Dev* __restrict__ Dp, const int32_t* __restrict__ task,
-                                                           int n, long long* placed) {
-  const Dev& D = *Dp;
-  __shared__ SCtl S;
-  ev_init(S);
-  const int lane = lane_id();
-  if (lane == 0) {
-    *placed = 0;
-    for (int i = 0; i < n; i++) {
-      const int t = task[i];
-      if (D.state[t] != S_MEMORY) continue;  // released already: nothing held
-      const int64_t nb = nbv(D, D.res_nbytes[t]);
-      for (int b = 0; b < D.WB; b++) {
-        unsigned long long m = D.holders[(size_t)t * D.WB + b];
-        D.holders[(size_t)t * D.WB + b] = 0;
-        for (; m; m &= m - 1) D.w_nbytes[b * 64 + __builtin_ctzll(m)] -= nb;
-      }
-      D.tdyn[t] &= (uint8_t)~TD_MULTI;
-      D.holder_of[t] = -1;
-      D.state[t] = S_RELEASED;
-      atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], 1ull);
-    }
-  }
-  __threadfence();
-  __syncthreads();
-  const long long m = st::refill_queue(D, S);
-  if (lane == 0) *placed = m;
-}
-
 // ================================================================= worker loss (f2)
 // Scheduler.remove_worker (scheduler.py:5180-5303) of a worker with processing tasks or
 // sole replicas, decided here instead of by the scheduler. The host passes the worker's
@@ -506,7 +487,7 @@ __device__ __forceinline__ void rec_push(const Dev& D, long long& sp, int t, int
 // WorkerState.remove_from_processing (:759-771) of t on its worker x, then (a current
 // worker) check_idle_saturated (:3278). needs_what membership is the line's (the removed
 // worker's replicas are gone already: TD_WHELD names what it held, for scan mode).
-__device__ void loss_exit_processing(const Dev& D, int t, int lost_w) {
+__device__ void loss_exit_processing(const Dev& D, int t, int lost_w, bool tree = true) {
   const int x = D.proc_on[t];
   const int p = D.prefix[t];
   uint32_t* L = D.gw_needs_saved + (size_t)x * SNLW;
@@ -542,7 +523,7 @@ __device__ void loss_exit_processing(const Dev& D, int t, int lost_w) {
   D.proc_on[t] = -1;
   if (x != lost_w) {  // _exit_processing_common: a removed worker is not checked (:3275-3276)
     walk_flags(D, x, occupancy(D, x, D.pdur_walk), D.w_nproc[x]);
-    itc_check(D, x, true);
+    itc_check(D, x, tree);
   }
 }
 
@@ -637,6 +618,89 @@ __device__ bool loss_killed(const Dev& D, const LossOrder& O, long long& sp, int
   if (!loss_discard_waiter(D, O, sp, t)) return false;
   D.waiters[t] = 0;  // ts.waiters = None
   return true;
+}
+
+// client-releases-keys (:5417-5430): the transitions _client_releases_keys' recommendations
+// reach (:3400-3419) -- released or forgotten, with every release / forget they recommend in
+// turn -- in the order the scheduler runs them, listed by the host (distributed_amd/loss.py
+// release_plan restates the recommendation dict LIFO); each applied here by its state now:
+//   memory -> released      _transition_memory_released :2444-2505 (remove_all_replicas)
+//   processing -> released  _transition_processing_released :2606-2628 (_exit_processing_common
+//                           :3258-3281, then _propagate_released :3337-3357)
+//   waiting -> released     _transition_waiting_released :2579-2604
+//   queued -> released      _transition_queued_released :2784-2795 (queued.remove)
+//   no-worker -> released   _transition_no_worker_released :2747-2759 (unrunnable.remove)
+//   released                on to forgotten (_propagate_forgotten :3359-3398): the row stays,
+//                           released, TF_FORGOTTEN (the host sets the flags)
+// A cancelled task leaves its dependencies' waiters (a released one has none). Nothing is
+// placed until the queue refill at the end (stimulus_queue_slots_maybe_opened :5430).
+__device__ __forceinline__ void cancel_discard(const Dev& D, int t) {
+  for (int64_t k = D.dep_ptr[t]; k < D.dep_ptr[t + 1]; k++) {
+    const int d = D.dep_idx[k];
+    if (D.state[d] != S_RELEASED && D.waiters[d] > 0) D.waiters[d] -= 1;
+  }
+  D.waiters[t] = 0;  // ts.waiters = None
+}
+
+__global__ void __launch_bounds__(64) k_ev_release_tasks(const Dev* __restrict__ Dp, const int32_t* __restrict__ task,
+                                                           int n, long long* placed) {
+  const Dev& D = *Dp;
+  __shared__ SCtl S;
+  ev_init(S);
+  const int lane = lane_id();
+  if (lane == 0) {
+    *placed = 0;
+    Ctl* c = D.ctl;
+    for (int i = 0; i < n && c->error == 0; i++) {
+      const int t = task[i];
+      const uint8_t st = D.state[t];
+      if (st == S_RELEASED) continue;  // on to forgotten: the flag only
+      if (st == S_MEMORY) {
+        const int64_t nb = nbv(D, D.res_nbytes[t]);
+        for (int b = 0; b < D.WB; b++) {
+          unsigned long long m = D.holders[(size_t)t * D.WB + b];
+          D.holders[(size_t)t * D.WB + b] = 0;
+          for (; m; m &= m - 1) D.w_nbytes[b * 64 + __builtin_ctzll(m)] -= nb;
+        }
+        D.tdyn[t] &= (uint8_t)~TD_MULTI;
+        D.holder_of[t] = -1;
+      } else if (st == S_PROCESSING) {
+        loss_exit_processing(D, t, -1, false);
+        D.holder_of[t] = -1;
+        cancel_discard(D, t);
+      } else if (st == S_WAITING) {
+        cancel_discard(D, t);
+        // waiting_on = None: no later completion of a dependency makes it runnable (the
+        // builder counts completions down on every dependent)
+        D.remaining[t] = ERRED_REMAINING;
+      } else if (st == S_QUEUED) {
+        long long q = c->qhead;
+        const long long e = c->qhead + c->qlen;
+        while (q < e && D.qarr[q] != t) q++;
+        if (q == e) {
+          set_error(D, ERR_BAD_STATE, t);
+          break;
+        }
+        for (; q + 1 < e; q++) D.qarr[q] = D.qarr[q + 1];
+        c->qlen -= 1;
+        cancel_discard(D, t);
+      } else if (st == S_NO_WORKER) {
+        c->n_unrunnable--;
+        cancel_discard(D, t);
+      } else {
+        set_error(D, ERR_UNSUPPORTED, t);
+        break;
+      }
+      if (st != S_WAITING) atomicAdd((unsigned long long*)&D.g_relwait[D.group[t]], 1ull);  // released + waiting
+      D.state[t] = S_RELEASED;
+    }
+    if (S.error) set_error(D, S.error, S.err_task);
+  }
+  __threadfence();
+  __syncthreads();
+  if (D.ctl->error) return;
+  const long long m = st::refill_queue(D, S);
+  if (lane == 0) *placed = m;
 }
 
 // lane 0: pop recommendations until one is a placement (returns its task) or none is left

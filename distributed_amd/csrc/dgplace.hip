@@ -2439,13 +2439,16 @@ int dgp_release_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8
     if (task[i] < 0 || task[i] >= D.N) return fail(e, DGP_E_ARG, "dgp_release_tasks: task out of range");
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  // only results in memory or released: anything else (a cancellation) is the scheduler's
+  // results in memory, released tasks and cancelled work (waiting, processing, queued,
+  // no-worker); an erred or forgotten task is the scheduler's (then dgp_sync_*)
   std::vector<uint8_t> st((size_t)D.N);
   HIPCHK(e, hipMemcpy(st.data(), D.state, (size_t)D.N, hipMemcpyDeviceToHost));
-  for (int64_t i = 0; i < n; i++)
-    if ((st[task[i]] != dgp::S_MEMORY && st[task[i]] != dgp::S_RELEASED) || (e->tflags_h[task[i]] & dgp::TF_FORGOTTEN))
-      return fail(e, DGP_E_UNSUPPORTED, "dgp_release_tasks: a task that is not in memory or released (a "
-                                        "cancellation: the scheduler decides, then dgp_sync_*)");
+  for (int64_t i = 0; i < n; i++) {
+    const uint8_t x = st[task[i]];
+    if (x > dgp::S_MEMORY || (e->tflags_h[task[i]] & dgp::TF_FORGOTTEN))
+      return fail(e, DGP_E_UNSUPPORTED, "dgp_release_tasks: an erred or forgotten task (the scheduler decides, "
+                                        "then dgp_sync_*)");
+  }
   // who_wants emptied; forgotten ones leave SchedulerState.tasks (their rows stay, flagged)
   for (int64_t i = 0; i < n; i++) {
     const int32_t t = task[i];

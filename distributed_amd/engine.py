@@ -509,10 +509,12 @@ class PlacementEngine:
         return int(newp.value)
 
     def release_tasks(self, task, forget) -> int | None:
-        """client-releases-keys (distributed/scheduler.py:5417-5430) that reaches only results in
-        memory or released (dgp_release_tasks): each task released with its replicas, forgotten
-        where flagged, then the queue refill. Returns its placements, or None when the engine
-        leaves it to the scheduler (a cancellation), with nothing changed."""
+        """client-releases-keys (distributed/scheduler.py:5417-5430, dgp_release_tasks): the
+        tasks its transitions reach in the scheduler's order (loss.release_plan), each released
+        from its state -- a result with its replicas, cancelled work (processing, waiting,
+        queued, no-worker) leaving its worker / the queue and its dependencies' waiters --
+        forgotten where flagged, then the queue refill. Returns its placements, or None when the
+        engine leaves it to the scheduler (an erred or forgotten task), with nothing changed."""
         t, f = self._arr(task, np.int32), self._arr(forget, np.uint8)
         if len(t) != len(f):
             raise ValueError("one forget flag per task")

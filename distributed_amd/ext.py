@@ -88,10 +88,11 @@ _REFILL_TRANSITIONS = _ADD_WORKER_TRANSITIONS
 # waits for released, then the queue refill
 _ERRED_TRANSITIONS = frozenset({("processing", "erred"), ("waiting", "released"), ("released", "erred"),
                                 ("memory", "released"), ("queued", "processing")})
-# client-releases-keys of results in memory (:5417-5430): memory -> released / forgotten,
-# released -> forgotten (dgp_release_tasks), then the queue refill
+# client-releases-keys (:5417-5430): memory -> released / forgotten, released -> forgotten,
+# cancelled work -> released (dgp_release_tasks), then the queue refill
 _RELEASE_TRANSITIONS = frozenset({("memory", "released"), ("memory", "forgotten"), ("released", "forgotten"),
-                                  ("queued", "processing")})
+                                  ("processing", "released"), ("waiting", "released"), ("queued", "released"),
+                                  ("no-worker", "released"), ("queued", "processing")})
 # reschedule (Scheduler._reschedule :7900-7924): processing -> released -> waiting, then
 # decide_worker (dgp_reschedule)
 _RESCHEDULE_TRANSITIONS = frozenset({("processing", "released"), ("released", "waiting"), ("waiting", "processing"),
@@ -1599,10 +1600,11 @@ class GPUPlacementExtension(SchedulerPlugin):
 
     def _on_client_releases_keys(self, kw):
         """client-releases-keys (:5417-5430): tasks no longer wanted are released or
-        forgotten. When its transitions reach only results in memory (or released), the engine
-        follows on the device (dgp_release_tasks: replicas, who_wants, forgotten rows, the
-        queue refill); otherwise (a cancellation) the scheduler's own stimulus, then a resync
-        of those keys."""
+        forgotten -- results in memory, and cancelled work (waiting, processing, queued,
+        no-worker). The engine follows on the device (dgp_release_tasks: the transitions in the
+        scheduler's order from loss.release_plan, then the queue refill); a release the engine
+        does not restate (a re-wait, an erred task, lost dependencies) is the scheduler's own
+        stimulus, then a resync of those keys."""
         s = self.scheduler
         keys = [k for k in kw.get("keys") or () if k in self.task_index]
         if not keys:

@@ -170,46 +170,152 @@ def graph_orders(new, chain, index_of) -> list:
             for t in list(new) + list(chain) if sum(d in cs for d in t.dependencies) >= 2]
 
 
+class _NotModelled(Exception):
+    pass
+
+
 def release_plan(s, client, keys) -> list | None:
-    """client-releases-keys (scheduler.py:5417-5430): the tasks its transitions reach, each
-    with its forget flag -- the keys no other client wants (_client_releases_keys
-    :3400-3419: forgotten without dependents, else released when nothing waits on them), then
-    every dependency _propagate_forgotten forgets (:3378-3385: no dependent left, not wanted)
-    -- when all of them are results in memory or released (dgp_release_tasks); None when
-    the release reaches anything else (a cancellation, an erred or actor task, a forgotten
-    task with dependents still live): the scheduler's stimulus, then a resync."""
+    """client-releases-keys (scheduler.py:5417-5430): every task its transitions reach, each
+    with its forget flag, in the order the scheduler runs them (dgp_release_tasks applies them
+    in that order). _client_releases_keys (:3400-3419) recommends the keys no other client
+    wants -- forgotten without dependents, else released when nothing waits on them -- and
+    SchedulerState._transitions pops that dict LIFO, merging what each transition recommends
+    (dict.update: a key already present keeps its place). Restated here on a shadow of the
+    states, waiters, dependents and who_wants it changes:
+
+      memory -> released       :2444-2505    processing -> released  :2606-2628 (+ :3337-3357)
+      waiting -> released      :2579-2604    queued / no-worker -> released  :2784-2795, :2747-2759
+      released / memory -> forgotten  :2853-2881, :2821-2851 (_propagate_forgotten :3359-3398)
+      anything else -> released first, then on (:1961-1984)
+
+    None when the release reaches a case the engine does not restate: a task re-waited (a
+    released task something still needs), an erred or actor task, a forgotten task whose
+    dependents would be flagged with lost dependencies, a cancelled task that is not in one of
+    its dependencies' waiters: the scheduler's stimulus, then a resync."""
     cs = s.clients.get(client)
     if cs is None:
         return []
-    recs, seen = [], set()
+    recs, wants = {}, {}
     for key in keys:
         ts = s.tasks.get(key)
-        if ts is None or ts in seen or ts not in (cs.wants_what or ()):
+        if ts is None or ts in wants or ts not in (cs.wants_what or ()):
             continue
-        seen.add(ts)
-        if (ts.who_wants or set()) - {cs}:
+        left = set(ts.who_wants or ()) - {cs}
+        wants[ts] = left
+        if left:
             continue  # still wanted by another client: who_wants changes, nothing transitions
         if not ts.dependents:
-            recs.append((ts, True))
+            recs[ts] = "forgotten"
         elif ts.state != "erred" and not ts.waiters:
-            recs.append((ts, False))
-    plan, forgotten, stack = {}, set(), list(recs)
-    while stack:
-        ts, forget = stack.pop()
-        if ts.state not in ("memory", "released") or ts.actor:
-            return None
-        if not forget and (not ts.run_spec or ts.has_lost_dependencies):
-            forget = True  # memory -> released of pure data / lost dependencies: forgotten (:2485-2488)
-        if not forget:
-            plan.setdefault(ts, False)
-            continue
-        if ts in forgotten:
-            continue
-        forgotten.add(ts)
-        plan[ts] = True
-        if any(d not in forgotten for d in ts.dependents):
-            return None  # its dependents would be forgotten or flagged with lost dependencies
+            recs[ts] = "released"
+    state, wset, dset = {}, {}, {}
+
+    def st(ts):
+        return state.get(ts, ts.state)
+
+    def waiters(ts):
+        if ts not in wset:
+            wset[ts] = set(ts.waiters or ())
+        return wset[ts]
+
+    def dependents(ts):
+        if ts not in dset:
+            dset[ts] = set(ts.dependents)
+        return dset[ts]
+
+    def who(ts):
+        return wants[ts] if ts in wants else (ts.who_wants or set())
+
+    ops, forget = {}, set()
+
+    def leave_waiters(ts, r):  # a cancelled task leaves its dependencies' waiters
         for dts in ts.dependencies:
-            if not any(x not in forgotten for x in dts.dependents) and not dts.who_wants:
-                stack.append((dts, True))
-    return list(plan.items())
+            if st(dts) == "released":
+                continue
+            w = waiters(dts)
+            if ts not in w:
+                raise _NotModelled  # the engine's count would drop a task the set never held
+            w.discard(ts)
+            if not w and not who(dts):
+                r[dts] = "released"
+
+    def propagate_released(ts, r):  # :3337-3357
+        state[ts] = "released"
+        if ts.has_lost_dependencies:
+            r[ts] = "forgotten"
+        elif waiters(ts) or who(ts):
+            raise _NotModelled  # re-waited
+        leave_waiters(ts, r)
+        wset[ts] = set()
+
+    def to_released(ts, start):
+        r = {}
+        if ts.actor:
+            raise _NotModelled
+        ops.setdefault(ts, None)
+        if start == "memory":
+            state[ts] = "released"
+            if not ts.run_spec or ts.has_lost_dependencies:
+                r[ts] = "forgotten"
+            elif who(ts) or waiters(ts):
+                raise _NotModelled  # re-waited (and its waiters' recommendations)
+        elif start in ("processing", "queued", "no-worker"):
+            propagate_released(ts, r)
+        elif start == "waiting":
+            for dts in ts.dependencies:
+                w = waiters(dts)
+                if ts in w:
+                    w.discard(ts)
+                    if not w and not who(dts):
+                        r[dts] = "released"
+                elif st(dts) != "released":
+                    raise _NotModelled
+            state[ts] = "released"
+            if ts.has_lost_dependencies:
+                r[ts] = "forgotten"
+            elif not ts.exception_blame and (who(ts) or waiters(ts)):
+                raise _NotModelled
+            wset[ts] = set()
+        else:
+            raise _NotModelled
+        return r
+
+    def to_forgotten(ts, start):  # :2853-2881 / :2821-2851 -> _propagate_forgotten (a result's replicas go)
+        if ts.actor or dependents(ts):
+            raise _NotModelled  # its dependents would be flagged with lost dependencies
+        ops.setdefault(ts, None)
+        forget.add(ts)
+        r = {}
+        for dts in ts.dependencies:
+            dependents(dts).discard(ts)
+            waiters(dts).discard(ts)
+            if not dependents(dts) and not who(dts):
+                r[dts] = "forgotten"
+        state[ts] = "forgotten"
+        return r
+
+    def transition(ts, finish):  # SchedulerState._transition :1910-1990
+        start = st(ts)
+        if start == "forgotten" or start == finish:
+            return {}
+        if finish == "released":
+            return to_released(ts, start)
+        if finish == "forgotten":
+            if start in ("released", "memory"):
+                return to_forgotten(ts, start)
+            a = to_released(ts, start)
+            v = a.get(ts, finish)
+            if v != "forgotten":
+                raise _NotModelled
+            b = to_forgotten(ts, "released")
+            a.update(b)
+            return a
+        raise _NotModelled
+
+    try:
+        while recs:
+            ts, finish = recs.popitem()
+            recs.update(transition(ts, finish))
+    except _NotModelled:
+        return None
+    return [(ts, ts in forget) for ts in ops]

@@ -297,14 +297,18 @@ int dgp_add_graph_deferred(dgp_engine* e, int64_t n_new, const int64_t* dep_ptr,
  * stimulus and the caller resynchronises as before. Replaces the scheduler's Python for that
  * stimulus (scheduler.py:4600-4653). */
 int dgp_graph_stimulus(dgp_engine* e, int64_t* n_new_placements);
-/* dgp_release_tasks (ABI 21): client-releases-keys (scheduler.py:5417-5430) whose transitions
- * reach only results in memory or released: task[i] (the closure the scheduler's transitions
- * reach: the released keys, then the dependencies _propagate_forgotten forgets, :3359-3398)
- * memory -> released with its replicas (remove_all_replicas :3161-3171), who_wants emptied,
- * forget[i] != 0: forgotten (the row stays, released, out of every dependents walk); then the
- * queue refill (:5430). *n_new_placements: its placements. DGP_E_UNSUPPORTED with nothing
- * changed for a task in any other state (a cancellation: the scheduler decides, then
- * dgp_sync_*). */
+/* dgp_release_tasks (ABI 21): client-releases-keys (scheduler.py:5417-5430). task[i]: every
+ * task its transitions reach -- the released / forgotten keys (_client_releases_keys
+ * :3400-3419), the dependencies they release or forget in turn (_propagate_released
+ * :3337-3357, _transition_waiting_released :2579-2604, _propagate_forgotten :3359-3398) -- in
+ * the order the scheduler's recommendation dict runs them (distributed_amd/loss.py
+ * release_plan). Each is applied by its state: memory -> released with its replicas;
+ * processing -> released (it leaves its worker); waiting / queued / no-worker -> released
+ * (waiting_on, queued, unrunnable); a cancelled task leaves its dependencies' waiters.
+ * who_wants emptied; forget[i] != 0: forgotten (the row stays, released, out of every
+ * dependents walk). Then the queue refill (:5430). *n_new_placements: its placements.
+ * DGP_E_UNSUPPORTED with nothing changed for an erred or forgotten task (the scheduler
+ * decides, then dgp_sync_*). */
 int dgp_release_tasks(dgp_engine* e, int64_t n, const int32_t* task, const uint8_t* forget, int64_t* n_new_placements);
 /* dgp_reschedule (ABI 21): Scheduler._reschedule (scheduler.py:7900-7924) of a processing task
  * -- transitions({key: "released"}): it leaves its worker (check_idle_saturated), is

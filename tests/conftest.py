@@ -19,7 +19,7 @@ def golden_files():
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
                   and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcgdep_", "svcev_",
                                             "svcrs_", "svcrt_", "svcwl_", "svcp2p_", "svcgrst_", "svcgprio_", "svcpfx_",
-                                            "svcgrec_", "svcrel_")))
+                                            "svcgrec_", "svcrel_", "svccan_")))
 
 
 def svc_second_graph_files():
@@ -87,8 +87,9 @@ def svc_retire_files():
 
 
 def svc_release_files():
-    """Service streams where clients release results in memory (gen_service.py resync svcrel_*)."""
-    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcrel_") and f.endswith(".npz"))
+    """Service streams where clients release results in memory (gen_service.py resync svcrel_*)
+    and wanted tasks in any state: cancelled work with what it releases and forgets (svccan_*)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith(("svcrel_", "svccan_")) and f.endswith(".npz"))
 
 
 def svc_loss_files():

@@ -941,6 +941,8 @@ def _erred_is_simple(s, ts):
     for x in closure:
         for d in x.dependencies:
             if d in closure:
+                if d is not ts and not d.who_wants:  # x's release may override d's "erred" (dgp_events.h)
+                    return False
                 continue
             if not (d.waiters or set()) - closure and not d.who_wants and d.state != "memory":
                 return False
@@ -948,7 +950,7 @@ def _erred_is_simple(s, ts):
 
 
 def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_scale=0.3, dumps=None, chains=False,
-                  allowed_failures=3, release_memory=False):
+                  allowed_failures=3, release_memory=False, release_cancel=False):
     """The replay protocol's completions as task-finished messages, interleaved with the
     other worker stimuli that change placement inputs, each through the reference's own
     handler (``Scheduler.*`` borrowed onto the replay state):
@@ -1210,19 +1212,35 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
             s._reschedule(ts.key, addr[w], stimulus_id=sid)
             push(EV_RESCHEDULE, tidx[ts.key], w)
         elif kind == EV_RELEASE_KEYS:
-            states = ("memory",) if release_memory else ("waiting", "processing", "queued")
+            states = (("memory",) if release_memory else
+                      ("waiting", "processing", "queued", "no-worker", "memory") if release_cancel else
+                      ("waiting", "processing", "queued"))
             wanted = [ts for ts in tss if ts.who_wants and ts.state in states]
             if not wanted:
                 return
             ts = wanted[int(rng.integers(0, len(wanted)))]
-            if release_memory:  # what the engine takes (distributed_amd/loss.py release_plan, as the extension)
+            if release_memory or release_cancel:  # what the engine takes (loss.release_plan, as the extension)
                 LR = _load_repo_module("loss")
                 plan = LR.release_plan(s, "client-0", [ts.key])
+                for _ in range(32 if release_cancel else 0):  # a release the engine restates
+                    if plan is not None:
+                        break
+                    ts = wanted[int(rng.integers(0, len(wanted)))]
+                    plan = LR.release_plan(s, "client-0", [ts.key])
+                if plan is None and release_cancel:
+                    return
                 assert plan is not None, ts.key
                 for x, f in plan:
                     lo["rtask"].append(tidx[x.key])
                     lo["rforget"].append(1 if f else 0)
+            before = [x.state for x in tss] if release_cancel else None
             s.client_releases_keys(keys=[ts.key], client="client-0", stimulus_id=sid)
+            if release_cancel:  # the plan names exactly the tasks the transitions changed (the refill aside)
+                ops = {tidx[x.key] for x, _ in plan}
+                chg = {i for i, x in enumerate(tss) if x.state != before[i] and not
+                       (before[i] == "queued" and x.state == "processing")}
+                assert chg == ops, (sorted(chg - ops)[:8], sorted(ops - chg)[:8],
+                                    [(i, before[i], tss[i].state) for i in sorted(chg ^ ops)[:8]])
             push(EV_RELEASE_KEYS, tidx[ts.key], -1)
         elif kind == EV_ERRED:
             proc = [ts for ts in tss if ts.state == "processing" and _erred_is_simple(s, ts)]
@@ -1308,6 +1326,10 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
     assert len(tm["task"]) == len(rec["task"]) - n_ug and tm["task"] == rec["task"][n_ug:]
     ev["tm"] = dict(tm, first=n_ug)
     states = np.array([G.STATE_CODES[ts.state] for ts in tss], np.uint8)
+    if os.environ.get("DGP_DEBUG_STORY"):  # diagnostics: the transitions of the named tasks
+        for q in [int(x) for x in os.environ["DGP_DEBUG_STORY"].split(",") if x]:
+            for e in s.story(tss[q].key):
+                print("STORY", q, tss[q].key, e[0] == tss[q].key, e[1], e[2], e[4], flush=True)
     return rec, rounds, nplaced, states, ev, hb, round_ptr
 
 
@@ -1544,6 +1566,11 @@ def main_resync(only):
         "svcrel_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=63, n_inner_prefixes=3,
                                                              random_durations=True, nthreads="random"), 1.1, 63, 0.12),
         "svcrel_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=64), float("inf"), 64, 0.12),
+        # clients release wanted tasks in any state: cancelled work (waiting, processing, queued,
+        # no-worker) and results, with what the transitions release and forget in turn
+        "svccan_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=65, n_inner_prefixes=3,
+                                                             random_durations=True, nthreads="random"), 1.1, 65, 0.12),
+        "svccan_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=66), float("inf"), 66, 0.12),
         # allowed_failures 0: every processing task of a lost worker errs
         "svcwl_killed0_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=61, n_inner_prefixes=3,
                                                                     random_durations=True, nthreads="random"), 1.1, 61, 0.12),
@@ -1558,10 +1585,12 @@ def main_resync(only):
         dumps = []
         kinds_ = ((1, 2, 3, 4, 5, 6, 7, EV_RETIRE, EV_RETIRE, EV_PAUSE) if name.startswith("svcrt_") else
                   (1, 2, 3, 4, 5, 6, 7, EV_LOSE_WORKER, EV_LOSE_WORKER, EV_RESUME) if name.startswith("svcwl_") else
-                  (1, 2, 3, 4, 5, 6, 7, EV_RELEASE_KEYS, EV_RELEASE_KEYS) if name.startswith("svcrel_") else kinds)
+                  (1, 2, 3, 4, 5, 6, 7, EV_RELEASE_KEYS, EV_RELEASE_KEYS) if name.startswith(("svcrel_", "svccan_"))
+                  else kinds)
         rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(
             g, cfg, seed, p_event, kinds_, dumps=dumps, chains=name.startswith(("svcwl_chain_", "svcwl_killed")),
-            allowed_failures=loss_allowed_failures(name), release_memory=name.startswith("svcrel_"))
+            allowed_failures=loss_allowed_failures(name), release_memory=name.startswith("svcrel_"),
+            release_cancel=name.startswith("svccan_"))
         G.save(name, g, cfg, rec, rounds, nplaced, states, 0.0)
         path = os.path.join(HERE, f"{name}.npz")
         z = dict(np.load(path, allow_pickle=False))

@@ -192,20 +192,31 @@ def test_extension_follows_the_p2p_shuffle_lifecycle():
 
 def test_extension_resyncs_after_stimuli_it_does_not_model():
     """Worker removal (Scheduler.remove_worker), rescheduling and client releases in the
-    stream: the plugin transition hook suspends the engine at the first transition it does
-    not model, the scheduler decides that stimulus, and the extension resynchronises the
+    stream, with an engine that does not restate them (no lose_worker / reschedule /
+    release_tasks): the plugin transition hook suspends the engine at the first transition it
+    does not model, the scheduler decides that stimulus, and the extension resynchronises the
     engine (dgp_remove_worker, dgp_sync_*): the rows it sends cover every task whose state
     changed (checked against a full dump), the worker / global rows equal the fixture's
     dumps, the extension stays active and every other placement is the engine's
     (validate=True)."""
+    res = drive(RESYNC, "--resync-only")
+    assert [r["fixture"] for r in res] == RESYNC
+    for r in res:
+        assert r["active"] and r["resyncs"] > 0 and r["calls"].get("workers_lost_on_device", 0) == 0, r
+        assert r["device_decisions"] + r["host_placements"] == r["placements"], r
+
+
+def test_extension_decides_every_resync_stimulus_on_the_engine():
+    """The same streams with the engine's worker-loss, reschedule and client-release
+    operations: every one of those stimuli is restated on the engine (dgp_lose_worker_ordered,
+    dgp_reschedule, dgp_release_tasks), no resync, every placement the engine's."""
     res = drive(RESYNC)
     assert [r["fixture"] for r in res] == RESYNC
     for r in res:
-        assert r["active"] and r["resyncs"] > 0, r
-        # the losses the engine restates are decided there (since recompute chains: all of
-        # these streams'); any other one is the scheduler's, then dgp_remove_worker + resync
-        assert r["calls"]["workers_lost_on_device"] > 0, r
-        assert r["device_decisions"] + r["host_placements"] == r["placements"], r
+        assert r["active"] and r["resyncs"] == 0, r
+        for op in ("workers_lost_on_device", "reschedule", "release_tasks"):
+            assert r["calls"].get(op, 0) > 0, (op, r)
+        assert r["device_decisions"] == r["placements"], r
 
 
 def test_extension_follows_retiring_workers_on_the_device():
@@ -244,12 +255,14 @@ def test_extension_runs_worker_losses_on_the_engine():
 
 
 def test_extension_follows_client_releases_on_the_engine():
-    """Clients release results in memory (svcrel_*): the extension computes what the
-    scheduler's transitions will reach (loss.release_plan: the keys forgotten or released, the
-    dependencies forgotten with them) and the engine follows on the device
-    (dgp_release_tasks) before the handler runs; the closures equal the generator's, no
-    resync, every placement the engine's (validate=True)."""
-    names = ["svcrel_c2var_sat1.1.npz", "svcrel_c2mini_satinf.npz"]
+    """Clients release results in memory (svcrel_*) and cancel wanted work in any state
+    (svccan_*): the extension computes what the scheduler's transitions will reach, in their
+    order (loss.release_plan: the keys released or forgotten, the work and results released
+    and forgotten with them) and the engine follows on the device (dgp_release_tasks) before
+    the handler runs; the closures equal the generator's, no resync, every placement the
+    engine's (validate=True)."""
+    names = ["svcrel_c2var_sat1.1.npz", "svcrel_c2mini_satinf.npz", "svccan_c2var_sat1.1.npz",
+             "svccan_c2mini_satinf.npz"]
     res = drive(names)
     assert [r["fixture"] for r in res] == names
     for r in res:
