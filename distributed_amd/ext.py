@@ -430,9 +430,16 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._wrap(handlers, "reschedule", self._on_reschedule, _RESCHEDULE_TRANSITIONS)
             # client stream handlers (:3781-3792)
             self._wrap(handlers, "client-desires-keys", self._on_client_desires_keys, ())
-            self._wrap(handlers, "client-releases-keys", self._on_client_releases_keys, _RELEASE_TRANSITIONS)
-            self._wrap(handlers, "cancel-keys", self._on_cancel_keys, ())
-            self._wrap(handlers, "close-client", self._on_close_client, ())
+            # Scheduler.client_releases_keys per instance, from any caller: the stream handler,
+            # stimulus_cancel (cancel-keys :5364-5396, once per cancelled dependent level and
+            # client) and remove_client (close-client :5727-5750) -- each call one stimulus
+            rel = {"m": getattr(s, "client_releases_keys", None)}
+            self._wrap(rel, "m", self._on_client_releases_keys, _RELEASE_TRANSITIONS)
+            if rel["m"] is not None:
+                s.client_releases_keys = rel["m"]
+                handlers["client-releases-keys"] = rel["m"]
+            self._wrap(handlers, "cancel-keys", None, ())
+            self._wrap(handlers, "close-client", None, ())
             self._wrap(handlers, "update-data", self._on_update_data, ())
         rpc = getattr(s, "handlers", None)
         if isinstance(rpc, dict):
@@ -1622,19 +1629,6 @@ class GPUPlacementExtension(SchedulerPlugin):
         self._suspend("client-releases-keys")
         for k in keys:
             self._mark_dirty(k)
-
-    def _on_cancel_keys(self, kw):
-        """cancel-keys (:5364-5396): the scheduler's own stimulus, then a resync of those keys."""
-        keys = [k for k in kw.get("keys") or () if k in self.task_index]
-        if keys:
-            self._suspend("cancel-keys")
-            for k in keys:
-                self._mark_dirty(k)
-
-    def _on_close_client(self, kw):
-        if self.task_index:
-            self._suspend("close-client releases the client's keys (remove_client :5727)")
-            self._dirty_all = True
 
     def _on_update_data(self, kw):
         """update-data (:7394-7425): scattered data; a key of the engine's graph set to

@@ -1130,6 +1130,10 @@ def run_events(name, plain=False, resync_only=False):
         S.transition = Scheduler.transition  # a KilledWorker's processing -> erred (:5249-5256)
         S._reschedule = Scheduler._reschedule
         S.client_releases_keys = Scheduler.client_releases_keys
+        S.stimulus_cancel = Scheduler.stimulus_cancel  # cancel-keys (:5364-5396)
+        S.remove_client = Scheduler.remove_client  # close-client (:5727-5750)
+        S.log_event = lambda self, topic, msg: None
+        S.report = lambda self, msg, ts=None, client=None: None
         S.remove_resources = lambda self, address: None
         S.coerce_address = lambda self, a, resolve=True: a
         s.status = Status.running
@@ -1183,6 +1187,8 @@ def run_events(name, plain=False, resync_only=False):
     if resyncs:
         s.stream_handlers["reschedule"] = s._reschedule
         s.stream_handlers["client-releases-keys"] = s.client_releases_keys
+        s.stream_handlers["cancel-keys"] = s.stimulus_cancel
+        s.stream_handlers["close-client"] = s.remove_client
     s.handlers = {"heartbeat_worker": heartbeat_worker}
     plugin = spec = None
     if (z["ev_kind"] == EV_SHUFFLE_INIT).any():  # the P2P shuffle plugin, bound to this state
@@ -1213,6 +1219,7 @@ def run_events(name, plain=False, resync_only=False):
     s._transitions(recs, {}, {}, "update-graph")
     want = []  # the engine calls the events imply
     n_sync = 0
+    n_cancel = 0  # releases sent as cancel-keys (svccan_* leaves)
     on_device = set()  # EV_REMOVE_WORKER / EV_RESCHEDULE events the engine decided (dgp_lose_worker, dgp_reschedule)
 
     def check_sync():
@@ -1343,7 +1350,14 @@ def run_events(name, plain=False, resync_only=False):
                     continue
             else:
                 rl0 = ext.stats["release_tasks"]
-                H["client-releases-keys"](keys=[tss[t].key], client="client-0", stimulus_id=sid)
+                cs0 = s.clients["client-0"]
+                if name.startswith("svccan_") and not tss[t].dependents and tss[t].who_wants == {cs0}:
+                    # a wanted leaf: Client.cancel's cancel-keys, whose stimulus_cancel releases it
+                    # through Scheduler.client_releases_keys (the extension's per-instance wrapper)
+                    H["cancel-keys"](keys=[tss[t].key], client="client-0")
+                    n_cancel += 1
+                else:
+                    H["client-releases-keys"](keys=[tss[t].key], client="client-0", stimulus_id=sid)
                 if ext.stats["release_tasks"] > rl0:  # followed by the engine (dgp_release_tasks): no resync
                     c = eng.calls[-1]
                     assert c[0] == "release", c
@@ -1394,7 +1408,7 @@ def run_events(name, plain=False, resync_only=False):
     assert ext.stats["device_decisions"] == n - host, (ext.stats, n, host)
     return dict(fixture=name, placements=n, events=len(want), device_decisions=ext.stats["device_decisions"],
                 host_placements=host, resyncs=ext.stats["resyncs"], active=ext.active, reason=ext.reason,
-                calls=dict(ext.stats))
+                calls=dict(ext.stats), cancels=n_cancel)
 
 
 class NullEngine:

@@ -268,6 +268,8 @@ def test_extension_follows_client_releases_on_the_engine():
     for r in res:
         assert r["active"] and r["resyncs"] == 0 and r["calls"]["release_tasks"] >= 50, r
         assert r["device_decisions"] == r["placements"], r
+        if r["fixture"].startswith("svccan_"):  # wanted leaves cancelled through cancel-keys
+            assert r["cancels"] > 0, r
 
 
 def test_extension_hands_back_on_unmodelled_events():
