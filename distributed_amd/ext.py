@@ -426,7 +426,7 @@ class GPUPlacementExtension(SchedulerPlugin):
             self._wrap(handlers, "release-worker-data", None, ())
             self._wrap(handlers, "long-running", self._on_long_running, _REFILL_TRANSITIONS)
             self._wrap(handlers, "worker-status-change", self._on_worker_status_change, _REFILL_TRANSITIONS)
-            self._wrap(handlers, "task-erred", self._on_task_erred, _ERRED_TRANSITIONS)
+            self._wrap(handlers, "task-erred", self._on_task_erred, _ERRED_TRANSITIONS | _RESCHEDULE_TRANSITIONS)
             self._wrap(handlers, "reschedule", self._on_reschedule, _RESCHEDULE_TRANSITIONS)
             # client stream handlers (:3781-3792)
             self._wrap(handlers, "client-desires-keys", self._on_client_desires_keys, ())
@@ -1583,18 +1583,41 @@ class GPUPlacementExtension(SchedulerPlugin):
 
     def _on_task_erred(self, kw):
         """task-erred (Scheduler.handle_task_erred :5799-5805 -> stimulus_task_erred
-        :5094-5127): a current run that erred with no retries left leaves its worker
-        (_exit_processing_common :3258), its waiting dependents err transitively, the
-        dependencies nobody waits for any more are released, then the queue refill. A stale
-        run, or one with retries left, reschedules: not modelled."""
+        :5094-5127, then the queue refill). A current run with no retries left errs: it leaves
+        its worker (_exit_processing_common :3258), its waiting dependents err transitively,
+        the dependencies nobody waits for any more are released (dgp_task_erred). A retry
+        (:5116-5118: processing -> waiting through released) or a stale run's report from the
+        worker it runs on (:5111-5113: processing -> released, re-waited when needed) of a task
+        something needs is the reschedule's transitions (dgp_reschedule), then the refill
+        (dgp_release_tasks of nothing); a task nobody needs: the scheduler's, then resync."""
         s = self.scheduler
         ts = s.tasks.get(kw.get("key"))
         if ts is None or ts.state != "processing" or ts.key not in self.task_index:
             return
-        if ts.run_id != kw.get("run_id") or ts.retries > 0:
-            self._suspend(f"task-erred of {ts.key!r} reschedules it (stale run or retries left)")
+        stale = ts.run_id != kw.get("run_id")
+        if stale and not (ts.processing_on is not None and ts.processing_on.address == kw.get("worker")):
+            return  # another worker's stale report: no transition (:5114)
+        if not stale and ts.retries <= 0:
+            self._engine_op("task_erred", self.task_index[ts.key])
             return
-        self._engine_op("task_erred", self.task_index[ts.key])
+        what = "a stale run's task-erred" if stale else "a retry"
+        if not (ts.waiters or ts.who_wants) or ts.has_lost_dependencies or ts.actor or \
+                not hasattr(self.engine, "reschedule") or not hasattr(self.engine, "release_tasks"):
+            self._suspend(f"{what} of {ts.key!r} is not restated by the engine")
+            self._mark_dirty(ts.key)
+            return
+        if self._engine_op("reschedule", self.task_index[ts.key]) is None:
+            if self.active:
+                self._suspend(f"{what} of {ts.key!r}: {getattr(self.engine, 'refusal', 'refused by the engine')}")
+                self._mark_dirty(ts.key)
+            return
+        try:  # stimulus_queue_slots_maybe_opened (:5805): after the transitions' placements
+            self.engine.release_tasks(np.zeros(0, np.int32), np.zeros(0, np.uint8))
+            self._fetch()
+        except Exception as e:
+            self.fallback(f"task-erred refill: {e}")
+            return
+        self.stats["erred_retries"] += 1
 
     def _on_client_desires_keys(self, kw):
         """client-desires-keys (:5398-5415): who_wants decides whether a finished task is

@@ -19,7 +19,7 @@ def golden_files():
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")
                   and not f.startswith(("steal_", "svc_steal_", "svcaddw_", "svcgraph_", "svcgdep_", "svcev_",
                                             "svcrs_", "svcrt_", "svcwl_", "svcp2p_", "svcgrst_", "svcgprio_", "svcpfx_",
-                                            "svcgrec_", "svcrel_", "svccan_")))
+                                            "svcgrec_", "svcrel_", "svccan_", "svcretry_")))
 
 
 def svc_second_graph_files():
@@ -90,6 +90,12 @@ def svc_release_files():
     """Service streams where clients release results in memory (gen_service.py resync svcrel_*)
     and wanted tasks in any state: cancelled work with what it releases and forgets (svccan_*)."""
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith(("svcrel_", "svccan_")) and f.endswith(".npz"))
+
+
+def svc_retry_files():
+    """Service streams with task-erred reports that do not err -- retries and stale runs,
+    re-placed by the engine (gen_service.py resync svcretry_*)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("svcretry_") and f.endswith(".npz"))
 
 
 def svc_loss_files():

@@ -1095,7 +1095,8 @@ def run_events(name, plain=False, resync_only=False):
 
     from gen_service import (EV_ADD_KEYS, EV_ERRED, EV_FINISHED, EV_HEARTBEAT, EV_LONG_RUNNING, EV_PAUSE,
                              EV_RELEASE_DATA, EV_RELEASE_KEYS, EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RESTRICT,
-                             EV_RESUME, EV_RETIRE, EV_RETIRE_REPLICA, EV_SHUFFLE_INIT, EV_LOSE_WORKER)
+                             EV_RESUME, EV_RETIRE, EV_RETIRE_REPLICA, EV_SHUFFLE_INIT, EV_LOSE_WORKER, EV_ERRED_RETRY,
+                             EV_REFILL)
 
     from distributed_amd import sync as dsync
 
@@ -1220,6 +1221,7 @@ def run_events(name, plain=False, resync_only=False):
     want = []  # the engine calls the events imply
     n_sync = 0
     n_cancel = 0  # releases sent as cancel-keys (svccan_* leaves)
+    n_retry = 0  # task-erred retries / stale runs (svcretry_*)
     on_device = set()  # EV_REMOVE_WORKER / EV_RESCHEDULE events the engine decided (dgp_lose_worker, dgp_reschedule)
 
     def check_sync():
@@ -1294,6 +1296,20 @@ def run_events(name, plain=False, resync_only=False):
             H["task-erred"](key=ts.key, worker=addr[w], stimulus_id=sid, run_id=ts.run_id, exception=None,
                             traceback=None)
             want.append(("erred", t))
+        elif kd == EV_ERRED_RETRY:  # a retry (ev_x 0) or a stale run (1): reschedule + refill on the engine
+            ts = tss[t]
+            stale = bool(x)
+            if not stale:
+                ts.retries = 1
+            er0 = ext.stats["erred_retries"]
+            H["task-erred"](key=ts.key, worker=addr[w], stimulus_id=sid, run_id=ts.run_id - 1 if stale else ts.run_id,
+                            exception=None, traceback=None)
+            assert ext.stats["erred_retries"] == er0 + 1 and not ext.suspended, (i, ext.stats, ext.suspend_reason)
+            want.append(("resched", ext.task_index[fkeys[t]]))
+            want.append(("release", [], []))
+            n_retry += 1
+        elif kd == EV_REFILL:  # consumed by the EV_ERRED_RETRY before it (the handler's refill)
+            pass
         elif kd == EV_SHUFFLE_INIT:  # the first transfer runs: _ensure_output_tasks_are_non_rootish
             plugin._ensure_output_tasks_are_non_rootish(spec)
             ts_ = sorted(ext.task_index[fkeys[int(q)]] for q in ht[hp[i]:hp[i + 1]])
@@ -1408,7 +1424,7 @@ def run_events(name, plain=False, resync_only=False):
     assert ext.stats["device_decisions"] == n - host, (ext.stats, n, host)
     return dict(fixture=name, placements=n, events=len(want), device_decisions=ext.stats["device_decisions"],
                 host_placements=host, resyncs=ext.stats["resyncs"], active=ext.active, reason=ext.reason,
-                calls=dict(ext.stats), cancels=n_cancel)
+                calls=dict(ext.stats), cancels=n_cancel, retries=n_retry)
 
 
 class NullEngine:
@@ -1482,7 +1498,7 @@ if __name__ == "__main__":
             continue
         fn = (run_joins if nm.startswith("svcaddw_") else (lambda x: run_second_graph(x, "--resync" in args))
               if nm.startswith(("svcgraph_", "svcgdep_", "svcgrst_", "svcgprio_", "svcgrec_"))
-              else (lambda x: run_events(x, plain, "--resync-only" in args)) if nm.startswith(("svcev_", "svcrs_", "svcrt_", "svcwl_", "svcp2p_", "svcrel_", "svccan_"))
+              else (lambda x: run_events(x, plain, "--resync-only" in args)) if nm.startswith(("svcev_", "svcrs_", "svcrt_", "svcwl_", "svcp2p_", "svcrel_", "svccan_", "svcretry_"))
               else run_prefixes if nm.startswith("svcpfx_")
               else None)
         print(json.dumps(fn(nm) if fn else run(nm, diverge, stream=stream,

@@ -871,6 +871,11 @@ EV_RETIRE, EV_RETIRE_REPLICA = 13, 14
 # decides the whole stimulus (dgp_lose_worker). hb_task holds the worker's processing tasks
 # in ws.processing iteration order (ev_x of them), then its replicas in ws.has_what order.
 EV_LOSE_WORKER = 15
+# a task-erred that does not err (svcretry_*): a retry (ts.retries > 0, ev_x 0) or a stale run's
+# report from the worker it runs on (ev_x 1) of a task something needs -- stimulus_task_erred
+# :5111-5118 and its transitions (processing -> released -> waiting -> decide_worker), then
+# handle_task_erred's queue refill (:5805) as the EV_REFILL event that follows it
+EV_ERRED_RETRY, EV_REFILL = 16, 17
 
 
 def _loss_is_supported(s, ws):
@@ -1242,6 +1247,27 @@ def replay_events(g, cfg, seed, p_event=0.08, kinds=(1, 2, 3, 4, 5, 6, 7), bw_sc
                 assert chg == ops, (sorted(chg - ops)[:8], sorted(ops - chg)[:8],
                                     [(i, before[i], tss[i].state) for i in sorted(chg ^ ops)[:8]])
             push(EV_RELEASE_KEYS, tidx[ts.key], -1)
+        elif kind == EV_ERRED_RETRY:
+            proc = [ts for ts in tss if ts.state == "processing" and (ts.waiters or ts.who_wants)
+                    and not ts.has_lost_dependencies]
+            if not proc:
+                return
+            ts = proc[int(rng.integers(0, len(proc)))]
+            w = widx[ts.processing_on.address]
+            stale = bool(rng.random() < 0.3)
+            if not stale:
+                ts.retries = 1
+            run = ts.run_id - 1 if stale else ts.run_id
+            # Scheduler.handle_task_erred (:5799-5805), its two parts as two events
+            r = s.stimulus_task_erred(key=ts.key, stimulus_id=sid, worker=addr[w], run_id=run, exception=None,
+                                      traceback=None)
+            s._transitions(r[0], r[1], r[2], sid)
+            assert ts.state != "erred", ts.state
+            push(EV_ERRED_RETRY, tidx[ts.key], w, 1.0 if stale else 0.0, runid=run)
+            stim.append(len(rec["task"]) - n0)
+            n0 = len(rec["task"])
+            s.stimulus_queue_slots_maybe_opened(stimulus_id=sid)
+            push(EV_REFILL)
         elif kind == EV_ERRED:
             proc = [ts for ts in tss if ts.state == "processing" and _erred_is_simple(s, ts)]
             if not proc:
@@ -1571,6 +1597,10 @@ def main_resync(only):
         "svccan_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=65, n_inner_prefixes=3,
                                                              random_durations=True, nthreads="random"), 1.1, 65, 0.12),
         "svccan_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=66), float("inf"), 66, 0.12),
+        # task-erred reports that do not err: retries and stale runs, re-placed by the engine
+        "svcretry_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=67, n_inner_prefixes=3,
+                                                               random_durations=True, nthreads="random"), 1.1, 67, 0.1),
+        "svcretry_c2mini_satinf": (lambda: G.graphs.random_dag(2500, 40, seed=68), float("inf"), 68, 0.1),
         # allowed_failures 0: every processing task of a lost worker errs
         "svcwl_killed0_c2var_sat1.1": (lambda: G.graphs.random_dag(3000, 48, seed=61, n_inner_prefixes=3,
                                                                     random_durations=True, nthreads="random"), 1.1, 61, 0.12),
@@ -1586,6 +1616,7 @@ def main_resync(only):
         kinds_ = ((1, 2, 3, 4, 5, 6, 7, EV_RETIRE, EV_RETIRE, EV_PAUSE) if name.startswith("svcrt_") else
                   (1, 2, 3, 4, 5, 6, 7, EV_LOSE_WORKER, EV_LOSE_WORKER, EV_RESUME) if name.startswith("svcwl_") else
                   (1, 2, 3, 4, 5, 6, 7, EV_RELEASE_KEYS, EV_RELEASE_KEYS) if name.startswith(("svcrel_", "svccan_"))
+                  else (1, 2, 3, 4, 5, 6, 7, EV_ERRED_RETRY, EV_ERRED_RETRY) if name.startswith("svcretry_")
                   else kinds)
         rec, rounds, nplaced, states, ev, hb, round_ptr = replay_events(
             g, cfg, seed, p_event, kinds_, dumps=dumps, chains=name.startswith(("svcwl_chain_", "svcwl_killed")),

@@ -272,6 +272,20 @@ def test_extension_follows_client_releases_on_the_engine():
             assert r["cancels"] > 0, r
 
 
+def test_extension_follows_erred_retries_on_the_engine():
+    """task-erred reports that do not err (svcretry_*): a retry or a stale run's report from the
+    worker the task runs on, of a task something needs, is the reschedule's transitions on the
+    engine (dgp_reschedule) followed by handle_task_erred's queue refill (dgp_release_tasks of
+    nothing); no resync, every placement the engine's (validate=True)."""
+    names = ["svcretry_c2var_sat1.1.npz", "svcretry_c2mini_satinf.npz"]
+    res = drive(names)
+    assert [r["fixture"] for r in res] == names
+    for r in res:
+        assert r["active"] and r["resyncs"] == 0 and r["retries"] >= 40, r
+        assert r["calls"]["erred_retries"] == r["retries"] == r["calls"]["reschedule"], r
+        assert r["device_decisions"] == r["placements"], r
+
+
 def test_extension_hands_back_on_unmodelled_events():
     """An engine without the event calls: the first such event ends GPU placement loudly
     ("not modelled") and the scheduler's own decisions carry on, equal to the reference's."""

@@ -21,7 +21,8 @@ import numpy as np
 import pytest
 
 from conftest import (GOLDEN, second_graph, svc_dep_graph_files, svc_event_files, svc_p2p_files, svc_prio_graph_files,
-                      svc_loss_files, svc_release_files, svc_resync_files, svc_restr_graph_files, svc_retire_files)
+                      svc_loss_files, svc_release_files, svc_restr_graph_files, svc_resync_files, svc_retire_files,
+                      svc_retry_files)
 from oracle import oracle
 from test_gpu_parity import PL_KEYS, ROUND_KEYS, assert_same
 
@@ -32,6 +33,7 @@ EV_REMOVE_WORKER, EV_RESCHEDULE, EV_RELEASE_KEYS = 8, 9, 10
 EV_SHUFFLE_INIT, EV_RESTRICT = 11, 12
 EV_RETIRE, EV_RETIRE_REPLICA = 13, 14
 EV_LOSE_WORKER = 15
+EV_ERRED_RETRY, EV_REFILL = 16, 17
 
 
 def sync_dump(z, j):
@@ -116,6 +118,10 @@ def drive_events(eng, g, z, exp=None, device_resched=False, device_release=False
                 npr = int(x[i])
                 assert eng.lose_worker(w, lst[:npr], lst[npr:], loss_order_rows(z, i),
                                        loss_killed(z, i, lst[:npr])) is not None, (i, eng.refusal)
+            elif kd == EV_ERRED_RETRY:  # a retry / stale run: the reschedule's transitions on the device
+                assert eng.reschedule(t) is not None, (i, eng.refusal)
+            elif kd == EV_REFILL:  # handle_task_erred's queue refill (dgp_release_tasks of nothing)
+                eng.release_tasks(np.zeros(0, np.int32), np.zeros(0, np.uint8))
             elif kd == EV_RESCHEDULE and device_resched and eng.reschedule(t) is not None:
                 n_sync += 1  # decided on the device (dgp_reschedule): the fixture's resync rows unused
             elif kd == EV_RELEASE_KEYS and device_release:
@@ -322,6 +328,35 @@ def test_service_client_releases(name, device_release):
         print(name, "release ops by engine state (released, waiting, processing, queued, no-worker, memory):",
               cnt[:6].tolist())
         assert cnt[1] > 0 and cnt[2] > 0 and cnt[5] > 0, cnt
+
+
+@pytest.mark.parametrize("name", svc_retry_files())
+def test_service_erred_retries(name):
+    """task-erred reports that do not err (stimulus_task_erred, scheduler.py:5111-5118): a
+    retry (retries left: processing -> waiting through released) or a stale run's report from
+    the worker the task runs on (processing -> released, re-waited) of a task something needs,
+    re-placed on the device (dgp_reschedule), then handle_task_erred's queue refill (:5805,
+    dgp_release_tasks of nothing). Every placement, snapshot and final state equals the
+    reference's."""
+    from distributed_amd.engine import PlacementEngine
+
+    path = os.path.join(GOLDEN, name)
+    g, cfg, exp, meta = oracle.load_fixture(path)
+    z = np.load(path, allow_pickle=False)
+    kinds = set(np.unique(z["ev_kind"]).tolist())
+    assert {EV_ERRED_RETRY, EV_REFILL} <= kinds
+    assert {0.0, 1.0} <= set(z["ev_x"][z["ev_kind"] == EV_ERRED_RETRY].tolist())  # retries and stale runs
+    R = len(exp["round_nplaced"]) + 2
+    with PlacementEngine(0) as eng:
+        eng.load(g, cfg, snapshots=R, results=False)
+        eng.update_graph()
+        stim = drive_events(eng, g, z, exp)
+        out = eng.placements()
+        out.update(eng.snapshots(R))
+        out["final_state"] = eng.task_states()
+    assert np.array_equal(stim, exp["stim_nplaced"]), np.nonzero(stim != exp["stim_nplaced"])[0][:5]
+    assert_same(out, exp, PL_KEYS + ROUND_KEYS)
+    assert np.array_equal(out["final_state"], exp["final_state"])
 
 
 @pytest.mark.parametrize("name", svc_p2p_files())
