@@ -1992,14 +1992,24 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
 #endif
     // predecessor count of stimulus b = its workers that an earlier in-flight stimulus holds:
     // it waits on each for the latest one only, whose release of that worker wakes it
-    // (release_worker picks the earliest successor). Each lane adds its own count to the slot
-    // (no-return LDS adds, in order after the guard)
+    // (release_worker picks the earliest successor). With wait-in-place claims each lane adds
+    // its own count to the slot (pred, or predc for a candidate-only worker: no-return LDS
+    // adds, in order after the guard); without them (the 64-slot build, registrar-bound on
+    // C3) the count is summed per slot in registers, a ballot each, and added by the guard
+    // drop below in the same atomic (same-box A/B, profiles/r06/registrar_fused_count_ab.txt:
+    // C3 +0.5 %, C2 -0.6 % in the 32-slot build, which keeps the adds)
+    int pc_my = 0;  // lane b: slot b's predecessor count (64-slot build)
 #pragma unroll
     for (int b = 0; b < RB; b++) {
       if (b >= nloc) break;
       const int c = (lane < ntb[b] && (oldb[b] & ~(1ull << sb[b])) != 0) ? 1 : 0;
-      const bool co = WAITC && lane > 0 && (TB[b] & T_CAND);
-      if (c) __hip_atomic_fetch_add(co ? &L.predc[sb[b]] : &L.pred[sb[b]], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (WAITC) {
+        const bool co = lane > 0 && (TB[b] & T_CAND);
+        if (c) __hip_atomic_fetch_add(co ? &L.predc[sb[b]] : &L.pred[sb[b]], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        const int pb = __builtin_popcountll(ballot(c != 0));
+        if (lane == b) pc_my = pb;
+      }
     }
     if (glob_end) {  // a global stimulus waits for every in-flight stimulus on every worker
       const int sg = sb[nbat - 1];
@@ -2015,12 +2025,12 @@ __device__ __attribute__((always_inline)) void role_reg(const Dev& D, SLds& L, c
     // lane b drops slot b's registration guard; the count left is its predecessors not yet
     // released (releases that came first were never counted)
     if (lane < nbat) {
-      const int op = __hip_atomic_fetch_add(&L.pred[my_s], -BIG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (op == BIG) atomicOr(&S.ready, 1ull << my_s);
+      const int op = __hip_atomic_fetch_add(&L.pred[my_s], pc_my - BIG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (op + pc_my == BIG) atomicOr(&S.ready, 1ull << my_s);
       if (DGP_TRACE) {
         if (TRL) TR(r0 + lane, 0);
         if (TRL && op == BIG) TR(r0 + lane, 1);
-        trace_at(D, r0 + lane, 7, (unsigned long long)((op - BIG) | (nt << 16)));
+        trace_at(D, r0 + lane, 7, (unsigned long long)((op + pc_my - BIG) | (nt << 16)));
       }
     }
     const unsigned long long tB = mclk();
