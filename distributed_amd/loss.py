@@ -280,7 +280,7 @@ def release_plan(s, client, keys) -> list | None:
             raise _NotModelled
         return r
 
-    def to_forgotten(ts, start):  # :2853-2881 / :2821-2851 -> _propagate_forgotten (a result's replicas go)
+    def to_forgotten(ts):  # :2853-2881 / :2821-2851 -> _propagate_forgotten (a result's replicas go)
         if ts.actor or dependents(ts):
             raise _NotModelled  # its dependents would be flagged with lost dependencies
         ops.setdefault(ts, None)
@@ -302,12 +302,12 @@ def release_plan(s, client, keys) -> list | None:
             return to_released(ts, start)
         if finish == "forgotten":
             if start in ("released", "memory"):
-                return to_forgotten(ts, start)
+                return to_forgotten(ts)
             a = to_released(ts, start)
             v = a.get(ts, finish)
             if v != "forgotten":
                 raise _NotModelled
-            b = to_forgotten(ts, "released")
+            b = to_forgotten(ts)
             a.update(b)
             return a
         raise _NotModelled
